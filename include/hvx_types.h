@@ -1,0 +1,94 @@
+/* hvx_types.h -- plain-C data structures shared by the hvx C-ABI (hvx.h) and its
+ * CPU parity oracle (oracle/hvx_oracle.h).  No torch / HIP types.
+ *
+ * Every struct below is a snapshot of the HM-16.5rc1 object state that the
+ * reference kernel reads at call time ("Threading":
+ * lambda, predictor, cost scale, estBits, ... are mutated by the callers, so
+ * each batched job carries its own copy).
+ */
+#ifndef HVX_TYPES_H
+#define HVX_TYPES_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Layout-identical to HM's estBitsSbacStruct (hm-16.5rc1 TComTrQuant.h:60-73,
+ * context counts from ContextTables.h): the fractional-bit tables (15-bit fixed
+ * point) that TEncSbac::estBit (TEncSbac.cpp:1726) derives from the CABAC state. */
+typedef struct hvx_estbits {
+  int32_t significantCoeffGroupBits[2][2];
+  int32_t significantBits[44][2];
+  int32_t lastXBits[2][10];
+  int32_t lastYBits[2][10];
+  int32_t greaterOneBits[24][2];
+  int32_t levelAbsBits[6][2];
+  int32_t blockCbpBits[10][2];
+  int32_t blockRootCbpBits[4][2];
+  int32_t golombRiceAdaptationStatistics[4];
+} hvx_estbits;
+
+/* One transform unit (TComTU + the TComDataCU/TComSlice/TComTrQuant state the
+ * forward/inverse TU path reads: TComTrQuant.cpp:1126-1676, 2129-2671). */
+typedef struct hvx_tu_desc {
+  int32_t comp;               /* ComponentID: 0 Y, 1 Cb, 2 Cr */
+  int32_t width, height;      /* TU rectangle of this component */
+  int32_t log2_size;          /* TComTU::GetEquivalentLog2TrSize */
+  int32_t scan_type;          /* TComDataCU::getCoefScanIdx: 0 diag, 1 hor, 2 ver */
+  int32_t use_dst;            /* TComTU::useDST (4x4 intra luma) */
+  int32_t transform_skip;
+  int32_t is_intra;
+  int32_t tr_idx;             /* TComDataCU::getTransformIdx(absPartIdx) */
+  int32_t ctx_qt_cbf;         /* TComDataCU::getCtxQtCbf(rTu, chType) */
+  int32_t slice_type;         /* HM SliceType: 0 B, 1 P, 2 I */
+  int32_t qp_per, qp_rem;     /* QpParam */
+  int32_t sign_hiding;        /* PPS sign_data_hiding */
+  int32_t use_rdoq, use_rdoq_ts, selective_rdoq, adaptive_qp_select;
+  int32_t transquant_bypass;
+  int32_t golomb_rice_stat;   /* estBits->golombRiceAdaptationStatistics[statIdx] */
+  int32_t persistent_rice, extended_precision, ts_context;
+  int32_t max_log2_tr_range;  /* 15 for 8-bit Main */
+  int32_t bit_depth;          /* 8 */
+  int32_t pad_;
+  double lambda;              /* TComTrQuant::m_dLambda after selectLambda(compID) */
+} hvx_tu_desc;
+
+/* One uni-prediction motion search: TEncSearch::xMotionEstimation with bBi=false
+ * (TEncSearch.cpp:3663-3760): TZ integer search + half/quarter refinement. */
+typedef struct hvx_me_job {
+  int32_t pic_w, pic_h;       /* SPS picture size in luma samples (clipMv, TComDataCU.cpp:2788) */
+  int32_t max_cu;             /* SPS max CU width/height (64) */
+  int32_t cu_x, cu_y;         /* TComDataCU::m_uiCUPelX/Y of the CU owning the PU */
+  int32_t pu_x, pu_y, w, h;   /* PU rectangle in luma samples */
+  int32_t pred_x, pred_y;     /* AMVP predictor (quarter-pel) */
+  int32_t use_int2nx2n;       /* pIntegerMv2Nx2NPred != 0 (TEncSearch.cpp:3734) */
+  int32_t i2_x, i2_y;         /* m_integerMv2Nx2N[list][ref] (integer-pel) */
+  int32_t bits_in;            /* ruiBits on entry */
+  int32_t search_range;       /* m_iSearchRange (SearchRange cfg) */
+  uint32_t lambda_motion;     /* TComRdCost m_uiLambdaMotionSAD[0] = floor(65536*sqrt(lambda)) */
+  int32_t flags;              /* HVX_ME_* below */
+  int32_t ref_idx;            /* index into the reference-plane array of a batch */
+  int32_t cur_idx;            /* index into the current-plane array of a batch */
+  int32_t pad_;
+} hvx_me_job;
+
+#define HVX_ME_FEN        1   /* FEN: subsampled SAD when rows > 8 (TEncSearch.cpp:346) */
+#define HVX_ME_HADME      2   /* HadamardME: SATD in fractional refinement */
+#define HVX_ME_SMOOTHMV   4   /* FastMEAssumingSmootherMV: stop first search after 3 rounds */
+
+typedef struct hvx_me_result {
+  int32_t mv_int_x, mv_int_y; /* integer-pel TZ result */
+  uint32_t sad_int;           /* ruiSAD after xTZSearch (SAD without MV cost) */
+  int32_t half_x, half_y;     /* cMvHalf */
+  int32_t qtr_x, qtr_y;       /* cMvQter */
+  uint32_t cost_frac;         /* ruiCost after xPatternSearchFracDIF */
+  int32_t mv_x, mv_y;         /* final quarter-pel MV */
+  uint32_t bits;              /* ruiBits on exit */
+  uint32_t cost;              /* ruiCost on exit */
+} hvx_me_result;
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,207 @@
+"""ctypes binding of the CPU parity oracle (oracle/hvx_oracle.c -> oracle/_build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY.  Imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- always as the checker / the timed CPU baseline,
+never as the product path (the product is video_codecs_amd's HIP library).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from video_codecs_amd import _abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE, "oracle"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P, I, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+        L.hvxo_sad.restype = ctypes.c_uint32
+        L.hvxo_sad.argtypes = [P, I, P, I, I, I, I]
+        L.hvxo_sad_me.restype = ctypes.c_uint32
+        L.hvxo_sad_me.argtypes = [P, I, P, I, I, I, I]
+        L.hvxo_satd.restype = ctypes.c_uint32
+        L.hvxo_satd.argtypes = [P, I, P, I, I, I]
+        L.hvxo_sse.restype = ctypes.c_uint32
+        L.hvxo_sse.argtypes = [P, I, P, I, I, I]
+        L.hvxo_sse_weighted.restype = ctypes.c_uint32
+        L.hvxo_sse_weighted.argtypes = [P, I, P, I, I, I, D]
+        L.hvxo_eg_bits.restype = ctypes.c_uint32
+        L.hvxo_eg_bits.argtypes = [I]
+        L.hvxo_filter_hor.argtypes = [I, P, I, P, I, I, I, I, I]
+        L.hvxo_filter_ver.argtypes = [I, P, I, P, I, I, I, I, I, I]
+        L.hvxo_fwd_transform.argtypes = [P, P, I, I]
+        L.hvxo_inv_transform.argtypes = [P, P, I, I]
+        L.hvxo_transform_nxn.argtypes = [P, P, P, I, P, P, P, P]
+        L.hvxo_quant.argtypes = [P, P, P, P, P, P]
+        L.hvxo_inv_transform_nxn.argtypes = [P, P, P, I]
+        L.hvxo_motion_estimation.argtypes = [P, I, P, I, P, P]
+        L.hvxo_luma_block_qpel.argtypes = [P, I, I, I, I, I, I, I, P, I]
+        L.hvxo_ssim.restype = ctypes.c_float
+        L.hvxo_ssim.argtypes = [P, I, P, I, I, I, I, I]
+        L.hvxo_stvssim.restype = ctypes.c_float
+        L.hvxo_stvssim.argtypes = [P, P, I, P, I, I, I, I, I, I, I, P, P, P]
+        L.hvxo_lambda_2.restype = D
+        L.hvxo_lambda_2.argtypes = [I]
+        L.hvxo_adjust_lambda.restype = D
+        L.hvxo_adjust_lambda.argtypes = [D, D]
+        L.hvxo_dct_matrix.argtypes = [I, P]
+        L.hvxo_scan.restype = ctypes.POINTER(ctypes.c_uint32)
+        L.hvxo_scan.argtypes = [I, I, I, I]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+# ---- distortion ---------------------------------------------------------------------------
+def sad(org, cur, w, h, sub_shift=0, me_dispatch=False):
+    o, c = _c(org, np.int16), _c(cur, np.int16)
+    f = lib().hvxo_sad_me if me_dispatch else lib().hvxo_sad
+    return int(f(_p(o), o.shape[-1], _p(c), c.shape[-1], w, h, sub_shift))
+
+
+def satd(org, cur, w, h):
+    o, c = _c(org, np.int16), _c(cur, np.int16)
+    return int(lib().hvxo_satd(_p(o), o.shape[-1], _p(c), c.shape[-1], w, h))
+
+
+def sse(org, cur, w, h, weight=None):
+    o, c = _c(org, np.int16), _c(cur, np.int16)
+    if weight is None:
+        return int(lib().hvxo_sse(_p(o), o.shape[-1], _p(c), c.shape[-1], w, h))
+    return int(lib().hvxo_sse_weighted(_p(o), o.shape[-1], _p(c), c.shape[-1], w, h, float(weight)))
+
+
+def eg_bits(v):
+    return int(lib().hvxo_eg_bits(int(v)))
+
+
+# ---- interpolation ------------------------------------------------------------------------
+def filter_block(src, origin, is_luma, vertical, frac, is_first, is_last, w, h):
+    """Run filterHor/filterVer on a 2-D int16 `src` whose block origin is `origin` (row, col)."""
+    s = _c(src, np.int16)
+    out = np.zeros((max(h, 1), max(w, 1)), np.int16)
+    base = s.ctypes.data + (origin[0] * s.shape[1] + origin[1]) * 2
+    if vertical:
+        lib().hvxo_filter_ver(is_luma, ctypes.c_void_p(base), s.shape[1], _p(out), out.shape[1], w, h, frac,
+                              is_first, is_last)
+    else:
+        lib().hvxo_filter_hor(is_luma, ctypes.c_void_p(base), s.shape[1], _p(out), out.shape[1], w, h, frac, is_last)
+    return out
+
+
+# ---- transforms / quant ---------------------------------------------------------------------
+def fwd_transform(block, n, use_dst=False):
+    b = _c(block, np.int32).reshape(-1)
+    out = np.zeros(n * n, np.int32)
+    lib().hvxo_fwd_transform(_p(b), _p(out), n, int(use_dst))
+    return out.reshape(n, n)
+
+
+def inv_transform(coeff, n, use_dst=False):
+    c = _c(coeff, np.int32).reshape(-1)
+    out = np.zeros(n * n, np.int32)
+    lib().hvxo_inv_transform(_p(c), _p(out), n, int(use_dst))
+    return out.reshape(n, n)
+
+
+def transform_nxn(desc, est, residual):
+    """transformNxN: returns (temp_coeff, levels, arl, abs_sum)."""
+    d = np.ascontiguousarray(desc, dtype=_abi.TU_DESC).reshape(1)
+    e = _c(est, np.int32).reshape(-1)
+    r = _c(residual, np.int16)
+    n = int(d["width"][0] * d["height"][0])
+    temp, lev, arl = np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n, np.int32)
+    absum = np.zeros(1, np.int32)
+    lib().hvxo_transform_nxn(_p(d), _p(e), _p(r), r.shape[-1], _p(temp), _p(lev), _p(arl), _p(absum))
+    return temp, lev, arl, int(absum[0])
+
+
+def quant(desc, est, coeff):
+    d = np.ascontiguousarray(desc, dtype=_abi.TU_DESC).reshape(1)
+    e = _c(est, np.int32).reshape(-1)
+    c = _c(coeff, np.int32).reshape(-1)
+    lev, arl, absum = np.zeros_like(c), np.zeros_like(c), np.zeros(1, np.int32)
+    lib().hvxo_quant(_p(d), _p(e), _p(c), _p(lev), _p(arl), _p(absum))
+    return lev, arl, int(absum[0])
+
+
+def inv_transform_nxn(desc, levels):
+    d = np.ascontiguousarray(desc, dtype=_abi.TU_DESC).reshape(1)
+    c = _c(levels, np.int32).reshape(-1)
+    w, h = int(d["width"][0]), int(d["height"][0])
+    out = np.zeros((h, w), np.int16)
+    lib().hvxo_inv_transform_nxn(_p(d), _p(c), _p(out), w)
+    return out
+
+
+# ---- motion estimation ---------------------------------------------------------------------
+def motion_estimation(cur_plane, ref_plane, job, margin=_abi.PLANE_MARGIN):
+    """cur_plane/ref_plane: padded uint8 2-D planes; job: one ME_JOB record.  Returns ME_RESULT."""
+    c, r = _c(cur_plane, np.uint8), _c(ref_plane, np.uint8)
+    j = np.ascontiguousarray(job, dtype=_abi.ME_JOB).reshape(1)
+    res = np.zeros(1, _abi.ME_RESULT)
+    c0 = c.ctypes.data + margin * c.shape[1] + margin
+    r0 = r.ctypes.data + margin * r.shape[1] + margin
+    lib().hvxo_motion_estimation(ctypes.c_void_p(c0), c.shape[1], ctypes.c_void_p(r0), r.shape[1], _p(j), _p(res))
+    return res[0]
+
+
+# ---- SSIM ------------------------------------------------------------------------------------
+def ssim(org, rec, w, h, wint=8, overlap=4):
+    o, r = _c(org, np.uint8), _c(rec, np.uint8)
+    return float(lib().hvxo_ssim(_p(o), o.shape[-1], _p(r), r.shape[-1], w, h, wint, overlap))
+
+
+def stvssim(org_frames, rec_frames, dirs, w, h, wint, overlap, gama, comp):
+    """org_frames/rec_frames: lists of 2-D uint8 arrays (same stride), the last one is the current frame."""
+    used = min(gama, 26)
+    of = [_c(x, np.uint8) for x in org_frames]
+    rf = [_c(x, np.uint8) for x in rec_frames]
+    assert len(of) >= used and len(rf) >= used
+    po = (ctypes.c_void_p * used)(*[x.ctypes.data for x in of[:used]])
+    pr = (ctypes.c_void_p * used)(*[x.ctypes.data for x in rf[:used]])
+    d = _c(dirs, np.float32)
+    s1, s2, s3 = (ctypes.c_float(), ctypes.c_float(), ctypes.c_float())
+    ret = lib().hvxo_stvssim(po, pr, of[0].shape[-1], _p(d), d.shape[-1], w, h, wint, overlap, gama, comp,
+                             ctypes.byref(s1), ctypes.byref(s2), ctypes.byref(s3))
+    return float(ret), s1.value, s2.value, s3.value
+
+
+def lambda_2(qp):
+    return float(lib().hvxo_lambda_2(int(qp)))
+
+
+def adjust_lambda(lam, eta):
+    return float(lib().hvxo_adjust_lambda(float(lam), float(eta)))
+
+
+def dct_matrix(n):
+    m = np.zeros(n * n, np.int16)
+    lib().hvxo_dct_matrix(n, _p(m))
+    return m.reshape(n, n)
+
+
+def scan(grouped, scan_type, log2w, log2h):
+    p = lib().hvxo_scan(int(grouped), scan_type, log2w, log2h)
+    n = 1 << (log2w + log2h)
+    return np.ctypeslib.as_array(p, shape=(n,)).copy()

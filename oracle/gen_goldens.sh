@@ -1,0 +1,30 @@
+#!/bin/bash
+# TEST INFRASTRUCTURE: regenerate every golden fixture under tests/golden/ from the
+# reference (HM-16.5rc1 + stvssim.c compiled by oracle/Makefile into oracle/_ref/).
+# Needs /root/reference (this container only).  Usage: oracle/gen_goldens.sh
+set -euo pipefail
+cd "$(dirname "$0")"
+make -s -j8 ref
+cd ..
+ORC=oracle/_ref
+CFG=/root/reference/hm-16.5rc1/cfg
+TMP=$(mktemp -d)
+trap 'rm -rf "$TMP"' EXIT
+
+# kernel-level vectors (dist, interp, xform, me, ssim)
+$ORC/golden_gen tests/golden
+
+python3 oracle/make_yuv.py random 416 240 2 "$TMP/rand.yuv"
+python3 oracle/make_yuv.py smooth 416 240 3 "$TMP/smooth.yuv"
+
+enc() {  # enc <out.bin> <cfg> <yuv> <frames> <qp> [extra args...]
+  local out=$1 cfg=$2 yuv=$3 frames=$4 qp=$5; shift 5
+  HVX_CAPTURE=$out HVX_CAPTURE_PER_BUCKET=${PER_BUCKET:-6} $ORC/TAppEncoder_capture -c "$cfg" -i "$yuv" \
+    -wdt 416 -hgt 240 -fr 30 -f "$frames" -q "$qp" -b "$TMP/str.bin" -o "$TMP/rec.yuv" "$@" > "$TMP/log.txt"
+}
+# transform/quant/RDOQ/dequant/inverse captured from real encodes
+enc tests/golden/tu_intra.bin  $CFG/encoder_intra_main.cfg       "$TMP/rand.yuv"   1 32
+enc tests/golden/tu_ldp.bin    $CFG/encoder_lowdelay_P_main.cfg  "$TMP/smooth.yuv" 3 27
+enc tests/golden/tu_ldp22.bin  $CFG/encoder_lowdelay_P_main.cfg  "$TMP/smooth.yuv" 2 22
+enc tests/golden/tu_noqrd.bin  $CFG/encoder_lowdelay_P_main.cfg  "$TMP/smooth.yuv" 2 37 --RDOQ=0 --RDOQTS=0
+ls -la tests/golden

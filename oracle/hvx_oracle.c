@@ -1,0 +1,1317 @@
+/* hvx_oracle.c -- CPU restatement of the HM-16.5rc1 CU mode-decision kernels.
+ *
+ * TEST INFRASTRUCTURE ONLY (see hvx_oracle.h).  Plain C, scalar, written from
+ * the reference's behaviour; every function cites the reference file:line it
+ * restates (paths relative to /root/reference/hm-16.5rc1/source/Lib unless noted).
+ * Floating point follows the reference's operation order exactly; build with
+ * -ffp-contract=off (x86-64 SSE2 semantics, as the reference was compiled).
+ * Parity is pinned by tests/test_oracle_golden.py against tests/golden/.
+ */
+#include "hvx_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ============================================================================================
+ * Tables.  Values are HEVC-specification constants (the reference stores the same numbers in
+ * TComRom.cpp:354-362, 489-515, 598 and TComTrQuant.cpp ctxIndMap4x4); generated or listed here.
+ * ========================================================================================== */
+static const int kQuantScales[6] = {26214, 23302, 20560, 18396, 16384, 14564};
+static const int kInvQuantScales[6] = {40, 45, 51, 57, 64, 72};
+static const int kGroupIdx[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
+                                  8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9};
+static const int kCtxIndMap4x4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+static const int kDst4[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
+/* |cos| samples of the 32-point HEVC core transform: c[j] ~ 64*sqrt(2)*cos(pi*j/64) */
+static const int kCos[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
+                             61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9, 4, 0};
+static const int kLumaFilter[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
+                                      {-1, 4, -10, 58, 17, -5, 1, 0},
+                                      {-1, 4, -11, 40, 40, -11, 4, -1},
+                                      {0, 1, -5, 17, 58, -10, 4, -1}};
+static const int kChromaFilter[8][4] = {{0, 64, 0, 0},   {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
+                                        {-4, 36, 36, -4}, {-4, 28, 46, -6}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
+
+/* T32[k][n] = sign * kCos[fold(k*(2n+1) mod 128)]; smaller sizes are row subsets (T_N[k] = T32[k*32/N]). */
+static int dct32(int k, int n) {
+  if (k == 0) return 64;
+  int j = (k * (2 * n + 1)) % 128;
+  int sign = 1;
+  if (j > 64) j = 128 - j;           /* cos(2pi - a) = cos(a) */
+  if (j > 32) { j = 64 - j; sign = -1; } /* cos(pi - a) = -cos(a) */
+  return sign * kCos[j];
+}
+
+void hvxo_dct_matrix(int n, int16_t *m) {
+  for (int k = 0; k < n; k++)
+    for (int x = 0; x < n; x++) m[k * n + x] = (int16_t)dct32(k * (32 / n), x);
+}
+
+static int16_t g_mat[4][32 * 32];
+static int g_tables_ready = 0;
+/* scans: [grouped][type][log2w][log2h] (TComRom.cpp:192-262 generation rules; diag = up-right) */
+static uint32_t *g_scan[2][3][6][6];
+
+static void gen_scan(uint32_t *out, int w, int h, int stride, int type, int offx, int offy) {
+  int i = 0;
+  if (type == 0) {
+    for (int d = 0; d < w + h - 1; d++) {
+      int y = d < h - 1 ? d : h - 1;
+      int x = d - y;
+      while (y >= 0 && x < w) out[i++] = (uint32_t)((y + offy) * stride + x + offx), y--, x++;
+    }
+  } else if (type == 1) {
+    for (int y = 0; y < h; y++)
+      for (int x = 0; x < w; x++) out[i++] = (uint32_t)((y + offy) * stride + x + offx);
+  } else {
+    for (int x = 0; x < w; x++)
+      for (int y = 0; y < h; y++) out[i++] = (uint32_t)((y + offy) * stride + x + offx);
+  }
+}
+
+static void init_tables(void) {
+  if (g_tables_ready) return;
+  for (int l = 0; l < 4; l++) hvxo_dct_matrix(4 << l, g_mat[l]);
+  for (int lw = 0; lw < 6; lw++)
+    for (int lh = 0; lh < 6; lh++)
+      for (int t = 0; t < 3; t++) {
+        int w = 1 << lw, h = 1 << lh;
+        g_scan[0][t][lw][lh] = (uint32_t *)malloc(sizeof(uint32_t) * w * h);
+        gen_scan(g_scan[0][t][lw][lh], w, h, w, t, 0, 0);
+        g_scan[1][t][lw][lh] = (uint32_t *)malloc(sizeof(uint32_t) * w * h);
+        if (lw >= 2 && lh >= 2) {
+          int gw = w >> 2, gh = h >> 2;
+          uint32_t cg[256];
+          gen_scan(cg, gw, gh, gw, t, 0, 0);
+          for (int g = 0; g < gw * gh; g++) {
+            int gx = cg[g] % gw, gy = cg[g] / gw;
+            gen_scan(g_scan[1][t][lw][lh] + g * 16, 4, 4, w, t, gx * 4, gy * 4);
+          }
+        } else {
+          gen_scan(g_scan[1][t][lw][lh], w, h, w, t, 0, 0);
+        }
+      }
+  g_tables_ready = 1;
+}
+
+const uint32_t *hvxo_scan(int grouped, int scan_type, int log2w, int log2h) {
+  init_tables();
+  return g_scan[grouped ? 1 : 0][scan_type][log2w][log2h];
+}
+
+/* ============================================================================================
+ * Distortion: TComRdCost.cpp
+ * ========================================================================================== */
+/* xGetSAD4..64/12/24/48/16N (:489-950): every 2^s-th row, result << s.  xGetSAD (:461) = s 0. */
+uint32_t hvxo_sad(const int16_t *org, int so, const int16_t *cur, int sc, int w, int h, int sub_shift) {
+  uint32_t sum = 0;
+  int step = 1 << sub_shift;
+  for (int y = 0; y < h; y += step)
+    for (int x = 0; x < w; x++) sum += (uint32_t)abs(org[y * so + x] - cur[y * sc + x]);
+  return sum << sub_shift;
+}
+
+/* ME dispatch (setDistParam(pattern) :306-335): widths 4/8/16/32/64/12/24/48 honour the row
+ * subsampling; any other width goes to the generic xGetSAD, which ignores it. */
+uint32_t hvxo_sad_me(const int16_t *org, int so, const int16_t *cur, int sc, int w, int h, int sub_shift) {
+  int specialised = (w == 4 || w == 8 || w == 16 || w == 32 || w == 64 || w == 12 || w == 24 || w == 48);
+  return hvxo_sad(org, so, cur, sc, w, h, specialised ? sub_shift : 0);
+}
+
+/* xCalcHADs2x2 (:1310) */
+static uint32_t had2(const int16_t *o, int so, const int16_t *c, int sc) {
+  int d0 = o[0] - c[0], d1 = o[1] - c[1], d2 = o[so] - c[sc], d3 = o[so + 1] - c[sc + 1];
+  int m0 = d0 + d2, m1 = d1 + d3, m2 = d0 - d2, m3 = d1 - d3;
+  return (uint32_t)(abs(m0 + m1) + abs(m0 - m1) + abs(m2 + m3) + abs(m2 - m3));
+}
+
+/* 1-D 4-point Hadamard in the reference's butterfly order */
+static void hadamard4(const int *in, int *out) {
+  int a0 = in[0] + in[2], a1 = in[1] + in[3], a2 = in[0] - in[2], a3 = in[1] - in[3];
+  out[0] = a0 + a1; out[1] = a0 - a1; out[2] = a2 + a3; out[3] = a2 - a3;
+}
+
+/* xCalcHADs4x4 (:1332): 2-D Hadamard of the 4x4 difference, (sum|.|+1)>>1.  The absolute sum
+ * of a full 2-D Hadamard is independent of the row/column order of the butterflies. */
+static uint32_t had4(const int16_t *o, int so, const int16_t *c, int sc) {
+  int d[4][4], t[4][4];
+  for (int y = 0; y < 4; y++)
+    for (int x = 0; x < 4; x++) d[y][x] = o[y * so + x] - c[y * sc + x];
+  for (int y = 0; y < 4; y++) hadamard4(d[y], t[y]);
+  uint32_t s = 0;
+  for (int x = 0; x < 4; x++) {
+    int col[4] = {t[0][x], t[1][x], t[2][x], t[3][x]}, r[4];
+    hadamard4(col, r);
+    for (int k = 0; k < 4; k++) s += (uint32_t)abs(r[k]);
+  }
+  return (s + 1) >> 1;
+}
+
+static void hadamard8(const int *in, int *out) {
+  int a[8], b[8];
+  for (int i = 0; i < 4; i++) { a[i] = in[i] + in[i + 4]; a[i + 4] = in[i] - in[i + 4]; }
+  b[0] = a[0] + a[2]; b[1] = a[1] + a[3]; b[2] = a[0] - a[2]; b[3] = a[1] - a[3];
+  b[4] = a[4] + a[6]; b[5] = a[5] + a[7]; b[6] = a[4] - a[6]; b[7] = a[5] - a[7];
+  for (int i = 0; i < 4; i++) { out[2 * i] = b[2 * i] + b[2 * i + 1]; out[2 * i + 1] = b[2 * i] - b[2 * i + 1]; }
+}
+
+/* xCalcHADs8x8 (:1428): (sum|.|+2)>>2 */
+static uint32_t had8(const int16_t *o, int so, const int16_t *c, int sc) {
+  int d[8][8], t[8][8];
+  for (int y = 0; y < 8; y++)
+    for (int x = 0; x < 8; x++) d[y][x] = o[y * so + x] - c[y * sc + x];
+  for (int y = 0; y < 8; y++) hadamard8(d[y], t[y]);
+  uint32_t s = 0;
+  for (int x = 0; x < 8; x++) {
+    int col[8], r[8];
+    for (int y = 0; y < 8; y++) col[y] = t[y][x];
+    hadamard8(col, r);
+    for (int k = 0; k < 8; k++) s += (uint32_t)abs(r[k]);
+  }
+  return (s + 2) >> 2;
+}
+
+/* xGetHADs (:1526): tile by 8x8 if both dims % 8 == 0, else 4x4, else 2x2 */
+uint32_t hvxo_satd(const int16_t *org, int so, const int16_t *cur, int sc, int w, int h) {
+  uint32_t sum = 0;
+  int t = (w % 8 == 0 && h % 8 == 0) ? 8 : (w % 4 == 0 && h % 4 == 0) ? 4 : 2;
+  for (int y = 0; y < h; y += t)
+    for (int x = 0; x < w; x += t) {
+      const int16_t *o = org + y * so + x, *c = cur + y * sc + x;
+      sum += t == 8 ? had8(o, so, c, sc) : t == 4 ? had4(o, so, c, sc) : had2(o, so, c, sc);
+    }
+  return sum;
+}
+
+/* xGetSSE* (:959-1300) */
+uint32_t hvxo_sse(const int16_t *org, int so, const int16_t *cur, int sc, int w, int h) {
+  uint32_t sum = 0;
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      int d = org[y * so + x] - cur[y * sc + x];
+      sum += (uint32_t)(d * d);
+    }
+  return sum;
+}
+
+/* getDistPart for a chroma component (:443-446): (Distortion)(weight * sse) */
+uint32_t hvxo_sse_weighted(const int16_t *org, int so, const int16_t *cur, int sc, int w, int h, double weight) {
+  return (uint32_t)(weight * (double)hvxo_sse(org, so, cur, sc, w, h));
+}
+
+/* xGetExpGolombNumberOfBits (:279) */
+uint32_t hvxo_eg_bits(int v) {
+  uint32_t len = 1;
+  uint32_t t = (v <= 0) ? ((uint32_t)(-v) << 1) + 1 : (uint32_t)v << 1;
+  while (t != 1) { t >>= 1; len += 2; }
+  return len;
+}
+
+/* ============================================================================================
+ * Interpolation: TComInterpolationFilter.cpp (8-bit: IF_INTERNAL_PREC 14, IF_FILTER_PREC 6)
+ * ========================================================================================== */
+#define IF_OFFS 8192
+static inline int16_t clip_pel(int v) { return (int16_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+/* filterCopy (:94) */
+static void filter_copy(const int16_t *src, int ss, int16_t *dst, int ds, int w, int h, int is_first, int is_last) {
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      int v = src[y * ss + x];
+      if (is_first == is_last) dst[y * ds + x] = (int16_t)v;
+      else if (is_first) dst[y * ds + x] = (int16_t)((int16_t)(v << 6) - IF_OFFS);
+      else dst[y * ds + x] = clip_pel((v + IF_OFFS + 32) >> 6);
+    }
+}
+
+/* filter<N,isVertical,isFirst,isLast> (:172-257) */
+static void filter_n(int ntaps, const int *c, int vertical, const int16_t *src, int ss, int16_t *dst, int ds,
+                     int w, int h, int is_first, int is_last) {
+  int cstride = vertical ? ss : 1;
+  src -= (ntaps / 2 - 1) * cstride;
+  int head = 6, shift = 6, offset;
+  if (is_last) {
+    shift += is_first ? 0 : head;
+    offset = 1 << (shift - 1);
+    offset += is_first ? 0 : IF_OFFS << 6;
+  } else {
+    shift -= is_first ? head : 0;
+    offset = is_first ? -IF_OFFS << shift : 0;
+  }
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      int sum = 0;
+      for (int k = 0; k < ntaps; k++) sum += src[y * ss + x + k * cstride] * c[k];
+      int16_t v = (int16_t)((sum + offset) >> shift);
+      if (is_last) v = clip_pel(v);
+      dst[y * ds + x] = v;
+    }
+}
+
+/* filterHor (:341); chroma frac is the 1/8-pel index at 4:2:0 (frac << (1 - csx), csx = 1) */
+void hvxo_filter_hor(int is_luma, const int16_t *src, int ss, int16_t *dst, int ds, int w, int h, int frac, int is_last) {
+  if (frac == 0) filter_copy(src, ss, dst, ds, w, h, 1, is_last);
+  else if (is_luma) filter_n(8, kLumaFilter[frac], 0, src, ss, dst, ds, w, h, 1, is_last);
+  else filter_n(4, kChromaFilter[frac], 0, src, ss, dst, ds, w, h, 1, is_last);
+}
+
+/* filterVer (:377) */
+void hvxo_filter_ver(int is_luma, const int16_t *src, int ss, int16_t *dst, int ds, int w, int h, int frac,
+                     int is_first, int is_last) {
+  if (frac == 0) filter_copy(src, ss, dst, ds, w, h, is_first, is_last);
+  else if (is_luma) filter_n(8, kLumaFilter[frac], 1, src, ss, dst, ds, w, h, is_first, is_last);
+  else filter_n(4, kChromaFilter[frac], 1, src, ss, dst, ds, w, h, is_first, is_last);
+}
+
+/* Quarter-sample luma block at quarter-pel MV, standard two-stage (TComPrediction::xPredInterBlk
+ * TComPrediction.cpp:668-706 order: horizontal non-last into 16-bit, then vertical last). */
+void hvxo_luma_block_qpel(const uint8_t *ref, int stride, int x, int y, int mvx, int mvy, int w, int h, int16_t *out, int os) {
+  int fx = mvx & 3, fy = mvy & 3, ix = x + (mvx >> 2), iy = y + (mvy >> 2);
+  for (int r = 0; r < h; r++)
+    for (int c = 0; c < w; c++) {
+      const uint8_t *p = ref + (iy + r) * stride + ix + c;
+      int v;
+      if (!fx && !fy) v = p[0];
+      else if (!fy) {
+        int s = 0;
+        for (int k = 0; k < 8; k++) s += kLumaFilter[fx][k] * p[k - 3];
+        v = clip_pel((s + 32) >> 6);
+      } else if (!fx) {
+        int s = 0;
+        for (int k = 0; k < 8; k++) s += kLumaFilter[fy][k] * p[(k - 3) * stride];
+        v = clip_pel((s + 32) >> 6);
+      } else {
+        int s2 = 0;
+        for (int t = 0; t < 8; t++) {
+          int s = 0;
+          for (int k = 0; k < 8; k++) s += kLumaFilter[fx][k] * p[(t - 3) * stride + k - 3];
+          s2 += kLumaFilter[fy][t] * (int16_t)(s - IF_OFFS);
+        }
+        v = clip_pel((s2 + (1 << 11) + (IF_OFFS << 6)) >> 12);
+      }
+      out[r * os + c] = (int16_t)v;
+    }
+}
+
+/* ============================================================================================
+ * Transforms: xTrMxN / xITrMxN (TComTrQuant.cpp:860-987).  Partial butterflies (:388-848) are
+ * exact integer matrix products; written here as the products they compute.
+ * 8-bit: forward shift_1st = log2 - 1, shift_2nd = log2 + 6; inverse 7 and 12, clip to 16 bits.
+ * ========================================================================================== */
+static int mat(int n, int use_dst, int k, int x) {
+  if (use_dst) return kDst4[k][x];
+  init_tables();
+  int l = n == 4 ? 0 : n == 8 ? 1 : n == 16 ? 2 : 3;
+  return g_mat[l][k * n + x];
+}
+
+void hvxo_fwd_transform(const int32_t *block, int32_t *coeff, int n, int use_dst) {
+  int log2 = n == 4 ? 2 : n == 8 ? 3 : n == 16 ? 4 : 5;
+  int s1 = log2 - 1, s2 = log2 + 6;
+  int a1 = s1 > 0 ? 1 << (s1 - 1) : 0, a2 = 1 << (s2 - 1);
+  int32_t tmp[32 * 32];
+  for (int y = 0; y < n; y++)
+    for (int u = 0; u < n; u++) {
+      int s = 0;
+      for (int x = 0; x < n; x++) s += mat(n, use_dst, u, x) * block[y * n + x];
+      tmp[u * n + y] = (s + a1) >> s1;
+    }
+  for (int u = 0; u < n; u++)
+    for (int v = 0; v < n; v++) {
+      int s = 0;
+      for (int y = 0; y < n; y++) s += mat(n, use_dst, v, y) * tmp[u * n + y];
+      coeff[v * n + u] = (s + a2) >> s2;
+    }
+}
+
+static inline int clip3(int lo, int hi, int v) { return v < lo ? lo : v > hi ? hi : v; }
+
+void hvxo_inv_transform(const int32_t *coeff, int32_t *block, int n, int use_dst) {
+  int32_t tmp[32 * 32];
+  for (int u = 0; u < n; u++)
+    for (int y = 0; y < n; y++) {
+      int s = 0;
+      for (int v = 0; v < n; v++) s += mat(n, use_dst, v, y) * coeff[v * n + u];
+      tmp[u * n + y] = clip3(-32768, 32767, (s + 64) >> 7);
+    }
+  for (int y = 0; y < n; y++)
+    for (int x = 0; x < n; x++) {
+      int s = 0;
+      for (int u = 0; u < n; u++) s += mat(n, use_dst, u, x) * tmp[u * n + y];
+      block[y * n + x] = clip3(-32768, 32767, (s + 2048) >> 12);
+    }
+}
+
+/* ============================================================================================
+ * Quantisation.  TComTrQuant.cpp:991-1430, 2129-3052; context selection from
+ * TComChromaFormat.h:203-262 / TComChromaFormat.cpp:96-150 and ContextTables.h.
+ * ========================================================================================== */
+typedef struct {
+  const uint32_t *scan, *scan_cg;
+  int wg, hg;          /* width/height in 4x4 groups */
+  int scan_type;
+  int first_sig_ctx;   /* firstSignificanceMapContext */
+} coding_params;
+
+static const int kSigCtxSetStart[2][4] = {{0, 9, 21, 27}, {0, 9, 12, 15}};
+
+static void get_coding_params(const hvx_tu_desc *tu, coding_params *cp) {
+  int lw = tu->width == 4 ? 2 : tu->width == 8 ? 3 : tu->width == 16 ? 4 : 5;
+  int lh = tu->height == 4 ? 2 : tu->height == 8 ? 3 : tu->height == 16 ? 4 : 5;
+  int ch = tu->comp ? 1 : 0;
+  cp->scan_type = tu->scan_type;
+  cp->wg = tu->width >> 2;
+  cp->hg = tu->height >> 2;
+  cp->scan = hvxo_scan(1, tu->scan_type, lw, lh);
+  cp->scan_cg = hvxo_scan(0, tu->scan_type, lw - 2, lh - 2);
+  if (tu->ts_context && (tu->transquant_bypass || tu->transform_skip)) cp->first_sig_ctx = kSigCtxSetStart[ch][3];
+  else if (tu->width == 4 && tu->height == 4) cp->first_sig_ctx = kSigCtxSetStart[ch][0];
+  else if (tu->width == 8 && tu->height == 8) cp->first_sig_ctx = kSigCtxSetStart[ch][1] + (tu->scan_type != 0 ? (ch ? 0 : 6) : 0);
+  else cp->first_sig_ctx = kSigCtxSetStart[ch][2];
+}
+
+static int transform_shift(const hvx_tu_desc *tu) {
+  int s = tu->max_log2_tr_range - tu->bit_depth - tu->log2_size;
+  if (tu->transform_skip && tu->extended_precision && s < 0) s = 0;
+  return s;
+}
+
+/* calcPatternSigCtx (:2682) */
+static int pattern_sig_ctx(const uint32_t *flags, int cx, int cy, int wg, int hg) {
+  if (wg <= 1 && hg <= 1) return 0;
+  int r = cx < wg - 1 ? (flags[cy * wg + cx + 1] != 0) : 0;
+  int b = cy < hg - 1 ? (flags[(cy + 1) * wg + cx] != 0) : 0;
+  return r + (b << 1);
+}
+
+/* getSigCtxInc (:2717) */
+static int sig_ctx_inc(int pattern, const coding_params *cp, int scan_pos, int lw, int lh, int ch) {
+  if (cp->first_sig_ctx == kSigCtxSetStart[ch][3]) return kSigCtxSetStart[ch][3];
+  int raster = (int)cp->scan[scan_pos];
+  int py = raster >> lw, px = raster - (py << lw);
+  if (px + py == 0) return 0;
+  int offset;
+  if (lw == 2 && lh == 2) offset = kCtxIndMap4x4[4 * py + px];
+  else {
+    int cnt;
+    switch (pattern) {
+      case 0: { int t = (px & 3) + (py & 3); cnt = t >= 3 ? 0 : t >= 1 ? 1 : 2; } break;
+      case 1: { int y = py & 3; cnt = y >= 2 ? 0 : y >= 1 ? 1 : 2; } break;
+      case 2: { int x = px & 3; cnt = x >= 2 ? 0 : x >= 1 ? 1 : 2; } break;
+      default: cnt = 2; break;
+    }
+    int not_first = ((px >> 2) + (py >> 2)) > 0;
+    offset = (not_first ? (ch ? 0 : 3) : 0) + cnt;
+  }
+  return cp->first_sig_ctx + offset;
+}
+
+/* getSigCoeffGroupCtxInc (:3033) */
+static int sig_cg_ctx(const uint32_t *flags, int cx, int cy, int wg, int hg) {
+  int r = cx < wg - 1 ? (flags[cy * wg + cx + 1] != 0) : 0;
+  int b = cy < hg - 1 ? (flags[(cy + 1) * wg + cx] != 0) : 0;
+  return (r + b) != 0;
+}
+
+/* getContextSetIndex (TComChromaFormat.h:243) */
+static int ctx_set_index(int comp, int subset, int found_gt1) {
+  return (comp ? 4 : 0) + ((comp == 0 && subset > 0) ? 2 : 0) + (found_gt1 ? 1 : 0);
+}
+
+typedef struct {
+  const hvx_estbits *est;
+  double lambda;
+} rd_ctx;
+
+static inline double icost(const rd_ctx *r, double rate) { return r->lambda * rate; }  /* xGetICost :3012 */
+
+/* xGetICRate (:2891) */
+static int ic_rate(const rd_ctx *r, uint32_t level, int ctx_one, int ctx_abs, int rice, uint32_t c1_idx, uint32_t c2_idx,
+                   int limited_prefix, int max_log2) {
+  int rate = 32768;
+  uint32_t base = (c1_idx < 8) ? (2 + (c2_idx < 1)) : 1;
+  if (level >= base) {
+    uint32_t symbol = level - base;
+    if (symbol < (3u << rice)) {
+      uint32_t len = symbol >> rice;
+      rate += (int)((len + 1 + rice) << 15);
+    } else if (limited_prefix) {
+      uint32_t maxp = 32 - (3 + max_log2), prefix = 0, suffix = (symbol >> rice) - 3;
+      while (prefix < maxp && suffix > ((2u << prefix) - 2)) prefix++;
+      uint32_t suffix_len = prefix == maxp ? (uint32_t)(max_log2 - rice) : prefix + 1;
+      rate += (int)((3 + prefix + suffix_len + rice) << 15);
+    } else {
+      uint32_t len = rice;
+      symbol = symbol - (3u << rice);
+      while (symbol >= (1u << len)) { symbol -= (1u << (len++)); }
+      rate += (int)((3 + len + 1 - rice + len) << 15);
+    }
+    if (c1_idx < 8) {
+      rate += r->est->greaterOneBits[ctx_one][1];
+      if (c2_idx < 1) rate += r->est->levelAbsBits[ctx_abs][1];
+    }
+  } else if (level == 1) {
+    rate += r->est->greaterOneBits[ctx_one][0];
+  } else if (level == 2) {
+    rate += r->est->greaterOneBits[ctx_one][1];
+    rate += r->est->levelAbsBits[ctx_abs][0];
+  } else {
+    rate = 0;
+  }
+  return rate;
+}
+
+static inline double rate_sig(const rd_ctx *r, int v, int ctx) { return icost(r, (double)r->est->significantBits[ctx][v]); }
+static inline double rate_sig_cg(const rd_ctx *r, int v, int ctx) { return icost(r, (double)r->est->significantCoeffGroupBits[ctx][v]); }
+
+/* xGetRateLast (:2982) */
+static double rate_last(const rd_ctx *r, int px, int py, int ch) {
+  int cx = kGroupIdx[px], cy = kGroupIdx[py];
+  double c = (double)(r->est->lastXBits[ch][cx] + r->est->lastYBits[ch][cy]);
+  if (cx > 3) c += 32768.0 * ((cx - 2) >> 1);
+  if (cy > 3) c += 32768.0 * ((cy - 2) >> 1);
+  return icost(r, c);
+}
+
+/* wrapping int32 helpers (Intermediate_Int is 32-bit in the reference Main build) */
+static inline int32_t shl32(int32_t v, int s) { return (int32_t)((uint32_t)v << s); }
+static inline int32_t sub32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+
+/* xGetCodedLevel (:2822) */
+static uint32_t coded_level(const rd_ctx *r, double *cost, double *cost0, double *cost_sig, int32_t level_double,
+                            uint32_t max_abs, int ctx_sig, int ctx_one, int ctx_abs, int rice, uint32_t c1_idx,
+                            uint32_t c2_idx, int qbits, double err_scale, int last, int limited, int max_log2) {
+  double cur_sig = 0;
+  uint32_t best = 0;
+  if (!last && max_abs < 3) {
+    *cost_sig = rate_sig(r, 0, ctx_sig);
+    *cost = *cost0 + *cost_sig;
+    if (max_abs == 0) return best;
+  } else {
+    *cost = 1.7e+308;  /* MAX_DOUBLE (CommonDef.h) */
+  }
+  if (!last) cur_sig = rate_sig(r, 1, ctx_sig);
+  uint32_t min_abs = max_abs > 1 ? max_abs - 1 : 1;
+  for (int lv = (int)max_abs; lv >= (int)min_abs; lv--) {
+    double err = (double)sub32(level_double, shl32(lv, qbits));
+    double c = err * err * err_scale + icost(r, (double)ic_rate(r, (uint32_t)lv, ctx_one, ctx_abs, rice, c1_idx, c2_idx, limited, max_log2));
+    c += cur_sig;
+    if (c < *cost) { best = (uint32_t)lv; *cost = c; *cost_sig = cur_sig; }
+  }
+  return best;
+}
+
+/* setErrScaleCoeff (:3106-3129), flat scaling list */
+static double err_scale(const hvx_tu_desc *tu) {
+  int ts = tu->max_log2_tr_range - tu->bit_depth - tu->log2_size;
+  double e = (double)(1 << 15);
+  e = e * pow(2.0, (-2.0 * ts));
+  int q = kQuantScales[tu->qp_rem];
+  return e / q / q / (1 << 0);
+}
+
+/* xRateDistOptQuant (:2129-2671) */
+static void rdoq(const hvx_tu_desc *tu, const hvx_estbits *est, const int32_t *src, int32_t *dst, int32_t *arl, int32_t *abs_sum) {
+  const int w = tu->width, h = tu->height, ch = tu->comp ? 1 : 0, comp = tu->comp;
+  const int lw = w == 4 ? 2 : w == 8 ? 3 : w == 16 ? 4 : 5, lh = h == 4 ? 2 : h == 8 ? 3 : h == 16 ? 4 : 5;
+  const int n = w * h, ext = tu->extended_precision, max_log2 = tu->max_log2_tr_range;
+  const int ts = transform_shift(tu);
+  rd_ctx rc = {est, tu->lambda};
+  const uint32_t rice0 = (uint32_t)tu->golomb_rice_stat / 4;
+  uint32_t rice = rice0;
+  double block_uncoded = 0;
+  double cost_coeff[1024], cost_sig[1024], cost_coeff0[1024];
+  int rate_up[1024], rate_down[1024], sig_delta[1024];
+  int32_t delta_u[1024];
+  memset(cost_coeff, 0, sizeof(double) * n);
+  memset(cost_sig, 0, sizeof(double) * n);
+  memset(rate_up, 0, sizeof(int) * n);
+  memset(rate_down, 0, sizeof(int) * n);
+  memset(sig_delta, 0, sizeof(int) * n);
+  memset(delta_u, 0, sizeof(int32_t) * n);
+  if (arl) memset(arl, 0, sizeof(int32_t) * n);
+  const int qbits = 14 + tu->qp_per + ts;
+  const double escale = err_scale(tu);
+  const int qcoef = kQuantScales[tu->qp_rem];
+  const int32_t ecmax = (1 << max_log2) - 1, ecmin = -(1 << max_log2);
+  const int qbits_c = qbits - 7, add_c = 1 << (qbits_c - 1);
+  coding_params cp;
+  get_coding_params(tu, &cp);
+  double cost_cg_sig[64];
+  uint32_t sig_cg[64];
+  memset(cost_cg_sig, 0, sizeof(cost_cg_sig));
+  memset(sig_cg, 0, sizeof(sig_cg));
+  int cg_last = -1, last = -1;
+  uint32_t ctx_set = 0, c1_idx = 0, c2_idx = 0;
+  int c1 = 1, c2 = 0;
+  double base_cost = 0;
+  const int ncg = n >> 4;
+  const int sig_off = ch ? 28 : 0;
+
+  for (int cgp = ncg - 1; cgp >= 0; cgp--) {
+    int cgblk = (int)cp.scan_cg[cgp];
+    int cy = cgblk / cp.wg, cx = cgblk - cy * cp.wg;
+    int nnz_before0 = 0;
+    double coded_level_dist = 0, uncoded_dist = 0, sig_cost = 0, sig_cost0 = 0;
+    int pattern = pattern_sig_ctx(sig_cg, cx, cy, cp.wg, cp.hg);
+    for (int pin = 15; pin >= 0; pin--) {
+      int sp = cgp * 16 + pin;
+      int blk = (int)cp.scan[sp];
+      int64_t tmp = (int64_t)abs(src[blk]) * qcoef;
+      int64_t lim = (int64_t)INT32_MAX - ((int64_t)1 << (qbits - 1));
+      int32_t ld = (int32_t)(tmp < lim ? tmp : lim);
+      if (tu->adaptive_qp_select && arl) arl[blk] = (ld + add_c) >> qbits_c;
+      uint32_t q = (uint32_t)((ld + (1 << (qbits - 1))) >> qbits);
+      uint32_t max_abs = (uint32_t)ecmax < q ? (uint32_t)ecmax : q;
+      double err = (double)ld;
+      cost_coeff0[sp] = err * err * escale;
+      block_uncoded += cost_coeff0[sp];
+      dst[blk] = (int32_t)max_abs;
+      if (max_abs > 0 && last < 0) {
+        last = sp;
+        ctx_set = (uint32_t)ctx_set_index(comp, sp >> 4, 0);
+        cg_last = cgp;
+      }
+      if (last >= 0) {
+        uint32_t level;
+        int ctx_one = 4 * (int)ctx_set + c1, ctx_abs = (int)ctx_set + c2;
+        if (sp == last) {
+          level = coded_level(&rc, &cost_coeff[sp], &cost_coeff0[sp], &cost_sig[sp], ld, max_abs, sig_off, ctx_one,
+                              ctx_abs, (int)rice, c1_idx, c2_idx, qbits, escale, 1, ext, max_log2);
+        } else {
+          int ctx_sig = sig_off + sig_ctx_inc(pattern, &cp, sp, lw, lh, ch);
+          level = coded_level(&rc, &cost_coeff[sp], &cost_coeff0[sp], &cost_sig[sp], ld, max_abs, ctx_sig, ctx_one,
+                              ctx_abs, (int)rice, c1_idx, c2_idx, qbits, escale, 0, ext, max_log2);
+          sig_delta[blk] = est->significantBits[ctx_sig][1] - est->significantBits[ctx_sig][0];
+        }
+        delta_u[blk] = sub32(ld, shl32((int32_t)level, qbits)) >> (qbits - 8);
+        if (level > 0) {
+          int now = ic_rate(&rc, level, ctx_one, ctx_abs, (int)rice, c1_idx, c2_idx, ext, max_log2);
+          rate_up[blk] = ic_rate(&rc, level + 1, ctx_one, ctx_abs, (int)rice, c1_idx, c2_idx, ext, max_log2) - now;
+          rate_down[blk] = ic_rate(&rc, level - 1, ctx_one, ctx_abs, (int)rice, c1_idx, c2_idx, ext, max_log2) - now;
+        } else {
+          rate_up[blk] = est->greaterOneBits[ctx_one][0];
+        }
+        dst[blk] = (int32_t)level;
+        base_cost += cost_coeff[sp];
+        uint32_t base = (c1_idx < 8) ? (2 + (c2_idx < 1)) : 1;
+        if (level >= base && level > 3u * (1u << rice)) rice = tu->persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
+        if (level >= 1) c1_idx++;
+        if (level > 1) { c1 = 0; c2 += (c2 < 2); c2_idx++; }
+        else if (c1 < 3 && c1 > 0 && level) c1++;
+        if ((sp % 16 == 0) && sp > 0) {
+          ctx_set = (uint32_t)ctx_set_index(comp, (sp - 1) >> 4, c1 == 0);
+          c1 = 1; c2 = 0; c1_idx = 0; c2_idx = 0;
+          rice = rice0;
+        }
+      } else {
+        base_cost += cost_coeff0[sp];
+      }
+      sig_cost += cost_sig[sp];
+      if (pin == 0) sig_cost0 = cost_sig[sp];
+      if (dst[blk]) {
+        sig_cg[cgblk] = 1;
+        coded_level_dist += cost_coeff[sp] - cost_sig[sp];
+        uncoded_dist += cost_coeff0[sp];
+        if (pin != 0) nnz_before0++;
+      }
+    }
+    if (cg_last >= 0) {
+      if (cgp) {
+        if (sig_cg[cgblk] == 0) {
+          int ctx = sig_cg_ctx(sig_cg, cx, cy, cp.wg, cp.hg);
+          base_cost += rate_sig_cg(&rc, 0, ctx) - sig_cost;
+          cost_cg_sig[cgp] = rate_sig_cg(&rc, 0, ctx);
+        } else if (cgp < cg_last) {
+          if (nnz_before0 == 0) { base_cost -= sig_cost0; sig_cost -= sig_cost0; }
+          double cost_zero_cg = base_cost;
+          int ctx = sig_cg_ctx(sig_cg, cx, cy, cp.wg, cp.hg);
+          base_cost += rate_sig_cg(&rc, 1, ctx);
+          cost_zero_cg += rate_sig_cg(&rc, 0, ctx);
+          cost_cg_sig[cgp] = rate_sig_cg(&rc, 1, ctx);
+          cost_zero_cg += uncoded_dist;
+          cost_zero_cg -= coded_level_dist;
+          cost_zero_cg -= sig_cost;
+          if (cost_zero_cg < base_cost) {
+            sig_cg[cgblk] = 0;
+            base_cost = cost_zero_cg;
+            cost_cg_sig[cgp] = rate_sig_cg(&rc, 0, ctx);
+            for (int pin = 15; pin >= 0; pin--) {
+              int sp = cgp * 16 + pin;
+              int blk = (int)cp.scan[sp];
+              if (dst[blk]) { dst[blk] = 0; cost_coeff[sp] = cost_coeff0[sp]; cost_sig[sp] = 0; }
+            }
+          }
+        }
+      } else {
+        sig_cg[cgblk] = 1;
+      }
+    }
+  }
+
+  if (last < 0) return;
+
+  double best_cost;
+  int best_last_p1 = 0;
+  if (!tu->is_intra && ch == 0 && tu->tr_idx == 0) {
+    best_cost = block_uncoded + icost(&rc, (double)est->blockRootCbpBits[0][0]);
+    base_cost += icost(&rc, (double)est->blockRootCbpBits[0][1]);
+  } else {
+    int ctx = tu->ctx_qt_cbf + (ch ? 5 : 0);
+    best_cost = block_uncoded + icost(&rc, (double)est->blockCbpBits[ctx][0]);
+    base_cost += icost(&rc, (double)est->blockCbpBits[ctx][1]);
+  }
+  int found = 0;
+  for (int cgp = cg_last; cgp >= 0; cgp--) {
+    int cgblk = (int)cp.scan_cg[cgp];
+    base_cost -= cost_cg_sig[cgp];
+    if (sig_cg[cgblk]) {
+      for (int pin = 15; pin >= 0; pin--) {
+        int sp = cgp * 16 + pin;
+        if (sp > last) continue;
+        int blk = (int)cp.scan[sp];
+        if (dst[blk]) {
+          int py = blk >> lw, px = blk - (py << lw);
+          double cl = cp.scan_type == 2 ? rate_last(&rc, py, px, ch) : rate_last(&rc, px, py, ch);
+          double total = base_cost + cl - cost_sig[sp];
+          if (total < best_cost) { best_last_p1 = sp + 1; best_cost = total; }
+          if (dst[blk] > 1) { found = 1; break; }
+          base_cost -= cost_coeff[sp];
+          base_cost += cost_coeff0[sp];
+        } else {
+          base_cost -= cost_sig[sp];
+        }
+      }
+      if (found) break;
+    }
+  }
+  for (int sp = 0; sp < best_last_p1; sp++) {
+    int blk = (int)cp.scan[sp];
+    int32_t lv = dst[blk];
+    *abs_sum += lv;
+    dst[blk] = src[blk] < 0 ? -lv : lv;
+  }
+  for (int sp = best_last_p1; sp <= last; sp++) dst[cp.scan[sp]] = 0;
+
+  if (tu->sign_hiding && *abs_sum >= 2) {
+    const double iq = (double)kInvQuantScales[tu->qp_rem];
+    int64_t rd_factor = (int64_t)(iq * iq * (1 << (2 * tu->qp_per)) / tu->lambda / 16 / (1 << 0) + 0.5);
+    int last_cg = -1;
+    for (int sub = (n - 1) >> 4; sub >= 0; sub--) {
+      int pos = sub << 4, first_nz = 16, last_nz = -1, abs_in = 0, k;
+      for (k = 15; k >= 0; k--) if (dst[cp.scan[k + pos]]) { last_nz = k; break; }
+      for (k = 0; k < 16; k++) if (dst[cp.scan[k + pos]]) { first_nz = k; break; }
+      for (k = first_nz; k <= last_nz; k++) abs_in += dst[cp.scan[k + pos]];
+      if (last_nz >= 0 && last_cg == -1) last_cg = 1;
+      if (last_nz - first_nz >= 4) {
+        uint32_t signbit = dst[cp.scan[pos + first_nz]] > 0 ? 0 : 1;
+        if (signbit != (uint32_t)(abs_in & 1)) {
+          int64_t min_inc = INT64_MAX, cur = INT64_MAX;
+          int min_pos = -1, final_change = 0, cur_change = 0;
+          for (k = (last_cg == 1 ? last_nz : 15); k >= 0; k--) {
+            int blk = (int)cp.scan[k + pos];
+            if (dst[blk] != 0) {
+              int64_t up = rd_factor * (-delta_u[blk]) + rate_up[blk];
+              int64_t down = rd_factor * (delta_u[blk]) + rate_down[blk] - ((abs(dst[blk]) == 1) ? sig_delta[blk] : 0);
+              if (last_cg == 1 && last_nz == k && abs(dst[blk]) == 1) down -= (4 << 15);
+              if (up < down) { cur = up; cur_change = 1; }
+              else {
+                cur_change = -1;
+                cur = (k == first_nz && abs(dst[blk]) == 1) ? INT64_MAX : down;
+              }
+            } else {
+              cur = rd_factor * (-(abs(delta_u[blk]))) + (1 << 15) + rate_up[blk] + sig_delta[blk];
+              cur_change = 1;
+              if (k < first_nz) {
+                uint32_t ts_bit = src[blk] >= 0 ? 0 : 1;
+                if (ts_bit != signbit) cur = INT64_MAX;
+              }
+            }
+            if (cur < min_inc) { min_inc = cur; final_change = cur_change; min_pos = blk; }
+          }
+          if (dst[min_pos] == ecmax || dst[min_pos] == ecmin) final_change = -1;
+          if (src[min_pos] >= 0) dst[min_pos] += final_change;
+          else dst[min_pos] -= final_change;
+        }
+      }
+      if (last_cg == 1) last_cg = 0;
+    }
+  }
+}
+
+/* signBitHidingHDQ (:991) */
+static void sbh_hdq(int32_t *q, const int32_t *coef, const int32_t *delta_u, const coding_params *cp, int n, int max_log2) {
+  const int32_t ecmax = (1 << max_log2) - 1, ecmin = -(1 << max_log2);
+  int last_cg = -1;
+  for (int sub = (n - 1) >> 4; sub >= 0; sub--) {
+    int pos = sub << 4, first_nz = 16, last_nz = -1, abs_in = 0, k;
+    for (k = 15; k >= 0; k--) if (q[cp->scan[k + pos]]) { last_nz = k; break; }
+    for (k = 0; k < 16; k++) if (q[cp->scan[k + pos]]) { first_nz = k; break; }
+    for (k = first_nz; k <= last_nz; k++) abs_in += q[cp->scan[k + pos]];
+    if (last_nz >= 0 && last_cg == -1) last_cg = 1;
+    if (last_nz - first_nz >= 4) {
+      uint32_t signbit = q[cp->scan[pos + first_nz]] > 0 ? 0 : 1;
+      if (signbit != (uint32_t)(abs_in & 1)) {
+        int32_t cur = INT32_MAX, min_inc = INT32_MAX;
+        int min_pos = -1, final_change = 0, cur_change = 0;
+        for (k = (last_cg == 1 ? last_nz : 15); k >= 0; k--) {
+          int blk = (int)cp->scan[k + pos];
+          if (q[blk] != 0) {
+            if (delta_u[blk] > 0) { cur = -delta_u[blk]; cur_change = 1; }
+            else if (k == first_nz && abs(q[blk]) == 1) cur = INT32_MAX;
+            else { cur = delta_u[blk]; cur_change = -1; }
+          } else if (k < first_nz) {
+            uint32_t tsb = coef[blk] >= 0 ? 0 : 1;
+            if (tsb != signbit) cur = INT32_MAX;
+            else { cur = -delta_u[blk]; cur_change = 1; }
+          } else {
+            cur = -delta_u[blk]; cur_change = 1;
+          }
+          if (cur < min_inc) { min_inc = cur; final_change = cur_change; min_pos = blk; }
+        }
+        if (q[min_pos] == ecmax || q[min_pos] == ecmin) final_change = -1;
+        if (coef[min_pos] >= 0) q[min_pos] += final_change;
+        else q[min_pos] -= final_change;
+      }
+    }
+    if (last_cg == 1) last_cg = 0;
+  }
+}
+
+/* xQuant (:1126) incl. T0196 selective RDOQ (xNeedRDOQ :1257) */
+void hvxo_quant(const hvx_tu_desc *tu, const hvx_estbits *est, const int32_t *coef, int32_t *levels, int32_t *arl, int32_t *abs_sum) {
+  const int n = tu->width * tu->height;
+  const int ts = transform_shift(tu);
+  const int qbits = 14 + tu->qp_per + ts;
+  const int qc = kQuantScales[tu->qp_rem];
+  *abs_sum = 0;
+  int use_rdoq = tu->transform_skip ? tu->use_rdoq_ts : tu->use_rdoq;
+  if (use_rdoq) {
+    int need = 1;
+    if (tu->selective_rdoq) {
+      int add = (tu->comp == 0 ? 171 : 256) << (qbits - 9);
+      need = 0;
+      for (int i = 0; i < n && !need; i++) {
+        int64_t t = (int64_t)abs(coef[i]) * qc;
+        if ((int32_t)((t + add) >> qbits) != 0) need = 1;
+      }
+    }
+    if (need) rdoq(tu, est, coef, levels, arl, abs_sum);
+    else { memset(levels, 0, sizeof(int32_t) * n); *abs_sum = 0; }
+    return;
+  }
+  coding_params cp;
+  get_coding_params(tu, &cp);
+  const int32_t ecmax = (1 << tu->max_log2_tr_range) - 1, ecmin = -(1 << tu->max_log2_tr_range);
+  int32_t delta_u[1024];
+  const int add = (tu->slice_type == 2 ? 171 : 85) << (qbits - 9);
+  const int qbits8 = qbits - 8;
+  const int qbits_c = qbits - 7, add_c = 1 << (qbits_c - 1);
+  for (int i = 0; i < n; i++) {
+    int32_t lv = coef[i];
+    int sign = lv < 0 ? -1 : 1;
+    int64_t t = (int64_t)abs(lv) * qc;
+    if (tu->adaptive_qp_select && arl) arl[i] = (int32_t)((t + add_c) >> qbits_c);
+    int32_t qm = (int32_t)((t + add) >> qbits);
+    delta_u[i] = (int32_t)((t - (int64_t)shl32(qm, qbits)) >> qbits8);
+    *abs_sum += qm;
+    levels[i] = clip3(ecmin, ecmax, qm * sign);
+  }
+  if (tu->sign_hiding && *abs_sum >= 2) sbh_hdq(levels, coef, delta_u, &cp, n, tu->max_log2_tr_range);
+}
+
+/* transformNxN (:1460): bypass / transform-skip (:2021) / xT, then xQuant */
+void hvxo_transform_nxn(const hvx_tu_desc *tu, const hvx_estbits *est, const int16_t *residual, int stride,
+                        int32_t *temp, int32_t *levels, int32_t *arl, int32_t *abs_sum) {
+  const int w = tu->width, h = tu->height;
+  *abs_sum = 0;
+  if (tu->transquant_bypass) {
+    for (int y = 0; y < h; y++)
+      for (int x = 0; x < w; x++) { levels[y * w + x] = residual[y * stride + x]; *abs_sum += abs(residual[y * stride + x]); }
+    return;
+  }
+  if (tu->transform_skip) {
+    int ts = transform_shift(tu);
+    for (int y = 0; y < h; y++)
+      for (int x = 0; x < w; x++) {
+        int32_t v = residual[y * stride + x];
+        temp[y * w + x] = ts >= 0 ? shl32(v, ts) : (v + (1 << (-ts - 1))) >> -ts;
+      }
+  } else {
+    int32_t blk[1024];
+    for (int y = 0; y < h; y++)
+      for (int x = 0; x < w; x++) blk[y * w + x] = residual[y * stride + x];
+    hvxo_fwd_transform(blk, temp, w, tu->use_dst && w == 4 && h == 4);  /* xTrMxN :876 */
+  }
+  hvxo_quant(tu, est, temp, levels, arl, abs_sum);
+}
+
+/* invTransformNxN (:1547) = xDeQuant (:1314, flat list) + xITransformSkip (:2070) / xIT (:1988) */
+void hvxo_inv_transform_nxn(const hvx_tu_desc *tu, const int32_t *levels, int16_t *residual, int stride) {
+  const int w = tu->width, h = tu->height, n = w * h;
+  if (tu->transquant_bypass) {
+    for (int y = 0; y < h; y++)
+      for (int x = 0; x < w; x++) residual[y * stride + x] = (int16_t)levels[y * w + x];
+    return;
+  }
+  const int ts = transform_shift(tu);
+  const int max_log2 = tu->max_log2_tr_range;
+  const int32_t tmin = -(1 << max_log2), tmax = (1 << max_log2) - 1;
+  const int right = 6 - (ts + tu->qp_per);
+  const int scale = kInvQuantScales[tu->qp_rem];
+  int tib = 32 + right - 7;
+  if (max_log2 + 1 < tib) tib = max_log2 + 1;
+  const int32_t imin = -(1 << (tib - 1)), imax = (1 << (tib - 1)) - 1;
+  int32_t deq[1024];
+  for (int i = 0; i < n; i++) {
+    int32_t c = clip3(imin, imax, levels[i]);
+    int32_t v = right > 0 ? (c * scale + (1 << (right - 1))) >> right : shl32(c * scale, -right);
+    deq[i] = clip3(tmin, tmax, v);
+  }
+  if (tu->transform_skip) {
+    for (int y = 0; y < h; y++)
+      for (int x = 0; x < w; x++) {
+        int32_t v = deq[y * w + x];
+        residual[y * stride + x] = (int16_t)(ts >= 0 ? (v + (ts == 0 ? 0 : 1 << (ts - 1))) >> ts : shl32(v, -ts));
+      }
+  } else {
+    int32_t blk[1024];
+    hvxo_inv_transform(deq, blk, w, tu->use_dst && w == 4 && h == 4);  /* xITrMxN :945 */
+    for (int y = 0; y < h; y++)
+      for (int x = 0; x < w; x++) residual[y * stride + x] = (int16_t)blk[y * w + x];
+  }
+}
+
+/* ============================================================================================
+ * Motion estimation: TEncSearch.cpp (uni-prediction xMotionEstimation, TZ search config :297)
+ * ========================================================================================== */
+typedef struct {
+  const uint8_t *org; int so;  /* PU origin in the current plane */
+  const uint8_t *ref; int sr;  /* PU origin in the reference plane (MV 0) */
+  int w, h, sub;
+  uint32_t lam;                /* m_uiCost */
+  int px, py, cost_scale;      /* m_mvPredictor, m_iCostScale */
+  int best_x, best_y, best_dist, best_round, point_nr;
+  uint32_t best_sad;
+} tz_state;
+
+/* TComRdCost::getCost(x, y) (TComRdCost.h:172) */
+static inline uint32_t mv_cost(const tz_state *t, int x, int y) {
+  uint32_t bits = hvxo_eg_bits((x << t->cost_scale) - t->px) + hvxo_eg_bits((y << t->cost_scale) - t->py);
+  return (t->lam * bits) >> 16;
+}
+
+static uint32_t sad_u8(const uint8_t *o, int so, const uint8_t *c, int sc, int w, int h, int sub) {
+  int specialised = (w == 4 || w == 8 || w == 16 || w == 32 || w == 64 || w == 12 || w == 24 || w == 48);
+  if (!specialised) sub = 0;
+  uint32_t s = 0;
+  for (int y = 0; y < h; y += 1 << sub)
+    for (int x = 0; x < w; x++) s += (uint32_t)abs((int)o[y * so + x] - (int)c[y * sc + x]);
+  return s << sub;
+}
+
+/* xTZSearchHelp (:332), non-SELECTIVE branch */
+static void tz_help(tz_state *t, int x, int y, int point_nr, int dist) {
+  uint32_t sad = sad_u8(t->org, t->so, t->ref + y * t->sr + x, t->sr, t->w, t->h, t->sub);
+  sad += mv_cost(t, x, y);
+  if (sad < t->best_sad) {
+    t->best_sad = sad; t->best_x = x; t->best_y = y; t->best_dist = dist; t->best_round = 0; t->point_nr = point_nr;
+  }
+}
+
+typedef struct { int l, r, t, b; } srch_rng;
+
+/* xTZ2PointSearch (:438) */
+static void tz_2point(tz_state *t, const srch_rng *g) {
+  int sx = t->best_x, sy = t->best_y;
+  switch (t->point_nr) {
+    case 1:
+      if (sx - 1 >= g->l) tz_help(t, sx - 1, sy, 0, 2);
+      if (sy - 1 >= g->t) tz_help(t, sx, sy - 1, 0, 2);
+      break;
+    case 2:
+      if (sy - 1 >= g->t) {
+        if (sx - 1 >= g->l) tz_help(t, sx - 1, sy - 1, 0, 2);
+        if (sx + 1 <= g->r) tz_help(t, sx + 1, sy - 1, 0, 2);
+      }
+      break;
+    case 3:
+      if (sy - 1 >= g->t) tz_help(t, sx, sy - 1, 0, 2);
+      if (sx + 1 <= g->r) tz_help(t, sx + 1, sy, 0, 2);
+      break;
+    case 4:
+      if (sx - 1 >= g->l) {
+        if (sy + 1 <= g->b) tz_help(t, sx - 1, sy + 1, 0, 2);
+        if (sy - 1 >= g->t) tz_help(t, sx - 1, sy - 1, 0, 2);
+      }
+      break;
+    case 5:
+      if (sx + 1 <= g->r) {
+        if (sy - 1 >= g->t) tz_help(t, sx + 1, sy - 1, 0, 2);
+        if (sy + 1 <= g->b) tz_help(t, sx + 1, sy + 1, 0, 2);
+      }
+      break;
+    case 6:
+      if (sx - 1 >= g->l) tz_help(t, sx - 1, sy, 0, 2);
+      if (sy + 1 <= g->b) tz_help(t, sx, sy + 1, 0, 2);
+      break;
+    case 7:
+      if (sy + 1 <= g->b) {
+        if (sx - 1 >= g->l) tz_help(t, sx - 1, sy + 1, 0, 2);
+        if (sx + 1 <= g->r) tz_help(t, sx + 1, sy + 1, 0, 2);
+      }
+      break;
+    case 8:
+      if (sx + 1 <= g->r) tz_help(t, sx + 1, sy, 0, 2);
+      if (sy + 1 <= g->b) tz_help(t, sx, sy + 1, 0, 2);
+      break;
+    default: abort();
+  }
+}
+
+/* xTZ8PointDiamondSearch (:629) */
+static void tz_diamond(tz_state *t, const srch_rng *g, int sx, int sy, int d) {
+  const int top = sy - d, bottom = sy + d, left = sx - d, right = sx + d;
+  t->best_round += 1;
+  if (d == 1) {
+    if (top >= g->t) tz_help(t, sx, top, 2, d);
+    if (left >= g->l) tz_help(t, left, sy, 4, d);
+    if (right <= g->r) tz_help(t, right, sy, 5, d);
+    if (bottom <= g->b) tz_help(t, sx, bottom, 7, d);
+    return;
+  }
+  const int inside = top >= g->t && left >= g->l && right <= g->r && bottom <= g->b;
+  if (d <= 8) {
+    const int t2 = sy - (d >> 1), b2 = sy + (d >> 1), l2 = sx - (d >> 1), r2 = sx + (d >> 1);
+    if (inside) {
+      tz_help(t, sx, top, 2, d);
+      tz_help(t, l2, t2, 1, d >> 1);
+      tz_help(t, r2, t2, 3, d >> 1);
+      tz_help(t, left, sy, 4, d);
+      tz_help(t, right, sy, 5, d);
+      tz_help(t, l2, b2, 6, d >> 1);
+      tz_help(t, r2, b2, 8, d >> 1);
+      tz_help(t, sx, bottom, 7, d);
+    } else {
+      if (top >= g->t) tz_help(t, sx, top, 2, d);
+      if (t2 >= g->t) {
+        if (l2 >= g->l) tz_help(t, l2, t2, 1, d >> 1);
+        if (r2 <= g->r) tz_help(t, r2, t2, 3, d >> 1);
+      }
+      if (left >= g->l) tz_help(t, left, sy, 4, d);
+      if (right <= g->r) tz_help(t, right, sy, 5, d);
+      if (b2 <= g->b) {
+        if (l2 >= g->l) tz_help(t, l2, b2, 6, d >> 1);
+        if (r2 <= g->r) tz_help(t, r2, b2, 8, d >> 1);
+      }
+      if (bottom <= g->b) tz_help(t, sx, bottom, 7, d);
+    }
+  } else {
+    if (inside) {
+      tz_help(t, sx, top, 0, d);
+      tz_help(t, left, sy, 0, d);
+      tz_help(t, right, sy, 0, d);
+      tz_help(t, sx, bottom, 0, d);
+      for (int i = 1; i < 4; i++) {
+        int yt = top + ((d >> 2) * i), yb = bottom - ((d >> 2) * i);
+        int xl = sx - ((d >> 2) * i), xr = sx + ((d >> 2) * i);
+        tz_help(t, xl, yt, 0, d);
+        tz_help(t, xr, yt, 0, d);
+        tz_help(t, xl, yb, 0, d);
+        tz_help(t, xr, yb, 0, d);
+      }
+    } else {
+      if (top >= g->t) tz_help(t, sx, top, 0, d);
+      if (left >= g->l) tz_help(t, left, sy, 0, d);
+      if (right <= g->r) tz_help(t, right, sy, 0, d);
+      if (bottom <= g->b) tz_help(t, sx, bottom, 0, d);
+      for (int i = 1; i < 4; i++) {
+        int yt = top + ((d >> 2) * i), yb = bottom - ((d >> 2) * i);
+        int xl = sx - ((d >> 2) * i), xr = sx + ((d >> 2) * i);
+        if (yt >= g->t) {
+          if (xl >= g->l) tz_help(t, xl, yt, 0, d);
+          if (xr <= g->r) tz_help(t, xr, yt, 0, d);
+        }
+        if (yb <= g->b) {
+          if (xl >= g->l) tz_help(t, xl, yb, 0, d);
+          if (xr <= g->r) tz_help(t, xr, yb, 0, d);
+        }
+      }
+    }
+  }
+}
+
+/* TComDataCU::clipMv (TComDataCU.cpp:2788), MV in quarter-pel, stored as Short */
+static void clip_mv(const hvx_me_job *j, int *mx, int *my) {
+  int hmax = (j->pic_w + 8 - j->cu_x - 1) << 2, hmin = (-j->max_cu - 8 - j->cu_x + 1) << 2;
+  int vmax = (j->pic_h + 8 - j->cu_y - 1) << 2, vmin = (-j->max_cu - 8 - j->cu_y + 1) << 2;
+  *mx = (int16_t)(*mx < hmin ? hmin : *mx > hmax ? hmax : *mx);
+  *my = (int16_t)(*my < vmin ? vmin : *my > vmax ? vmax : *my);
+}
+
+/* xSetSearchRange (:3765); returns integer-pel bounds */
+static void set_search_range(const hvx_me_job *j, int px, int py, int sr, srch_rng *g) {
+  int cx = px, cy = py;
+  clip_mv(j, &cx, &cy);
+  int lx = cx - (sr << 2), ly = cy - (sr << 2), rx = cx + (sr << 2), ry = cy + (sr << 2);
+  clip_mv(j, &lx, &ly);
+  clip_mv(j, &rx, &ry);
+  g->l = lx >> 2; g->t = ly >> 2; g->r = rx >> 2; g->b = ry >> 2;
+}
+
+/* xTZSearch (:3881) with TZ_SEARCH_CONFIGURATION (:297-313) */
+static void tz_search(tz_state *t, const hvx_me_job *j, const srch_rng *g0, int *mvx, int *mvy, uint32_t *sad) {
+  const int sr = j->search_range;
+  srch_rng g = *g0;          /* raster range (re-centred when a 2Nx2N integer MV is given) */
+  int mx = *mvx, my = *mvy;
+  clip_mv(j, &mx, &my);
+  mx >>= 2; my >>= 2;
+  t->best_sad = 0xFFFFFFFFu;
+  t->best_x = t->best_y = 0; t->best_dist = 0; t->best_round = 0; t->point_nr = 0;
+  tz_help(t, mx, my, 0, 0);
+  tz_help(t, 0, 0, 0, 0);    /* bTestZeroVector */
+  if (j->use_int2nx2n) {
+    int ix = j->i2_x << 2, iy = j->i2_y << 2;
+    clip_mv(j, &ix, &iy);
+    ix >>= 2; iy >>= 2;
+    tz_help(t, ix, iy, 0, 0);
+    set_search_range(j, t->best_x << 2, t->best_y << 2, sr, &g);
+  }
+  int sx = t->best_x, sy = t->best_y;
+  for (int d = 1; d <= sr; d *= 2) {
+    tz_diamond(t, g0, sx, sy, d);
+    if ((j->flags & HVX_ME_SMOOTHMV) && t->best_round >= 3) break;
+  }
+  if (t->best_dist == 1) { t->best_dist = 0; tz_2point(t, g0); }
+  if (t->best_dist > 5) {
+    t->best_dist = 5;
+    for (sy = g.t; sy <= g.b; sy += 5)
+      for (sx = g.l; sx <= g.r; sx += 5) tz_help(t, sx, sy, 0, 5);
+  }
+  while (t->best_dist > 0) {  /* star refinement */
+    sx = t->best_x; sy = t->best_y;
+    t->best_dist = 0; t->point_nr = 0;
+    for (int d = 1; d < sr + 1; d *= 2) tz_diamond(t, g0, sx, sy, d);
+    if (t->best_dist == 1) {
+      t->best_dist = 0;
+      if (t->point_nr != 0) tz_2point(t, g0);
+    }
+  }
+  *mvx = t->best_x; *mvy = t->best_y;
+  *sad = t->best_sad - mv_cost(t, t->best_x, t->best_y);
+}
+
+/* xPatternRefinement (:808) over interpolated candidates: iFrac 2 (half) or 1 (quarter).
+ * base_q: quarter-pel position of the refinement centre relative to the PU at MV 0. */
+static uint32_t pattern_refine(tz_state *t, int use_had, int base_qx, int base_qy, int frac, int *fx, int *fy) {
+  static const int kRefH[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
+  static const int kRefQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
+  const int (*ref)[2] = frac == 2 ? kRefH : kRefQ;
+  uint32_t best = 0xFFFFFFFFu;
+  int bi = 0;
+  int16_t org[64 * 64], blk[64 * 64];
+  for (int y = 0; y < t->h; y++)
+    for (int x = 0; x < t->w; x++) org[y * 64 + x] = t->org[y * t->so + x];
+  for (int i = 0; i < 9; i++) {
+    int qx = base_qx + ref[i][0] * frac, qy = base_qy + ref[i][1] * frac;
+    hvxo_luma_block_qpel(t->ref, t->sr, 0, 0, qx, qy, t->w, t->h, blk, 64);
+    uint32_t d = use_had ? hvxo_satd(org, 64, blk, 64, t->w, t->h) : hvxo_sad_me(org, 64, blk, 64, t->w, t->h, 0);
+    d += mv_cost(t, ref[i][0] + *fx, ref[i][1] + *fy);
+    if (d < best) { best = d; bi = i; }
+  }
+  *fx = ref[bi][0];
+  *fy = ref[bi][1];
+  return best;
+}
+
+void hvxo_motion_estimation(const uint8_t *cur, int cur_stride, const uint8_t *refp, int ref_stride,
+                            const hvx_me_job *j, hvx_me_result *r) {
+  tz_state t;
+  t.org = cur + j->pu_y * cur_stride + j->pu_x; t.so = cur_stride;
+  t.ref = refp + j->pu_y * ref_stride + j->pu_x; t.sr = ref_stride;
+  t.w = j->w; t.h = j->h;
+  t.sub = ((j->flags & HVX_ME_FEN) && j->h > 8) ? 1 : 0;
+  t.lam = j->lambda_motion;
+  t.px = j->pred_x; t.py = j->pred_y;
+  srch_rng g;
+  set_search_range(j, j->pred_x, j->pred_y, j->search_range, &g);
+  t.cost_scale = 2;
+  int mvx = j->pred_x, mvy = j->pred_y;
+  uint32_t sad;
+  tz_search(&t, j, &g, &mvx, &mvy, &sad);
+  r->mv_int_x = mvx; r->mv_int_y = mvy; r->sad_int = sad;
+  /* xPatternSearchFracDIF (:4240) */
+  const int had = (j->flags & HVX_ME_HADME) != 0;
+  t.cost_scale = 1;
+  int hx = mvx << 1, hy = mvy << 1;
+  uint32_t cost = pattern_refine(&t, had, mvx << 2, mvy << 2, 2, &hx, &hy);
+  t.cost_scale = 0;
+  int qx = ((mvx << 1) + hx) << 1, qy = ((mvy << 1) + hy) << 1;
+  cost = pattern_refine(&t, had, (mvx << 2) + (hx << 1), (mvy << 2) + (hy << 1), 1, &qx, &qy);
+  r->half_x = hx; r->half_y = hy; r->qtr_x = qx; r->qtr_y = qy; r->cost_frac = cost;
+  int fmx = (mvx << 2) + (hx << 1) + qx, fmy = (mvy << 2) + (hy << 1) + qy;
+  uint32_t mv_bits = hvxo_eg_bits(fmx - t.px) + hvxo_eg_bits(fmy - t.py);
+  uint32_t bits = (uint32_t)j->bits_in + mv_bits;
+  r->mv_x = fmx; r->mv_y = fmy; r->bits = bits;
+  r->cost = (uint32_t)(floor(1.0 * ((double)cost - (double)((t.lam * mv_bits) >> 16))) + (double)((t.lam * bits) >> 16));
+}
+
+/* ============================================================================================
+ * SSIM metric: stvssim_src/stvssimrdo2_att/lencod/src/stvssim.c
+ * ========================================================================================== */
+/* compute_SSIM (:491-566), _SSIM_WEIGHTED_ 0: uniform weights 1/wint^2 */
+float hvxo_ssim(const uint8_t *org, int so, const uint8_t *rec, int sr, int w, int h, int wint, int overlap) {
+  const float K1 = 0.01f, K2 = 0.03f;
+  float maxsq = (float)(255 * 255);
+  float C1 = K1 * K1 * maxsq, C2 = K2 * K2 * maxsq;
+  float win_pixels = (float)(wint * wint);
+  float dist = 0.0f;
+  int cnt = 0;
+  for (int j = 0; j <= h - wint; j += overlap)
+    for (int i = 0; i <= w - wint; i += overlap) {
+      float mo = 0, me = 0, vo = 0, ve = 0, cov = 0;
+      for (int n = j; n < j + wint; n++)
+        for (int m = i; m < i + wint; m++) {
+          float wgt = 1.0f / win_pixels;
+          int po = org[n * so + m], pe = rec[n * sr + m];
+          mo += wgt * po; me += wgt * pe;
+          vo += wgt * po * po; ve += wgt * pe * pe; cov += wgt * po * pe;
+        }
+      float varo = fabsf(vo - mo * mo), vare = fabsf(ve - me * me), covo = fabsf(cov - mo * me);
+      float s = (float)((2.0 * mo * me + C1) * (2.0 * covo + C2));
+      s /= (float)(mo * mo + me * me + C1) * (varo + vare + C2);
+      dist += s;
+      cnt++;
+    }
+  dist /= (float)cnt;
+  if (dist >= 1.0 && dist < 1.01) dist = 1.0f;
+  return dist;
+}
+
+/* orientation filters (:116-334): weight wa on the oriented line, wb elsewhere */
+static float orient_w(int k, int beta, int y, int x, float wa, float wb) {
+  if (wa < 0) wa = 1.0f;
+  if (wb < 0) wb = 1.0f;
+  if (wa < wb) { float c = wb; wb = wa; wa = c; }
+  int on;
+  if (beta == 4) {
+    switch (k) {
+      case 0: on = x == beta / 2 - 1; break;          /* hFilter_4 */
+      case 1: on = x + y == beta - 1; break;          /* rFilter_4 */
+      case 2: on = y == beta / 2 - 1; break;          /* vFilter_4 */
+      default: on = x == y; break;                    /* lFilter_4 */
+    }
+  } else {
+    switch (k) {
+      case 0: on = x >= beta / 2 - 1 && x <= beta / 2 + 1; break;        /* hFilter */
+      case 1: on = x + y - beta >= -2 && x + y - beta <= 0; break;       /* rFilter */
+      case 2: on = y >= beta / 2 - 1 && y <= beta / 2 + 1; break;        /* vFilter */
+      default: on = abs(x - y) <= 1; break;                              /* lFilter */
+    }
+  }
+  return on ? wa : wb;
+}
+
+/* calOrit (:336) */
+static void cal_orit(float o, short *orit) {
+  static const float orient[4] = {0, 3.1415926f / 4, 3.1415926f / 2, 3.1415926f * 3 / 4};
+  float dn[4], dx = 10000.0f;
+  for (int k = 0; k < 4; k++) {
+    dn[k] = (float)fabs(o - orient[k]);
+    if (dn[k] < dx) dx = dn[k];
+  }
+  for (int k = 0; k < 4; k++)
+    if (fabs(dx - dn[k]) < 0.01f) orit[k]++;
+}
+
+/* compute_stVSSIM (:587-830).  org_hist[o] / rec_hist[o] for o < frameused-1 are the history
+ * frames (refPicsData / srcPicsData); the current frame is org_hist[frameused-1]. */
+float hvxo_stvssim(const uint8_t *const *org_hist, const uint8_t *const *rec_hist, int hs, const float *dirs,
+                   int ds, int w, int h, int wint, int overlap, int gama, int comp, float *ssim, float *ssim3d,
+                   float *stvssim) {
+  const float K1 = 0.01f, K2 = 0.03f;
+  const int used = gama < 26 ? gama : 26;
+  const int uv = comp > 0 ? 2 : 1;
+  float wa = 0.6f, wb = 1.0f - wa, wgta[4], wgtb[4];
+  if (wint == 4) {
+    wgta[0] = wgta[2] = wgta[1] = wgta[3] = wa / (wint * (used));
+    wgtb[0] = wgtb[2] = wgtb[1] = wgtb[3] = wb / ((wint * wint - wint) * (used));
+  } else {
+    wgta[0] = wgta[2] = wa / (3 * wint * (used));
+    wgta[1] = wgta[3] = wa / ((3 * wint - 2) * (used));
+    wgtb[0] = wgtb[2] = wb / ((wint * wint - 3 * wint) * (used));
+    wgtb[1] = wgtb[3] = wb / ((wint * wint - 3 * wint + 2) * (used));
+  }
+  float maxsq = (float)(255 * 255);
+  float C1 = K1 * K1 * maxsq, C2 = K2 * K2 * maxsq;
+  float s3x = 0, sx = 0, stx = 0;
+  int cnt = 0;
+  for (int j = 0; j <= h - wint; j += overlap)
+    for (int i = 0; i <= w - wint; i += overlap) {
+      float s3[4];
+      for (int k = 0; k < 4; k++) {
+        float mo = 0, me = 0, vo = 0, ve = 0, cov = 0;
+        for (int o = 0; o < used; o++) {
+          const uint8_t *ro = o != used - 1 ? org_hist[o] : org_hist[used - 1];
+          const uint8_t *re = o != used - 1 ? rec_hist[o] : rec_hist[used - 1];
+          for (int n = j; n < j + wint; n++)
+            for (int m = i; m < i + wint; m++) {
+              float wgt = orient_w(k, wint, n - j, m - i, wgta[k], wgtb[k]);
+              int po = ro[n * hs + m], pe = re[n * hs + m];
+              mo += wgt * po; me += wgt * pe;
+              vo += wgt * po * po; ve += wgt * pe * pe; cov += wgt * po * pe;
+            }
+        }
+        float varo = fabsf(vo - mo * mo), vare = fabsf(ve - me * me), covo = fabsf(cov - mo * me);
+        float s = (float)((2.0 * mo * me + C1) * (2.0 * covo + C2));
+        s /= (float)(mo * mo + me * me + C1) * (varo + vare + C2);
+        s3[k] = s;
+        if (s3[k] >= 1.0 && s3[k] < 1.01) s3[k] = 1.0f;
+      }
+      short orit[4] = {0, 0, 0, 0};
+      for (int n = j; n < j + wint; n++)
+        for (int m = i; m < i + wint; m++) cal_orit(dirs[(n * uv) * ds + m * uv], orit);
+      short tmp = 0, inx = 0;
+      for (int n = 0; n < 4; n++)
+        if (orit[n] > tmp) { tmp = orit[n]; inx = (short)n; }
+      int n;
+      for (n = 0; n < 4; ++n)
+        if ((tmp - orit[n]) < 10 && inx != n) break;
+      float t3;
+      if (n == 4) { s3x += s3[inx]; t3 = s3[inx]; }
+      else { s3x += (s3[inx] + s3[n]) / 2; t3 = (s3[inx] + s3[n]) / 2; }
+      /* plain SSIM on the current frame */
+      const uint8_t *ro = org_hist[used - 1], *re = rec_hist[used - 1];
+      float mo = 0, me = 0, vo = 0, ve = 0, cov = 0;
+      float wgt = 1.0f / (wint * wint);
+      for (int nn = j; nn < j + wint; nn++)
+        for (int m = i; m < i + wint; m++) {
+          int po = ro[nn * hs + m], pe = re[nn * hs + m];
+          mo += wgt * po; me += wgt * pe;
+          vo += wgt * po * po; ve += wgt * pe * pe; cov += wgt * po * pe;
+        }
+      float varo = fabsf(vo - mo * mo), vare = fabsf(ve - me * me), covo = fabsf(cov - mo * me);
+      float s = (float)((2.0 * mo * me + C1) * (2.0 * covo + C2));
+      s /= (float)(mo * mo + me * me + C1) * (varo + vare + C2);
+      sx += s;
+      stx += s * t3;
+      cnt++;
+    }
+  s3x /= (float)cnt;
+  sx /= (float)cnt;
+  stx /= (float)cnt;
+  float ret = sx * s3x;
+  if (stx >= 1.0 && stx < 1.01) stx = 1.0f;
+  *ssim = sx; *ssim3d = s3x; *stvssim = stx;
+  return ret;
+}
+
+/* lambda_2 (:1782-1806, active expression :1805) */
+double hvxo_lambda_2(int qp) {
+  double a1 = 5.883060266548170e-03, b2 = -2.229472265847692e-02, b1 = 9.279543980380707e-02;
+  return -a1 * b2 * exp(b1 * (qp - 15));
+}
+
+/* adjust_lambda (:1565, active _ADJUST_L2_ body :1707) */
+double hvxo_adjust_lambda(double lambda, double eta) { return lambda * pow(eta, 0.85); }

@@ -1,0 +1,52 @@
+"""Synthetic 8-bit 4:2:0 YUV generator (TEST INFRASTRUCTURE and bench input recipe).
+
+Kinds:
+  random  -- BASELINE.md section 3: splitmix64 seeded 0x5EED0000 + frame index,
+             every sample is the top byte (x >> 56) of the next draw, Y then Cb then Cr.
+  smooth  -- moving sinusoid texture + small splitmix64 noise: gives the encoder real
+             motion and a realistic coefficient distribution (used for golden capture).
+"""
+import sys
+
+import numpy as np
+
+MASK = (1 << 64) - 1
+
+
+def splitmix64_stream(seed: int, n: int) -> np.ndarray:
+    """n successive splitmix64 outputs (uint64) from state `seed` (vectorised)."""
+    with np.errstate(over="ignore"):
+        k = np.arange(1, n + 1, dtype=np.uint64)
+        z = np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def random_frame(w: int, h: int, index: int) -> np.ndarray:
+    n = w * h * 3 // 2
+    return (splitmix64_stream(0x5EED0000 + index, n) >> np.uint64(56)).astype(np.uint8)
+
+
+def smooth_frame(w: int, h: int, index: int) -> np.ndarray:
+    out = []
+    for cw, ch, scale in ((w, h, 1.0), (w // 2, h // 2, 0.5), (w // 2, h // 2, 0.5)):
+        y, x = np.mgrid[0:ch, 0:cw].astype(np.float64)
+        x = x / scale + 2.0 * index
+        y = y / scale - 1.0 * index
+        v = 128 + 60 * np.sin(x * 0.11 + y * 0.05) + 40 * np.cos(y * 0.13 - x * 0.03)
+        noise = (splitmix64_stream(0x5EED8000 + index * 7 + len(out), cw * ch) >> np.uint64(61)).astype(np.int64) - 4
+        out.append(np.clip(np.rint(v) + noise.reshape(ch, cw), 0, 255).astype(np.uint8).ravel())
+    return np.concatenate(out)
+
+
+def write_yuv(path: str, kind: str, w: int, h: int, frames: int) -> None:
+    gen = random_frame if kind == "random" else smooth_frame
+    with open(path, "wb") as f:
+        for i in range(frames):
+            f.write(gen(w, h, i).tobytes())
+
+
+if __name__ == "__main__":
+    kind, w, h, frames, path = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+    write_yuv(path, kind, w, h, frames)

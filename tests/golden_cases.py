@@ -1,0 +1,78 @@
+"""Helpers turning golden records (tests/golden/*.bin) into hvx ABI descriptors."""
+import os
+
+import numpy as np
+
+from oracle import golden_io
+from video_codecs_amd import _abi
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+TU_FILES = ("tu_intra.bin", "tu_ldp.bin", "tu_ldp22.bin", "tu_noqrd.bin")
+
+
+def load(name):
+    return golden_io.load(os.path.join(GOLDEN, name))
+
+
+def fwd_desc(meta, lam):
+    """tu_capture.cpp fwd_meta (28 ints) + lambda -> TU_DESC."""
+    d = np.zeros(1, _abi.TU_DESC)
+    m = [int(x) for x in meta]
+    for f, v in (("comp", m[0]), ("width", m[1]), ("height", m[2]), ("log2_size", m[3]), ("scan_type", m[4]),
+                 ("use_dst", m[5]), ("transform_skip", m[6]), ("is_intra", m[7]), ("tr_idx", m[8]),
+                 ("ctx_qt_cbf", m[9]), ("slice_type", m[10]), ("qp_per", m[12]), ("qp_rem", m[13]),
+                 ("sign_hiding", m[14]), ("use_rdoq", m[15]), ("use_rdoq_ts", m[16]), ("selective_rdoq", m[17]),
+                 ("adaptive_qp_select", m[18]), ("transquant_bypass", m[19]), ("golomb_rice_stat", m[20]),
+                 ("persistent_rice", m[21]), ("extended_precision", m[22]), ("max_log2_tr_range", m[23]),
+                 ("bit_depth", m[24]), ("ts_context", m[26])):
+        d[f] = v
+    d["lambda"] = lam
+    return d
+
+
+def inv_desc(meta):
+    """tu_capture.cpp inv_meta (12 ints) -> TU_DESC."""
+    d = np.zeros(1, _abi.TU_DESC)
+    m = [int(x) for x in meta]
+    for f, v in (("comp", m[0]), ("width", m[1]), ("height", m[2]), ("log2_size", m[3]), ("use_dst", m[4]),
+                 ("transform_skip", m[5]), ("qp_per", m[7]), ("qp_rem", m[8]), ("transquant_bypass", m[9]),
+                 ("max_log2_tr_range", m[10]), ("bit_depth", m[11])):
+        d[f] = v
+    return d
+
+
+def fwd_records(g):
+    """Yield (desc, estbits, residual[h,w], temp, levels, absSum) per captured forward TU."""
+    off = g["fwd_off"]
+    for i in range(g["fwd_meta"].shape[0]):
+        m = g["fwd_meta"][i]
+        w, h = int(m[1]), int(m[2])
+        o = int(off[i])
+        yield (fwd_desc(m, g["fwd_lambda"][i]), g["fwd_estbits"][i], g["fwd_res"][o:o + w * h].reshape(h, w),
+               g["fwd_temp"][o:o + w * h], g["fwd_coef"][o:o + w * h], int(m[25]))
+
+
+def inv_records(g):
+    off = g["inv_off"]
+    for i in range(g["inv_meta"].shape[0]):
+        m = g["inv_meta"][i]
+        w, h = int(m[1]), int(m[2])
+        o = int(off[i])
+        yield inv_desc(m), g["inv_coef"][o:o + w * h], g["inv_res"][o:o + w * h].reshape(h, w)
+
+
+def me_jobs(g):
+    """me.bin -> (planes[pair][cur/ref], ME_JOB array, expected results [n,12])."""
+    W, H, margin, maxcu = (int(x) for x in g["dims"])
+    jobs = np.zeros(g["jobs"].shape[0], _abi.ME_JOB)
+    j = g["jobs"]
+    jobs["pic_w"], jobs["pic_h"], jobs["max_cu"] = W, H, maxcu
+    jobs["cur_idx"] = j[:, 0]
+    jobs["ref_idx"] = j[:, 0]
+    jobs["cu_x"], jobs["cu_y"], jobs["pu_x"], jobs["pu_y"] = j[:, 1], j[:, 2], j[:, 3], j[:, 4]
+    jobs["w"], jobs["h"], jobs["pred_x"], jobs["pred_y"] = j[:, 5], j[:, 6], j[:, 7], j[:, 8]
+    jobs["use_int2nx2n"], jobs["i2_x"], jobs["i2_y"], jobs["bits_in"] = j[:, 9], j[:, 10], j[:, 11], j[:, 12]
+    jobs["search_range"] = 64
+    jobs["lambda_motion"] = [_abi.lambda_motion_sad(l) for l in g["lambda"]]
+    jobs["flags"] = _abi.ME_FEN | _abi.ME_HADME | _abi.ME_SMOOTHMV
+    return g["planes"], jobs, g["res"]

@@ -1,0 +1,98 @@
+"""Pin the CPU oracle (oracle/hvx_oracle.c) against golden vectors produced by the
+reference itself (HM-16.5rc1 / stvssim.c, see oracle/gen_goldens.sh).  CPU only."""
+import numpy as np
+import pytest
+
+import oracle
+from tests import golden_cases as gc
+
+
+def test_dist_golden():
+    g = gc.load("dist.bin")
+    meta, org, cur, wgt, out = g["meta"], g["org"], g["cur"], g["weight"], g["out"]
+    for i in range(meta.shape[0]):
+        kind, w, h, sub = (int(x) for x in meta[i])
+        o, c = org[i].astype(np.int16), cur[i].astype(np.int16)
+        if kind in (0, 1):
+            got = oracle.sad(o, c, w, h, sub, me_dispatch=True)
+        elif kind == 2:
+            got = oracle.satd(o, c, w, h)
+        elif kind == 3:
+            got = oracle.sse(o, c, w, h)
+        elif kind == 4:
+            got = oracle.sse(o, c, w, h, weight=wgt[i])
+        else:
+            got = oracle.sad(o, c, w, h, 0)
+        assert got == int(out[i]), (i, kind, w, h, sub)
+
+
+def test_interp_golden():
+    g = gc.load("interp.bin")
+    meta, src, out = g["meta"], g["src"], g["out"]
+    for i in range(meta.shape[0]):
+        is_luma, d, frac, first, last, w, h = (int(x) for x in meta[i])
+        got = oracle.filter_block(src[i], (8, 8), is_luma, d, frac, first, last, w, h)
+        np.testing.assert_array_equal(got[:h, :w], out[i][:h, :w], err_msg=str(meta[i]))
+
+
+def test_xform_golden():
+    g = gc.load("xform.bin")
+    for i in range(g["meta"].shape[0]):
+        n, dst = (int(x) for x in g["meta"][i])
+        f = oracle.fwd_transform(g["fwd_in"][i][:n * n], n, dst)
+        np.testing.assert_array_equal(f.reshape(-1), g["fwd_out"][i][:n * n], err_msg=f"fwd {n} {dst}")
+        r = oracle.inv_transform(g["inv_in"][i][:n * n], n, dst)
+        np.testing.assert_array_equal(r.reshape(-1), g["inv_out"][i][:n * n], err_msg=f"inv {n} {dst}")
+
+
+@pytest.mark.parametrize("name", gc.TU_FILES)
+def test_tu_forward_golden(name):
+    g = gc.load(name)
+    n = 0
+    for desc, est, res, temp, lev, absum in gc.fwd_records(g):
+        t, l, _, a = oracle.transform_nxn(desc, est, res)
+        if not desc["transquant_bypass"][0]:
+            np.testing.assert_array_equal(t, temp, err_msg=f"{name} rec {n} transform")
+        np.testing.assert_array_equal(l, lev, err_msg=f"{name} rec {n} levels {desc}")
+        assert a == absum, (name, n)
+        n += 1
+    assert n > 50
+
+
+@pytest.mark.parametrize("name", gc.TU_FILES)
+def test_tu_inverse_golden(name):
+    g = gc.load(name)
+    n = 0
+    for desc, coef, res in gc.inv_records(g):
+        got = oracle.inv_transform_nxn(desc, coef)
+        np.testing.assert_array_equal(got, res, err_msg=f"{name} rec {n}")
+        n += 1
+    assert n > 10
+
+
+def test_me_golden():
+    g = gc.load("me.bin")
+    planes, jobs, exp = gc.me_jobs(g)
+    for i in range(jobs.shape[0]):
+        p = int(jobs["cur_idx"][i])
+        r = oracle.motion_estimation(planes[p, 0], planes[p, 1], jobs[i])
+        got = [int(r[f]) for f in r.dtype.names]
+        assert got == [int(x) for x in exp[i]], (i, jobs[i], got, exp[i])
+
+
+def test_ssim_golden():
+    g = gc.load("ssim.bin")
+    for i in range(g["meta"].shape[0]):
+        w, h, wint, ov, gama, comp = (int(x) for x in g["meta"][i])
+        oh, rh = g["org_hist"][i], g["rec_hist"][i]
+        s = oracle.ssim(oh[-1], rh[-1], w, h, wint, ov)
+        assert s == g["out"][i][0], (i, s, g["out"][i][0])
+        used = min(gama, 26)
+        of = [oh[k] for k in range(used - 1)] + [oh[-1]]
+        rf = [rh[k] for k in range(used - 1)] + [rh[-1]]
+        ret, s1, s2, s3 = oracle.stvssim(of, rf, g["dirs"][i], w, h, wint, ov, gama, comp)
+        np.testing.assert_array_equal(np.float32([s1, s2, s3, ret]), g["out"][i][1:], err_msg=str(g["meta"][i]))
+    lam = g["lambda"]
+    for qp in range(52):
+        assert oracle.lambda_2(qp) == lam[qp, 0]
+        assert oracle.adjust_lambda(oracle.lambda_2(qp), 0.25 + qp * 0.05) == lam[qp, 1]
