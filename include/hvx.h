@@ -1,0 +1,151 @@
+/* hvx.h -- C-ABI of the MI355X-native HM-16.5rc1 CU mode-decision hot path (libhvx.so).
+ *
+ * Plain pointers and sizes only (no torch / HIP types in signatures).  All
+ * batch entry points are asynchronous on the context's HIP stream; every
+ * pointer argument named d_* is DEVICE memory (hipMalloc'd or a torch tensor),
+ * h_* is host memory.  The caller owns all buffers; the context owns only its
+ * stream and constant tables.  Every function returns 0 on success or a
+ * negative HVX_E_* code (HIP errors are mapped to HVX_E_HIP - hipError_t);
+ * hvx_last_error() gives the message.  HM itself has no return codes and
+ * fails fast (assert/exit, TComTrQuant.cpp:891,913), so the C++ shims over this
+ * ABI abort() on a negative status.
+ *
+ * Each entry point replaces a reference interface (paths relative to
+ * /root/reference/hm-16.5rc1/source/Lib, or stvssim_src/...):
+ *
+ *   hvx_dist_batch        TComRdCost::setDistParam + DistParam::DistFunc, getDistPart
+ *                         (TComRdCost.h:60,153-158,221; TComRdCost.cpp:294-451) -- the
+ *                         FpDistFunc function pointer is HM's native plug-in seam.
+ *   hvx_interp_batch      TComInterpolationFilter::filterHor / filterVer
+ *                         (TComInterpolationFilter.h:56-77; .cpp:341,377)
+ *   hvx_tu_forward_batch  TComTrQuant::transformNxN (TComTrQuant.h:98-337; .cpp:1460)
+ *   hvx_tu_inverse_batch  TComTrQuant::invTransformNxN (TComTrQuant.cpp:1547)
+ *   hvx_tu_pipeline_batch transformNxN + invTransformNxN + TComRdCost::getDistPart(SSE)
+ *                         as called back-to-back per TU by TEncSearch::xEstimateInterResidualQT
+ *                         (TEncSearch.cpp:4632-4711) and xIntraCodingTUBlock (:1262-1384)
+ *   hvx_me_batch          TEncSearch::xMotionEstimation, uni-prediction path
+ *                         (TEncSearch.h:126-215; TEncSearch.cpp:3663-3760, xTZSearch :3881,
+ *                         xPatternSearchFracDIF :4240)
+ *   hvx_ssim_batch        compute_SSIM (stvssim_src/stvssimrdo2_att/lencod/src/stvssim.c:491)
+ *   hvx_stvssim_batch     compute_stVSSIM (stvssim.c:587)
+ *   hvx_plane_from_pel    TComPicYuv int16 padded plane -> device 8-bit padded plane, with
+ *                         TComPicYuv::extendPicBorder (TComPicYuv.cpp:197)
+ */
+#ifndef HVX_H
+#define HVX_H
+#include <stddef.h>
+#include <stdint.h>
+#include "hvx_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HVX_OK 0
+#define HVX_E_INVALID -1   /* bad argument (shape/size the kernel does not support) */
+#define HVX_E_NODEV -2     /* no HIP device */
+#define HVX_E_HIP -1000    /* HVX_E_HIP - (int)hipError_t */
+
+typedef struct hvx_ctx hvx_ctx;
+
+int hvx_create(int device, hvx_ctx **out);
+int hvx_destroy(hvx_ctx *ctx);
+/* Run subsequent batches on an external stream (hipStream_t passed as void*); NULL = own stream. */
+int hvx_set_stream(hvx_ctx *ctx, void *stream);
+void *hvx_get_stream(hvx_ctx *ctx);
+int hvx_sync(hvx_ctx *ctx);
+const char *hvx_last_error(void);
+int hvx_version(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Distortion.  kind: HVX_DIST_* below.  org/cur are int16 (HM Pel) sample arrays; each
+ * job gives element offsets and strides into d_org / d_cur.  Output: Distortion (uint32).
+ * ------------------------------------------------------------------------------------- */
+#define HVX_DIST_SAD_ME 0   /* setDistParam(pattern) dispatch: 4/8/16/32/64/12/24/48 honour sub_shift */
+#define HVX_DIST_SAD 1      /* getDistPart(DF_SAD) / xGetSAD: all rows (sub_shift ignored) */
+#define HVX_DIST_SATD 2     /* xGetHADs: 8x8 / 4x4 / 2x2 Hadamard tiles */
+#define HVX_DIST_SSE 3      /* getDistPart(DF_SSE), luma */
+#define HVX_DIST_SSE_W 4    /* getDistPart(DF_SSE), chroma: (uint32)(weight * sse) */
+
+typedef struct hvx_dist_job {
+  int32_t kind, w, h, sub_shift;
+  int64_t org_off, cur_off;       /* element offsets */
+  int32_t org_stride, cur_stride; /* elements */
+  double weight;                  /* m_distortionWeight[compID] for HVX_DIST_SSE_W */
+} hvx_dist_job;
+
+int hvx_dist_batch(hvx_ctx *ctx, const int16_t *d_org, const int16_t *d_cur, const hvx_dist_job *d_jobs, int n,
+                   uint32_t *d_out);
+
+/* ---------------------------------------------------------------------------------------
+ * Interpolation.  One job = one filterHor (vertical=0) or filterVer (vertical=1) call.
+ * is_luma: 8-tap quarter-pel luma, else 4-tap eighth-pel chroma (4:2:0 frac index).
+ * src_off points at the block origin (the filter reads (N/2-1) samples before it).
+ * ------------------------------------------------------------------------------------- */
+typedef struct hvx_interp_job {
+  int32_t is_luma, vertical, frac, is_first, is_last, w, h, pad_;
+  int64_t src_off, dst_off;
+  int32_t src_stride, dst_stride;
+} hvx_interp_job;
+
+int hvx_interp_batch(hvx_ctx *ctx, const int16_t *d_src, int16_t *d_dst, const hvx_interp_job *d_jobs, int n);
+
+/* ---------------------------------------------------------------------------------------
+ * Transform units.  TU i reads its desc d_desc[i], its estBits table d_est[d_est_idx[i]]
+ * (d_est_idx may be NULL: TU i uses d_est[i]) and w*h contiguous elements at element
+ * offset d_off[i] of every per-TU array (residual in/out int16 row-major, levels int32,
+ * optional temp (transform output) / arl (adaptive-QP levels) int32, may be NULL).
+ * d_abs_sum[i] receives uiAbsSum.
+ * ------------------------------------------------------------------------------------- */
+int hvx_tu_forward_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const hvx_estbits *d_est, const int32_t *d_est_idx,
+                         const int64_t *d_off, int n, const int16_t *d_residual, int32_t *d_temp, int32_t *d_levels,
+                         int32_t *d_arl, int32_t *d_abs_sum);
+int hvx_tu_inverse_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t *d_off, int n, const int32_t *d_levels,
+                         int16_t *d_residual_out);
+/* forward + inverse + SSE(residual, reconstructed residual) = distortion of the coded TU */
+int hvx_tu_pipeline_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const hvx_estbits *d_est, const int32_t *d_est_idx,
+                          const int64_t *d_off, int n, const int16_t *d_residual, int32_t *d_levels,
+                          int32_t *d_abs_sum, int16_t *d_residual_out, uint32_t *d_sse);
+
+/* ---------------------------------------------------------------------------------------
+ * Motion estimation.  Planes are 8-bit padded planes (margin HVX_PLANE_MARGIN on every
+ * side, luma stride `stride` bytes); d_cur_planes[j.cur_idx] / d_ref_planes[j.ref_idx]
+ * point at sample (0,0) of each picture (device pointers, array itself in device memory).
+ * ------------------------------------------------------------------------------------- */
+#define HVX_PLANE_MARGIN 80
+int hvx_me_batch(hvx_ctx *ctx, const uint8_t *const *d_cur_planes, const uint8_t *const *d_ref_planes, int stride,
+                 const hvx_me_job *d_jobs, int n, hvx_me_result *d_out);
+
+/* ---------------------------------------------------------------------------------------
+ * SSIM metric (float32, JM stvssim semantics).  Blocks are 8-bit with their own strides.
+ * ------------------------------------------------------------------------------------- */
+typedef struct hvx_ssim_job {
+  int32_t w, h, wint, overlap;
+  int64_t org_off, rec_off;
+  int32_t org_stride, rec_stride;
+} hvx_ssim_job;
+int hvx_ssim_batch(hvx_ctx *ctx, const uint8_t *d_org, const uint8_t *d_rec, const hvx_ssim_job *d_jobs, int n,
+                   float *d_out);
+
+/* stVSSIM: job j uses frames d_hist_org[j*26 + o], d_hist_rec[j*26 + o] (o < min(gama,26);
+ * entry min(gama,26)-1 is the current frame) with stride hist_stride, and the per-pixel
+ * direction map d_dirs + dirs_off (float, stride dirs_stride, luma resolution).
+ * Output per job: {ssim, ssim3d, stvssim, return value}. */
+typedef struct hvx_stvssim_job {
+  int32_t w, h, wint, overlap, gama, comp, hist_stride, dirs_stride;
+  int64_t dirs_off;
+} hvx_stvssim_job;
+int hvx_stvssim_batch(hvx_ctx *ctx, const uint8_t *const *d_hist_org, const uint8_t *const *d_hist_rec,
+                      const float *d_dirs, const hvx_stvssim_job *d_jobs, int n, float *d_out4);
+
+/* ---------------------------------------------------------------------------------------
+ * Picture upload: HM int16 plane (width x height samples, any stride, device copy) ->
+ * 8-bit padded plane (stride = width + 2*HVX_PLANE_MARGIN), borders extended.
+ * ------------------------------------------------------------------------------------- */
+int hvx_plane_from_pel(hvx_ctx *ctx, const int16_t *d_pel, int pel_stride, int width, int height, uint8_t *d_plane);
+int hvx_plane_extend(hvx_ctx *ctx, uint8_t *d_plane, int width, int height);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

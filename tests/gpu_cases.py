@@ -1,0 +1,198 @@
+"""GPU-vs-oracle parity cases shared by tests/test_gpu_parity.py and __graft_entry__.smoke().
+
+Every function runs the HIP path (video_codecs_amd.hvx -> libhvx.so) and checks it
+against the CPU oracle (test infrastructure) and/or the reference goldens; it raises
+AssertionError on the first mismatch.
+"""
+import numpy as np
+
+import oracle
+from oracle import make_yuv
+from tests import golden_cases as gc
+from video_codecs_amd import _abi, hvx
+
+M = _abi.PLANE_MARGIN
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def padded_plane(img):
+    """uint8 HxW -> padded plane (H+2M)x(W+2M) with replicated borders (extendPicBorder)."""
+    return np.pad(img, M, mode="edge")
+
+
+def device_planes(planes):
+    """list of padded uint8 planes (same shape) -> (device tensors, int64 device tensor of origin pointers)."""
+    torch = _torch()
+    ts = [torch.from_numpy(np.ascontiguousarray(p)).cuda() for p in planes]
+    W = planes[0].shape[1] - 2 * M
+    ptrs = torch.tensor([hvx.plane_origin_ptr(t, W) for t in ts], dtype=torch.int64).cuda()
+    return ts, ptrs
+
+
+def run_me(planes_cur, planes_ref, jobs):
+    torch = _torch()
+    cur_t, cur_p = device_planes(planes_cur)
+    ref_t, ref_p = device_planes(planes_ref)
+    stride = planes_cur[0].shape[1]
+    jd = hvx.to_device(jobs)
+    out = torch.zeros(len(jobs) * _abi.ME_RESULT.itemsize, dtype=torch.uint8, device="cuda")
+    hvx.me_batch(cur_p, ref_p, stride, jd, len(jobs), out)
+    torch.cuda.synchronize()
+    del cur_t, ref_t
+    return hvx.from_device(out, _abi.ME_RESULT)
+
+
+def me_jobs_random(rng, n, W, H, n_planes=1):
+    jobs = np.zeros(n, _abi.ME_JOB)
+    shapes = [(64, 64), (32, 32), (16, 16), (8, 8), (64, 32), (32, 64), (16, 8), (8, 16), (64, 16), (64, 48),
+              (16, 64), (48, 64), (32, 8), (32, 24), (8, 32), (24, 32), (16, 4), (16, 12), (4, 16), (12, 16), (8, 4), (4, 8)]
+    for i in range(n):
+        w, h = shapes[rng.integers(len(shapes))]
+        cu = max(w, h)
+        cu = 64 if cu > 32 else 32 if cu > 16 else 16 if cu > 8 else 8
+        cux = rng.integers(0, (W - cu) // cu + 1) * cu
+        cuy = rng.integers(0, (H - cu) // cu + 1) * cu
+        pux = cux + (rng.integers(0, (cu - w) // 4 + 1) * 4 if w < cu else 0)
+        puy = cuy + (rng.integers(0, (cu - h) // 4 + 1) * 4 if h < cu else 0)
+        lam = 0.57 * 2.0 ** ((int(rng.integers(22, 38)) - 12) / 3.0)
+        j = jobs[i]
+        j["pic_w"], j["pic_h"], j["max_cu"] = W, H, 64
+        j["cu_x"], j["cu_y"], j["pu_x"], j["pu_y"], j["w"], j["h"] = cux, cuy, pux, puy, w, h
+        j["pred_x"], j["pred_y"] = rng.integers(-60, 61), rng.integers(-60, 61)
+        if i % 6 == 1:
+            j["pred_x"], j["pred_y"] = rng.integers(-900, 900), rng.integers(-600, 600)
+        j["use_int2nx2n"] = i % 3 == 0
+        j["i2_x"], j["i2_y"] = rng.integers(-20, 21), rng.integers(-20, 21)
+        j["bits_in"] = rng.integers(0, 8)
+        j["search_range"] = 64
+        j["lambda_motion"] = _abi.lambda_motion_sad(lam)
+        j["flags"] = _abi.ME_FEN | _abi.ME_HADME | _abi.ME_SMOOTHMV
+        j["cur_idx"] = j["ref_idx"] = rng.integers(0, n_planes)
+    return jobs
+
+
+def check_me_random(seed, n_jobs, width, height):
+    rng = np.random.default_rng(seed)
+    cur, ref = [], []
+    for p in range(2):
+        if p == 0:
+            a = make_yuv.random_frame(width, height, seed)[:width * height].reshape(height, width)
+            b = make_yuv.random_frame(width, height, seed + 1)[:width * height].reshape(height, width)
+        else:
+            a = make_yuv.smooth_frame(width, height, 3)[:width * height].reshape(height, width)
+            b = make_yuv.smooth_frame(width, height, 2)[:width * height].reshape(height, width)
+        cur.append(padded_plane(a))
+        ref.append(padded_plane(b))
+    jobs = me_jobs_random(rng, n_jobs, width, height, n_planes=2)
+    got = run_me(cur, ref, jobs)
+    for i in range(n_jobs):
+        exp = oracle.motion_estimation(cur[jobs["cur_idx"][i]], ref[jobs["ref_idx"][i]], jobs[i])
+        assert tuple(got[i]) == tuple(exp), (i, jobs[i], got[i], exp)
+    return True
+
+
+def check_me_golden():
+    g = gc.load("me.bin")
+    planes, jobs, exp = gc.me_jobs(g)
+    cur = [planes[p, 0] for p in range(planes.shape[0])]
+    ref = [planes[p, 1] for p in range(planes.shape[0])]
+    got = run_me(cur, ref, jobs)
+    for i in range(len(jobs)):
+        assert [int(x) for x in got[i]] == [int(x) for x in exp[i]], (i, jobs[i], got[i], exp[i])
+    return len(jobs)
+
+
+# ------------------------------------------------------------------------------------------ TUs
+def run_tu(descs, ests, residuals, mode="forward", levels_in=None):
+    """descs: TU_DESC array; ests: [n, 224] int32; residuals/levels_in: list of arrays (w*h)."""
+    torch = _torch()
+    n = len(descs)
+    sizes = [int(d["width"]) * int(d["height"]) for d in descs]
+    off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    total = int(sum(sizes))
+    d_desc = hvx.to_device(descs)
+    d_off = torch.from_numpy(off).cuda()
+    if mode == "inverse":
+        lev = torch.from_numpy(np.concatenate([np.asarray(x, np.int32).reshape(-1) for x in levels_in])).cuda()
+        res_out = torch.zeros(total, dtype=torch.int16, device="cuda")
+        hvx.tu_inverse_batch(d_desc, d_off, n, lev, res_out)
+        torch.cuda.synchronize()
+        r = res_out.cpu().numpy()
+        return [r[o:o + s] for o, s in zip(off, sizes)]
+    d_est = torch.from_numpy(np.ascontiguousarray(ests, np.int32).reshape(-1)).cuda()
+    res = torch.from_numpy(np.concatenate([np.asarray(x, np.int16).reshape(-1) for x in residuals])).cuda()
+    lev = torch.zeros(total, dtype=torch.int32, device="cuda")
+    absum = torch.zeros(n, dtype=torch.int32, device="cuda")
+    if mode == "forward":
+        temp = torch.zeros(total, dtype=torch.int32, device="cuda")
+        arl = torch.zeros(total, dtype=torch.int32, device="cuda")
+        hvx.tu_forward_batch(d_desc, d_est, None, d_off, n, res, temp, lev, arl, absum)
+        torch.cuda.synchronize()
+        t, l, a = temp.cpu().numpy(), lev.cpu().numpy(), absum.cpu().numpy()
+        return [(t[o:o + s], l[o:o + s], int(a[i])) for i, (o, s) in enumerate(zip(off, sizes))]
+    res_out = torch.zeros(total, dtype=torch.int16, device="cuda")
+    sse = torch.zeros(n, dtype=torch.int32, device="cuda")
+    hvx.tu_pipeline_batch(d_desc, d_est, None, d_off, n, res, lev, absum, res_out, sse)
+    torch.cuda.synchronize()
+    l, a, r, s_ = lev.cpu().numpy(), absum.cpu().numpy(), res_out.cpu().numpy(), sse.cpu().numpy().view(np.uint32)
+    return [(l[o:o + s], int(a[i]), r[o:o + s], int(s_[i])) for i, (o, s) in enumerate(zip(off, sizes))]
+
+
+def golden_estbits_pool():
+    pool = []
+    for f in gc.TU_FILES:
+        g = gc.load(f)
+        pool.append(g["fwd_estbits"])
+    return np.concatenate(pool)
+
+
+def random_tus(rng, n, est_pool):
+    descs = np.zeros(n, _abi.TU_DESC)
+    ests, res = [], []
+    for i in range(n):
+        d = descs[i]
+        log2 = int(rng.integers(2, 6))
+        comp = int(rng.integers(0, 3)) if log2 < 5 else 0
+        qp = int(rng.integers(0, 52))
+        d["comp"], d["width"], d["height"], d["log2_size"] = comp, 1 << log2, 1 << log2, log2
+        d["is_intra"] = int(rng.integers(0, 2))
+        d["scan_type"] = int(rng.integers(0, 3)) if (d["is_intra"] and log2 <= 3) else 0
+        d["use_dst"] = int(d["is_intra"] and comp == 0 and log2 == 2)
+        d["transform_skip"] = int(log2 == 2 and rng.integers(0, 4) == 0)
+        d["tr_idx"] = int(rng.integers(0, 2))
+        d["ctx_qt_cbf"] = int(rng.integers(0, 3 if comp == 0 else 5))
+        d["slice_type"] = int(rng.integers(0, 3))
+        d["qp_per"], d["qp_rem"] = qp // 6, qp % 6
+        d["sign_hiding"] = int(rng.integers(0, 4) != 0)
+        mode = int(rng.integers(0, 5))
+        d["use_rdoq"] = int(mode != 0)
+        d["use_rdoq_ts"] = int(mode != 0)
+        d["selective_rdoq"] = int(mode == 4)
+        d["max_log2_tr_range"], d["bit_depth"] = 15, 8
+        d["golomb_rice_stat"] = 0
+        d["lambda"] = 0.57 * 2.0 ** ((qp - 12) / 3.0) * (1.0 if comp == 0 else 0.8)
+        ests.append(est_pool[int(rng.integers(0, len(est_pool)))])
+        amp = [255, 60, 12, 3][int(rng.integers(0, 4))]
+        res.append(rng.integers(-amp, amp + 1, size=(1 << log2) * (1 << log2)).astype(np.int16))
+    return descs, np.stack(ests), res
+
+
+def check_tu_random(seed, n):
+    rng = np.random.default_rng(seed)
+    descs, ests, res = random_tus(rng, n, golden_estbits_pool())
+    got = run_tu(descs, ests, res, "pipeline")
+    for i in range(n):
+        w = int(descs[i]["width"])
+        t, l, _, a = oracle.transform_nxn(descs[i], ests[i], res[i].reshape(w, w))
+        rr = oracle.inv_transform_nxn(descs[i], l)
+        gl, ga, gr, gs = got[i]
+        np.testing.assert_array_equal(gl, l, err_msg=f"levels tu {i} {descs[i]}")
+        assert ga == a, (i, ga, a)
+        np.testing.assert_array_equal(gr, rr.reshape(-1), err_msg=f"recon residual tu {i}")
+        sse = int(((res[i].astype(np.int64) - rr.reshape(-1)) ** 2).sum())
+        assert gs == sse, (i, gs, sse)
+    return True

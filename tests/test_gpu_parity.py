@@ -1,0 +1,140 @@
+"""HIP path (libhvx.so via the C-ABI) vs reference goldens and the CPU oracle.  MI355X only."""
+import numpy as np
+import pytest
+
+import oracle
+from tests import golden_cases as gc
+from tests import gpu_cases
+from video_codecs_amd import _abi, hvx
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def test_dist_golden_gpu(torch):
+    g = gc.load("dist.bin")
+    meta, org, cur, wgt, out = g["meta"], g["org"], g["cur"], g["weight"], g["out"]
+    n = meta.shape[0]
+    jobs = np.zeros(n, hvx.DIST_JOB)
+    kind_map = {0: hvx.DIST_SAD_ME, 1: hvx.DIST_SAD_ME, 2: hvx.DIST_SATD, 3: hvx.DIST_SSE, 4: hvx.DIST_SSE_W, 5: hvx.DIST_SAD}
+    for i in range(n):
+        k, w, h, sub = (int(x) for x in meta[i])
+        jobs[i] = (kind_map[k], w, h, sub, i * 4096, i * 4096, 64, 64, wgt[i])
+    d_org = torch.from_numpy(org.astype(np.int16).reshape(-1)).cuda()
+    d_cur = torch.from_numpy(cur.astype(np.int16).reshape(-1)).cuda()
+    d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    hvx.dist_batch(d_org, d_cur, hvx.to_device(jobs), n, d_out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d_out.cpu().numpy().view(np.uint32), out)
+
+
+def test_interp_golden_gpu(torch):
+    g = gc.load("interp.bin")
+    meta, src, out = g["meta"], g["src"], g["out"]
+    n = meta.shape[0]
+    jobs = np.zeros(n, hvx.INTERP_JOB)
+    for i in range(n):
+        is_luma, d, frac, first, last, w, h = (int(x) for x in meta[i])
+        jobs[i] = (is_luma, d, frac, first, last, w, h, 0, i * 6400 + 8 * 80 + 8, i * 6400, 80, 80)
+    d_src = torch.from_numpy(src.reshape(-1).copy()).cuda()
+    d_dst = torch.zeros(n * 6400, dtype=torch.int16, device="cuda")
+    hvx.interp_batch(d_src, d_dst, hvx.to_device(jobs), n)
+    torch.cuda.synchronize()
+    got = d_dst.cpu().numpy().reshape(n, 80, 80)
+    for i in range(n):
+        w, h = int(meta[i][5]), int(meta[i][6])
+        np.testing.assert_array_equal(got[i][:h, :w], out[i][:h, :w], err_msg=str(meta[i]))
+
+
+@pytest.mark.parametrize("name", gc.TU_FILES)
+def test_tu_forward_golden_gpu(torch, name):
+    recs = list(gc.fwd_records(gc.load(name)))
+    descs = np.concatenate([r[0] for r in recs])
+    ests = np.stack([r[1] for r in recs])
+    got = gpu_cases.run_tu(descs, ests, [r[2] for r in recs], "forward")
+    for i, (desc, _, _, temp, lev, absum) in enumerate(recs):
+        t, l, a = got[i]
+        if not desc["transquant_bypass"][0]:
+            np.testing.assert_array_equal(t, temp, err_msg=f"{name} {i} transform")
+        np.testing.assert_array_equal(l, lev, err_msg=f"{name} {i} levels {desc}")
+        assert a == absum, (name, i)
+
+
+@pytest.mark.parametrize("name", gc.TU_FILES)
+def test_tu_inverse_golden_gpu(torch, name):
+    recs = list(gc.inv_records(gc.load(name)))
+    descs = np.concatenate([r[0] for r in recs])
+    got = gpu_cases.run_tu(descs, None, None, "inverse", levels_in=[r[1] for r in recs])
+    for i, (_, _, res) in enumerate(recs):
+        np.testing.assert_array_equal(got[i], res.reshape(-1), err_msg=f"{name} {i}")
+
+
+def test_tu_pipeline_random_gpu(torch):
+    assert gpu_cases.check_tu_random(seed=1234, n=600)
+
+
+def test_me_golden_gpu(torch):
+    assert gpu_cases.check_me_golden() > 300
+
+
+def test_me_random_gpu(torch):
+    assert gpu_cases.check_me_random(seed=99, n_jobs=300, width=640, height=384)
+
+
+def test_me_edge_pictures_gpu(torch):
+    # tiny / non-CTU-multiple pictures exercise clipMv and the border extension margins
+    assert gpu_cases.check_me_random(seed=5, n_jobs=80, width=136, height=72)
+
+
+def test_ssim_golden_gpu(torch):
+    g = gc.load("ssim.bin")
+    meta, oh, rh, dirs, out = g["meta"], g["org_hist"], g["rec_hist"], g["dirs"], g["out"]
+    n = meta.shape[0]
+    B = oh.shape[-1]
+    jobs = np.zeros(n, hvx.SSIM_JOB)
+    for i in range(n):
+        w, h, wint, ov, gama, comp = (int(x) for x in meta[i])
+        base = (i * 26 + 25) * B * B
+        jobs[i] = (w, h, wint, ov, base, base, B, B)
+    d_o = torch.from_numpy(oh.reshape(-1).copy()).cuda()
+    d_r = torch.from_numpy(rh.reshape(-1).copy()).cuda()
+    d_out = torch.zeros(n, dtype=torch.float32, device="cuda")
+    hvx.ssim_batch(d_o, d_r, hvx.to_device(jobs), n, d_out)
+    # stVSSIM
+    sj = np.zeros(n, hvx.STVSSIM_JOB)
+    po, pr = [], []
+    for i in range(n):
+        w, h, wint, ov, gama, comp = (int(x) for x in meta[i])
+        used = min(gama, 26)
+        sj[i] = (w, h, wint, ov, gama, comp, B, 2 * B, i * 4 * B * B)
+        frames = list(range(used - 1)) + [25] + [25] * (26 - used)
+        po += [d_o.data_ptr() + (i * 26 + f) * B * B for f in frames]
+        pr += [d_r.data_ptr() + (i * 26 + f) * B * B for f in frames]
+    d_po = torch.tensor(po, dtype=torch.int64).cuda()
+    d_pr = torch.tensor(pr, dtype=torch.int64).cuda()
+    d_dirs = torch.from_numpy(dirs.reshape(-1).copy()).cuda()
+    d_out4 = torch.zeros(n * 4, dtype=torch.float32, device="cuda")
+    hvx.stvssim_batch(d_po, d_pr, d_dirs, hvx.to_device(sj), n, d_out4)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d_out.cpu().numpy(), out[:, 0])
+    np.testing.assert_array_equal(d_out4.cpu().numpy().reshape(n, 4), out[:, 1:])
+
+
+def test_plane_from_pel_gpu(torch):
+    rng = np.random.default_rng(3)
+    W, H, stride = 200, 120, 224
+    pel = rng.integers(0, 256, size=(H, stride)).astype(np.int16)
+    d_pel = torch.from_numpy(pel.reshape(-1).copy()).cuda()
+    M = _abi.PLANE_MARGIN
+    plane = torch.zeros((H + 2 * M) * (W + 2 * M), dtype=torch.uint8, device="cuda")
+    hvx.plane_from_pel(d_pel, stride, W, H, plane)
+    torch.cuda.synchronize()
+    exp = np.pad(pel[:, :W].astype(np.uint8), M, mode="edge")
+    np.testing.assert_array_equal(plane.cpu().numpy().reshape(H + 2 * M, W + 2 * M), exp)

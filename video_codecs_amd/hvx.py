@@ -1,0 +1,165 @@
+"""Python binding of libhvx.so (include/hvx.h), the MI355X HIP implementation of the
+HM-16.5rc1 CU mode-decision kernels.
+
+Device memory comes from torch (ROCm); torch is plumbing here, not the product.  Every
+batch runs on torch's current HIP stream so it orders naturally with torch copies.
+There is no CPU fallback: if libhvx.so or the GPU is missing, these calls raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhvx.so")
+
+_lib = None
+_ctx = {}
+
+
+class HvxError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libhvx.so (raises if it was not built: run __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HvxError(f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        P, I = ctypes.c_void_p, ctypes.c_int
+        for name, args in {
+            "hvx_create": [I, ctypes.POINTER(P)], "hvx_destroy": [P], "hvx_set_stream": [P, P], "hvx_sync": [P],
+            "hvx_dist_batch": [P, P, P, P, I, P], "hvx_interp_batch": [P, P, P, P, I],
+            "hvx_tu_forward_batch": [P, P, P, P, P, I, P, P, P, P, P],
+            "hvx_tu_inverse_batch": [P, P, P, I, P, P],
+            "hvx_tu_pipeline_batch": [P, P, P, P, P, I, P, P, P, P, P],
+            "hvx_me_batch": [P, P, P, I, P, I, P], "hvx_ssim_batch": [P, P, P, P, I, P],
+            "hvx_stvssim_batch": [P, P, P, P, P, I, P],
+            "hvx_plane_from_pel": [P, P, I, I, I, P], "hvx_plane_extend": [P, P, I, I],
+        }.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = I
+        L.hvx_last_error.restype = ctypes.c_char_p
+        L.hvx_last_error.argtypes = []
+        L.hvx_version.restype = I
+        L.hvx_get_stream.restype = P
+        L.hvx_get_stream.argtypes = [P]
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise HvxError(f"{what} failed ({rc}): {lib().hvx_last_error().decode(errors='replace')}")
+
+
+def context(device=None):
+    """Per-device hvx_ctx bound to torch's current stream."""
+    import torch
+    if not torch.cuda.is_available():
+        raise HvxError("no HIP device visible: the hvx path needs an MI355X (no CPU fallback)")
+    dev = torch.cuda.current_device() if device is None else int(device)
+    if dev not in _ctx:
+        p = ctypes.c_void_p()
+        _check(lib().hvx_create(dev, ctypes.byref(p)), "hvx_create")
+        _ctx[dev] = p
+    c = _ctx[dev]
+    _check(lib().hvx_set_stream(c, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "hvx_set_stream")
+    return c
+
+
+def _ptr(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def to_device(arr, device="cuda"):
+    """numpy (incl. structured job arrays) -> torch uint8/typed device tensor (raw bytes for structs)."""
+    import torch
+    a = np.ascontiguousarray(arr)
+    if a.dtype.fields is not None:
+        return torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to(device)
+    return torch.from_numpy(a.copy()).to(device)
+
+
+def from_device(t, dtype, count=None):
+    """device tensor -> numpy; `dtype` may be a structured dtype (bytes are reinterpreted)."""
+    a = t.detach().cpu().numpy()
+    if np.dtype(dtype).fields is not None:
+        a = a.view(np.uint8).reshape(-1).view(dtype)
+    return a if count is None else a[:count]
+
+
+# -------------------------------------------------------------------------------------- batches
+DIST_JOB = np.dtype([("kind", "<i4"), ("w", "<i4"), ("h", "<i4"), ("sub_shift", "<i4"), ("org_off", "<i8"),
+                     ("cur_off", "<i8"), ("org_stride", "<i4"), ("cur_stride", "<i4"), ("weight", "<f8")], align=True)
+INTERP_JOB = np.dtype([("is_luma", "<i4"), ("vertical", "<i4"), ("frac", "<i4"), ("is_first", "<i4"),
+                       ("is_last", "<i4"), ("w", "<i4"), ("h", "<i4"), ("pad_", "<i4"), ("src_off", "<i8"),
+                       ("dst_off", "<i8"), ("src_stride", "<i4"), ("dst_stride", "<i4")], align=True)
+SSIM_JOB = np.dtype([("w", "<i4"), ("h", "<i4"), ("wint", "<i4"), ("overlap", "<i4"), ("org_off", "<i8"),
+                     ("rec_off", "<i8"), ("org_stride", "<i4"), ("rec_stride", "<i4")], align=True)
+STVSSIM_JOB = np.dtype([("w", "<i4"), ("h", "<i4"), ("wint", "<i4"), ("overlap", "<i4"), ("gama", "<i4"),
+                        ("comp", "<i4"), ("hist_stride", "<i4"), ("dirs_stride", "<i4"), ("dirs_off", "<i8")], align=True)
+assert DIST_JOB.itemsize == 48 and INTERP_JOB.itemsize == 56 and SSIM_JOB.itemsize == 40 and STVSSIM_JOB.itemsize == 40
+
+DIST_SAD_ME, DIST_SAD, DIST_SATD, DIST_SSE, DIST_SSE_W = 0, 1, 2, 3, 4
+
+
+def dist_batch(org, cur, jobs_dev, n, out):
+    _check(lib().hvx_dist_batch(context(), _ptr(org), _ptr(cur), _ptr(jobs_dev), n, _ptr(out)), "hvx_dist_batch")
+
+
+def interp_batch(src, dst, jobs_dev, n):
+    _check(lib().hvx_interp_batch(context(), _ptr(src), _ptr(dst), _ptr(jobs_dev), n), "hvx_interp_batch")
+
+
+def tu_forward_batch(desc, est, est_idx, off, n, residual, temp, levels, arl, abs_sum):
+    _check(lib().hvx_tu_forward_batch(context(), _ptr(desc), _ptr(est), _ptr(est_idx), _ptr(off), n, _ptr(residual),
+                                      _ptr(temp), _ptr(levels), _ptr(arl), _ptr(abs_sum)), "hvx_tu_forward_batch")
+
+
+def tu_inverse_batch(desc, off, n, levels, residual_out):
+    _check(lib().hvx_tu_inverse_batch(context(), _ptr(desc), _ptr(off), n, _ptr(levels), _ptr(residual_out)),
+           "hvx_tu_inverse_batch")
+
+
+def tu_pipeline_batch(desc, est, est_idx, off, n, residual, levels, abs_sum, residual_out, sse):
+    _check(lib().hvx_tu_pipeline_batch(context(), _ptr(desc), _ptr(est), _ptr(est_idx), _ptr(off), n, _ptr(residual),
+                                       _ptr(levels), _ptr(abs_sum), _ptr(residual_out), _ptr(sse)),
+           "hvx_tu_pipeline_batch")
+
+
+def me_batch(cur_planes_ptrs, ref_planes_ptrs, stride, jobs_dev, n, out):
+    """cur/ref_planes_ptrs: int64 device tensors holding device pointers to plane sample (0,0)."""
+    _check(lib().hvx_me_batch(context(), _ptr(cur_planes_ptrs), _ptr(ref_planes_ptrs), stride, _ptr(jobs_dev), n,
+                              _ptr(out)), "hvx_me_batch")
+
+
+def ssim_batch(org, rec, jobs_dev, n, out):
+    _check(lib().hvx_ssim_batch(context(), _ptr(org), _ptr(rec), _ptr(jobs_dev), n, _ptr(out)), "hvx_ssim_batch")
+
+
+def stvssim_batch(hist_org_ptrs, hist_rec_ptrs, dirs, jobs_dev, n, out4):
+    _check(lib().hvx_stvssim_batch(context(), _ptr(hist_org_ptrs), _ptr(hist_rec_ptrs), _ptr(dirs), _ptr(jobs_dev), n,
+                                   _ptr(out4)), "hvx_stvssim_batch")
+
+
+def plane_from_pel(pel, pel_stride, width, height, plane):
+    _check(lib().hvx_plane_from_pel(context(), _ptr(pel), pel_stride, width, height, _ptr(plane)), "hvx_plane_from_pel")
+
+
+def plane_extend(plane, width, height):
+    _check(lib().hvx_plane_extend(context(), _ptr(plane), width, height), "hvx_plane_extend")
+
+
+def sync():
+    _check(lib().hvx_sync(context()), "hvx_sync")
+
+
+def plane_origin_ptr(plane, width, margin=_abi.PLANE_MARGIN):
+    """device address of sample (0,0) of a padded plane tensor of row stride width + 2*margin."""
+    return plane.data_ptr() + margin * (width + 2 * margin) + margin
