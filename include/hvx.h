@@ -28,6 +28,9 @@
  *                         xPatternSearchFracDIF :4240)
  *   hvx_ssim_batch        compute_SSIM (stvssim_src/stvssimrdo2_att/lencod/src/stvssim.c:491)
  *   hvx_stvssim_batch     compute_stVSSIM (stvssim.c:587)
+ *   hvx_ctu_analyze       TEncCu::compressCtu's inter 2Nx2N analysis for every CU of every CTU
+ *                         (TEncCu.cpp:228,349,1291 -> predInterSearch/encodeResAndCalcRdInterCU):
+ *                         the bench workload, composition of the kernels above
  *   hvx_plane_from_pel    TComPicYuv int16 padded plane -> device 8-bit padded plane, with
  *                         TComPicYuv::extendPicBorder (TComPicYuv.cpp:197)
  */
@@ -139,8 +142,26 @@ int hvx_stvssim_batch(hvx_ctx *ctx, const uint8_t *const *d_hist_org, const uint
                       const float *d_dirs, const hvx_stvssim_job *d_jobs, int n, float *d_out4);
 
 /* ---------------------------------------------------------------------------------------
+ * CTU analysis pass over a whole picture (hvx_types.h): d_cur = sample (0,0) of the current
+ * 8-bit padded plane, d_refs = device array of n_ref reference-plane origins, d_est4 = device
+ * array of 4 luma estBits tables (TU 4x4..32x32), d_out = nctu*85 hvx_cu_result.  The
+ * caller allocates a device workspace of hvx_ctu_workspace_size() bytes.
+ * ------------------------------------------------------------------------------------- */
+int hvx_ctu_workspace_size(int pic_w, int pic_h, int n_ref, size_t *bytes);
+int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
+                    const hvx_ctu_params *h_params, const hvx_estbits *d_est4, void *d_workspace, size_t ws_bytes,
+                    hvx_cu_result *d_out);
+/* Optional phase timing of hvx_ctu_analyze with HIP events on the launch stream.  Phases:
+ * 0..3 ME of CU depth 0..3 (k_ctu_me_jobs + k_me_ctu_depth), 4 MC/residual (k_ctu_pred_resid),
+ * 5..7 TU pipeline 32x32 / 16x16 / 8x8 (k_tu), 8 per-CU sums (k_ctu_finalize).  Accumulated ms. */
+#define HVX_NPHASE 9
+int hvx_set_timing(hvx_ctx *ctx, int on);
+int hvx_phase_times(hvx_ctx *ctx, double *ms_out, int n, int reset);
+
+/* ---------------------------------------------------------------------------------------
  * Picture upload: HM int16 plane (width x height samples, any stride, device copy) ->
- * 8-bit padded plane (stride = width + 2*HVX_PLANE_MARGIN), borders extended.
+ * 8-bit padded plane (stride = width + 2*HVX_PLANE_MARGIN), borders extended.  d_plane is
+ * the START of the padded allocation ((height + 2*M) rows); sample (0,0) is at M*stride + M.
  * ------------------------------------------------------------------------------------- */
 int hvx_plane_from_pel(hvx_ctx *ctx, const int16_t *d_pel, int pel_stride, int width, int height, uint8_t *d_plane);
 int hvx_plane_extend(hvx_ctx *ctx, uint8_t *d_plane, int width, int height);

@@ -88,6 +88,37 @@ typedef struct hvx_me_result {
   uint32_t cost;              /* ruiCost on exit */
 } hvx_me_result;
 
+/* ---------------------------------------------------------------------------------------
+ * CTU analysis pass (the bench workload; see DESIGN.md "CTU analysis pass").
+ * For every 64x64 CTU and every CU of depth 0..3 (85 square CUs) lying inside the picture:
+ * uni-prediction ME (hvx_me_job semantics) against each reference, best reference =
+ * first minimum of the ME cost, luma motion compensation at the chosen quarter-pel MV,
+ * residual, then every min(CU,32)^2 luma TU of the CU through transformNxN (RDOQ) +
+ * invTransformNxN + SSE.  CU index inside a CTU: depth-major, raster inside each depth
+ * (0 | 1..4 | 5..20 | 21..84).
+ * ------------------------------------------------------------------------------------- */
+#define HVX_CUS_PER_CTU 85
+typedef struct hvx_ctu_params {
+  int32_t pic_w, pic_h;      /* luma samples */
+  int32_t n_ref;             /* reference pictures (<= 8) */
+  int32_t qp;                /* slice QP (luma) */
+  int32_t search_range;      /* 64 */
+  int32_t me_flags;          /* HVX_ME_* */
+  int32_t slice_type;        /* HM SliceType (1 = P) */
+  uint32_t lambda_motion;    /* floor(65536*sqrt(lambda)) */
+  double lambda;             /* RD lambda (TComTrQuant m_dLambda for luma) */
+} hvx_ctu_params;
+
+typedef struct hvx_cu_result {
+  int32_t valid;             /* CU inside the picture */
+  int32_t ref;               /* chosen reference index */
+  int32_t mv_x, mv_y;        /* quarter-pel MV */
+  uint32_t me_cost;          /* ruiCost of the chosen reference */
+  uint32_t sse;              /* sum over the CU's TUs of residual-domain SSE after coding */
+  int32_t abs_sum;           /* sum of uiAbsSum over the CU's TUs */
+  int32_t n_tu;
+} hvx_cu_result;
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,7 @@ def lib():
         L.hvxo_lambda_2.argtypes = [I]
         L.hvxo_adjust_lambda.restype = D
         L.hvxo_adjust_lambda.argtypes = [D, D]
+        L.hvxo_ctu_analyze.argtypes = [P, P, I, P, P, I, I, P]
         L.hvxo_dct_matrix.argtypes = [I, P]
         L.hvxo_scan.restype = ctypes.POINTER(ctypes.c_uint32)
         L.hvxo_scan.argtypes = [I, I, I, I]
@@ -185,6 +186,19 @@ def stvssim(org_frames, rec_frames, dirs, w, h, wint, overlap, gama, comp):
     ret = lib().hvxo_stvssim(po, pr, of[0].shape[-1], _p(d), d.shape[-1], w, h, wint, overlap, gama, comp,
                              ctypes.byref(s1), ctypes.byref(s2), ctypes.byref(s3))
     return float(ret), s1.value, s2.value, s3.value
+
+
+def ctu_analyze(cur_plane, ref_planes, params, est4, ctu_x, ctu_y, margin=_abi.PLANE_MARGIN):
+    """hvxo_ctu_analyze for one CTU: padded uint8 planes -> 85 CU_RESULT records."""
+    c = _c(cur_plane, np.uint8)
+    refs = [_c(r, np.uint8) for r in ref_planes]
+    off = margin * c.shape[1] + margin
+    rp = (ctypes.c_void_p * len(refs))(*[r.ctypes.data + off for r in refs])
+    p = np.ascontiguousarray(params, dtype=_abi.CTU_PARAMS).reshape(1)
+    e = _c(est4, np.int32).reshape(-1)
+    out = np.zeros(_abi.CUS_PER_CTU, _abi.CU_RESULT)
+    lib().hvxo_ctu_analyze(ctypes.c_void_p(c.ctypes.data + off), rp, c.shape[1], _p(p), _p(e), ctu_x, ctu_y, _p(out))
+    return out
 
 
 def lambda_2(qp):

@@ -1315,3 +1315,81 @@ double hvxo_lambda_2(int qp) {
 
 /* adjust_lambda (:1565, active _ADJUST_L2_ body :1707) */
 double hvxo_adjust_lambda(double lambda, double eta) { return lambda * pow(eta, 0.85); }
+
+/* ============================================================================================
+ * CTU analysis pass (hvx_types.h): composition of the restated kernels above.
+ * ========================================================================================== */
+void hvxo_ctu_tu_desc(const hvx_ctu_params *p, int cu_size, int log2, hvx_tu_desc *d) {
+  memset(d, 0, sizeof(*d));
+  d->comp = 0;
+  d->width = d->height = 1 << log2;
+  d->log2_size = log2;
+  d->tr_idx = cu_size > 32 ? 1 : 0;     /* a 64x64 CU is coded with a split transform tree */
+  d->ctx_qt_cbf = 0;                    /* luma getCtxQtCbf at transform depth >= 1 */
+  d->slice_type = p->slice_type;
+  d->qp_per = p->qp / 6;
+  d->qp_rem = p->qp % 6;
+  d->sign_hiding = 1;
+  d->use_rdoq = d->use_rdoq_ts = 1;
+  d->max_log2_tr_range = 15;
+  d->bit_depth = 8;
+  d->lambda = p->lambda;
+}
+
+void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
+                      const hvx_estbits *est, int ctu_x, int ctu_y, hvx_cu_result *out) {
+  int imv[HVX_CUS_PER_CTU][8][2];
+  int base = 0;
+  for (int d = 0; d < 4; d++) {
+    const int S = 64 >> d, g = 1 << d;
+    for (int j = 0; j < g * g; j++) {
+      const int cy = j / g, cx = j % g, ci = base + j;
+      const int x = ctu_x * 64 + cx * S, y = ctu_y * 64 + cy * S;
+      hvx_cu_result *r = &out[ci];
+      memset(r, 0, sizeof(*r));
+      r->valid = (x + S <= p->pic_w) && (y + S <= p->pic_h);
+      if (!r->valid) continue;
+      const int parent = d ? (base - (g / 2) * (g / 2)) + (cy / 2) * (g / 2) + (cx / 2) : -1;
+      uint32_t best_cost = 0;
+      hvx_me_result best;
+      memset(&best, 0, sizeof(best));
+      for (int ref = 0; ref < p->n_ref; ref++) {
+        hvx_me_job jb;
+        memset(&jb, 0, sizeof(jb));
+        jb.pic_w = p->pic_w; jb.pic_h = p->pic_h; jb.max_cu = 64;
+        jb.cu_x = jb.pu_x = x; jb.cu_y = jb.pu_y = y; jb.w = jb.h = S;
+        jb.use_int2nx2n = parent >= 0 && out[parent].valid;
+        if (jb.use_int2nx2n) { jb.i2_x = imv[parent][ref][0]; jb.i2_y = imv[parent][ref][1]; }
+        jb.search_range = p->search_range;
+        jb.lambda_motion = p->lambda_motion;
+        jb.flags = p->me_flags;
+        hvx_me_result mr;
+        hvxo_motion_estimation(cur, stride, refs[ref], stride, &jb, &mr);
+        imv[ci][ref][0] = mr.mv_int_x;
+        imv[ci][ref][1] = mr.mv_int_y;
+        if (ref == 0 || mr.cost < best_cost) { best_cost = mr.cost; best = mr; r->ref = ref; }
+      }
+      r->mv_x = best.mv_x; r->mv_y = best.mv_y; r->me_cost = best_cost;
+      int16_t pred[64 * 64], resi[32 * 32], rec[32 * 32];
+      hvxo_luma_block_qpel(refs[r->ref], stride, x, y, best.mv_x, best.mv_y, S, S, pred, 64);
+      const int T = S < 32 ? S : 32, log2 = T == 4 ? 2 : T == 8 ? 3 : T == 16 ? 4 : 5;
+      hvx_tu_desc td;
+      hvxo_ctu_tu_desc(p, S, log2, &td);
+      for (int ty = 0; ty < S; ty += T)
+        for (int tx = 0; tx < S; tx += T) {
+          for (int yy = 0; yy < T; yy++)
+            for (int xx = 0; xx < T; xx++)
+              resi[yy * T + xx] = (int16_t)((int)cur[(y + ty + yy) * stride + x + tx + xx] - pred[(ty + yy) * 64 + tx + xx]);
+          int32_t temp[1024], lev[1024], abs_sum = 0;
+          hvxo_transform_nxn(&td, &est[log2 - 2], resi, T, temp, lev, NULL, &abs_sum);
+          hvxo_inv_transform_nxn(&td, lev, rec, T);
+          uint32_t sse = 0;
+          for (int k = 0; k < T * T; k++) { int df = resi[k] - rec[k]; sse += (uint32_t)(df * df); }
+          r->sse += sse;
+          r->abs_sum += abs_sum;
+          r->n_tu++;
+        }
+    }
+    base += g * g;
+  }
+}

@@ -60,6 +60,12 @@ float hvxo_stvssim(const uint8_t *const *org_hist, const uint8_t *const *rec_his
 double hvxo_lambda_2(int qp);
 double hvxo_adjust_lambda(double lambda, double eta);
 
+/* ---- CTU analysis pass (the bench workload, hvx_types.h) ---- */
+void hvxo_ctu_tu_desc(const hvx_ctu_params *p, int cu_size, int log2, hvx_tu_desc *d);
+void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
+                      const hvx_estbits *est /* [4]: luma 4x4..32x32 */, int ctu_x, int ctu_y,
+                      hvx_cu_result *out /* [HVX_CUS_PER_CTU] */);
+
 /* tables (generated, HEVC spec values) */
 void hvxo_dct_matrix(int n, int16_t *m /* n*n, [k][x] */);
 const uint32_t *hvxo_scan(int grouped, int scan_type, int log2w, int log2h);

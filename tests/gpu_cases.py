@@ -196,3 +196,32 @@ def check_tu_random(seed, n):
         sse = int(((res[i].astype(np.int64) - rr.reshape(-1)) ** 2).sum())
         assert gs == sse, (i, gs, sse)
     return True
+
+
+# ------------------------------------------------------------------------------ CTU analysis pass
+def check_ctu_pass(seed, width, height, nref, qp, max_ctus=None):
+    """hvx_ctu_analyze over a whole picture vs hvxo_ctu_analyze per CTU (bit-exact)."""
+    torch = _torch()
+    cur = padded_plane(make_yuv.random_frame(width, height, seed)[:width * height].reshape(height, width))
+    refs = []
+    for k in range(nref):
+        if k % 2:
+            img = make_yuv.smooth_frame(width, height, seed + k)[:width * height].reshape(height, width)
+        else:
+            img = make_yuv.random_frame(width, height, seed + 10 + k)[:width * height].reshape(height, width)
+        refs.append(padded_plane(img))
+    an = hvx.CtuAnalyzer(width, height, nref, qp)
+    cur_t = torch.from_numpy(cur).cuda()
+    ref_t = [torch.from_numpy(r).cuda() for r in refs]
+    ptrs = torch.tensor([hvx.plane_origin_ptr(t, width) for t in ref_t], dtype=torch.int64).cuda()
+    an.run(cur_t, ptrs)
+    torch.cuda.synchronize()
+    got = an.results()
+    ncx = (width + 63) // 64
+    est = _abi.load_estbits_p_luma()
+    n = an.nctu if max_ctus is None else min(max_ctus, an.nctu)
+    for c in range(n):
+        exp = oracle.ctu_analyze(cur, refs, an.params, est, c % ncx, c // ncx)
+        for ci in range(_abi.CUS_PER_CTU):
+            assert got[c][ci].tobytes() == exp[ci].tobytes(), (c, ci, got[c][ci], exp[ci])
+    return n

@@ -138,3 +138,13 @@ def test_plane_from_pel_gpu(torch):
     torch.cuda.synchronize()
     exp = np.pad(pel[:, :W].astype(np.uint8), M, mode="edge")
     np.testing.assert_array_equal(plane.cpu().numpy().reshape(H + 2 * M, W + 2 * M), exp)
+
+
+def test_ctu_pass_gpu(torch):
+    # 320x200: 20 CTUs incl. a partial bottom row (only 8x8 CUs valid there) and 2 references
+    assert gpu_cases.check_ctu_pass(seed=21, width=320, height=200, nref=2, qp=32) == 20
+
+
+def test_ctu_pass_qp_sweep_gpu(torch):
+    for qp in (22, 27, 37):
+        assert gpu_cases.check_ctu_pass(seed=qp, width=192, height=128, nref=1, qp=qp) == 6

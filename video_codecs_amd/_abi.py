@@ -31,6 +31,31 @@ assert ME_RESULT.itemsize == 48
 
 ME_FEN, ME_HADME, ME_SMOOTHMV = 1, 2, 4
 
+CTU_PARAMS = np.dtype([("pic_w", "<i4"), ("pic_h", "<i4"), ("n_ref", "<i4"), ("qp", "<i4"), ("search_range", "<i4"),
+                       ("me_flags", "<i4"), ("slice_type", "<i4"), ("lambda_motion", "<u4"), ("lambda", "<f8")], align=True)
+assert CTU_PARAMS.itemsize == 40
+CU_RESULT = np.dtype([("valid", "<i4"), ("ref", "<i4"), ("mv_x", "<i4"), ("mv_y", "<i4"), ("me_cost", "<u4"),
+                      ("sse", "<u4"), ("abs_sum", "<i4"), ("n_tu", "<i4")])
+assert CU_RESULT.itemsize == 32
+CUS_PER_CTU = 85
+
+
+def load_estbits_p_luma():
+    """4 x 224 int32 luma inter estBits tables (video_codecs_amd/data/README.md)."""
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "estbits_p_luma.bin")
+    return np.fromfile(p, dtype="<i4").reshape(4, ESTBITS_INTS)
+
+
+def ctu_params(pic_w, pic_h, n_ref, qp, lam=None, search_range=64, slice_type=1):
+    """HM-style P-slice parameters; lambda defaults to 0.57*2^((qp-12)/3) (TEncSlice::initEncSlice form)."""
+    p = np.zeros(1, CTU_PARAMS)
+    lam = 0.57 * 2.0 ** ((qp - 12) / 3.0) if lam is None else lam
+    p["pic_w"], p["pic_h"], p["n_ref"], p["qp"] = pic_w, pic_h, n_ref, qp
+    p["search_range"], p["me_flags"], p["slice_type"] = search_range, ME_FEN | ME_HADME | ME_SMOOTHMV, slice_type
+    p["lambda_motion"], p["lambda"] = lambda_motion_sad(lam), lam
+    return p
+
 # picture layout: 8-bit padded planes, HM TComPicYuv geometry (margin = MaxCU + 16 = 80)
 PLANE_MARGIN = 80
 

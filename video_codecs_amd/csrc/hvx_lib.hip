@@ -13,12 +13,49 @@
 #include "hvx_me.hpp"
 #include "hvx_ssim.hpp"
 #include "hvx_tu.hpp"
+#include "hvx_ctu.hpp"
 
 struct hvx_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
+  // optional per-phase timing of hvx_ctu_analyze (HIP events on the launch stream)
+  int timing = 0;
+  hipEvent_t ev[HVX_NPHASE + 1] = {};
+  bool ev_ok = false;
+  double phase_ms[HVX_NPHASE] = {};
+  int pending = 0;  // events recorded and not yet folded into phase_ms
 };
+
+namespace {
+size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+struct CtuWs {
+  size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, total;
+};
+CtuWs ctu_ws_layout(const CtuLayout &L) {
+  CtuWs w;
+  size_t o = 0;
+  const size_t ncu = (size_t)L.nctu * HVX_CUS_PER_CTU, ntu = (size_t)L.ntu(), nres = (size_t)L.nres();
+  w.jobs = o; o = align_up(o + ncu * L.nref * sizeof(hvx_me_job));
+  w.res = o; o = align_up(o + ncu * L.nref * sizeof(hvx_me_result));
+  w.desc = o; o = align_up(o + ntu * sizeof(hvx_tu_desc));
+  w.off = o; o = align_up(o + ntu * sizeof(int64_t));
+  w.est_idx = o; o = align_up(o + ntu * sizeof(int32_t));
+  w.resid = o; o = align_up(o + nres * sizeof(int16_t));
+  w.lev = o; o = align_up(o + nres * sizeof(int32_t));
+  w.res_out = o; o = align_up(o + nres * sizeof(int16_t));
+  w.abs = o; o = align_up(o + ntu * sizeof(int32_t));
+  w.sse = o; o = align_up(o + ntu * sizeof(uint32_t));
+  w.ptr = o; o = align_up(o + 8 * sizeof(void *));
+  w.total = o;
+  return w;
+}
+CtuLayout ctu_layout(int w, int h, int nref) {
+  CtuLayout L;
+  L.nctu_x = (w + 63) / 64; L.nctu_y = (h + 63) / 64; L.nctu = L.nctu_x * L.nctu_y; L.nref = nref;
+  return L;
+}
+}  // namespace
 
 namespace {
 thread_local std::string g_err;
@@ -143,6 +180,8 @@ int hvx_create(int device, hvx_ctx **out) {
 int hvx_destroy(hvx_ctx *ctx) {
   if (!ctx) return HVX_OK;
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
+  if (ctx->ev_ok)
+    for (int i = 0; i <= HVX_NPHASE; i++) (void)hipEventDestroy(ctx->ev[i]);
   delete ctx;
   return HVX_OK;
 }
@@ -230,11 +269,108 @@ int hvx_stvssim_batch(hvx_ctx *ctx, const uint8_t *const *d_hist_org, const uint
   return launched("k_stvssim");
 }
 
+static void fold_timing(hvx_ctx *ctx) {
+  if (!ctx->pending) return;
+  (void)hipEventSynchronize(ctx->ev[HVX_NPHASE]);
+  for (int i = 0; i < HVX_NPHASE; i++) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) == hipSuccess) ctx->phase_ms[i] += ms;
+  }
+  ctx->pending = 0;
+}
+
+static inline void mark(hvx_ctx *ctx, int i) {
+  if (ctx->timing && ctx->ev_ok) (void)hipEventRecord(ctx->ev[i], ctx->stream);
+}
+
+int hvx_set_timing(hvx_ctx *ctx, int on) {
+  if (!ctx) return fail(HVX_E_INVALID, "hvx_set_timing: NULL ctx");
+  if (on && !ctx->ev_ok) {
+    for (int i = 0; i <= HVX_NPHASE; i++) HVX_HIP(hipEventCreate(&ctx->ev[i]));
+    ctx->ev_ok = true;
+  }
+  ctx->timing = on;
+  return HVX_OK;
+}
+
+int hvx_phase_times(hvx_ctx *ctx, double *ms_out, int n, int reset) {
+  if (!ctx || !ms_out || n < HVX_NPHASE) return fail(HVX_E_INVALID, "hvx_phase_times: bad args");
+  fold_timing(ctx);
+  for (int i = 0; i < HVX_NPHASE; i++) ms_out[i] = ctx->phase_ms[i];
+  if (reset)
+    for (int i = 0; i < HVX_NPHASE; i++) ctx->phase_ms[i] = 0;
+  return HVX_OK;
+}
+
+int hvx_ctu_workspace_size(int pic_w, int pic_h, int n_ref, size_t *bytes) {
+  if (!bytes || pic_w <= 0 || pic_h <= 0 || n_ref <= 0 || n_ref > 8) return fail(HVX_E_INVALID, "hvx_ctu_workspace_size: bad args");
+  *bytes = ctu_ws_layout(ctu_layout(pic_w, pic_h, n_ref)).total;
+  return HVX_OK;
+}
+
+int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
+                    const hvx_ctu_params *h_params, const hvx_estbits *d_est4, void *d_workspace, size_t ws_bytes,
+                    hvx_cu_result *d_out) {
+  if (!ctx || !d_cur || !d_refs || !h_params || !d_est4 || !d_workspace || !d_out)
+    return fail(HVX_E_INVALID, "hvx_ctu_analyze: NULL argument");
+  const hvx_ctu_params P = *h_params;
+  if (P.pic_w <= 0 || P.pic_h <= 0 || P.n_ref <= 0 || P.n_ref > 8 || P.qp < 0 || P.qp > 51 ||
+      stride < P.pic_w + 2 * HVX_PLANE_MARGIN || P.search_range <= 0 || P.search_range > 256)
+    return fail(HVX_E_INVALID, "hvx_ctu_analyze: bad parameters");
+  const CtuLayout L = ctu_layout(P.pic_w, P.pic_h, P.n_ref);
+  const CtuWs W = ctu_ws_layout(L);
+  if (ws_bytes < W.total) return fail(HVX_E_INVALID, "hvx_ctu_analyze: workspace too small");
+  char *ws = (char *)d_workspace;
+  hvx_me_job *jobs = (hvx_me_job *)(ws + W.jobs);
+  hvx_me_result *res = (hvx_me_result *)(ws + W.res);
+  hvx_tu_desc *desc = (hvx_tu_desc *)(ws + W.desc);
+  int64_t *off = (int64_t *)(ws + W.off);
+  int32_t *est_idx = (int32_t *)(ws + W.est_idx);
+  int16_t *resid = (int16_t *)(ws + W.resid);
+  int32_t *lev = (int32_t *)(ws + W.lev);
+  int16_t *res_out = (int16_t *)(ws + W.res_out);
+  int32_t *abs_sum = (int32_t *)(ws + W.abs);
+  uint32_t *sse = (uint32_t *)(ws + W.sse);
+  const uint8_t **cur_slot = (const uint8_t **)(ws + W.ptr);
+  hipStream_t st = ctx->stream;
+  fold_timing(ctx);  // a previous call's events must be read before they are re-recorded
+  hipLaunchKernelGGL(k_set_ptr, dim3(1), dim3(1), 0, st, cur_slot, d_cur);
+  for (int d = 0; d < 4; d++) {
+    mark(ctx, d);
+    const int ncu = 1 << (2 * d), nt = L.nctu * ncu * L.nref;
+    hipLaunchKernelGGL(k_ctu_me_jobs, dim3((nt + 255) / 256), dim3(256), 0, st, L, P, d, res, jobs);
+    // the depth's jobs are contiguous per CTU but interleaved across CTUs: launch over all CUs of
+    // this depth via a per-depth view (blocks of other depths return at once)
+    const int first = d == 0 ? 0 : d == 1 ? 1 : d == 2 ? 5 : 21;
+    hipLaunchKernelGGL(k_me_ctu_depth, dim3(L.nctu * ncu * L.nref), dim3(64), 0, st, (const uint8_t *const *)cur_slot,
+                       d_refs, stride, jobs, res, L.nref, ncu, first);
+  }
+  mark(ctx, 4);
+  hipLaunchKernelGGL(k_ctu_pred_resid, dim3(L.nctu * HVX_CUS_PER_CTU), dim3(64), 0, st, L, P, d_cur, d_refs, stride,
+                     res, resid, desc, off, est_idx, d_out);
+  const int n = L.nctu;
+  mark(ctx, 5);
+  hipLaunchKernelGGL((k_tu<3, 2>), dim3(8 * n), dim3(64), 0, st, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev,
+                     nullptr, abs_sum, res_out, sse);
+  mark(ctx, 6);
+  hipLaunchKernelGGL((k_tu<2, 2>), dim3(16 * n), dim3(64), 0, st, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n,
+                     16 * n, resid, nullptr, lev, nullptr, abs_sum + 8 * n, res_out, sse + 8 * n);
+  mark(ctx, 7);
+  hipLaunchKernelGGL((k_tu<1, 2>), dim3(64 * n), dim3(64), 0, st, desc + 24 * n, d_est4, est_idx + 24 * n, off + 24 * n,
+                     64 * n, resid, nullptr, lev, nullptr, abs_sum + 24 * n, res_out, sse + 24 * n);
+  mark(ctx, 8);
+  hipLaunchKernelGGL(k_ctu_finalize, dim3((n * HVX_CUS_PER_CTU + 255) / 256), dim3(256), 0, st, L, abs_sum, sse, d_out);
+  mark(ctx, 9);
+  if (ctx->timing && ctx->ev_ok) ctx->pending = 1;
+  return launched("hvx_ctu_analyze");
+}
+
 int hvx_plane_extend(hvx_ctx *ctx, uint8_t *d_plane, int width, int height) {
   if (!ctx || !d_plane || width <= 0 || height <= 0) return fail(HVX_E_INVALID, "hvx_plane_extend: bad args");
   const int M = HVX_PLANE_MARGIN, stride = width + 2 * M;
-  hipLaunchKernelGGL(k_plane_extend, dim3((2 * M + 255) / 256, height), dim3(256), 0, ctx->stream, d_plane, stride, width, height, M, 0);
-  hipLaunchKernelGGL(k_plane_extend, dim3((stride + 255) / 256, 2 * M), dim3(256), 0, ctx->stream, d_plane, stride, width, height, M, 1);
+  uint8_t *origin = d_plane + (size_t)M * stride + M;  // d_plane = start of the padded allocation
+  hipLaunchKernelGGL(k_plane_extend, dim3((2 * M + 255) / 256, height), dim3(256), 0, ctx->stream, origin, stride, width, height, M, 0);
+  hipLaunchKernelGGL(k_plane_extend, dim3((stride + 255) / 256, 2 * M), dim3(256), 0, ctx->stream, origin, stride, width, height, M, 1);
   return launched("k_plane_extend");
 }
 
@@ -242,7 +378,8 @@ int hvx_plane_from_pel(hvx_ctx *ctx, const int16_t *d_pel, int pel_stride, int w
   if (!ctx || !d_pel || !d_plane || width <= 0 || height <= 0 || pel_stride < width)
     return fail(HVX_E_INVALID, "hvx_plane_from_pel: bad args");
   const int stride = width + 2 * HVX_PLANE_MARGIN;
-  hipLaunchKernelGGL(k_plane_from_pel, dim3((width + 255) / 256, height), dim3(256), 0, ctx->stream, d_pel, pel_stride, width, height, d_plane, stride);
+  uint8_t *origin = d_plane + (size_t)HVX_PLANE_MARGIN * stride + HVX_PLANE_MARGIN;
+  hipLaunchKernelGGL(k_plane_from_pel, dim3((width + 255) / 256, height), dim3(256), 0, ctx->stream, d_pel, pel_stride, width, height, origin, stride);
   int rc = launched("k_plane_from_pel");
   if (rc) return rc;
   return hvx_plane_extend(ctx, d_plane, width, height);

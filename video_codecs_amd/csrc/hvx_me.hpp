@@ -208,14 +208,14 @@ __device__ uint32_t me_refine(MeState &m, int16_t *blk, bool had, int bqx, int b
   return best;
 }
 
-__global__ __launch_bounds__(64) void k_me(const uint8_t *const *__restrict__ cur_planes,
-                                          const uint8_t *const *__restrict__ ref_planes, int stride,
-                                          const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
-  __shared__ uint8_t org[64 * 64];
-  __shared__ int16_t blk[64 * 64];
-  const int jid = blockIdx.x;
-  if (jid >= n) return;
-  const hvx_me_job j = jobs[jid];
+// one whole xMotionEstimation for job j by the calling wave; writes *out (lane 0)
+__device__ void me_run(const hvx_me_job &j, const uint8_t *const *__restrict__ cur_planes,
+                       const uint8_t *const *__restrict__ ref_planes, int stride, uint8_t *org, int16_t *blk,
+                       hvx_me_result *out) {
+  if (j.w <= 0 || j.h <= 0) {  // empty slot (e.g. a CU outside the picture): defined zero result
+    if (lane_id() == 0) { hvx_me_result z; memset(&z, 0, sizeof(z)); *out = z; }
+    return;
+  }
   const uint8_t *cur = cur_planes[j.cur_idx] + j.pu_y * stride + j.pu_x;
   for (int k = lane_id(); k < j.w * j.h; k += HVX_WAVE) {
     const int y = k / j.w, x = k - y * j.w;
@@ -293,6 +293,32 @@ __global__ __launch_bounds__(64) void k_me(const uint8_t *const *__restrict__ cu
     r.half_x = hx; r.half_y = hy; r.qtr_x = qx; r.qtr_y = qy; r.cost_frac = cost;
     r.mv_x = fmx; r.mv_y = fmy; r.bits = bits;
     r.cost = (uint32_t)(floor(1.0 * ((double)cost - (double)((m.lam * mv_bits) >> 16))) + (double)((m.lam * bits) >> 16));
-    out[jid] = r;
+    *out = r;
   }
+}
+
+__global__ __launch_bounds__(64) void k_me(const uint8_t *const *__restrict__ cur_planes,
+                                          const uint8_t *const *__restrict__ ref_planes, int stride,
+                                          const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
+  __shared__ uint8_t org[64 * 64];
+  __shared__ int16_t blk[64 * 64];
+  const int jid = blockIdx.x;
+  if (jid >= n) return;
+  const hvx_me_job j = jobs[jid];
+  me_run(j, cur_planes, ref_planes, stride, org, blk, out + jid);
+}
+
+// CTU-pass view: block b = (ctu * ncu + cu) * nref + ref of one depth -> job slot
+// ((ctu * 85 + first + cu) * nref + ref)
+__global__ __launch_bounds__(64) void k_me_ctu_depth(const uint8_t *const *__restrict__ cur_planes,
+                                                    const uint8_t *const *__restrict__ ref_planes, int stride,
+                                                    const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
+                                                    int nref, int ncu, int first) {
+  __shared__ uint8_t org[64 * 64];
+  __shared__ int16_t blk[64 * 64];
+  const int b = blockIdx.x;
+  const int ref = b % nref, cu = (b / nref) % ncu, ctu = b / (nref * ncu);
+  const size_t slot = ((size_t)ctu * HVX_CUS_PER_CTU + first + cu) * nref + ref;
+  const hvx_me_job j = jobs[slot];
+  me_run(j, cur_planes, ref_planes, stride, org, blk, out + slot);
 }

@@ -40,6 +40,9 @@ def lib():
             "hvx_me_batch": [P, P, P, I, P, I, P], "hvx_ssim_batch": [P, P, P, P, I, P],
             "hvx_stvssim_batch": [P, P, P, P, P, I, P],
             "hvx_plane_from_pel": [P, P, I, I, I, P], "hvx_plane_extend": [P, P, I, I],
+            "hvx_ctu_workspace_size": [I, I, I, ctypes.POINTER(ctypes.c_size_t)],
+            "hvx_ctu_analyze": [P, P, P, I, P, P, P, ctypes.c_size_t, P],
+            "hvx_set_timing": [P, I], "hvx_phase_times": [P, ctypes.POINTER(ctypes.c_double), I, I],
         }.items():
             f = getattr(L, name)
             f.argtypes = args
@@ -154,6 +157,52 @@ def plane_from_pel(pel, pel_stride, width, height, plane):
 
 def plane_extend(plane, width, height):
     _check(lib().hvx_plane_extend(context(), _ptr(plane), width, height), "hvx_plane_extend")
+
+
+def ctu_workspace_size(pic_w, pic_h, n_ref):
+    n = ctypes.c_size_t()
+    _check(lib().hvx_ctu_workspace_size(pic_w, pic_h, n_ref, ctypes.byref(n)), "hvx_ctu_workspace_size")
+    return n.value
+
+
+class CtuAnalyzer:
+    """Device-resident CTU analysis pass (hvx_ctu_analyze) for one picture geometry."""
+
+    def __init__(self, pic_w, pic_h, n_ref, qp, lam=None, est4=None):
+        import torch
+        self.params = _abi.ctu_params(pic_w, pic_h, n_ref, qp, lam)
+        self.pic_w, self.pic_h, self.n_ref = pic_w, pic_h, n_ref
+        self.stride = pic_w + 2 * _abi.PLANE_MARGIN
+        self.nctu = ((pic_w + 63) // 64) * ((pic_h + 63) // 64)
+        self.ws_bytes = ctu_workspace_size(pic_w, pic_h, n_ref)
+        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device="cuda")
+        est4 = _abi.load_estbits_p_luma() if est4 is None else est4
+        self.est = torch.from_numpy(np.ascontiguousarray(est4, np.int32).reshape(-1)).cuda()
+        self.out = torch.zeros(self.nctu * _abi.CUS_PER_CTU * _abi.CU_RESULT.itemsize, dtype=torch.uint8, device="cuda")
+
+    def run(self, cur_plane, ref_planes_ptrs):
+        """cur_plane: padded uint8 device tensor; ref_planes_ptrs: int64 device tensor of origin pointers."""
+        origin = plane_origin_ptr(cur_plane, self.pic_w)
+        p = np.ascontiguousarray(self.params)
+        _check(lib().hvx_ctu_analyze(context(), ctypes.c_void_p(origin), _ptr(ref_planes_ptrs), self.stride,
+                                     p.ctypes.data_as(ctypes.c_void_p), _ptr(self.est), _ptr(self.ws),
+                                     self.ws_bytes, _ptr(self.out)), "hvx_ctu_analyze")
+
+    def results(self):
+        return from_device(self.out, _abi.CU_RESULT).reshape(self.nctu, _abi.CUS_PER_CTU)
+
+
+PHASES = ("me_d0", "me_d1", "me_d2", "me_d3", "mc_resid", "tu32", "tu16", "tu8", "finalize")
+
+
+def set_timing(on):
+    _check(lib().hvx_set_timing(context(), int(on)), "hvx_set_timing")
+
+
+def phase_times(reset=True):
+    buf = (ctypes.c_double * len(PHASES))()
+    _check(lib().hvx_phase_times(context(), buf, len(PHASES), int(reset)), "hvx_phase_times")
+    return dict(zip(PHASES, list(buf)))
 
 
 def sync():
