@@ -110,6 +110,13 @@ int hvx_tu_pipeline_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const hvx_est
                           const int64_t *d_off, int n, const int16_t *d_residual, int32_t *d_levels,
                           int32_t *d_abs_sum, int16_t *d_residual_out, uint32_t *d_sse);
 
+/* Synchronous single-TU convenience forms over HOST memory (the per-call seam used by the
+ * HM shim in integration/; staged through a device scratch buffer owned by the context). */
+int hvx_tu_forward_host(hvx_ctx *ctx, const hvx_tu_desc *h_desc, const hvx_estbits *h_est, const int16_t *h_residual,
+                        int residual_stride, int32_t *h_levels, int32_t *h_arl, int32_t *h_abs_sum);
+int hvx_tu_inverse_host(hvx_ctx *ctx, const hvx_tu_desc *h_desc, const int32_t *h_levels, int16_t *h_residual,
+                        int residual_stride);
+
 /* ---------------------------------------------------------------------------------------
  * Motion estimation.  Planes are 8-bit padded planes (margin HVX_PLANE_MARGIN on every
  * side, luma stride `stride` bytes); d_cur_planes[j.cur_idx] / d_ref_planes[j.ref_idx]

@@ -1,0 +1,33 @@
+"""End-to-end drop-in check: the UNCHANGED reference TAppEncoder (HM-16.5rc1), with every
+TComTrQuant::transformNxN / invTransformNxN call served by libhvx.so on the MI355X
+(integration/hm_tu_seam.cpp), must produce the same bitstream and reconstruction MD5 as the
+reference CPU build (tests/hm_seam/expected_md5.json, recorded by make_expected.py)."""
+import json
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+from tests.hm_seam import make_expected as mk
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "oracle", "_ref", "TAppEncoder_hvx")
+EXPECTED = json.load(open(os.path.join(ROOT, "tests", "hm_seam", "expected_md5.json")))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(mk.CASES))
+def test_hm_encoder_with_hvx_tu_seam(case):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if not os.path.exists(EXE):
+        pytest.skip("TAppEncoder_hvx not built (needs /root/reference at build time)")
+    with tempfile.TemporaryDirectory() as tmp:
+        got = mk.encode(EXE, case, tmp)
+    assert got == EXPECTED[case], (case, got, EXPECTED[case])
+
+
+def test_expected_md5_cases_present():
+    assert set(EXPECTED) == set(mk.CASES)

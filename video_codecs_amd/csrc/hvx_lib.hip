@@ -25,7 +25,21 @@ struct hvx_ctx {
   bool ev_ok = false;
   double phase_ms[HVX_NPHASE] = {};
   int pending = 0;  // events recorded and not yet folded into phase_ms
+  // staging for the host-memory single-TU forms
+  char *scratch = nullptr;
+  char *pinned = nullptr;
 };
+
+// staging layout (bytes): desc | est | off | residual (1024 int16) | levels | arl | abs | resout
+#define HVX_STG_DESC 0
+#define HVX_STG_EST 128
+#define HVX_STG_OFF (HVX_STG_EST + 1024)
+#define HVX_STG_RES (HVX_STG_OFF + 64)
+#define HVX_STG_LEV (HVX_STG_RES + 2048)
+#define HVX_STG_ARL (HVX_STG_LEV + 4096)
+#define HVX_STG_ABS (HVX_STG_ARL + 4096)
+#define HVX_STG_OUT (HVX_STG_ABS + 64)
+#define HVX_STG_SIZE (HVX_STG_OUT + 2048)
 
 namespace {
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -179,6 +193,8 @@ int hvx_create(int device, hvx_ctx **out) {
 
 int hvx_destroy(hvx_ctx *ctx) {
   if (!ctx) return HVX_OK;
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   if (ctx->ev_ok)
     for (int i = 0; i <= HVX_NPHASE; i++) (void)hipEventDestroy(ctx->ev[i]);
@@ -241,6 +257,82 @@ int hvx_tu_pipeline_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const hvx_est
   if (!n) return HVX_OK;
   return tu_launch<2>(ctx, d_desc, d_est, d_est_idx, d_off, n, d_residual, nullptr, d_levels, nullptr, d_abs_sum,
                       d_residual_out, d_sse);
+}
+
+static int staging(hvx_ctx *ctx) {
+  if (!ctx->scratch) {
+    HVX_HIP(hipMalloc(&ctx->scratch, HVX_STG_SIZE));
+    HVX_HIP(hipHostMalloc(&ctx->pinned, HVX_STG_SIZE, 0));
+  }
+  return HVX_OK;
+}
+
+int hvx_tu_forward_host(hvx_ctx *ctx, const hvx_tu_desc *h_desc, const hvx_estbits *h_est, const int16_t *h_residual,
+                        int residual_stride, int32_t *h_levels, int32_t *h_arl, int32_t *h_abs_sum) {
+  if (!ctx || !h_desc || !h_est || !h_residual || !h_levels || !h_abs_sum) return fail(HVX_E_INVALID, "hvx_tu_forward_host: NULL");
+  const int w = h_desc->width, h = h_desc->height;
+  if (w != h || (w != 4 && w != 8 && w != 16 && w != 32) || residual_stride < w) return fail(HVX_E_INVALID, "hvx_tu_forward_host: TU size");
+  int rc = staging(ctx);
+  if (rc) return rc;
+  char *p = ctx->pinned;
+  memcpy(p + HVX_STG_DESC, h_desc, sizeof(hvx_tu_desc));
+  memcpy(p + HVX_STG_EST, h_est, sizeof(hvx_estbits));
+  *(int64_t *)(p + HVX_STG_OFF) = 0;
+  for (int y = 0; y < h; y++) memcpy(p + HVX_STG_RES + y * w * 2, h_residual + (size_t)y * residual_stride, w * 2);
+  hipStream_t st = ctx->stream;
+  char *d = ctx->scratch;
+  HVX_HIP(hipMemcpyAsync(d, p, HVX_STG_LEV, hipMemcpyHostToDevice, st));
+  const hvx_tu_desc *dd = (const hvx_tu_desc *)(d + HVX_STG_DESC);
+  const hvx_estbits *de = (const hvx_estbits *)(d + HVX_STG_EST);
+  const int64_t *doff = (const int64_t *)(d + HVX_STG_OFF);
+  const int16_t *dres = (const int16_t *)(d + HVX_STG_RES);
+  int32_t *dlev = (int32_t *)(d + HVX_STG_LEV), *darl = (int32_t *)(d + HVX_STG_ARL), *dabs = (int32_t *)(d + HVX_STG_ABS);
+  switch (w) {  // one size class: no idle launches
+    case 4: hipLaunchKernelGGL((k_tu<0, 0>), dim3(1), dim3(64), 0, st, dd, de, nullptr, doff, 1, dres, nullptr, dlev, darl, dabs, nullptr, nullptr); break;
+    case 8: hipLaunchKernelGGL((k_tu<1, 0>), dim3(1), dim3(64), 0, st, dd, de, nullptr, doff, 1, dres, nullptr, dlev, darl, dabs, nullptr, nullptr); break;
+    case 16: hipLaunchKernelGGL((k_tu<2, 0>), dim3(1), dim3(64), 0, st, dd, de, nullptr, doff, 1, dres, nullptr, dlev, darl, dabs, nullptr, nullptr); break;
+    default: hipLaunchKernelGGL((k_tu<3, 0>), dim3(1), dim3(64), 0, st, dd, de, nullptr, doff, 1, dres, nullptr, dlev, darl, dabs, nullptr, nullptr); break;
+  }
+  rc = launched("hvx_tu_forward_host");
+  if (rc) return rc;
+  HVX_HIP(hipMemcpyAsync(p + HVX_STG_LEV, d + HVX_STG_LEV, HVX_STG_OUT - HVX_STG_LEV, hipMemcpyDeviceToHost, st));
+  HVX_HIP(hipStreamSynchronize(st));
+  memcpy(h_levels, p + HVX_STG_LEV, (size_t)w * h * 4);
+  if (h_arl) memcpy(h_arl, p + HVX_STG_ARL, (size_t)w * h * 4);
+  *h_abs_sum = *(int32_t *)(p + HVX_STG_ABS);
+  return HVX_OK;
+}
+
+int hvx_tu_inverse_host(hvx_ctx *ctx, const hvx_tu_desc *h_desc, const int32_t *h_levels, int16_t *h_residual,
+                        int residual_stride) {
+  if (!ctx || !h_desc || !h_levels || !h_residual) return fail(HVX_E_INVALID, "hvx_tu_inverse_host: NULL");
+  const int w = h_desc->width, h = h_desc->height;
+  if (w != h || (w != 4 && w != 8 && w != 16 && w != 32) || residual_stride < w) return fail(HVX_E_INVALID, "hvx_tu_inverse_host: TU size");
+  int rc = staging(ctx);
+  if (rc) return rc;
+  char *p = ctx->pinned;
+  memcpy(p + HVX_STG_DESC, h_desc, sizeof(hvx_tu_desc));
+  *(int64_t *)(p + HVX_STG_OFF) = 0;
+  memcpy(p + HVX_STG_LEV, h_levels, (size_t)w * h * 4);
+  hipStream_t st = ctx->stream;
+  char *d = ctx->scratch;
+  HVX_HIP(hipMemcpyAsync(d, p, HVX_STG_ARL, hipMemcpyHostToDevice, st));
+  const hvx_tu_desc *dd = (const hvx_tu_desc *)(d + HVX_STG_DESC);
+  const int64_t *doff = (const int64_t *)(d + HVX_STG_OFF);
+  int32_t *dlev = (int32_t *)(d + HVX_STG_LEV);
+  int16_t *dout = (int16_t *)(d + HVX_STG_OUT);
+  switch (w) {
+    case 4: hipLaunchKernelGGL((k_tu<0, 1>), dim3(1), dim3(64), 0, st, dd, nullptr, nullptr, doff, 1, nullptr, nullptr, dlev, nullptr, nullptr, dout, nullptr); break;
+    case 8: hipLaunchKernelGGL((k_tu<1, 1>), dim3(1), dim3(64), 0, st, dd, nullptr, nullptr, doff, 1, nullptr, nullptr, dlev, nullptr, nullptr, dout, nullptr); break;
+    case 16: hipLaunchKernelGGL((k_tu<2, 1>), dim3(1), dim3(64), 0, st, dd, nullptr, nullptr, doff, 1, nullptr, nullptr, dlev, nullptr, nullptr, dout, nullptr); break;
+    default: hipLaunchKernelGGL((k_tu<3, 1>), dim3(1), dim3(64), 0, st, dd, nullptr, nullptr, doff, 1, nullptr, nullptr, dlev, nullptr, nullptr, dout, nullptr); break;
+  }
+  rc = launched("hvx_tu_inverse_host");
+  if (rc) return rc;
+  HVX_HIP(hipMemcpyAsync(p + HVX_STG_OUT, d + HVX_STG_OUT, (size_t)w * h * 2, hipMemcpyDeviceToHost, st));
+  HVX_HIP(hipStreamSynchronize(st));
+  for (int y = 0; y < h; y++) memcpy(h_residual + (size_t)y * residual_stride, p + HVX_STG_OUT + y * w * 2, w * 2);
+  return HVX_OK;
 }
 
 int hvx_me_batch(hvx_ctx *ctx, const uint8_t *const *d_cur_planes, const uint8_t *const *d_ref_planes, int stride,
