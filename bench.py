@@ -95,7 +95,7 @@ def main():
     if rank == 0:
         ctus = nctu * args.steps * world
         value = ctus / elapsed
-        # roofline of the dominant kernel: k_me_ctu_depth (4 launches per step, one per CU depth)
+        # roofline of the dominant kernel: k_me_int_ctu (4 launches per step, one per CU depth)
         me_ms_step = sum(phases[f"me_d{d}"] for d in range(4)) / args.steps
         launch_ms = me_ms_step / 4.0
         bytes_per_launch = nctu * 4096 * (1 + nref)  # each luma sample of cur + refs once
@@ -103,7 +103,7 @@ def main():
         traffic = None
         tr_path = os.path.join(ROOT, "profiles", "hbm_traffic_r01.json")
         if os.path.exists(tr_path):
-            tr = json.load(open(tr_path)).get("k_me_ctu_depth")
+            tr = json.load(open(tr_path)).get("k_me_int_ctu")
             if tr:
                 traffic = tr["bytes_per_launch"]
         out = {
@@ -123,7 +123,7 @@ def main():
                        "resolution": f"{W}x{H}", "ctus_per_frame": nctu, "qp": args.qp, "search_range": 64,
                        "n_ref": nref, "parallelism": f"segments x{world}"},
             "phase_ms_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()},
-            "roofline": {"bound": "hbm", "kernel": "k_me_ctu_depth", "achieved": round(achieved, 3),
+            "roofline": {"bound": "hbm", "kernel": "k_me_int_ctu", "achieved": round(achieved, 3),
                          "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / MI355X_HBM_PEAK_GBS,
                          "traffic": traffic, "bytes_per_launch": bytes_per_launch,
                          "avg_launch_ms": round(launch_ms, 3)},

@@ -159,9 +159,10 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
                     const hvx_ctu_params *h_params, const hvx_estbits *d_est4, void *d_workspace, size_t ws_bytes,
                     hvx_cu_result *d_out);
 /* Optional phase timing of hvx_ctu_analyze with HIP events on the launch stream.  Phases:
- * 0..3 ME of CU depth 0..3 (k_ctu_me_jobs + k_me_ctu_depth), 4 MC/residual (k_ctu_pred_resid),
- * 5..7 TU pipeline 32x32 / 16x16 / 8x8 (k_tu), 8 per-CU sums (k_ctu_finalize).  Accumulated ms. */
-#define HVX_NPHASE 9
+ * 0..3 integer ME of CU depth 0..3 (k_ctu_me_jobs + k_me_int_ctu), 4 fractional ME of all depths
+ * (k_me_frac_ctu), 5 MC/residual (k_ctu_pred_resid), 6..8 TU pipeline 32x32 / 16x16 / 8x8
+ * (k_tu), 9 per-CU sums (k_ctu_finalize).  Accumulated ms. */
+#define HVX_NPHASE 10
 int hvx_set_timing(hvx_ctx *ctx, int on);
 int hvx_phase_times(hvx_ctx *ctx, double *ms_out, int n, int reset);
 

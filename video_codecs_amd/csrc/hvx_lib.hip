@@ -340,7 +340,8 @@ int hvx_me_batch(hvx_ctx *ctx, const uint8_t *const *d_cur_planes, const uint8_t
   if (!ctx || n < 0 || stride <= 0 || (n && (!d_cur_planes || !d_ref_planes || !d_jobs || !d_out)))
     return fail(HVX_E_INVALID, "hvx_me_batch: bad args");
   if (!n) return HVX_OK;
-  hipLaunchKernelGGL(k_me, dim3(n), dim3(64), 0, ctx->stream, d_cur_planes, d_ref_planes, stride, d_jobs, n, d_out);
+  hipLaunchKernelGGL(k_me_int, dim3(n), dim3(64), 0, ctx->stream, d_cur_planes, d_ref_planes, stride, d_jobs, n, d_out);
+  hipLaunchKernelGGL(k_me_frac<64>, dim3(n), dim3(64), 0, ctx->stream, d_cur_planes, d_ref_planes, stride, d_jobs, n, d_out);
   return launched("k_me");
 }
 
@@ -434,25 +435,35 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
     // the depth's jobs are contiguous per CTU but interleaved across CTUs: launch over all CUs of
     // this depth via a per-depth view (blocks of other depths return at once)
     const int first = d == 0 ? 0 : d == 1 ? 1 : d == 2 ? 5 : 21;
-    hipLaunchKernelGGL(k_me_ctu_depth, dim3(L.nctu * ncu * L.nref), dim3(64), 0, st, (const uint8_t *const *)cur_slot,
+    hipLaunchKernelGGL(k_me_int_ctu, dim3(L.nctu * ncu * L.nref), dim3(64), 0, st, (const uint8_t *const *)cur_slot,
                        d_refs, stride, jobs, res, L.nref, ncu, first);
   }
+  // fractional refinement of every depth (only the integer MVs feed the next depth's jobs)
   mark(ctx, 4);
+  {
+    const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
+    const int nb = L.nctu * L.nref;
+    hipLaunchKernelGGL(k_me_frac_ctu<64>, dim3(nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 1, 0);
+    hipLaunchKernelGGL(k_me_frac_ctu<32>, dim3(4 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 4, 1);
+    hipLaunchKernelGGL(k_me_frac_ctu<16>, dim3(16 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 16, 5);
+    hipLaunchKernelGGL(k_me_frac_ctu<8>, dim3(64 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 64, 21);
+  }
+  mark(ctx, 5);
   hipLaunchKernelGGL(k_ctu_pred_resid, dim3(L.nctu * HVX_CUS_PER_CTU), dim3(64), 0, st, L, P, d_cur, d_refs, stride,
                      res, resid, desc, off, est_idx, d_out);
   const int n = L.nctu;
-  mark(ctx, 5);
+  mark(ctx, 6);
   hipLaunchKernelGGL((k_tu<3, 2>), dim3(8 * n), dim3(64), 0, st, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev,
                      nullptr, abs_sum, res_out, sse);
-  mark(ctx, 6);
+  mark(ctx, 7);
   hipLaunchKernelGGL((k_tu<2, 2>), dim3(16 * n), dim3(64), 0, st, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n,
                      16 * n, resid, nullptr, lev, nullptr, abs_sum + 8 * n, res_out, sse + 8 * n);
-  mark(ctx, 7);
+  mark(ctx, 8);
   hipLaunchKernelGGL((k_tu<1, 2>), dim3(64 * n), dim3(64), 0, st, desc + 24 * n, d_est4, est_idx + 24 * n, off + 24 * n,
                      64 * n, resid, nullptr, lev, nullptr, abs_sum + 24 * n, res_out, sse + 24 * n);
-  mark(ctx, 8);
-  hipLaunchKernelGGL(k_ctu_finalize, dim3((n * HVX_CUS_PER_CTU + 255) / 256), dim3(256), 0, st, L, abs_sum, sse, d_out);
   mark(ctx, 9);
+  hipLaunchKernelGGL(k_ctu_finalize, dim3((n * HVX_CUS_PER_CTU + 255) / 256), dim3(256), 0, st, L, abs_sum, sse, d_out);
+  mark(ctx, 10);
   if (ctx->timing && ctx->ev_ok) ctx->pending = 1;
   return launched("hvx_ctu_analyze");
 }

@@ -5,124 +5,35 @@
 // xSetSearchRange :3765, xPatternSearchFracDIF :4240, xPatternRefinement :808;
 // TComDataCU::clipMv TComDataCU.cpp:2788; TComRdCost::getCost TComRdCost.h:172).
 //
-// Mapping: one 64-lane wave per (PU, reference) search job.  The PU's original block is
-// staged once into LDS (8-bit); reference pixels stream from the 8-bit padded plane through
-// L1/L2 (a 2160p plane is 9.4 MB: the 4 references of an LDP slice stay resident in the
-// 256 MB Infinity Cache).  Every candidate SAD is a wave-wide sum (samples over lanes,
-// shuffle all-reduce) so the TZ control flow stays wave-uniform and the candidates are
-// visited in exactly the reference's order with its strict '<' tie-break -> identical MVs.
-// Fractional refinement interpolates each candidate block into LDS with the reference's
-// 16-bit two-stage arithmetic and takes an 8x8/4x4 Hadamard SATD across lanes.
+// Two kernels, one 64-lane wave per (PU, reference) job each:
+//
+//  k_me_int  -- the TZ integer search.  The reference visits candidates one at a time
+//     (xTZSearchHelp, strict '<').  Each search step here evaluates its whole candidate
+//     LIST at once: all diamonds of a stage around their common start, the 2-point pair,
+//     64 raster points per pass.  Lanes split over candidates (64/2^ceil(log2 n) lanes per
+//     candidate, one 4-pixel row group per lane-iteration, v_sad_u8 on dword loads) and the
+//     list is then reduced to its FIRST minimum with a wave-wide (cost, index) key-min --
+//     exactly the point a sequence of strict '<' updates would keep.  The smooth-MV early
+//     stop of the first stage replays the diamonds' minima in order.  Low register use
+//     (no interpolation state) keeps 8 waves per SIMD resident.
+//
+//  k_me_frac -- xPatternSearchFracDIF from the integer result.  Per stage (half, quarter)
+//     the 3 horizontal sub-pel phases the 9 candidates need are filtered once into LDS
+//     planes (the reference's first-stage 16-bit intermediates), each candidate is one
+//     vertical pass over a plane, and its SATD is an 8x8 Hadamard done ACROSS lanes (one
+//     sample per lane, butterflies on xor-shuffles) for blocks of <= 16 tiles; larger or
+//     4x4-tiled blocks go through an LDS block + per-lane tiles.  Templated on the largest
+//     block size so a depth's launch only reserves the LDS its blocks need.
 #pragma once
 #include "hvx_dev.hpp"
 
-struct MeState {
-  const uint8_t *org;  // LDS, stride 64
-  const uint8_t *ref;  // PU origin at MV (0,0) in the reference plane
-  int sr, w, h, sub;
-  uint32_t lam;
-  int px, py, cost_scale;
-  int best_x, best_y, best_dist, best_round, point_nr;
-  uint32_t best_sad;
-};
-
 struct MeRange { int l, r, t, b; };
 
-__device__ __forceinline__ uint32_t me_mv_cost(const MeState &m, int x, int y) {
-  const uint32_t bits = eg_bits((x << m.cost_scale) - m.px) + eg_bits((y << m.cost_scale) - m.py);
-  return (m.lam * bits) >> 16;
-}
-
-__device__ __forceinline__ uint32_t me_sad(const MeState &m, int x, int y) {
-  const uint8_t *r = m.ref + y * m.sr + x;
-  const int w = m.w, rows = (m.h + (1 << m.sub) - 1) >> m.sub;
-  uint32_t s = 0;
-  for (int i = lane_id(); i < rows * w; i += HVX_WAVE) {
-    const int yy = (i / w) << m.sub, xx = i - (i / w) * w;
-    s += (uint32_t)abs((int)m.org[yy * 64 + xx] - (int)r[yy * m.sr + xx]);
-  }
-  return wave_sum_u32(s) << m.sub;
-}
-
-// xTZSearchHelp (:332), non-SELECTIVE branch
-__device__ __forceinline__ void me_help(MeState &m, int x, int y, int pnr, int dist) {
-  const uint32_t sad = me_sad(m, x, y) + me_mv_cost(m, x, y);
-  if (sad < m.best_sad) { m.best_sad = sad; m.best_x = x; m.best_y = y; m.best_dist = dist; m.best_round = 0; m.point_nr = pnr; }
-}
-
-// xTZ2PointSearch (:438)
-__device__ void me_2point(MeState &m, const MeRange &g) {
-  const int sx = m.best_x, sy = m.best_y;
-  switch (m.point_nr) {
-    case 1: if (sx - 1 >= g.l) me_help(m, sx - 1, sy, 0, 2); if (sy - 1 >= g.t) me_help(m, sx, sy - 1, 0, 2); break;
-    case 2: if (sy - 1 >= g.t) { if (sx - 1 >= g.l) me_help(m, sx - 1, sy - 1, 0, 2); if (sx + 1 <= g.r) me_help(m, sx + 1, sy - 1, 0, 2); } break;
-    case 3: if (sy - 1 >= g.t) me_help(m, sx, sy - 1, 0, 2); if (sx + 1 <= g.r) me_help(m, sx + 1, sy, 0, 2); break;
-    case 4: if (sx - 1 >= g.l) { if (sy + 1 <= g.b) me_help(m, sx - 1, sy + 1, 0, 2); if (sy - 1 >= g.t) me_help(m, sx - 1, sy - 1, 0, 2); } break;
-    case 5: if (sx + 1 <= g.r) { if (sy - 1 >= g.t) me_help(m, sx + 1, sy - 1, 0, 2); if (sy + 1 <= g.b) me_help(m, sx + 1, sy + 1, 0, 2); } break;
-    case 6: if (sx - 1 >= g.l) me_help(m, sx - 1, sy, 0, 2); if (sy + 1 <= g.b) me_help(m, sx, sy + 1, 0, 2); break;
-    case 7: if (sy + 1 <= g.b) { if (sx - 1 >= g.l) me_help(m, sx - 1, sy + 1, 0, 2); if (sx + 1 <= g.r) me_help(m, sx + 1, sy + 1, 0, 2); } break;
-    case 8: if (sx + 1 <= g.r) me_help(m, sx + 1, sy, 0, 2); if (sy + 1 <= g.b) me_help(m, sx, sy + 1, 0, 2); break;
-    default: break;  // unreachable: the reference asserts here
-  }
-}
-
-// xTZ8PointDiamondSearch (:629)
-__device__ void me_diamond(MeState &m, const MeRange &g, int sx, int sy, int d) {
-  const int top = sy - d, bottom = sy + d, left = sx - d, right = sx + d;
-  m.best_round += 1;
-  if (d == 1) {
-    if (top >= g.t) me_help(m, sx, top, 2, d);
-    if (left >= g.l) me_help(m, left, sy, 4, d);
-    if (right <= g.r) me_help(m, right, sy, 5, d);
-    if (bottom <= g.b) me_help(m, sx, bottom, 7, d);
-    return;
-  }
-  const bool inside = top >= g.t && left >= g.l && right <= g.r && bottom <= g.b;
-  if (d <= 8) {
-    const int t2 = sy - (d >> 1), b2 = sy + (d >> 1), l2 = sx - (d >> 1), r2 = sx + (d >> 1);
-    if (inside) {
-      me_help(m, sx, top, 2, d);
-      me_help(m, l2, t2, 1, d >> 1);
-      me_help(m, r2, t2, 3, d >> 1);
-      me_help(m, left, sy, 4, d);
-      me_help(m, right, sy, 5, d);
-      me_help(m, l2, b2, 6, d >> 1);
-      me_help(m, r2, b2, 8, d >> 1);
-      me_help(m, sx, bottom, 7, d);
-    } else {
-      if (top >= g.t) me_help(m, sx, top, 2, d);
-      if (t2 >= g.t) { if (l2 >= g.l) me_help(m, l2, t2, 1, d >> 1); if (r2 <= g.r) me_help(m, r2, t2, 3, d >> 1); }
-      if (left >= g.l) me_help(m, left, sy, 4, d);
-      if (right <= g.r) me_help(m, right, sy, 5, d);
-      if (b2 <= g.b) { if (l2 >= g.l) me_help(m, l2, b2, 6, d >> 1); if (r2 <= g.r) me_help(m, r2, b2, 8, d >> 1); }
-      if (bottom <= g.b) me_help(m, sx, bottom, 7, d);
-    }
-  } else {
-    const int q = d >> 2;
-    if (inside) {
-      me_help(m, sx, top, 0, d);
-      me_help(m, left, sy, 0, d);
-      me_help(m, right, sy, 0, d);
-      me_help(m, sx, bottom, 0, d);
-      for (int i = 1; i < 4; i++) {
-        const int yt = top + q * i, yb = bottom - q * i, xl = sx - q * i, xr = sx + q * i;
-        me_help(m, xl, yt, 0, d);
-        me_help(m, xr, yt, 0, d);
-        me_help(m, xl, yb, 0, d);
-        me_help(m, xr, yb, 0, d);
-      }
-    } else {
-      if (top >= g.t) me_help(m, sx, top, 0, d);
-      if (left >= g.l) me_help(m, left, sy, 0, d);
-      if (right <= g.r) me_help(m, right, sy, 0, d);
-      if (bottom <= g.b) me_help(m, sx, bottom, 0, d);
-      for (int i = 1; i < 4; i++) {
-        const int yt = top + q * i, yb = bottom - q * i, xl = sx - q * i, xr = sx + q * i;
-        if (yt >= g.t) { if (xl >= g.l) me_help(m, xl, yt, 0, d); if (xr <= g.r) me_help(m, xr, yt, 0, d); }
-        if (yb <= g.b) { if (xl >= g.l) me_help(m, xl, yb, 0, d); if (xr <= g.r) me_help(m, xr, yb, 0, d); }
-      }
-    }
-  }
+// The reference's per-point range tests (xTZ8PointDiamondSearch, xTZ2PointSearch) check only
+// the bound in each direction the point moved from the start -- a start outside the range
+// (the zero MV, a far predictor) still has its axis points searched.
+__device__ __forceinline__ bool me_in(const MeRange &g, int dx, int dy, int x, int y) {
+  return (dx >= 0 || x >= g.l) && (dx <= 0 || x <= g.r) && (dy >= 0 || y >= g.t) && (dy <= 0 || y <= g.b);
 }
 
 // TComDataCU::clipMv: quarter-pel, result stored as Short
@@ -133,6 +44,7 @@ __device__ __forceinline__ void me_clip(const hvx_me_job &j, int &mx, int &my) {
   my = (int16_t)(my < vmin ? vmin : my > vmax ? vmax : my);
 }
 
+// xSetSearchRange (:3765)
 __device__ __forceinline__ MeRange me_search_range(const hvx_me_job &j, int px, int py, int sr) {
   int cx = px, cy = py;
   me_clip(j, cx, cy);
@@ -144,7 +56,307 @@ __device__ __forceinline__ MeRange me_search_range(const hvx_me_job &j, int px, 
   return g;
 }
 
-// Quarter-sample luma sample at (x,y) + quarter-pel (qx,qy); standard two-stage 8-bit path.
+// TComRdCost::getCost(x, y) with the predictor at quarter-pel and the candidate at 1<<scale units
+__device__ __forceinline__ uint32_t me_mv_cost(uint32_t lam, int px, int py, int scale, int x, int y) {
+  const uint32_t bits = eg_bits((x << scale) - px) + eg_bits((y << scale) - py);
+  return (lam * bits) >> 16;
+}
+
+// 4 bytes at any address from two aligned dword loads (plane margins cover the over-read)
+__device__ __forceinline__ uint32_t ld4_any(const uint8_t *p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
+  return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t t = __shfl_xor(v, o, HVX_WAVE);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ======================================================================================
+// integer TZ search
+// ======================================================================================
+constexpr int kMeMaxList = 128;  // diamonds d = 1..256: 4 + 3*8 + 5*16 = 108 points
+
+struct MeInt {
+  const uint8_t *org;  // LDS, stride 64
+  const uint8_t *ref;  // PU origin at MV (0,0) in the reference plane
+  uint32_t *cost;      // LDS, cost of each point of the current candidate list
+  int sr, sub, rows, gw;
+  uint32_t lam;
+  int px, py;
+  int best_x, best_y, best_dist, best_round, point_nr;
+  uint32_t best_sad;
+};
+
+struct MeCand { int x, y, pnr, dist; bool ok; };
+
+// SAD (before the FEN scale) of the block at (x,y) over row groups s, s+L, s+2L, ...
+// (group = 4 pixels of one sampled row)
+__device__ __forceinline__ uint32_t me_sad_part(const MeInt &m, int x, int y, int s, int L) {
+  const int n = m.rows * m.gw;
+  int r = s / m.gw, g = s - r * m.gw;
+  const int dr = L / m.gw, dg = L - dr * m.gw;
+  const uint8_t *base = m.ref + y * m.sr + x;
+  const int rs = m.sr << m.sub, os = 64 << m.sub;
+  uint32_t acc = 0;
+  for (int i = s; i < n; i += L) {
+    const uint32_t o = *(const uint32_t *)(m.org + r * os + 4 * g);
+    acc = __builtin_amdgcn_sad_u8(o, ld4_any(base + r * rs + 4 * g), acc);
+    g += dg;
+    r += dr;
+    if (g >= m.gw) { g -= m.gw; r++; }
+  }
+  return acc;
+}
+
+// cost (SAD + MV cost, or ~0 for a point outside the range) of list points 0..n-1 -> m.cost
+template <typename F>
+__device__ __forceinline__ void me_eval(MeInt &m, int n, F cand) {
+  const int lane = lane_id();
+  for (int base = 0; base < n; base += HVX_WAVE) {
+    const int cnt = min(HVX_WAVE, n - base);
+    const int sh = 6 - (cnt <= 1 ? 0 : 32 - __clz(cnt - 1)), L = 1 << sh;
+    const int q = lane >> sh, s = lane & (L - 1);
+    MeCand c;
+    c.ok = false; c.x = c.y = 0;
+    if (q < cnt) c = cand(base + q);
+    uint32_t acc = c.ok ? me_sad_part(m, c.x, c.y, s, L) : 0u;
+    for (int o = 1; o < L; o <<= 1) acc += __shfl_xor(acc, o, HVX_WAVE);
+    if (s == 0 && q < cnt)
+      m.cost[base + q] = c.ok ? (acc << m.sub) + me_mv_cost(m.lam, m.px, m.py, 2, c.x, c.y) : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+}
+
+// xTZSearchHelp over list points [start, start+cnt) in order: first minimum, strict '<'
+template <typename F>
+__device__ __forceinline__ void me_take(MeInt &m, int start, int cnt, F cand) {
+  uint64_t key = ~0ull;
+  for (int i = lane_id(); i < cnt; i += HVX_WAVE) {
+    const uint64_t k = ((uint64_t)m.cost[start + i] << 32) | (uint32_t)i;
+    key = k < key ? k : key;
+  }
+  key = wave_min_u64(key);
+  const uint32_t c = (uint32_t)uni((int)(uint32_t)(key >> 32));
+  if (c < m.best_sad) {  // out-of-range points cost ~0 and never pass
+    const MeCand w = cand(start + uni((int)(uint32_t)key));
+    m.best_sad = c; m.best_x = w.x; m.best_y = w.y; m.best_dist = w.dist; m.best_round = 0; m.point_nr = w.pnr;
+  }
+  __syncthreads();  // m.cost is rewritten by the next list
+}
+
+// diamonds d = 1, 2, 4, ... around (sx,sy), concatenated in xTZ8PointDiamondSearch order
+__device__ __forceinline__ int me_dia_start(int k) { return k == 0 ? 0 : k <= 3 ? 4 + 8 * (k - 1) : 28 + 16 * (k - 4); }
+
+__device__ __forceinline__ MeCand me_dia_cand(const MeRange &g, int sx, int sy, int p) {
+  int k, q;
+  if (p < 4) { k = 0; q = p; }
+  else if (p < 28) { k = 1 + ((p - 4) >> 3); q = (p - 4) & 7; }
+  else { k = 4 + ((p - 28) >> 4); q = (p - 28) & 15; }
+  const int d = 1 << k;
+  int dx = 0, dy = 0, pnr = 0, dist = d;
+  if (k == 0) {
+    switch (q) {
+      case 0: dy = -1; pnr = 2; break;
+      case 1: dx = -1; pnr = 4; break;
+      case 2: dx = 1; pnr = 5; break;
+      default: dy = 1; pnr = 7; break;
+    }
+  } else if (k <= 3) {
+    const int h = d >> 1;
+    switch (q) {
+      case 0: dy = -d; pnr = 2; break;
+      case 1: dx = -h; dy = -h; pnr = 1; dist = h; break;
+      case 2: dx = h; dy = -h; pnr = 3; dist = h; break;
+      case 3: dx = -d; pnr = 4; break;
+      case 4: dx = d; pnr = 5; break;
+      case 5: dx = -h; dy = h; pnr = 6; dist = h; break;
+      case 6: dx = h; dy = h; pnr = 8; dist = h; break;
+      default: dy = d; pnr = 7; break;
+    }
+  } else {
+    if (q < 4) {
+      dx = q == 1 ? -d : q == 2 ? d : 0;
+      dy = q == 0 ? -d : q == 3 ? d : 0;
+    } else {
+      const int i = 1 + ((q - 4) >> 2), kk = (q - 4) & 3, o = (d >> 2) * i;
+      dx = (kk & 1) ? o : -o;
+      dy = (kk & 2) ? d - o : o - d;
+    }
+  }
+  MeCand c;
+  c.x = sx + dx; c.y = sy + dy; c.pnr = pnr; c.dist = dist;
+  c.ok = me_in(g, dx, dy, c.x, c.y);  // == the reference's tests, whether the diamond is inside or not
+  return c;
+}
+
+// xTZ2PointSearch (:438): the two points completing the diamond around point_nr
+__constant__ int8_t kTwoPoint[8][2][2] = {{{-1, 0}, {0, -1}}, {{-1, -1}, {1, -1}}, {{0, -1}, {1, 0}},
+                                          {{-1, 1}, {-1, -1}}, {{1, -1}, {1, 1}}, {{-1, 0}, {0, 1}},
+                                          {{-1, 1}, {1, 1}}, {{1, 0}, {0, 1}}};
+
+__device__ __forceinline__ void me_2point(MeInt &m, const MeRange &g) {
+  const int pn = m.point_nr, bx = m.best_x, by = m.best_y;
+  if (pn < 1 || pn > 8) return;  // unreachable: the reference asserts here
+  auto cand = [=](int p) {
+    MeCand c;
+    const int dx = kTwoPoint[pn - 1][p][0], dy = kTwoPoint[pn - 1][p][1];
+    c.x = bx + dx; c.y = by + dy;
+    c.pnr = 0; c.dist = 2; c.ok = me_in(g, dx, dy, c.x, c.y);
+    return c;
+  };
+  me_eval(m, 2, cand);
+  me_take(m, 0, 2, cand);
+}
+
+// xTZSearch (:3881) for job j; returns with m.best_* = the integer result
+__device__ void me_tz(const hvx_me_job &j, MeInt &m) {
+  const int sr = j.search_range;
+  const MeRange g0 = me_search_range(j, j.pred_x, j.pred_y, sr);
+  int mx = j.pred_x, my = j.pred_y;
+  me_clip(j, mx, my);
+  mx >>= 2; my >>= 2;
+  int ix = 0, iy = 0;
+  if (j.use_int2nx2n) {
+    ix = j.i2_x << 2; iy = j.i2_y << 2;
+    me_clip(j, ix, iy);
+    ix >>= 2; iy >>= 2;
+  }
+  m.best_sad = 0xFFFFFFFFu;
+  m.best_x = m.best_y = 0; m.best_dist = 0; m.best_round = 0; m.point_nr = 0;
+  // predictor, zero MV, then the 2Nx2N integer MV
+  {
+    auto cand = [=](int p) {
+      MeCand c;
+      c.x = p == 0 ? mx : p == 1 ? 0 : ix; c.y = p == 0 ? my : p == 1 ? 0 : iy;
+      c.pnr = 0; c.dist = 0; c.ok = true;
+      return c;
+    };
+    const int n = j.use_int2nx2n ? 3 : 2;
+    me_eval(m, n, cand);
+    me_take(m, 0, n, cand);
+  }
+  const MeRange g = j.use_int2nx2n ? me_search_range(j, m.best_x << 2, m.best_y << 2, sr) : g0;
+  int nd = 0;
+  while ((1 << nd) <= sr) nd++;
+  const int ndp = me_dia_start(nd);
+  // first stage: the diamonds around the start, stopped after 3 rounds without a gain
+  {
+    const int sx = m.best_x, sy = m.best_y;
+    auto cand = [=](int p) { return me_dia_cand(g0, sx, sy, p); };
+    me_eval(m, ndp, cand);
+    for (int k = 0; k < nd; k++) {
+      m.best_round += 1;
+      me_take(m, me_dia_start(k), me_dia_start(k + 1) - me_dia_start(k), cand);
+      if ((j.flags & HVX_ME_SMOOTHMV) && m.best_round >= 3) break;
+    }
+  }
+  if (m.best_dist == 1) { m.best_dist = 0; me_2point(m, g0); }
+  // raster (step 5) over the re-centred range
+  if (m.best_dist > 5) {
+    m.best_dist = 5;
+    const int nx = (g.r - g.l) / 5 + 1, ny = (g.b - g.t) / 5 + 1, n = nx * ny;
+    for (int base = 0; base < n; base += HVX_WAVE) {
+      const int cnt = min(HVX_WAVE, n - base);
+      auto cand = [=](int p) {
+        const int q = base + p, ry = q / nx, rx = q - ry * nx;
+        MeCand c;
+        c.x = g.l + 5 * rx; c.y = g.t + 5 * ry; c.pnr = 0; c.dist = 5; c.ok = true;
+        return c;
+      };
+      me_eval(m, cnt, cand);
+      me_take(m, 0, cnt, cand);
+    }
+  }
+  // star refinement: every round's diamonds share their start -> one list, one minimum
+  while (m.best_dist > 0) {
+    const int sx = m.best_x, sy = m.best_y;
+    m.best_dist = 0; m.point_nr = 0;
+    auto cand = [=](int p) { return me_dia_cand(g0, sx, sy, p); };
+    me_eval(m, ndp, cand);
+    me_take(m, 0, ndp, cand);
+    if (m.best_dist == 1) {
+      m.best_dist = 0;
+      if (m.point_nr != 0) me_2point(m, g0);
+    }
+  }
+}
+
+__device__ __forceinline__ void me_int_job(const hvx_me_job &j, const uint8_t *const *__restrict__ cur_planes,
+                                           const uint8_t *const *__restrict__ ref_planes, int stride, uint8_t *org,
+                                           uint32_t *cost, hvx_me_result *out) {
+  if (j.w <= 0 || j.h <= 0) {  // empty slot (e.g. a CU outside the picture): defined zero result
+    if (lane_id() == 0) { hvx_me_result z; memset(&z, 0, sizeof(z)); *out = z; }
+    return;
+  }
+  const uint8_t *cur = cur_planes[j.cur_idx] + j.pu_y * stride + j.pu_x;
+  for (int k = lane_id(); k < j.w * j.h; k += HVX_WAVE) {
+    const int y = k / j.w, x = k - y * j.w;
+    org[y * 64 + x] = cur[y * stride + x];
+  }
+  __syncthreads();
+  MeInt m;
+  m.org = org; m.cost = cost;
+  m.ref = ref_planes[j.ref_idx] + j.pu_y * stride + j.pu_x;
+  m.sr = stride;
+  const int w = j.w;
+  const bool spec = (w == 4 || w == 8 || w == 16 || w == 32 || w == 64 || w == 12 || w == 24 || w == 48);
+  m.sub = ((j.flags & HVX_ME_FEN) && j.h > 8 && spec) ? 1 : 0;
+  m.rows = (j.h + (1 << m.sub) - 1) >> m.sub;
+  m.gw = w >> 2;
+  m.lam = j.lambda_motion;
+  m.px = j.pred_x; m.py = j.pred_y;
+  me_tz(j, m);
+  if (lane_id() == 0) {
+    out->mv_int_x = m.best_x; out->mv_int_y = m.best_y;
+    out->sad_int = m.best_sad - me_mv_cost(m.lam, m.px, m.py, 2, m.best_x, m.best_y);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_me_int(const uint8_t *const *__restrict__ cur_planes,
+                                              const uint8_t *const *__restrict__ ref_planes, int stride,
+                                              const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t org[64 * 64];
+  __shared__ uint32_t cost[kMeMaxList];
+  const int jid = blockIdx.x;
+  if (jid >= n) return;
+  const hvx_me_job j = jobs[jid];
+  me_int_job(j, cur_planes, ref_planes, stride, org, cost, out + jid);
+}
+
+// CTU-pass view: block b = (ctu * ncu + cu) * nref + ref of one depth -> job slot
+// ((ctu * 85 + first + cu) * nref + ref)
+__device__ __forceinline__ size_t me_ctu_slot(int b, int nref, int ncu, int first) {
+  const int ref = b % nref, cu = (b / nref) % ncu, ctu = b / (nref * ncu);
+  return ((size_t)ctu * HVX_CUS_PER_CTU + first + cu) * nref + ref;
+}
+
+__global__ __launch_bounds__(64) void k_me_int_ctu(const uint8_t *const *__restrict__ cur_planes,
+                                                  const uint8_t *const *__restrict__ ref_planes, int stride,
+                                                  const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
+                                                  int nref, int ncu, int first) {
+  __shared__ __attribute__((aligned(16))) uint8_t org[64 * 64];
+  __shared__ uint32_t cost[kMeMaxList];
+  const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
+  const hvx_me_job j = jobs[slot];
+  me_int_job(j, cur_planes, ref_planes, stride, org, cost, out + slot);
+}
+
+// ======================================================================================
+// fractional refinement
+// ======================================================================================
+
+// Quarter-sample luma sample at (x,y) + quarter-pel (qx,qy); standard two-stage 8-bit path
+// (TComInterpolationFilter::filterHor/filterVer, isFirst/isLast offsets).  Used by the CTU
+// pass's motion compensation.
 __device__ __forceinline__ int me_qpel_sample(const uint8_t *ref, int sr, int x, int y, int qx, int qy) {
   const int fx = qx & 3, fy = qy & 3;
   const uint8_t *p = ref + (y + (qy >> 2)) * sr + x + (qx >> 2);
@@ -172,153 +384,160 @@ __device__ __forceinline__ int me_qpel_sample(const uint8_t *ref, int sr, int x,
   return clip_pel((s2 + (1 << 11) + (8192 << 6)) >> 12);
 }
 
-// xPatternRefinement (:808): 9 candidates around base (quarter-pel, relative to MV 0)
-// s_acMvRefineH / s_acMvRefineQ (TEncSearch.cpp:51-75)
+// xPatternRefinement (:808) candidate offsets: s_acMvRefineH / s_acMvRefineQ (TEncSearch.cpp:51-75)
 __constant__ int8_t kRefH[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
 __constant__ int8_t kRefQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
 
-__device__ uint32_t me_refine(MeState &m, int16_t *blk, bool had, int bqx, int bqy, int frac, int &fx, int &fy) {
-  uint32_t best = 0xFFFFFFFFu;
-  int bi = 0;
-  for (int i = 0; i < 9; i++) {
-    const int dx = frac == 2 ? kRefH[i][0] : kRefQ[i][0], dy = frac == 2 ? kRefH[i][1] : kRefQ[i][1];
-    const int qx = bqx + dx * frac, qy = bqy + dy * frac;
-    __syncthreads();
-    for (int k = lane_id(); k < m.w * m.h; k += HVX_WAVE) {
-      const int y = k / m.w, x = k - y * m.w;
-      blk[y * 64 + x] = (int16_t)me_qpel_sample(m.ref, m.sr, x, y, qx, qy);
+template <int S>
+struct MeFracSmem {
+  int16_t hp[3][(S + 8) * S];  // first-stage intermediates of the 3 horizontal phases, rows iy-4 ..
+  int16_t blk[S * S];          // candidate block (per-lane-tile SATD path)
+  uint8_t org[S * S];
+};
+
+// one prediction sample of candidate column phase c at vertical quarter position qy
+// (relative to the integer MV row iy): the reference's second filter stage on hp[c]
+template <int S>
+__device__ __forceinline__ int me_frac_sample(const MeFracSmem<S> &sm, int c, int ry, int fy, int x, int y) {
+  const int16_t *h = sm.hp[c] + x;
+  if (!fy) return clip_pel((h[(ry + 4 + y) * S] + 8192 + 32) >> 6);
+  int s = 0;
+  const int r0 = ry + 1 + y;
+#pragma unroll
+  for (int t = 0; t < 8; t++) s += kLumaFilter[fy][t] * h[(r0 + t) * S];
+  return clip_pel((s + (1 << 11) + (8192 << 6)) >> 12);
+}
+
+// 8x8 Hadamard of one tile held one difference per lane (lane = y*8 + x); every lane gets
+// the tile's (sum|coef| + 2) >> 2 (TComRdCost::xCalcHADs8x8; coefficient order and signs
+// do not change the sum of magnitudes)
+__device__ __forceinline__ uint32_t had8_xlane(int v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_xor(v, o, HVX_WAVE);
+    v = (lane & o) ? t - v : v + t;
+  }
+  return (wave_sum_u32((uint32_t)abs(v)) + 2) >> 2;
+}
+
+// xPatternRefinement (:808): the 9 candidates of one stage.  (qx0,qy0) = stage centre in
+// quarter-pel relative to the PU, step 2 (half) or 1 (quarter); (ix,iy) the integer MV.
+template <int S>
+__device__ uint32_t me_frac_stage(MeFracSmem<S> &sm, const hvx_me_job &j, const uint8_t *ref, int stride, int ix,
+                                  int iy, int qx0, int qy0, int step, int scale, int mvx0, int mvy0, int &bi) {
+  const int w = j.w, h = j.h, lane = lane_id();
+  const bool had = (j.flags & HVX_ME_HADME) != 0;
+  // 1. horizontal phases: column c at quarter x = qx0 + (c-1)*step
+  __syncthreads();
+  for (int c = 0; c < 3; c++) {
+    const int qx = qx0 + (c - 1) * step, ox = qx >> 2, fx = qx & 3;
+    const uint8_t *src = ref + (iy - 4) * stride + ox;
+    for (int k = lane; k < (h + 8) * w; k += HVX_WAVE) {
+      const int r = k / w, x = k - r * w;
+      const uint8_t *p = src + r * stride + x;
+      int v;
+      if (fx) {
+        v = 0;
+#pragma unroll
+        for (int t = 0; t < 8; t++) v += kLumaFilter[fx][t] * p[t - 3];
+        v -= 8192;
+      } else {
+        v = (p[0] << 6) - 8192;
+      }
+      sm.hp[c][r * S + x] = (int16_t)v;
     }
-    __syncthreads();
+  }
+  __syncthreads();
+  // 2. the 9 candidates, reference order, strict '<'
+  const bool xl = had && (w % 8 == 0) && (h % 8 == 0) && (w * h <= 1024);
+  const int tw = w >> 3, nt = (w * h) >> 6;
+  uint32_t best = 0xFFFFFFFFu;
+  bi = 0;
+  for (int i = 0; i < 9; i++) {
+    const int dx = step == 2 ? kRefH[i][0] : kRefQ[i][0], dy = step == 2 ? kRefH[i][1] : kRefQ[i][1];
+    const int qy = qy0 + dy * step, ry = (qy >> 2) - iy, fy = qy & 3, c = dx + 1;
     uint32_t d;
-    if (had) {
-      d = wave_satd(m.org, 64, blk, 64, m.w, m.h);
+    if (xl) {
+      d = 0;
+      for (int t = 0; t < nt; t++) {
+        const int x = ((t % tw) << 3) + (lane & 7), y = ((t / tw) << 3) + (lane >> 3);
+        d += had8_xlane((int)sm.org[y * S + x] - me_frac_sample(sm, c, ry, fy, x, y));
+      }
+    } else if (had) {
+      for (int k = lane; k < w * h; k += HVX_WAVE) {
+        const int y = k / w, x = k - y * w;
+        sm.blk[y * S + x] = (int16_t)me_frac_sample(sm, c, ry, fy, x, y);
+      }
+      __syncthreads();
+      d = wave_satd(sm.org, S, sm.blk, S, w, h);
+      __syncthreads();
     } else {
       uint32_t s = 0;
-      for (int k = lane_id(); k < m.w * m.h; k += HVX_WAVE) {
-        const int y = k / m.w, x = k - y * m.w;
-        s += (uint32_t)abs((int)m.org[y * 64 + x] - (int)blk[y * 64 + x]);
+      for (int k = lane; k < w * h; k += HVX_WAVE) {
+        const int y = k / w, x = k - y * w;
+        s += (uint32_t)abs((int)sm.org[y * S + x] - me_frac_sample(sm, c, ry, fy, x, y));
       }
       d = wave_sum_u32(s);
     }
-    d += me_mv_cost(m, dx + fx, dy + fy);
+    d += me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
     if (d < best) { best = d; bi = i; }
   }
-  fx = frac == 2 ? kRefH[bi][0] : kRefQ[bi][0];
-  fy = frac == 2 ? kRefH[bi][1] : kRefQ[bi][1];
   return best;
 }
 
-// one whole xMotionEstimation for job j by the calling wave; writes *out (lane 0)
-__device__ void me_run(const hvx_me_job &j, const uint8_t *const *__restrict__ cur_planes,
-                       const uint8_t *const *__restrict__ ref_planes, int stride, uint8_t *org, int16_t *blk,
-                       hvx_me_result *out) {
-  if (j.w <= 0 || j.h <= 0) {  // empty slot (e.g. a CU outside the picture): defined zero result
-    if (lane_id() == 0) { hvx_me_result z; memset(&z, 0, sizeof(z)); *out = z; }
-    return;
-  }
+template <int S>
+__device__ void me_frac_job(const hvx_me_job &j, const uint8_t *const *__restrict__ cur_planes,
+                            const uint8_t *const *__restrict__ ref_planes, int stride, MeFracSmem<S> &sm,
+                            hvx_me_result *out) {
+  if (j.w <= 0 || j.h <= 0 || j.w > S || j.h > S) return;  // k_me_int wrote the empty result
+  const int ix = out->mv_int_x, iy = out->mv_int_y;
+  const uint32_t sad_int = out->sad_int;
   const uint8_t *cur = cur_planes[j.cur_idx] + j.pu_y * stride + j.pu_x;
   for (int k = lane_id(); k < j.w * j.h; k += HVX_WAVE) {
     const int y = k / j.w, x = k - y * j.w;
-    org[y * 64 + x] = cur[y * stride + x];
+    sm.org[y * S + x] = cur[y * stride + x];
   }
-  __syncthreads();
-  MeState m;
-  m.org = org;
-  m.ref = ref_planes[j.ref_idx] + j.pu_y * stride + j.pu_x;
-  m.sr = stride; m.w = j.w; m.h = j.h;
-  m.sub = ((j.flags & HVX_ME_FEN) && j.h > 8) ? 1 : 0;
-  {
-    const int w = j.w;
-    const bool spec = (w == 4 || w == 8 || w == 16 || w == 32 || w == 64 || w == 12 || w == 24 || w == 48);
-    if (!spec) m.sub = 0;
-  }
-  m.lam = j.lambda_motion;
-  m.px = j.pred_x; m.py = j.pred_y;
-  m.cost_scale = 2;
-  const int sr = j.search_range;
-  const MeRange g0 = me_search_range(j, j.pred_x, j.pred_y, sr);
-
-  // ---- xTZSearch ----
-  int mx = j.pred_x, my = j.pred_y;
-  me_clip(j, mx, my);
-  mx >>= 2; my >>= 2;
-  m.best_sad = 0xFFFFFFFFu;
-  m.best_x = m.best_y = 0; m.best_dist = 0; m.best_round = 0; m.point_nr = 0;
-  me_help(m, mx, my, 0, 0);
-  me_help(m, 0, 0, 0, 0);
-  MeRange g = g0;
-  if (j.use_int2nx2n) {
-    int ix = j.i2_x << 2, iy = j.i2_y << 2;
-    me_clip(j, ix, iy);
-    me_help(m, ix >> 2, iy >> 2, 0, 0);
-    g = me_search_range(j, m.best_x << 2, m.best_y << 2, sr);
-  }
-  int sx = m.best_x, sy = m.best_y;
-  for (int d = 1; d <= sr; d *= 2) {
-    me_diamond(m, g0, sx, sy, d);
-    if ((j.flags & HVX_ME_SMOOTHMV) && m.best_round >= 3) break;
-  }
-  if (m.best_dist == 1) { m.best_dist = 0; me_2point(m, g0); }
-  if (m.best_dist > 5) {
-    m.best_dist = 5;
-    for (sy = g.t; sy <= g.b; sy += 5)
-      for (sx = g.l; sx <= g.r; sx += 5) me_help(m, sx, sy, 0, 5);
-  }
-  while (m.best_dist > 0) {
-    sx = m.best_x; sy = m.best_y;
-    m.best_dist = 0; m.point_nr = 0;
-    for (int d = 1; d < sr + 1; d *= 2) me_diamond(m, g0, sx, sy, d);
-    if (m.best_dist == 1) {
-      m.best_dist = 0;
-      if (m.point_nr != 0) me_2point(m, g0);
-    }
-  }
-  const int ix = m.best_x, iy = m.best_y;
-  const uint32_t sad_int = m.best_sad - me_mv_cost(m, ix, iy);
-
-  // ---- xPatternSearchFracDIF ----
-  const bool had = (j.flags & HVX_ME_HADME) != 0;
-  m.cost_scale = 1;
-  int hx = ix << 1, hy = iy << 1;
-  me_refine(m, blk, had, ix << 2, iy << 2, 2, hx, hy);
-  m.cost_scale = 0;
-  int qx = ((ix << 1) + hx) << 1, qy = ((iy << 1) + hy) << 1;
-  const uint32_t cost = me_refine(m, blk, had, (ix << 2) + (hx << 1), (iy << 2) + (hy << 1), 1, qx, qy);
-  const int fmx = (ix << 2) + (hx << 1) + qx, fmy = (iy << 2) + (hy << 1) + qy;
-  const uint32_t mv_bits = eg_bits(fmx - m.px) + eg_bits(fmy - m.py);
+  const uint8_t *ref = ref_planes[j.ref_idx] + j.pu_y * stride + j.pu_x;
+  // xPatternSearchFracDIF (:4240): half-pel around the integer MV, then quarter-pel
+  int bh, bq;
+  me_frac_stage(sm, j, ref, stride, ix, iy, ix << 2, iy << 2, 2, 1, ix << 1, iy << 1, bh);
+  const int hx = kRefH[bh][0], hy = kRefH[bh][1];
+  const int cqx = (ix << 2) + (hx << 1), cqy = (iy << 2) + (hy << 1);
+  const uint32_t cost = me_frac_stage(sm, j, ref, stride, ix, iy, cqx, cqy, 1, 0, cqx, cqy, bq);
+  const int qx = kRefQ[bq][0], qy = kRefQ[bq][1];
+  const int fmx = cqx + qx, fmy = cqy + qy;
+  const uint32_t mv_bits = eg_bits(fmx - j.pred_x) + eg_bits(fmy - j.pred_y);
   const uint32_t bits = (uint32_t)j.bits_in + mv_bits;
+  const uint32_t lam = j.lambda_motion;
   if (lane_id() == 0) {
     hvx_me_result r;
     r.mv_int_x = ix; r.mv_int_y = iy; r.sad_int = sad_int;
     r.half_x = hx; r.half_y = hy; r.qtr_x = qx; r.qtr_y = qy; r.cost_frac = cost;
     r.mv_x = fmx; r.mv_y = fmy; r.bits = bits;
-    r.cost = (uint32_t)(floor(1.0 * ((double)cost - (double)((m.lam * mv_bits) >> 16))) + (double)((m.lam * bits) >> 16));
+    r.cost = (uint32_t)(floor(1.0 * ((double)cost - (double)((lam * mv_bits) >> 16))) + (double)((lam * bits) >> 16));
     *out = r;
   }
 }
 
-__global__ __launch_bounds__(64) void k_me(const uint8_t *const *__restrict__ cur_planes,
-                                          const uint8_t *const *__restrict__ ref_planes, int stride,
-                                          const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
-  __shared__ uint8_t org[64 * 64];
-  __shared__ int16_t blk[64 * 64];
+template <int S>
+__global__ __launch_bounds__(64) void k_me_frac(const uint8_t *const *__restrict__ cur_planes,
+                                               const uint8_t *const *__restrict__ ref_planes, int stride,
+                                               const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
+  __shared__ MeFracSmem<S> sm;
   const int jid = blockIdx.x;
   if (jid >= n) return;
   const hvx_me_job j = jobs[jid];
-  me_run(j, cur_planes, ref_planes, stride, org, blk, out + jid);
+  me_frac_job<S>(j, cur_planes, ref_planes, stride, sm, out + jid);
 }
 
-// CTU-pass view: block b = (ctu * ncu + cu) * nref + ref of one depth -> job slot
-// ((ctu * 85 + first + cu) * nref + ref)
-__global__ __launch_bounds__(64) void k_me_ctu_depth(const uint8_t *const *__restrict__ cur_planes,
-                                                    const uint8_t *const *__restrict__ ref_planes, int stride,
-                                                    const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
-                                                    int nref, int ncu, int first) {
-  __shared__ uint8_t org[64 * 64];
-  __shared__ int16_t blk[64 * 64];
-  const int b = blockIdx.x;
-  const int ref = b % nref, cu = (b / nref) % ncu, ctu = b / (nref * ncu);
-  const size_t slot = ((size_t)ctu * HVX_CUS_PER_CTU + first + cu) * nref + ref;
+template <int S>
+__global__ __launch_bounds__(64) void k_me_frac_ctu(const uint8_t *const *__restrict__ cur_planes,
+                                                   const uint8_t *const *__restrict__ ref_planes, int stride,
+                                                   const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
+                                                   int nref, int ncu, int first) {
+  __shared__ MeFracSmem<S> sm;
+  const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
   const hvx_me_job j = jobs[slot];
-  me_run(j, cur_planes, ref_planes, stride, org, blk, out + slot);
+  me_frac_job<S>(j, cur_planes, ref_planes, stride, sm, out + slot);
 }

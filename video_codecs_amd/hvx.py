@@ -192,7 +192,7 @@ class CtuAnalyzer:
         return from_device(self.out, _abi.CU_RESULT).reshape(self.nctu, _abi.CUS_PER_CTU)
 
 
-PHASES = ("me_d0", "me_d1", "me_d2", "me_d3", "mc_resid", "tu32", "tu16", "tu8", "finalize")
+PHASES = ("me_d0", "me_d1", "me_d2", "me_d3", "me_frac", "mc_resid", "tu32", "tu16", "tu8", "finalize")
 
 
 def set_timing(on):
