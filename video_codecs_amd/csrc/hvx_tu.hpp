@@ -23,17 +23,16 @@
 template <int L>
 struct TuSmem {
   static constexpr int N = 4 << L, NN = N * N, NCG = NN / 16;
-  int32_t mt[NN];     // transform matrix, transposed: mt[x*N + k] = M[k][x]
-  int32_t m[NN];      // transform matrix: m[k*N + x]
-  int32_t a[NN];      // residual (int) / intermediate
+  int16_t mt[NN];     // transform matrix, transposed: mt[x*N + k] = M[k][x]
+  int16_t m[NN];      // transform matrix: m[k*N + x]
+  int16_t res[NN];    // input residual (kept for the pipeline SSE)
+  int32_t a[NN];      // residual (int) / dequantised coefficients; RDOQ: context state per scan position
   int32_t coef[NN];   // transform output (raster)
   int32_t lev[NN];    // levels (raster)
-  int32_t ld[NN];     // RDOQ lLevelDouble per scan position
-  int32_t rup[NN], rdown[NN], sigd[NN], du[NN];  // raster (SBH inputs)
-  double cc[NN], cs[NN], cc0[NN];                 // per scan position
-  double cgsig[NCG];
-  uint32_t sigcg[NCG];
-  int16_t res[NN];    // input residual (kept for the pipeline SSE)
+  int32_t ld[NN];     // RDOQ lLevelDouble per scan position; plain quant: deltaU; pipeline: reconstruction
+  int32_t csr[NN];    // RDOQ significance-flag rate of the chosen cost per scan position; IT scratch
+  double cc[NN];      // RDOQ cost of the chosen level per scan position
+  int32_t cgr[NCG];   // RDOQ coded-group flag rate per CG scan position
   int32_t scal[4];
 };
 
@@ -74,8 +73,8 @@ __device__ void tu_load_matrix(TuSmem<L> &s, bool dst) {
   for (int i = lane_id(); i < NN; i += HVX_WAVE) {
     const int k = i / N, x = i % N;
     const int v = dst ? kDst4[i] : kMat[mat_base(L) + i];
-    s.m[i] = v;
-    s.mt[x * N + k] = v;
+    s.m[i] = (int16_t)v;
+    s.mt[x * N + k] = (int16_t)v;
   }
 }
 
@@ -108,7 +107,7 @@ __device__ void tu_forward_transform(TuSmem<L> &s) {
 template <int L>
 __device__ void tu_inverse_transform(TuSmem<L> &s, const int32_t *in, int32_t *out) {
   constexpr int N = 4 << L, NN = N * N;
-  int32_t *tmp = s.rup;  // scratch: tmp[y*N + u]
+  int32_t *tmp = s.csr;  // scratch: tmp[y*N + u]
   for (int i = lane_id(); i < NN; i += HVX_WAVE) {
     const int y = i / N, u = i % N;
     int acc = 0;
@@ -128,18 +127,13 @@ __device__ void tu_inverse_transform(TuSmem<L> &s, const int32_t *in, int32_t *o
 }
 
 // ----------------------------------------------------------------------------------- RDOQ helpers
-struct RdState {
-  const hvx_estbits *est;
-  double lambda;
-};
-
-__device__ __forceinline__ double rd_icost(const RdState &r, double rate) { return r.lambda * rate; }
-
-// xGetICRate (:2891)
-__device__ int rd_ic_rate(const RdState &r, uint32_t level, int ctx_one, int ctx_abs, int rice, uint32_t c1_idx,
-                          uint32_t c2_idx, int limited, int max_log2) {
+// xGetICRate (:2891) with the context's table entries already fetched:
+// g0/g1 = greaterOneBits[ctx_one][0/1], a0/a1 = levelAbsBits[ctx_abs][0/1];
+// c1ok = c1Idx < 8, c2ok = c2Idx < 1
+__device__ __forceinline__ int rd_ic_rate(uint32_t level, int rice, bool c1ok, bool c2ok, int g0, int g1, int a0,
+                                          int a1, int limited, int max_log2) {
   int rate = 32768;
-  const uint32_t base = (c1_idx < 8) ? (2 + (c2_idx < 1)) : 1;
+  const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
   if (level >= base) {
     uint32_t symbol = level - base;
     if (symbol < (3u << rice)) {
@@ -156,15 +150,15 @@ __device__ int rd_ic_rate(const RdState &r, uint32_t level, int ctx_one, int ctx
       while (symbol >= (1u << len)) { symbol -= (1u << (len++)); }
       rate += (int)((3 + len + 1 - rice + len) << 15);
     }
-    if (c1_idx < 8) {
-      rate += r.est->greaterOneBits[ctx_one][1];
-      if (c2_idx < 1) rate += r.est->levelAbsBits[ctx_abs][1];
+    if (c1ok) {
+      rate += g1;
+      if (c2ok) rate += a1;
     }
   } else if (level == 1) {
-    rate += r.est->greaterOneBits[ctx_one][0];
+    rate += g0;
   } else if (level == 2) {
-    rate += r.est->greaterOneBits[ctx_one][1];
-    rate += r.est->levelAbsBits[ctx_abs][0];
+    rate += g1;
+    rate += a0;
   } else {
     rate = 0;
   }
@@ -195,15 +189,43 @@ __device__ __forceinline__ int rd_sig_ctx(int pattern, const TuCoding &c, int sp
   return c.first_sig + offset;
 }
 
-__device__ __forceinline__ double rd_rate_last(const RdState &r, int px, int py, int ch) {
+__device__ __forceinline__ double rd_rate_last(const hvx_estbits *est, double lambda, int px, int py, int ch) {
   const int cx = kGroupIdx[px], cy = kGroupIdx[py];
-  double c = (double)(r.est->lastXBits[ch][cx] + r.est->lastYBits[ch][cy]);
+  double c = (double)(est->lastXBits[ch][cx] + est->lastYBits[ch][cy]);
   if (cx > 3) c += 32768.0 * ((cx - 2) >> 1);
   if (cy > 3) c += 32768.0 * ((cy - 2) >> 1);
-  return rd_icost(r, c);
+  return lambda * c;
+}
+
+__device__ __forceinline__ int rl(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+
+// Context state of a scan position at its RDOQ decision, packed for the sign-hiding rate
+// deltas: ctx_one | ctx_abs<<5 | rice<<8 | c1ok<<13 | c2ok<<14 | has_sig<<15 | ctx_sig<<16
+struct RdCtx {
+  int ctx_one, ctx_abs, rice, ctx_sig;
+  bool c1ok, c2ok, has_sig;
+};
+__device__ __forceinline__ int rd_pack(int one, int abs_, int rice, bool c1ok, bool c2ok, bool has_sig, int sig) {
+  return one | (abs_ << 5) | (rice << 8) | ((int)c1ok << 13) | ((int)c2ok << 14) | ((int)has_sig << 15) | (sig << 16);
+}
+__device__ __forceinline__ RdCtx rd_unpack(int v) {
+  RdCtx r;
+  r.ctx_one = v & 31; r.ctx_abs = (v >> 5) & 7; r.rice = (v >> 8) & 31;
+  r.c1ok = (v >> 13) & 1; r.c2ok = (v >> 14) & 1; r.has_sig = (v >> 15) & 1; r.ctx_sig = (v >> 16) & 63;
+  return r;
 }
 
 // xRateDistOptQuant (:2129-2671).  Input s.coef (raster); output s.lev (signed levels), returns uiAbsSum.
+//
+// The reverse-scan state machine (c1/c2/Rice/context-set carry, CG zero-out, last-position
+// search) is inherently serial; it runs as WAVE-UNIFORM code: every lane executes the same
+// scalar control flow, the estBits tables it indexes with state-dependent contexts sit in
+// lane slices of four VGPRs and are fetched with v_readlane (no dependent memory loads),
+// each coefficient group's 16 inputs are loaded in one batch, and the 16 per-position
+// results are gathered into lanes 0..15 and stored once per group.  Double precision with
+// the reference's exact operation order (-ffp-contract=off) keeps every decision identical.
+// Sign hiding then runs one coefficient group per lane (groups are independent), with the
+// rate deltas recomputed from the packed context state of each position.
 template <int L>
 __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits *est, int32_t *arl_out) {
   constexpr int N = 4 << L, NN = N * N, NCG = NN / 16, LOG2 = L + 2;
@@ -218,246 +240,296 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   double escale = (double)(1 << 15);
   escale = escale * ldexp(1.0, -2 * tsn);  // == pow(2.0, -2.0*tsn) exactly
   escale = escale / qc / qc / (1 << 0);
+  const double lambda = d.lambda;
   const TuCoding c = tu_coding<L>(d);
   const int64_t lim = (int64_t)2147483647 - ((int64_t)1 << (qbits - 1));
   const int qbits_c = qbits - 7, add_c = 1 << (qbits_c - 1);
+  const int lane = lane_id();
+  int32_t *st = s.a;  // the residual copy is dead once the forward transform has run
 
-  // ---- per-coefficient work across lanes ----
-  for (int sp = lane_id(); sp < NN; sp += HVX_WAVE) {
+  // ---- A. per-coefficient work across lanes ----
+  for (int sp = lane; sp < NN; sp += HVX_WAVE) {
     const int blk = c.scan[sp];
     const int64_t t = (int64_t)abs(s.coef[blk]) * qc;
     const int32_t ld = (int32_t)(t < lim ? t : lim);
     s.ld[sp] = ld;
-    const double e = (double)ld;
-    s.cc0[sp] = e * e * escale;
-    s.cc[sp] = 0.0;
-    s.cs[sp] = 0.0;
-    s.rup[blk] = 0; s.rdown[blk] = 0; s.sigd[blk] = 0; s.du[blk] = 0;
     if (arl_out) arl_out[blk] = d.adaptive_qp_select ? (ld + add_c) >> qbits_c : 0;
   }
-  for (int g = lane_id(); g < NCG; g += HVX_WAVE) { s.cgsig[g] = 0.0; s.sigcg[g] = 0; }
+  // estBits in lane slices: entry [ctx][0] in lane ctx, [ctx][1] in lane 32 + ctx (or own VGPR)
+  const int t_sb0 = lane < 44 ? est->significantBits[lane][0] : 0;
+  const int t_sb1 = lane < 44 ? est->significantBits[lane][1] : 0;
+  const int t_g = lane < 24 ? est->greaterOneBits[lane][0] : (lane >= 32 && lane < 56) ? est->greaterOneBits[lane - 32][1] : 0;
+  const int t_a = lane < 6 ? est->levelAbsBits[lane][0] : (lane >= 32 && lane < 38) ? est->levelAbsBits[lane - 32][1] : 0;
   __syncthreads();
 
-  if (lane_id() == 0) {
-    const RdState r = {est, d.lambda};
-    const uint32_t rice0 = (uint32_t)d.golomb_rice_stat / 4;
-    uint32_t rice = rice0, ctx_set = 0, c1_idx = 0, c2_idx = 0;
-    int c1 = 1, c2 = 0, last = -1, cg_last = -1;
-    double block_uncoded = 0, base_cost = 0;
-    const int sig_off = ch ? 28 : 0;
-    for (int cgp = NCG - 1; cgp >= 0; cgp--) {
-      const int cgblk = c.scan_cg[cgp];
-      const int cy = cgblk / c.wg, cx = cgblk - cy * c.wg;
-      int nnz0 = 0;
-      double coded_ld = 0, uncoded = 0, sig_cost = 0, sig_cost0 = 0;
-      int pattern = 0;
-      if (NCG > 1) {
-        const int rr = cx < c.wg - 1 ? (s.sigcg[cy * c.wg + cx + 1] != 0) : 0;
-        const int bb = cy < c.wg - 1 ? (s.sigcg[(cy + 1) * c.wg + cx] != 0) : 0;
-        pattern = rr + (bb << 1);
-      }
-      for (int pin = 15; pin >= 0; pin--) {
-        const int sp = cgp * 16 + pin;
-        const int blk = c.scan[sp];
-        const int32_t ld = s.ld[sp];
-        const uint32_t q = (uint32_t)((ld + (1 << (qbits - 1))) >> qbits);
-        const uint32_t max_abs = (uint32_t)ecmax < q ? (uint32_t)ecmax : q;
-        block_uncoded += s.cc0[sp];
-        int32_t out = (int32_t)max_abs;
-        if (max_abs > 0 && last < 0) {
-          last = sp;
-          ctx_set = (comp ? 4 : 0) + ((comp == 0 && (sp >> 4) > 0) ? 2 : 0);
-          cg_last = cgp;
-        }
-        if (last >= 0) {
-          const int ctx_one = 4 * (int)ctx_set + c1, ctx_abs = (int)ctx_set + c2;
-          // xGetCodedLevel (:2822)
-          const bool is_last = sp == last;
-          int ctx_sig = sig_off;
-          if (!is_last) ctx_sig = sig_off + rd_sig_ctx<L>(pattern, c, sp, ch);
-          double cur_sig = 0, cost, cost_sig = 0;
-          uint32_t best = 0;
-          bool done = false;
-          if (!is_last && max_abs < 3) {
-            cost_sig = rd_icost(r, (double)est->significantBits[ctx_sig][0]);
-            cost = s.cc0[sp] + cost_sig;
-            if (max_abs == 0) done = true;
-          } else {
-            cost = 1.7e+308;
-          }
-          if (!done) {
-            if (!is_last) cur_sig = rd_icost(r, (double)est->significantBits[ctx_sig][1]);
-            const uint32_t min_abs = max_abs > 1 ? max_abs - 1 : 1;
-            for (int lv = (int)max_abs; lv >= (int)min_abs; lv--) {
-              const double err = (double)sub32(ld, shl32(lv, qbits));
-              double cc = err * err * escale +
-                          rd_icost(r, (double)rd_ic_rate(r, (uint32_t)lv, ctx_one, ctx_abs, (int)rice, c1_idx, c2_idx, ext, max_log2));
-              cc += cur_sig;
-              if (cc < cost) { best = (uint32_t)lv; cost = cc; cost_sig = cur_sig; }
-            }
-          }
-          s.cc[sp] = cost;
-          s.cs[sp] = cost_sig;
-          const uint32_t level = best;
-          if (!is_last) s.sigd[blk] = est->significantBits[ctx_sig][1] - est->significantBits[ctx_sig][0];
-          s.du[blk] = sub32(ld, shl32((int32_t)level, qbits)) >> (qbits - 8);
-          if (level > 0) {
-            const int now = rd_ic_rate(r, level, ctx_one, ctx_abs, (int)rice, c1_idx, c2_idx, ext, max_log2);
-            s.rup[blk] = rd_ic_rate(r, level + 1, ctx_one, ctx_abs, (int)rice, c1_idx, c2_idx, ext, max_log2) - now;
-            s.rdown[blk] = rd_ic_rate(r, level - 1, ctx_one, ctx_abs, (int)rice, c1_idx, c2_idx, ext, max_log2) - now;
-          } else {
-            s.rup[blk] = est->greaterOneBits[ctx_one][0];
-          }
-          out = (int32_t)level;
-          base_cost += s.cc[sp];
-          const uint32_t base = (c1_idx < 8) ? (2 + (c2_idx < 1)) : 1;
-          if (level >= base && level > 3u * (1u << rice)) rice = d.persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
-          if (level >= 1) c1_idx++;
-          if (level > 1) { c1 = 0; c2 += (c2 < 2); c2_idx++; }
-          else if (c1 < 3 && c1 > 0 && level) c1++;
-          if ((sp % 16 == 0) && sp > 0) {
-            ctx_set = (comp ? 4 : 0) + ((comp == 0 && ((sp - 1) >> 4) > 0) ? 2 : 0) + (c1 == 0 ? 1 : 0);
-            c1 = 1; c2 = 0; c1_idx = 0; c2_idx = 0;
-            rice = rice0;
-          }
-        } else {
-          base_cost += s.cc0[sp];
-        }
-        s.lev[blk] = out;
-        sig_cost += s.cs[sp];
-        if (pin == 0) sig_cost0 = s.cs[sp];
-        if (out) {
-          s.sigcg[cgblk] = 1;
-          coded_ld += s.cc[sp] - s.cs[sp];
-          uncoded += s.cc0[sp];
-          if (pin != 0) nnz0++;
-        }
-      }
-      if (cg_last >= 0) {
-        if (cgp) {
-          const int rr = cx < c.wg - 1 ? (s.sigcg[cy * c.wg + cx + 1] != 0) : 0;
-          const int bb = cy < c.wg - 1 ? (s.sigcg[(cy + 1) * c.wg + cx] != 0) : 0;
-          const int ctx = (rr + bb) != 0;
-          if (s.sigcg[cgblk] == 0) {
-            base_cost += rd_icost(r, (double)est->significantCoeffGroupBits[ctx][0]) - sig_cost;
-            s.cgsig[cgp] = rd_icost(r, (double)est->significantCoeffGroupBits[ctx][0]);
-          } else if (cgp < cg_last) {
-            if (nnz0 == 0) { base_cost -= sig_cost0; sig_cost -= sig_cost0; }
-            double zero_cost = base_cost;
-            base_cost += rd_icost(r, (double)est->significantCoeffGroupBits[ctx][1]);
-            zero_cost += rd_icost(r, (double)est->significantCoeffGroupBits[ctx][0]);
-            s.cgsig[cgp] = rd_icost(r, (double)est->significantCoeffGroupBits[ctx][1]);
-            zero_cost += uncoded;
-            zero_cost -= coded_ld;
-            zero_cost -= sig_cost;
-            if (zero_cost < base_cost) {
-              s.sigcg[cgblk] = 0;
-              base_cost = zero_cost;
-              s.cgsig[cgp] = rd_icost(r, (double)est->significantCoeffGroupBits[ctx][0]);
-              for (int pin = 15; pin >= 0; pin--) {
-                const int sp = cgp * 16 + pin;
-                const int blk = c.scan[sp];
-                if (s.lev[blk]) { s.lev[blk] = 0; s.cc[sp] = s.cc0[sp]; s.cs[sp] = 0; }
-              }
-            }
-          }
-        } else {
-          s.sigcg[cgblk] = 1;
-        }
-      }
+  // ---- B. reverse-scan decisions (wave-uniform) ----
+  const uint32_t rice0 = (uint32_t)d.golomb_rice_stat / 4;
+  uint32_t rice = rice0, ctx_set = 0, c1_idx = 0, c2_idx = 0;
+  int c1 = 1, c2 = 0, last = -1, cg_last = -1;
+  double block_uncoded = 0, base_cost = 0;
+  const int sig_off = ch ? 28 : 0;
+  uint64_t sigmask = 0;  // coded_sub_block_flag by CG raster index
+  for (int cgp = NCG - 1; cgp >= 0; cgp--) {
+    const int cgblk = c.scan_cg[cgp];
+    const int cy = cgblk / c.wg, cx = cgblk - cy * c.wg;
+    int pattern = 0;
+    if (NCG > 1) {
+      const int rr = cx < c.wg - 1 ? (int)((sigmask >> (cgblk + 1)) & 1) : 0;
+      const int bb = cy < c.wg - 1 ? (int)((sigmask >> (cgblk + c.wg)) & 1) : 0;
+      pattern = rr + (bb << 1);
     }
-
-    int32_t abs_sum = 0;
-    if (last >= 0) {
-      double best_cost;
-      int best_p1 = 0;
-      if (!d.is_intra && ch == 0 && d.tr_idx == 0) {
-        best_cost = block_uncoded + rd_icost(r, (double)est->blockRootCbpBits[0][0]);
-        base_cost += rd_icost(r, (double)est->blockRootCbpBits[0][1]);
+    int ldv[16];
+#pragma unroll
+    for (int pin = 0; pin < 16; pin++) ldv[pin] = s.ld[cgp * 16 + pin];
+    int nnz0 = 0;
+    bool any = false;
+    double coded_ld = 0, uncoded = 0, sig_cost = 0, sig_cost0 = 0;
+    int o_lev = 0, o_csr = 0, o_st = 0;  // lane pin: results of scan position cgp*16 + pin
+    double o_cc = 0.0;
+#pragma unroll
+    for (int pin = 15; pin >= 0; pin--) {
+      const int sp = cgp * 16 + pin;
+      const int32_t ld = ldv[pin];
+      const uint32_t q = (uint32_t)((ld + (1 << (qbits - 1))) >> qbits);
+      const uint32_t max_abs = (uint32_t)ecmax < q ? (uint32_t)ecmax : q;
+      const double e = (double)ld;
+      const double cc0 = e * e * escale;
+      block_uncoded += cc0;
+      int32_t out = (int32_t)max_abs;
+      double cc = 0.0, cs = 0.0;
+      int csr = 0, stv = 0;
+      if (max_abs > 0 && last < 0) {
+        last = sp;
+        ctx_set = (comp ? 4 : 0) + ((comp == 0 && (sp >> 4) > 0) ? 2 : 0);
+        cg_last = cgp;
+      }
+      if (last >= 0) {
+        const int ctx_one = 4 * (int)ctx_set + c1, ctx_abs = (int)ctx_set + c2;
+        const int g0 = rl(t_g, ctx_one), g1 = rl(t_g, ctx_one + 32), a0 = rl(t_a, ctx_abs), a1 = rl(t_a, ctx_abs + 32);
+        const bool c1ok = c1_idx < 8, c2ok = c2_idx < 1;
+        // xGetCodedLevel (:2822)
+        const bool is_last = sp == last;
+        int ctx_sig = 0, sb0 = 0, sb1 = 0;
+        if (!is_last) {
+          ctx_sig = sig_off + rd_sig_ctx<L>(pattern, c, sp, ch);
+          sb0 = rl(t_sb0, ctx_sig);
+          sb1 = rl(t_sb1, ctx_sig);
+        }
+        double cur_sig = 0, cost, cost_sig = 0;
+        int cs_rate = 0;
+        uint32_t best = 0;
+        bool done = false;
+        if (!is_last && max_abs < 3) {
+          cost_sig = lambda * (double)sb0;
+          cs_rate = sb0;
+          cost = cc0 + cost_sig;
+          if (max_abs == 0) done = true;
+        } else {
+          cost = 1.7e+308;
+        }
+        if (!done) {
+          if (!is_last) cur_sig = lambda * (double)sb1;
+          const uint32_t min_abs = max_abs > 1 ? max_abs - 1 : 1;
+          for (int lv = (int)max_abs; lv >= (int)min_abs; lv--) {
+            const double err = (double)sub32(ld, shl32(lv, qbits));
+            double cl = err * err * escale +
+                        lambda * (double)rd_ic_rate((uint32_t)lv, (int)rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2);
+            cl += cur_sig;
+            if (cl < cost) { best = (uint32_t)lv; cost = cl; cost_sig = cur_sig; cs_rate = is_last ? 0 : sb1; }
+          }
+        }
+        cc = cost;
+        cs = cost_sig;
+        csr = cs_rate;
+        const uint32_t level = best;
+        stv = rd_pack(ctx_one, ctx_abs, (int)rice, c1ok, c2ok, !is_last, ctx_sig);
+        out = (int32_t)level;
+        base_cost += cc;
+        const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
+        if (level >= base && level > 3u * (1u << rice)) rice = d.persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
+        if (level >= 1) c1_idx++;
+        if (level > 1) { c1 = 0; c2 += (c2 < 2); c2_idx++; }
+        else if (c1 < 3 && c1 > 0 && level) c1++;
+        if (pin == 0 && sp > 0) {
+          ctx_set = (comp ? 4 : 0) + ((comp == 0 && ((sp - 1) >> 4) > 0) ? 2 : 0) + (c1 == 0 ? 1 : 0);
+          c1 = 1; c2 = 0; c1_idx = 0; c2_idx = 0;
+          rice = rice0;
+        }
       } else {
-        const int ctx = d.ctx_qt_cbf + (ch ? 5 : 0);
-        best_cost = block_uncoded + rd_icost(r, (double)est->blockCbpBits[ctx][0]);
-        base_cost += rd_icost(r, (double)est->blockCbpBits[ctx][1]);
+        base_cost += cc0;
       }
-      bool found = false;
-      for (int cgp = cg_last; cgp >= 0 && !found; cgp--) {
-        const int cgblk = c.scan_cg[cgp];
-        base_cost -= s.cgsig[cgp];
-        if (s.sigcg[cgblk]) {
-          for (int pin = 15; pin >= 0; pin--) {
-            const int sp = cgp * 16 + pin;
-            if (sp > last) continue;
-            const int blk = c.scan[sp];
-            if (s.lev[blk]) {
-              const int py = blk >> LOG2, px = blk - (py << LOG2);
-              const double cl = c.scan_type == 2 ? rd_rate_last(r, py, px, ch) : rd_rate_last(r, px, py, ch);
-              const double total = base_cost + cl - s.cs[sp];
-              if (total < best_cost) { best_p1 = sp + 1; best_cost = total; }
-              if (s.lev[blk] > 1) { found = true; break; }
-              base_cost -= s.cc[sp];
-              base_cost += s.cc0[sp];
-            } else {
-              base_cost -= s.cs[sp];
+      sig_cost += cs;
+      if (pin == 0) sig_cost0 = cs;
+      if (out) {
+        any = true;
+        coded_ld += cc - cs;
+        uncoded += cc0;
+        if (pin != 0) nnz0++;
+      }
+      if (lane == pin) { o_lev = out; o_cc = cc; o_csr = csr; o_st = stv; }
+    }
+    if (any) sigmask |= 1ull << cgblk;
+    int cgrate = 0;
+    if (cg_last >= 0) {
+      if (cgp) {
+        const int rr = cx < c.wg - 1 ? (int)((sigmask >> (cgblk + 1)) & 1) : 0;
+        const int bb = cy < c.wg - 1 ? (int)((sigmask >> (cgblk + c.wg)) & 1) : 0;
+        const int ctx = (rr + bb) != 0;
+        const int r0 = est->significantCoeffGroupBits[ctx][0], r1 = est->significantCoeffGroupBits[ctx][1];
+        if (!any) {
+          base_cost += lambda * (double)r0 - sig_cost;
+          cgrate = r0;
+        } else if (cgp < cg_last) {
+          if (nnz0 == 0) { base_cost -= sig_cost0; sig_cost -= sig_cost0; }
+          double zero_cost = base_cost;
+          base_cost += lambda * (double)r1;
+          zero_cost += lambda * (double)r0;
+          cgrate = r1;
+          zero_cost += uncoded;
+          zero_cost -= coded_ld;
+          zero_cost -= sig_cost;
+          if (zero_cost < base_cost) {
+            sigmask &= ~(1ull << cgblk);
+            base_cost = zero_cost;
+            cgrate = r0;
+            if (lane < 16 && o_lev) {
+              const double e = (double)s.ld[cgp * 16 + lane];
+              o_lev = 0; o_cc = e * e * escale; o_csr = 0;
             }
           }
         }
-      }
-      for (int sp = 0; sp < best_p1; sp++) {
-        const int blk = c.scan[sp];
-        const int32_t lv = s.lev[blk];
-        abs_sum += lv;
-        s.lev[blk] = s.coef[blk] < 0 ? -lv : lv;
-      }
-      for (int sp = best_p1; sp <= last; sp++) s.lev[c.scan[sp]] = 0;
-
-      if (d.sign_hiding && abs_sum >= 2) {
-        const double iq = (double)kInvQuantScales[d.qp_rem];
-        const int64_t rdf = (int64_t)(iq * iq * (1 << (2 * d.qp_per)) / d.lambda / 16 / (1 << 0) + 0.5);
-        int last_cg = -1;
-        for (int sub = (NN - 1) >> 4; sub >= 0; sub--) {
-          const int pos = sub << 4;
-          int first_nz = 16, last_nz = -1, abs_in = 0, k;
-          for (k = 15; k >= 0; k--) if (s.lev[c.scan[k + pos]]) { last_nz = k; break; }
-          for (k = 0; k < 16; k++) if (s.lev[c.scan[k + pos]]) { first_nz = k; break; }
-          for (k = first_nz; k <= last_nz; k++) abs_in += s.lev[c.scan[k + pos]];
-          if (last_nz >= 0 && last_cg == -1) last_cg = 1;
-          if (last_nz - first_nz >= 4) {
-            const uint32_t signbit = s.lev[c.scan[pos + first_nz]] > 0 ? 0 : 1;
-            if (signbit != (uint32_t)(abs_in & 1)) {
-              int64_t min_inc = INT64_MAX, cur = INT64_MAX;
-              int min_pos = -1, fch = 0, cch = 0;
-              for (k = (last_cg == 1 ? last_nz : 15); k >= 0; k--) {
-                const int blk = c.scan[k + pos];
-                const int32_t lv = s.lev[blk];
-                if (lv != 0) {
-                  const int64_t up = rdf * (-s.du[blk]) + s.rup[blk];
-                  int64_t down = rdf * (s.du[blk]) + s.rdown[blk] - ((abs(lv) == 1) ? s.sigd[blk] : 0);
-                  if (last_cg == 1 && last_nz == k && abs(lv) == 1) down -= (4 << 15);
-                  if (up < down) { cur = up; cch = 1; }
-                  else { cch = -1; cur = (k == first_nz && abs(lv) == 1) ? INT64_MAX : down; }
-                } else {
-                  cur = rdf * (-(abs(s.du[blk]))) + (1 << 15) + s.rup[blk] + s.sigd[blk];
-                  cch = 1;
-                  if (k < first_nz) {
-                    const uint32_t tsb = s.coef[blk] >= 0 ? 0 : 1;
-                    if (tsb != signbit) cur = INT64_MAX;
-                  }
-                }
-                if (cur < min_inc) { min_inc = cur; fch = cch; min_pos = blk; }
-              }
-              if (s.lev[min_pos] == ecmax || s.lev[min_pos] == ecmin) fch = -1;
-              if (s.coef[min_pos] >= 0) s.lev[min_pos] += fch;
-              else s.lev[min_pos] -= fch;
-            }
-          }
-          if (last_cg == 1) last_cg = 0;
-        }
+      } else {
+        sigmask |= 1ull << cgblk;
       }
     }
-    s.scal[0] = abs_sum;
+    if (lane < 16) {
+      const int sp = cgp * 16 + lane;
+      s.lev[c.scan[sp]] = o_lev;
+      s.cc[sp] = o_cc;
+      s.csr[sp] = o_csr;
+      st[sp] = o_st;
+    }
+    if (lane == 0) s.cgr[cgp] = cgrate;
   }
   __syncthreads();
-  return s.scal[0];
+
+  if (last < 0) return 0;  // every level is 0 (written above)
+
+  // ---- C. best last position (wave-uniform) ----
+  double best_cost;
+  int best_p1 = 0;
+  if (!d.is_intra && ch == 0 && d.tr_idx == 0) {
+    best_cost = block_uncoded + lambda * (double)est->blockRootCbpBits[0][0];
+    base_cost += lambda * (double)est->blockRootCbpBits[0][1];
+  } else {
+    const int ctx = d.ctx_qt_cbf + (ch ? 5 : 0);
+    best_cost = block_uncoded + lambda * (double)est->blockCbpBits[ctx][0];
+    base_cost += lambda * (double)est->blockCbpBits[ctx][1];
+  }
+  bool found = false;
+  for (int cgp = cg_last; cgp >= 0 && !found; cgp--) {
+    const int cgblk = c.scan_cg[cgp];
+    base_cost -= lambda * (double)s.cgr[cgp];
+    if ((sigmask >> cgblk) & 1) {
+      for (int pin = 15; pin >= 0; pin--) {
+        const int sp = cgp * 16 + pin;
+        if (sp > last) continue;
+        const int blk = c.scan[sp];
+        const int lvv = s.lev[blk];
+        if (lvv) {
+          const int py = blk >> LOG2, px = blk - (py << LOG2);
+          const double cl = c.scan_type == 2 ? rd_rate_last(est, lambda, py, px, ch) : rd_rate_last(est, lambda, px, py, ch);
+          const double total = base_cost + cl - lambda * (double)s.csr[sp];
+          if (total < best_cost) { best_p1 = sp + 1; best_cost = total; }
+          if (lvv > 1) { found = true; break; }
+          base_cost -= s.cc[sp];
+          const double e = (double)s.ld[sp];
+          base_cost += e * e * escale;
+        } else {
+          base_cost -= lambda * (double)s.csr[sp];
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- D. signs, zeroing past the chosen last position, uiAbsSum (lanes) ----
+  int part = 0;
+  for (int sp = lane; sp <= last; sp += HVX_WAVE) {
+    const int blk = c.scan[sp];
+    if (sp < best_p1) {
+      const int32_t lv = s.lev[blk];
+      part += lv;
+      s.lev[blk] = s.coef[blk] < 0 ? -lv : lv;
+    } else {
+      s.lev[blk] = 0;
+    }
+  }
+  const int32_t abs_sum = wave_sum_i32(part);
+  __syncthreads();
+
+  // ---- E. RD sign-bit hiding (:2541-2660): one coefficient group per lane ----
+  if (d.sign_hiding && abs_sum >= 2) {
+    const double iq = (double)kInvQuantScales[d.qp_rem];
+    const int64_t rdf = (int64_t)(iq * iq * (1 << (2 * d.qp_per)) / d.lambda / 16 / (1 << 0) + 0.5);
+    const int sub = lane, pos = sub << 4;
+    int first_nz = 16, last_nz = -1, abs_in = 0;
+    if (sub < NCG) {
+      for (int k = 15; k >= 0; k--) if (s.lev[c.scan[k + pos]]) { last_nz = k; break; }
+      for (int k = 0; k < 16; k++) if (s.lev[c.scan[k + pos]]) { first_nz = k; break; }
+      for (int k = first_nz; k <= last_nz; k++) abs_in += s.lev[c.scan[k + pos]];
+    }
+    // the highest group holding a level is the reference's lastCG
+    int top = last_nz >= 0 ? sub : -1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) top = max(top, __shfl_xor(top, o, HVX_WAVE));
+    if (sub < NCG && last_nz - first_nz >= 4) {
+      const uint32_t signbit = s.lev[c.scan[pos + first_nz]] > 0 ? 0 : 1;
+      if (signbit != (uint32_t)(abs_in & 1)) {
+        const bool is_top = sub == top;
+        int64_t min_inc = INT64_MAX, cur = INT64_MAX;
+        int min_pos = -1, fch = 0, cch = 0;
+        for (int k = (is_top ? last_nz : 15); k >= 0; k--) {
+          const int sp = k + pos;
+          const int blk = c.scan[sp];
+          const int32_t lv = s.lev[blk];
+          const uint32_t lev0 = (uint32_t)abs(lv);
+          const int32_t du = sub32(s.ld[sp], shl32((int32_t)lev0, qbits)) >> (qbits - 8);
+          const RdCtx x = rd_unpack(st[sp]);
+          const int g0 = est->greaterOneBits[x.ctx_one][0];
+          const int sigd = x.has_sig ? est->significantBits[x.ctx_sig][1] - est->significantBits[x.ctx_sig][0] : 0;
+          int rup = g0, rdown = 0;
+          if (lev0 > 0) {
+            const int g1 = est->greaterOneBits[x.ctx_one][1];
+            const int a0 = est->levelAbsBits[x.ctx_abs][0], a1 = est->levelAbsBits[x.ctx_abs][1];
+            const int now = rd_ic_rate(lev0, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2);
+            rup = rd_ic_rate(lev0 + 1, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2) - now;
+            rdown = rd_ic_rate(lev0 - 1, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2) - now;
+          }
+          if (lv != 0) {
+            const int64_t up = rdf * (-du) + rup;
+            int64_t down = rdf * (du) + rdown - ((abs(lv) == 1) ? sigd : 0);
+            if (is_top && last_nz == k && abs(lv) == 1) down -= (4 << 15);
+            if (up < down) { cur = up; cch = 1; }
+            else { cch = -1; cur = (k == first_nz && abs(lv) == 1) ? INT64_MAX : down; }
+          } else {
+            cur = rdf * (-(abs(du))) + (1 << 15) + rup + sigd;
+            cch = 1;
+            if (k < first_nz) {
+              const uint32_t tsb = s.coef[blk] >= 0 ? 0 : 1;
+              if (tsb != signbit) cur = INT64_MAX;
+            }
+          }
+          if (cur < min_inc) { min_inc = cur; fch = cch; min_pos = blk; }
+        }
+        if (s.lev[min_pos] == ecmax || s.lev[min_pos] == ecmin) fch = -1;
+        if (s.coef[min_pos] >= 0) s.lev[min_pos] += fch;
+        else s.lev[min_pos] -= fch;
+      }
+    }
+    __syncthreads();
+  }
+  return abs_sum;
 }
 
 // xQuant (:1126) non-RDOQ path + signBitHidingHDQ (:991).  Input s.coef, output s.lev.
@@ -477,7 +549,7 @@ __device__ int32_t tu_quant_plain(TuSmem<L> &s, const hvx_tu_desc &d, int32_t *a
     const int64_t t = (int64_t)abs(lv) * qc;
     if (arl_out) arl_out[i] = d.adaptive_qp_select ? (int32_t)((t + add_c) >> qbits_c) : 0;
     const int32_t qm = (int32_t)((t + add) >> qbits);
-    s.du[i] = (int32_t)((t - (int64_t)shl32(qm, qbits)) >> qbits8);
+    s.ld[i] = (int32_t)((t - (int64_t)shl32(qm, qbits)) >> qbits8);  // deltaU
     part += qm;
     s.lev[i] = clip3(ecmin, ecmax, qm * sign);
   }
@@ -502,15 +574,15 @@ __device__ int32_t tu_quant_plain(TuSmem<L> &s, const hvx_tu_desc &d, int32_t *a
             const int blk = c.scan[k + pos];
             const int32_t q = s.lev[blk];
             if (q != 0) {
-              if (s.du[blk] > 0) { cur = -s.du[blk]; cch = 1; }
+              if (s.ld[blk] > 0) { cur = -s.ld[blk]; cch = 1; }
               else if (k == first_nz && abs(q) == 1) cur = INT32_MAX;
-              else { cur = s.du[blk]; cch = -1; }
+              else { cur = s.ld[blk]; cch = -1; }
             } else if (k < first_nz) {
               const uint32_t tsb = s.coef[blk] >= 0 ? 0 : 1;
               if (tsb != signbit) cur = INT32_MAX;
-              else { cur = -s.du[blk]; cch = 1; }
+              else { cur = -s.ld[blk]; cch = 1; }
             } else {
-              cur = -s.du[blk]; cch = 1;
+              cur = -s.ld[blk]; cch = 1;
             }
             if (cur < min_inc) { min_inc = cur; fch = cch; min_pos = blk; }
           }
@@ -647,10 +719,10 @@ __global__ __launch_bounds__(64) void k_tu(const hvx_tu_desc *__restrict__ descs
   if (lane_id() == 0 && abs_out) abs_out[t] = abs_sum;
   if (MODE == 2) {
     __syncthreads();
-    tu_inverse<L>(s, d, s.lev, s.rdown);
+    tu_inverse<L>(s, d, s.lev, s.ld);
     uint32_t part = 0;
     for (int i = lane_id(); i < NN; i += HVX_WAVE) {
-      const int r = (int16_t)s.rdown[i];
+      const int r = (int16_t)s.ld[i];
       res_out[off + i] = (int16_t)r;
       const int df = (int)s.res[i] - r;
       part += (uint32_t)(df * df);
