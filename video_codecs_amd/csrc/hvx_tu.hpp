@@ -6,34 +6,26 @@
 // xDeQuant :1314, invTransformNxN :1547, xIT :1988, xTransformSkip :2021/:2070) and
 // TComRdCost::getDistPart SSE (TComRdCost.cpp:429).
 //
-// Mapping: one 64-lane wave (one workgroup) per TU, templated on the TU size so the LDS
-// image is sized exactly (4x4: ~1 KB ... 32x32: ~62 KB).  The integer transforms are
-// LDS-tiled matrix products (partial butterflies compute the same exact integer sums; no
-// MFMA -- small integer transforms).  The two stages are laid out so that every LDS access
-// in the inner loops is either lane-consecutive or wave-uniform (broadcast): no bank
-// conflicts.  Quantisation / RDOQ per-coefficient work (scaled levels, uncoded costs,
-// candidate distortions) runs across the 64 lanes; the inherently serial RDOQ state
-// machine (c1/c2/Rice/context-set carry in reverse scan order, CG zero-out, last-position
-// search, RD sign hiding) runs on lane 0 over the LDS image in the reference's exact
-// operation order, in double precision (the build uses -ffp-contract=off), so the
-// decisions are bit-identical.
+// Mapping: one 64-lane wave (one workgroup) per TU, templated on the TU size.  The LDS
+// image is three int32 planes of the TU (12 KB at 32x32) so that several TUs stay resident
+// per SIMD to hide the latency of RDOQ's serial part:
+//   a    : residual -> (RDOQ) context state per scan position -> dequantised coefficients
+//   coef : transform output -> inverse-transform scratch
+//   lev  : forward-transform scratch -> levels -> reconstructed residual
+// The integer transforms are matrix products over LDS (partial butterflies compute the same
+// exact integer sums; small integer transforms, no MFMA) with the DCT/DST matrix read from
+// the constant table; every LDS access in the inner loops is lane-consecutive or
+// wave-uniform (broadcast).  RDOQ: see tu_rdoq.
 #pragma once
 #include "hvx_dev.hpp"
 
 template <int L>
 struct TuSmem {
   static constexpr int N = 4 << L, NN = N * N, NCG = NN / 16;
-  int16_t mt[NN];     // transform matrix, transposed: mt[x*N + k] = M[k][x]
-  int16_t m[NN];      // transform matrix: m[k*N + x]
-  int16_t res[NN];    // input residual (kept for the pipeline SSE)
-  int32_t a[NN];      // residual (int) / dequantised coefficients; RDOQ: context state per scan position
-  int32_t coef[NN];   // transform output (raster)
-  int32_t lev[NN];    // levels (raster)
-  int32_t ld[NN];     // RDOQ lLevelDouble per scan position; plain quant: deltaU; pipeline: reconstruction
-  int32_t csr[NN];    // RDOQ significance-flag rate of the chosen cost per scan position; IT scratch
-  double cc[NN];      // RDOQ cost of the chosen level per scan position
-  int32_t cgr[NCG];   // RDOQ coded-group flag rate per CG scan position
-  int32_t scal[4];
+  int32_t a[NN];
+  int32_t coef[NN];
+  int32_t lev[NN];
+  int32_t cgr[NCG];  // RDOQ coded-group flag rate per CG scan position
 };
 
 struct TuCoding {
@@ -67,29 +59,26 @@ __device__ __forceinline__ TuCoding tu_coding(const hvx_tu_desc &d) {
 }
 
 // ----------------------------------------------------------------------------------- transforms
+// M[k][x] of the TU's transform (the 4x4 DST for intra luma 4x4)
 template <int L>
-__device__ void tu_load_matrix(TuSmem<L> &s, bool dst) {
-  constexpr int N = 4 << L, NN = N * N;
-  for (int i = lane_id(); i < NN; i += HVX_WAVE) {
-    const int k = i / N, x = i % N;
-    const int v = dst ? kDst4[i] : kMat[mat_base(L) + i];
-    s.m[i] = (int16_t)v;
-    s.mt[x * N + k] = (int16_t)v;
-  }
+__device__ __forceinline__ int tu_mat(bool dst, int k, int x) {
+  constexpr int N = 4 << L;
+  if (L == 0 && dst) return kDst4[k * 4 + x];
+  return kMat[mat_base(L) + k * N + x];
 }
 
-// xTrMxN (:860): in s.a (int residual), out s.coef
+// xTrMxN (:860): in s.a (int residual), out s.coef; s.lev is scratch
 template <int L>
-__device__ void tu_forward_transform(TuSmem<L> &s) {
+__device__ void tu_forward_transform(TuSmem<L> &s, bool dst) {
   constexpr int N = 4 << L, NN = N * N, LOG2 = L + 2;
   const int s1 = LOG2 - 1, s2 = LOG2 + 6;
   const int a1 = s1 > 0 ? 1 << (s1 - 1) : 0, a2 = 1 << (s2 - 1);
-  int32_t *tmpT = s.lev;  // scratch: tmpT[y*N + u]
+  int32_t *tmpT = s.lev;  // tmpT[y*N + u]
   for (int i = lane_id(); i < NN; i += HVX_WAVE) {
     const int y = i / N, u = i % N;
     int acc = 0;
 #pragma unroll 8
-    for (int x = 0; x < N; x++) acc += s.mt[x * N + u] * s.a[y * N + x];
+    for (int x = 0; x < N; x++) acc += tu_mat<L>(dst, u, x) * s.a[y * N + x];
     tmpT[y * N + u] = (acc + a1) >> s1;
   }
   __syncthreads();
@@ -97,22 +86,21 @@ __device__ void tu_forward_transform(TuSmem<L> &s) {
     const int v = i / N, u = i % N;
     int acc = 0;
 #pragma unroll 8
-    for (int y = 0; y < N; y++) acc += s.m[v * N + y] * tmpT[y * N + u];
+    for (int y = 0; y < N; y++) acc += tu_mat<L>(dst, v, y) * tmpT[y * N + u];
     s.coef[v * N + u] = (acc + a2) >> s2;
   }
   __syncthreads();
 }
 
-// xITrMxN (:927): in `in` (dequantised, raster), out int16 residual (stride N) in s.res? no: `out`
+// xITrMxN (:927): in (dequantised, raster) -> out (clipped to Pel range); tmp is scratch
 template <int L>
-__device__ void tu_inverse_transform(TuSmem<L> &s, const int32_t *in, int32_t *out) {
+__device__ void tu_inverse_transform(bool dst, const int32_t *in, int32_t *tmp, int32_t *out) {
   constexpr int N = 4 << L, NN = N * N;
-  int32_t *tmp = s.csr;  // scratch: tmp[y*N + u]
   for (int i = lane_id(); i < NN; i += HVX_WAVE) {
     const int y = i / N, u = i % N;
     int acc = 0;
 #pragma unroll 8
-    for (int v = 0; v < N; v++) acc += s.m[v * N + y] * in[v * N + u];
+    for (int v = 0; v < N; v++) acc += tu_mat<L>(dst, v, y) * in[v * N + u];
     tmp[y * N + u] = clip3(-32768, 32767, (acc + 64) >> 7);
   }
   __syncthreads();
@@ -120,7 +108,7 @@ __device__ void tu_inverse_transform(TuSmem<L> &s, const int32_t *in, int32_t *o
     const int y = i / N, x = i % N;
     int acc = 0;
 #pragma unroll 8
-    for (int u = 0; u < N; u++) acc += s.m[u * N + x] * tmp[y * N + u];
+    for (int u = 0; u < N; u++) acc += tu_mat<L>(dst, u, x) * tmp[y * N + u];
     out[y * N + x] = clip3(-32768, 32767, (acc + 2048) >> 12);
   }
   __syncthreads();
@@ -145,9 +133,10 @@ __device__ __forceinline__ int rd_ic_rate(uint32_t level, int rice, bool c1ok, b
       const uint32_t sl = prefix == maxp ? (uint32_t)(max_log2 - rice) : prefix + 1;
       rate += (int)((3 + prefix + sl + rice) << 15);
     } else {
-      uint32_t len = rice;
-      symbol -= (3u << rice);
-      while (symbol >= (1u << len)) { symbol -= (1u << (len++)); }
+      // the reference's loop `while (symbol >= (1 << len)) symbol -= 1 << len++` from
+      // len = rice runs floor(log2((symbol >> rice) + 1)) times
+      const uint32_t v = ((symbol - (3u << rice)) >> rice) + 1;
+      const uint32_t len = (uint32_t)rice + (31u - (uint32_t)__clz(v));
       rate += (int)((3 + len + 1 - rice + len) << 15);
     }
     if (c1ok) {
@@ -199,20 +188,36 @@ __device__ __forceinline__ double rd_rate_last(const hvx_estbits *est, double la
 
 __device__ __forceinline__ int rl(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 
-// Context state of a scan position at its RDOQ decision, packed for the sign-hiding rate
-// deltas: ctx_one | ctx_abs<<5 | rice<<8 | c1ok<<13 | c2ok<<14 | has_sig<<15 | ctx_sig<<16
+// Per scan position, the RDOQ pass keeps one packed int in s.a:
+//   before the serial pass: the significance context under each of the 4 neighbour-CG
+//     patterns (6 bits each);
+//   after it: the context state of its decision -- ctx_one | ctx_abs<<5 | rice<<8 |
+//     c1ok<<13 | c2ok<<14 | has_sig<<15 | ctx_sig<<16 | sig_sel<<22, where sig_sel says
+//     which significance-flag rate its cost carried (0 none, 1 sig=0, 2 sig=1).
+// From it (and the level and lLevelDouble) every per-position quantity the later passes
+// need -- the chosen cost, the flag cost, the sign-hiding rate deltas -- is recomputed
+// with the same operations, hence bit-identically.
 struct RdCtx {
-  int ctx_one, ctx_abs, rice, ctx_sig;
+  int ctx_one, ctx_abs, rice, ctx_sig, sig_sel;
   bool c1ok, c2ok, has_sig;
 };
-__device__ __forceinline__ int rd_pack(int one, int abs_, int rice, bool c1ok, bool c2ok, bool has_sig, int sig) {
-  return one | (abs_ << 5) | (rice << 8) | ((int)c1ok << 13) | ((int)c2ok << 14) | ((int)has_sig << 15) | (sig << 16);
+__device__ __forceinline__ int rd_pack(int one, int abs_, int rice, bool c1ok, bool c2ok, bool has_sig, int sig,
+                                       int sel) {
+  return one | (abs_ << 5) | (rice << 8) | ((int)c1ok << 13) | ((int)c2ok << 14) | ((int)has_sig << 15) |
+         (sig << 16) | (sel << 22);
 }
 __device__ __forceinline__ RdCtx rd_unpack(int v) {
   RdCtx r;
   r.ctx_one = v & 31; r.ctx_abs = (v >> 5) & 7; r.rice = (v >> 8) & 31;
   r.c1ok = (v >> 13) & 1; r.c2ok = (v >> 14) & 1; r.has_sig = (v >> 15) & 1; r.ctx_sig = (v >> 16) & 63;
+  r.sig_sel = (v >> 22) & 3;
   return r;
+}
+
+// lLevelDouble (:2210) of a coefficient
+__device__ __forceinline__ int32_t rd_level_double(int32_t coef, int qc, int64_t lim) {
+  const int64_t t = (int64_t)abs(coef) * qc;
+  return (int32_t)(t < lim ? t : lim);
 }
 
 // xRateDistOptQuant (:2129-2671).  Input s.coef (raster); output s.lev (signed levels), returns uiAbsSum.
@@ -221,11 +226,12 @@ __device__ __forceinline__ RdCtx rd_unpack(int v) {
 // search) is inherently serial; it runs as WAVE-UNIFORM code: every lane executes the same
 // scalar control flow, the estBits tables it indexes with state-dependent contexts sit in
 // lane slices of four VGPRs and are fetched with v_readlane (no dependent memory loads),
-// each coefficient group's 16 inputs are loaded in one batch, and the 16 per-position
-// results are gathered into lanes 0..15 and stored once per group.  Double precision with
-// the reference's exact operation order (-ffp-contract=off) keeps every decision identical.
-// Sign hiding then runs one coefficient group per lane (groups are independent), with the
-// rate deltas recomputed from the packed context state of each position.
+// each coefficient group's 16 inputs are loaded in one batch (one per lane, read back by
+// v_readlane), and the 16 per-position results are gathered into lanes 0..15 and stored
+// once per group.  Double precision with the reference's exact operation order
+// (-ffp-contract=off) keeps every decision identical.  Sign hiding then runs one
+// coefficient group per lane (groups are independent), with the rate deltas recomputed
+// from the packed context state of each position.
 template <int L>
 __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits *est, int32_t *arl_out) {
   constexpr int N = 4 << L, NN = N * N, NCG = NN / 16, LOG2 = L + 2;
@@ -245,15 +251,17 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   const int64_t lim = (int64_t)2147483647 - ((int64_t)1 << (qbits - 1));
   const int qbits_c = qbits - 7, add_c = 1 << (qbits_c - 1);
   const int lane = lane_id();
-  int32_t *st = s.a;  // the residual copy is dead once the forward transform has run
+  const int sig_off = ch ? 28 : 0;
+  int32_t *st = s.a;  // the residual is dead once the forward transform has run
 
   // ---- A. per-coefficient work across lanes ----
   for (int sp = lane; sp < NN; sp += HVX_WAVE) {
     const int blk = c.scan[sp];
-    const int64_t t = (int64_t)abs(s.coef[blk]) * qc;
-    const int32_t ld = (int32_t)(t < lim ? t : lim);
-    s.ld[sp] = ld;
-    if (arl_out) arl_out[blk] = d.adaptive_qp_select ? (ld + add_c) >> qbits_c : 0;
+    if (arl_out) arl_out[blk] = d.adaptive_qp_select ? (rd_level_double(s.coef[blk], qc, lim) + add_c) >> qbits_c : 0;
+    int info = 0;
+#pragma unroll
+    for (int pat = 0; pat < 4; pat++) info |= (sig_off + rd_sig_ctx<L>(pat, c, sp, ch)) << (6 * pat);
+    st[sp] = info;
   }
   // estBits in lane slices: entry [ctx][0] in lane ctx, [ctx][1] in lane 32 + ctx (or own VGPR)
   const int t_sb0 = lane < 44 ? est->significantBits[lane][0] : 0;
@@ -267,7 +275,6 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   uint32_t rice = rice0, ctx_set = 0, c1_idx = 0, c2_idx = 0;
   int c1 = 1, c2 = 0, last = -1, cg_last = -1;
   double block_uncoded = 0, base_cost = 0;
-  const int sig_off = ch ? 28 : 0;
   uint64_t sigmask = 0;  // coded_sub_block_flag by CG raster index
   for (int cgp = NCG - 1; cgp >= 0; cgp--) {
     const int cgblk = c.scan_cg[cgp];
@@ -278,18 +285,18 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
       const int bb = cy < c.wg - 1 ? (int)((sigmask >> (cgblk + c.wg)) & 1) : 0;
       pattern = rr + (bb << 1);
     }
-    int ldv[16];
-#pragma unroll
-    for (int pin = 0; pin < 16; pin++) ldv[pin] = s.ld[cgp * 16 + pin];
+    // the group's 16 inputs, one per lane (read back with v_readlane)
+    const int myblk = c.scan[cgp * 16 + (lane & 15)];
+    const int ldl = rd_level_double(s.coef[myblk], qc, lim);
+    const int infl = st[cgp * 16 + (lane & 15)];
+    const int shp = 6 * pattern;
     int nnz0 = 0;
     bool any = false;
     double coded_ld = 0, uncoded = 0, sig_cost = 0, sig_cost0 = 0;
-    int o_lev = 0, o_csr = 0, o_st = 0;  // lane pin: results of scan position cgp*16 + pin
-    double o_cc = 0.0;
-#pragma unroll
+    int o_lev = 0, o_st = 0;  // lane pin: results of scan position cgp*16 + pin
     for (int pin = 15; pin >= 0; pin--) {
       const int sp = cgp * 16 + pin;
-      const int32_t ld = ldv[pin];
+      const int32_t ld = rl(ldl, pin);
       const uint32_t q = (uint32_t)((ld + (1 << (qbits - 1))) >> qbits);
       const uint32_t max_abs = (uint32_t)ecmax < q ? (uint32_t)ecmax : q;
       const double e = (double)ld;
@@ -297,7 +304,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
       block_uncoded += cc0;
       int32_t out = (int32_t)max_abs;
       double cc = 0.0, cs = 0.0;
-      int csr = 0, stv = 0;
+      int stv = 0;
       if (max_abs > 0 && last < 0) {
         last = sp;
         ctx_set = (comp ? 4 : 0) + ((comp == 0 && (sp >> 4) > 0) ? 2 : 0);
@@ -311,17 +318,17 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
         const bool is_last = sp == last;
         int ctx_sig = 0, sb0 = 0, sb1 = 0;
         if (!is_last) {
-          ctx_sig = sig_off + rd_sig_ctx<L>(pattern, c, sp, ch);
+          ctx_sig = (rl(infl, pin) >> shp) & 63;
           sb0 = rl(t_sb0, ctx_sig);
           sb1 = rl(t_sb1, ctx_sig);
         }
         double cur_sig = 0, cost, cost_sig = 0;
-        int cs_rate = 0;
+        int sel = 0;
         uint32_t best = 0;
         bool done = false;
         if (!is_last && max_abs < 3) {
           cost_sig = lambda * (double)sb0;
-          cs_rate = sb0;
+          sel = 1;
           cost = cc0 + cost_sig;
           if (max_abs == 0) done = true;
         } else {
@@ -335,14 +342,13 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
             double cl = err * err * escale +
                         lambda * (double)rd_ic_rate((uint32_t)lv, (int)rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2);
             cl += cur_sig;
-            if (cl < cost) { best = (uint32_t)lv; cost = cl; cost_sig = cur_sig; cs_rate = is_last ? 0 : sb1; }
+            if (cl < cost) { best = (uint32_t)lv; cost = cl; cost_sig = cur_sig; sel = is_last ? 0 : 2; }
           }
         }
         cc = cost;
         cs = cost_sig;
-        csr = cs_rate;
         const uint32_t level = best;
-        stv = rd_pack(ctx_one, ctx_abs, (int)rice, c1ok, c2ok, !is_last, ctx_sig);
+        stv = rd_pack(ctx_one, ctx_abs, (int)rice, c1ok, c2ok, !is_last, ctx_sig, sel);
         out = (int32_t)level;
         base_cost += cc;
         const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
@@ -366,7 +372,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
         uncoded += cc0;
         if (pin != 0) nnz0++;
       }
-      if (lane == pin) { o_lev = out; o_cc = cc; o_csr = csr; o_st = stv; }
+      if (lane == pin) { o_lev = out; o_st = stv; }
     }
     if (any) sigmask |= 1ull << cgblk;
     int cgrate = 0;
@@ -388,14 +394,11 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
           zero_cost += uncoded;
           zero_cost -= coded_ld;
           zero_cost -= sig_cost;
-          if (zero_cost < base_cost) {
+          if (zero_cost < base_cost) {  // the whole group is zeroed (its cost/flag entries are never read again)
             sigmask &= ~(1ull << cgblk);
             base_cost = zero_cost;
             cgrate = r0;
-            if (lane < 16 && o_lev) {
-              const double e = (double)s.ld[cgp * 16 + lane];
-              o_lev = 0; o_cc = e * e * escale; o_csr = 0;
-            }
+            o_lev = 0;
           }
         }
       } else {
@@ -403,11 +406,8 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
       }
     }
     if (lane < 16) {
-      const int sp = cgp * 16 + lane;
-      s.lev[c.scan[sp]] = o_lev;
-      s.cc[sp] = o_cc;
-      s.csr[sp] = o_csr;
-      st[sp] = o_st;
+      s.lev[myblk] = o_lev;
+      st[cgp * 16 + lane] = o_st;
     }
     if (lane == 0) s.cgr[cgp] = cgrate;
   }
@@ -436,17 +436,28 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
         if (sp > last) continue;
         const int blk = c.scan[sp];
         const int lvv = s.lev[blk];
+        const RdCtx x = rd_unpack(st[sp]);
+        // the flag cost this position's decision carried
+        const int sbr = x.sig_sel == 1 ? rl(t_sb0, x.ctx_sig) : x.sig_sel == 2 ? rl(t_sb1, x.ctx_sig) : 0;
+        const double cs = x.sig_sel ? lambda * (double)sbr : 0.0;
         if (lvv) {
           const int py = blk >> LOG2, px = blk - (py << LOG2);
           const double cl = c.scan_type == 2 ? rd_rate_last(est, lambda, py, px, ch) : rd_rate_last(est, lambda, px, py, ch);
-          const double total = base_cost + cl - lambda * (double)s.csr[sp];
+          const double total = base_cost + cl - cs;
           if (total < best_cost) { best_p1 = sp + 1; best_cost = total; }
           if (lvv > 1) { found = true; break; }
-          base_cost -= s.cc[sp];
-          const double e = (double)s.ld[sp];
+          // the cost of the chosen level 1, recomputed as the serial pass computed it
+          const int32_t ld = rd_level_double(s.coef[blk], qc, lim);
+          const double err = (double)sub32(ld, shl32(1, qbits));
+          const int rate = rd_ic_rate(1u, x.rice, x.c1ok, x.c2ok, rl(t_g, x.ctx_one), rl(t_g, x.ctx_one + 32),
+                                      rl(t_a, x.ctx_abs), rl(t_a, x.ctx_abs + 32), ext, max_log2);
+          double cc = err * err * escale + lambda * (double)rate;
+          cc += x.has_sig ? lambda * (double)rl(t_sb1, x.ctx_sig) : 0.0;
+          base_cost -= cc;
+          const double e = (double)ld;
           base_cost += e * e * escale;
         } else {
-          base_cost -= lambda * (double)s.csr[sp];
+          base_cost -= cs;
         }
       }
     }
@@ -493,8 +504,9 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
           const int sp = k + pos;
           const int blk = c.scan[sp];
           const int32_t lv = s.lev[blk];
-          const uint32_t lev0 = (uint32_t)abs(lv);
-          const int32_t du = sub32(s.ld[sp], shl32((int32_t)lev0, qbits)) >> (qbits - 8);
+          const uint32_t lev0 = (uint32_t)abs(lv);  // == the serial pass's level at every position scanned here
+          const int32_t ld = rd_level_double(s.coef[blk], qc, lim);
+          const int32_t du = sub32(ld, shl32((int32_t)lev0, qbits)) >> (qbits - 8);
           const RdCtx x = rd_unpack(st[sp]);
           const int g0 = est->greaterOneBits[x.ctx_one][0];
           const int sigd = x.has_sig ? est->significantBits[x.ctx_sig][1] - est->significantBits[x.ctx_sig][0] : 0;
@@ -532,7 +544,8 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   return abs_sum;
 }
 
-// xQuant (:1126) non-RDOQ path + signBitHidingHDQ (:991).  Input s.coef, output s.lev.
+// xQuant (:1126) non-RDOQ path + signBitHidingHDQ (:991).  Input s.coef, output s.lev;
+// deltaU is kept in s.a.
 template <int L>
 __device__ int32_t tu_quant_plain(TuSmem<L> &s, const hvx_tu_desc &d, int32_t *arl_out) {
   constexpr int NN = (4 << L) * (4 << L);
@@ -542,6 +555,7 @@ __device__ int32_t tu_quant_plain(TuSmem<L> &s, const hvx_tu_desc &d, int32_t *a
   const int add = (d.slice_type == 2 ? 171 : 85) << (qbits - 9);
   const int qbits8 = qbits - 8, qbits_c = qbits - 7, add_c = 1 << (qbits_c - 1);
   const int32_t ecmax = (1 << d.max_log2_tr_range) - 1, ecmin = -(1 << d.max_log2_tr_range);
+  int32_t *du = s.a;
   int part = 0;
   for (int i = lane_id(); i < NN; i += HVX_WAVE) {
     const int32_t lv = s.coef[i];
@@ -549,7 +563,7 @@ __device__ int32_t tu_quant_plain(TuSmem<L> &s, const hvx_tu_desc &d, int32_t *a
     const int64_t t = (int64_t)abs(lv) * qc;
     if (arl_out) arl_out[i] = d.adaptive_qp_select ? (int32_t)((t + add_c) >> qbits_c) : 0;
     const int32_t qm = (int32_t)((t + add) >> qbits);
-    s.ld[i] = (int32_t)((t - (int64_t)shl32(qm, qbits)) >> qbits8);  // deltaU
+    du[i] = (int32_t)((t - (int64_t)shl32(qm, qbits)) >> qbits8);
     part += qm;
     s.lev[i] = clip3(ecmin, ecmax, qm * sign);
   }
@@ -574,15 +588,15 @@ __device__ int32_t tu_quant_plain(TuSmem<L> &s, const hvx_tu_desc &d, int32_t *a
             const int blk = c.scan[k + pos];
             const int32_t q = s.lev[blk];
             if (q != 0) {
-              if (s.ld[blk] > 0) { cur = -s.ld[blk]; cch = 1; }
+              if (du[blk] > 0) { cur = -du[blk]; cch = 1; }
               else if (k == first_nz && abs(q) == 1) cur = INT32_MAX;
-              else { cur = s.ld[blk]; cch = -1; }
+              else { cur = du[blk]; cch = -1; }
             } else if (k < first_nz) {
               const uint32_t tsb = s.coef[blk] >= 0 ? 0 : 1;
               if (tsb != signbit) cur = INT32_MAX;
-              else { cur = -s.ld[blk]; cch = 1; }
+              else { cur = -du[blk]; cch = 1; }
             } else {
-              cur = -s.ld[blk]; cch = 1;
+              cur = -du[blk]; cch = 1;
             }
             if (cur < min_inc) { min_inc = cur; fch = cch; min_pos = blk; }
           }
@@ -598,29 +612,26 @@ __device__ int32_t tu_quant_plain(TuSmem<L> &s, const hvx_tu_desc &d, int32_t *a
   return abs_sum;
 }
 
-// transformNxN (:1460) on s.res (int16, raster N*N).  Leaves s.coef (transform output) and
-// s.lev (levels); returns uiAbsSum.
+// transformNxN (:1460) on s.a (the residual as int, raster N*N).  Leaves s.coef (transform
+// output) and s.lev (levels); returns uiAbsSum.
 template <int L>
 __device__ int32_t tu_forward(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits *est, int32_t *arl_out) {
   constexpr int N = 4 << L, NN = N * N;
   if (d.transquant_bypass) {
     int part = 0;
-    for (int i = lane_id(); i < NN; i += HVX_WAVE) { s.lev[i] = s.res[i]; s.coef[i] = s.res[i]; part += abs((int)s.res[i]); }
+    for (int i = lane_id(); i < NN; i += HVX_WAVE) { s.lev[i] = s.a[i]; s.coef[i] = s.a[i]; part += abs(s.a[i]); }
     __syncthreads();
     return wave_sum_i32(part);
   }
   if (d.transform_skip) {
     const int ts = tu_transform_shift(d);
     for (int i = lane_id(); i < NN; i += HVX_WAVE) {
-      const int32_t v = s.res[i];
+      const int32_t v = s.a[i];
       s.coef[i] = ts >= 0 ? shl32(v, ts) : (v + (1 << (-ts - 1))) >> -ts;
     }
     __syncthreads();
   } else {
-    tu_load_matrix<L>(s, d.use_dst && N == 4);
-    for (int i = lane_id(); i < NN; i += HVX_WAVE) s.a[i] = s.res[i];
-    __syncthreads();
-    tu_forward_transform<L>(s);
+    tu_forward_transform<L>(s, d.use_dst && N == 4);
   }
   const int use_rdoq = d.transform_skip ? d.use_rdoq_ts : d.use_rdoq;
   if (use_rdoq) {
@@ -645,12 +656,13 @@ __device__ int32_t tu_forward(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estb
   return tu_quant_plain<L>(s, d, arl_out);
 }
 
-// invTransformNxN (:1547) on levels `in` (raster) -> `out` (int32 raster, values fit Pel).
+// invTransformNxN (:1547) on the levels in s.lev (raster) -> reconstructed residual in s.lev
+// (values fit Pel); s.a and s.coef are scratch.
 template <int L>
-__device__ void tu_inverse(TuSmem<L> &s, const hvx_tu_desc &d, const int32_t *in, int32_t *out) {
+__device__ void tu_inverse(TuSmem<L> &s, const hvx_tu_desc &d) {
   constexpr int N = 4 << L, NN = N * N;
   if (d.transquant_bypass) {
-    for (int i = lane_id(); i < NN; i += HVX_WAVE) out[i] = (int16_t)in[i];
+    for (int i = lane_id(); i < NN; i += HVX_WAVE) s.lev[i] = (int16_t)s.lev[i];
     __syncthreads();
     return;
   }
@@ -664,7 +676,7 @@ __device__ void tu_inverse(TuSmem<L> &s, const hvx_tu_desc &d, const int32_t *in
   const int32_t imin = -(1 << (tib - 1)), imax = (1 << (tib - 1)) - 1;
   int32_t *deq = s.a;
   for (int i = lane_id(); i < NN; i += HVX_WAVE) {
-    const int32_t c = clip3(imin, imax, in[i]);
+    const int32_t c = clip3(imin, imax, s.lev[i]);
     const int32_t v = right > 0 ? (c * scale + (1 << (right - 1))) >> right : shl32(c * scale, -right);
     deq[i] = clip3(tmin, tmax, v);
   }
@@ -672,19 +684,15 @@ __device__ void tu_inverse(TuSmem<L> &s, const hvx_tu_desc &d, const int32_t *in
   if (d.transform_skip) {
     for (int i = lane_id(); i < NN; i += HVX_WAVE) {
       const int32_t v = deq[i];
-      out[i] = (int16_t)(ts >= 0 ? (v + (ts == 0 ? 0 : 1 << (ts - 1))) >> ts : shl32(v, -ts));
+      s.lev[i] = (int16_t)(ts >= 0 ? (v + (ts == 0 ? 0 : 1 << (ts - 1))) >> ts : shl32(v, -ts));
     }
     __syncthreads();
   } else {
-    tu_load_matrix<L>(s, d.use_dst && N == 4);
-    __syncthreads();
-    tu_inverse_transform<L>(s, deq, out);
-    for (int i = lane_id(); i < NN; i += HVX_WAVE) out[i] = (int16_t)out[i];
+    tu_inverse_transform<L>(d.use_dst && N == 4, deq, s.coef, s.lev);
+    for (int i = lane_id(); i < NN; i += HVX_WAVE) s.lev[i] = (int16_t)s.lev[i];
     __syncthreads();
   }
 }
-
-__device__ __forceinline__ int tu_class(const hvx_tu_desc &d) { return d.log2_size - 2; }
 
 // mode: 0 forward, 1 inverse, 2 pipeline
 template <int L, int MODE>
@@ -704,12 +712,12 @@ __global__ __launch_bounds__(64) void k_tu(const hvx_tu_desc *__restrict__ descs
   if (MODE == 1) {
     for (int i = lane_id(); i < NN; i += HVX_WAVE) s.lev[i] = lev_io[off + i];
     __syncthreads();
-    tu_inverse<L>(s, d, s.lev, s.coef);
-    for (int i = lane_id(); i < NN; i += HVX_WAVE) res_out[off + i] = (int16_t)s.coef[i];
+    tu_inverse<L>(s, d);
+    for (int i = lane_id(); i < NN; i += HVX_WAVE) res_out[off + i] = (int16_t)s.lev[i];
     return;
   }
   const hvx_estbits *e = est + (est_idx ? est_idx[t] : t);
-  for (int i = lane_id(); i < NN; i += HVX_WAVE) s.res[i] = res_in[off + i];
+  for (int i = lane_id(); i < NN; i += HVX_WAVE) s.a[i] = res_in[off + i];
   __syncthreads();
   const int32_t abs_sum = tu_forward<L>(s, d, e, arl_out ? arl_out + off : nullptr);
   for (int i = lane_id(); i < NN; i += HVX_WAVE) {
@@ -719,12 +727,12 @@ __global__ __launch_bounds__(64) void k_tu(const hvx_tu_desc *__restrict__ descs
   if (lane_id() == 0 && abs_out) abs_out[t] = abs_sum;
   if (MODE == 2) {
     __syncthreads();
-    tu_inverse<L>(s, d, s.lev, s.ld);
+    tu_inverse<L>(s, d);
     uint32_t part = 0;
     for (int i = lane_id(); i < NN; i += HVX_WAVE) {
-      const int r = (int16_t)s.ld[i];
+      const int r = (int16_t)s.lev[i];
       res_out[off + i] = (int16_t)r;
-      const int df = (int)s.res[i] - r;
+      const int df = (int)res_in[off + i] - r;
       part += (uint32_t)(df * df);
     }
     const uint32_t sse = wave_sum_u32(part);
