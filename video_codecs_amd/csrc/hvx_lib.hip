@@ -341,7 +341,7 @@ int hvx_me_batch(hvx_ctx *ctx, const uint8_t *const *d_cur_planes, const uint8_t
     return fail(HVX_E_INVALID, "hvx_me_batch: bad args");
   if (!n) return HVX_OK;
   hipLaunchKernelGGL(k_me_int, dim3(n), dim3(64), 0, ctx->stream, d_cur_planes, d_ref_planes, stride, d_jobs, n, d_out);
-  hipLaunchKernelGGL(k_me_frac<64>, dim3(n), dim3(64), 0, ctx->stream, d_cur_planes, d_ref_planes, stride, d_jobs, n, d_out);
+  hipLaunchKernelGGL(k_me_frac, dim3(n), dim3(256), 0, ctx->stream, d_cur_planes, d_ref_planes, stride, d_jobs, n, d_out);
   return launched("k_me");
 }
 
@@ -443,10 +443,10 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
   {
     const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
     const int nb = L.nctu * L.nref;
-    hipLaunchKernelGGL(k_me_frac_ctu<64>, dim3(nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 1, 0);
-    hipLaunchKernelGGL(k_me_frac_ctu<32>, dim3(4 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 4, 1);
-    hipLaunchKernelGGL(k_me_frac_ctu<16>, dim3(16 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 16, 5);
-    hipLaunchKernelGGL(k_me_frac_ctu<8>, dim3(64 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 64, 21);
+    hipLaunchKernelGGL((k_me_frac_ctu<64, 4>), dim3(nb), dim3(256), 0, st, cs, d_refs, stride, jobs, res, L.nref, 1, 0);
+    hipLaunchKernelGGL((k_me_frac_ctu<32, 2>), dim3(4 * nb), dim3(128), 0, st, cs, d_refs, stride, jobs, res, L.nref, 4, 1);
+    hipLaunchKernelGGL((k_me_frac_ctu<16, 1>), dim3(16 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 16, 5);
+    hipLaunchKernelGGL((k_me_frac_ctu<8, 1>), dim3(64 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 64, 21);
   }
   mark(ctx, 5);
   hipLaunchKernelGGL(k_ctu_pred_resid, dim3(L.nctu * HVX_CUS_PER_CTU), dim3(64), 0, st, L, P, d_cur, d_refs, stride,

@@ -388,23 +388,29 @@ __device__ __forceinline__ int me_qpel_sample(const uint8_t *ref, int sr, int x,
 __constant__ int8_t kRefH[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
 __constant__ int8_t kRefQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
 
-template <int S>
+// Fractional-search LDS image for blocks up to SxS, NW waves per job.  The phase planes use
+// a row stride of S+8 int16: an 8x8 tile row of 8 samples then covers 4 banks and the 8
+// rows of a tile land on disjoint banks (conflict-free cross-lane tiles).
+template <int S, int NW>
 struct MeFracSmem {
-  int16_t hp[3][(S + 8) * S];  // first-stage intermediates of the 3 horizontal phases, rows iy-4 ..
-  int16_t blk[S * S];          // candidate block (per-lane-tile SATD path)
+  static constexpr int HS = S + 8;
+  int16_t hp[3][(S + 8) * HS];  // first-stage intermediates of the 3 horizontal phases, rows iy-4 ..
+  uint8_t blk[NW][S * S];       // per-wave candidate block (per-lane-tile SATD path)
   uint8_t org[S * S];
+  uint32_t cost[9];
 };
 
 // one prediction sample of candidate column phase c at vertical quarter position qy
 // (relative to the integer MV row iy): the reference's second filter stage on hp[c]
-template <int S>
-__device__ __forceinline__ int me_frac_sample(const MeFracSmem<S> &sm, int c, int ry, int fy, int x, int y) {
+template <int S, int NW>
+__device__ __forceinline__ int me_frac_sample(const MeFracSmem<S, NW> &sm, int c, int ry, int fy, int x, int y) {
+  constexpr int HS = MeFracSmem<S, NW>::HS;
   const int16_t *h = sm.hp[c] + x;
-  if (!fy) return clip_pel((h[(ry + 4 + y) * S] + 8192 + 32) >> 6);
+  if (!fy) return clip_pel((h[(ry + 4 + y) * HS] + 8192 + 32) >> 6);
   int s = 0;
   const int r0 = ry + 1 + y;
 #pragma unroll
-  for (int t = 0; t < 8; t++) s += kLumaFilter[fy][t] * h[(r0 + t) * S];
+  for (int t = 0; t < 8; t++) s += kLumaFilter[fy][t] * h[(r0 + t) * HS];
   return clip_pel((s + (1 << 11) + (8192 << 6)) >> 12);
 }
 
@@ -423,17 +429,20 @@ __device__ __forceinline__ uint32_t had8_xlane(int v) {
 
 // xPatternRefinement (:808): the 9 candidates of one stage.  (qx0,qy0) = stage centre in
 // quarter-pel relative to the PU, step 2 (half) or 1 (quarter); (ix,iy) the integer MV.
-template <int S>
-__device__ uint32_t me_frac_stage(MeFracSmem<S> &sm, const hvx_me_job &j, const uint8_t *ref, int stride, int ix,
+// The NW waves of the job share the phase planes and take candidates i = wave, wave+NW, ...
+// GENERIC: any block shape up to SxS; otherwise square SxS blocks only (the CTU pass).
+template <int S, int NW, bool GENERIC>
+__device__ uint32_t me_frac_stage(MeFracSmem<S, NW> &sm, const hvx_me_job &j, const uint8_t *ref, int stride, int ix,
                                   int iy, int qx0, int qy0, int step, int scale, int mvx0, int mvy0, int &bi) {
-  const int w = j.w, h = j.h, lane = lane_id();
+  constexpr int HS = MeFracSmem<S, NW>::HS;
+  const int w = GENERIC ? j.w : S, h = GENERIC ? j.h : S, lane = lane_id(), wave = threadIdx.x >> 6;
   const bool had = (j.flags & HVX_ME_HADME) != 0;
   // 1. horizontal phases: column c at quarter x = qx0 + (c-1)*step
   __syncthreads();
   for (int c = 0; c < 3; c++) {
     const int qx = qx0 + (c - 1) * step, ox = qx >> 2, fx = qx & 3;
     const uint8_t *src = ref + (iy - 4) * stride + ox;
-    for (int k = lane; k < (h + 8) * w; k += HVX_WAVE) {
+    for (int k = threadIdx.x; k < (h + 8) * w; k += 64 * NW) {
       const int r = k / w, x = k - r * w;
       const uint8_t *p = src + r * stride + x;
       int v;
@@ -445,72 +454,81 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S> &sm, const hvx_me_job &j, const 
       } else {
         v = (p[0] << 6) - 8192;
       }
-      sm.hp[c][r * S + x] = (int16_t)v;
+      sm.hp[c][r * HS + x] = (int16_t)v;
     }
   }
   __syncthreads();
-  // 2. the 9 candidates, reference order, strict '<'
-  const bool xl = had && (w % 8 == 0) && (h % 8 == 0) && (w * h <= 1024);
+  // 2. the 9 candidates' costs (SATD or SAD + MV cost), spread over the waves
+  const bool xl = had && (!GENERIC || ((w % 8 == 0) && (h % 8 == 0))) && (w * h <= 1024);
   const int tw = w >> 3, nt = (w * h) >> 6;
-  uint32_t best = 0xFFFFFFFFu;
-  bi = 0;
-  for (int i = 0; i < 9; i++) {
+  for (int i = wave; i < 9; i += NW) {
     const int dx = step == 2 ? kRefH[i][0] : kRefQ[i][0], dy = step == 2 ? kRefH[i][1] : kRefQ[i][1];
     const int qy = qy0 + dy * step, ry = (qy >> 2) - iy, fy = qy & 3, c = dx + 1;
-    uint32_t d;
+    uint32_t d = 0;
     if (xl) {
-      d = 0;
       for (int t = 0; t < nt; t++) {
         const int x = ((t % tw) << 3) + (lane & 7), y = ((t / tw) << 3) + (lane >> 3);
         d += had8_xlane((int)sm.org[y * S + x] - me_frac_sample(sm, c, ry, fy, x, y));
       }
     } else if (had) {
-      for (int k = lane; k < w * h; k += HVX_WAVE) {
-        const int y = k / w, x = k - y * w;
-        sm.blk[y * S + x] = (int16_t)me_frac_sample(sm, c, ry, fy, x, y);
+      if (GENERIC || S * S > 1024) {
+        uint8_t *blk = sm.blk[wave];
+        for (int k = lane; k < w * h; k += HVX_WAVE) {
+          const int y = k / w, x = k - y * w;
+          blk[y * S + x] = (uint8_t)me_frac_sample(sm, c, ry, fy, x, y);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        d = wave_satd(sm.org, S, (const uint8_t *)blk, S, w, h);
       }
-      __syncthreads();
-      d = wave_satd(sm.org, S, sm.blk, S, w, h);
-      __syncthreads();
     } else {
-      uint32_t s = 0;
+      uint32_t sacc = 0;
       for (int k = lane; k < w * h; k += HVX_WAVE) {
         const int y = k / w, x = k - y * w;
-        s += (uint32_t)abs((int)sm.org[y * S + x] - me_frac_sample(sm, c, ry, fy, x, y));
+        sacc += (uint32_t)abs((int)sm.org[y * S + x] - me_frac_sample(sm, c, ry, fy, x, y));
       }
-      d = wave_sum_u32(s);
+      d = wave_sum_u32(sacc);
     }
     d += me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
+    if (lane == 0) sm.cost[i] = d;
+  }
+  __syncthreads();
+  // 3. reference order, strict '<'
+  uint32_t best = 0xFFFFFFFFu;
+  bi = 0;
+  for (int i = 0; i < 9; i++) {
+    const uint32_t d = sm.cost[i];
     if (d < best) { best = d; bi = i; }
   }
   return best;
 }
 
-template <int S>
+template <int S, int NW, bool GENERIC>
 __device__ void me_frac_job(const hvx_me_job &j, const uint8_t *const *__restrict__ cur_planes,
-                            const uint8_t *const *__restrict__ ref_planes, int stride, MeFracSmem<S> &sm,
+                            const uint8_t *const *__restrict__ ref_planes, int stride, MeFracSmem<S, NW> &sm,
                             hvx_me_result *out) {
   if (j.w <= 0 || j.h <= 0 || j.w > S || j.h > S) return;  // k_me_int wrote the empty result
+  if (!GENERIC && (j.w != S || j.h != S)) return;
   const int ix = out->mv_int_x, iy = out->mv_int_y;
   const uint32_t sad_int = out->sad_int;
   const uint8_t *cur = cur_planes[j.cur_idx] + j.pu_y * stride + j.pu_x;
-  for (int k = lane_id(); k < j.w * j.h; k += HVX_WAVE) {
+  for (int k = threadIdx.x; k < j.w * j.h; k += 64 * NW) {
     const int y = k / j.w, x = k - y * j.w;
     sm.org[y * S + x] = cur[y * stride + x];
   }
   const uint8_t *ref = ref_planes[j.ref_idx] + j.pu_y * stride + j.pu_x;
   // xPatternSearchFracDIF (:4240): half-pel around the integer MV, then quarter-pel
   int bh, bq;
-  me_frac_stage(sm, j, ref, stride, ix, iy, ix << 2, iy << 2, 2, 1, ix << 1, iy << 1, bh);
+  me_frac_stage<S, NW, GENERIC>(sm, j, ref, stride, ix, iy, ix << 2, iy << 2, 2, 1, ix << 1, iy << 1, bh);
   const int hx = kRefH[bh][0], hy = kRefH[bh][1];
   const int cqx = (ix << 2) + (hx << 1), cqy = (iy << 2) + (hy << 1);
-  const uint32_t cost = me_frac_stage(sm, j, ref, stride, ix, iy, cqx, cqy, 1, 0, cqx, cqy, bq);
+  const uint32_t cost = me_frac_stage<S, NW, GENERIC>(sm, j, ref, stride, ix, iy, cqx, cqy, 1, 0, cqx, cqy, bq);
   const int qx = kRefQ[bq][0], qy = kRefQ[bq][1];
   const int fmx = cqx + qx, fmy = cqy + qy;
   const uint32_t mv_bits = eg_bits(fmx - j.pred_x) + eg_bits(fmy - j.pred_y);
   const uint32_t bits = (uint32_t)j.bits_in + mv_bits;
   const uint32_t lam = j.lambda_motion;
-  if (lane_id() == 0) {
+  if (threadIdx.x == 0) {
     hvx_me_result r;
     r.mv_int_x = ix; r.mv_int_y = iy; r.sad_int = sad_int;
     r.half_x = hx; r.half_y = hy; r.qtr_x = qx; r.qtr_y = qy; r.cost_frac = cost;
@@ -520,24 +538,25 @@ __device__ void me_frac_job(const hvx_me_job &j, const uint8_t *const *__restric
   }
 }
 
-template <int S>
-__global__ __launch_bounds__(64) void k_me_frac(const uint8_t *const *__restrict__ cur_planes,
-                                               const uint8_t *const *__restrict__ ref_planes, int stride,
-                                               const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
-  __shared__ MeFracSmem<S> sm;
+// generic jobs (any PU shape up to 64x64), 4 waves per job
+__global__ __launch_bounds__(256) void k_me_frac(const uint8_t *const *__restrict__ cur_planes,
+                                                const uint8_t *const *__restrict__ ref_planes, int stride,
+                                                const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
+  __shared__ MeFracSmem<64, 4> sm;
   const int jid = blockIdx.x;
   if (jid >= n) return;
   const hvx_me_job j = jobs[jid];
-  me_frac_job<S>(j, cur_planes, ref_planes, stride, sm, out + jid);
+  me_frac_job<64, 4, true>(j, cur_planes, ref_planes, stride, sm, out + jid);
 }
 
-template <int S>
-__global__ __launch_bounds__(64) void k_me_frac_ctu(const uint8_t *const *__restrict__ cur_planes,
-                                                   const uint8_t *const *__restrict__ ref_planes, int stride,
-                                                   const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
-                                                   int nref, int ncu, int first) {
-  __shared__ MeFracSmem<S> sm;
+// CTU pass: square SxS jobs of one depth, NW waves per job
+template <int S, int NW>
+__global__ __launch_bounds__(64 * NW) void k_me_frac_ctu(const uint8_t *const *__restrict__ cur_planes,
+                                                        const uint8_t *const *__restrict__ ref_planes, int stride,
+                                                        const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
+                                                        int nref, int ncu, int first) {
+  __shared__ MeFracSmem<S, NW> sm;
   const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
   const hvx_me_job j = jobs[slot];
-  me_frac_job<S>(j, cur_planes, ref_planes, stride, sm, out + slot);
+  me_frac_job<S, NW, false>(j, cur_planes, ref_planes, stride, sm, out + slot);
 }
