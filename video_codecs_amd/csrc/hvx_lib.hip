@@ -435,8 +435,26 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
     // the depth's jobs are contiguous per CTU but interleaved across CTUs: launch over all CUs of
     // this depth via a per-depth view (blocks of other depths return at once)
     const int first = d == 0 ? 0 : d == 1 ? 1 : d == 2 ? 5 : 21;
-    hipLaunchKernelGGL(k_me_int_ctu, dim3(L.nctu * ncu * L.nref), dim3(64), 0, st, (const uint8_t *const *)cur_slot,
-                       d_refs, stride, jobs, res, L.nref, ncu, first);
+    const bool fen = (P.me_flags & HVX_ME_FEN) != 0;
+    const dim3 grid(L.nctu * ncu * L.nref);
+    const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
+    switch (d) {  // block size, FEN row subsampling and waves per job are compile-time per depth
+      case 0:
+        if (fen) hipLaunchKernelGGL((k_me_int_ctu<64, 1, 4>), grid, dim3(256), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+        else hipLaunchKernelGGL((k_me_int_ctu<64, 0, 4>), grid, dim3(256), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+        break;
+      case 1:
+        if (fen) hipLaunchKernelGGL((k_me_int_ctu<32, 1, 2>), grid, dim3(128), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+        else hipLaunchKernelGGL((k_me_int_ctu<32, 0, 2>), grid, dim3(128), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+        break;
+      case 2:
+        if (fen) hipLaunchKernelGGL((k_me_int_ctu<16, 1, 1>), grid, dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+        else hipLaunchKernelGGL((k_me_int_ctu<16, 0, 1>), grid, dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+        break;
+      default:  // 8x8: FEN never applies (rows <= 8)
+        hipLaunchKernelGGL((k_me_int_ctu<8, 0, 1>), grid, dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+        break;
+    }
   }
   // fractional refinement of every depth (only the integer MVs feed the next depth's jobs)
   mark(ctx, 4);

@@ -83,13 +83,13 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 // ======================================================================================
 // integer TZ search
 // ======================================================================================
-constexpr int kMeMaxList = 128;  // diamonds d = 1..256: 4 + 3*8 + 5*16 = 108 points
+constexpr int kMeMaxList = 256;  // diamonds d = 1..256: 4 + 3*8 + 5*16 = 108 points; raster passes <= 256
 
 struct MeInt {
-  const uint8_t *org;  // LDS, stride 64
+  const uint8_t *org;  // LDS, stride os (64 for the generic kernel, S for the CTU kernels)
   const uint8_t *ref;  // PU origin at MV (0,0) in the reference plane
   uint32_t *cost;      // LDS, cost of each point of the current candidate list
-  int sr, sub, rows, gw;
+  int sr, sub, rows, gw, os;
   uint32_t lam;
   int px, py;
   int best_x, best_y, best_dist, best_round, point_nr;
@@ -99,13 +99,13 @@ struct MeInt {
 struct MeCand { int x, y, pnr, dist; bool ok; };
 
 // SAD (before the FEN scale) of the block at (x,y) over row groups s, s+L, s+2L, ...
-// (group = 4 pixels of one sampled row)
+// (group = 4 pixels of one sampled row).  Runtime geometry (generic PU shapes).
 __device__ __forceinline__ uint32_t me_sad_part(const MeInt &m, int x, int y, int s, int L) {
   const int n = m.rows * m.gw;
   int r = s / m.gw, g = s - r * m.gw;
   const int dr = L / m.gw, dg = L - dr * m.gw;
   const uint8_t *base = m.ref + y * m.sr + x;
-  const int rs = m.sr << m.sub, os = 64 << m.sub;
+  const int rs = m.sr << m.sub, os = m.os << m.sub;
   uint32_t acc = 0;
   for (int i = s; i < n; i += L) {
     const uint32_t o = *(const uint32_t *)(m.org + r * os + 4 * g);
@@ -117,18 +117,59 @@ __device__ __forceinline__ uint32_t me_sad_part(const MeInt &m, int x, int y, in
   return acc;
 }
 
-// cost (SAD + MV cost, or ~0 for a point outside the range) of list points 0..n-1 -> m.cost
-template <typename F>
+// Same for a square SxS block with compile-time FEN shift and lanes-per-point 1<<SH: the
+// whole item loop unrolls, so every load of the candidate is in flight at once.
+template <int S, int SUB, int SH>
+__device__ __forceinline__ uint32_t me_sad_part_ct(const MeInt &m, int x, int y, int s) {
+  constexpr int GW = S / 4, ROWS = S >> SUB, NI = ROWS * GW, L = 1 << SH, PER = (NI + L - 1) / L;
+  const uint8_t *base = m.ref + y * m.sr + x;
+  constexpr int UNR = PER <= 4 ? PER : 4;  // bound the loads in flight (VGPRs)
+  uint32_t acc = 0;
+#pragma unroll UNR
+  for (int k = 0; k < PER; k++) {
+    const int idx = s + k * L;
+    if (NI % L == 0 || idx < NI) {
+      const int r = idx / GW, g = idx % GW;
+      const uint32_t o = *(const uint32_t *)(m.org + ((r << SUB) * S) + 4 * g);
+      acc = __builtin_amdgcn_sad_u8(o, ld4_any(base + (r << SUB) * m.sr + 4 * g), acc);
+    }
+  }
+  return acc;
+}
+
+// S == 0: runtime geometry
+template <int S, int SUB>
+__device__ __forceinline__ uint32_t me_sad_any(const MeInt &m, int x, int y, int s, int sh) {
+  if constexpr (S == 0) {
+    return me_sad_part(m, x, y, s, 1 << sh);
+  } else {
+    switch (sh) {
+      case 0: return me_sad_part_ct<S, SUB, 0>(m, x, y, s);
+      case 1: return me_sad_part_ct<S, SUB, 1>(m, x, y, s);
+      case 2: return me_sad_part_ct<S, SUB, 2>(m, x, y, s);
+      case 3: return me_sad_part_ct<S, SUB, 3>(m, x, y, s);
+      case 4: return me_sad_part_ct<S, SUB, 4>(m, x, y, s);
+      case 5: return me_sad_part_ct<S, SUB, 5>(m, x, y, s);
+      default: return me_sad_part_ct<S, SUB, 6>(m, x, y, s);
+    }
+  }
+}
+
+// cost (SAD + MV cost, or ~0 for a point outside the range) of list points 0..n-1 -> m.cost.
+// The NW waves of the job take equal contiguous shares of the list; inside a wave,
+// 64/2^ceil(log2 share) lanes work on each point.
+template <int S, int SUB, int NW, typename F>
 __device__ __forceinline__ void me_eval(MeInt &m, int n, F cand) {
-  const int lane = lane_id();
-  for (int base = 0; base < n; base += HVX_WAVE) {
-    const int cnt = min(HVX_WAVE, n - base);
+  const int lane = lane_id(), wave = NW > 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int per = (n + NW - 1) / NW, lo = wave * per, hi = min(n, lo + per);
+  for (int base = lo; base < hi; base += HVX_WAVE) {
+    const int cnt = min(HVX_WAVE, hi - base);
     const int sh = 6 - (cnt <= 1 ? 0 : 32 - __clz(cnt - 1)), L = 1 << sh;
     const int q = lane >> sh, s = lane & (L - 1);
     MeCand c;
     c.ok = false; c.x = c.y = 0;
     if (q < cnt) c = cand(base + q);
-    uint32_t acc = c.ok ? me_sad_part(m, c.x, c.y, s, L) : 0u;
+    uint32_t acc = c.ok ? me_sad_any<S, SUB>(m, c.x, c.y, s, sh) : 0u;
     for (int o = 1; o < L; o <<= 1) acc += __shfl_xor(acc, o, HVX_WAVE);
     if (s == 0 && q < cnt)
       m.cost[base + q] = c.ok ? (acc << m.sub) + me_mv_cost(m.lam, m.px, m.py, 2, c.x, c.y) : 0xFFFFFFFFu;
@@ -136,7 +177,8 @@ __device__ __forceinline__ void me_eval(MeInt &m, int n, F cand) {
   __syncthreads();
 }
 
-// xTZSearchHelp over list points [start, start+cnt) in order: first minimum, strict '<'
+// xTZSearchHelp over list points [start, start+cnt) in order: first minimum, strict '<'.
+// Every wave of the job reduces the same costs, so the search state stays identical in all.
 template <typename F>
 __device__ __forceinline__ void me_take(MeInt &m, int start, int cnt, F cand) {
   uint64_t key = ~0ull;
@@ -203,6 +245,7 @@ __constant__ int8_t kTwoPoint[8][2][2] = {{{-1, 0}, {0, -1}}, {{-1, -1}, {1, -1}
                                           {{-1, 1}, {-1, -1}}, {{1, -1}, {1, 1}}, {{-1, 0}, {0, 1}},
                                           {{-1, 1}, {1, 1}}, {{1, 0}, {0, 1}}};
 
+template <int S, int SUB, int NW>
 __device__ __forceinline__ void me_2point(MeInt &m, const MeRange &g) {
   const int pn = m.point_nr, bx = m.best_x, by = m.best_y;
   if (pn < 1 || pn > 8) return;  // unreachable: the reference asserts here
@@ -213,11 +256,12 @@ __device__ __forceinline__ void me_2point(MeInt &m, const MeRange &g) {
     c.pnr = 0; c.dist = 2; c.ok = me_in(g, dx, dy, c.x, c.y);
     return c;
   };
-  me_eval(m, 2, cand);
+  me_eval<S, SUB, NW>(m, 2, cand);
   me_take(m, 0, 2, cand);
 }
 
 // xTZSearch (:3881) for job j; returns with m.best_* = the integer result
+template <int S, int SUB, int NW>
 __device__ void me_tz(const hvx_me_job &j, MeInt &m) {
   const int sr = j.search_range;
   const MeRange g0 = me_search_range(j, j.pred_x, j.pred_y, sr);
@@ -241,7 +285,7 @@ __device__ void me_tz(const hvx_me_job &j, MeInt &m) {
       return c;
     };
     const int n = j.use_int2nx2n ? 3 : 2;
-    me_eval(m, n, cand);
+    me_eval<S, SUB, NW>(m, n, cand);
     me_take(m, 0, n, cand);
   }
   const MeRange g = j.use_int2nx2n ? me_search_range(j, m.best_x << 2, m.best_y << 2, sr) : g0;
@@ -252,27 +296,27 @@ __device__ void me_tz(const hvx_me_job &j, MeInt &m) {
   {
     const int sx = m.best_x, sy = m.best_y;
     auto cand = [=](int p) { return me_dia_cand(g0, sx, sy, p); };
-    me_eval(m, ndp, cand);
+    me_eval<S, SUB, NW>(m, ndp, cand);
     for (int k = 0; k < nd; k++) {
       m.best_round += 1;
       me_take(m, me_dia_start(k), me_dia_start(k + 1) - me_dia_start(k), cand);
       if ((j.flags & HVX_ME_SMOOTHMV) && m.best_round >= 3) break;
     }
   }
-  if (m.best_dist == 1) { m.best_dist = 0; me_2point(m, g0); }
+  if (m.best_dist == 1) { m.best_dist = 0; me_2point<S, SUB, NW>(m, g0); }
   // raster (step 5) over the re-centred range
   if (m.best_dist > 5) {
     m.best_dist = 5;
     const int nx = (g.r - g.l) / 5 + 1, ny = (g.b - g.t) / 5 + 1, n = nx * ny;
-    for (int base = 0; base < n; base += HVX_WAVE) {
-      const int cnt = min(HVX_WAVE, n - base);
+    for (int base = 0; base < n; base += HVX_WAVE * NW) {
+      const int cnt = min(HVX_WAVE * NW, n - base);
       auto cand = [=](int p) {
         const int q = base + p, ry = q / nx, rx = q - ry * nx;
         MeCand c;
         c.x = g.l + 5 * rx; c.y = g.t + 5 * ry; c.pnr = 0; c.dist = 5; c.ok = true;
         return c;
       };
-      me_eval(m, cnt, cand);
+      me_eval<S, SUB, NW>(m, cnt, cand);
       me_take(m, 0, cnt, cand);
     }
   }
@@ -281,41 +325,48 @@ __device__ void me_tz(const hvx_me_job &j, MeInt &m) {
     const int sx = m.best_x, sy = m.best_y;
     m.best_dist = 0; m.point_nr = 0;
     auto cand = [=](int p) { return me_dia_cand(g0, sx, sy, p); };
-    me_eval(m, ndp, cand);
+    me_eval<S, SUB, NW>(m, ndp, cand);
     me_take(m, 0, ndp, cand);
     if (m.best_dist == 1) {
       m.best_dist = 0;
-      if (m.point_nr != 0) me_2point(m, g0);
+      if (m.point_nr != 0) me_2point<S, SUB, NW>(m, g0);
     }
   }
 }
 
+// S == 0: any PU shape (org stride 64, runtime FEN); otherwise square SxS with FEN shift SUB.
+template <int S, int SUB, int NW>
 __device__ __forceinline__ void me_int_job(const hvx_me_job &j, const uint8_t *const *__restrict__ cur_planes,
                                            const uint8_t *const *__restrict__ ref_planes, int stride, uint8_t *org,
                                            uint32_t *cost, hvx_me_result *out) {
   if (j.w <= 0 || j.h <= 0) {  // empty slot (e.g. a CU outside the picture): defined zero result
-    if (lane_id() == 0) { hvx_me_result z; memset(&z, 0, sizeof(z)); *out = z; }
+    if (threadIdx.x == 0) { hvx_me_result z; memset(&z, 0, sizeof(z)); *out = z; }
     return;
   }
+  constexpr int OS = S ? S : 64;
   const uint8_t *cur = cur_planes[j.cur_idx] + j.pu_y * stride + j.pu_x;
-  for (int k = lane_id(); k < j.w * j.h; k += HVX_WAVE) {
+  for (int k = threadIdx.x; k < j.w * j.h; k += HVX_WAVE * NW) {
     const int y = k / j.w, x = k - y * j.w;
-    org[y * 64 + x] = cur[y * stride + x];
+    org[y * OS + x] = cur[y * stride + x];
   }
   __syncthreads();
   MeInt m;
-  m.org = org; m.cost = cost;
+  m.org = org; m.cost = cost; m.os = OS;
   m.ref = ref_planes[j.ref_idx] + j.pu_y * stride + j.pu_x;
   m.sr = stride;
   const int w = j.w;
-  const bool spec = (w == 4 || w == 8 || w == 16 || w == 32 || w == 64 || w == 12 || w == 24 || w == 48);
-  m.sub = ((j.flags & HVX_ME_FEN) && j.h > 8 && spec) ? 1 : 0;
+  if (S) {
+    m.sub = SUB;
+  } else {
+    const bool spec = (w == 4 || w == 8 || w == 16 || w == 32 || w == 64 || w == 12 || w == 24 || w == 48);
+    m.sub = ((j.flags & HVX_ME_FEN) && j.h > 8 && spec) ? 1 : 0;
+  }
   m.rows = (j.h + (1 << m.sub) - 1) >> m.sub;
   m.gw = w >> 2;
   m.lam = j.lambda_motion;
   m.px = j.pred_x; m.py = j.pred_y;
-  me_tz(j, m);
-  if (lane_id() == 0) {
+  me_tz<S, SUB, NW>(j, m);
+  if (threadIdx.x == 0) {
     out->mv_int_x = m.best_x; out->mv_int_y = m.best_y;
     out->sad_int = m.best_sad - me_mv_cost(m.lam, m.px, m.py, 2, m.best_x, m.best_y);
   }
@@ -329,7 +380,7 @@ __global__ __launch_bounds__(64) void k_me_int(const uint8_t *const *__restrict_
   const int jid = blockIdx.x;
   if (jid >= n) return;
   const hvx_me_job j = jobs[jid];
-  me_int_job(j, cur_planes, ref_planes, stride, org, cost, out + jid);
+  me_int_job<0, 0, 1>(j, cur_planes, ref_planes, stride, org, cost, out + jid);
 }
 
 // CTU-pass view: block b = (ctu * ncu + cu) * nref + ref of one depth -> job slot
@@ -339,15 +390,18 @@ __device__ __forceinline__ size_t me_ctu_slot(int b, int nref, int ncu, int firs
   return ((size_t)ctu * HVX_CUS_PER_CTU + first + cu) * nref + ref;
 }
 
-__global__ __launch_bounds__(64) void k_me_int_ctu(const uint8_t *const *__restrict__ cur_planes,
-                                                  const uint8_t *const *__restrict__ ref_planes, int stride,
-                                                  const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
-                                                  int nref, int ncu, int first) {
-  __shared__ __attribute__((aligned(16))) uint8_t org[64 * 64];
+// CTU pass: square SxS jobs of one depth (FEN shift SUB decided on the host), NW waves per job
+template <int S, int SUB, int NW>
+__global__ __launch_bounds__(64 * NW) void k_me_int_ctu(const uint8_t *const *__restrict__ cur_planes,
+                                                       const uint8_t *const *__restrict__ ref_planes, int stride,
+                                                       const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
+                                                       int nref, int ncu, int first) {
+  __shared__ __attribute__((aligned(16))) uint8_t org[S * S];
   __shared__ uint32_t cost[kMeMaxList];
   const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
   const hvx_me_job j = jobs[slot];
-  me_int_job(j, cur_planes, ref_planes, stride, org, cost, out + slot);
+  if (j.w > 0 && (j.w != S || j.h != S)) return;  // not this depth's shape (cannot happen in the pass)
+  me_int_job<S, SUB, NW>(j, cur_planes, ref_planes, stride, org, cost, out + slot);
 }
 
 // ======================================================================================
