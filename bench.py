@@ -39,10 +39,57 @@ def parse():
     return p.parse_args()
 
 
+def b_ctu_luma(nref):
+    """SURVEY.md 8(d) algorithmic bytes per CTU, B = S(1 + N_ref + 1) + 2S + 16(64*64/16), with
+    S = 64*64 (the pass is luma-only): read the original and N_ref references once, write the
+    reconstruction, int16 levels and the 16 B-per-4x4 MV/mode field."""
+    S = 64 * 64
+    return S * (1 + nref + 1) + 2 * S + 16 * (64 * 64 // 16)
+
+
 def luma_plane(w, h, index):
     from oracle import make_yuv  # synthetic-input recipe (BASELINE.md section 3)
     y = make_yuv.random_frame(w, h, index)[: w * h].reshape(h, w)
     return np.pad(y, 80, mode="edge")
+
+
+def segment_frames(rank, nref):
+    """Frame indices of rank's independent GOP segment: nref references, then the current picture
+    (closed segments, one per GPU; no data-path collective)."""
+    base = rank * (nref + 1)
+    return list(range(base, base + nref + 1))
+
+
+def timed_steps(step, steps, warmup, world, device, sync, before=None):
+    """W untimed warmup steps, then EXACTLY `steps` steps bracketed by barrier + device sync on
+    both sides; returns the MAX elapsed seconds over ranks (all ranks receive it)."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    sync()
+    if before is not None:
+        before()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def aggregate(units_per_step, steps, world, elapsed):
+    """Whole-job throughput: the units ALL ranks processed / the max-over-ranks time."""
+    return units_per_step * steps * world / elapsed
 
 
 def main():
@@ -60,52 +107,44 @@ def main():
     from video_codecs_amd import _abi, hvx
 
     W, H, nref = args.width, args.height, args.nref
-    # independent GOP segment per rank: frames base .. base+nref (refs, then the current picture)
-    base = rank * (nref + 1)
-    planes = [luma_plane(W, H, base + i) for i in range(nref + 1)]
+    planes = [luma_plane(W, H, f) for f in segment_frames(rank, nref)]
     cur_t = torch.from_numpy(planes[nref]).cuda()
     ref_t = [torch.from_numpy(p).cuda() for p in planes[:nref]]
     ref_ptrs = torch.tensor([hvx.plane_origin_ptr(t, W) for t in ref_t], dtype=torch.int64).cuda()
     an = hvx.CtuAnalyzer(W, H, nref, args.qp)
     nctu = an.nctu
 
-    for _ in range(args.warmup):
-        an.run(cur_t, ref_ptrs)
-    torch.cuda.synchronize()
-    hvx.set_timing(True)
-    hvx.phase_times(reset=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        an.run(cur_t, ref_ptrs)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def before():
+        hvx.set_timing(True)
+        hvx.phase_times(reset=True)
+
+    elapsed = timed_steps(lambda: an.run(cur_t, ref_ptrs), args.steps, args.warmup, world, "cuda",
+                          torch.cuda.synchronize, before)
     phases = hvx.phase_times(reset=True)
     hvx.set_timing(False)
     gpu_res = an.results()
 
     if rank == 0:
-        ctus = nctu * args.steps * world
-        value = ctus / elapsed
-        # roofline of the dominant kernel: k_me_int_ctu (4 launches per step, one per CU depth)
-        me_ms_step = sum(phases[f"me_d{d}"] for d in range(4)) / args.steps
-        launch_ms = me_ms_step / 4.0
-        bytes_per_launch = nctu * 4096 * (1 + nref)  # each luma sample of cur + refs once
+        value = aggregate(nctu, args.steps, world, elapsed)
+        # roofline of the dominant kernel = the longest single launch of the step, timed with
+        # HIP events on the launch stream (hvx phase events bracket exactly one launch each here).
+        # Algorithmic bytes per launch = SURVEY 8(d)'s per-CTU figure (luma form, DESIGN.md
+        # "Roofline") x the CTUs one launch covers (every launch of the pass covers the picture).
+        single = {"k_tu<3,2>": "tu32", "k_tu<2,2>": "tu16", "k_tu<1,2>": "tu8", "k_ctu_pred_resid": "mc_resid",
+                  "k_me_int_ctu<64,1,4>": "me_d0", "k_me_int_ctu<32,1,2>": "me_d1",
+                  "k_me_int_ctu<16,1,1>": "me_d2", "k_me_int_ctu<8,0,1>": "me_d3"}
+        kernel = max(single, key=lambda k: phases[single[k]])
+        launch_ms = phases[single[kernel]] / args.steps
+        b_ctu = b_ctu_luma(nref)
+        bytes_per_launch = b_ctu * nctu
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         traffic = None
         tr_path = os.path.join(ROOT, "profiles", "hbm_traffic_r01.json")
         if os.path.exists(tr_path):
-            tr = json.load(open(tr_path)).get("k_me_int_ctu")
+            tr = json.load(open(tr_path)).get(kernel)
             if tr:
                 traffic = tr["bytes_per_launch"]
+        step_s = elapsed / args.steps
         out = {
             "metric": "64x64 CTUs/s (ME+transform+RDOQ) on 2160p YUV, 1->8 MI355X; bit-exact vs HM",
             "value": round(value, 2),
@@ -123,10 +162,12 @@ def main():
                        "resolution": f"{W}x{H}", "ctus_per_frame": nctu, "qp": args.qp, "search_range": 64,
                        "n_ref": nref, "parallelism": f"segments x{world}"},
             "phase_ms_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()},
-            "roofline": {"bound": "hbm", "kernel": "k_me_int_ctu", "achieved": round(achieved, 3),
+            "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 3),
                          "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / MI355X_HBM_PEAK_GBS,
                          "traffic": traffic, "bytes_per_launch": bytes_per_launch,
-                         "avg_launch_ms": round(launch_ms, 3)},
+                         "avg_launch_ms": round(launch_ms, 3), "b_ctu": b_ctu,
+                         "path_achieved_gbs": round(b_ctu * nctu / step_s / 1e9, 3),
+                         "path_frac": b_ctu * nctu / step_s / 1e9 / MI355X_HBM_PEAK_GBS},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu:

@@ -1,0 +1,83 @@
+"""The multi-rank path of bench.py on CPU: world_size-2 torch.distributed over gloo.
+
+bench.py shards the CTU analysis pass by independent GOP segments: each rank
+analyses its own frames, the timed region is bracketed by barriers on every rank, the time
+is the MAX over ranks and the value counts the units of ALL ranks.  Here the per-rank step is
+the CPU restatement of the same pass (oracle/hvx_oracle.c) on a small picture, so the
+orchestration (segment assignment, barrier + max-over-ranks timing, aggregation) is tested
+without a GPU.  The gloo rendezvous uses 127.0.0.1.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+W, H, NREF, QP, STEPS, WARMUP = 128, 64, 1, 32, 2, 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _analyze(planes):
+    import oracle
+    from video_codecs_amd import _abi
+    params = _abi.ctu_params(W, H, NREF, QP)
+    est = _abi.load_estbits_p_luma()
+    ncx, ncy = (W + 63) // 64, (H + 63) // 64
+    return np.stack([oracle.ctu_analyze(planes[NREF], planes[:NREF], params, est, c % ncx, c // ncx)
+                     for c in range(ncx * ncy)])
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    frames = bench.segment_frames(rank, NREF)
+    planes = [bench.luma_plane(W, H, f) for f in frames]
+    box = {}
+
+    def step():
+        box["res"] = _analyze(planes)
+
+    elapsed = bench.timed_steps(step, STEPS, WARMUP, world, "cpu", lambda: None)
+    nctu = box["res"].shape[0]
+    value = bench.aggregate(nctu, STEPS, world, elapsed)
+    np.save(os.path.join(outdir, f"res{rank}.npy"), box["res"].view(np.uint8))
+    np.save(os.path.join(outdir, f"meta{rank}.npy"), np.array([elapsed, value, nctu] + frames, dtype=np.float64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_segments_gloo(tmp_path):
+    import torch.multiprocessing as tmp
+    world = 2
+    tmp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    metas = [np.load(tmp_path / f"meta{r}.npy") for r in range(world)]
+    res = [np.load(tmp_path / f"res{r}.npy") for r in range(world)]
+    # max-over-ranks timing: every rank ends with the same elapsed and the same whole-job value
+    assert metas[0][0] == metas[1][0]
+    nctu = int(metas[0][2])
+    assert metas[0][1] == pytest.approx(nctu * STEPS * world / metas[0][0])
+    # disjoint segments: rank r analyses frames r*(nref+1) .. r*(nref+1)+nref
+    f0, f1 = [int(x) for x in metas[0][3:]], [int(x) for x in metas[1][3:]]
+    assert f0 == [0, 1] and f1 == [2, 3] and not set(f0) & set(f1)
+    assert res[0].tobytes() != res[1].tobytes()
+    # each rank's result is exactly the single-process result for its own segment
+    import bench
+    for r, frames in ((0, f0), (1, f1)):
+        exp = _analyze([bench.luma_plane(W, H, f) for f in frames])
+        assert res[r].tobytes() == exp.view(np.uint8).tobytes()
+
+
+def test_segment_and_aggregate_contract():
+    import bench
+    segs = [bench.segment_frames(r, 4) for r in range(8)]
+    flat = [f for s in segs for f in s]
+    assert len(flat) == len(set(flat)) == 40  # 8 closed, disjoint segments of nref+1 frames
+    assert bench.aggregate(2040, 10, 8, 2.0) == 2040 * 10 * 8 / 2.0
+    assert bench.b_ctu_luma(4) == 4096 * 6 + 2 * 4096 + 16 * 256
