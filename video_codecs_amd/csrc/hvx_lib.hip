@@ -28,6 +28,9 @@ struct hvx_ctx {
   // staging for the host-memory single-TU forms
   char *scratch = nullptr;
   char *pinned = nullptr;
+  // interleaved per-TU scratch of the batched TU pipeline (grown on demand)
+  char *tu_scr = nullptr;
+  size_t tu_scr_bytes = 0;
 };
 
 // staging layout (bytes): desc | est | off | residual (1024 int16) | levels | arl | abs | resout
@@ -44,7 +47,7 @@ struct hvx_ctx {
 namespace {
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 struct CtuWs {
-  size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, total;
+  size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, coefI, levI, stI, flags, total;
 };
 CtuWs ctu_ws_layout(const CtuLayout &L) {
   CtuWs w;
@@ -61,6 +64,10 @@ CtuWs ctu_ws_layout(const CtuLayout &L) {
   w.abs = o; o = align_up(o + ntu * sizeof(int32_t));
   w.sse = o; o = align_up(o + ntu * sizeof(uint32_t));
   w.ptr = o; o = align_up(o + 8 * sizeof(void *));
+  w.coefI = o; o = align_up(o + nres * sizeof(int32_t));
+  w.levI = o; o = align_up(o + nres * sizeof(int32_t));
+  w.stI = o; o = align_up(o + nres * sizeof(int32_t));
+  w.flags = o; o = align_up(o + ntu);
   w.total = o;
   return w;
 }
@@ -156,6 +163,51 @@ int upload_tables() {
 }
 }  // namespace
 
+// Batched TU pipeline (k_tu_fwd -> k_tu_rdoq -> k_tu_fin) for one size class over TUs
+// [0, n) of the arrays; G TUs per RDOQ wave; scratch arrays hold ceil(n/G)*G*NN words.
+template <int L, int MODE>
+static void tu_class_launch(hipStream_t st, const hvx_tu_desc *desc, const hvx_estbits *est, const int32_t *est_idx,
+                            const int64_t *off, int n, const int16_t *res_in, int32_t *temp, int32_t *lev, int32_t *arl,
+                            int32_t *abs_sum, int16_t *res_out, uint32_t *sse, int32_t *coefI, int32_t *levI,
+                            int32_t *stI, int8_t *flags, int G, int n_est_lds) {
+  hipLaunchKernelGGL((k_tu_fwd<L>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, temp, arl, coefI, levI, abs_sum, flags, G);
+  hipLaunchKernelGGL((k_tu_rdoq<L>), dim3((n + G - 1) / G), dim3(64), 0, st, desc, est, est_idx, n, coefI, levI, stI,
+                     abs_sum, flags, G, n_est_lds);
+  hipLaunchKernelGGL((k_tu_fin<L, MODE>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, levI, lev, res_out, sse, G);
+}
+
+// TUs per lane-parallel RDOQ wave: enough waves to fill the chip (~2 per SIMD), at most 64
+static int tu_group(int n) {
+  int g = 1;
+  while (g < 64 && (size_t)(g * 2) * 2048 <= (size_t)n) g *= 2;
+  return g;
+}
+
+template <int MODE>
+static int tu_batch(hvx_ctx *ctx, const hvx_tu_desc *desc, const hvx_estbits *est, const int32_t *est_idx,
+                    const int64_t *off, int n, const int16_t *res_in, int32_t *temp, int32_t *lev, int32_t *arl,
+                    int32_t *abs_sum, int16_t *res_out, uint32_t *sse) {
+  const int G = tu_group(n);
+  const size_t npad = (size_t)(n + G - 1) / G * G;
+  const size_t need = 3 * npad * 1024 * sizeof(int32_t) + npad + 256;
+  if (ctx->tu_scr_bytes < need) {
+    if (ctx->tu_scr) (void)hipFree(ctx->tu_scr);
+    ctx->tu_scr = nullptr;
+    ctx->tu_scr_bytes = 0;
+    HVX_HIP(hipMalloc(&ctx->tu_scr, need));
+    ctx->tu_scr_bytes = need;
+  }
+  int32_t *coefI = (int32_t *)ctx->tu_scr, *levI = coefI + npad * 1024, *stI = levI + npad * 1024;
+  int8_t *flags = (int8_t *)(stI + npad * 1024);
+  hipStream_t st = ctx->stream;
+  // one pipeline per size class; workgroups / lanes of TUs of another size exit at once
+  tu_class_launch<0, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, levI, stI, flags, G, 0);
+  tu_class_launch<1, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, levI, stI, flags, G, 0);
+  tu_class_launch<2, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, levI, stI, flags, G, 0);
+  tu_class_launch<3, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, levI, stI, flags, G, 0);
+  return launched("tu_batch");
+}
+
 template <int MODE>
 static int tu_launch(hvx_ctx *ctx, const hvx_tu_desc *desc, const hvx_estbits *est, const int32_t *est_idx,
                      const int64_t *off, int n, const int16_t *res_in, int32_t *temp, int32_t *lev, int32_t *arl,
@@ -194,6 +246,7 @@ int hvx_create(int device, hvx_ctx **out) {
 int hvx_destroy(hvx_ctx *ctx) {
   if (!ctx) return HVX_OK;
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->tu_scr) (void)hipFree(ctx->tu_scr);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   if (ctx->ev_ok)
@@ -237,7 +290,7 @@ int hvx_tu_forward_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const hvx_estb
   if (!ctx || n < 0 || (n && (!d_desc || !d_est || !d_off || !d_residual || !d_levels)))
     return fail(HVX_E_INVALID, "hvx_tu_forward_batch: bad args");
   if (!n) return HVX_OK;
-  return tu_launch<0>(ctx, d_desc, d_est, d_est_idx, d_off, n, d_residual, d_temp, d_levels, d_arl, d_abs_sum, nullptr, nullptr);
+  return tu_batch<0>(ctx, d_desc, d_est, d_est_idx, d_off, n, d_residual, d_temp, d_levels, d_arl, d_abs_sum, nullptr, nullptr);
 }
 
 int hvx_tu_inverse_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t *d_off, int n, const int32_t *d_levels,
@@ -255,8 +308,8 @@ int hvx_tu_pipeline_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const hvx_est
   if (!ctx || n < 0 || (n && (!d_desc || !d_est || !d_off || !d_residual || !d_levels || !d_residual_out)))
     return fail(HVX_E_INVALID, "hvx_tu_pipeline_batch: bad args");
   if (!n) return HVX_OK;
-  return tu_launch<2>(ctx, d_desc, d_est, d_est_idx, d_off, n, d_residual, nullptr, d_levels, nullptr, d_abs_sum,
-                      d_residual_out, d_sse);
+  return tu_batch<2>(ctx, d_desc, d_est, d_est_idx, d_off, n, d_residual, nullptr, d_levels, nullptr, d_abs_sum,
+                     d_residual_out, d_sse);
 }
 
 static int staging(hvx_ctx *ctx) {
@@ -471,14 +524,24 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
                      res, resid, desc, off, est_idx, d_out);
   const int n = L.nctu;
   mark(ctx, 6);
-  hipLaunchKernelGGL((k_tu<3, 2>), dim3(8 * n), dim3(64), 0, st, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev,
-                     nullptr, abs_sum, res_out, sse);
+  int32_t *coefI = (int32_t *)(ws + W.coefI), *levI = (int32_t *)(ws + W.levI), *stI = (int32_t *)(ws + W.stI);
+  int8_t *flags = (int8_t *)(ws + W.flags);
+  // size classes are contiguous: [0,8n) 32x32 | [8n,24n) 16x16 | [24n,88n) 8x8; scratch regions
+  // of 8n*1024, 16n*256 and 64n*64 words; 8/16/64 TUs per RDOQ wave (~2 waves per SIMD at 2160p)
+  tu_class_launch<3, 2>(st, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev, nullptr, abs_sum, res_out, sse,
+                        coefI, levI, stI, flags, 8, 4);
   mark(ctx, 7);
-  hipLaunchKernelGGL((k_tu<2, 2>), dim3(16 * n), dim3(64), 0, st, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n,
-                     16 * n, resid, nullptr, lev, nullptr, abs_sum + 8 * n, res_out, sse + 8 * n);
+  {
+    const size_t o = (size_t)8 * n * 1024;
+    tu_class_launch<2, 2>(st, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n, 16 * n, resid, nullptr, lev, nullptr,
+                          abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, levI + o, stI + o, flags + 8 * n, 16, 4);
+  }
   mark(ctx, 8);
-  hipLaunchKernelGGL((k_tu<1, 2>), dim3(64 * n), dim3(64), 0, st, desc + 24 * n, d_est4, est_idx + 24 * n, off + 24 * n,
-                     64 * n, resid, nullptr, lev, nullptr, abs_sum + 24 * n, res_out, sse + 24 * n);
+  {
+    const size_t o = (size_t)8 * n * 1024 + (size_t)16 * n * 256;
+    tu_class_launch<1, 2>(st, desc + 24 * n, d_est4, est_idx + 24 * n, off + 24 * n, 64 * n, resid, nullptr, lev, nullptr,
+                          abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, levI + o, stI + o, flags + 24 * n, 64, 4);
+  }
   mark(ctx, 9);
   hipLaunchKernelGGL(k_ctu_finalize, dim3((n * HVX_CUS_PER_CTU + 255) / 256), dim3(256), 0, st, L, abs_sum, sse, d_out);
   mark(ctx, 10);

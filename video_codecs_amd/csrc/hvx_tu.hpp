@@ -739,3 +739,450 @@ __global__ __launch_bounds__(64) void k_tu(const hvx_tu_desc *__restrict__ descs
     if (lane_id() == 0 && sse_out) sse_out[t] = sse;
   }
 }
+
+// =======================================================================================
+// Batched TU pipeline with lane-parallel RDOQ.
+//
+// The wave-uniform tu_rdoq above leaves 63 of 64 lanes idle and is bound by the SIMD's
+// scalar issue rate (one SALU instruction per 4 cycles, shared by the SIMD's waves).  For
+// batches, the serial xRateDistOptQuant instead runs ONE TU PER LANE: G TUs of a size class
+// advance through their reverse scans together, so every VALU instruction serves G TUs.
+// Three kernels per size class:
+//   k_tu_fwd  (wave per TU)  transform + the non-RDOQ quantisers; for RDOQ TUs the
+//                            coefficients go to an interleaved scan-order array
+//   k_tu_rdoq (lane per TU)  rdoq_lane: decisions, last position, sign hiding
+//   k_tu_fin  (wave per TU)  scan-order levels -> raster output, dequant + inverse + SSE
+// Per-TU scratch arrays are interleaved so that the G lanes of a wave touch G consecutive
+// words: element sp of TU t lives at ((t / G) * NN + sp) * G + t % G.
+// =======================================================================================
+__device__ __forceinline__ size_t tu_il(int t, int sp, int NN, int G) {
+  return ((size_t)(t / G) * NN + sp) * G + (t % G);
+}
+
+// xRateDistOptQuant (:2129-2671) for one TU by one lane.  coef/lev/st: the TU's interleaved
+// arrays (element sp at [sp * G]); coef in scan order; lev receives the signed final levels
+// in scan order; st the packed per-position context state (rd_pack).  Returns uiAbsSum.
+// Same operations, in the same order, as tu_rdoq and the reference.
+template <int L>
+__device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const int32_t *coef, int32_t *lev,
+                             int32_t *st, int G) {
+  constexpr int N = 4 << L, NN = N * N, NCG = NN / 16;
+  constexpr int LOG2 = L + 2;
+  const int ch = d.comp ? 1 : 0, comp = d.comp;
+  const int ts = tu_transform_shift(d);
+  const int qbits = 14 + d.qp_per + ts;
+  const int qc = kQuantScales[d.qp_rem];
+  const int ext = d.extended_precision, max_log2 = d.max_log2_tr_range;
+  const int32_t ecmax = (1 << max_log2) - 1, ecmin = -(1 << max_log2);
+  const int tsn = d.max_log2_tr_range - d.bit_depth - d.log2_size;
+  double escale = (double)(1 << 15);
+  escale = escale * ldexp(1.0, -2 * tsn);
+  escale = escale / qc / qc / (1 << 0);
+  const double lambda = d.lambda;
+  const TuCoding c = tu_coding<L>(d);
+  const int64_t lim = (int64_t)2147483647 - ((int64_t)1 << (qbits - 1));
+  const int sig_off = ch ? 28 : 0;
+
+  // ---- reverse-scan decisions ----
+  const uint32_t rice0 = (uint32_t)d.golomb_rice_stat / 4;
+  uint32_t rice = rice0, ctx_set = 0, c1_idx = 0, c2_idx = 0;
+  int c1 = 1, c2 = 0, last = -1, cg_last = -1;
+  double block_uncoded = 0, base_cost = 0;
+  uint64_t sigmask = 0;
+  for (int cgp = NCG - 1; cgp >= 0; cgp--) {
+    const int cgblk = c.scan_cg[cgp];
+    const int cy = cgblk / c.wg, cx = cgblk - cy * c.wg;
+    int pattern = 0;
+    if (NCG > 1) {
+      const int rr = cx < c.wg - 1 ? (int)((sigmask >> (cgblk + 1)) & 1) : 0;
+      const int bb = cy < c.wg - 1 ? (int)((sigmask >> (cgblk + c.wg)) & 1) : 0;
+      pattern = rr + (bb << 1);
+    }
+    int nnz0 = 0;
+    bool any = false;
+    double coded_ld = 0, uncoded = 0, sig_cost = 0, sig_cost0 = 0;
+    for (int pin = 15; pin >= 0; pin--) {
+      const int sp = cgp * 16 + pin;
+      const int32_t ld = rd_level_double(coef[(size_t)sp * G], qc, lim);
+      const uint32_t q = (uint32_t)((ld + (1 << (qbits - 1))) >> qbits);
+      const uint32_t max_abs = (uint32_t)ecmax < q ? (uint32_t)ecmax : q;
+      const double e = (double)ld;
+      const double cc0 = e * e * escale;
+      block_uncoded += cc0;
+      int32_t out = (int32_t)max_abs;
+      double cc = 0.0, cs = 0.0;
+      if (max_abs > 0 && last < 0) {
+        last = sp;
+        ctx_set = (comp ? 4 : 0) + ((comp == 0 && (sp >> 4) > 0) ? 2 : 0);
+        cg_last = cgp;
+      }
+      if (last >= 0) {
+        const int ctx_one = 4 * (int)ctx_set + c1, ctx_abs = (int)ctx_set + c2;
+        const int g0 = est->greaterOneBits[ctx_one][0], g1 = est->greaterOneBits[ctx_one][1];
+        const int a0 = est->levelAbsBits[ctx_abs][0], a1 = est->levelAbsBits[ctx_abs][1];
+        const bool c1ok = c1_idx < 8, c2ok = c2_idx < 1;
+        // xGetCodedLevel (:2822)
+        const bool is_last = sp == last;
+        int ctx_sig = 0, sb0 = 0, sb1 = 0;
+        if (!is_last) {
+          ctx_sig = sig_off + rd_sig_ctx<L>(pattern, c, sp, ch);
+          sb0 = est->significantBits[ctx_sig][0];
+          sb1 = est->significantBits[ctx_sig][1];
+        }
+        double cur_sig = 0, cost, cost_sig = 0;
+        int sel = 0;
+        uint32_t best = 0;
+        bool done = false;
+        if (!is_last && max_abs < 3) {
+          cost_sig = lambda * (double)sb0;
+          sel = 1;
+          cost = cc0 + cost_sig;
+          if (max_abs == 0) done = true;
+        } else {
+          cost = 1.7e+308;
+        }
+        if (!done) {
+          if (!is_last) cur_sig = lambda * (double)sb1;
+          const uint32_t min_abs = max_abs > 1 ? max_abs - 1 : 1;
+          for (int lv = (int)max_abs; lv >= (int)min_abs; lv--) {
+            const double err = (double)sub32(ld, shl32(lv, qbits));
+            double cl = err * err * escale +
+                        lambda * (double)rd_ic_rate((uint32_t)lv, (int)rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2);
+            cl += cur_sig;
+            if (cl < cost) { best = (uint32_t)lv; cost = cl; cost_sig = cur_sig; sel = is_last ? 0 : 2; }
+          }
+        }
+        cc = cost;
+        cs = cost_sig;
+        const uint32_t level = best;
+        st[(size_t)sp * G] = rd_pack(ctx_one, ctx_abs, (int)rice, c1ok, c2ok, !is_last, ctx_sig, sel);
+        out = (int32_t)level;
+        base_cost += cc;
+        const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
+        if (level >= base && level > 3u * (1u << rice)) rice = d.persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
+        if (level >= 1) c1_idx++;
+        if (level > 1) { c1 = 0; c2 += (c2 < 2); c2_idx++; }
+        else if (c1 < 3 && c1 > 0 && level) c1++;
+        if (pin == 0 && sp > 0) {
+          ctx_set = (comp ? 4 : 0) + ((comp == 0 && ((sp - 1) >> 4) > 0) ? 2 : 0) + (c1 == 0 ? 1 : 0);
+          c1 = 1; c2 = 0; c1_idx = 0; c2_idx = 0;
+          rice = rice0;
+        }
+      } else {
+        base_cost += cc0;
+      }
+      lev[(size_t)sp * G] = out;
+      sig_cost += cs;
+      if (pin == 0) sig_cost0 = cs;
+      if (out) {
+        any = true;
+        coded_ld += cc - cs;
+        uncoded += cc0;
+        if (pin != 0) nnz0++;
+      }
+    }
+    if (any) sigmask |= 1ull << cgblk;
+    if (cg_last >= 0) {
+      if (cgp) {
+        const int rr = cx < c.wg - 1 ? (int)((sigmask >> (cgblk + 1)) & 1) : 0;
+        const int bb = cy < c.wg - 1 ? (int)((sigmask >> (cgblk + c.wg)) & 1) : 0;
+        const int ctx = (rr + bb) != 0;
+        const int r0 = est->significantCoeffGroupBits[ctx][0], r1 = est->significantCoeffGroupBits[ctx][1];
+        if (!any) {
+          base_cost += lambda * (double)r0 - sig_cost;
+        } else if (cgp < cg_last) {
+          if (nnz0 == 0) { base_cost -= sig_cost0; sig_cost -= sig_cost0; }
+          double zero_cost = base_cost;
+          base_cost += lambda * (double)r1;
+          zero_cost += lambda * (double)r0;
+          zero_cost += uncoded;
+          zero_cost -= coded_ld;
+          zero_cost -= sig_cost;
+          if (zero_cost < base_cost) {
+            sigmask &= ~(1ull << cgblk);
+            base_cost = zero_cost;
+            for (int pin = 0; pin < 16; pin++) lev[(size_t)(cgp * 16 + pin) * G] = 0;
+          }
+        }
+      } else {
+        sigmask |= 1ull << cgblk;
+      }
+    }
+  }
+  if (last < 0) return 0;
+
+  // ---- best last position ----
+  double best_cost;
+  int best_p1 = 0;
+  if (!d.is_intra && ch == 0 && d.tr_idx == 0) {
+    best_cost = block_uncoded + lambda * (double)est->blockRootCbpBits[0][0];
+    base_cost += lambda * (double)est->blockRootCbpBits[0][1];
+  } else {
+    const int ctx = d.ctx_qt_cbf + (ch ? 5 : 0);
+    best_cost = block_uncoded + lambda * (double)est->blockCbpBits[ctx][0];
+    base_cost += lambda * (double)est->blockCbpBits[ctx][1];
+  }
+  bool found = false;
+  for (int cgp = cg_last; cgp >= 0 && !found; cgp--) {
+    const int cgblk = c.scan_cg[cgp];
+    // the coded-group flag rate the decision pass added for this group: 0 for the first
+    // and the last coded group, else the flag's final value under the right/below context
+    // (those neighbours were final before this group was decided)
+    int cgrate = 0;
+    if (cgp && cgp < cg_last) {
+      const int cy = cgblk / c.wg, cx = cgblk - cy * c.wg;
+      const int rr = cx < c.wg - 1 ? (int)((sigmask >> (cgblk + 1)) & 1) : 0;
+      const int bb = cy < c.wg - 1 ? (int)((sigmask >> (cgblk + c.wg)) & 1) : 0;
+      cgrate = est->significantCoeffGroupBits[(rr + bb) != 0][(sigmask >> cgblk) & 1];
+    }
+    base_cost -= lambda * (double)cgrate;
+    if ((sigmask >> cgblk) & 1) {
+      for (int pin = 15; pin >= 0; pin--) {
+        const int sp = cgp * 16 + pin;
+        if (sp > last) continue;
+        const int lvv = lev[(size_t)sp * G];
+        const RdCtx x = rd_unpack(st[(size_t)sp * G]);
+        const int sbr = x.sig_sel == 1 ? est->significantBits[x.ctx_sig][0]
+                                       : x.sig_sel == 2 ? est->significantBits[x.ctx_sig][1] : 0;
+        const double cs = x.sig_sel ? lambda * (double)sbr : 0.0;
+        if (lvv) {
+          const int blk = c.scan[sp];
+          const int py = blk >> LOG2, px = blk - (py << LOG2);
+          const double cl = c.scan_type == 2 ? rd_rate_last(est, lambda, py, px, ch) : rd_rate_last(est, lambda, px, py, ch);
+          const double total = base_cost + cl - cs;
+          if (total < best_cost) { best_p1 = sp + 1; best_cost = total; }
+          if (lvv > 1) { found = true; break; }
+          const int32_t ld = rd_level_double(coef[(size_t)sp * G], qc, lim);
+          const double err = (double)sub32(ld, shl32(1, qbits));
+          const int rate = rd_ic_rate(1u, x.rice, x.c1ok, x.c2ok, est->greaterOneBits[x.ctx_one][0],
+                                      est->greaterOneBits[x.ctx_one][1], est->levelAbsBits[x.ctx_abs][0],
+                                      est->levelAbsBits[x.ctx_abs][1], ext, max_log2);
+          double cc = err * err * escale + lambda * (double)rate;
+          cc += x.has_sig ? lambda * (double)est->significantBits[x.ctx_sig][1] : 0.0;
+          base_cost -= cc;
+          const double e = (double)ld;
+          base_cost += e * e * escale;
+        } else {
+          base_cost -= cs;
+        }
+      }
+    }
+  }
+
+  // ---- signs, zeroing past the chosen last position, uiAbsSum ----
+  int32_t abs_sum = 0;
+  for (int sp = 0; sp <= last; sp++) {
+    if (sp < best_p1) {
+      const int32_t lv = lev[(size_t)sp * G];
+      abs_sum += lv;
+      if (coef[(size_t)sp * G] < 0) lev[(size_t)sp * G] = -lv;
+    } else {
+      lev[(size_t)sp * G] = 0;
+    }
+  }
+
+  // ---- RD sign-bit hiding (:2541-2660), groups from the top ----
+  if (d.sign_hiding && abs_sum >= 2) {
+    const double iq = (double)kInvQuantScales[d.qp_rem];
+    const int64_t rdf = (int64_t)(iq * iq * (1 << (2 * d.qp_per)) / d.lambda / 16 / (1 << 0) + 0.5);
+    int last_cg = -1;
+    for (int sub = NCG - 1; sub >= 0; sub--) {
+      const int pos = sub << 4;
+      int first_nz = 16, last_nz = -1, abs_in = 0, k;
+      for (k = 15; k >= 0; k--) if (lev[(size_t)(k + pos) * G]) { last_nz = k; break; }
+      for (k = 0; k < 16; k++) if (lev[(size_t)(k + pos) * G]) { first_nz = k; break; }
+      for (k = first_nz; k <= last_nz; k++) abs_in += lev[(size_t)(k + pos) * G];
+      if (last_nz >= 0 && last_cg == -1) last_cg = 1;
+      if (last_nz - first_nz >= 4) {
+        const uint32_t signbit = lev[(size_t)(pos + first_nz) * G] > 0 ? 0 : 1;
+        if (signbit != (uint32_t)(abs_in & 1)) {
+          int64_t min_inc = INT64_MAX, cur = INT64_MAX;
+          int min_sp = -1, fch = 0, cch = 0;
+          for (k = (last_cg == 1 ? last_nz : 15); k >= 0; k--) {
+            const int sp = k + pos;
+            const int32_t lv = lev[(size_t)sp * G];
+            const uint32_t lev0 = (uint32_t)abs(lv);
+            const int32_t ld = rd_level_double(coef[(size_t)sp * G], qc, lim);
+            const int32_t du = sub32(ld, shl32((int32_t)lev0, qbits)) >> (qbits - 8);
+            const RdCtx x = rd_unpack(st[(size_t)sp * G]);
+            const int g0 = est->greaterOneBits[x.ctx_one][0];
+            const int sigd = x.has_sig ? est->significantBits[x.ctx_sig][1] - est->significantBits[x.ctx_sig][0] : 0;
+            int rup = g0, rdown = 0;
+            if (lev0 > 0) {
+              const int g1 = est->greaterOneBits[x.ctx_one][1];
+              const int a0 = est->levelAbsBits[x.ctx_abs][0], a1 = est->levelAbsBits[x.ctx_abs][1];
+              const int now = rd_ic_rate(lev0, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2);
+              rup = rd_ic_rate(lev0 + 1, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2) - now;
+              rdown = rd_ic_rate(lev0 - 1, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2) - now;
+            }
+            if (lv != 0) {
+              const int64_t up = rdf * (-du) + rup;
+              int64_t down = rdf * (du) + rdown - ((abs(lv) == 1) ? sigd : 0);
+              if (last_cg == 1 && last_nz == k && abs(lv) == 1) down -= (4 << 15);
+              if (up < down) { cur = up; cch = 1; }
+              else { cch = -1; cur = (k == first_nz && abs(lv) == 1) ? INT64_MAX : down; }
+            } else {
+              cur = rdf * (-(abs(du))) + (1 << 15) + rup + sigd;
+              cch = 1;
+              if (k < first_nz) {
+                const uint32_t tsb = coef[(size_t)sp * G] >= 0 ? 0 : 1;
+                if (tsb != signbit) cur = INT64_MAX;
+              }
+            }
+            if (cur < min_inc) { min_inc = cur; fch = cch; min_sp = sp; }
+          }
+          int32_t &m = lev[(size_t)min_sp * G];
+          if (m == ecmax || m == ecmin) fch = -1;
+          if (coef[(size_t)min_sp * G] >= 0) m += fch;
+          else m -= fch;
+        }
+      }
+      if (last_cg == 1) last_cg = 0;
+    }
+  }
+  return abs_sum;
+}
+
+// transformNxN up to (not including) RDOQ, wave per TU.  RDOQ TUs: coefficients in scan
+// order -> coefI, flag 1.  Others (bypass, plain quant, RDOQ not needed): final levels in
+// scan order -> levI, uiAbsSum -> abs_out, flag 0.
+template <int L>
+__global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
+                                               int n, const int16_t *__restrict__ res_in, int32_t *__restrict__ temp_out,
+                                               int32_t *__restrict__ arl_out, int32_t *__restrict__ coefI,
+                                               int32_t *__restrict__ levI, int32_t *__restrict__ abs_out,
+                                               int8_t *__restrict__ flags, int G) {
+  constexpr int N = 4 << L, NN = N * N;
+  __shared__ TuSmem<L> s;
+  const int t = blockIdx.x;
+  if (t >= n) return;
+  const hvx_tu_desc d = descs[t];
+  if (d.width != N || d.height != N) return;
+  const int64_t off = offs[t];
+  const int lane = lane_id();
+  for (int i = lane; i < NN; i += HVX_WAVE) s.a[i] = res_in[off + i];
+  __syncthreads();
+  int32_t *arl = arl_out ? arl_out + off : nullptr;
+  const TuCoding c = tu_coding<L>(d);
+  bool rdoq = false;
+  int32_t abs_sum = 0;
+  if (d.transquant_bypass) {
+    int part = 0;
+    for (int i = lane; i < NN; i += HVX_WAVE) { s.lev[i] = s.a[i]; s.coef[i] = s.a[i]; part += abs(s.a[i]); }
+    abs_sum = wave_sum_i32(part);
+    __syncthreads();
+  } else {
+    if (d.transform_skip) {
+      const int ts = tu_transform_shift(d);
+      for (int i = lane; i < NN; i += HVX_WAVE) {
+        const int32_t v = s.a[i];
+        s.coef[i] = ts >= 0 ? shl32(v, ts) : (v + (1 << (-ts - 1))) >> -ts;
+      }
+      __syncthreads();
+    } else {
+      tu_forward_transform<L>(s, d.use_dst && N == 4);
+    }
+    const int use_rdoq = d.transform_skip ? d.use_rdoq_ts : d.use_rdoq;
+    const int ts = tu_transform_shift(d);
+    const int qbits = 14 + d.qp_per + ts;
+    const int qc = kQuantScales[d.qp_rem];
+    if (use_rdoq) {
+      bool need = true;
+      if (d.selective_rdoq) {  // xNeedRDOQ (:1257)
+        const int add = (d.comp == 0 ? 171 : 256) << (qbits - 9);
+        int any = 0;
+        for (int i = lane; i < NN; i += HVX_WAVE) any |= ((int32_t)(((int64_t)abs(s.coef[i]) * qc + add) >> qbits)) != 0;
+        need = wave_sum_i32(any) != 0;
+      }
+      if (need) {
+        rdoq = true;
+        const int64_t lim = (int64_t)2147483647 - ((int64_t)1 << (qbits - 1));
+        const int qbits_c = qbits - 7, add_c = 1 << (qbits_c - 1);
+        for (int sp = lane; sp < NN; sp += HVX_WAVE) {
+          const int blk = c.scan[sp];
+          coefI[tu_il(t, sp, NN, G)] = s.coef[blk];
+          if (arl) arl[blk] = d.adaptive_qp_select ? (rd_level_double(s.coef[blk], qc, lim) + add_c) >> qbits_c : 0;
+        }
+      } else {
+        for (int i = lane; i < NN; i += HVX_WAVE) {
+          s.lev[i] = 0;
+          if (arl) arl[i] = 0;
+        }
+        __syncthreads();
+      }
+    } else {
+      abs_sum = tu_quant_plain<L>(s, d, arl);
+    }
+  }
+  if (temp_out)
+    for (int i = lane; i < NN; i += HVX_WAVE) temp_out[off + i] = s.coef[i];
+  if (!rdoq) {
+    for (int sp = lane; sp < NN; sp += HVX_WAVE) levI[tu_il(t, sp, NN, G)] = s.lev[c.scan[sp]];
+    if (lane == 0 && abs_out) abs_out[t] = abs_sum;
+  }
+  if (lane == 0) flags[t] = rdoq ? 1 : 0;
+}
+
+// xRateDistOptQuant, one TU per lane: wave w handles TUs w*G .. w*G+G-1 of the launch.
+// n_est_lds > 0: the launch's TUs index the first n_est_lds tables of `est` (est_idx), which
+// are staged in LDS; otherwise each lane reads its own table from global memory.
+template <int L>
+__global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ descs, const hvx_estbits *__restrict__ est,
+                                                const int32_t *__restrict__ est_idx, int n,
+                                                const int32_t *__restrict__ coefI, int32_t *__restrict__ levI,
+                                                int32_t *__restrict__ stI, int32_t *__restrict__ abs_out,
+                                                const int8_t *__restrict__ flags, int G, int n_est_lds) {
+  constexpr int N = 4 << L, NN = N * N;
+  __shared__ hvx_estbits tbl[4];
+  const int lane = lane_id();
+  if (n_est_lds > 0) {
+    const int32_t *src = (const int32_t *)est;
+    int32_t *dst = (int32_t *)tbl;
+    const int words = n_est_lds * (int)(sizeof(hvx_estbits) / 4);
+    for (int i = lane; i < words; i += HVX_WAVE) dst[i] = src[i];
+    __syncthreads();
+  }
+  const int t = blockIdx.x * G + lane;
+  if (lane >= G || t >= n) return;
+  if (!flags[t]) return;
+  const hvx_tu_desc d = descs[t];
+  if (d.width != N || d.height != N) return;
+  const int ei = est_idx ? est_idx[t] : t;
+  const hvx_estbits *e = n_est_lds > 0 ? &tbl[ei] : est + ei;
+  const size_t base = tu_il(t, 0, NN, G);
+  const int32_t a = rdoq_lane<L>(d, e, coefI + base, levI + base, stI + base, G);
+  if (abs_out) abs_out[t] = a;
+}
+
+// Levels (scan order, interleaved) -> raster lev_io; MODE 2 also dequant + inverse + SSE.
+template <int L, int MODE>
+__global__ __launch_bounds__(64) void k_tu_fin(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
+                                               int n, const int16_t *__restrict__ res_in,
+                                               const int32_t *__restrict__ levI, int32_t *__restrict__ lev_io,
+                                               int16_t *__restrict__ res_out, uint32_t *__restrict__ sse_out, int G) {
+  constexpr int N = 4 << L, NN = N * N;
+  __shared__ TuSmem<L> s;
+  const int t = blockIdx.x;
+  if (t >= n) return;
+  const hvx_tu_desc d = descs[t];
+  if (d.width != N || d.height != N) return;
+  const int64_t off = offs[t];
+  const int lane = lane_id();
+  const TuCoding c = tu_coding<L>(d);
+  for (int sp = lane; sp < NN; sp += HVX_WAVE) s.lev[c.scan[sp]] = levI[tu_il(t, sp, NN, G)];
+  __syncthreads();
+  for (int i = lane; i < NN; i += HVX_WAVE) lev_io[off + i] = s.lev[i];
+  if (MODE == 2) {
+    __syncthreads();
+    tu_inverse<L>(s, d);
+    uint32_t part = 0;
+    for (int i = lane; i < NN; i += HVX_WAVE) {
+      const int r = (int16_t)s.lev[i];
+      res_out[off + i] = (int16_t)r;
+      const int df = (int)res_in[off + i] - r;
+      part += (uint32_t)(df * df);
+    }
+    const uint32_t sse = wave_sum_u32(part);
+    if (lane == 0 && sse_out) sse_out[t] = sse;
+  }
+}
