@@ -130,9 +130,7 @@ def main():
         # HIP events on the launch stream (hvx phase events bracket exactly one launch each here).
         # Algorithmic bytes per launch = SURVEY 8(d)'s per-CTU figure (luma form, DESIGN.md
         # "Roofline") x the CTUs one launch covers (every launch of the pass covers the picture).
-        single = {"k_tu<3,2>": "tu32", "k_tu<2,2>": "tu16", "k_tu<1,2>": "tu8", "k_ctu_pred_resid": "mc_resid",
-                  "k_me_int_ctu<64,1,4>": "me_d0", "k_me_int_ctu<32,1,2>": "me_d1",
-                  "k_me_int_ctu<16,1,1>": "me_d2", "k_me_int_ctu<8,0,1>": "me_d3"}
+        single = dict(zip(hvx.PHASE_KERNELS, hvx.PHASES))
         kernel = max(single, key=lambda k: phases[single[k]])
         launch_ms = phases[single[kernel]] / args.steps
         b_ctu = b_ctu_luma(nref)

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -46,6 +47,13 @@ struct hvx_ctx {
 
 namespace {
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+// interleaved RDOQ scratch of the CTU pass: the 3 TU classes (8n 32x32, 16n 16x16, 64n 8x8),
+// each padded to whole groups of kCtuG TUs
+constexpr int kCtuG = 64;
+size_t pad_g(size_t n) { return (n + kCtuG - 1) / kCtuG * kCtuG; }
+size_t ctu_il_off16(int n) { return pad_g((size_t)8 * n) * 1024; }
+size_t ctu_il_off8(int n) { return ctu_il_off16(n) + pad_g((size_t)16 * n) * 256; }
+size_t ctu_il_words(int n) { return ctu_il_off8(n) + pad_g((size_t)64 * n) * 64; }
 struct CtuWs {
   size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, coefI, levI, stI, flags, total;
 };
@@ -64,9 +72,10 @@ CtuWs ctu_ws_layout(const CtuLayout &L) {
   w.abs = o; o = align_up(o + ntu * sizeof(int32_t));
   w.sse = o; o = align_up(o + ntu * sizeof(uint32_t));
   w.ptr = o; o = align_up(o + 8 * sizeof(void *));
-  w.coefI = o; o = align_up(o + nres * sizeof(int32_t));
-  w.levI = o; o = align_up(o + nres * sizeof(int32_t));
-  w.stI = o; o = align_up(o + nres * sizeof(int32_t));
+  const size_t nil = ctu_il_words(L.nctu);
+  w.coefI = o; o = align_up(o + nil * sizeof(int32_t));
+  w.levI = o; o = align_up(o + nil * sizeof(int32_t));
+  w.stI = o; o = align_up(o + nil * sizeof(int32_t));
   w.flags = o; o = align_up(o + ntu);
   w.total = o;
   return w;
@@ -163,16 +172,34 @@ int upload_tables() {
 }
 }  // namespace
 
+static void fold_timing(hvx_ctx *ctx) {
+  if (!ctx->pending) return;
+  (void)hipEventSynchronize(ctx->ev[HVX_NPHASE]);
+  for (int i = 0; i < HVX_NPHASE; i++) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) == hipSuccess) ctx->phase_ms[i] += ms;
+  }
+  ctx->pending = 0;
+}
+
+static inline void mark(hvx_ctx *ctx, int i) {
+  if (ctx->timing && ctx->ev_ok) (void)hipEventRecord(ctx->ev[i], ctx->stream);
+}
+
 // Batched TU pipeline (k_tu_fwd -> k_tu_rdoq -> k_tu_fin) for one size class over TUs
 // [0, n) of the arrays; G TUs per RDOQ wave; scratch arrays hold ceil(n/G)*G*NN words.
 template <int L, int MODE>
 static void tu_class_launch(hipStream_t st, const hvx_tu_desc *desc, const hvx_estbits *est, const int32_t *est_idx,
                             const int64_t *off, int n, const int16_t *res_in, int32_t *temp, int32_t *lev, int32_t *arl,
                             int32_t *abs_sum, int16_t *res_out, uint32_t *sse, int32_t *coefI, int32_t *levI,
-                            int32_t *stI, int8_t *flags, int G, int n_est_lds) {
+                            int32_t *stI, int8_t *flags, int G, int n_est_lds, hvx_ctx *tctx = nullptr,
+                            int phase0 = 0) {
+  if (tctx) mark(tctx, phase0);
   hipLaunchKernelGGL((k_tu_fwd<L>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, temp, arl, coefI, levI, abs_sum, flags, G);
+  if (tctx) mark(tctx, phase0 + 1);
   hipLaunchKernelGGL((k_tu_rdoq<L>), dim3((n + G - 1) / G), dim3(64), 0, st, desc, est, est_idx, n, coefI, levI, stI,
                      abs_sum, flags, G, n_est_lds);
+  if (tctx) mark(tctx, phase0 + 2);
   hipLaunchKernelGGL((k_tu_fin<L, MODE>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, levI, lev, res_out, sse, G);
 }
 
@@ -415,20 +442,6 @@ int hvx_stvssim_batch(hvx_ctx *ctx, const uint8_t *const *d_hist_org, const uint
   return launched("k_stvssim");
 }
 
-static void fold_timing(hvx_ctx *ctx) {
-  if (!ctx->pending) return;
-  (void)hipEventSynchronize(ctx->ev[HVX_NPHASE]);
-  for (int i = 0; i < HVX_NPHASE; i++) {
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) == hipSuccess) ctx->phase_ms[i] += ms;
-  }
-  ctx->pending = 0;
-}
-
-static inline void mark(hvx_ctx *ctx, int i) {
-  if (ctx->timing && ctx->ev_ok) (void)hipEventRecord(ctx->ev[i], ctx->stream);
-}
-
 int hvx_set_timing(hvx_ctx *ctx, int on) {
   if (!ctx) return fail(HVX_E_INVALID, "hvx_set_timing: NULL ctx");
   if (on && !ctx->ev_ok) {
@@ -515,36 +528,39 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
     const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
     const int nb = L.nctu * L.nref;
     hipLaunchKernelGGL((k_me_frac_ctu<64, 4>), dim3(nb), dim3(256), 0, st, cs, d_refs, stride, jobs, res, L.nref, 1, 0);
+    mark(ctx, 5);
     hipLaunchKernelGGL((k_me_frac_ctu<32, 2>), dim3(4 * nb), dim3(128), 0, st, cs, d_refs, stride, jobs, res, L.nref, 4, 1);
+    mark(ctx, 6);
     hipLaunchKernelGGL((k_me_frac_ctu<16, 1>), dim3(16 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 16, 5);
+    mark(ctx, 7);
     hipLaunchKernelGGL((k_me_frac_ctu<8, 1>), dim3(64 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 64, 21);
   }
-  mark(ctx, 5);
+  mark(ctx, 8);
   hipLaunchKernelGGL(k_ctu_pred_resid, dim3(L.nctu * HVX_CUS_PER_CTU), dim3(64), 0, st, L, P, d_cur, d_refs, stride,
                      res, resid, desc, off, est_idx, d_out);
   const int n = L.nctu;
-  mark(ctx, 6);
+  // kCtuG = 64 TUs per RDOQ wave for every class: measured best at 2160p (G = 8/16/32/64 for
+  // 32x32: 3.1/2.9/2.6/2.5 ms) -- the per-lane chain is latency-bound, so wider waves win
+  const int g32 = kCtuG, g16 = kCtuG, g8 = kCtuG;
   int32_t *coefI = (int32_t *)(ws + W.coefI), *levI = (int32_t *)(ws + W.levI), *stI = (int32_t *)(ws + W.stI);
   int8_t *flags = (int8_t *)(ws + W.flags);
-  // size classes are contiguous: [0,8n) 32x32 | [8n,24n) 16x16 | [24n,88n) 8x8; scratch regions
-  // of 8n*1024, 16n*256 and 64n*64 words; 8/16/64 TUs per RDOQ wave (~2 waves per SIMD at 2160p)
+  // size classes are contiguous: [0,8n) 32x32 | [8n,24n) 16x16 | [24n,88n) 8x8; their
+  // interleaved scratch regions start at 0, ctu_il_off16(n), ctu_il_off8(n)
   tu_class_launch<3, 2>(st, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev, nullptr, abs_sum, res_out, sse,
-                        coefI, levI, stI, flags, 8, 4);
-  mark(ctx, 7);
+                        coefI, levI, stI, flags, g32, 4, ctx, 9);
   {
-    const size_t o = (size_t)8 * n * 1024;
+    const size_t o = ctu_il_off16(n);
     tu_class_launch<2, 2>(st, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n, 16 * n, resid, nullptr, lev, nullptr,
-                          abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, levI + o, stI + o, flags + 8 * n, 16, 4);
+                          abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, levI + o, stI + o, flags + 8 * n, g16, 4, ctx, 12);
   }
-  mark(ctx, 8);
   {
-    const size_t o = (size_t)8 * n * 1024 + (size_t)16 * n * 256;
+    const size_t o = ctu_il_off8(n);
     tu_class_launch<1, 2>(st, desc + 24 * n, d_est4, est_idx + 24 * n, off + 24 * n, 64 * n, resid, nullptr, lev, nullptr,
-                          abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, levI + o, stI + o, flags + 24 * n, 64, 4);
+                          abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, levI + o, stI + o, flags + 24 * n, g8, 4, ctx, 15);
   }
-  mark(ctx, 9);
+  mark(ctx, 18);
   hipLaunchKernelGGL(k_ctu_finalize, dim3((n * HVX_CUS_PER_CTU + 255) / 256), dim3(256), 0, st, L, abs_sum, sse, d_out);
-  mark(ctx, 10);
+  mark(ctx, 19);
   if (ctx->timing && ctx->ev_ok) ctx->pending = 1;
   return launched("hvx_ctu_analyze");
 }

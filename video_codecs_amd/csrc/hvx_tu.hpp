@@ -762,10 +762,18 @@ __device__ __forceinline__ size_t tu_il(int t, int sp, int NN, int G) {
 // xRateDistOptQuant (:2129-2671) for one TU by one lane.  coef/lev/st: the TU's interleaved
 // arrays (element sp at [sp * G]); coef in scan order; lev receives the signed final levels
 // in scan order; st the packed per-position context state (rd_pack).  Returns uiAbsSum.
-// Same operations, in the same order, as tu_rdoq and the reference.
+// Same operations, in the same order, as tu_rdoq and the reference.  Every pass works a
+// coefficient group at a time: the group's 16 loads are issued together (the arrays live in
+// HBM / the infinity cache) and staged in the lane's LDS column, and the decision pass
+// prefetches the next group while it decides the current one.
+// Per-lane LDS staging of one coefficient group: column `lane` of [16][64] arrays.
+struct RdLaneStage {
+  int32_t cf[16][64], lv[16][64], st[16][64];
+};
+
 template <int L>
 __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const int32_t *coef, int32_t *lev,
-                             int32_t *st, int G) {
+                             int32_t *st, int G, RdLaneStage &sg, int lane) {
   constexpr int N = 4 << L, NN = N * N, NCG = NN / 16;
   constexpr int LOG2 = L + 2;
   const int ch = d.comp ? 1 : 0, comp = d.comp;
@@ -782,6 +790,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
   const TuCoding c = tu_coding<L>(d);
   const int64_t lim = (int64_t)2147483647 - ((int64_t)1 << (qbits - 1));
   const int sig_off = ch ? 28 : 0;
+  const size_t g16 = (size_t)16 * G;
 
   // ---- reverse-scan decisions ----
   const uint32_t rice0 = (uint32_t)d.golomb_rice_stat / 4;
@@ -789,7 +798,16 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
   int c1 = 1, c2 = 0, last = -1, cg_last = -1;
   double block_uncoded = 0, base_cost = 0;
   uint64_t sigmask = 0;
+  int32_t nxt[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) nxt[k] = coef[(NCG - 1) * g16 + (size_t)k * G];
   for (int cgp = NCG - 1; cgp >= 0; cgp--) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) sg.cf[k][lane] = nxt[k];
+    if (cgp > 0) {
+#pragma unroll
+      for (int k = 0; k < 16; k++) nxt[k] = coef[(cgp - 1) * g16 + (size_t)k * G];
+    }
     const int cgblk = c.scan_cg[cgp];
     const int cy = cgblk / c.wg, cx = cgblk - cy * c.wg;
     int pattern = 0;
@@ -803,7 +821,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
     double coded_ld = 0, uncoded = 0, sig_cost = 0, sig_cost0 = 0;
     for (int pin = 15; pin >= 0; pin--) {
       const int sp = cgp * 16 + pin;
-      const int32_t ld = rd_level_double(coef[(size_t)sp * G], qc, lim);
+      const int32_t ld = rd_level_double(sg.cf[pin][lane], qc, lim);
       const uint32_t q = (uint32_t)((ld + (1 << (qbits - 1))) >> qbits);
       const uint32_t max_abs = (uint32_t)ecmax < q ? (uint32_t)ecmax : q;
       const double e = (double)ld;
@@ -901,6 +919,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
           if (zero_cost < base_cost) {
             sigmask &= ~(1ull << cgblk);
             base_cost = zero_cost;
+#pragma unroll
             for (int pin = 0; pin < 16; pin++) lev[(size_t)(cgp * 16 + pin) * G] = 0;
           }
         }
@@ -937,11 +956,22 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
     }
     base_cost -= lambda * (double)cgrate;
     if ((sigmask >> cgblk) & 1) {
+      {
+        int32_t a16[16], b16[16], c16[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+          a16[k] = lev[cgp * g16 + (size_t)k * G];
+          b16[k] = st[cgp * g16 + (size_t)k * G];
+          c16[k] = coef[cgp * g16 + (size_t)k * G];
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) { sg.lv[k][lane] = a16[k]; sg.st[k][lane] = b16[k]; sg.cf[k][lane] = c16[k]; }
+      }
       for (int pin = 15; pin >= 0; pin--) {
         const int sp = cgp * 16 + pin;
         if (sp > last) continue;
-        const int lvv = lev[(size_t)sp * G];
-        const RdCtx x = rd_unpack(st[(size_t)sp * G]);
+        const int lvv = sg.lv[pin][lane];
+        const RdCtx x = rd_unpack(sg.st[pin][lane]);
         const int sbr = x.sig_sel == 1 ? est->significantBits[x.ctx_sig][0]
                                        : x.sig_sel == 2 ? est->significantBits[x.ctx_sig][1] : 0;
         const double cs = x.sig_sel ? lambda * (double)sbr : 0.0;
@@ -952,7 +982,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
           const double total = base_cost + cl - cs;
           if (total < best_cost) { best_p1 = sp + 1; best_cost = total; }
           if (lvv > 1) { found = true; break; }
-          const int32_t ld = rd_level_double(coef[(size_t)sp * G], qc, lim);
+          const int32_t ld = rd_level_double(sg.cf[pin][lane], qc, lim);
           const double err = (double)sub32(ld, shl32(1, qbits));
           const int rate = rd_ic_rate(1u, x.rice, x.c1ok, x.c2ok, est->greaterOneBits[x.ctx_one][0],
                                       est->greaterOneBits[x.ctx_one][1], est->levelAbsBits[x.ctx_abs][0],
@@ -971,13 +1001,23 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
 
   // ---- signs, zeroing past the chosen last position, uiAbsSum ----
   int32_t abs_sum = 0;
-  for (int sp = 0; sp <= last; sp++) {
-    if (sp < best_p1) {
-      const int32_t lv = lev[(size_t)sp * G];
-      abs_sum += lv;
-      if (coef[(size_t)sp * G] < 0) lev[(size_t)sp * G] = -lv;
-    } else {
-      lev[(size_t)sp * G] = 0;
+  for (int cgp = 0; cgp <= (last >> 4); cgp++) {
+    int32_t lv16[16], cf16[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      lv16[k] = lev[cgp * g16 + (size_t)k * G];
+      cf16[k] = coef[cgp * g16 + (size_t)k * G];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int sp = cgp * 16 + k;
+      if (sp > last) continue;
+      if (sp < best_p1) {
+        abs_sum += lv16[k];
+        if (cf16[k] < 0) lev[cgp * g16 + (size_t)k * G] = -lv16[k];
+      } else {
+        lev[cgp * g16 + (size_t)k * G] = 0;
+      }
     }
   }
 
@@ -987,24 +1027,39 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
     const int64_t rdf = (int64_t)(iq * iq * (1 << (2 * d.qp_per)) / d.lambda / 16 / (1 << 0) + 0.5);
     int last_cg = -1;
     for (int sub = NCG - 1; sub >= 0; sub--) {
-      const int pos = sub << 4;
+      {
+        int32_t a16[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) a16[k] = lev[sub * g16 + (size_t)k * G];
+#pragma unroll
+        for (int k = 0; k < 16; k++) sg.lv[k][lane] = a16[k];
+      }
       int first_nz = 16, last_nz = -1, abs_in = 0, k;
-      for (k = 15; k >= 0; k--) if (lev[(size_t)(k + pos) * G]) { last_nz = k; break; }
-      for (k = 0; k < 16; k++) if (lev[(size_t)(k + pos) * G]) { first_nz = k; break; }
-      for (k = first_nz; k <= last_nz; k++) abs_in += lev[(size_t)(k + pos) * G];
+      for (k = 15; k >= 0; k--) if (sg.lv[k][lane]) { last_nz = k; break; }
+      for (k = 0; k < 16; k++) if (sg.lv[k][lane]) { first_nz = k; break; }
+      for (k = first_nz; k <= last_nz; k++) abs_in += sg.lv[k][lane];
       if (last_nz >= 0 && last_cg == -1) last_cg = 1;
       if (last_nz - first_nz >= 4) {
-        const uint32_t signbit = lev[(size_t)(pos + first_nz) * G] > 0 ? 0 : 1;
+        const uint32_t signbit = sg.lv[first_nz][lane] > 0 ? 0 : 1;
         if (signbit != (uint32_t)(abs_in & 1)) {
+          {
+            int32_t b16[16], c16[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+              c16[q] = coef[sub * g16 + (size_t)q * G];
+              b16[q] = st[sub * g16 + (size_t)q * G];
+            }
+#pragma unroll
+            for (int q = 0; q < 16; q++) { sg.cf[q][lane] = c16[q]; sg.st[q][lane] = b16[q]; }
+          }
           int64_t min_inc = INT64_MAX, cur = INT64_MAX;
-          int min_sp = -1, fch = 0, cch = 0;
+          int min_k = -1, fch = 0, cch = 0;
           for (k = (last_cg == 1 ? last_nz : 15); k >= 0; k--) {
-            const int sp = k + pos;
-            const int32_t lv = lev[(size_t)sp * G];
+            const int32_t lv = sg.lv[k][lane];
             const uint32_t lev0 = (uint32_t)abs(lv);
-            const int32_t ld = rd_level_double(coef[(size_t)sp * G], qc, lim);
+            const int32_t ld = rd_level_double(sg.cf[k][lane], qc, lim);
             const int32_t du = sub32(ld, shl32((int32_t)lev0, qbits)) >> (qbits - 8);
-            const RdCtx x = rd_unpack(st[(size_t)sp * G]);
+            const RdCtx x = rd_unpack(sg.st[k][lane]);
             const int g0 = est->greaterOneBits[x.ctx_one][0];
             const int sigd = x.has_sig ? est->significantBits[x.ctx_sig][1] - est->significantBits[x.ctx_sig][0] : 0;
             int rup = g0, rdown = 0;
@@ -1025,16 +1080,18 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
               cur = rdf * (-(abs(du))) + (1 << 15) + rup + sigd;
               cch = 1;
               if (k < first_nz) {
-                const uint32_t tsb = coef[(size_t)sp * G] >= 0 ? 0 : 1;
+                const uint32_t tsb = sg.cf[k][lane] >= 0 ? 0 : 1;
                 if (tsb != signbit) cur = INT64_MAX;
               }
             }
-            if (cur < min_inc) { min_inc = cur; fch = cch; min_sp = sp; }
+            if (cur < min_inc) { min_inc = cur; fch = cch; min_k = k; }
           }
-          int32_t &m = lev[(size_t)min_sp * G];
-          if (m == ecmax || m == ecmin) fch = -1;
-          if (coef[(size_t)min_sp * G] >= 0) m += fch;
-          else m -= fch;
+          int32_t mv = sg.lv[min_k][lane];
+          const int32_t mc = sg.cf[min_k][lane];
+          if (mv == ecmax || mv == ecmin) fch = -1;
+          if (mc >= 0) mv += fch;
+          else mv -= fch;
+          lev[sub * g16 + (size_t)min_k * G] = mv;
         }
       }
       if (last_cg == 1) last_cg = 0;
@@ -1134,6 +1191,7 @@ __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ 
                                                 const int8_t *__restrict__ flags, int G, int n_est_lds) {
   constexpr int N = 4 << L, NN = N * N;
   __shared__ hvx_estbits tbl[4];
+  __shared__ RdLaneStage stage;
   const int lane = lane_id();
   if (n_est_lds > 0) {
     const int32_t *src = (const int32_t *)est;
@@ -1150,7 +1208,7 @@ __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ 
   const int ei = est_idx ? est_idx[t] : t;
   const hvx_estbits *e = n_est_lds > 0 ? &tbl[ei] : est + ei;
   const size_t base = tu_il(t, 0, NN, G);
-  const int32_t a = rdoq_lane<L>(d, e, coefI + base, levI + base, stI + base, G);
+  const int32_t a = rdoq_lane<L>(d, e, coefI + base, levI + base, stI + base, G, stage, lane);
   if (abs_out) abs_out[t] = a;
 }
 
