@@ -491,24 +491,52 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW> &sm, const hvx_me_job &j, co
   constexpr int HS = MeFracSmem<S, NW>::HS;
   const int w = GENERIC ? j.w : S, h = GENERIC ? j.h : S, lane = lane_id(), wave = threadIdx.x >> 6;
   const bool had = (j.flags & HVX_ME_HADME) != 0;
-  // 1. horizontal phases: column c at quarter x = qx0 + (c-1)*step
+  // 1. horizontal phases: column c at quarter x = qx0 + (c-1)*step.  Integer offsets of the
+  // phases are ix-1 or ix, so one item (row r, columns x0..x0+3) filters all 3 phases from the
+  // 12 bytes at columns x0+ix-4 .. x0+ix+7 (3 dword loads into registers).
   __syncthreads();
-  for (int c = 0; c < 3; c++) {
-    const int qx = qx0 + (c - 1) * step, ox = qx >> 2, fx = qx & 3;
-    const uint8_t *src = ref + (iy - 4) * stride + ox;
-    for (int k = threadIdx.x; k < (h + 8) * w; k += 64 * NW) {
-      const int r = k / w, x = k - r * w;
-      const uint8_t *p = src + r * stride + x;
-      int v;
-      if (fx) {
-        v = 0;
+  {
+    int oxo[3], fxs[3];
 #pragma unroll
-        for (int t = 0; t < 8; t++) v += kLumaFilter[fx][t] * p[t - 3];
-        v -= 8192;
-      } else {
-        v = (p[0] << 6) - 8192;
+    for (int c = 0; c < 3; c++) {
+      const int qx = qx0 + (c - 1) * step;
+      oxo[c] = (qx >> 2) - ix + 1;  // 0 or 1
+      fxs[c] = qx & 3;
+    }
+    const int gw = w >> 2;
+    const uint8_t *src = ref + (iy - 4) * stride + (ix - 4);
+    for (int k = threadIdx.x; k < (h + 8) * gw; k += 64 * NW) {
+      const int r = k / gw, x0 = (k - r * gw) << 2;
+      const uint8_t *p = src + r * stride + x0;
+      const uint32_t w0 = ld4_any(p), w1 = ld4_any(p + 4), w2 = ld4_any(p + 8);
+      int b[12];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        b[q] = (w0 >> (8 * q)) & 255;
+        b[4 + q] = (w1 >> (8 * q)) & 255;
+        b[8 + q] = (w2 >> (8 * q)) & 255;
       }
-      sm.hp[c][r * HS + x] = (int16_t)v;
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        int bo[11];
+#pragma unroll
+        for (int q = 0; q < 11; q++) bo[q] = oxo[c] ? b[q + 1] : b[q];
+        const int fx = fxs[c];
+        int16_t *dst = sm.hp[c] + r * HS + x0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          int v;
+          if (fx) {
+            v = 0;
+#pragma unroll
+            for (int t = 0; t < 8; t++) v += kLumaFilter[fx][t] * bo[i + t];
+            v -= 8192;
+          } else {
+            v = (bo[i + 3] << 6) - 8192;
+          }
+          dst[i] = (int16_t)v;
+        }
+      }
     }
   }
   __syncthreads();
