@@ -159,11 +159,11 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
                     const hvx_ctu_params *h_params, const hvx_estbits *d_est4, void *d_workspace, size_t ws_bytes,
                     hvx_cu_result *d_out);
 /* Optional per-launch timing of hvx_ctu_analyze with HIP events on the launch stream.  Phases:
- * 0..3 integer ME of CU depth 0..3 (k_ctu_me_jobs + k_me_int_ctu), 4..7 fractional ME of
- * depth 0..3 (k_me_frac_ctu), 8 MC/residual (k_ctu_pred_resid), 9..11 TU 32x32 (k_tu_fwd,
- * k_tu_rdoq, k_tu_fin), 12..14 TU 16x16, 15..17 TU 8x8, 18 per-CU sums (k_ctu_finalize).
- * Accumulated ms. */
-#define HVX_NPHASE 19
+ * 0 integer ME of the 64x64 depth (k_ctu_me_jobs + k_me_int_ctu), 1..3 integer + fractional
+ * ME of the 32/16/8 depths (k_ctu_me_jobs + k_me_ctu), 4 fractional ME of the 64x64 depth
+ * (k_me_frac_ctu), 5 MC/residual (k_ctu_pred_resid), 6..8 TU 32x32 (k_tu_fwd, k_tu_rdoq,
+ * k_tu_fin), 9..11 TU 16x16, 12..14 TU 8x8, 15 per-CU sums (k_ctu_finalize).  Accumulated ms. */
+#define HVX_NPHASE 16
 int hvx_set_timing(hvx_ctx *ctx, int on);
 int hvx_phase_times(hvx_ctx *ctx, double *ms_out, int n, int reset);
 

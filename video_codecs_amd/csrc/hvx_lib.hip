@@ -505,37 +505,28 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
     const dim3 grid(L.nctu * ncu * L.nref);
     const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
     switch (d) {  // block size, FEN row subsampling and waves per job are compile-time per depth
-      case 0:
+      case 0:  // 64x64: integer search here, fractional refinement by k_me_frac_ctu below
         if (fen) hipLaunchKernelGGL((k_me_int_ctu<64, 1, 4>), grid, dim3(256), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
         else hipLaunchKernelGGL((k_me_int_ctu<64, 0, 4>), grid, dim3(256), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
         break;
-      case 1:
-        if (fen) hipLaunchKernelGGL((k_me_int_ctu<32, 1, 2>), grid, dim3(128), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
-        else hipLaunchKernelGGL((k_me_int_ctu<32, 0, 2>), grid, dim3(128), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+      case 1:  // fused integer + fractional search
+        if (fen) hipLaunchKernelGGL((k_me_ctu<32, 1, 2>), grid, dim3(128), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+        else hipLaunchKernelGGL((k_me_ctu<32, 0, 2>), grid, dim3(128), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
         break;
       case 2:
-        if (fen) hipLaunchKernelGGL((k_me_int_ctu<16, 1, 1>), grid, dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
-        else hipLaunchKernelGGL((k_me_int_ctu<16, 0, 1>), grid, dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+        if (fen) hipLaunchKernelGGL((k_me_ctu<16, 1, 1>), grid, dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+        else hipLaunchKernelGGL((k_me_ctu<16, 0, 1>), grid, dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
         break;
       default:  // 8x8: FEN never applies (rows <= 8)
-        hipLaunchKernelGGL((k_me_int_ctu<8, 0, 1>), grid, dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
+        hipLaunchKernelGGL((k_me_ctu<8, 0, 1>), grid, dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
         break;
     }
   }
-  // fractional refinement of every depth (only the integer MVs feed the next depth's jobs)
+  // fractional refinement of the 64x64 depth (the others were fused above)
   mark(ctx, 4);
-  {
-    const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
-    const int nb = L.nctu * L.nref;
-    hipLaunchKernelGGL((k_me_frac_ctu<64, 4>), dim3(nb), dim3(256), 0, st, cs, d_refs, stride, jobs, res, L.nref, 1, 0);
-    mark(ctx, 5);
-    hipLaunchKernelGGL((k_me_frac_ctu<32, 2>), dim3(4 * nb), dim3(128), 0, st, cs, d_refs, stride, jobs, res, L.nref, 4, 1);
-    mark(ctx, 6);
-    hipLaunchKernelGGL((k_me_frac_ctu<16, 1>), dim3(16 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 16, 5);
-    mark(ctx, 7);
-    hipLaunchKernelGGL((k_me_frac_ctu<8, 1>), dim3(64 * nb), dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, 64, 21);
-  }
-  mark(ctx, 8);
+  hipLaunchKernelGGL((k_me_frac_ctu<64, 4>), dim3(L.nctu * L.nref), dim3(256), 0, st, (const uint8_t *const *)cur_slot,
+                     d_refs, stride, jobs, res, L.nref, 1, 0);
+  mark(ctx, 5);
   hipLaunchKernelGGL(k_ctu_pred_resid, dim3(L.nctu * HVX_CUS_PER_CTU), dim3(64), 0, st, L, P, d_cur, d_refs, stride,
                      res, resid, desc, off, est_idx, d_out);
   const int n = L.nctu;
@@ -547,20 +538,20 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
   // size classes are contiguous: [0,8n) 32x32 | [8n,24n) 16x16 | [24n,88n) 8x8; their
   // interleaved scratch regions start at 0, ctu_il_off16(n), ctu_il_off8(n)
   tu_class_launch<3, 2>(st, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev, nullptr, abs_sum, res_out, sse,
-                        coefI, levI, stI, flags, g32, 4, ctx, 9);
+                        coefI, levI, stI, flags, g32, 4, ctx, 6);
   {
     const size_t o = ctu_il_off16(n);
     tu_class_launch<2, 2>(st, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n, 16 * n, resid, nullptr, lev, nullptr,
-                          abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, levI + o, stI + o, flags + 8 * n, g16, 4, ctx, 12);
+                          abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, levI + o, stI + o, flags + 8 * n, g16, 4, ctx, 9);
   }
   {
     const size_t o = ctu_il_off8(n);
     tu_class_launch<1, 2>(st, desc + 24 * n, d_est4, est_idx + 24 * n, off + 24 * n, 64 * n, resid, nullptr, lev, nullptr,
-                          abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, levI + o, stI + o, flags + 24 * n, g8, 4, ctx, 15);
+                          abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, levI + o, stI + o, flags + 24 * n, g8, 4, ctx, 12);
   }
-  mark(ctx, 18);
+  mark(ctx, 15);
   hipLaunchKernelGGL(k_ctu_finalize, dim3((n * HVX_CUS_PER_CTU + 255) / 256), dim3(256), 0, st, L, abs_sum, sse, d_out);
-  mark(ctx, 19);
+  mark(ctx, 16);
   if (ctx->timing && ctx->ev_ok) ctx->pending = 1;
   return launched("hvx_ctu_analyze");
 }

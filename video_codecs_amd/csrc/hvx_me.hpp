@@ -543,16 +543,57 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW> &sm, const hvx_me_job &j, co
   // 2. the 9 candidates' costs (SATD or SAD + MV cost), spread over the waves
   const bool xl = had && (!GENERIC || ((w % 8 == 0) && (h % 8 == 0))) && (w * h <= 1024);
   const int tw = w >> 3, nt = (w * h) >> 6;
-  for (int i = wave; i < 9; i += NW) {
+  if (xl) {
+    // this wave's candidates i = wave + NW*ii share each tile pass: their sample gathers and
+    // Hadamard butterflies are independent and interleave
+    constexpr int CPW = (9 + NW - 1) / NW;
+    int cc[CPW], cry[CPW], cfy[CPW];
+    uint32_t dsum[CPW];
+#pragma unroll
+    for (int ii = 0; ii < CPW; ii++) {
+      const int i = wave + NW * ii < 9 ? wave + NW * ii : 0;
+      const int dx = step == 2 ? kRefH[i][0] : kRefQ[i][0], dy = step == 2 ? kRefH[i][1] : kRefQ[i][1];
+      const int qy = qy0 + dy * step;
+      cc[ii] = dx + 1; cry[ii] = (qy >> 2) - iy; cfy[ii] = qy & 3; dsum[ii] = 0;
+    }
+    for (int t = 0; t < nt; t++) {
+      const int x = ((t % tw) << 3) + (lane & 7), y = ((t / tw) << 3) + (lane >> 3);
+      const int o = sm.org[y * S + x];
+      int v[CPW];
+#pragma unroll
+      for (int ii = 0; ii < CPW; ii++) v[ii] = o - me_frac_sample(sm, cc[ii], cry[ii], cfy[ii], x, y);
+#pragma unroll
+      for (int st = 1; st < 64; st <<= 1) {
+#pragma unroll
+        for (int ii = 0; ii < CPW; ii++) {
+          const int q = __shfl_xor(v[ii], st, HVX_WAVE);
+          v[ii] = (lane & st) ? q - v[ii] : v[ii] + q;
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < CPW; ii++) v[ii] = abs(v[ii]);
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1) {
+#pragma unroll
+        for (int ii = 0; ii < CPW; ii++) v[ii] += __shfl_xor(v[ii], st, HVX_WAVE);
+      }
+#pragma unroll
+      for (int ii = 0; ii < CPW; ii++) dsum[ii] += ((uint32_t)v[ii] + 2) >> 2;
+    }
+#pragma unroll
+    for (int ii = 0; ii < CPW; ii++) {
+      const int i = wave + NW * ii;
+      if (i < 9 && lane == 0) {
+        const int dx = step == 2 ? kRefH[i][0] : kRefQ[i][0], dy = step == 2 ? kRefH[i][1] : kRefQ[i][1];
+        sm.cost[i] = dsum[ii] + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
+      }
+    }
+  }
+  for (int i = wave; i < 9 && !xl; i += NW) {
     const int dx = step == 2 ? kRefH[i][0] : kRefQ[i][0], dy = step == 2 ? kRefH[i][1] : kRefQ[i][1];
     const int qy = qy0 + dy * step, ry = (qy >> 2) - iy, fy = qy & 3, c = dx + 1;
     uint32_t d = 0;
-    if (xl) {
-      for (int t = 0; t < nt; t++) {
-        const int x = ((t % tw) << 3) + (lane & 7), y = ((t / tw) << 3) + (lane >> 3);
-        d += had8_xlane((int)sm.org[y * S + x] - me_frac_sample(sm, c, ry, fy, x, y));
-      }
-    } else if (had) {
+    if (had) {
       if (GENERIC || S * S > 1024) {
         uint8_t *blk = sm.blk[wave];
         for (int k = lane; k < w * h; k += HVX_WAVE) {
@@ -586,6 +627,10 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW> &sm, const hvx_me_job &j, co
 }
 
 template <int S, int NW, bool GENERIC>
+__device__ void me_frac_refine(const hvx_me_job &j, const uint8_t *ref, int stride, int ix, int iy, uint32_t sad_int,
+                               MeFracSmem<S, NW> &sm, hvx_me_result *out);
+
+template <int S, int NW, bool GENERIC>
 __device__ void me_frac_job(const hvx_me_job &j, const uint8_t *const *__restrict__ cur_planes,
                             const uint8_t *const *__restrict__ ref_planes, int stride, MeFracSmem<S, NW> &sm,
                             hvx_me_result *out) {
@@ -599,7 +644,15 @@ __device__ void me_frac_job(const hvx_me_job &j, const uint8_t *const *__restric
     sm.org[y * S + x] = cur[y * stride + x];
   }
   const uint8_t *ref = ref_planes[j.ref_idx] + j.pu_y * stride + j.pu_x;
-  // xPatternSearchFracDIF (:4240): half-pel around the integer MV, then quarter-pel
+  me_frac_refine<S, NW, GENERIC>(j, ref, stride, ix, iy, sad_int, sm, out);
+}
+
+// xPatternSearchFracDIF (:4240) from the integer result (ix, iy, sad_int), the original block
+// already in sm.org; writes the complete hvx_me_result.
+template <int S, int NW, bool GENERIC>
+__device__ void me_frac_refine(const hvx_me_job &j, const uint8_t *ref, int stride, int ix, int iy, uint32_t sad_int,
+                               MeFracSmem<S, NW> &sm, hvx_me_result *out) {
+  // half-pel around the integer MV, then quarter-pel
   int bh, bq;
   me_frac_stage<S, NW, GENERIC>(sm, j, ref, stride, ix, iy, ix << 2, iy << 2, 2, 1, ix << 1, iy << 1, bh);
   const int hx = kRefH[bh][0], hy = kRefH[bh][1];
@@ -641,4 +694,41 @@ __global__ __launch_bounds__(64 * NW) void k_me_frac_ctu(const uint8_t *const *_
   const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
   const hvx_me_job j = jobs[slot];
   me_frac_job<S, NW, false>(j, cur_planes, ref_planes, stride, sm, out + slot);
+}
+
+// CTU pass, fused: TZ integer search then the fractional refinement of the same job in one
+// workgroup (the original block stays in LDS, the integer result in registers) -- used for
+// the 32/16/8 depths, where the separate kernels' per-job reloads dominated.
+template <int S, int SUB, int NW>
+__global__ __launch_bounds__(64 * NW) void k_me_ctu(const uint8_t *const *__restrict__ cur_planes,
+                                                   const uint8_t *const *__restrict__ ref_planes, int stride,
+                                                   const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
+                                                   int nref, int ncu, int first) {
+  __shared__ MeFracSmem<S, NW> sm;
+  __shared__ uint32_t cost[kMeMaxList];
+  const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
+  const hvx_me_job j = jobs[slot];
+  if (j.w > 0 && (j.w != S || j.h != S)) return;
+  if (j.w <= 0 || j.h <= 0) {
+    if (threadIdx.x == 0) { hvx_me_result z; memset(&z, 0, sizeof(z)); out[slot] = z; }
+    return;
+  }
+  const uint8_t *cur = cur_planes[j.cur_idx] + j.pu_y * stride + j.pu_x;
+  for (int k = threadIdx.x; k < S * S; k += HVX_WAVE * NW) {
+    const int y = k / S, x = k - y * S;
+    sm.org[y * S + x] = cur[y * stride + x];
+  }
+  __syncthreads();
+  MeInt m;
+  m.org = sm.org; m.cost = cost; m.os = S;
+  m.ref = ref_planes[j.ref_idx] + j.pu_y * stride + j.pu_x;
+  m.sr = stride;
+  m.sub = SUB;
+  m.rows = S >> SUB;
+  m.gw = S >> 2;
+  m.lam = j.lambda_motion;
+  m.px = j.pred_x; m.py = j.pred_y;
+  me_tz<S, SUB, NW>(j, m);
+  const uint32_t sad_int = m.best_sad - me_mv_cost(m.lam, m.px, m.py, 2, m.best_x, m.best_y);
+  me_frac_refine<S, NW, false>(j, m.ref, stride, m.best_x, m.best_y, sad_int, sm, out + slot);
 }

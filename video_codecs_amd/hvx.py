@@ -192,14 +192,14 @@ class CtuAnalyzer:
         return from_device(self.out, _abi.CU_RESULT).reshape(self.nctu, _abi.CUS_PER_CTU)
 
 
-PHASES = ("me_d0", "me_d1", "me_d2", "me_d3", "frac_d0", "frac_d1", "frac_d2", "frac_d3", "mc_resid",
+PHASES = ("me_d0", "me_d1", "me_d2", "me_d3", "frac_d0", "mc_resid",
           "tu32_fwd", "tu32_rdoq", "tu32_fin", "tu16_fwd", "tu16_rdoq", "tu16_fin", "tu8_fwd", "tu8_rdoq", "tu8_fin",
           "finalize")
-# the kernel each phase times (one launch per phase, except me_dN = k_ctu_me_jobs + k_me_int_ctu)
-PHASE_KERNELS = ("k_me_int_ctu<64,1,4>", "k_me_int_ctu<32,1,2>", "k_me_int_ctu<16,1,1>", "k_me_int_ctu<8,0,1>",
-                 "k_me_frac_ctu<64,4>", "k_me_frac_ctu<32,2>", "k_me_frac_ctu<16,1>", "k_me_frac_ctu<8,1>",
-                 "k_ctu_pred_resid", "k_tu_fwd<3>", "k_tu_rdoq<3>", "k_tu_fin<3,2>", "k_tu_fwd<2>", "k_tu_rdoq<2>",
-                 "k_tu_fin<2,2>", "k_tu_fwd<1>", "k_tu_rdoq<1>", "k_tu_fin<1,2>", "k_ctu_finalize")
+# the kernel each phase times (one launch per phase, plus the tiny k_ctu_me_jobs in me_dN)
+PHASE_KERNELS = ("k_me_int_ctu<64,1,4>", "k_me_ctu<32,1,2>", "k_me_ctu<16,1,1>", "k_me_ctu<8,0,1>",
+                 "k_me_frac_ctu<64,4>", "k_ctu_pred_resid", "k_tu_fwd<3>", "k_tu_rdoq<3>", "k_tu_fin<3,2>",
+                 "k_tu_fwd<2>", "k_tu_rdoq<2>", "k_tu_fin<2,2>", "k_tu_fwd<1>", "k_tu_rdoq<1>", "k_tu_fin<1,2>",
+                 "k_ctu_finalize")
 
 
 def set_timing(on):
