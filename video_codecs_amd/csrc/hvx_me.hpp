@@ -117,22 +117,38 @@ __device__ __forceinline__ uint32_t me_sad_part(const MeInt &m, int x, int y, in
   return acc;
 }
 
-// Same for a square SxS block with compile-time FEN shift and lanes-per-point 1<<SH: the
-// whole item loop unrolls, so every load of the candidate is in flight at once.
+// SAD of one S-wide row at any alignment: S/4+1 consecutive aligned dwords (merged into
+// wide loads), v_alignbyte into place, v_sad_u8 against the LDS original.
+template <int S>
+__device__ __forceinline__ uint32_t me_sad_row(const uint8_t *o, const uint8_t *p, uint32_t acc) {
+  constexpr int GW = S / 4;
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  uint32_t w[GW + 1];
+#pragma unroll
+  for (int i = 0; i <= GW; i++) w[i] = q[i];
+  const uint32_t *ow = (const uint32_t *)o;
+#pragma unroll
+  for (int i = 0; i < GW; i++) acc = __builtin_amdgcn_sad_u8(ow[i], __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh), acc);
+  return acc;
+}
+
+// Same for a square SxS block with compile-time FEN shift and lanes-per-point 1<<SH: lane s
+// takes sampled rows s, s+L, ...; the row loop unrolls so that up to ~24 dwords per lane are
+// in flight at once.
 template <int S, int SUB, int SH>
 __device__ __forceinline__ uint32_t me_sad_part_ct(const MeInt &m, int x, int y, int s) {
-  constexpr int GW = S / 4, ROWS = S >> SUB, NI = ROWS * GW, L = 1 << SH, PER = (NI + L - 1) / L;
+  constexpr int ROWS = S >> SUB, L = 1 << SH, PER = (ROWS + L - 1) / L;
+  constexpr int BUDGET = S == 8 ? 12 : 24;  // dwords in flight per lane (8x8: keep occupancy)
+  constexpr int RUN = (S / 4 + 1) * PER <= BUDGET ? PER : (BUDGET / (S / 4 + 1) > 0 ? BUDGET / (S / 4 + 1) : 1);
+  constexpr int UNR = RUN < 1 ? 1 : RUN;
   const uint8_t *base = m.ref + y * m.sr + x;
-  constexpr int UNR = PER <= 4 ? PER : 4;  // bound the loads in flight (VGPRs)
   uint32_t acc = 0;
 #pragma unroll UNR
   for (int k = 0; k < PER; k++) {
-    const int idx = s + k * L;
-    if (NI % L == 0 || idx < NI) {
-      const int r = idx / GW, g = idx % GW;
-      const uint32_t o = *(const uint32_t *)(m.org + ((r << SUB) * S) + 4 * g);
-      acc = __builtin_amdgcn_sad_u8(o, ld4_any(base + (r << SUB) * m.sr + 4 * g), acc);
-    }
+    const int r = s + k * L;
+    if (ROWS % L == 0 || r < ROWS) acc = me_sad_row<S>(m.org + (r << SUB) * S, base + (r << SUB) * m.sr, acc);
   }
   return acc;
 }
