@@ -28,6 +28,7 @@
  *                         xPatternSearchFracDIF :4240)
  *   hvx_ssim_batch        compute_SSIM (stvssim_src/stvssimrdo2_att/lencod/src/stvssim.c:491)
  *   hvx_stvssim_batch     compute_stVSSIM (stvssim.c:587)
+ *   hvx_estbits_update / hvx_estbits_batch   TEncSbac::estBit (TEncSbac.cpp:1726)
  *   hvx_ctu_analyze       TEncCu::compressCtu's inter 2Nx2N analysis for every CU of every CTU
  *                         (TEncCu.cpp:228,349,1291 -> predInterSearch/encodeResAndCalcRdInterCU):
  *                         the bench workload, composition of the kernels above
@@ -147,6 +148,34 @@ typedef struct hvx_stvssim_job {
 } hvx_stvssim_job;
 int hvx_stvssim_batch(hvx_ctx *ctx, const uint8_t *const *d_hist_org, const uint8_t *const *d_hist_rec,
                       const float *d_dirs, const hvx_stvssim_job *d_jobs, int n, float *d_out4);
+
+/* ---------------------------------------------------------------------------------------
+ * Rate tables from CABAC state: TEncSbac::estBit (TEncSbac.cpp:1726-1950), i.e.
+ * estCBFBit, estSignificantCoeffGroupMapBit, estSignificantMapBit,
+ * estLastSignificantPositionBit, estSignificantCoefficientsBit + the Golomb-Rice statistics.
+ * ctx_states: the encoder's context models in TEncSbac::m_contextModels order, one
+ * ContextModel::m_ucState byte (state << 1 | MPS) each, HVX_NUM_CTX of them;
+ * entropy_bits: ContextModel::m_entropyBits (128 entries, ContextModel.cpp:106 -- the caller
+ * passes the encoder's own table); rice_stats: m_golombRiceAdaptationStatistics[4].  Exactly
+ * the entries the reference writes for a width x height TU of channel type ch_type are
+ * written; the rest of *inout is left as it was (the reference keeps a persistent table).
+ * ------------------------------------------------------------------------------------- */
+#define HVX_NUM_CTX 202
+#define HVX_CTX_QT_CBF 28      /* 2 sets x 5 (blockCbpBits) */
+#define HVX_CTX_QT_ROOT_CBF 41 /* estCBFBit reads 4 models from here (the reference's loop bound) */
+#define HVX_CTX_SIG_CG 42      /* [chType][2] */
+#define HVX_CTX_SIG 46         /* 28 luma + 16 chroma */
+#define HVX_CTX_LAST_X 90      /* [chType][15] */
+#define HVX_CTX_LAST_Y 120     /* [chType][15] */
+#define HVX_CTX_ONE 150        /* 16 luma + 8 chroma */
+#define HVX_CTX_ABS 174        /* 4 luma + 2 chroma */
+typedef struct hvx_estbit_job { int32_t width, height, ch_type, pad_; } hvx_estbit_job;
+/* host form (no device work; usable from the encoder thread) */
+int hvx_estbits_update(const uint8_t *ctx_states, const int32_t *entropy_bits, const uint32_t *rice_stats, int width,
+                       int height, int ch_type, hvx_estbits *inout);
+/* batched device form: job i reads d_states[i*HVX_NUM_CTX ..], d_rice[i*4 ..], updates d_inout[i] */
+int hvx_estbits_batch(hvx_ctx *ctx, const uint8_t *d_states, const int32_t *d_entropy_bits, const uint32_t *d_rice,
+                      const hvx_estbit_job *d_jobs, int n, hvx_estbits *d_inout);
 
 /* ---------------------------------------------------------------------------------------
  * CTU analysis pass over a whole picture (hvx_types.h): d_cur = sample (0,0) of the current

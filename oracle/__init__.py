@@ -58,6 +58,7 @@ def lib():
         L.hvxo_adjust_lambda.restype = D
         L.hvxo_adjust_lambda.argtypes = [D, D]
         L.hvxo_ctu_analyze.argtypes = [P, P, I, P, P, I, I, P]
+        L.hvxo_estbits_update.argtypes = [P, P, P, I, I, I, P]
         L.hvxo_dct_matrix.argtypes = [I, P]
         L.hvxo_scan.restype = ctypes.POINTER(ctypes.c_uint32)
         L.hvxo_scan.argtypes = [I, I, I, I]
@@ -219,3 +220,13 @@ def scan(grouped, scan_type, log2w, log2h):
     p = lib().hvxo_scan(int(grouped), scan_type, log2w, log2h)
     n = 1 << (log2w + log2h)
     return np.ctypeslib.as_array(p, shape=(n,)).copy()
+
+
+def estbits_update(states, entropy_bits, rice, w, h, ch, est_in):
+    """hvxo_estbits_update: context states (>= 202 bytes) -> updated copy of est_in (224 int32)."""
+    st = _c(states, np.uint8)
+    eb = _c(entropy_bits, np.int32)
+    rc = _c(rice, np.uint32)
+    e = np.array(est_in, dtype=np.int32, copy=True).reshape(-1)
+    lib().hvxo_estbits_update(_p(st), _p(eb), _p(rc), int(w), int(h), int(ch), _p(e))
+    return e

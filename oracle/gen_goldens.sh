@@ -27,4 +27,10 @@ enc tests/golden/tu_intra.bin  $CFG/encoder_intra_main.cfg       "$TMP/rand.yuv"
 enc tests/golden/tu_ldp.bin    $CFG/encoder_lowdelay_P_main.cfg  "$TMP/smooth.yuv" 3 27
 enc tests/golden/tu_ldp22.bin  $CFG/encoder_lowdelay_P_main.cfg  "$TMP/smooth.yuv" 2 22
 enc tests/golden/tu_noqrd.bin  $CFG/encoder_lowdelay_P_main.cfg  "$TMP/smooth.yuv" 2 37 --RDOQ=0 --RDOQTS=0
+# CABAC context states -> estBits tables (TEncSbac::estBit), from an intra and an LDP encode
+HVX_CAPTURE="$TMP/est_i.bin" $ORC/TAppEncoder_estcap -c $CFG/encoder_intra_main.cfg -i "$TMP/rand.yuv" \
+  -wdt 416 -hgt 240 -fr 30 -f 1 -q 32 -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+HVX_CAPTURE="$TMP/est_p.bin" $ORC/TAppEncoder_estcap -c $CFG/encoder_lowdelay_P_main.cfg -i "$TMP/smooth.yuv" \
+  -wdt 416 -hgt 240 -fr 30 -f 3 -q 27 -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+python3 oracle/merge_goldens.py tests/golden/estbit.bin "$TMP/est_i.bin" "$TMP/est_p.bin"
 ls -la tests/golden

@@ -29,3 +29,19 @@ def load(path):
         out[name] = np.frombuffer(data, dtype=dtype, count=count, offset=off).reshape(shape).copy()
         off += count * dtype.itemsize
     return out
+
+
+_NAME = {np.dtype(v): k for k, v in _DT.items()}
+
+
+def save(path, arrays):
+    """Write {name: ndarray} (<= 4 dims) as an HVXG container (same layout as golden_writer.h)."""
+    parts = [b"HVXG", struct.pack("<I", len(arrays))]
+    for name, a in arrays.items():
+        a = np.ascontiguousarray(a)
+        shape = list(a.shape) + [0] * (4 - a.ndim)
+        parts.append(name.encode().ljust(32, b"\0") + _NAME[a.dtype].encode().ljust(8, b"\0"))
+        parts.append(struct.pack("<5I", a.ndim, *shape))
+        parts.append(a.tobytes())
+    with open(path, "wb") as f:
+        f.write(b"".join(parts))

@@ -1393,3 +1393,67 @@ void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride
     base += g * g;
   }
 }
+
+
+/* ============================================================================================
+ * estBit: TLibEncoder/TEncSbac.cpp:1726-1950 (estCBFBit :1751, estSignificantCoeffGroupMapBit
+ * :1778, estSignificantMapBit :1797, estLastSignificantPositionBit :1860,
+ * estSignificantCoefficientsBit :1920); context buffer order = the TEncSbac constructor;
+ * significanceMapContextSetStart/Size ContextTables.h:85-86;
+ * getLastSignificantContextParameters TComChromaFormat.h:211.
+ * ========================================================================================== */
+static int ctx_bits(const uint8_t *states, const int32_t *eb, int ctx, int val) {
+  return eb[states[ctx] ^ val]; /* ContextModel::getEntropyBits, ContextModel.h:79 */
+}
+
+void hvxo_estbits_update(const uint8_t *states, const int32_t *eb, const uint32_t *rice, int w, int h, int ch,
+                         hvx_estbits *e) {
+  /* context buffer offsets: split 3, skip 3, merge flag 1, merge idx 1, part size 4, pred mode 1,
+   * intra 1, chroma 2, dqp 3, inter dir 5, ref 2, mvd 2 -> qt cbf at 28 (10), subdiv 3, root cbf
+   * at 41 (1), sig CG at 42 (2x2), sig at 46 (44), last X at 90 (2x15), last Y at 120, one at
+   * 150 (24), abs at 174 (6) */
+  static const int start[2][4] = {{0, 9, 21, 27}, {0, 9, 12, 15}};
+  static const int size[2][4] = {{9, 12, 6, 1}, {9, 3, 3, 1}};
+  int i, b, k;
+  for (i = 0; i < 10; i++)
+    for (b = 0; b < 2; b++) e->blockCbpBits[i][b] = ctx_bits(states, eb, 28 + i, b);
+  for (i = 0; i < 4; i++) /* the reference's loop runs to 4 over a 1-model buffer: models 41..44 */
+    for (b = 0; b < 2; b++) e->blockRootCbpBits[i][b] = ctx_bits(states, eb, 41 + i, b);
+  for (i = 0; i < 2; i++)
+    for (b = 0; b < 2; b++) e->significantCoeffGroupBits[i][b] = ctx_bits(states, eb, 42 + ch * 2 + i, b);
+  {
+    const int type = (w == 4 && h == 4) ? 0 : (w == 8 && h == 8) ? 1 : 2;
+    const int first = start[ch][type], num = size[ch][type], off = ch ? 28 : 0;
+    if (first > 0)
+      for (b = 0; b < 2; b++) e->significantBits[off][b] = ctx_bits(states, eb, 46 + off, b);
+    for (b = 0; b < 2; b++) e->significantBits[off + start[ch][3]][b] = ctx_bits(states, eb, 46 + off + start[ch][3], b);
+    for (k = first; k < first + num; k++)
+      for (b = 0; b < 2; b++) e->significantBits[off + k][b] = ctx_bits(states, eb, 46 + off + k, b);
+  }
+  {
+    static const int group[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
+                                  8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9}; /* g_uiGroupIdx */
+    const int cw = (w == 4 ? 0 : w == 8 ? 1 : w == 16 ? 2 : 3), chh = (h == 4 ? 0 : h == 8 ? 1 : h == 16 ? 2 : 3);
+    const int ox = ch ? 0 : cw * 3 + ((cw + 1) >> 2), oy = ch ? 0 : chh * 3 + ((chh + 1) >> 2);
+    const int sx = ch ? cw : (cw + 3) >> 2, sy = ch ? chh : (chh + 3) >> 2;
+    int bits = 0, c;
+    for (c = 0; c < group[w - 1]; c++) {
+      const int m = 90 + ch * 15 + ox + (c >> sx);
+      e->lastXBits[ch][c] = bits + ctx_bits(states, eb, m, 0);
+      bits += ctx_bits(states, eb, m, 1);
+    }
+    e->lastXBits[ch][c] = bits;
+    bits = 0;
+    for (c = 0; c < group[h - 1]; c++) {
+      const int m = 120 + ch * 15 + oy + (c >> sy);
+      e->lastYBits[ch][c] = bits + ctx_bits(states, eb, m, 0);
+      bits += ctx_bits(states, eb, m, 1);
+    }
+    e->lastYBits[ch][c] = bits;
+  }
+  for (i = (ch ? 16 : 0); i < (ch ? 24 : 16); i++)
+    for (b = 0; b < 2; b++) e->greaterOneBits[i][b] = ctx_bits(states, eb, 150 + i, b);
+  for (i = (ch ? 4 : 0); i < (ch ? 6 : 4); i++)
+    for (b = 0; b < 2; b++) e->levelAbsBits[i][b] = ctx_bits(states, eb, 174 + i, b);
+  for (i = 0; i < 4; i++) e->golombRiceAdaptationStatistics[i] = (int32_t)rice[i];
+}

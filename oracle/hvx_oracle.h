@@ -58,6 +58,11 @@ float hvxo_stvssim(const uint8_t *const *org_hist, const uint8_t *const *rec_his
                    const float *dirs, int dirs_stride, int w, int h, int wint, int overlap, int gama, int comp,
                    float *ssim, float *ssim3d, float *stvssim);
 double hvxo_lambda_2(int qp);
+/* TEncSbac::estBit (TEncSbac.cpp:1726): context states (TEncSbac::m_contextModels order,
+ * m_ucState bytes) + ContextModel::m_entropyBits -> the estBits entries for a w x h TU of
+ * channel type ch (other entries untouched) */
+void hvxo_estbits_update(const uint8_t *states, const int32_t *entropy_bits, const uint32_t *rice, int w, int h, int ch,
+                         hvx_estbits *e);
 double hvxo_adjust_lambda(double lambda, double eta);
 
 /* ---- CTU analysis pass (the bench workload, hvx_types.h) ---- */

@@ -65,3 +65,18 @@ def test_golden_estbits_layout():
     from tests import golden_cases as gc
     g = gc.load("tu_ldp.bin")
     assert g["fwd_estbits"].shape[1] == _abi.ESTBITS_INTS
+
+
+def test_estbits_update_host_golden():
+    # the library's host form of TEncSbac::estBit (product code, no device) vs the reference
+    from tests import golden_cases as gc
+    g = gc.load("estbit.bin")
+    meta, states, rice, before, after, eb = g["meta"], g["states"], g["rice"], g["before"], g["after"], g["entropy_bits"]
+    for i in range(meta.shape[0]):
+        w, h, ch = (int(x) for x in meta[i, :3])
+        got = hvx.estbits_update(states[i], eb, rice[i], w, h, ch, before[i])
+        np.testing.assert_array_equal(got, after[i], err_msg=f"record {i}")
+    # invalid geometry is an error, not a silent result
+    import pytest
+    with pytest.raises(hvx.HvxError):
+        hvx.estbits_update(states[0], eb, rice[0], 64, 64, 0, before[0])

@@ -148,3 +148,19 @@ def test_ctu_pass_gpu(torch):
 def test_ctu_pass_qp_sweep_gpu(torch):
     for qp in (22, 27, 37):
         assert gpu_cases.check_ctu_pass(seed=qp, width=192, height=128, nref=1, qp=qp) == 6
+
+
+def test_estbits_batch_golden_gpu(torch):
+    g = gc.load("estbit.bin")
+    meta, states, rice, before, after, eb = g["meta"], g["states"], g["rice"], g["before"], g["after"], g["entropy_bits"]
+    n = meta.shape[0]
+    jobs = np.zeros(n, hvx.ESTBIT_JOB)
+    jobs["width"], jobs["height"], jobs["ch_type"] = meta[:, 0], meta[:, 1], meta[:, 2]
+    st = np.ascontiguousarray(states[:, :hvx.NUM_CTX])
+    d_st = torch.from_numpy(st.reshape(-1).copy()).cuda()
+    d_eb = torch.from_numpy(eb.copy()).cuda()
+    d_rc = torch.from_numpy(rice.astype(np.int32).reshape(-1).copy()).cuda()
+    d_io = torch.from_numpy(before.astype(np.int32).reshape(-1).copy()).cuda()
+    hvx.estbits_batch(d_st, d_eb, d_rc, hvx.to_device(jobs), n, d_io)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d_io.cpu().numpy().reshape(n, -1), after)

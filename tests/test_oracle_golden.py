@@ -96,3 +96,15 @@ def test_ssim_golden():
     for qp in range(52):
         assert oracle.lambda_2(qp) == lam[qp, 0]
         assert oracle.adjust_lambda(oracle.lambda_2(qp), 0.25 + qp * 0.05) == lam[qp, 1]
+
+
+def test_estbit_golden():
+    # TEncSbac::estBit captured from an intra and an LDP encode (oracle/estbit_capture.cpp):
+    # context states + the table before -> the table after
+    g = gc.load("estbit.bin")
+    meta, states, rice, before, after, eb = g["meta"], g["states"], g["rice"], g["before"], g["after"], g["entropy_bits"]
+    assert meta.shape[0] > 500 and int(meta[0, 3]) == 202
+    for i in range(meta.shape[0]):
+        w, h, ch = (int(x) for x in meta[i, :3])
+        got = oracle.estbits_update(states[i], eb, rice[i].astype(np.uint32), w, h, ch, before[i])
+        np.testing.assert_array_equal(got, after[i], err_msg=f"record {i} ({w}x{h} ch{ch})")

@@ -15,6 +15,7 @@
 #include "hvx_ssim.hpp"
 #include "hvx_tu.hpp"
 #include "hvx_ctu.hpp"
+#include "hvx_estbit.hpp"
 
 struct hvx_ctx {
   int device = 0;
@@ -423,6 +424,25 @@ int hvx_me_batch(hvx_ctx *ctx, const uint8_t *const *d_cur_planes, const uint8_t
   hipLaunchKernelGGL(k_me_int, dim3(n), dim3(64), 0, ctx->stream, d_cur_planes, d_ref_planes, stride, d_jobs, n, d_out);
   hipLaunchKernelGGL(k_me_frac, dim3(n), dim3(256), 0, ctx->stream, d_cur_planes, d_ref_planes, stride, d_jobs, n, d_out);
   return launched("k_me");
+}
+
+int hvx_estbits_update(const uint8_t *ctx_states, const int32_t *entropy_bits, const uint32_t *rice_stats, int width,
+                       int height, int ch_type, hvx_estbits *inout) {
+  if (!ctx_states || !entropy_bits || !rice_stats || !inout) return fail(HVX_E_INVALID, "hvx_estbits_update: NULL");
+  if (width != height || (width != 4 && width != 8 && width != 16 && width != 32) || ch_type < 0 || ch_type > 1)
+    return fail(HVX_E_INVALID, "hvx_estbits_update: bad TU geometry");
+  estbit_update(ctx_states, entropy_bits, rice_stats, width, height, ch_type, inout);
+  return HVX_OK;
+}
+
+int hvx_estbits_batch(hvx_ctx *ctx, const uint8_t *d_states, const int32_t *d_entropy_bits, const uint32_t *d_rice,
+                      const hvx_estbit_job *d_jobs, int n, hvx_estbits *d_inout) {
+  if (!ctx || n < 0 || (n && (!d_states || !d_entropy_bits || !d_rice || !d_jobs || !d_inout)))
+    return fail(HVX_E_INVALID, "hvx_estbits_batch: bad args");
+  if (!n) return HVX_OK;
+  hipLaunchKernelGGL(k_estbits, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, d_states, d_entropy_bits, d_rice, d_jobs, n,
+                     d_inout);
+  return launched("k_estbits");
 }
 
 int hvx_ssim_batch(hvx_ctx *ctx, const uint8_t *d_org, const uint8_t *d_rec, const hvx_ssim_job *d_jobs, int n,

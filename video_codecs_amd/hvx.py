@@ -43,6 +43,7 @@ def lib():
             "hvx_ctu_workspace_size": [I, I, I, ctypes.POINTER(ctypes.c_size_t)],
             "hvx_ctu_analyze": [P, P, P, I, P, P, P, ctypes.c_size_t, P],
             "hvx_set_timing": [P, I], "hvx_phase_times": [P, ctypes.POINTER(ctypes.c_double), I, I],
+            "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
         }.items():
             f = getattr(L, name)
             f.argtypes = args
@@ -144,6 +145,27 @@ def me_batch(cur_planes_ptrs, ref_planes_ptrs, stride, jobs_dev, n, out):
 
 def ssim_batch(org, rec, jobs_dev, n, out):
     _check(lib().hvx_ssim_batch(context(), _ptr(org), _ptr(rec), _ptr(jobs_dev), n, _ptr(out)), "hvx_ssim_batch")
+
+
+NUM_CTX = 202  # HVX_NUM_CTX
+ESTBIT_JOB = np.dtype([("width", "<i4"), ("height", "<i4"), ("ch_type", "<i4"), ("pad_", "<i4")])
+
+
+def estbits_update(states, entropy_bits, rice, w, h, ch, est_in):
+    """Host form of hvx_estbits_update (TEncSbac::estBit); returns an updated copy of est_in
+    (224 int32).  Runs in the library on the CPU: no device needed."""
+    st = np.ascontiguousarray(states, np.uint8)
+    eb = np.ascontiguousarray(entropy_bits, np.int32)
+    rc = np.ascontiguousarray(rice, np.uint32)
+    e = np.array(est_in, dtype=np.int32, copy=True).reshape(-1)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    _check(lib().hvx_estbits_update(vp(st), vp(eb), vp(rc), int(w), int(h), int(ch), vp(e)), "hvx_estbits_update")
+    return e
+
+
+def estbits_batch(states_dev, entropy_dev, rice_dev, jobs_dev, n, inout_dev):
+    _check(lib().hvx_estbits_batch(context(), _ptr(states_dev), _ptr(entropy_dev), _ptr(rice_dev), _ptr(jobs_dev), n,
+                                   _ptr(inout_dev)), "hvx_estbits_batch")
 
 
 def stvssim_batch(hist_org_ptrs, hist_rec_ptrs, dirs, jobs_dev, n, out4):
