@@ -29,6 +29,7 @@
  *   hvx_ssim_batch        compute_SSIM (stvssim_src/stvssimrdo2_att/lencod/src/stvssim.c:491)
  *   hvx_stvssim_batch     compute_stVSSIM (stvssim.c:587)
  *   hvx_estbits_update / hvx_estbits_batch   TEncSbac::estBit (TEncSbac.cpp:1726)
+ *   hvx_mc_batch          TComPrediction::motionCompensation (TComPrediction.cpp:517)
  *   hvx_ctu_analyze       TEncCu::compressCtu's inter 2Nx2N analysis for every CU of every CTU
  *                         (TEncCu.cpp:228,349,1291 -> predInterSearch/encodeResAndCalcRdInterCU):
  *                         the bench workload, composition of the kernels above
@@ -148,6 +149,23 @@ typedef struct hvx_stvssim_job {
 } hvx_stvssim_job;
 int hvx_stvssim_batch(hvx_ctx *ctx, const uint8_t *const *d_hist_org, const uint8_t *const *d_hist_rec,
                       const float *d_dirs, const hvx_stvssim_job *d_jobs, int n, float *d_out4);
+
+/* ---------------------------------------------------------------------------------------
+ * Motion compensation (hvx_types.h hvx_mc_job): TComPrediction::motionCompensation /
+ * xPredInterUni / xPredInterBi / xPredInterBlk / xWeightedAverage (TComPrediction.cpp:517-722)
+ * and TComYuv::addAvg (TComYuv.cpp:352).  d_planes: device array of 3*n_refs pointers, entry
+ * 3*r + c = sample (0,0) of component c (0 Y, 1 Cb, 2 Cr) of reference r, HM TComPicYuv int16
+ * planes (margins >= the MV clip range + filter reach, e.g. HM's 80/40); luma_stride /
+ * chroma_stride in samples.  d_dst receives int16 prediction samples.
+ * ------------------------------------------------------------------------------------- */
+int hvx_mc_batch(hvx_ctx *ctx, const int16_t *const *d_planes, int luma_stride, int chroma_stride,
+                 const hvx_mc_job *d_jobs, int n, int16_t *d_dst);
+
+/* Device memory helpers for callers without HIP headers (ordered on the context's stream). */
+int hvx_alloc(hvx_ctx *ctx, size_t bytes, void **d_out);
+int hvx_free(hvx_ctx *ctx, void *d);
+int hvx_upload(hvx_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);   /* async */
+int hvx_download(hvx_ctx *ctx, void *h_dst, const void *d_src, size_t bytes); /* async */
 
 /* ---------------------------------------------------------------------------------------
  * Rate tables from CABAC state: TEncSbac::estBit (TEncSbac.cpp:1726-1950), i.e.

@@ -119,6 +119,24 @@ typedef struct hvx_cu_result {
   int32_t n_tu;
 } hvx_cu_result;
 
+/* One PU's motion compensation (TComPrediction::motionCompensation for one partition, no
+ * weighted prediction; TComPrediction.cpp:517-722).  Lists with ref >= 0 are used: both ->
+ * bi-prediction (14-bit intermediates + TComYuv::addAvg), unless HVX_MC_B_SLICE is set and the
+ * two lists carry identical motion (same POC and MV: xCheckIdenticalMotion :500), which
+ * predicts from list 0 alone; one -> uni-prediction from that list.  MVs are clipped here as
+ * xPredInterUni does (TComDataCU::clipMv).  4:2:0, 8-bit. */
+#define HVX_MC_B_SLICE 1
+typedef struct hvx_mc_job {
+  int32_t pic_w, pic_h, max_cu;  /* clipMv */
+  int32_t cu_x, cu_y;            /* CU origin, luma samples (clipMv) */
+  int32_t pu_x, pu_y, w, h;      /* PU, luma samples */
+  int32_t ref[2];                /* per list: reference picture index into the plane table, -1 = unused */
+  int32_t poc[2];                /* per list: the reference's POC (identical-motion check) */
+  int32_t mv_x[2], mv_y[2];      /* per list: quarter-pel MV before clipMv */
+  int32_t flags;                 /* HVX_MC_B_SLICE */
+  int64_t dst_offset;            /* element offset of the output: Y w*h, Cb, Cr (w/2)*(h/2) each */
+} hvx_mc_job;
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,6 +59,8 @@ def lib():
         L.hvxo_adjust_lambda.argtypes = [D, D]
         L.hvxo_ctu_analyze.argtypes = [P, P, I, P, P, I, I, P]
         L.hvxo_estbits_update.argtypes = [P, P, P, I, I, I, P]
+        L.hvxo_mc.argtypes = [P, I, I, P, P]
+        L.hvxo_add_avg.argtypes = [P, P, P, I]
         L.hvxo_dct_matrix.argtypes = [I, P]
         L.hvxo_scan.restype = ctypes.POINTER(ctypes.c_uint32)
         L.hvxo_scan.argtypes = [I, I, I, I]
@@ -230,3 +232,22 @@ def estbits_update(states, entropy_bits, rice, w, h, ch, est_in):
     e = np.array(est_in, dtype=np.int32, copy=True).reshape(-1)
     lib().hvxo_estbits_update(_p(st), _p(eb), _p(rc), int(w), int(h), int(ch), _p(e))
     return e
+
+
+def mc(planes, luma_stride, chroma_stride, job):
+    """hvxo_mc for one MC_JOB; planes: list of 3*n_ref (array, origin element offset) pairs of
+    int16 HM planes.  Returns the Y|Cb|Cr prediction samples."""
+    arrs = [_c(a, np.int16) for a, _ in planes]
+    ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data + 2 * int(o) for a, (_, o) in zip(arrs, planes)])
+    j = np.ascontiguousarray(job, dtype=_abi.MC_JOB).reshape(1)
+    w, h = int(j["w"][0]), int(j["h"][0])
+    out = np.zeros(w * h + 2 * (w // 2) * (h // 2), np.int16)
+    lib().hvxo_mc(ptrs, int(luma_stride), int(chroma_stride), _p(j), _p(out))
+    return out
+
+
+def add_avg(a, b):
+    a, b = _c(a, np.int16), _c(b, np.int16)
+    out = np.zeros_like(a)
+    lib().hvxo_add_avg(_p(a), _p(b), _p(out), a.size)
+    return out

@@ -38,6 +38,7 @@
 #include "TLibCommon/CommonDef.h"
 #include "TLibCommon/TComRom.h"
 #include "TLibCommon/TComRdCost.h"
+#include "TLibCommon/TComYuv.h"
 #include "TLibCommon/TComInterpolationFilter.h"
 #include "TLibCommon/TComTrQuant.h"
 #include "TLibCommon/TComDataCU.h"
@@ -458,6 +459,54 @@ static void gen_ssim() {
   gw.write(g_out + "/ssim.bin");
 }
 
+// TComYuv::addAvg (TComYuv.cpp:352) on random 14-bit intermediates, 4:2:0, several PU sizes
+static void gen_addavg() {
+  SplitMix64 rng(0x5EED0A06);
+  const int shapes[][2] = {{64, 64}, {32, 32}, {16, 16}, {8, 8}, {16, 8}, {8, 16}, {64, 16}, {12, 16}, {32, 24}, {8, 4}, {4, 8}};
+  const int n = sizeof(shapes) / sizeof(shapes[0]);
+  std::vector<int32_t> meta;
+  std::vector<int16_t> in0, in1, out;
+  BitDepths bd;
+  bd.recon[CHANNEL_TYPE_LUMA] = 8;
+  bd.recon[CHANNEL_TYPE_CHROMA] = 8;
+  for (int i = 0; i < n; i++) {
+    const int w = shapes[i][0], h = shapes[i][1];
+    TComYuv a, b, d;
+    a.create(64, 64, CHROMA_420);
+    b.create(64, 64, CHROMA_420);
+    d.create(64, 64, CHROMA_420);
+    for (int c = 0; c < 3; c++) {
+      const ComponentID id = ComponentID(c);
+      for (int k = 0; k < a.getHeight(id) * a.getStride(id); k++) {
+        // first-stage-like intermediates: (sample << 6) - 8192 plus filter overshoot
+        a.getAddr(id)[k] = (Pel)rng.range(-8192 - 2600, 8192 + 2600);
+        b.getAddr(id)[k] = (Pel)rng.range(-8192 - 2600, 8192 + 2600);
+      }
+    }
+    d.addAvg(&a, &b, 0, w, h, bd);
+    meta.insert(meta.end(), {w, h});
+    for (int c = 0; c < 3; c++) {
+      const ComponentID id = ComponentID(c);
+      const int cw = c ? w >> 1 : w, ch = c ? h >> 1 : h, st = a.getStride(id);
+      for (int y = 0; y < ch; y++)
+        for (int x = 0; x < cw; x++) {
+          in0.push_back(a.getAddr(id)[y * st + x]);
+          in1.push_back(b.getAddr(id)[y * st + x]);
+          out.push_back(d.getAddr(id)[y * st + x]);
+        }
+    }
+    a.destroy();
+    b.destroy();
+    d.destroy();
+  }
+  GoldenWriter gw;
+  gw.add("meta", "i32", {(uint32_t)n, 2}, meta);
+  gw.add("in0", "i16", {(uint32_t)in0.size()}, in0);
+  gw.add("in1", "i16", {(uint32_t)in1.size()}, in1);
+  gw.add("out", "i16", {(uint32_t)out.size()}, out);
+  gw.write(g_out + "/addavg.bin");
+}
+
 int main(int argc, char **argv) {
   if (argc > 1) g_out = argv[1];
   initROM();
@@ -466,6 +515,7 @@ int main(int argc, char **argv) {
   gen_xform();
   gen_me();
   gen_ssim();
+  gen_addavg();
   destroyROM();
   return 0;
 }

@@ -1457,3 +1457,65 @@ void hvxo_estbits_update(const uint8_t *states, const int32_t *eb, const uint32_
     for (b = 0; b < 2; b++) e->levelAbsBits[i][b] = ctx_bits(states, eb, 174 + i, b);
   for (i = 0; i < 4; i++) e->golombRiceAdaptationStatistics[i] = (int32_t)rice[i];
 }
+
+
+/* ============================================================================================
+ * Motion compensation: TComPrediction.cpp:517-722, TComYuv.cpp:352 (8-bit, 4:2:0, no WP)
+ * ========================================================================================== */
+/* TComYuv::addAvg: shiftNum = max(2, IF_INTERNAL_PREC - 8) + 1 = 7,
+ * offset = (1 << 6) + 2 * IF_INTERNAL_OFFS, ClipBD */
+void hvxo_add_avg(const int16_t *a, const int16_t *b, int16_t *dst, int n) {
+  for (int i = 0; i < n; i++) dst[i] = clip_pel((a[i] + b[i] + (1 << 6) + 2 * IF_OFFS) >> 7);
+}
+
+/* xPredInterBlk (:668-706) for one component of the PU at component position (x, y) */
+static void mc_pred_blk(int is_luma, const int16_t *plane, int stride, int x, int y, int mvx, int mvy, int w, int h,
+                        int bi, int16_t *dst) {
+  const int sh = is_luma ? 2 : 3; /* shiftHor/Ver = 2 + component scale (4:2:0 chroma: 1) */
+  const int xf = mvx & ((1 << sh) - 1), yf = mvy & ((1 << sh) - 1);
+  const int16_t *ref = plane + (y + (mvy >> sh)) * stride + x + (mvx >> sh);
+  if (yf == 0) {
+    hvxo_filter_hor(is_luma, ref, stride, dst, w, w, h, xf, !bi);
+  } else if (xf == 0) {
+    hvxo_filter_ver(is_luma, ref, stride, dst, w, w, h, yf, 1, !bi);
+  } else {
+    static int16_t tmp[(64 + 7) * 64];
+    const int n = is_luma ? 8 : 4;
+    hvxo_filter_hor(is_luma, ref - (n / 2 - 1) * stride, stride, tmp, w, w, h + n - 1, xf, 0);
+    hvxo_filter_ver(is_luma, tmp + (n / 2 - 1) * w, w, dst, w, w, h, yf, 0, !bi);
+  }
+}
+
+static void mc_clip(const hvx_mc_job *j, int *mx, int *my) { /* TComDataCU::clipMv (TComDataCU.cpp:2788) */
+  const int hmax = (j->pic_w + 8 - j->cu_x - 1) << 2, hmin = (-j->max_cu - 8 - j->cu_x + 1) << 2;
+  const int vmax = (j->pic_h + 8 - j->cu_y - 1) << 2, vmin = (-j->max_cu - 8 - j->cu_y + 1) << 2;
+  *mx = (int16_t)(*mx < hmin ? hmin : *mx > hmax ? hmax : *mx);
+  *my = (int16_t)(*my < vmin ? vmin : *my > vmax ? vmax : *my);
+}
+
+void hvxo_mc(const int16_t *const *planes, int ls, int cs, const hvx_mc_job *j, int16_t *out) {
+  const int v0 = j->ref[0] >= 0, v1 = j->ref[1] >= 0;
+  /* xCheckIdenticalMotion (:500): B slice without WP, same POC and same (unclipped) MV */
+  const int identical = (j->flags & HVX_MC_B_SLICE) && v0 && v1 && j->poc[0] == j->poc[1] &&
+                        j->mv_x[0] == j->mv_x[1] && j->mv_y[0] == j->mv_y[1];
+  const int bi = v0 && v1 && !identical;
+  const int lu = v0 ? 0 : 1;
+  int mx[2] = {j->mv_x[0], j->mv_x[1]}, my[2] = {j->mv_y[0], j->mv_y[1]};
+  mc_clip(j, &mx[0], &my[0]); /* xPredInterUni clips its list's MV */
+  mc_clip(j, &mx[1], &my[1]);
+  static int16_t pa[64 * 64], pb[64 * 64];
+  for (int comp = 0; comp < 3; comp++) {
+    const int luma = comp == 0;
+    const int w = luma ? j->w : j->w >> 1, h = luma ? j->h : j->h >> 1;
+    const int x = luma ? j->pu_x : j->pu_x >> 1, y = luma ? j->pu_y : j->pu_y >> 1;
+    const int stride = luma ? ls : cs;
+    int16_t *o = out + (comp == 0 ? 0 : comp == 1 ? j->w * j->h : j->w * j->h + w * h);
+    if (bi) { /* xPredInterBi: both lists as 14-bit intermediates, then xWeightedAverage -> addAvg */
+      mc_pred_blk(luma, planes[3 * j->ref[0] + comp], stride, x, y, mx[0], my[0], w, h, 1, pa);
+      mc_pred_blk(luma, planes[3 * j->ref[1] + comp], stride, x, y, mx[1], my[1], w, h, 1, pb);
+      hvxo_add_avg(pa, pb, o, w * h);
+    } else {
+      mc_pred_blk(luma, planes[3 * j->ref[lu] + comp], stride, x, y, mx[lu], my[lu], w, h, 0, o);
+    }
+  }
+}

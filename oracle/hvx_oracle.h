@@ -58,6 +58,12 @@ float hvxo_stvssim(const uint8_t *const *org_hist, const uint8_t *const *rec_his
                    const float *dirs, int dirs_stride, int w, int h, int wint, int overlap, int gama, int comp,
                    float *ssim, float *ssim3d, float *stvssim);
 double hvxo_lambda_2(int qp);
+/* TComPrediction::motionCompensation for one PU, no WP (TComPrediction.cpp:517-722) + addAvg
+ * (TComYuv.cpp:352): planes[3*r + c] = sample (0,0) of component c of reference r (HM int16
+ * planes); out = Y w*h, Cb, Cr (w/2)*(h/2) */
+void hvxo_mc(const int16_t *const *planes, int luma_stride, int chroma_stride, const hvx_mc_job *j, int16_t *out);
+/* TComYuv::addAvg per sample, 8-bit (TComYuv.cpp:352) */
+void hvxo_add_avg(const int16_t *a, const int16_t *b, int16_t *dst, int n);
 /* TEncSbac::estBit (TEncSbac.cpp:1726): context states (TEncSbac::m_contextModels order,
  * m_ucState bytes) + ContextModel::m_entropyBits -> the estBits entries for a w x h TU of
  * channel type ch (other entries untouched) */

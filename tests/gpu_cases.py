@@ -225,3 +225,73 @@ def check_ctu_pass(seed, width, height, nref, qp, max_ctus=None):
         for ci in range(_abi.CUS_PER_CTU):
             assert got[c][ci].tobytes() == exp[ci].tobytes(), (c, ci, got[c][ci], exp[ci])
     return n
+
+
+# ------------------------------------------------------------------------------------------- MC
+def mc_planes(rng, W, H, n_ref):
+    """HM-like int16 4:2:0 reference planes (margins 80 luma / 40 chroma, borders replicated),
+    smooth random content.  Returns [(array, origin_offset)] * 3*n_ref, strides."""
+    out = []
+    ML, MC = 80, 40
+    for _ in range(n_ref):
+        for c in range(3):
+            w, h, m = (W, H, ML) if c == 0 else (W // 2, H // 2, MC)
+            base = rng.integers(0, 256, size=(h // 4 + 2, w // 4 + 2)).astype(np.float64)
+            img = np.kron(base, np.ones((4, 4)))[:h, :w] + rng.normal(0, 12, size=(h, w))
+            img = np.clip(np.rint(img), 0, 255).astype(np.int16)
+            p = np.pad(img, m, mode="edge")
+            out.append((p, m * p.shape[1] + m))
+    return out, W + 2 * ML, W // 2 + 2 * MC
+
+
+def mc_jobs_random(rng, n, W, H, n_ref):
+    shapes = [(64, 64), (32, 32), (16, 16), (8, 8), (64, 32), (32, 64), (16, 8), (8, 16), (64, 16), (64, 48),
+              (16, 64), (32, 8), (8, 32), (16, 12), (12, 16), (8, 4), (4, 8), (24, 32), (32, 24)]
+    jobs = np.zeros(n, _abi.MC_JOB)
+    off = 0
+    for i in range(n):
+        w, h = shapes[rng.integers(len(shapes))]
+        cu = 64 if max(w, h) > 32 else 32 if max(w, h) > 16 else 16 if max(w, h) > 8 else 8
+        cux = int(rng.integers(0, (W - cu) // cu + 1)) * cu
+        cuy = int(rng.integers(0, (H - cu) // cu + 1)) * cu
+        j = jobs[i]
+        j["pic_w"], j["pic_h"], j["max_cu"], j["cu_x"], j["cu_y"] = W, H, 64, cux, cuy
+        j["pu_x"] = cux + (int(rng.integers(0, (cu - w) // 4 + 1)) * 4 if w < cu else 0)
+        j["pu_y"] = cuy + (int(rng.integers(0, (cu - h) // 4 + 1)) * 4 if h < cu else 0)
+        j["w"], j["h"] = w, h
+        kind = i % 6  # 0/1 uni L0/L1, 2/3 bi, 4 identical (B), 5 identical motion in a P-style job (no shortcut)
+        big = i % 7 == 0  # far MVs exercise clipMv
+        for l in range(2):
+            j["ref"][l] = int(rng.integers(0, n_ref))
+            j["poc"][l] = int(j["ref"][l]) * 2
+            j["mv_x"][l] = int(rng.integers(-700, 701)) if big else int(rng.integers(-96, 97))
+            j["mv_y"][l] = int(rng.integers(-700, 701)) if big else int(rng.integers(-96, 97))
+        if kind == 0:
+            j["ref"][1] = -1
+        elif kind == 1:
+            j["ref"][0] = -1
+        elif kind in (4, 5):
+            j["ref"][1], j["poc"][1] = j["ref"][0], j["poc"][0]
+            j["mv_x"][1], j["mv_y"][1] = j["mv_x"][0], j["mv_y"][0]
+        j["flags"] = _abi.MC_B_SLICE if kind != 5 else 0
+        j["dst_offset"] = off
+        off += w * h + 2 * (w // 2) * (h // 2)
+    return jobs, off
+
+
+def check_mc_random(seed, n, W=320, H=192, n_ref=2):
+    torch = _torch()
+    rng = np.random.default_rng(seed)
+    planes, ls, cs = mc_planes(rng, W, H, n_ref)
+    jobs, total = mc_jobs_random(rng, n, W, H, n_ref)
+    dev = [torch.from_numpy(p.reshape(-1).copy()).cuda() for p, _ in planes]
+    ptrs = torch.tensor([t.data_ptr() + 2 * o for t, (_, o) in zip(dev, planes)], dtype=torch.int64).cuda()
+    dst = torch.zeros(total, dtype=torch.int16, device="cuda")
+    hvx.mc_batch(ptrs, ls, cs, hvx.to_device(jobs), n, dst)
+    torch.cuda.synchronize()
+    got = dst.cpu().numpy()
+    for i in range(n):
+        exp = oracle.mc(planes, ls, cs, jobs[i])
+        o = int(jobs[i]["dst_offset"])
+        np.testing.assert_array_equal(got[o:o + exp.size], exp, err_msg=f"mc job {i}: {jobs[i]}")
+    return True

@@ -164,3 +164,9 @@ def test_estbits_batch_golden_gpu(torch):
     hvx.estbits_batch(d_st, d_eb, d_rc, hvx.to_device(jobs), n, d_io)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(d_io.cpu().numpy().reshape(n, -1), after)
+
+
+def test_mc_random_gpu(torch):
+    # uni L0/L1, bi (addAvg), identical motion with and without the B-slice shortcut, AMP and
+    # 4xN/Nx4 PUs (2-wide chroma), far MVs through clipMv, every luma/chroma fractional phase
+    assert gpu_cases.check_mc_random(seed=17, n=240)

@@ -108,3 +108,9 @@ def test_estbit_golden():
         w, h, ch = (int(x) for x in meta[i, :3])
         got = oracle.estbits_update(states[i], eb, rice[i].astype(np.uint32), w, h, ch, before[i])
         np.testing.assert_array_equal(got, after[i], err_msg=f"record {i} ({w}x{h} ch{ch})")
+
+
+def test_addavg_golden():
+    # TComYuv::addAvg (reference, via oracle/golden_gen.cpp) on random 14-bit intermediates
+    g = gc.load("addavg.bin")
+    np.testing.assert_array_equal(oracle.add_avg(g["in0"], g["in1"]), g["out"])

@@ -63,3 +63,11 @@ PLANE_MARGIN = 80
 def lambda_motion_sad(lam: float) -> int:
     """TComRdCost::setLambda, m_uiLambdaMotionSAD[0] = (UInt)floor(65536.0 * sqrt(lambda)) (TComRdCost.cpp:210)."""
     return int(np.floor(65536.0 * np.sqrt(lam)))
+
+
+# hvx_mc_job (hvx_types.h): 18 int32 + int64 dst_offset at 72 -> 80 bytes
+MC_B_SLICE = 1
+MC_JOB = np.dtype([("pic_w", "<i4"), ("pic_h", "<i4"), ("max_cu", "<i4"), ("cu_x", "<i4"), ("cu_y", "<i4"),
+                   ("pu_x", "<i4"), ("pu_y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("ref", "<i4", (2,)),
+                   ("poc", "<i4", (2,)), ("mv_x", "<i4", (2,)), ("mv_y", "<i4", (2,)), ("flags", "<i4"),
+                   ("dst_offset", "<i8")], align=True)

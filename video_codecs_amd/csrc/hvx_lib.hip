@@ -16,6 +16,7 @@
 #include "hvx_tu.hpp"
 #include "hvx_ctu.hpp"
 #include "hvx_estbit.hpp"
+#include "hvx_mc.hpp"
 
 struct hvx_ctx {
   int device = 0;
@@ -424,6 +425,36 @@ int hvx_me_batch(hvx_ctx *ctx, const uint8_t *const *d_cur_planes, const uint8_t
   hipLaunchKernelGGL(k_me_int, dim3(n), dim3(64), 0, ctx->stream, d_cur_planes, d_ref_planes, stride, d_jobs, n, d_out);
   hipLaunchKernelGGL(k_me_frac, dim3(n), dim3(256), 0, ctx->stream, d_cur_planes, d_ref_planes, stride, d_jobs, n, d_out);
   return launched("k_me");
+}
+
+int hvx_mc_batch(hvx_ctx *ctx, const int16_t *const *d_planes, int luma_stride, int chroma_stride,
+                 const hvx_mc_job *d_jobs, int n, int16_t *d_dst) {
+  if (!ctx || n < 0 || luma_stride <= 0 || chroma_stride <= 0 || (n && (!d_planes || !d_jobs || !d_dst)))
+    return fail(HVX_E_INVALID, "hvx_mc_batch: bad args");
+  if (!n) return HVX_OK;
+  hipLaunchKernelGGL(k_mc, dim3(n), dim3(256), 0, ctx->stream, d_planes, luma_stride, chroma_stride, d_jobs, n, d_dst);
+  return launched("k_mc");
+}
+
+int hvx_alloc(hvx_ctx *ctx, size_t bytes, void **d_out) {
+  if (!ctx || !d_out) return fail(HVX_E_INVALID, "hvx_alloc: NULL");
+  HVX_HIP(hipMalloc(d_out, bytes ? bytes : 1));
+  return HVX_OK;
+}
+int hvx_free(hvx_ctx *ctx, void *d) {
+  if (!ctx) return fail(HVX_E_INVALID, "hvx_free: NULL ctx");
+  if (d) HVX_HIP(hipFree(d));
+  return HVX_OK;
+}
+int hvx_upload(hvx_ctx *ctx, void *d_dst, const void *h_src, size_t bytes) {
+  if (!ctx || (bytes && (!d_dst || !h_src))) return fail(HVX_E_INVALID, "hvx_upload: NULL");
+  if (bytes) HVX_HIP(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return HVX_OK;
+}
+int hvx_download(hvx_ctx *ctx, void *h_dst, const void *d_src, size_t bytes) {
+  if (!ctx || (bytes && (!d_src || !h_dst))) return fail(HVX_E_INVALID, "hvx_download: NULL");
+  if (bytes) HVX_HIP(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  return HVX_OK;
 }
 
 int hvx_estbits_update(const uint8_t *ctx_states, const int32_t *entropy_bits, const uint32_t *rice_stats, int width,
