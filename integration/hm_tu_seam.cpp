@@ -62,6 +62,9 @@ static hvx_ctx *ctx() {
   return g_ctx;
 }
 
+// the one libhvx context of the process, shared with hm_mc_seam.cpp
+hvx_ctx *hvx_seam_ctx() { return ctx(); }
+
 static bool ported(TComTU &rTu, ComponentID compID) {
   TComDataCU *cu = rTu.getCU();
   const UInt idx = rTu.GetAbsPartIdxTU();

@@ -16,6 +16,7 @@ CASES = {  # name: (cfg, yuv kind, frames, qp)
     "intra_rand_qp32": ("intra.cfg", "random", 1, 32),
     "intra_smooth_qp22": ("intra.cfg", "smooth", 1, 22),
     "ldp_smooth_qp32": ("ldp.cfg", "smooth", 3, 32),
+    "ldb_smooth_qp32": ("ldb.cfg", "smooth", 3, 32),  # B slices: bi-prediction, identical-motion shortcut
 }
 W, H = 416, 240
 
