@@ -30,6 +30,7 @@
  *   hvx_stvssim_batch     compute_stVSSIM (stvssim.c:587)
  *   hvx_estbits_update / hvx_estbits_batch   TEncSbac::estBit (TEncSbac.cpp:1726)
  *   hvx_mc_batch          TComPrediction::motionCompensation (TComPrediction.cpp:517)
+ *   hvx_me_full_batch     TEncSearch::xMotionEstimation with xPatternSearch (:3786), incl. bBi
  *   hvx_ctu_analyze       TEncCu::compressCtu's inter 2Nx2N analysis for every CU of every CTU
  *                         (TEncCu.cpp:228,349,1291 -> predInterSearch/encodeResAndCalcRdInterCU):
  *                         the bench workload, composition of the kernels above
@@ -136,6 +137,17 @@ typedef struct hvx_ssim_job {
   int64_t org_off, rec_off;
   int32_t org_stride, rec_stride;
 } hvx_ssim_job;
+/* xMotionEstimation with the integer FULL search (TEncSearch.cpp:3663-3760 with
+ * FastSearch=0 or bBi; xPatternSearch :3786) + xPatternSearchFracDIF.  The search pattern is an
+ * int16 plane: d_tgt_planes[job.cur_idx] (stride tgt_stride) at (pu_x, pu_y) -- the original,
+ * or for bi-prediction refinement the removeHighFreq target 2*org - pred(other list)
+ * (TComYuv.cpp:409).  Search range: job.search_range (BipredSearchRange for bBi) around
+ * (center_x, center_y); HVX_ME_BI weights the final cost by 0.5.  Result as hvx_me_batch
+ * (mv_int/sad_int are the full-search result). */
+int hvx_me_full_batch(hvx_ctx *ctx, const int16_t *const *d_tgt_planes, int tgt_stride,
+                      const uint8_t *const *d_ref_planes, int stride, const hvx_me_job *d_jobs, int n,
+                      hvx_me_result *d_out);
+
 int hvx_ssim_batch(hvx_ctx *ctx, const uint8_t *d_org, const uint8_t *d_rec, const hvx_ssim_job *d_jobs, int n,
                    float *d_out);
 

@@ -70,12 +70,15 @@ typedef struct hvx_me_job {
   int32_t flags;              /* HVX_ME_* below */
   int32_t ref_idx;            /* index into the reference-plane array of a batch */
   int32_t cur_idx;            /* index into the current-plane array of a batch */
+  int32_t center_x, center_y; /* hvx_me_full_batch: xSetSearchRange centre (quarter-pel) -- the
+                                 predictor (FastSearch=0) or the list's current MV rcMv (bBi) */
   int32_t pad_;
 } hvx_me_job;
 
 #define HVX_ME_FEN        1   /* FEN: subsampled SAD when rows > 8 (TEncSearch.cpp:346) */
 #define HVX_ME_HADME      2   /* HadamardME: SATD in fractional refinement */
 #define HVX_ME_SMOOTHMV   4   /* FastMEAssumingSmootherMV: stop first search after 3 rounds */
+#define HVX_ME_BI         8   /* bi-prediction refinement (bBi): final cost weight 0.5 (TEncSearch.cpp:3759) */
 
 typedef struct hvx_me_result {
   int32_t mv_int_x, mv_int_y; /* integer-pel TZ result */

@@ -60,6 +60,7 @@ def lib():
         L.hvxo_ctu_analyze.argtypes = [P, P, I, P, P, I, I, P]
         L.hvxo_estbits_update.argtypes = [P, P, P, I, I, I, P]
         L.hvxo_mc.argtypes = [P, I, I, P, P]
+        L.hvxo_me_full.argtypes = [P, I, P, I, P, P]
         L.hvxo_add_avg.argtypes = [P, P, P, I]
         L.hvxo_dct_matrix.argtypes = [I, P]
         L.hvxo_scan.restype = ctypes.POINTER(ctypes.c_uint32)
@@ -251,3 +252,16 @@ def add_avg(a, b):
     out = np.zeros_like(a)
     lib().hvxo_add_avg(_p(a), _p(b), _p(out), a.size)
     return out
+
+
+def me_full(tgt_block, job, ref_plane, margin=_abi.PLANE_MARGIN):
+    """hvxo_me_full for one ME_JOB: tgt_block = the job's int16 pattern (64x64, stride 64, at
+    the PU), ref_plane = padded uint8 plane.  Returns one ME_RESULT record."""
+    t = _c(tgt_block, np.int16).reshape(-1)
+    j = np.ascontiguousarray(job, dtype=_abi.ME_JOB).reshape(1)
+    r = _c(ref_plane, np.uint8)
+    origin = r.ctypes.data + margin * r.shape[1] + margin
+    virt = t.ctypes.data - 2 * (int(j["pu_y"][0]) * 64 + int(j["pu_x"][0]))  # plane whose (pu_x, pu_y) is the block
+    out = np.zeros(1, _abi.ME_RESULT)
+    lib().hvxo_me_full(ctypes.c_void_p(virt), 64, ctypes.c_void_p(origin), r.shape[1], _p(j), _p(out))
+    return out[0]

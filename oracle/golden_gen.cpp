@@ -459,6 +459,153 @@ static void gen_ssim() {
   gw.write(g_out + "/ssim.bin");
 }
 
+// xMotionEstimation with the integer full search (TEncSearch.cpp:3663-3760, xPatternSearch
+// :3786): FastSearch=0 jobs (SR 16/64 around the predictor, pattern = the original) and
+// bi-prediction refinement jobs (bBi: pattern = removeHighFreq target 2*org - other,
+// TComYuv.cpp:409, unclipped; SR = BipredSearchRange 4 around the list's current MV; final
+// cost weighted by 0.5).
+static void gen_me_full() {
+  const int W = 416, H = 240;
+  SplitMix64 rng(0x5EED1005);
+  GoldenWriter gw;
+  std::vector<int32_t> jobs, res;
+  std::vector<double> lambdas;
+  std::vector<uint8_t> planes;
+  std::vector<int16_t> targets;
+  int njobs = 0;
+
+  TEncCfg cfg;
+  cfg.m_iFastSearch = 0;
+  cfg.m_bUseFastEnc = true;
+  cfg.m_bUseHADME = true;
+  cfg.m_iSearchRange = 64;
+  TComRdCost rd;
+  rd.init();
+  TEncSearch es;
+  es.m_pcEncCfg = &cfg;
+  es.m_pcRdCost = &rd;
+  es.m_iSearchRange = 64;
+  es.m_iFastSearch = 0;
+  es.initTempBuff(CHROMA_420);
+  es.m_cDistParam.bApplyWeight = false;
+
+  TComSPS sps;
+  sps.setPicWidthInLumaSamples(W);
+  sps.setPicHeightInLumaSamples(H);
+  sps.setMaxCUWidth(64);
+  sps.setMaxCUHeight(64);
+  sps.setBitDepth(CHANNEL_TYPE_LUMA, 8);
+  sps.setBitDepth(CHANNEL_TYPE_CHROMA, 8);
+  TComSlice slice;
+  slice.setSPS(&sps);
+  TComDataCU cu;
+  cu.m_pcSlice = &slice;
+
+  for (int pair = 0; pair < 2; pair++) {
+    Plane cur, ref;
+    cur.init(W, H); ref.init(W, H);
+    std::vector<int> tex((W + 64) * (H + 64));
+    for (int y = 0; y < H + 64; y++)
+      for (int x = 0; x < W + 64; x++)
+        tex[y * (W + 64) + x] = (int)(128 + 60 * sin(x * 0.09 + y * 0.04) + 40 * cos(y * 0.12 - x * 0.05)) + rng.range(-6, 6);
+    for (int y = 0; y < H; y++)
+      for (int x = 0; x < W; x++) {
+        if (pair == 0) { ref.org()[y * ref.stride + x] = rng.u8(); cur.org()[y * cur.stride + x] = rng.u8(); }
+        else {
+          int v = tex[(y + 32) * (W + 64) + x + 32];
+          ref.org()[y * ref.stride + x] = v < 0 ? 0 : v > 255 ? 255 : v;
+          int u = tex[(y + 32 - 5) * (W + 64) + x + 32 + 7] + rng.range(-3, 3);
+          cur.org()[y * cur.stride + x] = u < 0 ? 0 : u > 255 ? 255 : u;
+        }
+      }
+    cur.extend(); ref.extend();
+    for (auto &p : {&cur, &ref})
+      for (auto v : p->buf) planes.push_back((uint8_t)v);
+
+    auto shapes = pu_shapes();
+    for (int j = 0; j < 60; j++) {
+      auto wh = shapes[rng.range(0, (int)shapes.size() - 1)];
+      int pw = wh.first, ph = wh.second;
+      int cuSize = 64;
+      while (cuSize > 8 && (cuSize / 2 >= pw && cuSize / 2 >= ph)) cuSize >>= 1;
+      if (pw < cuSize && ph < cuSize && cuSize > 8) cuSize = std::max(pw, ph);
+      int ctux = rng.range(0, (W - 1) / 64), ctuy = rng.range(0, (H - 1) / 64);
+      int cux = ctux * 64 + rng.range(0, 64 / cuSize - 1) * cuSize;
+      int cuy = ctuy * 64 + rng.range(0, 64 / cuSize - 1) * cuSize;
+      int pux = cux + (pw < cuSize ? rng.range(0, (cuSize - pw) / 4) * 4 : 0);
+      int puy = cuy + (ph < cuSize ? rng.range(0, (cuSize - ph) / 4) * 4 : 0);
+      if (pux + pw > cux + cuSize) pux = cux + cuSize - pw;
+      if (puy + ph > cuy + cuSize) puy = cuy + cuSize - ph;
+      if (pux + pw > W || puy + ph > H) { j--; continue; }
+      cu.m_uiCUPelX = cux;
+      cu.m_uiCUPelY = cuy;
+      int qp = rng.range(22, 37);
+      double lambda = 0.57 * pow(2.0, (qp - 12) / 3.0) * (rng.range(0, 1) ? 1.0 : 0.68);
+      rd.setLambda(lambda, sps.getBitDepths());
+      const bool bi = (j % 2) == 1;
+      const int sr = bi ? 4 : ((j % 4) == 0 ? 64 : 16);
+      TComMv pred(rng.range(-40, 40), rng.range(-40, 40));
+      if (j % 7 == 3) pred.set(rng.range(-700, 700), rng.range(-500, 500));  // far / clipped predictor
+      TComMv center = bi ? TComMv(pred.getHor() + rng.range(-24, 24), pred.getVer() + rng.range(-24, 24)) : pred;
+      if (bi && j % 9 == 5) center.set(rng.range(-600, 600), rng.range(-400, 400));
+      UInt bitsIn = rng.range(0, 9);
+
+      // the search pattern: the original, or the bi target 2*org - other (removeHighFreq, no clip)
+      std::vector<Pel> tgt(64 * 64, 0);
+      for (int y = 0; y < ph; y++)
+        for (int x = 0; x < pw; x++) {
+          const int o = cur.org()[(puy + y) * cur.stride + pux + x];
+          const int other = bi ? (int)((o + rng.range(-40, 40)) < 0 ? 0 : (o + rng.range(-40, 40)) > 255 ? 255 : (o + rng.range(-40, 40))) : 0;
+          tgt[y * 64 + x] = (Pel)(bi ? 2 * o - other : o);
+        }
+      TComPattern pat;
+      pat.initPattern(tgt.data(), pw, ph, 64, 8);
+      Pel *piRefY = ref.org() + puy * ref.stride + pux;
+      TComMv lt, rb, mv;
+      es.xSetSearchRange(&cu, center, sr, lt, rb);
+      rd.getMotionCost(true, 0, false);
+      rd.setPredictor(pred);
+      rd.setCostScale(2);
+      Distortion sad = 0;
+      es.xPatternSearch(&pat, piRefY, ref.stride, &lt, &rb, mv, sad);
+      TComMv mvInt = mv;
+      Distortion sadInt = sad;
+      rd.getMotionCost(true, 0, false);
+      rd.setCostScale(1);
+      TComMv half, qter;
+      Distortion cost = 0;
+      es.xPatternSearchFracDIF(false, &pat, piRefY, ref.stride, &mv, half, qter, cost);
+      TComMv mvHalf = half, mvQ = qter;
+      Distortion costFrac = cost;
+      rd.setCostScale(0);
+      mv <<= 2;
+      mv += (half <<= 1);
+      mv += qter;
+      UInt mvBits = rd.getBits(mv.getHor(), mv.getVer());
+      UInt bits = bitsIn + mvBits;
+      const double wgt = bi ? 0.5 : 1.0;
+      Distortion fin = (Distortion)(floor(wgt * ((Double)costFrac - (Double)rd.getCost(mvBits))) + (Double)rd.getCost(bits));
+
+      jobs.insert(jobs.end(), {pair, cux, cuy, pux, puy, pw, ph, pred.getHor(), pred.getVer(), bi ? 1 : 0,
+                               center.getHor(), center.getVer(), (int)bitsIn, qp, sr});
+      lambdas.push_back(lambda);
+      targets.insert(targets.end(), tgt.begin(), tgt.end());
+      res.insert(res.end(), {mvInt.getHor(), mvInt.getVer(), (int)sadInt, mvHalf.getHor(), mvHalf.getVer(),
+                             mvQ.getHor(), mvQ.getVer(), (int)costFrac, mv.getHor(), mv.getVer(), (int)bits, (int)fin});
+      njobs++;
+    }
+  }
+  gw.add("dims", "i32", {4}, std::vector<int32_t>{W, H, MARGIN, 64});
+  gw.add("planes", "u8", {2, 2, (uint32_t)(H + 2 * MARGIN), (uint32_t)(W + 2 * MARGIN)}, planes);
+  gw.add("jobs", "i32", {(uint32_t)njobs, 15}, jobs);
+  gw.add("lambda", "f64", {(uint32_t)njobs}, lambdas);
+  gw.add("targets", "i16", {(uint32_t)njobs, 64, 64}, targets);
+  gw.add("res", "i32", {(uint32_t)njobs, 12}, res);
+  gw.write(g_out + "/me_full.bin");
+  es.m_pcEncCfg = NULL;
+  cu.m_pcSlice = NULL;
+}
+
 // TComYuv::addAvg (TComYuv.cpp:352) on random 14-bit intermediates, 4:2:0, several PU sizes
 static void gen_addavg() {
   SplitMix64 rng(0x5EED0A06);
@@ -516,6 +663,7 @@ int main(int argc, char **argv) {
   gen_me();
   gen_ssim();
   gen_addavg();
+  gen_me_full();
   destroyROM();
   return 0;
 }

@@ -888,6 +888,7 @@ void hvxo_inv_transform_nxn(const hvx_tu_desc *tu, const int32_t *levels, int16_
  * ========================================================================================== */
 typedef struct {
   const uint8_t *org; int so;  /* PU origin in the current plane */
+  const int16_t *org16;        /* or an int16 pattern (full search / bi target), stride so */
   const uint8_t *ref; int sr;  /* PU origin in the reference plane (MV 0) */
   int w, h, sub;
   uint32_t lam;                /* m_uiCost */
@@ -1112,7 +1113,7 @@ static uint32_t pattern_refine(tz_state *t, int use_had, int base_qx, int base_q
   int bi = 0;
   int16_t org[64 * 64], blk[64 * 64];
   for (int y = 0; y < t->h; y++)
-    for (int x = 0; x < t->w; x++) org[y * 64 + x] = t->org[y * t->so + x];
+    for (int x = 0; x < t->w; x++) org[y * 64 + x] = t->org16 ? t->org16[y * t->so + x] : t->org[y * t->so + x];
   for (int i = 0; i < 9; i++) {
     int qx = base_qx + ref[i][0] * frac, qy = base_qy + ref[i][1] * frac;
     hvxo_luma_block_qpel(t->ref, t->sr, 0, 0, qx, qy, t->w, t->h, blk, 64);
@@ -1128,6 +1129,7 @@ static uint32_t pattern_refine(tz_state *t, int use_had, int base_qx, int base_q
 void hvxo_motion_estimation(const uint8_t *cur, int cur_stride, const uint8_t *refp, int ref_stride,
                             const hvx_me_job *j, hvx_me_result *r) {
   tz_state t;
+  t.org16 = NULL;
   t.org = cur + j->pu_y * cur_stride + j->pu_x; t.so = cur_stride;
   t.ref = refp + j->pu_y * ref_stride + j->pu_x; t.sr = ref_stride;
   t.w = j->w; t.h = j->h;
@@ -1518,4 +1520,53 @@ void hvxo_mc(const int16_t *const *planes, int ls, int cs, const hvx_mc_job *j, 
       mc_pred_blk(luma, planes[3 * j->ref[lu] + comp], stride, x, y, mx[lu], my[lu], w, h, 0, o);
     }
   }
+}
+
+
+/* xMotionEstimation with the integer full search (TEncSearch.cpp:3663-3760, FastSearch=0 or
+ * bBi): xSetSearchRange around (center_x, center_y) (:3765), xPatternSearch (:3786; FEN
+ * subsampling when rows > 8 :3810, strict '<' in raster order), xPatternSearchFracDIF, and the
+ * final cost with fWeight 0.5 for bBi (:3696, :3759).  tgt: int16 pattern plane (sample 0,0). */
+void hvxo_me_full(const int16_t *tgt, int tstride, const uint8_t *refp, int ref_stride, const hvx_me_job *j,
+                  hvx_me_result *r) {
+  tz_state t;
+  memset(&t, 0, sizeof(t));
+  t.org = NULL;
+  t.org16 = tgt + j->pu_y * tstride + j->pu_x; t.so = tstride;
+  t.ref = refp + j->pu_y * ref_stride + j->pu_x; t.sr = ref_stride;
+  t.w = j->w; t.h = j->h;
+  const int w = j->w;
+  const int spec = (w == 4 || w == 8 || w == 16 || w == 32 || w == 64 || w == 12 || w == 24 || w == 48);
+  const int sub = ((j->flags & HVX_ME_FEN) && j->h > 8 && spec) ? 1 : 0;
+  t.lam = j->lambda_motion;
+  t.px = j->pred_x; t.py = j->pred_y;
+  srch_rng g;
+  set_search_range(j, j->center_x, j->center_y, j->search_range, &g);
+  t.cost_scale = 2;
+  uint32_t best = 0xFFFFFFFFu;
+  int bx = 0, by = 0;
+  for (int y = g.t; y <= g.b; y++)
+    for (int x = g.l; x <= g.r; x++) {
+      const uint8_t *c = t.ref + y * ref_stride + x;
+      uint32_t s = 0;
+      for (int row = 0; row < t.h; row += 1 << sub)
+        for (int col = 0; col < w; col++) s += (uint32_t)abs((int)t.org16[row * tstride + col] - (int)c[row * ref_stride + col]);
+      s = (s << sub) + mv_cost(&t, x, y);
+      if (s < best) { best = s; bx = x; by = y; }
+    }
+  r->mv_int_x = bx; r->mv_int_y = by; r->sad_int = best - mv_cost(&t, bx, by);
+  const int had = (j->flags & HVX_ME_HADME) != 0;
+  t.cost_scale = 1;
+  int hx = bx << 1, hy = by << 1;
+  uint32_t cost = pattern_refine(&t, had, bx << 2, by << 2, 2, &hx, &hy);
+  t.cost_scale = 0;
+  int qx = ((bx << 1) + hx) << 1, qy = ((by << 1) + hy) << 1;
+  cost = pattern_refine(&t, had, (bx << 2) + (hx << 1), (by << 2) + (hy << 1), 1, &qx, &qy);
+  r->half_x = hx; r->half_y = hy; r->qtr_x = qx; r->qtr_y = qy; r->cost_frac = cost;
+  const int fmx = (bx << 2) + (hx << 1) + qx, fmy = (by << 2) + (hy << 1) + qy;
+  const uint32_t mv_bits = hvxo_eg_bits(fmx - t.px) + hvxo_eg_bits(fmy - t.py);
+  const uint32_t bits = (uint32_t)j->bits_in + mv_bits;
+  const double wgt = (j->flags & HVX_ME_BI) ? 0.5 : 1.0;
+  r->mv_x = fmx; r->mv_y = fmy; r->bits = bits;
+  r->cost = (uint32_t)(floor(wgt * ((double)cost - (double)((t.lam * mv_bits) >> 16))) + (double)((t.lam * bits) >> 16));
 }

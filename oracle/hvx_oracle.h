@@ -62,6 +62,9 @@ double hvxo_lambda_2(int qp);
  * (TComYuv.cpp:352): planes[3*r + c] = sample (0,0) of component c of reference r (HM int16
  * planes); out = Y w*h, Cb, Cr (w/2)*(h/2) */
 void hvxo_mc(const int16_t *const *planes, int luma_stride, int chroma_stride, const hvx_mc_job *j, int16_t *out);
+/* xMotionEstimation with the integer full search (FastSearch=0 / bBi), int16 pattern plane */
+void hvxo_me_full(const int16_t *tgt, int tstride, const uint8_t *refp, int ref_stride, const hvx_me_job *j,
+                  hvx_me_result *r);
 /* TComYuv::addAvg per sample, 8-bit (TComYuv.cpp:352) */
 void hvxo_add_avg(const int16_t *a, const int16_t *b, int16_t *dst, int n);
 /* TEncSbac::estBit (TEncSbac.cpp:1726): context states (TEncSbac::m_contextModels order,

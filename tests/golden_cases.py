@@ -76,3 +76,21 @@ def me_jobs(g):
     jobs["lambda_motion"] = [_abi.lambda_motion_sad(l) for l in g["lambda"]]
     jobs["flags"] = _abi.ME_FEN | _abi.ME_HADME | _abi.ME_SMOOTHMV
     return g["planes"], jobs, g["res"]
+
+
+def me_full_jobs(g):
+    """me_full.bin -> (planes[pair][cur/ref], ME_JOB array, int16 targets [n,64,64], expected [n,12]).
+    job.cur_idx = the record index (one virtual target plane per job)."""
+    W, H, margin, maxcu = (int(x) for x in g["dims"])
+    j = g["jobs"]
+    n = j.shape[0]
+    jobs = np.zeros(n, _abi.ME_JOB)
+    jobs["pic_w"], jobs["pic_h"], jobs["max_cu"] = W, H, maxcu
+    jobs["cur_idx"] = np.arange(n)
+    jobs["ref_idx"] = j[:, 0]
+    jobs["cu_x"], jobs["cu_y"], jobs["pu_x"], jobs["pu_y"] = j[:, 1], j[:, 2], j[:, 3], j[:, 4]
+    jobs["w"], jobs["h"], jobs["pred_x"], jobs["pred_y"] = j[:, 5], j[:, 6], j[:, 7], j[:, 8]
+    jobs["center_x"], jobs["center_y"], jobs["bits_in"], jobs["search_range"] = j[:, 10], j[:, 11], j[:, 12], j[:, 14]
+    jobs["lambda_motion"] = [_abi.lambda_motion_sad(l) for l in g["lambda"]]
+    jobs["flags"] = _abi.ME_FEN | _abi.ME_HADME | np.where(j[:, 9] != 0, _abi.ME_BI, 0)
+    return g["planes"], jobs, g["targets"], g["res"]

@@ -295,3 +295,26 @@ def check_mc_random(seed, n, W=320, H=192, n_ref=2):
         o = int(jobs[i]["dst_offset"])
         np.testing.assert_array_equal(got[o:o + exp.size], exp, err_msg=f"mc job {i}: {jobs[i]}")
     return True
+
+
+def check_me_full_golden():
+    """hvx_me_full_batch vs the reference's xPatternSearch / bi refinement (me_full.bin)."""
+    torch = _torch()
+    g = gc.load("me_full.bin")
+    planes, jobs, tg, exp = gc.me_full_jobs(g)
+    n = len(jobs)
+    ref_t, ref_p = device_planes([planes[p, 1] for p in range(planes.shape[0])])
+    stride = planes.shape[-1]
+    d_tg = torch.from_numpy(np.ascontiguousarray(tg).reshape(-1)).cuda()
+    base = d_tg.data_ptr()
+    # one virtual int16 plane per job whose (pu_x, pu_y) is the job's 64x64 pattern block
+    tptr = [base + 2 * (i * 4096 - (int(jobs[i]["pu_y"]) * 64 + int(jobs[i]["pu_x"]))) for i in range(n)]
+    d_tp = torch.tensor(tptr, dtype=torch.int64).cuda()
+    out = torch.zeros(n * _abi.ME_RESULT.itemsize, dtype=torch.uint8, device="cuda")
+    hvx.me_full_batch(d_tp, 64, ref_p, stride, hvx.to_device(jobs), n, out)
+    torch.cuda.synchronize()
+    got = hvx.from_device(out, _abi.ME_RESULT)
+    for i in range(n):
+        assert [int(x) for x in got[i]] == [int(x) for x in exp[i]], (i, jobs[i], got[i], exp[i])
+    del ref_t
+    return n

@@ -170,3 +170,7 @@ def test_mc_random_gpu(torch):
     # uni L0/L1, bi (addAvg), identical motion with and without the B-slice shortcut, AMP and
     # 4xN/Nx4 PUs (2-wide chroma), far MVs through clipMv, every luma/chroma fractional phase
     assert gpu_cases.check_mc_random(seed=17, n=240)
+
+
+def test_me_full_golden_gpu(torch):
+    assert gpu_cases.check_me_full_golden() == 120

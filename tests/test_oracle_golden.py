@@ -114,3 +114,12 @@ def test_addavg_golden():
     # TComYuv::addAvg (reference, via oracle/golden_gen.cpp) on random 14-bit intermediates
     g = gc.load("addavg.bin")
     np.testing.assert_array_equal(oracle.add_avg(g["in0"], g["in1"]), g["out"])
+
+
+def test_me_full_golden():
+    # xMotionEstimation with xPatternSearch (FastSearch=0, SR 16/64) and the bi-pred
+    # refinement (bBi: 2*org-other target, SR 4, weight 0.5), from the reference (golden_gen.cpp)
+    planes, jobs, tg, exp = gc.me_full_jobs(gc.load("me_full.bin"))
+    for i in range(len(jobs)):
+        r = oracle.me_full(tg[i], jobs[i], planes[int(jobs[i]["ref_idx"]), 1])
+        assert [int(x) for x in r] == [int(x) for x in exp[i]], (i, jobs[i], r, exp[i])

@@ -21,15 +21,15 @@ ESTBITS = np.dtype([("v", "<i4", (ESTBITS_INTS,))])
 ME_JOB = np.dtype([(f, "<u4" if f == "lambda_motion" else "<i4") for f in (
     "pic_w", "pic_h", "max_cu", "cu_x", "cu_y", "pu_x", "pu_y", "w", "h", "pred_x", "pred_y",
     "use_int2nx2n", "i2_x", "i2_y", "bits_in", "search_range", "lambda_motion", "flags", "ref_idx",
-    "cur_idx", "pad_")])
-assert ME_JOB.itemsize == 84
+    "cur_idx", "center_x", "center_y", "pad_")])
+assert ME_JOB.itemsize == 92
 
 ME_RESULT = np.dtype([(f, "<u4" if f in ("sad_int", "cost_frac", "bits", "cost") else "<i4") for f in (
     "mv_int_x", "mv_int_y", "sad_int", "half_x", "half_y", "qtr_x", "qtr_y", "cost_frac",
     "mv_x", "mv_y", "bits", "cost")])
 assert ME_RESULT.itemsize == 48
 
-ME_FEN, ME_HADME, ME_SMOOTHMV = 1, 2, 4
+ME_FEN, ME_HADME, ME_SMOOTHMV, ME_BI = 1, 2, 4, 8
 
 CTU_PARAMS = np.dtype([("pic_w", "<i4"), ("pic_h", "<i4"), ("n_ref", "<i4"), ("qp", "<i4"), ("search_range", "<i4"),
                        ("me_flags", "<i4"), ("slice_type", "<i4"), ("lambda_motion", "<u4"), ("lambda", "<f8")], align=True)

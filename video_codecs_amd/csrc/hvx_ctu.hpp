@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void k_ctu_me_jobs(CtuLayout L, hvx_ctu_params
   jb.search_range = P.search_range;
   jb.lambda_motion = P.lambda_motion;
   jb.flags = P.me_flags;
-  jb.ref_idx = ref; jb.cur_idx = 0; jb.pad_ = 0;
+  jb.ref_idx = ref; jb.cur_idx = 0; jb.center_x = jb.center_y = 0; jb.pad_ = 0;
   jobs[((size_t)ctu * HVX_CUS_PER_CTU + ci) * L.nref + ref] = jb;
 }
 

@@ -476,6 +476,17 @@ int hvx_estbits_batch(hvx_ctx *ctx, const uint8_t *d_states, const int32_t *d_en
   return launched("k_estbits");
 }
 
+int hvx_me_full_batch(hvx_ctx *ctx, const int16_t *const *d_tgt_planes, int tgt_stride,
+                      const uint8_t *const *d_ref_planes, int stride, const hvx_me_job *d_jobs, int n,
+                      hvx_me_result *d_out) {
+  if (!ctx || n < 0 || stride <= 0 || tgt_stride <= 0 || (n && (!d_tgt_planes || !d_ref_planes || !d_jobs || !d_out)))
+    return fail(HVX_E_INVALID, "hvx_me_full_batch: bad args");
+  if (!n) return HVX_OK;
+  hipLaunchKernelGGL(k_me_full, dim3(n), dim3(256), 0, ctx->stream, d_tgt_planes, tgt_stride, d_ref_planes, stride, d_jobs,
+                     n, d_out);
+  return launched("k_me_full");
+}
+
 int hvx_ssim_batch(hvx_ctx *ctx, const uint8_t *d_org, const uint8_t *d_rec, const hvx_ssim_job *d_jobs, int n,
                    float *d_out) {
   if (!ctx || n < 0 || (n && (!d_org || !d_rec || !d_jobs || !d_out))) return fail(HVX_E_INVALID, "hvx_ssim_batch: bad args");

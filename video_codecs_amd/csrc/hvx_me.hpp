@@ -461,20 +461,20 @@ __constant__ int8_t kRefQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {
 // Fractional-search LDS image for blocks up to SxS, NW waves per job.  The phase planes use
 // a row stride of S+8 int16: an 8x8 tile row of 8 samples then covers 4 banks and the 8
 // rows of a tile land on disjoint banks (conflict-free cross-lane tiles).
-template <int S, int NW>
+template <int S, int NW, typename TO = uint8_t>
 struct MeFracSmem {
   static constexpr int HS = S + 8;
   int16_t hp[3][(S + 8) * HS];  // first-stage intermediates of the 3 horizontal phases, rows iy-4 ..
   uint8_t blk[NW][S * S];       // per-wave candidate block (per-lane-tile SATD path)
-  uint8_t org[S * S];
+  TO org[S * S];                // the search pattern: the original (8-bit) or a bi target (int16)
   uint32_t cost[9];
 };
 
 // one prediction sample of candidate column phase c at vertical quarter position qy
 // (relative to the integer MV row iy): the reference's second filter stage on hp[c]
-template <int S, int NW>
-__device__ __forceinline__ int me_frac_sample(const MeFracSmem<S, NW> &sm, int c, int ry, int fy, int x, int y) {
-  constexpr int HS = MeFracSmem<S, NW>::HS;
+template <int S, int NW, typename TO>
+__device__ __forceinline__ int me_frac_sample(const MeFracSmem<S, NW, TO> &sm, int c, int ry, int fy, int x, int y) {
+  constexpr int HS = MeFracSmem<S, NW, TO>::HS;
   const int16_t *h = sm.hp[c] + x;
   if (!fy) return clip_pel((h[(ry + 4 + y) * HS] + 8192 + 32) >> 6);
   int s = 0;
@@ -501,10 +501,10 @@ __device__ __forceinline__ uint32_t had8_xlane(int v) {
 // quarter-pel relative to the PU, step 2 (half) or 1 (quarter); (ix,iy) the integer MV.
 // The NW waves of the job share the phase planes and take candidates i = wave, wave+NW, ...
 // GENERIC: any block shape up to SxS; otherwise square SxS blocks only (the CTU pass).
-template <int S, int NW, bool GENERIC>
-__device__ uint32_t me_frac_stage(MeFracSmem<S, NW> &sm, const hvx_me_job &j, const uint8_t *ref, int stride, int ix,
+template <int S, int NW, bool GENERIC, typename TO>
+__device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j, const uint8_t *ref, int stride, int ix,
                                   int iy, int qx0, int qy0, int step, int scale, int mvx0, int mvy0, int &bi) {
-  constexpr int HS = MeFracSmem<S, NW>::HS;
+  constexpr int HS = MeFracSmem<S, NW, TO>::HS;
   const int w = GENERIC ? j.w : S, h = GENERIC ? j.h : S, lane = lane_id(), wave = threadIdx.x >> 6;
   const bool had = (j.flags & HVX_ME_HADME) != 0;
   // 1. horizontal phases: column c at quarter x = qx0 + (c-1)*step.  Integer offsets of the
@@ -642,9 +642,9 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW> &sm, const hvx_me_job &j, co
   return best;
 }
 
-template <int S, int NW, bool GENERIC>
+template <int S, int NW, bool GENERIC, typename TO>
 __device__ void me_frac_refine(const hvx_me_job &j, const uint8_t *ref, int stride, int ix, int iy, uint32_t sad_int,
-                               MeFracSmem<S, NW> &sm, hvx_me_result *out);
+                               MeFracSmem<S, NW, TO> &sm, hvx_me_result *out);
 
 template <int S, int NW, bool GENERIC>
 __device__ void me_frac_job(const hvx_me_job &j, const uint8_t *const *__restrict__ cur_planes,
@@ -660,20 +660,20 @@ __device__ void me_frac_job(const hvx_me_job &j, const uint8_t *const *__restric
     sm.org[y * S + x] = cur[y * stride + x];
   }
   const uint8_t *ref = ref_planes[j.ref_idx] + j.pu_y * stride + j.pu_x;
-  me_frac_refine<S, NW, GENERIC>(j, ref, stride, ix, iy, sad_int, sm, out);
+  me_frac_refine<S, NW, GENERIC, uint8_t>(j, ref, stride, ix, iy, sad_int, sm, out);
 }
 
 // xPatternSearchFracDIF (:4240) from the integer result (ix, iy, sad_int), the original block
 // already in sm.org; writes the complete hvx_me_result.
-template <int S, int NW, bool GENERIC>
+template <int S, int NW, bool GENERIC, typename TO>
 __device__ void me_frac_refine(const hvx_me_job &j, const uint8_t *ref, int stride, int ix, int iy, uint32_t sad_int,
-                               MeFracSmem<S, NW> &sm, hvx_me_result *out) {
+                               MeFracSmem<S, NW, TO> &sm, hvx_me_result *out) {
   // half-pel around the integer MV, then quarter-pel
   int bh, bq;
-  me_frac_stage<S, NW, GENERIC>(sm, j, ref, stride, ix, iy, ix << 2, iy << 2, 2, 1, ix << 1, iy << 1, bh);
+  me_frac_stage<S, NW, GENERIC, TO>(sm, j, ref, stride, ix, iy, ix << 2, iy << 2, 2, 1, ix << 1, iy << 1, bh);
   const int hx = kRefH[bh][0], hy = kRefH[bh][1];
   const int cqx = (ix << 2) + (hx << 1), cqy = (iy << 2) + (hy << 1);
-  const uint32_t cost = me_frac_stage<S, NW, GENERIC>(sm, j, ref, stride, ix, iy, cqx, cqy, 1, 0, cqx, cqy, bq);
+  const uint32_t cost = me_frac_stage<S, NW, GENERIC, TO>(sm, j, ref, stride, ix, iy, cqx, cqy, 1, 0, cqx, cqy, bq);
   const int qx = kRefQ[bq][0], qy = kRefQ[bq][1];
   const int fmx = cqx + qx, fmy = cqy + qy;
   const uint32_t mv_bits = eg_bits(fmx - j.pred_x) + eg_bits(fmy - j.pred_y);
@@ -684,7 +684,8 @@ __device__ void me_frac_refine(const hvx_me_job &j, const uint8_t *ref, int stri
     r.mv_int_x = ix; r.mv_int_y = iy; r.sad_int = sad_int;
     r.half_x = hx; r.half_y = hy; r.qtr_x = qx; r.qtr_y = qy; r.cost_frac = cost;
     r.mv_x = fmx; r.mv_y = fmy; r.bits = bits;
-    r.cost = (uint32_t)(floor(1.0 * ((double)cost - (double)((lam * mv_bits) >> 16))) + (double)((lam * bits) >> 16));
+    const double wgt = (j.flags & HVX_ME_BI) ? 0.5 : 1.0;  // fWeight (TEncSearch.cpp:3696, :3759)
+    r.cost = (uint32_t)(floor(wgt * ((double)cost - (double)((lam * mv_bits) >> 16))) + (double)((lam * bits) >> 16));
     *out = r;
   }
 }
@@ -746,5 +747,62 @@ __global__ __launch_bounds__(64 * NW) void k_me_ctu(const uint8_t *const *__rest
   m.px = j.pred_x; m.py = j.pred_y;
   me_tz<S, SUB, NW>(j, m);
   const uint32_t sad_int = m.best_sad - me_mv_cost(m.lam, m.px, m.py, 2, m.best_x, m.best_y);
-  me_frac_refine<S, NW, false>(j, m.ref, stride, m.best_x, m.best_y, sad_int, sm, out + slot);
+  me_frac_refine<S, NW, false, uint8_t>(j, m.ref, stride, m.best_x, m.best_y, sad_int, sm, out + slot);
+}
+
+// ======================================================================================
+// integer full search: xMotionEstimation with FastSearch=0 or bBi (TEncSearch.cpp:3728-3730)
+// ======================================================================================
+// xPatternSearch (:3786): every integer position of the (clipped) range around the centre in
+// raster order, strict '<' -> the first minimum of SAD + MV cost.  One 256-thread workgroup
+// per job: thread t takes points t, t+256, ... and keeps its first minimum as a
+// (cost, raster index) key; a workgroup key-min picks the reference's point.  The pattern is
+// int16 (a bi target 2*org - other spans [-255, 510]), so SADs are plain |a - b| sums.
+__global__ __launch_bounds__(256) void k_me_full(const int16_t *const *__restrict__ tgt_planes, int tstride,
+                                                const uint8_t *const *__restrict__ ref_planes, int stride,
+                                                const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
+  __shared__ MeFracSmem<64, 4, int16_t> sm;
+  __shared__ uint64_t wkey[4];
+  const int jid = blockIdx.x;
+  if (jid >= n) return;
+  const hvx_me_job j = jobs[jid];
+  if (j.w <= 0 || j.h <= 0 || j.w > 64 || j.h > 64) {
+    if (threadIdx.x == 0) { hvx_me_result z; memset(&z, 0, sizeof(z)); out[jid] = z; }
+    return;
+  }
+  const int16_t *tg = tgt_planes[j.cur_idx] + (size_t)j.pu_y * tstride + j.pu_x;
+  for (int k = threadIdx.x; k < j.w * j.h; k += 256) {
+    const int y = k / j.w, x = k - y * j.w;
+    sm.org[y * 64 + x] = tg[y * tstride + x];
+  }
+  __syncthreads();
+  const uint8_t *ref = ref_planes[j.ref_idx] + j.pu_y * stride + j.pu_x;
+  const MeRange g = me_search_range(j, j.center_x, j.center_y, j.search_range);
+  // FEN (m_bUseFastEnc) subsamples rows when iRows > 8 (:3810); the reference's specialised
+  // SAD widths honour iSubShift, the generic one does not (TComRdCost.cpp:461-950)
+  const int w = j.w;
+  const bool spec = (w == 4 || w == 8 || w == 16 || w == 32 || w == 64 || w == 12 || w == 24 || w == 48);
+  const int sub = ((j.flags & HVX_ME_FEN) && j.h > 8 && spec) ? 1 : 0;
+  const int nx = g.r - g.l + 1, np = nx * (g.b - g.t + 1);
+  uint64_t best = ~0ull;
+  for (int p = threadIdx.x; p < np; p += 256) {
+    const int py = p / nx, x = g.l + (p - py * nx), y = g.t + py;
+    const uint8_t *r = ref + y * stride + x;
+    uint32_t s = 0;
+    for (int row = 0; row < j.h; row += 1 << sub)
+      for (int c = 0; c < w; c++) s += (uint32_t)abs((int)sm.org[row * 64 + c] - (int)r[row * stride + c]);
+    const uint32_t cost = (s << sub) + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, 2, x, y);
+    const uint64_t key = ((uint64_t)cost << 32) | (uint32_t)p;
+    best = key < best ? key : best;
+  }
+  best = wave_min_u64(best);
+  if (lane_id() == 0) wkey[threadIdx.x >> 6] = best;
+  __syncthreads();
+  best = wkey[0];
+  for (int k = 1; k < 4; k++) best = wkey[k] < best ? wkey[k] : best;
+  const int bp = (int)(uint32_t)best, by = bp / nx;
+  const int ix = g.l + (bp - by * nx), iy = g.t + by;
+  const uint32_t sad_int = (uint32_t)(best >> 32) - me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, 2, ix, iy);
+  // the fractional refinement reads the same pattern (stride 64 = S)
+  me_frac_refine<64, 4, true, int16_t>(j, ref, stride, ix, iy, sad_int, sm, out + jid);
 }

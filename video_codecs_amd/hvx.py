@@ -44,7 +44,7 @@ def lib():
             "hvx_ctu_analyze": [P, P, P, I, P, P, P, ctypes.c_size_t, P],
             "hvx_set_timing": [P, I], "hvx_phase_times": [P, ctypes.POINTER(ctypes.c_double), I, I],
             "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
-            "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
+            "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
             "hvx_free": [P, P], "hvx_upload": [P, P, P, ctypes.c_size_t], "hvx_download": [P, P, P, ctypes.c_size_t],
         }.items():
             f = getattr(L, name)
@@ -168,6 +168,11 @@ def estbits_update(states, entropy_bits, rice, w, h, ch, est_in):
 def estbits_batch(states_dev, entropy_dev, rice_dev, jobs_dev, n, inout_dev):
     _check(lib().hvx_estbits_batch(context(), _ptr(states_dev), _ptr(entropy_dev), _ptr(rice_dev), _ptr(jobs_dev), n,
                                    _ptr(inout_dev)), "hvx_estbits_batch")
+
+
+def me_full_batch(tgt_planes, tgt_stride, ref_planes, stride, jobs_dev, n, out):
+    _check(lib().hvx_me_full_batch(context(), _ptr(tgt_planes), int(tgt_stride), _ptr(ref_planes), int(stride),
+                                   _ptr(jobs_dev), n, _ptr(out)), "hvx_me_full_batch")
 
 
 def mc_batch(plane_ptrs_dev, luma_stride, chroma_stride, jobs_dev, n, dst):
