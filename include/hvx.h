@@ -211,7 +211,8 @@ int hvx_estbits_batch(hvx_ctx *ctx, const uint8_t *d_states, const int32_t *d_en
  * CTU analysis pass over a whole picture (hvx_types.h): d_cur = sample (0,0) of the current
  * 8-bit padded plane, d_refs = device array of n_ref reference-plane origins, d_est4 = device
  * array of 4 luma estBits tables (TU 4x4..32x32), d_out = nctu*85 hvx_cu_result.  The
- * caller allocates a device workspace of hvx_ctu_workspace_size() bytes.
+ * caller allocates a device workspace of hvx_ctu_workspace_size() bytes.  Planes carry the
+ * HVX_PLANE_MARGIN border and a stride that is a multiple of 4 (HVX_E_INVALID otherwise).
  * ------------------------------------------------------------------------------------- */
 int hvx_ctu_workspace_size(int pic_w, int pic_h, int n_ref, size_t *bytes);
 int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,

@@ -536,7 +536,7 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
     return fail(HVX_E_INVALID, "hvx_ctu_analyze: NULL argument");
   const hvx_ctu_params P = *h_params;
   if (P.pic_w <= 0 || P.pic_h <= 0 || P.n_ref <= 0 || P.n_ref > 8 || P.qp < 0 || P.qp > 51 ||
-      stride < P.pic_w + 2 * HVX_PLANE_MARGIN || P.search_range <= 0 || P.search_range > 256)
+      stride < P.pic_w + 2 * HVX_PLANE_MARGIN || stride % 4 != 0 || P.search_range <= 0 || P.search_range > 256)
     return fail(HVX_E_INVALID, "hvx_ctu_analyze: bad parameters");
   const CtuLayout L = ctu_layout(P.pic_w, P.pic_h, P.n_ref);
   const CtuWs W = ctu_ws_layout(L);

@@ -80,6 +80,72 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+#define ME_DPP(v, ctrl) ((uint32_t)__builtin_amdgcn_update_dpp((int)0, (int)(v), (ctrl), 0xf, 0xf, false))
+
+// Wave-wide minimum (every lane active): v_min_u32_dpp inside rows of 16 lanes (quad swaps,
+// half-row and row mirrors), then the 4 row minima on the SALU.  Result is wave-uniform.
+__device__ __forceinline__ uint32_t wave_min_key(uint32_t v) {
+  v = min(v, ME_DPP(v, 0xB1));   // quad_perm [1,0,3,2]
+  v = min(v, ME_DPP(v, 0x4E));   // quad_perm [2,3,0,1]
+  v = min(v, ME_DPP(v, 0x141));  // row_half_mirror
+  v = min(v, ME_DPP(v, 0x140));  // row_mirror
+  const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+  const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  return min(min(a, b), min(c, d));
+}
+
+// Sum over aligned groups of 1<<sh lanes, every lane of a group ends with its sum (every lane
+// active; sh wave-uniform).
+__device__ __forceinline__ uint32_t seg_sum(uint32_t v, int sh) {
+  if (sh >= 1) v += ME_DPP(v, 0xB1);
+  if (sh >= 2) v += ME_DPP(v, 0x4E);
+  if (sh >= 3) v += ME_DPP(v, 0x141);
+  if (sh >= 4) v += ME_DPP(v, 0x140);
+  if (sh >= 5) v += __shfl_xor(v, 16, HVX_WAVE);
+  if (sh >= 6) v += __shfl_xor(v, 32, HVX_WAVE);
+  return v;
+}
+
+// (cost, list index) key of one candidate of a list of <= 256 points.  Costs stay below 2^24
+// (SAD <= 64*64*255, MV costs of a few thousand), so key order == cost order, ties broken by
+// the lower index: the first minimum, i.e. the point a chain of strict '<' updates keeps.
+constexpr uint32_t kMeKeyNone = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t me_key(uint32_t cost, int idx) { return (cost << 8) | (uint32_t)idx; }
+
+typedef uint32_t me_v2u __attribute__((ext_vector_type(2)));
+typedef uint32_t me_v3u __attribute__((ext_vector_type(3)));
+typedef uint32_t me_v4u __attribute__((ext_vector_type(4)));
+
+// N consecutive dwords at byte offset voff + soff of a buffer (dwordx4 pieces + remainder)
+template <int N>
+__device__ __forceinline__ void me_ldw(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int soff, uint32_t *w) {
+#pragma unroll
+  for (int i = 0; i + 4 <= N; i += 4) {
+    const me_v4u t = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 4 * i, soff, 0);
+    w[i] = t.x; w[i + 1] = t.y; w[i + 2] = t.z; w[i + 3] = t.w;
+  }
+  constexpr int B = N & ~3;
+  if constexpr (N % 4 == 1) {
+    w[B] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 4 * B, soff, 0);
+  } else if constexpr (N % 4 == 2) {
+    const me_v2u t = __builtin_amdgcn_raw_buffer_load_b64(rs, voff + 4 * B, soff, 0);
+    w[B] = t.x; w[B + 1] = t.y;
+  } else if constexpr (N % 4 == 3) {
+    const me_v3u t = __builtin_amdgcn_raw_buffer_load_b96(rs, voff + 4 * B, soff, 0);
+    w[B] = t.x; w[B + 1] = t.y; w[B + 2] = t.z;
+  }
+}
+
+// buffer resource over a whole padded 8-bit plane given its sample-(0,0) pointer (ME plane
+// contract: margin HVX_PLANE_MARGIN on every side); built from wave-uniform values
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t me_plane_rsrc(const uint8_t *origin, int stride, int pic_h) {
+  const uint8_t *base = origin - (size_t)HVX_PLANE_MARGIN * stride - HVX_PLANE_MARGIN;
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int bytes = __builtin_amdgcn_readfirstlane(stride * (pic_h + 2 * HVX_PLANE_MARGIN));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+
 // ======================================================================================
 // integer TZ search
 // ======================================================================================
@@ -88,7 +154,10 @@ constexpr int kMeMaxList = 256;  // diamonds d = 1..256: 4 + 3*8 + 5*16 = 108 po
 struct MeInt {
   const uint8_t *org;  // LDS, stride os (64 for the generic kernel, S for the CTU kernels)
   const uint8_t *ref;  // PU origin at MV (0,0) in the reference plane
-  uint32_t *cost;      // LDS, cost of each point of the current candidate list
+  uint32_t *red;       // LDS, [2][kMeMaxRanges][NW] per-wave range minima (ping-pong), NW > 1 only
+  int par;             // ping-pong parity of red
+  __amdgpu_buffer_rsrc_t rs;  // the reference plane as a buffer (compile-time-shape kernels)
+  uint32_t roff;              // byte offset of the PU origin at MV (0,0) in rs
   int sr, sub, rows, gw, os;
   uint32_t lam;
   int px, py;
@@ -117,38 +186,29 @@ __device__ __forceinline__ uint32_t me_sad_part(const MeInt &m, int x, int y, in
   return acc;
 }
 
-// SAD of one S-wide row at any alignment: S/4+1 consecutive aligned dwords (merged into
-// wide loads), v_alignbyte into place, v_sad_u8 against the LDS original.
-template <int S>
-__device__ __forceinline__ uint32_t me_sad_row(const uint8_t *o, const uint8_t *p, uint32_t acc) {
-  constexpr int GW = S / 4;
-  const uintptr_t a = (uintptr_t)p;
-  const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
-  const uint32_t sh = (uint32_t)(a & 3);
-  uint32_t w[GW + 1];
-#pragma unroll
-  for (int i = 0; i <= GW; i++) w[i] = q[i];
-  const uint32_t *ow = (const uint32_t *)o;
-#pragma unroll
-  for (int i = 0; i < GW; i++) acc = __builtin_amdgcn_sad_u8(ow[i], __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh), acc);
-  return acc;
-}
-
 // Same for a square SxS block with compile-time FEN shift and lanes-per-point 1<<SH: lane s
-// takes sampled rows s, s+L, ...; the row loop unrolls so that up to ~24 dwords per lane are
-// in flight at once.
+// takes sampled rows s, s+L, ...  Rows come from buffer loads at the point's dword-aligned
+// offset + an SGPR row offset (plane strides are multiples of 4, so one alignbyte shift serves
+// every row); the row loop unrolls so that up to ~24 dwords per lane are in flight at once.
 template <int S, int SUB, int SH>
 __device__ __forceinline__ uint32_t me_sad_part_ct(const MeInt &m, int x, int y, int s) {
-  constexpr int ROWS = S >> SUB, L = 1 << SH, PER = (ROWS + L - 1) / L;
+  constexpr int ROWS = S >> SUB, L = 1 << SH, PER = (ROWS + L - 1) / L, GW = S / 4;
   constexpr int BUDGET = S == 8 ? 12 : 24;  // dwords in flight per lane (8x8: keep occupancy)
-  constexpr int RUN = (S / 4 + 1) * PER <= BUDGET ? PER : (BUDGET / (S / 4 + 1) > 0 ? BUDGET / (S / 4 + 1) : 1);
+  constexpr int RUN = (GW + 1) * PER <= BUDGET ? PER : (BUDGET / (GW + 1) > 0 ? BUDGET / (GW + 1) : 1);
   constexpr int UNR = RUN < 1 ? 1 : RUN;
-  const uint8_t *base = m.ref + y * m.sr + x;
+  const uint32_t a = m.roff + (uint32_t)(y * m.sr + x) + (uint32_t)((s << SUB) * m.sr);
+  const uint32_t va = a & ~3u, sh = a & 3u;
+  const uint8_t *o = m.org + (s << SUB) * S;
   uint32_t acc = 0;
 #pragma unroll UNR
   for (int k = 0; k < PER; k++) {
-    const int r = s + k * L;
-    if (ROWS % L == 0 || r < ROWS) acc = me_sad_row<S>(m.org + (r << SUB) * S, base + (r << SUB) * m.sr, acc);
+    if (ROWS % L == 0 || s + k * L < ROWS) {
+      uint32_t w[GW + 1];
+      me_ldw<GW + 1>(m.rs, va, ((k * L) << SUB) * m.sr, w);
+      const uint32_t *ow = (const uint32_t *)(o + ((k * L) << SUB) * S);
+#pragma unroll
+      for (int i = 0; i < GW; i++) acc = __builtin_amdgcn_sad_u8(ow[i], __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh), acc);
+    }
   }
   return acc;
 }
@@ -171,13 +231,21 @@ __device__ __forceinline__ uint32_t me_sad_any(const MeInt &m, int x, int y, int
   }
 }
 
-// cost (SAD + MV cost, or ~0 for a point outside the range) of list points 0..n-1 -> m.cost.
-// The NW waves of the job take equal contiguous shares of the list; inside a wave,
-// 64/2^ceil(log2 share) lanes work on each point.
-template <int S, int SUB, int NW, typename F>
-__device__ __forceinline__ void me_eval(MeInt &m, int n, F cand) {
-  const int lane = lane_id(), wave = NW > 1 ? (int)(threadIdx.x >> 6) : 0;
+constexpr int kMeMaxRanges = 9;  // first-stage diamonds d = 1 .. 256
+
+// Costs (SAD + MV cost; points outside the search range excluded) of list points [0, n),
+// n <= kMeMaxList, reduced to the FIRST-minimum key of each range r < nr -- range r being the
+// points p with rng(p) == r -- identical in every wave of the job on return.  The NW waves take
+// equal contiguous shares of the list; inside a wave, 64/2^ceil(log2 share) lanes work on each
+// point of a pass; each lane keeps its points' per-range minima in registers, reduced once per
+// list (DPP + SALU; across waves through a ping-pong LDS slot, one barrier).
+template <int S, int SUB, int NW, int NR, typename F, typename R>
+__device__ __forceinline__ void me_eval_min(MeInt &m, int n, int nr, F cand, R rng, uint32_t (&key)[NR]) {
+  const int lane = lane_id(), wave = NW > 1 ? uni((int)(threadIdx.x >> 6)) : 0;
   const int per = (n + NW - 1) / NW, lo = wave * per, hi = min(n, lo + per);
+  uint32_t part[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) part[r] = kMeKeyNone;
   for (int base = lo; base < hi; base += HVX_WAVE) {
     const int cnt = min(HVX_WAVE, hi - base);
     const int sh = 6 - (cnt <= 1 ? 0 : 32 - __clz(cnt - 1)), L = 1 << sh;
@@ -186,62 +254,82 @@ __device__ __forceinline__ void me_eval(MeInt &m, int n, F cand) {
     c.ok = false; c.x = c.y = 0;
     if (q < cnt) c = cand(base + q);
     uint32_t acc = c.ok ? me_sad_any<S, SUB>(m, c.x, c.y, s, sh) : 0u;
-    for (int o = 1; o < L; o <<= 1) acc += __shfl_xor(acc, o, HVX_WAVE);
-    if (s == 0 && q < cnt)
-      m.cost[base + q] = c.ok ? (acc << m.sub) + me_mv_cost(m.lam, m.px, m.py, 2, c.x, c.y) : 0xFFFFFFFFu;
+    acc = seg_sum(acc, sh);  // every lane of the point's group holds its SAD
+    if (c.ok) {
+      const int p = base + q;
+      const uint32_t k = me_key((acc << m.sub) + me_mv_cost(m.lam, m.px, m.py, 2, c.x, c.y), p);
+      const int r = NR == 1 ? 0 : rng(p);
+#pragma unroll
+      for (int i = 0; i < NR; i++)
+        if (i == r) part[i] = min(part[i], k);
+    }
   }
-  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    key[r] = kMeKeyNone;
+    if (r < nr) {
+      const uint32_t w = wave_min_key(part[r]);
+      if constexpr (NW == 1) key[r] = w;
+      else if (lane == 0) m.red[(m.par * kMeMaxRanges + r) * NW + wave] = w;
+    }
+  }
+  if constexpr (NW > 1) {
+    __syncthreads();  // the other parity slot is rewritten only after the NEXT list's barrier
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      if (r < nr) {
+        uint32_t v = kMeKeyNone;
+#pragma unroll
+        for (int w = 0; w < NW; w++) v = min(v, m.red[(m.par * kMeMaxRanges + r) * NW + w]);
+        key[r] = (uint32_t)uni((int)v);
+      }
+    }
+    m.par ^= 1;
+  }
 }
 
-// xTZSearchHelp over list points [start, start+cnt) in order: first minimum, strict '<'.
-// Every wave of the job reduces the same costs, so the search state stays identical in all.
+// xTZSearchHelp applied to a list's first minimum (strict '<' against the running best)
 template <typename F>
-__device__ __forceinline__ void me_take(MeInt &m, int start, int cnt, F cand) {
-  uint64_t key = ~0ull;
-  for (int i = lane_id(); i < cnt; i += HVX_WAVE) {
-    const uint64_t k = ((uint64_t)m.cost[start + i] << 32) | (uint32_t)i;
-    key = k < key ? k : key;
+__device__ __forceinline__ void me_take(MeInt &m, uint32_t key, F cand) {
+  if (key != kMeKeyNone && (key >> 8) < m.best_sad) {
+    const MeCand w = cand((int)(key & 255u));
+    m.best_sad = key >> 8; m.best_x = w.x; m.best_y = w.y; m.best_dist = w.dist; m.best_round = 0; m.point_nr = w.pnr;
   }
-  key = wave_min_u64(key);
-  const uint32_t c = (uint32_t)uni((int)(uint32_t)(key >> 32));
-  if (c < m.best_sad) {  // out-of-range points cost ~0 and never pass
-    const MeCand w = cand(start + uni((int)(uint32_t)key));
-    m.best_sad = c; m.best_x = w.x; m.best_y = w.y; m.best_dist = w.dist; m.best_round = 0; m.point_nr = w.pnr;
-  }
-  __syncthreads();  // m.cost is rewritten by the next list
 }
+
+__device__ __forceinline__ int me_rng0(int) { return 0; }
 
 // diamonds d = 1, 2, 4, ... around (sx,sy), concatenated in xTZ8PointDiamondSearch order
 __device__ __forceinline__ int me_dia_start(int k) { return k == 0 ? 0 : k <= 3 ? 4 + 8 * (k - 1) : 28 + 16 * (k - 4); }
+__device__ __forceinline__ int me_dia_k(int p) { return p < 4 ? 0 : p < 28 ? 1 + ((p - 4) >> 3) : 4 + ((p - 28) >> 4); }
 
-__device__ __forceinline__ MeCand me_dia_cand(const MeRange &g, int sx, int sy, int p) {
-  int k, q;
-  if (p < 4) { k = 0; q = p; }
-  else if (p < 28) { k = 1 + ((p - 4) >> 3); q = (p - 4) & 7; }
-  else { k = 4 + ((p - 28) >> 4); q = (p - 28) & 15; }
-  const int d = 1 << k;
-  int dx = 0, dy = 0, pnr = 0, dist = d;
-  if (k == 0) {
-    switch (q) {
-      case 0: dy = -1; pnr = 2; break;
-      case 1: dx = -1; pnr = 4; break;
-      case 2: dx = 1; pnr = 5; break;
-      default: dy = 1; pnr = 7; break;
-    }
-  } else if (k <= 3) {
-    const int h = d >> 1;
-    switch (q) {
-      case 0: dy = -d; pnr = 2; break;
-      case 1: dx = -h; dy = -h; pnr = 1; dist = h; break;
-      case 2: dx = h; dy = -h; pnr = 3; dist = h; break;
-      case 3: dx = -d; pnr = 4; break;
-      case 4: dx = d; pnr = 5; break;
-      case 5: dx = -h; dy = h; pnr = 6; dist = h; break;
-      case 6: dx = h; dy = h; pnr = 8; dist = h; break;
-      default: dy = d; pnr = 7; break;
-    }
-  } else {
-    if (q < 4) {
+// Point p of that list as an offset from the start (xTZ8PointDiamondSearch :629-800: d = 1 is
+// the 4-point cross; d = 2..8 the 8-point diamond with half-distance diagonals; d >= 16 the
+// 4 axis points + 3 rows of 4 points per quadrant edge), packed into one table word:
+// dx | dy << 10 (10-bit two's complement) | point_nr << 20 | log2(distance) << 24.
+struct MeDiaTab { uint32_t v[108]; };
+constexpr uint32_t me_dia_pack(int dx, int dy, int pnr, int dist) {
+  int dl = 0;
+  while ((1 << dl) < dist) dl++;
+  return ((uint32_t)dx & 0x3FFu) | (((uint32_t)dy & 0x3FFu) << 10) | ((uint32_t)pnr << 20) | ((uint32_t)dl << 24);
+}
+constexpr MeDiaTab me_dia_build() {
+  MeDiaTab t{};
+  for (int p = 0; p < 108; p++) {
+    int k = 0, q = 0;
+    if (p < 4) { k = 0; q = p; }
+    else if (p < 28) { k = 1 + ((p - 4) >> 3); q = (p - 4) & 7; }
+    else { k = 4 + ((p - 28) >> 4); q = (p - 28) & 15; }
+    const int d = 1 << k, h = d >> 1;
+    int dx = 0, dy = 0, pnr = 0, dist = d;
+    if (k == 0) {
+      const int tab[4][3] = {{0, -1, 2}, {-1, 0, 4}, {1, 0, 5}, {0, 1, 7}};
+      dx = tab[q][0]; dy = tab[q][1]; pnr = tab[q][2];
+    } else if (k <= 3) {
+      const int tab[8][4] = {{0, -2, 2, 2}, {-1, -1, 1, 1}, {1, -1, 3, 1}, {-2, 0, 4, 2},
+                             {2, 0, 5, 2},  {-1, 1, 6, 1},  {1, 1, 8, 1},  {0, 2, 7, 2}};  // units of h
+      dx = tab[q][0] * h; dy = tab[q][1] * h; pnr = tab[q][2]; dist = tab[q][3] * h;
+    } else if (q < 4) {
       dx = q == 1 ? -d : q == 2 ? d : 0;
       dy = q == 0 ? -d : q == 3 ? d : 0;
     } else {
@@ -249,9 +337,17 @@ __device__ __forceinline__ MeCand me_dia_cand(const MeRange &g, int sx, int sy, 
       dx = (kk & 1) ? o : -o;
       dy = (kk & 2) ? d - o : o - d;
     }
+    t.v[p] = me_dia_pack(dx, dy, pnr, dist);
   }
+  return t;
+}
+__constant__ MeDiaTab kDiaTab = me_dia_build();
+
+__device__ __forceinline__ MeCand me_dia_cand(const MeRange &g, int sx, int sy, int p) {
+  const uint32_t v = kDiaTab.v[p];
+  const int dx = (int)(v << 22) >> 22, dy = (int)(v << 12) >> 22;
   MeCand c;
-  c.x = sx + dx; c.y = sy + dy; c.pnr = pnr; c.dist = dist;
+  c.x = sx + dx; c.y = sy + dy; c.pnr = (int)((v >> 20) & 15u); c.dist = 1 << ((v >> 24) & 15u);
   c.ok = me_in(g, dx, dy, c.x, c.y);  // == the reference's tests, whether the diamond is inside or not
   return c;
 }
@@ -272,8 +368,9 @@ __device__ __forceinline__ void me_2point(MeInt &m, const MeRange &g) {
     c.pnr = 0; c.dist = 2; c.ok = me_in(g, dx, dy, c.x, c.y);
     return c;
   };
-  me_eval<S, SUB, NW>(m, 2, cand);
-  me_take(m, 0, 2, cand);
+  uint32_t key[1];
+  me_eval_min<S, SUB, NW, 1>(m, 2, 1, cand, me_rng0, key);
+  me_take(m, key[0], cand);
 }
 
 // xTZSearch (:3881) for job j; returns with m.best_* = the integer result
@@ -300,40 +397,50 @@ __device__ void me_tz(const hvx_me_job &j, MeInt &m) {
       c.pnr = 0; c.dist = 0; c.ok = true;
       return c;
     };
-    const int n = j.use_int2nx2n ? 3 : 2;
-    me_eval<S, SUB, NW>(m, n, cand);
-    me_take(m, 0, n, cand);
+    uint32_t key[1];
+    me_eval_min<S, SUB, NW, 1>(m, j.use_int2nx2n ? 3 : 2, 1, cand, me_rng0, key);
+    me_take(m, key[0], cand);
   }
   const MeRange g = j.use_int2nx2n ? me_search_range(j, m.best_x << 2, m.best_y << 2, sr) : g0;
   int nd = 0;
   while ((1 << nd) <= sr) nd++;
   const int ndp = me_dia_start(nd);
-  // first stage: the diamonds around the start, stopped after 3 rounds without a gain
+  // first stage: the diamonds around the start (one list, one minimum per diamond), replayed
+  // in order and stopped after 3 rounds without a gain
   {
     const int sx = m.best_x, sy = m.best_y;
     auto cand = [=](int p) { return me_dia_cand(g0, sx, sy, p); };
-    me_eval<S, SUB, NW>(m, ndp, cand);
-    for (int k = 0; k < nd; k++) {
-      m.best_round += 1;
-      me_take(m, me_dia_start(k), me_dia_start(k + 1) - me_dia_start(k), cand);
-      if ((j.flags & HVX_ME_SMOOTHMV) && m.best_round >= 3) break;
+    uint32_t key[kMeMaxRanges];
+    me_eval_min<S, SUB, NW, kMeMaxRanges>(m, ndp, nd, cand, me_dia_k, key);
+    bool stop = false;
+#pragma unroll
+    for (int k = 0; k < kMeMaxRanges; k++) {
+      if (k < nd && !stop) {
+        m.best_round += 1;
+        me_take(m, key[k], cand);
+        if ((j.flags & HVX_ME_SMOOTHMV) && m.best_round >= 3) stop = true;
+      }
     }
   }
   if (m.best_dist == 1) { m.best_dist = 0; me_2point<S, SUB, NW>(m, g0); }
-  // raster (step 5) over the re-centred range
+  // raster (step 5) over the re-centred range, lists of kMeMaxList points
   if (m.best_dist > 5) {
     m.best_dist = 5;
     const int nx = (g.r - g.l) / 5 + 1, ny = (g.b - g.t) / 5 + 1, n = nx * ny;
-    for (int base = 0; base < n; base += HVX_WAVE * NW) {
-      const int cnt = min(HVX_WAVE * NW, n - base);
+    const float rnx = 1.0f / (float)nx;
+    for (int base = 0; base < n; base += kMeMaxList) {
+      const int cnt = min(kMeMaxList, n - base);
       auto cand = [=](int p) {
-        const int q = base + p, ry = q / nx, rx = q - ry * nx;
+        const int q = base + p;
+        int ry = (int)((float)q * rnx), rx = q - ry * nx;  // float quotient, exact after one correction
+        if (rx < 0) { ry--; rx += nx; } else if (rx >= nx) { ry++; rx -= nx; }
         MeCand c;
         c.x = g.l + 5 * rx; c.y = g.t + 5 * ry; c.pnr = 0; c.dist = 5; c.ok = true;
         return c;
       };
-      me_eval<S, SUB, NW>(m, cnt, cand);
-      me_take(m, 0, cnt, cand);
+      uint32_t key[1];
+      me_eval_min<S, SUB, NW, 1>(m, cnt, 1, cand, me_rng0, key);
+      me_take(m, key[0], cand);
     }
   }
   // star refinement: every round's diamonds share their start -> one list, one minimum
@@ -341,8 +448,9 @@ __device__ void me_tz(const hvx_me_job &j, MeInt &m) {
     const int sx = m.best_x, sy = m.best_y;
     m.best_dist = 0; m.point_nr = 0;
     auto cand = [=](int p) { return me_dia_cand(g0, sx, sy, p); };
-    me_eval<S, SUB, NW>(m, ndp, cand);
-    me_take(m, 0, ndp, cand);
+    uint32_t key[1];
+    me_eval_min<S, SUB, NW, 1>(m, ndp, 1, cand, me_rng0, key);
+    me_take(m, key[0], cand);
     if (m.best_dist == 1) {
       m.best_dist = 0;
       if (m.point_nr != 0) me_2point<S, SUB, NW>(m, g0);
@@ -350,11 +458,19 @@ __device__ void me_tz(const hvx_me_job &j, MeInt &m) {
   }
 }
 
+// the job's reference: PU-origin pointer (generic SAD, fractional stage) and buffer view
+__device__ __forceinline__ void me_ref_setup(MeInt &m, const hvx_me_job &j, const uint8_t *ref_origin, int stride) {
+  m.ref = ref_origin + j.pu_y * stride + j.pu_x;
+  m.sr = stride;
+  m.rs = me_plane_rsrc(ref_origin, stride, j.pic_h);
+  m.roff = (uint32_t)((HVX_PLANE_MARGIN + j.pu_y) * stride + HVX_PLANE_MARGIN + j.pu_x);
+}
+
 // S == 0: any PU shape (org stride 64, runtime FEN); otherwise square SxS with FEN shift SUB.
 template <int S, int SUB, int NW>
 __device__ __forceinline__ void me_int_job(const hvx_me_job &j, const uint8_t *const *__restrict__ cur_planes,
                                            const uint8_t *const *__restrict__ ref_planes, int stride, uint8_t *org,
-                                           uint32_t *cost, hvx_me_result *out) {
+                                           uint32_t *red, hvx_me_result *out) {
   if (j.w <= 0 || j.h <= 0) {  // empty slot (e.g. a CU outside the picture): defined zero result
     if (threadIdx.x == 0) { hvx_me_result z; memset(&z, 0, sizeof(z)); *out = z; }
     return;
@@ -367,9 +483,8 @@ __device__ __forceinline__ void me_int_job(const hvx_me_job &j, const uint8_t *c
   }
   __syncthreads();
   MeInt m;
-  m.org = org; m.cost = cost; m.os = OS;
-  m.ref = ref_planes[j.ref_idx] + j.pu_y * stride + j.pu_x;
-  m.sr = stride;
+  m.org = org; m.red = red; m.par = 0; m.os = OS;
+  me_ref_setup(m, j, ref_planes[j.ref_idx], stride);
   const int w = j.w;
   if (S) {
     m.sub = SUB;
@@ -392,11 +507,11 @@ __global__ __launch_bounds__(64) void k_me_int(const uint8_t *const *__restrict_
                                               const uint8_t *const *__restrict__ ref_planes, int stride,
                                               const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t org[64 * 64];
-  __shared__ uint32_t cost[kMeMaxList];
+  __shared__ uint32_t red[2 * kMeMaxRanges];
   const int jid = blockIdx.x;
   if (jid >= n) return;
   const hvx_me_job j = jobs[jid];
-  me_int_job<0, 0, 1>(j, cur_planes, ref_planes, stride, org, cost, out + jid);
+  me_int_job<0, 0, 1>(j, cur_planes, ref_planes, stride, org, red, out + jid);
 }
 
 // CTU-pass view: block b = (ctu * ncu + cu) * nref + ref of one depth -> job slot
@@ -413,11 +528,11 @@ __global__ __launch_bounds__(64 * NW) void k_me_int_ctu(const uint8_t *const *__
                                                        const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
                                                        int nref, int ncu, int first) {
   __shared__ __attribute__((aligned(16))) uint8_t org[S * S];
-  __shared__ uint32_t cost[kMeMaxList];
+  __shared__ uint32_t red[2 * kMeMaxRanges * NW];
   const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
   const hvx_me_job j = jobs[slot];
   if (j.w > 0 && (j.w != S || j.h != S)) return;  // not this depth's shape (cannot happen in the pass)
-  me_int_job<S, SUB, NW>(j, cur_planes, ref_planes, stride, org, cost, out + slot);
+  me_int_job<S, SUB, NW>(j, cur_planes, ref_planes, stride, org, red, out + slot);
 }
 
 // ======================================================================================
@@ -722,7 +837,7 @@ __global__ __launch_bounds__(64 * NW) void k_me_ctu(const uint8_t *const *__rest
                                                    const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
                                                    int nref, int ncu, int first) {
   __shared__ MeFracSmem<S, NW> sm;
-  __shared__ uint32_t cost[kMeMaxList];
+  __shared__ uint32_t red[2 * kMeMaxRanges * NW];
   const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
   const hvx_me_job j = jobs[slot];
   if (j.w > 0 && (j.w != S || j.h != S)) return;
@@ -737,9 +852,8 @@ __global__ __launch_bounds__(64 * NW) void k_me_ctu(const uint8_t *const *__rest
   }
   __syncthreads();
   MeInt m;
-  m.org = sm.org; m.cost = cost; m.os = S;
-  m.ref = ref_planes[j.ref_idx] + j.pu_y * stride + j.pu_x;
-  m.sr = stride;
+  m.org = sm.org; m.red = red; m.par = 0; m.os = S;
+  me_ref_setup(m, j, ref_planes[j.ref_idx], stride);
   m.sub = SUB;
   m.rows = S >> SUB;
   m.gw = S >> 2;
