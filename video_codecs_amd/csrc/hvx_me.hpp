@@ -599,18 +599,73 @@ __device__ __forceinline__ int me_frac_sample(const MeFracSmem<S, NW, TO> &sm, i
   return clip_pel((s + (1 << 11) + (8192 << 6)) >> 12);
 }
 
-// 8x8 Hadamard of one tile held one difference per lane (lane = y*8 + x); every lane gets
-// the tile's (sum|coef| + 2) >> 2 (TComRdCost::xCalcHADs8x8; coefficient order and signs
-// do not change the sum of magnitudes)
-__device__ __forceinline__ uint32_t had8_xlane(int v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_xor(v, o, HVX_WAVE);
-    v = (lane & o) ? t - v : v + t;
-  }
-  return (wave_sum_u32((uint32_t)abs(v)) + 2) >> 2;
+// 8x8 Hadamard across the wave on VALU partner fetches only (every lane active): the stages
+// pair lane L with L^1, L^2 (quad swaps), L^7 (row_half_mirror), L^15 (row_mirror), L^16,
+// L^32 (gfx950 permlane16/32 swaps).  Over GF(2) the masks {1,2,7,15,16,32} are a basis of
+// the lane index; in its coordinates c(L) every stage is the standard xor butterfly, so lane L
+// holds the sample at x = c & 7, y = c >> 3 (me_had_xy) and takes the butterfly role of
+// coordinate bit k (low: a + b, high: b - a).  The result is the reference's 8x8 Hadamard up
+// to coefficient order (TComRdCost::xCalcHADs8x8 sums magnitudes, so the SATD is identical).
+__device__ __forceinline__ int me_had_c(int lane) {
+  const int b2 = (lane >> 2) & 1, b3 = (lane >> 3) & 1;
+  return lane ^ (b2 * 3) ^ (b3 * 4);
 }
+__device__ __forceinline__ void me_had_xy(int lane, int &x, int &y) {
+  const int c = me_had_c(lane);
+  x = c & 7; y = c >> 3;
+}
+template <int N>
+__device__ __forceinline__ void had8_xlane_dpp(int (&v)[N]) {
+  const int c = me_had_c(lane_id());
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const int sg = 1 - (((c >> k) & 1) << 1);  // +1: v + partner, -1: partner - v
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      if (k < 4) {
+        int t;
+        if (k == 0) t = __builtin_amdgcn_mov_dpp(v[i], 0xB1, 0xf, 0xf, false);
+        else if (k == 1) t = __builtin_amdgcn_mov_dpp(v[i], 0x4E, 0xf, 0xf, false);
+        else if (k == 2) t = __builtin_amdgcn_mov_dpp(v[i], 0x141, 0xf, 0xf, false);
+        else t = __builtin_amdgcn_mov_dpp(v[i], 0x140, 0xf, 0xf, false);
+        v[i] = t + __mul24(sg, v[i]);
+      } else {
+        // with both operands = v the swap returns (low-half value, high-half value) in every lane
+        const auto pr = k == 4 ? __builtin_amdgcn_permlane16_swap((unsigned)v[i], (unsigned)v[i], false, false)
+                               : __builtin_amdgcn_permlane32_swap((unsigned)v[i], (unsigned)v[i], false, false);
+        v[i] = (int)pr[0] + __mul24(sg, (int)pr[1]);
+      }
+    }
+  }
+}
+
+// wave-wide sum (every lane active): DPP adds inside rows of 16, the 4 row sums on the SALU
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
+  v += ME_DPP(v, 0xB1);
+  v += ME_DPP(v, 0x4E);
+  v += ME_DPP(v, 0x141);
+  v += ME_DPP(v, 0x140);
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
+
+// second filter stage of one candidate sample from a column window hw[t] = hp[c] row
+// (ryb + 1 + y + t), t = 0..8; off = ry - ryb (0 or 1) and fy are wave-uniform
+__device__ __forceinline__ int me_vsample(const int *hw, int off, int fy) {
+  if (!fy) return clip_pel(((off ? hw[4] : hw[3]) + 8192 + 32) >> 6);
+  int s = 0;
+  if (off) {
+#pragma unroll
+    for (int t = 0; t < 8; t++) s += kLumaFilter[fy][t] * hw[t + 1];
+  } else {
+#pragma unroll
+    for (int t = 0; t < 8; t++) s += kLumaFilter[fy][t] * hw[t];
+  }
+  return clip_pel((s + (1 << 11) + (8192 << 6)) >> 12);
+}
+
+// candidate index of (column c = dx+1, row d = dy+1) in s_acMvRefineH / s_acMvRefineQ order
+__constant__ int8_t kRefIdx[2][3][3] = {{{5, 3, 7}, {1, 0, 2}, {6, 4, 8}}, {{3, 5, 7}, {1, 0, 2}, {4, 6, 8}}};
 
 // xPatternRefinement (:808): the 9 candidates of one stage.  (qx0,qy0) = stage centre in
 // quarter-pel relative to the PU, step 2 (half) or 1 (quarter); (ix,iy) the integer MV.
@@ -674,7 +729,49 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
   // 2. the 9 candidates' costs (SATD or SAD + MV cost), spread over the waves
   const bool xl = had && (!GENERIC || ((w % 8 == 0) && (h % 8 == 0))) && (w * h <= 1024);
   const int tw = w >> 3, nt = (w * h) >> 6;
-  if (xl) {
+  int hx, hy;
+  me_had_xy(lane, hx, hy);
+  if (xl && NW == 1) {
+    // one wave, all 9 candidates: per column phase c the 9-row window of hp[c] the 3 vertical
+    // phases need is read once; the 9 tiles' Hadamards run side by side on DPP butterflies
+    int offs[3], fys[3];
+    int ryb = 0;
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const int qy = qy0 + (d - 1) * step, ry = (qy >> 2) - iy;
+      if (d == 0) ryb = ry;
+      offs[d] = ry - ryb; fys[d] = qy & 3;
+    }
+    uint32_t dsum[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) dsum[i] = 0;
+    for (int t = 0; t < nt; t++) {
+      const int x = ((t % tw) << 3) + hx, y = ((t / tw) << 3) + hy;
+      const int o = sm.org[y * S + x];
+      int v[9];
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        int hw[9];
+        const int16_t *h = sm.hp[c] + (ryb + 1 + y) * HS + x;
+#pragma unroll
+        for (int k = 0; k < 9; k++) hw[k] = h[k * HS];
+#pragma unroll
+        for (int d = 0; d < 3; d++) v[c * 3 + d] = o - me_vsample(hw, offs[d], fys[d]);
+      }
+      had8_xlane_dpp<9>(v);
+#pragma unroll
+      for (int i = 0; i < 9; i++) dsum[i] += (wave_sum_dpp((uint32_t)abs(v[i])) + 2) >> 2;
+    }
+    const int sel = step == 2 ? 0 : 1;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+        const int i = kRefIdx[sel][c][d];
+        if (lane == 0) sm.cost[i] = dsum[c * 3 + d] + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + c - 1, mvy0 + d - 1);
+      }
+    }
+  } else if (xl) {
     // this wave's candidates i = wave + NW*ii share each tile pass: their sample gathers and
     // Hadamard butterflies are independent and interleave
     constexpr int CPW = (9 + NW - 1) / NW;
@@ -688,28 +785,14 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
       cc[ii] = dx + 1; cry[ii] = (qy >> 2) - iy; cfy[ii] = qy & 3; dsum[ii] = 0;
     }
     for (int t = 0; t < nt; t++) {
-      const int x = ((t % tw) << 3) + (lane & 7), y = ((t / tw) << 3) + (lane >> 3);
+      const int x = ((t % tw) << 3) + hx, y = ((t / tw) << 3) + hy;
       const int o = sm.org[y * S + x];
       int v[CPW];
 #pragma unroll
       for (int ii = 0; ii < CPW; ii++) v[ii] = o - me_frac_sample(sm, cc[ii], cry[ii], cfy[ii], x, y);
+      had8_xlane_dpp<CPW>(v);
 #pragma unroll
-      for (int st = 1; st < 64; st <<= 1) {
-#pragma unroll
-        for (int ii = 0; ii < CPW; ii++) {
-          const int q = __shfl_xor(v[ii], st, HVX_WAVE);
-          v[ii] = (lane & st) ? q - v[ii] : v[ii] + q;
-        }
-      }
-#pragma unroll
-      for (int ii = 0; ii < CPW; ii++) v[ii] = abs(v[ii]);
-#pragma unroll
-      for (int st = 32; st > 0; st >>= 1) {
-#pragma unroll
-        for (int ii = 0; ii < CPW; ii++) v[ii] += __shfl_xor(v[ii], st, HVX_WAVE);
-      }
-#pragma unroll
-      for (int ii = 0; ii < CPW; ii++) dsum[ii] += ((uint32_t)v[ii] + 2) >> 2;
+      for (int ii = 0; ii < CPW; ii++) dsum[ii] += (wave_sum_dpp((uint32_t)abs(v[ii])) + 2) >> 2;
     }
 #pragma unroll
     for (int ii = 0; ii < CPW; ii++) {
