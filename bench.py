@@ -127,10 +127,11 @@ def main():
     if rank == 0:
         value = aggregate(nctu, args.steps, world, elapsed)
         # roofline of the dominant kernel = the longest single launch of the step, timed with
-        # HIP events on the launch stream (hvx phase events bracket exactly one launch each here).
+        # HIP events on the launch stream (a begin/end pair around exactly one launch; the pass
+        # runs on 3 streams, so phases overlap and their sum exceeds ms_per_step).
         # Algorithmic bytes per launch = SURVEY 8(d)'s per-CTU figure (luma form, DESIGN.md
         # "Roofline") x the CTUs one launch covers (every launch of the pass covers the picture).
-        single = dict(zip(hvx.PHASE_KERNELS, hvx.PHASES))
+        single = {k: p for k, p, nl in zip(hvx.PHASE_KERNELS, hvx.PHASES, hvx.PHASE_LAUNCHES) if nl == 1}
         kernel = max(single, key=lambda k: phases[single[k]])
         launch_ms = phases[single[kernel]] / args.steps
         b_ctu = b_ctu_luma(nref)

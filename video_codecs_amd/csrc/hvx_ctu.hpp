@@ -84,9 +84,11 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
                                                        const uint8_t *const *__restrict__ refs, int stride,
                                                        const hvx_me_result *__restrict__ res, int16_t *__restrict__ resid,
                                                        hvx_tu_desc *__restrict__ descs, int64_t *__restrict__ offs,
-                                                       int32_t *__restrict__ est_idx, hvx_cu_result *__restrict__ out) {
-  const int cuid = blockIdx.x;
-  const int ctu = cuid / HVX_CUS_PER_CTU, ci = cuid % HVX_CUS_PER_CTU;
+                                                       int32_t *__restrict__ est_idx, hvx_cu_result *__restrict__ out,
+                                                       int first, int ncu) {
+  // blocks cover CUs [first, first + ncu) of every CTU (one depth range per launch)
+  const int ctu = blockIdx.x / ncu, ci = first + (int)(blockIdx.x % ncu);
+  const int cuid = ctu * HVX_CUS_PER_CTU + ci;
   int d, j, S, g;
   cu_geom(ci, d, j, S, g);
   const int x = (ctu % L.nctu_x) * 64 + (j % g) * S, y = (ctu / L.nctu_x) * 64 + (j / g) * S;

@@ -22,12 +22,18 @@ struct hvx_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
-  // optional per-phase timing of hvx_ctu_analyze (HIP events on the launch stream)
+  // hvx_ctu_analyze runs its independent branches on two more streams (fork/join events)
+  hipStream_t aux[2] = {};
+  hipEvent_t fj[5] = {};
+  // optional per-phase timing of hvx_ctu_analyze: a begin/end event pair on the launch's own
+  // stream around every timed launch, folded into phase_ms[phase] (phases may overlap)
   int timing = 0;
-  hipEvent_t ev[HVX_NPHASE + 1] = {};
+  static constexpr int kMaxTimed = 32;
+  hipEvent_t tev[2 * kMaxTimed] = {};
+  int tphase[kMaxTimed] = {};
+  int ntev = 0;
   bool ev_ok = false;
   double phase_ms[HVX_NPHASE] = {};
-  int pending = 0;  // events recorded and not yet folded into phase_ms
   // staging for the host-memory single-TU forms
   char *scratch = nullptr;
   char *pinned = nullptr;
@@ -175,17 +181,24 @@ int upload_tables() {
 }  // namespace
 
 static void fold_timing(hvx_ctx *ctx) {
-  if (!ctx->pending) return;
-  (void)hipEventSynchronize(ctx->ev[HVX_NPHASE]);
-  for (int i = 0; i < HVX_NPHASE; i++) {
+  for (int k = 0; k < ctx->ntev; k++) {
     float ms = 0;
-    if (hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) == hipSuccess) ctx->phase_ms[i] += ms;
+    (void)hipEventSynchronize(ctx->tev[2 * k + 1]);
+    if (hipEventElapsedTime(&ms, ctx->tev[2 * k], ctx->tev[2 * k + 1]) == hipSuccess) ctx->phase_ms[ctx->tphase[k]] += ms;
   }
-  ctx->pending = 0;
+  ctx->ntev = 0;
 }
 
-static inline void mark(hvx_ctx *ctx, int i) {
-  if (ctx->timing && ctx->ev_ok) (void)hipEventRecord(ctx->ev[i], ctx->stream);
+// time the launches between t_begin and t_end on stream st as phase `phase` (no-op unless timing)
+static int t_begin(hvx_ctx *ctx, hipStream_t st, int phase) {
+  if (!ctx || !ctx->timing || !ctx->ev_ok || ctx->ntev >= hvx_ctx::kMaxTimed) return -1;
+  const int k = ctx->ntev++;
+  ctx->tphase[k] = phase;
+  (void)hipEventRecord(ctx->tev[2 * k], st);
+  return k;
+}
+static void t_end(hvx_ctx *ctx, hipStream_t st, int k) {
+  if (k >= 0) (void)hipEventRecord(ctx->tev[2 * k + 1], st);
 }
 
 // Batched TU pipeline (k_tu_fwd -> k_tu_rdoq -> k_tu_fin) for one size class over TUs
@@ -196,13 +209,16 @@ static void tu_class_launch(hipStream_t st, const hvx_tu_desc *desc, const hvx_e
                             int32_t *abs_sum, int16_t *res_out, uint32_t *sse, int32_t *coefI, int32_t *levI,
                             int32_t *stI, int8_t *flags, int G, int n_est_lds, hvx_ctx *tctx = nullptr,
                             int phase0 = 0) {
-  if (tctx) mark(tctx, phase0);
+  int k = t_begin(tctx, st, phase0);
   hipLaunchKernelGGL((k_tu_fwd<L>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, temp, arl, coefI, levI, abs_sum, flags, G);
-  if (tctx) mark(tctx, phase0 + 1);
+  t_end(tctx, st, k);
+  k = t_begin(tctx, st, phase0 + 1);
   hipLaunchKernelGGL((k_tu_rdoq<L>), dim3((n + G - 1) / G), dim3(64), 0, st, desc, est, est_idx, n, coefI, levI, stI,
                      abs_sum, flags, G, n_est_lds);
-  if (tctx) mark(tctx, phase0 + 2);
+  t_end(tctx, st, k);
+  k = t_begin(tctx, st, phase0 + 2);
   hipLaunchKernelGGL((k_tu_fin<L, MODE>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, levI, lev, res_out, sse, G);
+  t_end(tctx, st, k);
 }
 
 // TUs per lane-parallel RDOQ wave: enough waves to fill the chip (~2 per SIMD), at most 64
@@ -268,6 +284,13 @@ int hvx_create(int device, hvx_ctx **out) {
   hipError_t e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
   if (e != hipSuccess) { delete c; return hip_fail(e, "hipStreamCreate"); }
   c->stream = c->own;
+  // the side streams carry few, latency-bound workgroups (RDOQ chains): highest priority, so
+  // they dispatch ahead of the ME kernels' backlog instead of waiting behind it
+  int prio_lo = 0, prio_hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
+  for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipStreamCreateWithPriority(&c->aux[i], hipStreamNonBlocking, prio_hi);
+  for (int i = 0; i < 5 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&c->fj[i], hipEventDisableTiming);
+  if (e != hipSuccess) { hvx_destroy(c); return hip_fail(e, "hvx_create: streams/events"); }
   *out = c;
   return HVX_OK;
 }
@@ -278,8 +301,12 @@ int hvx_destroy(hvx_ctx *ctx) {
   if (ctx->tu_scr) (void)hipFree(ctx->tu_scr);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
+  for (int i = 0; i < 2; i++)
+    if (ctx->aux[i]) (void)hipStreamDestroy(ctx->aux[i]);
+  for (int i = 0; i < 5; i++)
+    if (ctx->fj[i]) (void)hipEventDestroy(ctx->fj[i]);
   if (ctx->ev_ok)
-    for (int i = 0; i <= HVX_NPHASE; i++) (void)hipEventDestroy(ctx->ev[i]);
+    for (int i = 0; i < 2 * hvx_ctx::kMaxTimed; i++) (void)hipEventDestroy(ctx->tev[i]);
   delete ctx;
   return HVX_OK;
 }
@@ -507,7 +534,7 @@ int hvx_stvssim_batch(hvx_ctx *ctx, const uint8_t *const *d_hist_org, const uint
 int hvx_set_timing(hvx_ctx *ctx, int on) {
   if (!ctx) return fail(HVX_E_INVALID, "hvx_set_timing: NULL ctx");
   if (on && !ctx->ev_ok) {
-    for (int i = 0; i <= HVX_NPHASE; i++) HVX_HIP(hipEventCreate(&ctx->ev[i]));
+    for (int i = 0; i < 2 * hvx_ctx::kMaxTimed; i++) HVX_HIP(hipEventCreate(&ctx->tev[i]));
     ctx->ev_ok = true;
   }
   ctx->timing = on;
@@ -553,21 +580,33 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
   int32_t *abs_sum = (int32_t *)(ws + W.abs);
   uint32_t *sse = (uint32_t *)(ws + W.sse);
   const uint8_t **cur_slot = (const uint8_t **)(ws + W.ptr);
-  hipStream_t st = ctx->stream;
+  // Three streams, joined back into ctx->stream before the per-CU totals:
+  //   A (ctx->stream): ME depth 0 -> 1 -> 2 -> 3 (depth d+1 starts from depth d's integer MVs),
+  //                    then residuals + the 8x8 TU pipeline of depth 3
+  //   B (aux[0], high priority): residuals of depths 0-1 and the 32x32 TU pipeline -- its
+  //                    latency-bound RDOQ waves run beside the depth 2/3 searches, not after them
+  //   C (aux[1], high priority): residuals of depth 2 and the 16x16 TU pipeline
+  // The 64x64 fractional refinement stays on A after depth 0 (it fills the chip by itself).
+  hipStream_t st = ctx->stream, sb = ctx->aux[0], sc = ctx->aux[1];
   fold_timing(ctx);  // a previous call's events must be read before they are re-recorded
   hipLaunchKernelGGL(k_set_ptr, dim3(1), dim3(1), 0, st, cur_slot, d_cur);
+  const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
+  const bool fen = (P.me_flags & HVX_ME_FEN) != 0;
+  const int n = L.nctu;
+  auto resid_range = [&](hipStream_t s, int first, int ncu) {
+    hipLaunchKernelGGL(k_ctu_pred_resid, dim3(n * ncu), dim3(64), 0, s, L, P, d_cur, d_refs, stride, res, resid, desc, off,
+                       est_idx, d_out, first, ncu);
+  };
   for (int d = 0; d < 4; d++) {
-    mark(ctx, d);
     const int ncu = 1 << (2 * d), nt = L.nctu * ncu * L.nref;
+    const int tk = t_begin(ctx, st, d);
     hipLaunchKernelGGL(k_ctu_me_jobs, dim3((nt + 255) / 256), dim3(256), 0, st, L, P, d, res, jobs);
     // the depth's jobs are contiguous per CTU but interleaved across CTUs: launch over all CUs of
     // this depth via a per-depth view (blocks of other depths return at once)
     const int first = d == 0 ? 0 : d == 1 ? 1 : d == 2 ? 5 : 21;
-    const bool fen = (P.me_flags & HVX_ME_FEN) != 0;
     const dim3 grid(L.nctu * ncu * L.nref);
-    const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
     switch (d) {  // block size, FEN row subsampling and waves per job are compile-time per depth
-      case 0:  // 64x64: integer search here, fractional refinement by k_me_frac_ctu below
+      case 0:  // 64x64: integer search here, fractional refinement by k_me_frac_ctu on stream B
         if (fen) hipLaunchKernelGGL((k_me_int_ctu<64, 1, 4>), grid, dim3(256), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
         else hipLaunchKernelGGL((k_me_int_ctu<64, 0, 4>), grid, dim3(256), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
         break;
@@ -583,15 +622,16 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
         hipLaunchKernelGGL((k_me_ctu<8, 0, 1>), grid, dim3(64), 0, st, cs, d_refs, stride, jobs, res, L.nref, ncu, first);
         break;
     }
+    t_end(ctx, st, tk);
+    if (d == 0) {  // fractional refinement of the 64x64 depth (the others are fused above)
+      const int tf = t_begin(ctx, st, 4);
+      hipLaunchKernelGGL((k_me_frac_ctu<64, 4>), dim3(L.nctu * L.nref), dim3(256), 0, st, cs, d_refs, stride, jobs, res,
+                         L.nref, 1, 0);
+      t_end(ctx, st, tf);
+    }
+    if (d == 1) HVX_HIP(hipEventRecord(ctx->fj[1], st));
+    if (d == 2) HVX_HIP(hipEventRecord(ctx->fj[2], st));
   }
-  // fractional refinement of the 64x64 depth (the others were fused above)
-  mark(ctx, 4);
-  hipLaunchKernelGGL((k_me_frac_ctu<64, 4>), dim3(L.nctu * L.nref), dim3(256), 0, st, (const uint8_t *const *)cur_slot,
-                     d_refs, stride, jobs, res, L.nref, 1, 0);
-  mark(ctx, 5);
-  hipLaunchKernelGGL(k_ctu_pred_resid, dim3(L.nctu * HVX_CUS_PER_CTU), dim3(64), 0, st, L, P, d_cur, d_refs, stride,
-                     res, resid, desc, off, est_idx, d_out);
-  const int n = L.nctu;
   // kCtuG = 64 TUs per RDOQ wave for every class: measured best at 2160p (G = 8/16/32/64 for
   // 32x32: 3.1/2.9/2.6/2.5 ms) -- the per-lane chain is latency-bound, so wider waves win
   const int g32 = kCtuG, g16 = kCtuG, g8 = kCtuG;
@@ -599,22 +639,38 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
   int8_t *flags = (int8_t *)(ws + W.flags);
   // size classes are contiguous: [0,8n) 32x32 | [8n,24n) 16x16 | [24n,88n) 8x8; their
   // interleaved scratch regions start at 0, ctu_il_off16(n), ctu_il_off8(n)
-  tu_class_launch<3, 2>(st, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev, nullptr, abs_sum, res_out, sse,
-                        coefI, levI, stI, flags, g32, 4, ctx, 6);
-  {
-    const size_t o = ctu_il_off16(n);
-    tu_class_launch<2, 2>(st, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n, 16 * n, resid, nullptr, lev, nullptr,
-                          abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, levI + o, stI + o, flags + 8 * n, g16, 4, ctx, 9);
+  {  // stream B
+    HVX_HIP(hipStreamWaitEvent(sb, ctx->fj[1], 0));
+    const int tk = t_begin(ctx, sb, 5);
+    resid_range(sb, 0, 5);
+    t_end(ctx, sb, tk);
+    tu_class_launch<3, 2>(sb, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev, nullptr, abs_sum, res_out, sse,
+                          coefI, levI, stI, flags, g32, 4, ctx, 6);
+    HVX_HIP(hipEventRecord(ctx->fj[3], sb));
   }
-  {
+  {  // stream C
+    HVX_HIP(hipStreamWaitEvent(sc, ctx->fj[2], 0));
+    const int tk = t_begin(ctx, sc, 5);
+    resid_range(sc, 5, 16);
+    t_end(ctx, sc, tk);
+    const size_t o = ctu_il_off16(n);
+    tu_class_launch<2, 2>(sc, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n, 16 * n, resid, nullptr, lev, nullptr,
+                          abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, levI + o, stI + o, flags + 8 * n, g16, 4, ctx, 9);
+    HVX_HIP(hipEventRecord(ctx->fj[4], sc));
+  }
+  {  // stream A: depth 3
+    const int tk = t_begin(ctx, st, 5);
+    resid_range(st, 21, 64);
+    t_end(ctx, st, tk);
     const size_t o = ctu_il_off8(n);
     tu_class_launch<1, 2>(st, desc + 24 * n, d_est4, est_idx + 24 * n, off + 24 * n, 64 * n, resid, nullptr, lev, nullptr,
                           abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, levI + o, stI + o, flags + 24 * n, g8, 4, ctx, 12);
   }
-  mark(ctx, 15);
+  HVX_HIP(hipStreamWaitEvent(st, ctx->fj[3], 0));
+  HVX_HIP(hipStreamWaitEvent(st, ctx->fj[4], 0));
+  const int tk = t_begin(ctx, st, 15);
   hipLaunchKernelGGL(k_ctu_finalize, dim3((n * HVX_CUS_PER_CTU + 255) / 256), dim3(256), 0, st, L, abs_sum, sse, d_out);
-  mark(ctx, 16);
-  if (ctx->timing && ctx->ev_ok) ctx->pending = 1;
+  t_end(ctx, st, tk);
   return launched("hvx_ctu_analyze");
 }
 

@@ -229,7 +229,9 @@ class CtuAnalyzer:
 PHASES = ("me_d0", "me_d1", "me_d2", "me_d3", "frac_d0", "mc_resid",
           "tu32_fwd", "tu32_rdoq", "tu32_fin", "tu16_fwd", "tu16_rdoq", "tu16_fin", "tu8_fwd", "tu8_rdoq", "tu8_fin",
           "finalize")
-# the kernel each phase times (one launch per phase, plus the tiny k_ctu_me_jobs in me_dN)
+# the kernel each phase times (plus the tiny k_ctu_me_jobs in me_dN) and its launches per
+# hvx_ctu_analyze call; phases run on 3 streams and may overlap (DESIGN.md "CTU analysis pass")
+PHASE_LAUNCHES = (1, 1, 1, 1, 1, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1)
 PHASE_KERNELS = ("k_me_int_ctu<64,1,4>", "k_me_ctu<32,1,2>", "k_me_ctu<16,1,1>", "k_me_ctu<8,0,1>",
                  "k_me_frac_ctu<64,4>", "k_ctu_pred_resid", "k_tu_fwd<3>", "k_tu_rdoq<3>", "k_tu_fin<3,2>",
                  "k_tu_fwd<2>", "k_tu_rdoq<2>", "k_tu_fin<2,2>", "k_tu_fwd<1>", "k_tu_rdoq<1>", "k_tu_fin<1,2>",
