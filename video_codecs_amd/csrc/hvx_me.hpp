@@ -664,8 +664,46 @@ __device__ __forceinline__ int me_vsample(const int *hw, int off, int fy) {
   return clip_pel((s + (1 << 11) + (8192 << 6)) >> 12);
 }
 
-// candidate index of (column c = dx+1, row d = dy+1) in s_acMvRefineH / s_acMvRefineQ order
-__constant__ int8_t kRefIdx[2][3][3] = {{{5, 3, 7}, {1, 0, 2}, {6, 4, 8}}, {{3, 5, 7}, {1, 0, 2}, {4, 6, 8}}};
+// Sums over the wave of the 9 candidates' |coefficient| vectors at once: permlane32 swaps
+// fold candidate pairs (2k, 2k+1) into the two wave halves, permlane16 swaps fold those pairs
+// into rows, DPP adds finish inside rows.  Every lane of row r of u[k] then holds the sum of
+// candidate 4k + {0,2,1,3}[r] (u[2]: row 0 = candidate 8, other rows 0).
+__device__ __forceinline__ void me_sum9(const int (&a)[9], uint32_t (&u)[3]) {
+  uint32_t w[5];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const auto p = __builtin_amdgcn_permlane32_swap((unsigned)a[2 * k], (unsigned)a[2 * k + 1], false, false);
+    w[k] = p[0] + p[1];
+  }
+  {
+    const auto p = __builtin_amdgcn_permlane32_swap((unsigned)a[8], 0u, false, false);
+    w[4] = p[0] + p[1];
+  }
+  {
+    const auto p = __builtin_amdgcn_permlane16_swap(w[0], w[1], false, false);
+    u[0] = p[0] + p[1];
+  }
+  {
+    const auto p = __builtin_amdgcn_permlane16_swap(w[2], w[3], false, false);
+    u[1] = p[0] + p[1];
+  }
+  {
+    const auto p = __builtin_amdgcn_permlane16_swap(w[4], 0u, false, false);
+    u[2] = p[0] + p[1];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    u[k] += ME_DPP(u[k], 0xB1);
+    u[k] += ME_DPP(u[k], 0x4E);
+    u[k] += ME_DPP(u[k], 0x141);
+    u[k] += ME_DPP(u[k], 0x140);
+  }
+}
+
+// candidate index (s_acMvRefineH / s_acMvRefineQ order) of slot c*3 + d, (dx, dy) = (c-1, d-1),
+// as 4-bit fields
+constexpr uint64_t kRefSlotH = 0x846201735ull, kRefSlotQ = 0x864201753ull;
+
 
 // xPatternRefinement (:808): the 9 candidates of one stage.  (qx0,qy0) = stage centre in
 // quarter-pel relative to the PU, step 2 (half) or 1 (quarter); (ix,iy) the integer MV.
@@ -742,9 +780,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
       if (d == 0) ryb = ry;
       offs[d] = ry - ryb; fys[d] = qy & 3;
     }
-    uint32_t dsum[9];
-#pragma unroll
-    for (int i = 0; i < 9; i++) dsum[i] = 0;
+    uint32_t acc[3] = {0u, 0u, 0u};
     for (int t = 0; t < nt; t++) {
       const int x = ((t % tw) << 3) + hx, y = ((t / tw) << 3) + hy;
       const int o = sm.org[y * S + x];
@@ -760,17 +796,25 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
       }
       had8_xlane_dpp<9>(v);
 #pragma unroll
-      for (int i = 0; i < 9; i++) dsum[i] += (wave_sum_dpp((uint32_t)abs(v[i])) + 2) >> 2;
-    }
-    const int sel = step == 2 ? 0 : 1;
+      for (int i = 0; i < 9; i++) v[i] = abs(v[i]);
+      uint32_t u[3];
+      me_sum9(v, u);
 #pragma unroll
-    for (int c = 0; c < 3; c++) {
-#pragma unroll
-      for (int d = 0; d < 3; d++) {
-        const int i = kRefIdx[sel][c][d];
-        if (lane == 0) sm.cost[i] = dsum[c * 3 + d] + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + c - 1, mvy0 + d - 1);
-      }
+      for (int k = 0; k < 3; k++) acc[k] += (u[k] + 2) >> 2;  // xCalcHADs8x8 rounding per tile
     }
+    // lane-parallel costs: lane (row r, kk = lane & 15 < 3) takes the slot s = c*3 + d me_sum9
+    // put there; the first minimum in the reference's candidate order is a (cost, index) key-min
+    const int kk = lane & 15, r = lane >> 4;
+    const bool valid = kk < 2 || (kk == 2 && r == 0);
+    const int sl = kk >= 2 ? 8 : 4 * kk + ((0xD8 >> (2 * r)) & 3);
+    const int c = (sl * 11) >> 5, dx = c - 1, dy = sl - 3 * c - 1;  // sl / 3, sl % 3 for sl < 9
+    const uint64_t idx = step == 2 ? kRefSlotH : kRefSlotQ;
+    const int ci = (int)((idx >> (4 * sl)) & 15);
+    const uint32_t dsum = kk == 0 ? acc[0] : kk == 1 ? acc[1] : acc[2];
+    const uint32_t cost = dsum + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
+    const uint32_t key = wave_min_key(valid ? (cost << 4) | (uint32_t)ci : kMeKeyNone);
+    bi = (int)(key & 15u);
+    return key >> 4;
   } else if (xl) {
     // this wave's candidates i = wave + NW*ii share each tile pass: their sample gathers and
     // Hadamard butterflies are independent and interleave
