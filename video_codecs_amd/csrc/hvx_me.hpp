@@ -585,12 +585,26 @@ struct MeFracSmem {
   uint32_t cost[9];
 };
 
-// one prediction sample of candidate column phase c at vertical quarter position qy
-// (relative to the integer MV row iy): the reference's second filter stage on hp[c]
+typedef short me_s2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int me_sel3(const int (&v)[3], int i) { return i == 0 ? v[0] : i == 1 ? v[1] : v[2]; }
+
+// first filter stage of two adjacent outputs: sum_t c[fx][t] * (b[t], b[t+1]) - 8192 on int16
+// pairs (P[t] = (b[t], b[t+1])), one v_pk_mad per tap
+__device__ __forceinline__ me_s2 me_fir_pk(int fx, const uint32_t *P) {
+  me_s2 acc = {-8192, -8192};
+#pragma unroll
+  for (int t = 0; t < 8; t++) acc = acc + (short)kLumaFilter[fx][t] * __builtin_bit_cast(me_s2, P[t]);
+  return acc;
+}
+
+// one prediction sample of a candidate column phase (its plane at element offset po of hp) at
+// vertical quarter position qy (relative to the integer MV row iy): the reference's second
+// filter stage
 template <int S, int NW, typename TO>
-__device__ __forceinline__ int me_frac_sample(const MeFracSmem<S, NW, TO> &sm, int c, int ry, int fy, int x, int y) {
+__device__ __forceinline__ int me_frac_sample(const MeFracSmem<S, NW, TO> &sm, int po, int ry, int fy, int x, int y) {
   constexpr int HS = MeFracSmem<S, NW, TO>::HS;
-  const int16_t *h = sm.hp[c] + x;
+  const int16_t *h = &sm.hp[0][0] + po + x;
   if (!fy) return clip_pel((h[(ry + 4 + y) * HS] + 8192 + 32) >> 6);
   int s = 0;
   const int r0 = ry + 1 + y;
@@ -715,10 +729,14 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
   constexpr int HS = MeFracSmem<S, NW, TO>::HS;
   const int w = GENERIC ? j.w : S, h = GENERIC ? j.h : S, lane = lane_id(), wave = threadIdx.x >> 6;
   const bool had = (j.flags & HVX_ME_HADME) != 0;
-  // 1. horizontal phases: column c at quarter x = qx0 + (c-1)*step.  Integer offsets of the
-  // phases are ix-1 or ix, so one item (row r, columns x0..x0+3) filters all 3 phases from the
-  // 12 bytes at columns x0+ix-4 .. x0+ix+7 (3 dword loads into registers).
+  // 1. horizontal phases: column c at quarter x = qx0 + (c-1)*step, integer offset ix-1 or ix
+  // (oxo 0/1), phase fx.  In the half stage columns 0 and 2 are the same half-sample filter one
+  // pixel apart: one plane of S+1 columns serves both (po[2] = po[0] + 1).  An item (row r,
+  // columns x0..x0+3) loads the 12 bytes at columns x0+ix-4 .. x0+ix+7 (one buffer load),
+  // forms the byte pairs and filters two outputs per v_pk_mad (8-bit taps and samples, 16-bit
+  // intermediates: the reference's first stage, offset -8192, fits int16 exactly).
   __syncthreads();
+  int po[3];
   {
     int oxo[3], fxs[3];
 #pragma unroll
@@ -727,39 +745,46 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
       oxo[c] = (qx >> 2) - ix + 1;  // 0 or 1
       fxs[c] = qx & 3;
     }
-    const int gw = w >> 2;
-    const uint8_t *src = ref + (iy - 4) * stride + (ix - 4);
-    for (int k = threadIdx.x; k < (h + 8) * gw; k += 64 * NW) {
-      const int r = k / gw, x0 = (k - r * gw) << 2;
-      const uint8_t *p = src + r * stride + x0;
-      const uint32_t w0 = ld4_any(p), w1 = ld4_any(p + 4), w2 = ld4_any(p + 8);
-      int b[12];
+    constexpr int PL = (S + 8) * HS;  // elements per plane
+    const bool shared = fxs[0] == fxs[2] && oxo[2] == oxo[0] + 1;
+    po[0] = 0; po[1] = PL; po[2] = shared ? 1 : 2 * PL;
+    const int gw = w >> 2, gwp = gw + (shared ? 1 : 0);
+    const __amdgpu_buffer_rsrc_t rs = me_plane_rsrc(ref - (j.pu_y * stride + j.pu_x), stride, j.pic_h);
+    const uint32_t base = (uint32_t)((HVX_PLANE_MARGIN + j.pu_y + iy - 4) * stride + HVX_PLANE_MARGIN + j.pu_x + ix - 4);
+    for (int k = threadIdx.x; k < (h + 8) * gwp; k += 64 * NW) {
+      const int r = k / gwp, x0 = (k - r * gwp) << 2;
+      const uint32_t a = base + (uint32_t)(r * stride + x0);
+      const me_v4u q = __builtin_amdgcn_raw_buffer_load_b128(rs, a & ~3u, 0, 0);
+      const uint32_t sh = a & 3u;
+      const uint32_t wv[3] = {__builtin_amdgcn_alignbyte(q.y, q.x, sh), __builtin_amdgcn_alignbyte(q.z, q.y, sh),
+                              __builtin_amdgcn_alignbyte(q.w, q.z, sh)};
+      uint32_t P[11];  // P[s] = (b[s], b[s+1]) as an int16 pair
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        b[q] = (w0 >> (8 * q)) & 255;
-        b[4 + q] = (w1 >> (8 * q)) & 255;
-        b[8 + q] = (w2 >> (8 * q)) & 255;
+      for (int t = 0; t < 11; t++) {
+        const uint32_t lo = wv[t >> 2], hi = wv[(t + 1) >> 2];
+        const uint32_t b0 = t & 3, b1 = ((t + 1) >> 2) == (t >> 2) ? ((t + 1) & 3) : 4;
+        P[t] = __builtin_amdgcn_perm(hi, lo, 0x0c000c00u | (b1 << 16) | b0);
       }
 #pragma unroll
       for (int c = 0; c < 3; c++) {
-        int bo[11];
-#pragma unroll
-        for (int q = 0; q < 11; q++) bo[q] = oxo[c] ? b[q + 1] : b[q];
+        if (c == 2 && shared) continue;
+        if (c != 0 && x0 >= w) continue;  // the extra column item only feeds the shared plane
         const int fx = fxs[c];
-        int16_t *dst = sm.hp[c] + r * HS + x0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          int v;
-          if (fx) {
-            v = 0;
-#pragma unroll
-            for (int t = 0; t < 8; t++) v += kLumaFilter[fx][t] * bo[i + t];
-            v -= 8192;
-          } else {
-            v = (bo[i + 3] << 6) - 8192;
-          }
-          dst[i] = (int16_t)v;
+        me_s2 o01, o23;
+        if (!fx) {
+          const me_s2 off = {-8192, -8192};
+          o01 = (oxo[c] ? __builtin_bit_cast(me_s2, P[4]) : __builtin_bit_cast(me_s2, P[3])) * (short)64 + off;
+          o23 = (oxo[c] ? __builtin_bit_cast(me_s2, P[6]) : __builtin_bit_cast(me_s2, P[5])) * (short)64 + off;
+        } else if (oxo[c]) {
+          o01 = me_fir_pk(fx, P + 1);
+          o23 = me_fir_pk(fx, P + 3);
+        } else {
+          o01 = me_fir_pk(fx, P);
+          o23 = me_fir_pk(fx, P + 2);
         }
+        uint32_t *dst = (uint32_t *)(&sm.hp[0][0] + po[c] + r * HS + x0);  // 8-byte aligned
+        dst[0] = __builtin_bit_cast(uint32_t, o01);
+        dst[1] = __builtin_bit_cast(uint32_t, o23);
       }
     }
   }
@@ -788,7 +813,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
 #pragma unroll
       for (int c = 0; c < 3; c++) {
         int hw[9];
-        const int16_t *h = sm.hp[c] + (ryb + 1 + y) * HS + x;
+        const int16_t *h = &sm.hp[0][0] + po[c] + (ryb + 1 + y) * HS + x;
 #pragma unroll
         for (int k = 0; k < 9; k++) hw[k] = h[k * HS];
 #pragma unroll
@@ -833,7 +858,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
       const int o = sm.org[y * S + x];
       int v[CPW];
 #pragma unroll
-      for (int ii = 0; ii < CPW; ii++) v[ii] = o - me_frac_sample(sm, cc[ii], cry[ii], cfy[ii], x, y);
+      for (int ii = 0; ii < CPW; ii++) v[ii] = o - me_frac_sample(sm, me_sel3(po, cc[ii]), cry[ii], cfy[ii], x, y);
       had8_xlane_dpp<CPW>(v);
 #pragma unroll
       for (int ii = 0; ii < CPW; ii++) dsum[ii] += (wave_sum_dpp((uint32_t)abs(v[ii])) + 2) >> 2;
@@ -856,7 +881,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
         uint8_t *blk = sm.blk[wave];
         for (int k = lane; k < w * h; k += HVX_WAVE) {
           const int y = k / w, x = k - y * w;
-          blk[y * S + x] = (uint8_t)me_frac_sample(sm, c, ry, fy, x, y);
+          blk[y * S + x] = (uint8_t)me_frac_sample(sm, me_sel3(po, c), ry, fy, x, y);
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -866,7 +891,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
       uint32_t sacc = 0;
       for (int k = lane; k < w * h; k += HVX_WAVE) {
         const int y = k / w, x = k - y * w;
-        sacc += (uint32_t)abs((int)sm.org[y * S + x] - me_frac_sample(sm, c, ry, fy, x, y));
+        sacc += (uint32_t)abs((int)sm.org[y * S + x] - me_frac_sample(sm, me_sel3(po, c), ry, fy, x, y));
       }
       d = wave_sum_u32(sacc);
     }
