@@ -17,19 +17,28 @@ CASES = {  # name: (cfg, yuv kind, frames, qp)
     "intra_smooth_qp22": ("intra.cfg", "smooth", 1, 22),
     "ldp_smooth_qp32": ("ldp.cfg", "smooth", 3, 32),
     "ldb_smooth_qp32": ("ldb.cfg", "smooth", 3, 32),  # B slices: bi-prediction, identical-motion shortcut
+    "ldp_rand_qp32": ("ldp.cfg", "random", 3, 32),    # uniform random: long TZ raster searches
+    "ra_smooth_qp27": ("ra.cfg", "smooth", 9, 27),    # GOP8 hierarchical B: future refs, bBi refinement
 }
+YUV_FRAMES = max(c[2] for c in CASES.values())
 W, H = 416, 240
 
 
-def encode(binary, case, tmp):
+def encode(binary, case, tmp, log=None):
+    """Encode `case` with `binary`; the encoder's stderr (the seams' call counters) is appended
+    to the list `log` when given."""
     cfg, kind, frames, qp = CASES[case]
     yuv = os.path.join(tmp, f"{kind}.yuv")
     if not os.path.exists(yuv):
-        make_yuv.write_yuv(yuv, kind, W, H, 3)
+        make_yuv.write_yuv(yuv, kind, W, H, YUV_FRAMES)
     bs, rec = os.path.join(tmp, case + ".bin"), os.path.join(tmp, case + ".rec.yuv")
-    subprocess.check_call([binary, "-c", os.path.join(HERE, cfg), "-i", yuv, "-wdt", str(W), "-hgt", str(H), "-fr", "30",
-                           "-f", str(frames), "-q", str(qp), "-b", bs, "-o", rec],
-                          stdout=subprocess.DEVNULL)
+    p = subprocess.run([binary, "-c", os.path.join(HERE, cfg), "-i", yuv, "-wdt", str(W), "-hgt", str(H), "-fr", "30",
+                        "-f", str(frames), "-q", str(qp), "-b", bs, "-o", rec],
+                       stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    if log is not None:
+        log.append(p.stderr)
+    if p.returncode:
+        raise RuntimeError(f"{binary} failed ({p.returncode}): {p.stderr[-2000:]}")
     md5 = lambda p: hashlib.md5(open(p, "rb").read()).hexdigest()
     return {"bitstream_md5": md5(bs), "recon_md5": md5(rec)}
 

@@ -1,7 +1,10 @@
 """End-to-end drop-in check: the UNCHANGED reference TAppEncoder (HM-16.5rc1), with every
-TComTrQuant::transformNxN / invTransformNxN call served by libhvx.so on the MI355X
-(integration/hm_tu_seam.cpp), must produce the same bitstream and reconstruction MD5 as the
-reference CPU build (tests/hm_seam/expected_md5.json, recorded by make_expected.py)."""
+TComTrQuant::transformNxN / invTransformNxN call (integration/hm_tu_seam.cpp), every
+TComPrediction::motionCompensation call (hm_mc_seam.cpp) and every TEncSearch::xMotionEstimation
+call (hm_me_seam.cpp) served by libhvx.so on the MI355X, must produce the same bitstream and
+reconstruction MD5 as the reference CPU build (tests/hm_seam/expected_md5.json, recorded by
+make_expected.py)."""
+import re
 import json
 import os
 import subprocess
@@ -18,15 +21,23 @@ EXPECTED = json.load(open(os.path.join(ROOT, "tests", "hm_seam", "expected_md5.j
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", sorted(mk.CASES))
-def test_hm_encoder_with_hvx_tu_seam(case):
+def test_hm_encoder_with_hvx_seams(case):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     if not os.path.exists(EXE):
         pytest.skip("TAppEncoder_hvx not built (needs /root/reference at build time)")
+    log = []
     with tempfile.TemporaryDirectory() as tmp:
-        got = mk.encode(EXE, case, tmp)
+        got = mk.encode(EXE, case, tmp, log)
+    print(log[0][-600:])
     assert got == EXPECTED[case], (case, got, EXPECTED[case])
+    m = re.search(r"hm_me_seam: (\d+) xMotionEstimation calls served .* (\d+) fell through", log[0])
+    assert m, log[0][-2000:]
+    served, fell = int(m.group(1)), int(m.group(2))
+    assert fell == 0
+    if not case.startswith("intra"):
+        assert served > 0
 
 
 def test_expected_md5_cases_present():
