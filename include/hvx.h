@@ -30,6 +30,9 @@
  *   hvx_stvssim_batch     compute_stVSSIM (stvssim.c:587)
  *   hvx_estbits_update / hvx_estbits_batch   TEncSbac::estBit (TEncSbac.cpp:1726)
  *   hvx_mc_batch          TComPrediction::motionCompensation (TComPrediction.cpp:517)
+ *   hvx_coeff_bits_batch  TEncEntropy::encodeCoeffNxN -> TEncSbac::codeCoeffNxN (TEncEntropy.cpp:654,
+ *                         TEncSbac.cpp:1181) under TEncBinCABACCounter (TEncBinCoderCABACCounter.cpp:74):
+ *                         the RD search's coefficient rate (TEncSearch.cpp:969, 4706, 4875, 5136)
  *   hvx_me_full_batch     TEncSearch::xMotionEstimation with xPatternSearch (:3786), incl. bBi
  *   hvx_ctu_analyze       TEncCu::compressCtu's inter 2Nx2N analysis for every CU of every CTU
  *                         (TEncCu.cpp:228,349,1291 -> predInterSearch/encodeResAndCalcRdInterCU):
@@ -206,6 +209,20 @@ int hvx_estbits_update(const uint8_t *ctx_states, const int32_t *entropy_bits, c
 /* batched device form: job i reads d_states[i*HVX_NUM_CTX ..], d_rice[i*4 ..], updates d_inout[i] */
 int hvx_estbits_batch(hvx_ctx *ctx, const uint8_t *d_states, const int32_t *d_entropy_bits, const uint32_t *d_rice,
                       const hvx_estbit_job *d_jobs, int n, hvx_estbits *d_inout);
+
+/* ---------------------------------------------------------------------------------------
+ * Coefficient rate: TEncSbac::codeCoeffNxN counted by TEncBinCABACCounter (the RD search's
+ * bit estimate of one TU's levels; TEncSbac.cpp:1181).  TU i reads its desc d_desc[i] (comp,
+ * width == height in {4,8,16,32}, scan_type, transform_skip, pps_tskip, sign_hiding,
+ * transquant_bypass, golomb_rice_stat, persistent_rice, ts_context, extended_precision,
+ * max_log2_tr_range), w*h raster int32 levels at element offset d_off[i] of d_levels, and
+ * the RD coder's context states d_states[i*HVX_NUM_CTX ..] (m_contextModels order, advanced in
+ * place bin by bin as the counter does).  d_entropy_bits = ContextModel::m_entropyBits (128).
+ * d_out[i].frac_bits = increase of m_fracBits (bits = frac >> 15); num_sig = 0 for an all-zero
+ * TU (nothing coded; the reference refuses such a call), 0xffffffff for an unsupported shape.
+ * ------------------------------------------------------------------------------------- */
+int hvx_coeff_bits_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t *d_off, int n, const int32_t *d_levels,
+                         const int32_t *d_entropy_bits, uint8_t *d_states, hvx_coeff_bits *d_out);
 
 /* ---------------------------------------------------------------------------------------
  * CTU analysis pass over a whole picture (hvx_types.h): d_cur = sample (0,0) of the current

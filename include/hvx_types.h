@@ -50,9 +50,19 @@ typedef struct hvx_tu_desc {
   int32_t persistent_rice, extended_precision, ts_context;
   int32_t max_log2_tr_range;  /* 15 for 8-bit Main */
   int32_t bit_depth;          /* 8 */
-  int32_t pad_;
+  int32_t pps_tskip;          /* PPS transform_skip_enabled_flag (read by codeCoeffNxN's
+                                 codeTransformSkipFlags only; log2MaxTransformSkipBlockSize 2) */
   double lambda;              /* TComTrQuant::m_dLambda after selectLambda(compID) */
 } hvx_tu_desc;
+
+/* TEncSbac::codeCoeffNxN (TEncSbac.cpp:1181) counted by TEncBinCABACCounter
+ * (TEncBinCoderCABACCounter.cpp:74-120): the rate of one TU's coefficients as the RD search
+ * measures it, from the RD coder's context states (which the count also advances). */
+typedef struct hvx_coeff_bits {
+  uint64_t frac_bits;         /* increase of TEncBinCABACCounter::m_fracBits (15-bit fixed point) */
+  uint32_t rice_stat;         /* m_golombRiceAdaptationStatistics[statIdx] after the call */
+  uint32_t num_sig;           /* non-zero coefficients (0: the reference's empty-TU exit, nothing coded) */
+} hvx_coeff_bits;
 
 /* One uni-prediction motion search: TEncSearch::xMotionEstimation with bBi=false
  * (TEncSearch.cpp:3663-3760): TZ integer search + half/quarter refinement. */

@@ -265,3 +265,18 @@ def me_full(tgt_block, job, ref_plane, margin=_abi.PLANE_MARGIN):
     out = np.zeros(1, _abi.ME_RESULT)
     lib().hvxo_me_full(ctypes.c_void_p(virt), 64, ctypes.c_void_p(origin), r.shape[1], _p(j), _p(out))
     return out[0]
+
+
+def coeff_bits(desc, levels, states, entropy_bits):
+    """hvxo_coeff_bits: TEncSbac::codeCoeffNxN under TEncBinCABACCounter.  Returns
+    (frac_bits, rice_stat_after, num_sig, states_after)."""
+    L = lib()
+    d = np.ascontiguousarray(desc, dtype=_abi.TU_DESC).reshape(1)
+    lv = _c(levels, np.int32)
+    st = np.zeros(256, np.uint8)
+    st[:len(states)] = states
+    eb = _c(entropy_bits, np.int32)
+    out = np.zeros(1, _abi.COEFF_BITS)
+    L.hvxo_coeff_bits.argtypes = [ctypes.c_void_p] * 5
+    L.hvxo_coeff_bits(_p(d), _p(lv), _p(st), _p(eb), _p(out))
+    return int(out["frac_bits"][0]), int(out["rice_stat"][0]), int(out["num_sig"][0]), st[:len(states)].copy()

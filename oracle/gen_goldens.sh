@@ -33,4 +33,15 @@ HVX_CAPTURE="$TMP/est_i.bin" $ORC/TAppEncoder_estcap -c $CFG/encoder_intra_main.
 HVX_CAPTURE="$TMP/est_p.bin" $ORC/TAppEncoder_estcap -c $CFG/encoder_lowdelay_P_main.cfg -i "$TMP/smooth.yuv" \
   -wdt 416 -hgt 240 -fr 30 -f 3 -q 27 -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
 python3 oracle/merge_goldens.py tests/golden/estbit.bin "$TMP/est_i.bin" "$TMP/est_p.bin"
+# coefficient rate: TEncSbac::codeCoeffNxN under TEncBinCABACCounter (oracle/cabac_capture.cpp)
+cab() {  # cab <out.bin> <cfg> <yuv> <frames> <qp>
+  HVX_CAPTURE=$1 $ORC/TAppEncoder_cabcap -c "$2" -i "$3" -wdt 416 -hgt 240 -fr 30 -f "$4" -q "$5" \
+    -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+}
+cab "$TMP/cab_i.bin"   $CFG/encoder_intra_main.cfg      "$TMP/rand.yuv"   1 32
+cab "$TMP/cab_i22.bin" $CFG/encoder_intra_main.cfg      "$TMP/smooth.yuv" 1 22
+cab "$TMP/cab_p.bin"   $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth.yuv" 3 27
+cab "$TMP/cab_p22.bin" $CFG/encoder_lowdelay_P_main.cfg "$TMP/rand.yuv"   2 22
+python3 oracle/merge_goldens.py tests/golden/cabac.bin "$TMP"/cab_i.bin "$TMP"/cab_i22.bin "$TMP"/cab_p.bin "$TMP"/cab_p22.bin
+python3 oracle/compact_cabac.py tests/golden/cabac.bin
 ls -la tests/golden

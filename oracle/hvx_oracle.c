@@ -1462,6 +1462,190 @@ void hvxo_estbits_update(const uint8_t *states, const int32_t *eb, const uint32_
 
 
 /* ============================================================================================
+ * Coefficient rate: TEncSbac::codeCoeffNxN (TEncSbac.cpp:1181-1540) with codeTransformSkipFlags
+ * (:997), codeLastSignificantXY (:1115), xWriteCoefRemainExGolomb (:337), counted by
+ * TEncBinCABACCounter (TEncBinCoderCABACCounter.cpp:74-120): encodeBin adds
+ * m_entropyBits[state ^ bin] and advances the state (ContextModel.h:79-85), bypass bins add
+ * 32768 each.  State transitions are the specification's (transIdxLps; MPS: +1 up to 62).
+ * Main-profile scope: no RDPCM, no CABAC bypass alignment.
+ * ========================================================================================== */
+static const uint8_t kTransIdxLps[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7,  8,  9,  9,  11, 11, 12,
+                                         13, 13, 15, 15, 16, 16, 18, 18, 19, 19, 21, 21, 22, 22, 23, 24,
+                                         24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30, 31, 32, 32, 33,
+                                         33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63};
+static const int kMinInGroup[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};
+
+typedef struct {
+  uint8_t *st;
+  const int32_t *eb;
+  uint64_t frac;
+} cab_counter;
+
+/* TEncBinCABACCounter::encodeBin + ContextModel::update */
+static void cab_bin(cab_counter *c, int ctx, int v) {
+  const int s = c->st[ctx], p = s >> 1, mps = s & 1;
+  c->frac += (uint32_t)c->eb[s ^ v];
+  if (v == mps) c->st[ctx] = (uint8_t)(((p < 62 ? p + 1 : p) << 1) | mps);
+  else c->st[ctx] = (uint8_t)((kTransIdxLps[p] << 1) | (p == 0 ? mps ^ 1 : mps));
+}
+static inline void cab_ep(cab_counter *c, int n) { c->frac += 32768u * (uint32_t)n; } /* encodeBinsEP */
+
+/* xWriteCoefRemainExGolomb (:337): number of bypass bins */
+static int remain_bins(uint32_t symbol, int r, int limited, int max_log2) {
+  if (symbol < (3u << r)) return (int)(symbol >> r) + 1 + r;
+  if (limited) {
+    const uint32_t maxp = 32 - (3 + max_log2);
+    uint32_t prefix = 0, suffix_len;
+    const uint32_t v = (symbol >> r) - 3;
+    if (v >= ((1u << maxp) - 1)) {
+      prefix = maxp;
+      suffix_len = (uint32_t)(max_log2 - r);
+    } else {
+      while (v > ((2u << prefix) - 2)) prefix++;
+      suffix_len = prefix + 1;
+    }
+    return (int)(prefix + 3 + suffix_len + r);
+  }
+  int len = r;
+  uint32_t cn = symbol - (3u << r);
+  while (cn >= (1u << len)) cn -= (1u << (len++));
+  return 3 + len + 1 - r + len;
+}
+
+static int log2_4_32(int n) { return n == 4 ? 2 : n == 8 ? 3 : n == 16 ? 4 : 5; }
+
+void hvxo_coeff_bits(const hvx_tu_desc *tu, const int32_t *coef, uint8_t *states, const int32_t *eb, hvx_coeff_bits *out) {
+  const int w = tu->width, h = tu->height, lw = log2_4_32(w), lh = log2_4_32(h), n = w * h;
+  const int ch = tu->comp ? 1 : 0;
+  cab_counter c = {states, eb, 0};
+  uint32_t rice_stat = (uint32_t)tu->golomb_rice_stat;
+  int num_sig = 0, i;
+  for (i = 0; i < n; i++) num_sig += coef[i] != 0;
+  out->num_sig = (uint32_t)num_sig;
+  if (num_sig == 0) { /* the reference exits (1) here; nothing is coded */
+    out->frac_bits = 0;
+    out->rice_stat = rice_stat;
+    return;
+  }
+  const int be_valid = tu->transquant_bypass ? 0 : tu->sign_hiding;
+  /* codeTransformSkipFlags (:997): TUCompRectHasAssociatedTransformSkipFlag, log2 max 2 */
+  if (tu->pps_tskip && !tu->transquant_bypass && w <= 4) cab_bin(&c, 183 + ch, tu->transform_skip ? 1 : 0);
+  coding_params cp;
+  get_coding_params(tu, &cp);
+  uint32_t cg_flags[64];
+  memset(cg_flags, 0, sizeof(cg_flags));
+  int scan_last = -1, pos_last = 0, left = num_sig;
+  do {
+    pos_last = (int)cp.scan[++scan_last];
+    if (coef[pos_last]) {
+      const int py = pos_last >> lw, px = pos_last - (py << lw);
+      cg_flags[cp.wg * (py >> 2) + (px >> 2)] = 1;
+      left--;
+    }
+  } while (left > 0);
+  /* codeLastSignificantXY (:1115) */
+  {
+    int py = pos_last >> lw, px = pos_last - (py << lw), bw = w, bh = h;
+    if (cp.scan_type == 2) { int t = px; px = py; py = t; t = bw; bw = bh; bh = t; }
+    const int gx = kGroupIdx[px], gy = kGroupIdx[py];
+    const int cw = log2_4_32(bw) - 2, chh = log2_4_32(bh) - 2; /* getLastSignificantContextParameters */
+    const int ox = ch ? 0 : cw * 3 + ((cw + 1) >> 2), oy = ch ? 0 : chh * 3 + ((chh + 1) >> 2);
+    const int sx = ch ? cw : (cw + 3) >> 2, sy = ch ? chh : (chh + 3) >> 2;
+    const int bx = 90 + ch * 15 + ox, by = 120 + ch * 15 + oy;
+    int k;
+    for (k = 0; k < gx; k++) cab_bin(&c, bx + (k >> sx), 1);
+    if (gx < kGroupIdx[bw - 1]) cab_bin(&c, bx + (k >> sx), 0);
+    for (k = 0; k < gy; k++) cab_bin(&c, by + (k >> sy), 1);
+    if (gy < kGroupIdx[bh - 1]) cab_bin(&c, by + (k >> sy), 0);
+    if (gx > 3) cab_ep(&c, (gx - 2) >> 1);
+    if (gy > 3) cab_ep(&c, (gy - 2) >> 1);
+    (void)kMinInGroup;
+  }
+  const int base_cg = 42 + ch * 2, base_sig = 46 + (ch ? 28 : 0);
+  const int last_set = scan_last >> 4;
+  int c1 = 1, scan_sig = scan_last;
+  for (int sub = last_set; sub >= 0; sub--) {
+    int nnz = 0, sub_pos = sub << 4, last_nz = -1, first_nz = 16, escape = 0;
+    int rice = (int)(rice_stat / 4);
+    int upd_rice = tu->persistent_rice;
+    uint32_t signs = 0;
+    int absc[16];
+    if (scan_sig == scan_last) {
+      absc[0] = abs(coef[pos_last]);
+      signs = coef[pos_last] < 0;
+      nnz = 1;
+      last_nz = first_nz = scan_sig;
+      scan_sig--;
+    }
+    const int cg = (int)cp.scan_cg[sub], cgy = cg / cp.wg, cgx = cg - cgy * cp.wg;
+    if (sub == last_set || sub == 0) cg_flags[cg] = 1;
+    else cab_bin(&c, base_cg + sig_cg_ctx(cg_flags, cgx, cgy, cp.wg, cp.hg), cg_flags[cg] != 0);
+    if (cg_flags[cg]) {
+      const int pattern = pattern_sig_ctx(cg_flags, cgx, cgy, cp.wg, cp.hg);
+      for (; scan_sig >= sub_pos; scan_sig--) {
+        const int blk = (int)cp.scan[scan_sig], sig = coef[blk] != 0;
+        if (scan_sig > sub_pos || sub == 0 || nnz) cab_bin(&c, base_sig + sig_ctx_inc(pattern, &cp, scan_sig, lw, lh, ch), sig);
+        if (sig) {
+          absc[nnz] = abs(coef[blk]);
+          signs = 2 * signs + (coef[blk] < 0);
+          nnz++;
+          if (last_nz == -1) last_nz = scan_sig;
+          first_nz = scan_sig;
+        }
+      }
+    } else {
+      scan_sig = sub_pos - 1;
+    }
+    if (nnz > 0) {
+      const int hidden = (last_nz - first_nz) >= 4; /* SBH_THRESHOLD */
+      const int set = ctx_set_index(tu->comp, sub, c1 == 0);
+      c1 = 1;
+      const int base_one = 150 + 4 * set;
+      const int nc1 = nnz < 8 ? nnz : 8;
+      int first_c2 = -1;
+      for (int k = 0; k < nc1; k++) {
+        const int gt1 = absc[k] > 1;
+        cab_bin(&c, base_one + c1, gt1);
+        if (gt1) {
+          c1 = 0;
+          if (first_c2 == -1) first_c2 = k;
+          else escape = 1;
+        } else if (c1 < 3 && c1 > 0) {
+          c1++;
+        }
+      }
+      if (c1 == 0 && first_c2 != -1) {
+        const int gt2 = absc[first_c2] > 2;
+        cab_bin(&c, 174 + set, gt2);
+        if (gt2) escape = 1;
+      }
+      escape = escape || nnz > 8;
+      cab_ep(&c, (be_valid && hidden) ? nnz - 1 : nnz);
+      if (escape) {
+        int first2 = 1;
+        for (int k = 0; k < nnz; k++) {
+          const int base = k < 8 ? 2 + first2 : 1;
+          if (absc[k] >= base) {
+            const uint32_t esc = (uint32_t)(absc[k] - base);
+            cab_ep(&c, remain_bins(esc, rice, tu->extended_precision, tu->max_log2_tr_range));
+            if (absc[k] > (3 << rice)) rice = tu->persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
+            if (upd_rice) {
+              const uint32_t init = rice_stat / 4;
+              if (esc >= (3u << init)) rice_stat++;
+              else if (esc * 2 < (1u << init) && rice_stat > 0) rice_stat--;
+              upd_rice = 0;
+            }
+          }
+          if (absc[k] >= 2) first2 = 0;
+        }
+      }
+    }
+  }
+  out->frac_bits = c.frac;
+  out->rice_stat = rice_stat;
+}
+
+/* ============================================================================================
  * Motion compensation: TComPrediction.cpp:517-722, TComYuv.cpp:352 (8-bit, 4:2:0, no WP)
  * ========================================================================================== */
 /* TComYuv::addAvg: shiftNum = max(2, IF_INTERNAL_PREC - 8) + 1 = 7,

@@ -73,6 +73,10 @@ void hvxo_add_avg(const int16_t *a, const int16_t *b, int16_t *dst, int n);
 void hvxo_estbits_update(const uint8_t *states, const int32_t *entropy_bits, const uint32_t *rice, int w, int h, int ch,
                          hvx_estbits *e);
 double hvxo_adjust_lambda(double lambda, double eta);
+/* TEncSbac::codeCoeffNxN counted by TEncBinCABACCounter (TEncSbac.cpp:1181): coef = w*h levels
+ * (raster), states = the RD coder's HVX_NUM_CTX context states (advanced in place), eb =
+ * ContextModel::m_entropyBits (128) */
+void hvxo_coeff_bits(const hvx_tu_desc *tu, const int32_t *coef, uint8_t *states, const int32_t *eb, hvx_coeff_bits *out);
 
 /* ---- CTU analysis pass (the bench workload, hvx_types.h) ---- */
 void hvxo_ctu_tu_desc(const hvx_ctu_params *p, int cu_size, int log2, hvx_tu_desc *d);

@@ -94,3 +94,19 @@ def me_full_jobs(g):
     jobs["lambda_motion"] = [_abi.lambda_motion_sad(l) for l in g["lambda"]]
     jobs["flags"] = _abi.ME_FEN | _abi.ME_HADME | np.where(j[:, 9] != 0, _abi.ME_BI, 0)
     return g["planes"], jobs, g["targets"], g["res"]
+
+
+def cabac_cases(g):
+    """cabac.bin (oracle/cabac_capture.cpp) -> (TU_DESC[n], list of int32 level arrays)."""
+    meta = g["meta"]
+    n = meta.shape[0]
+    d = np.zeros(n, _abi.TU_DESC)
+    for k, f in enumerate(("width", "height", "comp", "scan_type", "transform_skip", "pps_tskip", "sign_hiding",
+                           "transquant_bypass", "is_intra", "golomb_rice_stat", "persistent_rice", "ts_context",
+                           "extended_precision", "max_log2_tr_range")):
+        d[f] = meta[:, k]
+    d["bit_depth"] = 8
+    d["log2_size"] = np.log2(meta[:, 0]).astype(np.int32)
+    off = g["coef_off"]
+    levels = [g["coef_flat"][off[i]:off[i + 1]].astype(np.int32) for i in range(n)]
+    return d, levels

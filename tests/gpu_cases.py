@@ -318,3 +318,57 @@ def check_me_full_golden():
         assert [int(x) for x in got[i]] == [int(x) for x in exp[i]], (i, jobs[i], got[i], exp[i])
     del ref_t
     return n
+
+
+def random_coeff_tus(seed, n):
+    """Random TUs for the coefficient-rate counter: sizes 4-32, both channels, all scans,
+    sparse to dense levels with large escape values, random (valid) context states."""
+    rng = np.random.default_rng(seed)
+    descs = np.zeros(n, _abi.TU_DESC)
+    levels, states = [], np.zeros((n, _abi.NUM_CTX), np.uint8)
+    for i in range(n):
+        w = int(rng.choice([4, 8, 16, 32]))
+        d = descs[i:i + 1]
+        d["width"] = d["height"] = w
+        d["log2_size"] = int(np.log2(w))
+        d["comp"] = int(rng.integers(0, 3))
+        d["scan_type"] = int(rng.integers(0, 3)) if w <= 8 else 0
+        d["pps_tskip"] = int(rng.integers(0, 2))
+        d["transform_skip"] = int(rng.integers(0, 2)) if w == 4 else 0
+        d["sign_hiding"] = int(rng.integers(0, 2))
+        d["transquant_bypass"] = int(rng.random() < 0.1)
+        d["ts_context"] = int(rng.random() < 0.2)
+        d["persistent_rice"] = int(rng.integers(0, 2))
+        d["golomb_rice_stat"] = int(rng.integers(0, 16)) if d["persistent_rice"][0] else 0
+        d["extended_precision"] = int(rng.random() < 0.2)
+        d["max_log2_tr_range"] = 15
+        d["bit_depth"] = 8
+        dens = rng.choice([0.0, 0.02, 0.1, 0.4, 1.0])
+        mag = rng.choice([2, 4, 40, 2000, 32767])
+        lv = (rng.random(w * w) < dens) * rng.integers(1, mag + 1, w * w)
+        lv = np.where(rng.random(w * w) < 0.5, -lv, lv).astype(np.int32)
+        if not lv.any() and rng.random() < 0.7:
+            lv[int(rng.integers(0, w * w))] = int(rng.integers(-3, 4)) or 1
+        levels.append(lv)
+        states[i] = rng.integers(0, 126, _abi.NUM_CTX)
+    return descs, levels, states
+
+
+def check_coeff_bits_random(seed, n):
+    import torch
+    descs, levels, states = random_coeff_tus(seed, n)
+    eb = gc.load("cabac.bin")["entropy_bits"].astype(np.int32)
+    off = np.concatenate([[0], np.cumsum([len(l) for l in levels])[:-1]]).astype(np.int64)
+    d_st = torch.from_numpy(states.reshape(-1).copy()).cuda()
+    out = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    hvx.coeff_bits_batch(hvx.to_device(descs), hvx.to_device(off), n, hvx.to_device(np.concatenate(levels)),
+                         hvx.to_device(eb), d_st, out)
+    torch.cuda.synchronize()
+    r = out.cpu().numpy().view(_abi.COEFF_BITS)
+    st_gpu = d_st.cpu().numpy().reshape(n, -1)
+    for i in range(n):
+        fb, rice, ns, st = oracle.coeff_bits(descs[i], levels[i], states[i], eb)
+        got = (int(r["frac_bits"][i]), int(r["rice_stat"][i]), int(r["num_sig"][i]))
+        assert got == (fb, rice, ns), (i, descs[i], got, (fb, rice, ns))
+        np.testing.assert_array_equal(st_gpu[i], st, err_msg=f"TU {i}")
+    return True

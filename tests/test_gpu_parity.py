@@ -174,3 +174,28 @@ def test_mc_random_gpu(torch):
 
 def test_me_full_golden_gpu(torch):
     assert gpu_cases.check_me_full_golden() == 120
+
+
+def test_coeff_bits_golden_gpu(torch):
+    # codeCoeffNxN rate on the device, one TU per lane: the 3154 captured reference calls
+    g = gc.load("cabac.bin")
+    descs, levels = gc.cabac_cases(g)
+    n = len(levels)
+    off = np.asarray(g["coef_off"][:n], np.int64)
+    flat = np.concatenate(levels).astype(np.int32)
+    d_st = torch.from_numpy(np.ascontiguousarray(g["states_before"]).reshape(-1).copy()).cuda()
+    out = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    hvx.coeff_bits_batch(hvx.to_device(descs), hvx.to_device(off), n, hvx.to_device(flat),
+                         hvx.to_device(g["entropy_bits"].astype(np.int32)), d_st, out)
+    torch.cuda.synchronize()
+    r = out.cpu().numpy().view(hvx._abi.COEFF_BITS)
+    np.testing.assert_array_equal(r["frac_bits"].astype(np.int64), g["frac"][:, 1] - g["frac"][:, 0])
+    np.testing.assert_array_equal(r["rice_stat"], g["rice_after"].astype(np.uint32))
+    np.testing.assert_array_equal(r["num_sig"], [np.count_nonzero(l) for l in levels])
+    np.testing.assert_array_equal(d_st.cpu().numpy().reshape(n, -1), g["states_after"])
+
+
+def test_coeff_bits_random_gpu(torch):
+    # random levels (sparse, dense, large escapes; every size / scan / channel / transform skip,
+    # persistent Rice adaptation on and off) and random context states vs the oracle
+    assert gpu_cases.check_coeff_bits_random(seed=23, n=700)

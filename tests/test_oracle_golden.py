@@ -123,3 +123,20 @@ def test_me_full_golden():
     for i in range(len(jobs)):
         r = oracle.me_full(tg[i], jobs[i], planes[int(jobs[i]["ref_idx"]), 1])
         assert [int(x) for x in r] == [int(x) for x in exp[i]], (i, jobs[i], r, exp[i])
+
+
+def test_coeff_bits_golden():
+    # TEncSbac::codeCoeffNxN under TEncBinCABACCounter, captured from intra and LDP encodes at
+    # QP 22-32 (oracle/cabac_capture.cpp): levels + context states before -> the counter's
+    # fracBits increase, the context states after and the Golomb-Rice statistic after
+    g = gc.load("cabac.bin")
+    descs, levels = gc.cabac_cases(g)
+    n = len(levels)
+    assert n > 3000
+    assert {int(w) for w in descs["width"]} == {4, 8, 16, 32} and descs["transform_skip"].any()
+    for i in range(n):
+        fb, rice, ns, st = oracle.coeff_bits(descs[i], levels[i], g["states_before"][i], g["entropy_bits"])
+        assert ns == int(np.count_nonzero(levels[i]))
+        assert fb == int(g["frac"][i, 1] - g["frac"][i, 0]), (i, descs[i])
+        assert rice == int(g["rice_after"][i])
+        np.testing.assert_array_equal(st, g["states_after"][i], err_msg=f"record {i}")

@@ -9,7 +9,7 @@ TU_INT_FIELDS = (
     "comp", "width", "height", "log2_size", "scan_type", "use_dst", "transform_skip", "is_intra",
     "tr_idx", "ctx_qt_cbf", "slice_type", "qp_per", "qp_rem", "sign_hiding", "use_rdoq", "use_rdoq_ts",
     "selective_rdoq", "adaptive_qp_select", "transquant_bypass", "golomb_rice_stat", "persistent_rice",
-    "extended_precision", "ts_context", "max_log2_tr_range", "bit_depth", "pad_",
+    "extended_precision", "ts_context", "max_log2_tr_range", "bit_depth", "pps_tskip",
 )
 TU_DESC = np.dtype([(f, "<i4") for f in TU_INT_FIELDS] + [("lambda", "<f8")], align=True)
 assert TU_DESC.itemsize == 112
@@ -71,3 +71,8 @@ MC_JOB = np.dtype([("pic_w", "<i4"), ("pic_h", "<i4"), ("max_cu", "<i4"), ("cu_x
                    ("pu_x", "<i4"), ("pu_y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("ref", "<i4", (2,)),
                    ("poc", "<i4", (2,)), ("mv_x", "<i4", (2,)), ("mv_y", "<i4", (2,)), ("flags", "<i4"),
                    ("dst_offset", "<i8")], align=True)
+
+# hvx_coeff_bits (hvx_types.h): TEncSbac::codeCoeffNxN counted by TEncBinCABACCounter
+COEFF_BITS = np.dtype([("frac_bits", "<u8"), ("rice_stat", "<u4"), ("num_sig", "<u4")])
+assert COEFF_BITS.itemsize == 16
+NUM_CTX = 202

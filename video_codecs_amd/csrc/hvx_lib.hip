@@ -17,6 +17,7 @@
 #include "hvx_ctu.hpp"
 #include "hvx_estbit.hpp"
 #include "hvx_mc.hpp"
+#include "hvx_cabac.hpp"
 
 struct hvx_ctx {
   int device = 0;
@@ -501,6 +502,16 @@ int hvx_estbits_batch(hvx_ctx *ctx, const uint8_t *d_states, const int32_t *d_en
   hipLaunchKernelGGL(k_estbits, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, d_states, d_entropy_bits, d_rice, d_jobs, n,
                      d_inout);
   return launched("k_estbits");
+}
+
+int hvx_coeff_bits_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t *d_off, int n, const int32_t *d_levels,
+                         const int32_t *d_entropy_bits, uint8_t *d_states, hvx_coeff_bits *d_out) {
+  if (!ctx || n < 0 || (n && (!d_desc || !d_off || !d_levels || !d_entropy_bits || !d_states || !d_out)))
+    return fail(HVX_E_INVALID, "hvx_coeff_bits_batch: bad args");
+  if (!n) return HVX_OK;
+  hipLaunchKernelGGL(k_coeff_bits, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, d_desc, d_off, n, d_levels,
+                     d_entropy_bits, d_states, d_out);
+  return launched("k_coeff_bits");
 }
 
 int hvx_me_full_batch(hvx_ctx *ctx, const int16_t *const *d_tgt_planes, int tgt_stride,

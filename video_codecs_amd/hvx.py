@@ -44,7 +44,7 @@ def lib():
             "hvx_ctu_analyze": [P, P, P, I, P, P, P, ctypes.c_size_t, P],
             "hvx_set_timing": [P, I], "hvx_phase_times": [P, ctypes.POINTER(ctypes.c_double), I, I],
             "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
-            "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
+            "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
             "hvx_free": [P, P], "hvx_upload": [P, P, P, ctypes.c_size_t], "hvx_download": [P, P, P, ctypes.c_size_t],
         }.items():
             f = getattr(L, name)
@@ -168,6 +168,12 @@ def estbits_update(states, entropy_bits, rice, w, h, ch, est_in):
 def estbits_batch(states_dev, entropy_dev, rice_dev, jobs_dev, n, inout_dev):
     _check(lib().hvx_estbits_batch(context(), _ptr(states_dev), _ptr(entropy_dev), _ptr(rice_dev), _ptr(jobs_dev), n,
                                    _ptr(inout_dev)), "hvx_estbits_batch")
+
+
+def coeff_bits_batch(desc_dev, off_dev, n, levels, entropy_dev, states_dev, out_dev):
+    """hvx_coeff_bits_batch: TEncSbac::codeCoeffNxN under TEncBinCABACCounter, one TU per lane."""
+    _check(lib().hvx_coeff_bits_batch(context(), _ptr(desc_dev), _ptr(off_dev), n, _ptr(levels), _ptr(entropy_dev),
+                                      _ptr(states_dev), _ptr(out_dev)), "hvx_coeff_bits_batch")
 
 
 def me_full_batch(tgt_planes, tgt_stride, ref_planes, stride, jobs_dev, n, out):
