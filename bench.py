@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
-"""Benchmark: 64x64 CTUs/s of the CTU analysis pass (ME + transform + RDOQ) on 2160p random YUV.
+"""Benchmark: 64x64 CTUs/s of CU mode decision (ME + transform + RDOQ) on 2160p random YUV.
 
-One step = hvx_ctu_analyze over one 3840x2160 picture (2040 CTUs): for each of the 85 CUs
-of every CTU, TZ integer + half/quarter motion search against 4 reference pictures, luma MC
-of the best reference, then transform + RDOQ + dequant + inverse transform + SSE of every
-TU (DESIGN.md "CTU analysis pass").  Inputs are resident in HBM before timing starts.
+One step = one 3840x2160 picture (2040 CTUs): hvx_ctu_analyze (for each of the 85 CUs of every
+CTU: TZ integer + half/quarter motion search against 4 reference pictures, luma MC of the best
+reference, transform + RDOQ + dequant + inverse transform + SSE of every TU), then
+hvx_ctu_decide (CABAC coefficient rate of every TU, the residual and CU-quadtree RD decisions,
+the reconstructed picture with extended borders) -- DESIGN.md sections 3 and 3a.  Inputs are
+resident in HBM before timing starts.
 
-Multi-GPU (torch.distributed.run): one rank per GPU, each rank analyses its own independent
-GOP segment (different synthetic frames) -- no data-path collective; weak scaling.
+Multi-GPU (torch.distributed.run): one rank per GPU, each rank encodes its own independent GOP
+segment (different synthetic frames); the only collective is the per-picture gather of every
+rank's reconstruction to rank 0's DPB (video_codecs_amd/dpb.py, RCCL over xGMI); weak scaling.
 
 Contract: python bench.py --gpus N --steps K --warmup W  -> one JSON line on rank 0.
 """
@@ -105,6 +108,7 @@ def main():
     torch.cuda.set_device(local_rank)
 
     from video_codecs_amd import _abi, hvx
+    from video_codecs_amd.dpb import DpbGather
 
     W, H, nref = args.width, args.height, args.nref
     planes = [luma_plane(W, H, f) for f in segment_frames(rank, nref)]
@@ -113,16 +117,30 @@ def main():
     ref_ptrs = torch.tensor([hvx.plane_origin_ptr(t, W) for t in ref_t], dtype=torch.int64).cuda()
     an = hvx.CtuAnalyzer(W, H, nref, args.qp)
     nctu = an.nctu
+    dpb = DpbGather(world, rank, tuple(cur_t.shape), "cuda")
 
     def before():
         hvx.set_timing(True)
         hvx.phase_times(reset=True)
 
-    elapsed = timed_steps(lambda: an.run(cur_t, ref_ptrs), args.steps, args.warmup, world, "cuda",
-                          torch.cuda.synchronize, before)
+    def step():
+        # one picture: analysis (ME + TU pipeline) -> CU decision + reconstruction -> DPB gather
+        an.encode(cur_t, ref_ptrs, dpb.buffer())  # hvx_ctu_encode = hvx_ctu_analyze + hvx_ctu_decide
+        dpb.send()
+
+    def sync():
+        dpb.drain()
+        torch.cuda.synchronize()
+
+    elapsed = timed_steps(step, args.steps, args.warmup, world, "cuda", sync, before)
     phases = hvx.phase_times(reset=True)
     hvx.set_timing(False)
-    gpu_res = an.results()
+    gpu_res, gpu_dec = an.results(), an.decisions()
+    own, gathered = dpb.last()
+    gpu_rec = own.cpu().numpy()
+    dpb_ok = None
+    if gathered is not None:  # rank 0 holds every rank's picture; its own slot must be its own
+        dpb_ok = bool(torch.equal(gathered[0], own))
 
     if rank == 0:
         value = aggregate(nctu, args.steps, world, elapsed)
@@ -145,7 +163,7 @@ def main():
                 traffic = tr["bytes_per_launch"]
         step_s = elapsed / args.steps
         out = {
-            "metric": "64x64 CTUs/s (ME+transform+RDOQ) on 2160p YUV, 1->8 MI355X; bit-exact vs HM",
+            "metric": "64\u00d764 CTUs/s (ME+transform+RDOQ) on 2160p YUV, 1\u21928 MI355X; bit-exact vs HM",
             "value": round(value, 2),
             "unit": "CTUs/s",
             "n_gpus": world,
@@ -157,9 +175,11 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic: splitmix64 uniform random 8-bit luma (BASELINE.md sec. 3), independent segment per rank",
-            "config": {"workload": "CTU analysis pass: 85 CUs x TZ+frac ME vs %d refs, MC, TU RDOQ/dequant/IT/SSE" % nref,
+            "config": {"workload": "CTU mode decision: 85 CUs x TZ+frac ME vs %d refs, MC, TU RDOQ/dequant/IT, "
+                                   "CABAC coefficient rate, CU quadtree RD decision, reconstruction" % nref,
                        "resolution": f"{W}x{H}", "ctus_per_frame": nctu, "qp": args.qp, "search_range": 64,
-                       "n_ref": nref, "parallelism": f"segments x{world}"},
+                       "n_ref": nref, "parallelism": f"segments x{world}",
+                       "dpb": "gather of every rank's reconstructed picture to rank 0 per step" if world > 1 else "local"},
             "phase_ms_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()},
             "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 3),
                          "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / MI355X_HBM_PEAK_GBS,
@@ -169,26 +189,35 @@ def main():
                          "path_frac": b_ctu * nctu / step_s / 1e9 / MI355X_HBM_PEAK_GBS},
             "cpu_baseline": None,
         }
+        if dpb_ok is not None:
+            out["dpb_gather_ok"] = dpb_ok
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(planes, an, gpu_res, args)
+            out["cpu_baseline"] = cpu_baseline(planes, an, gpu_res, gpu_dec, gpu_rec, args)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(planes, an, gpu_res, args):
-    """The oracle (scalar C port of the same pass, 1 core) on a bounded sample of the same
-    picture's CTUs in raster order; also checks the GPU result of every sampled CTU."""
+def cpu_baseline(planes, an, gpu_res, gpu_dec, gpu_rec, args):
+    """The oracle (scalar C port of the same step, 1 core) on a bounded sample of the same
+    picture's CTUs in raster order; also checks the GPU's CU results, CU decisions and
+    reconstructed samples of every sampled CTU."""
     import oracle
     from video_codecs_amd import _abi
     nref = args.nref
-    est = _abi.load_estbits_p_luma()
+    est, st, eb = _abi.load_estbits_p_luma(), _abi.load_ctx_p_states(), _abi.load_entropy_bits()
     ncx = (args.width + 63) // 64
+    M = _abi.PLANE_MARGIN
+    rec = np.zeros_like(planes[nref])
     n_done, mismatches = 0, 0
     t0 = time.perf_counter()
     for c in range(an.nctu):
-        r = oracle.ctu_analyze(planes[nref], planes[:nref], an.params, est, c % ncx, c // ncx)
-        if r.tobytes() != gpu_res[c].tobytes():
+        cx, cy = c % ncx, c // ncx
+        r, d = oracle.ctu_decide(planes[nref], planes[:nref], an.params, est, st, eb, cx, cy, rec)
+        ys = slice(M + cy * 64, M + min(args.height, cy * 64 + 64))
+        xs = slice(M + cx * 64, M + min(args.width, cx * 64 + 64))
+        if (r.tobytes() != gpu_res[c].tobytes() or d.tobytes() != gpu_dec[c].tobytes()
+                or not np.array_equal(rec[ys, xs], gpu_rec[ys, xs])):
             mismatches += 1
         n_done += 1
         if time.perf_counter() - t0 > args.cpu_seconds:

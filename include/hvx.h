@@ -37,6 +37,11 @@
  *   hvx_ctu_analyze       TEncCu::compressCtu's inter 2Nx2N analysis for every CU of every CTU
  *                         (TEncCu.cpp:228,349,1291 -> predInterSearch/encodeResAndCalcRdInterCU):
  *                         the bench workload, composition of the kernels above
+ *   hvx_ctu_decide        TEncCu::xCompressCU's depth decision (TEncCu.cpp:349-877, xCheckBestMode
+ *                         :1166) over the analysed CUs, then TComYuv::addClip + copyToPic of the
+ *                         chosen leaves (the reconstructed picture) and extendPicBorder
+ *   hvx_ctu_encode        hvx_ctu_analyze + hvx_ctu_decide as one schedule (TEncSlice::compressSlice's
+ *                         compressCtu loop over a picture, TEncSlice.cpp:814)
  *   hvx_plane_from_pel    TComPicYuv int16 padded plane -> device 8-bit padded plane, with
  *                         TComPicYuv::extendPicBorder (TComPicYuv.cpp:197)
  */
@@ -193,7 +198,6 @@ int hvx_download(hvx_ctx *ctx, void *h_dst, const void *d_src, size_t bytes); /*
  * the entries the reference writes for a width x height TU of channel type ch_type are
  * written; the rest of *inout is left as it was (the reference keeps a persistent table).
  * ------------------------------------------------------------------------------------- */
-#define HVX_NUM_CTX 202
 #define HVX_CTX_QT_CBF 28      /* 2 sets x 5 (blockCbpBits) */
 #define HVX_CTX_QT_ROOT_CBF 41 /* estCBFBit reads 4 models from here (the reference's loop bound) */
 #define HVX_CTX_SIG_CG 42      /* [chType][2] */
@@ -239,10 +243,35 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
  * 0 integer ME of the 64x64 depth (k_ctu_me_jobs + k_me_int_ctu), 1..3 integer + fractional
  * ME of the 32/16/8 depths (k_ctu_me_jobs + k_me_ctu), 4 fractional ME of the 64x64 depth
  * (k_me_frac_ctu), 5 MC/residual (k_ctu_pred_resid), 6..8 TU 32x32 (k_tu_fwd, k_tu_rdoq,
- * k_tu_fin), 9..11 TU 16x16, 12..14 TU 8x8, 15 per-CU sums (k_ctu_finalize).  Accumulated ms. */
-#define HVX_NPHASE 16
+ * k_tu_fin), 9..11 TU 16x16, 12..14 TU 8x8, 15 per-CU sums (k_ctu_finalize); hvx_ctu_decide:
+ * 16 coefficient rate (3 x k_coeff_bits), 17 CU tree + reconstruction (k_ctu_decide, k_ctu_recon,
+ * border extension).  Accumulated ms. */
+#define HVX_NPHASE 18
 int hvx_set_timing(hvx_ctx *ctx, int on);
 int hvx_phase_times(hvx_ctx *ctx, double *ms_out, int n, int reset);
+
+/* ---------------------------------------------------------------------------------------
+ * CU decision + reconstruction after hvx_ctu_analyze (same workspace, same stream order):
+ * counts every TU's coefficient rate (codeCoeffNxN under TEncBinCABACCounter, as
+ * hvx_coeff_bits_batch) from one RD-coder context snapshot d_ctx_states (HVX_NUM_CTX bytes,
+ * device) with d_entropy_bits (128 int32, device), then runs TEncCu::xCompressCU's depth
+ * recursion per CTU (hvx_types.h hvx_cu_decision; d_cu = hvx_ctu_analyze's output, d_dec =
+ * nctu*85 records) and writes the luma of the chosen leaves, clip(pred + reconstructed
+ * residual), into d_recon (sample (0,0) of an 8-bit padded plane with the same stride as
+ * d_cur), borders extended as TComPicYuv::extendPicBorder -- the next picture's reference.
+ * Picture width and height must be multiples of 8.
+ * ------------------------------------------------------------------------------------- */
+int hvx_ctu_decide(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const hvx_ctu_params *h_params,
+                   const uint8_t *d_ctx_states, const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes,
+                   const hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon);
+
+/* The whole picture step: hvx_ctu_analyze + hvx_ctu_decide with the same results, scheduled
+ * together (each TU size class's coefficient rate is counted on that class's stream as soon as
+ * its TU pipeline ends, overlapping the remaining motion searches). */
+int hvx_ctu_encode(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
+                   const hvx_ctu_params *h_params, const hvx_estbits *d_est4, const uint8_t *d_ctx_states,
+                   const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes, hvx_cu_result *d_cu,
+                   hvx_cu_decision *d_dec, uint8_t *d_recon);
 
 /* ---------------------------------------------------------------------------------------
  * Picture upload: HM int16 plane (width x height samples, any stride, device copy) ->

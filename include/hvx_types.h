@@ -55,6 +55,9 @@ typedef struct hvx_tu_desc {
   double lambda;              /* TComTrQuant::m_dLambda after selectLambda(compID) */
 } hvx_tu_desc;
 
+/* CABAC context models of HM's TEncSbac (m_contextModels, constructor order TEncSbac.cpp:62-92) */
+#define HVX_NUM_CTX 202
+
 /* TEncSbac::codeCoeffNxN (TEncSbac.cpp:1181) counted by TEncBinCABACCounter
  * (TEncBinCoderCABACCounter.cpp:74-120): the rate of one TU's coefficients as the RD search
  * measures it, from the RD coder's context states (which the count also advances). */
@@ -131,6 +134,28 @@ typedef struct hvx_cu_result {
   int32_t abs_sum;           /* sum of uiAbsSum over the CU's TUs */
   int32_t n_tu;
 } hvx_cu_result;
+
+/* CU decision over the analysed CTU (hvx_ctu_decide; DESIGN.md "CU decision").  Per CU, the residual
+ * decisions of TEncSearch::encodeResAndCalcRdInterCU (TEncSearch.cpp:4341-4421) for its luma TUs:
+ * xEstimateInterResidualQT's forced-zero test per TU (:4647-4768; cbf=0 + zero-residual distortion
+ * against cbf=1 + counted coefficients + coded distortion), the TU tree's rate counted once
+ * (:4973-4984), the qt_root_cbf test (:4361-4366) and the distortion of the clipped
+ * reconstruction (:4408-4417); leaf bits = the ME's ruiBits + that residual rate (fracBits >> 15).
+ * Then TEncCu::xCompressCU's depth recursion (TEncCu.cpp:349-877) with split_cu_flag bits
+ * (TEncSbac.cpp:613; context from the left/above CU depths inside the CTU, TComDataCU.cpp:1487)
+ * added as TEncCu.cpp:681,797 do, costs by TComRdCost::calcRdCost (TComRdCost.cpp:57:
+ * floor(dist + bits*lambda + 0.5)) and a split taken only on a strictly smaller cost
+ * (xCheckBestMode :1166).  All rates from one context snapshot.  One record per CU, same order
+ * as hvx_cu_result. */
+typedef struct hvx_cu_decision {
+  uint64_t coef_frac;        /* sum over the CU's TUs of the counted coefficient rate (15-bit fixed point) */
+  uint32_t bits, dist;       /* the CU coded as a leaf (without its split_cu_flag) */
+  uint32_t best_bits, best_dist; /* the chosen sub-tree rooted at this CU, split flags included */
+  int32_t split;             /* 1: the sub-tree rooted here splits (forced for CUs crossing the picture edge) */
+  int32_t leaf;              /* 1: a leaf of the CTU's final CU tree (its samples are in the reconstruction) */
+  int32_t cbf;               /* bit t: luma TU t of the CU is coded (0: qt_root_cbf 0, prediction only) */
+  int32_t pad_;
+} hvx_cu_decision;
 
 /* One PU's motion compensation (TComPrediction::motionCompensation for one partition, no
  * weighted prediction; TComPrediction.cpp:517-722).  Lists with ref >= 0 are used: both ->

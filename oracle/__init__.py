@@ -205,6 +205,30 @@ def ctu_analyze(cur_plane, ref_planes, params, est4, ctu_x, ctu_y, margin=_abi.P
     return out
 
 
+def ctu_decide(cur_plane, ref_planes, params, est4, states, entropy_bits, ctu_x, ctu_y, recon_plane,
+               margin=_abi.PLANE_MARGIN):
+    """hvxo_ctu_decide for one CTU: -> (85 CU_RESULT, 85 CU_DECISION); the leaves' luma is
+    written into recon_plane (a padded uint8 plane like cur_plane, modified in place)."""
+    L = lib()
+    c = _c(cur_plane, np.uint8)
+    refs = [_c(r, np.uint8) for r in ref_planes]
+    off = margin * c.shape[1] + margin
+    rp = (ctypes.c_void_p * len(refs))(*[r.ctypes.data + off for r in refs])
+    p = np.ascontiguousarray(params, dtype=_abi.CTU_PARAMS).reshape(1)
+    e = _c(est4, np.int32).reshape(-1)
+    st = _c(states, np.uint8)
+    eb = _c(entropy_bits, np.int32)
+    assert recon_plane.dtype == np.uint8 and recon_plane.flags.c_contiguous and recon_plane.shape == c.shape
+    out = np.zeros(_abi.CUS_PER_CTU, _abi.CU_RESULT)
+    dec = np.zeros(_abi.CUS_PER_CTU, _abi.CU_DECISION)
+    L.hvxo_ctu_decide.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    L.hvxo_ctu_decide(ctypes.c_void_p(c.ctypes.data + off), rp, c.shape[1], _p(p), _p(e), _p(st), _p(eb), ctu_x, ctu_y,
+                      _p(out), _p(dec), ctypes.c_void_p(recon_plane.ctypes.data + off), c.shape[1])
+    return out, dec
+
+
 def lambda_2(qp):
     return float(lib().hvxo_lambda_2(int(qp)))
 

@@ -1338,8 +1338,23 @@ void hvxo_ctu_tu_desc(const hvx_ctu_params *p, int cu_size, int log2, hvx_tu_des
   d->lambda = p->lambda;
 }
 
-void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
-                      const hvx_estbits *est, int ctu_x, int ctu_y, hvx_cu_result *out) {
+/* The analysis of one CTU; with ex != NULL it also keeps, per TU of every CU, the counted
+ * coefficient rate, uiAbsSum, the coded (residual-domain) SSE and the zero-residual distortion,
+ * and per CU the ME bits of the chosen reference, the prediction and the reconstructed residual
+ * (64x64 per CU). */
+typedef struct {
+  const uint8_t *states;
+  const int32_t *eb;
+  uint64_t coef_frac[HVX_CUS_PER_CTU][4];
+  int32_t abs_sum[HVX_CUS_PER_CTU][4];
+  uint32_t sse[HVX_CUS_PER_CTU][4], zdist[HVX_CUS_PER_CTU][4];
+  uint32_t me_bits[HVX_CUS_PER_CTU];
+  uint8_t *pred;  /* HVX_CUS_PER_CTU * 4096 */
+  int16_t *rres;  /* HVX_CUS_PER_CTU * 4096 */
+} ctu_extra;
+
+static void ctu_analyze_core(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
+                             const hvx_estbits *est, int ctu_x, int ctu_y, hvx_cu_result *out, ctu_extra *ex) {
   int imv[HVX_CUS_PER_CTU][8][2];
   int base = 0;
   for (int d = 0; d < 4; d++) {
@@ -1371,6 +1386,7 @@ void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride
         imv[ci][ref][1] = mr.mv_int_y;
         if (ref == 0 || mr.cost < best_cost) { best_cost = mr.cost; best = mr; r->ref = ref; }
       }
+      if (ex) ex->me_bits[ci] = best.bits;
       r->mv_x = best.mv_x; r->mv_y = best.mv_y; r->me_cost = best_cost;
       int16_t pred[64 * 64], resi[32 * 32], rec[32 * 32];
       hvxo_luma_block_qpel(refs[r->ref], stride, x, y, best.mv_x, best.mv_y, S, S, pred, 64);
@@ -1387,6 +1403,24 @@ void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride
           hvxo_inv_transform_nxn(&td, lev, rec, T);
           uint32_t sse = 0;
           for (int k = 0; k < T * T; k++) { int df = resi[k] - rec[k]; sse += (uint32_t)(df * df); }
+          if (ex) {
+            const int ti = (ty / T) * (S / T) + tx / T;
+            uint8_t st[HVX_NUM_CTX];
+            hvx_coeff_bits cb;
+            memcpy(st, ex->states, sizeof(st)); /* every TU counts from the same snapshot */
+            hvxo_coeff_bits(&td, lev, st, ex->eb, &cb);
+            uint32_t zd = 0;
+            for (int k = 0; k < T * T; k++) zd += (uint32_t)(resi[k] * resi[k]);
+            ex->coef_frac[ci][ti] = cb.frac_bits;
+            ex->abs_sum[ci][ti] = abs_sum;
+            ex->sse[ci][ti] = sse;
+            ex->zdist[ci][ti] = zd;
+            for (int yy = 0; yy < T; yy++)
+              for (int xx = 0; xx < T; xx++) {
+                ex->pred[ci * 4096 + (ty + yy) * 64 + tx + xx] = (uint8_t)pred[(ty + yy) * 64 + tx + xx];
+                ex->rres[ci * 4096 + (ty + yy) * 64 + tx + xx] = rec[yy * T + xx];
+              }
+          }
           r->sse += sse;
           r->abs_sum += abs_sum;
           r->n_tu++;
@@ -1394,6 +1428,178 @@ void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride
     }
     base += g * g;
   }
+}
+
+void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
+                      const hvx_estbits *est, int ctu_x, int ctu_y, hvx_cu_result *out) {
+  ctu_analyze_core(cur, refs, stride, p, est, ctu_x, ctu_y, out, NULL);
+}
+
+/* ---- CU decision: TEncCu::xCompressCU's depth recursion (TEncCu.cpp:349-877) ---- */
+typedef struct {
+  const hvx_ctu_params *p;
+  const hvx_cu_result *cu;
+  const ctu_extra *ex;
+  hvx_cu_decision *dec;
+  uint8_t depth[8][8]; /* final CU depth per 8x8 of the CTU (TComDataCU::getDepth) */
+  int ctu_x, ctu_y;
+  const uint8_t *cur;  /* sample (0,0) of the original */
+  int stride;
+} decide_ctx;
+
+/* TComRdCost::calcRdCost, DF_DEFAULT lossy (TComRdCost.cpp:57-120) */
+static double rd_cost(uint32_t bits, uint32_t dist, double lambda) {
+  return floor((double)dist + (double)bits * lambda + 0.5);
+}
+
+/* split_cu_flag bits: TEncSbac::codeSplitFlag (TEncSbac.cpp:613) counted alone (resetBits ..
+ * getNumberOfWrittenBits, TEncCu.cpp:681,797), context TComDataCU::getCtxSplitFlag
+ * (TComDataCU.cpp:1487) from the left / above CU depths; neighbours outside the CTU count as
+ * unavailable here (the CTUs are analysed independently) */
+static uint32_t split_flag_bits(const decide_ctx *c, int d, int x8, int y8, int bin) {
+  int ctx = 0;
+  if (x8 > 0 && c->depth[y8][x8 - 1] > d) ctx++;
+  if (y8 > 0 && c->depth[y8 - 1][x8] > d) ctx++;
+  const uint8_t st = c->ex->states[ctx]; /* models 0..2: split flag */
+  return (uint32_t)c->ex->eb[st ^ bin] >> 15;
+}
+
+/* TEncSearch::encodeResAndCalcRdInterCU's residual decisions for the CU's luma TUs (transform depth
+ * 1 in a 64x64 CU, else 0): per TU the forced-zero test of xEstimateInterResidualQT
+ * (TEncSearch.cpp:4647-4768: cbf=0 with the zero-residual distortion against cbf=1 + the counted
+ * coefficients with the coded distortion, each counted alone), the TU tree's rate counted once
+ * (:4973-4984), the qt_root_cbf test (:4361-4366), then the distortion of the clipped
+ * reconstruction (:4408-4417).  Context models: luma qt_cbf 28 + getCtxQtCbf (TComDataCU.cpp:1503,
+ * 1 at transform depth 0), qt_root_cbf 41 (TEncSbac::codeQtRootCbfZero :1097). */
+static void leaf_eval(const decide_ctx *c, int ci, int S, int x, int y, hvx_cu_decision *o) {
+  const ctu_extra *ex = c->ex;
+  const int T = S < 32 ? S : 32, ntu = (S / T) * (S / T);
+  const int m_cbf = 28 + (S > 32 ? 0 : 1);
+  const double lam = c->p->lambda;
+  const uint32_t c0 = (uint32_t)ex->eb[ex->states[m_cbf] ^ 0], c1 = (uint32_t)ex->eb[ex->states[m_cbf] ^ 1];
+  uint64_t tree = 0, cf = 0;
+  uint32_t nz_dist = 0, zero_dist = 0;
+  int cbf = 0;
+  for (int t = 0; t < ntu; t++) {
+    uint64_t tf = c0;
+    uint32_t td = ex->zdist[ci][t];
+    zero_dist += td;
+    cf += ex->coef_frac[ci][t];
+    if (ex->abs_sum[ci][t] > 0) {
+      const uint64_t f1 = c1 + ex->coef_frac[ci][t];
+      if (!(rd_cost(c0 >> 15, td, lam) < rd_cost((uint32_t)(f1 >> 15), ex->sse[ci][t], lam))) {
+        tf = f1;
+        td = ex->sse[ci][t];
+        cbf |= 1 << t;
+      }
+    }
+    tree += tf;
+    nz_dist += td;
+  }
+  const uint32_t r0 = (uint32_t)ex->eb[ex->states[41] ^ 0], r1 = (uint32_t)ex->eb[ex->states[41] ^ 1];
+  if (rd_cost(r0 >> 15, zero_dist, lam) < rd_cost((uint32_t)(tree >> 15), nz_dist, lam)) cbf = 0;
+  uint32_t dist = 0;
+  for (int yy = 0; yy < S; yy++)
+    for (int xx = 0; xx < S; xx++) {
+      const int t = (yy / T) * (S / T) + xx / T, k = ci * 4096 + yy * 64 + xx;
+      const int rec = clip_pel(ex->pred[k] + (((cbf >> t) & 1) ? ex->rres[k] : 0));
+      const int df = (int)c->cur[(y + yy) * c->stride + x + xx] - rec;
+      dist += (uint32_t)(df * df);
+    }
+  o->coef_frac = cf;
+  o->cbf = cbf;
+  o->bits = ex->me_bits[ci] + (uint32_t)((cbf ? r1 + tree : r0) >> 15);
+  o->dist = dist;
+}
+
+/* returns 0 if the CU lies wholly outside the picture; else fills bits and dist of its best tree */
+static int decide_node(decide_ctx *c, int d, int j, uint32_t *bits, uint32_t *dist) {
+  static const int base[4] = {0, 1, 5, 21};
+  const int g = 1 << d, S = 64 >> d, cx = j % g, cy = j / g, ci = base[d] + j;
+  const int x = c->ctu_x * 64 + cx * S, y = c->ctu_y * 64 + cy * S;
+  const int x8 = cx * S / 8, y8 = cy * S / 8, n8 = S / 8;
+  if (x >= c->p->pic_w || y >= c->p->pic_h) return 0;
+  hvx_cu_decision *o = &c->dec[ci];
+  const int valid = c->cu[ci].valid;
+  uint32_t lb = 0, ld = 0;
+  if (valid) {
+    leaf_eval(c, ci, S, x, y, o);
+    lb = o->bits + (d < 3 ? split_flag_bits(c, d, x8, y8, 0) : 0);
+    ld = o->dist;
+  }
+  int split = !valid;
+  uint32_t sb = 0, sd = 0;
+  if (d < 3) {
+    for (int k = 0; k < 4; k++) {
+      uint32_t b, dd;
+      const int cj = (2 * cy + (k >> 1)) * (2 * g) + 2 * cx + (k & 1);
+      if (decide_node(c, d + 1, cj, &b, &dd)) { sb += b; sd += dd; }
+    }
+    if (valid) sb += split_flag_bits(c, d, x8, y8, 1); /* no split flag at a boundary CU */
+    if (valid && rd_cost(sb, sd, c->p->lambda) < rd_cost(lb, ld, c->p->lambda)) split = 1;
+  }
+  o->split = split;
+  o->best_bits = split ? sb : lb;
+  o->best_dist = split ? sd : ld;
+  if (!split) {
+    for (int yy = 0; yy < n8; yy++)
+      for (int xx = 0; xx < n8; xx++) c->depth[y8 + yy][x8 + xx] = (uint8_t)d;
+  }
+  *bits = o->best_bits;
+  *dist = o->best_dist;
+  return 1;
+}
+
+void hvxo_ctu_decide(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
+                     const hvx_estbits *est, const uint8_t *states, const int32_t *eb, int ctu_x, int ctu_y,
+                     hvx_cu_result *out_cu, hvx_cu_decision *out_dec, uint8_t *recon, int recon_stride) {
+  ctu_extra *ex = (ctu_extra *)calloc(1, sizeof(ctu_extra));
+  ex->states = states;
+  ex->eb = eb;
+  ex->pred = (uint8_t *)calloc(HVX_CUS_PER_CTU, 4096);
+  ex->rres = (int16_t *)calloc(HVX_CUS_PER_CTU * 4096, sizeof(int16_t));
+  ctu_analyze_core(cur, refs, stride, p, est, ctu_x, ctu_y, out_cu, ex);
+  decide_ctx c;
+  memset(&c, 0, sizeof(c));
+  c.p = p; c.cu = out_cu; c.ex = ex; c.dec = out_dec; c.ctu_x = ctu_x; c.ctu_y = ctu_y;
+  c.cur = cur; c.stride = stride;
+  memset(out_dec, 0, sizeof(hvx_cu_decision) * HVX_CUS_PER_CTU);
+  uint32_t b, d;
+  decide_node(&c, 0, 0, &b, &d);
+  static const int base[4] = {0, 1, 5, 21};
+  /* the final tree, top-down: a CU is a leaf when it is reached (the root, or a child of a
+   * reached CU that splits), lies in the picture and does not split itself */
+  {
+    int reached[HVX_CUS_PER_CTU];
+    memset(reached, 0, sizeof(reached));
+    reached[0] = 1;
+    for (int dd = 0; dd < 4; dd++) {
+      const int g = 1 << dd, S = 64 >> dd;
+      for (int j = 0; j < g * g; j++) {
+        const int ci = base[dd] + j, x = ctu_x * 64 + (j % g) * S, y = ctu_y * 64 + (j / g) * S;
+        if (!reached[ci] || x >= p->pic_w || y >= p->pic_h) continue;
+        if (!out_dec[ci].split) { out_dec[ci].leaf = 1; continue; }
+        for (int k = 0; k < 4 && dd < 3; k++)
+          reached[base[dd + 1] + (2 * (j / g) + (k >> 1)) * (2 * g) + 2 * (j % g) + (k & 1)] = 1;
+      }
+    }
+  }
+  for (int dd = 0; dd < 4; dd++) {
+    const int g = 1 << dd, S = 64 >> dd;
+    for (int j = 0; j < g * g; j++) {
+      if (!out_dec[base[dd] + j].leaf) continue;
+      const int x = ctu_x * 64 + (j % g) * S, y = ctu_y * 64 + (j / g) * S;
+      const int ci = base[dd] + j, T = S < 32 ? S : 32, cbf = out_dec[ci].cbf;
+      for (int yy = 0; yy < S; yy++)
+        for (int xx = 0; xx < S; xx++) {
+          const int t = (yy / T) * (S / T) + xx / T, k = ci * 4096 + yy * 64 + xx;
+          recon[(y + yy) * recon_stride + x + xx] = (uint8_t)clip_pel(ex->pred[k] + (((cbf >> t) & 1) ? ex->rres[k] : 0));
+        }
+    }
+  }
+  free(ex->pred);
+  free(ex->rres);
+  free(ex);
 }
 
 

@@ -80,6 +80,11 @@ void hvxo_coeff_bits(const hvx_tu_desc *tu, const int32_t *coef, uint8_t *states
 
 /* ---- CTU analysis pass (the bench workload, hvx_types.h) ---- */
 void hvxo_ctu_tu_desc(const hvx_ctu_params *p, int cu_size, int log2, hvx_tu_desc *d);
+/* analysis + CU decision + reconstruction of one CTU (hvx_ctu_decide semantics): out_cu[85],
+ * out_dec[85]; the leaf CUs' luma is written into recon (sample (0,0) of a picture plane) */
+void hvxo_ctu_decide(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
+                     const hvx_estbits *est, const uint8_t *states, const int32_t *eb, int ctu_x, int ctu_y,
+                     hvx_cu_result *out_cu, hvx_cu_decision *out_dec, uint8_t *recon, int recon_stride);
 void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
                       const hvx_estbits *est /* [4]: luma 4x4..32x32 */, int ctu_x, int ctu_y,
                       hvx_cu_result *out /* [HVX_CUS_PER_CTU] */);

@@ -227,6 +227,41 @@ def check_ctu_pass(seed, width, height, nref, qp, max_ctus=None):
     return n
 
 
+def check_ctu_decide(seed, width, height, nref, qp, fused=False):
+    """hvx_ctu_analyze + hvx_ctu_decide over a whole picture vs hvxo_ctu_decide per CTU: CU
+    results, decision records and the reconstructed picture incl. its extended border (bit-exact)."""
+    torch = _torch()
+    cur = padded_plane(make_yuv.random_frame(width, height, seed)[:width * height].reshape(height, width))
+    refs = [padded_plane((make_yuv.smooth_frame if k % 2 else make_yuv.random_frame)(width, height, seed + 10 + k)
+                         [:width * height].reshape(height, width)) for k in range(nref)]
+    an = hvx.CtuAnalyzer(width, height, nref, qp)
+    cur_t = torch.from_numpy(cur).cuda()
+    ref_t = [torch.from_numpy(r).cuda() for r in refs]
+    ptrs = torch.tensor([hvx.plane_origin_ptr(t, width) for t in ref_t], dtype=torch.int64).cuda()
+    recon_t = torch.zeros_like(cur_t)
+    if fused:
+        an.encode(cur_t, ptrs, recon_t)
+    else:
+        an.run(cur_t, ptrs)
+        an.decide(cur_t, recon_t)
+    torch.cuda.synchronize()
+    got_cu, got_dec, got_rec = an.results(), an.decisions(), recon_t.cpu().numpy()
+    est, st, eb = _abi.load_estbits_p_luma(), _abi.load_ctx_p_states(), _abi.load_entropy_bits()
+    ncx = (width + 63) // 64
+    exp_rec = np.zeros_like(cur)
+    n_leaf = 0
+    for c in range(an.nctu):
+        cu, dec = oracle.ctu_decide(cur, refs, an.params, est, st, eb, c % ncx, c // ncx, exp_rec)
+        assert got_cu[c].tobytes() == cu.tobytes(), c
+        for ci in range(_abi.CUS_PER_CTU):
+            assert got_dec[c][ci].tobytes() == dec[ci].tobytes(), (c, ci, got_dec[c][ci], dec[ci])
+        n_leaf += int(dec["leaf"].sum())
+    M = _abi.PLANE_MARGIN
+    exp_rec = np.pad(exp_rec[M:M + height, M:M + width], M, mode="edge")  # extendPicBorder
+    np.testing.assert_array_equal(got_rec, exp_rec)
+    return an.nctu, n_leaf
+
+
 # ------------------------------------------------------------------------------------------- MC
 def mc_planes(rng, W, H, n_ref):
     """HM-like int16 4:2:0 reference planes (margins 80 luma / 40 chroma, borders replicated),

@@ -81,3 +81,57 @@ def test_segment_and_aggregate_contract():
     assert len(flat) == len(set(flat)) == 40  # 8 closed, disjoint segments of nref+1 frames
     assert bench.aggregate(2040, 10, 8, 2.0) == 2040 * 10 * 8 / 2.0
     assert bench.b_ctu_luma(4) == 4096 * 6 + 2 * 4096 + 16 * 256
+
+
+def _decide_picture(planes, rec):
+    """The oracle's full step (analysis + CU decision + reconstruction) into rec (padded plane)."""
+    import oracle
+    from video_codecs_amd import _abi
+    params = _abi.ctu_params(W, H, NREF, QP)
+    est, st, eb = _abi.load_estbits_p_luma(), _abi.load_ctx_p_states(), _abi.load_entropy_bits()
+    ncx, ncy = (W + 63) // 64, (H + 63) // 64
+    for c in range(ncx * ncy):
+        oracle.ctu_decide(planes[NREF], planes[:NREF], params, est, st, eb, c % ncx, c // ncx, rec)
+
+
+def _dpb_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from video_codecs_amd.dpb import DpbGather
+    planes = [bench.luma_plane(W, H, f) for f in bench.segment_frames(rank, NREF)]
+    g = DpbGather(world, rank, planes[0].shape, "cpu")
+
+    def step():  # the bench step's shape: decide into the DPB buffer, then the async gather
+        _decide_picture(planes, g.buffer().numpy())
+        g.send()
+
+    elapsed = bench.timed_steps(step, STEPS, WARMUP, world, "cpu", g.drain)
+    own, gathered = g.last()
+    np.save(os.path.join(outdir, f"own{rank}.npy"), own.numpy())
+    if rank == 0:
+        np.save(os.path.join(outdir, "dpb.npy"), np.stack([t.numpy() for t in gathered]))
+    np.save(os.path.join(outdir, f"t{rank}.npy"), np.array([elapsed, g.k]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_dpb_gather_gloo(tmp_path):
+    # the per-picture DPB gather (SURVEY 8(e)): after STEPS + WARMUP pictures through two
+    # alternating buffers, rank 0 holds each rank's latest reconstruction, and that
+    # reconstruction is exactly the single-process one of the rank's own segment
+    import torch.multiprocessing as tmp
+    world = 2
+    tmp.spawn(_dpb_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    dpb = np.load(tmp_path / "dpb.npy")
+    assert dpb.shape[0] == world
+    import bench
+    for r in range(world):
+        own = np.load(tmp_path / f"own{r}.npy")
+        np.testing.assert_array_equal(dpb[r], own)
+        exp = np.zeros_like(own)
+        _decide_picture([bench.luma_plane(W, H, f) for f in bench.segment_frames(r, NREF)], exp)
+        np.testing.assert_array_equal(own, exp)
+        assert int(np.load(tmp_path / f"t{r}.npy")[1]) == STEPS + WARMUP
+    assert not np.array_equal(dpb[0], dpb[1])

@@ -145,6 +145,25 @@ def test_ctu_pass_gpu(torch):
     assert gpu_cases.check_ctu_pass(seed=21, width=320, height=200, nref=2, qp=32) == 20
 
 
+def test_ctu_decide_gpu(torch):
+    # analysis + coefficient rate + CU tree + reconstruction; 200x136 has partial CTUs on both
+    # edges (forced splits, CUs outside the picture)
+    n, leaves = gpu_cases.check_ctu_decide(seed=5, width=200, height=136, nref=2, qp=32)
+    assert n == 12 and leaves > 12
+
+
+def test_ctu_encode_fused_gpu(torch):
+    # hvx_ctu_encode (the bench step's schedule) gives hvx_ctu_analyze + hvx_ctu_decide's results
+    n, leaves = gpu_cases.check_ctu_decide(seed=9, width=264, height=200, nref=3, qp=27, fused=True)
+    assert n == 20 and leaves > 20
+
+
+def test_ctu_decide_qp_sweep_gpu(torch):
+    for qp in (22, 37):
+        n, leaves = gpu_cases.check_ctu_decide(seed=qp, width=128, height=128, nref=1, qp=qp)
+        assert n == 4 and leaves >= 4
+
+
 def test_ctu_pass_qp_sweep_gpu(torch):
     for qp in (22, 27, 37):
         assert gpu_cases.check_ctu_pass(seed=qp, width=192, height=128, nref=1, qp=qp) == 6

@@ -76,3 +76,23 @@ MC_JOB = np.dtype([("pic_w", "<i4"), ("pic_h", "<i4"), ("max_cu", "<i4"), ("cu_x
 COEFF_BITS = np.dtype([("frac_bits", "<u8"), ("rice_stat", "<u4"), ("num_sig", "<u4")])
 assert COEFF_BITS.itemsize == 16
 NUM_CTX = 202
+
+# hvx_cu_decision (hvx_types.h)
+CU_DECISION = np.dtype([("coef_frac", "<u8"), ("bits", "<u4"), ("dist", "<u4"), ("best_bits", "<u4"),
+                        ("best_dist", "<u4"), ("split", "<i4"), ("leaf", "<i4"), ("cbf", "<i4"), ("pad_", "<i4")])
+assert CU_DECISION.itemsize == 40
+
+
+def load_ctx_p_states():
+    """202 CABAC context states (TEncSbac::m_contextModels order) of HM's RD coder in a P-slice
+    (video_codecs_amd/data/README.md)."""
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "ctx_p_states.bin")
+    return np.fromfile(p, dtype=np.uint8)
+
+
+def load_entropy_bits():
+    """ContextModel::m_entropyBits, 128 int32 (video_codecs_amd/data/README.md)."""
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "entropy_bits.bin")
+    return np.fromfile(p, dtype="<i4")

@@ -104,21 +104,26 @@ __device__ __forceinline__ int sig_ctx(int pattern, int first_sig, int single, i
 
 // codeCoeffNxN for one square TU.  lev(sp) returns the level at GROUPED SCAN position sp
 // (scan = kScan[scan_type] at the TU's size).  Returns num_sig; frac accumulates in L.
+// Coefficient groups are the unit of work: each group's 16 levels are fetched by 16
+// independent loads into registers (fully unrolled, static indices), so a group costs one
+// memory latency, and every later pass over the group reads registers.
 template <class LevAt>
 __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &rice_stat) {
-  const int n = d.width, lw = log2_tu(n), l = lw - 2, wg = n >> 2, nn = n * n;
+  const int n = d.width, lw = log2_tu(n), l = lw - 2, wg = n >> 2, ncg = wg * wg;
   const int ch = d.comp ? 1 : 0;
-  const uint16_t *scan = kScan[d.scan_type] + scan_base(l);
   const uint8_t *scan_cg = kScanCG[d.scan_type] + cg_base(l);
-  // significant-CG map (raster CG index) and the last significant scan position
+  const uint16_t *scan = kScan[d.scan_type] + scan_base(l);
+  // significant-CG map (raster CG index), the last significant scan position, the count
   uint64_t cgm = 0;
   int num_sig = 0, scan_last = -1;
-  for (int sp = 0; sp < nn; sp++) {
-    if (lev(sp) != 0) {
-      const int r = scan[sp], py = r >> lw, px = r - (py << lw);
-      cgm |= 1ull << (wg * (py >> 2) + (px >> 2));
-      num_sig++;
-      scan_last = sp;
+  for (int sub = 0; sub < ncg; sub++) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) m |= (uint32_t)(lev(sub * 16 + k) != 0) << k;
+    if (m) {
+      cgm |= 1ull << scan_cg[sub];
+      num_sig += __popc(m);
+      scan_last = sub * 16 + 31 - __clz(m);
     }
   }
   if (num_sig == 0) return 0;  // the reference exits here (empty TU); nothing is coded
@@ -149,21 +154,23 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
     if (gy > 3) L.ep((gy - 2) >> 1);
   }
   const int base_cg = kSigCG + ch * 2, base_sig = kSig + (ch ? 28 : 0);
-  const int last_set = scan_last >> 4;
+  const int last_set = scan_last >> 4, last_pin = scan_last & 15;
   int c1 = 1;
   for (int sub = last_set; sub >= 0; sub--) {
     const int sub_pos = sub << 4;
     const int cg = scan_cg[sub], cgy = cg / wg, cgx = cg - cgy * wg;
+    int a[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) a[k] = lev(sub_pos + k);
     if (sub == last_set || sub == 0) cgm |= 1ull << cg;
     else {
       const int rr = cgx < wg - 1 ? (int)((cgm >> (cg + 1)) & 1) : 0;
       const int bb = cgy < wg - 1 ? (int)((cgm >> (cg + wg)) & 1) : 0;
       L.bin(base_cg + ((rr + bb) != 0), (int)((cgm >> cg) & 1));
     }
-    // significance flags; nnz / first / last non-zero positions of the group
-    int nnz = 0, last_nz = -1, first_nz = 16;
-    const int top = sub == last_set ? scan_last : sub_pos + 15;
-    if (sub == last_set) { nnz = 1; last_nz = first_nz = scan_last; }
+    // significance flags (reverse scan inside the group); non-zero count, first/last positions
+    const bool is_last_set = sub == last_set;
+    int nnz = is_last_set ? 1 : 0, last_nz = is_last_set ? last_pin : -1, first_nz = is_last_set ? last_pin : 16;
     if ((cgm >> cg) & 1) {
       int pattern = 0;
       if (wg > 1) {
@@ -171,13 +178,15 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
         const int bb = cgy < wg - 1 ? (int)((cgm >> (cg + wg)) & 1) : 0;
         pattern = rr + (bb << 1);
       }
-      for (int sp = (sub == last_set ? scan_last - 1 : top); sp >= sub_pos; sp--) {
-        const int sig = lev(sp) != 0;
-        if (sp > sub_pos || sub == 0 || nnz) L.bin(base_sig + sig_ctx(pattern, first_sig, single, scan[sp], lw, ch), sig);
+#pragma unroll
+      for (int pin = 15; pin >= 0; pin--) {
+        if (is_last_set && pin >= last_pin) continue;
+        const int sig = a[pin] != 0;
+        if (pin > 0 || sub == 0 || nnz) L.bin(base_sig + sig_ctx(pattern, first_sig, single, scan[sub_pos + pin], lw, ch), sig);
         if (sig) {
           nnz++;
-          if (last_nz == -1) last_nz = sp;
-          first_nz = sp;
+          if (last_nz == -1) last_nz = pin;
+          first_nz = pin;
         }
       }
     }
@@ -190,14 +199,15 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
     bool escape = nnz > 8;
     int idx = 0, first_c2_abs = 0;
     bool have_c2 = false;
-    for (int sp = top; sp >= sub_pos && idx < 8; sp--) {
-      const int a = abs(lev(sp));
-      if (!a) continue;
-      const int gt1 = a > 1;
+#pragma unroll
+    for (int pin = 15; pin >= 0; pin--) {
+      const int av = abs(a[pin]);
+      if (!av || idx >= 8) continue;
+      const int gt1 = av > 1;
       L.bin(base_one + c1, gt1);
       if (gt1) {
         c1 = 0;
-        if (!have_c2) { have_c2 = true; first_c2_abs = a; }
+        if (!have_c2) { have_c2 = true; first_c2_abs = av; }
         else escape = true;
       } else if (c1 < 3 && c1 > 0) {
         c1++;
@@ -215,14 +225,15 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
       bool upd = d.persistent_rice != 0;
       int first2 = 1;
       idx = 0;
-      for (int sp = top; sp >= sub_pos; sp--) {
-        const int a = abs(lev(sp));
-        if (!a) continue;
+#pragma unroll
+      for (int pin = 15; pin >= 0; pin--) {
+        const int av = abs(a[pin]);
+        if (!av) continue;
         const int base = idx < 8 ? 2 + first2 : 1;
-        if (a >= base) {
-          const uint32_t esc = (uint32_t)(a - base);
+        if (av >= base) {
+          const uint32_t esc = (uint32_t)(av - base);
           L.ep(remain_bins(esc, rice, d.extended_precision != 0, d.max_log2_tr_range));
-          if (a > (3 << rice)) rice = d.persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
+          if (av > (3 << rice)) rice = d.persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
           if (upd) {
             const uint32_t init = rice_stat / 4;
             if (esc >= (3u << init)) rice_stat++;
@@ -230,7 +241,7 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
             upd = false;
           }
         }
-        if (a >= 2) first2 = 0;
+        if (av >= 2) first2 = 0;
         idx++;
       }
     }
@@ -238,13 +249,14 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
   return num_sig;
 }
 
-// copy the lanes' states between global (HVX_NUM_CTX bytes per TU) and the LDS columns,
-// coalesced across the wave; tu0 = first TU of the wave, cnt = TUs in the wave
-__device__ __forceinline__ void states_load(Shared &s, const uint8_t *g, int tu0, int cnt) {
+// copy the lanes' states between global (`stride` bytes per TU; stride 0 = one snapshot shared
+// by every TU) and the LDS columns, coalesced across the wave; tu0 = first TU of the wave,
+// cnt = TUs in the wave
+__device__ __forceinline__ void states_load(Shared &s, const uint8_t *g, size_t stride, int tu0, int cnt) {
   const int lane = threadIdx.x & 63;
   for (int i = lane; i < cnt * kRows; i += 64) {
     const int t = i / kRows, r = i - t * kRows;
-    s.st[r * 64 + t] = g[(size_t)(tu0 + t) * HVX_NUM_CTX + kCtxLo + r];
+    s.st[r * 64 + t] = g[(size_t)(tu0 + t) * stride + kCtxLo + r];
   }
 }
 __device__ __forceinline__ void states_store(const Shared &s, uint8_t *g, int tu0, int cnt) {
@@ -256,15 +268,17 @@ __device__ __forceinline__ void states_store(const Shared &s, uint8_t *g, int tu
 }
 }  // namespace cab
 
-// hvx_coeff_bits_batch: TU i = lane (i % 64) of block i / 64; raster int32 levels at d_off[i]
+// hvx_coeff_bits_batch: TU i = lane (i % 64) of block i / 64; raster int32 levels at d_off[i].
+// states_stride HVX_NUM_CTX: per-TU states, advanced in place; 0: one shared snapshot (read only:
+// the CTU decision counts every TU from the same state)
 __global__ __launch_bounds__(64) void k_coeff_bits(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
                                                    int n, const int32_t *__restrict__ levels,
                                                    const int32_t *__restrict__ entropy_bits, uint8_t *__restrict__ states,
-                                                   hvx_coeff_bits *__restrict__ out) {
+                                                   int states_stride, hvx_coeff_bits *__restrict__ out) {
   __shared__ cab::Shared s;
   const int lane = threadIdx.x, tu0 = blockIdx.x * 64, cnt = min(64, n - tu0), t = tu0 + lane;
   cab::init_tables(s, entropy_bits);
-  cab::states_load(s, states, tu0, cnt);
+  cab::states_load(s, states, (size_t)states_stride, tu0, cnt);
   __syncthreads();
   if (lane < cnt) {
     const hvx_tu_desc d = descs[t];
@@ -282,6 +296,39 @@ __global__ __launch_bounds__(64) void k_coeff_bits(const hvx_tu_desc *__restrict
     }
     out[t] = r;
   }
+  if (states_stride) {
+    __syncthreads();
+    cab::states_store(s, states, tu0, cnt);
+  }
+}
+
+// The CTU decision's variant (hvx_ctu_decide): one size class of the CTU pass, levels read from
+// the RDOQ's interleaved scan-order array (G = 64 TUs per group: lane l of block b counts TU
+// b*64 + l, whose element sp sits at ((b*NN + sp)*64 + l) -- the 64 lanes of every level load
+// touch 64 consecutive words), every TU from the same snapshot.
+template <int L>
+__global__ __launch_bounds__(64) void k_coeff_bits_il(const hvx_tu_desc *__restrict__ descs, int n,
+                                                      const int32_t *__restrict__ levI,
+                                                      const int32_t *__restrict__ entropy_bits,
+                                                      const uint8_t *__restrict__ snapshot,
+                                                      hvx_coeff_bits *__restrict__ out) {
+  constexpr int N = 4 << L, NN = N * N;
+  __shared__ cab::Shared s;
+  const int lane = threadIdx.x, tu0 = blockIdx.x * 64, cnt = min(64, n - tu0), t = tu0 + lane;
+  cab::init_tables(s, entropy_bits);
+  cab::states_load(s, snapshot, 0, tu0, cnt);
   __syncthreads();
-  cab::states_store(s, states, tu0, cnt);
+  if (lane >= cnt) return;
+  const hvx_tu_desc d = descs[t];
+  hvx_coeff_bits r{0, (uint32_t)d.golomb_rice_stat, 0xffffffffu};
+  if (d.width == N && d.height == N && (unsigned)d.scan_type <= 2u) {
+    const int32_t *lv = levI + tu_il(t, 0, NN, 64);
+    cab::Lane Lc{&s.st[lane], &s, 0};
+    uint32_t rice = (uint32_t)d.golomb_rice_stat;
+    const int ns = cab::coeff_bits(d, [&](int sp) { return lv[(size_t)sp * 64]; }, Lc, rice);
+    r.frac_bits = Lc.frac;
+    r.rice_stat = rice;
+    r.num_sig = (uint32_t)ns;
+  }
+  out[t] = r;
 }

@@ -156,3 +156,210 @@ __global__ __launch_bounds__(256) void k_ctu_finalize(CtuLayout L, const int32_t
   o.abs_sum = a;
   out[cuid] = o;
 }
+
+// ------------------------------------------------------------------------------------------
+// CU decision (hvx_ctu_decide; restated by hvxo_ctu_decide).  TEncCu::xCompressCU's depth
+// recursion (TEncCu.cpp:349-877): a CU's leaf cost (ME ruiBits + counted coefficient rate +
+// split_cu_flag=0, TEncCu.cpp:681) against its four children's best trees + split_cu_flag=1
+// (:797), costs by calcRdCost (TComRdCost.cpp:57), the split taken only on a strictly smaller
+// cost (xCheckBestMode :1166).  One THREAD per CTU walks the 85-node tree in z-order (the
+// recursion is compile-time unrolled), so each split flag's context sees the final depths of
+// its left/above neighbours inside the CTU exactly as getCtxSplitFlag (TComDataCU.cpp:1487) does;
+// the CTU's final depth map lives in two 64-bit planes (2 bits per 8x8).
+struct DecideArgs {
+  CtuLayout L;
+  int pic_w, pic_h;
+  double lambda;
+  const hvx_cu_result *cu;
+  const hvx_me_result *res;
+  const hvx_coeff_bits *cb;
+  const uint8_t *st;          // the context snapshot (split flag 0..2, luma qt_cbf 28.., qt_root_cbf 41)
+  const int32_t *eb;
+  hvx_cu_decision *dec;
+};
+
+__device__ __forceinline__ double dec_rd_cost(uint32_t bits, uint32_t dist, double lambda) {
+  return floor((double)dist + (double)bits * lambda + 0.5);
+}
+
+struct DepthMap {
+  uint64_t lo = 0, hi = 0;
+  __device__ __forceinline__ int at(int x8, int y8) const {
+    const int i = y8 * 8 + x8;
+    return (int)((lo >> i) & 1) | ((int)((hi >> i) & 1) << 1);
+  }
+  __device__ __forceinline__ void fill(int x8, int y8, int n8, int d) {
+    uint64_t m = 0;
+    const uint64_t row = (n8 == 8) ? 0xffull : ((1ull << n8) - 1);
+    for (int y = 0; y < n8; y++) m |= row << ((y8 + y) * 8 + x8);
+    lo = (d & 1) ? (lo | m) : (lo & ~m);
+    hi = (d & 2) ? (hi | m) : (hi & ~m);
+  }
+};
+
+template <int D>
+__device__ bool dec_node(const DecideArgs &A, int ctu, int cx, int cy, DepthMap &dm, uint32_t &bits, uint32_t &dist) {
+  constexpr int g = 1 << D, S = 64 >> D, n8 = S / 8;
+  const int j = cy * g + cx, ci = (D == 0 ? 0 : D == 1 ? 1 : D == 2 ? 5 : 21) + j;
+  const int x = (ctu % A.L.nctu_x) * 64 + cx * S, y = (ctu / A.L.nctu_x) * 64 + cy * S;
+  if (x >= A.pic_w || y >= A.pic_h) return false;
+  const int x8 = cx * n8, y8 = cy * n8;
+  const size_t cuid = (size_t)ctu * HVX_CUS_PER_CTU + ci;
+  const hvx_cu_result cu = A.cu[cuid];
+  hvx_cu_decision o;
+  o.coef_frac = 0; o.bits = 0; o.dist = 0; o.leaf = 0; o.cbf = 0; o.pad_ = 0;
+  const int ctx = (x8 > 0 && dm.at(x8 - 1, y8) > D) + (y8 > 0 && dm.at(x8, y8 - 1) > D);
+  const int sfs = D < 3 ? A.st[ctx] : 0;
+  uint32_t lb = 0, ld = 0;
+  if (cu.valid) {
+    const hvx_cu_decision lf = A.dec[cuid];  // the leaf evaluation (k_ctu_leaf)
+    o.coef_frac = lf.coef_frac; o.bits = lf.bits; o.dist = lf.dist; o.cbf = lf.cbf;
+    lb = o.bits + (D < 3 ? ((uint32_t)A.eb[sfs ^ 0] >> 15) : 0u);
+    ld = o.dist;
+  }
+  bool split = !cu.valid;
+  uint32_t sb = 0, sd = 0;
+  if constexpr (D < 3) {
+    for (int k = 0; k < 4; k++) {
+      uint32_t b, dd;
+      if (dec_node<D + 1>(A, ctu, 2 * cx + (k & 1), 2 * cy + (k >> 1), dm, b, dd)) { sb += b; sd += dd; }
+    }
+    if (cu.valid) {
+      sb += (uint32_t)A.eb[sfs ^ 1] >> 15;
+      if (dec_rd_cost(sb, sd, A.lambda) < dec_rd_cost(lb, ld, A.lambda)) split = true;
+    }
+  }
+  o.split = split;
+  o.best_bits = split ? sb : lb;
+  o.best_dist = split ? sd : ld;
+  if (!split) dm.fill(x8, y8, n8, D);
+  A.dec[cuid] = o;
+  bits = o.best_bits;
+  dist = o.best_dist;
+  return true;
+}
+
+// Leaf evaluation of every CU (hvxo_ctu_decide's leaf_eval: encodeResAndCalcRdInterCU's residual
+// decisions, TEncSearch.cpp:4341-4421): one wave per CU.  The TU / root-cbf decisions are
+// wave-uniform scalar code on the TU records; the zero-residual and the final clipped
+// distortions are wave sums over the CU's samples.  Writes coef_frac, bits, dist and cbf.
+__global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const uint8_t *__restrict__ cur, int stride,
+                                                 const int16_t *__restrict__ resid, const int16_t *__restrict__ res_out,
+                                                 const int32_t *__restrict__ abs_sum, const uint32_t *__restrict__ sse) {
+  const int cuid = blockIdx.x, ctu = cuid / HVX_CUS_PER_CTU, ci = cuid % HVX_CUS_PER_CTU;
+  const hvx_cu_result cu = A.cu[cuid];
+  if (!cu.valid) return;
+  int d, j, S, g;
+  cu_geom(ci, d, j, S, g);
+  const int x = (ctu % A.L.nctu_x) * 64 + (j % g) * S, y = (ctu / A.L.nctu_x) * 64 + (j / g) * S;
+  const int T = S < 32 ? S : 32, ntu = (S / T) * (S / T), lane = lane_id();
+  const int m_cbf = 28 + (S > 32 ? 0 : 1);
+  const double lam = A.lambda;
+  const uint32_t c0 = (uint32_t)A.eb[A.st[m_cbf] ^ 0], c1 = (uint32_t)A.eb[A.st[m_cbf] ^ 1];
+  uint64_t tree = 0, cf = 0;
+  uint32_t nz_dist = 0, zero_dist = 0;
+  int cbf = 0;
+  for (int t = 0; t < ntu; t++) {
+    const int tu = ctu_tu_index(A.L, ctu, d, j, t);
+    const int64_t o = ctu_tu_offset(A.L, tu);
+    uint32_t part = 0;
+    for (int k = lane; k < T * T; k += HVX_WAVE) {
+      const int r = resid[o + k];
+      part += (uint32_t)(r * r);
+    }
+    uint32_t td = wave_sum_u32(part);
+    const uint64_t fr = A.cb[tu].frac_bits;
+    uint64_t tf = c0;
+    zero_dist += td;
+    cf += fr;
+    if (abs_sum[tu] > 0) {
+      const uint64_t f1 = c1 + fr;
+      if (!(dec_rd_cost(c0 >> 15, td, lam) < dec_rd_cost((uint32_t)(f1 >> 15), sse[tu], lam))) {
+        tf = f1;
+        td = sse[tu];
+        cbf |= 1 << t;
+      }
+    }
+    tree += tf;
+    nz_dist += td;
+  }
+  const uint32_t r0 = (uint32_t)A.eb[A.st[41] ^ 0], r1 = (uint32_t)A.eb[A.st[41] ^ 1];
+  if (dec_rd_cost(r0 >> 15, zero_dist, lam) < dec_rd_cost((uint32_t)(tree >> 15), nz_dist, lam)) cbf = 0;
+  uint32_t part = 0;
+  for (int k = lane; k < S * S; k += HVX_WAVE) {
+    const int yy = k / S, xx = k % S, t = (yy / T) * (S / T) + xx / T;
+    const int64_t o = ctu_tu_offset(A.L, ctu_tu_index(A.L, ctu, d, j, t)) + (yy % T) * T + (xx % T);
+    const int org = cur[(y + yy) * stride + x + xx];
+    int v = org - resid[o] + (((cbf >> t) & 1) ? res_out[o] : 0);
+    v = v < 0 ? 0 : v > 255 ? 255 : v;
+    part += (uint32_t)((org - v) * (org - v));
+  }
+  const uint32_t dist = wave_sum_u32(part);
+  if (lane == 0) {
+    hvx_cu_decision &r = A.dec[cuid];
+    r.coef_frac = cf;
+    r.cbf = cbf;
+    r.dist = dist;
+    r.bits = A.res[(size_t)cuid * A.L.nref + cu.ref].bits + (uint32_t)((cbf ? r1 + tree : r0) >> 15);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_ctu_decide(DecideArgs A) {
+  const int ctu = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ctu >= A.L.nctu) return;
+  // CUs wholly outside the picture keep a zero record
+  for (int ci = 0; ci < HVX_CUS_PER_CTU; ci++) {
+    int d, j, S, g;
+    cu_geom(ci, d, j, S, g);
+    const int x = (ctu % A.L.nctu_x) * 64 + (j % g) * S, y = (ctu / A.L.nctu_x) * 64 + (j / g) * S;
+    if (x >= A.pic_w || y >= A.pic_h) A.dec[(size_t)ctu * HVX_CUS_PER_CTU + ci] = hvx_cu_decision{0, 0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  DepthMap dm;
+  uint32_t b, d;
+  dec_node<0>(A, ctu, 0, 0, dm, b, d);
+  // the final tree, top-down: leaf = reached (root, or child of a reached splitting CU), in the
+  // picture, not splitting; reached set as an 85-bit mask
+  uint64_t r_lo = 1, r_hi = 0;
+  for (int ci = 0; ci < HVX_CUS_PER_CTU; ci++) {
+    const bool reached = ci < 64 ? ((r_lo >> ci) & 1) : ((r_hi >> (ci - 64)) & 1);
+    int dd, j, S, g;
+    cu_geom(ci, dd, j, S, g);
+    const int x = (ctu % A.L.nctu_x) * 64 + (j % g) * S, y = (ctu / A.L.nctu_x) * 64 + (j / g) * S;
+    if (!reached || x >= A.pic_w || y >= A.pic_h) continue;
+    hvx_cu_decision &o = A.dec[(size_t)ctu * HVX_CUS_PER_CTU + ci];
+    if (!o.split) { o.leaf = 1; continue; }
+    if (dd == 3) continue;
+    for (int k = 0; k < 4; k++) {
+      const int c = depth_base(dd + 1) + (2 * (j / g) + (k >> 1)) * (2 * g) + 2 * (j % g) + (k & 1);
+      if (c < 64) r_lo |= 1ull << c; else r_hi |= 1ull << (c - 64);
+    }
+  }
+}
+
+// reconstruction of the leaves: recon = clip(org - residual + coded reconstructed residual)
+// (= pred + the residual the leaf keeps, TComYuv::addClip) into the 8-bit picture plane; one
+// 256-thread block per CTU, each thread 16 samples of a 64x64 CTU
+__global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int pic_h, const uint8_t *__restrict__ cur,
+                                                   int stride, const hvx_cu_decision *__restrict__ dec,
+                                                   const int16_t *__restrict__ resid, const int16_t *__restrict__ res_out,
+                                                   uint8_t *__restrict__ recon) {
+  const int ctu = blockIdx.x;
+  const int x0 = (ctu % L.nctu_x) * 64, y0 = (ctu / L.nctu_x) * 64;
+  const hvx_cu_decision *dc = dec + (size_t)ctu * HVX_CUS_PER_CTU;
+  for (int k = threadIdx.x; k < 64 * 64; k += 256) {
+    const int yy = k >> 6, xx = k & 63, x = x0 + xx, y = y0 + yy;
+    if (x >= pic_w || y >= pic_h) continue;
+    int d = 0, j = 0;
+    for (d = 0; d < 4; d++) {
+      const int S = 64 >> d, g = 1 << d;
+      j = (yy / S) * g + (xx / S);
+      if (dc[depth_base(d) + j].leaf) break;
+    }
+    if (d == 4) continue;  // not reached for a decided CTU
+    const int S = 64 >> d, T = S < 32 ? S : 32, cx = xx % S, cy = yy % S, t = (cy / T) * (S / T) + (cx / T);
+    const int tu = ctu_tu_index(L, ctu, d, j, t);
+    const int64_t o = ctu_tu_offset(L, tu) + (cy % T) * T + (cx % T);
+    const int v = (int)cur[y * stride + x] - resid[o] + (((dc[depth_base(d) + j].cbf >> t) & 1) ? res_out[o] : 0);
+    recon[y * stride + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+  }
+}

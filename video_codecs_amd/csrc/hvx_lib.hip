@@ -64,7 +64,7 @@ size_t ctu_il_off16(int n) { return pad_g((size_t)8 * n) * 1024; }
 size_t ctu_il_off8(int n) { return ctu_il_off16(n) + pad_g((size_t)16 * n) * 256; }
 size_t ctu_il_words(int n) { return ctu_il_off8(n) + pad_g((size_t)64 * n) * 64; }
 struct CtuWs {
-  size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, coefI, levI, stI, flags, total;
+  size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, coefI, levI, stI, flags, cbits, total;
 };
 CtuWs ctu_ws_layout(const CtuLayout &L) {
   CtuWs w;
@@ -86,6 +86,7 @@ CtuWs ctu_ws_layout(const CtuLayout &L) {
   w.levI = o; o = align_up(o + nil * sizeof(int32_t));
   w.stI = o; o = align_up(o + nil * sizeof(int32_t));
   w.flags = o; o = align_up(o + ntu);
+  w.cbits = o; o = align_up(o + ntu * sizeof(hvx_coeff_bits));
   w.total = o;
   return w;
 }
@@ -510,7 +511,7 @@ int hvx_coeff_bits_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t 
     return fail(HVX_E_INVALID, "hvx_coeff_bits_batch: bad args");
   if (!n) return HVX_OK;
   hipLaunchKernelGGL(k_coeff_bits, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, d_desc, d_off, n, d_levels,
-                     d_entropy_bits, d_states, d_out);
+                     d_entropy_bits, d_states, HVX_NUM_CTX, d_out);
   return launched("k_coeff_bits");
 }
 
@@ -567,9 +568,11 @@ int hvx_ctu_workspace_size(int pic_w, int pic_h, int n_ref, size_t *bytes) {
   return HVX_OK;
 }
 
-int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
-                    const hvx_ctu_params *h_params, const hvx_estbits *d_est4, void *d_workspace, size_t ws_bytes,
-                    hvx_cu_result *d_out) {
+// cnt_states != NULL (hvx_ctu_encode): each TU size class's coefficient rate is counted on the
+// class's own stream right behind its TU pipeline, so it overlaps the remaining searches
+static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
+                            const hvx_ctu_params *h_params, const hvx_estbits *d_est4, void *d_workspace, size_t ws_bytes,
+                            hvx_cu_result *d_out, const uint8_t *cnt_states, const int32_t *cnt_eb) {
   if (!ctx || !d_cur || !d_refs || !h_params || !d_est4 || !d_workspace || !d_out)
     return fail(HVX_E_INVALID, "hvx_ctu_analyze: NULL argument");
   const hvx_ctu_params P = *h_params;
@@ -648,6 +651,16 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
   const int g32 = kCtuG, g16 = kCtuG, g8 = kCtuG;
   int32_t *coefI = (int32_t *)(ws + W.coefI), *levI = (int32_t *)(ws + W.levI), *stI = (int32_t *)(ws + W.stI);
   int8_t *flags = (int8_t *)(ws + W.flags);
+  hvx_coeff_bits *cb = (hvx_coeff_bits *)(ws + W.cbits);
+  auto count_class = [&](hipStream_t s, int first, int cnt, size_t il_off, int L2) {
+    if (!cnt_states) return;
+    const int tc = t_begin(ctx, s, 16);
+    const dim3 grid((cnt + 63) / 64);
+    if (L2 == 3) hipLaunchKernelGGL((k_coeff_bits_il<3>), grid, dim3(64), 0, s, desc + first, cnt, levI + il_off, cnt_eb, cnt_states, cb + first);
+    else if (L2 == 2) hipLaunchKernelGGL((k_coeff_bits_il<2>), grid, dim3(64), 0, s, desc + first, cnt, levI + il_off, cnt_eb, cnt_states, cb + first);
+    else hipLaunchKernelGGL((k_coeff_bits_il<1>), grid, dim3(64), 0, s, desc + first, cnt, levI + il_off, cnt_eb, cnt_states, cb + first);
+    t_end(ctx, s, tc);
+  };
   // size classes are contiguous: [0,8n) 32x32 | [8n,24n) 16x16 | [24n,88n) 8x8; their
   // interleaved scratch regions start at 0, ctu_il_off16(n), ctu_il_off8(n)
   {  // stream B
@@ -657,6 +670,7 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
     t_end(ctx, sb, tk);
     tu_class_launch<3, 2>(sb, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev, nullptr, abs_sum, res_out, sse,
                           coefI, levI, stI, flags, g32, 4, ctx, 6);
+    count_class(sb, 0, 8 * n, 0, 3);
     HVX_HIP(hipEventRecord(ctx->fj[3], sb));
   }
   {  // stream C
@@ -667,6 +681,7 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
     const size_t o = ctu_il_off16(n);
     tu_class_launch<2, 2>(sc, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n, 16 * n, resid, nullptr, lev, nullptr,
                           abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, levI + o, stI + o, flags + 8 * n, g16, 4, ctx, 9);
+    count_class(sc, 8 * n, 16 * n, o, 2);
     HVX_HIP(hipEventRecord(ctx->fj[4], sc));
   }
   {  // stream A: depth 3
@@ -676,6 +691,7 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
     const size_t o = ctu_il_off8(n);
     tu_class_launch<1, 2>(st, desc + 24 * n, d_est4, est_idx + 24 * n, off + 24 * n, 64 * n, resid, nullptr, lev, nullptr,
                           abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, levI + o, stI + o, flags + 24 * n, g8, 4, ctx, 12);
+    count_class(st, 24 * n, 64 * n, o, 1);
   }
   HVX_HIP(hipStreamWaitEvent(st, ctx->fj[3], 0));
   HVX_HIP(hipStreamWaitEvent(st, ctx->fj[4], 0));
@@ -683,6 +699,81 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
   hipLaunchKernelGGL(k_ctu_finalize, dim3((n * HVX_CUS_PER_CTU + 255) / 256), dim3(256), 0, st, L, abs_sum, sse, d_out);
   t_end(ctx, st, tk);
   return launched("hvx_ctu_analyze");
+}
+
+int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
+                    const hvx_ctu_params *h_params, const hvx_estbits *d_est4, void *d_workspace, size_t ws_bytes,
+                    hvx_cu_result *d_out) {
+  return ctu_analyze_impl(ctx, d_cur, d_refs, stride, h_params, d_est4, d_workspace, ws_bytes, d_out, nullptr, nullptr);
+}
+
+static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const hvx_ctu_params *h_params,
+                           const uint8_t *d_ctx_states, const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes,
+                           const hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon, bool count) {
+  if (!ctx || !d_cur || !h_params || !d_ctx_states || !d_entropy_bits || !d_workspace || !d_cu || !d_dec || !d_recon)
+    return fail(HVX_E_INVALID, "hvx_ctu_decide: NULL argument");
+  const hvx_ctu_params P = *h_params;
+  if (P.pic_w <= 0 || P.pic_h <= 0 || P.pic_w % 8 || P.pic_h % 8 || P.n_ref <= 0 || P.n_ref > 8 ||
+      stride < P.pic_w + 2 * HVX_PLANE_MARGIN || stride % 4 != 0)
+    return fail(HVX_E_INVALID, "hvx_ctu_decide: bad parameters");
+  const CtuLayout L = ctu_layout(P.pic_w, P.pic_h, P.n_ref);
+  const CtuWs W = ctu_ws_layout(L);
+  if (ws_bytes < W.total) return fail(HVX_E_INVALID, "hvx_ctu_decide: workspace too small");
+  char *ws = (char *)d_workspace;
+  hipStream_t st = ctx->stream;
+  const int n = L.nctu;
+  const hvx_tu_desc *desc = (const hvx_tu_desc *)(ws + W.desc);
+  hvx_coeff_bits *cb = (hvx_coeff_bits *)(ws + W.cbits);
+  // 1. coefficient rate of every TU, one lane per TU, per size class (no mixed-size waves), from
+  //    the RDOQ's interleaved scan-order levels; every TU counts from the same context snapshot
+  int tk = -1;
+  const int32_t *levI = (const int32_t *)(ws + W.levI);
+  if (count) {
+  tk = t_begin(ctx, st, 16);
+  hipLaunchKernelGGL((k_coeff_bits_il<3>), dim3((8 * n + 63) / 64), dim3(64), 0, st, desc, 8 * n, levI, d_entropy_bits,
+                     d_ctx_states, cb);
+  hipLaunchKernelGGL((k_coeff_bits_il<2>), dim3((16 * n + 63) / 64), dim3(64), 0, st, desc + 8 * n, 16 * n,
+                     levI + ctu_il_off16(n), d_entropy_bits, d_ctx_states, cb + 8 * n);
+  hipLaunchKernelGGL((k_coeff_bits_il<1>), dim3((64 * n + 63) / 64), dim3(64), 0, st, desc + 24 * n, 64 * n,
+                     levI + ctu_il_off8(n), d_entropy_bits, d_ctx_states, cb + 24 * n);
+  t_end(ctx, st, tk);
+  }
+  // 2. the CU tree of every CTU, 3. the reconstruction of its leaves + border extension
+  tk = t_begin(ctx, st, 17);
+  DecideArgs A;
+  A.L = L; A.pic_w = P.pic_w; A.pic_h = P.pic_h; A.lambda = P.lambda;
+  A.cu = d_cu; A.res = (const hvx_me_result *)(ws + W.res); A.cb = cb;
+  A.st = d_ctx_states; A.eb = d_entropy_bits; A.dec = d_dec;
+  hipLaunchKernelGGL(k_ctu_leaf, dim3(n * HVX_CUS_PER_CTU), dim3(64), 0, st, A, d_cur, stride, (const int16_t *)(ws + W.resid),
+                     (const int16_t *)(ws + W.res_out), (const int32_t *)(ws + W.abs), (const uint32_t *)(ws + W.sse));
+  hipLaunchKernelGGL(k_ctu_decide, dim3((n + 63) / 64), dim3(64), 0, st, A);
+  hipLaunchKernelGGL(k_ctu_recon, dim3(n), dim3(256), 0, st, L, P.pic_w, P.pic_h, d_cur, stride, (const hvx_cu_decision *)d_dec,
+                     (const int16_t *)(ws + W.resid), (const int16_t *)(ws + W.res_out), d_recon);
+  const int M = HVX_PLANE_MARGIN;
+  hipLaunchKernelGGL(k_plane_extend, dim3((2 * M + 255) / 256, P.pic_h), dim3(256), 0, st, d_recon, stride, P.pic_w, P.pic_h, M, 0);
+  hipLaunchKernelGGL(k_plane_extend, dim3((P.pic_w + 2 * M + 255) / 256, 2 * M), dim3(256), 0, st, d_recon, stride, P.pic_w,
+                     P.pic_h, M, 1);
+  t_end(ctx, st, tk);
+  return launched("hvx_ctu_decide");
+}
+
+int hvx_ctu_decide(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const hvx_ctu_params *h_params,
+                   const uint8_t *d_ctx_states, const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes,
+                   const hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon) {
+  return ctu_decide_impl(ctx, d_cur, stride, h_params, d_ctx_states, d_entropy_bits, d_workspace, ws_bytes, d_cu, d_dec,
+                         d_recon, true);
+}
+
+int hvx_ctu_encode(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
+                   const hvx_ctu_params *h_params, const hvx_estbits *d_est4, const uint8_t *d_ctx_states,
+                   const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes, hvx_cu_result *d_cu,
+                   hvx_cu_decision *d_dec, uint8_t *d_recon) {
+  if (!d_ctx_states || !d_entropy_bits || !d_dec || !d_recon) return fail(HVX_E_INVALID, "hvx_ctu_encode: NULL argument");
+  const int rc = ctu_analyze_impl(ctx, d_cur, d_refs, stride, h_params, d_est4, d_workspace, ws_bytes, d_cu, d_ctx_states,
+                                  d_entropy_bits);
+  if (rc) return rc;
+  return ctu_decide_impl(ctx, d_cur, stride, h_params, d_ctx_states, d_entropy_bits, d_workspace, ws_bytes, d_cu, d_dec,
+                         d_recon, false);
 }
 
 int hvx_plane_extend(hvx_ctx *ctx, uint8_t *d_plane, int width, int height) {

@@ -1,0 +1,52 @@
+"""The writer rank's shared decoded-picture buffer.
+
+CTUs shard across GPUs by independent closed GOP segments, one per rank.  After every picture
+each rank's reconstruction -- the padded 8-bit plane that hvx_ctu_decide wrote, borders already
+extended, i.e. a ready reference picture -- is gathered to rank 0 with ONE torch.distributed
+gather per picture (RCCL over xGMI on the GPUs; gloo in the CPU tests).  The gather is the only
+data-path collective of the path.  It is asynchronous and the reconstruction buffers are
+double-buffered, so picture k+1 is analysed while picture k's samples move; a buffer is handed
+out again only after the gather that read it has completed.  Rank 0 keeps one plane per rank.
+"""
+
+
+class DpbGather:
+    def __init__(self, world, rank, plane_shape, device, nbuf=2):
+        import torch
+        self.world, self.rank, self.nbuf, self.k = world, rank, nbuf, 0
+        self.recon = [torch.zeros(plane_shape, dtype=torch.uint8, device=device) for _ in range(nbuf)]
+        self.dpb = None
+        if world > 1 and rank == 0:
+            self.dpb = [[torch.zeros(plane_shape, dtype=torch.uint8, device=device) for _ in range(world)]
+                        for _ in range(nbuf)]
+        self.pending = [None] * nbuf
+
+    def buffer(self):
+        """The reconstruction buffer of the current picture (waits for the gather that last read it)."""
+        b = self.k % self.nbuf
+        if self.pending[b] is not None:
+            self.pending[b].wait()
+            self.pending[b] = None
+        return self.recon[b]
+
+    def send(self):
+        """Gather the current picture to rank 0 (no-op on one rank) and advance; returns its buffer index."""
+        import torch.distributed as dist
+        b = self.k % self.nbuf
+        if self.world > 1:
+            self.pending[b] = dist.gather(self.recon[b], self.dpb[b] if self.rank == 0 else None, dst=0,
+                                          async_op=True)
+        self.k += 1
+        return b
+
+    def drain(self):
+        """Wait for every outstanding gather."""
+        for b in range(self.nbuf):
+            if self.pending[b] is not None:
+                self.pending[b].wait()
+                self.pending[b] = None
+
+    def last(self):
+        """(own reconstruction, rank 0's gathered planes or None) of the latest sent picture."""
+        b = (self.k - 1) % self.nbuf
+        return self.recon[b], (self.dpb[b] if self.dpb is not None else None)
