@@ -17,7 +17,7 @@ CASES = {  # name: (cfg, yuv kind, frames, qp)
     "intra_smooth_qp22": ("intra.cfg", "smooth", 1, 22),
     "ldp_smooth_qp32": ("ldp.cfg", "smooth", 3, 32),
     "ldb_smooth_qp32": ("ldb.cfg", "smooth", 3, 32),  # B slices: bi-prediction, identical-motion shortcut
-    "ldp_rand_qp32": ("ldp.cfg", "random", 3, 32),    # uniform random: long TZ raster searches
+    "ldp_rand_qp32": ("ldp.cfg", "random", 2, 32),    # uniform random: long TZ raster searches
     "ra_smooth_qp27": ("ra.cfg", "smooth", 9, 27),    # GOP8 hierarchical B: future refs, bBi refinement
 }
 YUV_FRAMES = max(c[2] for c in CASES.values())
@@ -32,9 +32,16 @@ def encode(binary, case, tmp, log=None):
     if not os.path.exists(yuv):
         make_yuv.write_yuv(yuv, kind, W, H, YUV_FRAMES)
     bs, rec = os.path.join(tmp, case + ".bin"), os.path.join(tmp, case + ".rec.yuv")
-    p = subprocess.run([binary, "-c", os.path.join(HERE, cfg), "-i", yuv, "-wdt", str(W), "-hgt", str(H), "-fr", "30",
-                        "-f", str(frames), "-q", str(qp), "-b", bs, "-o", rec],
-                       stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    # the encoder's per-picture lines go to HVX_SEAM_LOG_DIR/<case>.log when set (progress of a long run)
+    log_dir = os.environ.get("HVX_SEAM_LOG_DIR")
+    out = open(os.path.join(log_dir, case + ".log"), "w") if log_dir else subprocess.DEVNULL
+    try:
+        p = subprocess.run([binary, "-c", os.path.join(HERE, cfg), "-i", yuv, "-wdt", str(W), "-hgt", str(H), "-fr",
+                            "30", "-f", str(frames), "-q", str(qp), "-b", bs, "-o", rec],
+                           stdout=out, stderr=subprocess.PIPE, text=True)
+    finally:
+        if log_dir:
+            out.close()
     if log is not None:
         log.append(p.stderr)
     if p.returncode:

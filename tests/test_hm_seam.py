@@ -20,6 +20,7 @@ EXPECTED = json.load(open(os.path.join(ROOT, "tests", "hm_seam", "expected_md5.j
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(600)  # ~1M synchronous per-call offloads per encode: correctness, not speed
 @pytest.mark.parametrize("case", sorted(mk.CASES))
 def test_hm_encoder_with_hvx_seams(case):
     import torch
