@@ -157,6 +157,45 @@ typedef struct hvx_cu_decision {
   int32_t pad_;
 } hvx_cu_decision;
 
+/* One intra block: TComPrediction::initIntraPatternChType's reference
+ * samples (TComPattern.cpp:115-360: fillReferenceSamples :364 substitution + the [1 2 1] /
+ * strong bilinear smoothing), predIntraAng (TComPrediction.cpp:455: planar :756, DC :183 +
+ * xDCPredFiltering :816, angular xPredIntraAng :247 with its edge filters), and
+ * TEncSearch::estIntraPredLumaQT's first pass (TEncSearch.cpp:2244-2323: Hadamard SATD of all 35
+ * modes + xModeBitsIntra :5222 rate, sqrt-lambda cost, xUpdateCandList :5254, MPM append).
+ * The block is square, size 1 << log2_size, at (x, y) of an 8-bit padded plane; 8-bit video. */
+#define HVX_INTRA_STRONG   1   /* SPS strong_intra_smoothing_enabled_flag (luma 32x32) */
+#define HVX_INTRA_FAST_MPM 2   /* FastUDIUseMPM: g_aucIntraModeNumFast_UseMPM + MPM append */
+typedef struct hvx_intra_job {
+  int32_t x, y;              /* block origin in its plane, samples */
+  int32_t log2_size;         /* 2..6 luma, 2..5 chroma */
+  int32_t ch_type;           /* 0 luma, 1 chroma (4:2:0: no reference smoothing, no edge/DC filters) */
+  int32_t unit_log2;         /* neighbour unit in samples (minimum CU/TU grid): 2 luma, 1 chroma 4:2:0 */
+  uint32_t avail[3];         /* bNeighborFlags (TComPattern.cpp:140-147), bit i = unit i: 0..L-1 the left and
+                                below-left units bottom-up (L = 2*size >> unit_log2), L the above-left unit,
+                                L+1..2L the above and above-right units left to right */
+  int32_t mode;              /* hvx_intra_pred_batch: 0 planar, 1 DC, 2..34 angular */
+  int32_t flags;             /* HVX_INTRA_STRONG | HVX_INTRA_FAST_MPM */
+  int32_t left_dir, above_dir; /* first pass: the intra dirs TComDataCU::getIntraDirPredictor reads
+                                  (TComDataCU.cpp:1413-1428; DC = 1 when unavailable / not intra) */
+  int32_t ctx_state;         /* first pass: m_ucState of prev_intra_luma_pred_flag's context */
+  int32_t frac_bits;         /* first pass: m_fracBits & 32767 of the bin counter of the coder xModeBitsIntra
+                                loads from (m_pppcRDSbacCoder[depth][CI_CURR_BEST]): loadIntraDirMode copies
+                                it (TEncSbac.cpp:403) and resetBits keeps those bits (TEncBinCoderCABAC.cpp:172) */
+  double sqrt_lambda;        /* first pass: TComRdCost::getSqrtLambda */
+} hvx_intra_job;
+
+/* First-pass result of one intra PU (estIntraPredLumaQT's uiRdModeList / CandCostList). */
+typedef struct hvx_intra_search_result {
+  double cand_cost[8];       /* CandCostList[0..num_rd), ascending */
+  uint32_t satd[35];         /* Hadamard SATD of each mode's prediction against the original */
+  uint8_t mode_bits[35];     /* xModeBitsIntra of each mode */
+  uint8_t num_rd;            /* numModesForFullRD before the MPM append */
+  uint8_t n_cand;            /* candidates after the MPM append (<= 11) */
+  uint8_t cand[11];          /* uiRdModeList */
+  uint8_t pad_[4];
+} hvx_intra_search_result;
+
 /* One PU's motion compensation (TComPrediction::motionCompensation for one partition, no
  * weighted prediction; TComPrediction.cpp:517-722).  Lists with ref >= 0 are used: both ->
  * bi-prediction (14-bit intermediates + TComYuv::addAvg), unless HVX_MC_B_SLICE is set and the

@@ -304,3 +304,65 @@ def coeff_bits(desc, levels, states, entropy_bits):
     L.hvxo_coeff_bits.argtypes = [ctypes.c_void_p] * 5
     L.hvxo_coeff_bits(_p(d), _p(lv), _p(st), _p(eb), _p(out))
     return int(out["frac_bits"][0]), int(out["rice_stat"][0]), int(out["num_sig"][0]), st[:len(states)].copy()
+
+
+# ------------------------------------------------------------------------------------------ intra
+def _intra_lib():
+    L = lib()
+    if not getattr(L, "_intra_ready", False):
+        P, I = ctypes.c_void_p, ctypes.c_int
+        L.hvxo_intra_fill.argtypes = [P, P, I, I, P]
+        L.hvxo_intra_filter.argtypes = [P, I, I, I, P]
+        L.hvxo_intra_use_filter.argtypes = [I, I, I]
+        L.hvxo_intra_use_filter.restype = I
+        L.hvxo_intra_pred.argtypes = [P, I, I, I, P]
+        L.hvxo_intra_search.argtypes = [P, P, P, P, P]
+        L._intra_ready = True
+    return L
+
+
+def avail_words(flags):
+    """bNeighborFlags (one 0/1 per unit) -> hvx_intra_job.avail (3 x uint32)."""
+    w = np.zeros(3, np.uint32)
+    for i, f in enumerate(np.asarray(flags).reshape(-1)):
+        if f:
+            w[i >> 5] |= np.uint32(1 << (i & 31))
+    return w
+
+
+def intra_fill(raw, flags, n, unit_log2):
+    """hvxo_intra_fill: raw border samples (>= 4n+1) + per-unit flags -> border (4n+1, int16)."""
+    r = _c(np.asarray(raw)[:4 * n + 1], np.int16)
+    a = avail_words(flags)
+    b = np.zeros(4 * n + 1, np.int16)
+    _intra_lib().hvxo_intra_fill(_p(r), _p(a), int(n), int(unit_log2), _p(b))
+    return b
+
+
+def intra_filter(border, n, is_luma, strong):
+    b = _c(np.asarray(border)[:4 * n + 1], np.int16)
+    o = np.zeros(4 * n + 1, np.int16)
+    _intra_lib().hvxo_intra_filter(_p(b), int(n), int(is_luma), int(strong), _p(o))
+    return o
+
+
+def intra_use_filter(mode, n, is_luma):
+    return bool(_intra_lib().hvxo_intra_use_filter(int(mode), int(n), int(is_luma)))
+
+
+def intra_pred(border, n, is_luma, mode):
+    b = _c(np.asarray(border)[:4 * n + 1], np.int16)
+    o = np.zeros(n * n, np.uint8)
+    _intra_lib().hvxo_intra_pred(_p(b), int(n), int(is_luma), int(mode), _p(o))
+    return o.reshape(n, n)
+
+
+def intra_search(org, raw, job, entropy_bits):
+    """hvxo_intra_search: org (n*n uint8), raw border (int16), job (_abi.INTRA_JOB record) -> result record."""
+    o = _c(np.asarray(org).reshape(-1), np.uint8)
+    r = _c(np.asarray(raw).reshape(-1)[:257], np.int16)
+    j = np.array(job, dtype=_abi.INTRA_JOB).reshape(1)
+    eb = _c(entropy_bits, np.int32)
+    out = np.zeros(1, _abi.INTRA_RESULT)
+    _intra_lib().hvxo_intra_search(_p(o), _p(r), _p(j), _p(eb), _p(out))
+    return out[0]

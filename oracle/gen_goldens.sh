@@ -44,4 +44,13 @@ cab "$TMP/cab_p.bin"   $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth.yuv" 3 27
 cab "$TMP/cab_p22.bin" $CFG/encoder_lowdelay_P_main.cfg "$TMP/rand.yuv"   2 22
 python3 oracle/merge_goldens.py tests/golden/cabac.bin "$TMP"/cab_i.bin "$TMP"/cab_i22.bin "$TMP"/cab_p.bin "$TMP"/cab_p22.bin
 python3 oracle/compact_cabac.py tests/golden/cabac.bin
+# intra reference samples, predictions and the first-pass mode search (oracle/intra_capture.cpp)
+icap() {  # icap <out.bin> <cfg> <yuv> <frames> <qp>
+  HVX_CAPTURE=$1 $ORC/TAppEncoder_intracap -c "$2" -i "$3" -wdt 416 -hgt 240 -fr 30 -f "$4" -q "$5" \
+    -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+}
+icap "$TMP/in_i.bin"   $CFG/encoder_intra_main.cfg      "$TMP/rand.yuv"   1 32
+icap "$TMP/in_i22.bin" $CFG/encoder_intra_main.cfg      "$TMP/smooth.yuv" 1 22
+icap "$TMP/in_p.bin"   $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth.yuv" 3 27
+python3 oracle/merge_goldens.py tests/golden/intra.bin "$TMP"/in_i.bin "$TMP"/in_i22.bin "$TMP"/in_p.bin
 ls -la tests/golden

@@ -1960,3 +1960,220 @@ void hvxo_me_full(const int16_t *tgt, int tstride, const uint8_t *refp, int ref_
   r->mv_x = fmx; r->mv_y = fmy; r->bits = bits;
   r->cost = (uint32_t)(floor(wgt * ((double)cost - (double)((t.lam * mv_bits) >> 16))) + (double)((t.lam * bits) >> 16));
 }
+
+/* ============================================================================================
+ * Intra prediction.  Border layout B (4N+1 samples): B[0] = above-left,
+ * B[1..2N] = above + above-right row left to right, B[2N+1..4N] = left + below-left column top
+ * to bottom -- the row 0 / column 0 of HM's (2N+1)x(2N+1) m_piYuvExt buffer.
+ * ========================================================================================== */
+static int avail_bit(const uint32_t *a, int i) { return (int)((a[i >> 5] >> (i & 31)) & 1); }
+
+/* fillReferenceSamples (TComPattern.cpp:364-540), 8-bit.  raw = reconstructed samples at the
+ * border positions (read whatever their availability); the line of the reference is
+ * L[0..2N) = left column bottom-up, L[2N..2N+u) = the above-left unit, L[2N+u..) = above row. */
+static int line_raw(const int16_t *raw, int n, int u, int l) {
+  if (l < 2 * n) return raw[2 * n + 1 + (2 * n - 1 - l)];
+  if (l < 2 * n + u) return raw[0];
+  return raw[1 + (l - 2 * n - u)];
+}
+
+void hvxo_intra_fill(const int16_t *raw, const uint32_t *avail, int n, int unit_log2, int16_t *B) {
+  const int u = 1 << unit_log2, lu = (2 * n) >> unit_log2, nunits = 2 * lu + 1, nl = 4 * n + u;
+  int16_t L[4 * 64 + 8];
+  int navail = 0;
+  for (int i = 0; i < nunits; i++) navail += avail_bit(avail, i);
+  if (navail == 0) { /* :384-395 DC fill */
+    for (int k = 0; k <= 4 * n; k++) B[k] = 128;
+    return;
+  }
+  for (int l = 0; l < nl; l++) L[l] = 128; /* :425-429 */
+  for (int i = 0; i < nunits; i++)
+    if (avail_bit(avail, i))
+      for (int k = 0; k < u; k++) L[i * u + k] = (int16_t)line_raw(raw, n, u, i * u + k);
+  int cur = 0;
+  if (!avail_bit(avail, 0)) { /* :476-506: pad the bottom run with the first available sample */
+    int next = 1;
+    while (next < nunits && !avail_bit(avail, next)) next++;
+    const int16_t ref = L[next * u];
+    for (; cur < next; cur++)
+      for (int k = 0; k < u; k++) L[cur * u + k] = ref;
+  }
+  for (; cur < nunits; cur++) /* :508-526: every other gap takes the sample just below it */
+    if (!avail_bit(avail, cur))
+      for (int k = 0; k < u; k++) L[cur * u + k] = L[cur * u - 1];
+  B[0] = L[2 * n + u - 1]; /* :530-539 */
+  for (int i = 0; i < 2 * n; i++) B[1 + i] = L[2 * n + u + i];
+  for (int j = 0; j < 2 * n; j++) B[2 * n + 1 + j] = L[2 * n - 1 - j];
+}
+
+/* the smoothing of initIntraPatternChType (TComPattern.cpp:190-330) over F = B in the order
+ * bottom-left .. above-left .. above-right */
+static int f_index(int n, int k) { return k < 2 * n ? 4 * n - k : k == 2 * n ? 0 : k - 2 * n; }
+
+void hvxo_intra_filter(const int16_t *B, int n, int is_luma, int strong_enabled, int16_t *out) {
+  const int bl = B[4 * n], tl = B[0], tr = B[2 * n];
+  int strong = is_luma && strong_enabled;
+  if (strong) { /* :214-226, threshold 1 << (8 - 5) */
+    const int bil_left = abs(bl + tl - 2 * B[3 * n]) < 8, bil_above = abs(tl + tr - 2 * B[n]) < 8;
+    if (n < 32 || !bil_left || !bil_above) strong = 0;
+  }
+  const int shift = strong ? (n == 64 ? 7 : n == 32 ? 6 : n == 16 ? 5 : n == 8 ? 4 : 3) : 0;
+  for (int k = 0; k <= 4 * n; k++) {
+    int v;
+    if (k == 0 || k == 4 * n) v = B[f_index(n, k)];                  /* ends unfiltered */
+    else if (strong && k == 2 * n) v = tl;                             /* :262 */
+    else if (strong && k < 2 * n) v = ((2 * n - k) * bl + k * tl + n) >> shift;  /* :236-243 */
+    else if (strong) v = ((4 * n - k) * tl + (k - 2 * n) * tr + n) >> shift;     /* :281-288 */
+    else v = (B[f_index(n, k - 1)] + 2 * B[f_index(n, k)] + B[f_index(n, k + 1)] + 2) >> 2;
+    out[f_index(n, k)] = (int16_t)v;
+  }
+}
+
+/* TComPrediction::filteringIntraReferenceSamples (TComPattern.cpp:544-569), 4:2:0 */
+int hvxo_intra_use_filter(int mode, int n, int is_luma) {
+  static const int thr[5] = {10, 7, 1, 0, 10}; /* m_aucIntraFilter (TComPrediction.cpp:50) */
+  if (!is_luma || mode == 1) return 0;
+  int l = 0;
+  while ((4 << l) < n) l++;
+  const int d10 = abs(mode - 10), d26 = abs(mode - 26);
+  return (d10 < d26 ? d10 : d26) > thr[l];
+}
+
+/* predIntraAng (TComPrediction.cpp:455-516) with bAbove = bLeft = true (initIntraPatternChType
+ * always reports both, TComPattern.cpp:152-153) and the edge filters enabled (no RDPCM). */
+void hvxo_intra_pred(const int16_t *B, int n, int is_luma, int mode, uint8_t *pred) {
+  int log2n = 0;
+  while ((1 << log2n) < n) log2n++;
+  const int edge = is_luma && n <= 16;
+#define A(i) ((int)B[1 + (i)])
+#define LF(j) ((int)B[2 * n + 1 + (j)])
+  if (mode == 0) { /* xPredIntraPlanar (:756) */
+    for (int r = 0; r < n; r++)
+      for (int c = 0; c < n; c++)
+        pred[r * n + c] = (uint8_t)(((n - 1 - c) * LF(r) + (c + 1) * A(n) + (n - 1 - r) * A(c) + (r + 1) * LF(n) + n) >>
+                                    (log2n + 1));
+    return;
+  }
+  if (mode == 1) { /* predIntraGetPredValDC (:183) + xDCPredFiltering (:816) */
+    int sum = 0;
+    for (int i = 0; i < n; i++) sum += A(i) + LF(i);
+    const int dc = (sum + n) / (2 * n);
+    for (int r = 0; r < n; r++)
+      for (int c = 0; c < n; c++) {
+        int v = dc;
+        if (edge && r == 0 && c == 0) v = (A(0) + LF(0) + 2 * dc + 2) >> 2;
+        else if (edge && r == 0) v = (A(c) + 3 * dc + 2) >> 2;
+        else if (edge && c == 0) v = (LF(r) + 3 * dc + 2) >> 2;
+        pred[r * n + c] = (uint8_t)v;
+      }
+    return;
+  }
+  /* xPredIntraAng (:247-452) */
+  static const int ang_table[9] = {0, 2, 5, 9, 13, 17, 21, 26, 32};
+  static const int inv_table[9] = {0, 4096, 1638, 910, 630, 482, 390, 315, 256};
+  const int ver = mode >= 18, am = ver ? mode - 26 : 10 - mode, aa = abs(am);
+  const int angle = (am < 0 ? -1 : 1) * ang_table[aa], inv = inv_table[aa];
+  int ref_above[2 * 64 + 1 + 64], ref_left[2 * 64 + 1 + 64];
+  int *above = ref_above + 64, *left = ref_left + 64; /* index -64..2n */
+  for (int k = 0; k <= 2 * n; k++) { above[k] = B[k]; left[k] = k ? LF(k - 1) : B[0]; }
+  int *mainr = ver ? above : left, *side = ver ? left : above;
+  if (angle < 0) { /* :321-329 extend the main reference with the projected side */
+    int sum = 128;
+    for (int k = -1; k > (n * angle) >> 5; k--) { sum += inv; mainr[k] = side[sum >> 8]; }
+  }
+  int tmp[64 * 64];
+  for (int y = 0; y < n; y++) {
+    const int dp = (y + 1) * angle, di = dp >> 5, f = dp & 31;
+    for (int x = 0; x < n; x++) {
+      int v;
+      if (angle == 0) v = mainr[x + 1];
+      else if (f) v = ((32 - f) * mainr[x + di + 1] + f * mainr[x + di + 2] + 16) >> 5;
+      else v = mainr[x + di + 1];
+      tmp[y * n + x] = v;
+    }
+    if (angle == 0 && edge) { /* :375-381 */
+      int v = tmp[y * n] + ((side[y + 1] - side[0]) >> 1);
+      tmp[y * n] = v < 0 ? 0 : v > 255 ? 255 : v;
+    }
+  }
+  for (int r = 0; r < n; r++)
+    for (int c = 0; c < n; c++) pred[r * n + c] = (uint8_t)(ver ? tmp[r * n + c] : tmp[c * n + r]);
+#undef A
+#undef LF
+}
+
+/* TComDataCU::getIntraDirPredictor (TComDataCU.cpp:1441-1478) from the two neighbour dirs;
+ * returns iMode (1: left == above, 2 otherwise) */
+static int intra_mpm(int ld, int ad, int *p) {
+  if (ld == ad) {
+    if (ld > 1) { p[0] = ld; p[1] = ((ld + 29) % 32) + 2; p[2] = ((ld - 1) % 32) + 2; }
+    else { p[0] = 0; p[1] = 1; p[2] = 26; }
+    return 1;
+  }
+  p[0] = ld; p[1] = ad;
+  p[2] = (ld && ad) ? 0 : ((ld + ad) < 2 ? 26 : 1);
+  return 2;
+}
+
+/* estIntraPredLumaQT's first pass (TEncSearch.cpp:2244-2323) for one luma PU: org = n*n
+ * original samples, raw = reconstructed samples at the border positions. */
+void hvxo_intra_search(const uint8_t *org, const int16_t *raw, const hvx_intra_job *j, const int32_t *eb,
+                       hvx_intra_search_result *r) {
+  const int n = 1 << j->log2_size;
+  int16_t unf[257], filt[257];
+  hvxo_intra_fill(raw, j->avail, n, j->unit_log2, unf);
+  hvxo_intra_filter(unf, n, 1, (j->flags & HVX_INTRA_STRONG) != 0, filt); /* bFilterRefSamples = true (:2256) */
+  memset(r, 0, sizeof(*r));
+  int mpm[3];
+  const int imode = intra_mpm(j->left_dir, j->above_dir, mpm);
+  const int fast = (j->flags & HVX_INTRA_FAST_MPM) != 0;
+  static const int num_mpm[6] = {3, 8, 8, 3, 3, 3}, num_nompm[6] = {3, 9, 9, 4, 4, 5}; /* TComRom.cpp:545-562 */
+  const int widx = j->log2_size - 1; /* getIntraSizeIdx (TComDataCU.cpp:2804) */
+  int num = fast ? num_mpm[widx] : num_nompm[widx];
+  uint32_t list[35];
+  double ccost[35];
+  for (int i = 0; i < 35; i++) { list[i] = 0; ccost[i] = 1.7e308; }
+  uint8_t pred[64 * 64];
+  int16_t org16[64 * 64], pred16[64 * 64];
+  for (int i = 0; i < n * n; i++) org16[i] = org[i];
+  /* xModeBitsIntra: loadIntraDirMode copies the source coder's bin state, m_fracBits included
+   * (TEncSbac.cpp:403), and resetBits keeps its low 15 bits (TEncBinCoderCABAC.cpp:172): every
+   * mode counts from the same fraction */
+  const uint64_t frac = (uint64_t)j->frac_bits;
+  for (int m = 0; m < 35; m++) {
+    hvxo_intra_pred(hvxo_intra_use_filter(m, n, 1) ? filt : unf, n, 1, m, pred);
+    for (int i = 0; i < n * n; i++) pred16[i] = pred[i];
+    const uint32_t satd = hvxo_satd(org16, n, pred16, n, n, n);
+    /* xModeBitsIntra (:5222): TEncSbac::codeIntraDirLumaAng (TEncSbac.cpp:643) counted by
+     * TEncBinCABACCounter: flag bin + 1/2 (MPM idx) or 5 bypass bins */
+    int idx = -1;
+    for (int i = 0; i < 3; i++)
+      if (m == mpm[i]) idx = i;
+    const uint64_t total = frac + (uint64_t)eb[j->ctx_state ^ (idx >= 0 ? 1 : 0)] +
+                           32768ull * (uint64_t)(idx < 0 ? 5 : idx ? 2 : 1);
+    const uint32_t bits = (uint32_t)(total >> 15);
+    r->satd[m] = satd;
+    r->mode_bits[m] = (uint8_t)bits;
+    const double cost = (double)satd + (double)bits * j->sqrt_lambda;
+    /* xUpdateCandList (:5254) */
+    int shift = 0;
+    while (shift < num && cost < ccost[num - 1 - shift]) shift++;
+    if (shift) {
+      for (int i = 1; i < shift; i++) { list[num - i] = list[num - 1 - i]; ccost[num - i] = ccost[num - 1 - i]; }
+      list[num - shift] = (uint32_t)m;
+      ccost[num - shift] = cost;
+    }
+  }
+  r->num_rd = (uint8_t)num;
+  for (int i = 0; i < num && i < 8; i++) r->cand_cost[i] = ccost[i];
+  if (fast) { /* :2299-2321 */
+    const int ncand = imode >= 0 ? imode : 3;
+    for (int jj = 0; jj < ncand; jj++) {
+      int inc = 0;
+      for (int i = 0; i < num; i++) inc |= mpm[jj] == (int)list[i];
+      if (!inc) list[num++] = (uint32_t)mpm[jj];
+    }
+  }
+  r->n_cand = (uint8_t)num;
+  for (int i = 0; i < num; i++) r->cand[i] = (uint8_t)list[i];
+}

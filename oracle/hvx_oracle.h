@@ -89,6 +89,19 @@ void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride
                       const hvx_estbits *est /* [4]: luma 4x4..32x32 */, int ctu_x, int ctu_y,
                       hvx_cu_result *out /* [HVX_CUS_PER_CTU] */);
 
+/* ---- intra (border layout: hvx_oracle.c "Intra prediction") ---- */
+/* fillReferenceSamples (TComPattern.cpp:364): raw border samples + bNeighborFlags -> border */
+void hvxo_intra_fill(const int16_t *raw, const uint32_t *avail, int n, int unit_log2, int16_t *border);
+/* initIntraPatternChType's [1 2 1] / strong smoothing (TComPattern.cpp:190-330) */
+void hvxo_intra_filter(const int16_t *border, int n, int is_luma, int strong_enabled, int16_t *out);
+/* filteringIntraReferenceSamples (TComPattern.cpp:544), 4:2:0 */
+int hvxo_intra_use_filter(int mode, int n, int is_luma);
+/* predIntraAng (TComPrediction.cpp:455): pred = n*n */
+void hvxo_intra_pred(const int16_t *border, int n, int is_luma, int mode, uint8_t *pred);
+/* estIntraPredLumaQT's first pass (TEncSearch.cpp:2244-2323); eb = ContextModel::m_entropyBits */
+void hvxo_intra_search(const uint8_t *org, const int16_t *raw, const hvx_intra_job *j, const int32_t *eb,
+                       hvx_intra_search_result *r);
+
 /* tables (generated, HEVC spec values) */
 void hvxo_dct_matrix(int n, int16_t *m /* n*n, [k][x] */);
 const uint32_t *hvxo_scan(int grouped, int scan_type, int log2w, int log2h);

@@ -110,3 +110,55 @@ def cabac_cases(g):
     off = g["coef_off"]
     levels = [g["coef_flat"][off[i]:off[i + 1]].astype(np.int32) for i in range(n)]
     return d, levels
+
+
+# ------------------------------------------------------------------------------------------ intra
+def intra_ref_cases(g):
+    """initIntraPatternChType records: (n, is_luma, unit_log2, filtered?, raw border, flags, unf, filt)."""
+    out = []
+    for i, (log2n, ch, ul, filt, _ab, nfl) in enumerate(g["ref_meta"]):
+        n = 1 << int(log2n)
+        out.append((n, ch == 0, int(ul), bool(filt), g["ref_raw"][i][:4 * n + 1], g["ref_flags"][i][:nfl],
+                    g["ref_unf"][i][:4 * n + 1], g["ref_filt"][i][:4 * n + 1]))
+    return out
+
+
+def intra_pred_cases(g):
+    """predIntraAng records: (n, is_luma, mode, use_filter, border, expected n x n)."""
+    out, off = [], 0
+    for i, (log2n, ch, mode, uf, _a, _l) in enumerate(g["pred_meta"]):
+        n = 1 << int(log2n)
+        out.append((n, ch == 0, int(mode), bool(uf), g["pred_border"][i][:4 * n + 1],
+                    g["pred_out"][off:off + n * n].reshape(n, n)))
+        off += n * n
+    assert off == len(g["pred_out"])
+    return out
+
+
+def intra_fp_cases(g):
+    """estIntraPredLumaQT first-pass records: (job record, org n*n, raw border, expected dict)."""
+    from oracle import avail_words
+    out, off = [], 0
+    for i, m in enumerate(g["fp_meta"]):
+        log2n, st, ld, ad, _imode, _p0, _p1, _p2, nrd, ncand, fast, frac0 = (int(v) for v in m)
+        n = 1 << log2n
+        job = np.zeros(1, _abi.INTRA_JOB)[0]
+        job["log2_size"], job["unit_log2"] = log2n, 2
+        job["avail"] = avail_words(g["fp_flags"][i][:n + 1])
+        job["flags"] = (_abi.INTRA_FAST_MPM if fast else 0) | _abi.INTRA_STRONG
+        job["left_dir"], job["above_dir"], job["ctx_state"], job["frac_bits"] = ld, ad, st, frac0
+        job["sqrt_lambda"] = g["fp_lambda"][i]
+        exp = {"satd": g["fp_satd"][i], "bits": g["fp_bits"][i], "num_rd": nrd, "n_cand": ncand,
+               "cand": g["fp_cand"][i][:ncand], "cand_cost": g["fp_cand_cost"][i][:nrd]}
+        out.append((job, g["fp_org"][off:off + n * n], g["fp_raw"][i], exp))
+        off += n * n
+    return out
+
+
+def intra_fp_matches(r, exp):
+    """One hvx_intra_search_result record against a golden first pass (bit-exact, costs as doubles)."""
+    nrd, nc = exp["num_rd"], exp["n_cand"]
+    return (np.array_equal(r["satd"], exp["satd"]) and np.array_equal(r["mode_bits"], exp["bits"])
+            and int(r["num_rd"]) == nrd and int(r["n_cand"]) == nc
+            and list(r["cand"][:nc]) == list(exp["cand"])
+            and np.array_equal(r["cand_cost"][:nrd], exp["cand_cost"]))

@@ -5,6 +5,7 @@ import pytest
 
 import oracle
 from tests import golden_cases as gc
+from video_codecs_amd import _abi
 
 
 def test_dist_golden():
@@ -140,3 +141,45 @@ def test_coeff_bits_golden():
         assert fb == int(g["frac"][i, 1] - g["frac"][i, 0]), (i, descs[i])
         assert rice == int(g["rice_after"][i])
         np.testing.assert_array_equal(st, g["states_after"][i], err_msg=f"record {i}")
+
+
+def test_intra_reference_samples_golden():
+    """fillReferenceSamples + smoothing vs 1188 initIntraPatternChType calls of real HM encodes."""
+    g = gc.load("intra.bin")
+    cases = gc.intra_ref_cases(g)
+    kinds = set()
+    for n, luma, ul, filt, raw, flags, unf, exp_filt in cases:
+        got = oracle.intra_fill(raw, flags, n, ul)
+        np.testing.assert_array_equal(got, unf)
+        if filt:
+            np.testing.assert_array_equal(oracle.intra_filter(got, n, luma, True), exp_filt)
+        na = int(np.sum(flags))
+        kinds.add((n, bool(luma), 0 if na == 0 else 1 if na == len(flags) else 2))
+    # every size of both channel types (4:2:0 chroma up to 16x16), no / all / some neighbours available
+    want = {(n, l, k) for n in (4, 8, 16, 32) for l in (True, False) for k in (0, 1, 2) if l or n < 32}
+    assert want <= kinds and (64, True, 2) in kinds
+
+
+def test_intra_pred_golden():
+    """predIntraAng (planar, DC, 33 angles, edge/DC filters) vs 2214 reference predictions."""
+    g = gc.load("intra.bin")
+    cases = gc.intra_pred_cases(g)
+    modes = set()
+    for n, luma, mode, uf, border, exp in cases:
+        assert oracle.intra_use_filter(mode, n, luma) == uf
+        np.testing.assert_array_equal(oracle.intra_pred(border, n, luma, mode), exp)
+        modes.add((luma, mode))
+    assert len(modes) == 70
+
+
+def test_intra_first_pass_golden():
+    """estIntraPredLumaQT's first pass: SATD of all 35 modes, xModeBitsIntra, the cost ranking
+    and MPM-extended candidate list vs 642 reference PUs (4x4..64x64)."""
+    g = gc.load("intra.bin")
+    eb = _abi.load_entropy_bits()
+    sizes = set()
+    for job, org, raw, exp in gc.intra_fp_cases(g):
+        r = oracle.intra_search(org, raw, job, eb)
+        assert gc.intra_fp_matches(r, exp)
+        sizes.add(int(job["log2_size"]))
+    assert sizes == {2, 3, 4, 5, 6}

@@ -96,3 +96,13 @@ def load_entropy_bits():
     import os
     p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "entropy_bits.bin")
     return np.fromfile(p, dtype="<i4")
+
+# hvx_intra_job / hvx_intra_search_result (hvx_types.h)
+INTRA_STRONG, INTRA_FAST_MPM = 1, 2
+INTRA_JOB = np.dtype([("x", "<i4"), ("y", "<i4"), ("log2_size", "<i4"), ("ch_type", "<i4"), ("unit_log2", "<i4"),
+                      ("avail", "<u4", (3,)), ("mode", "<i4"), ("flags", "<i4"), ("left_dir", "<i4"),
+                      ("above_dir", "<i4"), ("ctx_state", "<i4"), ("frac_bits", "<i4"), ("sqrt_lambda", "<f8")])
+assert INTRA_JOB.itemsize == 64
+INTRA_RESULT = np.dtype([("cand_cost", "<f8", (8,)), ("satd", "<u4", (35,)), ("mode_bits", "u1", (35,)),
+                         ("num_rd", "u1"), ("n_cand", "u1"), ("cand", "u1", (11,)), ("pad_", "u1", (4,))])
+assert INTRA_RESULT.itemsize == 256
