@@ -42,6 +42,10 @@
  *                         chosen leaves (the reconstructed picture) and extendPicBorder
  *   hvx_ctu_encode        hvx_ctu_analyze + hvx_ctu_decide as one schedule (TEncSlice::compressSlice's
  *                         compressCtu loop over a picture, TEncSlice.cpp:814)
+ *   hvx_intra_pred_batch  TComPrediction::initIntraPatternChType (TComPattern.cpp:115, reference
+ *                         samples + smoothing) + predIntraAng (TComPrediction.cpp:455)
+ *   hvx_intra_search_batch TEncSearch::estIntraPredLumaQT's first pass (TEncSearch.cpp:2244-2323):
+ *                         35-mode Hadamard cost ranking + MPM candidates per luma PU
  *   hvx_plane_from_pel    TComPicYuv int16 padded plane -> device 8-bit padded plane, with
  *                         TComPicYuv::extendPicBorder (TComPicYuv.cpp:197)
  */
@@ -227,6 +231,22 @@ int hvx_estbits_batch(hvx_ctx *ctx, const uint8_t *d_states, const int32_t *d_en
  * ------------------------------------------------------------------------------------- */
 int hvx_coeff_bits_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t *d_off, int n, const int32_t *d_levels,
                          const int32_t *d_entropy_bits, uint8_t *d_states, hvx_coeff_bits *d_out);
+
+/* ---------------------------------------------------------------------------------------
+ * Intra (hvx_types.h hvx_intra_job).  d_rec = sample (0,0) of the 8-bit plane holding the
+ * reconstructed neighbours (any stride; only samples of available units are read), d_org the
+ * original with the same stride.  hvx_intra_pred_batch writes job i's (1<<log2_size)^2
+ * prediction of job.mode at d_pred + d_pred_off[i] (row-major), and, when d_ref_out is not NULL,
+ * its unfiltered and filtered reference borders (2 x 257 int16 per job, hvx_types.h layout; the
+ * filtered one is zero for chroma).  hvx_intra_search_batch runs the first pass of luma PU jobs
+ * (rates from ctx_state / frac_bits with d_entropy_bits = ContextModel::m_entropyBits, 128
+ * int32).  A job with an out-of-range size, channel or unit is skipped (its output untouched).
+ * ------------------------------------------------------------------------------------- */
+int hvx_intra_pred_batch(hvx_ctx *ctx, const uint8_t *d_rec, int stride, const hvx_intra_job *d_jobs, int n,
+                         uint8_t *d_pred, const int64_t *d_pred_off, int16_t *d_ref_out);
+int hvx_intra_search_batch(hvx_ctx *ctx, const uint8_t *d_org, const uint8_t *d_rec, int stride,
+                           const hvx_intra_job *d_jobs, int n, const int32_t *d_entropy_bits,
+                           hvx_intra_search_result *d_out);
 
 /* ---------------------------------------------------------------------------------------
  * CTU analysis pass over a whole picture (hvx_types.h): d_cur = sample (0,0) of the current

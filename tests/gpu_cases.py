@@ -407,3 +407,174 @@ def check_coeff_bits_random(seed, n):
         assert got == (fb, rice, ns), (i, descs[i], got, (fb, rice, ns))
         np.testing.assert_array_equal(st_gpu[i], st, err_msg=f"TU {i}")
     return True
+
+
+# ----------------------------------------------------------------------------------------- intra
+INTRA_TILE = 144  # a block at (8, 8) of its tile: above-right / below-left reach 8 + 128
+
+
+def intra_planes(n_tiles, seed):
+    """org + rec planes (random bytes, HVX_PLANE_MARGIN border) holding n_tiles INTRA_TILE tiles."""
+    g = int(np.ceil(np.sqrt(max(n_tiles, 1))))
+    W = H = g * INTRA_TILE
+    rng = np.random.default_rng(seed)
+    M = _abi.PLANE_MARGIN
+    org = rng.integers(0, 256, (H + 2 * M, W + 2 * M), dtype=np.uint8)
+    rec = rng.integers(0, 256, (H + 2 * M, W + 2 * M), dtype=np.uint8)
+    return org, rec, g, W
+
+
+def intra_tile_origin(i, g):
+    M = _abi.PLANE_MARGIN
+    return M + (i // g) * INTRA_TILE + 8, M + (i % g) * INTRA_TILE + 8  # (row, col) in the padded plane
+
+
+def put_border(rec, r, c, n, raw):
+    """write border-layout samples (corner, above row, left column) around the block at (r, c)."""
+    raw = np.asarray(raw, np.int64) & 0xFF
+    rec[r - 1, c - 1] = raw[0]
+    rec[r - 1, c:c + 2 * n] = raw[1:2 * n + 1]
+    rec[r:r + 2 * n, c - 1] = raw[2 * n + 1:4 * n + 1]
+
+
+def run_intra_pred(org_or_none, rec, W, jobs):
+    """hvx_intra_pred_batch over `jobs` (structured INTRA_JOB, x/y relative to the plane origin)
+    -> (list of n x n predictions, ref borders [n, 2, 257])."""
+    torch = _torch()
+    n = len(jobs)
+    sizes = [1 << int(j["log2_size"]) for j in jobs]
+    off = np.concatenate([[0], np.cumsum([s * s for s in sizes])]).astype(np.int64)
+    rec_t = torch.from_numpy(rec).cuda()
+    jobs_t = hvx.to_device(jobs)
+    off_t = torch.from_numpy(off[:-1].copy()).cuda()
+    pred_t = torch.zeros(int(off[-1]), dtype=torch.uint8, device="cuda")
+    ref_t = torch.zeros(n * 2 * 257, dtype=torch.int16, device="cuda")
+    stride = rec.shape[1]
+    hvx.intra_pred_batch(hvx.plane_origin_ptr(rec_t, W), stride, jobs_t, n, pred_t, off_t, ref_t)
+    torch.cuda.synchronize()
+    pred = pred_t.cpu().numpy()
+    preds = [pred[off[i]:off[i + 1]].reshape(sizes[i], sizes[i]) for i in range(n)]
+    return preds, ref_t.cpu().numpy().reshape(n, 2, 257)
+
+
+def run_intra_search(org, rec, W, jobs):
+    torch = _torch()
+    n = len(jobs)
+    org_t, rec_t = torch.from_numpy(org).cuda(), torch.from_numpy(rec).cuda()
+    jobs_t = hvx.to_device(jobs)
+    eb_t = torch.from_numpy(_abi.load_entropy_bits().copy()).cuda()
+    out_t = torch.zeros(n * _abi.INTRA_RESULT.itemsize, dtype=torch.uint8, device="cuda")
+    hvx.intra_search_batch(hvx.plane_origin_ptr(org_t, W), hvx.plane_origin_ptr(rec_t, W), org.shape[1], jobs_t, n,
+                           eb_t, out_t)
+    torch.cuda.synchronize()
+    return hvx.from_device(out_t, _abi.INTRA_RESULT)
+
+
+def check_intra_ref_golden():
+    """initIntraPatternChType goldens through hvx_intra_pred_batch's border output: the raw samples
+    placed around each block (unavailable positions hold random bytes, which must not leak)."""
+    from tests import golden_cases as gc
+    cases = gc.intra_ref_cases(gc.load("intra.bin"))
+    org, rec, g, W = intra_planes(len(cases), 21)
+    M = _abi.PLANE_MARGIN
+    jobs = np.zeros(len(cases), _abi.INTRA_JOB)
+    for i, (n, luma, ul, _f, raw, flags, _u, _ff) in enumerate(cases):
+        r, c = intra_tile_origin(i, g)
+        put_border(rec, r, c, n, raw)
+        jobs[i]["x"], jobs[i]["y"] = c - M, r - M
+        jobs[i]["log2_size"], jobs[i]["ch_type"], jobs[i]["unit_log2"] = n.bit_length() - 1, 0 if luma else 1, ul
+        jobs[i]["avail"] = oracle.avail_words(flags)
+        jobs[i]["flags"] = _abi.INTRA_STRONG
+        jobs[i]["mode"] = 1
+    _, refs = run_intra_pred(None, rec, W, jobs)
+    for i, (n, luma, _ul, filt, _raw, _fl, unf, exp_filt) in enumerate(cases):
+        np.testing.assert_array_equal(refs[i, 0, :4 * n + 1], unf, err_msg=f"unfiltered border, record {i}")
+        if filt and luma:
+            np.testing.assert_array_equal(refs[i, 1, :4 * n + 1], exp_filt, err_msg=f"filtered border, record {i}")
+    return len(cases)
+
+
+def check_intra_first_pass_golden():
+    """estIntraPredLumaQT first-pass goldens through hvx_intra_search_batch."""
+    from tests import golden_cases as gc
+    cases = gc.intra_fp_cases(gc.load("intra.bin"))
+    org, rec, g, W = intra_planes(len(cases), 22)
+    M = _abi.PLANE_MARGIN
+    jobs = np.zeros(len(cases), _abi.INTRA_JOB)
+    for i, (job, o, raw, _exp) in enumerate(cases):
+        n = 1 << int(job["log2_size"])
+        r, c = intra_tile_origin(i, g)
+        org[r:r + n, c:c + n] = np.asarray(o).reshape(n, n)
+        put_border(rec, r, c, n, raw)
+        jobs[i] = job
+        jobs[i]["x"], jobs[i]["y"] = c - M, r - M
+    res = run_intra_search(org, rec, W, jobs)
+    bad = [i for i, (_j, _o, _r, exp) in enumerate(cases) if not gc.intra_fp_matches(res[i], exp)]
+    assert not bad, (len(bad), bad[:5])
+    return len(cases)
+
+
+def random_intra_jobs(rng, n_jobs, g):
+    """random luma/chroma blocks of every size with random neighbour availability (incl. none/all)."""
+    M = _abi.PLANE_MARGIN
+    jobs = np.zeros(n_jobs, _abi.INTRA_JOB)
+    for i in range(n_jobs):
+        ch = int(rng.integers(0, 2))
+        log2 = int(rng.integers(2, 6 if ch else 7))
+        ul = 1 if ch else 2
+        nunits = ((4 << log2) >> ul) + 1
+        kind = int(rng.integers(0, 4))
+        flags = np.zeros(nunits, np.uint8) if kind == 0 else np.ones(nunits, np.uint8) if kind == 1 else \
+            (rng.random(nunits) < (0.3 if kind == 2 else 0.8)).astype(np.uint8)
+        r, c = intra_tile_origin(i, g)
+        jobs[i]["x"], jobs[i]["y"], jobs[i]["log2_size"], jobs[i]["ch_type"] = c - M, r - M, log2, ch
+        jobs[i]["unit_log2"], jobs[i]["avail"] = ul, oracle.avail_words(flags)
+        jobs[i]["mode"] = int(rng.integers(0, 35))
+        jobs[i]["flags"] = int(rng.integers(0, 4))
+        jobs[i]["left_dir"], jobs[i]["above_dir"] = int(rng.integers(0, 35)), int(rng.integers(0, 35))
+        jobs[i]["ctx_state"], jobs[i]["frac_bits"] = int(rng.integers(0, 126)), int(rng.integers(0, 32768))
+        jobs[i]["sqrt_lambda"] = float(rng.uniform(2.0, 40.0))
+    return jobs
+
+
+def _raw_border(plane, r, c, n):
+    return np.concatenate([[plane[r - 1, c - 1]], plane[r - 1, c:c + 2 * n], plane[r:r + 2 * n, c - 1]]).astype(np.int16)
+
+
+def _flags_of(job):
+    n = 1 << int(job["log2_size"])
+    nunits = ((4 * n) >> int(job["unit_log2"])) + 1
+    a = job["avail"]
+    return np.array([(int(a[i >> 5]) >> (i & 31)) & 1 for i in range(nunits)], np.uint8)
+
+
+def check_intra_random(seed, n_jobs):
+    """random jobs: borders + prediction (hvx_intra_pred_batch) and the first pass
+    (hvx_intra_search_batch, luma jobs) vs the oracle, bit-exact."""
+    rng = np.random.default_rng(seed)
+    org, rec, g, W = intra_planes(n_jobs, seed)
+    jobs = random_intra_jobs(rng, n_jobs, g)
+    preds, refs = run_intra_pred(None, rec, W, jobs)
+    luma = np.nonzero(jobs["ch_type"] == 0)[0]
+    res = run_intra_search(org, rec, W, jobs[luma])
+    eb = _abi.load_entropy_bits()
+    M = _abi.PLANE_MARGIN
+    for i, j in enumerate(jobs):
+        n, is_luma = 1 << int(j["log2_size"]), int(j["ch_type"]) == 0
+        r, c = int(j["y"]) + M, int(j["x"]) + M
+        raw = _raw_border(rec, r, c, n)
+        unf = oracle.intra_fill(raw, _flags_of(j), n, int(j["unit_log2"]))
+        np.testing.assert_array_equal(refs[i, 0, :4 * n + 1], unf, err_msg=f"job {i}")
+        filt = oracle.intra_filter(unf, n, is_luma, bool(j["flags"] & _abi.INTRA_STRONG)) if is_luma else unf
+        if is_luma:
+            np.testing.assert_array_equal(refs[i, 1, :4 * n + 1], filt, err_msg=f"job {i}")
+        m = int(j["mode"])
+        exp = oracle.intra_pred(filt if oracle.intra_use_filter(m, n, is_luma) else unf, n, is_luma, m)
+        np.testing.assert_array_equal(preds[i], exp, err_msg=f"job {i} mode {m} n {n}")
+    for k, i in enumerate(luma):
+        j = jobs[i]
+        n = 1 << int(j["log2_size"])
+        r, c = int(j["y"]) + M, int(j["x"]) + M
+        exp = oracle.intra_search(org[r:r + n, c:c + n], _raw_border(rec, r, c, n), j, eb)
+        assert res[k].tobytes() == exp.tobytes(), (i, res[k], exp)
+    return n_jobs, len(luma)

@@ -116,3 +116,23 @@ def test_oracle_ctu_decide_tree():
         M = _abi.PLANE_MARGIN
         diff = rec[M:M + H, M:M + W][ys, xs].astype(float) - cur[M:M + H, M:M + W][ys, xs]
         assert 10 * np.log10(255 ** 2 / max(np.mean(diff ** 2), 1e-9)) > 20
+
+
+def test_intra_struct_layouts_match_c():
+    prog = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "hvx.h"
+int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(hvx_intra_job), offsetof(hvx_intra_job, avail),
+ offsetof(hvx_intra_job, ctx_state), offsetof(hvx_intra_job, sqrt_lambda), sizeof(hvx_intra_search_result),
+ offsetof(hvx_intra_search_result, satd), offsetof(hvx_intra_search_result, mode_bits),
+ offsetof(hvx_intra_search_result, n_cand), offsetof(hvx_intra_search_result, cand)); return 0;}
+"""
+    tmp = "/tmp/hvx_intra_layout_check"
+    with open(tmp + ".c", "w") as f:
+        f.write(prog)
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), tmp + ".c", "-o", tmp])
+    vals = [int(x) for x in subprocess.check_output([tmp]).split()]
+    J, R = _abi.INTRA_JOB, _abi.INTRA_RESULT
+    assert vals == [J.itemsize, J.fields["avail"][1], J.fields["ctx_state"][1], J.fields["sqrt_lambda"][1], R.itemsize,
+                    R.fields["satd"][1], R.fields["mode_bits"][1], R.fields["n_cand"][1], R.fields["cand"][1]]

@@ -218,3 +218,20 @@ def test_coeff_bits_random_gpu(torch):
     # random levels (sparse, dense, large escapes; every size / scan / channel / transform skip,
     # persistent Rice adaptation on and off) and random context states vs the oracle
     assert gpu_cases.check_coeff_bits_random(seed=23, n=700)
+
+
+def test_intra_reference_samples_golden_gpu(torch):
+    # initIntraPatternChType: 1188 captured reference borders (unfiltered + smoothed), every size
+    # and availability pattern; unavailable neighbour positions hold random bytes
+    assert gpu_cases.check_intra_ref_golden() == 1188
+
+
+def test_intra_first_pass_golden_gpu(torch):
+    # estIntraPredLumaQT's first pass: 642 captured PUs (SATD of 35 modes, rates, ranking, MPMs)
+    assert gpu_cases.check_intra_first_pass_golden() == 642
+
+
+def test_intra_random_gpu(torch):
+    # random luma/chroma blocks 4..64, random availability (none / all / sparse / dense), every mode
+    n, n_luma = gpu_cases.check_intra_random(seed=31, n_jobs=600)
+    assert n == 600 and n_luma > 200

@@ -18,6 +18,7 @@
 #include "hvx_estbit.hpp"
 #include "hvx_mc.hpp"
 #include "hvx_cabac.hpp"
+#include "hvx_intra.hpp"
 
 struct hvx_ctx {
   int device = 0;
@@ -463,6 +464,27 @@ int hvx_mc_batch(hvx_ctx *ctx, const int16_t *const *d_planes, int luma_stride, 
   if (!n) return HVX_OK;
   hipLaunchKernelGGL(k_mc, dim3(n), dim3(256), 0, ctx->stream, d_planes, luma_stride, chroma_stride, d_jobs, n, d_dst);
   return launched("k_mc");
+}
+
+int hvx_intra_pred_batch(hvx_ctx *ctx, const uint8_t *d_rec, int stride, const hvx_intra_job *d_jobs, int n,
+                         uint8_t *d_pred, const int64_t *d_pred_off, int16_t *d_ref_out) {
+  if (!ctx || n < 0 || stride <= 0 || (n && (!d_rec || !d_jobs || !d_pred || !d_pred_off)))
+    return fail(HVX_E_INVALID, "hvx_intra_pred_batch: bad args");
+  if (!n) return HVX_OK;
+  hipLaunchKernelGGL(k_intra_pred, dim3(n), dim3(64), 0, ctx->stream, d_rec, stride, d_jobs, n, d_pred, d_pred_off,
+                     d_ref_out);
+  return launched("k_intra_pred");
+}
+
+int hvx_intra_search_batch(hvx_ctx *ctx, const uint8_t *d_org, const uint8_t *d_rec, int stride,
+                           const hvx_intra_job *d_jobs, int n, const int32_t *d_entropy_bits,
+                           hvx_intra_search_result *d_out) {
+  if (!ctx || n < 0 || stride <= 0 || (n && (!d_org || !d_rec || !d_jobs || !d_entropy_bits || !d_out)))
+    return fail(HVX_E_INVALID, "hvx_intra_search_batch: bad args");
+  if (!n) return HVX_OK;
+  hipLaunchKernelGGL(k_intra_search, dim3(n), dim3(64), 0, ctx->stream, d_org, d_rec, stride, d_jobs, n,
+                     d_entropy_bits, d_out);
+  return launched("k_intra_search");
 }
 
 int hvx_alloc(hvx_ctx *ctx, size_t bytes, void **d_out) {

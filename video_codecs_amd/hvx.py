@@ -46,7 +46,8 @@ def lib():
             "hvx_ctu_encode": [P, P, P, I, P, P, P, P, P, ctypes.c_size_t, P, P, P],
             "hvx_set_timing": [P, I], "hvx_phase_times": [P, ctypes.POINTER(ctypes.c_double), I, I],
             "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
-            "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
+            "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P],
+            "hvx_intra_pred_batch": [P, P, I, P, I, P, P, P], "hvx_intra_search_batch": [P, P, P, I, P, I, P, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
             "hvx_free": [P, P], "hvx_upload": [P, P, P, ctypes.c_size_t], "hvx_download": [P, P, P, ctypes.c_size_t],
         }.items():
             f = getattr(L, name)
@@ -191,6 +192,18 @@ def mc_batch(plane_ptrs_dev, luma_stride, chroma_stride, jobs_dev, n, dst):
 def stvssim_batch(hist_org_ptrs, hist_rec_ptrs, dirs, jobs_dev, n, out4):
     _check(lib().hvx_stvssim_batch(context(), _ptr(hist_org_ptrs), _ptr(hist_rec_ptrs), _ptr(dirs), _ptr(jobs_dev), n,
                                    _ptr(out4)), "hvx_stvssim_batch")
+
+
+def intra_pred_batch(rec_origin, stride, jobs_dev, n, pred, off_dev, ref_out=None):
+    """hvx_intra_pred_batch: rec_origin = device address of sample (0,0) of the reconstructed plane."""
+    _check(lib().hvx_intra_pred_batch(context(), ctypes.c_void_p(rec_origin), int(stride), _ptr(jobs_dev), n,
+                                      _ptr(pred), _ptr(off_dev), _ptr(ref_out)), "hvx_intra_pred_batch")
+
+
+def intra_search_batch(org_origin, rec_origin, stride, jobs_dev, n, entropy_dev, out_dev):
+    """hvx_intra_search_batch: estIntraPredLumaQT's first pass, one luma PU per job."""
+    _check(lib().hvx_intra_search_batch(context(), ctypes.c_void_p(org_origin), ctypes.c_void_p(rec_origin), int(stride),
+                                        _ptr(jobs_dev), n, _ptr(entropy_dev), _ptr(out_dev)), "hvx_intra_search_batch")
 
 
 def plane_from_pel(pel, pel_stride, width, height, plane):
