@@ -39,6 +39,7 @@ def parse():
     p.add_argument("--qp", type=int, default=32)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-intra", action="store_true", help="skip the intra first-pass side measurement")
     return p.parse_args()
 
 
@@ -193,9 +194,43 @@ def main():
             out["dpb_gather_ok"] = dpb_ok
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(planes, an, gpu_res, gpu_dec, gpu_rec, args)
+        if not args.no_intra:
+            out["intra_first_pass"] = intra_measure(cur_t, ref_t[0], W, H, float(an.params["lambda"]), args.steps)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def intra_measure(cur_t, rec_t, W, H, lam, steps):
+    """Side measurement (not the headline): hvx_intra_search_batch -- estIntraPredLumaQT's first
+    pass -- over every luma PU of the picture at all five PU sizes (341 PUs per CTU,
+    video_codecs_amd/intra_grid.py), the current picture as the original and a reference picture
+    as the reconstructed neighbours.  Wall time per picture after a warmup launch."""
+    import math
+    import torch
+    from video_codecs_amd import _abi, hvx, intra_grid
+    jobs = intra_grid.picture_first_pass_jobs(W, H, math.sqrt(lam))
+    dev = {l: hvx.to_device(j) for l, j in jobs.items()}
+    total = sum(len(j) for j in jobs.values())
+    out = torch.empty(max(len(j) for j in jobs.values()) * _abi.INTRA_RESULT.itemsize, dtype=torch.uint8, device="cuda")
+    eb = torch.from_numpy(_abi.load_entropy_bits().copy()).cuda()
+    org, rec = hvx.plane_origin_ptr(cur_t, W), hvx.plane_origin_ptr(rec_t, W)
+    stride = cur_t.shape[1]
+
+    def one():
+        for l in jobs:
+            hvx.intra_search_batch(org, rec, stride, dev[l], len(jobs[l]), eb, out)
+    one()
+    hvx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    hvx.sync()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    return {"kernel": "k_intra_search", "pus_per_picture": total,
+            "pus_by_size": {str(1 << l): len(j) for l, j in jobs.items()}, "ms_per_picture": round(ms, 3),
+            "pus_per_s": round(total / ms * 1e3, 1),
+            "ctus_per_s": round(((W + 63) // 64) * ((H + 63) // 64) / ms * 1e3, 1)}
 
 
 def cpu_baseline(planes, an, gpu_res, gpu_dec, gpu_rec, args):

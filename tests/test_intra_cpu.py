@@ -1,0 +1,35 @@
+"""Host logic of the intra side workload (video_codecs_amd/intra_grid.py): HM's neighbour
+availability (TComPattern.cpp:571-749) for a uniformly tiled picture."""
+import numpy as np
+
+from video_codecs_amd import intra_grid
+
+
+def _flags(job):
+    n = 1 << int(job["log2_size"])
+    return [(int(job["avail"][i >> 5]) >> (i & 31)) & 1 for i in range(2 * (n // 2) + 1)]
+
+
+def test_first_pu_has_no_neighbours():
+    for l, jobs in intra_grid.picture_first_pass_jobs(256, 192, 10.0).items():
+        assert not jobs[0]["avail"].any(), l
+
+
+def test_zorder_availability_4x4():
+    j = intra_grid.first_pass_jobs(128, 64, 2, 10.0, 4, 0)
+    per_row = 128 // 4
+    at = lambda x, y: j[(y // 4) * per_row + x // 4]  # noqa: E731
+    # flags: [below-left, left, above-left, above, above-right]
+    assert _flags(at(4, 0)) == [0, 1, 0, 0, 0]   # below-left (0,4) is later in z-order
+    assert _flags(at(8, 0)) == [1, 1, 0, 0, 0]   # (4,4) precedes (8,0) in z-order
+    assert _flags(at(4, 4)) == [0, 1, 1, 1, 0]   # above-right (8,0) comes after (4,4)
+    assert _flags(at(64, 0)) == [1, 1, 0, 0, 0]  # left CTU is complete
+    assert _flags(at(60, 60)) == [0, 1, 1, 1, 0]  # below-left is the next CTU row
+
+
+def test_ctu_boundaries_64x64():
+    j = intra_grid.first_pass_jobs(192, 128, 6, 10.0, 4, 0)
+    f = [_flags(x) for x in j]
+    assert f[1] == [0] * 16 + [1] * 16 + [0] * 33                 # left CTU only
+    assert f[4] == [0] * 16 + [1] * 16 + [1] + [1] * 16 + [1] * 16  # CTU (1,1): left, corner, above, above-right
+    assert f[5] == [0] * 16 + [1] * 16 + [1] + [1] * 16 + [0] * 16  # right edge: no above-right
