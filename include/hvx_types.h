@@ -196,6 +196,20 @@ typedef struct hvx_intra_search_result {
   uint8_t pad_[4];
 } hvx_intra_search_result;
 
+/* Deblocking of a reconstructed picture (TComLoopFilter::loopFilterPic,
+ * TComLoopFilter.cpp:130): all vertical edges, then all horizontal edges, on the 8x8 grid (luma)
+ * and the 16x16-luma grid (4:2:0 chroma, bs 2 only).  Edge inputs are per 4x4 luma unit,
+ * raster over (pic_w/4) x (pic_h/4): bs_ver = boundary strength 0..2 of the unit's LEFT edge (read
+ * where x % 8 == 0), bs_hor = of its TOP edge (read where y % 8 == 0) -- xGetBoundaryStrengthSingle
+ * (:417) values, 0 where no TU/PU edge or at the picture border; qp = the unit's QpY
+ * (TComDataCU::getQP).  8-bit video, no PCM / transquant-bypass units. */
+typedef struct hvx_deblock_params {
+  int32_t pic_w, pic_h;            /* luma samples, multiples of 8 */
+  int32_t beta_offset_div2, tc_offset_div2;  /* slice_beta_offset_div2, slice_tc_offset_div2 */
+  int32_t cb_qp_offset, cr_qp_offset;        /* pps_cb_qp_offset, pps_cr_qp_offset */
+  int32_t flags, pad_;             /* reserved, 0 */
+} hvx_deblock_params;
+
 /* One PU's motion compensation (TComPrediction::motionCompensation for one partition, no
  * weighted prediction; TComPrediction.cpp:517-722).  Lists with ref >= 0 are used: both ->
  * bi-prediction (14-bit intermediates + TComYuv::addAvg), unless HVX_MC_B_SLICE is set and the

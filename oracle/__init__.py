@@ -366,3 +366,20 @@ def intra_search(org, raw, job, entropy_bits):
     out = np.zeros(1, _abi.INTRA_RESULT)
     _intra_lib().hvxo_intra_search(_p(o), _p(r), _p(j), _p(eb), _p(out))
     return out[0]
+
+
+# ------------------------------------------------------------------------------------- deblocking
+def deblock(y, cb, cr, bs_ver, bs_hor, qp, params):
+    """hvxo_deblock on copies of the planes (2-D uint8 arrays, any strides): returns (y, cb, cr)."""
+    L = lib()
+    if not getattr(L, "_dbk_ready", False):
+        L.hvxo_deblock.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L._dbk_ready = True
+    y, cb, cr = (np.array(a, dtype=np.uint8, copy=True, order="C") for a in (y, cb, cr))
+    assert cb.shape == cr.shape
+    bv, bh = _c(bs_ver, np.uint8), _c(bs_hor, np.uint8)
+    q = _c(qp, np.int8)
+    p = np.ascontiguousarray(params)
+    L.hvxo_deblock(_p(y), y.shape[1], _p(cb), _p(cr), cb.shape[1], _p(bv), _p(bh), _p(q), _p(p))
+    return y, cb, cr

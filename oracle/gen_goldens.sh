@@ -53,4 +53,17 @@ icap "$TMP/in_i.bin"   $CFG/encoder_intra_main.cfg      "$TMP/rand.yuv"   1 32
 icap "$TMP/in_i22.bin" $CFG/encoder_intra_main.cfg      "$TMP/smooth.yuv" 1 22
 icap "$TMP/in_p.bin"   $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth.yuv" 3 27
 python3 oracle/merge_goldens.py tests/golden/intra.bin "$TMP"/in_i.bin "$TMP"/in_i22.bin "$TMP"/in_p.bin
+# deblocking: TComLoopFilter::loopFilterPic with the boundary strengths it uses (oracle/deblock_capture.cpp)
+dcap() {  # dcap <out.bin> <cfg> <yuv> <frames> <qp> [extra args...]
+  local out=$1 cfg=$2 yuv=$3 frames=$4 qp=$5; shift 5
+  HVX_CAPTURE=$out $ORC/TAppEncoder_dbkcap -c "$cfg" -i "$yuv" -wdt 416 -hgt 240 -fr 30 -f "$frames" -q "$qp" \
+    -b "$TMP/str.bin" -o "$TMP/rec.yuv" "$@" > "$TMP/log.txt"
+}
+dcap "$TMP/d_i.bin"   $CFG/encoder_intra_main.cfg      "$TMP/smooth.yuv" 1 37
+dcap "$TMP/d_p.bin"   $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth.yuv" 3 32
+dcap "$TMP/d_b.bin"   tests/hm_seam/ldb.cfg            "$TMP/smooth.yuv" 3 27
+dcap "$TMP/d_pr.bin"  $CFG/encoder_lowdelay_P_main.cfg "$TMP/rand.yuv"   2 32
+dcap "$TMP/d_off.bin" $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth.yuv" 2 30 --LoopFilterOffsetInPPS=1 \
+  --LoopFilterBetaOffset_div2=3 --LoopFilterTcOffset_div2=-2 --CbQpOffset=4 --CrQpOffset=-3
+python3 oracle/merge_goldens.py tests/golden/deblock.bin "$TMP"/d_i.bin "$TMP"/d_p.bin "$TMP"/d_b.bin "$TMP"/d_pr.bin "$TMP"/d_off.bin
 ls -la tests/golden

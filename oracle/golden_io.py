@@ -6,7 +6,7 @@ import struct
 
 import numpy as np
 
-_DT = {"u8": np.uint8, "i16": np.int16, "i32": np.int32, "u32": np.uint32, "i64": np.int64,
+_DT = {"u8": np.uint8, "i8": np.int8, "i16": np.int16, "i32": np.int32, "u32": np.uint32, "i64": np.int64,
        "f32": np.float32, "f64": np.float64}
 
 

@@ -2177,3 +2177,108 @@ void hvxo_intra_search(const uint8_t *org, const int16_t *raw, const hvx_intra_j
   r->n_cand = (uint8_t)num;
   for (int i = 0; i < num; i++) r->cand[i] = (uint8_t)list[i];
 }
+
+/* ============================================================================================
+ * Deblocking: TComLoopFilter::loopFilterPic (TComLoopFilter.cpp:130) on
+ * given boundary strengths.  Vertical edges of the whole picture first (luma + chroma), then
+ * horizontal edges on that result -- the reference's two CTU sweeps (:132-154); inside one sweep
+ * the edges are 8 samples apart and touch at most 4 samples on each side, so their order is free.
+ * ========================================================================================== */
+static const uint8_t dbk_tc[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                   2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
+static const uint8_t dbk_beta[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
+                                     8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32,
+                                     34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};
+/* g_aucChromaScale[CHROMA_420] (TComRom.cpp:536) */
+static const uint8_t dbk_cscale[58] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 19,
+                                       20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 33, 33, 34, 34, 35, 35,
+                                       36, 36, 37, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51};
+static int clip3i(int lo, int hi, int v) { return v < lo ? lo : v > hi ? hi : v; }
+
+/* xEdgeFilterLuma's 4-line segment (:605-675) with xCalcDP/DQ (:948), xUseStrongFiltering (:936)
+ * and xPelFilterLuma (:833); s = sample q0 of line 0, step = to the next line, off = across */
+static void dbk_luma_seg(uint8_t *s, int step, int off, int bs, int qp, const hvx_deblock_params *p) {
+  const int tc = dbk_tc[clip3i(0, 53, qp + 2 * (bs - 1) + 2 * p->tc_offset_div2)];
+  const int beta = dbk_beta[clip3i(0, 51, qp + 2 * p->beta_offset_div2)];
+  const int side = (beta + (beta >> 1)) >> 3, thr_cut = tc * 10;
+#define PX(l, i) ((int)s[(l) * step + (i) * off])
+  const int dp0 = abs(PX(0, -3) - 2 * PX(0, -2) + PX(0, -1)), dq0 = abs(PX(0, 0) - 2 * PX(0, 1) + PX(0, 2));
+  const int dp3 = abs(PX(3, -3) - 2 * PX(3, -2) + PX(3, -1)), dq3 = abs(PX(3, 0) - 2 * PX(3, 1) + PX(3, 2));
+  const int d0 = dp0 + dq0, d3 = dp3 + dq3, dp = dp0 + dp3, dq = dq0 + dq3, d = d0 + d3;
+  if (d >= beta) return;
+  const int fp = dp < side, fq = dq < side;
+  int sw = 1;
+  for (int l = 0; l < 4; l += 3) {
+    const int dl = 2 * (l ? d3 : d0);
+    const int ds = abs(PX(l, -4) - PX(l, -1)) + abs(PX(l, 3) - PX(l, 0));
+    sw &= ds < (beta >> 3) && dl < (beta >> 2) && abs(PX(l, -1) - PX(l, 0)) < ((tc * 5 + 1) >> 1);
+  }
+  for (int l = 0; l < 4; l++) {
+    uint8_t *q = s + l * step;
+    const int m0 = q[-4 * off], m1 = q[-3 * off], m2 = q[-2 * off], m3 = q[-off], m4 = q[0], m5 = q[off],
+              m6 = q[2 * off], m7 = q[3 * off];
+    if (sw) {
+      q[-off] = (uint8_t)clip3i(m3 - 2 * tc, m3 + 2 * tc, (m1 + 2 * m2 + 2 * m3 + 2 * m4 + m5 + 4) >> 3);
+      q[0] = (uint8_t)clip3i(m4 - 2 * tc, m4 + 2 * tc, (m2 + 2 * m3 + 2 * m4 + 2 * m5 + m6 + 4) >> 3);
+      q[-2 * off] = (uint8_t)clip3i(m2 - 2 * tc, m2 + 2 * tc, (m1 + m2 + m3 + m4 + 2) >> 2);
+      q[off] = (uint8_t)clip3i(m5 - 2 * tc, m5 + 2 * tc, (m3 + m4 + m5 + m6 + 2) >> 2);
+      q[-3 * off] = (uint8_t)clip3i(m1 - 2 * tc, m1 + 2 * tc, (2 * m0 + 3 * m1 + m2 + m3 + m4 + 4) >> 3);
+      q[2 * off] = (uint8_t)clip3i(m6 - 2 * tc, m6 + 2 * tc, (m3 + m4 + m5 + 3 * m6 + 2 * m7 + 4) >> 3);
+    } else {
+      int delta = (9 * (m4 - m3) - 3 * (m5 - m2) + 8) >> 4;
+      if (abs(delta) < thr_cut) {
+        delta = clip3i(-tc, tc, delta);
+        q[-off] = (uint8_t)clip3i(0, 255, m3 + delta);
+        q[0] = (uint8_t)clip3i(0, 255, m4 - delta);
+        const int tc2 = tc >> 1;
+        if (fp) q[-2 * off] = (uint8_t)clip3i(0, 255, m2 + clip3i(-tc2, tc2, (((m1 + m3 + 1) >> 1) - m2 + delta) >> 1));
+        if (fq) q[off] = (uint8_t)clip3i(0, 255, m5 + clip3i(-tc2, tc2, (((m6 + m4 + 1) >> 1) - m5 - delta) >> 1));
+      }
+    }
+  }
+#undef PX
+}
+
+/* xEdgeFilterChroma's per-unit part (:750-815) with xPelFilterChroma (:904): 2 lines, bs 2 */
+static void dbk_chroma_seg(uint8_t *s, int step, int off, int bs, int qp_avg, int qp_offset,
+                           const hvx_deblock_params *p) {
+  int qp = qp_avg + qp_offset;
+  if (qp >= 58) qp -= 6;                  /* :791-796, 4:2:0 */
+  else if (qp >= 0) qp = dbk_cscale[qp];  /* getScaledChromaQP */
+  const int tc = dbk_tc[clip3i(0, 53, qp + 2 * (bs - 1) + 2 * p->tc_offset_div2)];
+  for (int l = 0; l < 2; l++) {
+    uint8_t *q = s + l * step;
+    const int m2 = q[-2 * off], m3 = q[-off], m4 = q[0], m5 = q[off];
+    const int delta = clip3i(-tc, tc, ((((m4 - m3) << 2) + m2 - m5 + 4) >> 3));
+    q[-off] = (uint8_t)clip3i(0, 255, m3 + delta);
+    q[0] = (uint8_t)clip3i(0, 255, m4 - delta);
+  }
+}
+
+void hvxo_deblock(uint8_t *y, int ys, uint8_t *cb, uint8_t *cr, int cs, const uint8_t *bs_ver, const uint8_t *bs_hor,
+                  const int8_t *qp, const hvx_deblock_params *p) {
+  const int uw = p->pic_w / 4, uh = p->pic_h / 4;
+  for (int dir = 0; dir < 2; dir++) {
+    const uint8_t *bsm = dir ? bs_hor : bs_ver;
+    for (int uy = 0; uy < uh; uy++)
+      for (int ux = 0; ux < uw; ux++) {
+        const int x = ux * 4, yy = uy * 4;
+        if ((dir ? yy : x) % 8 != 0 || (dir ? yy : x) == 0) continue;
+        const int bs = bsm[uy * uw + ux];
+        if (!bs) continue;
+        const int qq = qp[uy * uw + ux], qpp = dir ? qp[(uy - 1) * uw + ux] : qp[uy * uw + ux - 1];
+        const int avg = (qpp + qq + 1) >> 1;
+        if (dir == 0) dbk_luma_seg(y + yy * ys + x, ys, 1, bs, avg, p);
+        else dbk_luma_seg(y + yy * ys + x, 1, ys, bs, avg, p);
+        if (bs == 2 && (dir ? yy : x) % 16 == 0) {
+          const int cx = x / 2, cy = yy / 2;
+          for (int c = 0; c < 2; c++) {
+            uint8_t *pl = c ? cr : cb;
+            const int off = c ? p->cr_qp_offset : p->cb_qp_offset;
+            if (dir == 0) dbk_chroma_seg(pl + cy * cs + cx, cs, 1, bs, avg, off, p);
+            else dbk_chroma_seg(pl + cy * cs + cx, 1, cs, bs, avg, off, p);
+          }
+        }
+      }
+  }
+}

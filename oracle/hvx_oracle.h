@@ -102,6 +102,10 @@ void hvxo_intra_pred(const int16_t *border, int n, int is_luma, int mode, uint8_
 void hvxo_intra_search(const uint8_t *org, const int16_t *raw, const hvx_intra_job *j, const int32_t *eb,
                        hvx_intra_search_result *r);
 
+/* ---- deblocking: loopFilterPic on given BS / QP maps, planes in place ---- */
+void hvxo_deblock(uint8_t *y, int ys, uint8_t *cb, uint8_t *cr, int cs, const uint8_t *bs_ver, const uint8_t *bs_hor,
+                  const int8_t *qp, const hvx_deblock_params *p);
+
 /* tables (generated, HEVC spec values) */
 void hvxo_dct_matrix(int n, int16_t *m /* n*n, [k][x] */);
 const uint32_t *hvxo_scan(int grouped, int scan_type, int log2w, int log2h);

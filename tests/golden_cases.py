@@ -162,3 +162,25 @@ def intra_fp_matches(r, exp):
             and int(r["num_rd"]) == nrd and int(r["n_cand"]) == nc
             and list(r["cand"][:nc]) == list(exp["cand"])
             and np.array_equal(r["cand_cost"][:nrd], exp["cand_cost"]))
+
+
+# ------------------------------------------------------------------------------------ deblocking
+def deblock_cases(g):
+    """loopFilterPic records: (params, pre (y, cb, cr), post (y, cb, cr), bs_ver, bs_hor, qp)."""
+    out, po, pu = [], 0, 0
+    for m in g["meta"]:
+        w, h, beta, tc, cbo, cro, bypass = (int(v) for v in m)
+        assert bypass == 0
+        params = _abi.deblock_params(w, h, beta, tc, cbo, cro)
+        n = w * h + 2 * (w // 2) * (h // 2)
+        nu = (w // 4) * (h // 4)
+
+        def split(a):
+            cw, ch = w // 2, h // 2
+            return (a[:w * h].reshape(h, w), a[w * h:w * h + cw * ch].reshape(ch, cw), a[w * h + cw * ch:].reshape(ch, cw))
+        out.append((params, split(g["pre"][po:po + n]), split(g["post"][po:po + n]), g["bs_ver"][pu:pu + nu],
+                    g["bs_hor"][pu:pu + nu], g["qp"][pu:pu + nu]))
+        po += n
+        pu += nu
+    assert po == len(g["pre"]) and pu == len(g["qp"])
+    return out

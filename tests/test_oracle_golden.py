@@ -183,3 +183,15 @@ def test_intra_first_pass_golden():
         assert gc.intra_fp_matches(r, exp)
         sizes.add(int(job["log2_size"]))
     assert sizes == {2, 3, 4, 5, 6}
+
+
+def test_deblock_golden():
+    """loopFilterPic vs 9 reference pictures (intra, LDP, LDB, random-P, non-zero beta/tc/chroma
+    QP offsets): luma + chroma, bit-exact."""
+    cases = gc.deblock_cases(gc.load("deblock.bin"))
+    assert len(cases) == 9
+    for params, pre, post, bv, bh, qp in cases:
+        got = oracle.deblock(*pre, bv, bh, qp, params)
+        for c in range(3):
+            np.testing.assert_array_equal(got[c], post[c])
+    assert {1, 2} <= set(np.unique(np.concatenate([c[3] for c in cases])))

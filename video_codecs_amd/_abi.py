@@ -106,3 +106,15 @@ assert INTRA_JOB.itemsize == 64
 INTRA_RESULT = np.dtype([("cand_cost", "<f8", (8,)), ("satd", "<u4", (35,)), ("mode_bits", "u1", (35,)),
                          ("num_rd", "u1"), ("n_cand", "u1"), ("cand", "u1", (11,)), ("pad_", "u1", (4,))])
 assert INTRA_RESULT.itemsize == 256
+
+# hvx_deblock_params (hvx_types.h)
+DEBLOCK_PARAMS = np.dtype([("pic_w", "<i4"), ("pic_h", "<i4"), ("beta_offset_div2", "<i4"), ("tc_offset_div2", "<i4"),
+                           ("cb_qp_offset", "<i4"), ("cr_qp_offset", "<i4"), ("flags", "<i4"), ("pad_", "<i4")])
+assert DEBLOCK_PARAMS.itemsize == 32
+
+
+def deblock_params(w, h, beta_offset_div2=0, tc_offset_div2=0, cb_qp_offset=0, cr_qp_offset=0):
+    p = np.zeros(1, DEBLOCK_PARAMS)
+    p["pic_w"], p["pic_h"], p["beta_offset_div2"], p["tc_offset_div2"] = w, h, beta_offset_div2, tc_offset_div2
+    p["cb_qp_offset"], p["cr_qp_offset"] = cb_qp_offset, cr_qp_offset
+    return p
