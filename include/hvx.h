@@ -46,6 +46,8 @@
  *                         samples + smoothing) + predIntraAng (TComPrediction.cpp:455)
  *   hvx_intra_search_batch TEncSearch::estIntraPredLumaQT's first pass (TEncSearch.cpp:2244-2323):
  *                         35-mode Hadamard cost ranking + MPM candidates per luma PU
+ *   hvx_deblock           TComLoopFilter::loopFilterPic (TComLoopFilter.cpp:130, xEdgeFilterLuma :560,
+ *                         xEdgeFilterChroma :679) on given boundary strengths
  *   hvx_plane_from_pel    TComPicYuv int16 padded plane -> device 8-bit padded plane, with
  *                         TComPicYuv::extendPicBorder (TComPicYuv.cpp:197)
  */
@@ -247,6 +249,15 @@ int hvx_intra_pred_batch(hvx_ctx *ctx, const uint8_t *d_rec, int stride, const h
 int hvx_intra_search_batch(hvx_ctx *ctx, const uint8_t *d_org, const uint8_t *d_rec, int stride,
                            const hvx_intra_job *d_jobs, int n, const int32_t *d_entropy_bits,
                            hvx_intra_search_result *d_out);
+
+/* ---------------------------------------------------------------------------------------
+ * Deblocking in place (hvx_types.h hvx_deblock_params): d_y / d_cb / d_cr = sample (0,0) of the
+ * reconstructed 8-bit planes (4:2:0, any strides >= the plane widths), d_bs_ver / d_bs_hor /
+ * d_qp = (pic_w/4) x (pic_h/4) per-4x4-unit maps on the device.  Two launches on the context
+ * stream: all vertical edges, then all horizontal edges.
+ * ------------------------------------------------------------------------------------- */
+int hvx_deblock(hvx_ctx *ctx, uint8_t *d_y, int y_stride, uint8_t *d_cb, uint8_t *d_cr, int c_stride,
+                const uint8_t *d_bs_ver, const uint8_t *d_bs_hor, const int8_t *d_qp, const hvx_deblock_params *h_params);
 
 /* ---------------------------------------------------------------------------------------
  * CTU analysis pass over a whole picture (hvx_types.h): d_cur = sample (0,0) of the current

@@ -578,3 +578,68 @@ def check_intra_random(seed, n_jobs):
         exp = oracle.intra_search(org[r:r + n, c:c + n], _raw_border(rec, r, c, n), j, eb)
         assert res[k].tobytes() == exp.tobytes(), (i, res[k], exp)
     return n_jobs, len(luma)
+
+
+# ------------------------------------------------------------------------------------ deblocking
+def run_deblock(y, cb, cr, bs_ver, bs_hor, qp, params, margin=16):
+    """hvx_deblock on padded device copies of the planes (borders hold random bytes that must stay
+    untouched); returns the filtered (y, cb, cr) and whether every border byte survived."""
+    torch = _torch()
+    rng = np.random.default_rng(5)
+    outs, keep = [], True
+    pads = []
+    for a in (y, cb, cr):
+        pa = rng.integers(0, 256, (a.shape[0] + 2 * margin, a.shape[1] + 2 * margin), dtype=np.uint8)
+        pa[margin:-margin, margin:-margin] = a
+        pads.append(pa)
+    dev = [torch.from_numpy(pa.copy()).cuda() for pa in pads]
+    org = lambda t, w: t.data_ptr() + margin * (w + 2 * margin) + margin  # noqa: E731
+    hvx.deblock(org(dev[0], y.shape[1]), dev[0].shape[1], org(dev[1], cb.shape[1]), org(dev[2], cr.shape[1]),
+                dev[1].shape[1], hvx.to_device(np.asarray(bs_ver, np.uint8)), hvx.to_device(np.asarray(bs_hor, np.uint8)),
+                hvx.to_device(np.asarray(qp, np.int8)), params)
+    torch.cuda.synchronize()
+    for pa, d in zip(pads, dev):
+        got = d.cpu().numpy()
+        inner = got[margin:-margin, margin:-margin].copy()
+        got[margin:-margin, margin:-margin] = pa[margin:-margin, margin:-margin]
+        keep &= np.array_equal(got, pa)
+        outs.append(inner)
+    return outs, keep
+
+
+def check_deblock_golden():
+    cases = gc.deblock_cases(gc.load("deblock.bin"))
+    for k, (params, pre, post, bv, bh, qp) in enumerate(cases):
+        got, keep = run_deblock(*pre, bv, bh, qp, params)
+        assert keep, k
+        for c in range(3):
+            np.testing.assert_array_equal(got[c], post[c], err_msg=f"picture {k} plane {c}")
+    return len(cases)
+
+
+def check_deblock_random(seed, w=1920, h=1080):
+    """random pictures, BS maps (0/1/2 on the edge grid), QP maps 0..51 and offsets vs the oracle."""
+    rng = np.random.default_rng(seed)
+    h8 = h - h % 8
+    y = rng.integers(0, 256, (h8, w), dtype=np.uint8)
+    # smooth-ish content so the filters actually fire: blocks of a ramp plus small noise
+    base = (np.add.outer(np.arange(h8), np.arange(w)) // 3 % 256).astype(np.int32)
+    y = np.clip(base + rng.integers(-3, 4, base.shape) + (rng.integers(0, 2, base.shape) * (y % 8)), 0, 255).astype(np.uint8)
+    cb = (y[::2, ::2] // 2 + 64).astype(np.uint8)
+    cr = (255 - y[::2, ::2]).astype(np.uint8)
+    uw, uh = w // 4, h8 // 4
+    bs_ver = rng.integers(0, 3, (uh, uw)).astype(np.uint8)
+    bs_hor = rng.integers(0, 3, (uh, uw)).astype(np.uint8)
+    bs_ver[:, 1::2] = 0
+    bs_ver[:, 0] = 0
+    bs_hor[1::2, :] = 0
+    bs_hor[0, :] = 0
+    qp = rng.integers(0, 52, (uh, uw)).astype(np.int8)
+    params = _abi.deblock_params(w, h8, int(rng.integers(-6, 7)), int(rng.integers(-6, 7)), int(rng.integers(-12, 13)),
+                                 int(rng.integers(-12, 13)))
+    exp = oracle.deblock(y, cb, cr, bs_ver.ravel(), bs_hor.ravel(), qp.ravel(), params)
+    got, keep = run_deblock(y, cb, cr, bs_ver.ravel(), bs_hor.ravel(), qp.ravel(), params)
+    assert keep
+    for c in range(3):
+        np.testing.assert_array_equal(got[c], exp[c], err_msg=f"plane {c}")
+    return int((exp[0] != y).sum())

@@ -136,3 +136,35 @@ int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(hvx_intra_job)
     J, R = _abi.INTRA_JOB, _abi.INTRA_RESULT
     assert vals == [J.itemsize, J.fields["avail"][1], J.fields["ctx_state"][1], J.fields["sqrt_lambda"][1], R.itemsize,
                     R.fields["satd"][1], R.fields["mode_bits"][1], R.fields["n_cand"][1], R.fields["cand"][1]]
+
+
+def test_deblock_params_layout_matches_c():
+    prog = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "hvx.h"
+int main(){printf("%zu %zu %zu\n", sizeof(hvx_deblock_params), offsetof(hvx_deblock_params, cb_qp_offset),
+ offsetof(hvx_deblock_params, flags)); return 0;}
+"""
+    tmp = "/tmp/hvx_dbk_layout_check"
+    with open(tmp + ".c", "w") as f:
+        f.write(prog)
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), tmp + ".c", "-o", tmp])
+    vals = [int(x) for x in subprocess.check_output([tmp]).split()]
+    D = _abi.DEBLOCK_PARAMS
+    assert vals == [D.itemsize, D.fields["cb_qp_offset"][1], D.fields["flags"][1]]
+
+
+def test_oracle_deblock_random_smoke():
+    # the random-map recipe of the GPU test runs on the oracle alone (CPU): filters fire, borders fixed
+    import numpy as np
+    import oracle
+    rng = np.random.default_rng(1)
+    ramp = np.add.outer(np.arange(64), np.arange(64)) // 3
+    y = (ramp + 6 * ((np.arange(64)[None, :] // 8) % 2) + 6 * ((np.arange(64)[:, None] // 8) % 2)).astype(np.uint8)
+    cb, cr = y[::2, ::2].copy(), y[::2, ::2].copy()
+    bv = np.zeros((16, 16), np.uint8); bv[:, 2::2] = 2
+    bh = np.zeros((16, 16), np.uint8); bh[2::2, :] = 1
+    qp = np.full((16, 16), 37, np.int8)
+    out = oracle.deblock(y, cb, cr, bv.ravel(), bh.ravel(), qp.ravel(), _abi.deblock_params(64, 64))
+    assert (out[0] != y).any() and (out[1] != cb).any()

@@ -235,3 +235,13 @@ def test_intra_random_gpu(torch):
     # random luma/chroma blocks 4..64, random availability (none / all / sparse / dense), every mode
     n, n_luma = gpu_cases.check_intra_random(seed=31, n_jobs=600)
     assert n == 600 and n_luma > 200
+
+
+def test_deblock_golden_gpu(torch):
+    # loopFilterPic: 9 captured reference pictures (intra, LDP, LDB, random P, offsets), Y/Cb/Cr
+    assert gpu_cases.check_deblock_golden() == 9
+
+
+def test_deblock_random_gpu(torch):
+    # 1080p random BS / QP maps and offsets vs the oracle; plane borders must stay untouched
+    assert gpu_cases.check_deblock_random(seed=41) > 10000

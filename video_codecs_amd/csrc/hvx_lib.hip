@@ -19,6 +19,7 @@
 #include "hvx_mc.hpp"
 #include "hvx_cabac.hpp"
 #include "hvx_intra.hpp"
+#include "hvx_deblock.hpp"
 
 struct hvx_ctx {
   int device = 0;
@@ -485,6 +486,25 @@ int hvx_intra_search_batch(hvx_ctx *ctx, const uint8_t *d_org, const uint8_t *d_
   hipLaunchKernelGGL(k_intra_search, dim3(n), dim3(64), 0, ctx->stream, d_org, d_rec, stride, d_jobs, n,
                      d_entropy_bits, d_out);
   return launched("k_intra_search");
+}
+
+int hvx_deblock(hvx_ctx *ctx, uint8_t *d_y, int y_stride, uint8_t *d_cb, uint8_t *d_cr, int c_stride,
+                const uint8_t *d_bs_ver, const uint8_t *d_bs_hor, const int8_t *d_qp, const hvx_deblock_params *h_params) {
+  if (!ctx || !d_y || !d_cb || !d_cr || !d_bs_ver || !d_bs_hor || !d_qp || !h_params)
+    return fail(HVX_E_INVALID, "hvx_deblock: NULL argument");
+  const hvx_deblock_params P = *h_params;
+  if (P.pic_w <= 0 || P.pic_h <= 0 || P.pic_w % 8 || P.pic_h % 8 || y_stride < P.pic_w || c_stride < P.pic_w / 2 ||
+      P.beta_offset_div2 < -6 || P.beta_offset_div2 > 6 || P.tc_offset_div2 < -6 || P.tc_offset_div2 > 6 ||
+      P.cb_qp_offset < -12 || P.cb_qp_offset > 12 || P.cr_qp_offset < -12 || P.cr_qp_offset > 12 || P.flags)
+    return fail(HVX_E_INVALID, "hvx_deblock: bad parameters");
+  const int nv = (P.pic_w / 8 - 1) * (P.pic_h / 4), nh = (P.pic_h / 8 - 1) * (P.pic_w / 4);
+  if (nv > 0)
+    hipLaunchKernelGGL(k_deblock<0>, dim3((nv + 255) / 256), dim3(256), 0, ctx->stream, d_y, y_stride, d_cb, d_cr,
+                       c_stride, d_bs_ver, d_qp, P);
+  if (nh > 0)
+    hipLaunchKernelGGL(k_deblock<1>, dim3((nh + 255) / 256), dim3(256), 0, ctx->stream, d_y, y_stride, d_cb, d_cr,
+                       c_stride, d_bs_hor, d_qp, P);
+  return launched("k_deblock");
 }
 
 int hvx_alloc(hvx_ctx *ctx, size_t bytes, void **d_out) {

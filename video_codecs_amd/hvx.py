@@ -47,7 +47,7 @@ def lib():
             "hvx_set_timing": [P, I], "hvx_phase_times": [P, ctypes.POINTER(ctypes.c_double), I, I],
             "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
             "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P],
-            "hvx_intra_pred_batch": [P, P, I, P, I, P, P, P], "hvx_intra_search_batch": [P, P, P, I, P, I, P, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
+            "hvx_intra_pred_batch": [P, P, I, P, I, P, P, P], "hvx_deblock": [P, P, I, P, P, I, P, P, P, P], "hvx_intra_search_batch": [P, P, P, I, P, I, P, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
             "hvx_free": [P, P], "hvx_upload": [P, P, P, ctypes.c_size_t], "hvx_download": [P, P, P, ctypes.c_size_t],
         }.items():
             f = getattr(L, name)
@@ -204,6 +204,14 @@ def intra_search_batch(org_origin, rec_origin, stride, jobs_dev, n, entropy_dev,
     """hvx_intra_search_batch: estIntraPredLumaQT's first pass, one luma PU per job."""
     _check(lib().hvx_intra_search_batch(context(), ctypes.c_void_p(org_origin), ctypes.c_void_p(rec_origin), int(stride),
                                         _ptr(jobs_dev), n, _ptr(entropy_dev), _ptr(out_dev)), "hvx_intra_search_batch")
+
+
+def deblock(y_origin, y_stride, cb_origin, cr_origin, c_stride, bs_ver, bs_hor, qp, params):
+    """hvx_deblock in place: *_origin = device addresses of sample (0,0) of each plane."""
+    p = np.ascontiguousarray(params)
+    _check(lib().hvx_deblock(context(), ctypes.c_void_p(y_origin), int(y_stride), ctypes.c_void_p(cb_origin),
+                             ctypes.c_void_p(cr_origin), int(c_stride), _ptr(bs_ver), _ptr(bs_hor), _ptr(qp),
+                             p.ctypes.data_as(ctypes.c_void_p)), "hvx_deblock")
 
 
 def plane_from_pel(pel, pel_stride, width, height, plane):
