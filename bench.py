@@ -5,12 +5,13 @@ One step = one 3840x2160 picture (2040 CTUs): hvx_ctu_analyze (for each of the 8
 CTU: TZ integer + half/quarter motion search against 4 reference pictures, luma MC of the best
 reference, transform + RDOQ + dequant + inverse transform + SSE of every TU), then
 hvx_ctu_decide (CABAC coefficient rate of every TU, the residual and CU-quadtree RD decisions,
-the reconstructed picture with extended borders) -- DESIGN.md sections 3 and 3a.  Inputs are
+the reconstructed picture, and the reference picture: boundary strengths of the decided trees,
+luma deblocking, extended borders) -- DESIGN.md sections 3 and 3a.  Inputs are
 resident in HBM before timing starts.
 
 Multi-GPU (torch.distributed.run): one rank per GPU, each rank encodes its own independent GOP
 segment (different synthetic frames); the only collective is the per-picture gather of every
-rank's reconstruction to rank 0's DPB (video_codecs_amd/dpb.py, RCCL over xGMI); weak scaling.
+rank's deblocked reference picture to rank 0's DPB (video_codecs_amd/dpb.py, RCCL over xGMI); weak scaling.
 
 Contract: python bench.py --gpus N --steps K --warmup W  -> one JSON line on rank 0.
 """
@@ -124,9 +125,12 @@ def main():
         hvx.set_timing(True)
         hvx.phase_times(reset=True)
 
+    recon_t = torch.zeros_like(cur_t)
+
     def step():
-        # one picture: analysis (ME + TU pipeline) -> CU decision + reconstruction -> DPB gather
-        an.encode(cur_t, ref_ptrs, dpb.buffer())  # hvx_ctu_encode = hvx_ctu_analyze + hvx_ctu_decide
+        # one picture: analysis (ME + TU pipeline) -> CU decision + reconstruction -> deblocked
+        # reference picture -> DPB gather of that reference
+        an.encode(cur_t, ref_ptrs, recon_t, dpb.buffer())  # hvx_ctu_encode = hvx_ctu_analyze + hvx_ctu_decide
         dpb.send()
 
     def sync():
@@ -138,7 +142,7 @@ def main():
     hvx.set_timing(False)
     gpu_res, gpu_dec = an.results(), an.decisions()
     own, gathered = dpb.last()
-    gpu_rec = own.cpu().numpy()
+    gpu_rec = recon_t.cpu().numpy()
     dpb_ok = None
     if gathered is not None:  # rank 0 holds every rank's picture; its own slot must be its own
         dpb_ok = bool(torch.equal(gathered[0], own))
@@ -177,10 +181,10 @@ def main():
             "dtype": "u8",
             "data": "synthetic: splitmix64 uniform random 8-bit luma (BASELINE.md sec. 3), independent segment per rank",
             "config": {"workload": "CTU mode decision: 85 CUs x TZ+frac ME vs %d refs, MC, TU RDOQ/dequant/IT, "
-                                   "CABAC coefficient rate, CU quadtree RD decision, reconstruction" % nref,
+                                   "CABAC coefficient rate, CU quadtree RD decision, reconstruction, deblocked reference picture" % nref,
                        "resolution": f"{W}x{H}", "ctus_per_frame": nctu, "qp": args.qp, "search_range": 64,
                        "n_ref": nref, "parallelism": f"segments x{world}",
-                       "dpb": "gather of every rank's reconstructed picture to rank 0 per step" if world > 1 else "local"},
+                       "dpb": "gather of every rank's deblocked reference picture to rank 0 per step" if world > 1 else "local"},
             "phase_ms_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()},
             "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 3),
                          "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / MI355X_HBM_PEAK_GBS,
@@ -195,7 +199,7 @@ def main():
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(planes, an, gpu_res, gpu_dec, gpu_rec, args)
         if not args.no_intra:
-            out["intra_first_pass"] = intra_measure(cur_t, ref_t[0], W, H, float(an.params["lambda"]), args.steps)
+            out["intra_first_pass"] = intra_measure(cur_t, ref_t[0], W, H, float(an.params["lambda"][0]), args.steps)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -276,8 +276,8 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
  * (k_me_frac_ctu), 5 MC/residual (k_ctu_pred_resid), 6..8 TU 32x32 (k_tu_fwd, k_tu_rdoq,
  * k_tu_fin), 9..11 TU 16x16, 12..14 TU 8x8, 15 per-CU sums (k_ctu_finalize); hvx_ctu_decide:
  * 16 coefficient rate (3 x k_coeff_bits), 17 CU tree + reconstruction (k_ctu_decide, k_ctu_recon,
- * border extension).  Accumulated ms. */
-#define HVX_NPHASE 18
+ * border extension), 18 reference picture (k_ctu_bs, deblocking, border extension).  Accumulated ms. */
+#define HVX_NPHASE 19
 int hvx_set_timing(hvx_ctx *ctx, int on);
 int hvx_phase_times(hvx_ctx *ctx, double *ms_out, int n, int reset);
 
@@ -289,12 +289,16 @@ int hvx_phase_times(hvx_ctx *ctx, double *ms_out, int n, int reset);
  * recursion per CTU (hvx_types.h hvx_cu_decision; d_cu = hvx_ctu_analyze's output, d_dec =
  * nctu*85 records) and writes the luma of the chosen leaves, clip(pred + reconstructed
  * residual), into d_recon (sample (0,0) of an 8-bit padded plane with the same stride as
- * d_cur), borders extended as TComPicYuv::extendPicBorder -- the next picture's reference.
+ * d_cur), borders extended as TComPicYuv::extendPicBorder.  When d_ref_pic is not NULL it also
+ * writes the REFERENCE picture there (may equal d_recon: in place): that reconstruction deblocked
+ * (boundary strengths of the decided CU/TU trees as TComLoopFilter's xSetEdgefilterTU/PU +
+ * xGetBoundaryStrengthSingle give them, slice QP, luma loopFilterPic as hvx_deblock) with its
+ * borders extended again -- the next picture's reference (TEncGOP.cpp:1465).
  * Picture width and height must be multiples of 8.
  * ------------------------------------------------------------------------------------- */
 int hvx_ctu_decide(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const hvx_ctu_params *h_params,
                    const uint8_t *d_ctx_states, const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes,
-                   const hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon);
+                   const hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic);
 
 /* The whole picture step: hvx_ctu_analyze + hvx_ctu_decide with the same results, scheduled
  * together (each TU size class's coefficient rate is counted on that class's stream as soon as
@@ -302,7 +306,7 @@ int hvx_ctu_decide(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const hvx_ctu
 int hvx_ctu_encode(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
                    const hvx_ctu_params *h_params, const hvx_estbits *d_est4, const uint8_t *d_ctx_states,
                    const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes, hvx_cu_result *d_cu,
-                   hvx_cu_decision *d_dec, uint8_t *d_recon);
+                   hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic);
 
 /* ---------------------------------------------------------------------------------------
  * Picture upload: HM int16 plane (width x height samples, any stride, device copy) ->

@@ -383,3 +383,15 @@ def deblock(y, cb, cr, bs_ver, bs_hor, qp, params):
     p = np.ascontiguousarray(params)
     L.hvxo_deblock(_p(y), y.shape[1], _p(cb), _p(cr), cb.shape[1], _p(bv), _p(bh), _p(q), _p(p))
     return y, cb, cr
+
+
+def ctu_bs(cu, dec, pic_w, pic_h):
+    """hvxo_ctu_bs: (bs_ver, bs_hor) maps of a whole analysed + decided picture."""
+    L = lib()
+    L.hvxo_ctu_bs.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int] * 2 + [ctypes.c_void_p] * 2
+    c = np.ascontiguousarray(cu, dtype=_abi.CU_RESULT).reshape(-1)
+    d = np.ascontiguousarray(dec, dtype=_abi.CU_DECISION).reshape(-1)
+    bv = np.zeros((pic_h // 4) * (pic_w // 4), np.uint8)
+    bh = np.zeros_like(bv)
+    L.hvxo_ctu_bs(_p(c), _p(d), int(pic_w), int(pic_h), _p(bv), _p(bh))
+    return bv, bh

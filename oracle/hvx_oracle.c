@@ -2282,3 +2282,45 @@ void hvxo_deblock(uint8_t *y, int ys, uint8_t *cb, uint8_t *cr, int cs, const ui
       }
   }
 }
+
+/* ============================================================================================
+ * Boundary strengths of the analysed picture (the bench step's deblocking input): what
+ * TComLoopFilter's xSetEdgefilterTU/PU (TComLoopFilter.cpp:274-359) and xGetBoundaryStrengthSingle
+ * (:417-557) give for hvx_ctu_decide's CU trees -- 2Nx2N inter CUs of a P slice, luma TUs of
+ * min(CU, 32): an edge is a CU or TU boundary (all of them transform edges); bs 1 when either side's
+ * TU has a coded luma block, else when the two sides use different reference pictures or their
+ * MVs differ by >= 4 quarter samples in x or y; 0 at the picture border and off the 8x8 grid.
+ * ========================================================================================== */
+static void unit_block(const hvx_cu_decision *dec, int nctu_x, int ux, int uy, int *ctu, int *ci, int *t) {
+  const int c = (uy / 16) * nctu_x + ux / 16, lx = ux % 16, ly = uy % 16;
+  static const int base[4] = {0, 1, 5, 21};
+  for (int d = 0; d < 4; d++) {
+    const int su = 16 >> d, j = (ly / su) * (1 << d) + lx / su, k = base[d] + j;
+    if (dec[(size_t)c * HVX_CUS_PER_CTU + k].leaf || d == 3) {
+      const int tu = su < 8 ? su : 8;
+      *ctu = c; *ci = k;
+      *t = ((ly % su) / tu) * (su / tu) + (lx % su) / tu;
+      return;
+    }
+  }
+}
+
+void hvxo_ctu_bs(const hvx_cu_result *cu, const hvx_cu_decision *dec, int pic_w, int pic_h, uint8_t *bs_ver,
+                 uint8_t *bs_hor) {
+  const int uw = pic_w / 4, uh = pic_h / 4, nctu_x = (pic_w + 63) / 64;
+  for (int uy = 0; uy < uh; uy++)
+    for (int ux = 0; ux < uw; ux++)
+      for (int dir = 0; dir < 2; dir++) {
+        uint8_t *o = dir ? &bs_hor[uy * uw + ux] : &bs_ver[uy * uw + ux];
+        *o = 0;
+        if (dir == 0 ? (ux % 2 || ux == 0) : (uy % 2 || uy == 0)) continue;
+        int cq, kq, tq, cp, kp, tp;
+        unit_block(dec, nctu_x, ux, uy, &cq, &kq, &tq);
+        unit_block(dec, nctu_x, dir ? ux : ux - 1, dir ? uy - 1 : uy, &cp, &kp, &tp);
+        if (cq == cp && kq == kp && tq == tp) continue; /* not a transform / CU edge */
+        const hvx_cu_decision *dq = &dec[(size_t)cq * HVX_CUS_PER_CTU + kq], *dp = &dec[(size_t)cp * HVX_CUS_PER_CTU + kp];
+        const hvx_cu_result *rq = &cu[(size_t)cq * HVX_CUS_PER_CTU + kq], *rp = &cu[(size_t)cp * HVX_CUS_PER_CTU + kp];
+        if (((dq->cbf >> tq) & 1) || ((dp->cbf >> tp) & 1)) *o = 1;
+        else *o = (rq->ref != rp->ref || abs(rq->mv_x - rp->mv_x) >= 4 || abs(rq->mv_y - rp->mv_y) >= 4) ? 1 : 0;
+      }
+}

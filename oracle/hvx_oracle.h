@@ -106,6 +106,11 @@ void hvxo_intra_search(const uint8_t *org, const int16_t *raw, const hvx_intra_j
 void hvxo_deblock(uint8_t *y, int ys, uint8_t *cb, uint8_t *cr, int cs, const uint8_t *bs_ver, const uint8_t *bs_hor,
                   const int8_t *qp, const hvx_deblock_params *p);
 
+/* boundary strengths of hvx_ctu_decide's CU trees (the bench step's deblocking input); cu/dec =
+ * nctu*85 records of the whole picture, maps (pic_w/4) x (pic_h/4) */
+void hvxo_ctu_bs(const hvx_cu_result *cu, const hvx_cu_decision *dec, int pic_w, int pic_h, uint8_t *bs_ver,
+                 uint8_t *bs_hor);
+
 /* tables (generated, HEVC spec values) */
 void hvxo_dct_matrix(int n, int16_t *m /* n*n, [k][x] */);
 const uint32_t *hvxo_scan(int grouped, int scan_type, int log2w, int log2h);

@@ -239,11 +239,12 @@ def check_ctu_decide(seed, width, height, nref, qp, fused=False):
     ref_t = [torch.from_numpy(r).cuda() for r in refs]
     ptrs = torch.tensor([hvx.plane_origin_ptr(t, width) for t in ref_t], dtype=torch.int64).cuda()
     recon_t = torch.zeros_like(cur_t)
+    refpic_t = torch.zeros_like(cur_t)
     if fused:
-        an.encode(cur_t, ptrs, recon_t)
+        an.encode(cur_t, ptrs, recon_t, refpic_t)
     else:
         an.run(cur_t, ptrs)
-        an.decide(cur_t, recon_t)
+        an.decide(cur_t, recon_t, ref_pic=refpic_t)
     torch.cuda.synchronize()
     got_cu, got_dec, got_rec = an.results(), an.decisions(), recon_t.cpu().numpy()
     est, st, eb = _abi.load_estbits_p_luma(), _abi.load_ctx_p_states(), _abi.load_entropy_bits()
@@ -257,8 +258,14 @@ def check_ctu_decide(seed, width, height, nref, qp, fused=False):
             assert got_dec[c][ci].tobytes() == dec[ci].tobytes(), (c, ci, got_dec[c][ci], dec[ci])
         n_leaf += int(dec["leaf"].sum())
     M = _abi.PLANE_MARGIN
-    exp_rec = np.pad(exp_rec[M:M + height, M:M + width], M, mode="edge")  # extendPicBorder
-    np.testing.assert_array_equal(got_rec, exp_rec)
+    inner = exp_rec[M:M + height, M:M + width]
+    np.testing.assert_array_equal(got_rec, np.pad(inner, M, mode="edge"))  # extendPicBorder
+    # the reference picture: boundary strengths of the decided trees + luma deblocking
+    bv, bh = oracle.ctu_bs(got_cu.reshape(-1), got_dec.reshape(-1), width, height)
+    qp = np.full(len(bv), int(an.params["qp"][0]), np.int8)
+    zc = np.zeros((height // 2, width // 2), np.uint8)
+    dy, _, _ = oracle.deblock(inner, zc, zc, bv, bh, qp, _abi.deblock_params(width, height))
+    np.testing.assert_array_equal(refpic_t.cpu().numpy(), np.pad(dy, M, mode="edge"))
     return an.nctu, n_leaf
 
 

@@ -168,3 +168,43 @@ def test_oracle_deblock_random_smoke():
     qp = np.full((16, 16), 37, np.int8)
     out = oracle.deblock(y, cb, cr, bv.ravel(), bh.ravel(), qp.ravel(), _abi.deblock_params(64, 64))
     assert (out[0] != y).any() and (out[1] != cb).any()
+
+
+def test_oracle_ctu_bs_edges():
+    # boundary strengths of decided trees: only on the 8x8 grid, never at the picture border, at
+    # most 1 (inter P slice), and exactly at CU/TU boundaries -- never inside one transform block
+    import oracle
+    from oracle import make_yuv
+    from video_codecs_amd import _abi
+    W, H = 128, 128
+    pad = lambda img: np.pad(img, _abi.PLANE_MARGIN, mode="edge")  # noqa: E731
+    cur = pad(make_yuv.random_frame(W, H, 5)[:W * H].reshape(H, W))
+    refs = [pad(make_yuv.smooth_frame(W, H, 6)[:W * H].reshape(H, W))]
+    p = _abi.ctu_params(W, H, 1, 32)
+    est, st, eb = _abi.load_estbits_p_luma(), _abi.load_ctx_p_states(), _abi.load_entropy_bits()
+    rec = np.zeros_like(cur)
+    cus, decs = [], []
+    for c in range(4):
+        cu, dec = oracle.ctu_decide(cur, refs, p, est, st, eb, c % 2, c // 2, rec)
+        cus.append(cu)
+        decs.append(dec)
+    bv, bh = oracle.ctu_bs(np.concatenate(cus), np.concatenate(decs), W, H)
+    bv, bh = bv.reshape(H // 4, W // 4), bh.reshape(H // 4, W // 4)
+    assert bv.max() <= 1 and bh.max() <= 1 and bv.any() and bh.any()
+    assert not bv[:, 1::2].any() and not bv[:, 0].any() and not bh[1::2, :].any() and not bh[0, :].any()
+    # block id of every 4x4 unit: (ctu, leaf CU, TU) -- edges with bs 1 separate different blocks
+    dec_all = np.concatenate(decs)
+    block = np.zeros((H // 4, W // 4), np.int64)
+    for uy in range(H // 4):
+        for ux in range(W // 4):
+            c = (uy // 16) * 2 + ux // 16
+            for d in range(4):
+                su = 16 >> d
+                k = (0, 1, 5, 21)[d] + ((uy % 16) // su) * (1 << d) + (ux % 16) // su
+                if dec_all[c * 85 + k]["leaf"]:
+                    tu = min(su, 8)
+                    t = (((uy % 16) % su) // tu) * (su // tu) + ((ux % 16) % su) // tu
+                    block[uy, ux] = (c * 85 + k) * 16 + t
+                    break
+    assert not (bv[:, 1:] & (block[:, 1:] == block[:, :-1])).any()
+    assert not (bh[1:, :] & (block[1:, :] == block[:-1, :])).any()

@@ -363,3 +363,52 @@ __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int p
     recon[y * stride + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
   }
 }
+
+// Boundary strengths of the decided CU trees (restated by hvxo_ctu_bs): TComLoopFilter's
+// xSetEdgefilterTU/PU (TComLoopFilter.cpp:274-359) + xGetBoundaryStrengthSingle (:417-557) for
+// 2Nx2N inter CUs of a P slice with luma TUs of min(CU, 32).  One thread per 4x4 luma unit writes
+// the BS of its left and top edges (0 off the 8x8 grid / at the picture border) and its QP.
+__device__ __forceinline__ void unit_block(const hvx_cu_decision *dec, int nctu_x, int ux, int uy, int &ctu, int &ci,
+                                           int &t) {
+  ctu = (uy >> 4) * nctu_x + (ux >> 4);
+  const int lx = ux & 15, ly = uy & 15;
+  for (int d = 0; d < 4; d++) {
+    const int su = 16 >> d, j = (ly / su) * (1 << d) + lx / su, k = depth_base(d) + j;
+    if (d == 3 || dec[(size_t)ctu * HVX_CUS_PER_CTU + k].leaf) {
+      const int tu = su < 8 ? su : 8;
+      ci = k;
+      t = ((ly % su) / tu) * (su / tu) + (lx % su) / tu;
+      return;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ctu_bs(const hvx_cu_result *__restrict__ cu,
+                                                const hvx_cu_decision *__restrict__ dec, int pic_w, int pic_h, int qp,
+                                                uint8_t *__restrict__ bs_ver, uint8_t *__restrict__ bs_hor,
+                                                int8_t *__restrict__ qpm) {
+  const int uw = pic_w >> 2, uh = pic_h >> 2, nctu_x = (pic_w + 63) >> 6;
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= uw * uh) return;
+  const int ux = u % uw, uy = u / uw;
+  qpm[u] = (int8_t)qp;
+  int cq, kq, tq;
+  unit_block(dec, nctu_x, ux, uy, cq, kq, tq);
+  const hvx_cu_decision &dq = dec[(size_t)cq * HVX_CUS_PER_CTU + kq];
+  const hvx_cu_result &rq = cu[(size_t)cq * HVX_CUS_PER_CTU + kq];
+#pragma unroll
+  for (int dir = 0; dir < 2; dir++) {
+    uint8_t bs = 0;
+    if (dir == 0 ? ((ux & 1) == 0 && ux > 0) : ((uy & 1) == 0 && uy > 0)) {
+      int cp, kp, tp;
+      unit_block(dec, nctu_x, dir ? ux : ux - 1, dir ? uy - 1 : uy, cp, kp, tp);
+      if (cq != cp || kq != kp || tq != tp) {
+        const hvx_cu_decision &dp = dec[(size_t)cp * HVX_CUS_PER_CTU + kp];
+        const hvx_cu_result &rp = cu[(size_t)cp * HVX_CUS_PER_CTU + kp];
+        if (((dq.cbf >> tq) & 1) || ((dp.cbf >> tp) & 1)) bs = 1;
+        else bs = (rq.ref != rp.ref || abs(rq.mv_x - rp.mv_x) >= 4 || abs(rq.mv_y - rp.mv_y) >= 4) ? 1 : 0;
+      }
+    }
+    (dir ? bs_hor : bs_ver)[u] = bs;
+  }
+}

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void k_deblock(uint8_t *__restrict__ y, int ys
   const int x = ux * 4, yy = uy * 4;
   if (DIR == 0) luma_seg(y + (int64_t)yy * ys + x, ys, 1, bs, avg, p.beta_offset_div2, p.tc_offset_div2);
   else luma_seg(y + (int64_t)yy * ys + x, 1, ys, bs, avg, p.beta_offset_div2, p.tc_offset_div2);
-  if (bs == 2 && (e & 1) == 0) {  // the 16-sample luma grid = the 8-sample chroma grid
+  if (cb && bs == 2 && (e & 1) == 0) {  // the 16-sample luma grid = the 8-sample chroma grid (cb NULL: luma only)
     const int64_t o = (int64_t)(yy / 2) * cs + x / 2;
     if (DIR == 0) {
       chroma_seg(cb + o, cs, 1, bs, avg, p.cb_qp_offset, p.tc_offset_div2);

@@ -66,7 +66,8 @@ size_t ctu_il_off16(int n) { return pad_g((size_t)8 * n) * 1024; }
 size_t ctu_il_off8(int n) { return ctu_il_off16(n) + pad_g((size_t)16 * n) * 256; }
 size_t ctu_il_words(int n) { return ctu_il_off8(n) + pad_g((size_t)64 * n) * 64; }
 struct CtuWs {
-  size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, coefI, levI, stI, flags, cbits, total;
+  size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, coefI, levI, stI, flags, cbits, bsv, bsh,
+      qpm, total;
 };
 CtuWs ctu_ws_layout(const CtuLayout &L) {
   CtuWs w;
@@ -89,6 +90,10 @@ CtuWs ctu_ws_layout(const CtuLayout &L) {
   w.stI = o; o = align_up(o + nil * sizeof(int32_t));
   w.flags = o; o = align_up(o + ntu);
   w.cbits = o; o = align_up(o + ntu * sizeof(hvx_coeff_bits));
+  const size_t nunit = (size_t)L.nctu * 256;  // deblocking maps of the reference picture (>= (w/4)*(h/4))
+  w.bsv = o; o = align_up(o + nunit);
+  w.bsh = o; o = align_up(o + nunit);
+  w.qpm = o; o = align_up(o + nunit);
   w.total = o;
   return w;
 }
@@ -751,7 +756,8 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
 
 static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const hvx_ctu_params *h_params,
                            const uint8_t *d_ctx_states, const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes,
-                           const hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon, bool count) {
+                           const hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic,
+                           bool count) {
   if (!ctx || !d_cur || !h_params || !d_ctx_states || !d_entropy_bits || !d_workspace || !d_cu || !d_dec || !d_recon)
     return fail(HVX_E_INVALID, "hvx_ctu_decide: NULL argument");
   const hvx_ctu_params P = *h_params;
@@ -796,26 +802,53 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
   hipLaunchKernelGGL(k_plane_extend, dim3((P.pic_w + 2 * M + 255) / 256, 2 * M), dim3(256), 0, st, d_recon, stride, P.pic_w,
                      P.pic_h, M, 1);
   t_end(ctx, st, tk);
+  if (d_ref_pic) {
+    // 4. the reference picture: the reconstruction deblocked (boundary strengths of the decided
+    //    trees, k_ctu_bs; TComLoopFilter::loopFilterPic, luma) with borders extended again
+    tk = t_begin(ctx, st, 18);
+    const int nunit = (P.pic_w / 4) * (P.pic_h / 4);
+    uint8_t *bsv = (uint8_t *)(ws + W.bsv), *bsh = (uint8_t *)(ws + W.bsh);
+    int8_t *qpm = (int8_t *)(ws + W.qpm);
+    hipLaunchKernelGGL(k_ctu_bs, dim3((nunit + 255) / 256), dim3(256), 0, st, d_cu, (const hvx_cu_decision *)d_dec,
+                       P.pic_w, P.pic_h, P.qp, bsv, bsh, qpm);
+    uint8_t *base_src = d_recon - (int64_t)M * stride - M, *base_dst = d_ref_pic - (int64_t)M * stride - M;
+    if (d_ref_pic != d_recon)
+      HVX_HIP(hipMemcpyAsync(base_dst, base_src, (size_t)stride * (P.pic_h + 2 * M), hipMemcpyDeviceToDevice, st));
+    hvx_deblock_params dp = {};
+    dp.pic_w = P.pic_w; dp.pic_h = P.pic_h;
+    const int nv = (P.pic_w / 8 - 1) * (P.pic_h / 4), nh = (P.pic_h / 8 - 1) * (P.pic_w / 4);
+    if (nv > 0)
+      hipLaunchKernelGGL(k_deblock<0>, dim3((nv + 255) / 256), dim3(256), 0, st, d_ref_pic, stride, (uint8_t *)nullptr,
+                         (uint8_t *)nullptr, 0, bsv, qpm, dp);
+    if (nh > 0)
+      hipLaunchKernelGGL(k_deblock<1>, dim3((nh + 255) / 256), dim3(256), 0, st, d_ref_pic, stride, (uint8_t *)nullptr,
+                         (uint8_t *)nullptr, 0, bsh, qpm, dp);
+    hipLaunchKernelGGL(k_plane_extend, dim3((2 * M + 255) / 256, P.pic_h), dim3(256), 0, st, d_ref_pic, stride, P.pic_w,
+                       P.pic_h, M, 0);
+    hipLaunchKernelGGL(k_plane_extend, dim3((P.pic_w + 2 * M + 255) / 256, 2 * M), dim3(256), 0, st, d_ref_pic, stride,
+                       P.pic_w, P.pic_h, M, 1);
+    t_end(ctx, st, tk);
+  }
   return launched("hvx_ctu_decide");
 }
 
 int hvx_ctu_decide(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const hvx_ctu_params *h_params,
                    const uint8_t *d_ctx_states, const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes,
-                   const hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon) {
+                   const hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic) {
   return ctu_decide_impl(ctx, d_cur, stride, h_params, d_ctx_states, d_entropy_bits, d_workspace, ws_bytes, d_cu, d_dec,
-                         d_recon, true);
+                         d_recon, d_ref_pic, true);
 }
 
 int hvx_ctu_encode(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
                    const hvx_ctu_params *h_params, const hvx_estbits *d_est4, const uint8_t *d_ctx_states,
                    const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes, hvx_cu_result *d_cu,
-                   hvx_cu_decision *d_dec, uint8_t *d_recon) {
+                   hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic) {
   if (!d_ctx_states || !d_entropy_bits || !d_dec || !d_recon) return fail(HVX_E_INVALID, "hvx_ctu_encode: NULL argument");
   const int rc = ctu_analyze_impl(ctx, d_cur, d_refs, stride, h_params, d_est4, d_workspace, ws_bytes, d_cu, d_ctx_states,
                                   d_entropy_bits);
   if (rc) return rc;
   return ctu_decide_impl(ctx, d_cur, stride, h_params, d_ctx_states, d_entropy_bits, d_workspace, ws_bytes, d_cu, d_dec,
-                         d_recon, false);
+                         d_recon, d_ref_pic, false);
 }
 
 int hvx_plane_extend(hvx_ctx *ctx, uint8_t *d_plane, int width, int height) {

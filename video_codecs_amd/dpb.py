@@ -1,8 +1,8 @@
 """The writer rank's shared decoded-picture buffer.
 
 CTUs shard across GPUs by independent closed GOP segments, one per rank.  After every picture
-each rank's reconstruction -- the padded 8-bit plane that hvx_ctu_decide wrote, borders already
-extended, i.e. a ready reference picture -- is gathered to rank 0 with ONE torch.distributed
+each rank's reference picture -- the padded 8-bit plane hvx_ctu_decide wrote: the reconstruction
+deblocked, borders extended, i.e. a ready reference picture -- is gathered to rank 0 with ONE torch.distributed
 gather per picture (RCCL over xGMI on the GPUs; gloo in the CPU tests).  The gather is the only
 data-path collective of the path.  It is asynchronous and the reconstruction buffers are
 double-buffered, so picture k+1 is analysed while picture k's samples move; a buffer is handed

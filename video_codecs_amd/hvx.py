@@ -42,8 +42,8 @@ def lib():
             "hvx_plane_from_pel": [P, P, I, I, I, P], "hvx_plane_extend": [P, P, I, I],
             "hvx_ctu_workspace_size": [I, I, I, ctypes.POINTER(ctypes.c_size_t)],
             "hvx_ctu_analyze": [P, P, P, I, P, P, P, ctypes.c_size_t, P],
-            "hvx_ctu_decide": [P, P, I, P, P, P, P, ctypes.c_size_t, P, P, P],
-            "hvx_ctu_encode": [P, P, P, I, P, P, P, P, P, ctypes.c_size_t, P, P, P],
+            "hvx_ctu_decide": [P, P, I, P, P, P, P, ctypes.c_size_t, P, P, P, P],
+            "hvx_ctu_encode": [P, P, P, I, P, P, P, P, P, ctypes.c_size_t, P, P, P, P],
             "hvx_set_timing": [P, I], "hvx_phase_times": [P, ctypes.POINTER(ctypes.c_double), I, I],
             "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
             "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P],
@@ -264,7 +264,7 @@ class CtuAnalyzer:
             self.dec = torch.zeros(self.nctu * _abi.CUS_PER_CTU * _abi.CU_DECISION.itemsize, dtype=torch.uint8,
                                    device="cuda")
 
-    def encode(self, cur_plane, ref_planes_ptrs, recon_plane):
+    def encode(self, cur_plane, ref_planes_ptrs, recon_plane, ref_pic=None):
         """hvx_ctu_encode: run() + decide() as one schedule (same results)."""
         self._rate_model()
         p = np.ascontiguousarray(self.params)
@@ -272,17 +272,22 @@ class CtuAnalyzer:
                                     _ptr(ref_planes_ptrs), self.stride, p.ctypes.data_as(ctypes.c_void_p),
                                     _ptr(self.est), _ptr(self.states), _ptr(self.eb), _ptr(self.ws), self.ws_bytes,
                                     _ptr(self.out), _ptr(self.dec),
-                                    ctypes.c_void_p(plane_origin_ptr(recon_plane, self.pic_w))), "hvx_ctu_encode")
+                                    ctypes.c_void_p(plane_origin_ptr(recon_plane, self.pic_w)),
+                                    ctypes.c_void_p(0 if ref_pic is None else plane_origin_ptr(ref_pic, self.pic_w))),
+               "hvx_ctu_encode")
 
-    def decide(self, cur_plane, recon_plane, states=None, entropy_bits=None):
+    def decide(self, cur_plane, recon_plane, states=None, entropy_bits=None, ref_pic=None):
         """hvx_ctu_decide after run(): CU tree of every CTU + the reconstructed picture (the leaves'
-        luma, borders extended) into recon_plane (padded uint8 device tensor shaped like cur_plane)."""
+        luma, borders extended) into recon_plane (padded uint8 device tensor shaped like cur_plane);
+        with ref_pic, also the deblocked reference picture."""
         self._rate_model(states, entropy_bits)
         p = np.ascontiguousarray(self.params)
         _check(lib().hvx_ctu_decide(context(), ctypes.c_void_p(plane_origin_ptr(cur_plane, self.pic_w)), self.stride,
                                     p.ctypes.data_as(ctypes.c_void_p), _ptr(self.states), _ptr(self.eb), _ptr(self.ws),
                                     self.ws_bytes, _ptr(self.out), _ptr(self.dec),
-                                    ctypes.c_void_p(plane_origin_ptr(recon_plane, self.pic_w))), "hvx_ctu_decide")
+                                    ctypes.c_void_p(plane_origin_ptr(recon_plane, self.pic_w)),
+                                    ctypes.c_void_p(0 if ref_pic is None else plane_origin_ptr(ref_pic, self.pic_w))),
+               "hvx_ctu_decide")
 
     def decisions(self):
         return from_device(self.dec, _abi.CU_DECISION).reshape(self.nctu, _abi.CUS_PER_CTU)
@@ -290,14 +295,14 @@ class CtuAnalyzer:
 
 PHASES = ("me_d0", "me_d1", "me_d2", "me_d3", "frac_d0", "mc_resid",
           "tu32_fwd", "tu32_rdoq", "tu32_fin", "tu16_fwd", "tu16_rdoq", "tu16_fin", "tu8_fwd", "tu8_rdoq", "tu8_fin",
-          "finalize", "coeff_bits", "decide_recon")
+          "finalize", "coeff_bits", "decide_recon", "ref_picture")
 # the kernel each phase times (plus the tiny k_ctu_me_jobs in me_dN) and its launches per
 # hvx_ctu_analyze call; phases run on 3 streams and may overlap (DESIGN.md "CTU analysis pass")
-PHASE_LAUNCHES = (1, 1, 1, 1, 1, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 3, 5)
+PHASE_LAUNCHES = (1, 1, 1, 1, 1, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 3, 5, 5)
 PHASE_KERNELS = ("k_me_int_ctu<64,1,4>", "k_me_ctu<32,1,2>", "k_me_ctu<16,1,1>", "k_me_ctu<8,0,1>",
                  "k_me_frac_ctu<64,4>", "k_ctu_pred_resid", "k_tu_fwd<3>", "k_tu_rdoq<3>", "k_tu_fin<3,2>",
                  "k_tu_fwd<2>", "k_tu_rdoq<2>", "k_tu_fin<2,2>", "k_tu_fwd<1>", "k_tu_rdoq<1>", "k_tu_fin<1,2>",
-                 "k_ctu_finalize", "k_coeff_bits_il", "k_ctu_leaf+k_ctu_decide")
+                 "k_ctu_finalize", "k_coeff_bits_il", "k_ctu_leaf+k_ctu_decide", "k_ctu_bs+k_deblock")
 
 
 def set_timing(on):
