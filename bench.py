@@ -221,18 +221,26 @@ def intra_measure(cur_t, rec_t, W, H, lam, steps):
     org, rec = hvx.plane_origin_ptr(cur_t, W), hvx.plane_origin_ptr(rec_t, W)
     stride = cur_t.shape[1]
 
-    def one():
-        for l in jobs:
+    def one(sizes):
+        for l in sizes:
             hvx.intra_search_batch(org, rec, stride, dev[l], len(jobs[l]), eb, out)
-    one()
+    one(jobs)
     hvx.sync()
+    per_size = {}
+    for l in jobs:  # each PU size alone (the per-size share of the picture time)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one([l])
+        hvx.sync()
+        per_size[str(1 << l)] = round((time.perf_counter() - t0) / steps * 1e3, 3)
     t0 = time.perf_counter()
     for _ in range(steps):
-        one()
+        one(jobs)
     hvx.sync()
     ms = (time.perf_counter() - t0) / steps * 1e3
     return {"kernel": "k_intra_search", "pus_per_picture": total,
-            "pus_by_size": {str(1 << l): len(j) for l, j in jobs.items()}, "ms_per_picture": round(ms, 3),
+            "pus_by_size": {str(1 << l): len(j) for l, j in jobs.items()}, "ms_by_size": per_size,
+            "ms_per_picture": round(ms, 3),
             "pus_per_s": round(total / ms * 1e3, 1),
             "ctus_per_s": round(((W + 63) // 64) * ((H + 63) // 64) / ms * 1e3, 1)}
 

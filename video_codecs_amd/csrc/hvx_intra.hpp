@@ -220,6 +220,8 @@ __global__ __launch_bounds__(64) void k_intra_search(const uint8_t *__restrict__
   __shared__ Border s;
   __shared__ uint8_t so[64 * 64];
   __shared__ uint32_t satd[36];
+  __shared__ int s_list[12], s_mpm[3];   // lane 0's candidate list in LDS (no dynamically indexed
+  __shared__ double s_cc[10];            // private arrays -> no scratch)
   const int i = blockIdx.x;
   if (i >= n_jobs) return;
   const hvx_intra_job j = jobs[i];
@@ -280,7 +282,9 @@ __global__ __launch_bounds__(64) void k_intra_search(const uint8_t *__restrict__
   __syncthreads();
   if (lane != 0) return;
   // rates, costs, ranking, MPM append: 35 scalar steps
-  int mpm[3], imode;
+  int imode;
+  int *mpm = s_mpm, *list = s_list;
+  double *cc = s_cc;
   const int ld = j.left_dir, ad = j.above_dir;  // getIntraDirPredictor (TComDataCU.cpp:1441-1478)
   if (ld == ad) {
     imode = 1;
@@ -291,19 +295,19 @@ __global__ __launch_bounds__(64) void k_intra_search(const uint8_t *__restrict__
     mpm[0] = ld; mpm[1] = ad;
     mpm[2] = (ld && ad) ? 0 : ((ld + ad) < 2 ? 26 : 1);
   }
+  const int mp0 = mpm[0], mp1 = mpm[1], mp2 = mpm[2];
   const bool fast = (j.flags & HVX_INTRA_FAST_MPM) != 0;
   int num = fast ? kNumRdMpm[log2n - 1] : kNumRdNoMpm[log2n - 1];
-  int list[11];
-  double cc[9];
-  for (int k = 0; k < 9; k++) { list[k] = 0; cc[k] = 1.7976931348623157e308; }
-  hvx_intra_search_result r;
+  for (int k = 0; k < 10; k++) { list[k] = 0; cc[k] = 1.7976931348623157e308; }
+  list[10] = list[11] = 0;
+  hvx_intra_search_result &r = out[i];  // written in place (a private copy would live in scratch)
   const uint64_t frac = (uint64_t)(uint32_t)j.frac_bits;
   const int st = j.ctx_state & 127;
+  const uint64_t eb_mpm = (uint64_t)(uint32_t)eb[st ^ 1], eb_no = (uint64_t)(uint32_t)eb[st];
   for (int m = 0; m < 35; m++) {
-    const int idx = m == mpm[0] ? 0 : m == mpm[1] ? 1 : m == mpm[2] ? 2 : -1;
+    const int idx = m == mp0 ? 0 : m == mp1 ? 1 : m == mp2 ? 2 : -1;
     // xModeBitsIntra (TEncSearch.cpp:5222): flag bin + 1/2 (MPM index) or 5 bypass bins
-    const uint64_t total = frac + (uint64_t)(uint32_t)eb[st ^ (idx >= 0 ? 1 : 0)] +
-                           32768ull * (uint64_t)(idx < 0 ? 5 : idx ? 2 : 1);
+    const uint64_t total = frac + (idx >= 0 ? eb_mpm : eb_no) + 32768ull * (uint64_t)(idx < 0 ? 5 : idx ? 2 : 1);
     const uint32_t bits = (uint32_t)(total >> 15);
     const uint32_t sd = satd[m];
     r.satd[m] = sd;
@@ -328,5 +332,4 @@ __global__ __launch_bounds__(64) void k_intra_search(const uint8_t *__restrict__
   r.n_cand = (uint8_t)num;
   for (int k = 0; k < 11; k++) r.cand[k] = (uint8_t)(k < num ? list[k] : 0);
   for (int k = 0; k < 4; k++) r.pad_[k] = 0;
-  out[i] = r;
 }
