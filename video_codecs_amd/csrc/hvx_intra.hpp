@@ -129,22 +129,24 @@ struct Mode {
 };
 
 // one sample of predIntraAng (TComPrediction.cpp:455-516) with bAbove = bLeft = true and edge
-// filters enabled: planar (:756), DC + xDCPredFiltering (:183, :816), xPredIntraAng (:247)
-__device__ __forceinline__ int pred_sample(const int16_t *B, int n, int log2n, const Mode &md, bool edge, int dc, int r,
-                                           int c) {
+// filters enabled: planar (:756), DC + xDCPredFiltering (:183, :816), xPredIntraAng (:247);
+// B(k) = border sample k
+template <class F>
+__device__ __forceinline__ int pred_sample_f(const F &B, int n, int log2n, const Mode &md, bool edge, int dc, int r,
+                                             int c) {
   if (md.mode == 0)
-    return ((n - 1 - c) * B[2 * n + 1 + r] + (c + 1) * B[1 + n] + (n - 1 - r) * B[1 + c] + (r + 1) * B[3 * n + 1] + n) >>
+    return ((n - 1 - c) * B(2 * n + 1 + r) + (c + 1) * B(1 + n) + (n - 1 - r) * B(1 + c) + (r + 1) * B(3 * n + 1) + n) >>
            (log2n + 1);
   if (md.mode == 1) {
-    if (edge && r == 0 && c == 0) return (B[1] + B[2 * n + 1] + 2 * dc + 2) >> 2;
-    if (edge && r == 0) return (B[1 + c] + 3 * dc + 2) >> 2;
-    if (edge && c == 0) return (B[2 * n + 1 + r] + 3 * dc + 2) >> 2;
+    if (edge && r == 0 && c == 0) return (B(1) + B(2 * n + 1) + 2 * dc + 2) >> 2;
+    if (edge && r == 0) return (B(1 + c) + 3 * dc + 2) >> 2;
+    if (edge && c == 0) return (B(2 * n + 1 + r) + 3 * dc + 2) >> 2;
     return dc;
   }
   const int y = md.ver ? r : c, x = md.ver ? c : r;
   // refMain[k] / refSide[k]: the above row (B[k]) or the left column (B[0], B[2n+k])
-  auto above = [&](int k) { return (int)B[k]; };
-  auto left = [&](int k) { return k ? (int)B[2 * n + k] : (int)B[0]; };
+  auto above = [&](int k) { return B(k); };
+  auto left = [&](int k) { return k ? B(2 * n + k) : B(0); };
   auto mainr = [&](int k) {
     if (k >= 0) return md.ver ? above(k) : left(k);
     const int s = (128 - k * md.inv) >> 8;  // the projected side (:321-329)
@@ -153,7 +155,7 @@ __device__ __forceinline__ int pred_sample(const int16_t *B, int n, int log2n, c
   if (md.angle == 0) {
     int v = mainr(x + 1);
     if (edge && x == 0) {
-      const int s1 = md.ver ? left(y + 1) : above(y + 1), s0 = (int)B[0];
+      const int s1 = md.ver ? left(y + 1) : above(y + 1), s0 = B(0);
       v = clip_pel(v + ((s1 - s0) >> 1));
     }
     return v;
@@ -161,6 +163,11 @@ __device__ __forceinline__ int pred_sample(const int16_t *B, int n, int log2n, c
   const int dp = (y + 1) * md.angle, di = dp >> 5, f = dp & 31;
   if (f) return ((32 - f) * mainr(x + di + 1) + f * mainr(x + di + 2) + 16) >> 5;
   return mainr(x + di + 1);
+}
+
+__device__ __forceinline__ int pred_sample(const int16_t *B, int n, int log2n, const Mode &md, bool edge, int dc, int r,
+                                           int c) {
+  return pred_sample_f([&](int k) { return (int)B[k]; }, n, log2n, md, edge, dc, r, c);
 }
 
 __device__ __forceinline__ int dc_value(const int16_t *B, int n, int log2n) {
@@ -212,20 +219,18 @@ __global__ __launch_bounds__(64) void k_intra_pred(const uint8_t *__restrict__ r
 }
 
 // hvx_intra_search_batch: one wave per luma PU
-__global__ __launch_bounds__(64) void k_intra_search(const uint8_t *__restrict__ org, const uint8_t *__restrict__ rec,
-                                                     int stride, const hvx_intra_job *__restrict__ jobs, int n_jobs,
-                                                     const int32_t *__restrict__ eb,
-                                                     hvx_intra_search_result *__restrict__ out) {
+__device__ __forceinline__ void intra_search_pu(const uint8_t *__restrict__ org, const uint8_t *__restrict__ rec,
+                                                int stride, const hvx_intra_job *__restrict__ jobs, int n_jobs,
+                                                const int32_t *__restrict__ eb,
+                                                hvx_intra_search_result *__restrict__ out, int skip_small, int i) {
   using namespace intra;
   __shared__ Border s;
   __shared__ uint8_t so[64 * 64];
   __shared__ uint32_t satd[36];
   __shared__ int s_list[12], s_mpm[3];   // lane 0's candidate list in LDS (no dynamically indexed
   __shared__ double s_cc[10];            // private arrays -> no scratch)
-  const int i = blockIdx.x;
-  if (i >= n_jobs) return;
   const hvx_intra_job j = jobs[i];
-  if (!job_ok(j) || j.ch_type != 0) return;
+  if (!job_ok(j) || j.ch_type != 0 || (skip_small && j.log2_size <= 3)) return;  // 4x4/8x8: k_intra_search_lane
   const int log2n = j.log2_size, n = 1 << log2n, lane = lane_id();
   const uint8_t *po = org + (int64_t)j.y * stride + j.x;
   for (int k = lane; k < n * n; k += HVX_WAVE) so[k] = po[(k >> log2n) * stride + (k & (n - 1))];
@@ -332,4 +337,167 @@ __global__ __launch_bounds__(64) void k_intra_search(const uint8_t *__restrict__
   r.n_cand = (uint8_t)num;
   for (int k = 0; k < 11; k++) r.cand[k] = (uint8_t)(k < num ? list[k] : 0);
   for (int k = 0; k < 4; k++) r.pad_[k] = 0;
+}
+
+// one wave per PU, grid-stride over the jobs (so that the 4x4/8x8 jobs it skips cost a load each)
+__global__ __launch_bounds__(64) void k_intra_search(const uint8_t *__restrict__ org, const uint8_t *__restrict__ rec,
+                                                     int stride, const hvx_intra_job *__restrict__ jobs, int n_jobs,
+                                                     const int32_t *__restrict__ eb,
+                                                     hvx_intra_search_result *__restrict__ out, int skip_small) {
+  for (int i = blockIdx.x; i < n_jobs; i += gridDim.x) {
+    intra_search_pu(org, rec, stride, jobs, n_jobs, eb, out, skip_small, i);
+    __syncthreads();  // the LDS of this PU is rewritten by the next
+  }
+}
+
+// hvx_intra_search_batch for 4x4 and 8x8 luma PUs (75% of a picture's PUs): one PU per LANE.
+// The 35-mode loop is uniform across the wave (mode constants and the filtered/unfiltered choice
+// are per size), each lane predicts its own PU from its own border column in LDS ([k][lane]:
+// conflict-free), transforms in registers and ranks its candidates in registers: xUpdateCandList's
+// insertion as a fixed 9-slot network with static indices, so nothing is dynamically indexed.
+template <int LOG2N>
+__global__ __launch_bounds__(64) void k_intra_search_lane(const uint8_t *__restrict__ org, const uint8_t *__restrict__ rec,
+                                                          int stride, const hvx_intra_job *__restrict__ jobs, int n_jobs,
+                                                          const int32_t *__restrict__ eb,
+                                                          hvx_intra_search_result *__restrict__ out) {
+  using namespace intra;
+  constexpr int N = 1 << LOG2N, NB = 4 * N + 1, T = N == 4 ? 4 : 8;
+  __shared__ int16_t su[NB * 64], sf[NB * 64];
+  const int lane = lane_id(), i = blockIdx.x * 64 + lane;
+  const bool active = i < n_jobs;
+  const hvx_intra_job j = jobs[active ? i : n_jobs - 1];
+  const bool ok = active && job_ok(j) && j.ch_type == 0 && j.log2_size == LOG2N;
+  if (__ballot(ok) == 0) return;  // no job of this size in the wave (a mixed batch)
+  {  // the border (fillReferenceSamples, TComPattern.cpp:364-540) of this lane's PU, position by position
+    const uint8_t *p = rec + (int64_t)j.y * stride + j.x;
+    const int ulog2 = j.unit_log2, u = 1 << ulog2, nunits = ((4 * N) >> ulog2) + 1;
+    uint32_t a[3];
+    int navail = 0;
+#pragma unroll
+    for (int w = 0; w < 3; w++) {
+      const int lo = w * 32;
+      a[w] = nunits >= lo + 32 ? j.avail[w] : nunits > lo ? j.avail[w] & ((1u << (nunits - lo)) - 1u) : 0u;
+      navail += __popc(a[w]);
+    }
+    for (int k = 0; k < NB; k++) {
+      const int l = k == 0 ? 2 * N + u - 1 : k <= 2 * N ? 2 * N + u + k - 1 : 4 * N - k;
+      int v = 128;
+      if (navail && ok) {
+        const int uu = l >> ulog2;
+        if ((a[uu >> 5] >> (uu & 31)) & 1) v = line_raw(p, stride, N, u, l);
+        else {
+          const int jj = highest_below(a, uu);
+          v = jj >= 0 ? line_raw(p, stride, N, u, jj * u + u - 1) : line_raw(p, stride, N, u, lowest_above(a, uu) * u);
+        }
+      }
+      su[k * 64 + lane] = (int16_t)v;
+    }
+    for (int k = 0; k <= 4 * N; k++) {  // [1 2 1] smoothing (strong smoothing needs 32x32)
+      const int fk = f_index(N, k);
+      int v;
+      if (k == 0 || k == 4 * N) v = su[fk * 64 + lane];
+      else v = (su[f_index(N, k - 1) * 64 + lane] + 2 * su[fk * 64 + lane] + su[f_index(N, k + 1) * 64 + lane] + 2) >> 2;
+      sf[fk * 64 + lane] = (int16_t)v;
+    }
+  }
+  auto bu = [&](int k) { return (int)su[k * 64 + lane]; };
+  int dcs = 0;
+#pragma unroll
+  for (int k = 0; k < N; k++) dcs += bu(1 + k) + bu(2 * N + 1 + k);
+  const int dc = (dcs + N) >> (LOG2N + 1);
+  __shared__ uint8_t so[N * N * 64];  // the original block, [sample][lane]
+  {
+    const uint8_t *po = org + (int64_t)j.y * stride + j.x;
+    for (int y = 0; y < N; y++)
+      for (int x = 0; x < N; x++) so[(y * N + x) * 64 + lane] = ok ? po[y * stride + x] : 0;
+  }
+  // MPMs (getIntraDirPredictor, TComDataCU.cpp:1441-1478) and the rate constants
+  const int ld = j.left_dir, ad = j.above_dir;
+  int mp0, mp1, mp2, imode;
+  if (ld == ad) {
+    imode = 1;
+    if (ld > 1) { mp0 = ld; mp1 = ((ld + 29) % 32) + 2; mp2 = ((ld - 1) % 32) + 2; }
+    else { mp0 = 0; mp1 = 1; mp2 = 26; }
+  } else {
+    imode = 2;
+    mp0 = ld; mp1 = ad;
+    mp2 = (ld && ad) ? 0 : ((ld + ad) < 2 ? 26 : 1);
+  }
+  const bool fast = (j.flags & HVX_INTRA_FAST_MPM) != 0;
+  const int num = fast ? kNumRdMpm[LOG2N - 1] : kNumRdNoMpm[LOG2N - 1];  // 8 or 9
+  const uint64_t frac = (uint64_t)(uint32_t)j.frac_bits;
+  const int st = j.ctx_state & 127;
+  const uint64_t eb_mpm = (uint64_t)(uint32_t)eb[st ^ 1], eb_no = (uint64_t)(uint32_t)eb[st];
+  hvx_intra_search_result *r = out + (active ? i : 0);
+  double cc[9];
+  int cl[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) { cc[k] = 1.7976931348623157e308; cl[k] = 0; }
+  for (int m = 0; m < 35; m++) {  // uniform across the wave
+    const Mode md(m);
+    const int16_t *bp = use_filter(m, LOG2N, true) ? sf : su;
+    auto bb = [&](int k) { return (int)bp[k * 64 + lane]; };
+    uint32_t sum = 0;
+    int d[T][T];
+#pragma unroll
+    for (int y = 0; y < T; y++) {
+      int row[T];
+#pragma unroll
+      for (int x = 0; x < T; x++) {
+        const int pv = pred_sample_f(bb, N, LOG2N, md, true, dc, y, x);
+        row[x] = (int)so[(y * N + x) * 64 + lane] - pv;
+      }
+      if constexpr (T == 8) hadamard8(row, d[y]);
+      else hadamard4(row, d[y]);
+    }
+#pragma unroll
+    for (int x = 0; x < T; x++) {
+      int col[T], rr[T];
+#pragma unroll
+      for (int y = 0; y < T; y++) col[y] = d[y][x];
+      if constexpr (T == 8) hadamard8(col, rr);
+      else hadamard4(col, rr);
+#pragma unroll
+      for (int k = 0; k < T; k++) sum += (uint32_t)abs(rr[k]);
+    }
+    sum = T == 8 ? (sum + 2) >> 2 : (sum + 1) >> 1;  // xCalcHADs8x8 / xCalcHADs4x4
+    const int idx = m == mp0 ? 0 : m == mp1 ? 1 : m == mp2 ? 2 : -1;
+    const uint64_t total = frac + (idx >= 0 ? eb_mpm : eb_no) + 32768ull * (uint64_t)(idx < 0 ? 5 : idx ? 2 : 1);
+    const uint32_t bits = (uint32_t)(total >> 15);
+    const double cost = __dadd_rn((double)sum, __dmul_rn((double)bits, j.sqrt_lambda));
+      if (ok) { r->satd[m] = sum; r->mode_bits[m] = (uint8_t)bits; }
+    // xUpdateCandList (:5254) on the sorted `num` slots: the new entry goes after every entry it
+    // does not beat (strict '<'), the last one drops out
+    bool c[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) c[k] = k < num && cost < cc[k];
+#pragma unroll
+    for (int k = 8; k >= 0; k--)
+      if (c[k]) {
+        const bool from_prev = k > 0 && c[k - 1];
+        cc[k] = from_prev ? cc[k - 1] : cost;
+        cl[k] = from_prev ? cl[k - 1] : m;
+      }
+  }
+  if (!ok) return;  // inactive lanes and jobs of other sizes (another launch serves them)
+  r->num_rd = (uint8_t)num;
+#pragma unroll
+  for (int k = 0; k < 8; k++) r->cand_cost[k] = k < num ? cc[k] : 0.0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) r->cand[k] = (uint8_t)(k < num ? cl[k] : 0);
+  r->cand[9] = r->cand[10] = 0;
+  int n2 = num;
+  if (fast) {  // :2299-2321 (the MPMs are distinct, so an appended one never matches another)
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const int mq = q == 0 ? mp0 : q == 1 ? mp1 : mp2;
+      bool inc = q >= imode;
+#pragma unroll
+      for (int k = 0; k < 9; k++) inc |= k < num && mq == cl[k];
+      if (!inc) r->cand[n2++] = (uint8_t)mq;
+    }
+  }
+  r->n_cand = (uint8_t)n2;
+#pragma unroll
+  for (int k = 0; k < 4; k++) r->pad_[k] = 0;
 }

@@ -488,8 +488,14 @@ int hvx_intra_search_batch(hvx_ctx *ctx, const uint8_t *d_org, const uint8_t *d_
   if (!ctx || n < 0 || stride <= 0 || (n && (!d_org || !d_rec || !d_jobs || !d_entropy_bits || !d_out)))
     return fail(HVX_E_INVALID, "hvx_intra_search_batch: bad args");
   if (!n) return HVX_OK;
-  hipLaunchKernelGGL(k_intra_search, dim3(n), dim3(64), 0, ctx->stream, d_org, d_rec, stride, d_jobs, n,
-                     d_entropy_bits, d_out);
+  // 16x16..64x64 PUs: one wave per PU; 4x4 / 8x8 PUs: one PU per lane (each launch skips the
+  // other sizes' jobs)
+  hipLaunchKernelGGL(k_intra_search, dim3(n < 16384 ? n : 16384), dim3(64), 0, ctx->stream, d_org, d_rec, stride, d_jobs,
+                     n, d_entropy_bits, d_out, 1);
+  hipLaunchKernelGGL(k_intra_search_lane<2>, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, d_org, d_rec, stride, d_jobs,
+                     n, d_entropy_bits, d_out);
+  hipLaunchKernelGGL(k_intra_search_lane<3>, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, d_org, d_rec, stride, d_jobs,
+                     n, d_entropy_bits, d_out);
   return launched("k_intra_search");
 }
 
