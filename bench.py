@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-intra", action="store_true", help="skip the intra first-pass side measurement")
+    p.add_argument("--no-ssim", action="store_true", help="skip the SSIM-RDO side measurement")
     return p.parse_args()
 
 
@@ -198,11 +199,41 @@ def main():
             out["dpb_gather_ok"] = dpb_ok
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(planes, an, gpu_res, gpu_dec, gpu_rec, args)
+        if not args.no_ssim:
+            out["ssim_rdo"] = ssim_rdo_measure(cur_t, ref_ptrs, W, H, nref, args.steps)
         if not args.no_intra:
             out["intra_first_pass"] = intra_measure(cur_t, ref_t[0], W, H, float(an.params["lambda"][0]), args.steps)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def ssim_rdo_measure(cur_t, ref_ptrs, W, H, nref, steps):
+    """Side measurement (BASELINE config 4's RD cost, not the headline): the same picture step with
+    the SSIM CU decision (HVX_RD_SSIM: D = sum of 1 - SSIM over 8x8 blocks, lambda_2(qp)) at QP 22,
+    27, 32, 37 -- wall time per picture and the leaf CUs chosen (vs the SSE decision at that QP)."""
+    import torch
+    from video_codecs_amd import _abi, hvx
+    res = {}
+    recon, refpic = torch.zeros_like(cur_t), torch.zeros_like(cur_t)
+    for qp in (22, 27, 32, 37):
+        leaves = {}
+        for metric in (_abi.RD_SSIM, _abi.RD_SSE):
+            an = hvx.CtuAnalyzer(W, H, nref, qp, rd_metric=metric)
+            an.encode(cur_t, ref_ptrs, recon, refpic)
+            torch.cuda.synchronize()
+            if metric == _abi.RD_SSIM:
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    an.encode(cur_t, ref_ptrs, recon, refpic)
+                torch.cuda.synchronize()
+                ms = (time.perf_counter() - t0) / steps * 1e3
+            leaves[metric] = int(an.decisions()["leaf"].sum())
+            del an
+        res[str(qp)] = {"ms_per_picture": round(ms, 3), "ctus_per_s": round(((W + 63) // 64) * ((H + 63) // 64) / ms * 1e3, 1),
+                        "lambda_ssim": _abi.lambda_ssim(qp), "leaf_cus_ssim": leaves[_abi.RD_SSIM],
+                        "leaf_cus_sse": leaves[_abi.RD_SSE]}
+    return res
 
 
 def intra_measure(cur_t, rec_t, W, H, lam, steps):

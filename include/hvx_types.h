@@ -123,7 +123,16 @@ typedef struct hvx_ctu_params {
   int32_t slice_type;        /* HM SliceType (1 = P) */
   uint32_t lambda_motion;    /* floor(65536*sqrt(lambda)) */
   double lambda;             /* RD lambda (TComTrQuant m_dLambda for luma) */
+  double lambda_ssim;        /* HVX_RD_SSIM: the SSIM-RDO lambda (stvssim.c lambda_2 :1805 x attention eta^0.85) */
+  int32_t rd_metric;         /* hvx_ctu_decide's CU-level distortion: HVX_RD_SSE (HM) or HVX_RD_SSIM */
+  int32_t pad_;
 } hvx_ctu_params;
+/* HVX_RD_SSIM (BASELINE config 4): the CU quadtree decision of hvx_ctu_decide
+ * weighs D_ssim = sum over the CU's 8x8 blocks of 1 - SSIM(original, reconstruction) (compute_SSIM,
+ * stvssim.c:491, one 8x8 window; distortionSSIM :567) against lambda_ssim * bits, the stvssim RD
+ * form J = D + lambda * R (rdopt.c:1631); the TU-level residual decisions stay on SSE as in HM. */
+#define HVX_RD_SSE 0
+#define HVX_RD_SSIM 1
 
 typedef struct hvx_cu_result {
   int32_t valid;             /* CU inside the picture */
@@ -154,6 +163,8 @@ typedef struct hvx_cu_decision {
   int32_t split;             /* 1: the sub-tree rooted here splits (forced for CUs crossing the picture edge) */
   int32_t leaf;              /* 1: a leaf of the CTU's final CU tree (its samples are in the reconstruction) */
   int32_t cbf;               /* bit t: luma TU t of the CU is coded (0: qt_root_cbf 0, prediction only) */
+  float ssim_dist;           /* HVX_RD_SSIM: D_ssim of the CU as a leaf (8x8 blocks in raster order, float sum) */
+  float best_ssim_dist;      /* HVX_RD_SSIM: D_ssim of the chosen sub-tree (children in z-order) */
   int32_t pad_;
 } hvx_cu_decision;
 

@@ -1510,10 +1510,35 @@ static void leaf_eval(const decide_ctx *c, int ci, int S, int x, int y, hvx_cu_d
   o->cbf = cbf;
   o->bits = ex->me_bits[ci] + (uint32_t)((cbf ? r1 + tree : r0) >> 15);
   o->dist = dist;
+  o->ssim_dist = 0.0f;
+  if (c->p->rd_metric == HVX_RD_SSIM) {
+    /* D_ssim: distortionSSIM's 1 - compute_SSIM (stvssim.c:567-575) per 8x8 block of the CU (one
+     * 8x8 window each), summed in raster block order as float */
+    float dsum = 0.0f;
+    for (int by = 0; by < S / 8; by++)
+      for (int bx = 0; bx < S / 8; bx++) {
+        uint8_t rb[64];
+        for (int r = 0; r < 8; r++)
+          for (int q = 0; q < 8; q++) {
+            const int yy = by * 8 + r, xx = bx * 8 + q, t = (yy / T) * (S / T) + xx / T, k = ci * 4096 + yy * 64 + xx;
+            rb[r * 8 + q] = (uint8_t)clip_pel(ex->pred[k] + (((cbf >> t) & 1) ? ex->rres[k] : 0));
+          }
+        const float sv = hvxo_ssim(c->cur + (y + by * 8) * c->stride + x + bx * 8, c->stride, rb, 8, 8, 8, 8, 8);
+        dsum += 1.0f - sv;
+      }
+    o->ssim_dist = dsum;
+  }
+}
+
+/* the CU-level RD cost: calcRdCost for HVX_RD_SSE; D_ssim + lambda_ssim * R for HVX_RD_SSIM
+ * (stvssim's J = D + lambda R, rdopt.c:1631) */
+static double cu_cost(const hvx_ctu_params *p, uint32_t bits, uint32_t dist, float sdist) {
+  if (p->rd_metric == HVX_RD_SSIM) return (double)sdist + p->lambda_ssim * (double)bits;
+  return rd_cost(bits, dist, p->lambda);
 }
 
 /* returns 0 if the CU lies wholly outside the picture; else fills bits and dist of its best tree */
-static int decide_node(decide_ctx *c, int d, int j, uint32_t *bits, uint32_t *dist) {
+static int decide_node(decide_ctx *c, int d, int j, uint32_t *bits, uint32_t *dist, float *sdist) {
   static const int base[4] = {0, 1, 5, 21};
   const int g = 1 << d, S = 64 >> d, cx = j % g, cy = j / g, ci = base[d] + j;
   const int x = c->ctu_x * 64 + cx * S, y = c->ctu_y * 64 + cy * S;
@@ -1522,31 +1547,37 @@ static int decide_node(decide_ctx *c, int d, int j, uint32_t *bits, uint32_t *di
   hvx_cu_decision *o = &c->dec[ci];
   const int valid = c->cu[ci].valid;
   uint32_t lb = 0, ld = 0;
+  float ls = 0.0f;
   if (valid) {
     leaf_eval(c, ci, S, x, y, o);
     lb = o->bits + (d < 3 ? split_flag_bits(c, d, x8, y8, 0) : 0);
     ld = o->dist;
+    ls = o->ssim_dist;
   }
   int split = !valid;
   uint32_t sb = 0, sd = 0;
+  float ss = 0.0f;
   if (d < 3) {
     for (int k = 0; k < 4; k++) {
       uint32_t b, dd;
+      float sv;
       const int cj = (2 * cy + (k >> 1)) * (2 * g) + 2 * cx + (k & 1);
-      if (decide_node(c, d + 1, cj, &b, &dd)) { sb += b; sd += dd; }
+      if (decide_node(c, d + 1, cj, &b, &dd, &sv)) { sb += b; sd += dd; ss += sv; }
     }
     if (valid) sb += split_flag_bits(c, d, x8, y8, 1); /* no split flag at a boundary CU */
-    if (valid && rd_cost(sb, sd, c->p->lambda) < rd_cost(lb, ld, c->p->lambda)) split = 1;
+    if (valid && cu_cost(c->p, sb, sd, ss) < cu_cost(c->p, lb, ld, ls)) split = 1;
   }
   o->split = split;
   o->best_bits = split ? sb : lb;
   o->best_dist = split ? sd : ld;
+  o->best_ssim_dist = split ? ss : ls;
   if (!split) {
     for (int yy = 0; yy < n8; yy++)
       for (int xx = 0; xx < n8; xx++) c->depth[y8 + yy][x8 + xx] = (uint8_t)d;
   }
   *bits = o->best_bits;
   *dist = o->best_dist;
+  *sdist = o->best_ssim_dist;
   return 1;
 }
 
@@ -1565,7 +1596,8 @@ void hvxo_ctu_decide(const uint8_t *cur, const uint8_t *const *refs, int stride,
   c.cur = cur; c.stride = stride;
   memset(out_dec, 0, sizeof(hvx_cu_decision) * HVX_CUS_PER_CTU);
   uint32_t b, d;
-  decide_node(&c, 0, 0, &b, &d);
+  float sd;
+  decide_node(&c, 0, 0, &b, &d, &sd);
   static const int base[4] = {0, 1, 5, 21};
   /* the final tree, top-down: a CU is a leaf when it is reached (the root, or a child of a
    * reached CU that splits), lies in the picture and does not split itself */

@@ -227,14 +227,14 @@ def check_ctu_pass(seed, width, height, nref, qp, max_ctus=None):
     return n
 
 
-def check_ctu_decide(seed, width, height, nref, qp, fused=False):
+def check_ctu_decide(seed, width, height, nref, qp, fused=False, rd_metric=0):
     """hvx_ctu_analyze + hvx_ctu_decide over a whole picture vs hvxo_ctu_decide per CTU: CU
     results, decision records and the reconstructed picture incl. its extended border (bit-exact)."""
     torch = _torch()
     cur = padded_plane(make_yuv.random_frame(width, height, seed)[:width * height].reshape(height, width))
     refs = [padded_plane((make_yuv.smooth_frame if k % 2 else make_yuv.random_frame)(width, height, seed + 10 + k)
                          [:width * height].reshape(height, width)) for k in range(nref)]
-    an = hvx.CtuAnalyzer(width, height, nref, qp)
+    an = hvx.CtuAnalyzer(width, height, nref, qp, rd_metric=rd_metric)
     cur_t = torch.from_numpy(cur).cuda()
     ref_t = [torch.from_numpy(r).cuda() for r in refs]
     ptrs = torch.tensor([hvx.plane_origin_ptr(t, width) for t in ref_t], dtype=torch.int64).cuda()

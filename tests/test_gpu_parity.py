@@ -245,3 +245,12 @@ def test_deblock_golden_gpu(torch):
 def test_deblock_random_gpu(torch):
     # 1080p random BS / QP maps and offsets vs the oracle; plane borders must stay untouched
     assert gpu_cases.check_deblock_random(seed=41) > 10000
+
+
+def test_ctu_decide_ssim_rdo_gpu(torch):
+    # HVX_RD_SSIM (BASELINE config 4's SSIM RD cost): D_ssim per 8x8 block (compute_SSIM floats) and
+    # lambda_2 in the CU quadtree decision, QP 22 and 37, bit-exact vs the oracle incl. the float sums
+    for qp in (22, 37):
+        n, leaves = gpu_cases.check_ctu_decide(seed=9 + qp, width=256, height=136, nref=2, qp=qp, fused=True,
+                                               rd_metric=hvx._abi.RD_SSIM)
+        assert n == 12 and leaves >= 12

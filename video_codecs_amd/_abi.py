@@ -32,8 +32,10 @@ assert ME_RESULT.itemsize == 48
 ME_FEN, ME_HADME, ME_SMOOTHMV, ME_BI = 1, 2, 4, 8
 
 CTU_PARAMS = np.dtype([("pic_w", "<i4"), ("pic_h", "<i4"), ("n_ref", "<i4"), ("qp", "<i4"), ("search_range", "<i4"),
-                       ("me_flags", "<i4"), ("slice_type", "<i4"), ("lambda_motion", "<u4"), ("lambda", "<f8")], align=True)
-assert CTU_PARAMS.itemsize == 40
+                       ("me_flags", "<i4"), ("slice_type", "<i4"), ("lambda_motion", "<u4"), ("lambda", "<f8"),
+                       ("lambda_ssim", "<f8"), ("rd_metric", "<i4"), ("pad_", "<i4")], align=True)
+assert CTU_PARAMS.itemsize == 56
+RD_SSE, RD_SSIM = 0, 1
 CU_RESULT = np.dtype([("valid", "<i4"), ("ref", "<i4"), ("mv_x", "<i4"), ("mv_y", "<i4"), ("me_cost", "<u4"),
                       ("sse", "<u4"), ("abs_sum", "<i4"), ("n_tu", "<i4")])
 assert CU_RESULT.itemsize == 32
@@ -47,9 +49,21 @@ def load_estbits_p_luma():
     return np.fromfile(p, dtype="<i4").reshape(4, ESTBITS_INTS)
 
 
-def ctu_params(pic_w, pic_h, n_ref, qp, lam=None, search_range=64, slice_type=1):
-    """HM-style P-slice parameters; lambda defaults to 0.57*2^((qp-12)/3) (TEncSlice::initEncSlice form)."""
+def lambda_ssim(qp, eta=1.0):
+    """The SSIM-RDO lambda of stvssim.c: lambda_2 (:1782-1806, active form :1805)
+    -a1*b2*exp(b1*(qp-15)), times the attention weight eta^0.85 (adjust_lambda :1707)."""
+    import math
+    a1, b2, b1 = 5.883060266548170e-3, -2.229472265847692e-2, 9.279543980380707e-2
+    lam = -a1 * b2 * math.exp(b1 * (qp - 15))
+    return lam * math.pow(eta, 0.85) if eta != 1.0 else lam
+
+
+def ctu_params(pic_w, pic_h, n_ref, qp, lam=None, search_range=64, slice_type=1, rd_metric=0, lam_ssim=None):
+    """HM-style P-slice parameters; lambda defaults to 0.57*2^((qp-12)/3) (TEncSlice::initEncSlice form).
+    rd_metric RD_SSIM selects the SSIM CU decision with lambda_ssim(qp) unless lam_ssim is given."""
     p = np.zeros(1, CTU_PARAMS)
+    p["rd_metric"] = rd_metric
+    p["lambda_ssim"] = lambda_ssim(qp) if lam_ssim is None else lam_ssim
     lam = 0.57 * 2.0 ** ((qp - 12) / 3.0) if lam is None else lam
     p["pic_w"], p["pic_h"], p["n_ref"], p["qp"] = pic_w, pic_h, n_ref, qp
     p["search_range"], p["me_flags"], p["slice_type"] = search_range, ME_FEN | ME_HADME | ME_SMOOTHMV, slice_type
@@ -79,8 +93,9 @@ NUM_CTX = 202
 
 # hvx_cu_decision (hvx_types.h)
 CU_DECISION = np.dtype([("coef_frac", "<u8"), ("bits", "<u4"), ("dist", "<u4"), ("best_bits", "<u4"),
-                        ("best_dist", "<u4"), ("split", "<i4"), ("leaf", "<i4"), ("cbf", "<i4"), ("pad_", "<i4")])
-assert CU_DECISION.itemsize == 40
+                        ("best_dist", "<u4"), ("split", "<i4"), ("leaf", "<i4"), ("cbf", "<i4"), ("ssim_dist", "<f4"),
+                        ("best_ssim_dist", "<f4"), ("pad_", "<i4")])
+assert CU_DECISION.itemsize == 48
 
 
 def load_ctx_p_states():

@@ -176,7 +176,15 @@ struct DecideArgs {
   const uint8_t *st;          // the context snapshot (split flag 0..2, luma qt_cbf 28.., qt_root_cbf 41)
   const int32_t *eb;
   hvx_cu_decision *dec;
+  int metric;                 // HVX_RD_SSE / HVX_RD_SSIM
+  double lambda_ssim;
 };
+
+// the CU-level RD cost (hvxo's cu_cost): calcRdCost, or D_ssim + lambda_ssim * R
+__device__ __forceinline__ double dec_cu_cost(const DecideArgs &A, uint32_t bits, uint32_t dist, float sdist) {
+  if (A.metric == HVX_RD_SSIM) return __dadd_rn((double)sdist, __dmul_rn(A.lambda_ssim, (double)bits));
+  return floor((double)dist + (double)bits * A.lambda + 0.5);
+}
 
 __device__ __forceinline__ double dec_rd_cost(uint32_t bits, uint32_t dist, double lambda) {
   return floor((double)dist + (double)bits * lambda + 0.5);
@@ -198,7 +206,8 @@ struct DepthMap {
 };
 
 template <int D>
-__device__ bool dec_node(const DecideArgs &A, int ctu, int cx, int cy, DepthMap &dm, uint32_t &bits, uint32_t &dist) {
+__device__ bool dec_node(const DecideArgs &A, int ctu, int cx, int cy, DepthMap &dm, uint32_t &bits, uint32_t &dist,
+                         float &sdist) {
   constexpr int g = 1 << D, S = 64 >> D, n8 = S / 8;
   const int j = cy * g + cx, ci = (D == 0 ? 0 : D == 1 ? 1 : D == 2 ? 5 : 21) + j;
   const int x = (ctu % A.L.nctu_x) * 64 + cx * S, y = (ctu / A.L.nctu_x) * 64 + cy * S;
@@ -207,35 +216,42 @@ __device__ bool dec_node(const DecideArgs &A, int ctu, int cx, int cy, DepthMap 
   const size_t cuid = (size_t)ctu * HVX_CUS_PER_CTU + ci;
   const hvx_cu_result cu = A.cu[cuid];
   hvx_cu_decision o;
-  o.coef_frac = 0; o.bits = 0; o.dist = 0; o.leaf = 0; o.cbf = 0; o.pad_ = 0;
+  o.coef_frac = 0; o.bits = 0; o.dist = 0; o.leaf = 0; o.cbf = 0; o.pad_ = 0; o.best_ssim_dist = 0.0f;
   const int ctx = (x8 > 0 && dm.at(x8 - 1, y8) > D) + (y8 > 0 && dm.at(x8, y8 - 1) > D);
   const int sfs = D < 3 ? A.st[ctx] : 0;
   uint32_t lb = 0, ld = 0;
+  float ls = 0.0f;
+  o.ssim_dist = 0.0f;
   if (cu.valid) {
     const hvx_cu_decision lf = A.dec[cuid];  // the leaf evaluation (k_ctu_leaf)
-    o.coef_frac = lf.coef_frac; o.bits = lf.bits; o.dist = lf.dist; o.cbf = lf.cbf;
+    o.coef_frac = lf.coef_frac; o.bits = lf.bits; o.dist = lf.dist; o.cbf = lf.cbf; o.ssim_dist = lf.ssim_dist;
     lb = o.bits + (D < 3 ? ((uint32_t)A.eb[sfs ^ 0] >> 15) : 0u);
     ld = o.dist;
+    ls = o.ssim_dist;
   }
   bool split = !cu.valid;
   uint32_t sb = 0, sd = 0;
+  float ss = 0.0f;
   if constexpr (D < 3) {
     for (int k = 0; k < 4; k++) {
       uint32_t b, dd;
-      if (dec_node<D + 1>(A, ctu, 2 * cx + (k & 1), 2 * cy + (k >> 1), dm, b, dd)) { sb += b; sd += dd; }
+      float sv;
+      if (dec_node<D + 1>(A, ctu, 2 * cx + (k & 1), 2 * cy + (k >> 1), dm, b, dd, sv)) { sb += b; sd += dd; ss += sv; }
     }
     if (cu.valid) {
       sb += (uint32_t)A.eb[sfs ^ 1] >> 15;
-      if (dec_rd_cost(sb, sd, A.lambda) < dec_rd_cost(lb, ld, A.lambda)) split = true;
+      if (dec_cu_cost(A, sb, sd, ss) < dec_cu_cost(A, lb, ld, ls)) split = true;
     }
   }
   o.split = split;
   o.best_bits = split ? sb : lb;
   o.best_dist = split ? sd : ld;
+  o.best_ssim_dist = split ? ss : ls;
   if (!split) dm.fill(x8, y8, n8, D);
   A.dec[cuid] = o;
   bits = o.best_bits;
   dist = o.best_dist;
+  sdist = o.best_ssim_dist;
   return true;
 }
 
@@ -295,12 +311,44 @@ __global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const uint8_t *__
     part += (uint32_t)((org - v) * (org - v));
   }
   const uint32_t dist = wave_sum_u32(part);
+  // HVX_RD_SSIM: D_ssim = sum over the CU's 8x8 blocks (raster order) of 1 - SSIM(org, rec), one
+  // block per lane with compute_SSIM's float operations in its order (stvssim.c:506-545)
+  __shared__ float sdist[64];
+  float dsum = 0.0f;
+  if (A.metric == HVX_RD_SSIM) {
+    const int nb8 = S / 8;
+    if (lane < nb8 * nb8) {
+      const int by = lane / nb8, bx = lane - by * nb8;
+      const float C1 = 0.01f * 0.01f * (float)(255 * 255), C2 = 0.03f * 0.03f * (float)(255 * 255);
+      const float wgt = 1.0f / (float)(8 * 8);
+      float mo = 0, me = 0, vo = 0, ve = 0, cov = 0;
+      for (int n = 0; n < 8; n++)
+        for (int m = 0; m < 8; m++) {
+          const int yy = by * 8 + n, xx = bx * 8 + m, t = (yy / T) * (S / T) + xx / T;
+          const int64_t o = ctu_tu_offset(A.L, ctu_tu_index(A.L, ctu, d, j, t)) + (yy % T) * T + (xx % T);
+          const int po = cur[(y + yy) * stride + x + xx];
+          const int pe = clip_pel(po - resid[o] + (((cbf >> t) & 1) ? res_out[o] : 0));
+          mo += wgt * po; me += wgt * pe;
+          vo += wgt * po * po; ve += wgt * pe * pe; cov += wgt * po * pe;
+        }
+      const float varo = fabsf(vo - mo * mo), vare = fabsf(ve - me * me), covo = fabsf(cov - mo * me);
+      float sv = (float)((2.0 * mo * me + C1) * (2.0 * covo + C2));
+      sv /= (float)(mo * mo + me * me + C1) * (varo + vare + C2);
+      sv /= 1.0f;  // one window (compute_SSIM's dist /= cnt)
+      if (sv >= 1.0 && sv < 1.01) sv = 1.0f;
+      sdist[lane] = 1.0f - sv;
+    }
+    __syncthreads();
+    if (lane == 0)
+      for (int b = 0; b < nb8 * nb8; b++) dsum += sdist[b];
+  }
   if (lane == 0) {
     hvx_cu_decision &r = A.dec[cuid];
     r.coef_frac = cf;
     r.cbf = cbf;
     r.dist = dist;
     r.bits = A.res[(size_t)cuid * A.L.nref + cu.ref].bits + (uint32_t)((cbf ? r1 + tree : r0) >> 15);
+    r.ssim_dist = dsum;
   }
 }
 
@@ -312,11 +360,12 @@ __global__ __launch_bounds__(64) void k_ctu_decide(DecideArgs A) {
     int d, j, S, g;
     cu_geom(ci, d, j, S, g);
     const int x = (ctu % A.L.nctu_x) * 64 + (j % g) * S, y = (ctu / A.L.nctu_x) * 64 + (j / g) * S;
-    if (x >= A.pic_w || y >= A.pic_h) A.dec[(size_t)ctu * HVX_CUS_PER_CTU + ci] = hvx_cu_decision{0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (x >= A.pic_w || y >= A.pic_h) A.dec[(size_t)ctu * HVX_CUS_PER_CTU + ci] = hvx_cu_decision{0, 0, 0, 0, 0, 0, 0, 0, 0.0f, 0.0f, 0};
   }
   DepthMap dm;
   uint32_t b, d;
-  dec_node<0>(A, ctu, 0, 0, dm, b, d);
+  float sd;
+  dec_node<0>(A, ctu, 0, 0, dm, b, d, sd);
   // the final tree, top-down: leaf = reached (root, or child of a reached splitting CU), in the
   // picture, not splitting; reached set as an 85-bit mask
   uint64_t r_lo = 1, r_hi = 0;

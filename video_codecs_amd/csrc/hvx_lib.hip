@@ -768,7 +768,7 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
     return fail(HVX_E_INVALID, "hvx_ctu_decide: NULL argument");
   const hvx_ctu_params P = *h_params;
   if (P.pic_w <= 0 || P.pic_h <= 0 || P.pic_w % 8 || P.pic_h % 8 || P.n_ref <= 0 || P.n_ref > 8 ||
-      stride < P.pic_w + 2 * HVX_PLANE_MARGIN || stride % 4 != 0)
+      stride < P.pic_w + 2 * HVX_PLANE_MARGIN || stride % 4 != 0 || (P.rd_metric != HVX_RD_SSE && P.rd_metric != HVX_RD_SSIM))
     return fail(HVX_E_INVALID, "hvx_ctu_decide: bad parameters");
   const CtuLayout L = ctu_layout(P.pic_w, P.pic_h, P.n_ref);
   const CtuWs W = ctu_ws_layout(L);
@@ -798,6 +798,7 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
   A.L = L; A.pic_w = P.pic_w; A.pic_h = P.pic_h; A.lambda = P.lambda;
   A.cu = d_cu; A.res = (const hvx_me_result *)(ws + W.res); A.cb = cb;
   A.st = d_ctx_states; A.eb = d_entropy_bits; A.dec = d_dec;
+  A.metric = P.rd_metric; A.lambda_ssim = P.lambda_ssim;
   hipLaunchKernelGGL(k_ctu_leaf, dim3(n * HVX_CUS_PER_CTU), dim3(64), 0, st, A, d_cur, stride, (const int16_t *)(ws + W.resid),
                      (const int16_t *)(ws + W.res_out), (const int32_t *)(ws + W.abs), (const uint32_t *)(ws + W.sse));
   hipLaunchKernelGGL(k_ctu_decide, dim3((n + 63) / 64), dim3(64), 0, st, A);

@@ -231,9 +231,9 @@ def ctu_workspace_size(pic_w, pic_h, n_ref):
 class CtuAnalyzer:
     """Device-resident CTU analysis pass (hvx_ctu_analyze) for one picture geometry."""
 
-    def __init__(self, pic_w, pic_h, n_ref, qp, lam=None, est4=None):
+    def __init__(self, pic_w, pic_h, n_ref, qp, lam=None, est4=None, rd_metric=_abi.RD_SSE):
         import torch
-        self.params = _abi.ctu_params(pic_w, pic_h, n_ref, qp, lam)
+        self.params = _abi.ctu_params(pic_w, pic_h, n_ref, qp, lam, rd_metric=rd_metric)
         self.pic_w, self.pic_h, self.n_ref = pic_w, pic_h, n_ref
         self.stride = pic_w + 2 * _abi.PLANE_MARGIN
         self.nctu = ((pic_w + 63) // 64) * ((pic_h + 63) // 64)
