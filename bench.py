@@ -199,9 +199,9 @@ def main():
             out["dpb_gather_ok"] = dpb_ok
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(planes, an, gpu_res, gpu_dec, gpu_rec, args)
-        if not args.no_ssim:
+        if world == 1 and not args.no_ssim:  # side measurements: single-GPU runs only
             out["ssim_rdo"] = ssim_rdo_measure(cur_t, ref_ptrs, W, H, nref, args.steps)
-        if not args.no_intra:
+        if world == 1 and not args.no_intra:
             out["intra_first_pass"] = intra_measure(cur_t, ref_t[0], W, H, float(an.params["lambda"][0]), args.steps)
         print(json.dumps(out), flush=True)
     if world > 1:
