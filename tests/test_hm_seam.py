@@ -1,7 +1,8 @@
 """End-to-end drop-in check: the UNCHANGED reference TAppEncoder (HM-16.5rc1), with every
 TComTrQuant::transformNxN / invTransformNxN call (integration/hm_tu_seam.cpp), every
 TComPrediction::motionCompensation call (hm_mc_seam.cpp) and every TEncSearch::xMotionEstimation
-call (hm_me_seam.cpp) and every picture's TComLoopFilter::loopFilterPic (hm_lf_seam.cpp) served by
+call (hm_me_seam.cpp), every picture's TComLoopFilter::loopFilterPic (hm_lf_seam.cpp) and, in the
+intra encodes, every TComPrediction::predIntraAng call (hm_intra_seam.cpp) served by
 libhvx.so on the MI355X, must produce the same bitstream and
 reconstruction MD5 as the reference CPU build (tests/hm_seam/expected_md5.json, recorded by
 make_expected.py)."""
@@ -23,12 +24,15 @@ EXPECTED = json.load(open(os.path.join(ROOT, "tests", "hm_seam", "expected_md5.j
 @pytest.mark.gpu
 @pytest.mark.timeout(600)  # ~1M synchronous per-call offloads per encode: correctness, not speed
 @pytest.mark.parametrize("case", sorted(mk.CASES))
-def test_hm_encoder_with_hvx_seams(case):
+def test_hm_encoder_with_hvx_seams(case, monkeypatch):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     if not os.path.exists(EXE):
         pytest.skip("TAppEncoder_hvx not built (needs /root/reference at build time)")
+    intra = case.startswith("intra")
+    # the intra prediction seam (hm_intra_seam.cpp) serves the intra-only encodes
+    monkeypatch.setenv("HVX_SEAM_INTRA", "1" if intra else "0")
     log = []
     with tempfile.TemporaryDirectory() as tmp:
         got = mk.encode(EXE, case, tmp, log)
@@ -43,6 +47,9 @@ def test_hm_encoder_with_hvx_seams(case):
     # every picture's deblocking ran on the device (hm_lf_seam.cpp, hvx_deblock)
     m = re.search(r"hm_lf_seam: (\d+) pictures deblocked by libhvx, (\d+) fell through", log[0])
     assert m and int(m.group(1)) == mk.CASES[case][2] and int(m.group(2)) == 0, log[0][-2000:]
+    if intra:  # every intra prediction of the encode ran on the device
+        m = re.search(r"hm_intra_seam: (\d+) predIntraAng calls served by libhvx, (\d+) fell through", log[0])
+        assert m and int(m.group(1)) > 100000 and int(m.group(2)) == 0, log[0][-2000:]
 
 
 def test_expected_md5_cases_present():
