@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-intra", action="store_true", help="skip the intra first-pass side measurement")
     p.add_argument("--no-ssim", action="store_true", help="skip the SSIM-RDO side measurement")
+    p.add_argument("--no-1080p", action="store_true", help="skip the 1080p side measurement")
     return p.parse_args()
 
 
@@ -54,9 +55,8 @@ def b_ctu_luma(nref):
 
 
 def luma_plane(w, h, index):
-    from oracle import make_yuv  # synthetic-input recipe
-    y = make_yuv.random_frame(w, h, index)[: w * h].reshape(h, w)
-    return np.pad(y, 80, mode="edge")
+    from video_codecs_amd import synth  # synthetic-input recipe
+    return synth.luma_plane(w, h, index)
 
 
 def segment_frames(rank, nref):
@@ -199,13 +199,36 @@ def main():
             out["dpb_gather_ok"] = dpb_ok
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(planes, an, gpu_res, gpu_dec, gpu_rec, args)
-        if world == 1 and not args.no_ssim:  # side measurements: single-GPU runs only
+        if world == 1 and not args.no_1080p:  # side measurements: single-GPU runs only
+            out["step_1080p"] = step_1080p_measure(nref, args.qp, args.steps)
+        if world == 1 and not args.no_ssim:
             out["ssim_rdo"] = ssim_rdo_measure(cur_t, ref_ptrs, W, H, nref, args.steps)
         if world == 1 and not args.no_intra:
             out["intra_first_pass"] = intra_measure(cur_t, ref_t[0], W, H, float(an.params["lambda"][0]), args.steps)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def step_1080p_measure(nref, qp, steps):
+    """Side measurement (BASELINE configs 2-3 geometry, not the headline): the same picture step on a
+    1920x1080 picture (510 CTUs, the bottom CTU row 56 lines high) -- CTUs/s and ms per picture."""
+    import torch
+    from video_codecs_amd import hvx
+    W, H = 1920, 1080
+    planes = [torch.from_numpy(luma_plane(W, H, 100 + f)).cuda() for f in range(nref + 1)]
+    ptrs = torch.tensor([hvx.plane_origin_ptr(t, W) for t in planes[:nref]], dtype=torch.int64).cuda()
+    an = hvx.CtuAnalyzer(W, H, nref, qp)
+    recon, refpic = torch.zeros_like(planes[nref]), torch.zeros_like(planes[nref])
+    an.encode(planes[nref], ptrs, recon, refpic)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        an.encode(planes[nref], ptrs, recon, refpic)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    return {"resolution": f"{W}x{H}", "ctus_per_frame": an.nctu, "ms_per_picture": round(ms, 3),
+            "ctus_per_s": round(an.nctu / ms * 1e3, 1)}
 
 
 def ssim_rdo_measure(cur_t, ref_ptrs, W, H, nref, steps):

@@ -241,3 +241,19 @@ def test_oracle_ctu_decide_ssim_mode():
         assert abs(float(dec[0]["best_ssim_dist"]) - float(dec["ssim_dist"][leaves].sum())) < 1e-3
         n_leaves.append(len(leaves))
     assert n_leaves[1] <= n_leaves[0]
+
+
+def test_new_entry_points_reject_bad_arguments_without_a_gpu():
+    # argument validation happens before any device work: NULL context / pointers and out-of-range
+    # deblocking parameters fail with HVX_E_INVALID and a message (HM-style fail-fast callers abort)
+    import ctypes
+    L = ctypes.CDLL(os.path.join(ROOT, "video_codecs_amd", "libhvx.so"))
+    L.hvx_last_error.restype = ctypes.c_char_p
+    E_INVALID = -1
+    P = ctypes.c_void_p
+    assert L.hvx_intra_pred_batch(P(0), P(0), 64, P(0), 1, P(0), P(0), P(0)) == E_INVALID
+    assert b"hvx_intra_pred_batch" in L.hvx_last_error()
+    assert L.hvx_intra_search_batch(P(0), P(0), P(0), 64, P(0), 1, P(0), P(0)) == E_INVALID
+    assert L.hvx_deblock(P(0), P(0), 64, P(0), P(0), 32, P(0), P(0), P(0), P(0)) == E_INVALID
+    assert b"hvx_deblock" in L.hvx_last_error()
+    assert L.hvx_ctu_decide(P(0), P(0), 0, P(0), P(0), P(0), P(0), ctypes.c_size_t(0), P(0), P(0), P(0), P(0)) == E_INVALID

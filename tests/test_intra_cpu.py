@@ -33,3 +33,11 @@ def test_ctu_boundaries_64x64():
     assert f[1] == [0] * 16 + [1] * 16 + [0] * 33                 # left CTU only
     assert f[4] == [0] * 16 + [1] * 16 + [1] + [1] * 16 + [1] * 16  # CTU (1,1): left, corner, above, above-right
     assert f[5] == [0] * 16 + [1] * 16 + [1] + [1] * 16 + [0] * 16  # right edge: no above-right
+
+
+def test_bench_input_recipe_matches_oracle_generator():
+    # bench.py draws its pictures from video_codecs_amd.synth; the tests' oracle/make_yuv must agree
+    from oracle import make_yuv
+    from video_codecs_amd import synth
+    for idx in (0, 3, 17):
+        np.testing.assert_array_equal(synth.random_frame(96, 64, idx), make_yuv.random_frame(96, 64, idx))

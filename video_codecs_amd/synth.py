@@ -1,0 +1,26 @@
+"""Synthetic bench input: splitmix64 seeded 0x5EED0000 + frame index, every
+sample the top byte (x >> 56) of the next draw, Y then Cb then Cr (8-bit 4:2:0).  The bench's own
+copy of the recipe, so the measured path imports nothing from oracle/ (tests check that the two
+generators agree)."""
+import numpy as np
+
+
+def splitmix64_stream(seed, n):
+    """n successive splitmix64 outputs (uint64) from state `seed`."""
+    with np.errstate(over="ignore"):
+        k = np.arange(1, n + 1, dtype=np.uint64)
+        z = np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def random_frame(w, h, index):
+    """One w x h 4:2:0 frame, planar Y | Cb | Cr bytes."""
+    return (splitmix64_stream(0x5EED0000 + index, w * h * 3 // 2) >> np.uint64(56)).astype(np.uint8)
+
+
+def luma_plane(w, h, index, margin=80):
+    """The frame's luma as an 8-bit padded plane (HVX_PLANE_MARGIN border, edges replicated)."""
+    y = random_frame(w, h, index)[: w * h].reshape(h, w)
+    return np.pad(y, margin, mode="edge")
