@@ -26,8 +26,8 @@ struct hvx_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   // hvx_ctu_analyze runs its independent branches on two more streams (fork/join events)
-  hipStream_t aux[2] = {};
-  hipEvent_t fj[5] = {};
+  hipStream_t aux[3] = {};
+  hipEvent_t fj[7] = {};
   // optional per-phase timing of hvx_ctu_analyze: a begin/end event pair on the launch's own
   // stream around every timed launch, folded into phase_ms[phase] (phases may overlap)
   int timing = 0;
@@ -217,7 +217,7 @@ static void tu_class_launch(hipStream_t st, const hvx_tu_desc *desc, const hvx_e
                             const int64_t *off, int n, const int16_t *res_in, int32_t *temp, int32_t *lev, int32_t *arl,
                             int32_t *abs_sum, int16_t *res_out, uint32_t *sse, int32_t *coefI, int32_t *levI,
                             int32_t *stI, int8_t *flags, int G, int n_est_lds, hvx_ctx *tctx = nullptr,
-                            int phase0 = 0) {
+                            int phase0 = 0, hipEvent_t after_rdoq = nullptr) {
   int k = t_begin(tctx, st, phase0);
   hipLaunchKernelGGL((k_tu_fwd<L>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, temp, arl, coefI, levI, abs_sum, flags, G);
   t_end(tctx, st, k);
@@ -225,6 +225,7 @@ static void tu_class_launch(hipStream_t st, const hvx_tu_desc *desc, const hvx_e
   hipLaunchKernelGGL((k_tu_rdoq<L>), dim3((n + G - 1) / G), dim3(64), 0, st, desc, est, est_idx, n, coefI, levI, stI,
                      abs_sum, flags, G, n_est_lds);
   t_end(tctx, st, k);
+  if (after_rdoq) (void)hipEventRecord(after_rdoq, st);  // the levels are final: their rate may be counted beside k_tu_fin
   k = t_begin(tctx, st, phase0 + 2);
   hipLaunchKernelGGL((k_tu_fin<L, MODE>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, levI, lev, res_out, sse, G);
   t_end(tctx, st, k);
@@ -297,8 +298,8 @@ int hvx_create(int device, hvx_ctx **out) {
   // they dispatch ahead of the ME kernels' backlog instead of waiting behind it
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
-  for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipStreamCreateWithPriority(&c->aux[i], hipStreamNonBlocking, prio_hi);
-  for (int i = 0; i < 5 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&c->fj[i], hipEventDisableTiming);
+  for (int i = 0; i < 3 && e == hipSuccess; i++) e = hipStreamCreateWithPriority(&c->aux[i], hipStreamNonBlocking, prio_hi);
+  for (int i = 0; i < 7 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&c->fj[i], hipEventDisableTiming);
   if (e != hipSuccess) { hvx_destroy(c); return hip_fail(e, "hvx_create: streams/events"); }
   *out = c;
   return HVX_OK;
@@ -310,9 +311,9 @@ int hvx_destroy(hvx_ctx *ctx) {
   if (ctx->tu_scr) (void)hipFree(ctx->tu_scr);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
-  for (int i = 0; i < 2; i++)
+  for (int i = 0; i < 3; i++)
     if (ctx->aux[i]) (void)hipStreamDestroy(ctx->aux[i]);
-  for (int i = 0; i < 5; i++)
+  for (int i = 0; i < 7; i++)
     if (ctx->fj[i]) (void)hipEventDestroy(ctx->fj[i]);
   if (ctx->ev_ok)
     for (int i = 0; i < 2 * hvx_ctx::kMaxTimed; i++) (void)hipEventDestroy(ctx->tev[i]);
@@ -654,7 +655,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   //                    latency-bound RDOQ waves run beside the depth 2/3 searches, not after them
   //   C (aux[1], high priority): residuals of depth 2 and the 16x16 TU pipeline
   // The 64x64 fractional refinement stays on A after depth 0 (it fills the chip by itself).
-  hipStream_t st = ctx->stream, sb = ctx->aux[0], sc = ctx->aux[1];
+  hipStream_t st = ctx->stream, sb = ctx->aux[0], sc = ctx->aux[1], se = ctx->aux[2];
   fold_timing(ctx);  // a previous call's events must be read before they are re-recorded
   hipLaunchKernelGGL(k_set_ptr, dim3(1), dim3(1), 0, st, cur_slot, d_cur);
   const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
@@ -716,14 +717,18 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   };
   // size classes are contiguous: [0,8n) 32x32 | [8n,24n) 16x16 | [24n,88n) 8x8; their
   // interleaved scratch regions start at 0, ctu_il_off16(n), ctu_il_off8(n)
-  {  // stream B
+  {  // stream B; with counting (hvx_ctu_encode) the 32x32 class's rate runs on stream E beside k_tu_fin
     HVX_HIP(hipStreamWaitEvent(sb, ctx->fj[1], 0));
     const int tk = t_begin(ctx, sb, 5);
     resid_range(sb, 0, 5);
     t_end(ctx, sb, tk);
     tu_class_launch<3, 2>(sb, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev, nullptr, abs_sum, res_out, sse,
-                          coefI, levI, stI, flags, g32, 4, ctx, 6);
-    count_class(sb, 0, 8 * n, 0, 3);
+                          coefI, levI, stI, flags, g32, 4, ctx, 6, cnt_states ? ctx->fj[5] : nullptr);
+    if (cnt_states) {
+      HVX_HIP(hipStreamWaitEvent(se, ctx->fj[5], 0));
+      count_class(se, 0, 8 * n, 0, 3);
+      HVX_HIP(hipEventRecord(ctx->fj[6], se));
+    }
     HVX_HIP(hipEventRecord(ctx->fj[3], sb));
   }
   {  // stream C
@@ -748,6 +753,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   }
   HVX_HIP(hipStreamWaitEvent(st, ctx->fj[3], 0));
   HVX_HIP(hipStreamWaitEvent(st, ctx->fj[4], 0));
+  if (cnt_states) HVX_HIP(hipStreamWaitEvent(st, ctx->fj[6], 0));
   const int tk = t_begin(ctx, st, 15);
   hipLaunchKernelGGL(k_ctu_finalize, dim3((n * HVX_CUS_PER_CTU + 255) / 256), dim3(256), 0, st, L, abs_sum, sse, d_out);
   t_end(ctx, st, tk);
