@@ -25,7 +25,7 @@ struct hvx_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
-  // hvx_ctu_analyze runs its independent branches on two more streams (fork/join events)
+  // hvx_ctu_analyze / hvx_ctu_encode run their independent branches on three more streams (fork/join events)
   hipStream_t aux[3] = {};
   hipEvent_t fj[7] = {};
   // optional per-phase timing of hvx_ctu_analyze: a begin/end event pair on the launch's own
