@@ -48,6 +48,10 @@
  *                         35-mode Hadamard cost ranking + MPM candidates per luma PU
  *   hvx_deblock           TComLoopFilter::loopFilterPic (TComLoopFilter.cpp:130, xEdgeFilterLuma :560,
  *                         xEdgeFilterChroma :679) on given boundary strengths
+ *   hvx_sao_stats         TEncSampleAdaptiveOffset::getStatistics (TEncSampleAdaptiveOffset.cpp:285,
+ *                         getBlkStats :892): per-CTU SAO statistics of a deblocked picture
+ *   hvx_sao_apply         TComSampleAdaptiveOffset::offsetCTU (TComSampleAdaptiveOffset.cpp:554,
+ *                         offsetBlock :313) of every CTU with given (merge-resolved) parameters
  *   hvx_plane_from_pel    TComPicYuv int16 padded plane -> device 8-bit padded plane, with
  *                         TComPicYuv::extendPicBorder (TComPicYuv.cpp:197)
  */
@@ -258,6 +262,23 @@ int hvx_intra_search_batch(hvx_ctx *ctx, const uint8_t *d_org, const uint8_t *d_
  * ------------------------------------------------------------------------------------- */
 int hvx_deblock(hvx_ctx *ctx, uint8_t *d_y, int y_stride, uint8_t *d_cb, uint8_t *d_cr, int c_stride,
                 const uint8_t *d_bs_ver, const uint8_t *d_bs_hor, const int8_t *d_qp, const hvx_deblock_params *h_params);
+
+/* ---------------------------------------------------------------------------------------
+ * SAO (hvx_types.h hvx_sao_*), single slice and tile, 8-bit 4:2:0, pic_w / pic_h multiples of 8.
+ * Plane pointers = sample (0,0); chroma pointers may both be NULL (luma only).
+ * hvx_sao_stats: d_stats = [ctu][3][5] hvx_sao_stat (components not computed are untouched) of
+ * the deblocked picture d_rec_* against the original d_org_* -- SAOProcess's statistics with
+ * SAOLcuBoundary (pre-deblocking samples) off.  hvx_sao_apply: every sample of d_dst_* = d_src_*
+ * with its CTU's offsets (d_params: one hvx_sao_ctu per CTU, raster order); d_dst must not
+ * overlap d_src (edge classes read the unmodified neighbours, as offsetCTU reads SAOProcess's copy).
+ * ------------------------------------------------------------------------------------- */
+int hvx_sao_stats(hvx_ctx *ctx, const uint8_t *d_org_y, const uint8_t *d_org_cb, const uint8_t *d_org_cr,
+                  int org_y_stride, int org_c_stride, const uint8_t *d_rec_y, const uint8_t *d_rec_cb,
+                  const uint8_t *d_rec_cr, int rec_y_stride, int rec_c_stride, int pic_w, int pic_h,
+                  hvx_sao_stat *d_stats);
+int hvx_sao_apply(hvx_ctx *ctx, const uint8_t *d_src_y, const uint8_t *d_src_cb, const uint8_t *d_src_cr,
+                  int src_y_stride, int src_c_stride, uint8_t *d_dst_y, uint8_t *d_dst_cb, uint8_t *d_dst_cr,
+                  int dst_y_stride, int dst_c_stride, int pic_w, int pic_h, const hvx_sao_ctu *d_params);
 
 /* ---------------------------------------------------------------------------------------
  * CTU analysis pass over a whole picture (hvx_types.h): d_cur = sample (0,0) of the current

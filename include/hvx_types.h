@@ -221,6 +221,32 @@ typedef struct hvx_deblock_params {
   int32_t flags, pad_;             /* reserved, 0 */
 } hvx_deblock_params;
 
+/* SAO parameters of one CTU component as offsetCTU applies them (TComSampleAdaptiveOffset.cpp:554:
+ * the decided parameters with merges resolved and offsets de-quantised, reconstructBlkSAOParam
+ * :248).  type: -1 off, 0..3 edge offset EO_0 / EO_90 / EO_135 / EO_45, 4 band offset.
+ * EO: offset[] = full valley, half valley, half peak, full peak (the plain class adds 0).
+ * BO: band = first of the 4 consecutive bands (mod 32) whose offsets are offset[0..3]. */
+#define HVX_SAO_OFF (-1)
+#define HVX_SAO_BO 4
+typedef struct hvx_sao_offset {
+  int8_t type;
+  uint8_t band;
+  int8_t offset[4];
+  int8_t pad_[2];
+} hvx_sao_offset;                  /* 8 bytes */
+typedef struct hvx_sao_ctu {
+  hvx_sao_offset comp[3];          /* Y, Cb, Cr */
+} hvx_sao_ctu;                     /* 24 bytes, one per CTU in raster order */
+
+/* SAO statistics of one CTU component and type (SAOStatData, TEncSampleAdaptiveOffset.h:66):
+ * EO: classes 0..4 (edge type + 2); BO: the 32 bands. */
+#define HVX_SAO_TYPES 5
+#define HVX_SAO_CLASSES 32
+typedef struct hvx_sao_stat {
+  int64_t diff[HVX_SAO_CLASSES];   /* sum of org - rec */
+  int64_t count[HVX_SAO_CLASSES];
+} hvx_sao_stat;                    /* 512 bytes; a picture: [ctu][comp 3][type 5] */
+
 /* One PU's motion compensation (TComPrediction::motionCompensation for one partition, no
  * weighted prediction; TComPrediction.cpp:517-722).  Lists with ref >= 0 are used: both ->
  * bi-prediction (14-bit intermediates + TComYuv::addAvg), unless HVX_MC_B_SLICE is set and the

@@ -395,3 +395,30 @@ def ctu_bs(cu, dec, pic_w, pic_h):
     bh = np.zeros_like(bv)
     L.hvxo_ctu_bs(_p(c), _p(d), int(pic_w), int(pic_h), _p(bv), _p(bh))
     return bv, bh
+
+
+def sao_stats(org, rec, comp):
+    """hvxo_sao_stats of one plane (2-D uint8 arrays of the picture size): [nctu, 5] SAO_STAT."""
+    L = lib()
+    L.hvxo_sao_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    o, r = _c(org, np.uint8), _c(rec, np.uint8)
+    h, w = r.shape
+    cs = 32 if comp else 64
+    n = ((w + cs - 1) // cs) * ((h + cs - 1) // cs)
+    out = np.zeros((n, 5), _abi.SAO_STAT)
+    L.hvxo_sao_stats(_p(o), o.shape[1], _p(r), r.shape[1], w, h, int(comp), _p(out))
+    return out
+
+
+def sao_apply(src, comp, params):
+    """hvxo_sao_apply of one plane: the plane after SAO (params: SAO_CTU per CTU)."""
+    L = lib()
+    L.hvxo_sao_apply.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    s = _c(src, np.uint8)
+    h, w = s.shape
+    d = np.zeros_like(s)
+    p = np.ascontiguousarray(params, _abi.SAO_CTU)
+    L.hvxo_sao_apply(_p(s), s.shape[1], _p(d), d.shape[1], w, h, int(comp), _p(p))
+    return d

@@ -66,4 +66,13 @@ dcap "$TMP/d_pr.bin"  $CFG/encoder_lowdelay_P_main.cfg "$TMP/rand.yuv"   2 32
 dcap "$TMP/d_off.bin" $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth.yuv" 2 30 --LoopFilterOffsetInPPS=1 \
   --LoopFilterBetaOffset_div2=3 --LoopFilterTcOffset_div2=-2 --CbQpOffset=4 --CrQpOffset=-3
 python3 oracle/merge_goldens.py tests/golden/deblock.bin "$TMP"/d_i.bin "$TMP"/d_p.bin "$TMP"/d_b.bin "$TMP"/d_pr.bin "$TMP"/d_off.bin
+# SAO: TEncSampleAdaptiveOffset::SAOProcess statistics, applied parameters, output (oracle/sao_capture.cpp)
+scap() {  # scap <out.bin> <cfg> <yuv> <frames> <qp>
+  HVX_CAPTURE=$1 $ORC/TAppEncoder_saocap -c "$2" -i "$3" -wdt 416 -hgt 240 -fr 30 -f "$4" -q "$5" \
+    -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+}
+scap "$TMP/s_i.bin"  $CFG/encoder_intra_main.cfg      "$TMP/smooth.yuv" 1 37
+scap "$TMP/s_p.bin"  $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth.yuv" 3 32
+scap "$TMP/s_pr.bin" $CFG/encoder_lowdelay_P_main.cfg "$TMP/rand.yuv"   2 27
+python3 oracle/merge_goldens.py tests/golden/sao.bin "$TMP"/s_i.bin "$TMP"/s_p.bin "$TMP"/s_pr.bin
 ls -la tests/golden

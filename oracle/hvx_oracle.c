@@ -2356,3 +2356,83 @@ void hvxo_ctu_bs(const hvx_cu_result *cu, const hvx_cu_decision *dec, int pic_w,
         else *o = (rq->ref != rp->ref || abs(rq->mv_x - rp->mv_x) >= 4 || abs(rq->mv_y - rp->mv_y) >= 4) ? 1 : 0;
       }
 }
+
+/* =====================================================================================
+ * SAO: statistics and application on one plane, single slice and tile
+ * (deriveLoopFilterBoundaryAvailibility, TComPicSym.cpp:368: a neighbour CTU is available
+ * when it exists).  The reference walks each row with running sign buffers; each buffered
+ * sign equals the sign against the neighbour of the class, so the edge class is computed
+ * directly here: sgn(c - a) + sgn(c - b) + 2 over the class's two neighbours a, b.
+ * ===================================================================================== */
+static int sao_sgn(int v) { return (v > 0) - (v < 0); }
+/* the two neighbours of edge-offset type t (SAO_TYPE_EO_0/90/135/45) */
+static const int kSaoNb[4][2][2] = {{{-1, 0}, {1, 0}}, {{0, -1}, {0, 1}}, {{-1, -1}, {1, 1}}, {{1, -1}, {-1, 1}}};
+
+static int sao_edge(const uint8_t *p, int s, int t) {
+  const int c = p[0];
+  return sao_sgn(c - p[kSaoNb[t][0][1] * s + kSaoNb[t][0][0]]) + sao_sgn(c - p[kSaoNb[t][1][1] * s + kSaoNb[t][1][0]]) + 2;
+}
+
+/* getBlkStats (TEncSampleAdaptiveOffset.cpp:892-1282), isCalculatePreDeblockSamples = false;
+ * skipped right columns / bottom rows m_skipLinesR/B (createEncData :125-131: 5/4 luma, 3/2 chroma) */
+void hvxo_sao_stats(const uint8_t *org, int os, const uint8_t *rec, int rs, int w, int h, int comp, hvx_sao_stat *out) {
+  const int cs = comp ? 32 : 64, skr = comp ? 3 : 5, skb = comp ? 2 : 4;
+  const int ncx = (w + cs - 1) / cs, ncy = (h + cs - 1) / cs;
+  for (int cy = 0; cy < ncy; cy++)
+    for (int cx = 0; cx < ncx; cx++) {
+      const int x0 = cx * cs, y0 = cy * cs, bw = w - x0 < cs ? w - x0 : cs, bh = h - y0 < cs ? h - y0 : cs;
+      /* getStatistics :303-307: right / below from the picture boundary */
+      const int L = cx > 0, A = cy > 0, R = x0 + cs < w, B = y0 + cs < h;
+      hvx_sao_stat *st = out + (size_t)(cy * ncx + cx) * HVX_SAO_TYPES;
+      memset(st, 0, sizeof(hvx_sao_stat) * HVX_SAO_TYPES);
+      for (int t = 0; t < HVX_SAO_TYPES; t++) {
+        int xs, xe, ys, ye;
+        if (t == 4) { xs = 0; xe = R ? bw - skr : bw; ys = 0; ye = B ? bh - skb : bh; }       /* BO :1229 */
+        else if (t == 0) { xs = L ? 0 : 1; xe = R ? bw - skr : bw - 1; ys = 0; ye = B ? bh - skb : bh; } /* :941 */
+        else if (t == 1) { xs = 0; xe = R ? bw - skr : bw; ys = A ? 0 : 1; ye = B ? bh - skb : bh - 1; } /* :989 */
+        else { xs = L ? 0 : 1; xe = R ? bw - skr : bw - 1; ys = A ? 0 : 1; ye = B ? bh - skb : bh - 1; } /* :1051, :1140 */
+        /* EO_135 / EO_45 first row: nothing without the above CTU (:1069-1070, :1157-1161) */
+        for (int y = ys; y < ye; y++)
+          for (int x = xs; x < xe; x++) {
+            const uint8_t *p = rec + (size_t)(y0 + y) * rs + x0 + x;
+            const int d = (int)org[(size_t)(y0 + y) * os + x0 + x] - (int)p[0];
+            const int k = t == 4 ? p[0] >> 3 : sao_edge(p, rs, t);
+            st[t].diff[k] += d;
+            st[t].count[k]++;
+          }
+      }
+    }
+}
+
+/* offsetCTU / offsetBlock (TComSampleAdaptiveOffset.cpp:313-612): every class's region is the
+ * block minus the columns/rows whose neighbour lies outside the picture */
+void hvxo_sao_apply(const uint8_t *src, int ss, uint8_t *dst, int ds, int w, int h, int comp,
+                    const hvx_sao_ctu *params) {
+  const int cs = comp ? 32 : 64;
+  const int ncx = (w + cs - 1) / cs, ncy = (h + cs - 1) / cs;
+  for (int y = 0; y < h; y++) memcpy(dst + (size_t)y * ds, src + (size_t)y * ss, (size_t)w);
+  for (int cy = 0; cy < ncy; cy++)
+    for (int cx = 0; cx < ncx; cx++) {
+      const hvx_sao_offset *o = &params[cy * ncx + cx].comp[comp];
+      if (o->type < 0) continue;
+      const int x0 = cx * cs, y0 = cy * cs, bw = w - x0 < cs ? w - x0 : cs, bh = h - y0 < cs ? h - y0 : cs;
+      const int L = cx > 0, A = cy > 0, R = cx + 1 < ncx, B = cy + 1 < ncy;
+      const int t = o->type;
+      const int xs = (t == 0 || t >= 2) && t != 4 && !L ? 1 : 0, xe = (t == 0 || t == 2 || t == 3) && !R ? bw - 1 : bw;
+      const int ys = t >= 1 && t <= 3 && !A ? 1 : 0, ye = t >= 1 && t <= 3 && !B ? bh - 1 : bh;
+      for (int y = ys; y < ye; y++)
+        for (int x = xs; x < xe; x++) {
+          const uint8_t *p = src + (size_t)(y0 + y) * ss + x0 + x;
+          int off;
+          if (t == 4) {
+            const int k = ((p[0] >> 3) - o->band) & 31;
+            off = k < 4 ? o->offset[k] : 0;
+          } else {
+            const int e = sao_edge(p, ss, t);
+            off = e == 2 ? 0 : o->offset[e < 2 ? e : e - 1];
+          }
+          const int v = p[0] + off;
+          dst[(size_t)(y0 + y) * ds + x0 + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+        }
+    }
+}

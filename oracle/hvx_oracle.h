@@ -106,6 +106,13 @@ void hvxo_intra_search(const uint8_t *org, const int16_t *raw, const hvx_intra_j
 void hvxo_deblock(uint8_t *y, int ys, uint8_t *cb, uint8_t *cr, int cs, const uint8_t *bs_ver, const uint8_t *bs_hor,
                   const int8_t *qp, const hvx_deblock_params *p);
 
+/* ---- SAO, one plane (comp 0 luma / 1, 2 chroma 4:2:0; ctu = 64 >> (comp > 0)) ---- */
+/* TEncSampleAdaptiveOffset::getStatistics / getBlkStats (non-pre-deblocking samples): out[ctu][5] */
+void hvxo_sao_stats(const uint8_t *org, int os, const uint8_t *rec, int rs, int w, int h, int comp, hvx_sao_stat *out);
+/* TComSampleAdaptiveOffset::offsetCTU of every CTU: dst = src with the CTU's offsets (dst != src) */
+void hvxo_sao_apply(const uint8_t *src, int ss, uint8_t *dst, int ds, int w, int h, int comp,
+                    const hvx_sao_ctu *params);
+
 /* boundary strengths of hvx_ctu_decide's CU trees (the bench step's deblocking input); cu/dec =
  * nctu*85 records of the whole picture, maps (pic_w/4) x (pic_h/4) */
 void hvxo_ctu_bs(const hvx_cu_result *cu, const hvx_cu_decision *dec, int pic_w, int pic_h, uint8_t *bs_ver,

@@ -184,3 +184,22 @@ def deblock_cases(g):
         pu += nu
     assert po == len(g["pre"]) and pu == len(g["qp"])
     return out
+
+
+def sao_cases(g):
+    """SAOProcess records: (w, h, synthetic, org (y, cb, cr), pre, post, stats [nctu,3,5] SAO_STAT, SAO_CTU params)."""
+    out, po, pc = [], 0, 0
+    for m in g["meta"]:
+        w, h, nctu, syn = (int(v) for v in m)
+        n = w * h + 2 * (w // 2) * (h // 2)
+
+        def split(a):
+            cw, ch = w // 2, h // 2
+            return (a[:w * h].reshape(h, w), a[w * h:w * h + cw * ch].reshape(ch, cw), a[w * h + cw * ch:].reshape(ch, cw))
+        st = np.ascontiguousarray(g["stats"][pc:pc + nctu]).view(_abi.SAO_STAT).reshape(nctu, 3, 5)
+        out.append((w, h, bool(syn), split(g["org"][po:po + n]), split(g["pre"][po:po + n]),
+                    split(g["post"][po:po + n]), st, _abi.sao_ctu_params(g["params"][pc:pc + nctu])))
+        po += n
+        pc += nctu
+    assert po == len(g["pre"]) and pc == len(g["params"])
+    return out

@@ -650,3 +650,87 @@ def check_deblock_random(seed, w=1920, h=1080):
     for c in range(3):
         np.testing.assert_array_equal(got[c], exp[c], err_msg=f"plane {c}")
     return int((exp[0] != y).sum())
+
+
+def _padded_dev(planes, margin, rng):
+    """padded device copies of planes (random border bytes); returns (tensors, [(origin, stride)])."""
+    torch = _torch()
+    devs, views = [], []
+    for a in planes:
+        pa = rng.integers(0, 256, (a.shape[0] + 2 * margin, a.shape[1] + 2 * margin), dtype=np.uint8)
+        pa[margin:-margin, margin:-margin] = a
+        t = torch.from_numpy(pa).cuda()
+        devs.append(t)
+        views.append((t.data_ptr() + margin * pa.shape[1] + margin, pa.shape[1]))
+    return devs, views
+
+
+def run_sao(org, pre, params, w, h, margin=8, luma_only=False):
+    """hvx_sao_stats + hvx_sao_apply on padded device planes: (stats [nctu,3,5] SAO_STAT, applied
+    planes, destination borders untouched)."""
+    torch = _torch()
+    rng = np.random.default_rng(9)
+    k = 1 if luma_only else 3
+    keep_org, ov = _padded_dev(org[:k], margin, rng)  # the tensors must outlive the launches
+    keep_pre, pv = _padded_dev(pre[:k], margin, rng)
+    dst_init = [rng.integers(0, 256, (p.shape[0] + 2 * margin, p.shape[1] + 2 * margin), dtype=np.uint8) for p in pre[:k]]
+    dd = [torch.from_numpy(d.copy()).cuda() for d in dst_init]
+    dv = [(t.data_ptr() + margin * t.shape[1] + margin, t.shape[1]) for t in dd]
+    if luma_only:
+        ov, pv, dv = ov + [(0, 0)] * 2, pv + [(0, 0)] * 2, dv + [(0, 0)] * 2
+    nctu = ((w + 63) // 64) * ((h + 63) // 64)
+    stats = torch.full((nctu * 15 * _abi.SAO_STAT.itemsize,), 0x5A, dtype=torch.uint8, device="cuda")
+    hvx.sao_stats(ov, pv, w, h, stats)
+    prm = hvx.to_device(np.ascontiguousarray(params, _abi.SAO_CTU))
+    hvx.sao_apply(pv, dv, w, h, prm)
+    torch.cuda.synchronize()
+    del keep_org, keep_pre
+    st = stats.cpu().numpy().view(_abi.SAO_STAT).reshape(nctu, 3, 5)
+    outs, keep = [], True
+    for d, init in zip(dd, dst_init):
+        got = d.cpu().numpy()
+        outs.append(got[margin:-margin, margin:-margin].copy())
+        got[margin:-margin, margin:-margin] = init[margin:-margin, margin:-margin]
+        keep &= np.array_equal(got, init)
+    return st, outs, keep
+
+
+def check_sao_golden():
+    cases = gc.sao_cases(gc.load("sao.bin"))
+    for k, (w, h, syn, org, pre, post, st, params) in enumerate(cases):
+        got_st, got, keep = run_sao(org, pre, params, w, h)
+        assert keep, k
+        assert got_st.tobytes() == np.ascontiguousarray(st).tobytes(), f"record {k}: statistics"
+        for c in range(3):
+            np.testing.assert_array_equal(got[c], post[c], err_msg=f"record {k} plane {c}")
+    return len(cases)
+
+
+def sao_random_params(rng, nctu):
+    rows = np.zeros((nctu, 3, 6), np.int32)
+    rows[:, :, 0] = rng.integers(-1, 5, (nctu, 3))
+    rows[:, :, 1] = rng.integers(0, 32, (nctu, 3))
+    rows[:, :, 2:4] = rng.integers(0, 8, (nctu, 3, 2))
+    rows[:, :, 4:6] = rng.integers(-7, 1, (nctu, 3, 2))
+    bo = rows[:, :, 0] == 4
+    rows[:, :, 2:6][bo] = rng.integers(-7, 8, (int(bo.sum()), 4))
+    return _abi.sao_ctu_params(rows)
+
+
+def check_sao_random(seed, w=1920, h=1080, luma_only=False):
+    """random pictures (blocky, so every edge class occurs) and parameters vs the oracle."""
+    rng = np.random.default_rng(seed)
+    y = np.clip(np.kron(rng.integers(0, 256, (h // 4, w // 4)), np.ones((4, 4), np.int64))
+                + rng.integers(-2, 3, (h, w)), 0, 255).astype(np.uint8)
+    org = [np.clip(y.astype(np.int32) + rng.integers(-9, 10, y.shape), 0, 255).astype(np.uint8)]
+    pre = [y, (y[::2, ::2] // 2 + 64).astype(np.uint8), (255 - y[::2, ::2]).astype(np.uint8)]
+    org += [np.clip(p.astype(np.int32) + rng.integers(-5, 6, p.shape), 0, 255).astype(np.uint8) for p in pre[1:]]
+    nctu = ((w + 63) // 64) * ((h + 63) // 64)
+    params = sao_random_params(rng, nctu)
+    st, got, keep = run_sao(org, pre, params, w, h, luma_only=luma_only)
+    assert keep
+    for c in range(1 if luma_only else 3):
+        exp = oracle.sao_stats(org[c], pre[c], c)
+        assert st[:, c].tobytes() == exp.tobytes(), f"plane {c} statistics"
+        np.testing.assert_array_equal(got[c], oracle.sao_apply(pre[c], c, params), err_msg=f"plane {c}")
+    return nctu

@@ -257,3 +257,66 @@ def test_new_entry_points_reject_bad_arguments_without_a_gpu():
     assert L.hvx_deblock(P(0), P(0), 64, P(0), P(0), 32, P(0), P(0), P(0), P(0)) == E_INVALID
     assert b"hvx_deblock" in L.hvx_last_error()
     assert L.hvx_ctu_decide(P(0), P(0), 0, P(0), P(0), P(0), P(0), ctypes.c_size_t(0), P(0), P(0), P(0), P(0)) == E_INVALID
+
+
+def test_sao_layout_matches_c():
+    prog = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "hvx.h"
+int main(){printf("%zu %zu %zu %zu %zu\n", sizeof(hvx_sao_offset), offsetof(hvx_sao_offset, offset), sizeof(hvx_sao_ctu),
+ sizeof(hvx_sao_stat), offsetof(hvx_sao_stat, count)); return 0;}
+"""
+    tmp = "/tmp/hvx_sao_layout_check"
+    with open(tmp + ".c", "w") as f:
+        f.write(prog)
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), tmp + ".c", "-o", tmp])
+    vals = [int(x) for x in subprocess.check_output([tmp]).split()]
+    O, S = _abi.SAO_OFFSET, _abi.SAO_STAT
+    assert vals == [O.itemsize, O.fields["offset"][1], _abi.SAO_CTU.itemsize, S.itemsize, S.fields["count"][1]]
+
+
+def test_sao_entry_points_reject_bad_arguments_without_a_gpu():
+    # geometry / aliasing / partial-chroma checks run before any device work (the context is
+    # only dereferenced at the launch, so a dummy non-NULL handle is enough here)
+    import ctypes
+    L = ctypes.CDLL(os.path.join(ROOT, "video_codecs_amd", "libhvx.so"))
+    L.hvx_last_error.restype = ctypes.c_char_p
+    E_INVALID = -1
+    P = ctypes.c_void_p
+    fake = ctypes.create_string_buffer(4096)
+    ctx = P(ctypes.addressof(fake))
+    buf = [ctypes.create_string_buffer(64) for _ in range(7)]
+    a = [P(ctypes.addressof(b)) for b in buf]
+    assert L.hvx_sao_stats(P(0), a[0], a[1], a[2], 64, 32, a[3], a[4], a[5], 64, 32, 64, 64, a[6]) == E_INVALID
+    assert b"hvx_sao_stats" in L.hvx_last_error()
+    # 60 is not a multiple of 8; a stride below the width; only one chroma plane given
+    assert L.hvx_sao_stats(ctx, a[0], a[1], a[2], 64, 32, a[3], a[4], a[5], 64, 32, 60, 64, a[6]) == E_INVALID
+    assert L.hvx_sao_stats(ctx, a[0], a[1], a[2], 32, 32, a[3], a[4], a[5], 64, 32, 64, 64, a[6]) == E_INVALID
+    assert L.hvx_sao_stats(ctx, a[0], a[1], P(0), 64, 32, a[3], a[4], a[5], 64, 32, 64, 64, a[6]) == E_INVALID
+    assert L.hvx_sao_apply(ctx, a[0], a[1], a[2], 64, 32, a[3], a[4], a[5], 64, 32, 64, 60, a[6]) == E_INVALID
+    # in place is refused: edge classes must read the unmodified neighbours
+    assert L.hvx_sao_apply(ctx, a[0], a[1], a[2], 64, 32, a[0], a[4], a[5], 64, 32, 64, 64, a[6]) == E_INVALID
+    assert b"differ" in L.hvx_last_error()
+    assert L.hvx_sao_apply(ctx, a[0], P(0), P(0), 64, 0, a[3], a[4], P(0), 64, 32, 64, 64, a[6]) == E_INVALID
+
+
+def test_oracle_sao_random_smoke():
+    # the random recipe of the GPU test on the oracle alone: every class occurs, OFF CTUs unchanged
+    import numpy as np
+    import oracle
+    rng = np.random.default_rng(3)
+    w, h = 200, 136
+    y = np.clip(np.kron(rng.integers(0, 256, (h // 4, w // 4)), np.ones((4, 4), np.int64))
+                + rng.integers(-2, 3, (h, w)), 0, 255).astype(np.uint8)
+    org = np.clip(y.astype(np.int32) + rng.integers(-9, 10, y.shape), 0, 255).astype(np.uint8)
+    st = oracle.sao_stats(org, y, 0)
+    assert st.shape == (12, 5)
+    assert (st["count"][:, :4, :5].sum(axis=0) > 0).all() and st["count"][:, 4].sum() > 0
+    nctu = 12
+    rows = np.zeros((nctu, 3, 6), np.int32)
+    rows[:, :, 0] = -1
+    rows[1, 0] = (2, 0, 3, 1, -1, -3)
+    out = oracle.sao_apply(y, 0, _abi.sao_ctu_params(rows))
+    changed = np.argwhere(out != y)
+    assert len(changed) and changed[:, 0].max() < 64 and changed[:, 1].min() >= 64 and changed[:, 1].max() < 128

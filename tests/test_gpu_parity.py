@@ -247,6 +247,20 @@ def test_deblock_random_gpu(torch):
     assert gpu_cases.check_deblock_random(seed=41) > 10000
 
 
+def test_sao_golden_gpu(torch):
+    # SAOProcess: 8 records (5 encoder-decided pictures, 3 random parameter sets through the
+    # reference's offsetCTU), statistics of every CTU / component / type + Y/Cb/Cr after SAO
+    assert gpu_cases.check_sao_golden() == 8
+
+
+def test_sao_random_gpu(torch):
+    # 1080p and 1000x600 (partial CTUs on both axes) blocky pictures, random parameters vs the
+    # oracle; luma-only form; destination borders untouched
+    assert gpu_cases.check_sao_random(seed=51) == 510
+    assert gpu_cases.check_sao_random(seed=52, w=1000, h=600) == 160
+    assert gpu_cases.check_sao_random(seed=53, w=512, h=256, luma_only=True) == 32
+
+
 def test_ctu_decide_ssim_rdo_gpu(torch):
     # HVX_RD_SSIM (BASELINE config 4's SSIM RD cost): D_ssim per 8x8 block (compute_SSIM floats) and
     # lambda_2 in the CU quadtree decision, QP 22 and 37, bit-exact vs the oracle incl. the float sums

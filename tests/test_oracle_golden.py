@@ -195,3 +195,18 @@ def test_deblock_golden():
         for c in range(3):
             np.testing.assert_array_equal(got[c], post[c])
     assert {1, 2} <= set(np.unique(np.concatenate([c[3] for c in cases])))
+
+
+def test_sao_golden():
+    """SAOProcess vs the reference: per-CTU statistics of every component and type (getStatistics)
+    and the picture after SAO, for 5 encoder-decided pictures (intra QP37, LDP QP32, random-P QP27)
+    and 3 random parameter sets applied by the reference's own offsetCTU: bit-exact."""
+    cases = gc.sao_cases(gc.load("sao.bin"))
+    assert len(cases) == 8 and sum(c[2] for c in cases) == 3
+    types = set()
+    for w, h, syn, org, pre, post, st, params in cases:
+        for c in range(3):
+            assert oracle.sao_stats(org[c], pre[c], c).tobytes() == np.ascontiguousarray(st[:, c]).tobytes()
+            np.testing.assert_array_equal(oracle.sao_apply(pre[c], c, params), post[c])
+        types |= set(np.unique(params["comp"]["type"]).tolist())
+    assert types == {-1, 0, 1, 2, 3, 4}

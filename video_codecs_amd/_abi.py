@@ -128,6 +128,25 @@ DEBLOCK_PARAMS = np.dtype([("pic_w", "<i4"), ("pic_h", "<i4"), ("beta_offset_div
 assert DEBLOCK_PARAMS.itemsize == 32
 
 
+# hvx_types.h hvx_sao_offset / hvx_sao_ctu / hvx_sao_stat
+SAO_OFF, SAO_BO = -1, 4
+SAO_OFFSET = np.dtype([("type", "i1"), ("band", "u1"), ("offset", "i1", (4,)), ("pad_", "i1", (2,))])
+SAO_CTU = np.dtype([("comp", SAO_OFFSET, (3,))])
+assert SAO_CTU.itemsize == 24
+SAO_STAT = np.dtype([("diff", "<i8", (32,)), ("count", "<i8", (32,))])
+assert SAO_STAT.itemsize == 512
+
+
+def sao_ctu_params(rows):
+    """[nctu][3][6] int records (type, band, offset x4; the SAO golden layout) -> SAO_CTU array."""
+    r = np.asarray(rows, np.int32).reshape(-1, 3, 6)
+    out = np.zeros(len(r), SAO_CTU)
+    out["comp"]["type"] = r[:, :, 0]
+    out["comp"]["band"] = r[:, :, 1]
+    out["comp"]["offset"] = r[:, :, 2:6]
+    return out
+
+
 def deblock_params(w, h, beta_offset_div2=0, tc_offset_div2=0, cb_qp_offset=0, cr_qp_offset=0):
     p = np.zeros(1, DEBLOCK_PARAMS)
     p["pic_w"], p["pic_h"], p["beta_offset_div2"], p["tc_offset_div2"] = w, h, beta_offset_div2, tc_offset_div2

@@ -20,6 +20,7 @@
 #include "hvx_cabac.hpp"
 #include "hvx_intra.hpp"
 #include "hvx_deblock.hpp"
+#include "hvx_sao.hpp"
 
 struct hvx_ctx {
   int device = 0;
@@ -517,6 +518,44 @@ int hvx_deblock(hvx_ctx *ctx, uint8_t *d_y, int y_stride, uint8_t *d_cb, uint8_t
     hipLaunchKernelGGL(k_deblock<1>, dim3((nh + 255) / 256), dim3(256), 0, ctx->stream, d_y, y_stride, d_cb, d_cr,
                        c_stride, d_bs_hor, d_qp, P);
   return launched("k_deblock");
+}
+
+int hvx_sao_stats(hvx_ctx *ctx, const uint8_t *d_org_y, const uint8_t *d_org_cb, const uint8_t *d_org_cr,
+                  int org_y_stride, int org_c_stride, const uint8_t *d_rec_y, const uint8_t *d_rec_cb,
+                  const uint8_t *d_rec_cr, int rec_y_stride, int rec_c_stride, int pic_w, int pic_h,
+                  hvx_sao_stat *d_stats) {
+  if (!ctx || !d_org_y || !d_rec_y || !d_stats) return fail(HVX_E_INVALID, "hvx_sao_stats: NULL argument");
+  const bool chroma = d_org_cb || d_org_cr || d_rec_cb || d_rec_cr;
+  if (chroma && !(d_org_cb && d_org_cr && d_rec_cb && d_rec_cr))
+    return fail(HVX_E_INVALID, "hvx_sao_stats: chroma planes must be all set or all NULL");
+  if (pic_w <= 0 || pic_h <= 0 || pic_w % 8 || pic_h % 8 || org_y_stride < pic_w || rec_y_stride < pic_w ||
+      (chroma && (org_c_stride < pic_w / 2 || rec_c_stride < pic_w / 2)))
+    return fail(HVX_E_INVALID, "hvx_sao_stats: bad geometry");
+  const int nctu = ((pic_w + 63) / 64) * ((pic_h + 63) / 64);
+  hipLaunchKernelGGL(k_sao_stats, dim3(nctu, chroma ? 3 : 1), dim3(256), 0, ctx->stream, d_org_y, d_org_cb, d_org_cr,
+                     org_y_stride, org_c_stride, d_rec_y, d_rec_cb, d_rec_cr, rec_y_stride, rec_c_stride, pic_w, pic_h,
+                     d_stats);
+  return launched("k_sao_stats");
+}
+
+int hvx_sao_apply(hvx_ctx *ctx, const uint8_t *d_src_y, const uint8_t *d_src_cb, const uint8_t *d_src_cr,
+                  int src_y_stride, int src_c_stride, uint8_t *d_dst_y, uint8_t *d_dst_cb, uint8_t *d_dst_cr,
+                  int dst_y_stride, int dst_c_stride, int pic_w, int pic_h, const hvx_sao_ctu *d_params) {
+  if (!ctx || !d_src_y || !d_dst_y || !d_params) return fail(HVX_E_INVALID, "hvx_sao_apply: NULL argument");
+  const bool chroma = d_src_cb || d_src_cr || d_dst_cb || d_dst_cr;
+  if (chroma && !(d_src_cb && d_src_cr && d_dst_cb && d_dst_cr))
+    return fail(HVX_E_INVALID, "hvx_sao_apply: chroma planes must be all set or all NULL");
+  if (pic_w <= 0 || pic_h <= 0 || pic_w % 8 || pic_h % 8 || src_y_stride < pic_w || dst_y_stride < pic_w ||
+      (chroma && (src_c_stride < pic_w / 2 || dst_c_stride < pic_w / 2)))
+    return fail(HVX_E_INVALID, "hvx_sao_apply: bad geometry");
+  if (d_src_y == d_dst_y || (chroma && (d_src_cb == d_dst_cb || d_src_cr == d_dst_cr)))
+    return fail(HVX_E_INVALID, "hvx_sao_apply: src and dst planes must differ");
+  const int groups = ((pic_w + 3) / 4) * pic_h;
+  const int blocks = (groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096;
+  hipLaunchKernelGGL(k_sao_apply, dim3(blocks, chroma ? 3 : 1), dim3(256), 0, ctx->stream, d_src_y, d_src_cb, d_src_cr,
+                     src_y_stride, src_c_stride, d_dst_y, d_dst_cb, d_dst_cr, dst_y_stride, dst_c_stride, pic_w, pic_h,
+                     d_params);
+  return launched("k_sao_apply");
 }
 
 int hvx_alloc(hvx_ctx *ctx, size_t bytes, void **d_out) {

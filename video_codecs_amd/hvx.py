@@ -47,7 +47,7 @@ def lib():
             "hvx_set_timing": [P, I], "hvx_phase_times": [P, ctypes.POINTER(ctypes.c_double), I, I],
             "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
             "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P],
-            "hvx_intra_pred_batch": [P, P, I, P, I, P, P, P], "hvx_deblock": [P, P, I, P, P, I, P, P, P, P], "hvx_intra_search_batch": [P, P, P, I, P, I, P, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
+            "hvx_intra_pred_batch": [P, P, I, P, I, P, P, P], "hvx_deblock": [P, P, I, P, P, I, P, P, P, P], "hvx_sao_stats": [P, P, P, P, I, I, P, P, P, I, I, I, I, P], "hvx_sao_apply": [P, P, P, P, I, I, P, P, P, I, I, I, I, P], "hvx_intra_search_batch": [P, P, P, I, P, I, P, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
             "hvx_free": [P, P], "hvx_upload": [P, P, P, ctypes.c_size_t], "hvx_download": [P, P, P, ctypes.c_size_t],
         }.items():
             f = getattr(L, name)
@@ -67,19 +67,36 @@ def _check(rc, what):
         raise HvxError(f"{what} failed ({rc}): {lib().hvx_last_error().decode(errors='replace')}")
 
 
+def new_context(device=None):
+    """A private hvx_ctx: its own side streams, fork/join events and phase timers.  One per
+    concurrently encoded segment on a GPU (two encodes on one hvx_ctx would share its side
+    streams and events); bound to torch's current stream at each call like context()."""
+    import torch
+    if not torch.cuda.is_available():
+        raise HvxError("no HIP device visible: the hvx path needs an MI355X (no CPU fallback)")
+    dev = torch.cuda.current_device() if device is None else int(device)
+    p = ctypes.c_void_p()
+    _check(lib().hvx_create(dev, ctypes.byref(p)), "hvx_create")
+    return p
+
+
+def bind(c, device=None):
+    """Point hvx_ctx c at torch's current stream and return it."""
+    import torch
+    dev = torch.cuda.current_device() if device is None else int(device)
+    _check(lib().hvx_set_stream(c, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "hvx_set_stream")
+    return c
+
+
 def context(device=None):
-    """Per-device hvx_ctx bound to torch's current stream."""
+    """Per-device shared hvx_ctx bound to torch's current stream."""
     import torch
     if not torch.cuda.is_available():
         raise HvxError("no HIP device visible: the hvx path needs an MI355X (no CPU fallback)")
     dev = torch.cuda.current_device() if device is None else int(device)
     if dev not in _ctx:
-        p = ctypes.c_void_p()
-        _check(lib().hvx_create(dev, ctypes.byref(p)), "hvx_create")
-        _ctx[dev] = p
-    c = _ctx[dev]
-    _check(lib().hvx_set_stream(c, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "hvx_set_stream")
-    return c
+        _ctx[dev] = new_context(dev)
+    return bind(_ctx[dev], dev)
 
 
 def _ptr(t):
@@ -214,6 +231,25 @@ def deblock(y_origin, y_stride, cb_origin, cr_origin, c_stride, bs_ver, bs_hor, 
                              p.ctypes.data_as(ctypes.c_void_p)), "hvx_deblock")
 
 
+def sao_stats(org, rec, pic_w, pic_h, out):
+    """hvx_sao_stats: org / rec = (y, cb, cr) tuples of (device address of sample (0,0), stride),
+    chroma entries (0, 0) for luma only; out = device tensor of nctu*3*5 hvx_sao_stat."""
+    (oy, oys), (ocb, ocs), (ocr, _) = org
+    (ry, rys), (rcb, rcs), (rcr, _) = rec
+    v = ctypes.c_void_p
+    _check(lib().hvx_sao_stats(context(), v(oy), v(ocb), v(ocr), int(oys), int(ocs), v(ry), v(rcb), v(rcr), int(rys),
+                               int(rcs), int(pic_w), int(pic_h), _ptr(out)), "hvx_sao_stats")
+
+
+def sao_apply(src, dst, pic_w, pic_h, params):
+    """hvx_sao_apply: src / dst as in sao_stats; params = device tensor of hvx_sao_ctu per CTU."""
+    (sy, sys_), (scb, scs), (scr, _) = src
+    (dy, dys), (dcb, dcs), (dcr, _) = dst
+    v = ctypes.c_void_p
+    _check(lib().hvx_sao_apply(context(), v(sy), v(scb), v(scr), int(sys_), int(scs), v(dy), v(dcb), v(dcr), int(dys),
+                               int(dcs), int(pic_w), int(pic_h), _ptr(params)), "hvx_sao_apply")
+
+
 def plane_from_pel(pel, pel_stride, width, height, plane):
     _check(lib().hvx_plane_from_pel(context(), _ptr(pel), pel_stride, width, height, _ptr(plane)), "hvx_plane_from_pel")
 
@@ -231,8 +267,11 @@ def ctu_workspace_size(pic_w, pic_h, n_ref):
 class CtuAnalyzer:
     """Device-resident CTU analysis pass (hvx_ctu_analyze) for one picture geometry."""
 
-    def __init__(self, pic_w, pic_h, n_ref, qp, lam=None, est4=None, rd_metric=_abi.RD_SSE):
+    def __init__(self, pic_w, pic_h, n_ref, qp, lam=None, est4=None, rd_metric=_abi.RD_SSE, ctx=None):
+        """ctx: a private hvx_ctx (new_context()) for an analyzer that runs concurrently with
+        others on the same GPU; None = the shared per-device context."""
         import torch
+        self._c = ctx
         self.params = _abi.ctu_params(pic_w, pic_h, n_ref, qp, lam, rd_metric=rd_metric)
         self.pic_w, self.pic_h, self.n_ref = pic_w, pic_h, n_ref
         self.stride = pic_w + 2 * _abi.PLANE_MARGIN
@@ -243,11 +282,14 @@ class CtuAnalyzer:
         self.est = torch.from_numpy(np.ascontiguousarray(est4, np.int32).reshape(-1)).cuda()
         self.out = torch.zeros(self.nctu * _abi.CUS_PER_CTU * _abi.CU_RESULT.itemsize, dtype=torch.uint8, device="cuda")
 
+    def ctx(self):
+        return context() if self._c is None else bind(self._c)
+
     def run(self, cur_plane, ref_planes_ptrs):
         """cur_plane: padded uint8 device tensor; ref_planes_ptrs: int64 device tensor of origin pointers."""
         origin = plane_origin_ptr(cur_plane, self.pic_w)
         p = np.ascontiguousarray(self.params)
-        _check(lib().hvx_ctu_analyze(context(), ctypes.c_void_p(origin), _ptr(ref_planes_ptrs), self.stride,
+        _check(lib().hvx_ctu_analyze(self.ctx(), ctypes.c_void_p(origin), _ptr(ref_planes_ptrs), self.stride,
                                      p.ctypes.data_as(ctypes.c_void_p), _ptr(self.est), _ptr(self.ws),
                                      self.ws_bytes, _ptr(self.out)), "hvx_ctu_analyze")
 
@@ -268,7 +310,7 @@ class CtuAnalyzer:
         """hvx_ctu_encode: run() + decide() as one schedule (same results)."""
         self._rate_model()
         p = np.ascontiguousarray(self.params)
-        _check(lib().hvx_ctu_encode(context(), ctypes.c_void_p(plane_origin_ptr(cur_plane, self.pic_w)),
+        _check(lib().hvx_ctu_encode(self.ctx(), ctypes.c_void_p(plane_origin_ptr(cur_plane, self.pic_w)),
                                     _ptr(ref_planes_ptrs), self.stride, p.ctypes.data_as(ctypes.c_void_p),
                                     _ptr(self.est), _ptr(self.states), _ptr(self.eb), _ptr(self.ws), self.ws_bytes,
                                     _ptr(self.out), _ptr(self.dec),
@@ -282,7 +324,7 @@ class CtuAnalyzer:
         with ref_pic, also the deblocked reference picture."""
         self._rate_model(states, entropy_bits)
         p = np.ascontiguousarray(self.params)
-        _check(lib().hvx_ctu_decide(context(), ctypes.c_void_p(plane_origin_ptr(cur_plane, self.pic_w)), self.stride,
+        _check(lib().hvx_ctu_decide(self.ctx(), ctypes.c_void_p(plane_origin_ptr(cur_plane, self.pic_w)), self.stride,
                                     p.ctypes.data_as(ctypes.c_void_p), _ptr(self.states), _ptr(self.eb), _ptr(self.ws),
                                     self.ws_bytes, _ptr(self.out), _ptr(self.dec),
                                     ctypes.c_void_p(plane_origin_ptr(recon_plane, self.pic_w)),
@@ -305,13 +347,13 @@ PHASE_KERNELS = ("k_me_int_ctu<64,1,4>", "k_me_ctu<32,1,2>", "k_me_ctu<16,1,1>",
                  "k_ctu_finalize", "k_coeff_bits_il", "k_ctu_leaf+k_ctu_decide", "k_ctu_bs+k_deblock")
 
 
-def set_timing(on):
-    _check(lib().hvx_set_timing(context(), int(on)), "hvx_set_timing")
+def set_timing(on, ctx=None):
+    _check(lib().hvx_set_timing(context() if ctx is None else ctx, int(on)), "hvx_set_timing")
 
 
-def phase_times(reset=True):
+def phase_times(reset=True, ctx=None):
     buf = (ctypes.c_double * len(PHASES))()
-    _check(lib().hvx_phase_times(context(), buf, len(PHASES), int(reset)), "hvx_phase_times")
+    _check(lib().hvx_phase_times(context() if ctx is None else ctx, buf, len(PHASES), int(reset)), "hvx_phase_times")
     return dict(zip(PHASES, list(buf)))
 
 
