@@ -43,6 +43,7 @@ def parse():
     p.add_argument("--no-intra", action="store_true", help="skip the intra first-pass side measurement")
     p.add_argument("--no-ssim", action="store_true", help="skip the SSIM-RDO side measurement")
     p.add_argument("--no-1080p", action="store_true", help="skip the 1080p side measurement")
+    p.add_argument("--no-sao", action="store_true", help="skip the SAO side measurement")
     return p.parse_args()
 
 
@@ -203,6 +204,8 @@ def main():
             out["step_1080p"] = step_1080p_measure(nref, args.qp, args.steps)
         if world == 1 and not args.no_ssim:
             out["ssim_rdo"] = ssim_rdo_measure(cur_t, ref_ptrs, W, H, nref, args.steps)
+        if world == 1 and not args.no_sao:
+            out["sao"] = sao_measure(W, H, args.steps)
         if world == 1 and not args.no_intra:
             out["intra_first_pass"] = intra_measure(cur_t, ref_t[0], W, H, float(an.params["lambda"][0]), args.steps)
         print(json.dumps(out), flush=True)
@@ -256,6 +259,44 @@ def ssim_rdo_measure(cur_t, ref_ptrs, W, H, nref, steps):
         res[str(qp)] = {"ms_per_picture": round(ms, 3), "ctus_per_s": round(((W + 63) // 64) * ((H + 63) // 64) / ms * 1e3, 1),
                         "lambda_ssim": _abi.lambda_ssim(qp), "leaf_cus_ssim": leaves[_abi.RD_SSIM],
                         "leaf_cus_sse": leaves[_abi.RD_SSE]}
+    return res
+
+
+def sao_measure(W, H, steps):
+    """Side measurement (not the headline): hvx_sao_stats + hvx_sao_apply over a whole 4:2:0
+    picture (Y, Cb, Cr) with random parameters -- wall time per picture of each kernel and its
+    HBM rate against the algorithmic bytes (stats: read original + deblocked picture; apply:
+    read the deblocked picture, write the output picture; 1.5 B per luma sample each)."""
+    import torch
+    from video_codecs_amd import _abi, hvx, synth
+    y = synth.luma_plane(W, H, 200)
+    M = _abi.PLANE_MARGIN
+    planes = [torch.from_numpy(np.ascontiguousarray(y[M:M + h, M:M + w])).cuda()
+              for (w, h) in ((W, H), (W // 2, H // 2), (W // 2, H // 2))]
+    org = [torch.roll(p, 1, 1).contiguous() for p in planes]
+    dst = [torch.empty_like(p) for p in planes]
+    view = lambda ts: [(t.data_ptr(), t.shape[1]) for t in ts]  # noqa: E731
+    nctu = ((W + 63) // 64) * ((H + 63) // 64)
+    rng = np.random.default_rng(7)
+    rows = np.zeros((nctu, 3, 6), np.int32)
+    rows[:, :, 0] = rng.integers(-1, 5, (nctu, 3))
+    rows[:, :, 1] = rng.integers(0, 32, (nctu, 3))
+    rows[:, :, 2:6] = rng.integers(-7, 8, (nctu, 3, 4))
+    prm = hvx.to_device(_abi.sao_ctu_params(rows))
+    stats = torch.empty(nctu * 15 * _abi.SAO_STAT.itemsize, dtype=torch.uint8, device="cuda")
+    res = {}
+    for name, fn in (("stats", lambda: hvx.sao_stats(view(org), view(planes), W, H, stats)),
+                     ("apply", lambda: hvx.sao_apply(view(planes), view(dst), W, H, prm))):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        gbs = 2 * 1.5 * W * H / (ms * 1e-3) / 1e9
+        res[name] = {"ms_per_picture": round(ms, 4), "algorithmic_gbs": round(gbs, 1),
+                     "frac_hbm": round(gbs / MI355X_HBM_PEAK_GBS, 4)}
     return res
 
 

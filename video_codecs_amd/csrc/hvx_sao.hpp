@@ -3,15 +3,14 @@
 // (TEncSampleAdaptiveOffset.cpp:285, 892) and TComSampleAdaptiveOffset::offsetCTU/offsetBlock
 // (TComSampleAdaptiveOffset.cpp:313, 554), single slice and tile, 8-bit 4:2:0.
 //
-// Statistics: one workgroup per (CTU, component).  A thread takes 4 horizontally adjacent
-// samples per step (one dword of the reconstruction row plus the row above and below), finds
-// the edge class of every type and the band, and adds (org - rec, 1) into per-type LDS
-// histograms with LDS atomics (int32: at most 64*64 samples of |d| <= 255 per CTU); the
-// workgroup then widens them to the int64 SAOStatData layout.  Application: one thread per
+// Statistics: one workgroup per (CTU, component), the block staged in LDS; edge-offset sums in
+// registers, band histograms in LDS (int32: at most 64*64 samples of |d| <= 255 per CTU),
+// widened to the int64 SAOStatData layout at the end.  Application: one thread per
 // 4 output samples, reading the unmodified input picture (src != dst) so that CTUs are
 // independent -- the reference's copy of the deblocked picture (SAOProcess :246-249).
 #pragma once
 #include "hvx_dev.hpp"
+#include "hvx_me.hpp"  // wave_sum_dpp
 
 namespace sao {
 __device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
@@ -41,13 +40,22 @@ __device__ __forceinline__ Blk block(int ctu, int ncx, int w, int h, int cs) {
 }  // namespace sao
 
 // grid (nctu, ncomp); 256 threads.  out: [ctu][3][5] hvx_sao_stat
+// The CTU block and its 1-sample ring (where inside the picture) are staged in LDS; each thread
+// keeps the edge-offset sums of its samples in registers (4 types x 5 classes, diff and count)
+// and adds band-offset samples to LDS histograms; the register sums are reduced per wave with
+// DPP adds and once per wave into LDS.
 __global__ __launch_bounds__(256) void k_sao_stats(const uint8_t *__restrict__ org_y, const uint8_t *__restrict__ org_cb,
                                                   const uint8_t *__restrict__ org_cr, int os_y, int os_c,
                                                   const uint8_t *__restrict__ rec_y, const uint8_t *__restrict__ rec_cb,
                                                   const uint8_t *__restrict__ rec_cr, int rs_y, int rs_c, int pic_w,
                                                   int pic_h, hvx_sao_stat *__restrict__ out) {
   using namespace sao;
-  __shared__ int hist[HVX_SAO_TYPES][2][HVX_SAO_CLASSES];
+  constexpr int TS = 68;  // tile stride: 64 + ring, dword-aligned rows
+  __shared__ uint8_t tile[66 * TS];
+  __shared__ uint8_t otile[64 * 64];
+  constexpr int NC = 16;  // band-histogram copies (lane & 15): same-band lanes of one instruction spread over banks
+  __shared__ int bo[2][HVX_SAO_CLASSES][NC];
+  __shared__ int eo[4][2][5];
   const int comp = blockIdx.y, ctu = blockIdx.x;
   const int cs = comp ? 32 : 64, w = comp ? pic_w >> 1 : pic_w, h = comp ? pic_h >> 1 : pic_h;
   const int skr = comp ? 3 : 5, skb = comp ? 2 : 4;  // m_skipLinesR/B (createEncData :125-131)
@@ -55,43 +63,91 @@ __global__ __launch_bounds__(256) void k_sao_stats(const uint8_t *__restrict__ o
   const uint8_t *rec = comp == 0 ? rec_y : comp == 1 ? rec_cb : rec_cr;
   const int os = comp ? os_c : os_y, rs = comp ? rs_c : rs_y;
   const int ncx = (pic_w + 63) >> 6;
-  for (int i = threadIdx.x; i < HVX_SAO_TYPES * 2 * HVX_SAO_CLASSES; i += 256) (&hist[0][0][0])[i] = 0;
-  __syncthreads();
   const Blk b = block(ctu, ncx, w, h, cs);
+  for (int i = threadIdx.x; i < 2 * HVX_SAO_CLASSES * NC + 40; i += 256) {
+    if (i < 2 * HVX_SAO_CLASSES * NC) (&bo[0][0][0])[i] = 0;
+    else (&eo[0][0][0])[i - 2 * HVX_SAO_CLASSES * NC] = 0;
+  }
+  // staging: every load of the block issued before the first LDS store of a batch (latency overlap)
+  const int tw = b.bw + 2, th = b.bh + 2;
+  for (int i0 = threadIdx.x; i0 < tw * th; i0 += 256 * 8) {
+    uint8_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int i = i0 + u * 256, ty = i / tw, tx = i - ty * tw, gy = b.y0 + ty - 1, gx = b.x0 + tx - 1;
+      v[u] = (i < tw * th && gy >= 0 && gy < h && gx >= 0 && gx < w) ? rec[(size_t)gy * rs + gx] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int i = i0 + u * 256, ty = i / tw, tx = i - ty * tw;
+      if (i < tw * th) tile[ty * TS + tx] = v[u];
+    }
+  }
+  for (int i0 = threadIdx.x; i0 < b.bw * b.bh; i0 += 256 * 8) {
+    uint8_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int i = i0 + u * 256, y = i / b.bw, x = i - y * b.bw;
+      v[u] = i < b.bw * b.bh ? org[(size_t)(b.y0 + y) * os + b.x0 + x] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (i0 + u * 256 < b.bw * b.bh) otile[i0 + u * 256] = v[u];
+  }
+  __syncthreads();
   // per type: [xs, xe) x [ys, ye) (getBlkStats :941, 989, 1051, 1140, 1229)
-  int xs[5], xe[5], ys[5], ye[5];
-  xs[4] = 0; xe[4] = b.R ? b.bw - skr : b.bw; ys[4] = 0; ye[4] = b.B ? b.bh - skb : b.bh;
-  xs[0] = b.L ? 0 : 1; xe[0] = b.R ? b.bw - skr : b.bw - 1; ys[0] = 0; ye[0] = ye[4];
-  xs[1] = 0; xe[1] = xe[4]; ys[1] = b.A ? 0 : 1; ye[1] = b.B ? b.bh - skb : b.bh - 1;
-  xs[2] = xs[3] = xs[0]; xe[2] = xe[3] = xe[0]; ys[2] = ys[3] = ys[1]; ye[2] = ye[3] = ye[1];
-  const int nq = (b.bw + 3) >> 2;  // 4-sample groups per row
-  for (int q = threadIdx.x; q < nq * b.bh; q += 256) {
-    const int y = q / nq, xg = (q - y * nq) * 4;
-    const uint8_t *rr = rec + (size_t)(b.y0 + y) * rs + b.x0;
-    const uint8_t *orow = org + (size_t)(b.y0 + y) * os + b.x0;
+  const int bxe = b.R ? b.bw - skr : b.bw, bye = b.B ? b.bh - skb : b.bh;
+  const int exs = b.L ? 0 : 1, exe = b.R ? b.bw - skr : b.bw - 1;
+  const int vys = b.A ? 0 : 1, vye = b.B ? b.bh - skb : b.bh - 1;
+  int ad[4][5], ac[4][5];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int x = xg + i;
-      if (x >= b.bw) break;
-      const uint8_t *p = rr + x;
-      const int d = (int)orow[x] - (int)p[0];
+  for (int t = 0; t < 4; t++)
 #pragma unroll
-      for (int t = 0; t < 5; t++) {
-        if (x >= xs[t] && x < xe[t] && y >= ys[t] && y < ye[t]) {
-          const int k = t == 4 ? p[0] >> 3 : edge(p, rs, t);
-          atomicAdd(&hist[t][0][k], d);
-          atomicAdd(&hist[t][1][k], 1);
-        }
+    for (int k = 0; k < 5; k++) ad[t][k] = ac[t][k] = 0;
+  for (int i = threadIdx.x; i < b.bw * b.bh; i += 256) {
+    const int y = i / b.bw, x = i - y * b.bw;
+    const uint8_t *p = tile + (y + 1) * TS + x + 1;
+    const int c = p[0];
+    const int d = (int)otile[i] - c;
+    if (x < bxe && y < bye) {
+      atomicAdd(&bo[0][c >> 3][threadIdx.x & (NC - 1)], d);
+      atomicAdd(&bo[1][c >> 3][threadIdx.x & (NC - 1)], 1);
+    }
+    const bool in_x = x >= exs && x < exe, in_yv = y >= vys && y < vye;
+    const bool in[4] = {in_x && y < bye, x < bxe && in_yv, in_x && in_yv, in_x && in_yv};
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int k = in[t] ? edge(p, TS, t) : -1;
+#pragma unroll
+      for (int j = 0; j < 5; j++) {
+        ad[t][j] += k == j ? d : 0;
+        ac[t][j] += k == j ? 1 : 0;
       }
     }
   }
+#pragma unroll
+  for (int t = 0; t < 4; t++)
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+      const int vd = (int)wave_sum_dpp((uint32_t)ad[t][j]), vc = (int)wave_sum_dpp((uint32_t)ac[t][j]);
+      if (lane_id() == 0) {
+        atomicAdd(&eo[t][0][j], vd);
+        atomicAdd(&eo[t][1][j], vc);
+      }
+    }
   __syncthreads();
   hvx_sao_stat *st = out + ((size_t)ctu * 3 + comp) * HVX_SAO_TYPES;
   for (int i = threadIdx.x; i < HVX_SAO_TYPES * 2 * HVX_SAO_CLASSES; i += 256) {
-    const int t = i / (2 * HVX_SAO_CLASSES), r = i % (2 * HVX_SAO_CLASSES);
-    const int64_t v = (&hist[0][0][0])[i];
-    if (r < HVX_SAO_CLASSES) st[t].diff[r] = v;
-    else st[t].count[r - HVX_SAO_CLASSES] = v;
+    const int t = i / (2 * HVX_SAO_CLASSES), r = i % (2 * HVX_SAO_CLASSES), k = r % HVX_SAO_CLASSES, dc = r / HVX_SAO_CLASSES;
+    int64_t v = 0;
+    if (t == 4) {
+#pragma unroll
+      for (int j = 0; j < NC; j++) v += bo[dc][k][j];
+    } else if (k < 5) {
+      v = eo[t][dc][k];
+    }
+    if (dc == 0) st[t].diff[k] = v;
+    else st[t].count[k] = v;
   }
 }
 
