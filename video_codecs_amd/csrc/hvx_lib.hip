@@ -29,6 +29,8 @@ struct hvx_ctx {
   // hvx_ctu_analyze / hvx_ctu_encode run their independent branches on three more streams (fork/join events)
   hipStream_t aux[3] = {};
   hipEvent_t fj[7] = {};
+  // HVX_SERIAL_STREAMS=1: every branch on ctx->stream (profiling: isolated per-kernel times)
+  bool serial = false;
   // optional per-phase timing of hvx_ctu_analyze: a begin/end event pair on the launch's own
   // stream around every timed launch, folded into phase_ms[phase] (phases may overlap)
   int timing = 0;
@@ -67,7 +69,7 @@ size_t ctu_il_off16(int n) { return pad_g((size_t)8 * n) * 1024; }
 size_t ctu_il_off8(int n) { return ctu_il_off16(n) + pad_g((size_t)16 * n) * 256; }
 size_t ctu_il_words(int n) { return ctu_il_off8(n) + pad_g((size_t)64 * n) * 64; }
 struct CtuWs {
-  size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, coefI, levI, stI, flags, cbits, bsv, bsh,
+  size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, coefI, cxI, levI, stI, flags, cbits, bsv, bsh,
       qpm, total;
 };
 CtuWs ctu_ws_layout(const CtuLayout &L) {
@@ -87,6 +89,7 @@ CtuWs ctu_ws_layout(const CtuLayout &L) {
   w.ptr = o; o = align_up(o + 8 * sizeof(void *));
   const size_t nil = ctu_il_words(L.nctu);
   w.coefI = o; o = align_up(o + nil * sizeof(int32_t));
+  w.cxI = o; o = align_up(o + nil * sizeof(int32_t));
   w.levI = o; o = align_up(o + nil * sizeof(int32_t));
   w.stI = o; o = align_up(o + nil * sizeof(int32_t));
   w.flags = o; o = align_up(o + ntu);
@@ -216,14 +219,14 @@ static void t_end(hvx_ctx *ctx, hipStream_t st, int k) {
 template <int L, int MODE>
 static void tu_class_launch(hipStream_t st, const hvx_tu_desc *desc, const hvx_estbits *est, const int32_t *est_idx,
                             const int64_t *off, int n, const int16_t *res_in, int32_t *temp, int32_t *lev, int32_t *arl,
-                            int32_t *abs_sum, int16_t *res_out, uint32_t *sse, int32_t *coefI, int32_t *levI,
-                            int32_t *stI, int8_t *flags, int G, int n_est_lds, hvx_ctx *tctx = nullptr,
+                            int32_t *abs_sum, int16_t *res_out, uint32_t *sse, uint32_t *coefI, uint32_t *cxI,
+                            int32_t *levI, int32_t *stI, int8_t *flags, int G, int n_est_lds, hvx_ctx *tctx = nullptr,
                             int phase0 = 0, hipEvent_t after_rdoq = nullptr) {
   int k = t_begin(tctx, st, phase0);
-  hipLaunchKernelGGL((k_tu_fwd<L>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, temp, arl, coefI, levI, abs_sum, flags, G);
+  hipLaunchKernelGGL((k_tu_fwd<L>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, temp, arl, coefI, cxI, levI, abs_sum, flags, G);
   t_end(tctx, st, k);
   k = t_begin(tctx, st, phase0 + 1);
-  hipLaunchKernelGGL((k_tu_rdoq<L>), dim3((n + G - 1) / G), dim3(64), 0, st, desc, est, est_idx, n, coefI, levI, stI,
+  hipLaunchKernelGGL((k_tu_rdoq<L>), dim3((n + G - 1) / G), dim3(64), 0, st, desc, est, est_idx, n, coefI, cxI, levI, stI,
                      abs_sum, flags, G, n_est_lds);
   t_end(tctx, st, k);
   if (after_rdoq) (void)hipEventRecord(after_rdoq, st);  // the levels are final: their rate may be counted beside k_tu_fin
@@ -245,7 +248,7 @@ static int tu_batch(hvx_ctx *ctx, const hvx_tu_desc *desc, const hvx_estbits *es
                     int32_t *abs_sum, int16_t *res_out, uint32_t *sse) {
   const int G = tu_group(n);
   const size_t npad = (size_t)(n + G - 1) / G * G;
-  const size_t need = 3 * npad * 1024 * sizeof(int32_t) + npad + 256;
+  const size_t need = 4 * npad * 1024 * sizeof(int32_t) + npad + 256;
   if (ctx->tu_scr_bytes < need) {
     if (ctx->tu_scr) (void)hipFree(ctx->tu_scr);
     ctx->tu_scr = nullptr;
@@ -253,14 +256,15 @@ static int tu_batch(hvx_ctx *ctx, const hvx_tu_desc *desc, const hvx_estbits *es
     HVX_HIP(hipMalloc(&ctx->tu_scr, need));
     ctx->tu_scr_bytes = need;
   }
-  int32_t *coefI = (int32_t *)ctx->tu_scr, *levI = coefI + npad * 1024, *stI = levI + npad * 1024;
+  uint32_t *coefI = (uint32_t *)ctx->tu_scr, *cxI = coefI + npad * 1024;
+  int32_t *levI = (int32_t *)(cxI + npad * 1024), *stI = levI + npad * 1024;
   int8_t *flags = (int8_t *)(stI + npad * 1024);
   hipStream_t st = ctx->stream;
   // one pipeline per size class; workgroups / lanes of TUs of another size exit at once
-  tu_class_launch<0, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, levI, stI, flags, G, 0);
-  tu_class_launch<1, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, levI, stI, flags, G, 0);
-  tu_class_launch<2, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, levI, stI, flags, G, 0);
-  tu_class_launch<3, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, levI, stI, flags, G, 0);
+  tu_class_launch<0, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, cxI, levI, stI, flags, G, 0);
+  tu_class_launch<1, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, cxI, levI, stI, flags, G, 0);
+  tu_class_launch<2, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, cxI, levI, stI, flags, G, 0);
+  tu_class_launch<3, MODE>(st, desc, est, est_idx, off, n, res_in, temp, lev, arl, abs_sum, res_out, sse, coefI, cxI, levI, stI, flags, G, 0);
   return launched("tu_batch");
 }
 
@@ -295,6 +299,8 @@ int hvx_create(int device, hvx_ctx **out) {
   hipError_t e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
   if (e != hipSuccess) { delete c; return hip_fail(e, "hipStreamCreate"); }
   c->stream = c->own;
+  const char *ser = getenv("HVX_SERIAL_STREAMS");
+  c->serial = ser && ser[0] == '1';
   // the side streams carry few, latency-bound workgroups (RDOQ chains): highest priority, so
   // they dispatch ahead of the ME kernels' backlog instead of waiting behind it
   int prio_lo = 0, prio_hi = 0;
@@ -695,6 +701,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   //   C (aux[1], high priority): residuals of depth 2 and the 16x16 TU pipeline
   // The 64x64 fractional refinement stays on A after depth 0 (it fills the chip by itself).
   hipStream_t st = ctx->stream, sb = ctx->aux[0], sc = ctx->aux[1], se = ctx->aux[2];
+  if (ctx->serial) sb = sc = se = st;
   fold_timing(ctx);  // a previous call's events must be read before they are re-recorded
   hipLaunchKernelGGL(k_set_ptr, dim3(1), dim3(1), 0, st, cur_slot, d_cur);
   const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
@@ -742,7 +749,8 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   // kCtuG = 64 TUs per RDOQ wave for every class: measured best at 2160p (G = 8/16/32/64 for
   // 32x32: 3.1/2.9/2.6/2.5 ms) -- the per-lane chain is latency-bound, so wider waves win
   const int g32 = kCtuG, g16 = kCtuG, g8 = kCtuG;
-  int32_t *coefI = (int32_t *)(ws + W.coefI), *levI = (int32_t *)(ws + W.levI), *stI = (int32_t *)(ws + W.stI);
+  uint32_t *coefI = (uint32_t *)(ws + W.coefI), *cxI = (uint32_t *)(ws + W.cxI);
+  int32_t *levI = (int32_t *)(ws + W.levI), *stI = (int32_t *)(ws + W.stI);
   int8_t *flags = (int8_t *)(ws + W.flags);
   hvx_coeff_bits *cb = (hvx_coeff_bits *)(ws + W.cbits);
   auto count_class = [&](hipStream_t s, int first, int cnt, size_t il_off, int L2) {
@@ -762,7 +770,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     resid_range(sb, 0, 5);
     t_end(ctx, sb, tk);
     tu_class_launch<3, 2>(sb, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev, nullptr, abs_sum, res_out, sse,
-                          coefI, levI, stI, flags, g32, 4, ctx, 6, cnt_states ? ctx->fj[5] : nullptr);
+                          coefI, cxI, levI, stI, flags, g32, 4, ctx, 6, cnt_states ? ctx->fj[5] : nullptr);
     if (cnt_states) {
       HVX_HIP(hipStreamWaitEvent(se, ctx->fj[5], 0));
       count_class(se, 0, 8 * n, 0, 3);
@@ -777,7 +785,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     t_end(ctx, sc, tk);
     const size_t o = ctu_il_off16(n);
     tu_class_launch<2, 2>(sc, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n, 16 * n, resid, nullptr, lev, nullptr,
-                          abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, levI + o, stI + o, flags + 8 * n, g16, 4, ctx, 9);
+                          abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, cxI + o, levI + o, stI + o, flags + 8 * n, g16, 4, ctx, 9);
     count_class(sc, 8 * n, 16 * n, o, 2);
     HVX_HIP(hipEventRecord(ctx->fj[4], sc));
   }
@@ -787,7 +795,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     t_end(ctx, st, tk);
     const size_t o = ctu_il_off8(n);
     tu_class_launch<1, 2>(st, desc + 24 * n, d_est4, est_idx + 24 * n, off + 24 * n, 64 * n, resid, nullptr, lev, nullptr,
-                          abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, levI + o, stI + o, flags + 24 * n, g8, 4, ctx, 12);
+                          abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, cxI + o, levI + o, stI + o, flags + 24 * n, g8, 4, ctx, 12);
     count_class(st, 24 * n, 64 * n, o, 1);
   }
   HVX_HIP(hipStreamWaitEvent(st, ctx->fj[3], 0));

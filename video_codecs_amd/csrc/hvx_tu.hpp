@@ -759,21 +759,42 @@ __device__ __forceinline__ size_t tu_il(int t, int sp, int NN, int G) {
   return ((size_t)(t / G) * NN + sp) * G + (t % G);
 }
 
-// xRateDistOptQuant (:2129-2671) for one TU by one lane.  coef/lev/st: the TU's interleaved
-// arrays (element sp at [sp * G]); coef in scan order; lev receives the signed final levels
-// in scan order; st the packed per-position context state (rd_pack).  Returns uiAbsSum.
-// Same operations, in the same order, as tu_rdoq and the reference.  Every pass works a
-// coefficient group at a time: the group's 16 loads are issued together (the arrays live in
-// HBM / the infinity cache) and staged in the lane's LDS column, and the decision pass
-// prefetches the next group while it decides the current one.
-// Per-lane LDS staging of one coefficient group: column `lane` of [16][64] arrays.
+// xGetICRate (:2891) without branches (the rate of one candidate level; lanes are different
+// TUs, so every branch of the reference's form would be divergent).  Not for the limited-prefix
+// (extended precision) escape code, which keeps rd_ic_rate.
+__device__ __forceinline__ int rd_ic_rate_bf(uint32_t level, uint32_t rice, bool c1ok, bool c2ok, int g0, int g1, int a0,
+                                             int a1) {
+  const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
+  const uint32_t symbol = level - base, r3 = 3u << rice;
+  const int small = (int)(((symbol >> rice) + 1 + rice) << 15);
+  const uint32_t v = ((symbol - r3) >> rice) + 1;
+  const uint32_t len = rice + (31u - (uint32_t)__clz(v));
+  const int big = (int)((3 + len + 1 - rice + len) << 15);
+  const int esc = (symbol < r3 ? small : big) + (c1ok ? g1 + (c2ok ? a1 : 0) : 0);
+  const int lo = level == 1 ? g0 : g1 + a0;  // level 2 below base (c1ok && c2ok)
+  return level == 0 ? 0 : 32768 + (level >= base ? esc : lo);
+}
+
+// xRateDistOptQuant (:2129-2671) for one TU by one lane.  ldI/cxI/lev/st: the TU's
+// interleaved arrays (element sp at [sp * G]), all in scan order:
+//   ldI  lLevelDouble (:2210) | sign of the coefficient << 31       (k_tu_fwd)
+//   cxI  significance context (getSigCtxInc :2717, + the chroma offset) under each of the 4
+//        neighbour-group patterns, 6 bits per pattern               (k_tu_fwd)
+//   lev  receives the signed final levels; st the packed context state of every decided
+//        position (rd_pack), which the last-position and sign-hiding passes replay.
+// Returns uiAbsSum.  Same operations, in the same order, as tu_rdoq and the reference; the
+// decision pass is branch-free per position (selects on both candidate levels), keeps the
+// group's greater-one / level-abs rate pairs in registers (the context set is fixed inside a
+// group: xRateDistOptQuant resets c1/c2/Rice at every group start), and stages each group's 16
+// inputs in the lane's LDS column while the next group's are in flight.
 struct RdLaneStage {
-  int32_t cf[16][64], lv[16][64], st[16][64];
+  uint32_t ld[16][64], cx[16][64];
+  int32_t lv[16][64], st[16][64];
 };
 
 template <int L>
-__device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const int32_t *coef, int32_t *lev,
-                             int32_t *st, int G, RdLaneStage &sg, int lane) {
+__device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const uint32_t *ldI, const uint32_t *cxI,
+                             int32_t *lev, int32_t *st, int G, RdLaneStage &sg, int lane) {
   constexpr int N = 4 << L, NN = N * N, NCG = NN / 16;
   constexpr int LOG2 = L + 2;
   const int ch = d.comp ? 1 : 0, comp = d.comp;
@@ -788,25 +809,32 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
   escale = escale / qc / qc / (1 << 0);
   const double lambda = d.lambda;
   const TuCoding c = tu_coding<L>(d);
-  const int64_t lim = (int64_t)2147483647 - ((int64_t)1 << (qbits - 1));
-  const int sig_off = ch ? 28 : 0;
   const size_t g16 = (size_t)16 * G;
+  const int32_t rnd = 1 << (qbits - 1);
+  const int set0 = comp ? 4 : 0;
+  const bool persistent = d.persistent_rice != 0;
 
   // ---- reverse-scan decisions ----
   const uint32_t rice0 = (uint32_t)d.golomb_rice_stat / 4;
-  uint32_t rice = rice0, ctx_set = 0, c1_idx = 0, c2_idx = 0;
-  int c1 = 1, c2 = 0, last = -1, cg_last = -1;
+  int last = -1, cg_last = -1;
+  bool carry = false;  // c1 == 0 at the end of the previous group (decided lanes only)
   double block_uncoded = 0, base_cost = 0;
   uint64_t sigmask = 0;
-  int32_t nxt[16];
+  uint32_t nld[16], ncx[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++) nxt[k] = coef[(NCG - 1) * g16 + (size_t)k * G];
+  for (int k = 0; k < 16; k++) {
+    nld[k] = ldI[(NCG - 1) * g16 + (size_t)k * G];
+    ncx[k] = cxI[(NCG - 1) * g16 + (size_t)k * G];
+  }
   for (int cgp = NCG - 1; cgp >= 0; cgp--) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) sg.cf[k][lane] = nxt[k];
+    for (int k = 0; k < 16; k++) { sg.ld[k][lane] = nld[k]; sg.cx[k][lane] = ncx[k]; }
     if (cgp > 0) {
 #pragma unroll
-      for (int k = 0; k < 16; k++) nxt[k] = coef[(cgp - 1) * g16 + (size_t)k * G];
+      for (int k = 0; k < 16; k++) {
+        nld[k] = ldI[(cgp - 1) * g16 + (size_t)k * G];
+        ncx[k] = cxI[(cgp - 1) * g16 + (size_t)k * G];
+      }
     }
     const int cgblk = c.scan_cg[cgp];
     const int cy = cgblk / c.wg, cx = cgblk - cy * c.wg;
@@ -816,89 +844,87 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
       const int bb = cy < c.wg - 1 ? (int)((sigmask >> (cgblk + c.wg)) & 1) : 0;
       pattern = rr + (bb << 1);
     }
+    const int psh = 6 * pattern;
+    // the group's context set: a lane whose last position lies in this group starts it here
+    // without the carry (:2262-2266), a decided lane carries c1 == 0 of the previous group
+    const int ctx_set = set0 + ((comp == 0 && cgp > 0) ? 2 : 0) + ((last >= 0 && carry) ? 1 : 0);
+    int G0[4], G1[4], A0[3], A1[3];
+#pragma unroll
+    for (int k = 0; k < 4; k++) { G0[k] = est->greaterOneBits[4 * ctx_set + k][0]; G1[k] = est->greaterOneBits[4 * ctx_set + k][1]; }
+#pragma unroll
+    for (int k = 0; k < 3; k++) { A0[k] = est->levelAbsBits[ctx_set + k][0]; A1[k] = est->levelAbsBits[ctx_set + k][1]; }
+    int c1 = 1, c2 = 0;
+    uint32_t c1_idx = 0, c2_idx = 0, rice = rice0;
     int nnz0 = 0;
     bool any = false;
     double coded_ld = 0, uncoded = 0, sig_cost = 0, sig_cost0 = 0;
+#pragma unroll 2
     for (int pin = 15; pin >= 0; pin--) {
       const int sp = cgp * 16 + pin;
-      const int32_t ld = rd_level_double(sg.cf[pin][lane], qc, lim);
-      const uint32_t q = (uint32_t)((ld + (1 << (qbits - 1))) >> qbits);
+      const uint32_t w = sg.ld[pin][lane], cxw = sg.cx[pin][lane];
+      const int32_t ld = (int32_t)(w & 0x7fffffffu);
+      const uint32_t q = (uint32_t)((ld + rnd) >> qbits);
       const uint32_t max_abs = (uint32_t)ecmax < q ? (uint32_t)ecmax : q;
       const double e = (double)ld;
       const double cc0 = e * e * escale;
       block_uncoded += cc0;
-      int32_t out = (int32_t)max_abs;
-      double cc = 0.0, cs = 0.0;
-      if (max_abs > 0 && last < 0) {
-        last = sp;
-        ctx_set = (comp ? 4 : 0) + ((comp == 0 && (sp >> 4) > 0) ? 2 : 0);
-        cg_last = cgp;
+      const bool found = max_abs > 0 && last < 0;
+      last = found ? sp : last;
+      cg_last = found ? cgp : cg_last;
+      const bool act = last >= 0, is_last = sp == last;
+      const int ctx_sig = is_last ? 0 : (int)((cxw >> psh) & 63u);
+      const int sb0 = est->significantBits[ctx_sig][0], sb1 = est->significantBits[ctx_sig][1];
+      const int g0 = c1 == 0 ? G0[0] : c1 == 1 ? G0[1] : c1 == 2 ? G0[2] : G0[3];
+      const int g1 = c1 == 0 ? G1[0] : c1 == 1 ? G1[1] : c1 == 2 ? G1[2] : G1[3];
+      const int a0 = c2 == 0 ? A0[0] : c2 == 1 ? A0[1] : A0[2];
+      const int a1 = c2 == 0 ? A1[0] : c2 == 1 ? A1[1] : A1[2];
+      const bool c1ok = c1_idx < 8, c2ok = c2_idx < 1;
+      // xGetCodedLevel (:2822): level 0 (when allowed), then max, then max - 1
+      const bool zero_ok = !is_last && max_abs < 3;
+      const double sig0 = lambda * (double)sb0;
+      double cost = zero_ok ? cc0 + sig0 : 1.7e+308;
+      double cost_sig = zero_ok ? sig0 : 0.0;
+      int sel = zero_ok ? 1 : 0;
+      uint32_t best = 0;
+      const double cur_sig = is_last ? 0.0 : lambda * (double)sb1;
+      const int sel_nz = is_last ? 0 : 2;
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const uint32_t lv = max_abs - (uint32_t)k;
+        const int r = ext ? rd_ic_rate(lv, (int)rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2)
+                          : rd_ic_rate_bf(lv, rice, c1ok, c2ok, g0, g1, a0, a1);
+        const double err = (double)sub32(ld, shl32((int32_t)lv, qbits));
+        double cl = err * err * escale + lambda * (double)r;
+        cl += cur_sig;
+        const bool take = max_abs >= (uint32_t)(k + 1) && cl < cost;
+        best = take ? lv : best;
+        cost = take ? cl : cost;
+        cost_sig = take ? cur_sig : cost_sig;
+        sel = take ? sel_nz : sel;
       }
-      if (last >= 0) {
-        const int ctx_one = 4 * (int)ctx_set + c1, ctx_abs = (int)ctx_set + c2;
-        const int g0 = est->greaterOneBits[ctx_one][0], g1 = est->greaterOneBits[ctx_one][1];
-        const int a0 = est->levelAbsBits[ctx_abs][0], a1 = est->levelAbsBits[ctx_abs][1];
-        const bool c1ok = c1_idx < 8, c2ok = c2_idx < 1;
-        // xGetCodedLevel (:2822)
-        const bool is_last = sp == last;
-        int ctx_sig = 0, sb0 = 0, sb1 = 0;
-        if (!is_last) {
-          ctx_sig = sig_off + rd_sig_ctx<L>(pattern, c, sp, ch);
-          sb0 = est->significantBits[ctx_sig][0];
-          sb1 = est->significantBits[ctx_sig][1];
-        }
-        double cur_sig = 0, cost, cost_sig = 0;
-        int sel = 0;
-        uint32_t best = 0;
-        bool done = false;
-        if (!is_last && max_abs < 3) {
-          cost_sig = lambda * (double)sb0;
-          sel = 1;
-          cost = cc0 + cost_sig;
-          if (max_abs == 0) done = true;
-        } else {
-          cost = 1.7e+308;
-        }
-        if (!done) {
-          if (!is_last) cur_sig = lambda * (double)sb1;
-          const uint32_t min_abs = max_abs > 1 ? max_abs - 1 : 1;
-          for (int lv = (int)max_abs; lv >= (int)min_abs; lv--) {
-            const double err = (double)sub32(ld, shl32(lv, qbits));
-            double cl = err * err * escale +
-                        lambda * (double)rd_ic_rate((uint32_t)lv, (int)rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2);
-            cl += cur_sig;
-            if (cl < cost) { best = (uint32_t)lv; cost = cl; cost_sig = cur_sig; sel = is_last ? 0 : 2; }
-          }
-        }
-        cc = cost;
-        cs = cost_sig;
-        const uint32_t level = best;
-        st[(size_t)sp * G] = rd_pack(ctx_one, ctx_abs, (int)rice, c1ok, c2ok, !is_last, ctx_sig, sel);
-        out = (int32_t)level;
-        base_cost += cc;
-        const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
-        if (level >= base && level > 3u * (1u << rice)) rice = d.persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
-        if (level >= 1) c1_idx++;
-        if (level > 1) { c1 = 0; c2 += (c2 < 2); c2_idx++; }
-        else if (c1 < 3 && c1 > 0 && level) c1++;
-        if (pin == 0 && sp > 0) {
-          ctx_set = (comp ? 4 : 0) + ((comp == 0 && ((sp - 1) >> 4) > 0) ? 2 : 0) + (c1 == 0 ? 1 : 0);
-          c1 = 1; c2 = 0; c1_idx = 0; c2_idx = 0;
-          rice = rice0;
-        }
-      } else {
-        base_cost += cc0;
-      }
-      lev[(size_t)sp * G] = out;
+      const uint32_t level = act ? best : 0u;
+      const double cs = act ? cost_sig : 0.0;
+      sg.st[pin][lane] = rd_pack(4 * ctx_set + c1, ctx_set + c2, (int)rice, c1ok, c2ok, !is_last, ctx_sig, sel);
+      sg.lv[pin][lane] = (int32_t)level;
+      base_cost += act ? cost : cc0;
+      // context state after the level (:2300-2325): Rice parameter, c1Idx, c1/c2
+      const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
+      const bool rup = level >= base && level > (3u << rice);
+      rice = rup ? (persistent ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4)) : rice;
+      c1_idx += level >= 1 ? 1u : 0u;
+      const bool gt1 = level > 1;
+      c2_idx += gt1 ? 1u : 0u;
+      c2 = gt1 ? c2 + (c2 < 2) : c2;
+      c1 = gt1 ? 0 : ((c1 < 3 && c1 > 0 && level) ? c1 + 1 : c1);
       sig_cost += cs;
       if (pin == 0) sig_cost0 = cs;
-      if (out) {
-        any = true;
-        coded_ld += cc - cs;
-        uncoded += cc0;
-        if (pin != 0) nnz0++;
-      }
+      const bool nz = level != 0;
+      any = any || nz;
+      coded_ld = nz ? coded_ld + (cost - cs) : coded_ld;
+      uncoded = nz ? uncoded + cc0 : uncoded;
+      nnz0 += (nz && pin != 0) ? 1 : 0;
     }
+    carry = c1 == 0;
     if (any) sigmask |= 1ull << cgblk;
     if (cg_last >= 0) {
       if (cgp) {
@@ -920,12 +946,17 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
             sigmask &= ~(1ull << cgblk);
             base_cost = zero_cost;
 #pragma unroll
-            for (int pin = 0; pin < 16; pin++) lev[(size_t)(cgp * 16 + pin) * G] = 0;
+            for (int pin = 0; pin < 16; pin++) sg.lv[pin][lane] = 0;
           }
         }
       } else {
         sigmask |= 1ull << cgblk;
       }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      lev[cgp * g16 + (size_t)k * G] = sg.lv[k][lane];
+      st[cgp * g16 + (size_t)k * G] = sg.st[k][lane];
     }
   }
   if (last < 0) return 0;
@@ -957,15 +988,16 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
     base_cost -= lambda * (double)cgrate;
     if ((sigmask >> cgblk) & 1) {
       {
-        int32_t a16[16], b16[16], c16[16];
+        int32_t a16[16], b16[16];
+        uint32_t c16[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) {
           a16[k] = lev[cgp * g16 + (size_t)k * G];
           b16[k] = st[cgp * g16 + (size_t)k * G];
-          c16[k] = coef[cgp * g16 + (size_t)k * G];
+          c16[k] = ldI[cgp * g16 + (size_t)k * G];
         }
 #pragma unroll
-        for (int k = 0; k < 16; k++) { sg.lv[k][lane] = a16[k]; sg.st[k][lane] = b16[k]; sg.cf[k][lane] = c16[k]; }
+        for (int k = 0; k < 16; k++) { sg.lv[k][lane] = a16[k]; sg.st[k][lane] = b16[k]; sg.ld[k][lane] = c16[k]; }
       }
       for (int pin = 15; pin >= 0; pin--) {
         const int sp = cgp * 16 + pin;
@@ -982,7 +1014,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
           const double total = base_cost + cl - cs;
           if (total < best_cost) { best_p1 = sp + 1; best_cost = total; }
           if (lvv > 1) { found = true; break; }
-          const int32_t ld = rd_level_double(sg.cf[pin][lane], qc, lim);
+          const int32_t ld = (int32_t)(sg.ld[pin][lane] & 0x7fffffffu);
           const double err = (double)sub32(ld, shl32(1, qbits));
           const int rate = rd_ic_rate(1u, x.rice, x.c1ok, x.c2ok, est->greaterOneBits[x.ctx_one][0],
                                       est->greaterOneBits[x.ctx_one][1], est->levelAbsBits[x.ctx_abs][0],
@@ -1002,11 +1034,12 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
   // ---- signs, zeroing past the chosen last position, uiAbsSum ----
   int32_t abs_sum = 0;
   for (int cgp = 0; cgp <= (last >> 4); cgp++) {
-    int32_t lv16[16], cf16[16];
+    int32_t lv16[16];
+    uint32_t cf16[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       lv16[k] = lev[cgp * g16 + (size_t)k * G];
-      cf16[k] = coef[cgp * g16 + (size_t)k * G];
+      cf16[k] = ldI[cgp * g16 + (size_t)k * G];
     }
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -1014,7 +1047,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
       if (sp > last) continue;
       if (sp < best_p1) {
         abs_sum += lv16[k];
-        if (cf16[k] < 0) lev[cgp * g16 + (size_t)k * G] = -lv16[k];
+        if (cf16[k] >> 31) lev[cgp * g16 + (size_t)k * G] = -lv16[k];
       } else {
         lev[cgp * g16 + (size_t)k * G] = 0;
       }
@@ -1043,21 +1076,23 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
         const uint32_t signbit = sg.lv[first_nz][lane] > 0 ? 0 : 1;
         if (signbit != (uint32_t)(abs_in & 1)) {
           {
-            int32_t b16[16], c16[16];
+            int32_t b16[16];
+            uint32_t c16[16];
 #pragma unroll
             for (int q = 0; q < 16; q++) {
-              c16[q] = coef[sub * g16 + (size_t)q * G];
+              c16[q] = ldI[sub * g16 + (size_t)q * G];
               b16[q] = st[sub * g16 + (size_t)q * G];
             }
 #pragma unroll
-            for (int q = 0; q < 16; q++) { sg.cf[q][lane] = c16[q]; sg.st[q][lane] = b16[q]; }
+            for (int q = 0; q < 16; q++) { sg.ld[q][lane] = c16[q]; sg.st[q][lane] = b16[q]; }
           }
           int64_t min_inc = INT64_MAX, cur = INT64_MAX;
           int min_k = -1, fch = 0, cch = 0;
           for (k = (last_cg == 1 ? last_nz : 15); k >= 0; k--) {
             const int32_t lv = sg.lv[k][lane];
             const uint32_t lev0 = (uint32_t)abs(lv);
-            const int32_t ld = rd_level_double(sg.cf[k][lane], qc, lim);
+            const uint32_t wk = sg.ld[k][lane];
+            const int32_t ld = (int32_t)(wk & 0x7fffffffu);
             const int32_t du = sub32(ld, shl32((int32_t)lev0, qbits)) >> (qbits - 8);
             const RdCtx x = rd_unpack(sg.st[k][lane]);
             const int g0 = est->greaterOneBits[x.ctx_one][0];
@@ -1080,16 +1115,15 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
               cur = rdf * (-(abs(du))) + (1 << 15) + rup + sigd;
               cch = 1;
               if (k < first_nz) {
-                const uint32_t tsb = sg.cf[k][lane] >= 0 ? 0 : 1;
+                const uint32_t tsb = wk >> 31;
                 if (tsb != signbit) cur = INT64_MAX;
               }
             }
             if (cur < min_inc) { min_inc = cur; fch = cch; min_k = k; }
           }
           int32_t mv = sg.lv[min_k][lane];
-          const int32_t mc = sg.cf[min_k][lane];
           if (mv == ecmax || mv == ecmin) fch = -1;
-          if (mc >= 0) mv += fch;
+          if (!(sg.ld[min_k][lane] >> 31)) mv += fch;
           else mv -= fch;
           lev[sub * g16 + (size_t)min_k * G] = mv;
         }
@@ -1100,15 +1134,16 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
   return abs_sum;
 }
 
-// transformNxN up to (not including) RDOQ, wave per TU.  RDOQ TUs: coefficients in scan
-// order -> coefI, flag 1.  Others (bypass, plain quant, RDOQ not needed): final levels in
+// transformNxN up to (not including) RDOQ, wave per TU.  RDOQ TUs: per scan position the
+// state-independent inputs of the lane-parallel RDOQ (lLevelDouble | sign -> ldI, the
+// significance context under each neighbour pattern -> cxI), flag 1.  Others (bypass, plain quant, RDOQ not needed): final levels in
 // scan order -> levI, uiAbsSum -> abs_out, flag 0.
 template <int L>
 __global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
                                                int n, const int16_t *__restrict__ res_in, int32_t *__restrict__ temp_out,
-                                               int32_t *__restrict__ arl_out, int32_t *__restrict__ coefI,
-                                               int32_t *__restrict__ levI, int32_t *__restrict__ abs_out,
-                                               int8_t *__restrict__ flags, int G) {
+                                               int32_t *__restrict__ arl_out, uint32_t *__restrict__ ldI,
+                                               uint32_t *__restrict__ cxI, int32_t *__restrict__ levI,
+                                               int32_t *__restrict__ abs_out, int8_t *__restrict__ flags, int G) {
   constexpr int N = 4 << L, NN = N * N;
   __shared__ TuSmem<L> s;
   const int t = blockIdx.x;
@@ -1155,10 +1190,18 @@ __global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ d
         rdoq = true;
         const int64_t lim = (int64_t)2147483647 - ((int64_t)1 << (qbits - 1));
         const int qbits_c = qbits - 7, add_c = 1 << (qbits_c - 1);
+        const int ch = d.comp ? 1 : 0, sig_off = ch ? 28 : 0;
         for (int sp = lane; sp < NN; sp += HVX_WAVE) {
           const int blk = c.scan[sp];
-          coefI[tu_il(t, sp, NN, G)] = s.coef[blk];
-          if (arl) arl[blk] = d.adaptive_qp_select ? (rd_level_double(s.coef[blk], qc, lim) + add_c) >> qbits_c : 0;
+          const int32_t cf = s.coef[blk];
+          const int32_t ld = rd_level_double(cf, qc, lim);
+          const size_t il = tu_il(t, sp, NN, G);
+          ldI[il] = (uint32_t)ld | (cf < 0 ? 0x80000000u : 0u);
+          uint32_t cx = 0;
+#pragma unroll
+          for (int p = 0; p < 4; p++) cx |= (uint32_t)(sig_off + rd_sig_ctx<L>(p, c, sp, ch)) << (6 * p);
+          cxI[il] = cx;
+          if (arl) arl[blk] = d.adaptive_qp_select ? (ld + add_c) >> qbits_c : 0;
         }
       } else {
         for (int i = lane; i < NN; i += HVX_WAVE) {
@@ -1186,9 +1229,10 @@ __global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ d
 template <int L>
 __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ descs, const hvx_estbits *__restrict__ est,
                                                 const int32_t *__restrict__ est_idx, int n,
-                                                const int32_t *__restrict__ coefI, int32_t *__restrict__ levI,
-                                                int32_t *__restrict__ stI, int32_t *__restrict__ abs_out,
-                                                const int8_t *__restrict__ flags, int G, int n_est_lds) {
+                                                const uint32_t *__restrict__ ldI, const uint32_t *__restrict__ cxI,
+                                                int32_t *__restrict__ levI, int32_t *__restrict__ stI,
+                                                int32_t *__restrict__ abs_out, const int8_t *__restrict__ flags, int G,
+                                                int n_est_lds) {
   constexpr int N = 4 << L, NN = N * N;
   __shared__ hvx_estbits tbl[4];
   __shared__ RdLaneStage stage;
@@ -1208,7 +1252,7 @@ __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ 
   const int ei = est_idx ? est_idx[t] : t;
   const hvx_estbits *e = n_est_lds > 0 ? &tbl[ei] : est + ei;
   const size_t base = tu_il(t, 0, NN, G);
-  const int32_t a = rdoq_lane<L>(d, e, coefI + base, levI + base, stI + base, G, stage, lane);
+  const int32_t a = rdoq_lane<L>(d, e, ldI + base, cxI + base, levI + base, stI + base, G, stage, lane);
   if (abs_out) abs_out[t] = a;
 }
 
