@@ -580,9 +580,12 @@ template <int S, int NW, typename TO = uint8_t>
 struct MeFracSmem {
   static constexpr int HS = S + 8;
   int16_t hp[3][(S + 8) * HS];  // first-stage intermediates of the 3 horizontal phases, rows iy-4 ..
-  uint8_t blk[NW][S * S];       // per-wave candidate block (per-lane-tile SATD path)
+  // per-wave candidate block of the per-lane-tile SATD path: only shapes that are not multiples
+  // of 8 (<= 16 rows) take it, so 16 rows of the S stride suffice above S = 32
+  uint8_t blk[NW][S <= 32 ? S * S : 16 * S];
   TO org[S * S];                // the search pattern: the original (8-bit) or a bi target (int16)
   uint32_t cost[9];
+  uint32_t part[NW][3][4];      // per-wave SATD partial sums of the 9 candidates (me_sum9 slots)
 };
 
 typedef short me_s2 __attribute__((ext_vector_type(2)));
@@ -789,14 +792,15 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
     }
   }
   __syncthreads();
-  // 2. the 9 candidates' costs (SATD or SAD + MV cost), spread over the waves
-  const bool xl = had && (!GENERIC || ((w % 8 == 0) && (h % 8 == 0))) && (w * h <= 1024);
+  // 2. the 9 candidates' costs (SATD or SAD + MV cost)
+  const bool xl = had && (!GENERIC || ((w % 8 == 0) && (h % 8 == 0)));
   const int tw = w >> 3, nt = (w * h) >> 6;
   int hx, hy;
   me_had_xy(lane, hx, hy);
-  if (xl && NW == 1) {
-    // one wave, all 9 candidates: per column phase c the 9-row window of hp[c] the 3 vertical
-    // phases need is read once; the 9 tiles' Hadamards run side by side on DPP butterflies
+  if (xl) {
+    // all 9 candidates per 8x8 tile, the tiles spread over the job's waves: per column phase c
+    // the 9-row window of hp[c] the 3 vertical phases need is read once; the 9 tiles' Hadamards
+    // run side by side on DPP butterflies and are summed together (me_sum9)
     int offs[3], fys[3];
     int ryb = 0;
 #pragma unroll
@@ -806,7 +810,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
       offs[d] = ry - ryb; fys[d] = qy & 3;
     }
     uint32_t acc[3] = {0u, 0u, 0u};
-    for (int t = 0; t < nt; t++) {
+    for (int t = wave; t < nt; t += NW) {
       const int x = ((t % tw) << 3) + hx, y = ((t / tw) << 3) + hy;
       const int o = sm.org[y * S + x];
       int v[9];
@@ -831,53 +835,34 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
     // put there; the first minimum in the reference's candidate order is a (cost, index) key-min
     const int kk = lane & 15, r = lane >> 4;
     const bool valid = kk < 2 || (kk == 2 && r == 0);
+    uint32_t dsum = kk == 0 ? acc[0] : kk == 1 ? acc[1] : acc[2];
+    if constexpr (NW > 1) {  // the waves' partial sums, added in wave order through LDS
+      if (kk == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) sm.part[wave][k][r] = acc[k];
+      }
+      __syncthreads();
+      dsum = 0;
+      if (valid) {
+#pragma unroll
+        for (int ww = 0; ww < NW; ww++) dsum += sm.part[ww][kk < 3 ? kk : 0][r];
+      }
+    }
     const int sl = kk >= 2 ? 8 : 4 * kk + ((0xD8 >> (2 * r)) & 3);
     const int c = (sl * 11) >> 5, dx = c - 1, dy = sl - 3 * c - 1;  // sl / 3, sl % 3 for sl < 9
     const uint64_t idx = step == 2 ? kRefSlotH : kRefSlotQ;
     const int ci = (int)((idx >> (4 * sl)) & 15);
-    const uint32_t dsum = kk == 0 ? acc[0] : kk == 1 ? acc[1] : acc[2];
     const uint32_t cost = dsum + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
     const uint32_t key = wave_min_key(valid ? (cost << 4) | (uint32_t)ci : kMeKeyNone);
     bi = (int)(key & 15u);
     return key >> 4;
-  } else if (xl) {
-    // this wave's candidates i = wave + NW*ii share each tile pass: their sample gathers and
-    // Hadamard butterflies are independent and interleave
-    constexpr int CPW = (9 + NW - 1) / NW;
-    int cc[CPW], cry[CPW], cfy[CPW];
-    uint32_t dsum[CPW];
-#pragma unroll
-    for (int ii = 0; ii < CPW; ii++) {
-      const int i = wave + NW * ii < 9 ? wave + NW * ii : 0;
-      const int dx = step == 2 ? kRefH[i][0] : kRefQ[i][0], dy = step == 2 ? kRefH[i][1] : kRefQ[i][1];
-      const int qy = qy0 + dy * step;
-      cc[ii] = dx + 1; cry[ii] = (qy >> 2) - iy; cfy[ii] = qy & 3; dsum[ii] = 0;
-    }
-    for (int t = 0; t < nt; t++) {
-      const int x = ((t % tw) << 3) + hx, y = ((t / tw) << 3) + hy;
-      const int o = sm.org[y * S + x];
-      int v[CPW];
-#pragma unroll
-      for (int ii = 0; ii < CPW; ii++) v[ii] = o - me_frac_sample(sm, me_sel3(po, cc[ii]), cry[ii], cfy[ii], x, y);
-      had8_xlane_dpp<CPW>(v);
-#pragma unroll
-      for (int ii = 0; ii < CPW; ii++) dsum[ii] += (wave_sum_dpp((uint32_t)abs(v[ii])) + 2) >> 2;
-    }
-#pragma unroll
-    for (int ii = 0; ii < CPW; ii++) {
-      const int i = wave + NW * ii;
-      if (i < 9 && lane == 0) {
-        const int dx = step == 2 ? kRefH[i][0] : kRefQ[i][0], dy = step == 2 ? kRefH[i][1] : kRefQ[i][1];
-        sm.cost[i] = dsum[ii] + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
-      }
-    }
   }
   for (int i = wave; i < 9 && !xl; i += NW) {
     const int dx = step == 2 ? kRefH[i][0] : kRefQ[i][0], dy = step == 2 ? kRefH[i][1] : kRefQ[i][1];
     const int qy = qy0 + dy * step, ry = (qy >> 2) - iy, fy = qy & 3, c = dx + 1;
     uint32_t d = 0;
     if (had) {
-      if (GENERIC || S * S > 1024) {
+      if (GENERIC) {
         uint8_t *blk = sm.blk[wave];
         for (int k = lane; k < w * h; k += HVX_WAVE) {
           const int y = k / w, x = k - y * w;
