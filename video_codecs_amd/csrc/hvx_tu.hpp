@@ -792,7 +792,9 @@ struct RdLaneStage {
   int32_t lv[16][64], st[16][64];
 };
 
-template <int L>
+// FAST: the wave's tables are in LDS and no TU of the wave uses extended precision (the
+// limited-prefix escape code), so every table read is a ds_read and the rate has no branch.
+template <int L, bool FAST>
 __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const uint32_t *ldI, const uint32_t *cxI,
                              int32_t *lev, int32_t *st, int G, RdLaneStage &sg, int lane) {
   constexpr int N = 4 << L, NN = N * N, NCG = NN / 16;
@@ -891,8 +893,8 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
 #pragma unroll
       for (int k = 0; k < 2; k++) {
         const uint32_t lv = max_abs - (uint32_t)k;
-        const int r = ext ? rd_ic_rate(lv, (int)rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2)
-                          : rd_ic_rate_bf(lv, rice, c1ok, c2ok, g0, g1, a0, a1);
+        const int r = (!FAST && ext) ? rd_ic_rate(lv, (int)rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2)
+                                     : rd_ic_rate_bf(lv, rice, c1ok, c2ok, g0, g1, a0, a1);
         const double err = (double)sub32(ld, shl32((int32_t)lv, qbits));
         double cl = err * err * escale + lambda * (double)r;
         cl += cur_sig;
@@ -1250,9 +1252,14 @@ __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ 
   const hvx_tu_desc d = descs[t];
   if (d.width != N || d.height != N) return;
   const int ei = est_idx ? est_idx[t] : t;
-  const hvx_estbits *e = n_est_lds > 0 ? &tbl[ei] : est + ei;
   const size_t base = tu_il(t, 0, NN, G);
-  const int32_t a = rdoq_lane<L>(d, e, ldI + base, cxI + base, levI + base, stI + base, G, stage, lane);
+  const bool any_ext = __builtin_amdgcn_ballot_w64(d.extended_precision != 0) != 0;
+  int32_t a;
+  if (n_est_lds > 0 && !any_ext)
+    a = rdoq_lane<L, true>(d, &tbl[ei], ldI + base, cxI + base, levI + base, stI + base, G, stage, lane);
+  else
+    a = rdoq_lane<L, false>(d, n_est_lds > 0 ? &tbl[ei] : est + ei, ldI + base, cxI + base, levI + base, stI + base, G,
+                            stage, lane);
   if (abs_out) abs_out[t] = a;
 }
 
