@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """Benchmark: 64x64 CTUs/s of CU mode decision (ME + transform + RDOQ) on 2160p random YUV.
 
-One step = one 3840x2160 picture (2040 CTUs): hvx_ctu_analyze (for each of the 85 CUs of every
-CTU: TZ integer + half/quarter motion search against 4 reference pictures, luma MC of the best
-reference, transform + RDOQ + dequant + inverse transform + SSE of every TU), then
-hvx_ctu_decide (CABAC coefficient rate of every TU, the residual and CU-quadtree RD decisions,
-the reconstructed picture, and the reference picture: boundary strengths of the decided trees,
-luma deblocking, extended borders) -- DESIGN.md sections 3 and 3a.  Inputs are
-resident in HBM before timing starts.
+One step = one 3840x2160 4:2:0 picture (2040 CTUs) through hvx_ctu_encode_yuv: for each of the 85
+CUs of every CTU, TZ integer + half/quarter motion search against 4 reference pictures, luma and
+chroma MC of the best reference, transform + RDOQ + dequant + inverse transform + SSE of every
+Y/Cb/Cr TU; then the CABAC coefficient rate of every TU, the residual and CU-quadtree RD decisions
+(chroma-weighted distortion), the reconstructed Y/Cb/Cr picture, and the reference picture
+(boundary strengths of the decided trees, deblocking, extended borders) -- DESIGN.md sections 3
+and 3a.  Inputs are resident in HBM before timing starts.
 
 Multi-GPU (torch.distributed.run): one rank per GPU, each rank encodes its own independent GOP
 segment (different synthetic frames); the only collective is the per-picture gather of every
@@ -51,17 +51,39 @@ def parse():
     return p.parse_args()
 
 
-def b_ctu_luma(nref):
+def b_ctu(nref):
     """SURVEY.md 8(d) algorithmic bytes per CTU, B = S(1 + N_ref + 1) + 2S + 16(64*64/16), with
-    S = 64*64 (the pass is luma-only): read the original and N_ref references once, write the
-    reconstruction, int16 levels and the 16 B-per-4x4 MV/mode field."""
-    S = 64 * 64
+    S = 64*64*1.5 (4:2:0): read the original and N_ref references once, write the reconstruction,
+    int16 levels and the 16 B-per-4x4 MV/mode field (53,248 B at N_ref = 4)."""
+    S = 64 * 64 * 3 // 2
     return S * (1 + nref + 1) + 2 * S + 16 * (64 * 64 // 16)
 
 
 def luma_plane(w, h, index):
     from video_codecs_amd import synth  # synthetic-input recipe (BASELINE.md section 3)
     return synth.luma_plane(w, h, index)
+
+
+def yuv_planes(w, h, index):
+    from video_codecs_amd import synth
+    return synth.yuv_planes(w, h, index)
+
+
+class YuvInputs:
+    """A segment's current picture and references as device-resident padded Y/Cb/Cr planes, with the
+    origin-pointer tables hvx_ctu_encode_yuv reads (references' Y; their Cb then their Cr)."""
+
+    def __init__(self, W, H, frames):
+        import torch
+        from video_codecs_amd import _abi, hvx
+        pl = [yuv_planes(W, H, f) for f in frames]
+        self.host = pl
+        self.cur = [torch.from_numpy(x).cuda() for x in pl[-1]]
+        self.refs = [[torch.from_numpy(x).cuda() for x in p] for p in pl[:-1]]
+        mc = _abi.PLANE_MARGIN // 2
+        self.ptr_y = torch.tensor([hvx.plane_origin_ptr(r[0], W) for r in self.refs], dtype=torch.int64).cuda()
+        self.ptr_c = torch.tensor([hvx.plane_origin_ptr(r[c], W // 2, mc) for c in (1, 2) for r in self.refs],
+                                  dtype=torch.int64).cuda()
 
 
 def segment_frames(rank, nref):
@@ -134,20 +156,18 @@ def main():
     from video_codecs_amd.dpb import DpbGather
 
     W, H, nref = args.width, args.height, args.nref
-    planes = [luma_plane(W, H, f) for f in segment_frames(rank, nref)]
-    cur_t = torch.from_numpy(planes[nref]).cuda()
-    ref_t = [torch.from_numpy(p).cuda() for p in planes[:nref]]
-    ref_ptrs = torch.tensor([hvx.plane_origin_ptr(t, W) for t in ref_t], dtype=torch.int64).cuda()
-    an = hvx.CtuAnalyzer(W, H, nref, args.qp)
+    inp = YuvInputs(W, H, segment_frames(rank, nref))
+    cur_t = inp.cur[0]
+    an = hvx.CtuAnalyzer(W, H, nref, args.qp, chroma=True)
     nctu = an.nctu
-    dpb = DpbGather(world, rank, tuple(cur_t.shape), "cuda")
-
-    recon_t = torch.zeros_like(cur_t)
+    # the reference picture (Y | Cb | Cr padded planes in one buffer): one gather per picture
+    dpb = DpbGather(world, rank, (hvx.yuv_bytes(W, H),), "cuda")
+    recon = hvx.yuv_views(torch.zeros(hvx.yuv_bytes(W, H), dtype=torch.uint8, device="cuda"), W, H)
 
     def step():
-        # one picture: analysis (ME + TU pipeline) -> CU decision + reconstruction -> deblocked
-        # reference picture -> DPB gather of that reference
-        an.encode(cur_t, ref_ptrs, recon_t, dpb.buffer())  # hvx_ctu_encode = hvx_ctu_analyze + hvx_ctu_decide
+        # one picture: analysis (ME + Y/Cb/Cr TU pipelines) -> CU decision + reconstruction ->
+        # deblocked reference picture -> DPB gather of that reference
+        an.encode_yuv(inp.cur, inp.ptr_y, inp.ptr_c, recon, hvx.yuv_views(dpb.buffer(), W, H))
         dpb.send()
 
     def sync():
@@ -161,8 +181,8 @@ def main():
     phases = phase_pass(step, args.steps, sync)
     gpu_res, gpu_dec = an.results(), an.decisions()
     own, gathered = dpb.last()
-    gpu_rec = recon_t.cpu().numpy()
-    gpu_refpic = own.cpu().numpy()
+    gpu_rec = [x.cpu().numpy() for x in recon]
+    gpu_refpic = [x.cpu().numpy() for x in hvx.yuv_views(own, W, H)]
     dpb_ok = None
     if gathered is not None:  # rank 0 holds every rank's picture; its own slot must be its own
         dpb_ok = bool(torch.equal(gathered[0], own))
@@ -172,13 +192,13 @@ def main():
         # roofline of the dominant kernel = the longest single launch of the step, timed with
         # HIP events on the launch stream (a begin/end pair around exactly one launch; the pass
         # runs on 3 streams, so phases overlap and their sum exceeds ms_per_step).
-        # Algorithmic bytes per launch = SURVEY 8(d)'s per-CTU figure (luma form, DESIGN.md
-        # "Roofline") x the CTUs one launch covers (every launch of the pass covers the picture).
+        # Algorithmic bytes per launch = SURVEY 8(d)'s per-CTU figure (4:2:0, DESIGN.md "Roofline")
+        # x the CTUs one launch covers (every launch of the pass covers the picture).
         single = {k: p for k, p, nl in zip(hvx.PHASE_KERNELS, hvx.PHASES, hvx.PHASE_LAUNCHES) if nl == 1}
         kernel = max(single, key=lambda k: phases[single[k]])
         launch_ms = phases[single[kernel]] / args.steps
-        b_ctu = b_ctu_luma(nref)
-        bytes_per_launch = b_ctu * nctu
+        bpc = b_ctu(nref)
+        bytes_per_launch = bpc * nctu
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         traffic = None
         tr_path = os.path.join(ROOT, "profiles", "hbm_traffic_r01.json")
@@ -199,9 +219,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: splitmix64 uniform random 8-bit luma (BASELINE.md sec. 3), independent segment per rank",
-            "config": {"workload": "CTU mode decision: 85 CUs x TZ+frac ME vs %d refs, MC, TU RDOQ/dequant/IT, "
-                                   "CABAC coefficient rate, CU quadtree RD decision, reconstruction, deblocked reference picture" % nref,
+            "data": "synthetic: splitmix64 uniform random 8-bit 4:2:0 YUV (BASELINE.md sec. 3), independent segment per rank",
+            "config": {"workload": "CTU mode decision, 4:2:0: 85 CUs x TZ+frac ME vs %d refs, luma+chroma MC, Y/Cb/Cr TU "
+                                   "RDOQ/dequant/IT, CABAC coefficient rate, CU quadtree RD decision, Y/Cb/Cr "
+                                   "reconstruction, deblocked reference picture" % nref,
                        "resolution": f"{W}x{H}", "ctus_per_frame": nctu, "qp": args.qp, "search_range": 64,
                        "n_ref": nref, "parallelism": f"segments x{world}",
                        "dpb": "gather of every rank's deblocked reference picture to rank 0 per step" if world > 1 else "local"},
@@ -211,23 +232,24 @@ def main():
             "roofline": {"bound": "hbm", "limiter": "latency", "kernel": kernel, "achieved": round(achieved, 3),
                          "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / MI355X_HBM_PEAK_GBS,
                          "traffic": traffic, "bytes_per_launch": bytes_per_launch,
-                         "avg_launch_ms": round(launch_ms, 3), "b_ctu": b_ctu,
-                         "path_achieved_gbs": round(b_ctu * nctu / step_s / 1e9, 3),
-                         "path_frac": b_ctu * nctu / step_s / 1e9 / MI355X_HBM_PEAK_GBS},
+                         "avg_launch_ms": round(launch_ms, 3), "b_ctu": bpc,
+                         "path_achieved_gbs": round(bpc * nctu / step_s / 1e9, 3),
+                         "path_frac": bpc * nctu / step_s / 1e9 / MI355X_HBM_PEAK_GBS},
             "cpu_baseline": None,
         }
         if dpb_ok is not None:
             out["dpb_gather_ok"] = dpb_ok
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(planes, an, gpu_res, gpu_dec, gpu_rec, gpu_refpic, args)
+            out["cpu_baseline"] = cpu_baseline(inp.host, an, gpu_res, gpu_dec, gpu_rec, gpu_refpic, args)
         if world == 1 and not args.no_1080p:  # side measurements: single-GPU runs only
             out["step_1080p"] = step_1080p_measure(nref, args.qp, args.steps)
         if world == 1 and not args.no_ssim:
-            out["ssim_rdo"] = ssim_rdo_measure(cur_t, ref_ptrs, W, H, nref, args.steps)
+            out["ssim_rdo"] = ssim_rdo_measure(inp, W, H, nref, args.steps)
         if world == 1 and not args.no_sao:
             out["sao"] = sao_measure(W, H, args.steps)
         if world == 1 and not args.no_intra:
-            out["intra_first_pass"] = intra_measure(cur_t, ref_t[0], W, H, float(an.params["lambda"][0]), args.steps)
+            out["intra_first_pass"] = intra_measure(cur_t, inp.refs[0][0], W, H, float(an.params["lambda"][0]),
+                                                    args.steps)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -239,39 +261,41 @@ def step_1080p_measure(nref, qp, steps):
     import torch
     from video_codecs_amd import hvx
     W, H = 1920, 1080
-    planes = [torch.from_numpy(luma_plane(W, H, 100 + f)).cuda() for f in range(nref + 1)]
-    ptrs = torch.tensor([hvx.plane_origin_ptr(t, W) for t in planes[:nref]], dtype=torch.int64).cuda()
-    an = hvx.CtuAnalyzer(W, H, nref, qp)
-    recon, refpic = torch.zeros_like(planes[nref]), torch.zeros_like(planes[nref])
-    an.encode(planes[nref], ptrs, recon, refpic)
+    inp = YuvInputs(W, H, [100 + f for f in range(nref + 1)])
+    an = hvx.CtuAnalyzer(W, H, nref, qp, chroma=True)
+    recon = [torch.zeros_like(x) for x in inp.cur]
+    refpic = [torch.zeros_like(x) for x in inp.cur]
+    an.encode_yuv(inp.cur, inp.ptr_y, inp.ptr_c, recon, refpic)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        an.encode(planes[nref], ptrs, recon, refpic)
+        an.encode_yuv(inp.cur, inp.ptr_y, inp.ptr_c, recon, refpic)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
     return {"resolution": f"{W}x{H}", "ctus_per_frame": an.nctu, "ms_per_picture": round(ms, 3),
             "ctus_per_s": round(an.nctu / ms * 1e3, 1)}
 
 
-def ssim_rdo_measure(cur_t, ref_ptrs, W, H, nref, steps):
-    """Side measurement (BASELINE config 4's RD cost, not the headline): the same picture step with
-    the SSIM CU decision (HVX_RD_SSIM: D = sum of 1 - SSIM over 8x8 blocks, lambda_2(qp)) at QP 22,
-    27, 32, 37 -- wall time per picture and the leaf CUs chosen (vs the SSE decision at that QP)."""
+def ssim_rdo_measure(inp, W, H, nref, steps):
+    """Side measurement (BASELINE config 4's RD cost, not the headline): the same 4:2:0 picture step
+    with the SSIM CU decision (HVX_RD_SSIM: D = sum of 1 - SSIM over the luma 8x8 blocks,
+    lambda_2(qp)) at QP 22, 27, 32, 37 -- wall time per picture and the leaf CUs chosen (vs the SSE
+    decision at that QP)."""
     import torch
     from video_codecs_amd import _abi, hvx
     res = {}
-    recon, refpic = torch.zeros_like(cur_t), torch.zeros_like(cur_t)
+    recon = [torch.zeros_like(x) for x in inp.cur]
+    refpic = [torch.zeros_like(x) for x in inp.cur]
     for qp in (22, 27, 32, 37):
         leaves = {}
         for metric in (_abi.RD_SSIM, _abi.RD_SSE):
-            an = hvx.CtuAnalyzer(W, H, nref, qp, rd_metric=metric)
-            an.encode(cur_t, ref_ptrs, recon, refpic)
+            an = hvx.CtuAnalyzer(W, H, nref, qp, rd_metric=metric, chroma=True)
+            an.encode_yuv(inp.cur, inp.ptr_y, inp.ptr_c, recon, refpic)
             torch.cuda.synchronize()
             if metric == _abi.RD_SSIM:
                 t0 = time.perf_counter()
                 for _ in range(steps):
-                    an.encode(cur_t, ref_ptrs, recon, refpic)
+                    an.encode_yuv(inp.cur, inp.ptr_y, inp.ptr_c, recon, refpic)
                 torch.cuda.synchronize()
                 ms = (time.perf_counter() - t0) / steps * 1e3
             leaves[metric] = int(an.decisions()["leaf"].sum())
@@ -360,27 +384,33 @@ def intra_measure(cur_t, rec_t, W, H, lam, steps):
             "ctus_per_s": round(((W + 63) // 64) * ((H + 63) // 64) / ms * 1e3, 1)}
 
 
-def cpu_baseline(planes, an, gpu_res, gpu_dec, gpu_rec, gpu_refpic, args):
+def cpu_baseline(host, an, gpu_res, gpu_dec, gpu_rec, gpu_refpic, args):
     """The oracle (scalar C port of the same step, 1 core) on a bounded sample of the same
     picture's CTUs in raster order; also checks the GPU's CU results, CU decisions and
-    reconstructed samples of every sampled CTU."""
+    reconstructed Y/Cb/Cr samples of every sampled CTU, and the whole reference picture."""
     import oracle
     from video_codecs_amd import _abi
     nref = args.nref
-    est, st, eb = _abi.load_estbits_p_luma(), _abi.load_ctx_p_states(), _abi.load_entropy_bits()
+    est7 = _abi.estbits_p_yuv(oracle.estbits_update)
+    st, eb = _abi.load_ctx_p_states(), _abi.load_entropy_bits()
     ncx = (args.width + 63) // 64
-    M = _abi.PLANE_MARGIN
-    rec = np.zeros_like(planes[nref])
+    M, Mc = _abi.PLANE_MARGIN, _abi.PLANE_MARGIN // 2
+    cur, refs = host[nref], host[:nref]
+    refs3 = ([r[0] for r in refs], [r[1] for r in refs], [r[2] for r in refs])
+    rec = [np.zeros_like(x) for x in cur]
     n_done, mismatches = 0, 0
     t0 = time.perf_counter()
     for c in range(an.nctu):
         cx, cy = c % ncx, c // ncx
-        r, d = oracle.ctu_decide(planes[nref], planes[:nref], an.params, est, st, eb, cx, cy, rec)
-        ys = slice(M + cy * 64, M + min(args.height, cy * 64 + 64))
-        xs = slice(M + cx * 64, M + min(args.width, cx * 64 + 64))
-        if (r.tobytes() != gpu_res[c].tobytes() or d.tobytes() != gpu_dec[c].tobytes()
-                or not np.array_equal(rec[ys, xs], gpu_rec[ys, xs])):
-            mismatches += 1
+        r, d = oracle.ctu_decide_yuv(cur, refs3, an.params, est7, st, eb, cx, cy, rec)
+        same = r.tobytes() == gpu_res[c].tobytes() and d.tobytes() == gpu_dec[c].tobytes()
+        for k in range(3):
+            m, s = (M, 64) if k == 0 else (Mc, 32)
+            w, h = (args.width, args.height) if k == 0 else (args.width // 2, args.height // 2)
+            ys = slice(m + cy * s, m + min(h, cy * s + s))
+            xs = slice(m + cx * s, m + min(w, cx * s + s))
+            same = same and np.array_equal(rec[k][ys, xs], gpu_rec[k][ys, xs])
+        mismatches += 0 if same else 1
         n_done += 1
         if time.perf_counter() - t0 > args.cpu_seconds:
             break
@@ -388,11 +418,13 @@ def cpu_baseline(planes, an, gpu_res, gpu_dec, gpu_rec, gpu_refpic, args):
     W, H = args.width, args.height
     bv, bh = oracle.ctu_bs(gpu_res.reshape(-1), gpu_dec.reshape(-1), W, H)
     qp = np.full(len(bv), int(an.params["qp"][0]), np.int8)
-    zc = np.zeros((H // 2, W // 2), np.uint8)
-    dy, _, _ = oracle.deblock(gpu_rec[M:M + H, M:M + W], zc, zc, bv, bh, qp, _abi.deblock_params(W, H))
-    refpic_ok = bool(np.array_equal(gpu_refpic, np.pad(dy, M, mode="edge")))
+    inner = [gpu_rec[0][M:M + H, M:M + W], gpu_rec[1][Mc:Mc + H // 2, Mc:Mc + W // 2],
+             gpu_rec[2][Mc:Mc + H // 2, Mc:Mc + W // 2]]
+    dy, dcb, dcr = oracle.deblock(inner[0], inner[1], inner[2], bv, bh, qp, _abi.deblock_params(W, H))
+    refpic_ok = all(bool(np.array_equal(gpu_refpic[k], np.pad(p, M if k == 0 else Mc, mode="edge")))
+                    for k, p in enumerate((dy, dcb, dcr)))
     return {"value": round(n_done / dt, 3), "unit": "CTUs/s", "cores": 1, "kind": "port",
-            "sample": f"first {n_done} CTUs (raster) of the same 2160p picture, {dt:.1f} s, oracle/hvx_oracle.c",
+            "sample": f"first {n_done} CTUs (raster) of the same 2160p 4:2:0 picture, {dt:.1f} s, oracle/hvx_oracle.c",
             "gpu_parity_ctus": n_done, "gpu_parity_mismatches": mismatches,
             "gpu_ref_picture_ok": refpic_ok}
 

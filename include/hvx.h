@@ -329,6 +329,23 @@ int hvx_ctu_encode(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_r
                    const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes, hvx_cu_result *d_cu,
                    hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic);
 
+/* The whole picture step at 4:2:0 (YUV): hvx_ctu_encode plus, for every CU, the chroma of
+ * TEncSearch::encodeResAndCalcRdInterCU -- Cb/Cr motion compensation at the chosen MV (4-tap,
+ * 1/8 sample, TComPrediction::xPredInterBlk), the Cb and Cr TUs (half the luma TU) through
+ * transformNxN (RDOQ with the chroma QP and lambda_chroma, chroma estBits) + invTransformNxN, their
+ * coefficient rate and cbf flags, xEstimateInterResidualQT's forced-zero test per TU and component
+ * with chroma distortions weighted by chroma_weight (TComRdCost::getDistPart), the qt_root_cbf test
+ * and the leaf distortion over all three components; the leaves' Y, Cb and Cr are reconstructed and,
+ * with d_ref_pic, deblocked (loopFilterPic luma + chroma) and border-extended.  h_params->chroma_format
+ * must be 1 (hvx_ctu_analyze / _decide / _encode require 0); d_est7 = 7 device estBits tables
+ * (luma TU 4x4..32x32, chroma TU 4x4..16x16); h_chroma (host struct of device pointers, hvx_types.h)
+ * gives the chroma planes.  hvx_cu_result keeps the luma sums; hvx_cu_decision.cbf carries the
+ * chroma TU flags in bits 4..11. */
+int hvx_ctu_encode_yuv(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
+                       const hvx_chroma_planes *h_chroma, const hvx_ctu_params *h_params, const hvx_estbits *d_est7,
+                       const uint8_t *d_ctx_states, const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes,
+                       hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic);
+
 /* ---------------------------------------------------------------------------------------
  * Picture upload: HM int16 plane (width x height samples, any stride, device copy) ->
  * 8-bit padded plane (stride = width + 2*HVX_PLANE_MARGIN), borders extended.  d_plane is

@@ -125,7 +125,11 @@ typedef struct hvx_ctu_params {
   double lambda;             /* RD lambda (TComTrQuant m_dLambda for luma) */
   double lambda_ssim;        /* HVX_RD_SSIM: the SSIM-RDO lambda (stvssim.c lambda_2 :1805 x attention eta^0.85) */
   int32_t rd_metric;         /* hvx_ctu_decide's CU-level distortion: HVX_RD_SSE (HM) or HVX_RD_SSIM */
+  int32_t chroma_format;     /* 0: luma only (hvx_ctu_analyze/decide/encode); 1: 4:2:0 (hvx_ctu_encode_yuv) */
+  int32_t qp_chroma;         /* chroma QP: getScaledChromaQP(qp + chroma offset) (g_aucChromaScale, 4:2:0) */
   int32_t pad_;
+  double lambda_chroma;      /* RDOQ lambda of Cb/Cr: lambda / chroma_weight (TEncSlice::setUpLambda, RDOQ_CHROMA_LAMBDA) */
+  double chroma_weight;      /* TComRdCost::m_distortionWeight[Cb/Cr] = pow(2, (qp - qp_chroma) / 3) */
 } hvx_ctu_params;
 /* HVX_RD_SSIM (BASELINE config 4): the CU quadtree decision of hvx_ctu_decide
  * weighs D_ssim = sum over the CU's 8x8 blocks of 1 - SSIM(original, reconstruction) (compute_SSIM,
@@ -157,16 +161,29 @@ typedef struct hvx_cu_result {
  * (xCheckBestMode :1166).  All rates from one context snapshot.  One record per CU, same order
  * as hvx_cu_result. */
 typedef struct hvx_cu_decision {
-  uint64_t coef_frac;        /* sum over the CU's TUs of the counted coefficient rate (15-bit fixed point) */
-  uint32_t bits, dist;       /* the CU coded as a leaf (without its split_cu_flag) */
+  uint64_t coef_frac;        /* sum over the CU's TUs (all components) of the counted coefficient rate (15-bit fixed point) */
+  uint32_t bits, dist;       /* the CU coded as a leaf (without its split_cu_flag); 4:2:0: dist = luma SSE + each
+                                chroma SSE times chroma_weight, truncated (TComRdCost::getDistPart) */
   uint32_t best_bits, best_dist; /* the chosen sub-tree rooted at this CU, split flags included */
   int32_t split;             /* 1: the sub-tree rooted here splits (forced for CUs crossing the picture edge) */
   int32_t leaf;              /* 1: a leaf of the CTU's final CU tree (its samples are in the reconstruction) */
-  int32_t cbf;               /* bit t: luma TU t of the CU is coded (0: qt_root_cbf 0, prediction only) */
+  int32_t cbf;               /* bit t: luma TU t of the CU is coded; 4:2:0 also bit 4 + t: Cb TU t, bit 8 + t: Cr TU t
+                                (0: qt_root_cbf 0, prediction only) */
   float ssim_dist;           /* HVX_RD_SSIM: D_ssim of the CU as a leaf (8x8 blocks in raster order, float sum) */
   float best_ssim_dist;      /* HVX_RD_SSIM: D_ssim of the chosen sub-tree (children in z-order) */
   int32_t pad_;
 } hvx_cu_decision;
+
+/* The chroma planes of hvx_ctu_encode_yuv (4:2:0): device origins (sample (0,0)) of 8-bit padded
+ * planes of half the luma size with margin HVX_PLANE_MARGIN / 2 and stride c_stride (a multiple of 4).
+ * refs_c: device array of 2 * n_ref origins, the references' Cb planes then their Cr planes. */
+typedef struct hvx_chroma_planes {
+  const uint8_t *cur_cb, *cur_cr;
+  const uint8_t *const *refs_c;
+  uint8_t *recon_cb, *recon_cr;
+  uint8_t *ref_pic_cb, *ref_pic_cr;  /* NULL when no reference picture is written */
+  int32_t c_stride, pad_;
+} hvx_chroma_planes;
 
 /* One intra block: TComPrediction::initIntraPatternChType's reference
  * samples (TComPattern.cpp:115-360: fillReferenceSamples :364 substitution + the [1 2 1] /

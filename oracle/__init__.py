@@ -229,6 +229,35 @@ def ctu_decide(cur_plane, ref_planes, params, est4, states, entropy_bits, ctu_x,
     return out, dec
 
 
+def ctu_decide_yuv(cur3, refs3, params, est7, states, entropy_bits, ctu_x, ctu_y, recon3, margin=_abi.PLANE_MARGIN):
+    """hvxo_ctu_decide_yuv for one CTU (4:2:0): cur3 / recon3 = (Y, Cb, Cr) padded uint8 planes (chroma
+    margin margin // 2), refs3 = (list of Y planes, list of Cb planes, list of Cr planes), est7 = 7 estBits
+    tables (luma 4x4..32x32, chroma 4x4..16x16) -> (85 CU_RESULT, 85 CU_DECISION); the leaves' samples are
+    written into recon3 (modified in place)."""
+    L = lib()
+    P = ctypes.c_void_p
+    cs = [_c(x, np.uint8) for x in cur3]
+    offs = [margin * cs[0].shape[1] + margin, (margin // 2) * cs[1].shape[1] + margin // 2]
+    ptr = lambda a, c: a.ctypes.data + offs[1 if c else 0]  # noqa: E731
+    cur_p = (P * 3)(*[ptr(cs[c], c) for c in range(3)])
+    keep = [[_c(r, np.uint8) for r in refs3[c]] for c in range(3)]
+    rp = [(P * len(keep[c]))(*[ptr(r, c) for r in keep[c]]) for c in range(3)]
+    for c in range(3):
+        assert recon3[c].dtype == np.uint8 and recon3[c].flags.c_contiguous and recon3[c].shape == cs[c].shape
+    rec_p = (P * 3)(*[ptr(recon3[c], c) for c in range(3)])
+    p = np.ascontiguousarray(params, dtype=_abi.CTU_PARAMS).reshape(1)
+    e = _c(est7, np.int32).reshape(-1)
+    st = _c(states, np.uint8)
+    eb = _c(entropy_bits, np.int32)
+    out = np.zeros(_abi.CUS_PER_CTU, _abi.CU_RESULT)
+    dec = np.zeros(_abi.CUS_PER_CTU, _abi.CU_DECISION)
+    I = ctypes.c_int
+    L.hvxo_ctu_decide_yuv.argtypes = [P, P, P, P, I, I, P, P, P, P, I, I, P, P, P, I, I]
+    L.hvxo_ctu_decide_yuv(cur_p, rp[0], rp[1], rp[2], cs[0].shape[1], cs[1].shape[1], _p(p), _p(e), _p(st), _p(eb),
+                          ctu_x, ctu_y, _p(out), _p(dec), rec_p, cs[0].shape[1], cs[1].shape[1])
+    return out, dec
+
+
 def lambda_2(qp):
     return float(lib().hvxo_lambda_2(int(qp)))
 

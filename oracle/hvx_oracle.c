@@ -294,6 +294,40 @@ void hvxo_luma_block_qpel(const uint8_t *ref, int stride, int x, int y, int mvx,
     }
 }
 
+/* xPredInterBlk (TComPrediction.cpp:668) for a 4:2:0 chroma block of an 8-bit plane, uni-prediction:
+ * the luma quarter-pel MV in 1/8 chroma samples, the 4-tap filters (TComInterpolationFilter.cpp:67),
+ * filterHor / filterVer alone (first and last stage) or filterHor (first) then filterVer (last). */
+void hvxo_chroma_block_epel(const uint8_t *ref, int stride, int x, int y, int mvx, int mvy, int w, int h, int16_t *out,
+                            int os) {
+  static const int8_t cf[8][4] = {{0, 64, 0, 0},   {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
+                                  {-4, 36, 36, -4}, {-4, 28, 46, -6}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
+  const int fx = mvx & 7, fy = mvy & 7, ix = x + (mvx >> 3), iy = y + (mvy >> 3);
+  for (int r = 0; r < h; r++)
+    for (int c = 0; c < w; c++) {
+      const uint8_t *p = ref + (iy + r) * stride + ix + c;
+      int v;
+      if (!fx && !fy) v = p[0];
+      else if (!fy) {
+        int s = 0;
+        for (int k = 0; k < 4; k++) s += cf[fx][k] * p[k - 1];
+        v = clip_pel((s + 32) >> 6);
+      } else if (!fx) {
+        int s = 0;
+        for (int k = 0; k < 4; k++) s += cf[fy][k] * p[(k - 1) * stride];
+        v = clip_pel((s + 32) >> 6);
+      } else {
+        int s2 = 0;
+        for (int t = 0; t < 4; t++) {
+          int s = 0;
+          for (int k = 0; k < 4; k++) s += cf[fx][k] * p[(t - 1) * stride + k - 1];
+          s2 += cf[fy][t] * (int16_t)(s - IF_OFFS);
+        }
+        v = clip_pel((s2 + (1 << 11) + (IF_OFFS << 6)) >> 12);
+      }
+      out[r * os + c] = (int16_t)v;
+    }
+}
+
 /* ============================================================================================
  * Transforms: xTrMxN / xITrMxN (TComTrQuant.cpp:860-987).  Partial butterflies (:388-848) are
  * exact integer matrix products; written here as the products they compute.
@@ -1338,6 +1372,24 @@ void hvxo_ctu_tu_desc(const hvx_ctu_params *p, int cu_size, int log2, hvx_tu_des
   d->lambda = p->lambda;
 }
 
+/* the Cb/Cr TU of a CU (4:2:0, half the luma TU): chroma QP and the chroma RDOQ lambda, chroma
+ * getCtxQtCbf = the transform depth (TComDataCU.cpp:1503) */
+void hvxo_ctu_tu_desc_chroma(const hvx_ctu_params *p, int comp, int cu_size, int log2, hvx_tu_desc *d) {
+  hvxo_ctu_tu_desc(p, cu_size, log2, d);
+  d->comp = comp;
+  d->ctx_qt_cbf = cu_size > 32 ? 1 : 0;
+  d->qp_per = p->qp_chroma / 6;
+  d->qp_rem = p->qp_chroma % 6;
+  d->lambda = p->lambda_chroma;
+}
+
+/* chroma planes of the 4:2:0 analysis (hvx_chroma_planes in host form) */
+typedef struct {
+  const uint8_t *cur[2];
+  const uint8_t *const *refs[2];
+  int stride;
+} ctu_chroma;
+
 /* The analysis of one CTU; with ex != NULL it also keeps, per TU of every CU, the counted
  * coefficient rate, uiAbsSum, the coded (residual-domain) SSE and the zero-residual distortion,
  * and per CU the ME bits of the chosen reference, the prediction and the reconstructed residual
@@ -1345,16 +1397,63 @@ void hvxo_ctu_tu_desc(const hvx_ctu_params *p, int cu_size, int log2, hvx_tu_des
 typedef struct {
   const uint8_t *states;
   const int32_t *eb;
-  uint64_t coef_frac[HVX_CUS_PER_CTU][4];
-  int32_t abs_sum[HVX_CUS_PER_CTU][4];
-  uint32_t sse[HVX_CUS_PER_CTU][4], zdist[HVX_CUS_PER_CTU][4];
+  /* [cu][comp][tu]: comp 0 luma, 1 Cb, 2 Cr (4:2:0 only) */
+  uint64_t coef_frac[HVX_CUS_PER_CTU][3][4];
+  int32_t abs_sum[HVX_CUS_PER_CTU][3][4];
+  uint32_t sse[HVX_CUS_PER_CTU][3][4], zdist[HVX_CUS_PER_CTU][3][4];
   uint32_t me_bits[HVX_CUS_PER_CTU];
-  uint8_t *pred;  /* HVX_CUS_PER_CTU * 4096 */
-  int16_t *rres;  /* HVX_CUS_PER_CTU * 4096 */
+  uint8_t *pred;  /* HVX_CUS_PER_CTU * 4096 luma, then HVX_CUS_PER_CTU * 2 * 1024 chroma */
+  int16_t *rres;  /* same layout */
 } ctu_extra;
+#define EX_CHROMA(ci, c) (HVX_CUS_PER_CTU * 4096 + ((ci) * 2 + (c) - 1) * 1024)
 
-static void ctu_analyze_core(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
-                             const hvx_estbits *est, int ctu_x, int ctu_y, hvx_cu_result *out, ctu_extra *ex) {
+/* one component's TUs of a CU: residual (org - pred), transformNxN (RDOQ) + invTransformNxN + SSE
+ * per TU; with ex, the counted rate (own copy of the snapshot), uiAbsSum, SSEs, prediction and
+ * reconstructed residual.  Returns the summed (sse, abs_sum) through the pointers. */
+static void ctu_comp_tus(const uint8_t *org, int ostride, const int16_t *pred, int ps, int S, const hvx_tu_desc *td,
+                         const hvx_estbits *e, ctu_extra *ex, int ci, int comp, uint32_t *sse_sum, int32_t *abs_total,
+                         int *n_tu) {
+  const int T = td->width;
+  int16_t resi[32 * 32], rec[32 * 32];
+  for (int ty = 0; ty < S; ty += T)
+    for (int tx = 0; tx < S; tx += T) {
+      for (int yy = 0; yy < T; yy++)
+        for (int xx = 0; xx < T; xx++)
+          resi[yy * T + xx] = (int16_t)((int)org[(ty + yy) * ostride + tx + xx] - pred[(ty + yy) * ps + tx + xx]);
+      int32_t temp[1024], lev[1024], abs_sum = 0;
+      hvxo_transform_nxn(td, e, resi, T, temp, lev, NULL, &abs_sum);
+      hvxo_inv_transform_nxn(td, lev, rec, T);
+      uint32_t sse = 0;
+      for (int k = 0; k < T * T; k++) { int df = resi[k] - rec[k]; sse += (uint32_t)(df * df); }
+      if (ex) {
+        const int ti = (ty / T) * (S / T) + tx / T;
+        uint8_t st[HVX_NUM_CTX];
+        hvx_coeff_bits cb;
+        memcpy(st, ex->states, sizeof(st)); /* every TU counts from the same snapshot */
+        hvxo_coeff_bits(td, lev, st, ex->eb, &cb);
+        uint32_t zd = 0;
+        for (int k = 0; k < T * T; k++) zd += (uint32_t)(resi[k] * resi[k]);
+        ex->coef_frac[ci][comp][ti] = cb.frac_bits;
+        ex->abs_sum[ci][comp][ti] = abs_sum;
+        ex->sse[ci][comp][ti] = sse;
+        ex->zdist[ci][comp][ti] = zd;
+        const size_t base = comp ? (size_t)EX_CHROMA(ci, comp) : (size_t)ci * 4096;
+        const int es = comp ? 32 : 64;
+        for (int yy = 0; yy < T; yy++)
+          for (int xx = 0; xx < T; xx++) {
+            ex->pred[base + (ty + yy) * es + tx + xx] = (uint8_t)pred[(ty + yy) * ps + tx + xx];
+            ex->rres[base + (ty + yy) * es + tx + xx] = rec[yy * T + xx];
+          }
+      }
+      *sse_sum += sse;
+      *abs_total += abs_sum;
+      (*n_tu)++;
+    }
+}
+
+static void ctu_analyze_core(const uint8_t *cur, const uint8_t *const *refs, int stride, const ctu_chroma *cc,
+                             const hvx_ctu_params *p, const hvx_estbits *est, int ctu_x, int ctu_y, hvx_cu_result *out,
+                             ctu_extra *ex) {
   int imv[HVX_CUS_PER_CTU][8][2];
   int base = 0;
   for (int d = 0; d < 4; d++) {
@@ -1388,43 +1487,27 @@ static void ctu_analyze_core(const uint8_t *cur, const uint8_t *const *refs, int
       }
       if (ex) ex->me_bits[ci] = best.bits;
       r->mv_x = best.mv_x; r->mv_y = best.mv_y; r->me_cost = best_cost;
-      int16_t pred[64 * 64], resi[32 * 32], rec[32 * 32];
+      int16_t pred[64 * 64];
       hvxo_luma_block_qpel(refs[r->ref], stride, x, y, best.mv_x, best.mv_y, S, S, pred, 64);
       const int T = S < 32 ? S : 32, log2 = T == 4 ? 2 : T == 8 ? 3 : T == 16 ? 4 : 5;
       hvx_tu_desc td;
       hvxo_ctu_tu_desc(p, S, log2, &td);
-      for (int ty = 0; ty < S; ty += T)
-        for (int tx = 0; tx < S; tx += T) {
-          for (int yy = 0; yy < T; yy++)
-            for (int xx = 0; xx < T; xx++)
-              resi[yy * T + xx] = (int16_t)((int)cur[(y + ty + yy) * stride + x + tx + xx] - pred[(ty + yy) * 64 + tx + xx]);
-          int32_t temp[1024], lev[1024], abs_sum = 0;
-          hvxo_transform_nxn(&td, &est[log2 - 2], resi, T, temp, lev, NULL, &abs_sum);
-          hvxo_inv_transform_nxn(&td, lev, rec, T);
-          uint32_t sse = 0;
-          for (int k = 0; k < T * T; k++) { int df = resi[k] - rec[k]; sse += (uint32_t)(df * df); }
-          if (ex) {
-            const int ti = (ty / T) * (S / T) + tx / T;
-            uint8_t st[HVX_NUM_CTX];
-            hvx_coeff_bits cb;
-            memcpy(st, ex->states, sizeof(st)); /* every TU counts from the same snapshot */
-            hvxo_coeff_bits(&td, lev, st, ex->eb, &cb);
-            uint32_t zd = 0;
-            for (int k = 0; k < T * T; k++) zd += (uint32_t)(resi[k] * resi[k]);
-            ex->coef_frac[ci][ti] = cb.frac_bits;
-            ex->abs_sum[ci][ti] = abs_sum;
-            ex->sse[ci][ti] = sse;
-            ex->zdist[ci][ti] = zd;
-            for (int yy = 0; yy < T; yy++)
-              for (int xx = 0; xx < T; xx++) {
-                ex->pred[ci * 4096 + (ty + yy) * 64 + tx + xx] = (uint8_t)pred[(ty + yy) * 64 + tx + xx];
-                ex->rres[ci * 4096 + (ty + yy) * 64 + tx + xx] = rec[yy * T + xx];
-              }
-          }
-          r->sse += sse;
-          r->abs_sum += abs_sum;
-          r->n_tu++;
+      ctu_comp_tus(cur + y * stride + x, stride, pred, 64, S, &td, &est[log2 - 2], ex, ci, 0, &r->sse, &r->abs_sum,
+                   &r->n_tu);
+      if (cc) {  /* 4:2:0: the Cb / Cr TUs (half size) after the luma; hvx_cu_result keeps the luma sums */
+        uint32_t cs = 0;
+        int32_t ca = 0;
+        int cn = 0;
+        for (int c = 1; c <= 2; c++) {
+          int16_t cp[32 * 32];
+          hvxo_chroma_block_epel(cc->refs[c - 1][r->ref], cc->stride, x / 2, y / 2, best.mv_x, best.mv_y, S / 2, S / 2,
+                                 cp, 32);
+          hvx_tu_desc tc;
+          hvxo_ctu_tu_desc_chroma(p, c, S, log2 - 1, &tc);
+          ctu_comp_tus(cc->cur[c - 1] + (y / 2) * cc->stride + x / 2, cc->stride, cp, 32, S / 2, &tc, &est[4 + log2 - 3],
+                       ex, ci, c, &cs, &ca, &cn);
         }
+      }
     }
     base += g * g;
   }
@@ -1432,12 +1515,13 @@ static void ctu_analyze_core(const uint8_t *cur, const uint8_t *const *refs, int
 
 void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
                       const hvx_estbits *est, int ctu_x, int ctu_y, hvx_cu_result *out) {
-  ctu_analyze_core(cur, refs, stride, p, est, ctu_x, ctu_y, out, NULL);
+  ctu_analyze_core(cur, refs, stride, NULL, p, est, ctu_x, ctu_y, out, NULL);
 }
 
 /* ---- CU decision: TEncCu::xCompressCU's depth recursion (TEncCu.cpp:349-877) ---- */
 typedef struct {
   const hvx_ctu_params *p;
+  const ctu_chroma *cc;  /* 4:2:0, else NULL */
   const hvx_cu_result *cu;
   const ctu_extra *ex;
   hvx_cu_decision *dec;
@@ -1464,38 +1548,45 @@ static uint32_t split_flag_bits(const decide_ctx *c, int d, int x8, int y8, int 
   return (uint32_t)c->ex->eb[st ^ bin] >> 15;
 }
 
-/* TEncSearch::encodeResAndCalcRdInterCU's residual decisions for the CU's luma TUs (transform depth
- * 1 in a 64x64 CU, else 0): per TU the forced-zero test of xEstimateInterResidualQT
- * (TEncSearch.cpp:4647-4768: cbf=0 with the zero-residual distortion against cbf=1 + the counted
- * coefficients with the coded distortion, each counted alone), the TU tree's rate counted once
- * (:4973-4984), the qt_root_cbf test (:4361-4366), then the distortion of the clipped
- * reconstruction (:4408-4417).  Context models: luma qt_cbf 28 + getCtxQtCbf (TComDataCU.cpp:1503,
- * 1 at transform depth 0), qt_root_cbf 41 (TEncSbac::codeQtRootCbfZero :1097). */
+/* TComRdCost::getDistPart of a chroma block: m_distortionWeight * SSE, truncated (TComRdCost.cpp:443-446) */
+static uint32_t wdist(double w, uint32_t sse) { return (uint32_t)(w * (double)sse); }
+
+/* TEncSearch::encodeResAndCalcRdInterCU's residual decisions for the CU's TUs (transform depth
+ * 1 in a 64x64 CU, else 0), per TU and component (Y, and at 4:2:0 Cb, Cr): the forced-zero test of
+ * xEstimateInterResidualQT (TEncSearch.cpp:4647-4768: cbf=0 with the zero-residual distortion against
+ * cbf=1 + the counted coefficients with the coded distortion, each counted alone; chroma distortions
+ * weighted per TU by getDistPart), the TU tree's rate counted once (:4973-4984), the qt_root_cbf test
+ * (:4361-4366), then the distortion of the clipped reconstruction (:4408-4417, chroma weighted per
+ * component).  Context models: luma qt_cbf 28 + getCtxQtCbf (TComDataCU.cpp:1503, 1 at transform
+ * depth 0), chroma qt_cbf 33 + the transform depth, qt_root_cbf 41 (TEncSbac::codeQtRootCbfZero :1097).
+ * The chroma cbf of the 64x64 root node and split_transform_flag are not counted (no RQT here). */
 static void leaf_eval(const decide_ctx *c, int ci, int S, int x, int y, hvx_cu_decision *o) {
   const ctu_extra *ex = c->ex;
-  const int T = S < 32 ? S : 32, ntu = (S / T) * (S / T);
-  const int m_cbf = 28 + (S > 32 ? 0 : 1);
-  const double lam = c->p->lambda;
-  const uint32_t c0 = (uint32_t)ex->eb[ex->states[m_cbf] ^ 0], c1 = (uint32_t)ex->eb[ex->states[m_cbf] ^ 1];
+  const int T = S < 32 ? S : 32, ntu = (S / T) * (S / T), ncomp = c->cc ? 3 : 1;
+  const double lam = c->p->lambda, w = c->p->chroma_weight;
   uint64_t tree = 0, cf = 0;
   uint32_t nz_dist = 0, zero_dist = 0;
   int cbf = 0;
-  for (int t = 0; t < ntu; t++) {
-    uint64_t tf = c0;
-    uint32_t td = ex->zdist[ci][t];
-    zero_dist += td;
-    cf += ex->coef_frac[ci][t];
-    if (ex->abs_sum[ci][t] > 0) {
-      const uint64_t f1 = c1 + ex->coef_frac[ci][t];
-      if (!(rd_cost(c0 >> 15, td, lam) < rd_cost((uint32_t)(f1 >> 15), ex->sse[ci][t], lam))) {
-        tf = f1;
-        td = ex->sse[ci][t];
-        cbf |= 1 << t;
+  for (int t = 0; t < ntu; t++)
+    for (int comp = 0; comp < ncomp; comp++) {
+      const int m_cbf = comp ? 33 + (S > 32 ? 1 : 0) : 28 + (S > 32 ? 0 : 1);
+      const uint32_t c0 = (uint32_t)ex->eb[ex->states[m_cbf] ^ 0], c1 = (uint32_t)ex->eb[ex->states[m_cbf] ^ 1];
+      uint64_t tf = c0;
+      uint32_t td = comp ? wdist(w, ex->zdist[ci][comp][t]) : ex->zdist[ci][comp][t];
+      zero_dist += td;
+      cf += ex->coef_frac[ci][comp][t];
+      if (ex->abs_sum[ci][comp][t] > 0) {
+        const uint64_t f1 = c1 + ex->coef_frac[ci][comp][t];
+        const uint32_t sd = comp ? wdist(w, ex->sse[ci][comp][t]) : ex->sse[ci][comp][t];
+        if (!(rd_cost(c0 >> 15, td, lam) < rd_cost((uint32_t)(f1 >> 15), sd, lam))) {
+          tf = f1;
+          td = sd;
+          cbf |= 1 << (4 * comp + t);
+        }
       }
+      tree += tf;
+      nz_dist += td;
     }
-    tree += tf;
-    nz_dist += td;
-  }
   const uint32_t r0 = (uint32_t)ex->eb[ex->states[41] ^ 0], r1 = (uint32_t)ex->eb[ex->states[41] ^ 1];
   if (rd_cost(r0 >> 15, zero_dist, lam) < rd_cost((uint32_t)(tree >> 15), nz_dist, lam)) cbf = 0;
   uint32_t dist = 0;
@@ -1506,14 +1597,26 @@ static void leaf_eval(const decide_ctx *c, int ci, int S, int x, int y, hvx_cu_d
       const int df = (int)c->cur[(y + yy) * c->stride + x + xx] - rec;
       dist += (uint32_t)(df * df);
     }
+  for (int comp = 1; comp < ncomp; comp++) {
+    const int Sc = S / 2, Tc = T / 2;
+    uint32_t cd = 0;
+    for (int yy = 0; yy < Sc; yy++)
+      for (int xx = 0; xx < Sc; xx++) {
+        const int t = (yy / Tc) * (Sc / Tc) + xx / Tc, k = EX_CHROMA(ci, comp) + yy * 32 + xx;
+        const int rec = clip_pel(ex->pred[k] + (((cbf >> (4 * comp + t)) & 1) ? ex->rres[k] : 0));
+        const int df = (int)c->cc->cur[comp - 1][(y / 2 + yy) * c->cc->stride + x / 2 + xx] - rec;
+        cd += (uint32_t)(df * df);
+      }
+    dist += wdist(w, cd);
+  }
   o->coef_frac = cf;
   o->cbf = cbf;
   o->bits = ex->me_bits[ci] + (uint32_t)((cbf ? r1 + tree : r0) >> 15);
   o->dist = dist;
   o->ssim_dist = 0.0f;
   if (c->p->rd_metric == HVX_RD_SSIM) {
-    /* D_ssim: distortionSSIM's 1 - compute_SSIM (stvssim.c:567-575) per 8x8 block of the CU (one
-     * 8x8 window each), summed in raster block order as float */
+    /* D_ssim: distortionSSIM's 1 - compute_SSIM (stvssim.c:567-575) per 8x8 block of the CU's luma
+     * (one 8x8 window each), summed in raster block order as float */
     float dsum = 0.0f;
     for (int by = 0; by < S / 8; by++)
       for (int bx = 0; bx < S / 8; bx++) {
@@ -1581,18 +1684,19 @@ static int decide_node(decide_ctx *c, int d, int j, uint32_t *bits, uint32_t *di
   return 1;
 }
 
-void hvxo_ctu_decide(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
-                     const hvx_estbits *est, const uint8_t *states, const int32_t *eb, int ctu_x, int ctu_y,
-                     hvx_cu_result *out_cu, hvx_cu_decision *out_dec, uint8_t *recon, int recon_stride) {
+static void ctu_decide_core(const uint8_t *cur, const uint8_t *const *refs, int stride, const ctu_chroma *cc,
+                            const hvx_ctu_params *p, const hvx_estbits *est, const uint8_t *states, const int32_t *eb,
+                            int ctu_x, int ctu_y, hvx_cu_result *out_cu, hvx_cu_decision *out_dec, uint8_t *recon,
+                            int recon_stride, uint8_t *const *recon_c, int recon_c_stride) {
   ctu_extra *ex = (ctu_extra *)calloc(1, sizeof(ctu_extra));
   ex->states = states;
   ex->eb = eb;
-  ex->pred = (uint8_t *)calloc(HVX_CUS_PER_CTU, 4096);
-  ex->rres = (int16_t *)calloc(HVX_CUS_PER_CTU * 4096, sizeof(int16_t));
-  ctu_analyze_core(cur, refs, stride, p, est, ctu_x, ctu_y, out_cu, ex);
+  ex->pred = (uint8_t *)calloc(HVX_CUS_PER_CTU * 6144, 1);
+  ex->rres = (int16_t *)calloc(HVX_CUS_PER_CTU * 6144, sizeof(int16_t));
+  ctu_analyze_core(cur, refs, stride, cc, p, est, ctu_x, ctu_y, out_cu, ex);
   decide_ctx c;
   memset(&c, 0, sizeof(c));
-  c.p = p; c.cu = out_cu; c.ex = ex; c.dec = out_dec; c.ctu_x = ctu_x; c.ctu_y = ctu_y;
+  c.p = p; c.cc = cc; c.cu = out_cu; c.ex = ex; c.dec = out_dec; c.ctu_x = ctu_x; c.ctu_y = ctu_y;
   c.cur = cur; c.stride = stride;
   memset(out_dec, 0, sizeof(hvx_cu_decision) * HVX_CUS_PER_CTU);
   uint32_t b, d;
@@ -1627,11 +1731,40 @@ void hvxo_ctu_decide(const uint8_t *cur, const uint8_t *const *refs, int stride,
           const int t = (yy / T) * (S / T) + xx / T, k = ci * 4096 + yy * 64 + xx;
           recon[(y + yy) * recon_stride + x + xx] = (uint8_t)clip_pel(ex->pred[k] + (((cbf >> t) & 1) ? ex->rres[k] : 0));
         }
+      for (int comp = 1; cc && comp <= 2; comp++) {
+        const int Sc = S / 2, Tc = T / 2;
+        for (int yy = 0; yy < Sc; yy++)
+          for (int xx = 0; xx < Sc; xx++) {
+            const int t = (yy / Tc) * (Sc / Tc) + xx / Tc, k = EX_CHROMA(ci, comp) + yy * 32 + xx;
+            recon_c[comp - 1][(y / 2 + yy) * recon_c_stride + x / 2 + xx] =
+                (uint8_t)clip_pel(ex->pred[k] + (((cbf >> (4 * comp + t)) & 1) ? ex->rres[k] : 0));
+          }
+      }
     }
   }
   free(ex->pred);
   free(ex->rres);
   free(ex);
+}
+
+void hvxo_ctu_decide(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
+                     const hvx_estbits *est, const uint8_t *states, const int32_t *eb, int ctu_x, int ctu_y,
+                     hvx_cu_result *out_cu, hvx_cu_decision *out_dec, uint8_t *recon, int recon_stride) {
+  ctu_decide_core(cur, refs, stride, NULL, p, est, states, eb, ctu_x, ctu_y, out_cu, out_dec, recon, recon_stride, NULL,
+                  0);
+}
+
+void hvxo_ctu_decide_yuv(const uint8_t *const *cur3, const uint8_t *const *refs, const uint8_t *const *refs_cb,
+                         const uint8_t *const *refs_cr, int stride, int c_stride, const hvx_ctu_params *p,
+                         const hvx_estbits *est, const uint8_t *states, const int32_t *eb, int ctu_x, int ctu_y,
+                         hvx_cu_result *out_cu, hvx_cu_decision *out_dec, uint8_t *const *recon3, int recon_stride,
+                         int recon_c_stride) {
+  ctu_chroma cc;
+  cc.cur[0] = cur3[1]; cc.cur[1] = cur3[2];
+  cc.refs[0] = refs_cb; cc.refs[1] = refs_cr;
+  cc.stride = c_stride;
+  ctu_decide_core(cur3[0], refs, stride, &cc, p, est, states, eb, ctu_x, ctu_y, out_cu, out_dec, recon3[0], recon_stride,
+                  recon3 + 1, recon_c_stride);
 }
 
 

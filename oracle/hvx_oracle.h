@@ -85,6 +85,17 @@ void hvxo_ctu_tu_desc(const hvx_ctu_params *p, int cu_size, int log2, hvx_tu_des
 void hvxo_ctu_decide(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
                      const hvx_estbits *est, const uint8_t *states, const int32_t *eb, int ctu_x, int ctu_y,
                      hvx_cu_result *out_cu, hvx_cu_decision *out_dec, uint8_t *recon, int recon_stride);
+/* 4:2:0 form (hvx_ctu_encode_yuv semantics): cur3 / recon3 = Y, Cb, Cr sample-(0,0) pointers, the chroma
+ * planes with stride c_stride / recon_c_stride; est[7] = luma 4x4..32x32, chroma 4x4..16x16; the leaves'
+ * Y, Cb and Cr go into recon3 */
+void hvxo_ctu_decide_yuv(const uint8_t *const *cur3, const uint8_t *const *refs, const uint8_t *const *refs_cb,
+                         const uint8_t *const *refs_cr, int stride, int c_stride, const hvx_ctu_params *p,
+                         const hvx_estbits *est, const uint8_t *states, const int32_t *eb, int ctu_x, int ctu_y,
+                         hvx_cu_result *out_cu, hvx_cu_decision *out_dec, uint8_t *const *recon3, int recon_stride,
+                         int recon_c_stride);
+void hvxo_chroma_block_epel(const uint8_t *ref, int stride, int x, int y, int mvx, int mvy, int w, int h, int16_t *out,
+                            int os);
+void hvxo_ctu_tu_desc_chroma(const hvx_ctu_params *p, int comp, int cu_size, int log2, hvx_tu_desc *d);
 void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
                       const hvx_estbits *est /* [4]: luma 4x4..32x32 */, int ctu_x, int ctu_y,
                       hvx_cu_result *out /* [HVX_CUS_PER_CTU] */);

@@ -80,18 +80,23 @@ def test_segment_and_aggregate_contract():
     flat = [f for s in segs for f in s]
     assert len(flat) == len(set(flat)) == 40  # 8 closed, disjoint segments of nref+1 frames
     assert bench.aggregate(2040, 10, 8, 2.0) == 2040 * 10 * 8 / 2.0
-    assert bench.b_ctu_luma(4) == 4096 * 6 + 2 * 4096 + 16 * 256
+    assert bench.b_ctu(4) == 6144 * 6 + 2 * 6144 + 16 * 256 == 53248  # SURVEY 8(d), LDP 4 refs
 
 
-def _decide_picture(planes, rec):
-    """The oracle's full step (analysis + CU decision + reconstruction) into rec (padded plane)."""
+def _decide_picture(planes, rec_flat):
+    """The oracle's full 4:2:0 step (analysis + CU decision + reconstruction) into rec_flat (one
+    Y | Cb | Cr picture buffer, the layout the bench step gathers)."""
     import oracle
-    from video_codecs_amd import _abi
-    params = _abi.ctu_params(W, H, NREF, QP)
-    est, st, eb = _abi.load_estbits_p_luma(), _abi.load_ctx_p_states(), _abi.load_entropy_bits()
+    from video_codecs_amd import _abi, hvx
+    params = _abi.ctu_params(W, H, NREF, QP, chroma=True)
+    est7 = _abi.estbits_p_yuv(oracle.estbits_update)
+    st, eb = _abi.load_ctx_p_states(), _abi.load_entropy_bits()
+    rec = hvx.yuv_views(rec_flat, W, H)
+    refs = planes[:NREF]
+    refs3 = ([r[0] for r in refs], [r[1] for r in refs], [r[2] for r in refs])
     ncx, ncy = (W + 63) // 64, (H + 63) // 64
     for c in range(ncx * ncy):
-        oracle.ctu_decide(planes[NREF], planes[:NREF], params, est, st, eb, c % ncx, c // ncx, rec)
+        oracle.ctu_decide_yuv(planes[NREF], refs3, params, est7, st, eb, c % ncx, c // ncx, rec)
 
 
 def _dpb_worker(rank, world, port, outdir):
@@ -100,8 +105,9 @@ def _dpb_worker(rank, world, port, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
     from video_codecs_amd.dpb import DpbGather
-    planes = [bench.luma_plane(W, H, f) for f in bench.segment_frames(rank, NREF)]
-    g = DpbGather(world, rank, planes[0].shape, "cpu")
+    from video_codecs_amd import hvx
+    planes = [bench.yuv_planes(W, H, f) for f in bench.segment_frames(rank, NREF)]
+    g = DpbGather(world, rank, (hvx.yuv_bytes(W, H),), "cpu")
 
     def step():  # the bench step's shape: decide into the DPB buffer, then the async gather
         _decide_picture(planes, g.buffer().numpy())
@@ -119,8 +125,9 @@ def _dpb_worker(rank, world, port, outdir):
 
 def test_two_rank_dpb_gather_gloo(tmp_path):
     # the per-picture DPB gather: after STEPS + WARMUP pictures through two
-    # alternating buffers, rank 0 holds each rank's latest reconstruction, and that
-    # reconstruction is exactly the single-process one of the rank's own segment
+    # alternating buffers, rank 0 holds each rank's latest 4:2:0 reconstruction (one Y | Cb | Cr
+    # buffer per picture), and that reconstruction is exactly the single-process one of the rank's
+    # own segment
     import torch.multiprocessing as tmp
     world = 2
     tmp.spawn(_dpb_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
@@ -131,7 +138,7 @@ def test_two_rank_dpb_gather_gloo(tmp_path):
         own = np.load(tmp_path / f"own{r}.npy")
         np.testing.assert_array_equal(dpb[r], own)
         exp = np.zeros_like(own)
-        _decide_picture([bench.luma_plane(W, H, f) for f in bench.segment_frames(r, NREF)], exp)
+        _decide_picture([bench.yuv_planes(W, H, f) for f in bench.segment_frames(r, NREF)], exp)
         np.testing.assert_array_equal(own, exp)
         assert int(np.load(tmp_path / f"t{r}.npy")[1]) == STEPS + WARMUP
     assert not np.array_equal(dpb[0], dpb[1])

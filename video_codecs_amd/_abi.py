@@ -33,8 +33,12 @@ ME_FEN, ME_HADME, ME_SMOOTHMV, ME_BI = 1, 2, 4, 8
 
 CTU_PARAMS = np.dtype([("pic_w", "<i4"), ("pic_h", "<i4"), ("n_ref", "<i4"), ("qp", "<i4"), ("search_range", "<i4"),
                        ("me_flags", "<i4"), ("slice_type", "<i4"), ("lambda_motion", "<u4"), ("lambda", "<f8"),
-                       ("lambda_ssim", "<f8"), ("rd_metric", "<i4"), ("pad_", "<i4")], align=True)
-assert CTU_PARAMS.itemsize == 56
+                       ("lambda_ssim", "<f8"), ("rd_metric", "<i4"), ("chroma_format", "<i4"), ("qp_chroma", "<i4"),
+                       ("pad_", "<i4"), ("lambda_chroma", "<f8"), ("chroma_weight", "<f8")], align=True)
+assert CTU_PARAMS.itemsize == 80
+# g_aucChromaScale[CHROMA_420] (TComRom.cpp:536)
+CHROMA_SCALE_420 = tuple(range(30)) + (29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37) + tuple(range(38, 52))
+assert len(CHROMA_SCALE_420) == 58
 RD_SSE, RD_SSIM = 0, 1
 CU_RESULT = np.dtype([("valid", "<i4"), ("ref", "<i4"), ("mv_x", "<i4"), ("mv_y", "<i4"), ("me_cost", "<u4"),
                       ("sse", "<u4"), ("abs_sum", "<i4"), ("n_tu", "<i4")])
@@ -49,6 +53,22 @@ def load_estbits_p_luma():
     return np.fromfile(p, dtype="<i4").reshape(4, ESTBITS_INTS)
 
 
+def estbits_p_yuv(update):
+    """7 x 224 int32: the 4 luma tables (load_estbits_p_luma) + chroma TU 4x4, 8x8, 16x16 tables, each
+    TEncSbac::estBit (TEncSbac.cpp:1726) of the same context snapshot (ctx_p_states.bin) at chroma
+    channel type on top of the luma table of its size (every entry the chroma RDOQ reads is written by
+    that call).  update = an estbits_update(states, entropy_bits, rice, w, h, ch, est_in) callable:
+    the library's host restatement or the oracle's."""
+    luma = load_estbits_p_luma()
+    st, eb = load_ctx_p_states(), load_entropy_bits()
+    out = [t.copy() for t in luma]
+    for log2 in (2, 3, 4):
+        base = luma[log2 - 2]
+        rice = base[-4:].astype(np.uint32)
+        out.append(np.asarray(update(st, eb, rice, 1 << log2, 1 << log2, 1, base), np.int32).reshape(-1))
+    return np.stack(out)
+
+
 def lambda_ssim(qp, eta=1.0):
     """The SSIM-RDO lambda of stvssim.c: lambda_2 (:1782-1806, active form :1805)
     -a1*b2*exp(b1*(qp-15)), times the attention weight eta^0.85 (adjust_lambda :1707)."""
@@ -58,9 +78,18 @@ def lambda_ssim(qp, eta=1.0):
     return lam * math.pow(eta, 0.85) if eta != 1.0 else lam
 
 
-def ctu_params(pic_w, pic_h, n_ref, qp, lam=None, search_range=64, slice_type=1, rd_metric=0, lam_ssim=None):
+def chroma_qp(qp, offset=0):
+    """QpParam's chroma QP at 4:2:0 (getScaledChromaQP, TComChromaFormat.h; TEncSlice::setUpLambda)."""
+    q = qp + offset
+    return qp if q < 0 else CHROMA_SCALE_420[min(q, 57)]
+
+
+def ctu_params(pic_w, pic_h, n_ref, qp, lam=None, search_range=64, slice_type=1, rd_metric=0, lam_ssim=None,
+               chroma=False):
     """HM-style P-slice parameters; lambda defaults to 0.57*2^((qp-12)/3) (TEncSlice::initEncSlice form).
-    rd_metric RD_SSIM selects the SSIM CU decision with lambda_ssim(qp) unless lam_ssim is given."""
+    rd_metric RD_SSIM selects the SSIM CU decision with lambda_ssim(qp) unless lam_ssim is given.
+    chroma: 4:2:0 (hvx_ctu_encode_yuv) with TEncSlice::setUpLambda's chroma weight and RDOQ lambda."""
+    import math
     p = np.zeros(1, CTU_PARAMS)
     p["rd_metric"] = rd_metric
     p["lambda_ssim"] = lambda_ssim(qp) if lam_ssim is None else lam_ssim
@@ -68,6 +97,9 @@ def ctu_params(pic_w, pic_h, n_ref, qp, lam=None, search_range=64, slice_type=1,
     p["pic_w"], p["pic_h"], p["n_ref"], p["qp"] = pic_w, pic_h, n_ref, qp
     p["search_range"], p["me_flags"], p["slice_type"] = search_range, ME_FEN | ME_HADME | ME_SMOOTHMV, slice_type
     p["lambda_motion"], p["lambda"] = lambda_motion_sad(lam), lam
+    qpc = chroma_qp(qp)
+    w = math.pow(2.0, (qp - qpc) / 3.0)  # TEncSlice.cpp:159
+    p["chroma_format"], p["qp_chroma"], p["chroma_weight"], p["lambda_chroma"] = int(chroma), qpc, w, lam / w
     return p
 
 # picture layout: 8-bit padded planes, HM TComPicYuv geometry (margin = MaxCU + 16 = 80)

@@ -12,9 +12,18 @@
 
 struct CtuLayout {
   int nctu_x, nctu_y, nctu, nref;
-  // TU classes, contiguous: [0,8n) 32x32 | [8n,24n) 16x16 | [24n,88n) 8x8
-  __host__ __device__ int ntu() const { return 88 * nctu; }
-  __host__ __device__ int64_t nres() const { return (int64_t)16384 * nctu; }
+  // TU classes, contiguous: luma [0,8n) 32x32 | [8n,24n) 16x16 | [24n,88n) 8x8, then (4:2:0) chroma
+  // [88n,104n) 16x16 (the 64x64 and 32x32 CUs) | [104n,136n) 8x8 | [136n,264n) 4x4
+  __host__ __device__ int ntu() const { return 264 * nctu; }
+  __host__ __device__ int64_t nres() const { return (int64_t)24576 * nctu; }
+};
+
+// the chroma planes of a 4:2:0 pass (hvx_chroma_planes on the device side); on == 0: luma only
+struct CtuChroma {
+  const uint8_t *cur[2];
+  const uint8_t *const *refs;  // 2 * nref origins: Cb of each reference, then Cr
+  uint8_t *recon[2];
+  int stride, on;
 };
 
 __device__ __forceinline__ void cu_geom(int ci, int &d, int &j, int &S, int &g) {
@@ -28,19 +37,60 @@ __device__ __forceinline__ void cu_geom(int ci, int &d, int &j, int &S, int &g) 
 
 __device__ __forceinline__ int depth_base(int d) { return d == 0 ? 0 : d == 1 ? 1 : d == 2 ? 5 : 21; }
 
-// TU index and residual offset of TU t of CU (ctu, d, j)
-__device__ __forceinline__ int ctu_tu_index(const CtuLayout &L, int ctu, int d, int j, int t) {
+// TU index and residual offset of TU t of component c (0 Y, 1 Cb, 2 Cr) of CU (ctu, d, j)
+__device__ __forceinline__ int ctu_tu_index(const CtuLayout &L, int ctu, int d, int j, int t, int c = 0) {
   const int n = L.nctu;
-  if (d == 0) return ctu * 8 + t;
-  if (d == 1) return ctu * 8 + 4 + j;
-  if (d == 2) return 8 * n + ctu * 16 + j;
-  return 24 * n + ctu * 64 + j;
+  if (c == 0) {
+    if (d == 0) return ctu * 8 + t;
+    if (d == 1) return ctu * 8 + 4 + j;
+    if (d == 2) return 8 * n + ctu * 16 + j;
+    return 24 * n + ctu * 64 + j;
+  }
+  if (d == 0) return 88 * n + ctu * 16 + (c - 1) * 4 + t;
+  if (d == 1) return 88 * n + ctu * 16 + 8 + (c - 1) * 4 + j;
+  if (d == 2) return 104 * n + ctu * 32 + (c - 1) * 16 + j;
+  return 136 * n + ctu * 128 + (c - 1) * 64 + j;
 }
 __device__ __forceinline__ int64_t ctu_tu_offset(const CtuLayout &L, int tu) {
   const int64_t n = L.nctu;
   if (tu < 8 * n) return (int64_t)tu * 1024;
   if (tu < 24 * n) return 8 * n * 1024 + (int64_t)(tu - 8 * n) * 256;
-  return 8 * n * 1024 + 16 * n * 256 + (int64_t)(tu - 24 * n) * 64;
+  if (tu < 88 * n) return 8 * n * 1024 + 16 * n * 256 + (int64_t)(tu - 24 * n) * 64;
+  const int64_t c0 = 16384 * n;
+  if (tu < 104 * n) return c0 + (int64_t)(tu - 88 * n) * 256;
+  if (tu < 136 * n) return c0 + 4096 * n + (int64_t)(tu - 104 * n) * 64;
+  return c0 + 6144 * n + (int64_t)(tu - 136 * n) * 16;
+}
+
+// xPredInterBlk for one 4:2:0 chroma sample, uni-prediction (hvxo_chroma_block_epel): the luma
+// quarter-pel MV in 1/8 chroma samples, 4-tap filters, first (+ last) stage(s) of
+// TComInterpolationFilter (8-bit: the single stage rounds by 32 >> 6, the two-stage path keeps
+// the -8192-offset int16 intermediate, TComInterpolationFilter.cpp:94-257)
+__device__ __forceinline__ int ctu_epel_sample(const uint8_t *ref, int sr, int x, int y, int mvx, int mvy) {
+  const int fx = mvx & 7, fy = mvy & 7;
+  const uint8_t *p = ref + (y + (mvy >> 3)) * sr + x + (mvx >> 3);
+  if (!fx && !fy) return p[0];
+  if (!fy) {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) s += kChromaFilter[fx][k] * p[k - 1];
+    return clip_pel((s + 32) >> 6);
+  }
+  if (!fx) {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) s += kChromaFilter[fy][k] * p[(k - 1) * sr];
+    return clip_pel((s + 32) >> 6);
+  }
+  int s2 = 0;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) s += kChromaFilter[fx][k] * p[(t - 1) * sr + k - 1];
+    s2 += kChromaFilter[fy][t] * (int16_t)(s - 8192);
+  }
+  return clip_pel((s2 + (1 << 11) + (8192 << 6)) >> 12);
 }
 
 __global__ void k_set_ptr(const uint8_t **slot, const uint8_t *p) { *slot = p; }
@@ -85,7 +135,7 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
                                                        const hvx_me_result *__restrict__ res, int16_t *__restrict__ resid,
                                                        hvx_tu_desc *__restrict__ descs, int64_t *__restrict__ offs,
                                                        int32_t *__restrict__ est_idx, hvx_cu_result *__restrict__ out,
-                                                       int first, int ncu) {
+                                                       int first, int ncu, CtuChroma C) {
   // blocks cover CUs [first, first + ncu) of every CTU (one depth range per launch)
   const int ctu = blockIdx.x / ncu, ci = first + (int)(blockIdx.x % ncu);
   const int cuid = ctu * HVX_CUS_PER_CTU + ci;
@@ -123,6 +173,21 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
     descs[tu] = td;
     offs[tu] = ctu_tu_offset(L, tu);
     est_idx[tu] = log2 - 2;
+    if (C.on) {  // the Cb / Cr TUs: half size, chroma QP and RDOQ lambda, chroma cbf context = transform depth
+      for (int c = 1; c <= 2; c++) {
+        const int tc = ctu_tu_index(L, ctu, d, j, t, c);
+        hvx_tu_desc dc = td;
+        dc.comp = c;
+        dc.width = dc.height = valid ? T / 2 : 0;
+        dc.log2_size = log2 - 1;
+        dc.ctx_qt_cbf = S > 32 ? 1 : 0;
+        dc.qp_per = P.qp_chroma / 6; dc.qp_rem = P.qp_chroma % 6;
+        dc.lambda = P.lambda_chroma;
+        descs[tc] = dc;
+        offs[tc] = ctu_tu_offset(L, tc);
+        est_idx[tc] = 4 + log2 - 3;
+      }
+    }
   }
   if (!valid) return;
   const uint8_t *rp = refs[best];
@@ -133,6 +198,17 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
     const int t = (yy / T) * (S / T) + (xx / T);
     const int tu = ctu_tu_index(L, ctu, d, j, t);
     resid[ctu_tu_offset(L, tu) + (yy % T) * T + (xx % T)] = (int16_t)((int)cur[(y + yy) * stride + x + xx] - pred);
+  }
+  if (C.on) {
+    const int Sc = S / 2, Tc = T / 2, xc = x / 2, yc = y / 2;
+    for (int k = lane_id(); k < 2 * Sc * Sc; k += HVX_WAVE) {
+      const int c = k < Sc * Sc ? 1 : 2, kk = k - (c - 1) * Sc * Sc, yy = kk / Sc, xx = kk % Sc;
+      const int pred = ctu_epel_sample(C.refs[(c - 1) * L.nref + best] + yc * C.stride + xc, C.stride, xx, yy, mvx, mvy);
+      const int t = (yy / Tc) * (Sc / Tc) + (xx / Tc);
+      const int tu = ctu_tu_index(L, ctu, d, j, t, c);
+      resid[ctu_tu_offset(L, tu) + (yy % Tc) * Tc + (xx % Tc)] =
+          (int16_t)((int)C.cur[c - 1][(yc + yy) * C.stride + xc + xx] - pred);
+    }
   }
 }
 
@@ -178,7 +254,12 @@ struct DecideArgs {
   hvx_cu_decision *dec;
   int metric;                 // HVX_RD_SSE / HVX_RD_SSIM
   double lambda_ssim;
+  CtuChroma C;                // 4:2:0 planes (C.on), else luma only
+  double cw;                  // TComRdCost::m_distortionWeight of Cb / Cr
 };
+
+// TComRdCost::getDistPart of a chroma block: weight * SSE, truncated (TComRdCost.cpp:443-446)
+__device__ __forceinline__ uint32_t dec_wdist(double w, uint32_t sse) { return (uint32_t)__dmul_rn(w, (double)sse); }
 
 // the CU-level RD cost (hvxo's cu_cost): calcRdCost, or D_ssim + lambda_ssim * R
 __device__ __forceinline__ double dec_cu_cost(const DecideArgs &A, uint32_t bits, uint32_t dist, float sdist) {
@@ -268,36 +349,41 @@ __global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const uint8_t *__
   int d, j, S, g;
   cu_geom(ci, d, j, S, g);
   const int x = (ctu % A.L.nctu_x) * 64 + (j % g) * S, y = (ctu / A.L.nctu_x) * 64 + (j / g) * S;
-  const int T = S < 32 ? S : 32, ntu = (S / T) * (S / T), lane = lane_id();
-  const int m_cbf = 28 + (S > 32 ? 0 : 1);
+  const int T = S < 32 ? S : 32, ntu = (S / T) * (S / T), lane = lane_id(), ncomp = A.C.on ? 3 : 1;
   const double lam = A.lambda;
-  const uint32_t c0 = (uint32_t)A.eb[A.st[m_cbf] ^ 0], c1 = (uint32_t)A.eb[A.st[m_cbf] ^ 1];
   uint64_t tree = 0, cf = 0;
   uint32_t nz_dist = 0, zero_dist = 0;
   int cbf = 0;
   for (int t = 0; t < ntu; t++) {
-    const int tu = ctu_tu_index(A.L, ctu, d, j, t);
-    const int64_t o = ctu_tu_offset(A.L, tu);
-    uint32_t part = 0;
-    for (int k = lane; k < T * T; k += HVX_WAVE) {
-      const int r = resid[o + k];
-      part += (uint32_t)(r * r);
-    }
-    uint32_t td = wave_sum_u32(part);
-    const uint64_t fr = A.cb[tu].frac_bits;
-    uint64_t tf = c0;
-    zero_dist += td;
-    cf += fr;
-    if (abs_sum[tu] > 0) {
-      const uint64_t f1 = c1 + fr;
-      if (!(dec_rd_cost(c0 >> 15, td, lam) < dec_rd_cost((uint32_t)(f1 >> 15), sse[tu], lam))) {
-        tf = f1;
-        td = sse[tu];
-        cbf |= 1 << t;
+    for (int comp = 0; comp < ncomp; comp++) {  // per TU Y, Cb, Cr (xEstimateInterResidualQT's component loop)
+      const int Tq = comp ? T / 2 : T;
+      const int m_cbf = comp ? 33 + (S > 32 ? 1 : 0) : 28 + (S > 32 ? 0 : 1);
+      const uint32_t c0 = (uint32_t)A.eb[A.st[m_cbf] ^ 0], c1 = (uint32_t)A.eb[A.st[m_cbf] ^ 1];
+      const int tu = ctu_tu_index(A.L, ctu, d, j, t, comp);
+      const int64_t o = ctu_tu_offset(A.L, tu);
+      uint32_t part = 0;
+      for (int k = lane; k < Tq * Tq; k += HVX_WAVE) {
+        const int r = resid[o + k];
+        part += (uint32_t)(r * r);
       }
+      const uint32_t zd = wave_sum_u32(part);
+      uint32_t td = comp ? dec_wdist(A.cw, zd) : zd;
+      const uint64_t fr = A.cb[tu].frac_bits;
+      uint64_t tf = c0;
+      zero_dist += td;
+      cf += fr;
+      if (abs_sum[tu] > 0) {
+        const uint64_t f1 = c1 + fr;
+        const uint32_t sd = comp ? dec_wdist(A.cw, sse[tu]) : sse[tu];
+        if (!(dec_rd_cost(c0 >> 15, td, lam) < dec_rd_cost((uint32_t)(f1 >> 15), sd, lam))) {
+          tf = f1;
+          td = sd;
+          cbf |= 1 << (4 * comp + t);
+        }
+      }
+      tree += tf;
+      nz_dist += td;
     }
-    tree += tf;
-    nz_dist += td;
   }
   const uint32_t r0 = (uint32_t)A.eb[A.st[41] ^ 0], r1 = (uint32_t)A.eb[A.st[41] ^ 1];
   if (dec_rd_cost(r0 >> 15, zero_dist, lam) < dec_rd_cost((uint32_t)(tree >> 15), nz_dist, lam)) cbf = 0;
@@ -310,7 +396,20 @@ __global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const uint8_t *__
     v = v < 0 ? 0 : v > 255 ? 255 : v;
     part += (uint32_t)((org - v) * (org - v));
   }
-  const uint32_t dist = wave_sum_u32(part);
+  uint32_t dist = wave_sum_u32(part);
+  for (int comp = 1; comp < ncomp; comp++) {  // chroma: getDistPart per component over the CU, weighted
+    const int Sc = S / 2, Tc = T / 2;
+    uint32_t cpart = 0;
+    for (int k = lane; k < Sc * Sc; k += HVX_WAVE) {
+      const int yy = k / Sc, xx = k % Sc, t = (yy / Tc) * (Sc / Tc) + xx / Tc;
+      const int64_t o = ctu_tu_offset(A.L, ctu_tu_index(A.L, ctu, d, j, t, comp)) + (yy % Tc) * Tc + (xx % Tc);
+      const int org = A.C.cur[comp - 1][(y / 2 + yy) * A.C.stride + x / 2 + xx];
+      int v = org - resid[o] + (((cbf >> (4 * comp + t)) & 1) ? res_out[o] : 0);
+      v = v < 0 ? 0 : v > 255 ? 255 : v;
+      cpart += (uint32_t)((org - v) * (org - v));
+    }
+    dist += dec_wdist(A.cw, wave_sum_u32(cpart));
+  }
   // HVX_RD_SSIM: D_ssim = sum over the CU's 8x8 blocks (raster order) of 1 - SSIM(org, rec), one
   // block per lane with compute_SSIM's float operations in its order (stvssim.c:506-545)
   __shared__ float sdist[64];
@@ -391,7 +490,7 @@ __global__ __launch_bounds__(64) void k_ctu_decide(DecideArgs A) {
 __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int pic_h, const uint8_t *__restrict__ cur,
                                                    int stride, const hvx_cu_decision *__restrict__ dec,
                                                    const int16_t *__restrict__ resid, const int16_t *__restrict__ res_out,
-                                                   uint8_t *__restrict__ recon) {
+                                                   uint8_t *__restrict__ recon, CtuChroma C) {
   const int ctu = blockIdx.x;
   const int x0 = (ctu % L.nctu_x) * 64, y0 = (ctu / L.nctu_x) * 64;
   const hvx_cu_decision *dc = dec + (size_t)ctu * HVX_CUS_PER_CTU;
@@ -410,6 +509,24 @@ __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int p
     const int64_t o = ctu_tu_offset(L, tu) + (cy % T) * T + (cx % T);
     const int v = (int)cur[y * stride + x] - resid[o] + (((dc[depth_base(d) + j].cbf >> t) & 1) ? res_out[o] : 0);
     recon[y * stride + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+  }
+  if (!C.on) return;
+  for (int k = threadIdx.x; k < 2 * 32 * 32; k += 256) {  // Cb then Cr, 32x32 chroma samples per CTU
+    const int c = 1 + (k >> 10), yy = (k >> 5) & 31, xx = k & 31, x = x0 / 2 + xx, y = y0 / 2 + yy;
+    if (2 * x >= pic_w || 2 * y >= pic_h) continue;
+    int d = 0, j = 0;
+    for (d = 0; d < 4; d++) {
+      const int S = 64 >> d, g = 1 << d;
+      j = (2 * yy / S) * g + (2 * xx / S);
+      if (dc[depth_base(d) + j].leaf) break;
+    }
+    if (d == 4) continue;
+    const int Sc = 32 >> d, Tc = (Sc < 16 ? Sc : 16), cx = xx % Sc, cy = yy % Sc, t = (cy / Tc) * (Sc / Tc) + (cx / Tc);
+    const int tu = ctu_tu_index(L, ctu, d, j, t, c);
+    const int64_t o = ctu_tu_offset(L, tu) + (cy % Tc) * Tc + (cx % Tc);
+    const int v = (int)C.cur[c - 1][y * C.stride + x] - resid[o] +
+                  (((dc[depth_base(d) + j].cbf >> (4 * c + t)) & 1) ? res_out[o] : 0);
+    C.recon[c - 1][y * C.stride + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
   }
 }
 

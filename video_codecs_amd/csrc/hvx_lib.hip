@@ -28,13 +28,13 @@ struct hvx_ctx {
   hipStream_t stream = nullptr;
   // hvx_ctu_analyze / hvx_ctu_encode run their independent branches on three more streams (fork/join events)
   hipStream_t aux[3] = {};
-  hipEvent_t fj[7] = {};
+  hipEvent_t fj[8] = {};
   // HVX_SERIAL_STREAMS=1: every branch on ctx->stream (profiling: isolated per-kernel times)
   bool serial = false;
   // optional per-phase timing of hvx_ctu_analyze: a begin/end event pair on the launch's own
   // stream around every timed launch, folded into phase_ms[phase] (phases may overlap)
   int timing = 0;
-  static constexpr int kMaxTimed = 32;
+  static constexpr int kMaxTimed = 48;
   hipEvent_t tev[2 * kMaxTimed] = {};
   int tphase[kMaxTimed] = {};
   int ntev = 0;
@@ -67,7 +67,11 @@ constexpr int kCtuG = 64;
 size_t pad_g(size_t n) { return (n + kCtuG - 1) / kCtuG * kCtuG; }
 size_t ctu_il_off16(int n) { return pad_g((size_t)8 * n) * 1024; }
 size_t ctu_il_off8(int n) { return ctu_il_off16(n) + pad_g((size_t)16 * n) * 256; }
-size_t ctu_il_words(int n) { return ctu_il_off8(n) + pad_g((size_t)64 * n) * 64; }
+// 4:2:0 chroma classes: 16x16 (16n TUs), 8x8 (32n), 4x4 (128n)
+size_t ctu_il_offc16(int n) { return ctu_il_off8(n) + pad_g((size_t)64 * n) * 64; }
+size_t ctu_il_offc8(int n) { return ctu_il_offc16(n) + pad_g((size_t)16 * n) * 256; }
+size_t ctu_il_offc4(int n) { return ctu_il_offc8(n) + pad_g((size_t)32 * n) * 64; }
+size_t ctu_il_words(int n) { return ctu_il_offc4(n) + pad_g((size_t)128 * n) * 16; }
 struct CtuWs {
   size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, coefI, cxI, levI, stI, flags, cbits, bsv, bsh,
       qpm, total;
@@ -306,7 +310,7 @@ int hvx_create(int device, hvx_ctx **out) {
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
   for (int i = 0; i < 3 && e == hipSuccess; i++) e = hipStreamCreateWithPriority(&c->aux[i], hipStreamNonBlocking, prio_hi);
-  for (int i = 0; i < 7 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&c->fj[i], hipEventDisableTiming);
+  for (int i = 0; i < 8 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&c->fj[i], hipEventDisableTiming);
   if (e != hipSuccess) { hvx_destroy(c); return hip_fail(e, "hvx_create: streams/events"); }
   *out = c;
   return HVX_OK;
@@ -320,7 +324,7 @@ int hvx_destroy(hvx_ctx *ctx) {
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   for (int i = 0; i < 3; i++)
     if (ctx->aux[i]) (void)hipStreamDestroy(ctx->aux[i]);
-  for (int i = 0; i < 7; i++)
+  for (int i = 0; i < 8; i++)
     if (ctx->fj[i]) (void)hipEventDestroy(ctx->fj[i]);
   if (ctx->ev_ok)
     for (int i = 0; i < 2 * hvx_ctx::kMaxTimed; i++) (void)hipEventDestroy(ctx->tev[i]);
@@ -669,15 +673,36 @@ int hvx_ctu_workspace_size(int pic_w, int pic_h, int n_ref, size_t *bytes) {
 
 // cnt_states != NULL (hvx_ctu_encode): each TU size class's coefficient rate is counted on the
 // class's own stream right behind its TU pipeline, so it overlaps the remaining searches
+// the device-side view of hvx_chroma_planes (C.on = 0 without one)
+static CtuChroma ctu_chroma(const hvx_chroma_planes *cp) {
+  CtuChroma C;
+  memset(&C, 0, sizeof(C));
+  if (cp) {
+    C.cur[0] = cp->cur_cb; C.cur[1] = cp->cur_cr; C.refs = cp->refs_c;
+    C.recon[0] = cp->recon_cb; C.recon[1] = cp->recon_cr; C.stride = cp->c_stride; C.on = 1;
+  }
+  return C;
+}
+
+// chroma != NULL: 4:2:0 (P.chroma_format 1, d_est4 = 7 tables: luma 4x4..32x32, chroma 4x4..16x16)
 static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
                             const hvx_ctu_params *h_params, const hvx_estbits *d_est4, void *d_workspace, size_t ws_bytes,
-                            hvx_cu_result *d_out, const uint8_t *cnt_states, const int32_t *cnt_eb) {
+                            hvx_cu_result *d_out, const uint8_t *cnt_states, const int32_t *cnt_eb,
+                            const hvx_chroma_planes *chroma = nullptr) {
   if (!ctx || !d_cur || !d_refs || !h_params || !d_est4 || !d_workspace || !d_out)
     return fail(HVX_E_INVALID, "hvx_ctu_analyze: NULL argument");
   const hvx_ctu_params P = *h_params;
   if (P.pic_w <= 0 || P.pic_h <= 0 || P.n_ref <= 0 || P.n_ref > 8 || P.qp < 0 || P.qp > 51 ||
       stride < P.pic_w + 2 * HVX_PLANE_MARGIN || stride % 4 != 0 || P.search_range <= 0 || P.search_range > 256)
     return fail(HVX_E_INVALID, "hvx_ctu_analyze: bad parameters");
+  if (P.chroma_format != (chroma ? 1 : 0))
+    return fail(HVX_E_INVALID, "hvx_ctu_analyze: chroma_format must be 0 (luma entry points) or 1 (hvx_ctu_encode_yuv)");
+  if (chroma && (!chroma->cur_cb || !chroma->cur_cr || !chroma->refs_c || chroma->c_stride % 4 != 0 ||
+                 chroma->c_stride < P.pic_w / 2 + HVX_PLANE_MARGIN || P.pic_w % 8 || P.pic_h % 8 ||
+                 P.qp_chroma < 0 || P.qp_chroma > 51 || !(P.chroma_weight > 0.0)))
+    return fail(HVX_E_INVALID, "hvx_ctu_encode_yuv: bad chroma planes / parameters");
+  const CtuChroma C = ctu_chroma(chroma);
+  const int n_est = chroma ? 7 : 4;
   const CtuLayout L = ctu_layout(P.pic_w, P.pic_h, P.n_ref);
   const CtuWs W = ctu_ws_layout(L);
   if (ws_bytes < W.total) return fail(HVX_E_INVALID, "hvx_ctu_analyze: workspace too small");
@@ -709,7 +734,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   const int n = L.nctu;
   auto resid_range = [&](hipStream_t s, int first, int ncu) {
     hipLaunchKernelGGL(k_ctu_pred_resid, dim3(n * ncu), dim3(64), 0, s, L, P, d_cur, d_refs, stride, res, resid, desc, off,
-                       est_idx, d_out, first, ncu);
+                       est_idx, d_out, first, ncu, C);
   };
   for (int d = 0; d < 4; d++) {
     const int ncu = 1 << (2 * d), nt = L.nctu * ncu * L.nref;
@@ -759,7 +784,8 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     const dim3 grid((cnt + 63) / 64);
     if (L2 == 3) hipLaunchKernelGGL((k_coeff_bits_il<3>), grid, dim3(64), 0, s, desc + first, cnt, levI + il_off, cnt_eb, cnt_states, cb + first);
     else if (L2 == 2) hipLaunchKernelGGL((k_coeff_bits_il<2>), grid, dim3(64), 0, s, desc + first, cnt, levI + il_off, cnt_eb, cnt_states, cb + first);
-    else hipLaunchKernelGGL((k_coeff_bits_il<1>), grid, dim3(64), 0, s, desc + first, cnt, levI + il_off, cnt_eb, cnt_states, cb + first);
+    else if (L2 == 1) hipLaunchKernelGGL((k_coeff_bits_il<1>), grid, dim3(64), 0, s, desc + first, cnt, levI + il_off, cnt_eb, cnt_states, cb + first);
+    else hipLaunchKernelGGL((k_coeff_bits_il<0>), grid, dim3(64), 0, s, desc + first, cnt, levI + il_off, cnt_eb, cnt_states, cb + first);
     t_end(ctx, s, tc);
   };
   // size classes are contiguous: [0,8n) 32x32 | [8n,24n) 16x16 | [24n,88n) 8x8; their
@@ -769,13 +795,22 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     const int tk = t_begin(ctx, sb, 5);
     resid_range(sb, 0, 5);
     t_end(ctx, sb, tk);
+    if (C.on) {  // the chroma 16x16 TUs of these CUs on stream E, beside the luma 32x32 pipeline
+      HVX_HIP(hipEventRecord(ctx->fj[7], sb));
+      HVX_HIP(hipStreamWaitEvent(se, ctx->fj[7], 0));
+      const size_t o = ctu_il_offc16(n);
+      tu_class_launch<2, 2>(se, desc + 88 * n, d_est4, est_idx + 88 * n, off + 88 * n, 16 * n, resid, nullptr, lev,
+                            nullptr, abs_sum + 88 * n, res_out, sse + 88 * n, coefI + o, cxI + o, levI + o, stI + o,
+                            flags + 88 * n, kCtuG, n_est, ctx, 9);
+      count_class(se, 88 * n, 16 * n, o, 2);
+    }
     tu_class_launch<3, 2>(sb, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev, nullptr, abs_sum, res_out, sse,
-                          coefI, cxI, levI, stI, flags, g32, 4, ctx, 6, cnt_states ? ctx->fj[5] : nullptr);
+                          coefI, cxI, levI, stI, flags, g32, n_est, ctx, 6, cnt_states ? ctx->fj[5] : nullptr);
     if (cnt_states) {
       HVX_HIP(hipStreamWaitEvent(se, ctx->fj[5], 0));
       count_class(se, 0, 8 * n, 0, 3);
-      HVX_HIP(hipEventRecord(ctx->fj[6], se));
     }
+    HVX_HIP(hipEventRecord(ctx->fj[6], se));
     HVX_HIP(hipEventRecord(ctx->fj[3], sb));
   }
   {  // stream C
@@ -785,8 +820,16 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     t_end(ctx, sc, tk);
     const size_t o = ctu_il_off16(n);
     tu_class_launch<2, 2>(sc, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n, 16 * n, resid, nullptr, lev, nullptr,
-                          abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, cxI + o, levI + o, stI + o, flags + 8 * n, g16, 4, ctx, 9);
+                          abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, cxI + o, levI + o, stI + o, flags + 8 * n, g16,
+                          n_est, ctx, 9);
     count_class(sc, 8 * n, 16 * n, o, 2);
+    if (C.on) {
+      const size_t oc = ctu_il_offc8(n);
+      tu_class_launch<1, 2>(sc, desc + 104 * n, d_est4, est_idx + 104 * n, off + 104 * n, 32 * n, resid, nullptr, lev,
+                            nullptr, abs_sum + 104 * n, res_out, sse + 104 * n, coefI + oc, cxI + oc, levI + oc, stI + oc,
+                            flags + 104 * n, kCtuG, n_est, ctx, 12);
+      count_class(sc, 104 * n, 32 * n, oc, 1);
+    }
     HVX_HIP(hipEventRecord(ctx->fj[4], sc));
   }
   {  // stream A: depth 3
@@ -795,12 +838,20 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     t_end(ctx, st, tk);
     const size_t o = ctu_il_off8(n);
     tu_class_launch<1, 2>(st, desc + 24 * n, d_est4, est_idx + 24 * n, off + 24 * n, 64 * n, resid, nullptr, lev, nullptr,
-                          abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, cxI + o, levI + o, stI + o, flags + 24 * n, g8, 4, ctx, 12);
+                          abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, cxI + o, levI + o, stI + o, flags + 24 * n, g8,
+                          n_est, ctx, 12);
     count_class(st, 24 * n, 64 * n, o, 1);
+    if (C.on) {
+      const size_t oc = ctu_il_offc4(n);
+      tu_class_launch<0, 2>(st, desc + 136 * n, d_est4, est_idx + 136 * n, off + 136 * n, 128 * n, resid, nullptr, lev,
+                            nullptr, abs_sum + 136 * n, res_out, sse + 136 * n, coefI + oc, cxI + oc, levI + oc, stI + oc,
+                            flags + 136 * n, kCtuG, n_est, ctx, 12);
+      count_class(st, 136 * n, 128 * n, oc, 0);
+    }
   }
   HVX_HIP(hipStreamWaitEvent(st, ctx->fj[3], 0));
   HVX_HIP(hipStreamWaitEvent(st, ctx->fj[4], 0));
-  if (cnt_states) HVX_HIP(hipStreamWaitEvent(st, ctx->fj[6], 0));
+  HVX_HIP(hipStreamWaitEvent(st, ctx->fj[6], 0));
   const int tk = t_begin(ctx, st, 15);
   hipLaunchKernelGGL(k_ctu_finalize, dim3((n * HVX_CUS_PER_CTU + 255) / 256), dim3(256), 0, st, L, abs_sum, sse, d_out);
   t_end(ctx, st, tk);
@@ -816,7 +867,7 @@ int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_
 static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const hvx_ctu_params *h_params,
                            const uint8_t *d_ctx_states, const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes,
                            const hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic,
-                           bool count) {
+                           bool count, const hvx_chroma_planes *chroma = nullptr) {
   if (!ctx || !d_cur || !h_params || !d_ctx_states || !d_entropy_bits || !d_workspace || !d_cu || !d_dec || !d_recon)
     return fail(HVX_E_INVALID, "hvx_ctu_decide: NULL argument");
   const hvx_ctu_params P = *h_params;
@@ -852,15 +903,25 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
   A.cu = d_cu; A.res = (const hvx_me_result *)(ws + W.res); A.cb = cb;
   A.st = d_ctx_states; A.eb = d_entropy_bits; A.dec = d_dec;
   A.metric = P.rd_metric; A.lambda_ssim = P.lambda_ssim;
+  A.C = ctu_chroma(chroma); A.cw = P.chroma_weight;
+  if (chroma && (!chroma->recon_cb || !chroma->recon_cr || (d_ref_pic && (!chroma->ref_pic_cb || !chroma->ref_pic_cr))))
+    return fail(HVX_E_INVALID, "hvx_ctu_encode_yuv: NULL chroma reconstruction / reference plane");
   hipLaunchKernelGGL(k_ctu_leaf, dim3(n * HVX_CUS_PER_CTU), dim3(64), 0, st, A, d_cur, stride, (const int16_t *)(ws + W.resid),
                      (const int16_t *)(ws + W.res_out), (const int32_t *)(ws + W.abs), (const uint32_t *)(ws + W.sse));
   hipLaunchKernelGGL(k_ctu_decide, dim3((n + 63) / 64), dim3(64), 0, st, A);
   hipLaunchKernelGGL(k_ctu_recon, dim3(n), dim3(256), 0, st, L, P.pic_w, P.pic_h, d_cur, stride, (const hvx_cu_decision *)d_dec,
-                     (const int16_t *)(ws + W.resid), (const int16_t *)(ws + W.res_out), d_recon);
-  const int M = HVX_PLANE_MARGIN;
-  hipLaunchKernelGGL(k_plane_extend, dim3((2 * M + 255) / 256, P.pic_h), dim3(256), 0, st, d_recon, stride, P.pic_w, P.pic_h, M, 0);
-  hipLaunchKernelGGL(k_plane_extend, dim3((P.pic_w + 2 * M + 255) / 256, 2 * M), dim3(256), 0, st, d_recon, stride, P.pic_w,
-                     P.pic_h, M, 1);
+                     (const int16_t *)(ws + W.resid), (const int16_t *)(ws + W.res_out), d_recon, A.C);
+  const int M = HVX_PLANE_MARGIN, Mc = M / 2, cw = P.pic_w / 2, ch = P.pic_h / 2;
+  // extendPicBorder of a plane (margin m): left/right columns, then the top/bottom rows
+  auto extend = [&](uint8_t *pl, int s, int w, int h, int m) {
+    hipLaunchKernelGGL(k_plane_extend, dim3((2 * m + 255) / 256, h), dim3(256), 0, st, pl, s, w, h, m, 0);
+    hipLaunchKernelGGL(k_plane_extend, dim3((w + 2 * m + 255) / 256, 2 * m), dim3(256), 0, st, pl, s, w, h, m, 1);
+  };
+  extend(d_recon, stride, P.pic_w, P.pic_h, M);
+  if (chroma) {
+    extend(chroma->recon_cb, chroma->c_stride, cw, ch, Mc);
+    extend(chroma->recon_cr, chroma->c_stride, cw, ch, Mc);
+  }
   t_end(ctx, st, tk);
   if (d_ref_pic) {
     // 4. the reference picture: the reconstruction deblocked (boundary strengths of the decided
@@ -871,22 +932,34 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
     int8_t *qpm = (int8_t *)(ws + W.qpm);
     hipLaunchKernelGGL(k_ctu_bs, dim3((nunit + 255) / 256), dim3(256), 0, st, d_cu, (const hvx_cu_decision *)d_dec,
                        P.pic_w, P.pic_h, P.qp, bsv, bsh, qpm);
-    uint8_t *base_src = d_recon - (int64_t)M * stride - M, *base_dst = d_ref_pic - (int64_t)M * stride - M;
-    if (d_ref_pic != d_recon)
-      HVX_HIP(hipMemcpyAsync(base_dst, base_src, (size_t)stride * (P.pic_h + 2 * M), hipMemcpyDeviceToDevice, st));
+    auto copy_plane = [&](uint8_t *dst, const uint8_t *src, int s, int h, int m) -> int {
+      if (dst != src)
+        HVX_HIP(hipMemcpyAsync(dst - (int64_t)m * s - m, src - (int64_t)m * s - m, (size_t)s * (h + 2 * m),
+                               hipMemcpyDeviceToDevice, st));
+      return HVX_OK;
+    };
+    int rc = copy_plane(d_ref_pic, d_recon, stride, P.pic_h, M);
+    if (!rc && chroma) rc = copy_plane(chroma->ref_pic_cb, chroma->recon_cb, chroma->c_stride, ch, Mc);
+    if (!rc && chroma) rc = copy_plane(chroma->ref_pic_cr, chroma->recon_cr, chroma->c_stride, ch, Mc);
+    if (rc) return rc;
     hvx_deblock_params dp = {};
     dp.pic_w = P.pic_w; dp.pic_h = P.pic_h;
+    // loopFilterPic: luma, and at 4:2:0 the chroma edges (filtered only where bs == 2, i.e. never
+    // between the inter CUs of this pass)
+    uint8_t *dcb = chroma ? chroma->ref_pic_cb : nullptr, *dcr = chroma ? chroma->ref_pic_cr : nullptr;
+    const int dcs = chroma ? chroma->c_stride : 0;
     const int nv = (P.pic_w / 8 - 1) * (P.pic_h / 4), nh = (P.pic_h / 8 - 1) * (P.pic_w / 4);
     if (nv > 0)
-      hipLaunchKernelGGL(k_deblock<0>, dim3((nv + 255) / 256), dim3(256), 0, st, d_ref_pic, stride, (uint8_t *)nullptr,
-                         (uint8_t *)nullptr, 0, bsv, qpm, dp);
+      hipLaunchKernelGGL(k_deblock<0>, dim3((nv + 255) / 256), dim3(256), 0, st, d_ref_pic, stride, dcb, dcr, dcs, bsv, qpm,
+                         dp);
     if (nh > 0)
-      hipLaunchKernelGGL(k_deblock<1>, dim3((nh + 255) / 256), dim3(256), 0, st, d_ref_pic, stride, (uint8_t *)nullptr,
-                         (uint8_t *)nullptr, 0, bsh, qpm, dp);
-    hipLaunchKernelGGL(k_plane_extend, dim3((2 * M + 255) / 256, P.pic_h), dim3(256), 0, st, d_ref_pic, stride, P.pic_w,
-                       P.pic_h, M, 0);
-    hipLaunchKernelGGL(k_plane_extend, dim3((P.pic_w + 2 * M + 255) / 256, 2 * M), dim3(256), 0, st, d_ref_pic, stride,
-                       P.pic_w, P.pic_h, M, 1);
+      hipLaunchKernelGGL(k_deblock<1>, dim3((nh + 255) / 256), dim3(256), 0, st, d_ref_pic, stride, dcb, dcr, dcs, bsh, qpm,
+                         dp);
+    extend(d_ref_pic, stride, P.pic_w, P.pic_h, M);
+    if (chroma) {
+      extend(chroma->ref_pic_cb, chroma->c_stride, cw, ch, Mc);
+      extend(chroma->ref_pic_cr, chroma->c_stride, cw, ch, Mc);
+    }
     t_end(ctx, st, tk);
   }
   return launched("hvx_ctu_decide");
@@ -909,6 +982,19 @@ int hvx_ctu_encode(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_r
   if (rc) return rc;
   return ctu_decide_impl(ctx, d_cur, stride, h_params, d_ctx_states, d_entropy_bits, d_workspace, ws_bytes, d_cu, d_dec,
                          d_recon, d_ref_pic, false);
+}
+
+int hvx_ctu_encode_yuv(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
+                       const hvx_chroma_planes *h_chroma, const hvx_ctu_params *h_params, const hvx_estbits *d_est7,
+                       const uint8_t *d_ctx_states, const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes,
+                       hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic) {
+  if (!h_chroma || !d_ctx_states || !d_entropy_bits || !d_dec || !d_recon)
+    return fail(HVX_E_INVALID, "hvx_ctu_encode_yuv: NULL argument");
+  const int rc = ctu_analyze_impl(ctx, d_cur, d_refs, stride, h_params, d_est7, d_workspace, ws_bytes, d_cu, d_ctx_states,
+                                  d_entropy_bits, h_chroma);
+  if (rc) return rc;
+  return ctu_decide_impl(ctx, d_cur, stride, h_params, d_ctx_states, d_entropy_bits, d_workspace, ws_bytes, d_cu, d_dec,
+                         d_recon, d_ref_pic, false, h_chroma);
 }
 
 int hvx_plane_extend(hvx_ctx *ctx, uint8_t *d_plane, int width, int height) {

@@ -1236,7 +1236,7 @@ __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ 
                                                 int32_t *__restrict__ abs_out, const int8_t *__restrict__ flags, int G,
                                                 int n_est_lds) {
   constexpr int N = 4 << L, NN = N * N;
-  __shared__ hvx_estbits tbl[4];
+  __shared__ hvx_estbits tbl[8];  // n_est_lds <= 8 (the CTU pass: 4 luma + 3 chroma)
   __shared__ RdLaneStage stage;
   const int lane = lane_id();
   if (n_est_lds > 0) {

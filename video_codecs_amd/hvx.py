@@ -44,6 +44,7 @@ def lib():
             "hvx_ctu_analyze": [P, P, P, I, P, P, P, ctypes.c_size_t, P],
             "hvx_ctu_decide": [P, P, I, P, P, P, P, ctypes.c_size_t, P, P, P, P],
             "hvx_ctu_encode": [P, P, P, I, P, P, P, P, P, ctypes.c_size_t, P, P, P, P],
+            "hvx_ctu_encode_yuv": [P, P, P, I, P, P, P, P, P, P, ctypes.c_size_t, P, P, P, P],
             "hvx_set_timing": [P, I], "hvx_phase_times": [P, ctypes.POINTER(ctypes.c_double), I, I],
             "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
             "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P],
@@ -264,21 +265,32 @@ def ctu_workspace_size(pic_w, pic_h, n_ref):
     return n.value
 
 
-class CtuAnalyzer:
-    """Device-resident CTU analysis pass (hvx_ctu_analyze) for one picture geometry."""
+class ChromaPlanes(ctypes.Structure):
+    """hvx_chroma_planes (hvx_types.h): device origins of the 4:2:0 chroma planes."""
+    _fields_ = [("cur_cb", ctypes.c_void_p), ("cur_cr", ctypes.c_void_p), ("refs_c", ctypes.c_void_p),
+                ("recon_cb", ctypes.c_void_p), ("recon_cr", ctypes.c_void_p), ("ref_pic_cb", ctypes.c_void_p),
+                ("ref_pic_cr", ctypes.c_void_p), ("c_stride", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
-    def __init__(self, pic_w, pic_h, n_ref, qp, lam=None, est4=None, rd_metric=_abi.RD_SSE, ctx=None):
+
+class CtuAnalyzer:
+    """Device-resident CTU analysis pass (hvx_ctu_analyze) for one picture geometry; chroma=True:
+    the 4:2:0 step (hvx_ctu_encode_yuv, encode_yuv)."""
+
+    def __init__(self, pic_w, pic_h, n_ref, qp, lam=None, est4=None, rd_metric=_abi.RD_SSE, ctx=None, chroma=False):
         """ctx: a private hvx_ctx (new_context()) for an analyzer that runs concurrently with
         others on the same GPU; None = the shared per-device context."""
         import torch
         self._c = ctx
-        self.params = _abi.ctu_params(pic_w, pic_h, n_ref, qp, lam, rd_metric=rd_metric)
+        self.chroma = chroma
+        self.params = _abi.ctu_params(pic_w, pic_h, n_ref, qp, lam, rd_metric=rd_metric, chroma=chroma)
         self.pic_w, self.pic_h, self.n_ref = pic_w, pic_h, n_ref
         self.stride = pic_w + 2 * _abi.PLANE_MARGIN
+        self.c_stride = pic_w // 2 + _abi.PLANE_MARGIN
         self.nctu = ((pic_w + 63) // 64) * ((pic_h + 63) // 64)
         self.ws_bytes = ctu_workspace_size(pic_w, pic_h, n_ref)
         self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device="cuda")
-        est4 = _abi.load_estbits_p_luma() if est4 is None else est4
+        if est4 is None:
+            est4 = _abi.estbits_p_yuv(estbits_update) if chroma else _abi.load_estbits_p_luma()
         self.est = torch.from_numpy(np.ascontiguousarray(est4, np.int32).reshape(-1)).cuda()
         self.out = torch.zeros(self.nctu * _abi.CUS_PER_CTU * _abi.CU_RESULT.itemsize, dtype=torch.uint8, device="cuda")
 
@@ -317,6 +329,27 @@ class CtuAnalyzer:
                                     ctypes.c_void_p(plane_origin_ptr(recon_plane, self.pic_w)),
                                     ctypes.c_void_p(0 if ref_pic is None else plane_origin_ptr(ref_pic, self.pic_w))),
                "hvx_ctu_encode")
+
+    def encode_yuv(self, cur3, ref_ptrs_y, ref_ptrs_c, recon3, ref_pic3=None):
+        """hvx_ctu_encode_yuv: cur3 / recon3 / ref_pic3 = (Y, Cb, Cr) padded uint8 device tensors (chroma:
+        half size, margin PLANE_MARGIN // 2); ref_ptrs_y = int64 device tensor of the references' Y
+        origins, ref_ptrs_c = int64 device tensor of their Cb origins then their Cr origins."""
+        assert self.chroma
+        self._rate_model()
+        w2 = self.pic_w // 2
+        co = lambda t: plane_origin_ptr(t, w2, _abi.PLANE_MARGIN // 2)  # noqa: E731
+        cp = ChromaPlanes(co(cur3[1]), co(cur3[2]), ref_ptrs_c.data_ptr(), co(recon3[1]), co(recon3[2]),
+                          0 if ref_pic3 is None else co(ref_pic3[1]), 0 if ref_pic3 is None else co(ref_pic3[2]),
+                          self.c_stride, 0)
+        p = np.ascontiguousarray(self.params)
+        _check(lib().hvx_ctu_encode_yuv(self.ctx(), ctypes.c_void_p(plane_origin_ptr(cur3[0], self.pic_w)),
+                                        _ptr(ref_ptrs_y), self.stride, ctypes.byref(cp),
+                                        p.ctypes.data_as(ctypes.c_void_p), _ptr(self.est), _ptr(self.states),
+                                        _ptr(self.eb), _ptr(self.ws), self.ws_bytes, _ptr(self.out), _ptr(self.dec),
+                                        ctypes.c_void_p(plane_origin_ptr(recon3[0], self.pic_w)),
+                                        ctypes.c_void_p(0 if ref_pic3 is None else plane_origin_ptr(ref_pic3[0],
+                                                                                                     self.pic_w))),
+               "hvx_ctu_encode_yuv")
 
     def decide(self, cur_plane, recon_plane, states=None, entropy_bits=None, ref_pic=None):
         """hvx_ctu_decide after run(): CU tree of every CTU + the reconstructed picture (the leaves'
@@ -359,6 +392,28 @@ def phase_times(reset=True, ctx=None):
 
 def sync():
     _check(lib().hvx_sync(context()), "hvx_sync")
+
+
+def yuv_plane_shapes(width, height, margin=_abi.PLANE_MARGIN):
+    """Shapes of the three padded planes of a 4:2:0 picture: Y (margin), Cb and Cr (margin // 2)."""
+    mc = margin // 2
+    return ((height + 2 * margin, width + 2 * margin), (height // 2 + 2 * mc, width // 2 + 2 * mc),
+            (height // 2 + 2 * mc, width // 2 + 2 * mc))
+
+
+def yuv_views(flat, width, height, margin=_abi.PLANE_MARGIN):
+    """(Y, Cb, Cr) 2-D views of one contiguous uint8 picture buffer of sum(prod(shape)) bytes (a torch
+    tensor or a numpy array)."""
+    out, o = [], 0
+    for sh in yuv_plane_shapes(width, height, margin):
+        n = sh[0] * sh[1]
+        out.append(flat[o:o + n].reshape(sh))
+        o += n
+    return out
+
+
+def yuv_bytes(width, height, margin=_abi.PLANE_MARGIN):
+    return sum(a * b for a, b in yuv_plane_shapes(width, height, margin))
 
 
 def plane_origin_ptr(plane, width, margin=_abi.PLANE_MARGIN):

@@ -24,3 +24,13 @@ def luma_plane(w, h, index, margin=80):
     """The frame's luma as an 8-bit padded plane (HVX_PLANE_MARGIN border, edges replicated)."""
     y = random_frame(w, h, index)[: w * h].reshape(h, w)
     return np.pad(y, margin, mode="edge")
+
+
+def yuv_planes(w, h, index, margin=80):
+    """The frame as three 8-bit padded planes (Y with margin, Cb / Cr with margin // 2, edges replicated)."""
+    f = random_frame(w, h, index)
+    n, c = w * h, (w // 2) * (h // 2)
+    y = f[:n].reshape(h, w)
+    cb = f[n:n + c].reshape(h // 2, w // 2)
+    cr = f[n + c:n + 2 * c].reshape(h // 2, w // 2)
+    return np.pad(y, margin, mode="edge"), np.pad(cb, margin // 2, mode="edge"), np.pad(cr, margin // 2, mode="edge")
