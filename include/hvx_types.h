@@ -167,8 +167,9 @@ typedef struct hvx_cu_decision {
   uint32_t best_bits, best_dist; /* the chosen sub-tree rooted at this CU, split flags included */
   int32_t split;             /* 1: the sub-tree rooted here splits (forced for CUs crossing the picture edge) */
   int32_t leaf;              /* 1: a leaf of the CTU's final CU tree (its samples are in the reconstruction) */
-  int32_t cbf;               /* bit t: luma TU t of the CU is coded; 4:2:0 also bit 4 + t: Cb TU t, bit 8 + t: Cr TU t
-                                (0: qt_root_cbf 0, prediction only) */
+  int32_t cbf;               /* bit t: luma TU t of the CU is coded; 4:2:0 also bit 4 + t: Cb TU t, bit 8 + t: Cr TU t,
+                                and bit 12 + t / 16 + t: that Cb / Cr TU (4x4, 8x8 CU) is coded in transform-skip
+                                mode (0: qt_root_cbf 0, prediction only) */
   float ssim_dist;           /* HVX_RD_SSIM: D_ssim of the CU as a leaf (8x8 blocks in raster order, float sum) */
   float best_ssim_dist;      /* HVX_RD_SSIM: D_ssim of the chosen sub-tree (children in z-order) */
   int32_t pad_;

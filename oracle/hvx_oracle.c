@@ -1367,6 +1367,7 @@ void hvxo_ctu_tu_desc(const hvx_ctu_params *p, int cu_size, int log2, hvx_tu_des
   d->qp_rem = p->qp % 6;
   d->sign_hiding = 1;
   d->use_rdoq = d->use_rdoq_ts = 1;
+  d->pps_tskip = 1;                     /* TransformSkip=1 (cfg): 4x4 TUs code transform_skip_flag */
   d->max_log2_tr_range = 15;
   d->bit_depth = 8;
   d->lambda = p->lambda;
@@ -1404,6 +1405,11 @@ typedef struct {
   uint32_t me_bits[HVX_CUS_PER_CTU];
   uint8_t *pred;  /* HVX_CUS_PER_CTU * 4096 luma, then HVX_CUS_PER_CTU * 2 * 1024 chroma */
   int16_t *rres;  /* same layout */
+  /* the transform-skip mode of the 4x4 chroma TUs of the 8x8 CUs: [cu][comp - 1] */
+  uint64_t ts_frac[HVX_CUS_PER_CTU][2];
+  int32_t ts_abs[HVX_CUS_PER_CTU][2];
+  uint32_t ts_sse[HVX_CUS_PER_CTU][2];
+  int16_t ts_rres[HVX_CUS_PER_CTU][2][16];
 } ctu_extra;
 #define EX_CHROMA(ci, c) (HVX_CUS_PER_CTU * 4096 + ((ci) * 2 + (c) - 1) * 1024)
 
@@ -1504,8 +1510,28 @@ static void ctu_analyze_core(const uint8_t *cur, const uint8_t *const *refs, int
                                  cp, 32);
           hvx_tu_desc tc;
           hvxo_ctu_tu_desc_chroma(p, c, S, log2 - 1, &tc);
-          ctu_comp_tus(cc->cur[c - 1] + (y / 2) * cc->stride + x / 2, cc->stride, cp, 32, S / 2, &tc, &est[4 + log2 - 3],
-                       ex, ci, c, &cs, &ca, &cn);
+          const uint8_t *org = cc->cur[c - 1] + (y / 2) * cc->stride + x / 2;
+          ctu_comp_tus(org, cc->stride, cp, 32, S / 2, &tc, &est[4 + log2 - 3], ex, ci, c, &cs, &ca, &cn);
+          if (S == 8 && ex) {
+            /* xEstimateInterResidualQT's second mode of a 4x4 TU (TEncSearch.cpp:4516-4565,
+             * TransformSkip=1): the same residual through transformNxN with transform skip (RDOQTS) */
+            int16_t resi[16], rec[16];
+            for (int k = 0; k < 16; k++) resi[k] = (int16_t)((int)org[(k / 4) * cc->stride + k % 4] - cp[(k / 4) * 32 + k % 4]);
+            tc.transform_skip = 1;
+            int32_t temp[16], lev[16], abs_sum = 0;
+            hvxo_transform_nxn(&tc, &est[4], resi, 4, temp, lev, NULL, &abs_sum);
+            hvxo_inv_transform_nxn(&tc, lev, rec, 4);
+            uint32_t sse = 0;
+            for (int k = 0; k < 16; k++) { int df = resi[k] - rec[k]; sse += (uint32_t)(df * df); }
+            uint8_t st[HVX_NUM_CTX];
+            hvx_coeff_bits cb;
+            memcpy(st, ex->states, sizeof(st));
+            hvxo_coeff_bits(&tc, lev, st, ex->eb, &cb);
+            ex->ts_frac[ci][c - 1] = cb.frac_bits;
+            ex->ts_abs[ci][c - 1] = abs_sum;
+            ex->ts_sse[ci][c - 1] = sse;
+            memcpy(ex->ts_rres[ci][c - 1], rec, sizeof(rec));
+          }
         }
       }
     }
@@ -1559,7 +1585,9 @@ static uint32_t wdist(double w, uint32_t sse) { return (uint32_t)(w * (double)ss
  * (:4361-4366), then the distortion of the clipped reconstruction (:4408-4417, chroma weighted per
  * component).  Context models: luma qt_cbf 28 + getCtxQtCbf (TComDataCU.cpp:1503, 1 at transform
  * depth 0), chroma qt_cbf 33 + the transform depth, qt_root_cbf 41 (TEncSbac::codeQtRootCbfZero :1097).
- * The chroma cbf of the 64x64 root node and split_transform_flag are not counted (no RQT here). */
+ * A 4x4 chroma TU (8x8 CU) also tries its transform-skip mode (TransformSkip=1, :4516-4565,
+ * 4741-4753): chosen when its coded cost is <= mode 0's best.  The chroma cbf of the 64x64 root
+ * node and split_transform_flag are not counted (no RQT here). */
 static void leaf_eval(const decide_ctx *c, int ci, int S, int x, int y, hvx_cu_decision *o) {
   const ctu_extra *ex = c->ex;
   const int T = S < 32 ? S : 32, ntu = (S / T) * (S / T), ncomp = c->cc ? 3 : 1;
@@ -1584,6 +1612,16 @@ static void leaf_eval(const decide_ctx *c, int ci, int S, int x, int y, hvx_cu_d
           cbf |= 1 << (4 * comp + t);
         }
       }
+      if (comp && T == 8 && ex->ts_abs[ci][comp - 1] > 0) {
+        /* the transform-skip mode (:4741-4753): its coded cost replaces mode 0's best on <= */
+        const uint64_t f2 = c1 + ex->ts_frac[ci][comp - 1];
+        const uint32_t sd = wdist(w, ex->ts_sse[ci][comp - 1]);
+        if (rd_cost((uint32_t)(f2 >> 15), sd, lam) <= rd_cost((uint32_t)(tf >> 15), td, lam)) {
+          tf = f2;
+          td = sd;
+          cbf |= (1 << (4 * comp + t)) | (1 << (8 + 4 * comp + t));
+        }
+      }
       tree += tf;
       nz_dist += td;
     }
@@ -1603,7 +1641,8 @@ static void leaf_eval(const decide_ctx *c, int ci, int S, int x, int y, hvx_cu_d
     for (int yy = 0; yy < Sc; yy++)
       for (int xx = 0; xx < Sc; xx++) {
         const int t = (yy / Tc) * (Sc / Tc) + xx / Tc, k = EX_CHROMA(ci, comp) + yy * 32 + xx;
-        const int rec = clip_pel(ex->pred[k] + (((cbf >> (4 * comp + t)) & 1) ? ex->rres[k] : 0));
+        const int rr = ((cbf >> (8 + 4 * comp + t)) & 1) ? ex->ts_rres[ci][comp - 1][yy * 4 + xx] : ex->rres[k];
+        const int rec = clip_pel(ex->pred[k] + (((cbf >> (4 * comp + t)) & 1) ? rr : 0));
         const int df = (int)c->cc->cur[comp - 1][(y / 2 + yy) * c->cc->stride + x / 2 + xx] - rec;
         cd += (uint32_t)(df * df);
       }
@@ -1736,8 +1775,9 @@ static void ctu_decide_core(const uint8_t *cur, const uint8_t *const *refs, int 
         for (int yy = 0; yy < Sc; yy++)
           for (int xx = 0; xx < Sc; xx++) {
             const int t = (yy / Tc) * (Sc / Tc) + xx / Tc, k = EX_CHROMA(ci, comp) + yy * 32 + xx;
+            const int rr = ((cbf >> (8 + 4 * comp + t)) & 1) ? ex->ts_rres[ci][comp - 1][yy * 4 + xx] : ex->rres[k];
             recon_c[comp - 1][(y / 2 + yy) * recon_c_stride + x / 2 + xx] =
-                (uint8_t)clip_pel(ex->pred[k] + (((cbf >> (4 * comp + t)) & 1) ? ex->rres[k] : 0));
+                (uint8_t)clip_pel(ex->pred[k] + (((cbf >> (4 * comp + t)) & 1) ? rr : 0));
           }
       }
     }

@@ -301,7 +301,7 @@ def check_ctu_encode_yuv(seed, width, height, nref, qp):
     st, eb = _abi.load_ctx_p_states(), _abi.load_entropy_bits()
     ncx = (width + 63) // 64
     exp_rec = [np.zeros_like(x) for x in cur]
-    n_leaf = n_cbf_c = 0
+    n_leaf = n_cbf_c = n_ts_c = 0
     refs3 = ([r[0] for r in refs], [r[1] for r in refs], [r[2] for r in refs])
     for c in range(an.nctu):
         cu, dec = oracle.ctu_decide_yuv(cur, refs3, an.params, est7, st, eb, c % ncx, c // ncx, exp_rec)
@@ -310,6 +310,7 @@ def check_ctu_encode_yuv(seed, width, height, nref, qp):
             assert got_dec[c][ci].tobytes() == dec[ci].tobytes(), (c, ci, got_dec[c][ci], dec[ci])
         n_leaf += int(dec["leaf"].sum())
         n_cbf_c += int(((dec["cbf"] >> 4) & 0xff)[dec["leaf"] == 1].astype(bool).sum())
+        n_ts_c += int(((dec["cbf"] >> 12) & 0xff).astype(bool).sum())
     inner = []
     for k in range(3):
         m = M if k == 0 else M // 2
@@ -323,7 +324,7 @@ def check_ctu_encode_yuv(seed, width, height, nref, qp):
                                   _abi.deblock_params(width, height))
     for k, d in enumerate((dy, dcb, dcr)):
         np.testing.assert_array_equal(refpic_t[k].cpu().numpy(), np.pad(d, M if k == 0 else M // 2, mode="edge"))
-    return an.nctu, n_leaf, n_cbf_c
+    return an.nctu, n_leaf, n_cbf_c, n_ts_c
 
 
 # ------------------------------------------------------------------------------------------- MC

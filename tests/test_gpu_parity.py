@@ -161,13 +161,16 @@ def test_ctu_encode_fused_gpu(torch):
 def test_ctu_encode_yuv_gpu(torch):
     # 4:2:0 step: chroma MC, Cb/Cr TUs (4x4..16x16) through RDOQ + rate, chroma-weighted decisions,
     # Y/Cb/Cr reconstruction and reference picture; a 264x200 picture exercises partial CTUs
-    n_ctu, n_leaf, n_cbf_c = gpu_cases.check_ctu_encode_yuv(seed=41, width=264, height=200, nref=2, qp=27)
+    n_ctu, n_leaf, n_cbf_c, n_ts = gpu_cases.check_ctu_encode_yuv(seed=41, width=264, height=200, nref=2, qp=27)
     assert n_ctu == 20 and n_leaf > 20 and n_cbf_c > 0
+    print("yuv: %d leaves, %d coded chroma TUs, %d 4x4 chroma TUs in transform-skip mode" % (n_leaf, n_cbf_c, n_ts))
 
 
 def test_ctu_encode_yuv_qp_sweep_gpu(torch):
+    n_ts = 0
     for qp in (22, 37):
-        gpu_cases.check_ctu_encode_yuv(seed=qp, width=192, height=128, nref=1, qp=qp)
+        n_ts += gpu_cases.check_ctu_encode_yuv(seed=qp, width=192, height=128, nref=1, qp=qp)[3]
+    print("yuv qp sweep: %d 4x4 chroma TUs in transform-skip mode" % n_ts)
 
 
 def test_ctu_decide_qp_sweep_gpu(torch):

@@ -13,9 +13,10 @@
 struct CtuLayout {
   int nctu_x, nctu_y, nctu, nref;
   // TU classes, contiguous: luma [0,8n) 32x32 | [8n,24n) 16x16 | [24n,88n) 8x8, then (4:2:0) chroma
-  // [88n,104n) 16x16 (the 64x64 and 32x32 CUs) | [104n,136n) 8x8 | [136n,264n) 4x4
-  __host__ __device__ int ntu() const { return 264 * nctu; }
-  __host__ __device__ int64_t nres() const { return (int64_t)24576 * nctu; }
+  // [88n,104n) 16x16 (the 64x64 and 32x32 CUs) | [104n,136n) 8x8 | [136n,264n) 4x4 | [264n,392n) the
+  // transform-skip twins of the 4x4 TUs (same residual, transform_skip = 1)
+  __host__ __device__ int ntu() const { return 392 * nctu; }
+  __host__ __device__ int64_t nres() const { return (int64_t)26624 * nctu; }
 };
 
 // the chroma planes of a 4:2:0 pass (hvx_chroma_planes on the device side); on == 0: luma only
@@ -59,8 +60,10 @@ __device__ __forceinline__ int64_t ctu_tu_offset(const CtuLayout &L, int tu) {
   const int64_t c0 = 16384 * n;
   if (tu < 104 * n) return c0 + (int64_t)(tu - 88 * n) * 256;
   if (tu < 136 * n) return c0 + 4096 * n + (int64_t)(tu - 104 * n) * 64;
-  return c0 + 6144 * n + (int64_t)(tu - 136 * n) * 16;
+  return c0 + 6144 * n + (int64_t)(tu - 136 * n) * 16;  // the 4x4 TUs and their twins
 }
+// the transform-skip twin of a 4x4 chroma TU
+__device__ __forceinline__ int ctu_tu_ts(const CtuLayout &L, int tu) { return tu + 128 * L.nctu; }
 
 // xPredInterBlk for one 4:2:0 chroma sample, uni-prediction (hvxo_chroma_block_epel): the luma
 // quarter-pel MV in 1/8 chroma samples, 4-tap filters, first (+ last) stage(s) of
@@ -168,6 +171,7 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
     td.slice_type = P.slice_type;
     td.qp_per = P.qp / 6; td.qp_rem = P.qp % 6;
     td.sign_hiding = 1; td.use_rdoq = 1; td.use_rdoq_ts = 1;
+    td.pps_tskip = 1;  // TransformSkip=1: 4x4 TUs code transform_skip_flag
     td.max_log2_tr_range = 15; td.bit_depth = 8;
     td.lambda = P.lambda;
     descs[tu] = td;
@@ -186,6 +190,13 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
         descs[tc] = dc;
         offs[tc] = ctu_tu_offset(L, tc);
         est_idx[tc] = 4 + log2 - 3;
+        if (d == 3) {  // the 4x4 TU's transform-skip mode (xEstimateInterResidualQT's second mode)
+          const int tt = ctu_tu_ts(L, tc);
+          dc.transform_skip = 1;
+          descs[tt] = dc;
+          offs[tt] = ctu_tu_offset(L, tt);
+          est_idx[tt] = 4;
+        }
       }
     }
   }
@@ -206,8 +217,9 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
       const int pred = ctu_epel_sample(C.refs[(c - 1) * L.nref + best] + yc * C.stride + xc, C.stride, xx, yy, mvx, mvy);
       const int t = (yy / Tc) * (Sc / Tc) + (xx / Tc);
       const int tu = ctu_tu_index(L, ctu, d, j, t, c);
-      resid[ctu_tu_offset(L, tu) + (yy % Tc) * Tc + (xx % Tc)] =
-          (int16_t)((int)C.cur[c - 1][(yc + yy) * C.stride + xc + xx] - pred);
+      const int16_t r = (int16_t)((int)C.cur[c - 1][(yc + yy) * C.stride + xc + xx] - pred);
+      resid[ctu_tu_offset(L, tu) + (yy % Tc) * Tc + (xx % Tc)] = r;
+      if (d == 3) resid[ctu_tu_offset(L, ctu_tu_ts(L, tu)) + yy * 4 + xx] = r;
     }
   }
 }
@@ -381,6 +393,18 @@ __global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const uint8_t *__
           cbf |= 1 << (4 * comp + t);
         }
       }
+      if (comp && T == 8) {  // the transform-skip mode of a 4x4 TU: chosen when its coded cost <= mode 0's best
+        const int tt = ctu_tu_ts(A.L, tu);
+        if (abs_sum[tt] > 0) {
+          const uint64_t f2 = c1 + A.cb[tt].frac_bits;
+          const uint32_t sd = dec_wdist(A.cw, sse[tt]);
+          if (dec_rd_cost((uint32_t)(f2 >> 15), sd, lam) <= dec_rd_cost((uint32_t)(tf >> 15), td, lam)) {
+            tf = f2;
+            td = sd;
+            cbf |= (1 << (4 * comp + t)) | (1 << (8 + 4 * comp + t));
+          }
+        }
+      }
       tree += tf;
       nz_dist += td;
     }
@@ -402,9 +426,11 @@ __global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const uint8_t *__
     uint32_t cpart = 0;
     for (int k = lane; k < Sc * Sc; k += HVX_WAVE) {
       const int yy = k / Sc, xx = k % Sc, t = (yy / Tc) * (Sc / Tc) + xx / Tc;
-      const int64_t o = ctu_tu_offset(A.L, ctu_tu_index(A.L, ctu, d, j, t, comp)) + (yy % Tc) * Tc + (xx % Tc);
+      const int tu = ctu_tu_index(A.L, ctu, d, j, t, comp);
+      const int64_t o = ctu_tu_offset(A.L, tu) + (yy % Tc) * Tc + (xx % Tc);
+      const int64_t orr = ((cbf >> (8 + 4 * comp + t)) & 1) ? ctu_tu_offset(A.L, ctu_tu_ts(A.L, tu)) + yy * 4 + xx : o;
       const int org = A.C.cur[comp - 1][(y / 2 + yy) * A.C.stride + x / 2 + xx];
-      int v = org - resid[o] + (((cbf >> (4 * comp + t)) & 1) ? res_out[o] : 0);
+      int v = org - resid[o] + (((cbf >> (4 * comp + t)) & 1) ? res_out[orr] : 0);
       v = v < 0 ? 0 : v > 255 ? 255 : v;
       cpart += (uint32_t)((org - v) * (org - v));
     }
@@ -522,10 +548,10 @@ __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int p
     }
     if (d == 4) continue;
     const int Sc = 32 >> d, Tc = (Sc < 16 ? Sc : 16), cx = xx % Sc, cy = yy % Sc, t = (cy / Tc) * (Sc / Tc) + (cx / Tc);
-    const int tu = ctu_tu_index(L, ctu, d, j, t, c);
+    const int tu = ctu_tu_index(L, ctu, d, j, t, c), cbf = dc[depth_base(d) + j].cbf;
     const int64_t o = ctu_tu_offset(L, tu) + (cy % Tc) * Tc + (cx % Tc);
-    const int v = (int)C.cur[c - 1][y * C.stride + x] - resid[o] +
-                  (((dc[depth_base(d) + j].cbf >> (4 * c + t)) & 1) ? res_out[o] : 0);
+    const int64_t orr = ((cbf >> (8 + 4 * c + t)) & 1) ? ctu_tu_offset(L, ctu_tu_ts(L, tu)) + cy * 4 + cx : o;
+    const int v = (int)C.cur[c - 1][y * C.stride + x] - resid[o] + (((cbf >> (4 * c + t)) & 1) ? res_out[orr] : 0);
     C.recon[c - 1][y * C.stride + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
   }
 }

@@ -67,11 +67,11 @@ constexpr int kCtuG = 64;
 size_t pad_g(size_t n) { return (n + kCtuG - 1) / kCtuG * kCtuG; }
 size_t ctu_il_off16(int n) { return pad_g((size_t)8 * n) * 1024; }
 size_t ctu_il_off8(int n) { return ctu_il_off16(n) + pad_g((size_t)16 * n) * 256; }
-// 4:2:0 chroma classes: 16x16 (16n TUs), 8x8 (32n), 4x4 (128n)
+// 4:2:0 chroma classes: 16x16 (16n TUs), 8x8 (32n), 4x4 (128n + 128n transform-skip twins)
 size_t ctu_il_offc16(int n) { return ctu_il_off8(n) + pad_g((size_t)64 * n) * 64; }
 size_t ctu_il_offc8(int n) { return ctu_il_offc16(n) + pad_g((size_t)16 * n) * 256; }
 size_t ctu_il_offc4(int n) { return ctu_il_offc8(n) + pad_g((size_t)32 * n) * 64; }
-size_t ctu_il_words(int n) { return ctu_il_offc4(n) + pad_g((size_t)128 * n) * 16; }
+size_t ctu_il_words(int n) { return ctu_il_offc4(n) + pad_g((size_t)256 * n) * 16; }  // 4x4 TUs + their TS twins
 struct CtuWs {
   size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, coefI, cxI, levI, stI, flags, cbits, bsv, bsh,
       qpm, total;
@@ -843,10 +843,10 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     count_class(st, 24 * n, 64 * n, o, 1);
     if (C.on) {
       const size_t oc = ctu_il_offc4(n);
-      tu_class_launch<0, 2>(st, desc + 136 * n, d_est4, est_idx + 136 * n, off + 136 * n, 128 * n, resid, nullptr, lev,
+      tu_class_launch<0, 2>(st, desc + 136 * n, d_est4, est_idx + 136 * n, off + 136 * n, 256 * n, resid, nullptr, lev,
                             nullptr, abs_sum + 136 * n, res_out, sse + 136 * n, coefI + oc, cxI + oc, levI + oc, stI + oc,
                             flags + 136 * n, kCtuG, n_est, ctx, 12);
-      count_class(st, 136 * n, 128 * n, oc, 0);
+      count_class(st, 136 * n, 256 * n, oc, 0);
     }
   }
   HVX_HIP(hipStreamWaitEvent(st, ctx->fj[3], 0));
