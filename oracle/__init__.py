@@ -300,6 +300,18 @@ def mc(planes, luma_stride, chroma_stride, job):
     return out
 
 
+def chroma_block_epel(plane, x, y, mvx, mvy, w, h, margin=_abi.PLANE_MARGIN // 2):
+    """hvxo_chroma_block_epel on a padded uint8 chroma plane (sample (x, y) relative to its origin)."""
+    c = _c(plane, np.uint8)
+    out = np.zeros(w * h, np.int16)
+    L = lib()
+    L.hvxo_chroma_block_epel.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    L.hvxo_chroma_block_epel(ctypes.c_void_p(c.ctypes.data + margin * c.shape[1] + margin), c.shape[1], x, y, mvx, mvy,
+                             w, h, _p(out), w)
+    return out.reshape(h, w)
+
+
 def add_avg(a, b):
     a, b = _c(a, np.int16), _c(b, np.int16)
     out = np.zeros_like(a)
