@@ -136,6 +136,7 @@ __global__ __launch_bounds__(256) void k_ctu_me_jobs(CtuLayout L, hvx_ctu_params
 __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_params P, const uint8_t *__restrict__ cur,
                                                        const uint8_t *const *__restrict__ refs, int stride,
                                                        const hvx_me_result *__restrict__ res, int16_t *__restrict__ resid,
+                                                       uint8_t *__restrict__ pred_out,
                                                        hvx_tu_desc *__restrict__ descs, int64_t *__restrict__ offs,
                                                        int32_t *__restrict__ est_idx, hvx_cu_result *__restrict__ out,
                                                        int first, int ncu, CtuChroma C) {
@@ -208,7 +209,9 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
     const int pred = me_qpel_sample(rp + y * stride + x, stride, xx, yy, mvx, mvy);
     const int t = (yy / T) * (S / T) + (xx / T);
     const int tu = ctu_tu_index(L, ctu, d, j, t);
-    resid[ctu_tu_offset(L, tu) + (yy % T) * T + (xx % T)] = (int16_t)((int)cur[(y + yy) * stride + x + xx] - pred);
+    const int64_t o = ctu_tu_offset(L, tu) + (yy % T) * T + (xx % T);
+    resid[o] = (int16_t)((int)cur[(y + yy) * stride + x + xx] - pred);
+    pred_out[o] = (uint8_t)pred;
   }
   if (C.on) {
     const int Sc = S / 2, Tc = T / 2, xc = x / 2, yc = y / 2;
@@ -218,8 +221,14 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
       const int t = (yy / Tc) * (Sc / Tc) + (xx / Tc);
       const int tu = ctu_tu_index(L, ctu, d, j, t, c);
       const int16_t r = (int16_t)((int)C.cur[c - 1][(yc + yy) * C.stride + xc + xx] - pred);
-      resid[ctu_tu_offset(L, tu) + (yy % Tc) * Tc + (xx % Tc)] = r;
-      if (d == 3) resid[ctu_tu_offset(L, ctu_tu_ts(L, tu)) + yy * 4 + xx] = r;
+      const int64_t o = ctu_tu_offset(L, tu) + (yy % Tc) * Tc + (xx % Tc);
+      resid[o] = r;
+      pred_out[o] = (uint8_t)pred;
+      if (d == 3) {
+        const int64_t ot = ctu_tu_offset(L, ctu_tu_ts(L, tu)) + yy * 4 + xx;
+        resid[ot] = r;
+        pred_out[ot] = (uint8_t)pred;
+      }
     }
   }
 }
@@ -349,37 +358,32 @@ __device__ bool dec_node(const DecideArgs &A, int ctu, int cx, int cy, DepthMap 
 }
 
 // Leaf evaluation of every CU (hvxo_ctu_decide's leaf_eval: encodeResAndCalcRdInterCU's residual
-// decisions, TEncSearch.cpp:4341-4421): one wave per CU.  The TU / root-cbf decisions are
-// wave-uniform scalar code on the TU records; the zero-residual and the final clipped
-// distortions are wave sums over the CU's samples.  Writes coef_frac, bits, dist and cbf.
-__global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const uint8_t *__restrict__ cur, int stride,
-                                                 const int16_t *__restrict__ resid, const int16_t *__restrict__ res_out,
-                                                 const int32_t *__restrict__ abs_sum, const uint32_t *__restrict__ sse) {
-  const int cuid = blockIdx.x, ctu = cuid / HVX_CUS_PER_CTU, ci = cuid % HVX_CUS_PER_CTU;
+// decisions, TEncSearch.cpp:4341-4421): one THREAD per CU over its TUs' per-TU records -- counted
+// rate, uiAbsSum, coded SSE, zero-residual and clipped-reconstruction distortions (k_tu_fin) --
+// per TU and component the forced-zero test (and at 4x4 chroma the transform-skip mode), the
+// qt_root_cbf test and the leaf distortion as the sum of the chosen TU distortions (chroma
+// weighted per component).  Writes coef_frac, bits, dist and cbf.
+__global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const int32_t *__restrict__ abs_sum,
+                                                 const uint32_t *__restrict__ sse, const uint32_t *__restrict__ zd,
+                                                 const uint32_t *__restrict__ csse) {
+  const int cuid = blockIdx.x * 64 + threadIdx.x;
+  if (cuid >= A.L.nctu * HVX_CUS_PER_CTU) return;
+  const int ctu = cuid / HVX_CUS_PER_CTU, ci = cuid % HVX_CUS_PER_CTU;
   const hvx_cu_result cu = A.cu[cuid];
   if (!cu.valid) return;
   int d, j, S, g;
   cu_geom(ci, d, j, S, g);
-  const int x = (ctu % A.L.nctu_x) * 64 + (j % g) * S, y = (ctu / A.L.nctu_x) * 64 + (j / g) * S;
-  const int T = S < 32 ? S : 32, ntu = (S / T) * (S / T), lane = lane_id(), ncomp = A.C.on ? 3 : 1;
+  const int T = S < 32 ? S : 32, ntu = (S / T) * (S / T), ncomp = A.C.on ? 3 : 1;
   const double lam = A.lambda;
   uint64_t tree = 0, cf = 0;
   uint32_t nz_dist = 0, zero_dist = 0;
   int cbf = 0;
   for (int t = 0; t < ntu; t++) {
     for (int comp = 0; comp < ncomp; comp++) {  // per TU Y, Cb, Cr (xEstimateInterResidualQT's component loop)
-      const int Tq = comp ? T / 2 : T;
       const int m_cbf = comp ? 33 + (S > 32 ? 1 : 0) : 28 + (S > 32 ? 0 : 1);
       const uint32_t c0 = (uint32_t)A.eb[A.st[m_cbf] ^ 0], c1 = (uint32_t)A.eb[A.st[m_cbf] ^ 1];
       const int tu = ctu_tu_index(A.L, ctu, d, j, t, comp);
-      const int64_t o = ctu_tu_offset(A.L, tu);
-      uint32_t part = 0;
-      for (int k = lane; k < Tq * Tq; k += HVX_WAVE) {
-        const int r = resid[o + k];
-        part += (uint32_t)(r * r);
-      }
-      const uint32_t zd = wave_sum_u32(part);
-      uint32_t td = comp ? dec_wdist(A.cw, zd) : zd;
+      uint32_t td = comp ? dec_wdist(A.cw, zd[tu]) : zd[tu];
       const uint64_t fr = A.cb[tu].frac_bits;
       uint64_t tf = c0;
       zero_dist += td;
@@ -411,69 +415,67 @@ __global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const uint8_t *__
   }
   const uint32_t r0 = (uint32_t)A.eb[A.st[41] ^ 0], r1 = (uint32_t)A.eb[A.st[41] ^ 1];
   if (dec_rd_cost(r0 >> 15, zero_dist, lam) < dec_rd_cost((uint32_t)(tree >> 15), nz_dist, lam)) cbf = 0;
-  uint32_t part = 0;
-  for (int k = lane; k < S * S; k += HVX_WAVE) {
-    const int yy = k / S, xx = k % S, t = (yy / T) * (S / T) + xx / T;
-    const int64_t o = ctu_tu_offset(A.L, ctu_tu_index(A.L, ctu, d, j, t)) + (yy % T) * T + (xx % T);
-    const int org = cur[(y + yy) * stride + x + xx];
-    int v = org - resid[o] + (((cbf >> t) & 1) ? res_out[o] : 0);
-    v = v < 0 ? 0 : v > 255 ? 255 : v;
-    part += (uint32_t)((org - v) * (org - v));
-  }
-  uint32_t dist = wave_sum_u32(part);
-  for (int comp = 1; comp < ncomp; comp++) {  // chroma: getDistPart per component over the CU, weighted
-    const int Sc = S / 2, Tc = T / 2;
-    uint32_t cpart = 0;
-    for (int k = lane; k < Sc * Sc; k += HVX_WAVE) {
-      const int yy = k / Sc, xx = k % Sc, t = (yy / Tc) * (Sc / Tc) + xx / Tc;
+  // the clipped reconstruction's distortion: coded TUs' csse, prediction-only TUs' zero-residual sum
+  uint32_t dist = 0;
+  for (int comp = 0; comp < ncomp; comp++) {
+    uint32_t cd = 0;
+    for (int t = 0; t < ntu; t++) {
       const int tu = ctu_tu_index(A.L, ctu, d, j, t, comp);
-      const int64_t o = ctu_tu_offset(A.L, tu) + (yy % Tc) * Tc + (xx % Tc);
-      const int64_t orr = ((cbf >> (8 + 4 * comp + t)) & 1) ? ctu_tu_offset(A.L, ctu_tu_ts(A.L, tu)) + yy * 4 + xx : o;
-      const int org = A.C.cur[comp - 1][(y / 2 + yy) * A.C.stride + x / 2 + xx];
-      int v = org - resid[o] + (((cbf >> (4 * comp + t)) & 1) ? res_out[orr] : 0);
-      v = v < 0 ? 0 : v > 255 ? 255 : v;
-      cpart += (uint32_t)((org - v) * (org - v));
+      const bool coded = (cbf >> (4 * comp + t)) & 1, ts = comp && ((cbf >> (8 + 4 * comp + t)) & 1);
+      cd += coded ? csse[ts ? ctu_tu_ts(A.L, tu) : tu] : zd[tu];
     }
-    dist += dec_wdist(A.cw, wave_sum_u32(cpart));
+    dist += comp ? dec_wdist(A.cw, cd) : cd;
   }
-  // HVX_RD_SSIM: D_ssim = sum over the CU's 8x8 blocks (raster order) of 1 - SSIM(org, rec), one
-  // block per lane with compute_SSIM's float operations in its order (stvssim.c:506-545)
+  hvx_cu_decision &r = A.dec[cuid];
+  r.coef_frac = cf;
+  r.cbf = cbf;
+  r.dist = dist;
+  r.bits = A.res[(size_t)cuid * A.L.nref + cu.ref].bits + (uint32_t)((cbf ? r1 + tree : r0) >> 15);
+  r.ssim_dist = 0.0f;
+}
+
+// HVX_RD_SSIM (after k_ctu_leaf): D_ssim = sum over the CU's luma 8x8 blocks (raster order) of
+// 1 - SSIM(org, rec), one block per lane with compute_SSIM's float operations in its order
+// (stvssim.c:506-545); one wave per CU.
+__global__ __launch_bounds__(64) void k_ctu_leaf_ssim(DecideArgs A, const uint8_t *__restrict__ cur, int stride,
+                                                      const int16_t *__restrict__ resid,
+                                                      const int16_t *__restrict__ res_out) {
+  const int cuid = blockIdx.x, ctu = cuid / HVX_CUS_PER_CTU, ci = cuid % HVX_CUS_PER_CTU;
+  const hvx_cu_result cu = A.cu[cuid];
+  if (!cu.valid) return;
+  int d, j, S, g;
+  cu_geom(ci, d, j, S, g);
+  const int x = (ctu % A.L.nctu_x) * 64 + (j % g) * S, y = (ctu / A.L.nctu_x) * 64 + (j / g) * S;
+  const int T = S < 32 ? S : 32, lane = lane_id();
+  const int cbf = A.dec[cuid].cbf;
   __shared__ float sdist[64];
-  float dsum = 0.0f;
-  if (A.metric == HVX_RD_SSIM) {
-    const int nb8 = S / 8;
-    if (lane < nb8 * nb8) {
-      const int by = lane / nb8, bx = lane - by * nb8;
-      const float C1 = 0.01f * 0.01f * (float)(255 * 255), C2 = 0.03f * 0.03f * (float)(255 * 255);
-      const float wgt = 1.0f / (float)(8 * 8);
-      float mo = 0, me = 0, vo = 0, ve = 0, cov = 0;
-      for (int n = 0; n < 8; n++)
-        for (int m = 0; m < 8; m++) {
-          const int yy = by * 8 + n, xx = bx * 8 + m, t = (yy / T) * (S / T) + xx / T;
-          const int64_t o = ctu_tu_offset(A.L, ctu_tu_index(A.L, ctu, d, j, t)) + (yy % T) * T + (xx % T);
-          const int po = cur[(y + yy) * stride + x + xx];
-          const int pe = clip_pel(po - resid[o] + (((cbf >> t) & 1) ? res_out[o] : 0));
-          mo += wgt * po; me += wgt * pe;
-          vo += wgt * po * po; ve += wgt * pe * pe; cov += wgt * po * pe;
-        }
-      const float varo = fabsf(vo - mo * mo), vare = fabsf(ve - me * me), covo = fabsf(cov - mo * me);
-      float sv = (float)((2.0 * mo * me + C1) * (2.0 * covo + C2));
-      sv /= (float)(mo * mo + me * me + C1) * (varo + vare + C2);
-      sv /= 1.0f;  // one window (compute_SSIM's dist /= cnt)
-      if (sv >= 1.0 && sv < 1.01) sv = 1.0f;
-      sdist[lane] = 1.0f - sv;
-    }
-    __syncthreads();
-    if (lane == 0)
-      for (int b = 0; b < nb8 * nb8; b++) dsum += sdist[b];
+  const int nb8 = S / 8;
+  if (lane < nb8 * nb8) {
+    const int by = lane / nb8, bx = lane - by * nb8;
+    const float C1 = 0.01f * 0.01f * (float)(255 * 255), C2 = 0.03f * 0.03f * (float)(255 * 255);
+    const float wgt = 1.0f / (float)(8 * 8);
+    float mo = 0, me = 0, vo = 0, ve = 0, cov = 0;
+    for (int n = 0; n < 8; n++)
+      for (int m = 0; m < 8; m++) {
+        const int yy = by * 8 + n, xx = bx * 8 + m, t = (yy / T) * (S / T) + xx / T;
+        const int64_t o = ctu_tu_offset(A.L, ctu_tu_index(A.L, ctu, d, j, t)) + (yy % T) * T + (xx % T);
+        const int po = cur[(y + yy) * stride + x + xx];
+        const int pe = clip_pel(po - resid[o] + (((cbf >> t) & 1) ? res_out[o] : 0));
+        mo += wgt * po; me += wgt * pe;
+        vo += wgt * po * po; ve += wgt * pe * pe; cov += wgt * po * pe;
+      }
+    const float varo = fabsf(vo - mo * mo), vare = fabsf(ve - me * me), covo = fabsf(cov - mo * me);
+    float sv = (float)((2.0 * mo * me + C1) * (2.0 * covo + C2));
+    sv /= (float)(mo * mo + me * me + C1) * (varo + vare + C2);
+    sv /= 1.0f;  // one window (compute_SSIM's dist /= cnt)
+    if (sv >= 1.0 && sv < 1.01) sv = 1.0f;
+    sdist[lane] = 1.0f - sv;
   }
+  __syncthreads();
   if (lane == 0) {
-    hvx_cu_decision &r = A.dec[cuid];
-    r.coef_frac = cf;
-    r.cbf = cbf;
-    r.dist = dist;
-    r.bits = A.res[(size_t)cuid * A.L.nref + cu.ref].bits + (uint32_t)((cbf ? r1 + tree : r0) >> 15);
-    r.ssim_dist = dsum;
+    float dsum = 0.0f;
+    for (int b = 0; b < nb8 * nb8; b++) dsum += sdist[b];
+    A.dec[cuid].ssim_dist = dsum;
   }
 }
 

@@ -74,7 +74,7 @@ size_t ctu_il_offc4(int n) { return ctu_il_offc8(n) + pad_g((size_t)32 * n) * 64
 size_t ctu_il_words(int n) { return ctu_il_offc4(n) + pad_g((size_t)256 * n) * 16; }  // 4x4 TUs + their TS twins
 struct CtuWs {
   size_t jobs, res, desc, off, est_idx, resid, lev, res_out, abs, sse, ptr, coefI, cxI, levI, stI, flags, cbits, bsv, bsh,
-      qpm, total;
+      qpm, pred, zd, csse, total;
 };
 CtuWs ctu_ws_layout(const CtuLayout &L) {
   CtuWs w;
@@ -102,6 +102,9 @@ CtuWs ctu_ws_layout(const CtuLayout &L) {
   w.bsv = o; o = align_up(o + nunit);
   w.bsh = o; o = align_up(o + nunit);
   w.qpm = o; o = align_up(o + nunit);
+  w.pred = o; o = align_up(o + nres);                     // 8-bit prediction, residual layout
+  w.zd = o; o = align_up(o + ntu * sizeof(uint32_t));     // per TU: zero-residual distortion
+  w.csse = o; o = align_up(o + ntu * sizeof(uint32_t));   // per TU: clipped-reconstruction distortion
   w.total = o;
   return w;
 }
@@ -225,7 +228,8 @@ static void tu_class_launch(hipStream_t st, const hvx_tu_desc *desc, const hvx_e
                             const int64_t *off, int n, const int16_t *res_in, int32_t *temp, int32_t *lev, int32_t *arl,
                             int32_t *abs_sum, int16_t *res_out, uint32_t *sse, uint32_t *coefI, uint32_t *cxI,
                             int32_t *levI, int32_t *stI, int8_t *flags, int G, int n_est_lds, hvx_ctx *tctx = nullptr,
-                            int phase0 = 0, hipEvent_t after_rdoq = nullptr) {
+                            int phase0 = 0, hipEvent_t after_rdoq = nullptr, const uint8_t *pred = nullptr,
+                            uint32_t *zd = nullptr, uint32_t *csse = nullptr) {
   int k = t_begin(tctx, st, phase0);
   hipLaunchKernelGGL((k_tu_fwd<L>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, temp, arl, coefI, cxI, levI, abs_sum, flags, G);
   t_end(tctx, st, k);
@@ -235,7 +239,8 @@ static void tu_class_launch(hipStream_t st, const hvx_tu_desc *desc, const hvx_e
   t_end(tctx, st, k);
   if (after_rdoq) (void)hipEventRecord(after_rdoq, st);  // the levels are final: their rate may be counted beside k_tu_fin
   k = t_begin(tctx, st, phase0 + 2);
-  hipLaunchKernelGGL((k_tu_fin<L, MODE>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, levI, lev, res_out, sse, G);
+  hipLaunchKernelGGL((k_tu_fin<L, MODE>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, levI, lev, res_out, sse, G,
+                     pred, zd, csse);
   t_end(tctx, st, k);
 }
 
@@ -717,6 +722,8 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   int16_t *res_out = (int16_t *)(ws + W.res_out);
   int32_t *abs_sum = (int32_t *)(ws + W.abs);
   uint32_t *sse = (uint32_t *)(ws + W.sse);
+  uint8_t *pred = (uint8_t *)(ws + W.pred);
+  uint32_t *zd = (uint32_t *)(ws + W.zd), *csse = (uint32_t *)(ws + W.csse);
   const uint8_t **cur_slot = (const uint8_t **)(ws + W.ptr);
   // Three streams, joined back into ctx->stream before the per-CU totals:
   //   A (ctx->stream): ME depth 0 -> 1 -> 2 -> 3 (depth d+1 starts from depth d's integer MVs),
@@ -733,8 +740,8 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   const bool fen = (P.me_flags & HVX_ME_FEN) != 0;
   const int n = L.nctu;
   auto resid_range = [&](hipStream_t s, int first, int ncu) {
-    hipLaunchKernelGGL(k_ctu_pred_resid, dim3(n * ncu), dim3(64), 0, s, L, P, d_cur, d_refs, stride, res, resid, desc, off,
-                       est_idx, d_out, first, ncu, C);
+    hipLaunchKernelGGL(k_ctu_pred_resid, dim3(n * ncu), dim3(64), 0, s, L, P, d_cur, d_refs, stride, res, resid, pred, desc,
+                       off, est_idx, d_out, first, ncu, C);
   };
   for (int d = 0; d < 4; d++) {
     const int ncu = 1 << (2 * d), nt = L.nctu * ncu * L.nref;
@@ -801,17 +808,17 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
       const size_t o = ctu_il_offc16(n);
       tu_class_launch<2, 2>(se, desc + 88 * n, d_est4, est_idx + 88 * n, off + 88 * n, 16 * n, resid, nullptr, lev,
                             nullptr, abs_sum + 88 * n, res_out, sse + 88 * n, coefI + o, cxI + o, levI + o, stI + o,
-                            flags + 88 * n, kCtuG, n_est, ctx, 9);
+                            flags + 88 * n, kCtuG, n_est, ctx, 9, nullptr, pred, zd + 88 * n, csse + 88 * n);
       count_class(se, 88 * n, 16 * n, o, 2);
     }
     tu_class_launch<3, 2>(sb, desc, d_est4, est_idx, off, 8 * n, resid, nullptr, lev, nullptr, abs_sum, res_out, sse,
-                          coefI, cxI, levI, stI, flags, g32, n_est, ctx, 6, cnt_states ? ctx->fj[5] : nullptr);
+                          coefI, cxI, levI, stI, flags, g32, n_est, ctx, 6, cnt_states ? ctx->fj[5] : nullptr, pred, zd,
+                          csse);
     if (cnt_states) {
       HVX_HIP(hipStreamWaitEvent(se, ctx->fj[5], 0));
       count_class(se, 0, 8 * n, 0, 3);
     }
     HVX_HIP(hipEventRecord(ctx->fj[6], se));
-    HVX_HIP(hipEventRecord(ctx->fj[3], sb));
   }
   {  // stream C
     HVX_HIP(hipStreamWaitEvent(sc, ctx->fj[2], 0));
@@ -821,34 +828,37 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     const size_t o = ctu_il_off16(n);
     tu_class_launch<2, 2>(sc, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n, 16 * n, resid, nullptr, lev, nullptr,
                           abs_sum + 8 * n, res_out, sse + 8 * n, coefI + o, cxI + o, levI + o, stI + o, flags + 8 * n, g16,
-                          n_est, ctx, 9);
+                          n_est, ctx, 9, nullptr, pred, zd + 8 * n, csse + 8 * n);
     count_class(sc, 8 * n, 16 * n, o, 2);
     if (C.on) {
       const size_t oc = ctu_il_offc8(n);
       tu_class_launch<1, 2>(sc, desc + 104 * n, d_est4, est_idx + 104 * n, off + 104 * n, 32 * n, resid, nullptr, lev,
                             nullptr, abs_sum + 104 * n, res_out, sse + 104 * n, coefI + oc, cxI + oc, levI + oc, stI + oc,
-                            flags + 104 * n, kCtuG, n_est, ctx, 12);
+                            flags + 104 * n, kCtuG, n_est, ctx, 12, nullptr, pred, zd + 104 * n, csse + 104 * n);
       count_class(sc, 104 * n, 32 * n, oc, 1);
     }
     HVX_HIP(hipEventRecord(ctx->fj[4], sc));
   }
-  {  // stream A: depth 3
+  {  // stream A: depth 3 (its 4x4 chroma TUs go to stream B, idle by then, beside the luma 8x8 pipeline)
     const int tk = t_begin(ctx, st, 5);
     resid_range(st, 21, 64);
     t_end(ctx, st, tk);
+    if (C.on) HVX_HIP(hipEventRecord(ctx->fj[0], st));
     const size_t o = ctu_il_off8(n);
     tu_class_launch<1, 2>(st, desc + 24 * n, d_est4, est_idx + 24 * n, off + 24 * n, 64 * n, resid, nullptr, lev, nullptr,
                           abs_sum + 24 * n, res_out, sse + 24 * n, coefI + o, cxI + o, levI + o, stI + o, flags + 24 * n, g8,
-                          n_est, ctx, 12);
+                          n_est, ctx, 12, nullptr, pred, zd + 24 * n, csse + 24 * n);
     count_class(st, 24 * n, 64 * n, o, 1);
-    if (C.on) {
-      const size_t oc = ctu_il_offc4(n);
-      tu_class_launch<0, 2>(st, desc + 136 * n, d_est4, est_idx + 136 * n, off + 136 * n, 256 * n, resid, nullptr, lev,
-                            nullptr, abs_sum + 136 * n, res_out, sse + 136 * n, coefI + oc, cxI + oc, levI + oc, stI + oc,
-                            flags + 136 * n, kCtuG, n_est, ctx, 12);
-      count_class(st, 136 * n, 256 * n, oc, 0);
-    }
   }
+  if (C.on) {  // stream B, after its 32x32 pipeline: the 4x4 chroma TUs of depth 3 (+ transform-skip twins)
+    HVX_HIP(hipStreamWaitEvent(sb, ctx->fj[0], 0));
+    const size_t oc = ctu_il_offc4(n);
+    tu_class_launch<0, 2>(sb, desc + 136 * n, d_est4, est_idx + 136 * n, off + 136 * n, 256 * n, resid, nullptr, lev,
+                          nullptr, abs_sum + 136 * n, res_out, sse + 136 * n, coefI + oc, cxI + oc, levI + oc, stI + oc,
+                          flags + 136 * n, kCtuG, n_est, ctx, 12, nullptr, pred, zd + 136 * n, csse + 136 * n);
+    count_class(sb, 136 * n, 256 * n, oc, 0);
+  }
+  HVX_HIP(hipEventRecord(ctx->fj[3], sb));
   HVX_HIP(hipStreamWaitEvent(st, ctx->fj[3], 0));
   HVX_HIP(hipStreamWaitEvent(st, ctx->fj[4], 0));
   HVX_HIP(hipStreamWaitEvent(st, ctx->fj[6], 0));
@@ -906,8 +916,11 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
   A.C = ctu_chroma(chroma); A.cw = P.chroma_weight;
   if (chroma && (!chroma->recon_cb || !chroma->recon_cr || (d_ref_pic && (!chroma->ref_pic_cb || !chroma->ref_pic_cr))))
     return fail(HVX_E_INVALID, "hvx_ctu_encode_yuv: NULL chroma reconstruction / reference plane");
-  hipLaunchKernelGGL(k_ctu_leaf, dim3(n * HVX_CUS_PER_CTU), dim3(64), 0, st, A, d_cur, stride, (const int16_t *)(ws + W.resid),
-                     (const int16_t *)(ws + W.res_out), (const int32_t *)(ws + W.abs), (const uint32_t *)(ws + W.sse));
+  hipLaunchKernelGGL(k_ctu_leaf, dim3((n * HVX_CUS_PER_CTU + 63) / 64), dim3(64), 0, st, A, (const int32_t *)(ws + W.abs),
+                     (const uint32_t *)(ws + W.sse), (const uint32_t *)(ws + W.zd), (const uint32_t *)(ws + W.csse));
+  if (P.rd_metric == HVX_RD_SSIM)
+    hipLaunchKernelGGL(k_ctu_leaf_ssim, dim3(n * HVX_CUS_PER_CTU), dim3(64), 0, st, A, d_cur, stride,
+                       (const int16_t *)(ws + W.resid), (const int16_t *)(ws + W.res_out));
   hipLaunchKernelGGL(k_ctu_decide, dim3((n + 63) / 64), dim3(64), 0, st, A);
   hipLaunchKernelGGL(k_ctu_recon, dim3(n), dim3(256), 0, st, L, P.pic_w, P.pic_h, d_cur, stride, (const hvx_cu_decision *)d_dec,
                      (const int16_t *)(ws + W.resid), (const int16_t *)(ws + W.res_out), d_recon, A.C);

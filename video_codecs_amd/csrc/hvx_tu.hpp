@@ -1263,12 +1263,17 @@ __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ 
   if (abs_out) abs_out[t] = a;
 }
 
-// Levels (scan order, interleaved) -> raster lev_io; MODE 2 also dequant + inverse + SSE.
+// Levels (scan order, interleaved) -> raster lev_io; MODE 2 also dequant + inverse + SSE.  With
+// zd_out: the zero-residual distortion sum(res_in^2); with pred (8-bit, residual layout) and
+// csse_out: the distortion of the clipped reconstruction, sum((pred + res_in - clip(pred + r))^2)
+// (TComYuv::addClip + getDistPart over the TU).
 template <int L, int MODE>
 __global__ __launch_bounds__(64) void k_tu_fin(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
                                                int n, const int16_t *__restrict__ res_in,
                                                const int32_t *__restrict__ levI, int32_t *__restrict__ lev_io,
-                                               int16_t *__restrict__ res_out, uint32_t *__restrict__ sse_out, int G) {
+                                               int16_t *__restrict__ res_out, uint32_t *__restrict__ sse_out, int G,
+                                               const uint8_t *__restrict__ pred, uint32_t *__restrict__ zd_out,
+                                               uint32_t *__restrict__ csse_out) {
   constexpr int N = 4 << L, NN = N * N;
   __shared__ TuSmem<L> s;
   const int t = blockIdx.x;
@@ -1284,14 +1289,28 @@ __global__ __launch_bounds__(64) void k_tu_fin(const hvx_tu_desc *__restrict__ d
   if (MODE == 2) {
     __syncthreads();
     tu_inverse<L>(s, d);
-    uint32_t part = 0;
+    uint32_t part = 0, pz = 0, pc = 0;
     for (int i = lane; i < NN; i += HVX_WAVE) {
       const int r = (int16_t)s.lev[i];
       res_out[off + i] = (int16_t)r;
-      const int df = (int)res_in[off + i] - r;
+      const int ri = res_in[off + i];
+      const int df = ri - r;
       part += (uint32_t)(df * df);
+      pz += (uint32_t)(ri * ri);
+      if (pred) {
+        const int p = pred[off + i], v = p + r, c = ri + p - (v < 0 ? 0 : v > 255 ? 255 : v);
+        pc += (uint32_t)(c * c);
+      }
     }
     const uint32_t sse = wave_sum_u32(part);
     if (lane == 0 && sse_out) sse_out[t] = sse;
+    if (zd_out) {
+      const uint32_t z = wave_sum_u32(pz);
+      if (lane == 0) zd_out[t] = z;
+    }
+    if (pred && csse_out) {
+      const uint32_t c = wave_sum_u32(pc);
+      if (lane == 0) csse_out[t] = c;
+    }
   }
 }
