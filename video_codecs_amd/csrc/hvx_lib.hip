@@ -231,7 +231,14 @@ static void tu_class_launch(hipStream_t st, const hvx_tu_desc *desc, const hvx_e
                             int phase0 = 0, hipEvent_t after_rdoq = nullptr, const uint8_t *pred = nullptr,
                             uint32_t *zd = nullptr, uint32_t *csse = nullptr) {
   int k = t_begin(tctx, st, phase0);
-  hipLaunchKernelGGL((k_tu_fwd<L>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, temp, arl, coefI, cxI, levI, abs_sum, flags, G);
+  // the CTU pass's 4x4 / 8x8 TUs (RDOQ, inter: pred != nullptr marks that pass): one TU per lane
+  const bool lane = L <= 1 && pred && G == 64 && !temp && !arl;
+  if (lane)
+    hipLaunchKernelGGL((k_tu_fwd_lane<L < 2 ? L : 1>), dim3((n + 63) / 64), dim3(64), 0, st, desc, off, n, res_in, coefI,
+                       cxI, flags);
+  else
+    hipLaunchKernelGGL((k_tu_fwd<L>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, temp, arl, coefI, cxI, levI, abs_sum,
+                       flags, G);
   t_end(tctx, st, k);
   k = t_begin(tctx, st, phase0 + 1);
   hipLaunchKernelGGL((k_tu_rdoq<L>), dim3((n + G - 1) / G), dim3(64), 0, st, desc, est, est_idx, n, coefI, cxI, levI, stI,
@@ -239,8 +246,12 @@ static void tu_class_launch(hipStream_t st, const hvx_tu_desc *desc, const hvx_e
   t_end(tctx, st, k);
   if (after_rdoq) (void)hipEventRecord(after_rdoq, st);  // the levels are final: their rate may be counted beside k_tu_fin
   k = t_begin(tctx, st, phase0 + 2);
-  hipLaunchKernelGGL((k_tu_fin<L, MODE>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, levI, lev, res_out, sse, G,
-                     pred, zd, csse);
+  if (lane && MODE == 2)
+    hipLaunchKernelGGL((k_tu_fin_lane<L < 2 ? L : 1>), dim3((n + 63) / 64), dim3(64), 0, st, desc, off, n, res_in, levI,
+                       lev, res_out, sse, pred, zd, csse);
+  else
+    hipLaunchKernelGGL((k_tu_fin<L, MODE>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, levI, lev, res_out, sse, G,
+                       pred, zd, csse);
   t_end(tctx, st, k);
 }
 
