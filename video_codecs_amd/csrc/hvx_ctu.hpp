@@ -2,7 +2,7 @@
 // DESIGN.md).  All CTUs of a picture are independent here (no neighbour-dependent
 // predictors), so the pass is a fixed sequence of wide launches:
 //   for depth 0..3: k_ctu_me_jobs (one thread per CU x reference) -> k_me
-//   k_ctu_pred_resid (one wave per CU: best reference, luma MC, residual, TU descriptors)
+//   k_ctu_pred_resid<S> (one wave per CU: best reference, separable luma/chroma MC over LDS, residual, TU descriptors)
 //   k_tu<L,pipeline> per TU size class over contiguous class ranges
 //   k_ctu_finalize (per-CU sums)
 // The composition is restated on the CPU by hvxo_ctu_analyze (oracle/hvx_oracle.c).
@@ -131,23 +131,32 @@ __global__ __launch_bounds__(256) void k_ctu_me_jobs(CtuLayout L, hvx_ctu_params
   jobs[((size_t)ctu * HVX_CUS_PER_CTU + ci) * L.nref + ref] = jb;
 }
 
-// one wave per CU: best reference, luma MC (standard two-stage quarter-pel), residual into the
-// TU-class layout, TU descriptors (hvxo_ctu_tu_desc semantics).
+// one wave per CU of size S: best reference, luma MC (standard two-stage quarter-pel), residual
+// into the TU-class layout, TU descriptors (hvxo_ctu_tu_desc semantics).  The MC is separable
+// over LDS: the (S+7)^2 reference window is staged once, the first (horizontal) stage is
+// computed once per row of the window, the second stage reads it (the same int16 intermediate,
+// -8192 offset, as TComInterpolationFilter's two-stage path, .cpp:94-257); chroma likewise with
+// the 4-tap filters.  Descriptors are built one per lane and stored as 16-byte vectors.
+template <int S>
 __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_params P, const uint8_t *__restrict__ cur,
                                                        const uint8_t *const *__restrict__ refs, int stride,
                                                        const hvx_me_result *__restrict__ res, int16_t *__restrict__ resid,
                                                        uint8_t *__restrict__ pred_out,
                                                        hvx_tu_desc *__restrict__ descs, int64_t *__restrict__ offs,
                                                        int32_t *__restrict__ est_idx, hvx_cu_result *__restrict__ out,
-                                                       int first, int ncu, CtuChroma C) {
-  // blocks cover CUs [first, first + ncu) of every CTU (one depth range per launch)
-  const int ctu = blockIdx.x / ncu, ci = first + (int)(blockIdx.x % ncu);
-  const int cuid = ctu * HVX_CUS_PER_CTU + ci;
-  int d, j, S, g;
-  cu_geom(ci, d, j, S, g);
+                                                       CtuChroma C) {
+  constexpr int d = S == 64 ? 0 : S == 32 ? 1 : S == 16 ? 2 : 3, g = 1 << d, ncu = g * g;
+  constexpr int T = S < 32 ? S : 32, log2 = T == 8 ? 3 : T == 16 ? 4 : 5, ntu = (S / T) * (S / T);
+  constexpr int WP = S + 8, WR = S + 7;                    // luma window pitch / rows
+  constexpr int Sc = S / 2, Tc = T / 2, CWP = Sc + 4, CWR = Sc + 3;
+  static_assert(2 * CWR * CWP <= WR * WP && 2 * CWR * Sc <= WR * S, "chroma windows fit the luma buffers");
+  __shared__ uint8_t win[WR * WP];
+  __shared__ int16_t hs[WR * S];
+  const int lane = lane_id();
+  const int ctu = blockIdx.x / ncu, j = (int)(blockIdx.x % ncu);
+  const int cuid = ctu * HVX_CUS_PER_CTU + depth_base(d) + j;
   const int x = (ctu % L.nctu_x) * 64 + (j % g) * S, y = (ctu / L.nctu_x) * 64 + (j / g) * S;
   const bool valid = x + S <= P.pic_w && y + S <= P.pic_h;
-  const int T = S < 32 ? S : 32, log2 = T == 8 ? 3 : T == 16 ? 4 : 5, ntu = (S / T) * (S / T);
   int best = 0;
   uint32_t best_cost = 0;
   const hvx_me_result *r = res + (size_t)cuid * L.nref;
@@ -155,78 +164,145 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
     for (int k = 0; k < L.nref; k++)
       if (k == 0 || r[k].cost < best_cost) { best_cost = r[k].cost; best = k; }
   }
-  if (lane_id() == 0) {
+  if (lane == 0) {
     hvx_cu_result o;
     o.valid = valid; o.ref = valid ? best : 0;
     o.mv_x = valid ? r[best].mv_x : 0; o.mv_y = valid ? r[best].mv_y : 0;
     o.me_cost = valid ? best_cost : 0; o.sse = 0; o.abs_sum = 0; o.n_tu = valid ? ntu : 0;
     out[cuid] = o;
   }
-  for (int t = lane_id(); t < ntu; t += HVX_WAVE) {
-    const int tu = ctu_tu_index(L, ctu, d, j, t);
+  // descriptors: per luma TU position the luma TU, then (4:2:0) Cb, Cr and, at depth 3, the
+  // transform-skip twins of the 4x4 Cb / Cr TUs (xEstimateInterResidualQT's second mode)
+  const int nper = C.on ? (d == 3 ? 5 : 3) : 1;
+  for (int k = lane; k < ntu * nper; k += HVX_WAVE) {
+    const int t = k / nper, kind = k % nper, c = kind == 0 ? 0 : 1 + (kind - 1) % 2;
     hvx_tu_desc td;
     memset(&td, 0, sizeof(td));
-    td.width = td.height = valid ? T : 0;  // width 0: no size class picks it up
-    td.log2_size = log2;
-    td.tr_idx = S > 32 ? 1 : 0;
     td.slice_type = P.slice_type;
-    td.qp_per = P.qp / 6; td.qp_rem = P.qp % 6;
     td.sign_hiding = 1; td.use_rdoq = 1; td.use_rdoq_ts = 1;
     td.pps_tskip = 1;  // TransformSkip=1: 4x4 TUs code transform_skip_flag
     td.max_log2_tr_range = 15; td.bit_depth = 8;
-    td.lambda = P.lambda;
-    descs[tu] = td;
-    offs[tu] = ctu_tu_offset(L, tu);
-    est_idx[tu] = log2 - 2;
-    if (C.on) {  // the Cb / Cr TUs: half size, chroma QP and RDOQ lambda, chroma cbf context = transform depth
-      for (int c = 1; c <= 2; c++) {
-        const int tc = ctu_tu_index(L, ctu, d, j, t, c);
-        hvx_tu_desc dc = td;
-        dc.comp = c;
-        dc.width = dc.height = valid ? T / 2 : 0;
-        dc.log2_size = log2 - 1;
-        dc.ctx_qt_cbf = S > 32 ? 1 : 0;
-        dc.qp_per = P.qp_chroma / 6; dc.qp_rem = P.qp_chroma % 6;
-        dc.lambda = P.lambda_chroma;
-        descs[tc] = dc;
-        offs[tc] = ctu_tu_offset(L, tc);
-        est_idx[tc] = 4 + log2 - 3;
-        if (d == 3) {  // the 4x4 TU's transform-skip mode (xEstimateInterResidualQT's second mode)
-          const int tt = ctu_tu_ts(L, tc);
-          dc.transform_skip = 1;
-          descs[tt] = dc;
-          offs[tt] = ctu_tu_offset(L, tt);
-          est_idx[tt] = 4;
-        }
-      }
+    td.tr_idx = S > 32 ? 1 : 0;
+    int tu, ei;
+    if (c == 0) {
+      tu = ctu_tu_index(L, ctu, d, j, t);
+      td.width = td.height = valid ? T : 0;  // width 0: no size class picks it up
+      td.log2_size = log2;
+      td.qp_per = P.qp / 6; td.qp_rem = P.qp % 6;
+      td.lambda = P.lambda;
+      ei = log2 - 2;
+    } else {  // half size, chroma QP and RDOQ lambda, chroma cbf context = transform depth
+      tu = ctu_tu_index(L, ctu, d, j, t, c);
+      td.comp = c;
+      td.width = td.height = valid ? Tc : 0;
+      td.log2_size = log2 - 1;
+      td.ctx_qt_cbf = S > 32 ? 1 : 0;
+      td.qp_per = P.qp_chroma / 6; td.qp_rem = P.qp_chroma % 6;
+      td.lambda = P.lambda_chroma;
+      ei = 4 + log2 - 3;
+      if (kind >= 3) { tu = ctu_tu_ts(L, tu); td.transform_skip = 1; ei = 4; }
     }
+    static_assert(sizeof(hvx_tu_desc) % 16 == 0, "descriptor stored as 16-byte vectors");
+    const uint4 *src = reinterpret_cast<const uint4 *>(&td);
+    uint4 *dst = reinterpret_cast<uint4 *>(descs + tu);
+#pragma unroll
+    for (int q = 0; q < (int)(sizeof(hvx_tu_desc) / 16); q++) dst[q] = src[q];
+    offs[tu] = ctu_tu_offset(L, tu);
+    est_idx[tu] = ei;
   }
   if (!valid) return;
-  const uint8_t *rp = refs[best];
   const int mvx = r[best].mv_x, mvy = r[best].mv_y;
-  for (int k = lane_id(); k < S * S; k += HVX_WAVE) {
-    const int yy = k / S, xx = k % S;
-    const int pred = me_qpel_sample(rp + y * stride + x, stride, xx, yy, mvx, mvy);
-    const int t = (yy / T) * (S / T) + (xx / T);
-    const int tu = ctu_tu_index(L, ctu, d, j, t);
-    const int64_t o = ctu_tu_offset(L, tu) + (yy % T) * T + (xx % T);
-    resid[o] = (int16_t)((int)cur[(y + yy) * stride + x + xx] - pred);
-    pred_out[o] = (uint8_t)pred;
+  {  // luma
+    const int fx = mvx & 3, fy = mvy & 3;
+    const uint8_t *rp = refs[best] + (y + (mvy >> 2) - 3) * stride + x + (mvx >> 2) - 3;
+    for (int k = lane; k < WR * WR; k += HVX_WAVE) {
+      const int rr = k / WR, cc = k % WR;
+      win[rr * WP + cc] = rp[rr * stride + cc];
+    }
+    __syncthreads();
+    if (fx) {
+      const int r0 = fy ? 0 : 3, nr = fy ? WR : S;
+      for (int k = lane; k < nr * S; k += HVX_WAVE) {
+        const int rr = r0 + k / S, cc = k % S;
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) s += kLumaFilter[fx][i] * win[rr * WP + cc + i];
+        hs[rr * S + cc] = (int16_t)(s - 8192);
+      }
+      __syncthreads();
+    }
+    for (int k = lane; k < S * S; k += HVX_WAVE) {
+      const int yy = k / S, xx = k % S;
+      int pred;
+      if (!fy) {
+        pred = fx ? clip_pel((hs[(yy + 3) * S + xx] + 8192 + 32) >> 6) : win[(yy + 3) * WP + xx + 3];
+      } else if (!fx) {
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) s += kLumaFilter[fy][i] * win[(yy + i) * WP + xx + 3];
+        pred = clip_pel((s + 32) >> 6);
+      } else {
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) s += kLumaFilter[fy][i] * hs[(yy + i) * S + xx];
+        pred = clip_pel((s + (1 << 11) + (8192 << 6)) >> 12);
+      }
+      const int t = (yy / T) * (S / T) + (xx / T);
+      const int tu = ctu_tu_index(L, ctu, d, j, t);
+      const int64_t o = ctu_tu_offset(L, tu) + (yy % T) * T + (xx % T);
+      resid[o] = (int16_t)((int)cur[(y + yy) * stride + x + xx] - pred);
+      pred_out[o] = (uint8_t)pred;
+    }
   }
-  if (C.on) {
-    const int Sc = S / 2, Tc = T / 2, xc = x / 2, yc = y / 2;
-    for (int k = lane_id(); k < 2 * Sc * Sc; k += HVX_WAVE) {
-      const int c = k < Sc * Sc ? 1 : 2, kk = k - (c - 1) * Sc * Sc, yy = kk / Sc, xx = kk % Sc;
-      const int pred = ctu_epel_sample(C.refs[(c - 1) * L.nref + best] + yc * C.stride + xc, C.stride, xx, yy, mvx, mvy);
+  if (!C.on) return;
+  __syncthreads();  // the luma stages are done with win / hs
+  {  // Cb and Cr together: window c at win + (c-1)*CWR*CWP, first stage at hs + (c-1)*CWR*Sc
+    const int fx = mvx & 7, fy = mvy & 7, xc = x / 2, yc = y / 2;
+    const int wo = (yc + (mvy >> 3) - 1) * C.stride + xc + (mvx >> 3) - 1;
+    for (int k = lane; k < 2 * CWR * CWR; k += HVX_WAVE) {
+      const int c = k / (CWR * CWR), kk = k % (CWR * CWR), rr = kk / CWR, cc = kk % CWR;
+      win[c * CWR * CWP + rr * CWP + cc] = C.refs[c * L.nref + best][wo + rr * C.stride + cc];
+    }
+    __syncthreads();
+    if (fx) {
+      const int r0 = fy ? 0 : 1, nr = fy ? CWR : Sc;
+      for (int k = lane; k < 2 * nr * Sc; k += HVX_WAVE) {
+        const int c = k / (nr * Sc), kk = k % (nr * Sc), rr = r0 + kk / Sc, cc = kk % Sc;
+        const uint8_t *w = win + c * CWR * CWP + rr * CWP + cc;
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) s += kChromaFilter[fx][i] * w[i];
+        hs[c * CWR * Sc + rr * Sc + cc] = (int16_t)(s - 8192);
+      }
+      __syncthreads();
+    }
+    for (int k = lane; k < 2 * Sc * Sc; k += HVX_WAVE) {
+      const int c = k / (Sc * Sc), kk = k % (Sc * Sc), yy = kk / Sc, xx = kk % Sc;
+      const uint8_t *w = win + c * CWR * CWP;
+      const int16_t *h = hs + c * CWR * Sc;
+      int pred;
+      if (!fy) {
+        pred = fx ? clip_pel((h[(yy + 1) * Sc + xx] + 8192 + 32) >> 6) : w[(yy + 1) * CWP + xx + 1];
+      } else if (!fx) {
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) s += kChromaFilter[fy][i] * w[(yy + i) * CWP + xx + 1];
+        pred = clip_pel((s + 32) >> 6);
+      } else {
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) s += kChromaFilter[fy][i] * h[(yy + i) * Sc + xx];
+        pred = clip_pel((s + (1 << 11) + (8192 << 6)) >> 12);
+      }
       const int t = (yy / Tc) * (Sc / Tc) + (xx / Tc);
-      const int tu = ctu_tu_index(L, ctu, d, j, t, c);
-      const int16_t r = (int16_t)((int)C.cur[c - 1][(yc + yy) * C.stride + xc + xx] - pred);
+      const int tu = ctu_tu_index(L, ctu, d, j, t, c + 1);
+      const int16_t rv = (int16_t)((int)C.cur[c][(yc + yy) * C.stride + xc + xx] - pred);
       const int64_t o = ctu_tu_offset(L, tu) + (yy % Tc) * Tc + (xx % Tc);
-      resid[o] = r;
+      resid[o] = rv;
       pred_out[o] = (uint8_t)pred;
       if (d == 3) {
         const int64_t ot = ctu_tu_offset(L, ctu_tu_ts(L, tu)) + yy * 4 + xx;
-        resid[ot] = r;
+        resid[ot] = rv;
         pred_out[ot] = (uint8_t)pred;
       }
     }
@@ -518,7 +594,9 @@ __global__ __launch_bounds__(64) void k_ctu_decide(DecideArgs A) {
 __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int pic_h, const uint8_t *__restrict__ cur,
                                                    int stride, const hvx_cu_decision *__restrict__ dec,
                                                    const int16_t *__restrict__ resid, const int16_t *__restrict__ res_out,
-                                                   uint8_t *__restrict__ recon, CtuChroma C) {
+                                                   uint8_t *__restrict__ recon, CtuChroma C, uint8_t *__restrict__ rp_y,
+                                                   uint8_t *__restrict__ rp_cb, uint8_t *__restrict__ rp_cr) {
+  // rp_*: the reference picture's planes (nullable), written with the same samples before deblocking
   const int ctu = blockIdx.x;
   const int x0 = (ctu % L.nctu_x) * 64, y0 = (ctu / L.nctu_x) * 64;
   const hvx_cu_decision *dc = dec + (size_t)ctu * HVX_CUS_PER_CTU;
@@ -536,7 +614,9 @@ __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int p
     const int tu = ctu_tu_index(L, ctu, d, j, t);
     const int64_t o = ctu_tu_offset(L, tu) + (cy % T) * T + (cx % T);
     const int v = (int)cur[y * stride + x] - resid[o] + (((dc[depth_base(d) + j].cbf >> t) & 1) ? res_out[o] : 0);
-    recon[y * stride + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+    const uint8_t rv = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+    recon[y * stride + x] = rv;
+    if (rp_y) rp_y[y * stride + x] = rv;
   }
   if (!C.on) return;
   for (int k = threadIdx.x; k < 2 * 32 * 32; k += 256) {  // Cb then Cr, 32x32 chroma samples per CTU
@@ -554,7 +634,10 @@ __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int p
     const int64_t o = ctu_tu_offset(L, tu) + (cy % Tc) * Tc + (cx % Tc);
     const int64_t orr = ((cbf >> (8 + 4 * c + t)) & 1) ? ctu_tu_offset(L, ctu_tu_ts(L, tu)) + cy * 4 + cx : o;
     const int v = (int)C.cur[c - 1][y * C.stride + x] - resid[o] + (((cbf >> (4 * c + t)) & 1) ? res_out[orr] : 0);
-    C.recon[c - 1][y * C.stride + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+    const uint8_t rv = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+    C.recon[c - 1][y * C.stride + x] = rv;
+    uint8_t *rp = c == 1 ? rp_cb : rp_cr;
+    if (rp) rp[y * C.stride + x] = rv;
   }
 }
 

@@ -104,3 +104,31 @@ __global__ __launch_bounds__(256) void k_plane_extend(uint8_t *__restrict__ plan
     else plane[(h + y - margin) * stride + cx] = plane[(h - 1) * stride + cx];
   }
 }
+
+// extendPicBorder of up to three planes in one launch (blockIdx.y = plane): every margin sample
+// takes the picture sample at the clamped position, which is what the two passes above (left /
+// right columns, then whole top / bottom rows) produce
+struct PlaneSet {
+  uint8_t *p[3];
+  int s[3], w[3], h[3], m[3];
+};
+__global__ __launch_bounds__(256) void k_planes_extend(PlaneSet E) {
+  const int pi = blockIdx.y;
+  uint8_t *pl = E.p[pi];
+  const int s = E.s[pi], w = E.w[pi], h = E.h[pi], m = E.m[pi];
+  const int k = blockIdx.x * blockDim.x + threadIdx.x, nside = 2 * m * h, nrow = w + 2 * m;
+  int x, y;
+  if (k < nside) {
+    const int c = k % (2 * m);
+    y = k / (2 * m);
+    x = c < m ? c - m : w + c - m;
+  } else if (k < nside + 2 * m * nrow) {
+    const int k2 = k - nside, rr = k2 / nrow;
+    y = rr < m ? rr - m : h + rr - m;
+    x = k2 % nrow - m;
+  } else {
+    return;
+  }
+  const int cy = y < 0 ? 0 : y >= h ? h - 1 : y, cx = x < 0 ? 0 : x >= w ? w - 1 : x;
+  pl[(int64_t)y * s + x] = pl[(int64_t)cy * s + cx];
+}

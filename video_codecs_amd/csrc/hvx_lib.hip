@@ -750,9 +750,12 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
   const bool fen = (P.me_flags & HVX_ME_FEN) != 0;
   const int n = L.nctu;
-  auto resid_range = [&](hipStream_t s, int first, int ncu) {
-    hipLaunchKernelGGL(k_ctu_pred_resid, dim3(n * ncu), dim3(64), 0, s, L, P, d_cur, d_refs, stride, res, resid, pred, desc,
-                       off, est_idx, d_out, first, ncu, C);
+  auto resid_depth = [&](hipStream_t s, int d) {
+    const dim3 grid(n << (2 * d)), blk(64);
+    if (d == 0) hipLaunchKernelGGL(k_ctu_pred_resid<64>, grid, blk, 0, s, L, P, d_cur, d_refs, stride, res, resid, pred, desc, off, est_idx, d_out, C);
+    if (d == 1) hipLaunchKernelGGL(k_ctu_pred_resid<32>, grid, blk, 0, s, L, P, d_cur, d_refs, stride, res, resid, pred, desc, off, est_idx, d_out, C);
+    if (d == 2) hipLaunchKernelGGL(k_ctu_pred_resid<16>, grid, blk, 0, s, L, P, d_cur, d_refs, stride, res, resid, pred, desc, off, est_idx, d_out, C);
+    if (d == 3) hipLaunchKernelGGL(k_ctu_pred_resid<8>, grid, blk, 0, s, L, P, d_cur, d_refs, stride, res, resid, pred, desc, off, est_idx, d_out, C);
   };
   for (int d = 0; d < 4; d++) {
     const int ncu = 1 << (2 * d), nt = L.nctu * ncu * L.nref;
@@ -811,7 +814,8 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   {  // stream B; with counting (hvx_ctu_encode) the 32x32 class's rate runs on stream E beside k_tu_fin
     HVX_HIP(hipStreamWaitEvent(sb, ctx->fj[1], 0));
     const int tk = t_begin(ctx, sb, 5);
-    resid_range(sb, 0, 5);
+    resid_depth(sb, 0);
+    resid_depth(sb, 1);
     t_end(ctx, sb, tk);
     if (C.on) {  // the chroma 16x16 TUs of these CUs on stream E, beside the luma 32x32 pipeline
       HVX_HIP(hipEventRecord(ctx->fj[7], sb));
@@ -834,7 +838,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   {  // stream C
     HVX_HIP(hipStreamWaitEvent(sc, ctx->fj[2], 0));
     const int tk = t_begin(ctx, sc, 5);
-    resid_range(sc, 5, 16);
+    resid_depth(sc, 2);
     t_end(ctx, sc, tk);
     const size_t o = ctu_il_off16(n);
     tu_class_launch<2, 2>(sc, desc + 8 * n, d_est4, est_idx + 8 * n, off + 8 * n, 16 * n, resid, nullptr, lev, nullptr,
@@ -852,7 +856,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   }
   {  // stream A: depth 3 (its 4x4 chroma TUs go to stream B, idle by then, beside the luma 8x8 pipeline)
     const int tk = t_begin(ctx, st, 5);
-    resid_range(st, 21, 64);
+    resid_depth(st, 3);
     t_end(ctx, st, tk);
     if (C.on) HVX_HIP(hipEventRecord(ctx->fj[0], st));
     const size_t o = ctu_il_off8(n);
@@ -933,19 +937,22 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
     hipLaunchKernelGGL(k_ctu_leaf_ssim, dim3(n * HVX_CUS_PER_CTU), dim3(64), 0, st, A, d_cur, stride,
                        (const int16_t *)(ws + W.resid), (const int16_t *)(ws + W.res_out));
   hipLaunchKernelGGL(k_ctu_decide, dim3((n + 63) / 64), dim3(64), 0, st, A);
+  // the reference picture (if asked for) gets the reconstructed samples in the same pass; its
+  // margins are extended after deblocking
+  uint8_t *rp_y = d_ref_pic != d_recon ? d_ref_pic : nullptr;
+  uint8_t *rp_cb = chroma && d_ref_pic && chroma->ref_pic_cb != chroma->recon_cb ? chroma->ref_pic_cb : nullptr;
+  uint8_t *rp_cr = chroma && d_ref_pic && chroma->ref_pic_cr != chroma->recon_cr ? chroma->ref_pic_cr : nullptr;
   hipLaunchKernelGGL(k_ctu_recon, dim3(n), dim3(256), 0, st, L, P.pic_w, P.pic_h, d_cur, stride, (const hvx_cu_decision *)d_dec,
-                     (const int16_t *)(ws + W.resid), (const int16_t *)(ws + W.res_out), d_recon, A.C);
+                     (const int16_t *)(ws + W.resid), (const int16_t *)(ws + W.res_out), d_recon, A.C, rp_y, rp_cb, rp_cr);
   const int M = HVX_PLANE_MARGIN, Mc = M / 2, cw = P.pic_w / 2, ch = P.pic_h / 2;
-  // extendPicBorder of a plane (margin m): left/right columns, then the top/bottom rows
-  auto extend = [&](uint8_t *pl, int s, int w, int h, int m) {
-    hipLaunchKernelGGL(k_plane_extend, dim3((2 * m + 255) / 256, h), dim3(256), 0, st, pl, s, w, h, m, 0);
-    hipLaunchKernelGGL(k_plane_extend, dim3((w + 2 * m + 255) / 256, 2 * m), dim3(256), 0, st, pl, s, w, h, m, 1);
+  // extendPicBorder of Y (and Cb, Cr): one launch
+  auto extend = [&](uint8_t *y, uint8_t *cb, uint8_t *cr) {
+    PlaneSet E = {{y, cb, cr}, {stride, chroma ? chroma->c_stride : 0, chroma ? chroma->c_stride : 0},
+                  {P.pic_w, cw, cw}, {P.pic_h, ch, ch}, {M, Mc, Mc}};
+    const int np = chroma ? 3 : 1, nm = 2 * M * P.pic_h + 2 * M * (P.pic_w + 2 * M);
+    hipLaunchKernelGGL(k_planes_extend, dim3((nm + 255) / 256, np), dim3(256), 0, st, E);
   };
-  extend(d_recon, stride, P.pic_w, P.pic_h, M);
-  if (chroma) {
-    extend(chroma->recon_cb, chroma->c_stride, cw, ch, Mc);
-    extend(chroma->recon_cr, chroma->c_stride, cw, ch, Mc);
-  }
+  extend(d_recon, chroma ? chroma->recon_cb : nullptr, chroma ? chroma->recon_cr : nullptr);
   t_end(ctx, st, tk);
   if (d_ref_pic) {
     // 4. the reference picture: the reconstruction deblocked (boundary strengths of the decided
@@ -956,16 +963,6 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
     int8_t *qpm = (int8_t *)(ws + W.qpm);
     hipLaunchKernelGGL(k_ctu_bs, dim3((nunit + 255) / 256), dim3(256), 0, st, d_cu, (const hvx_cu_decision *)d_dec,
                        P.pic_w, P.pic_h, P.qp, bsv, bsh, qpm);
-    auto copy_plane = [&](uint8_t *dst, const uint8_t *src, int s, int h, int m) -> int {
-      if (dst != src)
-        HVX_HIP(hipMemcpyAsync(dst - (int64_t)m * s - m, src - (int64_t)m * s - m, (size_t)s * (h + 2 * m),
-                               hipMemcpyDeviceToDevice, st));
-      return HVX_OK;
-    };
-    int rc = copy_plane(d_ref_pic, d_recon, stride, P.pic_h, M);
-    if (!rc && chroma) rc = copy_plane(chroma->ref_pic_cb, chroma->recon_cb, chroma->c_stride, ch, Mc);
-    if (!rc && chroma) rc = copy_plane(chroma->ref_pic_cr, chroma->recon_cr, chroma->c_stride, ch, Mc);
-    if (rc) return rc;
     hvx_deblock_params dp = {};
     dp.pic_w = P.pic_w; dp.pic_h = P.pic_h;
     // loopFilterPic: luma, and at 4:2:0 the chroma edges (filtered only where bs == 2, i.e. never
@@ -979,11 +976,7 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
     if (nh > 0)
       hipLaunchKernelGGL(k_deblock<1>, dim3((nh + 255) / 256), dim3(256), 0, st, d_ref_pic, stride, dcb, dcr, dcs, bsh, qpm,
                          dp);
-    extend(d_ref_pic, stride, P.pic_w, P.pic_h, M);
-    if (chroma) {
-      extend(chroma->ref_pic_cb, chroma->c_stride, cw, ch, Mc);
-      extend(chroma->ref_pic_cr, chroma->c_stride, cw, ch, Mc);
-    }
+    extend(d_ref_pic, chroma ? chroma->ref_pic_cb : nullptr, chroma ? chroma->ref_pic_cr : nullptr);
     t_end(ctx, st, tk);
   }
   return launched("hvx_ctu_decide");
