@@ -121,7 +121,7 @@ typedef struct hvx_ctu_params {
   int32_t search_range;      /* 64 */
   int32_t me_flags;          /* HVX_ME_* */
   int32_t slice_type;        /* HM SliceType (1 = P) */
-  uint32_t lambda_motion;    /* floor(65536*sqrt(lambda)); < 2^24 (sqrt(lambda) < 256, any 8-bit QP) */
+  uint32_t lambda_motion;    /* floor(65536*sqrt(lambda)) */
   double lambda;             /* RD lambda (TComTrQuant m_dLambda for luma) */
   double lambda_ssim;        /* HVX_RD_SSIM: the SSIM-RDO lambda (stvssim.c lambda_2 :1805 x attention eta^0.85) */
   int32_t rd_metric;         /* hvx_ctu_decide's CU-level distortion: HVX_RD_SSE (HM) or HVX_RD_SSIM */

@@ -316,17 +316,15 @@ int hvx_create(int device, hvx_ctx **out) {
   if (rc) return rc;
   hvx_ctx *c = new hvx_ctx;
   c->device = device;
-  // the side streams carry few, latency-bound workgroups (RDOQ chains): highest priority, so
-  // they dispatch ahead of the ME kernels' backlog instead of waiting behind it
-  int prio_lo = 0, prio_hi = 0;
-  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = prio_lo = 0;
   hipError_t e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
   if (e != hipSuccess) { delete c; return hip_fail(e, "hipStreamCreate"); }
   c->stream = c->own;
   const char *ser = getenv("HVX_SERIAL_STREAMS");
   c->serial = ser && ser[0] == '1';
-  // (measured, 2160p YUV step: side streams at normal priority 8.35-8.56 ms, at low 8.9 ms, the
-  // main stream at low priority with the sides high or normal 7.72-7.88 ms, against 7.70-7.74)
+  // the side streams carry few, latency-bound workgroups (RDOQ chains): highest priority, so
+  // they dispatch ahead of the ME kernels' backlog instead of waiting behind it
+  int prio_lo = 0, prio_hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
   for (int i = 0; i < 3 && e == hipSuccess; i++) e = hipStreamCreateWithPriority(&c->aux[i], hipStreamNonBlocking, prio_hi);
   for (int i = 0; i < 8 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&c->fj[i], hipEventDisableTiming);
   if (e != hipSuccess) { hvx_destroy(c); return hip_fail(e, "hvx_create: streams/events"); }
@@ -711,8 +709,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     return fail(HVX_E_INVALID, "hvx_ctu_analyze: NULL argument");
   const hvx_ctu_params P = *h_params;
   if (P.pic_w <= 0 || P.pic_h <= 0 || P.n_ref <= 0 || P.n_ref > 8 || P.qp < 0 || P.qp > 51 ||
-      stride < P.pic_w + 2 * HVX_PLANE_MARGIN || stride % 4 != 0 || P.search_range <= 0 || P.search_range > 256 ||
-      P.lambda_motion >= (1u << 24))  // the CTU kernels' MV cost multiplies on 24 bits
+      stride < P.pic_w + 2 * HVX_PLANE_MARGIN || stride % 4 != 0 || P.search_range <= 0 || P.search_range > 256)
     return fail(HVX_E_INVALID, "hvx_ctu_analyze: bad parameters");
   if (P.chroma_format != (chroma ? 1 : 0))
     return fail(HVX_E_INVALID, "hvx_ctu_analyze: chroma_format must be 0 (luma entry points) or 1 (hvx_ctu_encode_yuv)");

@@ -56,13 +56,10 @@ __device__ __forceinline__ MeRange me_search_range(const hvx_me_job &j, int px, 
   return g;
 }
 
-// TComRdCost::getCost(x, y) with the predictor at quarter-pel and the candidate at 1<<scale units.
-// L24: lam < 2^24 (the CTU pass checks it on the host), so the product is a full-rate 24-bit
-// multiply (bits < 2^8) instead of the quarter-rate 32-bit one.
-template <bool L24 = false>
+// TComRdCost::getCost(x, y) with the predictor at quarter-pel and the candidate at 1<<scale units
 __device__ __forceinline__ uint32_t me_mv_cost(uint32_t lam, int px, int py, int scale, int x, int y) {
   const uint32_t bits = eg_bits((x << scale) - px) + eg_bits((y << scale) - py);
-  return (L24 ? __umul24(lam, bits) : lam * bits) >> 16;
+  return (lam * bits) >> 16;
 }
 
 // 4 bytes at any address from two aligned dword loads (plane margins cover the over-read)
@@ -193,37 +190,24 @@ __device__ __forceinline__ uint32_t me_sad_part(const MeInt &m, int x, int y, in
 // takes sampled rows s, s+L, ...  Rows come from buffer loads at the point's dword-aligned
 // offset + an SGPR row offset (plane strides are multiples of 4, so one alignbyte shift serves
 // every row); the row loop unrolls so that up to ~24 dwords per lane are in flight at once.
-// Row loads at the candidate's byte address (the memory system's unaligned access mode does
-// the shift) instead of dword-aligned loads + v_alignbyte per dword.  Bit-exact on MI355X but
-// slower (2160p step 7.7 -> 8.8 ms: the 64x64 integer search 0.49 -> 1.09 ms), so off.
-constexpr bool kMeUnalignedRows = false;
 template <int S, int SUB, int SH>
 __device__ __forceinline__ uint32_t me_sad_part_ct(const MeInt &m, int x, int y, int s) {
   constexpr int ROWS = S >> SUB, L = 1 << SH, PER = (ROWS + L - 1) / L, GW = S / 4;
-  constexpr int BUDGET = S == 8 ? (kMeUnalignedRows ? 16 : 12) : 24;  // dwords in flight per lane (8x8: keep occupancy)
-  constexpr int DW = kMeUnalignedRows ? GW : GW + 1;                   // dwords per row load
-  constexpr int RUN = DW * PER <= BUDGET ? PER : (BUDGET / DW > 0 ? BUDGET / DW : 1);
+  constexpr int BUDGET = S == 8 ? 12 : 24;  // dwords in flight per lane (8x8: keep occupancy)
+  constexpr int RUN = (GW + 1) * PER <= BUDGET ? PER : (BUDGET / (GW + 1) > 0 ? BUDGET / (GW + 1) : 1);
   constexpr int UNR = RUN < 1 ? 1 : RUN;
-  // 24-bit multiplies (full rate; |rows| < 2^23): the 32-bit v_mul_lo is quarter rate
-  const uint32_t a = m.roff + (uint32_t)(__mul24(y + (s << SUB), m.sr) + x);
+  const uint32_t a = m.roff + (uint32_t)(y * m.sr + x) + (uint32_t)((s << SUB) * m.sr);
   const uint32_t va = a & ~3u, sh = a & 3u;
   const uint8_t *o = m.org + (s << SUB) * S;
   uint32_t acc = 0;
 #pragma unroll UNR
   for (int k = 0; k < PER; k++) {
     if (ROWS % L == 0 || s + k * L < ROWS) {
+      uint32_t w[GW + 1];
+      me_ldw<GW + 1>(m.rs, va, ((k * L) << SUB) * m.sr, w);
       const uint32_t *ow = (const uint32_t *)(o + ((k * L) << SUB) * S);
-      if constexpr (kMeUnalignedRows) {
-        uint32_t w[GW];
-        me_ldw<GW>(m.rs, a, ((k * L) << SUB) * m.sr, w);
 #pragma unroll
-        for (int i = 0; i < GW; i++) acc = __builtin_amdgcn_sad_u8(ow[i], w[i], acc);
-      } else {
-        uint32_t w[GW + 1];
-        me_ldw<GW + 1>(m.rs, va, ((k * L) << SUB) * m.sr, w);
-#pragma unroll
-        for (int i = 0; i < GW; i++) acc = __builtin_amdgcn_sad_u8(ow[i], __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh), acc);
-      }
+      for (int i = 0; i < GW; i++) acc = __builtin_amdgcn_sad_u8(ow[i], __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh), acc);
     }
   }
   return acc;
@@ -273,7 +257,7 @@ __device__ __forceinline__ void me_eval_min(MeInt &m, int n, int nr, F cand, R r
     acc = seg_sum(acc, sh);  // every lane of the point's group holds its SAD
     if (c.ok) {
       const int p = base + q;
-      const uint32_t k = me_key((acc << m.sub) + me_mv_cost<S != 0>(m.lam, m.px, m.py, 2, c.x, c.y), p);
+      const uint32_t k = me_key((acc << m.sub) + me_mv_cost(m.lam, m.px, m.py, 2, c.x, c.y), p);
       const int r = NR == 1 ? 0 : rng(p);
 #pragma unroll
       for (int i = 0; i < NR; i++)
@@ -448,10 +432,10 @@ __device__ void me_tz(const hvx_me_job &j, MeInt &m) {
       const int cnt = min(kMeMaxList, n - base);
       auto cand = [=](int p) {
         const int q = base + p;
-        int ry = (int)((float)q * rnx), rx = q - __mul24(ry, nx);  // float quotient, exact after one correction
+        int ry = (int)((float)q * rnx), rx = q - ry * nx;  // float quotient, exact after one correction
         if (rx < 0) { ry--; rx += nx; } else if (rx >= nx) { ry++; rx -= nx; }
         MeCand c;
-        c.x = g.l + __mul24(5, rx); c.y = g.t + __mul24(5, ry); c.pnr = 0; c.dist = 5; c.ok = true;
+        c.x = g.l + 5 * rx; c.y = g.t + 5 * ry; c.pnr = 0; c.dist = 5; c.ok = true;
         return c;
       };
       uint32_t key[1];
@@ -770,10 +754,9 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
     const int gw = w >> 2, gwp = gw + (shared ? 1 : 0);
     const __amdgpu_buffer_rsrc_t rs = me_plane_rsrc(ref - (j.pu_y * stride + j.pu_x), stride, j.pic_h);
     const uint32_t base = (uint32_t)((HVX_PLANE_MARGIN + j.pu_y + iy - 4) * stride + HVX_PLANE_MARGIN + j.pu_x + ix - 4);
-    const float rgwp = 1.0f / (float)gwp;  // k < 2^12: (k + 0.5) / gwp truncates exactly in float
     for (int k = threadIdx.x; k < (h + 8) * gwp; k += 64 * NW) {
-      const int r = (int)(((float)k + 0.5f) * rgwp), x0 = (k - __mul24(r, gwp)) << 2;
-      const uint32_t a = base + (uint32_t)(__mul24(r, stride) + x0);
+      const int r = k / gwp, x0 = (k - r * gwp) << 2;
+      const uint32_t a = base + (uint32_t)(r * stride + x0);
       const me_v4u q = __builtin_amdgcn_raw_buffer_load_b128(rs, a & ~3u, 0, 0);
       const uint32_t sh = a & 3u;
       const uint32_t wv[3] = {__builtin_amdgcn_alignbyte(q.y, q.x, sh), __builtin_amdgcn_alignbyte(q.z, q.y, sh),
@@ -869,7 +852,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
     const int c = (sl * 11) >> 5, dx = c - 1, dy = sl - 3 * c - 1;  // sl / 3, sl % 3 for sl < 9
     const uint64_t idx = step == 2 ? kRefSlotH : kRefSlotQ;
     const int ci = (int)((idx >> (4 * sl)) & 15);
-    const uint32_t cost = dsum + me_mv_cost<!GENERIC>(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
+    const uint32_t cost = dsum + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
     const uint32_t key = wave_min_key(valid ? (cost << 4) | (uint32_t)ci : kMeKeyNone);
     bi = (int)(key & 15u);
     return key >> 4;
