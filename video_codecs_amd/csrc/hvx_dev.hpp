@@ -28,6 +28,13 @@ __constant__ int8_t kLumaFilter[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
                                          {-1, 4, -10, 58, 17, -5, 1, 0},
                                          {-1, 4, -11, 40, 40, -11, 4, -1},
                                          {0, 1, -5, 17, 58, -10, 4, -1}};
+// the luma taps as int16 pairs (t = 2u, 2u + 1) for v_dot2_i32_i16
+constexpr uint32_t luma_pair(int a, int b) { return ((uint32_t)a & 0xffffu) | ((uint32_t)b << 16); }
+__constant__ uint32_t kLumaPairs[4][4] = {
+    {luma_pair(0, 0), luma_pair(0, 64), luma_pair(0, 0), luma_pair(0, 0)},
+    {luma_pair(-1, 4), luma_pair(-10, 58), luma_pair(17, -5), luma_pair(1, 0)},
+    {luma_pair(-1, 4), luma_pair(-11, 40), luma_pair(40, -11), luma_pair(4, -1)},
+    {luma_pair(0, 1), luma_pair(-5, 17), luma_pair(58, -10), luma_pair(4, -1)}};
 __constant__ int8_t kChromaFilter[8][4] = {{0, 64, 0, 0},   {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
                                            {-4, 36, 36, -4}, {-4, 28, 46, -6}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
 

@@ -424,7 +424,11 @@ __device__ void me_tz(const hvx_me_job &j, MeInt &m) {
   }
   if (m.best_dist == 1) { m.best_dist = 0; me_2point<S, SUB, NW>(m, g0); }
   // raster (step 5) over the re-centred range, lists of kMeMaxList points
+#ifdef HVX_EXP_NORASTER
+  if (false) {
+#else
   if (m.best_dist > 5) {
+#endif
     m.best_dist = 5;
     const int nx = (g.r - g.l) / 5 + 1, ny = (g.b - g.t) / 5 + 1, n = nx * ny;
     const float rnx = 1.0f / (float)nx;
@@ -631,26 +635,30 @@ __device__ __forceinline__ void me_had_xy(int lane, int &x, int &y) {
   const int c = me_had_c(lane);
   x = c & 7; y = c >> 3;
 }
-template <int N>
-__device__ __forceinline__ void had8_xlane_dpp(int (&v)[N]) {
+// The same transform on int16 pairs: p[i] holds two candidates' values (lo, hi) and every
+// butterfly is one partner fetch + one v_pk_mad_i16 (sign * own + partner) for both.  8-bit
+// inputs: |values| <= 64 * 510 after the 6 stages, inside int16.
+template <int NP>
+__device__ __forceinline__ void had8_xlane_pk(uint32_t (&p)[NP]) {
   const int c = me_had_c(lane_id());
 #pragma unroll
   for (int k = 0; k < 6; k++) {
-    const int sg = 1 - (((c >> k) & 1) << 1);  // +1: v + partner, -1: partner - v
+    const short sg1 = (short)(1 - (((c >> k) & 1) << 1));
+    const me_s2 sg = {sg1, sg1};
 #pragma unroll
-    for (int i = 0; i < N; i++) {
+    for (int i = 0; i < NP; i++) {
       if (k < 4) {
-        int t;
-        if (k == 0) t = __builtin_amdgcn_mov_dpp(v[i], 0xB1, 0xf, 0xf, false);
-        else if (k == 1) t = __builtin_amdgcn_mov_dpp(v[i], 0x4E, 0xf, 0xf, false);
-        else if (k == 2) t = __builtin_amdgcn_mov_dpp(v[i], 0x141, 0xf, 0xf, false);
-        else t = __builtin_amdgcn_mov_dpp(v[i], 0x140, 0xf, 0xf, false);
-        v[i] = t + __mul24(sg, v[i]);
+        uint32_t t;
+        if (k == 0) t = (uint32_t)__builtin_amdgcn_mov_dpp((int)p[i], 0xB1, 0xf, 0xf, false);
+        else if (k == 1) t = (uint32_t)__builtin_amdgcn_mov_dpp((int)p[i], 0x4E, 0xf, 0xf, false);
+        else if (k == 2) t = (uint32_t)__builtin_amdgcn_mov_dpp((int)p[i], 0x141, 0xf, 0xf, false);
+        else t = (uint32_t)__builtin_amdgcn_mov_dpp((int)p[i], 0x140, 0xf, 0xf, false);
+        p[i] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(me_s2, t) + sg * __builtin_bit_cast(me_s2, p[i]));
       } else {
-        // with both operands = v the swap returns (low-half value, high-half value) in every lane
-        const auto pr = k == 4 ? __builtin_amdgcn_permlane16_swap((unsigned)v[i], (unsigned)v[i], false, false)
-                               : __builtin_amdgcn_permlane32_swap((unsigned)v[i], (unsigned)v[i], false, false);
-        v[i] = (int)pr[0] + __mul24(sg, (int)pr[1]);
+        const auto pr = k == 4 ? __builtin_amdgcn_permlane16_swap(p[i], p[i], false, false)
+                               : __builtin_amdgcn_permlane32_swap(p[i], p[i], false, false);
+        p[i] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(me_s2, (uint32_t)pr[0]) +
+                                                sg * __builtin_bit_cast(me_s2, (uint32_t)pr[1]));
       }
     }
   }
@@ -679,6 +687,22 @@ __device__ __forceinline__ int me_vsample(const int *hw, int off, int fy) {
     for (int t = 0; t < 8; t++) s += kLumaFilter[fy][t] * hw[t];
   }
   return clip_pel((s + (1 << 11) + (8192 << 6)) >> 12);
+}
+
+// The same second stage read straight from the phase plane: h points at the first tap's row
+// (row stride HS).  Each tap pair is loaded as an int16 pair (ds_read_u16 + _d16_hi) and
+// accumulated by one v_dot2_i32_i16, so the per-tap multiplies and the per-lane window
+// selection of me_vsample disappear.
+template <int HS>
+__device__ __forceinline__ int me_vsample_pk(const int16_t *h, int fy) {
+  if (!fy) return clip_pel((h[3 * HS] + 8192 + 32) >> 6);
+  int s = (1 << 11) + (8192 << 6);
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const me_s2 pr = {h[(2 * u) * HS], h[(2 * u + 1) * HS]};
+    s = __builtin_amdgcn_sdot2(pr, __builtin_bit_cast(me_s2, kLumaPairs[fy][u]), s, false);
+  }
+  return clip_pel(s >> 12);
 }
 
 // Sums over the wave of the 9 candidates' |coefficient| vectors at once: permlane32 swaps
@@ -730,6 +754,9 @@ template <int S, int NW, bool GENERIC, typename TO>
 __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j, const uint8_t *ref, int stride, int ix,
                                   int iy, int qx0, int qy0, int step, int scale, int mvx0, int mvy0, int &bi) {
   constexpr int HS = MeFracSmem<S, NW, TO>::HS;
+  // the stage geometry is wave-uniform: held in SGPRs, the phase / offset selections below are
+  // scalar branches instead of per-tap v_cndmask
+  ix = uni(ix); iy = uni(iy); qx0 = uni(qx0); qy0 = uni(qy0);
   const int w = GENERIC ? j.w : S, h = GENERIC ? j.h : S, lane = lane_id(), wave = threadIdx.x >> 6;
   const bool had = (j.flags & HVX_ME_HADME) != 0;
   // 1. horizontal phases: column c at quarter x = qx0 + (c-1)*step, integer offset ix-1 or ix
@@ -816,16 +843,23 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
       int v[9];
 #pragma unroll
       for (int c = 0; c < 3; c++) {
-        int hw[9];
         const int16_t *h = &sm.hp[0][0] + po[c] + (ryb + 1 + y) * HS + x;
 #pragma unroll
-        for (int k = 0; k < 9; k++) hw[k] = h[k * HS];
-#pragma unroll
-        for (int d = 0; d < 3; d++) v[c * 3 + d] = o - me_vsample(hw, offs[d], fys[d]);
+        for (int d = 0; d < 3; d++) v[c * 3 + d] = o - me_vsample_pk<HS>(h + offs[d] * HS, fys[d]);
       }
-      had8_xlane_dpp<9>(v);
+      uint32_t pk[5];  // candidate pairs (0,1) (2,3) (4,5) (6,7) (8,-) as int16 halves
 #pragma unroll
-      for (int i = 0; i < 9; i++) v[i] = abs(v[i]);
+      for (int k = 0; k < 4; k++) pk[k] = __builtin_amdgcn_perm((uint32_t)v[2 * k + 1], (uint32_t)v[2 * k], 0x05040100u);
+      pk[4] = (uint32_t)v[8] & 0xffffu;
+      had8_xlane_pk<5>(pk);
+#pragma unroll
+      for (int k = 0; k < 5; k++) {
+        const me_s2 x = __builtin_bit_cast(me_s2, pk[k]);
+        pk[k] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, -x));
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) { v[2 * k] = (int)(pk[k] & 0xffffu); v[2 * k + 1] = (int)(pk[k] >> 16); }
+      v[8] = (int)(pk[4] & 0xffffu);
       uint32_t u[3];
       me_sum9(v, u);
 #pragma unroll
@@ -1000,6 +1034,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(S == 8 
   m.px = j.pred_x; m.py = j.pred_y;
   me_tz<S, SUB, NW>(j, m);
   const uint32_t sad_int = m.best_sad - me_mv_cost(m.lam, m.px, m.py, 2, m.best_x, m.best_y);
+#ifdef HVX_EXP_NOFRAC
+  if (threadIdx.x == 0) { hvx_me_result r{}; r.mv_int_x = m.best_x; r.mv_int_y = m.best_y; r.sad_int = sad_int; r.cost = sad_int; out[slot] = r; }
+  return;
+#endif
   me_frac_refine<S, NW, false, uint8_t>(j, m.ref, stride, m.best_x, m.best_y, sad_int, sm, out + slot);
 }
 
