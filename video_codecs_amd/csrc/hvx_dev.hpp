@@ -18,6 +18,7 @@
 __constant__ uint16_t kScan[3][1360];
 __constant__ uint8_t kScanCG[3][85];
 __constant__ int16_t kMat[1360];
+__constant__ int16_t kMatT[1360];  // each size's matrix transposed: kMatT[x][k] = kMat[k][x]
 __constant__ int8_t kDst4[16] = {29, 55, 74, 84, 74, 74, 0, -74, 84, -29, -74, 55, 55, -84, 74, -29};
 __constant__ int32_t kQuantScales[6] = {26214, 23302, 20560, 18396, 16384, 14564};
 __constant__ int32_t kInvQuantScales[6] = {40, 45, 51, 57, 64, 72};

@@ -196,6 +196,15 @@ int upload_tables() {
   HVX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(kScan), scan, sizeof(scan)));
   HVX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(kScanCG), scan_cg, sizeof(scan_cg)));
   HVX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(kMat), mat, sizeof(mat)));
+  int16_t matT[1360];
+  mb = 0;
+  for (int l = 0; l < 4; l++) {
+    const int n = 4 << l;
+    for (int k = 0; k < n; k++)
+      for (int x = 0; x < n; x++) matT[mb + x * n + k] = mat[mb + k * n + x];
+    mb += n * n;
+  }
+  HVX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(kMatT), matT, sizeof(matT)));
   return HVX_OK;
 }
 }  // namespace

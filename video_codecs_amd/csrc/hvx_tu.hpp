@@ -22,9 +22,9 @@
 template <int L>
 struct TuSmem {
   static constexpr int N = 4 << L, NN = N * N, NCG = NN / 16;
-  int32_t a[NN];
-  int32_t coef[NN];
-  int32_t lev[NN];
+  alignas(16) int32_t a[NN];
+  alignas(16) int32_t coef[NN];
+  alignas(16) int32_t lev[NN];
   int32_t cgr[NCG];  // RDOQ coded-group flag rate per CG scan position
 };
 
@@ -88,6 +88,88 @@ __device__ void tu_forward_transform(TuSmem<L> &s, bool dst) {
 #pragma unroll 8
     for (int y = 0; y < N; y++) acc += tu_mat<L>(dst, v, y) * tmpT[y * N + u];
     s.coef[v * N + u] = (acc + a2) >> s2;
+  }
+  __syncthreads();
+}
+
+// ---- 16-bit transform form for the 16x16 / 32x32 TUs of 8-bit video with the 15-bit dynamic
+// range (the CTU pass): every operand of both directions is int16 there -- residuals, the
+// forward first stage ((sum + a1) >> s1 <= 2048 * 255 / 2^s1 in magnitude, the DCT rows' largest
+// absolute sum being 64N), dequantised coefficients (clipped to [-2^15, 2^15)) and the inverse
+// first stage (clipped) -- so each product pair is one v_dot2_i32_i16 on int16 pairs, and the
+// lane's matrix row (lane & (N-1), the same row in both passes) stays in registers.  The sums
+// are the same integers as tu_forward_transform / tu_inverse_transform.
+template <int L>
+__device__ __forceinline__ void tu_mat_row(const int16_t *tab, int r, uint32_t (&w)[(4 << L) / 2]) {
+  constexpr int N = 4 << L;
+  const uint4 *p = reinterpret_cast<const uint4 *>(tab + mat_base(L) + r * N);
+#pragma unroll
+  for (int q = 0; q < N / 8; q++) {
+    const uint4 v = p[q];
+    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+  }
+}
+// sum over the N/2 int16 pairs of a 16-byte aligned LDS row against the register row
+template <int L>
+__device__ __forceinline__ int tu_dot_row(const uint32_t (&m)[(4 << L) / 2], const int16_t *row, int acc) {
+  constexpr int N = 4 << L;
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  const uint4 *p = reinterpret_cast<const uint4 *>(row);
+#pragma unroll
+  for (int q = 0; q < N / 8; q++) {
+    const uint4 v = p[q];
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, m[4 * q]), __builtin_bit_cast(s2, v.x), acc, false);
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, m[4 * q + 1]), __builtin_bit_cast(s2, v.y), acc, false);
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, m[4 * q + 2]), __builtin_bit_cast(s2, v.z), acc, false);
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, m[4 * q + 3]), __builtin_bit_cast(s2, v.w), acc, false);
+  }
+  return acc;
+}
+template <int N> constexpr int tu_p16() { return N + 8; }  // int16 pitch of the transposed planes (16-byte rows)
+
+// xTrMxN: aH = int16 residual [y][x] (pitch N) -> coefT = int32 coefficient (v, u) at u*N + v;
+// tT (int16, N x tu_p16) is scratch
+template <int L>
+__device__ void tu_forward_dot2(const int16_t *aH, int16_t *tT, int32_t *coefT) {
+  constexpr int N = 4 << L, LOG2 = L + 2, P = tu_p16<N>(), R = HVX_WAVE / N;
+  static_assert(L >= 2, "16x16 / 32x32 only");
+  const int s1 = LOG2 - 1, s2 = LOG2 + 6, a1 = 1 << (s1 - 1), a2 = 1 << (s2 - 1);
+  const int lane = lane_id(), r = lane & (N - 1), g = lane / N;
+  uint32_t m[N / 2];
+  tu_mat_row<L>(kMat, r, m);
+#pragma unroll 2
+  for (int k = 0; k < N / R; k++) {  // out1[y][u = r] -> tT[u][y]
+    const int y = g + R * k;
+    tT[r * P + y] = (int16_t)(tu_dot_row<L>(m, aH + y * N, a1) >> s1);
+  }
+  __syncthreads();
+#pragma unroll 2
+  for (int k = 0; k < N / R; k++) {  // coefficient (v = r, u)
+    const int u = g + R * k;
+    coefT[u * N + r] = tu_dot_row<L>(m, tT + u * P, a2) >> s2;
+  }
+  __syncthreads();
+}
+
+// xITrMxN: deqT = int16 dequantised coefficient (v, u) at u*P + v -> out = int32 residual [y][x]
+// (pitch N, values clipped to int16); tmp (int16, N x P) is scratch
+template <int L>
+__device__ void tu_inverse_dot2(const int16_t *deqT, int16_t *tmp, int32_t *out) {
+  constexpr int N = 4 << L, P = tu_p16<N>(), R = HVX_WAVE / N;
+  static_assert(L >= 2, "16x16 / 32x32 only");
+  const int lane = lane_id(), r = lane & (N - 1), g = lane / N;
+  uint32_t m[N / 2];
+  tu_mat_row<L>(kMatT, r, m);  // M^T row r: M[.][r]
+#pragma unroll 2
+  for (int k = 0; k < N / R; k++) {  // tmp[y = r][u] = sum_v M[v][y] in[v][u]
+    const int u = g + R * k;
+    tmp[r * P + u] = (int16_t)clip3(-32768, 32767, tu_dot_row<L>(m, deqT + u * P, 64) >> 7);
+  }
+  __syncthreads();
+#pragma unroll 2
+  for (int k = 0; k < N / R; k++) {  // out[y][x = r] = sum_u M[u][x] tmp[y][u]
+    const int y = g + R * k;
+    out[y * N + r] = clip3(-32768, 32767, tu_dot_row<L>(m, tmp + y * P, 2048) >> 12);
   }
   __syncthreads();
 }
@@ -1154,10 +1236,39 @@ __global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ d
   if (d.width != N || d.height != N) return;
   const int64_t off = offs[t];
   const int lane = lane_id();
+  const TuCoding c = tu_coding<L>(d);
+  if constexpr (L >= 2) {
+    // the CTU pass's 16x16 / 32x32 TUs (8-bit, RDOQ): the 16-bit transform, coefficients transposed
+    if (!temp_out && !arl_out && d.bit_depth == 8 && d.max_log2_tr_range == 15 && !d.transquant_bypass &&
+        !d.transform_skip && !d.extended_precision && d.use_rdoq && !d.selective_rdoq) {
+      constexpr int LOG2 = L + 2;
+      int16_t *aH = reinterpret_cast<int16_t *>(s.a);
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(res_in + off);
+      for (int i = lane; i < NN / 2; i += HVX_WAVE) reinterpret_cast<uint32_t *>(aH)[i] = src[i];
+      __syncthreads();
+      tu_forward_dot2<L>(aH, reinterpret_cast<int16_t *>(s.lev), s.coef);
+      const int qbits = 14 + d.qp_per + tu_transform_shift(d);
+      const int qc = kQuantScales[d.qp_rem];
+      const int64_t lim = (int64_t)2147483647 - ((int64_t)1 << (qbits - 1));
+      const int ch = d.comp ? 1 : 0, sig_off = ch ? 28 : 0;
+      for (int sp = lane; sp < NN; sp += HVX_WAVE) {
+        const int blk = c.scan[sp];
+        const int32_t cf = s.coef[(blk & (N - 1)) * N + (blk >> LOG2)];
+        const int32_t ld = rd_level_double(cf, qc, lim);
+        const size_t il = tu_il(t, sp, NN, G);
+        ldI[il] = (uint32_t)ld | (cf < 0 ? 0x80000000u : 0u);
+        uint32_t cx = 0;
+#pragma unroll
+        for (int p = 0; p < 4; p++) cx |= (uint32_t)(sig_off + rd_sig_ctx<L>(p, c, sp, ch)) << (6 * p);
+        cxI[il] = cx;
+      }
+      if (lane == 0) flags[t] = 1;
+      return;
+    }
+  }
   for (int i = lane; i < NN; i += HVX_WAVE) s.a[i] = res_in[off + i];
   __syncthreads();
   int32_t *arl = arl_out ? arl_out + off : nullptr;
-  const TuCoding c = tu_coding<L>(d);
   bool rdoq = false;
   int32_t abs_sum = 0;
   if (d.transquant_bypass) {
@@ -1267,6 +1378,28 @@ __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ 
 // zd_out: the zero-residual distortion sum(res_in^2); with pred (8-bit, residual layout) and
 // csse_out: the distortion of the clipped reconstruction, sum((pred + res_in - clip(pred + r))^2)
 // (TComYuv::addClip + getDistPart over the TU).
+// tu_inverse for the CTU pass's 16x16 / 32x32 TUs (8-bit, 15-bit range, transform, no bypass):
+// dequantised coefficients transposed as int16, the 16-bit inverse transform; s.lev ends with
+// the reconstructed residual (raster) exactly as tu_inverse leaves it
+template <int L>
+__device__ void tu_inverse_fast(TuSmem<L> &s, const hvx_tu_desc &d) {
+  constexpr int N = 4 << L, NN = N * N, LOG2 = L + 2, P = tu_p16<N>();
+  const int ts = tu_transform_shift(d);
+  const int right = 6 - (ts + d.qp_per);
+  const int scale = kInvQuantScales[d.qp_rem];
+  int tib = 32 + right - 7;
+  if (16 < tib) tib = 16;
+  const int32_t imin = -(1 << (tib - 1)), imax = (1 << (tib - 1)) - 1;
+  int16_t *deqT = reinterpret_cast<int16_t *>(s.a);
+  for (int i = lane_id(); i < NN; i += HVX_WAVE) {
+    const int32_t c = clip3(imin, imax, s.lev[i]);
+    const int32_t v = right > 0 ? (c * scale + (1 << (right - 1))) >> right : shl32(c * scale, -right);
+    deqT[(i & (N - 1)) * P + (i >> LOG2)] = (int16_t)clip3(-32768, 32767, v);
+  }
+  __syncthreads();
+  tu_inverse_dot2<L>(deqT, reinterpret_cast<int16_t *>(s.coef), s.lev);
+}
+
 template <int L, int MODE>
 __global__ __launch_bounds__(64) void k_tu_fin(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
                                                int n, const int16_t *__restrict__ res_in,
@@ -1288,7 +1421,16 @@ __global__ __launch_bounds__(64) void k_tu_fin(const hvx_tu_desc *__restrict__ d
   for (int i = lane; i < NN; i += HVX_WAVE) lev_io[off + i] = s.lev[i];
   if (MODE == 2) {
     __syncthreads();
-    tu_inverse<L>(s, d);
+    bool fast = false;
+    if constexpr (L >= 2)
+      fast = d.bit_depth == 8 && d.max_log2_tr_range == 15 && !d.transquant_bypass && !d.transform_skip &&
+             !d.extended_precision;
+    if constexpr (L >= 2) {
+      if (fast) tu_inverse_fast<L>(s, d);
+      else tu_inverse<L>(s, d);
+    } else {
+      tu_inverse<L>(s, d);
+    }
     uint32_t part = 0, pz = 0, pc = 0;
     for (int i = lane; i < NN; i += HVX_WAVE) {
       const int r = (int16_t)s.lev[i];
