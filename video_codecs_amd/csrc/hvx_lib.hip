@@ -242,16 +242,18 @@ static void tu_class_launch(hipStream_t st, const hvx_tu_desc *desc, const hvx_e
   int k = t_begin(tctx, st, phase0);
   // the CTU pass's 4x4 / 8x8 TUs (RDOQ, inter: pred != nullptr marks that pass): one TU per lane
   const bool lane = L <= 1 && pred && G == 64 && !temp && !arl;
+  // 16x16 / 32x32 of that pass: the forward kernel (wave per TU) writes the RDOQ inputs TU-major
+  const int tm = L >= 2 && pred && !temp && !arl ? 1 : 0;
   if (lane)
     hipLaunchKernelGGL((k_tu_fwd_lane<L < 2 ? L : 1>), dim3((n + 63) / 64), dim3(64), 0, st, desc, off, n, res_in, coefI,
                        cxI, flags);
   else
     hipLaunchKernelGGL((k_tu_fwd<L>), dim3(n), dim3(64), 0, st, desc, off, n, res_in, temp, arl, coefI, cxI, levI, abs_sum,
-                       flags, G);
+                       flags, G, tm);
   t_end(tctx, st, k);
   k = t_begin(tctx, st, phase0 + 1);
   hipLaunchKernelGGL((k_tu_rdoq<L>), dim3((n + G - 1) / G), dim3(64), 0, st, desc, est, est_idx, n, coefI, cxI, levI, stI,
-                     abs_sum, flags, G, n_est_lds);
+                     abs_sum, flags, G, n_est_lds, tm);
   t_end(tctx, st, k);
   if (after_rdoq) (void)hipEventRecord(after_rdoq, st);  // the levels are final: their rate may be counted beside k_tu_fin
   k = t_begin(tctx, st, phase0 + 2);

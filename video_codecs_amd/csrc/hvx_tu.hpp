@@ -876,7 +876,9 @@ struct RdLaneStage {
 
 // FAST: the wave's tables are in LDS and no TU of the wave uses extended precision (the
 // limited-prefix escape code), so every table read is a ds_read and the rate has no branch.
-template <int L, bool FAST>
+// TM: ldI / cxI are TU-major (element sp at [sp], written coalesced by the wave-per-TU forward
+// kernel); otherwise interleaved like lev / st.
+template <int L, bool FAST, bool TM>
 __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const uint32_t *ldI, const uint32_t *cxI,
                              int32_t *lev, int32_t *st, int G, RdLaneStage &sg, int lane) {
   constexpr int N = 4 << L, NN = N * N, NCG = NN / 16;
@@ -894,6 +896,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
   const double lambda = d.lambda;
   const TuCoding c = tu_coding<L>(d);
   const size_t g16 = (size_t)16 * G;
+  const size_t gi = TM ? 1 : (size_t)G, gi16 = 16 * gi;  // ldI / cxI stride
   const int32_t rnd = 1 << (qbits - 1);
   const int set0 = comp ? 4 : 0;
   const bool persistent = d.persistent_rice != 0;
@@ -907,8 +910,8 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
   uint32_t nld[16], ncx[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    nld[k] = ldI[(NCG - 1) * g16 + (size_t)k * G];
-    ncx[k] = cxI[(NCG - 1) * g16 + (size_t)k * G];
+    nld[k] = ldI[(NCG - 1) * gi16 + (size_t)k * gi];
+    ncx[k] = cxI[(NCG - 1) * gi16 + (size_t)k * gi];
   }
   for (int cgp = NCG - 1; cgp >= 0; cgp--) {
 #pragma unroll
@@ -916,8 +919,8 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
     if (cgp > 0) {
 #pragma unroll
       for (int k = 0; k < 16; k++) {
-        nld[k] = ldI[(cgp - 1) * g16 + (size_t)k * G];
-        ncx[k] = cxI[(cgp - 1) * g16 + (size_t)k * G];
+        nld[k] = ldI[(cgp - 1) * gi16 + (size_t)k * gi];
+        ncx[k] = cxI[(cgp - 1) * gi16 + (size_t)k * gi];
       }
     }
     const int cgblk = c.scan_cg[cgp];
@@ -1078,7 +1081,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
         for (int k = 0; k < 16; k++) {
           a16[k] = lev[cgp * g16 + (size_t)k * G];
           b16[k] = st[cgp * g16 + (size_t)k * G];
-          c16[k] = ldI[cgp * g16 + (size_t)k * G];
+          c16[k] = ldI[cgp * gi16 + (size_t)k * gi];
         }
 #pragma unroll
         for (int k = 0; k < 16; k++) { sg.lv[k][lane] = a16[k]; sg.st[k][lane] = b16[k]; sg.ld[k][lane] = c16[k]; }
@@ -1123,7 +1126,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       lv16[k] = lev[cgp * g16 + (size_t)k * G];
-      cf16[k] = ldI[cgp * g16 + (size_t)k * G];
+      cf16[k] = ldI[cgp * gi16 + (size_t)k * gi];
     }
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -1164,7 +1167,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
             uint32_t c16[16];
 #pragma unroll
             for (int q = 0; q < 16; q++) {
-              c16[q] = ldI[sub * g16 + (size_t)q * G];
+              c16[q] = ldI[sub * gi16 + (size_t)q * gi];
               b16[q] = st[sub * g16 + (size_t)q * G];
             }
 #pragma unroll
@@ -1227,7 +1230,8 @@ __global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ d
                                                int n, const int16_t *__restrict__ res_in, int32_t *__restrict__ temp_out,
                                                int32_t *__restrict__ arl_out, uint32_t *__restrict__ ldI,
                                                uint32_t *__restrict__ cxI, int32_t *__restrict__ levI,
-                                               int32_t *__restrict__ abs_out, int8_t *__restrict__ flags, int G) {
+                                               int32_t *__restrict__ abs_out, int8_t *__restrict__ flags, int G,
+                                               int tm) {
   constexpr int N = 4 << L, NN = N * N;
   __shared__ TuSmem<L> s;
   const int t = blockIdx.x;
@@ -1255,7 +1259,7 @@ __global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ d
         const int blk = c.scan[sp];
         const int32_t cf = s.coef[(blk & (N - 1)) * N + (blk >> LOG2)];
         const int32_t ld = rd_level_double(cf, qc, lim);
-        const size_t il = tu_il(t, sp, NN, G);
+        const size_t il = tm ? (size_t)t * NN + sp : tu_il(t, sp, NN, G);
         ldI[il] = (uint32_t)ld | (cf < 0 ? 0x80000000u : 0u);
         uint32_t cx = 0;
 #pragma unroll
@@ -1308,7 +1312,7 @@ __global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ d
           const int blk = c.scan[sp];
           const int32_t cf = s.coef[blk];
           const int32_t ld = rd_level_double(cf, qc, lim);
-          const size_t il = tu_il(t, sp, NN, G);
+          const size_t il = tm ? (size_t)t * NN + sp : tu_il(t, sp, NN, G);
           ldI[il] = (uint32_t)ld | (cf < 0 ? 0x80000000u : 0u);
           uint32_t cx = 0;
 #pragma unroll
@@ -1345,7 +1349,7 @@ __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ 
                                                 const uint32_t *__restrict__ ldI, const uint32_t *__restrict__ cxI,
                                                 int32_t *__restrict__ levI, int32_t *__restrict__ stI,
                                                 int32_t *__restrict__ abs_out, const int8_t *__restrict__ flags, int G,
-                                                int n_est_lds) {
+                                                int n_est_lds, int tm) {
   constexpr int N = 4 << L, NN = N * N;
   __shared__ hvx_estbits tbl[8];  // n_est_lds <= 8 (the CTU pass: 4 luma + 3 chroma)
   __shared__ RdLaneStage stage;
@@ -1366,11 +1370,19 @@ __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ 
   const size_t base = tu_il(t, 0, NN, G);
   const bool any_ext = __builtin_amdgcn_ballot_w64(d.extended_precision != 0) != 0;
   int32_t a;
-  if (n_est_lds > 0 && !any_ext)
-    a = rdoq_lane<L, true>(d, &tbl[ei], ldI + base, cxI + base, levI + base, stI + base, G, stage, lane);
-  else
-    a = rdoq_lane<L, false>(d, n_est_lds > 0 ? &tbl[ei] : est + ei, ldI + base, cxI + base, levI + base, stI + base, G,
-                            stage, lane);
+  if (tm) {  // TU-major inputs (the CTU pass's 16x16 / 32x32 classes)
+    if (n_est_lds > 0 && !any_ext)
+      a = rdoq_lane<L, true, true>(d, &tbl[ei], ldI + (size_t)t * NN, cxI + (size_t)t * NN, levI + base, stI + base, G,
+                                   stage, lane);
+    else
+      a = rdoq_lane<L, false, true>(d, n_est_lds > 0 ? &tbl[ei] : est + ei, ldI + (size_t)t * NN, cxI + (size_t)t * NN,
+                                    levI + base, stI + base, G, stage, lane);
+  } else if (n_est_lds > 0 && !any_ext) {
+    a = rdoq_lane<L, true, false>(d, &tbl[ei], ldI + base, cxI + base, levI + base, stI + base, G, stage, lane);
+  } else {
+    a = rdoq_lane<L, false, false>(d, n_est_lds > 0 ? &tbl[ei] : est + ei, ldI + base, cxI + base, levI + base,
+                                   stI + base, G, stage, lane);
+  }
   if (abs_out) abs_out[t] = a;
 }
 
