@@ -709,6 +709,7 @@ __device__ __forceinline__ int me_vsample_pk(const int16_t *h, int fy) {
 // fold candidate pairs (2k, 2k+1) into the two wave halves, permlane16 swaps fold those pairs
 // into rows, DPP adds finish inside rows.  Every lane of row r of u[k] then holds the sum of
 // candidate 4k + {0,2,1,3}[r] (u[2]: row 0 = candidate 8, other rows 0).
+template <int NC = 9>  // NC = 8: a[8] unused, u[2] = 0
 __device__ __forceinline__ void me_sum9(const int (&a)[9], uint32_t (&u)[3]) {
   uint32_t w[5];
 #pragma unroll
@@ -716,9 +717,11 @@ __device__ __forceinline__ void me_sum9(const int (&a)[9], uint32_t (&u)[3]) {
     const auto p = __builtin_amdgcn_permlane32_swap((unsigned)a[2 * k], (unsigned)a[2 * k + 1], false, false);
     w[k] = p[0] + p[1];
   }
-  {
+  if constexpr (NC == 9) {
     const auto p = __builtin_amdgcn_permlane32_swap((unsigned)a[8], 0u, false, false);
     w[4] = p[0] + p[1];
+  } else {
+    w[4] = 0;
   }
   {
     const auto p = __builtin_amdgcn_permlane16_swap(w[0], w[1], false, false);
@@ -728,12 +731,14 @@ __device__ __forceinline__ void me_sum9(const int (&a)[9], uint32_t (&u)[3]) {
     const auto p = __builtin_amdgcn_permlane16_swap(w[2], w[3], false, false);
     u[1] = p[0] + p[1];
   }
-  {
+  if constexpr (NC == 9) {
     const auto p = __builtin_amdgcn_permlane16_swap(w[4], 0u, false, false);
     u[2] = p[0] + p[1];
+  } else {
+    u[2] = 0;
   }
 #pragma unroll
-  for (int k = 0; k < 3; k++) {
+  for (int k = 0; k < (NC == 9 ? 3 : 2); k++) {
     u[k] += ME_DPP(u[k], 0xB1);
     u[k] += ME_DPP(u[k], 0x4E);
     u[k] += ME_DPP(u[k], 0x141);
@@ -750,9 +755,12 @@ constexpr uint64_t kRefSlotH = 0x846201735ull, kRefSlotQ = 0x864201753ull;
 // quarter-pel relative to the PU, step 2 (half) or 1 (quarter); (ix,iy) the integer MV.
 // The NW waves of the job share the phase planes and take candidates i = wave, wave+NW, ...
 // GENERIC: any block shape up to SxS; otherwise square SxS blocks only (the CTU pass).
-template <int S, int NW, bool GENERIC, typename TO>
+// QC (quarter stage): the centre candidate is the half stage's best, whose cost (ccost) the half
+// stage already computed from the same samples and MV; the tile work covers the other 8 only.
+template <int S, int NW, bool GENERIC, typename TO, bool QC = false>
 __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j, const uint8_t *ref, int stride, int ix,
-                                  int iy, int qx0, int qy0, int step, int scale, int mvx0, int mvy0, int &bi) {
+                                  int iy, int qx0, int qy0, int step, int scale, int mvx0, int mvy0, int &bi,
+                                  uint32_t ccost = 0) {
   constexpr int HS = MeFracSmem<S, NW, TO>::HS;
   // the stage geometry is wave-uniform: held in SGPRs, the phase / offset selections below are
   // scalar branches instead of per-tap v_cndmask
@@ -840,30 +848,36 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
     for (int t = wave; t < nt; t += NW) {
       const int x = ((t % tw) << 3) + hx, y = ((t / tw) << 3) + hy;
       const int o = sm.org[y * S + x];
-      int v[9];
+      int v[9] = {};
 #pragma unroll
       for (int c = 0; c < 3; c++) {
         const int16_t *h = &sm.hp[0][0] + po[c] + (ryb + 1 + y) * HS + x;
 #pragma unroll
-        for (int d = 0; d < 3; d++) v[c * 3 + d] = o - me_vsample_pk<HS>(h + offs[d] * HS, fys[d]);
+        for (int d = 0; d < 3; d++)
+          if (!QC || c * 3 + d != 4) v[c * 3 + d] = o - me_vsample_pk<HS>(h + offs[d] * HS, fys[d]);
       }
-      uint32_t pk[5];  // candidate pairs (0,1) (2,3) (4,5) (6,7) (8,-) as int16 halves
+      // candidate pairs as int16 halves: (0,1) (2,3) (4,5) (6,7) (8,-); QC: (0,1) (2,3) (5,6) (7,8)
+      constexpr int NP = QC ? 4 : 5;
+      int w[9];
 #pragma unroll
-      for (int k = 0; k < 4; k++) pk[k] = __builtin_amdgcn_perm((uint32_t)v[2 * k + 1], (uint32_t)v[2 * k], 0x05040100u);
-      pk[4] = (uint32_t)v[8] & 0xffffu;
-      had8_xlane_pk<5>(pk);
+      for (int k = 0; k < 9; k++) w[k] = QC ? v[k < 4 ? k : (k < 8 ? k + 1 : 0)] : v[k];
+      uint32_t pk[NP];
 #pragma unroll
-      for (int k = 0; k < 5; k++) {
+      for (int k = 0; k < 4; k++) pk[k] = __builtin_amdgcn_perm((uint32_t)w[2 * k + 1], (uint32_t)w[2 * k], 0x05040100u);
+      if constexpr (!QC) pk[NP - 1] = (uint32_t)w[8] & 0xffffu;
+      had8_xlane_pk<NP>(pk);
+#pragma unroll
+      for (int k = 0; k < NP; k++) {
         const me_s2 x = __builtin_bit_cast(me_s2, pk[k]);
         pk[k] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, -x));
       }
 #pragma unroll
-      for (int k = 0; k < 4; k++) { v[2 * k] = (int)(pk[k] & 0xffffu); v[2 * k + 1] = (int)(pk[k] >> 16); }
-      v[8] = (int)(pk[4] & 0xffffu);
+      for (int k = 0; k < 4; k++) { w[2 * k] = (int)(pk[k] & 0xffffu); w[2 * k + 1] = (int)(pk[k] >> 16); }
+      w[8] = QC ? 0 : (int)(pk[NP - 1] & 0xffffu);
       uint32_t u[3];
-      me_sum9(v, u);
+      me_sum9<QC ? 8 : 9>(w, u);
 #pragma unroll
-      for (int k = 0; k < 3; k++) acc[k] += (u[k] + 2) >> 2;  // xCalcHADs8x8 rounding per tile
+      for (int k = 0; k < (QC ? 2 : 3); k++) acc[k] += (u[k] + 2) >> 2;  // xCalcHADs8x8 rounding per tile
     }
     // lane-parallel costs: lane (row r, kk = lane & 15 < 3) takes the slot s = c*3 + d me_sum9
     // put there; the first minimum in the reference's candidate order is a (cost, index) key-min
@@ -882,11 +896,13 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
         for (int ww = 0; ww < NW; ww++) dsum += sm.part[ww][kk < 3 ? kk : 0][r];
       }
     }
-    const int sl = kk >= 2 ? 8 : 4 * kk + ((0xD8 >> (2 * r)) & 3);
+    const int wi = 4 * kk + ((0xD8 >> (2 * r)) & 3);  // the me_sum9 slot of this lane (kk < 2)
+    const int sl = QC ? (kk >= 2 ? 4 : wi + (wi >= 4)) : (kk >= 2 ? 8 : wi);
     const int c = (sl * 11) >> 5, dx = c - 1, dy = sl - 3 * c - 1;  // sl / 3, sl % 3 for sl < 9
     const uint64_t idx = step == 2 ? kRefSlotH : kRefSlotQ;
     const int ci = (int)((idx >> (4 * sl)) & 15);
-    const uint32_t cost = dsum + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
+    const uint32_t cost = (QC && kk >= 2) ? ccost
+                                           : dsum + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
     const uint32_t key = wave_min_key(valid ? (cost << 4) | (uint32_t)ci : kMeKeyNone);
     bi = (int)(key & 15u);
     return key >> 4;
@@ -956,10 +972,12 @@ __device__ void me_frac_refine(const hvx_me_job &j, const uint8_t *ref, int stri
                                MeFracSmem<S, NW, TO> &sm, hvx_me_result *out) {
   // half-pel around the integer MV, then quarter-pel
   int bh, bq;
-  me_frac_stage<S, NW, GENERIC, TO>(sm, j, ref, stride, ix, iy, ix << 2, iy << 2, 2, 1, ix << 1, iy << 1, bh);
+  const uint32_t hcost =
+      me_frac_stage<S, NW, GENERIC, TO>(sm, j, ref, stride, ix, iy, ix << 2, iy << 2, 2, 1, ix << 1, iy << 1, bh);
   const int hx = kRefH[bh][0], hy = kRefH[bh][1];
   const int cqx = (ix << 2) + (hx << 1), cqy = (iy << 2) + (hy << 1);
-  const uint32_t cost = me_frac_stage<S, NW, GENERIC, TO>(sm, j, ref, stride, ix, iy, cqx, cqy, 1, 0, cqx, cqy, bq);
+  const uint32_t cost =
+      me_frac_stage<S, NW, GENERIC, TO, true>(sm, j, ref, stride, ix, iy, cqx, cqy, 1, 0, cqx, cqy, bq, hcost);
   const int qx = kRefQ[bq][0], qy = kRefQ[bq][1];
   const int fmx = cqx + qx, fmy = cqy + qy;
   const uint32_t mv_bits = eg_bits(fmx - j.pred_x) + eg_bits(fmy - j.pred_y);
