@@ -36,6 +36,14 @@ __constant__ uint32_t kLumaPairs[4][4] = {
     {luma_pair(-1, 4), luma_pair(-10, 58), luma_pair(17, -5), luma_pair(1, 0)},
     {luma_pair(-1, 4), luma_pair(-11, 40), luma_pair(40, -11), luma_pair(4, -1)},
     {luma_pair(0, 1), luma_pair(-5, 17), luma_pair(58, -10), luma_pair(4, -1)}};
+// the luma taps as packed int8: [fx][0] = taps 0..3, [fx][1] = taps 4..7 (byte k = tap k) for v_dot4_i32_i8
+constexpr uint32_t tap4(int a, int b, int c, int d) {
+  return ((uint32_t)a & 0xffu) | (((uint32_t)b & 0xffu) << 8) | (((uint32_t)c & 0xffu) << 16) | ((uint32_t)d << 24);
+}
+__constant__ uint32_t kLumaTap4[4][2] = {{tap4(0, 0, 0, 64), tap4(0, 0, 0, 0)},
+                                         {tap4(-1, 4, -10, 58), tap4(17, -5, 1, 0)},
+                                         {tap4(-1, 4, -11, 40), tap4(40, -11, 4, -1)},
+                                         {tap4(0, 1, -5, 17), tap4(58, -10, 4, -1)}};
 __constant__ int8_t kChromaFilter[8][4] = {{0, 64, 0, 0},   {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
                                            {-4, 36, 36, -4}, {-4, 28, 46, -6}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
 

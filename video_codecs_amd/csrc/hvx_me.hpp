@@ -794,35 +794,39 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
       const uint32_t a = base + (uint32_t)(r * stride + x0);
       const me_v4u q = __builtin_amdgcn_raw_buffer_load_b128(rs, a & ~3u, 0, 0);
       const uint32_t sh = a & 3u;
-      const uint32_t wv[3] = {__builtin_amdgcn_alignbyte(q.y, q.x, sh), __builtin_amdgcn_alignbyte(q.z, q.y, sh),
-                              __builtin_amdgcn_alignbyte(q.w, q.z, sh)};
-      uint32_t P[11];  // P[s] = (b[s], b[s+1]) as an int16 pair
+      // the 12 bytes as signed bytes b - 128: then sum_t c_t * (b_t - 128) = sum_t c_t * b_t - 64 * 128,
+      // which is the reference's first-stage value with its -8192 offset, one v_dot4_i32_i8 per 4 taps
+      const uint32_t wv[3] = {__builtin_amdgcn_alignbyte(q.y, q.x, sh) ^ 0x80808080u,
+                              __builtin_amdgcn_alignbyte(q.z, q.y, sh) ^ 0x80808080u,
+                              __builtin_amdgcn_alignbyte(q.w, q.z, sh) ^ 0x80808080u};
+      uint32_t W[9];  // W[s] = bytes s .. s+3
 #pragma unroll
-      for (int t = 0; t < 11; t++) {
-        const uint32_t lo = wv[t >> 2], hi = wv[(t + 1) >> 2];
-        const uint32_t b0 = t & 3, b1 = ((t + 1) >> 2) == (t >> 2) ? ((t + 1) & 3) : 4;
-        P[t] = __builtin_amdgcn_perm(hi, lo, 0x0c000c00u | (b1 << 16) | b0);
-      }
+      for (int t = 0; t < 9; t++) W[t] = (t & 3) ? __builtin_amdgcn_alignbyte(wv[(t >> 2) + 1], wv[t >> 2], t & 3) : wv[t >> 2];
 #pragma unroll
       for (int c = 0; c < 3; c++) {
         if (c == 2 && shared) continue;
         if (c != 0 && x0 >= w) continue;  // the extra column item only feeds the shared plane
-        const int fx = fxs[c];
-        me_s2 o01, o23;
+        const int fx = fxs[c], o0 = oxo[c];
+        int ov[4];
         if (!fx) {
-          const me_s2 off = {-8192, -8192};
-          o01 = (oxo[c] ? __builtin_bit_cast(me_s2, P[4]) : __builtin_bit_cast(me_s2, P[3])) * (short)64 + off;
-          o23 = (oxo[c] ? __builtin_bit_cast(me_s2, P[6]) : __builtin_bit_cast(me_s2, P[5])) * (short)64 + off;
-        } else if (oxo[c]) {
-          o01 = me_fir_pk(fx, P + 1);
-          o23 = me_fir_pk(fx, P + 3);
+#pragma unroll
+          for (int i = 0; i < 4; i++) {  // (b - 128) * 64 of byte 3 + o0 + i
+            const int bi = 3 + o0 + i;
+            ov[i] = (int)(int8_t)(W[bi & ~3] >> (8 * (bi & 3))) * 64;
+          }
         } else {
-          o01 = me_fir_pk(fx, P);
-          o23 = me_fir_pk(fx, P + 2);
+          const int clo = (int)kLumaTap4[fx][0], chi = (int)kLumaTap4[fx][1];
+          if (o0) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) ov[i] = __builtin_amdgcn_sdot4((int)W[i + 5], chi, __builtin_amdgcn_sdot4((int)W[i + 1], clo, 0, false), false);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) ov[i] = __builtin_amdgcn_sdot4((int)W[i + 4], chi, __builtin_amdgcn_sdot4((int)W[i], clo, 0, false), false);
+          }
         }
         uint32_t *dst = (uint32_t *)(&sm.hp[0][0] + po[c] + r * HS + x0);  // 8-byte aligned
-        dst[0] = __builtin_bit_cast(uint32_t, o01);
-        dst[1] = __builtin_bit_cast(uint32_t, o23);
+        dst[0] = __builtin_amdgcn_perm((uint32_t)ov[1], (uint32_t)ov[0], 0x05040100u);
+        dst[1] = __builtin_amdgcn_perm((uint32_t)ov[3], (uint32_t)ov[2], 0x05040100u);
       }
     }
   }
