@@ -201,7 +201,7 @@ def main():
         bytes_per_launch = bpc * nctu
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         traffic = None
-        tr_path = os.path.join(ROOT, "profiles", "hbm_traffic_r01.json")
+        tr_path = os.path.join(ROOT, "profiles", "hbm_traffic_r02.json")  # PMC passes of this round's tree
         if os.path.exists(tr_path):
             tr = json.load(open(tr_path)).get(kernel)
             if tr:

@@ -1,11 +1,15 @@
-# rocprofv3 kernel-trace summary + separate PMC passes (FETCH_SIZE, WRITE_SIZE) of the bench command.
+# Round profile of the bench step: rocprofv3 kernel-trace stats, then separate PMC passes
+# (FETCH_SIZE, WRITE_SIZE) for the HBM traffic per launch, then the full default bench run.
+# usage: bash scripts/gpu_profile.sh TAG     (outputs under gpurun_out/prof_TAG_*)
 set -o pipefail
 export TMPDIR=/tmp
-R=$(pwd)
+R=$(pwd); TAG=${1:-r02}
+B="--no-cpu --no-intra --no-ssim --no-1080p --no-sao"
 mkdir -p gpurun_out
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_kt -o kt --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/prof_kt.log 2>&1 &&
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/prof_fetch -o f --output-format csv -- python3 $R/bench.py --steps 2 --warmup 0 --no-cpu > gpurun_out/prof_fetch.log 2>&1 &&
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/prof_write -o w --output-format csv -- python3 $R/bench.py --steps 2 --warmup 0 --no-cpu > gpurun_out/prof_write.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_${TAG}_kt -o kt --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 $B > gpurun_out/prof_${TAG}_kt.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/prof_${TAG}_fetch -o f --output-format csv -- python3 $R/bench.py --steps 2 --warmup 0 $B > gpurun_out/prof_${TAG}_fetch.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/prof_${TAG}_write -o w --output-format csv -- python3 $R/bench.py --steps 2 --warmup 0 $B > gpurun_out/prof_${TAG}_write.log 2>&1 &&
+timeout -k 10 600 python3 bench.py > gpurun_out/bench_${TAG}.log 2>&1
 rc=$?
-find gpurun_out/prof_* -name "*.csv" | head -20
+grep '^{' gpurun_out/bench_${TAG}.log | cut -c1-400
 exit $rc
