@@ -238,16 +238,25 @@ __device__ __forceinline__ int rd_ic_rate(uint32_t level, int rice, bool c1ok, b
 
 // getSigCtxInc (:2717) for square TUs (log2 width = log2 height = LOG2)
 template <int L>
+__device__ __forceinline__ int rd_sig_ctx_raster(int pattern, int first_sig, int raster, int ch);
+template <int L>
 __device__ __forceinline__ int rd_sig_ctx(int pattern, const TuCoding &c, int sp, int ch) {
+  return rd_sig_ctx_raster<L>(pattern, c.first_sig, c.scan[sp], ch);
+}
+// the same with the position's raster index given (a compile-time scan)
+template <int L>
+__device__ __forceinline__ int rd_sig_ctx_raster(int pattern, int first_sig, int raster, int ch) {
   constexpr int LOG2 = L + 2;
   const int single = ch ? 15 : 27;
+  TuCoding c;
+  c.first_sig = first_sig;
   if (c.first_sig == single) return single;
-  const int raster = c.scan[sp];
   const int py = raster >> LOG2, px = raster - (py << LOG2);
   if (px + py == 0) return 0;
   int offset;
   if (L == 0) {
-    offset = kCtxIndMap4x4[4 * py + px];
+    constexpr int8_t map4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};  // ctxIndMap4x4
+    offset = map4[4 * py + px];
   } else {
     int cnt;
     if (pattern == 0) { const int t = (px & 3) + (py & 3); cnt = t >= 3 ? 0 : t >= 1 ? 1 : 2; }
@@ -1511,6 +1520,43 @@ __device__ __forceinline__ int lane_mat(bool dst, int k, int x) {  // wave-unifo
   return kMat[mat_base(L) + k * N + x];
 }
 
+// A lane's whole TU as 16-byte vector accesses (the TU regions are 16-byte aligned: offsets are
+// multiples of NN elements): one memory instruction per 8 residuals / 16 prediction samples
+// instead of one per element, each of which touched 64 different lines across the wave.
+template <int NN>
+__device__ __forceinline__ void lane_ld_i16(const int16_t *p, int32_t (&r)[NN]) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+  for (int k = 0; k < NN / 8; k++) {
+    const uint4 v = q[k];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; e++) { r[8 * k + 2 * e] = (int16_t)(w[e] & 0xffffu); r[8 * k + 2 * e + 1] = (int32_t)w[e] >> 16; }
+  }
+}
+template <int NN>
+__device__ __forceinline__ void lane_ld_u8(const uint8_t *p, int32_t (&r)[NN]) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+  for (int k = 0; k < NN / 16; k++) {
+    const uint4 v = q[k];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 16; e++) r[16 * k + e] = (int32_t)((w[e >> 2] >> (8 * (e & 3))) & 0xffu);
+  }
+}
+template <int NN>
+__device__ __forceinline__ void lane_st_i16(int16_t *p, const int32_t (&r)[NN]) {
+  uint4 *q = reinterpret_cast<uint4 *>(p);
+#pragma unroll
+  for (int k = 0; k < NN / 8; k++) {
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) w[e] = __builtin_amdgcn_perm((uint32_t)r[8 * k + 2 * e + 1], (uint32_t)r[8 * k + 2 * e], 0x05040100u);
+    q[k] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 template <int L>
 __global__ __launch_bounds__(64) void k_tu_fwd_lane(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
                                                     int n, const int16_t *__restrict__ res_in, uint32_t *__restrict__ ldI,
@@ -1520,10 +1566,8 @@ __global__ __launch_bounds__(64) void k_tu_fwd_lane(const hvx_tu_desc *__restric
   if (t >= n) return;
   const hvx_tu_desc d = descs[t];
   if (d.width != N || d.height != N) return;
-  const int16_t *src = res_in + offs[t];
   int32_t r[NN];
-#pragma unroll
-  for (int i = 0; i < NN; i++) r[i] = src[i];
+  lane_ld_i16<NN>(res_in + offs[t], r);
   int32_t c[NN];
   if (d.transform_skip) {  // xTransformSkip
     const int ts = tu_transform_shift(d);
@@ -1568,7 +1612,7 @@ __global__ __launch_bounds__(64) void k_tu_fwd_lane(const hvx_tu_desc *__restric
     ldI[il] = (uint32_t)ld | (cf < 0 ? 0x80000000u : 0u);
     uint32_t cx = 0;
 #pragma unroll
-    for (int p = 0; p < 4; p++) cx |= (uint32_t)(sig_off + rd_sig_ctx<L>(p, cd, sp, ch)) << (6 * p);
+    for (int p = 0; p < 4; p++) cx |= (uint32_t)(sig_off + rd_sig_ctx_raster<L>(p, cd.first_sig, blk, ch)) << (6 * p);
     cxI[il] = cx;
   }
   flags[t] = 1;
@@ -1636,16 +1680,22 @@ __global__ __launch_bounds__(64) void k_tu_fin_lane(const hvx_tu_desc *__restric
         rr[y * N + x] = (int16_t)clip3(-32768, 32767, (acc + 2048) >> 12);
       }
   }
+  lane_st_i16<NN>(res_out + off, rr);
+  int32_t rin[NN];
+  lane_ld_i16<NN>(res_in + off, rin);
   uint32_t sse = 0, z = 0, cs = 0;
 #pragma unroll
   for (int i = 0; i < NN; i++) {
-    const int r = rr[i];
-    res_out[off + i] = (int16_t)r;
-    const int ri = res_in[off + i];
+    const int r = rr[i], ri = rin[i];
     sse += (uint32_t)((ri - r) * (ri - r));
     z += (uint32_t)(ri * ri);
-    if (pred) {
-      const int p = pred[off + i], v = p + r, e = ri + p - (v < 0 ? 0 : v > 255 ? 255 : v);
+  }
+  if (pred) {
+    int32_t pv[NN];
+    lane_ld_u8<NN>(pred + off, pv);
+#pragma unroll
+    for (int i = 0; i < NN; i++) {
+      const int p = pv[i], v = p + rr[i], e = rin[i] + p - (v < 0 ? 0 : v > 255 ? 255 : v);
       cs += (uint32_t)(e * e);
     }
   }
