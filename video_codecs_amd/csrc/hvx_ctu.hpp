@@ -137,39 +137,61 @@ __global__ __launch_bounds__(256) void k_ctu_me_jobs(CtuLayout L, hvx_ctu_params
 // computed once per row of the window, the second stage reads it (the same int16 intermediate,
 // -8192 offset, as TComInterpolationFilter's two-stage path, .cpp:94-257); chroma likewise with
 // the 4-tap filters.  Descriptors are built one per lane and stored as 16-byte vectors.
-template <int S>
-__global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_params P, const uint8_t *__restrict__ cur,
-                                                       const uint8_t *const *__restrict__ refs, int stride,
-                                                       const hvx_me_result *__restrict__ res, int16_t *__restrict__ resid,
-                                                       uint8_t *__restrict__ pred_out,
-                                                       hvx_tu_desc *__restrict__ descs, int64_t *__restrict__ offs,
-                                                       int32_t *__restrict__ est_idx, hvx_cu_result *__restrict__ out,
-                                                       CtuChroma C) {
-  constexpr int d = S == 64 ? 0 : S == 32 ? 1 : S == 16 ? 2 : 3, g = 1 << d, ncu = g * g;
+// what the residual pass reads and writes
+struct CtuMc {
+  CtuLayout L;
+  hvx_ctu_params P;
+  const uint8_t *cur;
+  const uint8_t *const *refs;
+  int stride;
+  const hvx_me_result *res;
+  int16_t *resid;
+  uint8_t *pred_out;
+  hvx_tu_desc *descs;
+  int64_t *offs;
+  int32_t *est_idx;
+  hvx_cu_result *out;
+  CtuChroma C;
+};
+
+template <int S, bool ACQ>
+__device__ void ctu_pred_resid_cu(const CtuMc &M, int ctu, int j, uint8_t *win, int16_t *hs) {
+  const CtuLayout &L = M.L;
+  const hvx_ctu_params &P = M.P;
+  const uint8_t *__restrict__ cur = M.cur;
+  const uint8_t *const *__restrict__ refs = M.refs;
+  const int stride = M.stride;
+  int16_t *__restrict__ resid = M.resid;
+  uint8_t *__restrict__ pred_out = M.pred_out;
+  hvx_tu_desc *__restrict__ descs = M.descs;
+  int64_t *__restrict__ offs = M.offs;
+  int32_t *__restrict__ est_idx = M.est_idx;
+  const CtuChroma &C = M.C;
+  constexpr int d = S == 64 ? 0 : S == 32 ? 1 : S == 16 ? 2 : 3, g = 1 << d;
   constexpr int T = S < 32 ? S : 32, log2 = T == 8 ? 3 : T == 16 ? 4 : 5, ntu = (S / T) * (S / T);
   constexpr int WP = S + 8, WR = S + 7;                    // luma window pitch / rows
   constexpr int Sc = S / 2, Tc = T / 2, CWP = Sc + 4, CWR = Sc + 3;
   static_assert(2 * CWR * CWP <= WR * WP && 2 * CWR * Sc <= WR * S, "chroma windows fit the luma buffers");
-  __shared__ uint8_t win[WR * WP];
-  __shared__ int16_t hs[WR * S];
   const int lane = lane_id();
-  const int ctu = blockIdx.x / ncu, j = (int)(blockIdx.x % ncu);
   const int cuid = ctu * HVX_CUS_PER_CTU + depth_base(d) + j;
   const int x = (ctu % L.nctu_x) * 64 + (j % g) * S, y = (ctu / L.nctu_x) * 64 + (j / g) * S;
   const bool valid = x + S <= P.pic_w && y + S <= P.pic_h;
   int best = 0;
   uint32_t best_cost = 0;
-  const hvx_me_result *r = res + (size_t)cuid * L.nref;
+  const hvx_me_result *r = M.res + (size_t)cuid * L.nref;
   if (valid) {
-    for (int k = 0; k < L.nref; k++)
-      if (k == 0 || r[k].cost < best_cost) { best_cost = r[k].cost; best = k; }
+    for (int k = 0; k < L.nref; k++) {
+      const uint32_t ck = r[k].cost;
+      if (k == 0 || ck < best_cost) { best_cost = ck; best = k; }
+    }
   }
+  const int mvx = valid ? r[best].mv_x : 0, mvy = valid ? r[best].mv_y : 0;
   if (lane == 0) {
     hvx_cu_result o;
     o.valid = valid; o.ref = valid ? best : 0;
-    o.mv_x = valid ? r[best].mv_x : 0; o.mv_y = valid ? r[best].mv_y : 0;
+    o.mv_x = mvx; o.mv_y = mvy;
     o.me_cost = valid ? best_cost : 0; o.sse = 0; o.abs_sum = 0; o.n_tu = valid ? ntu : 0;
-    out[cuid] = o;
+    M.out[cuid] = o;
   }
   // descriptors: per luma TU position the luma TU, then (4:2:0) Cb, Cr and, at depth 3, the
   // transform-skip twins of the 4x4 Cb / Cr TUs (xEstimateInterResidualQT's second mode)
@@ -211,7 +233,6 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
     est_idx[tu] = ei;
   }
   if (!valid) return;
-  const int mvx = r[best].mv_x, mvy = r[best].mv_y;
   {  // luma
     const int fx = mvx & 3, fy = mvy & 3;
     const uint8_t *rp = refs[best] + (y + (mvy >> 2) - 3) * stride + x + (mvx >> 2) - 3;
@@ -307,6 +328,14 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuLayout L, hvx_ctu_para
       }
     }
   }
+}
+
+template <int S>
+__global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuMc M, int ctu0) {
+  constexpr int d = S == 64 ? 0 : S == 32 ? 1 : S == 16 ? 2 : 3, ncu = 1 << (2 * d);
+  __shared__ uint8_t win[(S + 7) * (S + 8)];
+  __shared__ int16_t hs[(S + 7) * S];
+  ctu_pred_resid_cu<S>(M, ctu0 + (int)(blockIdx.x / ncu), (int)(blockIdx.x % ncu), win, hs);
 }
 
 __global__ __launch_bounds__(256) void k_ctu_finalize(CtuLayout L, const int32_t *__restrict__ abs_sum,

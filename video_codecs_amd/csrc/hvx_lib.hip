@@ -761,12 +761,15 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
   const uint8_t *const *cs = (const uint8_t *const *)cur_slot;
   const bool fen = (P.me_flags & HVX_ME_FEN) != 0;
   const int n = L.nctu;
+  CtuMc M;
+  M.L = L; M.P = P; M.cur = d_cur; M.refs = d_refs; M.stride = stride; M.res = res; M.resid = resid; M.pred_out = pred;
+  M.descs = desc; M.offs = off; M.est_idx = est_idx; M.out = d_out; M.C = C;
   auto resid_depth = [&](hipStream_t s, int d) {
     const dim3 grid(n << (2 * d)), blk(64);
-    if (d == 0) hipLaunchKernelGGL(k_ctu_pred_resid<64>, grid, blk, 0, s, L, P, d_cur, d_refs, stride, res, resid, pred, desc, off, est_idx, d_out, C);
-    if (d == 1) hipLaunchKernelGGL(k_ctu_pred_resid<32>, grid, blk, 0, s, L, P, d_cur, d_refs, stride, res, resid, pred, desc, off, est_idx, d_out, C);
-    if (d == 2) hipLaunchKernelGGL(k_ctu_pred_resid<16>, grid, blk, 0, s, L, P, d_cur, d_refs, stride, res, resid, pred, desc, off, est_idx, d_out, C);
-    if (d == 3) hipLaunchKernelGGL(k_ctu_pred_resid<8>, grid, blk, 0, s, L, P, d_cur, d_refs, stride, res, resid, pred, desc, off, est_idx, d_out, C);
+    if (d == 0) hipLaunchKernelGGL(k_ctu_pred_resid<64>, grid, blk, 0, s, M, 0);
+    if (d == 1) hipLaunchKernelGGL(k_ctu_pred_resid<32>, grid, blk, 0, s, M, 0);
+    if (d == 2) hipLaunchKernelGGL(k_ctu_pred_resid<16>, grid, blk, 0, s, M, 0);
+    if (d == 3) hipLaunchKernelGGL(k_ctu_pred_resid<8>, grid, blk, 0, s, M, 0);
   };
   for (int d = 0; d < 4; d++) {
     const int ncu = 1 << (2 * d), nt = L.nctu * ncu * L.nref;

@@ -80,6 +80,22 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// A job of NW waves owns its workgroup when NW > 1; an NW == 1 job may share a workgroup with
+// other single-wave jobs (k_me_ctu8_cu), so its thread index is the lane and its LDS hand-offs
+// are wave-level (no workgroup barrier other waves would have to meet).
+template <int NW>
+__device__ __forceinline__ int me_tid() { return NW > 1 ? (int)threadIdx.x : lane_id(); }
+template <int NW>
+__device__ __forceinline__ void me_sync() {
+  if constexpr (NW > 1) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+}
+
 #define ME_DPP(v, ctrl) ((uint32_t)__builtin_amdgcn_update_dpp((int)0, (int)(v), (ctrl), 0xf, 0xf, false))
 
 // Wave-wide minimum (every lane active): v_min_u32_dpp inside rows of 16 lanes (quad swaps,
@@ -765,7 +781,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
   // the stage geometry is wave-uniform: held in SGPRs, the phase / offset selections below are
   // scalar branches instead of per-tap v_cndmask
   ix = uni(ix); iy = uni(iy); qx0 = uni(qx0); qy0 = uni(qy0);
-  const int w = GENERIC ? j.w : S, h = GENERIC ? j.h : S, lane = lane_id(), wave = threadIdx.x >> 6;
+  const int w = GENERIC ? j.w : S, h = GENERIC ? j.h : S, lane = lane_id(), wave = NW > 1 ? (int)(threadIdx.x >> 6) : 0;
   const bool had = (j.flags & HVX_ME_HADME) != 0;
   // 1. horizontal phases: column c at quarter x = qx0 + (c-1)*step, integer offset ix-1 or ix
   // (oxo 0/1), phase fx.  In the half stage columns 0 and 2 are the same half-sample filter one
@@ -773,7 +789,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
   // columns x0..x0+3) loads the 12 bytes at columns x0+ix-4 .. x0+ix+7 (one buffer load),
   // forms the byte pairs and filters two outputs per v_pk_mad (8-bit taps and samples, 16-bit
   // intermediates: the reference's first stage, offset -8192, fits int16 exactly).
-  __syncthreads();
+  me_sync<NW>();
   int po[3];
   {
     int oxo[3], fxs[3];
@@ -789,7 +805,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
     const int gw = w >> 2, gwp = gw + (shared ? 1 : 0);
     const __amdgpu_buffer_rsrc_t rs = me_plane_rsrc(ref - (j.pu_y * stride + j.pu_x), stride, j.pic_h);
     const uint32_t base = (uint32_t)((HVX_PLANE_MARGIN + j.pu_y + iy - 4) * stride + HVX_PLANE_MARGIN + j.pu_x + ix - 4);
-    for (int k = threadIdx.x; k < (h + 8) * gwp; k += 64 * NW) {
+    for (int k = me_tid<NW>(); k < (h + 8) * gwp; k += 64 * NW) {
       const int r = k / gwp, x0 = (k - r * gwp) << 2;
       const uint32_t a = base + (uint32_t)(r * stride + x0);
       const me_v4u q = __builtin_amdgcn_raw_buffer_load_b128(rs, a & ~3u, 0, 0);
@@ -830,7 +846,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
       }
     }
   }
-  __syncthreads();
+  me_sync<NW>();
   // 2. the 9 candidates' costs (SATD or SAD + MV cost)
   const bool xl = had && (!GENERIC || ((w % 8 == 0) && (h % 8 == 0)));
   const int tw = w >> 3, nt = (w * h) >> 6;
@@ -937,7 +953,7 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
     d += me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
     if (lane == 0) sm.cost[i] = d;
   }
-  __syncthreads();
+  me_sync<NW>();
   // 3. reference order, strict '<'
   uint32_t best = 0xFFFFFFFFu;
   bi = 0;
@@ -987,7 +1003,7 @@ __device__ void me_frac_refine(const hvx_me_job &j, const uint8_t *ref, int stri
   const uint32_t mv_bits = eg_bits(fmx - j.pred_x) + eg_bits(fmy - j.pred_y);
   const uint32_t bits = (uint32_t)j.bits_in + mv_bits;
   const uint32_t lam = j.lambda_motion;
-  if (threadIdx.x == 0) {
+  if (me_tid<NW>() == 0) {
     hvx_me_result r;
     r.mv_int_x = ix; r.mv_int_y = iy; r.sad_int = sad_int;
     r.half_x = hx; r.half_y = hy; r.qtr_x = qx; r.qtr_y = qy; r.cost_frac = cost;
@@ -1026,26 +1042,23 @@ __global__ __launch_bounds__(64 * NW) void k_me_frac_ctu(const uint8_t *const *_
 // the 32/16/8 depths, where the separate kernels' per-job reloads dominated.  The 8x8 form is
 // held to 72 VGPRs (7 waves per SIMD instead of 6, no spill): its launch is 8% shorter; the same
 // bound on the 16x16 form spills and slows the step.
+// one (CU, reference) job of the CTU pass: TZ integer search then the fractional refinement in
+// the same workgroup; writes out[slot] (a defined zero result for a CU outside the picture)
 template <int S, int SUB, int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(S == 8 ? 7 : 1))) void k_me_ctu(const uint8_t *const *__restrict__ cur_planes,
-                                                   const uint8_t *const *__restrict__ ref_planes, int stride,
-                                                   const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
-                                                   int nref, int ncu, int first) {
-  __shared__ MeFracSmem<S, NW> sm;
-  __shared__ uint32_t red[2 * kMeMaxRanges * NW];
-  const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
-  const hvx_me_job j = jobs[slot];
-  if (j.w > 0 && (j.w != S || j.h != S)) return;
+__device__ __forceinline__ void me_ctu_job(const uint8_t *const *__restrict__ cur_planes,
+                                           const uint8_t *const *__restrict__ ref_planes, int stride,
+                                           const hvx_me_job &j, hvx_me_result *__restrict__ out, size_t slot,
+                                           MeFracSmem<S, NW> &sm, uint32_t *red) {
   if (j.w <= 0 || j.h <= 0) {
-    if (threadIdx.x == 0) { hvx_me_result z; memset(&z, 0, sizeof(z)); out[slot] = z; }
+    if (me_tid<NW>() == 0) { hvx_me_result z; memset(&z, 0, sizeof(z)); out[slot] = z; }
     return;
   }
   const uint8_t *cur = cur_planes[j.cur_idx] + j.pu_y * stride + j.pu_x;
-  for (int k = threadIdx.x; k < S * S; k += HVX_WAVE * NW) {
+  for (int k = me_tid<NW>(); k < S * S; k += HVX_WAVE * NW) {
     const int y = k / S, x = k - y * S;
     sm.org[y * S + x] = cur[y * stride + x];
   }
-  __syncthreads();
+  me_sync<NW>();
   MeInt m;
   m.org = sm.org; m.red = red; m.par = 0; m.os = S;
   me_ref_setup(m, j, ref_planes[j.ref_idx], stride);
@@ -1057,10 +1070,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(S == 8 
   me_tz<S, SUB, NW>(j, m);
   const uint32_t sad_int = m.best_sad - me_mv_cost(m.lam, m.px, m.py, 2, m.best_x, m.best_y);
 #ifdef HVX_EXP_NOFRAC
-  if (threadIdx.x == 0) { hvx_me_result r{}; r.mv_int_x = m.best_x; r.mv_int_y = m.best_y; r.sad_int = sad_int; r.cost = sad_int; out[slot] = r; }
+  if (me_tid<NW>() == 0) { hvx_me_result r{}; r.mv_int_x = m.best_x; r.mv_int_y = m.best_y; r.sad_int = sad_int; r.cost = sad_int; out[slot] = r; }
   return;
 #endif
   me_frac_refine<S, NW, false, uint8_t>(j, m.ref, stride, m.best_x, m.best_y, sad_int, sm, out + slot);
+}
+
+template <int S, int SUB, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(S == 8 ? 7 : 1))) void k_me_ctu(const uint8_t *const *__restrict__ cur_planes,
+                                                   const uint8_t *const *__restrict__ ref_planes, int stride,
+                                                   const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
+                                                   int nref, int ncu, int first) {
+  __shared__ MeFracSmem<S, NW> sm;
+  __shared__ uint32_t red[2 * kMeMaxRanges * NW];
+  const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
+  const hvx_me_job j = jobs[slot];
+  if (j.w > 0 && (j.w != S || j.h != S)) return;
+  me_ctu_job<S, SUB, NW>(cur_planes, ref_planes, stride, j, out, slot, sm, red);
 }
 
 // ======================================================================================
