@@ -154,7 +154,8 @@ struct CtuMc {
   CtuChroma C;
 };
 
-template <int S, bool ACQ>
+// one CU of size S: the body of k_ctu_pred_resid<S> (win / hs: its LDS)
+template <int S>
 __device__ void ctu_pred_resid_cu(const CtuMc &M, int ctu, int j, uint8_t *win, int16_t *hs) {
   const CtuLayout &L = M.L;
   const hvx_ctu_params &P = M.P;
