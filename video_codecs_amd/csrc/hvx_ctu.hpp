@@ -154,6 +154,54 @@ struct CtuMc {
   CtuChroma C;
 };
 
+// TU descriptor `kind` (0 luma, 1 Cb, 2 Cr, 3 / 4 the Cb / Cr transform-skip twins at depth 3)
+// of luma TU position t of CU (ctu, j) of size S (hvxo_ctu_tu_desc semantics), stored as 16-byte
+// vectors, with the TU's residual offset and estBits table index
+template <int S>
+__device__ __forceinline__ void ctu_desc(const CtuMc &M, int ctu, int j, bool valid, int t, int kind) {
+  const CtuLayout &L = M.L;
+  const hvx_ctu_params &P = M.P;
+  hvx_tu_desc *__restrict__ descs = M.descs;
+  int64_t *__restrict__ offs = M.offs;
+  int32_t *__restrict__ est_idx = M.est_idx;
+  constexpr int d = S == 64 ? 0 : S == 32 ? 1 : S == 16 ? 2 : 3;
+  constexpr int T = S < 32 ? S : 32, log2 = T == 8 ? 3 : T == 16 ? 4 : 5, Tc = T / 2;
+  const int c = kind == 0 ? 0 : 1 + (kind - 1) % 2;
+  hvx_tu_desc td;
+  memset(&td, 0, sizeof(td));
+  td.slice_type = P.slice_type;
+  td.sign_hiding = 1; td.use_rdoq = 1; td.use_rdoq_ts = 1;
+  td.pps_tskip = 1;  // TransformSkip=1: 4x4 TUs code transform_skip_flag
+  td.max_log2_tr_range = 15; td.bit_depth = 8;
+  td.tr_idx = S > 32 ? 1 : 0;
+  int tu, ei;
+  if (c == 0) {
+    tu = ctu_tu_index(L, ctu, d, j, t);
+    td.width = td.height = valid ? T : 0;  // width 0: no size class picks it up
+    td.log2_size = log2;
+    td.qp_per = P.qp / 6; td.qp_rem = P.qp % 6;
+    td.lambda = P.lambda;
+    ei = log2 - 2;
+  } else {  // half size, chroma QP and RDOQ lambda, chroma cbf context = transform depth
+    tu = ctu_tu_index(L, ctu, d, j, t, c);
+    td.comp = c;
+    td.width = td.height = valid ? Tc : 0;
+    td.log2_size = log2 - 1;
+    td.ctx_qt_cbf = S > 32 ? 1 : 0;
+    td.qp_per = P.qp_chroma / 6; td.qp_rem = P.qp_chroma % 6;
+    td.lambda = P.lambda_chroma;
+    ei = 4 + log2 - 3;
+    if (kind >= 3) { tu = ctu_tu_ts(L, tu); td.transform_skip = 1; ei = 4; }
+  }
+  static_assert(sizeof(hvx_tu_desc) % 16 == 0, "descriptor stored as 16-byte vectors");
+  const uint4 *src = reinterpret_cast<const uint4 *>(&td);
+  uint4 *dst = reinterpret_cast<uint4 *>(descs + tu);
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(hvx_tu_desc) / 16); q++) dst[q] = src[q];
+  offs[tu] = ctu_tu_offset(L, tu);
+  est_idx[tu] = ei;
+}
+
 // one CU of size S: the body of k_ctu_pred_resid<S> (win / hs: its LDS)
 template <int S>
 __device__ void ctu_pred_resid_cu(const CtuMc &M, int ctu, int j, uint8_t *win, int16_t *hs) {
@@ -197,42 +245,7 @@ __device__ void ctu_pred_resid_cu(const CtuMc &M, int ctu, int j, uint8_t *win, 
   // descriptors: per luma TU position the luma TU, then (4:2:0) Cb, Cr and, at depth 3, the
   // transform-skip twins of the 4x4 Cb / Cr TUs (xEstimateInterResidualQT's second mode)
   const int nper = C.on ? (d == 3 ? 5 : 3) : 1;
-  for (int k = lane; k < ntu * nper; k += HVX_WAVE) {
-    const int t = k / nper, kind = k % nper, c = kind == 0 ? 0 : 1 + (kind - 1) % 2;
-    hvx_tu_desc td;
-    memset(&td, 0, sizeof(td));
-    td.slice_type = P.slice_type;
-    td.sign_hiding = 1; td.use_rdoq = 1; td.use_rdoq_ts = 1;
-    td.pps_tskip = 1;  // TransformSkip=1: 4x4 TUs code transform_skip_flag
-    td.max_log2_tr_range = 15; td.bit_depth = 8;
-    td.tr_idx = S > 32 ? 1 : 0;
-    int tu, ei;
-    if (c == 0) {
-      tu = ctu_tu_index(L, ctu, d, j, t);
-      td.width = td.height = valid ? T : 0;  // width 0: no size class picks it up
-      td.log2_size = log2;
-      td.qp_per = P.qp / 6; td.qp_rem = P.qp % 6;
-      td.lambda = P.lambda;
-      ei = log2 - 2;
-    } else {  // half size, chroma QP and RDOQ lambda, chroma cbf context = transform depth
-      tu = ctu_tu_index(L, ctu, d, j, t, c);
-      td.comp = c;
-      td.width = td.height = valid ? Tc : 0;
-      td.log2_size = log2 - 1;
-      td.ctx_qt_cbf = S > 32 ? 1 : 0;
-      td.qp_per = P.qp_chroma / 6; td.qp_rem = P.qp_chroma % 6;
-      td.lambda = P.lambda_chroma;
-      ei = 4 + log2 - 3;
-      if (kind >= 3) { tu = ctu_tu_ts(L, tu); td.transform_skip = 1; ei = 4; }
-    }
-    static_assert(sizeof(hvx_tu_desc) % 16 == 0, "descriptor stored as 16-byte vectors");
-    const uint4 *src = reinterpret_cast<const uint4 *>(&td);
-    uint4 *dst = reinterpret_cast<uint4 *>(descs + tu);
-#pragma unroll
-    for (int q = 0; q < (int)(sizeof(hvx_tu_desc) / 16); q++) dst[q] = src[q];
-    offs[tu] = ctu_tu_offset(L, tu);
-    est_idx[tu] = ei;
-  }
+  for (int k = lane; k < ntu * nper; k += HVX_WAVE) ctu_desc<S>(M, ctu, j, valid, k / nper, k % nper);
   if (!valid) return;
   {  // luma
     const int fx = mvx & 3, fy = mvy & 3;
@@ -337,6 +350,159 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuMc M, int ctu0) {
   __shared__ uint8_t win[(S + 7) * (S + 8)];
   __shared__ int16_t hs[(S + 7) * S];
   ctu_pred_resid_cu<S>(M, ctu0 + (int)(blockIdx.x / ncu), (int)(blockIdx.x % ncu), win, hs);
+}
+
+// Depth 3 (8x8 CUs), FOUR CUs per wave (one wave per CU left most of the launch waiting on two
+// dependent memory round trips with little work).  The MC is branch-free: the two-stage form with
+// the phase-0 filters ({0,0,0,64,0,0,0,0} / {0,64,0,0}) gives exactly the reference's
+// one-stage and copy cases ((64X + 2048) >> 12 == (X + 32) >> 6, (4096b + 2048) >> 12 == b), the
+// first stage is v_dot4_i32_i8 on sign-biased window bytes (b - 128: the -8192 offset), the
+// second v_dot2_i32_i16 on int16 tap pairs.
+__global__ __launch_bounds__(64) void k_ctu_pred_resid8q(CtuMc M) {
+  constexpr int NC = 4;
+  __shared__ uint32_t winY[NC][15 * 4];      // 15 rows x 16 bytes (15 used), biased
+  __shared__ int16_t hsY[NC][15 * 8];
+  __shared__ uint32_t winC[2 * NC][7 * 2];   // 7 rows x 8 bytes (7 used), biased
+  __shared__ int16_t hsC[2 * NC][7 * 4];
+  const CtuLayout &L = M.L;
+  const hvx_ctu_params &P = M.P;
+  const CtuChroma &C = M.C;
+  const int lane = lane_id(), ctu = (int)(blockIdx.x >> 4), j0 = (int)(blockIdx.x & 15) * NC;
+  const int stride = M.stride;
+  int x[NC], y[NC], bref[NC], mvx[NC], mvy[NC];
+  bool valid[NC];
+#pragma unroll
+  for (int c = 0; c < NC; c++) {  // wave-uniform: position, validity, first-minimum reference
+    const int j = j0 + c;
+    x[c] = (ctu % L.nctu_x) * 64 + (j % 8) * 8;
+    y[c] = (ctu / L.nctu_x) * 64 + (j / 8) * 8;
+    valid[c] = x[c] + 8 <= P.pic_w && y[c] + 8 <= P.pic_h;
+    const hvx_me_result *r = M.res + ((size_t)ctu * HVX_CUS_PER_CTU + 21 + j) * L.nref;
+    int best = 0;
+    uint32_t bc = 0;
+    if (valid[c])
+      for (int k = 0; k < L.nref; k++) {
+        const uint32_t ck = r[k].cost;
+        if (k == 0 || ck < bc) { bc = ck; best = k; }
+      }
+    bref[c] = best;
+    mvx[c] = valid[c] ? r[best].mv_x : 0;
+    mvy[c] = valid[c] ? r[best].mv_y : 0;
+    if (lane == c) {
+      hvx_cu_result o;
+      o.valid = valid[c]; o.ref = best; o.mv_x = mvx[c]; o.mv_y = mvy[c];
+      o.me_cost = valid[c] ? bc : 0; o.sse = 0; o.abs_sum = 0; o.n_tu = valid[c] ? 1 : 0;
+      M.out[(size_t)ctu * HVX_CUS_PER_CTU + 21 + j] = o;
+    }
+  }
+  const int nper = C.on ? 5 : 1;
+  if (lane < NC * nper) {
+    const int c = lane / nper;
+    ctu_desc<8>(M, ctu, j0 + c, c == 0 ? valid[0] : c == 1 ? valid[1] : c == 2 ? valid[2] : valid[3], 0, lane % nper);
+  }
+  // luma: windows (rows y-3 .. y+11, columns x-3 .. x+11), first stage on all 15 rows, second stage
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    if (!valid[c]) continue;
+    const uint8_t *rp = M.refs[bref[c]] + (y[c] + (mvy[c] >> 2) - 3) * stride + x[c] + (mvx[c] >> 2) - 3;
+    uint8_t *w = reinterpret_cast<uint8_t *>(winY[c]);
+    for (int k = lane; k < 225; k += HVX_WAVE) {
+      const int rr = k / 15, cc = k - rr * 15;
+      w[rr * 16 + cc] = rp[rr * stride + cc] ^ 0x80;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    if (!valid[c]) continue;
+    const int fx = mvx[c] & 3;
+    const int clo = (int)kLumaTap4[fx][0], chi = (int)kLumaTap4[fx][1];
+    for (int k = lane; k < 120; k += HVX_WAVE) {
+      const int rr = k >> 3, xx = k & 7;
+      const uint32_t *w = winY[c] + rr * 4 + (xx >> 2);
+      const uint32_t sh = xx & 3, lo = __builtin_amdgcn_alignbyte(w[1], w[0], sh), hi = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+      hsY[c][rr * 8 + xx] = (int16_t)__builtin_amdgcn_sdot4((int)lo, clo, __builtin_amdgcn_sdot4((int)hi, chi, 0, false), false);
+    }
+  }
+  __syncthreads();
+  {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    const int yy = lane >> 3, xx = lane & 7;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      if (!valid[c]) continue;
+      const int fy = mvy[c] & 3;
+      int s = (1 << 11) + (8192 << 6);
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const s2 pr = {hsY[c][(yy + 2 * u) * 8 + xx], hsY[c][(yy + 2 * u + 1) * 8 + xx]};
+        s = __builtin_amdgcn_sdot2(pr, __builtin_bit_cast(s2, kLumaPairs[fy][u]), s, false);
+      }
+      const int pred = clip_pel(s >> 12);
+      const int64_t o = ctu_tu_offset(L, ctu_tu_index(L, ctu, 3, j0 + c, 0)) + lane;
+      M.resid[o] = (int16_t)((int)M.cur[(y[c] + yy) * stride + x[c] + xx] - pred);
+      M.pred_out[o] = (uint8_t)pred;
+    }
+  }
+  if (!C.on) return;
+  // Cb, Cr: windows (rows yc-1 .. yc+5, columns xc-1 .. xc+5 at the 1/8-sample MV), 4-tap stages
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    if (!valid[c]) continue;
+    const int xc = x[c] / 2, yc = y[c] / 2, wo = (yc + (mvy[c] >> 3) - 1) * C.stride + xc + (mvx[c] >> 3) - 1;
+#pragma unroll
+    for (int comp = 0; comp < 2; comp++) {
+      const uint8_t *src = C.refs[comp * L.nref + bref[c]] + wo;
+      uint8_t *w = reinterpret_cast<uint8_t *>(winC[2 * c + comp]);
+      if (lane < 49) {
+        const int rr = lane / 7, cc = lane - rr * 7;
+        w[rr * 8 + cc] = src[rr * C.stride + cc] ^ 0x80;
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    if (!valid[c]) continue;
+    const int cw = (int)kChromaTap4[mvx[c] & 7];
+#pragma unroll
+    for (int comp = 0; comp < 2; comp++)
+      if (lane < 28) {
+        const int rr = lane >> 2, xx = lane & 3;
+        const uint32_t *w = winC[2 * c + comp] + rr * 2;
+        hsC[2 * c + comp][rr * 4 + xx] = (int16_t)__builtin_amdgcn_sdot4((int)__builtin_amdgcn_alignbyte(w[1], w[0], xx), cw, 0, false);
+      }
+  }
+  __syncthreads();
+  {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    const int yy = (lane >> 2) & 3, xx = lane & 3, comp = (lane >> 4) & 1, cq = lane >> 5;  // 2 CUs per pass
+#pragma unroll
+    for (int p = 0; p < NC / 2; p++) {
+      const int c = 2 * p + cq;
+      const bool v = c == 0 ? valid[0] : c == 1 ? valid[1] : c == 2 ? valid[2] : valid[3];
+      if (!v) continue;
+      const int cmx = c == 0 ? mvx[0] : c == 1 ? mvx[1] : c == 2 ? mvx[2] : mvx[3];
+      const int cmy = c == 0 ? mvy[0] : c == 1 ? mvy[1] : c == 2 ? mvy[2] : mvy[3];
+      const int cx = c == 0 ? x[0] : c == 1 ? x[1] : c == 2 ? x[2] : x[3];
+      const int cy = c == 0 ? y[0] : c == 1 ? y[1] : c == 2 ? y[2] : y[3];
+      (void)cmx;
+      const int fy = cmy & 7;
+      const int16_t *h = hsC[2 * c + comp];
+      int s = (1 << 11) + (8192 << 6);
+      const s2 p0 = {h[yy * 4 + xx], h[(yy + 1) * 4 + xx]}, p1 = {h[(yy + 2) * 4 + xx], h[(yy + 3) * 4 + xx]};
+      s = __builtin_amdgcn_sdot2(p0, __builtin_bit_cast(s2, kChromaPairs[fy][0]), s, false);
+      s = __builtin_amdgcn_sdot2(p1, __builtin_bit_cast(s2, kChromaPairs[fy][1]), s, false);
+      const int pred = clip_pel(s >> 12);
+      const int tu = ctu_tu_index(L, ctu, 3, j0 + c, 0, comp + 1);
+      const int16_t rv = (int16_t)((int)C.cur[comp][(cy / 2 + yy) * C.stride + cx / 2 + xx] - pred);
+      const int64_t o = ctu_tu_offset(L, tu) + yy * 4 + xx, ot = ctu_tu_offset(L, ctu_tu_ts(L, tu)) + yy * 4 + xx;
+      M.resid[o] = rv;
+      M.pred_out[o] = (uint8_t)pred;
+      M.resid[ot] = rv;
+      M.pred_out[ot] = (uint8_t)pred;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_ctu_finalize(CtuLayout L, const int32_t *__restrict__ abs_sum,

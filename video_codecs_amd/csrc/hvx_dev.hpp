@@ -44,6 +44,13 @@ __constant__ uint32_t kLumaTap4[4][2] = {{tap4(0, 0, 0, 64), tap4(0, 0, 0, 0)},
                                          {tap4(-1, 4, -10, 58), tap4(17, -5, 1, 0)},
                                          {tap4(-1, 4, -11, 40), tap4(40, -11, 4, -1)},
                                          {tap4(0, 1, -5, 17), tap4(58, -10, 4, -1)}};
+// the chroma taps packed for v_dot4_i32_i8 (byte k = tap k) and as int16 pairs (taps 0,1 | 2,3)
+__constant__ uint32_t kChromaTap4[8] = {tap4(0, 64, 0, 0),   tap4(-2, 58, 10, -2), tap4(-4, 54, 16, -2), tap4(-6, 46, 28, -4),
+                                        tap4(-4, 36, 36, -4), tap4(-4, 28, 46, -6), tap4(-2, 16, 54, -4), tap4(-2, 10, 58, -2)};
+__constant__ uint32_t kChromaPairs[8][2] = {
+    {luma_pair(0, 64), luma_pair(0, 0)},   {luma_pair(-2, 58), luma_pair(10, -2)}, {luma_pair(-4, 54), luma_pair(16, -2)},
+    {luma_pair(-6, 46), luma_pair(28, -4)}, {luma_pair(-4, 36), luma_pair(36, -4)}, {luma_pair(-4, 28), luma_pair(46, -6)},
+    {luma_pair(-2, 16), luma_pair(54, -4)}, {luma_pair(-2, 10), luma_pair(58, -2)}};
 __constant__ int8_t kChromaFilter[8][4] = {{0, 64, 0, 0},   {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
                                            {-4, 36, 36, -4}, {-4, 28, 46, -6}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
 

@@ -769,7 +769,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     if (d == 0) hipLaunchKernelGGL(k_ctu_pred_resid<64>, grid, blk, 0, s, M, 0);
     if (d == 1) hipLaunchKernelGGL(k_ctu_pred_resid<32>, grid, blk, 0, s, M, 0);
     if (d == 2) hipLaunchKernelGGL(k_ctu_pred_resid<16>, grid, blk, 0, s, M, 0);
-    if (d == 3) hipLaunchKernelGGL(k_ctu_pred_resid<8>, grid, blk, 0, s, M, 0);
+    if (d == 3) hipLaunchKernelGGL(k_ctu_pred_resid8q, dim3(n * 16), blk, 0, s, M);  // four 8x8 CUs per wave
   };
   for (int d = 0; d < 4; d++) {
     const int ncu = 1 << (2 * d), nt = L.nctu * ncu * L.nref;
