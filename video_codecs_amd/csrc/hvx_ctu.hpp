@@ -579,53 +579,61 @@ struct DepthMap {
   }
 };
 
-template <int D>
-__device__ bool dec_node(const DecideArgs &A, int ctu, int cx, int cy, DepthMap &dm, uint32_t &bits, uint32_t &dist,
-                         float &sdist) {
+// the CTU's leaf records held in lanes: CU ci in lane ci % 64 of register ci / 64
+struct DecLanes {
+  uint32_t valid[2], bits[2], dist[2], ssim[2];
+};
+// the walk's results, written back into the same lanes
+struct DecOuts {
+  uint32_t bb[2], bd[2], bs[2];
+  uint64_t split[2];  // bit ci % 64 of word ci / 64 (wave-uniform)
+};
+
+// TEncCu::xCompressCU's depth recursion for CU (D, CX, CY) of a CTU as wave-uniform code: the
+// node's leaf record comes from its lane by v_readlane (constant lane: the recursion is unrolled
+// at compile time), so the chain of decisions has no memory access on it.  rf[ctx][f] =
+// split_cu_flag f's rate under context ctx.
+template <int D, int CX, int CY>
+__device__ __forceinline__ bool dec_walk(const DecideArgs &A, const uint32_t (&rf)[3][2], int ctu, DepthMap &dm,
+                                         const DecLanes &V, DecOuts &O, uint32_t &bits, uint32_t &dist, float &sdist) {
   constexpr int g = 1 << D, S = 64 >> D, n8 = S / 8;
-  const int j = cy * g + cx, ci = (D == 0 ? 0 : D == 1 ? 1 : D == 2 ? 5 : 21) + j;
-  const int x = (ctu % A.L.nctu_x) * 64 + cx * S, y = (ctu / A.L.nctu_x) * 64 + cy * S;
+  constexpr int CI = (D == 0 ? 0 : D == 1 ? 1 : D == 2 ? 5 : 21) + CY * g + CX, H = CI / 64, LN = CI % 64;
+  const int x = (ctu % A.L.nctu_x) * 64 + CX * S, y = (ctu / A.L.nctu_x) * 64 + CY * S;
   if (x >= A.pic_w || y >= A.pic_h) return false;
-  const int x8 = cx * n8, y8 = cy * n8;
-  const size_t cuid = (size_t)ctu * HVX_CUS_PER_CTU + ci;
-  const hvx_cu_result cu = A.cu[cuid];
-  hvx_cu_decision o;
-  o.coef_frac = 0; o.bits = 0; o.dist = 0; o.leaf = 0; o.cbf = 0; o.pad_ = 0; o.best_ssim_dist = 0.0f;
+  constexpr int x8 = CX * n8, y8 = CY * n8;
+  const bool valid = __builtin_amdgcn_readlane((int)V.valid[H], LN) != 0;
   const int ctx = (x8 > 0 && dm.at(x8 - 1, y8) > D) + (y8 > 0 && dm.at(x8, y8 - 1) > D);
-  const int sfs = D < 3 ? A.st[ctx] : 0;
   uint32_t lb = 0, ld = 0;
   float ls = 0.0f;
-  o.ssim_dist = 0.0f;
-  if (cu.valid) {
-    const hvx_cu_decision lf = A.dec[cuid];  // the leaf evaluation (k_ctu_leaf)
-    o.coef_frac = lf.coef_frac; o.bits = lf.bits; o.dist = lf.dist; o.cbf = lf.cbf; o.ssim_dist = lf.ssim_dist;
-    lb = o.bits + (D < 3 ? ((uint32_t)A.eb[sfs ^ 0] >> 15) : 0u);
-    ld = o.dist;
-    ls = o.ssim_dist;
+  if (valid) {
+    lb = (uint32_t)__builtin_amdgcn_readlane((int)V.bits[H], LN) + (D < 3 ? rf[ctx][0] : 0u);
+    ld = (uint32_t)__builtin_amdgcn_readlane((int)V.dist[H], LN);
+    ls = __int_as_float(__builtin_amdgcn_readlane((int)V.ssim[H], LN));
   }
-  bool split = !cu.valid;
+  bool split = !valid;
   uint32_t sb = 0, sd = 0;
   float ss = 0.0f;
   if constexpr (D < 3) {
-    for (int k = 0; k < 4; k++) {
-      uint32_t b, dd;
-      float sv;
-      if (dec_node<D + 1>(A, ctu, 2 * cx + (k & 1), 2 * cy + (k >> 1), dm, b, dd, sv)) { sb += b; sd += dd; ss += sv; }
-    }
-    if (cu.valid) {
-      sb += (uint32_t)A.eb[sfs ^ 1] >> 15;
+    uint32_t b, dd;
+    float sv;
+    if (dec_walk<D + 1, 2 * CX, 2 * CY>(A, rf, ctu, dm, V, O, b, dd, sv)) { sb += b; sd += dd; ss += sv; }
+    if (dec_walk<D + 1, 2 * CX + 1, 2 * CY>(A, rf, ctu, dm, V, O, b, dd, sv)) { sb += b; sd += dd; ss += sv; }
+    if (dec_walk<D + 1, 2 * CX, 2 * CY + 1>(A, rf, ctu, dm, V, O, b, dd, sv)) { sb += b; sd += dd; ss += sv; }
+    if (dec_walk<D + 1, 2 * CX + 1, 2 * CY + 1>(A, rf, ctu, dm, V, O, b, dd, sv)) { sb += b; sd += dd; ss += sv; }
+    if (valid) {
+      sb += rf[ctx][1];
       if (dec_cu_cost(A, sb, sd, ss) < dec_cu_cost(A, lb, ld, ls)) split = true;
     }
   }
-  o.split = split;
-  o.best_bits = split ? sb : lb;
-  o.best_dist = split ? sd : ld;
-  o.best_ssim_dist = split ? ss : ls;
+  bits = split ? sb : lb;
+  dist = split ? sd : ld;
+  sdist = split ? ss : ls;
+  if (split) O.split[H] |= 1ull << LN;
+  const bool me = lane_id() == LN;  // this node's lane takes its results
+  O.bb[H] = me ? bits : O.bb[H];
+  O.bd[H] = me ? dist : O.bd[H];
+  O.bs[H] = me ? __float_as_uint(sdist) : O.bs[H];
   if (!split) dm.fill(x8, y8, n8, D);
-  A.dec[cuid] = o;
-  bits = o.best_bits;
-  dist = o.best_dist;
-  sdist = o.best_ssim_dist;
   return true;
 }
 
@@ -751,36 +759,63 @@ __global__ __launch_bounds__(64) void k_ctu_leaf_ssim(DecideArgs A, const uint8_
   }
 }
 
+// One WAVE per CTU: the 85 leaf records (k_ctu_leaf) and CU results are loaded lane-parallel, the
+// depth recursion (dec_walk) runs wave-uniform on them, and the decisions are stored lane-parallel.
 __global__ __launch_bounds__(64) void k_ctu_decide(DecideArgs A) {
-  const int ctu = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ctu >= A.L.nctu) return;
-  // CUs wholly outside the picture keep a zero record
-  for (int ci = 0; ci < HVX_CUS_PER_CTU; ci++) {
-    int d, j, S, g;
-    cu_geom(ci, d, j, S, g);
-    const int x = (ctu % A.L.nctu_x) * 64 + (j % g) * S, y = (ctu / A.L.nctu_x) * 64 + (j / g) * S;
-    if (x >= A.pic_w || y >= A.pic_h) A.dec[(size_t)ctu * HVX_CUS_PER_CTU + ci] = hvx_cu_decision{0, 0, 0, 0, 0, 0, 0, 0, 0.0f, 0.0f, 0};
+  const int ctu = blockIdx.x, lane = lane_id();
+  DecLanes V;
+  hvx_cu_decision lf[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int ci = lane + 64 * h;
+    const size_t cuid = (size_t)ctu * HVX_CUS_PER_CTU + ci;
+    lf[h] = hvx_cu_decision{0, 0, 0, 0, 0, 0, 0, 0, 0.0f, 0.0f, 0};
+    V.valid[h] = 0;
+    if (ci < HVX_CUS_PER_CTU && A.cu[cuid].valid) {
+      lf[h] = A.dec[cuid];
+      V.valid[h] = 1;
+    }
+    V.bits[h] = lf[h].bits; V.dist[h] = lf[h].dist; V.ssim[h] = __float_as_uint(lf[h].ssim_dist);
+  }
+  uint32_t rf[3][2];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    const int st = A.st[c];
+    rf[c][0] = (uint32_t)A.eb[st ^ 0] >> 15;
+    rf[c][1] = (uint32_t)A.eb[st ^ 1] >> 15;
   }
   DepthMap dm;
+  DecOuts O = {};
   uint32_t b, d;
   float sd;
-  dec_node<0>(A, ctu, 0, 0, dm, b, d, sd);
-  // the final tree, top-down: leaf = reached (root, or child of a reached splitting CU), in the
-  // picture, not splitting; reached set as an 85-bit mask
-  uint64_t r_lo = 1, r_hi = 0;
-  for (int ci = 0; ci < HVX_CUS_PER_CTU; ci++) {
-    const bool reached = ci < 64 ? ((r_lo >> ci) & 1) : ((r_hi >> (ci - 64)) & 1);
+  dec_walk<0, 0, 0>(A, rf, ctu, dm, V, O, b, d, sd);
+  // store: leaf = in the picture, not splitting, and every ancestor splits
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int ci = lane + 64 * h;
+    if (ci >= HVX_CUS_PER_CTU) continue;
     int dd, j, S, g;
     cu_geom(ci, dd, j, S, g);
     const int x = (ctu % A.L.nctu_x) * 64 + (j % g) * S, y = (ctu / A.L.nctu_x) * 64 + (j / g) * S;
-    if (!reached || x >= A.pic_w || y >= A.pic_h) continue;
-    hvx_cu_decision &o = A.dec[(size_t)ctu * HVX_CUS_PER_CTU + ci];
-    if (!o.split) { o.leaf = 1; continue; }
-    if (dd == 3) continue;
-    for (int k = 0; k < 4; k++) {
-      const int c = depth_base(dd + 1) + (2 * (j / g) + (k >> 1)) * (2 * g) + 2 * (j % g) + (k & 1);
-      if (c < 64) r_lo |= 1ull << c; else r_hi |= 1ull << (c - 64);
+    hvx_cu_decision o = hvx_cu_decision{0, 0, 0, 0, 0, 0, 0, 0, 0.0f, 0.0f, 0};
+    if (x < A.pic_w && y < A.pic_h) {
+      const bool sp = (O.split[h] >> (ci % 64)) & 1;
+      bool reached = true;
+      int pj = j, pg = g;
+      for (int pd = dd - 1; pd >= 0; pd--) {  // the ancestors, parent first
+        pj = ((pj / pg) >> 1) * (pg >> 1) + ((pj % pg) >> 1);
+        pg >>= 1;
+        const int pci = depth_base(pd) + pj;
+        reached = reached && ((O.split[pci / 64] >> (pci % 64)) & 1);
+      }
+      o = lf[h];
+      o.split = sp;
+      o.leaf = reached && !sp;
+      o.best_bits = O.bb[h];
+      o.best_dist = O.bd[h];
+      o.best_ssim_dist = __uint_as_float(O.bs[h]);
     }
+    A.dec[(size_t)ctu * HVX_CUS_PER_CTU + ci] = o;
   }
 }
 

@@ -950,7 +950,7 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
   if (P.rd_metric == HVX_RD_SSIM)
     hipLaunchKernelGGL(k_ctu_leaf_ssim, dim3(n * HVX_CUS_PER_CTU), dim3(64), 0, st, A, d_cur, stride,
                        (const int16_t *)(ws + W.resid), (const int16_t *)(ws + W.res_out));
-  hipLaunchKernelGGL(k_ctu_decide, dim3((n + 63) / 64), dim3(64), 0, st, A);
+  hipLaunchKernelGGL(k_ctu_decide, dim3(n), dim3(64), 0, st, A);  // one wave per CTU
   // the reference picture (if asked for) gets the reconstructed samples in the same pass; its
   // margins are extended after deblocking
   uint8_t *rp_y = d_ref_pic != d_recon ? d_ref_pic : nullptr;
