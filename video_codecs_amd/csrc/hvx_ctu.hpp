@@ -831,20 +831,35 @@ __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int p
   const int ctu = blockIdx.x;
   const int x0 = (ctu % L.nctu_x) * 64, y0 = (ctu / L.nctu_x) * 64;
   const hvx_cu_decision *dc = dec + (size_t)ctu * HVX_CUS_PER_CTU;
+  // the CTU's leaf CU of every 8x8 block (-1: none) and the CUs' cbf words, staged in LDS once
+  __shared__ int cbfm[HVX_CUS_PER_CTU];
+  __shared__ int8_t leafm[HVX_CUS_PER_CTU], blk[64];
+  if (threadIdx.x < HVX_CUS_PER_CTU) {
+    leafm[threadIdx.x] = (int8_t)dc[threadIdx.x].leaf;
+    cbfm[threadIdx.x] = dc[threadIdx.x].cbf;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int bx = threadIdx.x & 7, by = threadIdx.x >> 3;
+    int ci = -1;
+    for (int d = 0; d < 4 && ci < 0; d++) {
+      const int c = depth_base(d) + (by >> (3 - d)) * (1 << d) + (bx >> (3 - d));
+      if (leafm[c]) ci = c;
+    }
+    blk[threadIdx.x] = (int8_t)ci;
+  }
+  __syncthreads();
   for (int k = threadIdx.x; k < 64 * 64; k += 256) {
     const int yy = k >> 6, xx = k & 63, x = x0 + xx, y = y0 + yy;
     if (x >= pic_w || y >= pic_h) continue;
-    int d = 0, j = 0;
-    for (d = 0; d < 4; d++) {
-      const int S = 64 >> d, g = 1 << d;
-      j = (yy / S) * g + (xx / S);
-      if (dc[depth_base(d) + j].leaf) break;
-    }
-    if (d == 4) continue;  // not reached for a decided CTU
+    const int ci = blk[(yy >> 3) * 8 + (xx >> 3)];
+    if (ci < 0) continue;  // not reached for a decided CTU
+    int d, j, S0, g0;
+    cu_geom(ci, d, j, S0, g0);
     const int S = 64 >> d, T = S < 32 ? S : 32, cx = xx % S, cy = yy % S, t = (cy / T) * (S / T) + (cx / T);
     const int tu = ctu_tu_index(L, ctu, d, j, t);
     const int64_t o = ctu_tu_offset(L, tu) + (cy % T) * T + (cx % T);
-    const int v = (int)cur[y * stride + x] - resid[o] + (((dc[depth_base(d) + j].cbf >> t) & 1) ? res_out[o] : 0);
+    const int v = (int)cur[y * stride + x] - resid[o] + (((cbfm[ci] >> t) & 1) ? res_out[o] : 0);
     const uint8_t rv = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
     recon[y * stride + x] = rv;
     if (rp_y) rp_y[y * stride + x] = rv;
@@ -853,15 +868,12 @@ __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int p
   for (int k = threadIdx.x; k < 2 * 32 * 32; k += 256) {  // Cb then Cr, 32x32 chroma samples per CTU
     const int c = 1 + (k >> 10), yy = (k >> 5) & 31, xx = k & 31, x = x0 / 2 + xx, y = y0 / 2 + yy;
     if (2 * x >= pic_w || 2 * y >= pic_h) continue;
-    int d = 0, j = 0;
-    for (d = 0; d < 4; d++) {
-      const int S = 64 >> d, g = 1 << d;
-      j = (2 * yy / S) * g + (2 * xx / S);
-      if (dc[depth_base(d) + j].leaf) break;
-    }
-    if (d == 4) continue;
+    const int ci = blk[(yy >> 2) * 8 + (xx >> 2)];
+    if (ci < 0) continue;
+    int d, j, S0, g0;
+    cu_geom(ci, d, j, S0, g0);
     const int Sc = 32 >> d, Tc = (Sc < 16 ? Sc : 16), cx = xx % Sc, cy = yy % Sc, t = (cy / Tc) * (Sc / Tc) + (cx / Tc);
-    const int tu = ctu_tu_index(L, ctu, d, j, t, c), cbf = dc[depth_base(d) + j].cbf;
+    const int tu = ctu_tu_index(L, ctu, d, j, t, c), cbf = cbfm[ci];
     const int64_t o = ctu_tu_offset(L, tu) + (cy % Tc) * Tc + (cx % Tc);
     const int64_t orr = ((cbf >> (8 + 4 * c + t)) & 1) ? ctu_tu_offset(L, ctu_tu_ts(L, tu)) + cy * 4 + cx : o;
     const int v = (int)C.cur[c - 1][y * C.stride + x] - resid[o] + (((cbf >> (4 * c + t)) & 1) ? res_out[orr] : 0);
