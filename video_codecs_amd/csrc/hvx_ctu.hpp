@@ -822,13 +822,27 @@ __global__ __launch_bounds__(64) void k_ctu_decide(DecideArgs A) {
 // reconstruction of the leaves: recon = clip(org - residual + coded reconstructed residual)
 // (= pred + the residual the leaf keeps, TComYuv::addClip) into the 8-bit picture plane; one
 // 256-thread block per CTU, each thread 16 samples of a 64x64 CTU
+__device__ __forceinline__ void ctu_bs_unit(const hvx_cu_result *__restrict__ cu, const hvx_cu_decision *__restrict__ dec,
+                                            int pic_w, int pic_h, int qp, int ux, int uy, uint8_t *__restrict__ bs_ver,
+                                            uint8_t *__restrict__ bs_hor, int8_t *__restrict__ qpm);
+struct CtuBsArgs {
+  const hvx_cu_result *cu;
+  uint8_t *bsv, *bsh;  // nullptr: no boundary strengths
+  int8_t *qpm;
+  int qp;
+};
 __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int pic_h, const uint8_t *__restrict__ cur,
                                                    int stride, const hvx_cu_decision *__restrict__ dec,
                                                    const int16_t *__restrict__ resid, const int16_t *__restrict__ res_out,
                                                    uint8_t *__restrict__ recon, CtuChroma C, uint8_t *__restrict__ rp_y,
-                                                   uint8_t *__restrict__ rp_cb, uint8_t *__restrict__ rp_cr) {
-  // rp_*: the reference picture's planes (nullable), written with the same samples before deblocking
+                                                   uint8_t *__restrict__ rp_cb, uint8_t *__restrict__ rp_cr, CtuBsArgs B) {
+  // rp_*: the reference picture's planes (nullable), written with the same samples before deblocking;
+  // B.bsv: also the boundary strengths of the CTU's 16x16 units of 4x4 samples (k_ctu_bs)
   const int ctu = blockIdx.x;
+  if (B.bsv) {
+    const int ux = (ctu % L.nctu_x) * 16 + (int)(threadIdx.x & 15), uy = (ctu / L.nctu_x) * 16 + (int)(threadIdx.x >> 4);
+    if (ux < (pic_w >> 2) && uy < (pic_h >> 2)) ctu_bs_unit(B.cu, dec, pic_w, pic_h, B.qp, ux, uy, B.bsv, B.bsh, B.qpm);
+  }
   const int x0 = (ctu % L.nctu_x) * 64, y0 = (ctu / L.nctu_x) * 64;
   const hvx_cu_decision *dc = dec + (size_t)ctu * HVX_CUS_PER_CTU;
   // the CTU's leaf CU of every 8x8 block (-1: none) and the CUs' cbf words, staged in LDS once
@@ -882,6 +896,7 @@ __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int p
     uint8_t *rp = c == 1 ? rp_cb : rp_cr;
     if (rp) rp[y * C.stride + x] = rv;
   }
+
 }
 
 // Boundary strengths of the decided CU trees (restated by hvxo_ctu_bs): TComLoopFilter's
@@ -903,14 +918,10 @@ __device__ __forceinline__ void unit_block(const hvx_cu_decision *dec, int nctu_
   }
 }
 
-__global__ __launch_bounds__(256) void k_ctu_bs(const hvx_cu_result *__restrict__ cu,
-                                                const hvx_cu_decision *__restrict__ dec, int pic_w, int pic_h, int qp,
-                                                uint8_t *__restrict__ bs_ver, uint8_t *__restrict__ bs_hor,
-                                                int8_t *__restrict__ qpm) {
-  const int uw = pic_w >> 2, uh = pic_h >> 2, nctu_x = (pic_w + 63) >> 6;
-  const int u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= uw * uh) return;
-  const int ux = u % uw, uy = u / uw;
+__device__ __forceinline__ void ctu_bs_unit(const hvx_cu_result *__restrict__ cu, const hvx_cu_decision *__restrict__ dec,
+                                            int pic_w, int pic_h, int qp, int ux, int uy, uint8_t *__restrict__ bs_ver,
+                                            uint8_t *__restrict__ bs_hor, int8_t *__restrict__ qpm) {
+  const int uw = pic_w >> 2, nctu_x = (pic_w + 63) >> 6, u = uy * uw + ux;
   qpm[u] = (int8_t)qp;
   int cq, kq, tq;
   unit_block(dec, nctu_x, ux, uy, cq, kq, tq);
@@ -931,4 +942,13 @@ __global__ __launch_bounds__(256) void k_ctu_bs(const hvx_cu_result *__restrict_
     }
     (dir ? bs_hor : bs_ver)[u] = bs;
   }
+}
+__global__ __launch_bounds__(256) void k_ctu_bs(const hvx_cu_result *__restrict__ cu,
+                                                const hvx_cu_decision *__restrict__ dec, int pic_w, int pic_h, int qp,
+                                                uint8_t *__restrict__ bs_ver, uint8_t *__restrict__ bs_hor,
+                                                int8_t *__restrict__ qpm) {
+  const int uw = pic_w >> 2, uh = pic_h >> 2;
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= uw * uh) return;
+  ctu_bs_unit(cu, dec, pic_w, pic_h, qp, u % uw, u / uw, bs_ver, bs_hor, qpm);
 }

@@ -956,9 +956,13 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
   uint8_t *rp_y = d_ref_pic != d_recon ? d_ref_pic : nullptr;
   uint8_t *rp_cb = chroma && d_ref_pic && chroma->ref_pic_cb != chroma->recon_cb ? chroma->ref_pic_cb : nullptr;
   uint8_t *rp_cr = chroma && d_ref_pic && chroma->ref_pic_cr != chroma->recon_cr ? chroma->ref_pic_cr : nullptr;
-  hipLaunchKernelGGL(k_ctu_recon, dim3(n), dim3(256), 0, st, L, P.pic_w, P.pic_h, d_cur, stride, (const hvx_cu_decision *)d_dec,
-                     (const int16_t *)(ws + W.resid), (const int16_t *)(ws + W.res_out), d_recon, A.C, rp_y, rp_cb, rp_cr);
+  // the boundary strengths (for the reference picture's deblocking) run in the reconstruction launch
   const int M = HVX_PLANE_MARGIN, Mc = M / 2, cw = P.pic_w / 2, ch = P.pic_h / 2;
+  uint8_t *bsv = (uint8_t *)(ws + W.bsv), *bsh = (uint8_t *)(ws + W.bsh);
+  int8_t *qpm = (int8_t *)(ws + W.qpm);
+  CtuBsArgs B = {d_cu, d_ref_pic ? bsv : nullptr, bsh, qpm, P.qp};
+  hipLaunchKernelGGL(k_ctu_recon, dim3(n), dim3(256), 0, st, L, P.pic_w, P.pic_h, d_cur, stride, (const hvx_cu_decision *)d_dec,
+                     (const int16_t *)(ws + W.resid), (const int16_t *)(ws + W.res_out), d_recon, A.C, rp_y, rp_cb, rp_cr, B);
   // extendPicBorder of Y (and Cb, Cr): one launch
   auto extend = [&](uint8_t *y, uint8_t *cb, uint8_t *cr) {
     PlaneSet E = {{y, cb, cr}, {stride, chroma ? chroma->c_stride : 0, chroma ? chroma->c_stride : 0},
@@ -970,13 +974,8 @@ static int ctu_decide_impl(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const
   t_end(ctx, st, tk);
   if (d_ref_pic) {
     // 4. the reference picture: the reconstruction deblocked (boundary strengths of the decided
-    //    trees, k_ctu_bs; TComLoopFilter::loopFilterPic, luma) with borders extended again
+    //    trees, computed above; TComLoopFilter::loopFilterPic, luma) with borders extended again
     tk = t_begin(ctx, st, 18);
-    const int nunit = (P.pic_w / 4) * (P.pic_h / 4);
-    uint8_t *bsv = (uint8_t *)(ws + W.bsv), *bsh = (uint8_t *)(ws + W.bsh);
-    int8_t *qpm = (int8_t *)(ws + W.qpm);
-    hipLaunchKernelGGL(k_ctu_bs, dim3((nunit + 255) / 256), dim3(256), 0, st, d_cu, (const hvx_cu_decision *)d_dec,
-                       P.pic_w, P.pic_h, P.qp, bsv, bsh, qpm);
     hvx_deblock_params dp = {};
     dp.pic_w = P.pic_w; dp.pic_h = P.pic_h;
     // loopFilterPic: luma, and at 4:2:0 the chroma edges (filtered only where bs == 2, i.e. never

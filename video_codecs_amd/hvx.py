@@ -375,7 +375,7 @@ PHASES = ("me_d0", "me_d1", "me_d2", "me_d3", "frac_d0", "mc_resid",
 # hvx_ctu_encode_yuv call (the 4:2:0 bench step: tu16 = luma 16x16 + chroma 16x16, tu8 = luma 8x8 +
 # chroma 8x8 + chroma 4x4, coeff_bits = one count per TU class); phases run on 4 streams and may
 # overlap (DESIGN.md "Where the time goes")
-PHASE_LAUNCHES = (1, 1, 1, 1, 1, 3, 1, 1, 1, 2, 2, 2, 3, 3, 3, 1, 6, 4, 4)
+PHASE_LAUNCHES = (1, 1, 1, 1, 1, 3, 1, 1, 1, 2, 2, 2, 3, 3, 3, 1, 6, 4, 3)
 PHASE_KERNELS = ("k_me_int_ctu<64,1,4>", "k_me_ctu<32,1,2>", "k_me_ctu<16,1,1>", "k_me_ctu<8,0,1>",
                  "k_me_frac_ctu<64,4>", "k_ctu_pred_resid", "k_tu_fwd<3>", "k_tu_rdoq<3>", "k_tu_fin<3,2>",
                  "k_tu_fwd<2>", "k_tu_rdoq<2>", "k_tu_fin<2,2>", "k_tu_fwd<1>", "k_tu_rdoq<1>", "k_tu_fin<1,2>",
