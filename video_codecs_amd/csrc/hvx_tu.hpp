@@ -916,6 +916,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
   bool carry = false;  // c1 == 0 at the end of the previous group (decided lanes only)
   double block_uncoded = 0, base_cost = 0;
   uint64_t sigmask = 0;
+  int32_t tot = 0;  // sum of the decided levels (after the group zero-outs)
   uint32_t nld[16], ncx[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) {
@@ -951,7 +952,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
     for (int k = 0; k < 3; k++) { A0[k] = est->levelAbsBits[ctx_set + k][0]; A1[k] = est->levelAbsBits[ctx_set + k][1]; }
     int c1 = 1, c2 = 0;
     uint32_t c1_idx = 0, c2_idx = 0, rice = rice0;
-    int nnz0 = 0;
+    int nnz0 = 0, cgsum = 0;
     bool any = false;
     double coded_ld = 0, uncoded = 0, sig_cost = 0, sig_cost0 = 0;
 #pragma unroll 2
@@ -1002,6 +1003,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
       const double cs = act ? cost_sig : 0.0;
       sg.st[pin][lane] = rd_pack(4 * ctx_set + c1, ctx_set + c2, (int)rice, c1ok, c2ok, !is_last, ctx_sig, sel);
       sg.lv[pin][lane] = (int32_t)level;
+      cgsum += (int)level;
       base_cost += act ? cost : cc0;
       // context state after the level (:2300-2325): Rice parameter, c1Idx, c1/c2
       const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
@@ -1041,6 +1043,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
           if (zero_cost < base_cost) {
             sigmask &= ~(1ull << cgblk);
             base_cost = zero_cost;
+            cgsum = 0;
 #pragma unroll
             for (int pin = 0; pin < 16; pin++) sg.lv[pin][lane] = 0;
           }
@@ -1049,6 +1052,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
         sigmask |= 1ull << cgblk;
       }
     }
+    tot += cgsum;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       lev[cgp * g16 + (size_t)k * G] = sg.lv[k][lane];
@@ -1069,6 +1073,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
     base_cost += lambda * (double)est->blockCbpBits[ctx][1];
   }
   bool found = false;
+  int32_t above = 0, drop = 0;  // levels past the scanned position / past the best last one
   for (int cgp = cg_last; cgp >= 0 && !found; cgp--) {
     const int cgblk = c.scan_cg[cgp];
     // the coded-group flag rate the decision pass added for this group: 0 for the first
@@ -1108,13 +1113,15 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
           const int py = blk >> LOG2, px = blk - (py << LOG2);
           const double cl = c.scan_type == 2 ? rd_rate_last(est, lambda, py, px, ch) : rd_rate_last(est, lambda, px, py, ch);
           const double total = base_cost + cl - cs;
-          if (total < best_cost) { best_p1 = sp + 1; best_cost = total; }
+          if (total < best_cost) { best_p1 = sp + 1; best_cost = total; drop = above; }
+          above += lvv;
           if (lvv > 1) { found = true; break; }
           const int32_t ld = (int32_t)(sg.ld[pin][lane] & 0x7fffffffu);
           const double err = (double)sub32(ld, shl32(1, qbits));
-          const int rate = rd_ic_rate(1u, x.rice, x.c1ok, x.c2ok, est->greaterOneBits[x.ctx_one][0],
-                                      est->greaterOneBits[x.ctx_one][1], est->levelAbsBits[x.ctx_abs][0],
-                                      est->levelAbsBits[x.ctx_abs][1], ext, max_log2);
+          const int g0 = est->greaterOneBits[x.ctx_one][0], g1 = est->greaterOneBits[x.ctx_one][1];
+          const int a0 = est->levelAbsBits[x.ctx_abs][0], a1 = est->levelAbsBits[x.ctx_abs][1];
+          const int rate = FAST ? rd_ic_rate_bf(1u, (uint32_t)x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1)
+                                : rd_ic_rate(1u, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2);
           double cc = err * err * escale + lambda * (double)rate;
           cc += x.has_sig ? lambda * (double)est->significantBits[x.ctx_sig][1] : 0.0;
           base_cost -= cc;
@@ -1127,105 +1134,99 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
     }
   }
 
-  // ---- signs, zeroing past the chosen last position, uiAbsSum ----
-  int32_t abs_sum = 0;
-  for (int cgp = 0; cgp <= (last >> 4); cgp++) {
-    int32_t lv16[16];
-    uint32_t cf16[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      lv16[k] = lev[cgp * g16 + (size_t)k * G];
-      cf16[k] = ldI[cgp * gi16 + (size_t)k * gi];
-    }
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const int sp = cgp * 16 + k;
-      if (sp > last) continue;
-      if (sp < best_p1) {
-        abs_sum += lv16[k];
-        if (cf16[k] >> 31) lev[cgp * g16 + (size_t)k * G] = -lv16[k];
-      } else {
-        lev[cgp * g16 + (size_t)k * G] = 0;
-      }
-    }
-  }
+  // uiAbsSum over the kept levels (:2530-2538)
+  const int32_t abs_sum = best_p1 ? tot - drop : 0;
 
-  // ---- RD sign-bit hiding (:2541-2660), groups from the top ----
-  if (d.sign_hiding && abs_sum >= 2) {
-    const double iq = (double)kInvQuantScales[d.qp_rem];
-    const int64_t rdf = (int64_t)(iq * iq * (1 << (2 * d.qp_per)) / d.lambda / 16 / (1 << 0) + 0.5);
-    int last_cg = -1;
-    for (int sub = NCG - 1; sub >= 0; sub--) {
-      {
-        int32_t a16[16];
+  // ---- signs, zeroing past the chosen last position, RD sign-bit hiding (:2541-2660) ----
+  // one pass over the groups from the top: HM's sign loop and its SBH loop see each group with
+  // the same final levels, and the groups above the last position are all zero
+  const bool sbh = d.sign_hiding && abs_sum >= 2;
+  const double iq = (double)kInvQuantScales[d.qp_rem];
+  const int64_t rdf = sbh ? (int64_t)(iq * iq * (1 << (2 * d.qp_per)) / d.lambda / 16 / (1 << 0) + 0.5) : 0;
+  int last_cg = -1;
+  for (int sub = last >> 4; sub >= 0; sub--) {
+    int32_t v[16];
+    uint32_t w[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++) a16[k] = lev[sub * g16 + (size_t)k * G];
+    for (int k = 0; k < 16; k++) {
+      v[k] = lev[sub * g16 + (size_t)k * G];
+      w[k] = ldI[sub * gi16 + (size_t)k * gi];
+    }
+    uint32_t nzm = 0, negm = 0;
+    int abs_in = 0;
 #pragma unroll
-        for (int k = 0; k < 16; k++) sg.lv[k][lane] = a16[k];
-      }
-      int first_nz = 16, last_nz = -1, abs_in = 0, k;
-      for (k = 15; k >= 0; k--) if (sg.lv[k][lane]) { last_nz = k; break; }
-      for (k = 0; k < 16; k++) if (sg.lv[k][lane]) { first_nz = k; break; }
-      for (k = first_nz; k <= last_nz; k++) abs_in += sg.lv[k][lane];
-      if (last_nz >= 0 && last_cg == -1) last_cg = 1;
-      if (last_nz - first_nz >= 4) {
-        const uint32_t signbit = sg.lv[first_nz][lane] > 0 ? 0 : 1;
-        if (signbit != (uint32_t)(abs_in & 1)) {
-          {
-            int32_t b16[16];
-            uint32_t c16[16];
+    for (int k = 0; k < 16; k++) {
+      const int32_t a = sub * 16 + k < best_p1 ? v[k] : 0;
+      v[k] = (w[k] >> 31) ? -a : a;
+      nzm |= (a != 0 ? 1u : 0u) << k;
+      negm |= (w[k] >> 31) << k;
+      abs_in += v[k];
+    }
+    if (sbh && nzm) {
+      const int last_nz = 31 - __builtin_clz(nzm), first_nz = __builtin_ctz(nzm);
+      if (last_cg == -1) last_cg = 1;
+      const uint32_t signbit = (negm >> first_nz) & 1u;
+      if (last_nz - first_nz >= 4 && signbit != (uint32_t)(abs_in & 1)) {
+        {
+          int32_t b16[16];
 #pragma unroll
-            for (int q = 0; q < 16; q++) {
-              c16[q] = ldI[sub * gi16 + (size_t)q * gi];
-              b16[q] = st[sub * g16 + (size_t)q * G];
-            }
+          for (int q = 0; q < 16; q++) b16[q] = st[sub * g16 + (size_t)q * G];
 #pragma unroll
-            for (int q = 0; q < 16; q++) { sg.ld[q][lane] = c16[q]; sg.st[q][lane] = b16[q]; }
-          }
-          int64_t min_inc = INT64_MAX, cur = INT64_MAX;
-          int min_k = -1, fch = 0, cch = 0;
-          for (k = (last_cg == 1 ? last_nz : 15); k >= 0; k--) {
-            const int32_t lv = sg.lv[k][lane];
-            const uint32_t lev0 = (uint32_t)abs(lv);
-            const uint32_t wk = sg.ld[k][lane];
-            const int32_t ld = (int32_t)(wk & 0x7fffffffu);
-            const int32_t du = sub32(ld, shl32((int32_t)lev0, qbits)) >> (qbits - 8);
-            const RdCtx x = rd_unpack(sg.st[k][lane]);
-            const int g0 = est->greaterOneBits[x.ctx_one][0];
-            const int sigd = x.has_sig ? est->significantBits[x.ctx_sig][1] - est->significantBits[x.ctx_sig][0] : 0;
-            int rup = g0, rdown = 0;
-            if (lev0 > 0) {
-              const int g1 = est->greaterOneBits[x.ctx_one][1];
-              const int a0 = est->levelAbsBits[x.ctx_abs][0], a1 = est->levelAbsBits[x.ctx_abs][1];
+          for (int q = 0; q < 16; q++) { sg.lv[q][lane] = v[q]; sg.ld[q][lane] = w[q]; sg.st[q][lane] = b16[q]; }
+        }
+        int64_t min_inc = INT64_MAX, cur = INT64_MAX;
+        int min_k = -1, fch = 0, cch = 0;
+        for (int k = (last_cg == 1 ? last_nz : 15); k >= 0; k--) {
+          const int32_t lv = sg.lv[k][lane];
+          const uint32_t lev0 = (uint32_t)abs(lv);
+          const uint32_t wk = sg.ld[k][lane];
+          const int32_t ld = (int32_t)(wk & 0x7fffffffu);
+          const int32_t du = sub32(ld, shl32((int32_t)lev0, qbits)) >> (qbits - 8);
+          const RdCtx x = rd_unpack(sg.st[k][lane]);
+          const int g0 = est->greaterOneBits[x.ctx_one][0];
+          const int sigd = x.has_sig ? est->significantBits[x.ctx_sig][1] - est->significantBits[x.ctx_sig][0] : 0;
+          int rup = g0, rdown = 0;
+          if (lev0 > 0) {
+            const int g1 = est->greaterOneBits[x.ctx_one][1];
+            const int a0 = est->levelAbsBits[x.ctx_abs][0], a1 = est->levelAbsBits[x.ctx_abs][1];
+            if (FAST) {  // no extended precision in the wave: the branch-free rate
+              const uint32_t rc = (uint32_t)x.rice;
+              const int now = rd_ic_rate_bf(lev0, rc, x.c1ok, x.c2ok, g0, g1, a0, a1);
+              rup = rd_ic_rate_bf(lev0 + 1, rc, x.c1ok, x.c2ok, g0, g1, a0, a1) - now;
+              rdown = rd_ic_rate_bf(lev0 - 1, rc, x.c1ok, x.c2ok, g0, g1, a0, a1) - now;
+            } else {
               const int now = rd_ic_rate(lev0, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2);
               rup = rd_ic_rate(lev0 + 1, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2) - now;
               rdown = rd_ic_rate(lev0 - 1, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2) - now;
             }
-            if (lv != 0) {
-              const int64_t up = rdf * (-du) + rup;
-              int64_t down = rdf * (du) + rdown - ((abs(lv) == 1) ? sigd : 0);
-              if (last_cg == 1 && last_nz == k && abs(lv) == 1) down -= (4 << 15);
-              if (up < down) { cur = up; cch = 1; }
-              else { cch = -1; cur = (k == first_nz && abs(lv) == 1) ? INT64_MAX : down; }
-            } else {
-              cur = rdf * (-(abs(du))) + (1 << 15) + rup + sigd;
-              cch = 1;
-              if (k < first_nz) {
-                const uint32_t tsb = wk >> 31;
-                if (tsb != signbit) cur = INT64_MAX;
-              }
-            }
-            if (cur < min_inc) { min_inc = cur; fch = cch; min_k = k; }
           }
-          int32_t mv = sg.lv[min_k][lane];
-          if (mv == ecmax || mv == ecmin) fch = -1;
-          if (!(sg.ld[min_k][lane] >> 31)) mv += fch;
-          else mv -= fch;
-          lev[sub * g16 + (size_t)min_k * G] = mv;
+          if (lv != 0) {
+            const int64_t up = rdf * (-du) + rup;
+            int64_t down = rdf * (du) + rdown - ((abs(lv) == 1) ? sigd : 0);
+            if (last_cg == 1 && last_nz == k && abs(lv) == 1) down -= (4 << 15);
+            if (up < down) { cur = up; cch = 1; }
+            else { cch = -1; cur = (k == first_nz && abs(lv) == 1) ? INT64_MAX : down; }
+          } else {
+            cur = rdf * (-(abs(du))) + (1 << 15) + rup + sigd;
+            cch = 1;
+            if (k < first_nz) {
+              const uint32_t tsb = wk >> 31;
+              if (tsb != signbit) cur = INT64_MAX;
+            }
+          }
+          if (cur < min_inc) { min_inc = cur; fch = cch; min_k = k; }
         }
+        int32_t mv = sg.lv[min_k][lane];
+        if (mv == ecmax || mv == ecmin) fch = -1;
+        if (!(sg.ld[min_k][lane] >> 31)) mv += fch;
+        else mv -= fch;
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = k == min_k ? mv : v[k];
       }
       if (last_cg == 1) last_cg = 0;
     }
+#pragma unroll
+    for (int k = 0; k < 16; k++) lev[sub * g16 + (size_t)k * G] = v[k];
   }
   return abs_sum;
 }
