@@ -603,9 +603,10 @@ struct MeFracSmem {
   // per-wave candidate block of the per-lane-tile SATD path: only shapes that are not multiples
   // of 8 (<= 16 rows) take it, so 16 rows of the S stride suffice above S = 32
   uint8_t blk[NW][S <= 32 ? S * S : 16 * S];
-  TO org[S * S];                // the search pattern: the original (8-bit) or a bi target (int16)
+  alignas(16) TO org[S * S];    // the search pattern: the original (8-bit) or a bi target (int16)
   uint32_t cost[9];
   uint32_t part[NW][3][4];      // per-wave SATD partial sums of the 9 candidates (me_sum9 slots)
+  uint32_t sat[NW][9];          // per-wave SATD partial sums by candidate slot (MFMA path)
 };
 
 typedef short me_s2 __attribute__((ext_vector_type(2)));
@@ -762,6 +763,46 @@ __device__ __forceinline__ void me_sum9(const int (&a)[9], uint32_t (&u)[3]) {
   }
 }
 
+typedef _Float16 me_h4 __attribute__((ext_vector_type(4)));
+typedef float me_f4 __attribute__((ext_vector_type(4)));
+
+// The block-diagonal diag(H8, H8) (Sylvester order, symmetric) as a v_mfma_f32_16x16x16_f16
+// operand fragment: lane l holds element [l & 15][4 (l >> 4) + j] -- the A fragment, and by
+// symmetry also the B fragment.
+__device__ __forceinline__ me_h4 me_hb_frag(int lane) {
+  const int r = lane & 15;
+  me_h4 h;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int k = 4 * (lane >> 4) + j;
+    h[j] = (r >> 3) != (k >> 3) ? (_Float16)0.0f : (__popc(r & k & 7) & 1) ? (_Float16)-1.0f : (_Float16)1.0f;
+  }
+  return h;
+}
+
+// xCalcHADs8x8 (TComRdCost.cpp) of the four 8x8 tiles of a 16x16 difference block D on two
+// MFMAs.  (a0, a1) is the lane's A fragment -- row lane & 15, columns 4 (lane >> 4) .. +3 -- as
+// f16 bit patterns 0x6600 + d, i.e. exactly 1536 + d for |d| <= 255; cb holds -12288 in columns
+// 0 and 8, which cancels the bias through the H8 column sums.  X = D diag(H8,H8) (|X| <= 2040,
+// exact in f16), Z = diag(H8,H8) X = H8 D H8 per tile (|Z| <= 16320); all sums are integers
+// below 2^24, so f32 accumulation is exact in any order.  Returns in every lane (sum |Z| + 2) >> 2
+// of the tile at (row half lane >> 5, column half (lane >> 3) & 1) of Z's layout.
+__device__ __forceinline__ uint32_t me_satd4_mfma(uint32_t a0, uint32_t a1, me_h4 hb, me_f4 cb) {
+  const me_h4 a = __builtin_bit_cast(me_h4, me_v2u{a0, a1});
+  const me_f4 x = __builtin_amdgcn_mfma_f32_16x16x16f16(a, hb, cb, 0, 0, 0);
+  const uint32_t p0 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(x[0], x[1]));
+  const uint32_t p1 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(x[2], x[3]));
+  const me_h4 xb = __builtin_bit_cast(me_h4, me_v2u{p0, p1});
+  const me_f4 z = __builtin_amdgcn_mfma_f32_16x16x16f16(hb, xb, me_f4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+  uint32_t v = (uint32_t)(fabsf(z[0]) + fabsf(z[1]) + fabsf(z[2]) + fabsf(z[3]));
+  v += ME_DPP(v, 0xB1);   // lanes ^1
+  v += ME_DPP(v, 0x4E);   // ^2
+  v += ME_DPP(v, 0x141);  // the other quad of the half row
+  const auto pr = __builtin_amdgcn_permlane16_swap(v, v, false, false);  // lanes ^16
+  v = (uint32_t)pr[0] + (uint32_t)pr[1];
+  return (v + 2) >> 2;
+}
+
 // candidate index (s_acMvRefineH / s_acMvRefineQ order) of slot c*3 + d, (dx, dy) = (c-1, d-1),
 // as 4-bit fields
 constexpr uint64_t kRefSlotH = 0x846201735ull, kRefSlotQ = 0x864201753ull;
@@ -850,6 +891,88 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
   // 2. the 9 candidates' costs (SATD or SAD + MV cost)
   const bool xl = had && (!GENERIC || ((w % 8 == 0) && (h % 8 == 0)));
   const int tw = w >> 3, nt = (w * h) >> 6;
+  if constexpr (!GENERIC && sizeof(TO) == 1) {
+    if (xl) {
+      // Square blocks of the CTU pass: the Hadamards on MFMA (me_satd4_mfma), four 8x8 tiles per
+      // pair of MFMAs.  S == 8: one pair per vertical phase d, its tiles the candidates
+      // (c, d), c = 0..2, of the three column phases (the fourth tile repeats c = 2); S >= 16: one
+      // pair per 16x16 region and candidate, the regions spread over the job's waves.
+      const me_h4 hb = me_hb_frag(lane);
+      const float cbv = (lane & 7) == 0 ? -12288.0f : 0.0f;
+      const me_f4 cb = {cbv, cbv, cbv, cbv};
+      int offs[3], fys[3];
+      int ryb = 0;
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+        const int qy = qy0 + (d - 1) * step, ry = (qy >> 2) - iy;
+        if (d == 0) ryb = ry;
+        offs[d] = ry - ryb; fys[d] = qy & 3;
+      }
+      // A-fragment geometry: tile (row half b3, column half b5), tile row lane & 7, columns 4 b4 .. +3
+      const int b3 = (lane >> 3) & 1, b4 = (lane >> 4) & 1, b5 = lane >> 5;
+      if constexpr (S == 8) {
+        const int y = lane & 7, x = 4 * b4, qa = 2 * b3 + b5, qz = 2 * b5 + b3;
+        const int pol = qa == 0 ? po[0] : qa == 1 ? po[1] : po[2];
+        const uint32_t ow = *(const uint32_t *)&sm.org[y * S + x];
+        const uint32_t ob0 = __builtin_amdgcn_perm(0u, ow, 0x0c010c00u) + 0x66006600u;
+        const uint32_t ob1 = __builtin_amdgcn_perm(0u, ow, 0x0c030c02u) + 0x66006600u;
+        const bool rep = (lane & 0x17) == 0 && qz < 3;  // lanes 0, 8, 32: the sums of tiles 0, 1, 2
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+          const int16_t *h = &sm.hp[0][0] + pol + (ryb + 1 + y + offs[d]) * HS + x;
+          uint32_t pv[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) pv[k] = (uint32_t)me_vsample_pk<HS>(h + k, fys[d]);
+          const uint32_t t = me_satd4_mfma(ob0 - (pv[0] | (pv[1] << 16)), ob1 - (pv[2] | (pv[3] << 16)), hb, cb);
+          if (rep) sm.sat[0][3 * qz + d] = t;
+        }
+      } else {
+        constexpr int RW = S / 16, NRG = RW * RW;
+        uint32_t acc[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) acc[k] = 0;
+        for (int rg = wave; rg < NRG; rg += NW) {
+          const int y = (rg / RW) * 16 + 8 * b3 + (lane & 7), x = (rg % RW) * 16 + 8 * b5 + 4 * b4;
+          const uint32_t ow = *(const uint32_t *)&sm.org[y * S + x];
+          const uint32_t ob0 = __builtin_amdgcn_perm(0u, ow, 0x0c010c00u) + 0x66006600u;
+          const uint32_t ob1 = __builtin_amdgcn_perm(0u, ow, 0x0c030c02u) + 0x66006600u;
+#pragma unroll
+          for (int sl = 0; sl < 9; sl++) {
+            if (QC && sl == 4) continue;
+            const int c = sl / 3, d = sl % 3;
+            const int16_t *h = &sm.hp[0][0] + po[c] + (ryb + 1 + y + offs[d]) * HS + x;
+            uint32_t pv[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) pv[k] = (uint32_t)me_vsample_pk<HS>(h + k, fys[d]);
+            acc[sl] += me_satd4_mfma(ob0 - (pv[0] | (pv[1] << 16)), ob1 - (pv[2] | (pv[3] << 16)), hb, cb);
+          }
+        }
+#pragma unroll
+        for (int sl = 0; sl < 9; sl++) {
+          if (QC && sl == 4) continue;
+          uint32_t v = acc[sl] + ME_DPP(acc[sl], 0x140);  // the other column half (row_mirror)
+          const auto pr = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // the other row half
+          v = (uint32_t)pr[0] + (uint32_t)pr[1];
+          if (lane == 0) sm.sat[wave][sl] = v;
+        }
+      }
+      me_sync<NW>();
+      // lane-parallel costs: lane sl < 9 takes slot sl; first minimum in the reference's order
+      const bool valid = lane < 9;
+      const int sl = valid ? lane : 0;
+      uint32_t dsum = 0;
+#pragma unroll
+      for (int ww = 0; ww < NW; ww++) dsum += sm.sat[ww][sl];
+      const int c = (sl * 11) >> 5, dx = c - 1, dy = sl - 3 * c - 1;
+      const uint64_t idx = step == 2 ? kRefSlotH : kRefSlotQ;
+      const int ci = (int)((idx >> (4 * sl)) & 15);
+      const uint32_t cost = (QC && sl == 4) ? ccost
+                                            : dsum + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, scale, mvx0 + dx, mvy0 + dy);
+      const uint32_t key = wave_min_key(valid ? (cost << 4) | (uint32_t)ci : kMeKeyNone);
+      bi = (int)(key & 15u);
+      return key >> 4;
+    }
+  }
   int hx, hy;
   me_had_xy(lane, hx, hy);
   if (xl) {
