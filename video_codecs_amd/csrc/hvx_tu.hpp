@@ -1351,8 +1351,10 @@ __global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ d
 }
 
 // xRateDistOptQuant, one TU per lane: wave w handles TUs w*G .. w*G+G-1 of the launch.
-// n_est_lds > 0: the launch's TUs index the first n_est_lds tables of `est` (est_idx), which
-// are staged in LDS; otherwise each lane reads its own table from global memory.
+// n_est_lds > 0: the launch's TUs index the first n_est_lds tables of `est` (est_idx); the
+// (at most two consecutive) tables the wave's TUs use are staged in LDS -- a class launch of the
+// CTU pass uses one -- so the wave's LDS stays at the lane stage + 2 tables (8 waves per CU).
+// Otherwise each lane reads its own table from global memory.
 template <int L>
 __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ descs, const hvx_estbits *__restrict__ est,
                                                 const int32_t *__restrict__ est_idx, int n,
@@ -1361,37 +1363,49 @@ __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ 
                                                 int32_t *__restrict__ abs_out, const int8_t *__restrict__ flags, int G,
                                                 int n_est_lds, int tm) {
   constexpr int N = 4 << L, NN = N * N;
-  __shared__ hvx_estbits tbl[8];  // n_est_lds <= 8 (the CTU pass: 4 luma + 3 chroma)
+  __shared__ hvx_estbits tbl[2];
   __shared__ RdLaneStage stage;
   const int lane = lane_id();
-  if (n_est_lds > 0) {
-    const int32_t *src = (const int32_t *)est;
-    int32_t *dst = (int32_t *)tbl;
-    const int words = n_est_lds * (int)(sizeof(hvx_estbits) / 4);
-    for (int i = lane; i < words; i += HVX_WAVE) dst[i] = src[i];
-    __syncthreads();
-  }
   const int t = blockIdx.x * G + lane;
-  if (lane >= G || t >= n) return;
+  const bool live = lane < G && t < n;
+  int e0 = 0;
+  bool staged = false;
+  if (n_est_lds > 0) {
+    const int my = live ? (est_idx ? est_idx[t] : t) : -1;
+    int lo = live ? my : INT_MAX, hi = my;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, __shfl_xor(lo, o, HVX_WAVE));
+      hi = max(hi, __shfl_xor(hi, o, HVX_WAVE));
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo); hi = __builtin_amdgcn_readfirstlane(hi);
+    if (hi >= 0 && lo >= 0 && hi - lo <= 1 && hi < n_est_lds) {
+      const int32_t *src = (const int32_t *)(est + lo);
+      int32_t *dst = (int32_t *)tbl;
+      const int words = (hi - lo + 1) * (int)(sizeof(hvx_estbits) / 4);
+      for (int i = lane; i < words; i += HVX_WAVE) dst[i] = src[i];
+      __syncthreads();
+      e0 = lo; staged = true;
+    }
+  }
+  if (!live) return;
   if (!flags[t]) return;
   const hvx_tu_desc d = descs[t];
   if (d.width != N || d.height != N) return;
   const int ei = est_idx ? est_idx[t] : t;
+  const hvx_estbits *e = staged ? &tbl[ei - e0] : est + ei;
   const size_t base = tu_il(t, 0, NN, G);
   const bool any_ext = __builtin_amdgcn_ballot_w64(d.extended_precision != 0) != 0;
   int32_t a;
   if (tm) {  // TU-major inputs (the CTU pass's 16x16 / 32x32 classes)
-    if (n_est_lds > 0 && !any_ext)
-      a = rdoq_lane<L, true, true>(d, &tbl[ei], ldI + (size_t)t * NN, cxI + (size_t)t * NN, levI + base, stI + base, G,
-                                   stage, lane);
+    if (staged && !any_ext)
+      a = rdoq_lane<L, true, true>(d, e, ldI + (size_t)t * NN, cxI + (size_t)t * NN, levI + base, stI + base, G, stage, lane);
     else
-      a = rdoq_lane<L, false, true>(d, n_est_lds > 0 ? &tbl[ei] : est + ei, ldI + (size_t)t * NN, cxI + (size_t)t * NN,
-                                    levI + base, stI + base, G, stage, lane);
-  } else if (n_est_lds > 0 && !any_ext) {
-    a = rdoq_lane<L, true, false>(d, &tbl[ei], ldI + base, cxI + base, levI + base, stI + base, G, stage, lane);
+      a = rdoq_lane<L, false, true>(d, e, ldI + (size_t)t * NN, cxI + (size_t)t * NN, levI + base, stI + base, G, stage, lane);
+  } else if (staged && !any_ext) {
+    a = rdoq_lane<L, true, false>(d, e, ldI + base, cxI + base, levI + base, stI + base, G, stage, lane);
   } else {
-    a = rdoq_lane<L, false, false>(d, n_est_lds > 0 ? &tbl[ei] : est + ei, ldI + base, cxI + base, levI + base,
-                                   stI + base, G, stage, lane);
+    a = rdoq_lane<L, false, false>(d, e, ldI + base, cxI + base, levI + base, stI + base, G, stage, lane);
   }
   if (abs_out) abs_out[t] = a;
 }
