@@ -352,14 +352,17 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuMc M, int ctu0) {
   ctu_pred_resid_cu<S>(M, ctu0 + (int)(blockIdx.x / ncu), (int)(blockIdx.x % ncu), win, hs);
 }
 
-// Depth 3 (8x8 CUs), FOUR CUs per wave (one wave per CU left most of the launch waiting on two
-// dependent memory round trips with little work).  The MC is branch-free: the two-stage form with
-// the phase-0 filters ({0,0,0,64,0,0,0,0} / {0,64,0,0}) gives exactly the reference's
-// one-stage and copy cases ((64X + 2048) >> 12 == (X + 32) >> 6, (4096b + 2048) >> 12 == b), the
-// first stage is v_dot4_i32_i8 on sign-biased window bytes (b - 128: the -8192 offset), the
-// second v_dot2_i32_i16 on int16 tap pairs.
+// Depth 3 (8x8 CUs), NC CUs per wave (one wave per CU left most of the launch waiting on
+// dependent memory round trips with little work).  The originals are fetched first (they do not
+// depend on the search), the luma and chroma reference windows of all NC CUs in one round trip
+// once the references and MVs are known.  The MC is branch-free: the two-stage form with the
+// phase-0 filters ({0,0,0,64,0,0,0,0} / {0,64,0,0}) gives exactly the reference's one-stage and
+// copy cases ((64X + 2048) >> 12 == (X + 32) >> 6, (4096b + 2048) >> 12 == b), the first stage is
+// v_dot4_i32_i8 on sign-biased window bytes (b - 128: the -8192 offset), the second
+// v_dot2_i32_i16 on int16 tap pairs.
+template <int NC>
 __global__ __launch_bounds__(64) void k_ctu_pred_resid8q(CtuMc M) {
-  constexpr int NC = 4;
+  static_assert(NC % 2 == 0 && NC * 5 <= 64 && 64 % NC == 0, "CUs per wave");
   __shared__ uint32_t winY[NC][15 * 4];      // 15 rows x 16 bytes (15 used), biased
   __shared__ int16_t hsY[NC][15 * 8];
   __shared__ uint32_t winC[2 * NC][7 * 2];   // 7 rows x 8 bytes (7 used), biased
@@ -367,54 +370,88 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid8q(CtuMc M) {
   const CtuLayout &L = M.L;
   const hvx_ctu_params &P = M.P;
   const CtuChroma &C = M.C;
-  const int lane = lane_id(), ctu = (int)(blockIdx.x >> 4), j0 = (int)(blockIdx.x & 15) * NC;
+  constexpr int PER = 64 / NC;  // waves per CTU
+  const int lane = lane_id(), ctu = (int)(blockIdx.x / PER), j0 = (int)(blockIdx.x % PER) * NC;
   const int stride = M.stride;
-  int x[NC], y[NC], bref[NC], mvx[NC], mvy[NC];
-  bool valid[NC];
+  const int bx = (ctu % L.nctu_x) * 64, by = (ctu / L.nctu_x) * 64;
+  int x[NC], y[NC];
+  uint32_t vmask = 0;
 #pragma unroll
-  for (int c = 0; c < NC; c++) {  // wave-uniform: position, validity, first-minimum reference
+  for (int c = 0; c < NC; c++) {
     const int j = j0 + c;
-    x[c] = (ctu % L.nctu_x) * 64 + (j % 8) * 8;
-    y[c] = (ctu / L.nctu_x) * 64 + (j / 8) * 8;
-    valid[c] = x[c] + 8 <= P.pic_w && y[c] + 8 <= P.pic_h;
+    x[c] = bx + (j % 8) * 8;
+    y[c] = by + (j / 8) * 8;
+    vmask |= (x[c] + 8 <= P.pic_w && y[c] + 8 <= P.pic_h) ? 1u << c : 0u;
+  }
+  // the originals: luma sample (lane >> 3, lane & 7) of every CU; chroma sample
+  // ((lane >> 2) & 3, lane & 3) of component (lane >> 4) & 1 of CU 2p + (lane >> 5)
+  const int ly = lane >> 3, lx = lane & 7;
+  const int cyy = (lane >> 2) & 3, cxx = lane & 3, ccomp = (lane >> 4) & 1, cq = lane >> 5;
+  int curY[NC], curC[NC / 2];
+#pragma unroll
+  for (int c = 0; c < NC; c++) curY[c] = (vmask >> c) & 1 ? M.cur[(y[c] + ly) * stride + x[c] + lx] : 0;
+  if (C.on) {
+#pragma unroll
+    for (int p = 0; p < NC / 2; p++) {
+      const int c = 2 * p + cq;
+      const int cx0 = bx + ((j0 + c) % 8) * 8, cy0 = by + ((j0 + c) / 8) * 8;
+      curC[p] = (vmask >> c) & 1 ? C.cur[ccomp][(cy0 / 2 + cyy) * C.stride + cx0 / 2 + cxx] : 0;
+    }
+  }
+  int bref[NC], mvx[NC], mvy[NC];
+#pragma unroll
+  for (int c = 0; c < NC; c++) {  // wave-uniform: first-minimum reference
+    const int j = j0 + c;
+    const bool v = (vmask >> c) & 1;
     const hvx_me_result *r = M.res + ((size_t)ctu * HVX_CUS_PER_CTU + 21 + j) * L.nref;
     int best = 0;
     uint32_t bc = 0;
-    if (valid[c])
+    if (v)
       for (int k = 0; k < L.nref; k++) {
         const uint32_t ck = r[k].cost;
         if (k == 0 || ck < bc) { bc = ck; best = k; }
       }
     bref[c] = best;
-    mvx[c] = valid[c] ? r[best].mv_x : 0;
-    mvy[c] = valid[c] ? r[best].mv_y : 0;
+    mvx[c] = v ? r[best].mv_x : 0;
+    mvy[c] = v ? r[best].mv_y : 0;
     if (lane == c) {
       hvx_cu_result o;
-      o.valid = valid[c]; o.ref = best; o.mv_x = mvx[c]; o.mv_y = mvy[c];
-      o.me_cost = valid[c] ? bc : 0; o.sse = 0; o.abs_sum = 0; o.n_tu = valid[c] ? 1 : 0;
+      o.valid = v; o.ref = best; o.mv_x = mvx[c]; o.mv_y = mvy[c];
+      o.me_cost = v ? bc : 0; o.sse = 0; o.abs_sum = 0; o.n_tu = v ? 1 : 0;
       M.out[(size_t)ctu * HVX_CUS_PER_CTU + 21 + j] = o;
     }
   }
   const int nper = C.on ? 5 : 1;
   if (lane < NC * nper) {
     const int c = lane / nper;
-    ctu_desc<8>(M, ctu, j0 + c, c == 0 ? valid[0] : c == 1 ? valid[1] : c == 2 ? valid[2] : valid[3], 0, lane % nper);
+    ctu_desc<8>(M, ctu, j0 + c, (vmask >> c) & 1, 0, lane % nper);
   }
-  // luma: windows (rows y-3 .. y+11, columns x-3 .. x+11), first stage on all 15 rows, second stage
+  // reference windows: luma rows y-3 .. y+11, columns x-3 .. x+11; chroma rows yc-1 .. yc+5,
+  // columns xc-1 .. xc+5 at the 1/8-sample MV
 #pragma unroll
   for (int c = 0; c < NC; c++) {
-    if (!valid[c]) continue;
+    if (!((vmask >> c) & 1)) continue;
     const uint8_t *rp = M.refs[bref[c]] + (y[c] + (mvy[c] >> 2) - 3) * stride + x[c] + (mvx[c] >> 2) - 3;
     uint8_t *w = reinterpret_cast<uint8_t *>(winY[c]);
     for (int k = lane; k < 225; k += HVX_WAVE) {
       const int rr = k / 15, cc = k - rr * 15;
       w[rr * 16 + cc] = rp[rr * stride + cc] ^ 0x80;
     }
+    if (C.on) {
+      const int xc = x[c] / 2, yc = y[c] / 2, wo = (yc + (mvy[c] >> 3) - 1) * C.stride + xc + (mvx[c] >> 3) - 1;
+      if (lane < 49) {
+        const int rr = lane / 7, cc = lane - rr * 7;
+#pragma unroll
+        for (int comp = 0; comp < 2; comp++)
+          reinterpret_cast<uint8_t *>(winC[2 * c + comp])[rr * 8 + cc] = C.refs[comp * L.nref + bref[c]][wo + rr * C.stride + cc] ^ 0x80;
+      }
+    }
   }
   __syncthreads();
+  // first stages
 #pragma unroll
   for (int c = 0; c < NC; c++) {
-    if (!valid[c]) continue;
+    if (!((vmask >> c) & 1)) continue;
     const int fx = mvx[c] & 3;
     const int clo = (int)kLumaTap4[fx][0], chi = (int)kLumaTap4[fx][1];
     for (int k = lane; k < 120; k += HVX_WAVE) {
@@ -423,85 +460,55 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid8q(CtuMc M) {
       const uint32_t sh = xx & 3, lo = __builtin_amdgcn_alignbyte(w[1], w[0], sh), hi = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
       hsY[c][rr * 8 + xx] = (int16_t)__builtin_amdgcn_sdot4((int)lo, clo, __builtin_amdgcn_sdot4((int)hi, chi, 0, false), false);
     }
+    if (C.on) {
+      const int cw = (int)kChromaTap4[mvx[c] & 7];
+#pragma unroll
+      for (int comp = 0; comp < 2; comp++)
+        if (lane < 28) {
+          const int rr = lane >> 2, xx = lane & 3;
+          const uint32_t *w = winC[2 * c + comp] + rr * 2;
+          hsC[2 * c + comp][rr * 4 + xx] = (int16_t)__builtin_amdgcn_sdot4((int)__builtin_amdgcn_alignbyte(w[1], w[0], xx), cw, 0, false);
+        }
+    }
   }
   __syncthreads();
-  {
-    typedef short s2 __attribute__((ext_vector_type(2)));
-    const int yy = lane >> 3, xx = lane & 7;
+  typedef short s2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int c = 0; c < NC; c++) {
-      if (!valid[c]) continue;
-      const int fy = mvy[c] & 3;
-      int s = (1 << 11) + (8192 << 6);
+  for (int c = 0; c < NC; c++) {  // luma second stage, residual, prediction
+    if (!((vmask >> c) & 1)) continue;
+    const int fy = mvy[c] & 3;
+    int s = (1 << 11) + (8192 << 6);
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const s2 pr = {hsY[c][(yy + 2 * u) * 8 + xx], hsY[c][(yy + 2 * u + 1) * 8 + xx]};
-        s = __builtin_amdgcn_sdot2(pr, __builtin_bit_cast(s2, kLumaPairs[fy][u]), s, false);
-      }
-      const int pred = clip_pel(s >> 12);
-      const int64_t o = ctu_tu_offset(L, ctu_tu_index(L, ctu, 3, j0 + c, 0)) + lane;
-      M.resid[o] = (int16_t)((int)M.cur[(y[c] + yy) * stride + x[c] + xx] - pred);
-      M.pred_out[o] = (uint8_t)pred;
+    for (int u = 0; u < 4; u++) {
+      const s2 pr = {hsY[c][(ly + 2 * u) * 8 + lx], hsY[c][(ly + 2 * u + 1) * 8 + lx]};
+      s = __builtin_amdgcn_sdot2(pr, __builtin_bit_cast(s2, kLumaPairs[fy][u]), s, false);
     }
+    const int pred = clip_pel(s >> 12);
+    const int64_t o = ctu_tu_offset(L, ctu_tu_index(L, ctu, 3, j0 + c, 0)) + lane;
+    M.resid[o] = (int16_t)(curY[c] - pred);
+    M.pred_out[o] = (uint8_t)pred;
   }
   if (!C.on) return;
-  // Cb, Cr: windows (rows yc-1 .. yc+5, columns xc-1 .. xc+5 at the 1/8-sample MV), 4-tap stages
 #pragma unroll
-  for (int c = 0; c < NC; c++) {
-    if (!valid[c]) continue;
-    const int xc = x[c] / 2, yc = y[c] / 2, wo = (yc + (mvy[c] >> 3) - 1) * C.stride + xc + (mvx[c] >> 3) - 1;
-#pragma unroll
-    for (int comp = 0; comp < 2; comp++) {
-      const uint8_t *src = C.refs[comp * L.nref + bref[c]] + wo;
-      uint8_t *w = reinterpret_cast<uint8_t *>(winC[2 * c + comp]);
-      if (lane < 49) {
-        const int rr = lane / 7, cc = lane - rr * 7;
-        w[rr * 8 + cc] = src[rr * C.stride + cc] ^ 0x80;
-      }
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < NC; c++) {
-    if (!valid[c]) continue;
-    const int cw = (int)kChromaTap4[mvx[c] & 7];
-#pragma unroll
-    for (int comp = 0; comp < 2; comp++)
-      if (lane < 28) {
-        const int rr = lane >> 2, xx = lane & 3;
-        const uint32_t *w = winC[2 * c + comp] + rr * 2;
-        hsC[2 * c + comp][rr * 4 + xx] = (int16_t)__builtin_amdgcn_sdot4((int)__builtin_amdgcn_alignbyte(w[1], w[0], xx), cw, 0, false);
-      }
-  }
-  __syncthreads();
-  {
-    typedef short s2 __attribute__((ext_vector_type(2)));
-    const int yy = (lane >> 2) & 3, xx = lane & 3, comp = (lane >> 4) & 1, cq = lane >> 5;  // 2 CUs per pass
-#pragma unroll
-    for (int p = 0; p < NC / 2; p++) {
-      const int c = 2 * p + cq;
-      const bool v = c == 0 ? valid[0] : c == 1 ? valid[1] : c == 2 ? valid[2] : valid[3];
-      if (!v) continue;
-      const int cmx = c == 0 ? mvx[0] : c == 1 ? mvx[1] : c == 2 ? mvx[2] : mvx[3];
-      const int cmy = c == 0 ? mvy[0] : c == 1 ? mvy[1] : c == 2 ? mvy[2] : mvy[3];
-      const int cx = c == 0 ? x[0] : c == 1 ? x[1] : c == 2 ? x[2] : x[3];
-      const int cy = c == 0 ? y[0] : c == 1 ? y[1] : c == 2 ? y[2] : y[3];
-      (void)cmx;
-      const int fy = cmy & 7;
-      const int16_t *h = hsC[2 * c + comp];
-      int s = (1 << 11) + (8192 << 6);
-      const s2 p0 = {h[yy * 4 + xx], h[(yy + 1) * 4 + xx]}, p1 = {h[(yy + 2) * 4 + xx], h[(yy + 3) * 4 + xx]};
-      s = __builtin_amdgcn_sdot2(p0, __builtin_bit_cast(s2, kChromaPairs[fy][0]), s, false);
-      s = __builtin_amdgcn_sdot2(p1, __builtin_bit_cast(s2, kChromaPairs[fy][1]), s, false);
-      const int pred = clip_pel(s >> 12);
-      const int tu = ctu_tu_index(L, ctu, 3, j0 + c, 0, comp + 1);
-      const int16_t rv = (int16_t)((int)C.cur[comp][(cy / 2 + yy) * C.stride + cx / 2 + xx] - pred);
-      const int64_t o = ctu_tu_offset(L, tu) + yy * 4 + xx, ot = ctu_tu_offset(L, ctu_tu_ts(L, tu)) + yy * 4 + xx;
-      M.resid[o] = rv;
-      M.pred_out[o] = (uint8_t)pred;
-      M.resid[ot] = rv;
-      M.pred_out[ot] = (uint8_t)pred;
-    }
+  for (int p = 0; p < NC / 2; p++) {  // chroma second stage, two CUs per pass (lanes 32.. the odd one)
+    int c = 2 * p, cmy = mvy[2 * p];
+    bool v = (vmask >> (2 * p)) & 1;
+    if (cq) { c = 2 * p + 1; cmy = mvy[2 * p + 1]; v = (vmask >> (2 * p + 1)) & 1; }
+    if (!v) continue;
+    const int fy = cmy & 7;
+    const int16_t *h = hsC[2 * c + ccomp];
+    int s = (1 << 11) + (8192 << 6);
+    const s2 p0 = {h[cyy * 4 + cxx], h[(cyy + 1) * 4 + cxx]}, p1 = {h[(cyy + 2) * 4 + cxx], h[(cyy + 3) * 4 + cxx]};
+    s = __builtin_amdgcn_sdot2(p0, __builtin_bit_cast(s2, kChromaPairs[fy][0]), s, false);
+    s = __builtin_amdgcn_sdot2(p1, __builtin_bit_cast(s2, kChromaPairs[fy][1]), s, false);
+    const int pred = clip_pel(s >> 12);
+    const int tu = ctu_tu_index(L, ctu, 3, j0 + c, 0, ccomp + 1);
+    const int16_t rv = (int16_t)(curC[p] - pred);
+    const int64_t o = ctu_tu_offset(L, tu) + cyy * 4 + cxx, ot = ctu_tu_offset(L, ctu_tu_ts(L, tu)) + cyy * 4 + cxx;
+    M.resid[o] = rv;
+    M.pred_out[o] = (uint8_t)pred;
+    M.resid[ot] = rv;
+    M.pred_out[ot] = (uint8_t)pred;
   }
 }
 

@@ -59,6 +59,9 @@ struct hvx_ctx {
 #define HVX_STG_OUT (HVX_STG_ABS + 64)
 #define HVX_STG_SIZE (HVX_STG_OUT + 2048)
 
+#ifndef HVX_D3_NC
+#define HVX_D3_NC 4  // 8x8 CUs per wave of the depth-3 residual pass (8: 0.499 vs 0.473 ms isolated)
+#endif
 namespace {
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 // interleaved RDOQ scratch of the CTU pass: the 3 TU classes (8n 32x32, 16n 16x16, 64n 8x8),
@@ -769,7 +772,7 @@ static int ctu_analyze_impl(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *c
     if (d == 0) hipLaunchKernelGGL(k_ctu_pred_resid<64>, grid, blk, 0, s, M, 0);
     if (d == 1) hipLaunchKernelGGL(k_ctu_pred_resid<32>, grid, blk, 0, s, M, 0);
     if (d == 2) hipLaunchKernelGGL(k_ctu_pred_resid<16>, grid, blk, 0, s, M, 0);
-    if (d == 3) hipLaunchKernelGGL(k_ctu_pred_resid8q, dim3(n * 16), blk, 0, s, M);  // four 8x8 CUs per wave
+    if (d == 3) hipLaunchKernelGGL(k_ctu_pred_resid8q<HVX_D3_NC>, dim3(n * (64 / HVX_D3_NC)), blk, 0, s, M);  // NC 8x8 CUs per wave
   };
   for (int d = 0; d < 4; d++) {
     const int ncu = 1 << (2 * d), nt = L.nctu * ncu * L.nref;
