@@ -227,9 +227,11 @@ def main():
                        "n_ref": nref, "parallelism": f"segments x{world}",
                        "dpb": "gather of every rank's deblocked reference picture to rank 0 per step" if world > 1 else "local"},
             "phase_ms_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()},
-            # priced against HBM (integer work, no MFMA); the measured limiter is the
-            # serial per-lane decision chain, not bandwidth (frac << 1, PMC traffic in profiles/)
-            "roofline": {"bound": "hbm", "limiter": "latency", "kernel": kernel, "achieved": round(achieved, 3),
+            # priced against HBM (integer work); the measured limiter is VALU issue for
+            # the searches (SQ: VALU busy ~90% of the launch) and the serial per-lane decision chain
+            # for RDOQ / CABAC counting -- not bandwidth (frac << 1, PMC traffic in profiles/)
+            "roofline": {"bound": "hbm", "limiter": "valu-issue" if kernel.startswith("k_me") else "latency",
+                         "kernel": kernel, "achieved": round(achieved, 3),
                          "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / MI355X_HBM_PEAK_GBS,
                          "traffic": traffic, "bytes_per_launch": bytes_per_launch,
                          "avg_launch_ms": round(launch_ms, 3), "b_ctu": bpc,
