@@ -79,8 +79,9 @@ __device__ __forceinline__ int32_t sub32(int32_t a, int32_t b) { return (int32_t
 
 // TComRdCost::xGetExpGolombNumberOfBits (TComRdCost.cpp:279), closed form of the loop
 __device__ __forceinline__ uint32_t eg_bits(int v) {
-  uint32_t t = (v <= 0) ? ((uint32_t)(-v) << 1) + 1 : (uint32_t)v << 1;
-  return 1u + 2u * (31u - (uint32_t)__clz(t));
+  // t = 2|v| + (v <= 0) >= 1, branch-free (lanes are different candidates)
+  const uint32_t t = ((uint32_t)abs(v) << 1) | (v <= 0 ? 1u : 0u);
+  return 63u - 2u * (uint32_t)__builtin_clz(t);
 }
 
 // ---------------------------------------------------------------------------------------

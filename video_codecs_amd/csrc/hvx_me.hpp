@@ -33,7 +33,7 @@ struct MeRange { int l, r, t, b; };
 // the bound in each direction the point moved from the start -- a start outside the range
 // (the zero MV, a far predictor) still has its axis points searched.
 __device__ __forceinline__ bool me_in(const MeRange &g, int dx, int dy, int x, int y) {
-  return (dx >= 0 || x >= g.l) && (dx <= 0 || x <= g.r) && (dy >= 0 || y >= g.t) && (dy <= 0 || y <= g.b);
+  return ((dx >= 0) | (x >= g.l)) & ((dx <= 0) | (x <= g.r)) & ((dy >= 0) | (y >= g.t)) & ((dy <= 0) | (y <= g.b));
 }
 
 // TComDataCU::clipMv: quarter-pel, result stored as Short
@@ -304,6 +304,9 @@ __device__ __forceinline__ void me_eval_min(MeInt &m, int n, int nr, F cand, R r
   }
 }
 
+// diamonds d = 1, 2, 4, ... around (sx,sy), concatenated in xTZ8PointDiamondSearch order
+__device__ __forceinline__ int me_dia_start(int k) { return k == 0 ? 0 : k <= 3 ? 4 + 8 * (k - 1) : 28 + 16 * (k - 4); }
+
 // xTZSearchHelp applied to a list's first minimum (strict '<' against the running best)
 template <typename F>
 __device__ __forceinline__ void me_take(MeInt &m, uint32_t key, F cand) {
@@ -315,8 +318,6 @@ __device__ __forceinline__ void me_take(MeInt &m, uint32_t key, F cand) {
 
 __device__ __forceinline__ int me_rng0(int) { return 0; }
 
-// diamonds d = 1, 2, 4, ... around (sx,sy), concatenated in xTZ8PointDiamondSearch order
-__device__ __forceinline__ int me_dia_start(int k) { return k == 0 ? 0 : k <= 3 ? 4 + 8 * (k - 1) : 28 + 16 * (k - 4); }
 __device__ __forceinline__ int me_dia_k(int p) { return p < 4 ? 0 : p < 28 ? 1 + ((p - 4) >> 3) : 4 + ((p - 28) >> 4); }
 
 // Point p of that list as an offset from the start (xTZ8PointDiamondSearch :629-800: d = 1 is
