@@ -67,6 +67,15 @@ typedef struct hvx_coeff_bits {
   uint32_t num_sig;           /* non-zero coefficients (0: the reference's empty-TU exit, nothing coded) */
 } hvx_coeff_bits;
 
+/* The registers of the slice writer's arithmetic coder, TEncBinCABAC (TEncBinCoderCABAC.h):
+ * m_uiLow, m_uiRange, m_bitsLeft, m_numBufferedBytes, m_bufferedByte.  TEncBinCABAC::start()
+ * is {0, 510, 23, 0, 0xff}. */
+typedef struct hvx_cabac_regs {
+  uint32_t low, range;
+  int32_t bits_left, num_buffered;
+  uint32_t buffered_byte, pad;
+} hvx_cabac_regs;
+
 /* One uni-prediction motion search: TEncSearch::xMotionEstimation with bBi=false
  * (TEncSearch.cpp:3663-3760): TZ integer search + half/quarter refinement. */
 typedef struct hvx_me_job {

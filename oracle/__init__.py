@@ -347,6 +347,24 @@ def coeff_bits(desc, levels, states, entropy_bits):
     return int(out["frac_bits"][0]), int(out["rice_stat"][0]), int(out["num_sig"][0]), st[:len(states)].copy()
 
 
+def coeff_write(desc, levels, states, regs, cap=1 << 16):
+    """hvxo_coeff_write: TEncSbac::codeCoeffNxN through TEncBinCABAC.  regs = CABAC_REGS record
+    (or a 5/6-tuple) before the call.  Returns (bytes written, regs after, states after)."""
+    L = lib()
+    d = np.ascontiguousarray(desc, dtype=_abi.TU_DESC).reshape(1)
+    lv = _c(levels, np.int32)
+    st = np.zeros(256, np.uint8)
+    st[:len(states)] = states
+    r = np.zeros(1, _abi.CABAC_REGS)
+    r[0] = tuple(regs)[:5] + (0,) if not isinstance(regs, np.void) else regs
+    out = np.zeros(cap, np.uint8)
+    L.hvxo_coeff_write.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int]
+    L.hvxo_coeff_write.restype = ctypes.c_int
+    nb = L.hvxo_coeff_write(_p(d), _p(lv), _p(st), _p(r), _p(out), cap)
+    assert nb >= 0, "hvxo_coeff_write: output past cap"
+    return out[:nb].copy(), r[0], st[:len(states)].copy()
+
+
 # ------------------------------------------------------------------------------------------ intra
 def _intra_lib():
     L = lib()

@@ -44,6 +44,16 @@ cab "$TMP/cab_p.bin"   $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth.yuv" 3 27
 cab "$TMP/cab_p22.bin" $CFG/encoder_lowdelay_P_main.cfg "$TMP/rand.yuv"   2 22
 python3 oracle/merge_goldens.py tests/golden/cabac.bin "$TMP"/cab_i.bin "$TMP"/cab_i22.bin "$TMP"/cab_p.bin "$TMP"/cab_p22.bin
 python3 oracle/compact_cabac.py tests/golden/cabac.bin
+# CABAC residual writer: codeCoeffNxN through the real TEncBinCABAC of the slice writer
+# (registers and bytes, oracle/cabac_write_capture.cpp)
+cabw() {  # cabw <out.bin> <cfg> <yuv> <frames> <qp>
+  HVX_CAPTURE=$1 $ORC/TAppEncoder_cabwcap -c "$2" -i "$3" -wdt 416 -hgt 240 -fr 30 -f "$4" -q "$5" \
+    -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+}
+cabw "$TMP/cabw_i.bin" $CFG/encoder_intra_main.cfg      "$TMP/rand.yuv"   1 32
+cabw "$TMP/cabw_p.bin" $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth.yuv" 3 27
+cabw "$TMP/cabw_p22.bin" $CFG/encoder_lowdelay_P_main.cfg "$TMP/rand.yuv" 2 22
+python3 oracle/compact_cabac_write.py tests/golden/cabac_write.bin "$TMP"/cabw_i.bin "$TMP"/cabw_p.bin "$TMP"/cabw_p22.bin
 # intra reference samples, predictions and the first-pass mode search (oracle/intra_capture.cpp)
 icap() {  # icap <out.bin> <cfg> <yuv> <frames> <qp>
   HVX_CAPTURE=$1 $ORC/TAppEncoder_intracap -c "$2" -i "$3" -wdt 416 -hgt 240 -fr 30 -f "$4" -q "$5" \

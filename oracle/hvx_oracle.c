@@ -1886,25 +1886,193 @@ static const uint8_t kTransIdxLps[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7, 
                                          33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63};
 static const int kMinInGroup[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};
 
+/* Arithmetic coder of the slice writer, TEncBinCABAC (TEncBinCoderCABAC.cpp:60-460): rangeTabLps
+ * (TComCABACTables.cpp:44, the specification's Table 9-52) and the renormalisation shift table
+ * (:113). */
+static const uint8_t kLpsTable[64][4] = {
+  {128, 176, 208, 240},
+  {128, 167, 197, 227},
+  {128, 158, 187, 216},
+  {123, 150, 178, 205},
+  {116, 142, 169, 195},
+  {111, 135, 160, 185},
+  {105, 128, 152, 175},
+  {100, 122, 144, 166},
+  { 95, 116, 137, 158},
+  { 90, 110, 130, 150},
+  { 85, 104, 123, 142},
+  { 81,  99, 117, 135},
+  { 77,  94, 111, 128},
+  { 73,  89, 105, 122},
+  { 69,  85, 100, 116},
+  { 66,  80,  95, 110},
+  { 62,  76,  90, 104},
+  { 59,  72,  86,  99},
+  { 56,  69,  81,  94},
+  { 53,  65,  77,  89},
+  { 51,  62,  73,  85},
+  { 48,  59,  69,  80},
+  { 46,  56,  66,  76},
+  { 43,  53,  63,  72},
+  { 41,  50,  59,  69},
+  { 39,  48,  56,  65},
+  { 37,  45,  54,  62},
+  { 35,  43,  51,  59},
+  { 33,  41,  48,  56},
+  { 32,  39,  46,  53},
+  { 30,  37,  43,  50},
+  { 29,  35,  41,  48},
+  { 27,  33,  39,  45},
+  { 26,  31,  37,  43},
+  { 24,  30,  35,  41},
+  { 23,  28,  33,  39},
+  { 22,  27,  32,  37},
+  { 21,  26,  30,  35},
+  { 20,  24,  29,  33},
+  { 19,  23,  27,  31},
+  { 18,  22,  26,  30},
+  { 17,  21,  25,  28},
+  { 16,  20,  23,  27},
+  { 15,  19,  22,  25},
+  { 14,  18,  21,  24},
+  { 14,  17,  20,  23},
+  { 13,  16,  19,  22},
+  { 12,  15,  18,  21},
+  { 12,  14,  17,  20},
+  { 11,  14,  16,  19},
+  { 11,  13,  15,  18},
+  { 10,  12,  15,  17},
+  { 10,  12,  14,  16},
+  {  9,  11,  13,  15},
+  {  9,  11,  12,  14},
+  {  8,  10,  12,  14},
+  {  8,   9,  11,  13},
+  {  7,   9,  11,  12},
+  {  7,   9,  10,  12},
+  {  7,   8,  10,  11},
+  {  6,   8,   9,  11},
+  {  6,   7,   9,  10},
+  {  6,   7,   8,   9},
+  {  2,   2,   2,   2}};
+static const uint8_t kRenormTable[32] = {6, 5, 4, 4, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2,
+                                         1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+
+/* One coder for both bin sinks: w == NULL counts like TEncBinCABACCounter, otherwise the bins
+ * drive TEncBinCABAC's registers *w and the bytes go to out[0..cap) (nout counts every byte,
+ * also past cap). */
 typedef struct {
   uint8_t *st;
   const int32_t *eb;
   uint64_t frac;
+  hvx_cabac_regs *w;
+  uint8_t *out;
+  int nout, cap;
 } cab_counter;
 
-/* TEncBinCABACCounter::encodeBin + ContextModel::update */
+static void cab_put(cab_counter *c, uint32_t byte) {
+  if (c->nout < c->cap) c->out[c->nout] = (uint8_t)byte;
+  c->nout++;
+}
+/* TEncBinCABAC::writeOut (:425) / testAndWriteOut (:417) */
+static void cab_write_out(cab_counter *c) {
+  hvx_cabac_regs *r = c->w;
+  const uint32_t lead = r->low >> (24 - r->bits_left);
+  r->bits_left += 8;
+  r->low &= 0xffffffffu >> r->bits_left;
+  if (lead == 0xff) {
+    r->num_buffered++;
+  } else if (r->num_buffered > 0) {
+    const uint32_t carry = lead >> 8;
+    cab_put(c, r->buffered_byte + carry);
+    r->buffered_byte = lead & 0xff;
+    const uint32_t fill = (0xff + carry) & 0xff;
+    while (r->num_buffered > 1) {
+      cab_put(c, fill);
+      r->num_buffered--;
+    }
+  } else {
+    r->num_buffered = 1;
+    r->buffered_byte = lead;
+  }
+}
+static void cab_test(cab_counter *c) {
+  if (c->w->bits_left < 12) cab_write_out(c);
+}
+
+/* encodeBin (:200) or TEncBinCABACCounter::encodeBin, then ContextModel::update */
 static void cab_bin(cab_counter *c, int ctx, int v) {
   const int s = c->st[ctx], p = s >> 1, mps = s & 1;
-  c->frac += (uint32_t)c->eb[s ^ v];
+  if (c->w) {
+    hvx_cabac_regs *r = c->w;
+    const uint32_t lps = kLpsTable[p][(r->range >> 6) & 3];
+    r->range -= lps;
+    if (v != mps) {
+      const int nb = kRenormTable[lps >> 3];
+      r->low = (r->low + r->range) << nb;
+      r->range = lps << nb;
+      r->bits_left -= nb;
+      cab_test(c);
+    } else if (r->range < 256) {
+      r->low <<= 1;
+      r->range <<= 1;
+      r->bits_left--;
+      cab_test(c);
+    }
+  } else {
+    c->frac += (uint32_t)c->eb[s ^ v];
+  }
   if (v == mps) c->st[ctx] = (uint8_t)(((p < 62 ? p + 1 : p) << 1) | mps);
   else c->st[ctx] = (uint8_t)((kTransIdxLps[p] << 1) | (p == 0 ? mps ^ 1 : mps));
 }
-static inline void cab_ep(cab_counter *c, int n) { c->frac += 32768u * (uint32_t)n; } /* encodeBinsEP */
+/* encodeAlignedBinsEP (:334): only reachable with range == 256 (cabac_bypass_alignment) */
+static void cab_aligned_eps(cab_counter *c, uint32_t vals, int n) {
+  hvx_cabac_regs *r = c->w;
+  while (n > 0) {
+    const int k = n < 8 ? n : 8;
+    const uint32_t bins = (vals >> (n - k)) & ((1u << k) - 1);
+    r->low = (r->low << k) + (bins << 8);
+    n -= k;
+    r->bits_left -= k;
+    cab_test(c);
+  }
+}
+/* encodeBinEP (:262): one bypass bin */
+static void cab_ep1(cab_counter *c, uint32_t bin) {
+  if (!c->w) { c->frac += 32768u; return; }
+  hvx_cabac_regs *r = c->w;
+  if (r->range == 256) { cab_aligned_eps(c, bin, 1); return; }
+  r->low <<= 1;
+  if (bin) r->low += r->range;
+  r->bits_left--;
+  cab_test(c);
+}
+/* encodeBinsEP (:290): n bypass bins, most significant first, in pieces of 8 */
+static void cab_eps(cab_counter *c, uint32_t vals, int n) {
+  if (!c->w) { c->frac += 32768u * (uint32_t)n; return; }
+  hvx_cabac_regs *r = c->w;
+  if (r->range == 256) { cab_aligned_eps(c, vals, n); return; }
+  while (n > 8) {
+    n -= 8;
+    const uint32_t pat = vals >> n;
+    r->low <<= 8;
+    r->low += r->range * pat;
+    vals -= pat << n;
+    r->bits_left -= 8;
+    cab_test(c);
+  }
+  r->low <<= n;
+  r->low += r->range * vals;
+  r->bits_left -= n;
+  cab_test(c);
+}
 
-/* xWriteCoefRemainExGolomb (:337): number of bypass bins */
-static int remain_bins(uint32_t symbol, int r, int limited, int max_log2) {
-  if (symbol < (3u << r)) return (int)(symbol >> r) + 1 + r;
-  if (limited) {
+/* xWriteCoefRemainExGolomb (TEncSbac.cpp:337): the escape code of one level (COEF_REMAIN_BIN_REDUCTION 3) */
+static void cab_escape(cab_counter *c, uint32_t symbol, int r, int limited, int max_log2) {
+  if (symbol < (3u << r)) {
+    const uint32_t len = symbol >> r;
+    cab_eps(c, (1u << (len + 1)) - 2, (int)len + 1);
+    cab_eps(c, symbol % (1u << r), r);
+  } else if (limited) {
     const uint32_t maxp = 32 - (3 + max_log2);
     uint32_t prefix = 0, suffix_len;
     const uint32_t v = (symbol >> r) - 3;
@@ -1915,20 +2083,24 @@ static int remain_bins(uint32_t symbol, int r, int limited, int max_log2) {
       while (v > ((2u << prefix) - 2)) prefix++;
       suffix_len = prefix + 1;
     }
-    return (int)(prefix + 3 + suffix_len + r);
+    const uint32_t suffix = v - ((1u << prefix) - 1), tot = prefix + 3;
+    cab_eps(c, (1u << tot) - 1, (int)tot);
+    cab_eps(c, (suffix << r) | (symbol & ((1u << r) - 1)), (int)(suffix_len + r));
+  } else {
+    int len = r;
+    uint32_t cn = symbol - (3u << r);
+    while (cn >= (1u << len)) cn -= (1u << (len++));
+    cab_eps(c, (1u << (3 + len + 1 - r)) - 2, 3 + len + 1 - r);
+    cab_eps(c, cn, len);
   }
-  int len = r;
-  uint32_t cn = symbol - (3u << r);
-  while (cn >= (1u << len)) cn -= (1u << (len++));
-  return 3 + len + 1 - r + len;
 }
 
 static int log2_4_32(int n) { return n == 4 ? 2 : n == 8 ? 3 : n == 16 ? 4 : 5; }
 
-void hvxo_coeff_bits(const hvx_tu_desc *tu, const int32_t *coef, uint8_t *states, const int32_t *eb, hvx_coeff_bits *out) {
+static void coeff_code(const hvx_tu_desc *tu, const int32_t *coef, cab_counter *cc, hvx_coeff_bits *out) {
   const int w = tu->width, h = tu->height, lw = log2_4_32(w), lh = log2_4_32(h), n = w * h;
   const int ch = tu->comp ? 1 : 0;
-  cab_counter c = {states, eb, 0};
+  cab_counter c = *cc;
   uint32_t rice_stat = (uint32_t)tu->golomb_rice_stat;
   int num_sig = 0, i;
   for (i = 0; i < n; i++) num_sig += coef[i] != 0;
@@ -1968,9 +2140,9 @@ void hvxo_coeff_bits(const hvx_tu_desc *tu, const int32_t *coef, uint8_t *states
     if (gx < kGroupIdx[bw - 1]) cab_bin(&c, bx + (k >> sx), 0);
     for (k = 0; k < gy; k++) cab_bin(&c, by + (k >> sy), 1);
     if (gy < kGroupIdx[bh - 1]) cab_bin(&c, by + (k >> sy), 0);
-    if (gx > 3) cab_ep(&c, (gx - 2) >> 1);
-    if (gy > 3) cab_ep(&c, (gy - 2) >> 1);
-    (void)kMinInGroup;
+    /* the fixed-length suffixes, one encodeBinEP per bit, most significant first */
+    for (k = gx > 3 ? ((gx - 2) >> 1) - 1 : -1; k >= 0; k--) cab_ep1(&c, ((uint32_t)(px - kMinInGroup[gx]) >> k) & 1);
+    for (k = gy > 3 ? ((gy - 2) >> 1) - 1 : -1; k >= 0; k--) cab_ep1(&c, ((uint32_t)(py - kMinInGroup[gy]) >> k) & 1);
   }
   const int base_cg = 42 + ch * 2, base_sig = 46 + (ch ? 28 : 0);
   const int last_set = scan_last >> 4;
@@ -2031,14 +2203,15 @@ void hvxo_coeff_bits(const hvx_tu_desc *tu, const int32_t *coef, uint8_t *states
         if (gt2) escape = 1;
       }
       escape = escape || nnz > 8;
-      cab_ep(&c, (be_valid && hidden) ? nnz - 1 : nnz);
+      if (be_valid && hidden) cab_eps(&c, signs >> 1, nnz - 1); /* the first coefficient's sign is hidden */
+      else cab_eps(&c, signs, nnz);
       if (escape) {
         int first2 = 1;
         for (int k = 0; k < nnz; k++) {
           const int base = k < 8 ? 2 + first2 : 1;
           if (absc[k] >= base) {
             const uint32_t esc = (uint32_t)(absc[k] - base);
-            cab_ep(&c, remain_bins(esc, rice, tu->extended_precision, tu->max_log2_tr_range));
+            cab_escape(&c, esc, rice, tu->extended_precision, tu->max_log2_tr_range);
             if (absc[k] > (3 << rice)) rice = tu->persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
             if (upd_rice) {
               const uint32_t init = rice_stat / 4;
@@ -2054,6 +2227,24 @@ void hvxo_coeff_bits(const hvx_tu_desc *tu, const int32_t *coef, uint8_t *states
   }
   out->frac_bits = c.frac;
   out->rice_stat = rice_stat;
+  *cc = c;
+}
+
+void hvxo_coeff_bits(const hvx_tu_desc *tu, const int32_t *coef, uint8_t *states, const int32_t *eb, hvx_coeff_bits *out) {
+  cab_counter c = {states, eb, 0, NULL, NULL, 0, 0};
+  coeff_code(tu, coef, &c, out);
+}
+
+/* TEncSbac::codeCoeffNxN through the real arithmetic coder TEncBinCABAC: the same syntax and
+ * context evolution as hvxo_coeff_bits, the bins driving the registers *regs; the bytes the call
+ * completes go to out.  Returns the byte count (-1 past cap).  Main-profile scope as above (no
+ * cabac_bypass_alignment: the aligned path is restated but only reached with range 256). */
+int hvxo_coeff_write(const hvx_tu_desc *tu, const int32_t *coef, uint8_t *states, hvx_cabac_regs *regs, uint8_t *out,
+                     int cap) {
+  cab_counter c = {states, NULL, 0, regs, out, 0, cap};
+  hvx_coeff_bits o;
+  coeff_code(tu, coef, &c, &o);
+  return c.nout <= cap ? c.nout : -1;
 }
 
 /* ============================================================================================

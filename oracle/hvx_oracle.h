@@ -77,6 +77,11 @@ double hvxo_adjust_lambda(double lambda, double eta);
  * (raster), states = the RD coder's HVX_NUM_CTX context states (advanced in place), eb =
  * ContextModel::m_entropyBits (128) */
 void hvxo_coeff_bits(const hvx_tu_desc *tu, const int32_t *coef, uint8_t *states, const int32_t *eb, hvx_coeff_bits *out);
+/* TEncSbac::codeCoeffNxN written by TEncBinCABAC (TEncBinCoderCABAC.cpp): the same syntax, the
+ * bins driving *regs, the bytes the call completes into out (capacity cap); returns the byte
+ * count, -1 past cap */
+int hvxo_coeff_write(const hvx_tu_desc *tu, const int32_t *coef, uint8_t *states, hvx_cabac_regs *regs, uint8_t *out,
+                     int cap);
 
 /* ---- CTU analysis pass (the bench workload, hvx_types.h) ---- */
 void hvxo_ctu_tu_desc(const hvx_ctu_params *p, int cu_size, int log2, hvx_tu_desc *d);

@@ -143,6 +143,27 @@ def test_coeff_bits_golden():
         np.testing.assert_array_equal(st, g["states_after"][i], err_msg=f"record {i}")
 
 
+def test_coeff_write_golden():
+    # TEncSbac::codeCoeffNxN through the reference's real arithmetic coder TEncBinCABAC, one
+    # continuous stream over TUs sampled from intra and LDP encodes at QP 22-32
+    # (oracle/cabac_write_capture.cpp): levels + context states + coder registers before -> the
+    # bytes the call appended, the registers and context states after
+    g = gc.load("cabac_write.bin")
+    descs, levels = gc.cabac_cases(g)
+    n = len(levels)
+    assert n > 2000 and {int(w) for w in descs["width"]} == {4, 8, 16, 32} and descs["transform_skip"].any()
+    regs, bo = g["regs"], g["byte_off"]
+    carries = 0
+    for i in range(n):
+        got, r, st = oracle.coeff_write(descs[i], levels[i], g["states_before"][i], tuple(int(x) for x in regs[i, :5]))
+        np.testing.assert_array_equal(got, g["bytes"][bo[i]:bo[i + 1]], err_msg=f"record {i}")
+        assert tuple(int(r[k]) for k in ("low", "range", "bits_left", "num_buffered", "buffered_byte")) == \
+            tuple(int(x) for x in regs[i, 5:]), (i, r, regs[i])
+        np.testing.assert_array_equal(st, g["states_after"][i], err_msg=f"record {i}")
+        carries += int(regs[i, 8] > 1)
+    assert carries > 0  # runs of 0xff bytes held back for a carry occur in the stream
+
+
 def test_intra_reference_samples_golden():
     """fillReferenceSamples + smoothing vs 1188 initIntraPatternChType calls of real HM encodes."""
     g = gc.load("intra.bin")
