@@ -33,6 +33,9 @@
  *   hvx_coeff_bits_batch  TEncEntropy::encodeCoeffNxN -> TEncSbac::codeCoeffNxN (TEncEntropy.cpp:654,
  *                         TEncSbac.cpp:1181) under TEncBinCABACCounter (TEncBinCoderCABACCounter.cpp:74):
  *                         the RD search's coefficient rate (TEncSearch.cpp:969, 4706, 4875, 5136)
+ *   hvx_coeff_write_batch TEncSbac::codeCoeffNxN (TEncSbac.cpp:1181) through the slice writer's
+ *                         arithmetic coder TEncBinCABAC (TEncBinCoderCABAC.cpp:200-460): the residual
+ *                         syntax of TU runs written as CABAC bytes (TEncSlice::encodeSlice path)
  *   hvx_me_full_batch     TEncSearch::xMotionEstimation with xPatternSearch (:3786), incl. bBi
  *   hvx_ctu_analyze       TEncCu::compressCtu's inter 2Nx2N analysis for every CU of every CTU
  *                         (TEncCu.cpp:228,349,1291 -> predInterSearch/encodeResAndCalcRdInterCU):
@@ -237,6 +240,22 @@ int hvx_estbits_batch(hvx_ctx *ctx, const uint8_t *d_states, const int32_t *d_en
  * ------------------------------------------------------------------------------------- */
 int hvx_coeff_bits_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t *d_off, int n, const int32_t *d_levels,
                          const int32_t *d_entropy_bits, uint8_t *d_states, hvx_coeff_bits *d_out);
+
+/* ---------------------------------------------------------------------------------------
+ * CABAC residual writer (replaces TEncSbac::codeCoeffNxN with TEncBinCABAC as m_pcBinIf,
+ * TEncSbac.cpp:1181 / TEncBinCoderCABAC.cpp:200-460; called by TEncEntropy::encodeCoeffNxN,
+ * TEncEntropy.cpp:654, on the TEncSlice::encodeSlice path).  n_streams independent bitstream
+ * runs, one lane each: run k codes TUs [d_stream_first[k], d_stream_first[k+1]) (hvx_tu_desc
+ * and raster levels as in hvx_coeff_bits_batch) in order through ONE arithmetic coder whose
+ * registers start at d_regs[k] (TEncBinCABAC::start() = {0, 510, 23, 0, 0xff}) and whose context
+ * states start at d_states[k*HVX_NUM_CTX ..]; both are advanced in place.  The bytes the coder
+ * completes are written to d_out + d_out_off[k] (at most out_cap bytes) and counted in
+ * d_out_len[k] (-1: more than out_cap, -2: an unsupported TU shape).  Bytes still held in the
+ * registers (low, the buffered 0xff run) belong to the next call or to TEncBinCABAC::finish().
+ * ------------------------------------------------------------------------------------- */
+int hvx_coeff_write_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t *d_off, const int32_t *d_levels,
+                          const int32_t *d_stream_first, int n_streams, uint8_t *d_states, hvx_cabac_regs *d_regs,
+                          uint8_t *d_out, const int64_t *d_out_off, int out_cap, int32_t *d_out_len);
 
 /* ---------------------------------------------------------------------------------------
  * Intra (hvx_types.h hvx_intra_job).  d_rec = sample (0,0) of the 8-bit plane holding the

@@ -474,6 +474,73 @@ def check_coeff_bits_random(seed, n):
     return True
 
 
+def run_coeff_write(descs, levels, stream_first, states, regs, cap):
+    """hvx_coeff_write_batch on host arrays: stream k = TUs [stream_first[k], stream_first[k+1]).
+    Returns (list of byte arrays, regs after, states after)."""
+    import torch
+    ns = len(stream_first) - 1
+    off = np.concatenate([[0], np.cumsum([len(l) for l in levels])[:-1]]).astype(np.int64)
+    flat = np.concatenate(levels).astype(np.int32) if levels else np.zeros(1, np.int32)
+    d_st = torch.from_numpy(np.ascontiguousarray(states, np.uint8).reshape(-1).copy()).cuda()
+    d_rg = torch.from_numpy(np.ascontiguousarray(regs, _abi.CABAC_REGS).view(np.uint8).copy()).cuda()
+    out = torch.zeros(ns * cap, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(ns, dtype=torch.int32, device="cuda")
+    hvx.coeff_write_batch(hvx.to_device(descs), hvx.to_device(off), hvx.to_device(flat),
+                          hvx.to_device(np.asarray(stream_first, np.int32)), ns, d_st, d_rg, out,
+                          hvx.to_device(np.arange(ns, dtype=np.int64) * cap), cap, d_len)
+    torch.cuda.synchronize()
+    lens = d_len.cpu().numpy()
+    o = out.cpu().numpy().reshape(ns, cap)
+    assert (lens >= 0).all(), lens[lens < 0]
+    return [o[k, :lens[k]].copy() for k in range(ns)], d_rg.cpu().numpy().view(_abi.CABAC_REGS), \
+        d_st.cpu().numpy().reshape(ns, -1)
+
+
+def check_coeff_write_golden():
+    """Every record of cabac_write.bin as a one-TU run from its captured registers and states."""
+    g = gc.load("cabac_write.bin")
+    descs, levels = gc.cabac_cases(g)
+    n = len(levels)
+    regs = np.zeros(n, _abi.CABAC_REGS)
+    for k, f in enumerate(("low", "range", "bits_left", "num_buffered", "buffered_byte")):
+        regs[f] = g["regs"][:, k]
+    got, r, st = run_coeff_write(descs, levels, np.arange(n + 1), g["states_before"], regs, 4096)
+    bo = g["byte_off"]
+    for i in range(n):
+        np.testing.assert_array_equal(got[i], g["bytes"][bo[i]:bo[i + 1]], err_msg=f"record {i}")
+        assert tuple(int(r[i][f]) for f in ("low", "range", "bits_left", "num_buffered", "buffered_byte")) == \
+            tuple(int(x) for x in g["regs"][i, 5:]), (i, r[i], g["regs"][i])
+    np.testing.assert_array_equal(st, g["states_after"])
+    return n
+
+
+def check_coeff_write_random(seed, n_streams, max_tus):
+    """Random runs of random TUs (random_coeff_tus) from TEncBinCABAC::start() and random context
+    states; the oracle writes each run TU by TU carrying registers and states."""
+    rng = np.random.default_rng(seed)
+    counts = rng.integers(0, max_tus + 1, n_streams)
+    first = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    descs, levels, _ = random_coeff_tus(seed + 1, int(first[-1]))
+    states = rng.integers(0, 126, (n_streams, _abi.NUM_CTX)).astype(np.uint8)
+    regs = np.zeros(n_streams, _abi.CABAC_REGS)
+    regs[:] = _abi.CABAC_START
+    got, r, st = run_coeff_write(descs, levels, first, states, regs, 1 << 16)
+    total = 0
+    for k in range(n_streams):
+        rk, sk, exp = tuple(_abi.CABAC_START), states[k].copy(), []
+        for t in range(first[k], first[k + 1]):
+            b, rk, sk = oracle.coeff_write(descs[t], levels[t], sk, rk)
+            exp.append(b)
+        exp = np.concatenate(exp) if exp else np.zeros(0, np.uint8)
+        np.testing.assert_array_equal(got[k], exp, err_msg=f"run {k}")
+        assert tuple(int(r[k][f]) for f in ("low", "range", "bits_left", "num_buffered", "buffered_byte")) == \
+            tuple(int(rk[f]) if isinstance(rk, np.void) else int(rk[i]) for i, f in
+                  enumerate(("low", "range", "bits_left", "num_buffered", "buffered_byte"))), (k, r[k], rk)
+        np.testing.assert_array_equal(st[k], sk, err_msg=f"run {k}")
+        total += len(exp)
+    return int(first[-1]), total
+
+
 # ----------------------------------------------------------------------------------------- intra
 INTRA_TILE = 144  # a block at (8, 8) of its tile: above-right / below-left reach 8 + 128
 

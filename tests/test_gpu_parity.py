@@ -235,6 +235,19 @@ def test_coeff_bits_random_gpu(torch):
     assert gpu_cases.check_coeff_bits_random(seed=23, n=700)
 
 
+def test_coeff_write_golden_gpu(torch):
+    # the CABAC residual writer (TEncBinCABAC) on the device: the 2623 captured reference calls,
+    # each from its captured registers and context states -> bytes, registers, states
+    assert gpu_cases.check_coeff_write_golden() == 2623
+
+
+def test_coeff_write_random_gpu(torch):
+    # 200 runs of 0..12 random TUs (every size / scan / channel, transform skip, bypass, sign
+    # hiding, extended-precision escapes, persistent Rice) from start() vs the oracle, TU by TU
+    n_tu, n_bytes = gpu_cases.check_coeff_write_random(seed=41, n_streams=200, max_tus=12)
+    assert n_tu > 1000 and n_bytes > 100000
+
+
 def test_intra_reference_samples_golden_gpu(torch):
     # initIntraPatternChType: 1188 captured reference borders (unfiltered + smoothed), every size
     # and availability pattern; unavailable neighbour positions hold random bytes

@@ -28,6 +28,8 @@ __constant__ uint8_t kTransIdxLps[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7, 
                                          24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30, 31, 32, 32, 33,
                                          33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63};
 
+__constant__ uint8_t kMinInGroup[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};  // g_uiMinInGroup (TComRom.cpp)
+
 struct Shared {
   uint8_t st[kRows * 64];   // per-lane state columns
   uint8_t next[256];        // next[state*2 + bin]
@@ -38,7 +40,7 @@ struct Shared {
 __device__ __forceinline__ void init_tables(Shared &s, const int32_t *entropy_bits) {
   const int lane = threadIdx.x & 63;
   for (int i = lane; i < 128; i += 64) {
-    s.eb[i] = entropy_bits[i];
+    s.eb[i] = entropy_bits ? entropy_bits[i] : 0;  // the writer has no rate table
     const int p = i >> 1, mps = i & 1;
     s.next[i * 2 + mps] = (uint8_t)(((p < 62 ? p + 1 : p) << 1) | mps);                      // MPS
     s.next[i * 2 + (mps ^ 1)] = (uint8_t)((kTransIdxLps[p] << 1) | (p == 0 ? mps ^ 1 : mps)); // LPS
@@ -56,6 +58,10 @@ struct Lane {
     st = s->next[q * 2 + v];
   }
   __device__ __forceinline__ void ep(int n) { frac += 32768ull * (uint32_t)n; }
+  // the bypass forms the writer needs values for; the counter only counts them
+  __device__ __forceinline__ void ep_bits(uint32_t, int n) { ep(n); }
+  __device__ __forceinline__ void eps(uint32_t, int n) { ep(n); }
+  __device__ __forceinline__ void esc(uint32_t symbol, int r, bool limited, int max_log2);
 };
 
 // xWriteCoefRemainExGolomb (:337): bypass bins of one escape code
@@ -78,6 +84,10 @@ __device__ __forceinline__ int remain_bins(uint32_t symbol, int r, bool limited,
   uint32_t cn = symbol - (3u << r);
   while (cn >= (1u << len)) cn -= (1u << (len++));
   return 3 + len + 1 - r + len;
+}
+
+__device__ __forceinline__ void Lane::esc(uint32_t symbol, int r, bool limited, int max_log2) {
+  ep(remain_bins(symbol, r, limited, max_log2));
 }
 
 __device__ __forceinline__ int log2_tu(int n) { return n == 4 ? 2 : n == 8 ? 3 : n == 16 ? 4 : 5; }
@@ -107,8 +117,8 @@ __device__ __forceinline__ int sig_ctx(int pattern, int first_sig, int single, i
 // Coefficient groups are the unit of work: each group's 16 levels are fetched by 16
 // independent loads into registers (fully unrolled, static indices), so a group costs one
 // memory latency, and every later pass over the group reads registers.
-template <class LevAt>
-__device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &rice_stat) {
+template <class LevAt, class C>
+__device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, C &L, uint32_t &rice_stat) {
   const int n = d.width, lw = log2_tu(n), l = lw - 2, wg = n >> 2, ncg = wg * wg;
   const int ch = d.comp ? 1 : 0;
   const uint8_t *scan_cg = kScanCG[d.scan_type] + cg_base(l);
@@ -150,8 +160,9 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
     if (gx < gmax) L.bin(bx + (k >> sh), 0);
     for (k = 0; k < gy; k++) L.bin(by + (k >> sh), 1);
     if (gy < gmax) L.bin(by + (k >> sh), 0);
-    if (gx > 3) L.ep((gx - 2) >> 1);
-    if (gy > 3) L.ep((gy - 2) >> 1);
+    // the fixed-length suffixes: one encodeBinEP per bit, most significant first
+    if (gx > 3) L.ep_bits((uint32_t)(px - kMinInGroup[gx]), (gx - 2) >> 1);
+    if (gy > 3) L.ep_bits((uint32_t)(py - kMinInGroup[gy]), (gy - 2) >> 1);
   }
   const int base_cg = kSigCG + ch * 2, base_sig = kSig + (ch ? 28 : 0);
   const int last_set = scan_last >> 4, last_pin = scan_last & 15;
@@ -171,6 +182,7 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
     // significance flags (reverse scan inside the group); non-zero count, first/last positions
     const bool is_last_set = sub == last_set;
     int nnz = is_last_set ? 1 : 0, last_nz = is_last_set ? last_pin : -1, first_nz = is_last_set ? last_pin : 16;
+    uint32_t signs = is_last_set ? (uint32_t)(a[last_pin] < 0) : 0u;  // coeffSigns, in coding order
     if ((cgm >> cg) & 1) {
       int pattern = 0;
       if (wg > 1) {
@@ -185,6 +197,7 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
         if (pin > 0 || sub == 0 || nnz) L.bin(base_sig + sig_ctx(pattern, first_sig, single, scan[sub_pos + pin], lw, ch), sig);
         if (sig) {
           nnz++;
+          signs = 2 * signs + (uint32_t)(a[pin] < 0);
           if (last_nz == -1) last_nz = pin;
           first_nz = pin;
         }
@@ -219,7 +232,8 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
       L.bin(kAbs + set, gt2);
       if (gt2) escape = true;
     }
-    L.ep((be_valid && hidden) ? nnz - 1 : nnz);
+    if (be_valid && hidden) L.eps(signs >> 1, nnz - 1);  // the first coefficient's sign is hidden
+    else L.eps(signs, nnz);
     if (escape) {
       int rice = (int)(rice_stat / 4);
       bool upd = d.persistent_rice != 0;
@@ -232,7 +246,7 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
         const int base = idx < 8 ? 2 + first2 : 1;
         if (av >= base) {
           const uint32_t esc = (uint32_t)(av - base);
-          L.ep(remain_bins(esc, rice, d.extended_precision != 0, d.max_log2_tr_range));
+          L.esc(esc, rice, d.extended_precision != 0, d.max_log2_tr_range);
           if (av > (3 << rice)) rice = d.persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
           if (upd) {
             const uint32_t init = rice_stat / 4;
@@ -248,6 +262,151 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, Lane &L, uint32_t &ri
   }
   return num_sig;
 }
+
+// ---------------------------------------------------------------------------------------------
+// The slice writer's arithmetic coder, TEncBinCABAC (TEncBinCoderCABAC.cpp:60-460), as a second
+// bin sink for coeff_bits: the same context evolution as the counter, the bins driving the
+// lane's registers, completed bytes appended to the lane's output run.  rangeTabLps
+// (TComCABACTables.cpp:44, the specification's Table 9-52) is staged in LDS; renormalisation
+// shifts are the reference's table (:113).
+// ---------------------------------------------------------------------------------------------
+__constant__ uint8_t kLpsTable[64 * 4] = {
+    128, 176, 208, 240, 128, 167, 197, 227, 128, 158, 187, 216, 123, 150, 178, 205, 116, 142, 169, 195,
+    111, 135, 160, 185, 105, 128, 152, 175, 100, 122, 144, 166, 95,  116, 137, 158, 90,  110, 130, 150,
+    85,  104, 123, 142, 81,  99,  117, 135, 77,  94,  111, 128, 73,  89,  105, 122, 69,  85,  100, 116,
+    66,  80,  95,  110, 62,  76,  90,  104, 59,  72,  86,  99,  56,  69,  81,  94,  53,  65,  77,  89,
+    51,  62,  73,  85,  48,  59,  69,  80,  46,  56,  66,  76,  43,  53,  63,  72,  41,  50,  59,  69,
+    39,  48,  56,  65,  37,  45,  54,  62,  35,  43,  51,  59,  33,  41,  48,  56,  32,  39,  46,  53,
+    30,  37,  43,  50,  29,  35,  41,  48,  27,  33,  39,  45,  26,  31,  37,  43,  24,  30,  35,  41,
+    23,  28,  33,  39,  22,  27,  32,  37,  21,  26,  30,  35,  20,  24,  29,  33,  19,  23,  27,  31,
+    18,  22,  26,  30,  17,  21,  25,  28,  16,  20,  23,  27,  15,  19,  22,  25,  14,  18,  21,  24,
+    14,  17,  20,  23,  13,  16,  19,  22,  12,  15,  18,  21,  12,  14,  17,  20,  11,  14,  16,  19,
+    11,  13,  15,  18,  10,  12,  15,  17,  10,  12,  14,  16,  9,   11,  13,  15,  9,   11,  12,  14,
+    8,   10,  12,  14,  8,   9,   11,  13,  7,   9,   11,  12,  7,   9,   10,  12,  7,   8,   10,  11,
+    6,   8,   9,   11,  6,   7,   9,   10,  6,   7,   8,   9,   2,   2,   2,   2};
+__constant__ uint8_t kRenormTable[32] = {6, 5, 4, 4, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2,
+                                         1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+
+struct Writer {
+  uint8_t *col;          // &s.st[lane]
+  const Shared *s;
+  const uint8_t *lps;    // LDS copy of kLpsTable
+  uint32_t low, range;   // m_uiLow, m_uiRange
+  int bits_left, nbuf;   // m_bitsLeft, m_numBufferedBytes
+  uint32_t buffered;     // m_bufferedByte
+  uint8_t *out;
+  int nout, cap;
+  __device__ __forceinline__ void put(uint32_t b) {
+    if (nout < cap) out[nout] = (uint8_t)b;
+    nout++;
+  }
+  // writeOut (:425): the lead byte; 0xff bytes are held back until a carry can no longer reach them
+  __device__ __noinline__ void write_out() {
+    const uint32_t lead = low >> (24 - bits_left);
+    bits_left += 8;
+    low &= 0xffffffffu >> bits_left;
+    if (lead == 0xff) {
+      nbuf++;
+    } else if (nbuf > 0) {
+      const uint32_t carry = lead >> 8;
+      put(buffered + carry);
+      buffered = lead & 0xff;
+      const uint32_t fill = (0xff + carry) & 0xff;
+      for (; nbuf > 1; nbuf--) put(fill);
+    } else {
+      nbuf = 1;
+      buffered = lead;
+    }
+  }
+  __device__ __forceinline__ void test() {
+    if (bits_left < 12) write_out();
+  }
+  // encodeBin (:200) + ContextModel::update
+  __device__ __forceinline__ void bin(int row, int v) {
+    uint8_t &st = col[row * 64];
+    const int q = st, mps = q & 1;
+    const uint32_t l = lps[(q >> 1) * 4 + ((range >> 6) & 3)];
+    range -= l;
+    if (v != mps) {
+      const int nb = kRenormTable[l >> 3];
+      low = (low + range) << nb;
+      range = l << nb;
+      bits_left -= nb;
+      test();
+    } else if (range < 256) {
+      low <<= 1;
+      range <<= 1;
+      bits_left--;
+      test();
+    }
+    st = s->next[q * 2 + v];
+  }
+  // encodeAlignedBinsEP (:334): reached only with range == 256 (cabac_bypass_alignment)
+  __device__ void aligned(uint32_t vals, int n) {
+    while (n > 0) {
+      const int k = n < 8 ? n : 8;
+      low = (low << k) + (((vals >> (n - k)) & ((1u << k) - 1)) << 8);
+      n -= k;
+      bits_left -= k;
+      test();
+    }
+  }
+  // encodeBinEP (:262)
+  __device__ __forceinline__ void ep1(uint32_t b) {
+    if (range == 256) { aligned(b, 1); return; }
+    low <<= 1;
+    if (b) low += range;
+    bits_left--;
+    test();
+  }
+  // codeLastSignificantXY's suffix (TEncSbac.cpp:1163-1180): one encodeBinEP per bit, msb first
+  __device__ __forceinline__ void ep_bits(uint32_t v, int n) {
+    for (int i = n - 1; i >= 0; i--) ep1((v >> i) & 1u);
+  }
+  // encodeBinsEP (:290): most significant first, in pieces of 8
+  __device__ __forceinline__ void eps(uint32_t vals, int n) {
+    if (range == 256) { aligned(vals, n); return; }
+    while (n > 8) {
+      n -= 8;
+      const uint32_t pat = vals >> n;
+      low = (low << 8) + range * pat;
+      vals -= pat << n;
+      bits_left -= 8;
+      test();
+    }
+    low = (low << n) + range * vals;
+    bits_left -= n;
+    test();
+  }
+  // xWriteCoefRemainExGolomb (TEncSbac.cpp:337), COEF_REMAIN_BIN_REDUCTION 3
+  __device__ void esc(uint32_t symbol, int r, bool limited, int max_log2) {
+    if (symbol < (3u << r)) {
+      const uint32_t len = symbol >> r;
+      eps((1u << (len + 1)) - 2, (int)len + 1);
+      eps(symbol & ((1u << r) - 1), r);
+    } else if (limited) {
+      const uint32_t maxp = 32 - (3 + max_log2);
+      uint32_t prefix = 0, suffix_len;
+      const uint32_t v = (symbol >> r) - 3;
+      if (v >= ((1u << maxp) - 1)) {
+        prefix = maxp;
+        suffix_len = (uint32_t)(max_log2 - r);
+      } else {
+        while (v > ((2u << prefix) - 2)) prefix++;
+        suffix_len = prefix + 1;
+      }
+      const uint32_t suffix = v - ((1u << prefix) - 1), tot = prefix + 3;
+      eps((1u << tot) - 1, (int)tot);
+      eps((suffix << r) | (symbol & ((1u << r) - 1)), (int)(suffix_len + r));
+    } else {
+      int len = r;
+      uint32_t cn = symbol - (3u << r);
+      while (cn >= (1u << len)) cn -= (1u << (len++));
+      eps((1u << (3 + len + 1 - r)) - 2, 3 + len + 1 - r);
+      eps(cn, len);
+    }
+  }
+};
 
 // copy the lanes' states between global (`stride` bytes per TU; stride 0 = one snapshot shared
 // by every TU) and the LDS columns, coalesced across the wave; tu0 = first TU of the wave,
@@ -331,4 +490,49 @@ __global__ __launch_bounds__(64) void k_coeff_bits_il(const hvx_tu_desc *__restr
     r.num_sig = (uint32_t)ns;
   }
   out[t] = r;
+}
+
+// hvx_coeff_write_batch: stream k = lane (k % 64) of block k / 64 writes TUs
+// [stream_first[k], stream_first[k + 1]) through one TEncBinCABAC, from its own context states
+// (states + k * HVX_NUM_CTX, advanced in place) and registers (regs[k], advanced in place); the
+// completed bytes go to out + out_off[k] (at most out_cap), their count to out_len[k] (-1: past
+// out_cap, -2: a TU geometry the coder does not take).  Raster int32 levels at levels + offs[t].
+__global__ __launch_bounds__(64) void k_coeff_write(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
+                                                    const int32_t *__restrict__ levels,
+                                                    const int32_t *__restrict__ stream_first, int n_streams,
+                                                    uint8_t *__restrict__ states, hvx_cabac_regs *__restrict__ regs,
+                                                    uint8_t *__restrict__ out, const int64_t *__restrict__ out_off,
+                                                    int out_cap, int32_t *__restrict__ out_len) {
+  __shared__ cab::Shared s;
+  __shared__ uint8_t lps[256];
+  const int lane = threadIdx.x, k0 = blockIdx.x * 64, cnt = min(64, n_streams - k0), k = k0 + lane;
+  cab::init_tables(s, nullptr);
+  for (int i = lane; i < 256; i += 64) lps[i] = cab::kLpsTable[i];
+  cab::states_load(s, states, (size_t)HVX_NUM_CTX, k0, cnt);
+  __syncthreads();
+  if (lane < cnt) {
+    const hvx_cabac_regs r0 = regs[k];
+    cab::Writer W{&s.st[lane], &s, lps, r0.low, r0.range, r0.bits_left, r0.num_buffered, r0.buffered_byte,
+                  out + out_off[k], 0, out_cap};
+    bool ok = true;
+    for (int t = stream_first[k]; t < stream_first[k + 1] && ok; t++) {
+      const hvx_tu_desc d = descs[t];
+      if ((d.width == 4 || d.width == 8 || d.width == 16 || d.width == 32) && d.height == d.width &&
+          (unsigned)d.scan_type <= 2u) {
+        const int32_t *lv = levels + offs[t];
+        const uint16_t *scan = kScan[d.scan_type] + scan_base(cab::log2_tu(d.width) - 2);
+        uint32_t rice = (uint32_t)d.golomb_rice_stat;
+        cab::coeff_bits(d, [&](int sp) { return lv[scan[sp]]; }, W, rice);
+      } else {
+        ok = false;
+      }
+    }
+    hvx_cabac_regs r1;
+    r1.low = W.low; r1.range = W.range; r1.bits_left = W.bits_left; r1.num_buffered = W.nbuf;
+    r1.buffered_byte = W.buffered; r1.pad = 0;
+    regs[k] = r1;
+    out_len[k] = !ok ? -2 : W.nout <= out_cap ? W.nout : -1;
+  }
+  __syncthreads();
+  cab::states_store(s, states, k0, cnt);
 }

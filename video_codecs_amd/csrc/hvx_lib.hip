@@ -648,6 +648,19 @@ int hvx_coeff_bits_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t 
   return launched("k_coeff_bits");
 }
 
+int hvx_coeff_write_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t *d_off, const int32_t *d_levels,
+                          const int32_t *d_stream_first, int n_streams, uint8_t *d_states, hvx_cabac_regs *d_regs,
+                          uint8_t *d_out, const int64_t *d_out_off, int out_cap, int32_t *d_out_len) {
+  if (!ctx || n_streams < 0 || out_cap < 0 ||
+      (n_streams && (!d_desc || !d_off || !d_levels || !d_stream_first || !d_states || !d_regs || !d_out ||
+                     !d_out_off || !d_out_len)))
+    return fail(HVX_E_INVALID, "hvx_coeff_write_batch: bad args");
+  if (!n_streams) return HVX_OK;
+  hipLaunchKernelGGL(k_coeff_write, dim3((n_streams + 63) / 64), dim3(64), 0, ctx->stream, d_desc, d_off, d_levels,
+                     d_stream_first, n_streams, d_states, d_regs, d_out, d_out_off, out_cap, d_out_len);
+  return launched("k_coeff_write");
+}
+
 int hvx_me_full_batch(hvx_ctx *ctx, const int16_t *const *d_tgt_planes, int tgt_stride,
                       const uint8_t *const *d_ref_planes, int stride, const hvx_me_job *d_jobs, int n,
                       hvx_me_result *d_out) {

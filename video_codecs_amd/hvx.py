@@ -47,7 +47,7 @@ def lib():
             "hvx_ctu_encode_yuv": [P, P, P, I, P, P, P, P, P, P, ctypes.c_size_t, P, P, P, P],
             "hvx_set_timing": [P, I], "hvx_phase_times": [P, ctypes.POINTER(ctypes.c_double), I, I],
             "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
-            "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P],
+            "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_coeff_write_batch": [P, P, P, P, P, I, P, P, P, P, I, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P],
             "hvx_intra_pred_batch": [P, P, I, P, I, P, P, P], "hvx_deblock": [P, P, I, P, P, I, P, P, P, P], "hvx_sao_stats": [P, P, P, P, I, I, P, P, P, I, I, I, I, P], "hvx_sao_apply": [P, P, P, P, I, I, P, P, P, I, I, I, I, P], "hvx_intra_search_batch": [P, P, P, I, P, I, P, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
             "hvx_free": [P, P], "hvx_upload": [P, P, P, ctypes.c_size_t], "hvx_download": [P, P, P, ctypes.c_size_t],
         }.items():
@@ -195,6 +195,14 @@ def coeff_bits_batch(desc_dev, off_dev, n, levels, entropy_dev, states_dev, out_
     """hvx_coeff_bits_batch: TEncSbac::codeCoeffNxN under TEncBinCABACCounter, one TU per lane."""
     _check(lib().hvx_coeff_bits_batch(context(), _ptr(desc_dev), _ptr(off_dev), n, _ptr(levels), _ptr(entropy_dev),
                                       _ptr(states_dev), _ptr(out_dev)), "hvx_coeff_bits_batch")
+
+
+def coeff_write_batch(desc_dev, off_dev, levels, stream_first_dev, n_streams, states_dev, regs_dev, out_dev, out_off_dev,
+                      out_cap, out_len_dev):
+    """hvx_coeff_write_batch: TEncSbac::codeCoeffNxN through TEncBinCABAC, one bitstream run per lane."""
+    _check(lib().hvx_coeff_write_batch(context(), _ptr(desc_dev), _ptr(off_dev), _ptr(levels), _ptr(stream_first_dev),
+                                       n_streams, _ptr(states_dev), _ptr(regs_dev), _ptr(out_dev), _ptr(out_off_dev),
+                                       out_cap, _ptr(out_len_dev)), "hvx_coeff_write_batch")
 
 
 def me_full_batch(tgt_planes, tgt_stride, ref_planes, stride, jobs_dev, n, out):
