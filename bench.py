@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--no-ssim", action="store_true", help="skip the SSIM-RDO side measurement")
     p.add_argument("--no-1080p", action="store_true", help="skip the 1080p side measurement")
     p.add_argument("--no-sao", action="store_true", help="skip the SAO side measurement")
+    p.add_argument("--no-cabac", action="store_true", help="skip the CABAC residual writer side measurement")
     return p.parse_args()
 
 
@@ -249,6 +250,8 @@ def main():
             out["ssim_rdo"] = ssim_rdo_measure(inp, W, H, nref, args.steps)
         if world == 1 and not args.no_sao:
             out["sao"] = sao_measure(W, H, args.steps)
+        if world == 1 and not args.no_cabac:
+            out["cabac_write"] = cabac_write_measure(args.steps)
         if world == 1 and not args.no_intra:
             out["intra_first_pass"] = intra_measure(cur_t, inp.refs[0][0], W, H, float(an.params["lambda"][0]),
                                                     args.steps)
@@ -344,6 +347,65 @@ def sao_measure(W, H, steps):
         res[name] = {"ms_per_picture": round(ms, 4), "algorithmic_gbs": round(gbs, 1),
                      "frac_hbm": round(gbs / MI355X_HBM_PEAK_GBS, 4)}
     return res
+
+
+def cabac_write_measure(steps, n_runs=2040, seed=9):
+    """Side measurement (not the headline): hvx_coeff_write_batch writing the
+    residual syntax of a 2160p picture's worth of TUs through TEncBinCABAC, one run per CTU (16
+    luma 16x16 + 8 chroma 8x8 TUs; synthetic levels: 30% non-zero, magnitudes 1-3 with 10%
+    escapes up to 40, random signs), every run from TEncBinCABAC::start() and the same context
+    snapshot -- wall time per launch, TUs/s and output MB/s.  Runs are serial inside (the coder's
+    registers), parallel across runs."""
+    import torch
+    from video_codecs_amd import _abi, hvx
+    rng = np.random.default_rng(seed)
+    sizes = np.tile(np.array([16] * 16 + [8] * 8), n_runs)
+    comps = np.tile(np.array([0] * 16 + [1] * 4 + [2] * 4), n_runs)
+    n = len(sizes)
+    d = np.zeros(n, _abi.TU_DESC)
+    d["width"] = d["height"] = sizes
+    d["log2_size"] = np.log2(sizes).astype(np.int32)
+    d["comp"] = comps
+    d["sign_hiding"] = 1
+    d["pps_tskip"] = 1
+    d["max_log2_tr_range"] = 15
+    d["bit_depth"] = 8
+    lev = []
+    for w in sizes:
+        a = (rng.random(w * w) < 0.3) * rng.integers(1, 4, w * w)
+        a = np.where(rng.random(w * w) < 0.1, a * rng.integers(1, 14, w * w), a)
+        a[0] = max(a[0], 1)
+        lev.append(np.where(rng.random(w * w) < 0.5, -a, a).astype(np.int32))
+    off = np.concatenate([[0], np.cumsum(sizes * sizes)[:-1]]).astype(np.int64)
+    first = np.arange(n_runs + 1, dtype=np.int32) * 24
+    st0 = np.tile(rng.integers(0, 126, _abi.NUM_CTX).astype(np.uint8), n_runs)
+    rg0 = np.zeros(n_runs, _abi.CABAC_REGS)
+    rg0[:] = _abi.CABAC_START
+    cap = 1 << 14
+    d_desc, d_off, d_lev = hvx.to_device(d), hvx.to_device(off), hvx.to_device(np.concatenate(lev))
+    d_first, d_oo = hvx.to_device(first), hvx.to_device(np.arange(n_runs, dtype=np.int64) * cap)
+    d_st = torch.from_numpy(st0).cuda()
+    d_rg = torch.from_numpy(rg0.view(np.uint8).copy()).cuda()
+    out = torch.empty(n_runs * cap, dtype=torch.uint8, device="cuda")
+    d_len = torch.empty(n_runs, dtype=torch.int32, device="cuda")
+    st0_d, rg0_d = d_st.clone(), d_rg.clone()
+
+    def run():
+        d_st.copy_(st0_d)
+        d_rg.copy_(rg0_d)
+        hvx.coeff_write_batch(d_desc, d_off, d_lev, d_first, n_runs, d_st, d_rg, out, d_oo, cap, d_len)
+
+    run()
+    torch.cuda.synchronize()
+    nbytes = int(d_len.sum().item())
+    assert (d_len >= 0).all().item()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    return {"runs": n_runs, "tus": n, "bytes": nbytes, "ms_per_launch": round(ms, 3),
+            "tus_per_s": round(n / ms * 1e3, 1), "output_mb_per_s": round(nbytes / ms / 1e3, 2)}
 
 
 def intra_measure(cur_t, rec_t, W, H, lam, steps):
