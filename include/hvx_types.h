@@ -69,11 +69,12 @@ typedef struct hvx_coeff_bits {
 
 /* The registers of the slice writer's arithmetic coder, TEncBinCABAC (TEncBinCoderCABAC.h):
  * m_uiLow, m_uiRange, m_bitsLeft, m_numBufferedBytes, m_bufferedByte.  TEncBinCABAC::start()
- * is {0, 510, 23, 0, 0xff}. */
+ * is {0, 510, 23, 0, 0xff}.  bins counts the bins coded (context, bypass), as m_uiBinsCoded
+ * does with m_binCountIncrement 1; the writer adds to it. */
 typedef struct hvx_cabac_regs {
   uint32_t low, range;
   int32_t bits_left, num_buffered;
-  uint32_t buffered_byte, pad;
+  uint32_t buffered_byte, bins;
 } hvx_cabac_regs;
 
 /* One uni-prediction motion search: TEncSearch::xMotionEstimation with bBi=false

@@ -356,7 +356,7 @@ def coeff_write(desc, levels, states, regs, cap=1 << 16):
     st = np.zeros(256, np.uint8)
     st[:len(states)] = states
     r = np.zeros(1, _abi.CABAC_REGS)
-    r[0] = tuple(regs)[:5] + (0,) if not isinstance(regs, np.void) else regs
+    r[0] = (tuple(regs) + (0,))[:6] if not isinstance(regs, np.void) else regs
     out = np.zeros(cap, np.uint8)
     L.hvxo_coeff_write.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int]
     L.hvxo_coeff_write.restype = ctypes.c_int

@@ -2004,6 +2004,7 @@ static void cab_bin(cab_counter *c, int ctx, int v) {
   const int s = c->st[ctx], p = s >> 1, mps = s & 1;
   if (c->w) {
     hvx_cabac_regs *r = c->w;
+    r->bins++;
     const uint32_t lps = kLpsTable[p][(r->range >> 6) & 3];
     r->range -= lps;
     if (v != mps) {
@@ -2040,6 +2041,7 @@ static void cab_aligned_eps(cab_counter *c, uint32_t vals, int n) {
 static void cab_ep1(cab_counter *c, uint32_t bin) {
   if (!c->w) { c->frac += 32768u; return; }
   hvx_cabac_regs *r = c->w;
+  r->bins++;
   if (r->range == 256) { cab_aligned_eps(c, bin, 1); return; }
   r->low <<= 1;
   if (bin) r->low += r->range;
@@ -2050,6 +2052,7 @@ static void cab_ep1(cab_counter *c, uint32_t bin) {
 static void cab_eps(cab_counter *c, uint32_t vals, int n) {
   if (!c->w) { c->frac += 32768u * (uint32_t)n; return; }
   hvx_cabac_regs *r = c->w;
+  r->bins += (uint32_t)n;
   if (r->range == 256) { cab_aligned_eps(c, vals, n); return; }
   while (n > 8) {
     n -= 8;

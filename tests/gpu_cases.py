@@ -533,9 +533,9 @@ def check_coeff_write_random(seed, n_streams, max_tus):
             exp.append(b)
         exp = np.concatenate(exp) if exp else np.zeros(0, np.uint8)
         np.testing.assert_array_equal(got[k], exp, err_msg=f"run {k}")
-        assert tuple(int(r[k][f]) for f in ("low", "range", "bits_left", "num_buffered", "buffered_byte")) == \
-            tuple(int(rk[f]) if isinstance(rk, np.void) else int(rk[i]) for i, f in
-                  enumerate(("low", "range", "bits_left", "num_buffered", "buffered_byte"))), (k, r[k], rk)
+        fields = ("low", "range", "bits_left", "num_buffered", "buffered_byte", "bins")
+        assert tuple(int(r[k][f]) for f in fields) == \
+            tuple(int(rk[f]) if isinstance(rk, np.void) else int(rk[i]) for i, f in enumerate(fields)), (k, r[k], rk)
         np.testing.assert_array_equal(st[k], sk, err_msg=f"run {k}")
         total += len(exp)
     return int(first[-1]), total

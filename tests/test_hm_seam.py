@@ -1,7 +1,8 @@
 """End-to-end drop-in check: the UNCHANGED reference TAppEncoder (HM-16.5rc1), with every
 TComTrQuant::transformNxN / invTransformNxN call (integration/hm_tu_seam.cpp), every
 TComPrediction::motionCompensation call (hm_mc_seam.cpp) and every TEncSearch::xMotionEstimation
-call (hm_me_seam.cpp), every picture's TComLoopFilter::loopFilterPic (hm_lf_seam.cpp) and SAO
+call (hm_me_seam.cpp), every residual the slice writer codes (TEncSbac::codeCoeffNxN through
+TEncBinCABAC, hm_cabac_seam.cpp), every picture's TComLoopFilter::loopFilterPic (hm_lf_seam.cpp) and SAO
 statistics + offsets (hm_sao_seam.cpp, TEncSampleAdaptiveOffset::SAOProcess) and, in the
 intra encodes, every TComPrediction::predIntraAng call (hm_intra_seam.cpp) served by
 libhvx.so on the MI355X, must produce the same bitstream and
@@ -51,6 +52,10 @@ def test_hm_encoder_with_hvx_seams(case, monkeypatch):
     # every picture's SAO statistics and offsets ran on the device (hm_sao_seam.cpp)
     m = re.search(r"hm_sao_seam: (\d+) pictures through libhvx SAO, (\d+) fell through", log[0])
     assert m and int(m.group(1)) == mk.CASES[case][2] and int(m.group(2)) == 0, log[0][-2000:]
+    # the slice writer's residual syntax (TEncSbac::codeCoeffNxN through TEncBinCABAC) was written
+    # by the device (hm_cabac_seam.cpp, hvx_coeff_write_batch): the same bitstream MD5 as above
+    m = re.search(r"hm_cabac_seam: (\d+) codeCoeffNxN calls written by libhvx \((\d+) bytes\), (\d+) fell through", log[0])
+    assert m and int(m.group(1)) > 1000 and int(m.group(3)) == 0, log[0][-2000:]
     if intra:  # every intra prediction of the encode ran on the device
         m = re.search(r"hm_intra_seam: (\d+) predIntraAng calls served by libhvx, (\d+) fell through", log[0])
         assert m and int(m.group(1)) > 100000 and int(m.group(2)) == 0, log[0][-2000:]

@@ -118,7 +118,7 @@ __device__ __forceinline__ int sig_ctx(int pattern, int first_sig, int single, i
 // independent loads into registers (fully unrolled, static indices), so a group costs one
 // memory latency, and every later pass over the group reads registers.
 template <class LevAt, class C>
-__device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, C &L, uint32_t &rice_stat) {
+__device__ __forceinline__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, C &L, uint32_t &rice_stat) {
   const int n = d.width, lw = log2_tu(n), l = lw - 2, wg = n >> 2, ncg = wg * wg;
   const int ch = d.comp ? 1 : 0;
   const uint8_t *scan_cg = kScanCG[d.scan_type] + cg_base(l);
@@ -182,7 +182,10 @@ __device__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, C &L, uint32_t &rice_
     // significance flags (reverse scan inside the group); non-zero count, first/last positions
     const bool is_last_set = sub == last_set;
     int nnz = is_last_set ? 1 : 0, last_nz = is_last_set ? last_pin : -1, first_nz = is_last_set ? last_pin : 16;
-    uint32_t signs = is_last_set ? (uint32_t)(a[last_pin] < 0) : 0u;  // coeffSigns, in coding order
+    uint32_t signs = 0;  // coeffSigns, in coding order (the last position's sign first)
+#pragma unroll
+    for (int pin = 0; pin < 16; pin++)
+      if (is_last_set && pin == last_pin) signs = (uint32_t)(a[pin] < 0);  // static indices: no scratch
     if ((cgm >> cg) & 1) {
       int pattern = 0;
       if (wg > 1) {
@@ -296,12 +299,13 @@ struct Writer {
   uint32_t buffered;     // m_bufferedByte
   uint8_t *out;
   int nout, cap;
+  uint32_t bins;         // bins coded (m_uiBinsCoded with m_binCountIncrement 1)
   __device__ __forceinline__ void put(uint32_t b) {
     if (nout < cap) out[nout] = (uint8_t)b;
     nout++;
   }
   // writeOut (:425): the lead byte; 0xff bytes are held back until a carry can no longer reach them
-  __device__ __noinline__ void write_out() {
+  __device__ __forceinline__ void write_out() {
     const uint32_t lead = low >> (24 - bits_left);
     bits_left += 8;
     low &= 0xffffffffu >> bits_left;
@@ -323,6 +327,7 @@ struct Writer {
   }
   // encodeBin (:200) + ContextModel::update
   __device__ __forceinline__ void bin(int row, int v) {
+    bins++;
     uint8_t &st = col[row * 64];
     const int q = st, mps = q & 1;
     const uint32_t l = lps[(q >> 1) * 4 + ((range >> 6) & 3)];
@@ -342,7 +347,7 @@ struct Writer {
     st = s->next[q * 2 + v];
   }
   // encodeAlignedBinsEP (:334): reached only with range == 256 (cabac_bypass_alignment)
-  __device__ void aligned(uint32_t vals, int n) {
+  __device__ __forceinline__ void aligned(uint32_t vals, int n) {
     while (n > 0) {
       const int k = n < 8 ? n : 8;
       low = (low << k) + (((vals >> (n - k)) & ((1u << k) - 1)) << 8);
@@ -353,6 +358,7 @@ struct Writer {
   }
   // encodeBinEP (:262)
   __device__ __forceinline__ void ep1(uint32_t b) {
+    bins++;
     if (range == 256) { aligned(b, 1); return; }
     low <<= 1;
     if (b) low += range;
@@ -365,6 +371,7 @@ struct Writer {
   }
   // encodeBinsEP (:290): most significant first, in pieces of 8
   __device__ __forceinline__ void eps(uint32_t vals, int n) {
+    bins += (uint32_t)n;
     if (range == 256) { aligned(vals, n); return; }
     while (n > 8) {
       n -= 8;
@@ -379,7 +386,7 @@ struct Writer {
     test();
   }
   // xWriteCoefRemainExGolomb (TEncSbac.cpp:337), COEF_REMAIN_BIN_REDUCTION 3
-  __device__ void esc(uint32_t symbol, int r, bool limited, int max_log2) {
+  __device__ __forceinline__ void esc(uint32_t symbol, int r, bool limited, int max_log2) {
     if (symbol < (3u << r)) {
       const uint32_t len = symbol >> r;
       eps((1u << (len + 1)) - 2, (int)len + 1);
@@ -513,7 +520,7 @@ __global__ __launch_bounds__(64) void k_coeff_write(const hvx_tu_desc *__restric
   if (lane < cnt) {
     const hvx_cabac_regs r0 = regs[k];
     cab::Writer W{&s.st[lane], &s, lps, r0.low, r0.range, r0.bits_left, r0.num_buffered, r0.buffered_byte,
-                  out + out_off[k], 0, out_cap};
+                  out + out_off[k], 0, out_cap, r0.bins};
     bool ok = true;
     for (int t = stream_first[k]; t < stream_first[k + 1] && ok; t++) {
       const hvx_tu_desc d = descs[t];
@@ -529,7 +536,7 @@ __global__ __launch_bounds__(64) void k_coeff_write(const hvx_tu_desc *__restric
     }
     hvx_cabac_regs r1;
     r1.low = W.low; r1.range = W.range; r1.bits_left = W.bits_left; r1.num_buffered = W.nbuf;
-    r1.buffered_byte = W.buffered; r1.pad = 0;
+    r1.buffered_byte = W.buffered; r1.bins = W.bins;
     regs[k] = r1;
     out_len[k] = !ok ? -2 : W.nout <= out_cap ? W.nout : -1;
   }
