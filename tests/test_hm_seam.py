@@ -55,7 +55,7 @@ def test_hm_encoder_with_hvx_seams(case, monkeypatch):
     # the slice writer's residual syntax (TEncSbac::codeCoeffNxN through TEncBinCABAC) was written
     # by the device (hm_cabac_seam.cpp, hvx_coeff_write_batch): the same bitstream MD5 as above
     m = re.search(r"hm_cabac_seam: (\d+) codeCoeffNxN calls written by libhvx \((\d+) bytes\), (\d+) fell through", log[0])
-    assert m and int(m.group(1)) > 1000 and int(m.group(3)) == 0, log[0][-2000:]
+    assert m and int(m.group(1)) > 100 and int(m.group(3)) == 0, log[0][-2000:]
     if intra:  # every intra prediction of the encode ran on the device
         m = re.search(r"hm_intra_seam: (\d+) predIntraAng calls served by libhvx, (\d+) fell through", log[0])
         assert m and int(m.group(1)) > 100000 and int(m.group(2)) == 0, log[0][-2000:]
