@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export HVX_SERIAL_STREAMS=${SERIAL:-1}
-B="python bench.py --steps 30 --warmup 5 --no-cpu --no-ssim --no-intra --no-1080p --no-sao"
+B="python bench.py --steps 30 --warmup 5 --no-cpu --no-ssim --no-intra --no-1080p --no-sao --no-cabac"
 show() { grep '^{' "$1" | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); p=d['phase_ms_per_step']; print('$2', d['ms_per_step'], ' '.join('%s=%.3f' % kv for kv in p.items()))"; }
 cp -p video_codecs_amd/libhvx.so /tmp/libhvx_orig.so || exit 1
 restore() { cp -p /tmp/libhvx_orig.so video_codecs_amd/libhvx.so || rm -f video_codecs_amd/libhvx.so; }

@@ -4,7 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=$(pwd); TAG=${1:-r02}
-B="--no-cpu --no-intra --no-ssim --no-1080p --no-sao"
+B="--no-cpu --no-intra --no-ssim --no-1080p --no-sao --no-cabac"
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_${TAG}_kt -o kt --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 $B > gpurun_out/prof_${TAG}_kt.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/prof_${TAG}_fetch -o f --output-format csv -- python3 $R/bench.py --steps 2 --warmup 0 $B > gpurun_out/prof_${TAG}_fetch.log 2>&1 &&
