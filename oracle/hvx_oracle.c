@@ -2270,7 +2270,7 @@ static void mc_pred_blk(int is_luma, const int16_t *plane, int stride, int x, in
   } else if (xf == 0) {
     hvxo_filter_ver(is_luma, ref, stride, dst, w, w, h, yf, 1, !bi);
   } else {
-    static int16_t tmp[(64 + 7) * 64];
+    static _Thread_local int16_t tmp[(64 + 7) * 64]; /* per thread: bench.py's cpu_baseline runs CTUs on threads */
     const int n = is_luma ? 8 : 4;
     hvxo_filter_hor(is_luma, ref - (n / 2 - 1) * stride, stride, tmp, w, w, h + n - 1, xf, 0);
     hvxo_filter_ver(is_luma, tmp + (n / 2 - 1) * w, w, dst, w, w, h, yf, 0, !bi);
@@ -2294,7 +2294,7 @@ void hvxo_mc(const int16_t *const *planes, int ls, int cs, const hvx_mc_job *j, 
   int mx[2] = {j->mv_x[0], j->mv_x[1]}, my[2] = {j->mv_y[0], j->mv_y[1]};
   mc_clip(j, &mx[0], &my[0]); /* xPredInterUni clips its list's MV */
   mc_clip(j, &mx[1], &my[1]);
-  static int16_t pa[64 * 64], pb[64 * 64];
+  static _Thread_local int16_t pa[64 * 64], pb[64 * 64];
   for (int comp = 0; comp < 3; comp++) {
     const int luma = comp == 0;
     const int w = luma ? j->w : j->w >> 1, h = luma ? j->h : j->h >> 1;
