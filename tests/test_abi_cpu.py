@@ -257,6 +257,20 @@ def test_new_entry_points_reject_bad_arguments_without_a_gpu():
     assert L.hvx_deblock(P(0), P(0), 64, P(0), P(0), 32, P(0), P(0), P(0), P(0)) == E_INVALID
     assert b"hvx_deblock" in L.hvx_last_error()
     assert L.hvx_ctu_decide(P(0), P(0), 0, P(0), P(0), P(0), P(0), ctypes.c_size_t(0), P(0), P(0), P(0), P(0)) == E_INVALID
+    # the CABAC residual writer: NULL context, negative run count / capacity
+    assert L.hvx_coeff_write_batch(P(0), P(0), P(0), P(0), P(0), 1, P(0), P(0), P(0), P(0), 64, P(0)) == E_INVALID
+    assert b"hvx_coeff_write_batch" in L.hvx_last_error()
+    assert L.hvx_coeff_write_batch(P(0), P(0), P(0), P(0), P(0), -1, P(0), P(0), P(0), P(0), 64, P(0)) == E_INVALID
+
+
+def test_cabac_regs_layout_matches_c():
+    # hvx_cabac_regs (hvx_types.h) = TEncBinCABAC's registers + the bin count; start() values
+    from video_codecs_amd import _abi
+    assert _abi.CABAC_REGS.names == ("low", "range", "bits_left", "num_buffered", "buffered_byte", "bins")
+    assert [_abi.CABAC_REGS.fields[f][1] for f in _abi.CABAC_REGS.names] == [0, 4, 8, 12, 16, 20]
+    assert _abi.CABAC_START[:5] == (0, 510, 23, 0, 0xFF)
+    src = open(os.path.join(ROOT, "include", "hvx_types.h")).read()
+    assert "typedef struct hvx_cabac_regs" in src and "uint32_t buffered_byte, bins;" in src
 
 
 def test_sao_layout_matches_c():
