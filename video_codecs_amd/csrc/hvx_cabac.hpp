@@ -499,7 +499,12 @@ __global__ __launch_bounds__(64) void k_coeff_bits_il(const hvx_tu_desc *__restr
   out[t] = r;
 }
 
-// hvx_coeff_write_batch: stream k = lane (k % 64) of block k / 64 writes TUs
+// Runs per wave: the runs of a wave take different branches bin by bin (MPS / LPS, bypass lengths,
+// renormalisation, writeOut), and the wave executes the union; fewer runs per wave spread the
+// runs over more SIMDs, each wave still alone on its SIMD for a picture's worth of runs.
+constexpr int kWriteRuns = 16;
+
+// hvx_coeff_write_batch: stream k = lane (k % kWriteRuns) of block k / kWriteRuns writes TUs
 // [stream_first[k], stream_first[k + 1]) through one TEncBinCABAC, from its own context states
 // (states + k * HVX_NUM_CTX, advanced in place) and registers (regs[k], advanced in place); the
 // completed bytes go to out + out_off[k] (at most out_cap), their count to out_len[k] (-1: past
@@ -512,7 +517,7 @@ __global__ __launch_bounds__(64) void k_coeff_write(const hvx_tu_desc *__restric
                                                     int out_cap, int32_t *__restrict__ out_len) {
   __shared__ cab::Shared s;
   __shared__ uint8_t lps[256];
-  const int lane = threadIdx.x, k0 = blockIdx.x * 64, cnt = min(64, n_streams - k0), k = k0 + lane;
+  const int lane = threadIdx.x, k0 = blockIdx.x * kWriteRuns, cnt = min(kWriteRuns, n_streams - k0), k = k0 + lane;
   cab::init_tables(s, nullptr);
   for (int i = lane; i < 256; i += 64) lps[i] = cab::kLpsTable[i];
   cab::states_load(s, states, (size_t)HVX_NUM_CTX, k0, cnt);

@@ -656,7 +656,7 @@ int hvx_coeff_write_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t
                      !d_out_off || !d_out_len)))
     return fail(HVX_E_INVALID, "hvx_coeff_write_batch: bad args");
   if (!n_streams) return HVX_OK;
-  hipLaunchKernelGGL(k_coeff_write, dim3((n_streams + 63) / 64), dim3(64), 0, ctx->stream, d_desc, d_off, d_levels,
+  hipLaunchKernelGGL(k_coeff_write, dim3((n_streams + kWriteRuns - 1) / kWriteRuns), dim3(64), 0, ctx->stream, d_desc, d_off, d_levels,
                      d_stream_first, n_streams, d_states, d_regs, d_out, d_out_off, out_cap, d_out_len);
   return launched("k_coeff_write");
 }
