@@ -1,0 +1,129 @@
+"""Replay of captured HM-16.5rc1 CTU decisions through the CPU restatement (oracle/hvx_oracle_cu.c).
+
+TEST INFRASTRUCTURE ONLY.  Loads a tests/golden/ctu_*.bin capture (oracle/cu_capture.cpp), runs
+hvxo_hm_replay_picture on each picture and compares every CTU with the reference's own decision:
+the per-partition TComDataCU fields, the quantised coefficients, the reconstruction, the RD
+totals and the context state encodeCtu leaves for the next CTU.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+if _HERE not in sys.path:
+    sys.path.insert(0, _HERE)
+import golden_io  # noqa: E402
+
+PART_FIELDS = ["depth", "part", "pred", "skip", "merge", "merge_idx", "inter_dir", "ref0", "ref1", "mv0x", "mv0y",
+               "mv1x", "mv1y", "mvd0x", "mvd0y", "mvd1x", "mvd1y", "mvp0", "mvp1", "idir_y", "idir_c", "tr_idx",
+               "ts_y", "ts_cb", "ts_cr", "cbf_y", "cbf_cb", "cbf_cr", "qp"]
+P_FIRST_CTU, P_NCTU, P_COL_VALID = 41, 42, 45  # cu_capture.cpp pic_i32 indices
+
+
+def _lib():
+    import oracle
+    L = oracle.lib()
+    if not getattr(L, "_hm_ctu_bound", False):
+        P = ctypes.c_void_p
+        L.hvxo_hm_replay_picture.restype = ctypes.c_int
+        L.hvxo_hm_replay_picture.argtypes = [P, P, P, P, P, ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
+                                             P, P, P, P, P, P, P]
+        L._hm_ctu_bound = True
+    return L
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def entropy_bits():
+    from video_codecs_amd import _abi
+    return np.ascontiguousarray(_abi.load_entropy_bits(), np.int32)
+
+
+def load(path):
+    return golden_io.load(path)
+
+
+def replay(g, pic, mode=0):
+    """Replay picture `pic` of capture g; returns a dict of the restatement's per-CTU outputs."""
+    L = _lib()
+    pi = np.ascontiguousarray(g["pic_i32"][pic], np.int32)
+    pf = np.ascontiguousarray(g["pic_f64"][pic], np.float64)
+    w, h = int(pi[0]), int(pi[1])
+    psz = w * h * 3 // 2
+    org = np.ascontiguousarray(g["org"][pic * psz:(pic + 1) * psz])
+    nref = len(g["refpic_poc"])
+    refs = np.ascontiguousarray(g["refpic"]) if nref else np.zeros(1, np.uint8)
+    first, n = int(pi[P_FIRST_CTU]), int(pi[P_NCTU])
+    # the col field rows of this picture: pictures with a col field appear in order
+    colrows = g["col_field"]
+    col = None
+    if int(pi[P_COL_VALID]):
+        k = sum(1 for q in range(pic) if int(g["pic_i32"][q][P_COL_VALID]))
+        col = np.ascontiguousarray(colrows[k * n * 16:(k + 1) * n * 16])
+    sl = slice(first, first + n)
+    states = np.ascontiguousarray(g["ctu_states"][sl])
+    frac = np.ascontiguousarray(g["ctu_frac"][sl])
+    int2n = np.ascontiguousarray(g["ctu_int2n"][sl])
+    hparts = np.ascontiguousarray(g["ctu_parts"][sl])
+    hcoef = np.ascontiguousarray(g["ctu_coef"][sl])
+    hrec = np.ascontiguousarray(g["ctu_recon"][sl])
+    out = {"parts": np.zeros((n, 256, 29), np.int16), "coef": np.zeros((n, 6144), np.int32),
+           "recon": np.zeros((n, 6144), np.uint8), "cost": np.zeros(n, np.float64),
+           "bits_dist": np.zeros((n, 2), np.uint32), "states": np.zeros((n, 202), np.uint8),
+           "frac": np.zeros(n, np.int64)}
+    eb = entropy_bits()
+    L.hvxo_hm_replay_picture(_ptr(pi), _ptr(pf), _ptr(org), _ptr(refs), _ptr(np.ascontiguousarray(g["refpic_poc"])),
+                             nref, _ptr(col), _ptr(eb), _ptr(states), _ptr(frac), _ptr(int2n), _ptr(hparts),
+                             _ptr(hcoef), _ptr(hrec), mode, _ptr(out["parts"]), _ptr(out["coef"]),
+                             _ptr(out["recon"]), _ptr(out["cost"]), _ptr(out["bits_dist"]), _ptr(out["states"]),
+                             _ptr(out["frac"]))
+    return out
+
+
+def compare(g, pic, out, verbose=True):
+    """Per-CTU mismatch report: list of (ctu, what) for the first differences."""
+    pi = g["pic_i32"][pic]
+    first, n = int(pi[P_FIRST_CTU]), int(pi[P_NCTU])
+    bad = []
+    for a in range(n):
+        k = first + a
+        hp, op = g["ctu_parts"][k], out["parts"][a]
+        if not np.array_equal(hp, op):
+            d = np.argwhere(hp != op)
+            z, f = int(d[0][0]), int(d[0][1])
+            bad.append((a, "part z=%d %s hm=%d ours=%d (%d diffs; fields %s)" % (
+                z, PART_FIELDS[f], hp[z, f], op[z, f], len(d), sorted({PART_FIELDS[i] for i in d[:, 1]}))))
+            continue
+        if not np.array_equal(g["ctu_coef"][k], out["coef"][a]):
+            i = int(np.argwhere(g["ctu_coef"][k] != out["coef"][a])[0][0])
+            bad.append((a, "coef idx %d" % i))
+            continue
+        if not np.array_equal(g["ctu_recon"][k], out["recon"][a]):
+            i = int(np.argwhere(g["ctu_recon"][k] != out["recon"][a])[0][0])
+            bad.append((a, "recon idx %d" % i))
+            continue
+        hb, hd = int(g["ctu_meta"][k][2]), int(g["ctu_meta"][k][3])
+        if (hb, hd) != (int(out["bits_dist"][a][0]), int(out["bits_dist"][a][1])) or g["ctu_cost"][k] != out["cost"][a]:
+            bad.append((a, "totals hm=(%d,%d,%r) ours=(%d,%d,%r)" % (hb, hd, g["ctu_cost"][k], out["bits_dist"][a][0],
+                                                                     out["bits_dist"][a][1], out["cost"][a])))
+            continue
+        if k + 1 < len(g["ctu_states"]) and a + 1 < n:
+            if not np.array_equal(g["ctu_states"][k + 1], out["states"][a]) or int(g["ctu_frac"][k + 1]) != int(out["frac"][a]):
+                bad.append((a, "encodeCtu state"))
+    if verbose:
+        print("picture %d: %d/%d CTUs match" % (pic, n - len(bad), n))
+        for a, wht in bad[:10]:
+            print("  ctu %d: %s" % (a, wht))
+    return bad
+
+
+if __name__ == "__main__":
+    g = load(sys.argv[1])
+    mode = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    pics = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else range(len(g["pic_i32"]))
+    for p in pics:
+        compare(g, p, replay(g, p, mode))

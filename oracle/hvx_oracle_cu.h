@@ -1,0 +1,75 @@
+/* hvx_oracle_cu.h -- CPU restatement of HM-16.5rc1's CTU mode decision (TEncCu::compressCtu,
+ * TEncCu.cpp:228) and CTU syntax walk (TEncCu::encodeCtu, :252).
+ *
+ * TEST INFRASTRUCTURE ONLY: the parity oracle of the HM-exact CTU path (tests/, smoke()).
+ * Pinned against the reference's own CTU decisions (oracle/cu_capture.cpp -> tests/golden/ctu_*.bin).
+ */
+#ifndef HVX_ORACLE_CU_H
+#define HVX_ORACLE_CU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* an RD coder: TEncSbac's context states (m_ucState) + TEncBinCABACCounter::m_fracBits */
+typedef struct hvxo_hm_coder {
+  uint8_t st[202];
+  uint64_t frac;
+} hvxo_hm_coder;
+
+/* the picture-level state the CU decision reads (TComSlice / TComRdCost / TComTrQuant) */
+typedef struct hvxo_hm_pic {
+  int w, h, w_ctus, h_ctus, poc, slice_type, qp;
+  int nref[2], ref_poc[2][4], ref_plane_idx[2][4];
+  int chroma_qp[2];
+  int max_merge, tmvp, check_ldc, col_from_l0, col_valid, col_poc;
+  int col_ref_poc[2][4];
+  const int16_t *col_field;             /* the collocated picture, [ctu][16 blocks of 16x16][8] (cu_capture.cpp) */
+  double lambda, sqrt_lambda, chroma_weight[2], tq_lambda[3];
+  uint32_t lambda_motion;
+  int search_range, amp;
+  const int32_t *entropy_bits;          /* ContextModel::m_entropyBits[128] */
+  const int16_t *org[3];                /* original, sample (0,0) */
+  int org_stride[3];
+  const uint8_t *org8;                  /* original luma, 8-bit (ME pattern) */
+  int org8_stride;
+  const int16_t *const *ref_planes16;   /* [3 * plane + comp] sample (0,0), margins >= 80 / 40 */
+  int ref_stride16[2];
+  const uint8_t *const *ref_planes8;    /* [plane] luma sample (0,0), margin >= 80 */
+  int ref_stride8;
+} hvxo_hm_pic;
+
+/* the picture's CTU data (TComPic::getCtu): opaque, hvxo_hm_ctu_data_size() bytes per CTU */
+typedef struct hvxo_hm_ctu_data hvxo_hm_ctu_data;
+#define HVXO_HM_PART_FIELDS 29   /* the ctu_parts fields of cu_capture.cpp, in order */
+
+size_t hvxo_hm_ctu_data_size(void);
+void hvxo_hm_unpack_parts(const hvxo_hm_ctu_data *d, int16_t *out /* [256][HVXO_HM_PART_FIELDS] */);
+void hvxo_hm_pack_parts(hvxo_hm_ctu_data *d, const int16_t *in);
+
+/* TEncCu::compressCtu of CTU ctu_addr: ctus = the picture's CTU data (the CTUs before ctu_addr
+ * hold their final decisions; ctu_addr's is written), rec = the picture reconstruction planes
+ * (sample (0,0), sized to whole CTUs), entry = m_pppcRDSbacCoder[0][CI_CURR_BEST] on entry,
+ * int2n = TEncSearch::m_integerMv2Nx2N [2][4][2] on entry.  after_encode (optional) = that coder
+ * after TEncCu::encodeCtu, i.e. the next CTU's entry state. */
+void hvxo_hm_compress_ctu(const hvxo_hm_pic *pic, hvxo_hm_ctu_data *ctus, int16_t *const *rec, const int *rec_stride,
+                          int ctu_addr, const hvxo_hm_coder *entry, const int16_t *int2n, hvxo_hm_coder *after_encode);
+
+/* Replay one captured picture (tests/golden/ctu_*.bin arrays, cu_capture.cpp layouts).
+ * mode 0: every CTU from the reference's own entry state and its left/above CTUs' final data;
+ * mode 1: the CTUs in raster order, each from the previous CTU's restated encodeCtu state.
+ * Outputs per CTU (n = pic's CTU count): parts [n][256][29], coef [n][6144], recon [n][6144],
+ * cost [n], bits_dist [n][2], states/frac after encodeCtu [n][202] / [n]. */
+int hvxo_hm_replay_picture(const int32_t *pic_i32, const double *pic_f64, const uint8_t *org, const uint8_t *refpics,
+                           const int32_t *refpic_poc, int n_refpics, const int16_t *col_field, const int32_t *entropy_bits,
+                           const uint8_t *ctu_states, const int64_t *ctu_frac, const int16_t *ctu_int2n,
+                           const int16_t *hm_parts, const int32_t *hm_coef, const uint8_t *hm_recon, int mode,
+                           int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost,
+                           uint32_t *out_bits_dist, uint8_t *out_states, int64_t *out_frac);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
