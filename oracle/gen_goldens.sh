@@ -85,4 +85,14 @@ scap "$TMP/s_i.bin"  $CFG/encoder_intra_main.cfg      "$TMP/smooth.yuv" 1 37
 scap "$TMP/s_p.bin"  $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth.yuv" 3 32
 scap "$TMP/s_pr.bin" $CFG/encoder_lowdelay_P_main.cfg "$TMP/rand.yuv"   2 27
 python3 oracle/merge_goldens.py tests/golden/sao.bin "$TMP"/s_i.bin "$TMP"/s_p.bin "$TMP"/s_pr.bin
+# CTU decisions: TEncCu::compressCtu entry state and outputs of whole LDP encodes (oracle/cu_capture.cpp)
+python3 oracle/make_yuv.py random 416 240 4 "$TMP/rand4.yuv"
+python3 oracle/make_yuv.py smooth 416 240 4 "$TMP/smooth4.yuv"
+cucap() {  # cucap <out.bin> <cfg> <yuv> <frames> <qp>
+  HVX_CAPTURE="$TMP/cu.bin" $ORC/TAppEncoder_cucap -c "$2" -i "$3" -wdt 416 -hgt 240 -fr 30 -f "$4" -q "$5" \
+    -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+  python3 oracle/compact_ctu.py "$TMP/cu.bin" "$1"
+}
+cucap tests/golden/ctu_ldp_rand.bin   $CFG/encoder_lowdelay_P_main.cfg "$TMP/rand4.yuv"   3 32
+cucap tests/golden/ctu_ldp_smooth.bin $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth4.yuv" 4 27
 ls -la tests/golden

@@ -69,7 +69,7 @@ def replay(g, pic, mode=0):
     frac = np.ascontiguousarray(g["ctu_frac"][sl])
     int2n = np.ascontiguousarray(g["ctu_int2n"][sl])
     hparts = np.ascontiguousarray(g["ctu_parts"][sl])
-    hcoef = np.ascontiguousarray(g["ctu_coef"][sl])
+    hcoef = np.ascontiguousarray(g["ctu_coef"][sl], np.int32)
     hrec = np.ascontiguousarray(g["ctu_recon"][sl])
     out = {"parts": np.zeros((n, 256, 29), np.int16), "coef": np.zeros((n, 6144), np.int32),
            "recon": np.zeros((n, 6144), np.uint8), "cost": np.zeros(n, np.float64),
