@@ -373,6 +373,29 @@ int hvx_ctu_encode_yuv(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const 
 int hvx_plane_from_pel(hvx_ctx *ctx, const int16_t *d_pel, int pel_stride, int width, int height, uint8_t *d_plane);
 int hvx_plane_extend(hvx_ctx *ctx, uint8_t *d_plane, int width, int height);
 
+/* ---------------------------------------------------------------------------------------
+ * HM-exact CTU decision: TEncCu::compressCtu (hm-16.5rc1 TEncCu.cpp:228, called from
+ * TEncSlice::compressSlice TEncSlice.cpp:814) followed by the CTU syntax walk of
+ * TEncCu::encodeCtu (TEncCu.cpp:252) on the RD coder, whose context states start the next CTU
+ * (TEncSlice.cpp:821-828).  Replaces, per CTU, the whole xCompressCU recursion: merge/skip
+ * (xCheckRDCostMerge2Nx2N :1166), 2Nx2N / Nx2N / 2NxN / AMP inter search with AMVP, merge
+ * estimation and AMP_MRG (xCheckRDCostInter :1291, TEncSearch::predInterSearch :2912), the RQT
+ * (xEstimateInterResidualQT :4426), intra-in-inter and NxN intra (xCheckRDCostIntra :1330,
+ * estIntraPredLumaQT :2176, estIntraPredChromaQT :2563), split decisions and xCheckBestMode.
+ * Tool set of encoder_lowdelay_P_main.cfg (hvx_types.h hvx_hm_picture): CTU 64, depth 4, TU
+ * 4..32 with QuadtreeTUMaxDepthInter/Intra 3, RDOQ + RDOQTS, sign hiding, transform skip with
+ * TransformSkipFast, FEN, FDM, AMP, TZ search with HadamardME, TMVP, 5 merge candidates, no
+ * ECU/ESD/CFM, no PCM, no delta QP, no lossless, no weighted prediction, P and I slices.
+ * One wave per job (hvx_hm_job): the chain's CTUs are decided in raster order with the contexts
+ * carried; d_state = n_jobs * hvx_hm_state_size() bytes of device scratch.  Outputs per CTU
+ * slot: d_out_ctu (the CTU's final TComDataCU data and RD totals), d_out_rec (6144 bytes: its
+ * pre-loop-filter reconstruction, Y 64x64 | Cb 32x32 | Cr 32x32, 0 outside the picture),
+ * d_out_coder (optional: the RD coder after encodeCtu).
+ * ------------------------------------------------------------------------------------- */
+int hvx_hm_state_size(size_t *bytes);
+int hvx_hm_compress(hvx_ctx *ctx, const hvx_hm_picture *d_pics, const hvx_hm_job *d_jobs, int n_jobs, void *d_state,
+                    hvx_hm_ctu *d_out_ctu, uint8_t *d_out_rec, hvx_hm_coder *d_out_coder);
+
 #ifdef __cplusplus
 }
 #endif

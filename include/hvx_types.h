@@ -293,6 +293,84 @@ typedef struct hvx_mc_job {
   int64_t dst_offset;            /* element offset of the output: Y w*h, Cb, Cr (w/2)*(h/2) each */
 } hvx_mc_job;
 
+
+/* ---------------------------------------------------------------------------------------
+ * HM-exact CTU decision (hvx_hm_compress; TEncCu::compressCtu TEncCu.cpp:228 + the CTU syntax
+ * walk TEncCu::encodeCtu :252 that carries the CABAC contexts to the next CTU,
+ * TEncSlice.cpp:814-828).  4:2:0 8-bit, the encoder_lowdelay_P_main.cfg tool set (see hvx.h).
+ * ------------------------------------------------------------------------------------- */
+/* An RD coder of TEncCu: TEncSbac's 202 context states (m_ucState) + TEncBinCABACCounter::m_fracBits
+ * (TEncSbac::load/store copy both, TEncSbac.cpp:396-425). */
+typedef struct hvx_hm_coder {
+  uint8_t st[202];
+  uint8_t pad_[6];
+  uint64_t frac;
+} hvx_hm_coder;
+
+/* The per-partition fields of TComDataCU (TComDataCU.h) for one 4x4 partition (z-order). */
+typedef struct hvx_hm_part {
+  int8_t depth, part, pred, skip, merge, merge_idx, inter_dir, tr_idx;  /* part: PartSize, pred: PredMode */
+  int8_t ref[2], mvp_idx[2], mvp_num[2];                                 /* per list */
+  int16_t mv[2][2], mvd[2][2];                                           /* per list (x, y), quarter-pel */
+  uint8_t idir[2];                                                       /* intra dir luma / chroma (36 = DM) */
+  uint8_t ts[3], cbf[3];                                                 /* transform skip, cbf (bit = TU depth) */
+  uint8_t width;
+  int8_t qp;
+} hvx_hm_part;
+
+/* The final data of one CTU (TComPic::getCtu(addr)): partitions in z-order and the coefficients
+ * (m_pcTrCoeff: luma 64x64 then Cb, Cr 32x32, in the CU/TU z-order packing of TComDataCU). */
+typedef struct hvx_hm_ctu {
+  hvx_hm_part p[256];
+  int16_t coef[6144];
+  uint32_t bits, dist;       /* TComDataCU::getTotalBits / getTotalDistortion of the CTU */
+  double cost;               /* getTotalCost */
+} hvx_hm_ctu;
+
+/* One picture as the decision reads it (TComSlice / TComRdCost / TComTrQuant state + planes).
+ * All pointers are device pointers to sample (0,0).  org: 8-bit planes (strides org_stride[0]
+ * luma, [1] chroma).  rec: the picture reconstruction (TComPic::getPicYuvRec before the loop
+ * filters; read for intra neighbours outside the CTU being decided, written by chained jobs).
+ * ref8[i]: luma of reference plane i, 8-bit with HVX_PLANE_MARGIN on every side (stride
+ * ref8_stride, a multiple of 4, >= w + 2*margin); ref16[i][c]: the same picture as int16 planes
+ * with margins >= 80 (luma) / 40 (chroma) (strides ref16_stride[0/1]).  ctus: the picture's CTU
+ * array (neighbours of the CTU being decided; chained jobs write each CTU they finish).
+ * col_field: the collocated picture's compressed motion, [ctu][16 blocks of 16x16][8] =
+ * {pred mode (-1 outside), ref0, ref1, mv0x, mv0y, mv1x, mv1y, 0}. */
+typedef struct hvx_hm_picture {
+  int32_t w, h, w_ctus, h_ctus, poc, slice_type, qp;
+  int32_t nref[2], ref_poc[2][4], ref_plane[2][4];   /* ref_plane: index into ref8 / ref16 */
+  int32_t chroma_qp[2];
+  int32_t max_merge, tmvp, check_ldc, col_from_l0, col_valid, col_poc;
+  int32_t col_ref_poc[2][4];
+  int32_t search_range, amp;
+  uint32_t lambda_motion;    /* m_uiLambdaMotionSAD[0] */
+  int32_t pad_;
+  double lambda, sqrt_lambda, chroma_weight[2], tq_lambda[3];
+  const int16_t *col_field;
+  const uint8_t *org[3];
+  uint8_t *rec[3];
+  int32_t org_stride[2], rec_stride[2];
+  hvx_hm_ctu *ctus;
+  const uint8_t *ref8[8];
+  const int16_t *ref16[8][3];
+  int32_t ref8_stride, ref16_stride[2], pad2_;
+  const int32_t *entropy_bits;  /* ContextModel::m_entropyBits[128] */
+} hvx_hm_picture;
+
+/* One chain of CTUs decided in raster order by one wave: CTUs first_ctu .. first_ctu+n_ctus-1 of
+ * picture pic, the first from `entry` (m_pppcRDSbacCoder[0][CI_CURR_BEST] on entry) and
+ * int2n (TEncSearch::m_integerMv2Nx2N [2][4][2]), each later one from the previous CTU's
+ * encodeCtu state and search state.  chained = 1: every finished CTU is written into the
+ * picture (ctus[addr] and rec) before the next starts; 0: the picture is only read (n_ctus = 1,
+ * independent CTUs against a fixed neighbourhood).  Outputs go to slot out + k of the output
+ * arrays for the k-th CTU of the chain. */
+typedef struct hvx_hm_job {
+  int32_t pic, first_ctu, n_ctus, chained, out, pad_;
+  hvx_hm_coder entry;
+  int16_t int2n[16];
+} hvx_hm_job;
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,175 @@
+"""The HM-exact CTU engine (video_codecs_amd.hm -> libhvx.so hvx_hm_compress) against the
+reference's own compressCtu decisions (tests/golden/ctu_ldp_*.bin, oracle/cu_capture.cpp).
+
+Test infrastructure shared by tests/test_gpu_parity.py, __graft_entry__.smoke() and bench.py's
+parity check.  Layouts of the capture arrays: oracle/cu_capture.cpp.
+"""
+import numpy as np
+
+from tests import golden_cases as gc
+from video_codecs_amd import _abi
+from video_codecs_amd import hm
+
+CAPTURES = ("ctu_ldp_rand.bin", "ctu_ldp_smooth.bin")
+LAST_ENGINE = [None]
+# cu_capture.cpp pic_i32 / pic_f64 fields
+(P_W, P_H, P_POC, P_SLICE_TYPE, P_QP, P_NREF0, P_NREF1) = range(7)
+P_REFPOC0, P_REFPOC1, P_REFPIC0, P_REFPIC1 = 7, 11, 15, 19
+P_COL_FROM_L0, P_COL_REF_IDX, P_CHECK_LDC, P_TMVP, P_MAX_MERGE, P_COL_POC = 23, 24, 25, 26, 27, 28
+P_COL_REFPOC0, P_COL_REFPOC1 = 31, 35
+P_CHROMA_QP_CB, P_CHROMA_QP_CR, P_FIRST_CTU, P_NCTU, P_LAMBDA_MOTION, P_CABAC_TABLE, P_COL_VALID = 39, 40, 41, 42, 43, 44, 45
+
+
+def yuv_split(flat, w, h):
+    ysz, csz = w * h, w * h // 4
+    return (flat[:ysz].reshape(h, w), flat[ysz:ysz + csz].reshape(h // 2, w // 2),
+            flat[ysz + csz:ysz + 2 * csz].reshape(h // 2, w // 2))
+
+
+def pic_params(pi, pf):
+    return {
+        "poc": int(pi[P_POC]), "slice_type": int(pi[P_SLICE_TYPE]), "qp": int(pi[P_QP]),
+        "nref": [int(pi[P_NREF0]), int(pi[P_NREF1])],
+        "ref_poc": np.array([pi[P_REFPOC0:P_REFPOC0 + 4], pi[P_REFPOC1:P_REFPOC1 + 4]]),
+        "ref_plane": np.maximum(np.array([pi[P_REFPIC0:P_REFPIC0 + 4], pi[P_REFPIC1:P_REFPIC1 + 4]]), 0),
+        "chroma_qp": [int(pi[P_CHROMA_QP_CB]), int(pi[P_CHROMA_QP_CR])],
+        "max_merge": int(pi[P_MAX_MERGE]), "tmvp": int(pi[P_TMVP]), "check_ldc": int(pi[P_CHECK_LDC]),
+        "col_from_l0": int(pi[P_COL_FROM_L0]), "col_valid": int(pi[P_COL_VALID]), "col_poc": int(pi[P_COL_POC]),
+        "col_ref_poc": np.array([pi[P_COL_REFPOC0:P_COL_REFPOC0 + 4], pi[P_COL_REFPOC1:P_COL_REFPOC1 + 4]]),
+        "search_range": 64, "amp": 1, "lambda_motion": int(pi[P_LAMBDA_MOTION]) & 0xffffffff,
+        "lambda": float(pf[0]), "sqrt_lambda": float(pf[1]), "chroma_weight": [float(pf[2]), float(pf[3])],
+        "tq_lambda": [float(pf[4]), float(pf[5]), float(pf[6])],
+    }
+
+
+def hm_ctus(g, first, n):
+    """The reference's final CTU data of CTUs first..first+n-1 as HM_CTU records."""
+    ct = np.zeros(n, hm.HM_CTU)
+    ct["p"] = hm.pack_parts(g["ctu_parts"][first:first + n])
+    ct["coef"] = g["ctu_coef"][first:first + n].astype(np.int16)
+    ct["bits"] = g["ctu_meta"][first:first + n, 2]
+    ct["dist"] = g["ctu_meta"][first:first + n, 3]
+    ct["cost"] = g["ctu_cost"][first:first + n]
+    return ct
+
+
+def hm_recon(g, first, w, h):
+    """The reference's pre-loop-filter reconstruction of a picture (whole CTUs) from ctu_recon."""
+    wc, hc = (w + 63) // 64, (h + 63) // 64
+    planes = [np.zeros((hc * 64, wc * 64), np.uint8), np.zeros((hc * 32, wc * 32), np.uint8),
+              np.zeros((hc * 32, wc * 32), np.uint8)]
+    for a in range(wc * hc):
+        r = g["ctu_recon"][first + a]
+        ax, ay = a % wc, a // wc
+        planes[0][ay * 64:ay * 64 + 64, ax * 64:ax * 64 + 64] = r[:4096].reshape(64, 64)
+        for c in (1, 2):
+            planes[c][ay * 32:ay * 32 + 32, ax * 32:ax * 32 + 32] = r[4096 + (c - 1) * 1024:4096 + c * 1024].reshape(32, 32)
+    return planes
+
+
+def device_picture(g, pic, chained, entropy_bits):
+    pi, pf = g["pic_i32"][pic], g["pic_f64"][pic]
+    w, h = int(pi[P_W]), int(pi[P_H])
+    psz = w * h * 3 // 2
+    org = yuv_split(g["org"][pic * psz:(pic + 1) * psz], w, h)
+    nref = len(g["refpic_poc"])
+    refs = [yuv_split(g["refpic"][r * psz:(r + 1) * psz], w, h) for r in range(nref)]
+    first, n = int(pi[P_FIRST_CTU]), int(pi[P_NCTU])
+    col = None
+    if int(pi[P_COL_VALID]):
+        k = sum(1 for q in range(pic) if int(g["pic_i32"][q][P_COL_VALID]))
+        col = g["col_field"][k * n * 16:(k + 1) * n * 16]
+    rec = None if chained else hm_recon(g, first, w, h)
+    ctus = None if chained else hm_ctus(g, first, n)
+    return hm.DevicePicture(org, refs, pic_params(pi, pf), entropy_bits, rec=rec, ctus=ctus, col_field=col)
+
+
+def run_capture(name, mode, pics=None, stage=0):
+    """Decide the captured pictures on the device.  mode 0: every CTU as its own job from the
+    reference's entry state and neighbourhood; mode 1: one chained job per picture.  Returns
+    (g, list of (pic, first, n, out_slot0), (ctus, rec, coders))."""
+    g = gc.load(name)
+    eb = _abi.load_entropy_bits()
+    pics = range(g["pic_i32"].shape[0]) if pics is None else pics
+    dps, jobs, plan, slot = [], [], [], 0
+    for pi_idx, pic in enumerate(pics):
+        pi = g["pic_i32"][pic]
+        first, n = int(pi[P_FIRST_CTU]), int(pi[P_NCTU])
+        dps.append(device_picture(g, pic, mode == 1, eb))
+        plan.append((pic, first, n, slot))
+        ctus = [(a, 1) for a in range(n)] if mode == 0 else [(0, n)]
+        for a, cnt in ctus:
+            j = np.zeros(1, hm.HM_JOB)
+            j["pic"], j["first_ctu"], j["n_ctus"], j["chained"], j["out"] = pi_idx, a, cnt, mode, slot + a
+            j["entry"]["st"] = g["ctu_states"][first + a]
+            j["entry"]["frac"] = np.uint64(int(g["ctu_frac"][first + a]))
+            j["int2n"] = g["ctu_int2n"][first + a]
+            j["pad_"] = stage
+            jobs.append(j)
+        slot += n
+    eng = hm.Engine(dps)
+    LAST_ENGINE[:] = [eng]
+    out = eng.compress(np.concatenate(jobs), slot)
+    return g, plan, out
+
+
+def compare(g, plan, out):
+    """Mismatches (pic, ctu, what) of the engine's outputs against the reference's CTUs."""
+    ctus, rec, cod = out
+    bad = []
+    for pic, first, n, slot in plan:
+        parts = hm.unpack_parts(ctus["p"][slot:slot + n])
+        for a in range(n):
+            k = first + a
+            hp = g["ctu_parts"][k]
+            if not np.array_equal(hp, parts[a]):
+                d = np.argwhere(hp != parts[a])
+                z, f = int(d[0][0]), int(d[0][1])
+                bad.append((pic, a, "part z=%d %s hm=%d dev=%d (%d diffs; fields %s)" % (
+                    z, hm.PART_FIELDS[f], hp[z, f], parts[a][z, f], len(d), sorted({hm.PART_FIELDS[i] for i in d[:, 1]}))))
+                continue
+            if not np.array_equal(g["ctu_coef"][k].astype(np.int16), ctus["coef"][slot + a]):
+                i = int(np.argwhere(g["ctu_coef"][k] != ctus["coef"][slot + a])[0][0])
+                bad.append((pic, a, "coef idx %d" % i))
+                continue
+            if not np.array_equal(g["ctu_recon"][k], rec[slot + a]):
+                i = int(np.argwhere(g["ctu_recon"][k] != rec[slot + a])[0][0])
+                bad.append((pic, a, "recon idx %d" % i))
+                continue
+            c = ctus[slot + a]
+            hb, hd = int(g["ctu_meta"][k][2]), int(g["ctu_meta"][k][3])
+            if (hb, hd) != (int(c["bits"]), int(c["dist"])) or float(g["ctu_cost"][k]) != float(c["cost"]):
+                bad.append((pic, a, "totals hm=(%d,%d,%r) dev=(%d,%d,%r)" % (hb, hd, g["ctu_cost"][k], c["bits"], c["dist"],
+                                                                           c["cost"])))
+                continue
+            if a + 1 < n:
+                if (not np.array_equal(g["ctu_states"][k + 1], cod[slot + a]["st"])
+                        or int(g["ctu_frac"][k + 1]) != int(cod[slot + a]["frac"])):
+                    bad.append((pic, a, "encodeCtu state"))
+    return bad
+
+
+if __name__ == "__main__":  # debugging aid: python -m tests.hm_cases [mode]
+    import sys
+    mode = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+    per_pic = len(sys.argv) > 2 and sys.argv[2] == "per_pic"
+    if len(sys.argv) > 2 and sys.argv[2] == "stage":  # debugging: one picture up to one stage
+        name, pic, stage = sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+        import torch
+        g, plan, out = run_capture(name, mode, [pic], stage)
+        dbg = LAST_ENGINE[0].last_debug
+        print("stage %d ok; checks:" % stage, [(j, *dbg[j, :3]) for j in np.nonzero(dbg[:, 0])[0][:8]], flush=True)
+        sys.exit(0)
+    for name in CAPTURES:
+        npic = gc.load(name)["pic_i32"].shape[0]
+        for pics in ([[p] for p in range(npic)] if per_pic else [None]):
+            print("running %s mode %d pics %s" % (name, mode, pics), flush=True)
+            g, plan, out = run_capture(name, mode, pics)
+            bad = compare(g, plan, out)
+            n = sum(p[2] for p in plan)
+            print("%s mode %d: %d/%d CTUs match" % (name, mode, n - len(bad), n), flush=True)
+            for b in bad[:12]:
+                print("  pic %d ctu %d: %s" % b)
+            dbg = LAST_ENGINE[0].last_debug
+            for j in np.nonzero(dbg[:, 0])[0][:12]:
+                print("  job %d check %d a=%d b=%d" % (j, dbg[j, 0], dbg[j, 1], dbg[j, 2]))

@@ -5,6 +5,7 @@ import pytest
 import oracle
 from tests import golden_cases as gc
 from tests import gpu_cases
+from tests import hm_cases
 from video_codecs_amd import _abi, hvx
 
 pytestmark = pytest.mark.gpu
@@ -296,3 +297,13 @@ def test_ctu_decide_ssim_rdo_gpu(torch):
         n, leaves = gpu_cases.check_ctu_decide(seed=9 + qp, width=256, height=136, nref=2, qp=qp, fused=True,
                                                rd_metric=hvx._abi.RD_SSIM)
         assert n == 12 and leaves >= 12
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("name", hm_cases.CAPTURES)
+def test_hm_ctu_golden_gpu(torch, name, mode):
+    """hvx_hm_compress vs the reference's compressCtu + encodeCtu on every captured CTU: mode 0 each
+    CTU from HM's entry state and neighbourhood, mode 1 whole pictures chained on the device."""
+    g, plan, out = hm_cases.run_capture(name, mode)
+    bad = hm_cases.compare(g, plan, out)
+    assert not bad, bad[:5]

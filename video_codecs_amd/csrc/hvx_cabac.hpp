@@ -23,12 +23,12 @@ constexpr int kRows = 185 - kCtxLo; // ..184 (transform-skip chroma)
 constexpr int kSigCG = 42 - kCtxLo, kSig = 46 - kCtxLo, kLastX = 90 - kCtxLo, kLastY = 120 - kCtxLo;
 constexpr int kOne = 150 - kCtxLo, kAbs = 174 - kCtxLo, kTskip = 183 - kCtxLo;
 
-__constant__ uint8_t kTransIdxLps[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7,  8,  9,  9,  11, 11, 12,
+static __constant__ uint8_t kTransIdxLps[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7,  8,  9,  9,  11, 11, 12,
                                          13, 13, 15, 15, 16, 16, 18, 18, 19, 19, 21, 21, 22, 22, 23, 24,
                                          24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30, 31, 32, 32, 33,
                                          33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63};
 
-__constant__ uint8_t kMinInGroup[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};  // g_uiMinInGroup (TComRom.cpp)
+static __constant__ uint8_t kMinInGroup[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};  // g_uiMinInGroup (TComRom.cpp)
 
 struct Shared {
   uint8_t st[kRows * 64];   // per-lane state columns
@@ -273,7 +273,7 @@ __device__ __forceinline__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, C &L,
 // (TComCABACTables.cpp:44, the specification's Table 9-52) is staged in LDS; renormalisation
 // shifts are the reference's table (:113).
 // ---------------------------------------------------------------------------------------------
-__constant__ uint8_t kLpsTable[64 * 4] = {
+static __constant__ uint8_t kLpsTable[64 * 4] = {
     128, 176, 208, 240, 128, 167, 197, 227, 128, 158, 187, 216, 123, 150, 178, 205, 116, 142, 169, 195,
     111, 135, 160, 185, 105, 128, 152, 175, 100, 122, 144, 166, 95,  116, 137, 158, 90,  110, 130, 150,
     85,  104, 123, 142, 81,  99,  117, 135, 77,  94,  111, 128, 73,  89,  105, 122, 69,  85,  100, 116,
@@ -287,7 +287,7 @@ __constant__ uint8_t kLpsTable[64 * 4] = {
     11,  13,  15,  18,  10,  12,  15,  17,  10,  12,  14,  16,  9,   11,  13,  15,  9,   11,  12,  14,
     8,   10,  12,  14,  8,   9,   11,  13,  7,   9,   11,  12,  7,   9,   10,  12,  7,   8,   10,  11,
     6,   8,   9,   11,  6,   7,   9,   10,  6,   7,   8,   9,   2,   2,   2,   2};
-__constant__ uint8_t kRenormTable[32] = {6, 5, 4, 4, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2,
+static __constant__ uint8_t kRenormTable[32] = {6, 5, 4, 4, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2,
                                          1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
 
 struct Writer {
@@ -437,7 +437,7 @@ __device__ __forceinline__ void states_store(const Shared &s, uint8_t *g, int tu
 // hvx_coeff_bits_batch: TU i = lane (i % 64) of block i / 64; raster int32 levels at d_off[i].
 // states_stride HVX_NUM_CTX: per-TU states, advanced in place; 0: one shared snapshot (read only:
 // the CTU decision counts every TU from the same state)
-__global__ __launch_bounds__(64) void k_coeff_bits(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
+static __global__ __launch_bounds__(64) void k_coeff_bits(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
                                                    int n, const int32_t *__restrict__ levels,
                                                    const int32_t *__restrict__ entropy_bits, uint8_t *__restrict__ states,
                                                    int states_stride, hvx_coeff_bits *__restrict__ out) {
@@ -473,7 +473,7 @@ __global__ __launch_bounds__(64) void k_coeff_bits(const hvx_tu_desc *__restrict
 // b*64 + l, whose element sp sits at ((b*NN + sp)*64 + l) -- the 64 lanes of every level load
 // touch 64 consecutive words), every TU from the same snapshot.
 template <int L>
-__global__ __launch_bounds__(64) void k_coeff_bits_il(const hvx_tu_desc *__restrict__ descs, int n,
+static __global__ __launch_bounds__(64) void k_coeff_bits_il(const hvx_tu_desc *__restrict__ descs, int n,
                                                       const int32_t *__restrict__ levI,
                                                       const int32_t *__restrict__ entropy_bits,
                                                       const uint8_t *__restrict__ snapshot,
@@ -509,7 +509,7 @@ constexpr int kWriteRuns = 16;
 // (states + k * HVX_NUM_CTX, advanced in place) and registers (regs[k], advanced in place); the
 // completed bytes go to out + out_off[k] (at most out_cap), their count to out_len[k] (-1: past
 // out_cap, -2: a TU geometry the coder does not take).  Raster int32 levels at levels + offs[t].
-__global__ __launch_bounds__(64) void k_coeff_write(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
+static __global__ __launch_bounds__(64) void k_coeff_write(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
                                                     const int32_t *__restrict__ levels,
                                                     const int32_t *__restrict__ stream_first, int n_streams,
                                                     uint8_t *__restrict__ states, hvx_cabac_regs *__restrict__ regs,

@@ -96,10 +96,10 @@ __device__ __forceinline__ int ctu_epel_sample(const uint8_t *ref, int sr, int x
   return clip_pel((s2 + (1 << 11) + (8192 << 6)) >> 12);
 }
 
-__global__ void k_set_ptr(const uint8_t **slot, const uint8_t *p) { *slot = p; }
+static __global__ void k_set_ptr(const uint8_t **slot, const uint8_t *p) { *slot = p; }
 
 // one thread per (ctu, cu of this depth, ref)
-__global__ __launch_bounds__(256) void k_ctu_me_jobs(CtuLayout L, hvx_ctu_params P, int depth,
+static __global__ __launch_bounds__(256) void k_ctu_me_jobs(CtuLayout L, hvx_ctu_params P, int depth,
                                                      const hvx_me_result *__restrict__ res, hvx_me_job *__restrict__ jobs) {
   const int g = 1 << depth, ncu = g * g;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -345,7 +345,7 @@ __device__ void ctu_pred_resid_cu(const CtuMc &M, int ctu, int j, uint8_t *win, 
 }
 
 template <int S>
-__global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuMc M, int ctu0) {
+static __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuMc M, int ctu0) {
   constexpr int d = S == 64 ? 0 : S == 32 ? 1 : S == 16 ? 2 : 3, ncu = 1 << (2 * d);
   __shared__ uint8_t win[(S + 7) * (S + 8)];
   __shared__ int16_t hs[(S + 7) * S];
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid(CtuMc M, int ctu0) {
 // v_dot4_i32_i8 on sign-biased window bytes (b - 128: the -8192 offset), the second
 // v_dot2_i32_i16 on int16 tap pairs.
 template <int NC>
-__global__ __launch_bounds__(64) void k_ctu_pred_resid8q(CtuMc M) {
+static __global__ __launch_bounds__(64) void k_ctu_pred_resid8q(CtuMc M) {
   static_assert(NC % 2 == 0 && NC * 5 <= 64 && 64 % NC == 0, "CUs per wave");
   __shared__ uint32_t winY[NC][15 * 4];      // 15 rows x 16 bytes (15 used), biased
   __shared__ int16_t hsY[NC][15 * 8];
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(64) void k_ctu_pred_resid8q(CtuMc M) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_ctu_finalize(CtuLayout L, const int32_t *__restrict__ abs_sum,
+static __global__ __launch_bounds__(256) void k_ctu_finalize(CtuLayout L, const int32_t *__restrict__ abs_sum,
                                                       const uint32_t *__restrict__ sse, hvx_cu_result *__restrict__ out) {
   const int cuid = blockIdx.x * blockDim.x + threadIdx.x;
   if (cuid >= L.nctu * HVX_CUS_PER_CTU) return;
@@ -650,7 +650,7 @@ __device__ __forceinline__ bool dec_walk(const DecideArgs &A, const uint32_t (&r
 // per TU and component the forced-zero test (and at 4x4 chroma the transform-skip mode), the
 // qt_root_cbf test and the leaf distortion as the sum of the chosen TU distortions (chroma
 // weighted per component).  Writes coef_frac, bits, dist and cbf.
-__global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const int32_t *__restrict__ abs_sum,
+static __global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const int32_t *__restrict__ abs_sum,
                                                  const uint32_t *__restrict__ sse, const uint32_t *__restrict__ zd,
                                                  const uint32_t *__restrict__ csse) {
   const int cuid = blockIdx.x * 64 + threadIdx.x;
@@ -724,7 +724,7 @@ __global__ __launch_bounds__(64) void k_ctu_leaf(DecideArgs A, const int32_t *__
 // HVX_RD_SSIM (after k_ctu_leaf): D_ssim = sum over the CU's luma 8x8 blocks (raster order) of
 // 1 - SSIM(org, rec), one block per lane with compute_SSIM's float operations in its order
 // (stvssim.c:506-545); one wave per CU.
-__global__ __launch_bounds__(64) void k_ctu_leaf_ssim(DecideArgs A, const uint8_t *__restrict__ cur, int stride,
+static __global__ __launch_bounds__(64) void k_ctu_leaf_ssim(DecideArgs A, const uint8_t *__restrict__ cur, int stride,
                                                       const int16_t *__restrict__ resid,
                                                       const int16_t *__restrict__ res_out) {
   const int cuid = blockIdx.x, ctu = cuid / HVX_CUS_PER_CTU, ci = cuid % HVX_CUS_PER_CTU;
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(64) void k_ctu_leaf_ssim(DecideArgs A, const uint8_
 
 // One WAVE per CTU: the 85 leaf records (k_ctu_leaf) and CU results are loaded lane-parallel, the
 // depth recursion (dec_walk) runs wave-uniform on them, and the decisions are stored lane-parallel.
-__global__ __launch_bounds__(64) void k_ctu_decide(DecideArgs A) {
+static __global__ __launch_bounds__(64) void k_ctu_decide(DecideArgs A) {
   const int ctu = blockIdx.x, lane = lane_id();
   DecLanes V;
   hvx_cu_decision lf[2];
@@ -838,7 +838,7 @@ struct CtuBsArgs {
   int8_t *qpm;
   int qp;
 };
-__global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int pic_h, const uint8_t *__restrict__ cur,
+static __global__ __launch_bounds__(256) void k_ctu_recon(CtuLayout L, int pic_w, int pic_h, const uint8_t *__restrict__ cur,
                                                    int stride, const hvx_cu_decision *__restrict__ dec,
                                                    const int16_t *__restrict__ resid, const int16_t *__restrict__ res_out,
                                                    uint8_t *__restrict__ recon, CtuChroma C, uint8_t *__restrict__ rp_y,
@@ -950,7 +950,7 @@ __device__ __forceinline__ void ctu_bs_unit(const hvx_cu_result *__restrict__ cu
     (dir ? bs_hor : bs_ver)[u] = bs;
   }
 }
-__global__ __launch_bounds__(256) void k_ctu_bs(const hvx_cu_result *__restrict__ cu,
+static __global__ __launch_bounds__(256) void k_ctu_bs(const hvx_cu_result *__restrict__ cu,
                                                 const hvx_cu_decision *__restrict__ dec, int pic_w, int pic_h, int qp,
                                                 uint8_t *__restrict__ bs_ver, uint8_t *__restrict__ bs_hor,
                                                 int8_t *__restrict__ qpm) {

@@ -13,12 +13,12 @@
 #include "hvx_dev.hpp"
 
 namespace dbk {
-__constant__ uint8_t kTc[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+static __constant__ uint8_t kTc[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1,
                                 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
-__constant__ uint8_t kBeta[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
+static __constant__ uint8_t kBeta[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
                                   8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32,
                                   34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};
-__constant__ uint8_t kCScale[58] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 19,
+static __constant__ uint8_t kCScale[58] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 19,
                                     20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 33, 33, 34, 34, 35, 35,
                                     36, 36, 37, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51};
 
@@ -87,7 +87,7 @@ __device__ __forceinline__ void chroma_seg(uint8_t *s, int step, int off, int bs
 
 // DIR 0: vertical edges x = 8, 16, ..; thread (uy, e).  DIR 1: horizontal edges y = 8, 16, ..; thread (e, ux).
 template <int DIR>
-__global__ __launch_bounds__(256) void k_deblock(uint8_t *__restrict__ y, int ys, uint8_t *__restrict__ cb,
+static __global__ __launch_bounds__(256) void k_deblock(uint8_t *__restrict__ y, int ys, uint8_t *__restrict__ cb,
                                                  uint8_t *__restrict__ cr, int cs, const uint8_t *__restrict__ bsm,
                                                  const int8_t *__restrict__ qp, hvx_deblock_params p) {
   using namespace dbk;

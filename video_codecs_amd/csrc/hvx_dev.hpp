@@ -15,23 +15,23 @@
 //   kScanCG[type][l] : scan of the (1<<l)x(1<<l) coefficient-group grid
 //   kMat[l]          : DCT matrix of size 4<<l, [k][x]
 // ---------------------------------------------------------------------------------------
-__constant__ uint16_t kScan[3][1360];
-__constant__ uint8_t kScanCG[3][85];
-__constant__ int16_t kMat[1360];
-__constant__ int16_t kMatT[1360];  // each size's matrix transposed: kMatT[x][k] = kMat[k][x]
-__constant__ int8_t kDst4[16] = {29, 55, 74, 84, 74, 74, 0, -74, 84, -29, -74, 55, 55, -84, 74, -29};
-__constant__ int32_t kQuantScales[6] = {26214, 23302, 20560, 18396, 16384, 14564};
-__constant__ int32_t kInvQuantScales[6] = {40, 45, 51, 57, 64, 72};
-__constant__ uint8_t kGroupIdx[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
+static __constant__ uint16_t kScan[3][1360];
+static __constant__ uint8_t kScanCG[3][85];
+static __constant__ int16_t kMat[1360];
+static __constant__ int16_t kMatT[1360];  // each size's matrix transposed: kMatT[x][k] = kMat[k][x]
+static __constant__ int8_t kDst4[16] = {29, 55, 74, 84, 74, 74, 0, -74, 84, -29, -74, 55, 55, -84, 74, -29};
+static __constant__ int32_t kQuantScales[6] = {26214, 23302, 20560, 18396, 16384, 14564};
+static __constant__ int32_t kInvQuantScales[6] = {40, 45, 51, 57, 64, 72};
+static __constant__ uint8_t kGroupIdx[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
                                       8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9};
-__constant__ uint8_t kCtxIndMap4x4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
-__constant__ int8_t kLumaFilter[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
+static __constant__ uint8_t kCtxIndMap4x4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+static __constant__ int8_t kLumaFilter[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
                                          {-1, 4, -10, 58, 17, -5, 1, 0},
                                          {-1, 4, -11, 40, 40, -11, 4, -1},
                                          {0, 1, -5, 17, 58, -10, 4, -1}};
 // the luma taps as int16 pairs (t = 2u, 2u + 1) for v_dot2_i32_i16
 constexpr uint32_t luma_pair(int a, int b) { return ((uint32_t)a & 0xffffu) | ((uint32_t)b << 16); }
-__constant__ uint32_t kLumaPairs[4][4] = {
+static __constant__ uint32_t kLumaPairs[4][4] = {
     {luma_pair(0, 0), luma_pair(0, 64), luma_pair(0, 0), luma_pair(0, 0)},
     {luma_pair(-1, 4), luma_pair(-10, 58), luma_pair(17, -5), luma_pair(1, 0)},
     {luma_pair(-1, 4), luma_pair(-11, 40), luma_pair(40, -11), luma_pair(4, -1)},
@@ -40,18 +40,18 @@ __constant__ uint32_t kLumaPairs[4][4] = {
 constexpr uint32_t tap4(int a, int b, int c, int d) {
   return ((uint32_t)a & 0xffu) | (((uint32_t)b & 0xffu) << 8) | (((uint32_t)c & 0xffu) << 16) | ((uint32_t)d << 24);
 }
-__constant__ uint32_t kLumaTap4[4][2] = {{tap4(0, 0, 0, 64), tap4(0, 0, 0, 0)},
+static __constant__ uint32_t kLumaTap4[4][2] = {{tap4(0, 0, 0, 64), tap4(0, 0, 0, 0)},
                                          {tap4(-1, 4, -10, 58), tap4(17, -5, 1, 0)},
                                          {tap4(-1, 4, -11, 40), tap4(40, -11, 4, -1)},
                                          {tap4(0, 1, -5, 17), tap4(58, -10, 4, -1)}};
 // the chroma taps packed for v_dot4_i32_i8 (byte k = tap k) and as int16 pairs (taps 0,1 | 2,3)
-__constant__ uint32_t kChromaTap4[8] = {tap4(0, 64, 0, 0),   tap4(-2, 58, 10, -2), tap4(-4, 54, 16, -2), tap4(-6, 46, 28, -4),
+static __constant__ uint32_t kChromaTap4[8] = {tap4(0, 64, 0, 0),   tap4(-2, 58, 10, -2), tap4(-4, 54, 16, -2), tap4(-6, 46, 28, -4),
                                         tap4(-4, 36, 36, -4), tap4(-4, 28, 46, -6), tap4(-2, 16, 54, -4), tap4(-2, 10, 58, -2)};
-__constant__ uint32_t kChromaPairs[8][2] = {
+static __constant__ uint32_t kChromaPairs[8][2] = {
     {luma_pair(0, 64), luma_pair(0, 0)},   {luma_pair(-2, 58), luma_pair(10, -2)}, {luma_pair(-4, 54), luma_pair(16, -2)},
     {luma_pair(-6, 46), luma_pair(28, -4)}, {luma_pair(-4, 36), luma_pair(36, -4)}, {luma_pair(-4, 28), luma_pair(46, -6)},
     {luma_pair(-2, 16), luma_pair(54, -4)}, {luma_pair(-2, 10), luma_pair(58, -2)}};
-__constant__ int8_t kChromaFilter[8][4] = {{0, 64, 0, 0},   {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
+static __constant__ int8_t kChromaFilter[8][4] = {{0, 64, 0, 0},   {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
                                            {-4, 36, 36, -4}, {-4, 28, 46, -6}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
 
 __device__ __forceinline__ int scan_base(int l) { return l == 0 ? 0 : l == 1 ? 16 : l == 2 ? 80 : 336; }

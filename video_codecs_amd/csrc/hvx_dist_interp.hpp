@@ -7,7 +7,7 @@
 #pragma once
 #include "hvx_dev.hpp"
 
-__global__ __launch_bounds__(256) void k_dist(const int16_t *__restrict__ org, const int16_t *__restrict__ cur,
+static __global__ __launch_bounds__(256) void k_dist(const int16_t *__restrict__ org, const int16_t *__restrict__ cur,
                                               const hvx_dist_job *__restrict__ jobs, int n, uint32_t *__restrict__ out) {
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= n) return;
@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void k_dist(const int16_t *__restrict__ org, c
 }
 
 // filter<N,isVertical,isFirst,isLast> (TComInterpolationFilter.cpp:172) + filterCopy (:94)
-__global__ __launch_bounds__(256) void k_interp(const int16_t *__restrict__ src, int16_t *__restrict__ dst,
+static __global__ __launch_bounds__(256) void k_interp(const int16_t *__restrict__ src, int16_t *__restrict__ dst,
                                                 const hvx_interp_job *__restrict__ jobs) {
   const hvx_interp_job jb = jobs[blockIdx.x];
   const int16_t *s = src + jb.src_off;
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void k_interp(const int16_t *__restrict__ src,
 }
 
 // TComPicYuv int16 plane -> 8-bit padded plane interior
-__global__ __launch_bounds__(256) void k_plane_from_pel(const int16_t *__restrict__ pel, int pel_stride, int w, int h,
+static __global__ __launch_bounds__(256) void k_plane_from_pel(const int16_t *__restrict__ pel, int pel_stride, int w, int h,
                                                         uint8_t *__restrict__ plane, int stride) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
   if (x < w && y < h) plane[y * stride + x] = (uint8_t)clip_pel(pel[y * pel_stride + x]);
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void k_plane_from_pel(const int16_t *__restric
 
 // TComPicYuv::extendPicBorder (TComPicYuv.cpp:197): replicate edges into the margin.
 // pass 0: left/right margins of every interior row; pass 1: top/bottom rows (full width).
-__global__ __launch_bounds__(256) void k_plane_extend(uint8_t *__restrict__ plane, int stride, int w, int h, int margin, int pass) {
+static __global__ __launch_bounds__(256) void k_plane_extend(uint8_t *__restrict__ plane, int stride, int w, int h, int margin, int pass) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x;  // column incl. margin: [-margin, w+margin)
   const int y = blockIdx.y;
   if (pass == 0) {
@@ -112,7 +112,7 @@ struct PlaneSet {
   uint8_t *p[3];
   int s[3], w[3], h[3], m[3];
 };
-__global__ __launch_bounds__(256) void k_planes_extend(PlaneSet E) {
+static __global__ __launch_bounds__(256) void k_planes_extend(PlaneSet E) {
   const int pi = blockIdx.y;
   uint8_t *pl = E.p[pi];
   const int s = E.s[pi], w = E.w[pi], h = E.h[pi], m = E.m[pi];

@@ -77,7 +77,7 @@ __host__ __device__ inline void estbit_update(const uint8_t *st, const int32_t *
   for (int i = 0; i < 4; i++) e->golombRiceAdaptationStatistics[i] = (int32_t)rice[i];
 }
 
-__global__ __launch_bounds__(64) void k_estbits(const uint8_t *__restrict__ states, const int32_t *__restrict__ eb,
+static __global__ __launch_bounds__(64) void k_estbits(const uint8_t *__restrict__ states, const int32_t *__restrict__ eb,
                                                 const uint32_t *__restrict__ rice, const hvx_estbit_job *__restrict__ jobs,
                                                 int n, hvx_estbits *__restrict__ inout) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;

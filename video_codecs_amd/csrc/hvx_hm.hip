@@ -1,0 +1,38 @@
+// hvx_hm.hip -- the HM-exact CTU decision of libhvx.so (its own translation unit: the engine is
+// one large kernel, compiled apart from the leaf-kernel library in hvx_lib.hip).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "hvx_dev.hpp"
+#include "hvx_hm.hpp"
+#include "hvx_host.hpp"
+#include "hvx_tables.hpp"
+
+using namespace hvxi;
+
+int hvx_hm_module_init() { return upload_tables(); }
+
+extern "C" {
+
+int hvx_hm_state_size(size_t *bytes) {
+  if (!bytes) return fail(HVX_E_INVALID, "hvx_hm_state_size: NULL");
+  *bytes = (sizeof(hm::State) + 255) / 256 * 256;
+  return HVX_OK;
+}
+
+int hvx_hm_compress(hvx_ctx *ctx, const hvx_hm_picture *d_pics, const hvx_hm_job *d_jobs, int n_jobs, void *d_state,
+                    hvx_hm_ctu *d_out_ctu, uint8_t *d_out_rec, hvx_hm_coder *d_out_coder) {
+  if (!ctx || !d_pics || !d_jobs || n_jobs < 0 || !d_state || !d_out_ctu || !d_out_rec)
+    return fail(HVX_E_INVALID, "hvx_hm_compress: bad args");
+  if (n_jobs == 0) return HVX_OK;
+  size_t sb = 0;
+  hvx_hm_state_size(&sb);
+  hipLaunchKernelGGL(k_hm_compress, dim3(n_jobs), dim3(64), 0, ctx->stream, d_pics, d_jobs, n_jobs, (char *)d_state, sb,
+                     d_out_ctu, d_out_rec, d_out_coder);
+  return launched("k_hm_compress");
+}
+
+}  // extern "C"

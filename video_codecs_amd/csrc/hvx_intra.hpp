@@ -21,10 +21,10 @@
 
 namespace intra {
 constexpr int kB = 257;  // border samples of a 64x64 block
-__constant__ int8_t kAng[9] = {0, 2, 5, 9, 13, 17, 21, 26, 32};                    // TComPrediction.cpp:287
-__constant__ int16_t kInvAng[9] = {0, 4096, 1638, 910, 630, 482, 390, 315, 256};  // :288
-__constant__ int8_t kFilterThr[5] = {10, 7, 1, 0, 10};                             // m_aucIntraFilter (:50)
-__constant__ int8_t kNumRdMpm[6] = {3, 8, 8, 3, 3, 3}, kNumRdNoMpm[6] = {3, 9, 9, 4, 4, 5};  // TComRom.cpp:545-562
+static __constant__ int8_t kAng[9] = {0, 2, 5, 9, 13, 17, 21, 26, 32};                    // TComPrediction.cpp:287
+static __constant__ int16_t kInvAng[9] = {0, 4096, 1638, 910, 630, 482, 390, 315, 256};  // :288
+static __constant__ int8_t kFilterThr[5] = {10, 7, 1, 0, 10};                             // m_aucIntraFilter (:50)
+static __constant__ int8_t kNumRdMpm[6] = {3, 8, 8, 3, 3, 3}, kNumRdNoMpm[6] = {3, 9, 9, 4, 4, 5};  // TComRom.cpp:545-562
 
 struct Border {
   int16_t unf[kB + 3];
@@ -190,7 +190,7 @@ __device__ __forceinline__ int prepare(const hvx_intra_job &j, const uint8_t *re
 }  // namespace intra
 
 // hvx_intra_pred_batch: one wave per job
-__global__ __launch_bounds__(64) void k_intra_pred(const uint8_t *__restrict__ rec, int stride,
+static __global__ __launch_bounds__(64) void k_intra_pred(const uint8_t *__restrict__ rec, int stride,
                                                    const hvx_intra_job *__restrict__ jobs, int n_jobs,
                                                    uint8_t *__restrict__ pred, const int64_t *__restrict__ off,
                                                    int16_t *__restrict__ ref_out) {
@@ -340,7 +340,7 @@ __device__ __forceinline__ void intra_search_pu(const uint8_t *__restrict__ org,
 }
 
 // one wave per PU, grid-stride over the jobs (so that the 4x4/8x8 jobs it skips cost a load each)
-__global__ __launch_bounds__(64) void k_intra_search(const uint8_t *__restrict__ org, const uint8_t *__restrict__ rec,
+static __global__ __launch_bounds__(64) void k_intra_search(const uint8_t *__restrict__ org, const uint8_t *__restrict__ rec,
                                                      int stride, const hvx_intra_job *__restrict__ jobs, int n_jobs,
                                                      const int32_t *__restrict__ eb,
                                                      hvx_intra_search_result *__restrict__ out, int skip_small) {
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(64) void k_intra_search(const uint8_t *__restrict__
 // conflict-free), transforms in registers and ranks its candidates in registers: xUpdateCandList's
 // insertion as a fixed 9-slot network with static indices, so nothing is dynamically indexed.
 template <int LOG2N>
-__global__ __launch_bounds__(64) void k_intra_search_lane(const uint8_t *__restrict__ org, const uint8_t *__restrict__ rec,
+static __global__ __launch_bounds__(64) void k_intra_search_lane(const uint8_t *__restrict__ org, const uint8_t *__restrict__ rec,
                                                           int stride, const hvx_intra_job *__restrict__ jobs, int n_jobs,
                                                           const int32_t *__restrict__ eb,
                                                           hvx_intra_search_result *__restrict__ out) {

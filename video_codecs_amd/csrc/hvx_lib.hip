@@ -1,5 +1,7 @@
 // hvx_lib.hip -- libhvx.so: the C-ABI of include/hvx.h, HIP context and launchers (gfx950).
-// Single translation unit: the kernels live in the *.hpp files included below.
+// The kernels live in the *.hpp files included below; the HM-exact CTU engine is its own
+// translation unit (hvx_hm.hip).  Kernels and constant tables of the headers have internal
+// linkage, so each translation unit carries (and uploads) its own copies.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -21,32 +23,9 @@
 #include "hvx_intra.hpp"
 #include "hvx_deblock.hpp"
 #include "hvx_sao.hpp"
+#include "hvx_host.hpp"
+#include "hvx_tables.hpp"
 
-struct hvx_ctx {
-  int device = 0;
-  hipStream_t own = nullptr;
-  hipStream_t stream = nullptr;
-  // hvx_ctu_analyze / hvx_ctu_encode run their independent branches on three more streams (fork/join events)
-  hipStream_t aux[3] = {};
-  hipEvent_t fj[8] = {};
-  // HVX_SERIAL_STREAMS=1: every branch on ctx->stream (profiling: isolated per-kernel times)
-  bool serial = false;
-  // optional per-phase timing of hvx_ctu_analyze: a begin/end event pair on the launch's own
-  // stream around every timed launch, folded into phase_ms[phase] (phases may overlap)
-  int timing = 0;
-  static constexpr int kMaxTimed = 48;
-  hipEvent_t tev[2 * kMaxTimed] = {};
-  int tphase[kMaxTimed] = {};
-  int ntev = 0;
-  bool ev_ok = false;
-  double phase_ms[HVX_NPHASE] = {};
-  // staging for the host-memory single-TU forms
-  char *scratch = nullptr;
-  char *pinned = nullptr;
-  // interleaved per-TU scratch of the batched TU pipeline (grown on demand)
-  char *tu_scr = nullptr;
-  size_t tu_scr_bytes = 0;
-};
 
 // staging layout (bytes): desc | est | off | residual (1024 int16) | levels | arl | abs | resout
 #define HVX_STG_DESC 0
@@ -118,7 +97,7 @@ CtuLayout ctu_layout(int w, int h, int nref) {
 }
 }  // namespace
 
-namespace {
+namespace hvxi {
 thread_local std::string g_err;
 
 int fail(int code, const char *what) {
@@ -131,85 +110,15 @@ int hip_fail(hipError_t e, const char *what) {
   return HVX_E_HIP - (int)e;
 }
 
-#define HVX_HIP(call)                                   \
-  do {                                                  \
-    hipError_t e_ = (call);                             \
-    if (e_ != hipSuccess) return hip_fail(e_, #call);   \
-  } while (0)
-
 int launched(const char *what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, what);
   return HVX_OK;
 }
+}  // namespace hvxi
+using namespace hvxi;
 
-// ---- host generation of the constant tables (HEVC spec rules; TComRom.cpp:192-262) ----
-const int kCosH[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
-                       61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9, 4, 0};
-int dct32(int k, int n) {
-  if (k == 0) return 64;
-  int j = (k * (2 * n + 1)) % 128, sign = 1;
-  if (j > 64) j = 128 - j;
-  if (j > 32) { j = 64 - j; sign = -1; }
-  return sign * kCosH[j];
-}
-
-void gen_scan(std::vector<int> &out, int w, int h, int stride, int type, int offx, int offy) {
-  if (type == 0) {
-    for (int d = 0; d < w + h - 1; d++) {
-      int y = d < h - 1 ? d : h - 1, x = d - y;
-      while (y >= 0 && x < w) out.push_back((y + offy) * stride + x + offx), y--, x++;
-    }
-  } else if (type == 1) {
-    for (int y = 0; y < h; y++)
-      for (int x = 0; x < w; x++) out.push_back((y + offy) * stride + x + offx);
-  } else {
-    for (int x = 0; x < w; x++)
-      for (int y = 0; y < h; y++) out.push_back((y + offy) * stride + x + offx);
-  }
-}
-
-int upload_tables() {
-  uint16_t scan[3][1360];
-  uint8_t scan_cg[3][85];
-  int16_t mat[1360];
-  for (int t = 0; t < 3; t++) {
-    int sb = 0, cb = 0;
-    for (int l = 0; l < 4; l++) {
-      const int n = 4 << l, g = 1 << l;
-      std::vector<int> cg, full;
-      gen_scan(cg, g, g, g, t, 0, 0);
-      for (int i = 0; i < g * g; i++) {
-        const int gx = cg[i] % g, gy = cg[i] / g;
-        gen_scan(full, 4, 4, n, t, gx * 4, gy * 4);
-      }
-      for (int i = 0; i < n * n; i++) scan[t][sb + i] = (uint16_t)full[i];
-      for (int i = 0; i < g * g; i++) scan_cg[t][cb + i] = (uint8_t)cg[i];
-      sb += n * n;
-      cb += g * g;
-    }
-  }
-  int mb = 0;
-  for (int l = 0; l < 4; l++) {
-    const int n = 4 << l;
-    for (int k = 0; k < n; k++)
-      for (int x = 0; x < n; x++) mat[mb + k * n + x] = (int16_t)dct32(k * (32 / n), x);
-    mb += n * n;
-  }
-  HVX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(kScan), scan, sizeof(scan)));
-  HVX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(kScanCG), scan_cg, sizeof(scan_cg)));
-  HVX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(kMat), mat, sizeof(mat)));
-  int16_t matT[1360];
-  mb = 0;
-  for (int l = 0; l < 4; l++) {
-    const int n = 4 << l;
-    for (int k = 0; k < n; k++)
-      for (int x = 0; x < n; x++) matT[mb + x * n + k] = mat[mb + k * n + x];
-    mb += n * n;
-  }
-  HVX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(kMatT), matT, sizeof(matT)));
-  return HVX_OK;
-}
+namespace {
 }  // namespace
 
 static void fold_timing(hvx_ctx *ctx) {
@@ -326,7 +235,10 @@ int hvx_create(int device, hvx_ctx **out) {
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(HVX_E_NODEV, "hvx_create: no HIP device");
   if (device < 0 || device >= ndev) return fail(HVX_E_INVALID, "hvx_create: bad device index");
   HVX_HIP(hipSetDevice(device));
+  if (const char *st = getenv("HVX_STACK_LIMIT")) HVX_HIP(hipDeviceSetLimit(hipLimitStackSize, (size_t)atol(st)));  // debugging
   int rc = upload_tables();
+  if (rc) return rc;
+  rc = hvx_hm_module_init();
   if (rc) return rc;
   hvx_ctx *c = new hvx_ctx;
   c->device = device;
@@ -1064,3 +976,4 @@ int hvx_plane_from_pel(hvx_ctx *ctx, const int16_t *d_pel, int pel_stride, int w
 }
 
 }  // extern "C"
+

@@ -84,7 +84,7 @@ __device__ __forceinline__ void mc_clip(const hvx_mc_job &j, int &mx, int &my) {
   my = (int16_t)(my < vmin ? vmin : my > vmax ? vmax : my);
 }
 
-__global__ __launch_bounds__(256) void k_mc(const int16_t *const *__restrict__ planes, int ls, int cs,
+static __global__ __launch_bounds__(256) void k_mc(const int16_t *const *__restrict__ planes, int ls, int cs,
                                             const hvx_mc_job *__restrict__ jobs, int n, int16_t *__restrict__ out) {
   __shared__ McSmem sm;
   const int jid = blockIdx.x;

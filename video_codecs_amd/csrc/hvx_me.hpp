@@ -358,7 +358,7 @@ constexpr MeDiaTab me_dia_build() {
   }
   return t;
 }
-__constant__ MeDiaTab kDiaTab = me_dia_build();
+static __constant__ MeDiaTab kDiaTab = me_dia_build();
 
 __device__ __forceinline__ MeCand me_dia_cand(const MeRange &g, int sx, int sy, int p) {
   const uint32_t v = kDiaTab.v[p];
@@ -370,7 +370,7 @@ __device__ __forceinline__ MeCand me_dia_cand(const MeRange &g, int sx, int sy, 
 }
 
 // xTZ2PointSearch (:438): the two points completing the diamond around point_nr
-__constant__ int8_t kTwoPoint[8][2][2] = {{{-1, 0}, {0, -1}}, {{-1, -1}, {1, -1}}, {{0, -1}, {1, 0}},
+static __constant__ int8_t kTwoPoint[8][2][2] = {{{-1, 0}, {0, -1}}, {{-1, -1}, {1, -1}}, {{0, -1}, {1, 0}},
                                           {{-1, 1}, {-1, -1}}, {{1, -1}, {1, 1}}, {{-1, 0}, {0, 1}},
                                           {{-1, 1}, {1, 1}}, {{1, 0}, {0, 1}}};
 
@@ -524,7 +524,7 @@ __device__ __forceinline__ void me_int_job(const hvx_me_job &j, const uint8_t *c
   }
 }
 
-__global__ __launch_bounds__(64) void k_me_int(const uint8_t *const *__restrict__ cur_planes,
+static __global__ __launch_bounds__(64) void k_me_int(const uint8_t *const *__restrict__ cur_planes,
                                               const uint8_t *const *__restrict__ ref_planes, int stride,
                                               const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t org[64 * 64];
@@ -544,7 +544,7 @@ __device__ __forceinline__ size_t me_ctu_slot(int b, int nref, int ncu, int firs
 
 // CTU pass: square SxS jobs of one depth (FEN shift SUB decided on the host), NW waves per job
 template <int S, int SUB, int NW>
-__global__ __launch_bounds__(64 * NW) void k_me_int_ctu(const uint8_t *const *__restrict__ cur_planes,
+static __global__ __launch_bounds__(64 * NW) void k_me_int_ctu(const uint8_t *const *__restrict__ cur_planes,
                                                        const uint8_t *const *__restrict__ ref_planes, int stride,
                                                        const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
                                                        int nref, int ncu, int first) {
@@ -591,8 +591,8 @@ __device__ __forceinline__ int me_qpel_sample(const uint8_t *ref, int sr, int x,
 }
 
 // xPatternRefinement (:808) candidate offsets: s_acMvRefineH / s_acMvRefineQ (TEncSearch.cpp:51-75)
-__constant__ int8_t kRefH[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
-__constant__ int8_t kRefQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
+static __constant__ int8_t kRefH[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
+static __constant__ int8_t kRefQ[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
 
 // Fractional-search LDS image for blocks up to SxS, NW waves per job.  The phase planes use
 // a row stride of S+8 int16: an 8x8 tile row of 8 samples then covers 4 banks and the 8
@@ -1139,7 +1139,7 @@ __device__ void me_frac_refine(const hvx_me_job &j, const uint8_t *ref, int stri
 }
 
 // generic jobs (any PU shape up to 64x64), 4 waves per job
-__global__ __launch_bounds__(256) void k_me_frac(const uint8_t *const *__restrict__ cur_planes,
+static __global__ __launch_bounds__(256) void k_me_frac(const uint8_t *const *__restrict__ cur_planes,
                                                 const uint8_t *const *__restrict__ ref_planes, int stride,
                                                 const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
   __shared__ MeFracSmem<64, 4> sm;
@@ -1151,7 +1151,7 @@ __global__ __launch_bounds__(256) void k_me_frac(const uint8_t *const *__restric
 
 // CTU pass: square SxS jobs of one depth, NW waves per job
 template <int S, int NW>
-__global__ __launch_bounds__(64 * NW) void k_me_frac_ctu(const uint8_t *const *__restrict__ cur_planes,
+static __global__ __launch_bounds__(64 * NW) void k_me_frac_ctu(const uint8_t *const *__restrict__ cur_planes,
                                                         const uint8_t *const *__restrict__ ref_planes, int stride,
                                                         const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
                                                         int nref, int ncu, int first) {
@@ -1201,7 +1201,7 @@ __device__ __forceinline__ void me_ctu_job(const uint8_t *const *__restrict__ cu
 }
 
 template <int S, int SUB, int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(S == 8 ? 7 : 1))) void k_me_ctu(const uint8_t *const *__restrict__ cur_planes,
+static __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(S == 8 ? 7 : 1))) void k_me_ctu(const uint8_t *const *__restrict__ cur_planes,
                                                    const uint8_t *const *__restrict__ ref_planes, int stride,
                                                    const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
                                                    int nref, int ncu, int first) {
@@ -1221,7 +1221,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(S == 8 
 // per job: thread t takes points t, t+256, ... and keeps its first minimum as a
 // (cost, raster index) key; a workgroup key-min picks the reference's point.  The pattern is
 // int16 (a bi target 2*org - other spans [-255, 510]), so SADs are plain |a - b| sums.
-__global__ __launch_bounds__(256) void k_me_full(const int16_t *const *__restrict__ tgt_planes, int tstride,
+static __global__ __launch_bounds__(256) void k_me_full(const int16_t *const *__restrict__ tgt_planes, int tstride,
                                                 const uint8_t *const *__restrict__ ref_planes, int stride,
                                                 const hvx_me_job *__restrict__ jobs, int n, hvx_me_result *__restrict__ out) {
   __shared__ MeFracSmem<64, 4, int16_t> sm;

@@ -44,7 +44,7 @@ __device__ __forceinline__ Blk block(int ctu, int ncx, int w, int h, int cs) {
 // keeps the edge-offset sums of its samples in registers (4 types x 5 classes, diff and count)
 // and adds band-offset samples to LDS histograms; the register sums are reduced per wave with
 // DPP adds and once per wave into LDS.
-__global__ __launch_bounds__(256) void k_sao_stats(const uint8_t *__restrict__ org_y, const uint8_t *__restrict__ org_cb,
+static __global__ __launch_bounds__(256) void k_sao_stats(const uint8_t *__restrict__ org_y, const uint8_t *__restrict__ org_cb,
                                                   const uint8_t *__restrict__ org_cr, int os_y, int os_c,
                                                   const uint8_t *__restrict__ rec_y, const uint8_t *__restrict__ rec_cb,
                                                   const uint8_t *__restrict__ rec_cr, int rs_y, int rs_c, int pic_w,
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void k_sao_stats(const uint8_t *__restrict__ o
 }
 
 // grid-stride over every 4-sample group of the plane comp = blockIdx.y; dst = src with offsets
-__global__ __launch_bounds__(256) void k_sao_apply(const uint8_t *__restrict__ src_y, const uint8_t *__restrict__ src_cb,
+static __global__ __launch_bounds__(256) void k_sao_apply(const uint8_t *__restrict__ src_y, const uint8_t *__restrict__ src_cb,
                                                   const uint8_t *__restrict__ src_cr, int ss_y, int ss_c,
                                                   uint8_t *__restrict__ dst_y, uint8_t *__restrict__ dst_cb,
                                                   uint8_t *__restrict__ dst_cr, int ds_y, int ds_c, int pic_w, int pic_h,

@@ -25,7 +25,7 @@ __device__ __forceinline__ float ssim_window(const uint8_t *o, int so, const uin
   return s;
 }
 
-__global__ __launch_bounds__(64) void k_ssim(const uint8_t *__restrict__ org, const uint8_t *__restrict__ rec,
+static __global__ __launch_bounds__(64) void k_ssim(const uint8_t *__restrict__ org, const uint8_t *__restrict__ rec,
                                              const hvx_ssim_job *__restrict__ jobs, int n, float *__restrict__ out) {
   __shared__ float win[1024];
   const int jid = blockIdx.x;
@@ -71,7 +71,7 @@ __device__ __forceinline__ float orient_weight(int k, int beta, int y, int x, fl
   return on ? wa : wb;
 }
 
-__global__ __launch_bounds__(64) void k_stvssim(const uint8_t *const *__restrict__ hist_org,
+static __global__ __launch_bounds__(64) void k_stvssim(const uint8_t *const *__restrict__ hist_org,
                                                 const uint8_t *const *__restrict__ hist_rec,
                                                 const float *__restrict__ dirs, const hvx_stvssim_job *__restrict__ jobs,
                                                 int n, float *__restrict__ out4) {

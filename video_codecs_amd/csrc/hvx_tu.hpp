@@ -787,7 +787,7 @@ __device__ void tu_inverse(TuSmem<L> &s, const hvx_tu_desc &d) {
 
 // mode: 0 forward, 1 inverse, 2 pipeline
 template <int L, int MODE>
-__global__ __launch_bounds__(64) void k_tu(const hvx_tu_desc *__restrict__ descs, const hvx_estbits *__restrict__ est,
+static __global__ __launch_bounds__(64) void k_tu(const hvx_tu_desc *__restrict__ descs, const hvx_estbits *__restrict__ est,
                                            const int32_t *__restrict__ est_idx, const int64_t *__restrict__ offs,
                                            int n, const int16_t *__restrict__ res_in, int32_t *__restrict__ temp_out,
                                            int32_t *__restrict__ lev_io, int32_t *__restrict__ arl_out,
@@ -1236,7 +1236,7 @@ __device__ int32_t rdoq_lane(const hvx_tu_desc &d, const hvx_estbits *est, const
 // significance context under each neighbour pattern -> cxI), flag 1.  Others (bypass, plain quant, RDOQ not needed): final levels in
 // scan order -> levI, uiAbsSum -> abs_out, flag 0.
 template <int L>
-__global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
+static __global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
                                                int n, const int16_t *__restrict__ res_in, int32_t *__restrict__ temp_out,
                                                int32_t *__restrict__ arl_out, uint32_t *__restrict__ ldI,
                                                uint32_t *__restrict__ cxI, int32_t *__restrict__ levI,
@@ -1356,7 +1356,7 @@ __global__ __launch_bounds__(64) void k_tu_fwd(const hvx_tu_desc *__restrict__ d
 // CTU pass uses one -- so the wave's LDS stays at the lane stage + 2 tables (8 waves per CU).
 // Otherwise each lane reads its own table from global memory.
 template <int L>
-__global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ descs, const hvx_estbits *__restrict__ est,
+static __global__ __launch_bounds__(64) void k_tu_rdoq(const hvx_tu_desc *__restrict__ descs, const hvx_estbits *__restrict__ est,
                                                 const int32_t *__restrict__ est_idx, int n,
                                                 const uint32_t *__restrict__ ldI, const uint32_t *__restrict__ cxI,
                                                 int32_t *__restrict__ levI, int32_t *__restrict__ stI,
@@ -1437,7 +1437,7 @@ __device__ void tu_inverse_fast(TuSmem<L> &s, const hvx_tu_desc &d) {
 }
 
 template <int L, int MODE>
-__global__ __launch_bounds__(64) void k_tu_fin(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
+static __global__ __launch_bounds__(64) void k_tu_fin(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
                                                int n, const int16_t *__restrict__ res_in,
                                                const int32_t *__restrict__ levI, int32_t *__restrict__ lev_io,
                                                int16_t *__restrict__ res_out, uint32_t *__restrict__ sse_out, int G,
@@ -1573,7 +1573,7 @@ __device__ __forceinline__ void lane_st_i16(int16_t *p, const int32_t (&r)[NN]) 
 }
 
 template <int L>
-__global__ __launch_bounds__(64) void k_tu_fwd_lane(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
+static __global__ __launch_bounds__(64) void k_tu_fwd_lane(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
                                                     int n, const int16_t *__restrict__ res_in, uint32_t *__restrict__ ldI,
                                                     uint32_t *__restrict__ cxI, int8_t *__restrict__ flags) {
   constexpr int N = 4 << L, NN = N * N, LOG2 = L + 2;
@@ -1634,7 +1634,7 @@ __global__ __launch_bounds__(64) void k_tu_fwd_lane(const hvx_tu_desc *__restric
 }
 
 template <int L>
-__global__ __launch_bounds__(64) void k_tu_fin_lane(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
+static __global__ __launch_bounds__(64) void k_tu_fin_lane(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
                                                     int n, const int16_t *__restrict__ res_in,
                                                     const int32_t *__restrict__ levI, int32_t *__restrict__ lev_io,
                                                     int16_t *__restrict__ res_out, uint32_t *__restrict__ sse_out,

@@ -1,0 +1,203 @@
+"""Host side of the HM-exact CTU decision (libhvx.so hvx_hm_compress, include/hvx.h).
+
+Mirrors the interface the reference drives per CTU -- TEncCu::compressCtu(TComDataCU*) followed
+by TEncCu::encodeCtu on the RD coder (hm-16.5rc1 TEncSlice.cpp:814-828) -- over batches: a
+picture is described once (hvx_hm_picture: slice parameters, lambdas, original / reference /
+reconstruction planes, the CTU array, the collocated motion field), and jobs are chains of CTUs
+decided in raster order by one GPU wave each, the CABAC contexts carried from CTU to CTU.
+
+numpy / ctypes mirrors of the structs of include/hvx_types.h live here; device memory comes
+from torch (plumbing).  No CPU fallback: without libhvx.so or a GPU these calls raise.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _abi
+
+PART_FIELDS = ("depth", "part", "pred", "skip", "merge", "merge_idx", "inter_dir", "ref0", "ref1", "mv0x", "mv0y",
+               "mv1x", "mv1y", "mvd0x", "mvd0y", "mvd1x", "mvd1y", "mvp0", "mvp1", "idir_y", "idir_c", "tr_idx",
+               "ts_y", "ts_cb", "ts_cr", "cbf_y", "cbf_cb", "cbf_cr", "qp")
+HM_PART = np.dtype([("depth", "i1"), ("part", "i1"), ("pred", "i1"), ("skip", "i1"), ("merge", "i1"),
+                    ("merge_idx", "i1"), ("inter_dir", "i1"), ("tr_idx", "i1"), ("ref", "i1", 2), ("mvp_idx", "i1", 2),
+                    ("mvp_num", "i1", 2), ("mv", "<i2", (2, 2)), ("mvd", "<i2", (2, 2)), ("idir", "u1", 2),
+                    ("ts", "u1", 3), ("cbf", "u1", 3), ("width", "u1"), ("qp", "i1")])
+assert HM_PART.itemsize == 40
+HM_CTU = np.dtype([("p", HM_PART, 256), ("coef", "<i2", 6144), ("bits", "<u4"), ("dist", "<u4"), ("cost", "<f8")],
+                  align=True)
+assert HM_CTU.itemsize == 22544
+HM_CODER = np.dtype([("st", "u1", 202), ("pad_", "u1", 6), ("frac", "<u8")])
+assert HM_CODER.itemsize == 216
+HM_JOB = np.dtype([("pic", "<i4"), ("first_ctu", "<i4"), ("n_ctus", "<i4"), ("chained", "<i4"), ("out", "<i4"),
+                   ("pad_", "<i4"), ("entry", HM_CODER), ("int2n", "<i2", 16)], align=True)
+assert HM_JOB.itemsize == 272
+
+P_, I32, U32, F64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_double
+
+
+class HmPicture(ctypes.Structure):
+    """hvx_hm_picture (include/hvx_types.h)."""
+    _fields_ = [("w", I32), ("h", I32), ("w_ctus", I32), ("h_ctus", I32), ("poc", I32), ("slice_type", I32), ("qp", I32),
+                ("nref", I32 * 2), ("ref_poc", (I32 * 4) * 2), ("ref_plane", (I32 * 4) * 2), ("chroma_qp", I32 * 2),
+                ("max_merge", I32), ("tmvp", I32), ("check_ldc", I32), ("col_from_l0", I32), ("col_valid", I32),
+                ("col_poc", I32), ("col_ref_poc", (I32 * 4) * 2), ("search_range", I32), ("amp", I32),
+                ("lambda_motion", U32), ("pad_", I32), ("lambda_", F64), ("sqrt_lambda", F64), ("chroma_weight", F64 * 2),
+                ("tq_lambda", F64 * 3), ("col_field", P_), ("org", P_ * 3), ("rec", P_ * 3), ("org_stride", I32 * 2),
+                ("rec_stride", I32 * 2), ("ctus", P_), ("ref8", P_ * 8), ("ref16", (P_ * 3) * 8), ("ref8_stride", I32),
+                ("ref16_stride", I32 * 2), ("pad2_", I32), ("entropy_bits", P_)]
+
+
+def pack_parts(rows):
+    """[..., 256, 29] int16 rows (PART_FIELDS order, oracle/cu_capture.cpp) -> HM_PART records."""
+    rows = np.asarray(rows)
+    out = np.zeros(rows.shape[:-1], HM_PART)
+    f = {n: rows[..., i] for i, n in enumerate(PART_FIELDS)}
+    for n in ("depth", "part", "pred", "skip", "merge", "merge_idx", "inter_dir", "tr_idx", "qp"):
+        out[n] = f[n]
+    out["ref"][..., 0], out["ref"][..., 1] = f["ref0"], f["ref1"]
+    out["mvp_idx"][..., 0], out["mvp_idx"][..., 1] = f["mvp0"], f["mvp1"]
+    out["mv"][..., 0, 0], out["mv"][..., 0, 1], out["mv"][..., 1, 0], out["mv"][..., 1, 1] = f["mv0x"], f["mv0y"], f["mv1x"], f["mv1y"]
+    out["mvd"][..., 0, 0], out["mvd"][..., 0, 1] = f["mvd0x"], f["mvd0y"]
+    out["mvd"][..., 1, 0], out["mvd"][..., 1, 1] = f["mvd1x"], f["mvd1y"]
+    out["idir"][..., 0], out["idir"][..., 1] = f["idir_y"], f["idir_c"]
+    out["ts"][..., 0], out["ts"][..., 1], out["ts"][..., 2] = f["ts_y"], f["ts_cb"], f["ts_cr"]
+    out["cbf"][..., 0], out["cbf"][..., 1], out["cbf"][..., 2] = f["cbf_y"], f["cbf_cb"], f["cbf_cr"]
+    return out
+
+
+def unpack_parts(parts):
+    """HM_PART records [..., 256] -> [..., 256, 29] int16 rows (PART_FIELDS order)."""
+    p = np.asarray(parts)
+    cols = [p["depth"], p["part"], p["pred"], p["skip"], p["merge"], p["merge_idx"], p["inter_dir"], p["ref"][..., 0],
+            p["ref"][..., 1], p["mv"][..., 0, 0], p["mv"][..., 0, 1], p["mv"][..., 1, 0], p["mv"][..., 1, 1],
+            p["mvd"][..., 0, 0], p["mvd"][..., 0, 1], p["mvd"][..., 1, 0], p["mvd"][..., 1, 1], p["mvp_idx"][..., 0],
+            p["mvp_idx"][..., 1], p["idir"][..., 0], p["idir"][..., 1], p["tr_idx"], p["ts"][..., 0], p["ts"][..., 1],
+            p["ts"][..., 2], p["cbf"][..., 0], p["cbf"][..., 1], p["cbf"][..., 2], p["qp"]]
+    return np.stack([c.astype(np.int16) for c in cols], axis=-1)
+
+
+def state_size():
+    from . import hvx
+    n = ctypes.c_size_t()
+    hvx._check(hvx.lib().hvx_hm_state_size(ctypes.byref(n)), "hvx_hm_state_size")
+    return n.value
+
+
+def pad_plane(plane, margin, dtype):
+    """A copy of a 2-D plane with its border extended by `margin` (TComPicYuv::extendPicBorder)."""
+    return np.pad(np.asarray(plane), margin, mode="edge").astype(dtype)
+
+
+class DevicePicture:
+    """One picture's device-side description (hvx_hm_picture) and the buffers it points at.
+
+    org: (Y, Cb, Cr) uint8 arrays; refs: list of (Y, Cb, Cr) uint8 reference pictures (indexed by
+    ref_plane); params: the slice / RD scalars (see HmPicture); rec: optional (Y, Cb, Cr) uint8
+    initial reconstruction; ctus: optional HM_CTU array (the picture's CTU data); col_field:
+    optional int16 [nctu*16, 8] collocated motion field."""
+
+    M8, M16, M16C = _abi.PLANE_MARGIN, 80, 40
+
+    def __init__(self, org, refs, params, entropy_bits, rec=None, ctus=None, col_field=None, device="cuda"):
+        import torch
+        self.w, self.h = int(org[0].shape[1]), int(org[0].shape[0])
+        w, h = self.w, self.h
+        self.wc, self.hc = (w + 63) // 64, (h + 63) // 64
+        self.keep = []
+
+        def dev(a):
+            t = torch.from_numpy(np.ascontiguousarray(a)).to(device)
+            self.keep.append(t)
+            return t
+
+        s = HmPicture()
+        s.w, s.h, s.w_ctus, s.h_ctus = w, h, self.wc, self.hc
+        for k, v in params.items():
+            if k in ("nref", "ref_poc", "ref_plane", "chroma_qp", "col_ref_poc", "chroma_weight", "tq_lambda"):
+                a = getattr(s, k)
+                v = np.asarray(v)
+                if v.ndim == 2:
+                    for i in range(v.shape[0]):
+                        for j in range(v.shape[1]):
+                            a[i][j] = v[i, j].item()
+                else:
+                    for i in range(v.shape[0]):
+                        a[i] = v[i].item()
+            else:
+                setattr(s, "lambda_" if k == "lambda" else k, v)
+        self.org_t = [dev(np.asarray(p, np.uint8)) for p in org]
+        for c in range(3):
+            s.org[c] = self.org_t[c].data_ptr()
+        s.org_stride[0], s.org_stride[1] = w, w // 2
+        rw, rh = self.wc * 64, self.hc * 64
+        recs = []
+        for c in range(3):
+            sh = 1 if c else 0
+            buf = np.zeros((rh >> sh, rw >> sh), np.uint8)
+            if rec is not None:
+                r = np.asarray(rec[c], np.uint8)
+                buf[:r.shape[0], :r.shape[1]] = r
+            recs.append(dev(buf))
+        self.rec_t = recs
+        for c in range(3):
+            s.rec[c] = recs[c].data_ptr()
+        s.rec_stride[0], s.rec_stride[1] = rw, rw // 2
+        n = self.wc * self.hc
+        ct = np.zeros(n, HM_CTU) if ctus is None else np.ascontiguousarray(ctus)
+        assert ct.shape[0] == n
+        self.ctus_t = dev(ct.view(np.uint8).reshape(-1))
+        s.ctus = self.ctus_t.data_ptr()
+        if col_field is not None:
+            s.col_field = dev(np.asarray(col_field, np.int16)).data_ptr()
+        assert len(refs) <= 8
+        for i, ref in enumerate(refs):
+            y8 = dev(pad_plane(ref[0], self.M8, np.uint8))
+            s.ref8[i] = y8.data_ptr() + (self.M8 * y8.shape[1] + self.M8)
+            s.ref8_stride = int(y8.shape[1])
+            for c in range(3):
+                m = self.M16 if c == 0 else self.M16C
+                p16 = dev(pad_plane(ref[c], m, np.int16))
+                s.ref16[i][c] = p16.data_ptr() + 2 * (m * p16.shape[1] + m)
+                s.ref16_stride[1 if c else 0] = int(p16.shape[1])
+        s.entropy_bits = dev(np.asarray(entropy_bits, np.int32)).data_ptr()
+        self.struct = s
+
+    def ctus(self):
+        """The picture's CTU array (HM_CTU records) as it is on the device now."""
+        return self.ctus_t.cpu().numpy().view(HM_CTU)
+
+
+class Engine:
+    """hvx_hm_compress over a set of pictures: device picture table, job list, per-job state."""
+
+    def __init__(self, pictures, device="cuda"):
+        import torch
+        self.pictures = pictures
+        raw = b"".join(bytes(p.struct) for p in pictures)
+        self.pics_t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+        self.device = device
+        self.state = None
+
+    def compress(self, jobs, n_out):
+        """Run the jobs (HM_JOB array); returns (ctus [n_out] HM_CTU, rec [n_out, 6144] uint8,
+        coders [n_out] HM_CODER) copied to the host."""
+        import torch
+        from . import hvx
+        jobs = np.ascontiguousarray(jobs, HM_JOB)
+        n = len(jobs)
+        sb = state_size()
+        if self.state is None or self.state.numel() < n * sb:
+            self.state = torch.empty(n * sb, dtype=torch.uint8, device=self.device)
+        jobs_t = torch.from_numpy(jobs.view(np.uint8).reshape(-1).copy()).to(self.device)
+        out_ctu = torch.zeros(n_out * HM_CTU.itemsize, dtype=torch.uint8, device=self.device)
+        out_rec = torch.zeros(n_out * 6144, dtype=torch.uint8, device=self.device)
+        out_cod = torch.zeros(n_out * HM_CODER.itemsize, dtype=torch.uint8, device=self.device)
+        P = ctypes.c_void_p
+        hvx._check(hvx.lib().hvx_hm_compress(hvx.context(), P(self.pics_t.data_ptr()), P(jobs_t.data_ptr()), n,
+                                             P(self.state.data_ptr()), P(out_ctu.data_ptr()), P(out_rec.data_ptr()),
+                                             P(out_cod.data_ptr())), "hvx_hm_compress")
+        torch.cuda.synchronize()
+        st = self.state[:n * sb].view(n, sb)[:, :16].cpu().numpy().copy()
+        self.last_debug = st.view(np.int32).reshape(n, 4)  # State.dbg (HM_CHECKS builds)
+        return (out_ctu.cpu().numpy().view(HM_CTU), out_rec.cpu().numpy().reshape(n_out, 6144),
+                out_cod.cpu().numpy().view(HM_CODER))
