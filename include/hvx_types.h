@@ -361,12 +361,16 @@ typedef struct hvx_hm_picture {
 /* One chain of CTUs decided in raster order by one wave: CTUs first_ctu .. first_ctu+n_ctus-1 of
  * picture pic, the first from `entry` (m_pppcRDSbacCoder[0][CI_CURR_BEST] on entry) and
  * int2n (TEncSearch::m_integerMv2Nx2N [2][4][2]), each later one from the previous CTU's
- * encodeCtu state and search state.  chained = 1: every finished CTU is written into the
+ * encodeCtu state and search state.  Neighbours outside [slice_start, slice_end] are unavailable
+ * (TComDataCU::getPU* with the slice restriction; SliceMode=1 slices of whole CTUs), and the
+ * slice's last CTU ends without the end_of_slice_segment_flag bin.  chained = 1: every finished CTU is written into the
  * picture (ctus[addr] and rec) before the next starts; 0: the picture is only read (n_ctus = 1,
  * independent CTUs against a fixed neighbourhood).  Outputs go to slot out + k of the output
  * arrays for the k-th CTU of the chain. */
 typedef struct hvx_hm_job {
-  int32_t pic, first_ctu, n_ctus, chained, out, pad_;
+  int32_t pic, first_ctu, n_ctus, chained, out;
+  int32_t slice_start, slice_end;  /* the slice holding the chain: first / last CTU address (raster) */
+  int32_t debug_;                  /* 0 (debugging builds: stop stage) */
   hvx_hm_coder entry;
   int16_t int2n[16];
 } hvx_hm_job;

@@ -95,4 +95,9 @@ cucap() {  # cucap <out.bin> <cfg> <yuv> <frames> <qp>
 }
 cucap tests/golden/ctu_ldp_rand.bin   $CFG/encoder_lowdelay_P_main.cfg "$TMP/rand4.yuv"   3 32
 cucap tests/golden/ctu_ldp_smooth.bin $CFG/encoder_lowdelay_P_main.cfg "$TMP/smooth4.yuv" 4 27
+HVX_CAPTURE="$TMP/cu.bin" $ORC/TAppEncoder_cucap -c $CFG/encoder_lowdelay_P_main.cfg -i "$TMP/smooth4.yuv" -wdt 416 -hgt 240 \
+  -fr 30 -f 3 -q 30 --SliceMode=1 --SliceArgument=7 -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+python3 oracle/compact_ctu.py "$TMP/cu.bin" tests/golden/ctu_ldp_slices.bin
+# slice-start CABAC states of every slice type and QP (TEncSbac::resetEntropy)
+make -s -C oracle ctx_init
 ls -la tests/golden

@@ -48,3 +48,20 @@ def test_ctu_capture_covers_modes():
     assert (p[:, f["pred"]] == 1).any()          # intra CUs inside P pictures
     assert (p[:, f["tr_idx"]] > 0).any()         # RQT splits
     assert set(np.unique(p[:, f["depth"]])) >= {0, 1, 2, 3}
+
+
+def test_ctx_init_states_vs_hm():
+    """video_codecs_amd/data/ctx_init_states.bin (TEncSbac::resetEntropy of every slice type / QP,
+    oracle/ctx_init_dump.cpp) equals the slice-start states the captures recorded."""
+    import numpy as np
+    from video_codecs_amd import _abi
+    init = _abi.load_ctx_init_states()
+    for name in CAPTURES + ["ctu_ldp_slices.bin"]:
+        g = _load(name)
+        wc = (int(g["pic_i32"][0][0]) + 63) // 64
+        for pic in range(g["pic_i32"].shape[0]):
+            pi = g["pic_i32"][pic]
+            first, n, st, qp = int(pi[41]), int(pi[42]), int(pi[3]), int(pi[4])
+            starts = range(0, n, wc) if name == "ctu_ldp_slices.bin" else [0]
+            for a in starts:
+                np.testing.assert_array_equal(g["ctu_states"][first + a], init[st, qp], err_msg=(name, pic, a))

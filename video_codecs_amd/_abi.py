@@ -189,3 +189,11 @@ def deblock_params(w, h, beta_offset_div2=0, tc_offset_div2=0, cb_qp_offset=0, c
     p["pic_w"], p["pic_h"], p["beta_offset_div2"], p["tc_offset_div2"] = w, h, beta_offset_div2, tc_offset_div2
     p["cb_qp_offset"], p["cr_qp_offset"] = cb_qp_offset, cr_qp_offset
     return p
+
+
+def load_ctx_init_states():
+    """uint8 [3 slice types (B, P, I)][52 QP][HVX_NUM_CTX]: the CABAC context states at the start of
+    a slice (TEncSbac::resetEntropy, TEncSbac.cpp:105; video_codecs_amd/data/README.md)."""
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "ctx_init_states.bin")
+    return np.fromfile(p, dtype=np.uint8).reshape(3, 52, 202)

@@ -85,6 +85,7 @@ __device__ __forceinline__ int16_t *yaddr(Yuv *b, int c, int x, int y) { return 
 // per-chain state in HBM
 struct State {
   int dbg[4];  // HM_CHECKS: E.dbg of the last CTU
+  uint64_t prof[2][16];  // HM_PROFILE: per-category clock ticks and calls of the job
   Cu cu[8];
   Yuv yuv[28];                    // TComYuv sets (kind x depth), addressed through hm_e.yi
   Yuv qt_yuv[4], qt_ts_yuv, tmp_yuv_pred;
@@ -137,6 +138,7 @@ struct Enc {
   hvx_hm_picture P;
   State *S;
   int ctu_addr, ctu_x, ctu_y, slice_qp;
+  int slice_start, slice_end;  // the chain's slice (CTU addresses)
   int best[4], temp[4];  // Cu index in S->cu
   int yi[7][4];          // Yuv index: orig, pred_best, pred_temp, resi_best, resi_temp, reco_best, reco_temp
   int cur;               // the coder the entropy calls count with
@@ -148,6 +150,7 @@ struct Enc {
   uint32_t avail[4];
   int dbg[4];  // HM_CHECKS: first violated check (code, a, b) of the job
   int stage, stop;  // HM_CHECKS: stop the CTU at debugging stage `stage` (0: never)
+  uint64_t prof[2][16];  // HM_PROFILE accumulators
   Leaf u;
 };
 }  // namespace hm
@@ -162,6 +165,22 @@ __device__ __forceinline__ Cu *BEST(int d) { return &E.S->cu[E.best[d]]; }
 __device__ __forceinline__ Cu *TEMP(int d) { return &E.S->cu[E.temp[d]]; }
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 __device__ __forceinline__ int lid() { return (int)threadIdx.x; }
+// HM_PROFILE builds accumulate the clock ticks (s_memtime) and calls of the leaf categories
+enum { PR_ME, PR_MC, PR_TPL, PR_TUF, PR_TUI, PR_COEF, PR_EST, PR_IFP, PR_IPRED, PR_DIST, PR_CTU, PR_ENC, PR_N };
+#ifdef HM_PROFILE
+struct ProfScope {
+  int cat;
+  uint64_t t0;
+  __device__ __forceinline__ explicit ProfScope(int c) : cat(c), t0(__builtin_amdgcn_s_memtime()) {}
+  __device__ __forceinline__ ~ProfScope() {
+    hm_e.prof[0][cat] += __builtin_amdgcn_s_memtime() - t0;
+    hm_e.prof[1][cat] += 1;
+  }
+};
+#define HM_PROF(c) ProfScope prof_scope_(c)
+#else
+#define HM_PROF(c) ((void)0)
+#endif
 // HM_CHECKS builds validate the indices and sample positions below, record the first violation
 // in E.dbg and keep the access inside its buffer (a debugging aid; off in the product build)
 #ifdef HM_CHECKS
@@ -230,11 +249,15 @@ __device__ __forceinline__ const Part *ctu_parts(int addr) {
   if (HM_CHECKING && (addr < 0 || addr >= E.P.w_ctus * E.P.h_ctus)) addr = E.ctu_addr;
   return addr == E.ctu_addr ? E.S->ctu_p : E.P.ctus[addr].p;
 }
-__device__ __forceinline__ int ctu_left() { return E.ctu_x > 0 ? E.ctu_addr - 1 : -1; }
-__device__ __forceinline__ int ctu_above() { return E.ctu_y > 0 ? E.ctu_addr - E.P.w_ctus : -1; }
-__device__ __forceinline__ int ctu_above_left() { return (E.ctu_x > 0 && E.ctu_y > 0) ? E.ctu_addr - E.P.w_ctus - 1 : -1; }
+// getCtuLeft / getCtuAbove / ... with CUIsFromSameSliceAndTile (TComDataCU.cpp:1024-1238)
+__device__ __forceinline__ int ctu_in_slice(int a) { return a >= E.slice_start ? a : -1; }
+__device__ __forceinline__ int ctu_left() { return E.ctu_x > 0 ? ctu_in_slice(E.ctu_addr - 1) : -1; }
+__device__ __forceinline__ int ctu_above() { return E.ctu_y > 0 ? ctu_in_slice(E.ctu_addr - E.P.w_ctus) : -1; }
+__device__ __forceinline__ int ctu_above_left() {
+  return (E.ctu_x > 0 && E.ctu_y > 0) ? ctu_in_slice(E.ctu_addr - E.P.w_ctus - 1) : -1;
+}
 __device__ __forceinline__ int ctu_above_right() {
-  return (E.ctu_y > 0 && E.ctu_x < E.P.w_ctus - 1) ? E.ctu_addr - E.P.w_ctus + 1 : -1;
+  return (E.ctu_y > 0 && E.ctu_x < E.P.w_ctus - 1) ? ctu_in_slice(E.ctu_addr - E.P.w_ctus + 1) : -1;
 }
 __device__ __forceinline__ Nb nb_none() { return Nb{nullptr, 0, 0}; }
 __device__ __forceinline__ Nb nb_make(const Part *p, int idx) {
@@ -836,6 +859,7 @@ __device__ void tu_desc(const Cu *cu, const Tu &t, int comp, hvx_tu_desc &d) {
 }
 // codeCoeffNxN on the current coder, levels TU-packed int16
 __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_t *coef) {
+  HM_PROF(PR_COEF);
   hvx_tu_desc d;
   tu_desc(cu, t, comp, d);
   const uint16_t *scan = kScan[d.scan_type] + scan_base(ilog2(d.width) - 2);
@@ -845,9 +869,54 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
   E.cod[E.cur].frac += L.frac;
 }
 // TEncEntropy::estimateBit (TEncEntropy.cpp:685) from the current coder
+// The entries TEncSbac::estBit writes (exactly those of estbit_update), one per lane: two
+// rounds of 64 entries instead of ~200 serial table reads by the whole wave
 __device__ void estimate_bit(int w, int h, int ch) {
-  const uint32_t rice[4] = {0, 0, 0, 0};
-  estbit_update(E.cod[E.cur].st, E.eb, rice, w, h, ch, &E.est);
+  HM_PROF(PR_EST);
+  const uint8_t *st = E.cod[E.cur].st;
+  hvx_estbits *e = &E.est;
+#define EB(ctx, v) E.eb[st[(ctx)] ^ (v)]
+  const int l = lid(), b = l & 1;
+  // round 1: cbf (20), root cbf (8), sig CG (4), significance (<= 28)
+  if (l < 20) e->blockCbpBits[l >> 1][b] = EB(HVX_CTX_QT_CBF + (l >> 1), b);
+  else if (l < 28) e->blockRootCbpBits[(l - 20) >> 1][b] = EB(HVX_CTX_QT_ROOT_CBF + ((l - 20) >> 1), b);
+  else if (l < 32) e->significantCoeffGroupBits[(l - 28) >> 1][b] = EB(HVX_CTX_SIG_CG + ch * 2 + ((l - 28) >> 1), b);
+  else {
+    const int type = (w == 4 && h == 4) ? 0 : (w == 8 && h == 8) ? 1 : 2;
+    const int first = estbit_sig_start(ch, type), num = estbit_sig_size(ch, type), off = ch ? 28 : 0;
+    const int single = estbit_sig_start(ch, 3);
+    // the index list: [0 if first > 0], single, first .. first + num - 1
+    const int lead = first > 0 ? 2 : 1, k = (l - 32) >> 1;
+    int idx = -1;
+    if (k < lead + num) idx = (first > 0 && k == 0) ? 0 : (k == lead - 1) ? single : first + (k - lead);
+    if (idx >= 0) e->significantBits[off + idx][b] = EB(HVX_CTX_SIG + off + idx, b);
+  }
+  // round 2: greater-1 (<= 32), level-abs (<= 8), last X / Y prefixes (<= 11 each), rice (4)
+  if (l < 32) {
+    const int i = l >> 1;
+    if (i < (ch ? 8 : 16)) e->greaterOneBits[(ch ? 16 : 0) + i][b] = EB(HVX_CTX_ONE + (ch ? 16 : 0) + i, b);
+  } else if (l < 40) {
+    const int i = (l - 32) >> 1;
+    if (i < (ch ? 2 : 4)) e->levelAbsBits[(ch ? 4 : 0) + i][b] = EB(HVX_CTX_ABS + (ch ? 4 : 0) + i, b);
+  } else if (l < 62) {
+    const int yax = l >= 51, c = l - (yax ? 51 : 40);
+    const int n = yax ? h : w, cl = estbit_log2(n) - 2;
+    const int o = ch ? 0 : cl * 3 + ((cl + 1) >> 2), sft = ch ? cl : (cl + 3) >> 2;
+    const int base = (yax ? HVX_CTX_LAST_Y : HVX_CTX_LAST_X) + ch * 15 + o;
+    const int G = estbit_group_idx(n - 1);
+    if (c <= G) {
+      int bits = 0;
+      for (int q = 0; q < c; q++) bits += EB(base + (q >> sft), 1);
+      if (c < G) bits += EB(base + (c >> sft), 0);
+      if (yax) e->lastYBits[ch][c] = bits;
+      else e->lastXBits[ch][c] = bits;
+    }
+  } else {
+    e->golombRiceAdaptationStatistics[l - 62] = 0;
+    e->golombRiceAdaptationStatistics[l - 60] = 0;
+  }
+#undef EB
+  wsync();
 }
 
 // ============================================================================================
@@ -986,6 +1055,7 @@ __device__ __forceinline__ double rd_cost_sad(uint32_t bits, uint32_t dist) {
 }
 __device__ __forceinline__ uint32_t mv_cost_bits(uint32_t bits) { return (uint32_t)(E.P.lambda_motion * bits) >> 16; }
 __device__ uint32_t sse_wave(const int16_t *a, int sa, const int16_t *b, int sb, int w, int h) {
+  HM_PROF(PR_DIST);
   uint32_t s = 0;
   const int n = w * h, sh = ilog2(w);
   for (int i = lid(); i < n; i += 64) {
@@ -1016,6 +1086,10 @@ __device__ uint32_t yuv_dist(Yuv *a, Yuv *b, int w) {
 // ============================================================================================
 template <int L>
 __device__ int32_t tu_fwd_l(const hvx_tu_desc &d, const int16_t *resi, int rs, int16_t *coef) {
+  HM_PROF(PR_TUF);
+#ifdef HM_PROFILE
+  ProfScope prof_size_(12 + L);
+#endif
   TuSmem<L> &s = *reinterpret_cast<TuSmem<L> *>(&E.u);
   constexpr int N = 4 << L;
   for (int i = lid(); i < N * N; i += 64) s.a[i] = resi[(i >> (L + 2)) * rs + (i & (N - 1))];
@@ -1027,6 +1101,7 @@ __device__ int32_t tu_fwd_l(const hvx_tu_desc &d, const int16_t *resi, int rs, i
 }
 template <int L>
 __device__ void tu_inv_l(const hvx_tu_desc &d, const int16_t *coef, int16_t *resi, int rs) {
+  HM_PROF(PR_TUI);
   TuSmem<L> &s = *reinterpret_cast<TuSmem<L> *>(&E.u);
   constexpr int N = 4 << L;
   for (int i = lid(); i < N * N; i += 64) s.lev[i] = coef[i];
@@ -1142,6 +1217,7 @@ __device__ __forceinline__ void clip_mv(const Cu *cu, int &mx, int &my) {  // TC
   my = (int16_t)(my < vmin ? vmin : my > vmax ? vmax : my);
 }
 __device__ void mc_pu(const Cu *cu, int ps, int pu, Yuv *dst) {
+  HM_PROF(PR_MC);
   int a, w, h, xp, yp;
   part_index_size(cu, ps, pu, a, w, h);
   part_position(cu, ps, pu, xp, yp, w, h);
@@ -1702,6 +1778,7 @@ __device__ void enc_res_rd_inter(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Yuv *re
 // predInterSearch (TEncSearch.cpp:2912), P slices
 // ============================================================================================
 __device__ uint32_t template_cost(const Cu *cu, int ps, int pu, Yuv *org, int list, int ref_idx, const int16_t *mvc) {
+  HM_PROF(PR_TPL);
   int a, w, h, xp, yp;
   part_index_size(cu, ps, pu, a, w, h);
   part_position(cu, ps, pu, xp, yp, w, h);
@@ -1755,6 +1832,7 @@ __device__ void check_best_mvp(const Amvp &in, const int16_t *mv, int16_t *pred,
 // xMotionEstimation (uni): TZ search + fractional refinement through hvx_me.hpp
 __device__ void motion_estimation(Cu *cu, int ps, int pu, int list, int ref_idx, const int16_t *pred, int16_t *mv,
                                   uint32_t &bits, uint32_t &cost) {
+  HM_PROF(PR_ME);
   int a, w, h, xp, yp;
   part_index_size(cu, ps, pu, a, w, h);
   part_position(cu, ps, pu, xp, yp, w, h);
@@ -1981,6 +2059,7 @@ __device__ void intra_border(const Cu *cu, const Tu &t, int comp, int16_t *B) {
 }
 // predIntraAng of a TU into pred (stride ystride(comp))
 __device__ void intra_predict_tu(const Cu *cu, const Tu &t, int comp, int mode, int16_t *pred) {
+  HM_PROF(PR_IPRED);
   IntraScratch &is = E.u.in;
   const int n = t.w[comp], log2n = ilog2(n);
   const bool luma = comp == 0;
@@ -2005,6 +2084,7 @@ __device__ void intra_predict_tu(const Cu *cu, const Tu &t, int comp, int mode, 
 // the first pass of estIntraPredLumaQT (:2221-2330): SATD of 35 modes + xModeBitsIntra, the
 // candidate list and the MPM append (HHI_RQT_INTRA_SPEEDUP, FastUDIUseMPM)
 __device__ void intra_first_pass(const Cu *cu, const Tu &tpu, Yuv *org, int depth) {
+  HM_PROF(PR_IFP);
   IntraScratch &is = E.u.in;
   const int n = tpu.w[0], log2n = ilog2(n);
   intra_border(cu, tpu, 0, is.unf);
@@ -2903,7 +2983,10 @@ __device__ void compress_ctu(int addr, const Coder *entry_g, int entry_in_lds, C
   // the entry state aside for encodeCtu (CI_CHROMA_INTRA coders are never used by the decision)
   cload(RD(5, CI_CHROMA_INTRA), RD(0, CI_CURR_BEST));
   HM_STAGE(1);
-  compress_cu<0>(SIZE_NONE);
+  {
+    HM_PROF(PR_CTU);
+    compress_cu<0>(SIZE_NONE);
+  }
   HM_STAGE(5);
   if (HM_STOPPED) return;
   // encodeCtu on m_pppcRDSbacCoder[0][CI_CURR_BEST] after resetBits (TEncSlice.cpp:821-828)
@@ -2917,7 +3000,10 @@ __device__ void compress_ctu(int addr, const Coder *entry_g, int entry_in_lds, C
   copy_words(v->p, S->ctu_p, (int)sizeof(Part) * 256);
   copy_words(v->coef, S->ctu_coef, 2 * 6144);
   wsync();
-  encode_cu<0>(0, addr == E.P.w_ctus * E.P.h_ctus - 1);
+  {
+    HM_PROF(PR_ENC);
+    encode_cu<0>(0, addr == E.slice_end);
+  }
   if (after_g) {
     copy_words(after_g, &E.cod[E.cur], (int)sizeof(Coder));
     wsync();
@@ -2946,8 +3032,11 @@ static __global__ __launch_bounds__(64) void k_hm_compress(const hvx_hm_picture 
   State *S = (State *)(state_base + (size_t)jid * state_bytes);
   hm_e.S = S;
   if (l < 4) hm_e.dbg[l] = 0;
-  hm_e.stage = job.pad_;
+  hm_e.stage = job.debug_;
+  hm_e.slice_start = job.slice_start;
+  hm_e.slice_end = job.slice_end;
   hm_e.stop = 0;
+  if (l < 32) hm_e.prof[l >> 4][l & 15] = 0;
   copy_words(S->int2n, job.int2n, (int)sizeof(S->int2n));
   wsync();
   const int n = job.n_ctus;
@@ -2958,6 +3047,7 @@ static __global__ __launch_bounds__(64) void k_hm_compress(const hvx_hm_picture 
     // the next CTU starts from this CTU's encodeCtu state (m_pppcRDSbacCoder[0][CI_CURR_BEST])
     // which compress_ctu left in coder RD(0, CI_CURR_BEST)
     if (l < 4) S->dbg[l] = hm_e.dbg[l];
+    if (l < 32) S->prof[l >> 4][l & 15] = hm_e.prof[l >> 4][l & 15];
     hvx_hm_ctu *o = &out_ctu[slot];
     copy_words(o->p, S->ctu_p, (int)sizeof(Part) * 256);
     copy_words(o->coef, S->ctu_coef, 2 * 6144);

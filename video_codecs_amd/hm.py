@@ -29,8 +29,9 @@ assert HM_CTU.itemsize == 22544
 HM_CODER = np.dtype([("st", "u1", 202), ("pad_", "u1", 6), ("frac", "<u8")])
 assert HM_CODER.itemsize == 216
 HM_JOB = np.dtype([("pic", "<i4"), ("first_ctu", "<i4"), ("n_ctus", "<i4"), ("chained", "<i4"), ("out", "<i4"),
-                   ("pad_", "<i4"), ("entry", HM_CODER), ("int2n", "<i2", 16)], align=True)
-assert HM_JOB.itemsize == 272
+                   ("slice_start", "<i4"), ("slice_end", "<i4"), ("debug_", "<i4"), ("entry", HM_CODER),
+                   ("int2n", "<i2", 16)], align=True)
+assert HM_JOB.itemsize == 280
 
 P_, I32, U32, F64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_double
 
@@ -197,7 +198,8 @@ class Engine:
                                              P(self.state.data_ptr()), P(out_ctu.data_ptr()), P(out_rec.data_ptr()),
                                              P(out_cod.data_ptr())), "hvx_hm_compress")
         torch.cuda.synchronize()
-        st = self.state[:n * sb].view(n, sb)[:, :16].cpu().numpy().copy()
-        self.last_debug = st.view(np.int32).reshape(n, 4)  # State.dbg (HM_CHECKS builds)
+        st = self.state[:n * sb].view(n, sb)[:, :272].cpu().numpy().copy()
+        self.last_debug = st[:, :16].copy().view(np.int32).reshape(n, 4)  # State.dbg (HM_CHECKS builds)
+        self.last_prof = st[:, 16:272].copy().view(np.uint64).reshape(n, 2, 16)  # State.prof (HM_PROFILE builds)
         return (out_ctu.cpu().numpy().view(HM_CTU), out_rec.cpu().numpy().reshape(n_out, 6144),
                 out_cod.cpu().numpy().view(HM_CODER))
