@@ -135,6 +135,7 @@ struct hm_enc {
   yuv_t yuv_pred_l[2], yuv_pred_tmp, tmp_yuv_pred; /* m_acYuvPred, m_cYuvPredTemp, m_tmpYuvPred */
   int ctu_addr, ctu_x, ctu_y;
   int slice_qp;
+  int slice_start, slice_end;  /* SliceMode=1 slice of the CTU (CTU addresses) */
 };
 
 static void cbin(hm_enc *e, int ctx, int v) {
@@ -159,11 +160,15 @@ static void load(coder_t *dst, const coder_t *src) { *dst = *src; }
 typedef struct { const hm_part *p; int idx; int valid; } nb_t;
 
 static const hm_part *ctu_parts(const hm_enc *e, int addr) { return e->ctus[addr].p; }
-static int ctu_left(const hm_enc *e) { return e->ctu_x > 0 ? e->ctu_addr - 1 : -1; }
-static int ctu_above(const hm_enc *e) { return e->ctu_y > 0 ? e->ctu_addr - e->pic->w_ctus : -1; }
-static int ctu_above_left(const hm_enc *e) { return (e->ctu_x > 0 && e->ctu_y > 0) ? e->ctu_addr - e->pic->w_ctus - 1 : -1; }
+/* getCtuLeft / ... with CUIsFromSameSliceAndTile: a CTU before the slice is unavailable */
+static int in_slice(const hm_enc *e, int a) { return a >= e->slice_start ? a : -1; }
+static int ctu_left(const hm_enc *e) { return e->ctu_x > 0 ? in_slice(e, e->ctu_addr - 1) : -1; }
+static int ctu_above(const hm_enc *e) { return e->ctu_y > 0 ? in_slice(e, e->ctu_addr - e->pic->w_ctus) : -1; }
+static int ctu_above_left(const hm_enc *e) {
+  return (e->ctu_x > 0 && e->ctu_y > 0) ? in_slice(e, e->ctu_addr - e->pic->w_ctus - 1) : -1;
+}
 static int ctu_above_right(const hm_enc *e) {
-  return (e->ctu_y > 0 && e->ctu_x < e->pic->w_ctus - 1) ? e->ctu_addr - e->pic->w_ctus + 1 : -1;
+  return (e->ctu_y > 0 && e->ctu_x < e->pic->w_ctus - 1) ? in_slice(e, e->ctu_addr - e->pic->w_ctus + 1) : -1;
 }
 static nb_t nb_none(void) { nb_t n = {NULL, 0, 0}; return n; }
 static nb_t nb_make(const hm_part *p, int idx) { nb_t n = {p, idx, 1}; return n; }
@@ -2509,6 +2514,13 @@ static hm_enc *enc_new(void) {
 
 void hvxo_hm_compress_ctu(const hvxo_hm_pic *pic, hvxo_hm_ctu_data *ctus, int16_t *const *rec, const int *rec_stride,
                           int ctu_addr, const hvxo_hm_coder *entry, const int16_t *int2n, hvxo_hm_coder *after_encode) {
+  hvxo_hm_compress_ctu_slice(pic, ctus, rec, rec_stride, ctu_addr, 0, pic->w_ctus * pic->h_ctus - 1, entry, int2n, NULL,
+                             after_encode);
+}
+
+void hvxo_hm_compress_ctu_slice(const hvxo_hm_pic *pic, hvxo_hm_ctu_data *ctus, int16_t *const *rec, const int *rec_stride,
+                                int ctu_addr, int slice_start, int slice_end, const hvxo_hm_coder *entry,
+                                const int16_t *int2n, int16_t *int2n_out, hvxo_hm_coder *after_encode) {
   tables_init();
   hm_enc *e = enc_new();
   e->pic = pic;
@@ -2518,6 +2530,8 @@ void hvxo_hm_compress_ctu(const hvxo_hm_pic *pic, hvxo_hm_ctu_data *ctus, int16_
   e->ctu_x = ctu_addr % pic->w_ctus;
   e->ctu_y = ctu_addr / pic->w_ctus;
   e->slice_qp = pic->qp;
+  e->slice_start = slice_start;
+  e->slice_end = slice_end;
   memcpy(e->int2n, int2n, sizeof(e->int2n));
   /* TComDataCU::initCtu (TComDataCU.cpp:434) of the picture's CTU and of the depth-0 best/temp CUs */
   hvxo_hm_ctu_data *d = &ctus[ctu_addr];
@@ -2546,9 +2560,10 @@ void hvxo_hm_compress_ctu(const hvxo_hm_pic *pic, hvxo_hm_ctu_data *ctus, int16_
     view.x = e->ctu_x * 64; view.y = e->ctu_y * 64; view.ctu = ctu_addr;
     memcpy(view.p, d->p, sizeof(d->p));
     memcpy(view.coef, d->coef, sizeof(d->coef));
-    encode_cu(e, &view, 0, 0, ctu_addr == pic->w_ctus * pic->h_ctus - 1);
+    encode_cu(e, &view, 0, 0, ctu_addr == slice_end);
     *after_encode = *e->cur;
   }
+  if (int2n_out) memcpy(int2n_out, e->int2n, sizeof(e->int2n));
   free(e);
 }
 
@@ -2586,7 +2601,7 @@ int hvxo_hm_replay_picture(const int32_t *pi, const double *pf, const uint8_t *o
                            const int32_t *refpic_poc, int n_refpics, const int16_t *col_field, const int32_t *entropy_bits,
                            const uint8_t *ctu_states, const int64_t *ctu_frac, const int16_t *ctu_int2n,
                            const int16_t *hm_parts, const int32_t *hm_coef, const uint8_t *hm_recon, int mode,
-                           int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost,
+                           int slice_ctus, int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost,
                            uint32_t *out_bits_dist, uint8_t *out_states, int64_t *out_frac) {
   (void)refpic_poc;
   tables_init();
@@ -2658,7 +2673,9 @@ int hvxo_hm_replay_picture(const int32_t *pi, const double *pf, const uint8_t *o
   hvxo_hm_coder prev;
   for (int a = 0; a < n; a++) {
     hvxo_hm_coder entry;
-    if (mode == 0 || a == 0) {
+    const int s0 = slice_ctus > 0 ? a - a % slice_ctus : 0;
+    const int s1 = slice_ctus > 0 ? (s0 + slice_ctus < n ? s0 + slice_ctus : n) - 1 : n - 1;
+    if (mode == 0 || a == s0) {
       memcpy(entry.st, ctu_states + (size_t)a * 202, 202);
       entry.frac = (uint64_t)ctu_frac[a];
     } else entry = prev;
@@ -2677,7 +2694,7 @@ int hvxo_hm_replay_picture(const int32_t *pi, const double *pf, const uint8_t *o
           for (int x = 0; x < 32; x++) recb[c][(ay * 32 + y) * rs[c] + ax * 32 + x] = rr[4096 + (c - 1) * 1024 + y * 32 + x];
     }
     hvxo_hm_coder after;
-    hvxo_hm_compress_ctu(&P, ctus, recb, rs, a, &entry, ctu_int2n + (size_t)a * 16, &after);
+    hvxo_hm_compress_ctu_slice(&P, ctus, recb, rs, a, s0, s1, &entry, ctu_int2n + (size_t)a * 16, NULL, &after);
     prev = after;
     if (out_states) memcpy(out_states + (size_t)a * 202, after.st, 202);
     if (out_frac) out_frac[a] = (int64_t)after.frac;

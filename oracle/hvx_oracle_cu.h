@@ -57,16 +57,24 @@ void hvxo_hm_pack_parts(hvxo_hm_ctu_data *d, const int16_t *in);
 void hvxo_hm_compress_ctu(const hvxo_hm_pic *pic, hvxo_hm_ctu_data *ctus, int16_t *const *rec, const int *rec_stride,
                           int ctu_addr, const hvxo_hm_coder *entry, const int16_t *int2n, hvxo_hm_coder *after_encode);
 
+/* The same for a CTU of a SliceMode=1 slice [slice_start, slice_end] (CTU addresses): neighbours
+ * before the slice are unavailable, the slice's last CTU ends without the end_of_slice bin;
+ * int2n_out (optional) receives m_integerMv2Nx2N after the decision (the next CTU's). */
+void hvxo_hm_compress_ctu_slice(const hvxo_hm_pic *pic, hvxo_hm_ctu_data *ctus, int16_t *const *rec, const int *rec_stride,
+                                int ctu_addr, int slice_start, int slice_end, const hvxo_hm_coder *entry,
+                                const int16_t *int2n, int16_t *int2n_out, hvxo_hm_coder *after_encode);
+
 /* Replay one captured picture (tests/golden/ctu_*.bin arrays, cu_capture.cpp layouts).
  * mode 0: every CTU from the reference's own entry state and its left/above CTUs' final data;
  * mode 1: the CTUs in raster order, each from the previous CTU's restated encodeCtu state.
+ * slice_ctus > 0: SliceMode=1 slices of that many CTUs (each slice starts from the captured state).
  * Outputs per CTU (n = pic's CTU count): parts [n][256][29], coef [n][6144], recon [n][6144],
  * cost [n], bits_dist [n][2], states/frac after encodeCtu [n][202] / [n]. */
 int hvxo_hm_replay_picture(const int32_t *pic_i32, const double *pic_f64, const uint8_t *org, const uint8_t *refpics,
                            const int32_t *refpic_poc, int n_refpics, const int16_t *col_field, const int32_t *entropy_bits,
                            const uint8_t *ctu_states, const int64_t *ctu_frac, const int16_t *ctu_int2n,
                            const int16_t *hm_parts, const int32_t *hm_coef, const uint8_t *hm_recon, int mode,
-                           int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost,
+                           int slice_ctus, int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost,
                            uint32_t *out_bits_dist, uint8_t *out_states, int64_t *out_frac);
 
 #ifdef __cplusplus

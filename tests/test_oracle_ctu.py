@@ -65,3 +65,14 @@ def test_ctx_init_states_vs_hm():
             starts = range(0, n, wc) if name == "ctu_ldp_slices.bin" else [0]
             for a in starts:
                 np.testing.assert_array_equal(g["ctu_states"][first + a], init[st, qp], err_msg=(name, pic, a))
+
+
+def test_ctu_slices_vs_hm():
+    """SliceMode=1 slices of one CTU row each (neighbours across the slice boundary unavailable,
+    no end_of_slice bin at a slice's last CTU): chained per slice from HM's slice-start state."""
+    g = _load("ctu_ldp_slices.bin")
+    wc = (int(g["pic_i32"][0][0]) + 63) // 64
+    for pic in range(g["pic_i32"].shape[0]):
+        out = hm_ctu.replay(g, pic, mode=1, slice_ctus=wc)
+        bad = hm_ctu.compare(g, pic, out, verbose=False, slice_ctus=wc)
+        assert not bad, (pic, bad[:3])
