@@ -1,17 +1,18 @@
 #!/usr/bin/env python3
-"""Benchmark: 64x64 CTUs/s of CU mode decision (ME + transform + RDOQ) on 2160p random YUV.
+"""Benchmark: 64x64 CTUs/s of HM-16.5rc1's CU mode decision on 2160p random YUV, bit-exact vs HM.
 
-One step = one 3840x2160 4:2:0 picture (2040 CTUs) through hvx_ctu_encode_yuv: for each of the 85
-CUs of every CTU, TZ integer + half/quarter motion search against 4 reference pictures, luma and
-chroma MC of the best reference, transform + RDOQ + dequant + inverse transform + SSE of every
-Y/Cb/Cr TU; then the CABAC coefficient rate of every TU, the residual and CU-quadtree RD decisions
-(chroma-weighted distortion), the reconstructed Y/Cb/Cr picture, and the reference picture
-(boundary strengths of the decided trees, deblocking, extended borders) -- DESIGN.md sections 3
-and 3a.  Inputs are resident in HBM before timing starts.
+One step = one launch of hvx_hm_compress (include/hvx.h) over every SliceMode=1 slice of P
+pictures in flight: a 3840x2160 4:2:0 picture has 34 CTU rows, each row a slice; with 22 pictures
+per GPU that is 748 slice chains, one wave each, and a step advances every chain by --ctus CTUs
+(default 1), each CTU TEncCu::compressCtu + encodeCtu exactly as HM decides it: merge/skip, AMVP
++ TZ search + fractional refinement against 4 references, 2NxN/Nx2N/AMP, the RQT with RDOQ and
+transform skip, intra-in-inter, the CABAC context carry.  The chains' CABAC
+state and CTU data stay in HBM between steps (HVX_HM_RESUME).  Inputs are resident in HBM before
+timing starts; each picture's reference frames are the previous synthetic frames.
 
-Multi-GPU (torch.distributed.run): one rank per GPU, each rank encodes its own independent GOP
-segment (different synthetic frames); the only collective is the per-picture gather of every
-rank's deblocked reference picture to rank 0's DPB (video_codecs_amd/dpb.py, RCCL over xGMI); weak scaling.
+Multi-GPU (torch.distributed.run): one rank per GPU, each rank decides its own pictures (different
+synthetic frames); per step every rank's reconstructed CTUs are gathered to rank 0's shared DPB
+(video_codecs_amd/dpb.py, RCCL over xGMI, asynchronous, double-buffered); weak scaling.
 
 Contract: python bench.py --gpus N --steps K --warmup W  -> one JSON line on rank 0.
 """
@@ -27,22 +28,30 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 MI355X_HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters
-# BASELINE.json's metric, worded for what this step proves: every CTU of the CPU sample is checked
-# bit-exactly against the oracle's composition of the step (oracle/hvx_oracle.c), whose pieces are
-# pinned to HM-16.5rc1 goldens; the step itself deviates from HM's full xCompressCU
-METRIC = "64\u00d764 CTUs/s (ME+transform+RDOQ) on 2160p YUV; bit-exact vs HM-pinned oracle (oracle/hvx_oracle.c)"
+METRIC = "64\u00d764 CTUs/s (ME+transform+RDOQ) on 2160p YUV, 1\u21928 MI355X; bit-exact vs HM"
+# the reduced step of rounds 1-2 (side measurement): bit-exact against its own HM-pinned restatement
+REDUCED_METRIC = "64\u00d764 CTUs/s (ME+transform+RDOQ) on 2160p YUV; bit-exact vs HM-pinned oracle (oracle/hvx_oracle.c)"
+# the bench picture: GOP position 2 of tests/hm_seam/ldp.cfg's LDP GOP at base QP 32 -> QP 34,
+# QPFactor 0.4624, GOP depth 1 (TEncSlice.cpp:320-374)
+HM_QP_OFFSET, HM_QP_FACTOR = 2, 0.4624
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--pics", type=int, default=22, help="P pictures in flight per GPU (34 slice chains each at 2160p)")
+    p.add_argument("--ctus", type=int, default=1, help="CTUs each slice chain advances per step")
+    p.add_argument("--cpu-ref-procs", type=int, default=0, help="HM TAppEncoder processes for the reference "
+                                                                  "baseline (0: the host's CPU share)")
+    p.add_argument("--no-cpu-ref", action="store_true", help="skip the reference HM timing")
+    p.add_argument("--no-reduced", action="store_true", help="skip the reduced-step side measurement")
     p.add_argument("--width", type=int, default=3840)
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--nref", type=int, default=4)
     p.add_argument("--qp", type=int, default=32)
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the reduced step's CPU sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-intra", action="store_true", help="skip the intra first-pass side measurement")
     p.add_argument("--no-ssim", action="store_true", help="skip the SSIM-RDO side measurement")
@@ -141,6 +150,214 @@ def aggregate(units_per_step, steps, world, elapsed):
     return units_per_step * steps * world / elapsed
 
 
+def yuv_split(flat, w, h):
+    """Planar Y | Cb | Cr bytes -> the three 2-D planes."""
+    ysz, csz = w * h, w * h // 4
+    return (flat[:ysz].reshape(h, w), flat[ysz:ysz + csz].reshape(h // 2, w // 2),
+            flat[ysz + csz:ysz + 2 * csz].reshape(h // 2, w // 2))
+
+
+def synthetic_col_field(nctu, seed):
+    """The collocated picture's motion field (hvx_hm_picture.col_field: per 16x16 block mode,
+    ref idx L0/L1, MV L0/L1): synthetic, seeded -- 70% inter blocks with an L0 reference 0-3 and a
+    quarter-sample MV within +-32 samples, 30% intra -- so the TMVP candidate (TComDataCU::
+    getColMVP) is exercised with scaling."""
+    rng = np.random.default_rng(seed)
+    f = np.zeros((nctu * 16, 8), np.int16)
+    inter = rng.random(nctu * 16) < 0.7
+    f[:, 0] = np.where(inter, 0, 1)
+    f[:, 1] = np.where(inter, rng.integers(0, 4, nctu * 16), -1)
+    f[:, 2] = -1
+    f[:, 3:5] = np.where(inter[:, None], rng.integers(-128, 129, (nctu * 16, 2)), 0)
+    return f
+
+
+class HmWorkload:
+    """The headline workload on one GPU: `pics` P pictures of W x H random 4:2:0 YUV, picture p
+    (POC nref + p) predicted from the nref previous frames, every CTU row a SliceMode=1 slice
+    decided by one chain (one wave); slice parameters of GOP position 2 of the LDP GOP
+    (hm.slice_params).  Step k advances every chain by `ctus` CTUs from where step k-1 left it
+    (HVX_HM_RESUME); a chain that reaches its row's end starts the row again as a new slice."""
+
+    def __init__(self, W, H, pics, nref, base_qp, ctus, rank):
+        import torch
+        from video_codecs_amd import _abi, hm, synth
+        self.W, self.H, self.pics, self.nref, self.ctus = W, H, pics, nref, ctus
+        self.wc, self.hc = (W + 63) // 64, (H + 63) // 64
+        assert self.wc % ctus == 0, "--ctus must divide the CTUs per row"
+        self.qp = base_qp + HM_QP_OFFSET
+        self.base = rank * (pics + nref) + 1000
+        self.params = hm.slice_params(1, self.qp, HM_QP_FACTOR)
+        eb = _abi.load_entropy_bits()
+        self.entry = _abi.load_ctx_init_states()[1, self.qp]
+        frames = [hm.DeviceFrame(yuv_split(synth.random_frame(W, H, self.base + i), W, H))
+                  for i in range(nref + pics)]
+        self.pictures = []
+        for p in range(pics):
+            self.pictures.append(hm.DevicePicture(frames[nref + p], [frames[nref + p - 1 - k] for k in range(nref)],
+                                                  self.picture_params(p), eb,
+                                                  col_field=synthetic_col_field(self.wc * self.hc, self.base + p)))
+        self.eng = hm.Engine(self.pictures)
+        self.n_jobs = pics * self.hc
+        self.eng.reserve(self.n_jobs)
+        self.slots = self.n_jobs * ctus
+        # one device job array per position in the row (the step's first CTU of every chain)
+        self.phase_jobs = []
+        for pos in range(0, self.wc, ctus):
+            j = np.zeros(self.n_jobs, hm.HM_JOB)
+            for p in range(pics):
+                for r in range(self.hc):
+                    k = p * self.hc + r
+                    j[k]["pic"], j[k]["first_ctu"], j[k]["n_ctus"], j[k]["chained"] = p, r * self.wc + pos, ctus, 1
+                    j[k]["out"] = k * ctus
+                    j[k]["slice_start"], j[k]["slice_end"] = r * self.wc, r * self.wc + self.wc - 1
+                    j[k]["flags"] = _abi.HM_RESUME if pos else 0
+                    j[k]["entry"]["st"] = self.entry
+            self.phase_jobs.append(torch.from_numpy(j.view(np.uint8).reshape(-1).copy()).cuda())
+        self.out_ctu = torch.zeros(self.slots * hm.HM_CTU.itemsize, dtype=torch.uint8, device="cuda")
+        self.step_idx = 0
+        # picture 0's chains (slots 0 .. hc*ctus-1): every step's CTU records + reconstruction
+        # kept for the parity check against the oracle after the timed region
+        self.keep_steps = []
+        self.keep_n = self.hc * ctus
+
+    def picture_params(self, p):
+        poc, nref = self.nref + p, self.nref
+        q = dict(self.params)
+        q.update(poc=poc, nref=[nref, 0], ref_poc=np.array([[poc - 1 - k for k in range(4)], [0] * 4]),
+                 ref_plane=np.array([list(range(nref)) + [0] * (4 - nref), [0] * 4]), max_merge=5, tmvp=1, check_ldc=1,
+                 col_from_l0=1, col_valid=1, col_poc=poc - 1,
+                 col_ref_poc=np.array([[poc - 2 - k for k in range(4)], [0] * 4]), search_range=64, amp=1)
+        return q
+
+    def step(self, out_rec, events=None):
+        """One launch: every chain advances `ctus` CTUs; reconstructed CTUs go to out_rec."""
+        pos = self.step_idx % len(self.phase_jobs)
+        if events is not None:
+            events[0].record()
+        self.eng.launch(self.phase_jobs[pos], self.n_jobs, self.out_ctu, out_rec)
+        if events is not None:
+            events[1].record()
+        self.keep_steps.append((pos * self.ctus, self.out_ctu[:self.keep_n * 22544].clone(),
+                                out_rec[:self.keep_n * 6144].clone()))
+        self.step_idx += 1
+
+    def host_inputs(self, p):
+        """Picture p's arrays in the oracle's (cu_capture.cpp) layout: pic_i32, pic_f64, org,
+        reference frames, collocated field."""
+        from video_codecs_amd import synth
+        prm = self.picture_params(p)
+        pi = np.zeros(46, np.int32)
+        pi[0:7] = [self.W, self.H, prm["poc"], 1, self.qp, self.nref, 0]
+        pi[7:11] = prm["ref_poc"][0]
+        pi[15:19] = prm["ref_plane"][0]
+        pi[19:23] = -1
+        pi[23:29] = [1, 0, 1, 1, 5, prm["col_poc"]]
+        pi[29:31] = [4, 0]
+        pi[31:35] = prm["col_ref_poc"][0]
+        pi[39:41] = prm["chroma_qp"]
+        pi[41:43] = [0, self.wc * self.hc]
+        pi[43] = np.array(prm["lambda_motion"], np.uint32).view(np.int32)
+        pi[45] = 1
+        pf = np.array([prm["lambda"], prm["sqrt_lambda"], *prm["chroma_weight"], *prm["tq_lambda"]], np.float64)
+        org = synth.random_frame(self.W, self.H, self.base + self.nref + p)
+        refs = np.concatenate([synth.random_frame(self.W, self.H, self.base + self.nref + p - 1 - k)
+                               for k in range(self.nref)])
+        return pi, pf, org, refs, synthetic_col_field(self.wc * self.hc, self.base + p)
+
+
+def hm_cpu_port(work, threads, min_seconds=0.0):
+    """The oracle's restatement (oracle/hvx_oracle_cu.c hvxo_hm_chains) on picture 0's slice
+    chains -- the same CTUs the GPU decided in its warmup + timed steps, on `threads` host threads
+    -- and the bit-exact comparison of every one of them with the GPU's records."""
+    import oracle  # noqa: F401  (test infrastructure: the checker and the port baseline)
+    from oracle import hm_ctu
+    from video_codecs_amd import hm
+    pi, pf, org, refs, col = work.host_inputs(0)
+    wc, hc = work.wc, work.hc
+    done = min(work.step_idx * work.ctus, wc)  # CTUs of each row decided by the GPU (first pass)
+    chain_first = np.arange(hc, dtype=np.int32) * wc
+    hm_ctu.chains(pi, pf, org, refs, work.entry, chain_first[:1], 1, wc, threads=1, col_field=col)  # tables
+    t0 = time.perf_counter()
+    out = hm_ctu.chains(pi, pf, org, refs, work.entry, chain_first, done, wc, threads=threads, col_field=col)
+    dt = time.perf_counter() - t0
+    n = hc * done
+    # the GPU's records of the same CTUs: step s decided row position keep_steps[s][0] ..
+    dev_parts = np.zeros((hc, done, 256, 29), np.int16)
+    dev_coef = np.zeros((hc, done, 6144), np.int16)
+    dev_rec = np.zeros((hc, done, 6144), np.uint8)
+    dev_cost = np.zeros((hc, done), np.float64)
+    dev_bd = np.zeros((hc, done, 2), np.uint32)
+    seen = np.zeros(done, bool)
+    for pos, ct, rc in work.keep_steps:
+        if pos >= done or seen[pos]:
+            continue
+        c = ct.cpu().numpy().view(hm.HM_CTU).reshape(hc, work.ctus)
+        r = rc.cpu().numpy().reshape(hc, work.ctus, 6144)
+        for i in range(work.ctus):
+            if pos + i < done:
+                dev_parts[:, pos + i] = hm.unpack_parts(c[:, i]["p"])
+                dev_coef[:, pos + i] = c[:, i]["coef"]
+                dev_rec[:, pos + i] = r[:, i]
+                dev_cost[:, pos + i] = c[:, i]["cost"]
+                dev_bd[:, pos + i, 0], dev_bd[:, pos + i, 1] = c[:, i]["bits"], c[:, i]["dist"]
+                seen[pos + i] = True
+    mism = 0
+    for k in range(hc):
+        for i in range(done):
+            o = k * done + i
+            same = (np.array_equal(out["parts"][o], dev_parts[k, i]) and
+                    np.array_equal(out["coef"][o].astype(np.int16), dev_coef[k, i]) and
+                    np.array_equal(out["recon"][o], dev_rec[k, i]) and out["cost"][o] == dev_cost[k, i] and
+                    np.array_equal(out["bits_dist"][o], dev_bd[k, i]))
+            mism += 0 if same else 1
+    return {"value": round(n / dt, 3), "unit": "CTUs/s", "cores": threads, "kind": "port",
+            "sample": f"picture 0's {hc} slice chains x {done} CTUs ({n} CTUs) through oracle/hvx_oracle_cu.c "
+                      f"hvxo_hm_chains on {threads} host threads, {dt:.1f} s",
+            "gpu_parity_ctus": n, "gpu_parity_mismatches": mism}
+
+
+def hm_cpu_reference(procs, tmpdir):
+    """HM-16.5rc1's own TAppEncoder (oracle/_ref, built from /root/reference by oracle/Makefile)
+    on the host cores: `procs` concurrent single-threaded encodes of 416x240 random 4:2:0 YUV
+    (the bench's synthetic recipe) with oracle/hm_ref_bench.cfg -- the bench picture's slice
+    parameters (LDP P, QP 34, QPFactor 0.4624, RDOQ, AMP, FEN, TZ SR 64, row slices).  P-picture
+    CTUs/s = procs x 3 x 28 CTUs / (mean wall time of the 4-frame encode - that of the
+    1-frame, I-only encode)."""
+    import subprocess
+    from video_codecs_amd import synth
+    exe = os.path.join(ROOT, "oracle", "_ref", "TAppEncoder")
+    cfg = os.path.join(ROOT, "oracle", "hm_ref_bench.cfg")
+    if not os.path.exists(exe):
+        return None
+    yuv = os.path.join(tmpdir, "hvx_hm_ref.yuv")
+    with open(yuv, "wb") as f:
+        for i in range(4):
+            f.write(synth.random_frame(416, 240, 5000 + i).tobytes())
+
+    def batch(frames):
+        t0 = time.perf_counter()
+        ps = [subprocess.Popen([exe, "-c", cfg, "-i", yuv, "-wdt", "416", "-hgt", "240", "-fr", "30", "-f", str(frames),
+                                "-b", os.path.join(tmpdir, f"hvx_hm_ref{k}.bin"), "-o", "/dev/null"],
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL) for k in range(procs)]
+        ends = []
+        for p in ps:
+            p.wait()
+            ends.append(time.perf_counter() - t0)
+            if p.returncode != 0:
+                raise RuntimeError("TAppEncoder failed")
+        return float(np.mean(ends))
+
+    t1, t4 = batch(1), batch(4)
+    p_ctus = 3 * 28
+    per_ctu = (t4 - t1) / p_ctus
+    return {"value": round(procs / per_ctu, 3), "unit": "CTUs/s", "cores": procs, "kind": "reference",
+            "sample": f"{procs} concurrent TAppEncoder (HM-16.5rc1, oracle/_ref) encodes of 416x240 random YUV, "
+                      f"oracle/hm_ref_bench.cfg: 3 P pictures x 28 CTUs each (QP 34, 1-3 refs); "
+                      f"{t4:.1f} s (4 frames) - {t1:.1f} s (I only) per encode",
+            "s_per_ctu_per_core": round(per_ctu, 4)}
+
+
 def main():
     args = parse()
     import torch
@@ -152,7 +369,105 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local_rank)
+    from video_codecs_amd import hvx
+    from video_codecs_amd.dpb import DpbGather
 
+    W, H, nref = args.width, args.height, args.nref
+    hvx.context()
+    work = HmWorkload(W, H, args.pics, nref, args.qp, args.ctus, rank)
+    dpb = DpbGather(world, rank, (work.slots * 6144,), "cuda")
+    events = []
+
+    def step():
+        ev = None
+        if timing[0]:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            events.append(ev)
+        work.step(dpb.buffer(), ev)
+        dpb.send()
+
+    def sync():
+        dpb.drain()
+        torch.cuda.synchronize()
+
+    timing = [False]
+    elapsed = timed_steps(step, args.steps, args.warmup, world, "cuda", sync,
+                          before=lambda: timing.__setitem__(0, True))
+    timing[0] = False
+    launch_ms = sum(a.elapsed_time(b) for a, b in events) / max(1, len(events))
+    own, gathered = dpb.last()
+    dpb_ok = None
+    if gathered is not None:
+        dpb_ok = bool(torch.equal(gathered[0], own))
+    reduced = None
+    if not args.no_reduced:
+        reduced = reduced_step(args, rank, world, with_sides=(world == 1))
+    if rank == 0:
+        units = work.n_jobs * args.ctus
+        value = aggregate(units, args.steps, world, elapsed)
+        bpc = b_ctu(nref)
+        bytes_per_launch = bpc * units
+        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        traffic = None
+        tr_path = os.path.join(ROOT, "profiles", "hbm_traffic_r03.json")  # PMC passes of this round's tree
+        if os.path.exists(tr_path):
+            tr = json.load(open(tr_path)).get("k_hm_compress")
+            if tr:
+                traffic = tr["bytes_per_launch"] * units / tr.get("ctus_per_launch", units)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "CTUs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: splitmix64 uniform random 8-bit 4:2:0 YUV (BASELINE.md sec. 3), the previous 4 frames "
+                    "as references, seeded synthetic collocated motion field; own pictures per rank",
+            "config": {"workload": "HM-16.5rc1 TEncCu::compressCtu + encodeCtu, bit-exact: merge/skip, AMVP+TMVP, TZ "
+                                   "SR64 + frac ME vs %d refs, 2NxN/Nx2N/AMP, RQT + RDOQ + transform skip, "
+                                   "intra-in-inter, CABAC context carry; SliceMode=1 row slices" % nref,
+                       "resolution": f"{W}x{H}", "ctus_per_frame": work.wc * work.hc, "pictures_per_gpu": args.pics,
+                       "slice_chains_per_gpu": work.n_jobs, "ctus_per_chain_per_step": args.ctus,
+                       "slice": "P, QP %d (base %d + GOP offset %d), QPFactor %g, lambda %.6f" % (
+                           work.qp, args.qp, HM_QP_OFFSET, HM_QP_FACTOR, work.params["lambda"]),
+                       "n_ref": nref, "parallelism": f"pictures x{world}",
+                       "dpb": "gather of every rank's reconstructed CTUs to rank 0 per step" if world > 1 else "local"},
+            # priced against HBM (integer work); the limiter is the serial RD decision
+            # chain inside each wave (latency), not bandwidth -- frac << 1
+            "roofline": {"bound": "hbm", "limiter": "latency", "kernel": "k_hm_compress",
+                         "achieved": round(achieved, 4), "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / MI355X_HBM_PEAK_GBS, "traffic": traffic,
+                         "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(launch_ms, 3), "b_ctu": bpc},
+            "cpu_baseline": None,
+        }
+        if dpb_ok is not None:
+            out["dpb_gather_ok"] = dpb_ok
+        if world == 1:
+            threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
+            if not args.no_cpu_ref:
+                out["cpu_baseline"] = hm_cpu_reference(args.cpu_ref_procs or threads,
+                                                       os.environ.get("TMPDIR", "/tmp"))
+            if not args.no_cpu:
+                port = hm_cpu_port(work, threads)
+                out["cpu_port"] = port
+                if out["cpu_baseline"] is None:
+                    out["cpu_baseline"] = port
+        if reduced is not None:
+            out["reduced_step"] = reduced
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def reduced_step(args, rank, world, with_sides):
+    """The reduced picture step of rounds 1-2 (hvx_ctu_encode_yuv, DESIGN.md sections 3-3a): its
+    measurement dict, CPU sample (with_sides) and side measurements; timed like the headline."""
+    import torch
     from video_codecs_amd import _abi, hvx
     from video_codecs_amd.dpb import DpbGather
 
@@ -209,7 +524,7 @@ def main():
                 traffic = tr["bytes_per_launch"]
         step_s = elapsed / args.steps
         out = {
-            "metric": METRIC,
+            "metric": REDUCED_METRIC,
             "value": round(value, 2),
             "unit": "CTUs/s",
             "n_gpus": world,
@@ -242,22 +557,21 @@ def main():
         }
         if dpb_ok is not None:
             out["dpb_gather_ok"] = dpb_ok
-        if world == 1 and not args.no_cpu:
+        if with_sides and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(inp.host, an, gpu_res, gpu_dec, gpu_rec, gpu_refpic, args)
-        if world == 1 and not args.no_1080p:  # side measurements: single-GPU runs only
+        if with_sides and not args.no_1080p:
             out["step_1080p"] = step_1080p_measure(nref, args.qp, args.steps)
-        if world == 1 and not args.no_ssim:
+        if with_sides and not args.no_ssim:
             out["ssim_rdo"] = ssim_rdo_measure(inp, W, H, nref, args.steps)
-        if world == 1 and not args.no_sao:
+        if with_sides and not args.no_sao:
             out["sao"] = sao_measure(W, H, args.steps)
-        if world == 1 and not args.no_cabac:
+        if with_sides and not args.no_cabac:
             out["cabac_write"] = cabac_write_measure(args.steps)
-        if world == 1 and not args.no_intra:
+        if with_sides and not args.no_intra:
             out["intra_first_pass"] = intra_measure(cur_t, inp.refs[0][0], W, H, float(an.params["lambda"][0]),
                                                     args.steps)
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        return out
+    return None
 
 
 def step_1080p_measure(nref, qp, steps):

@@ -370,10 +370,13 @@ typedef struct hvx_hm_picture {
 typedef struct hvx_hm_job {
   int32_t pic, first_ctu, n_ctus, chained, out;
   int32_t slice_start, slice_end;  /* the slice holding the chain: first / last CTU address (raster) */
-  int32_t debug_;                  /* 0 (debugging builds: stop stage) */
+  int32_t flags;                   /* HVX_HM_RESUME; bits 8..15: 0 (debugging builds: stop stage) */
   hvx_hm_coder entry;
   int16_t int2n[16];
 } hvx_hm_job;
+/* hvx_hm_job.flags: continue the chain of the previous launch with the same job index -- the entry
+ * coder and m_integerMv2Nx2N come from that job's state (d_state), not from entry / int2n */
+#define HVX_HM_RESUME 1
 
 #ifdef __cplusplus
 }

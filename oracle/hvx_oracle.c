@@ -94,6 +94,8 @@ static void init_tables(void) {
       }
   g_tables_ready = 1;
 }
+/* the lazily built scan tables, once, before threads share the oracle */
+void hvxo_init_tables(void) { init_tables(); }
 
 const uint32_t *hvxo_scan(int grouped, int scan_type, int log2w, int log2h) {
   init_tables();

@@ -138,6 +138,8 @@ void hvxo_ctu_bs(const hvx_cu_result *cu, const hvx_cu_decision *dec, int pic_w,
 void hvxo_dct_matrix(int n, int16_t *m /* n*n, [k][x] */);
 const uint32_t *hvxo_scan(int grouped, int scan_type, int log2w, int log2h);
 
+void hvxo_init_tables(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2597,6 +2597,82 @@ static void pad_plane8(const uint8_t *src, int w, int h, int m, uint8_t *dst, in
   }
 }
 
+/* the picture the cu_capture.cpp arrays describe: parameters, 16-bit originals, padded references */
+typedef struct {
+  hvxo_hm_pic P;
+  int16_t *org16[3];
+  int16_t **planes16, **bufs16;
+  uint8_t **planes8, **bufs8;
+  int n_refpics;
+} pic_buf;
+static void pic_setup(pic_buf *B, const int32_t *pi, const double *pf, const uint8_t *org, const uint8_t *refpics, int n_refpics,
+                      const int16_t *col_field, const int32_t *entropy_bits) {
+  memset(B, 0, sizeof(*B));
+  B->n_refpics = n_refpics;
+  const int w = pi[P_W], h = pi[P_H], wc = (w + 63) / 64, hc = (h + 63) / 64;
+  const int M = 80, MC = 40;
+  B->P.w = w; B->P.h = h; B->P.w_ctus = wc; B->P.h_ctus = hc;
+  B->P.poc = pi[P_POC]; B->P.slice_type = pi[P_SLICE_TYPE]; B->P.qp = pi[P_QP];
+  B->P.nref[0] = pi[P_NREF0]; B->P.nref[1] = pi[P_NREF1];
+  for (int l = 0; l < 2; l++)
+    for (int i = 0; i < 4; i++) {
+      B->P.ref_poc[l][i] = pi[(l ? P_REFPOC1 : P_REFPOC0) + i];
+      B->P.ref_plane_idx[l][i] = pi[(l ? P_REFPIC1 : P_REFPIC0) + i];
+      B->P.col_ref_poc[l][i] = pi[(l ? P_COL_REFPOC1 : P_COL_REFPOC0) + i];
+    }
+  B->P.chroma_qp[0] = pi[P_CHROMA_QP_CB]; B->P.chroma_qp[1] = pi[P_CHROMA_QP_CR];
+  B->P.max_merge = pi[P_MAX_MERGE]; B->P.tmvp = pi[P_TMVP]; B->P.check_ldc = pi[P_CHECK_LDC];
+  B->P.col_from_l0 = pi[P_COL_FROM_L0]; B->P.col_valid = pi[P_COL_VALID]; B->P.col_poc = pi[P_COL_POC];
+  B->P.col_field = col_field;
+  B->P.lambda = pf[F_LAMBDA]; B->P.sqrt_lambda = pf[F_SQRT_LAMBDA];
+  B->P.chroma_weight[0] = pf[F_WEIGHT_CB]; B->P.chroma_weight[1] = pf[F_WEIGHT_CR];
+  B->P.tq_lambda[0] = pf[F_TQ_LAMBDA_Y]; B->P.tq_lambda[1] = pf[F_TQ_LAMBDA_CB]; B->P.tq_lambda[2] = pf[F_TQ_LAMBDA_CR];
+  B->P.lambda_motion = (uint32_t)pi[P_LAMBDA_MOTION];
+  B->P.search_range = 64;
+  B->P.amp = 1;
+  B->P.entropy_bits = entropy_bits;
+  /* original planes */
+  const size_t ysz = (size_t)w * h, csz = ysz / 4;
+  for (int c = 0; c < 3; c++) {
+    const size_t sz = c ? csz : ysz;
+    B->org16[c] = (int16_t *)malloc(sizeof(int16_t) * sz);
+    const uint8_t *s8 = org + (c == 0 ? 0 : c == 1 ? ysz : ysz + csz);
+    for (size_t i = 0; i < sz; i++) B->org16[c][i] = s8[i];
+    B->P.org[c] = B->org16[c];
+    B->P.org_stride[c] = c ? w / 2 : w;
+  }
+  B->P.org8 = org;
+  B->P.org8_stride = w;
+  /* reference planes, padded */
+  const int s16y = w + 2 * M, s16c = w / 2 + 2 * MC;
+  B->planes16 = (int16_t **)calloc((size_t)3 * (n_refpics ? n_refpics : 1), sizeof(int16_t *));
+  B->planes8 = (uint8_t **)calloc((size_t)(n_refpics ? n_refpics : 1), sizeof(uint8_t *));
+  B->bufs16 = (int16_t **)calloc((size_t)3 * (n_refpics ? n_refpics : 1), sizeof(int16_t *));
+  B->bufs8 = (uint8_t **)calloc((size_t)(n_refpics ? n_refpics : 1), sizeof(uint8_t *));
+  for (int r = 0; r < n_refpics; r++) {
+    const uint8_t *base = refpics + (size_t)r * (ysz + 2 * csz);
+    for (int c = 0; c < 3; c++) {
+      const int cw = c ? w / 2 : w, ch = c ? h / 2 : h, m = c ? MC : M, st = c ? s16c : s16y;
+      B->bufs16[3 * r + c] = (int16_t *)malloc(sizeof(int16_t) * (size_t)st * (ch + 2 * m));
+      pad_plane16(base + (c == 0 ? 0 : c == 1 ? ysz : ysz + csz), cw, ch, m, B->bufs16[3 * r + c], st);
+      B->planes16[3 * r + c] = B->bufs16[3 * r + c] + m * st + m;
+    }
+    B->bufs8[r] = (uint8_t *)malloc((size_t)s16y * (h + 2 * M));
+    pad_plane8(base, w, h, M, B->bufs8[r], s16y);
+    B->planes8[r] = B->bufs8[r] + M * s16y + M;
+  }
+  B->P.ref_planes16 = (const int16_t *const *)B->planes16;
+  B->P.ref_stride16[0] = s16y; B->P.ref_stride16[1] = s16c;
+  B->P.ref_planes8 = (const uint8_t *const *)B->planes8;
+  B->P.ref_stride8 = s16y;
+}
+static void pic_free(pic_buf *B) {
+  for (int c = 0; c < 3; c++) free(B->org16[c]);
+  for (int r = 0; r < 3 * B->n_refpics; r++) free(B->bufs16[r]);
+  for (int r = 0; r < B->n_refpics; r++) free(B->bufs8[r]);
+  free(B->planes16); free(B->planes8); free(B->bufs16); free(B->bufs8);
+}
+
 int hvxo_hm_replay_picture(const int32_t *pi, const double *pf, const uint8_t *org, const uint8_t *refpics,
                            const int32_t *refpic_poc, int n_refpics, const int16_t *col_field, const int32_t *entropy_bits,
                            const uint8_t *ctu_states, const int64_t *ctu_frac, const int16_t *ctu_int2n,
@@ -2606,64 +2682,9 @@ int hvxo_hm_replay_picture(const int32_t *pi, const double *pf, const uint8_t *o
   (void)refpic_poc;
   tables_init();
   const int w = pi[P_W], h = pi[P_H], wc = (w + 63) / 64, hc = (h + 63) / 64, n = wc * hc;
-  const int M = 80, MC = 40;
-  hvxo_hm_pic P;
-  memset(&P, 0, sizeof(P));
-  P.w = w; P.h = h; P.w_ctus = wc; P.h_ctus = hc;
-  P.poc = pi[P_POC]; P.slice_type = pi[P_SLICE_TYPE]; P.qp = pi[P_QP];
-  P.nref[0] = pi[P_NREF0]; P.nref[1] = pi[P_NREF1];
-  for (int l = 0; l < 2; l++)
-    for (int i = 0; i < 4; i++) {
-      P.ref_poc[l][i] = pi[(l ? P_REFPOC1 : P_REFPOC0) + i];
-      P.ref_plane_idx[l][i] = pi[(l ? P_REFPIC1 : P_REFPIC0) + i];
-      P.col_ref_poc[l][i] = pi[(l ? P_COL_REFPOC1 : P_COL_REFPOC0) + i];
-    }
-  P.chroma_qp[0] = pi[P_CHROMA_QP_CB]; P.chroma_qp[1] = pi[P_CHROMA_QP_CR];
-  P.max_merge = pi[P_MAX_MERGE]; P.tmvp = pi[P_TMVP]; P.check_ldc = pi[P_CHECK_LDC];
-  P.col_from_l0 = pi[P_COL_FROM_L0]; P.col_valid = pi[P_COL_VALID]; P.col_poc = pi[P_COL_POC];
-  P.col_field = col_field;
-  P.lambda = pf[F_LAMBDA]; P.sqrt_lambda = pf[F_SQRT_LAMBDA];
-  P.chroma_weight[0] = pf[F_WEIGHT_CB]; P.chroma_weight[1] = pf[F_WEIGHT_CR];
-  P.tq_lambda[0] = pf[F_TQ_LAMBDA_Y]; P.tq_lambda[1] = pf[F_TQ_LAMBDA_CB]; P.tq_lambda[2] = pf[F_TQ_LAMBDA_CR];
-  P.lambda_motion = (uint32_t)pi[P_LAMBDA_MOTION];
-  P.search_range = 64;
-  P.amp = 1;
-  P.entropy_bits = entropy_bits;
-  /* original planes */
-  const size_t ysz = (size_t)w * h, csz = ysz / 4;
-  int16_t *org16[3];
-  for (int c = 0; c < 3; c++) {
-    const size_t sz = c ? csz : ysz;
-    org16[c] = (int16_t *)malloc(sizeof(int16_t) * sz);
-    const uint8_t *s8 = org + (c == 0 ? 0 : c == 1 ? ysz : ysz + csz);
-    for (size_t i = 0; i < sz; i++) org16[c][i] = s8[i];
-    P.org[c] = org16[c];
-    P.org_stride[c] = c ? w / 2 : w;
-  }
-  P.org8 = org;
-  P.org8_stride = w;
-  /* reference planes, padded */
-  const int s16y = w + 2 * M, s16c = w / 2 + 2 * MC;
-  int16_t **planes16 = (int16_t **)calloc((size_t)3 * (n_refpics ? n_refpics : 1), sizeof(int16_t *));
-  uint8_t **planes8 = (uint8_t **)calloc((size_t)(n_refpics ? n_refpics : 1), sizeof(uint8_t *));
-  int16_t **bufs16 = (int16_t **)calloc((size_t)3 * (n_refpics ? n_refpics : 1), sizeof(int16_t *));
-  uint8_t **bufs8 = (uint8_t **)calloc((size_t)(n_refpics ? n_refpics : 1), sizeof(uint8_t *));
-  for (int r = 0; r < n_refpics; r++) {
-    const uint8_t *base = refpics + (size_t)r * (ysz + 2 * csz);
-    for (int c = 0; c < 3; c++) {
-      const int cw = c ? w / 2 : w, ch = c ? h / 2 : h, m = c ? MC : M, st = c ? s16c : s16y;
-      bufs16[3 * r + c] = (int16_t *)malloc(sizeof(int16_t) * (size_t)st * (ch + 2 * m));
-      pad_plane16(base + (c == 0 ? 0 : c == 1 ? ysz : ysz + csz), cw, ch, m, bufs16[3 * r + c], st);
-      planes16[3 * r + c] = bufs16[3 * r + c] + m * st + m;
-    }
-    bufs8[r] = (uint8_t *)malloc((size_t)s16y * (h + 2 * M));
-    pad_plane8(base, w, h, M, bufs8[r], s16y);
-    planes8[r] = bufs8[r] + M * s16y + M;
-  }
-  P.ref_planes16 = (const int16_t *const *)planes16;
-  P.ref_stride16[0] = s16y; P.ref_stride16[1] = s16c;
-  P.ref_planes8 = (const uint8_t *const *)planes8;
-  P.ref_stride8 = s16y;
+  pic_buf B;
+  pic_setup(&B, pi, pf, org, refpics, n_refpics, col_field, entropy_bits);
+  const hvxo_hm_pic P = B.P;
   /* the picture's CTU data and reconstruction (whole CTUs) */
   hvxo_hm_ctu_data *ctus = (hvxo_hm_ctu_data *)calloc((size_t)n, sizeof(hvxo_hm_ctu_data));
   const int rw = wc * 64, rh = hc * 64;
@@ -2721,12 +2742,117 @@ int hvxo_hm_replay_picture(const int32_t *pi, const double *pf, const uint8_t *o
                                                         : 0;
     }
   }
-  for (int c = 0; c < 3; c++) { free(recb[c]); free(org16[c]); }
-  for (int r = 0; r < 3 * n_refpics; r++) free(bufs16[r]);
-  for (int r = 0; r < n_refpics; r++) free(bufs8[r]);
-  free(planes16); free(planes8); free(bufs16); free(bufs8);
+  for (int c = 0; c < 3; c++) free(recb[c]);
+  pic_free(&B);
   free(ctus);
   return n;
+}
+
+/* ============================================================================================
+ * Independent slice chains (the bench's HM-exact workload): SliceMode=1 slices, each chain the
+ * first ctus_per_chain CTUs of its slice from the slice-start state, chains spread over threads
+ * ========================================================================================== */
+#include <pthread.h>
+typedef struct {
+  const hvxo_hm_pic *P;
+  hvxo_hm_ctu_data *ctus;
+  int16_t **rec;
+  const int *rs;
+  const int32_t *chain_first;
+  int n_chains, per_chain, slice_ctus, n;
+  const uint8_t *entry_states;
+  int16_t *out_parts;
+  int32_t *out_coef;
+  uint8_t *out_recon;
+  double *out_cost;
+  uint32_t *out_bits_dist;
+  int next;
+  pthread_mutex_t lock;
+} chain_job;
+
+static void chain_run(chain_job *J, int k) {
+  const hvxo_hm_pic *P = J->P;
+  const int first = J->chain_first[k];
+  const int s0 = first - first % J->slice_ctus;
+  const int s1 = (s0 + J->slice_ctus < J->n ? s0 + J->slice_ctus : J->n) - 1;
+  hvxo_hm_coder cur;
+  memset(&cur, 0, sizeof(cur));
+  memcpy(cur.st, J->entry_states, 202);
+  int16_t int2n[16], next2n[16];
+  memset(int2n, 0, sizeof(int2n));
+  for (int i = 0; i < J->per_chain; i++) {
+    const int a = first + i;
+    hvxo_hm_coder after;
+    hvxo_hm_compress_ctu_slice(P, J->ctus, J->rec, J->rs, a, s0, s1, &cur, int2n, next2n, &after);
+    cur = after;
+    memcpy(int2n, next2n, sizeof(int2n));
+    const size_t o = (size_t)k * J->per_chain + i;
+    hvxo_hm_ctu_data *q = &J->ctus[a];
+    hvxo_hm_unpack_parts(q, J->out_parts + o * 256 * HVXO_HM_PART_FIELDS);
+    memcpy(J->out_coef + o * 6144, q->coef[0], sizeof(int32_t) * 4096);
+    memcpy(J->out_coef + o * 6144 + 4096, q->coef[1], sizeof(int32_t) * 1024);
+    memcpy(J->out_coef + o * 6144 + 5120, q->coef[2], sizeof(int32_t) * 1024);
+    J->out_cost[o] = q->cost;
+    J->out_bits_dist[2 * o] = q->bits;
+    J->out_bits_dist[2 * o + 1] = q->dist;
+    const int ax = a % P->w_ctus, ay = a / P->w_ctus;
+    uint8_t *r = J->out_recon + o * 6144;
+    for (int c = 0; c < 3; c++) {
+      const int s = c ? 1 : 0, cs = 64 >> s, W = P->w >> s, H = P->h >> s;
+      for (int y = 0; y < cs; y++)
+        for (int x = 0; x < cs; x++)
+          r[(c ? 4096 + (c - 1) * 1024 : 0) + y * cs + x] =
+              (ax * cs + x < W && ay * cs + y < H) ? (uint8_t)J->rec[c][(ay * cs + y) * J->rs[c] + ax * cs + x] : 0;
+    }
+  }
+}
+static void *chain_worker(void *arg) {
+  chain_job *J = (chain_job *)arg;
+  for (;;) {
+    pthread_mutex_lock(&J->lock);
+    const int k = J->next++;
+    pthread_mutex_unlock(&J->lock);
+    if (k >= J->n_chains) return NULL;
+    chain_run(J, k);
+  }
+}
+
+int hvxo_hm_chains(const int32_t *pi, const double *pf, const uint8_t *org, const uint8_t *refpics, int n_refpics,
+                   const int16_t *col_field, const int32_t *entropy_bits, const uint8_t *entry_states, int n_chains,
+                   const int32_t *chain_first, int ctus_per_chain, int slice_ctus, int n_threads, int16_t *out_parts,
+                   int32_t *out_coef, uint8_t *out_recon, double *out_cost, uint32_t *out_bits_dist) {
+  tables_init();
+  hvxo_init_tables();
+  if (pi[P_COL_VALID] && !col_field) return -1;
+  const int w = pi[P_W], h = pi[P_H], wc = (w + 63) / 64, hc = (h + 63) / 64, n = wc * hc;
+  for (int k = 0; k < n_chains; k++)
+    if (slice_ctus < 1 || chain_first[k] < 0 || chain_first[k] + ctus_per_chain > n ||
+        chain_first[k] % slice_ctus + ctus_per_chain > slice_ctus)
+      return -1;
+  pic_buf B;
+  pic_setup(&B, pi, pf, org, refpics, n_refpics, col_field, entropy_bits);
+  hvxo_hm_ctu_data *ctus = (hvxo_hm_ctu_data *)calloc((size_t)n, sizeof(hvxo_hm_ctu_data));
+  const int rw = wc * 64, rh = hc * 64;
+  int16_t *recb[3];
+  int rs[3] = {rw, rw / 2, rw / 2};
+  for (int c = 0; c < 3; c++) recb[c] = (int16_t *)calloc((size_t)(c ? rw * rh / 4 : rw * rh), sizeof(int16_t));
+  chain_job J;
+  memset(&J, 0, sizeof(J));
+  J.P = &B.P; J.ctus = ctus; J.rec = recb; J.rs = rs; J.chain_first = chain_first;
+  J.n_chains = n_chains; J.per_chain = ctus_per_chain; J.slice_ctus = slice_ctus; J.n = n;
+  J.entry_states = entry_states; J.out_parts = out_parts; J.out_coef = out_coef; J.out_recon = out_recon;
+  J.out_cost = out_cost; J.out_bits_dist = out_bits_dist;
+  pthread_mutex_init(&J.lock, NULL);
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 64) n_threads = 64;
+  pthread_t th[64];
+  for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, chain_worker, &J);
+  for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  pthread_mutex_destroy(&J.lock);
+  for (int c = 0; c < 3; c++) free(recb[c]);
+  pic_free(&B);
+  free(ctus);
+  return n_chains * ctus_per_chain;
 }
 
 void hvxo_hm_unpack_parts(const hvxo_hm_ctu_data *d, int16_t *out /* [256][HVXO_HM_PART_FIELDS] */) {

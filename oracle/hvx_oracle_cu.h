@@ -77,6 +77,15 @@ int hvxo_hm_replay_picture(const int32_t *pic_i32, const double *pic_f64, const 
                            int slice_ctus, int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost,
                            uint32_t *out_bits_dist, uint8_t *out_states, int64_t *out_frac);
 
+/* Independent SliceMode=1 slice chains (slices of slice_ctus CTUs): chain k decides CTUs
+ * chain_first[k] .. + ctus_per_chain - 1 from entry_states (the slice-start contexts) and a zero
+ * m_integerMv2Nx2N, carrying both CTU to CTU; the chains run on n_threads threads.  Picture
+ * arrays as hvxo_hm_replay_picture; outputs per (chain, CTU) in that order. */
+int hvxo_hm_chains(const int32_t *pic_i32, const double *pic_f64, const uint8_t *org, const uint8_t *refpics,
+                   int n_refpics, const int16_t *col_field, const int32_t *entropy_bits, const uint8_t *entry_states,
+                   int n_chains, const int32_t *chain_first, int ctus_per_chain, int slice_ctus, int n_threads,
+                   int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost, uint32_t *out_bits_dist);
+
 #ifdef __cplusplus
 }
 #endif

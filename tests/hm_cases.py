@@ -112,7 +112,7 @@ def run_capture(name, mode, pics=None, stage=0):
             j["entry"]["st"] = g["ctu_states"][first + a]
             j["entry"]["frac"] = np.uint64(int(g["ctu_frac"][first + a]))
             j["int2n"] = g["ctu_int2n"][first + a]
-            j["debug_"] = stage
+            j["flags"] = stage << 8
             if rows:
                 j["slice_start"], j["slice_end"] = a - a % wc, a - a % wc + wc - 1
             else:
@@ -123,6 +123,48 @@ def run_capture(name, mode, pics=None, stage=0):
     LAST_ENGINE[:] = [eng]
     out = eng.compress(np.concatenate(jobs), slot)
     return g, plan, out
+
+
+def run_capture_resumed(name, split):
+    """The row-sliced capture decided in two launches per picture set: CTUs 0..split-1 of every
+    row, then (HVX_HM_RESUME, same job slots) CTUs split..end -- the bench's stepping.  Returns
+    (g, plan, out) like run_capture(mode=1)."""
+    import torch
+    g = gc.load(name)
+    g["_row_slices"] = True
+    eb = _abi.load_entropy_bits()
+    npic = g["pic_i32"].shape[0]
+    dps, plan, slot, rows = [], [], 0, []
+    for pic in range(npic):
+        pi = g["pic_i32"][pic]
+        first, n = int(pi[P_FIRST_CTU]), int(pi[P_NCTU])
+        wc = (int(pi[P_W]) + 63) // 64
+        dps.append(device_picture(g, pic, True, eb))
+        plan.append((pic, first, n, slot))
+        rows += [(pic, first, r, wc, slot) for r in range(0, n, wc)]
+        slot += n
+    eng = hm.Engine(dps)
+    LAST_ENGINE[:] = [eng]
+    out_ctu = torch.zeros(slot * hm.HM_CTU.itemsize, dtype=torch.uint8, device="cuda")
+    out_rec = torch.zeros(slot * 6144, dtype=torch.uint8, device="cuda")
+    out_cod = torch.zeros(slot * hm.HM_CODER.itemsize, dtype=torch.uint8, device="cuda")
+    for phase in (0, 1):
+        j = np.zeros(len(rows), hm.HM_JOB)
+        for k, (pic, first, r, wc, s0) in enumerate(rows):
+            a = r if phase == 0 else r + split
+            j[k]["pic"], j[k]["first_ctu"], j[k]["chained"], j[k]["out"] = pic, a, 1, s0 + a
+            j[k]["n_ctus"] = split if phase == 0 else wc - split
+            j[k]["slice_start"], j[k]["slice_end"] = r, r + wc - 1
+            j[k]["flags"] = _abi.HM_RESUME if phase else 0
+            if phase == 0:
+                j[k]["entry"]["st"] = g["ctu_states"][first + r]
+                j[k]["entry"]["frac"] = np.uint64(int(g["ctu_frac"][first + r]))
+                j[k]["int2n"] = g["ctu_int2n"][first + r]
+        jobs_t = torch.from_numpy(j.view(np.uint8).reshape(-1).copy()).cuda()
+        eng.launch(jobs_t, len(rows), out_ctu, out_rec, out_cod)
+    torch.cuda.synchronize()
+    return g, plan, (out_ctu.cpu().numpy().view(hm.HM_CTU), out_rec.cpu().numpy().reshape(slot, 6144),
+                     out_cod.cpu().numpy().view(hm.HM_CODER))
 
 
 def name_rows(g):

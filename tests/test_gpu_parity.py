@@ -307,3 +307,13 @@ def test_hm_ctu_golden_gpu(torch, name, mode):
     g, plan, out = hm_cases.run_capture(name, mode)
     bad = hm_cases.compare(g, plan, out)
     assert not bad, bad[:5]
+
+
+@pytest.mark.gpu
+def test_hm_ctu_resume_gpu(torch):
+    """HVX_HM_RESUME (the bench's stepping): every row slice decided in two launches, the second
+    continuing from the CABAC state and m_integerMv2Nx2N the first left in the job's state slot;
+    bit-exact vs HM."""
+    g, plan, out = hm_cases.run_capture_resumed("ctu_ldp_slices.bin", 3)
+    bad = hm_cases.compare(g, plan, out)
+    assert not bad, bad[:5]

@@ -76,3 +76,58 @@ def test_ctu_slices_vs_hm():
         out = hm_ctu.replay(g, pic, mode=1, slice_ctus=wc)
         bad = hm_ctu.compare(g, pic, out, verbose=False, slice_ctus=wc)
         assert not bad, (pic, bad[:3])
+
+
+def test_slice_params_vs_hm():
+    """video_codecs_amd.hm.slice_params (TEncSlice::initEncSlice / setUpLambda) reproduces every
+    captured picture's lambda, sqrt lambda, lambda_motion, chroma QPs / weights and TrQuant lambdas
+    bit for bit (LDP GOP: QPFactor 0.4624 at POC % 4 = 1-3, 0.578 at 0; I: 0.57 * (1 - 0.05 * 3))."""
+    from tests import hm_cases as hc
+    from video_codecs_amd import hm
+    for name in CAPTURES + ["ctu_ldp_slices.bin"]:
+        g = _load(name)
+        for pic in range(g["pic_i32"].shape[0]):
+            pi, pf = g["pic_i32"][pic], g["pic_f64"][pic]
+            st, qp, poc = int(pi[3]), int(pi[4]), int(pi[2])
+            fac = 0.57 * (1 - 0.05 * 3) if st == 2 else (0.578 if poc % 4 == 0 else 0.4624)
+            mine = hm.slice_params(st, qp, fac, gop_depth=0 if st == 2 else 1)
+            ref = hc.pic_params(pi, pf)
+            for k in ("lambda", "sqrt_lambda", "lambda_motion"):
+                assert mine[k] == ref[k], (name, pic, k)
+            for k in ("chroma_qp", "chroma_weight", "tq_lambda"):
+                assert list(mine[k]) == list(ref[k]), (name, pic, k)
+
+
+def test_hm_chains_vs_hm():
+    """hvxo_hm_chains (the bench's CPU port: independent row-slice chains on host threads) on
+    the sliced capture's QP 32 picture: 4 chains x 3 CTUs on 4 threads equal HM's CTUs."""
+    import numpy as np
+    g = _load("ctu_ldp_slices.bin")
+    pic = 2
+    pi, pf = g["pic_i32"][pic], g["pic_f64"][pic]
+    w, h = int(pi[0]), int(pi[1])
+    psz = w * h * 3 // 2
+    first, n = int(pi[41]), int(pi[42])
+    wc = (w + 63) // 64
+    col = g["col_field"][n * 16:2 * n * 16]  # pictures 1 and 2 carry a col field; this is picture 2's
+    chain_first = [r * wc for r in range(4)]
+    out = hm_ctu.chains(pi, pf, g["org"][pic * psz:(pic + 1) * psz], g["refpic"], g["ctu_states"][first],
+                        chain_first, 3, wc, threads=4, col_field=col)
+    for k, c in enumerate(chain_first):
+        for i in range(3):
+            a, o = first + c + i, k * 3 + i
+            np.testing.assert_array_equal(out["parts"][o], g["ctu_parts"][a], err_msg=(k, i))
+            np.testing.assert_array_equal(out["coef"][o], g["ctu_coef"][a], err_msg=(k, i))
+            np.testing.assert_array_equal(out["recon"][o], g["ctu_recon"][a], err_msg=(k, i))
+            assert out["cost"][o] == g["ctu_cost"][a]
+
+
+def test_hm_chains_rejects_bad_layout():
+    g = _load("ctu_ldp_slices.bin")
+    pi, pf = g["pic_i32"][2], g["pic_f64"][2]
+    psz = int(pi[0]) * int(pi[1]) * 3 // 2
+    with pytest.raises(ValueError):  # a chain crossing its slice's end
+        hm_ctu.chains(pi, pf, g["org"][2 * psz:3 * psz], g["refpic"], g["ctu_states"][56], [5], 3, 7,
+                      col_field=g["col_field"][448:896])
+    with pytest.raises(ValueError):  # TMVP on without a collocated field
+        hm_ctu.chains(pi, pf, g["org"][2 * psz:3 * psz], g["refpic"], g["ctu_states"][56], [0], 1, 7)

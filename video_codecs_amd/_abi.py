@@ -104,6 +104,7 @@ def ctu_params(pic_w, pic_h, n_ref, qp, lam=None, search_range=64, slice_type=1,
 
 # picture layout: 8-bit padded planes, HM TComPicYuv geometry (margin = MaxCU + 16 = 80)
 PLANE_MARGIN = 80
+HM_RESUME = 1  # HVX_HM_RESUME (hvx_hm_job.flags)
 
 
 def lambda_motion_sad(lam: float) -> int:

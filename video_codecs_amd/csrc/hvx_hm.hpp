@@ -102,6 +102,7 @@ struct State {
   double ctu_cost;
   uint8_t win[6144];              // its reconstruction: Y 64x64 | Cb 32x32 | Cr 32x32
   int16_t int2n[2][4][2];         // TEncSearch::m_integerMv2Nx2N
+  Coder carry;                    // the RD coder after the chain's last encodeCtu (HVX_HM_RESUME)
 };
 
 // the leaf scratch (one leaf runs at a time)
@@ -3032,20 +3033,23 @@ static __global__ __launch_bounds__(64) void k_hm_compress(const hvx_hm_picture 
   State *S = (State *)(state_base + (size_t)jid * state_bytes);
   hm_e.S = S;
   if (l < 4) hm_e.dbg[l] = 0;
-  hm_e.stage = job.debug_;
+  hm_e.stage = job.flags >> 8;
   hm_e.slice_start = job.slice_start;
   hm_e.slice_end = job.slice_end;
   hm_e.stop = 0;
   if (l < 32) hm_e.prof[l >> 4][l & 15] = 0;
-  copy_words(S->int2n, job.int2n, (int)sizeof(S->int2n));
+  const int resume = job.flags & HVX_HM_RESUME;
+  if (resume) copy_words(&hm_e.cod[RD(0, CI_CURR_BEST)], &S->carry, (int)sizeof(Coder));
+  else copy_words(S->int2n, job.int2n, (int)sizeof(S->int2n));
   wsync();
   const int n = job.n_ctus;
   for (int k = 0; k < n; k++) {
     const int addr = job.first_ctu + k;
     const int slot = job.out + k;
-    compress_ctu(addr, &job.entry, k > 0, out_coder ? &out_coder[slot] : nullptr);
+    compress_ctu(addr, &job.entry, k > 0 || resume, out_coder ? &out_coder[slot] : nullptr);
     // the next CTU starts from this CTU's encodeCtu state (m_pppcRDSbacCoder[0][CI_CURR_BEST])
     // which compress_ctu left in coder RD(0, CI_CURR_BEST)
+    copy_words(&S->carry, &hm_e.cod[RD(0, CI_CURR_BEST)], (int)sizeof(Coder));
     if (l < 4) S->dbg[l] = hm_e.dbg[l];
     if (l < 32) S->prof[l >> 4][l & 15] = hm_e.prof[l >> 4][l & 15];
     hvx_hm_ctu *o = &out_ctu[slot];

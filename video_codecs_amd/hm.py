@@ -29,7 +29,7 @@ assert HM_CTU.itemsize == 22544
 HM_CODER = np.dtype([("st", "u1", 202), ("pad_", "u1", 6), ("frac", "<u8")])
 assert HM_CODER.itemsize == 216
 HM_JOB = np.dtype([("pic", "<i4"), ("first_ctu", "<i4"), ("n_ctus", "<i4"), ("chained", "<i4"), ("out", "<i4"),
-                   ("slice_start", "<i4"), ("slice_end", "<i4"), ("debug_", "<i4"), ("entry", HM_CODER),
+                   ("slice_start", "<i4"), ("slice_end", "<i4"), ("flags", "<i4"), ("entry", HM_CODER),
                    ("int2n", "<i2", 16)], align=True)
 assert HM_JOB.itemsize == 280
 
@@ -89,22 +89,67 @@ def pad_plane(plane, margin, dtype):
     return np.pad(np.asarray(plane), margin, mode="edge").astype(dtype)
 
 
-class DevicePicture:
-    """One picture's device-side description (hvx_hm_picture) and the buffers it points at.
+def slice_params(slice_type, qp, qp_factor, gop_depth=1, chroma_offset=(0, 0)):
+    """The slice's RD scalars as TEncSlice::initEncSlice derives them (hm-16.5rc1
+    TEncSlice.cpp:320-374, HadamardME on, lambda modifier 1, DeltaQpRD 0): lambda = QPFactor *
+    2^((QP-12)/3), times Clip3(2, 4, (QP-12)/6) when the picture's GOP depth is > 0 (an I slice's
+    QPFactor is 0.57 * dLambda_scale: the caller passes it); then TEncSlice::setUpLambda
+    (:145-172): chroma weight 2^((QP - QPc)/3), TrQuant lambdas lambda / weight; and
+    TComRdCost::setLambda (TComRdCost.cpp:205-211): lambda_motion = floor(65536 sqrt(lambda))."""
+    import math
+    qt = qp - 12
+    lam = qp_factor * 2.0 ** (qt / 3.0)
+    if gop_depth > 0:
+        lam *= min(4.0, max(2.0, qt / 6.0))
+    cq = [_abi.chroma_qp(qp, chroma_offset[0]), _abi.chroma_qp(qp, chroma_offset[1])]
+    w = [2.0 ** ((qp - c) / 3.0) for c in cq]
+    sq = math.sqrt(lam)
+    return {"slice_type": slice_type, "qp": qp, "chroma_qp": cq, "lambda": lam, "sqrt_lambda": sq,
+            "lambda_motion": int(math.floor(65536.0 * sq)), "chroma_weight": w,
+            "tq_lambda": [lam, lam / w[0], lam / w[1]]}
 
-    org: (Y, Cb, Cr) uint8 arrays; refs: list of (Y, Cb, Cr) uint8 reference pictures (indexed by
-    ref_plane); params: the slice / RD scalars (see HmPicture); rec: optional (Y, Cb, Cr) uint8
-    initial reconstruction; ctus: optional HM_CTU array (the picture's CTU data); col_field:
-    optional int16 [nctu*16, 8] collocated motion field."""
+
+class DeviceFrame:
+    """A frame's device planes as the engine reads them: the 8-bit original (Y, Cb, Cr) for a
+    current picture, and the padded planes for a reference (8-bit luma with PLANE_MARGIN, int16
+    Y/Cb/Cr with 80/40 samples of extended border, TComPicYuv::extendPicBorder).  Built once and
+    shared by every picture that reads the frame."""
 
     M8, M16, M16C = _abi.PLANE_MARGIN, 80, 40
 
+    def __init__(self, planes, device="cuda"):
+        import torch
+        self.org = [torch.from_numpy(np.ascontiguousarray(p, np.uint8)).to(device) for p in planes]
+        y8 = torch.from_numpy(pad_plane(planes[0], self.M8, np.uint8)).to(device)
+        self.keep = [y8]
+        self.ref8 = y8.data_ptr() + (self.M8 * y8.shape[1] + self.M8)
+        self.ref8_stride = int(y8.shape[1])
+        self.ref16, self.ref16_stride = [], [0, 0]
+        for c in range(3):
+            m = self.M16 if c == 0 else self.M16C
+            p16 = torch.from_numpy(pad_plane(planes[c], m, np.int16)).to(device)
+            self.keep.append(p16)
+            self.ref16.append(p16.data_ptr() + 2 * (m * p16.shape[1] + m))
+            self.ref16_stride[1 if c else 0] = int(p16.shape[1])
+
+
+class DevicePicture:
+    """One picture's device-side description (hvx_hm_picture) and the buffers it points at.
+
+    org: (Y, Cb, Cr) uint8 arrays or a DeviceFrame; refs: reference pictures (indexed by
+    ref_plane), each (Y, Cb, Cr) uint8 arrays or a DeviceFrame; params: the slice / RD scalars (see
+    HmPicture); rec: optional (Y, Cb, Cr) uint8 initial reconstruction; ctus: optional HM_CTU
+    array (the picture's CTU data); col_field: optional int16 [nctu*16, 8] collocated motion field."""
+
     def __init__(self, org, refs, params, entropy_bits, rec=None, ctus=None, col_field=None, device="cuda"):
         import torch
-        self.w, self.h = int(org[0].shape[1]), int(org[0].shape[0])
+        self.keep = []
+        if not isinstance(org, DeviceFrame):
+            org = DeviceFrame(org, device)
+        self.keep.append(org)
+        self.w, self.h = int(org.org[0].shape[1]), int(org.org[0].shape[0])
         w, h = self.w, self.h
         self.wc, self.hc = (w + 63) // 64, (h + 63) // 64
-        self.keep = []
 
         def dev(a):
             t = torch.from_numpy(np.ascontiguousarray(a)).to(device)
@@ -126,7 +171,7 @@ class DevicePicture:
                         a[i] = v[i].item()
             else:
                 setattr(s, "lambda_" if k == "lambda" else k, v)
-        self.org_t = [dev(np.asarray(p, np.uint8)) for p in org]
+        self.org_t = org.org
         for c in range(3):
             s.org[c] = self.org_t[c].data_ptr()
         s.org_stride[0], s.org_stride[1] = w, w // 2
@@ -152,14 +197,14 @@ class DevicePicture:
             s.col_field = dev(np.asarray(col_field, np.int16)).data_ptr()
         assert len(refs) <= 8
         for i, ref in enumerate(refs):
-            y8 = dev(pad_plane(ref[0], self.M8, np.uint8))
-            s.ref8[i] = y8.data_ptr() + (self.M8 * y8.shape[1] + self.M8)
-            s.ref8_stride = int(y8.shape[1])
+            if not isinstance(ref, DeviceFrame):
+                ref = DeviceFrame(ref, device)
+            self.keep.append(ref)
+            s.ref8[i] = ref.ref8
+            s.ref8_stride = ref.ref8_stride
             for c in range(3):
-                m = self.M16 if c == 0 else self.M16C
-                p16 = dev(pad_plane(ref[c], m, np.int16))
-                s.ref16[i][c] = p16.data_ptr() + 2 * (m * p16.shape[1] + m)
-                s.ref16_stride[1 if c else 0] = int(p16.shape[1])
+                s.ref16[i][c] = ref.ref16[c]
+            s.ref16_stride[0], s.ref16_stride[1] = ref.ref16_stride
         s.entropy_bits = dev(np.asarray(entropy_bits, np.int32)).data_ptr()
         self.struct = s
 
@@ -179,24 +224,41 @@ class Engine:
         self.device = device
         self.state = None
 
+    def reserve(self, n_jobs):
+        """Per-job device state for n_jobs jobs (job i always uses slot i: HVX_HM_RESUME jobs
+        continue from the state their slot's previous launch left)."""
+        import torch
+        sb = state_size()
+        if self.state is None or self.state.numel() < n_jobs * sb:
+            old = self.state
+            self.state = torch.empty(n_jobs * sb, dtype=torch.uint8, device=self.device)
+            if old is not None:
+                self.state[:old.numel()].copy_(old)
+        return sb
+
+    def launch(self, jobs_t, n_jobs, out_ctu, out_rec, out_cod=None):
+        """Enqueue hvx_hm_compress on torch's current stream (no sync): device job array jobs_t
+        (HM_JOB bytes), outputs out_ctu (HM_CTU bytes), out_rec (6144 B per slot), out_cod
+        (HM_CODER bytes, optional)."""
+        from . import hvx
+        self.reserve(n_jobs)
+        P = ctypes.c_void_p
+        hvx._check(hvx.lib().hvx_hm_compress(hvx.context(), P(self.pics_t.data_ptr()), P(jobs_t.data_ptr()), n_jobs,
+                                             P(self.state.data_ptr()), P(out_ctu.data_ptr()), P(out_rec.data_ptr()),
+                                             P(0 if out_cod is None else out_cod.data_ptr())), "hvx_hm_compress")
+
     def compress(self, jobs, n_out):
         """Run the jobs (HM_JOB array); returns (ctus [n_out] HM_CTU, rec [n_out, 6144] uint8,
         coders [n_out] HM_CODER) copied to the host."""
         import torch
-        from . import hvx
         jobs = np.ascontiguousarray(jobs, HM_JOB)
         n = len(jobs)
-        sb = state_size()
-        if self.state is None or self.state.numel() < n * sb:
-            self.state = torch.empty(n * sb, dtype=torch.uint8, device=self.device)
+        sb = self.reserve(n)
         jobs_t = torch.from_numpy(jobs.view(np.uint8).reshape(-1).copy()).to(self.device)
         out_ctu = torch.zeros(n_out * HM_CTU.itemsize, dtype=torch.uint8, device=self.device)
         out_rec = torch.zeros(n_out * 6144, dtype=torch.uint8, device=self.device)
         out_cod = torch.zeros(n_out * HM_CODER.itemsize, dtype=torch.uint8, device=self.device)
-        P = ctypes.c_void_p
-        hvx._check(hvx.lib().hvx_hm_compress(hvx.context(), P(self.pics_t.data_ptr()), P(jobs_t.data_ptr()), n,
-                                             P(self.state.data_ptr()), P(out_ctu.data_ptr()), P(out_rec.data_ptr()),
-                                             P(out_cod.data_ptr())), "hvx_hm_compress")
+        self.launch(jobs_t, n, out_ctu, out_rec, out_cod)
         torch.cuda.synchronize()
         st = self.state[:n * sb].view(n, sb)[:, :272].cpu().numpy().copy()
         self.last_debug = st[:, :16].copy().view(np.int32).reshape(n, 4)  # State.dbg (HM_CHECKS builds)
