@@ -179,10 +179,10 @@ class HmWorkload:
     (hm.slice_params).  Step k advances every chain by `ctus` CTUs from where step k-1 left it
     (HVX_HM_RESUME); a chain that reaches its row's end starts the row again as a new slice."""
 
-    def __init__(self, W, H, pics, nref, base_qp, ctus, rank):
+    def __init__(self, W, H, pics, nref, base_qp, ctus, rank, col=True):
         import torch
         from video_codecs_amd import _abi, hm, synth
-        self.W, self.H, self.pics, self.nref, self.ctus = W, H, pics, nref, ctus
+        self.W, self.H, self.pics, self.nref, self.ctus, self.col = W, H, pics, nref, ctus, col
         self.wc, self.hc = (W + 63) // 64, (H + 63) // 64
         assert self.wc % ctus == 0, "--ctus must divide the CTUs per row"
         self.qp = base_qp + HM_QP_OFFSET
@@ -196,8 +196,10 @@ class HmWorkload:
         for p in range(pics):
             self.pictures.append(hm.DevicePicture(frames[nref + p], [frames[nref + p - 1 - k] for k in range(nref)],
                                                   self.picture_params(p), eb,
-                                                  col_field=synthetic_col_field(self.wc * self.hc, self.base + p)))
+                                                  col_field=self.col_field(p)))
         self.eng = hm.Engine(self.pictures)
+        self.stream = torch.cuda.Stream()
+        torch.cuda.synchronize()  # inputs resident before any launch on the workload's stream
         self.n_jobs = pics * self.hc
         self.eng.reserve(self.n_jobs)
         self.slots = self.n_jobs * ctus
@@ -221,25 +223,32 @@ class HmWorkload:
         self.keep_steps = []
         self.keep_n = self.hc * ctus
 
+    def col_field(self, p):
+        return synthetic_col_field(self.wc * self.hc, self.base + p) if self.col else None
+
     def picture_params(self, p):
         poc, nref = self.nref + p, self.nref
         q = dict(self.params)
         q.update(poc=poc, nref=[nref, 0], ref_poc=np.array([[poc - 1 - k for k in range(4)], [0] * 4]),
                  ref_plane=np.array([list(range(nref)) + [0] * (4 - nref), [0] * 4]), max_merge=5, tmvp=1, check_ldc=1,
-                 col_from_l0=1, col_valid=1, col_poc=poc - 1,
+                 col_from_l0=1, col_valid=int(self.col), col_poc=poc - 1,
                  col_ref_poc=np.array([[poc - 2 - k for k in range(4)], [0] * 4]), search_range=64, amp=1)
         return q
 
     def step(self, out_rec, events=None):
-        """One launch: every chain advances `ctus` CTUs; reconstructed CTUs go to out_rec."""
+        """One launch: every chain advances `ctus` CTUs; reconstructed CTUs go to out_rec.  The
+        launch, its HIP events and the copies of its records are ordered on the workload's own
+        stream (the library launches on torch's current stream when that is not the null stream)."""
+        import torch
         pos = self.step_idx % len(self.phase_jobs)
-        if events is not None:
-            events[0].record()
-        self.eng.launch(self.phase_jobs[pos], self.n_jobs, self.out_ctu, out_rec)
-        if events is not None:
-            events[1].record()
-        self.keep_steps.append((pos * self.ctus, self.out_ctu[:self.keep_n * 22544].clone(),
-                                out_rec[:self.keep_n * 6144].clone()))
+        with torch.cuda.stream(self.stream):
+            if events is not None:
+                events[0].record()
+            self.eng.launch(self.phase_jobs[pos], self.n_jobs, self.out_ctu, out_rec)
+            if events is not None:
+                events[1].record()
+            self.keep_steps.append((pos * self.ctus, self.out_ctu[:self.keep_n * 22544].clone(),
+                                    out_rec[:self.keep_n * 6144].clone()))
         self.step_idx += 1
 
     def host_inputs(self, p):
@@ -258,12 +267,12 @@ class HmWorkload:
         pi[39:41] = prm["chroma_qp"]
         pi[41:43] = [0, self.wc * self.hc]
         pi[43] = np.array(prm["lambda_motion"], np.uint32).view(np.int32)
-        pi[45] = 1
+        pi[45] = int(self.col)
         pf = np.array([prm["lambda"], prm["sqrt_lambda"], *prm["chroma_weight"], *prm["tq_lambda"]], np.float64)
         org = synth.random_frame(self.W, self.H, self.base + self.nref + p)
         refs = np.concatenate([synth.random_frame(self.W, self.H, self.base + self.nref + p - 1 - k)
                                for k in range(self.nref)])
-        return pi, pf, org, refs, synthetic_col_field(self.wc * self.hc, self.base + p)
+        return pi, pf, org, refs, self.col_field(p)
 
 
 def hm_cpu_port(work, threads, min_seconds=0.0):
@@ -302,19 +311,31 @@ def hm_cpu_port(work, threads, min_seconds=0.0):
                 dev_cost[:, pos + i] = c[:, i]["cost"]
                 dev_bd[:, pos + i, 0], dev_bd[:, pos + i, 1] = c[:, i]["bits"], c[:, i]["dist"]
                 seen[pos + i] = True
-    mism = 0
+    mism, first = 0, []
     for k in range(hc):
         for i in range(done):
             o = k * done + i
-            same = (np.array_equal(out["parts"][o], dev_parts[k, i]) and
-                    np.array_equal(out["coef"][o].astype(np.int16), dev_coef[k, i]) and
-                    np.array_equal(out["recon"][o], dev_rec[k, i]) and out["cost"][o] == dev_cost[k, i] and
-                    np.array_equal(out["bits_dist"][o], dev_bd[k, i]))
-            mism += 0 if same else 1
+            what = None
+            if not np.array_equal(out["parts"][o], dev_parts[k, i]):
+                d = np.argwhere(out["parts"][o] != dev_parts[k, i])
+                z, f = int(d[0][0]), int(d[0][1])
+                what = "part z=%d %s port=%d gpu=%d (%d fields differ)" % (z, hm.PART_FIELDS[f], out["parts"][o][z, f],
+                                                                          dev_parts[k, i][z, f], len(d))
+            elif not np.array_equal(out["coef"][o].astype(np.int16), dev_coef[k, i]):
+                what = "coef"
+            elif not np.array_equal(out["recon"][o], dev_rec[k, i]):
+                what = "recon"
+            elif out["cost"][o] != dev_cost[k, i] or not np.array_equal(out["bits_dist"][o], dev_bd[k, i]):
+                what = "totals port=(%s,%r) gpu=(%s,%r)" % (list(out["bits_dist"][o]), out["cost"][o], list(dev_bd[k, i]),
+                                                          dev_cost[k, i])
+            if what:
+                mism += 1
+                if len(first) < 4:
+                    first.append("row %d ctu %d: %s" % (k, i, what))
     return {"value": round(n / dt, 3), "unit": "CTUs/s", "cores": threads, "kind": "port",
             "sample": f"picture 0's {hc} slice chains x {done} CTUs ({n} CTUs) through oracle/hvx_oracle_cu.c "
                       f"hvxo_hm_chains on {threads} host threads, {dt:.1f} s",
-            "gpu_parity_ctus": n, "gpu_parity_mismatches": mism}
+            "gpu_parity_ctus": n, "gpu_parity_mismatches": mism, "first_mismatches": first}
 
 
 def hm_cpu_reference(procs, tmpdir):
@@ -383,8 +404,9 @@ def main():
         if timing[0]:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             events.append(ev)
-        work.step(dpb.buffer(), ev)
-        dpb.send()
+        with torch.cuda.stream(work.stream):  # the gather reads what this step's launch wrote
+            work.step(dpb.buffer(), ev)
+            dpb.send()
 
     def sync():
         dpb.drain()

@@ -3014,7 +3014,12 @@ __device__ void compress_ctu(int addr, const Coder *entry_g, int entry_in_lds, C
 }  // namespace hm
 
 // hvx_hm_compress: one workgroup (one wave) per job
-static __global__ __launch_bounds__(64) void k_hm_compress(const hvx_hm_picture *__restrict__ pics, const hvx_hm_job *__restrict__ jobs,
+#ifdef HM_WAVES_PER_EU
+#define HM_KATTR __attribute__((amdgpu_waves_per_eu(HM_WAVES_PER_EU)))
+#else
+#define HM_KATTR
+#endif
+static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm_picture *__restrict__ pics, const hvx_hm_job *__restrict__ jobs,
                                                     int n_jobs, char *state_base, size_t state_bytes, hvx_hm_ctu *out_ctu,
                                                     uint8_t *out_rec, hvx_hm_coder *out_coder) {
   using namespace hm;

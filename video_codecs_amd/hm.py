@@ -223,6 +223,7 @@ class Engine:
         self.pics_t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
         self.device = device
         self.state = None
+        self.stream = None
 
     def reserve(self, n_jobs):
         """Per-job device state for n_jobs jobs (job i always uses slot i: HVX_HM_RESUME jobs
@@ -240,12 +241,27 @@ class Engine:
         """Enqueue hvx_hm_compress on torch's current stream (no sync): device job array jobs_t
         (HM_JOB bytes), outputs out_ctu (HM_CTU bytes), out_rec (6144 B per slot), out_cod
         (HM_CODER bytes, optional)."""
+        import torch
         from . import hvx
         self.reserve(n_jobs)
         P = ctypes.c_void_p
-        hvx._check(hvx.lib().hvx_hm_compress(hvx.context(), P(self.pics_t.data_ptr()), P(jobs_t.data_ptr()), n_jobs,
-                                             P(self.state.data_ptr()), P(out_ctu.data_ptr()), P(out_rec.data_ptr()),
-                                             P(0 if out_cod is None else out_cod.data_ptr())), "hvx_hm_compress")
+
+        def go():
+            hvx._check(hvx.lib().hvx_hm_compress(hvx.context(), P(self.pics_t.data_ptr()), P(jobs_t.data_ptr()), n_jobs,
+                                                 P(self.state.data_ptr()), P(out_ctu.data_ptr()), P(out_rec.data_ptr()),
+                                                 P(0 if out_cod is None else out_cod.data_ptr())), "hvx_hm_compress")
+        cur = torch.cuda.current_stream()
+        if cur.cuda_stream:
+            go()
+            return
+        # the library maps the null stream to its context's own stream: launch on a stream of
+        # ours instead, ordered after and before the caller's work
+        if self.stream is None:
+            self.stream = torch.cuda.Stream()
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            go()
+        cur.wait_stream(self.stream)
 
     def compress(self, jobs, n_out):
         """Run the jobs (HM_JOB array); returns (ctus [n_out] HM_CTU, rec [n_out, 6144] uint8,
