@@ -41,7 +41,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--pics", type=int, default=22, help="P pictures in flight per GPU (34 slice chains each at 2160p)")
+    p.add_argument("--pics", type=int, default=60, help="P pictures in flight per GPU (34 slice chains each at 2160p: "
+                                                        "60 -> 2040 chains, two waves per SIMD)")
     p.add_argument("--ctus", type=int, default=1, help="CTUs each slice chain advances per step")
     p.add_argument("--cpu-ref-procs", type=int, default=0, help="HM TAppEncoder processes for the reference "
                                                                   "baseline (0: the host's CPU share)")
@@ -190,8 +191,11 @@ class HmWorkload:
         self.params = hm.slice_params(1, self.qp, HM_QP_FACTOR)
         eb = _abi.load_entropy_bits()
         self.entry = _abi.load_ctx_init_states()[1, self.qp]
-        frames = [hm.DeviceFrame(yuv_split(synth.random_frame(W, H, self.base + i), W, H))
-                  for i in range(nref + pics)]
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(8) as ex:
+            host = list(ex.map(lambda i: synth.random_frame(W, H, self.base + i), range(nref + pics)))
+        frames = [hm.DeviceFrame(yuv_split(f, W, H)) for f in host]
+        del host
         self.pictures = []
         for p in range(pics):
             self.pictures.append(hm.DevicePicture(frames[nref + p], [frames[nref + p - 1 - k] for k in range(nref)],

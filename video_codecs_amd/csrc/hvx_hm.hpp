@@ -82,6 +82,25 @@ struct Yuv { int16_t s[6144]; };
 __device__ __forceinline__ int ystride(int c) { return c ? 32 : 64; }
 __device__ __forceinline__ int16_t *yaddr(Yuv *b, int c, int x, int y) { return b->s + coff(c) + y * ystride(c) + x; }
 
+// the leaf scratch of motion search and motion compensation (in the chain state: global memory)
+struct MeScratch {
+  MeFracSmem<64, 1> sm;
+  uint32_t red[2 * kMeMaxRanges];
+  hvx_me_result r;
+};
+struct McScratch {
+  int16_t tmp[(64 + 7) * 64];
+  int16_t pr[2][64 * 64];
+};
+struct IntraScratch {
+  int16_t unf[intra::kB + 3], filt[intra::kB + 3];
+  uint8_t org[64 * 64];
+  uint32_t satd[36];
+  int list[12], mpm[3];
+  double cc[10];
+  int n_cand, pad_;
+  uint8_t cand[12];
+};
 // per-chain state in HBM
 struct State {
   int dbg[4];  // HM_CHECKS: E.dbg of the last CTU
@@ -103,35 +122,20 @@ struct State {
   uint8_t win[6144];              // its reconstruction: Y 64x64 | Cb 32x32 | Cr 32x32
   int16_t int2n[2][4][2];         // TEncSearch::m_integerMv2Nx2N
   Coder carry;                    // the RD coder after the chain's last encodeCtu (HVX_HM_RESUME)
+  MeScratch me;                   // leaf scratch outside LDS
+  McScratch mc;
+  TuSmem<3> tu3;
 };
 
-// the leaf scratch (one leaf runs at a time)
-struct MeScratch {
-  MeFracSmem<64, 1> sm;
-  uint32_t red[2 * kMeMaxRanges];
-  hvx_me_result r;
-};
-struct McScratch {
-  int16_t tmp[(64 + 7) * 64];
-  int16_t pr[2][64 * 64];
-};
-struct IntraScratch {
-  int16_t unf[intra::kB + 3], filt[intra::kB + 3];
-  uint8_t org[64 * 64];
-  uint32_t satd[36];
-  int list[12], mpm[3];
-  double cc[10];
-  int n_cand, pad_;
-  uint8_t cand[12];
-};
+// the LDS leaf scratch (one leaf runs at a time): TU pipelines up to 16x16 and the intra
+// first pass.  The 32x32 TU pipeline, motion search and motion compensation keep theirs in the
+// chain state (global memory), which holds the LDS footprint of a chain's wave near 16 KB
 union Leaf {
   TuSmem<0> tu0;
   TuSmem<1> tu1;
   TuSmem<2> tu2;
-  TuSmem<3> tu3;
-  MeScratch me;
-  McScratch mc;
   IntraScratch in;
+  int16_t cstage[1024];  // codeCoeffNxN's levels in scan order
 };
 
 // the decision's LDS-resident context (TEncCu / TEncSearch / TComTrQuant scalars + coders)
@@ -858,16 +862,70 @@ __device__ void tu_desc(const Cu *cu, const Tu &t, int comp, hvx_tu_desc &d) {
   d.bit_depth = 8;
   d.lambda = E.P.tq_lambda[comp];
 }
-// codeCoeffNxN on the current coder, levels TU-packed int16
+// The coefficient contexts of one coder held in registers for the duration of a TU's
+// codeCoeffNxN: row r (model kCtxLo + r) in lane r & 63 of VGPR r >> 6, the entropy-bit table
+// and transIdxLPS likewise; every bin is a few v_readlane / v_writelane on a wave-uniform
+// index instead of three dependent LDS round trips (ContextModel::update, TEncBinCABACCounter).
+struct RegCoder {
+  int r0, r1, r2, eb0, eb1, lps;
+  uint64_t frac;
+  __device__ __forceinline__ void load(const uint8_t *st) {
+    const int l = lid();
+    r0 = st[cab::kCtxLo + l];
+    r1 = st[cab::kCtxLo + 64 + l];
+    r2 = l < cab::kRows - 128 ? st[cab::kCtxLo + 128 + l] : 0;
+    eb0 = E.eb[l];
+    eb1 = E.eb[64 + l];
+    lps = cab::kTransIdxLps[l];
+    frac = 0;
+  }
+  __device__ __forceinline__ void store(uint8_t *st) const {
+    const int l = lid();
+    st[cab::kCtxLo + l] = (uint8_t)r0;
+    st[cab::kCtxLo + 64 + l] = (uint8_t)r1;
+    if (l < cab::kRows - 128) st[cab::kCtxLo + 128 + l] = (uint8_t)r2;
+  }
+  __device__ __forceinline__ void bin(int row, int v) {
+    row = __builtin_amdgcn_readfirstlane(row);
+    v = __builtin_amdgcn_readfirstlane(v);
+    const int k = row >> 6, ln = row & 63;
+    const int st = k == 0 ? __builtin_amdgcn_readlane(r0, ln) : k == 1 ? __builtin_amdgcn_readlane(r1, ln)
+                                                                        : __builtin_amdgcn_readlane(r2, ln);
+    const int i = st ^ v;
+    frac += (uint32_t)(i < 64 ? __builtin_amdgcn_readlane(eb0, i) : __builtin_amdgcn_readlane(eb1, i - 64));
+    const int p = st >> 1, mps = st & 1;
+    const int ns = v == mps ? (((p < 62 ? p + 1 : p) << 1) | mps)
+                            : ((__builtin_amdgcn_readlane(lps, p) << 1) | (p == 0 ? mps ^ 1 : mps));
+    if (k == 0) r0 = __builtin_amdgcn_writelane(ns, ln, r0);
+    else if (k == 1) r1 = __builtin_amdgcn_writelane(ns, ln, r1);
+    else r2 = __builtin_amdgcn_writelane(ns, ln, r2);
+  }
+  __device__ __forceinline__ void ep(int n) { frac += 32768ull * (uint32_t)n; }
+  __device__ __forceinline__ void ep_bits(uint32_t, int n) { ep(n); }
+  __device__ __forceinline__ void eps(uint32_t, int n) { ep(n); }
+  __device__ __forceinline__ void esc(uint32_t symbol, int r, bool limited, int max_log2) {
+    ep(cab::remain_bins(symbol, r, limited, max_log2));
+  }
+};
+
+// codeCoeffNxN on the current coder, levels TU-packed int16: the levels are first staged in
+// LDS in scan order by the whole wave (one memory latency), the syntax walk then reads LDS
 __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_t *coef) {
   HM_PROF(PR_COEF);
   hvx_tu_desc d;
   tu_desc(cu, t, comp, d);
+  const int n = d.width * d.width;
   const uint16_t *scan = kScan[d.scan_type] + scan_base(ilog2(d.width) - 2);
-  CoderLane L{E.cod[E.cur].st, 0};
+  int16_t *ls = E.u.cstage;
+  for (int i = lid(); i < n; i += 64) ls[i] = coef[scan[i]];
+  RegCoder L;
+  L.load(E.cod[E.cur].st);
+  wsync();
   uint32_t rice = 0;
-  cab::coeff_bits(d, [&](int sp) { return (int)coef[scan[sp]]; }, L, rice);
+  cab::coeff_bits(d, [&](int sp) { return (int)ls[sp]; }, L, rice);
+  L.store(E.cod[E.cur].st);
   E.cod[E.cur].frac += L.frac;
+  wsync();
 }
 // TEncEntropy::estimateBit (TEncEntropy.cpp:685) from the current coder
 // The entries TEncSbac::estBit writes (exactly those of estbit_update), one per lane: two
@@ -1085,13 +1143,19 @@ __device__ uint32_t yuv_dist(Yuv *a, Yuv *b, int w) {
 // ============================================================================================
 // Transform / quantisation / RDOQ / inverse through the pinned wave kernels (hvx_tu.hpp)
 // ============================================================================================
+// the TU pipeline's scratch: LDS up to 16x16, the chain state for 32x32
+template <int L>
+__device__ __forceinline__ TuSmem<L> &tu_smem() {
+  if constexpr (L == 3) return E.S->tu3;
+  else return *reinterpret_cast<TuSmem<L> *>(&E.u);
+}
 template <int L>
 __device__ int32_t tu_fwd_l(const hvx_tu_desc &d, const int16_t *resi, int rs, int16_t *coef) {
   HM_PROF(PR_TUF);
 #ifdef HM_PROFILE
   ProfScope prof_size_(12 + L);
 #endif
-  TuSmem<L> &s = *reinterpret_cast<TuSmem<L> *>(&E.u);
+  TuSmem<L> &s = tu_smem<L>();
   constexpr int N = 4 << L;
   for (int i = lid(); i < N * N; i += 64) s.a[i] = resi[(i >> (L + 2)) * rs + (i & (N - 1))];
   wsync();
@@ -1103,7 +1167,7 @@ __device__ int32_t tu_fwd_l(const hvx_tu_desc &d, const int16_t *resi, int rs, i
 template <int L>
 __device__ void tu_inv_l(const hvx_tu_desc &d, const int16_t *coef, int16_t *resi, int rs) {
   HM_PROF(PR_TUI);
-  TuSmem<L> &s = *reinterpret_cast<TuSmem<L> *>(&E.u);
+  TuSmem<L> &s = tu_smem<L>();
   constexpr int N = 4 << L;
   for (int i = lid(); i < N * N; i += 64) s.lev[i] = coef[i];
   wsync();
@@ -1152,7 +1216,7 @@ __device__ void blk_copy(int16_t *dst, int ds, const int16_t *src, int ss, int w
 // xPredInterBlk (:668) for one component and list, lane-parallel, dst with stride ds
 __device__ void mc_blk(bool luma, const int16_t *plane, int stride, int x, int y, int mvx, int mvy, int w, int h, bool bi,
                        int16_t *dst, int ds) {
-  int16_t *tmp = E.u.mc.tmp;
+  int16_t *tmp = E.S->mc.tmp;
   const int sh = luma ? 2 : 3, n = luma ? 8 : 4;
   const int xf = mvx & ((1 << sh) - 1), yf = mvy & ((1 << sh) - 1);
   const int16_t *ref = plane + (y + (mvy >> sh)) * stride + x + (mvx >> sh);
@@ -1242,11 +1306,11 @@ __device__ void mc_pu(const Cu *cu, int ps, int pu, Yuv *dst) {
     int16_t *o = yaddr(dst, comp, luma ? rx : rx >> 1, luma ? ry : ry >> 1);
     const int os = ystride(comp);
     if (bi) {
-      mc_blk(luma, E.P.ref16[pl0][comp], stride, x, y, mx[0], my[0], cw, chh, true, E.u.mc.pr[0], cw);
-      mc_blk(luma, E.P.ref16[pl1][comp], stride, x, y, mx[1], my[1], cw, chh, true, E.u.mc.pr[1], cw);
+      mc_blk(luma, E.P.ref16[pl0][comp], stride, x, y, mx[0], my[0], cw, chh, true, E.S->mc.pr[0], cw);
+      mc_blk(luma, E.P.ref16[pl1][comp], stride, x, y, mx[1], my[1], cw, chh, true, E.S->mc.pr[1], cw);
       for (int k = lid(); k < cw * chh; k += 64) {
         const int r = k / cw, c = k - r * cw;
-        o[r * os + c] = (int16_t)clip_pel((E.u.mc.pr[0][k] + E.u.mc.pr[1][k] + 16448) >> 7);
+        o[r * os + c] = (int16_t)clip_pel((E.S->mc.pr[0][k] + E.S->mc.pr[1][k] + 16448) >> 7);
       }
       wsync();
     } else {
@@ -1786,7 +1850,7 @@ __device__ uint32_t template_cost(const Cu *cu, int ps, int pu, Yuv *org, int li
   int mx = mvc[0], my = mvc[1];
   clip_mv(cu, mx, my);
   const int pl = E.P.ref_plane[list][ref_idx];
-  int16_t *pr = E.u.mc.pr[0];
+  int16_t *pr = E.S->mc.pr[0];
   mc_blk(true, E.P.ref16[pl][0], E.P.ref16_stride[0], xp, yp, mx, my, w, h, false, pr, w);
   const int16_t *o = yaddr(org, 0, xp - cu->x, yp - cu->y);
   uint32_t s = 0;
@@ -1853,7 +1917,7 @@ __device__ void motion_estimation(Cu *cu, int ps, int pu, int list, int ref_idx,
   const int pi = E.P.ref_plane[list][ref_idx];
   HMC(pi >= 0 && pi < 8 && E.P.ref8[pi] != nullptr && xp >= 0 && yp >= 0 && xp + w <= E.P.w && yp + h <= E.P.h, 6, pi,
       xp * 10000 + yp);
-  MeScratch &ms = E.u.me;
+  MeScratch &ms = E.S->me;
   const uint8_t *org = E.P.org[0] + yp * E.P.org_stride[0] + xp;
   const int os = E.P.org_stride[0];
   for (int k = lid(); k < w * h; k += 64) {
