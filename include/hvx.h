@@ -250,7 +250,10 @@ int hvx_coeff_bits_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t 
  * registers start at d_regs[k] (TEncBinCABAC::start() = {0, 510, 23, 0, 0xff}) and whose context
  * states start at d_states[k*HVX_NUM_CTX ..]; both are advanced in place.  The bytes the coder
  * completes are written to d_out + d_out_off[k] (at most out_cap bytes) and counted in
- * d_out_len[k] (-1: more than out_cap, -2: an unsupported TU shape).  Bytes still held in the
+ * d_out_len[k] (-1: more than out_cap, -2: a TU of the run is unsupported -- non-square, not
+ * 4..32, scan type > 2, or persistent_rice set -- checked before anything is coded, so the run's
+ * registers and states are left untouched).  d_regs[k].coded accumulates the context models the
+ * run coded a bin with (the caller sets their m_binsCoded).  Bytes still held in the
  * registers (low, the buffered 0xff run) belong to the next call or to TEncBinCABAC::finish().
  * ------------------------------------------------------------------------------------- */
 int hvx_coeff_write_batch(hvx_ctx *ctx, const hvx_tu_desc *d_desc, const int64_t *d_off, const int32_t *d_levels,

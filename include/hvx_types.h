@@ -70,11 +70,15 @@ typedef struct hvx_coeff_bits {
 /* The registers of the slice writer's arithmetic coder, TEncBinCABAC (TEncBinCoderCABAC.h):
  * m_uiLow, m_uiRange, m_bitsLeft, m_numBufferedBytes, m_bufferedByte.  TEncBinCABAC::start()
  * is {0, 510, 23, 0, 0xff}.  bins counts the bins coded (context, bypass), as m_uiBinsCoded
- * does with m_binCountIncrement 1; the writer adds to it. */
+ * does with m_binCountIncrement 1; the writer adds to it.  coded: bit (m - 42) of the 160-bit map
+ * is set for every context model m (42..184, the residual syntax) the writer codes a bin with --
+ * ContextModel::setBinsCoded(1) in encodeBin (TEncBinCoderCABAC.cpp:203), which
+ * ContextModel3DBuffer::calcCost reads for the cabac_init_flag choice; OR-accumulated. */
 typedef struct hvx_cabac_regs {
   uint32_t low, range;
   int32_t bits_left, num_buffered;
   uint32_t buffered_byte, bins;
+  uint32_t coded[5];
 } hvx_cabac_regs;
 
 /* One uni-prediction motion search: TEncSearch::xMotionEstimation with bBi=false

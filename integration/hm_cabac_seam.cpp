@@ -110,6 +110,7 @@ Void TEncSbac::codeCoeffNxN(TComTU &rTu, TCoeff *pcCoef, const ComponentID compI
   const bool ported = bin && g_cw.on() && w == h && (w == 4 || w == 8 || w == 16 || w == 32) &&
                       !cu->isRDPCMEnabled(abs) && !sps.getSpsRangeExtension().getCabacBypassAlignmentEnabledFlag() &&
                       !sps.getSpsRangeExtension().getPersistentRiceAdaptationEnabledFlag() &&
+                      pps.getPpsRangeExtension().getLog2MaxTransformSkipBlockSize() == 2 &&  // device: TS flag for 4x4 only
                       m_numContextModels <= HVX_NUM_CTX;
   if (!ported) {
     if (bin && g_cw.on()) g_cw.fallback++;
@@ -143,7 +144,8 @@ Void TEncSbac::codeCoeffNxN(TComTU &rTu, TCoeff *pcCoef, const ComponentID compI
   uint8_t st[HVX_NUM_CTX];
   memset(st, 0, sizeof(st));
   for (UInt i = 0; i < m_numContextModels; i++) st[i] = m_contextModels[i].m_ucState;
-  hvx_cabac_regs r = {bin->m_uiLow, bin->m_uiRange, bin->m_bitsLeft, bin->m_numBufferedBytes, bin->m_bufferedByte, 0};
+  hvx_cabac_regs r = {bin->m_uiLow, bin->m_uiRange, bin->m_bitsLeft, bin->m_numBufferedBytes, bin->m_bufferedByte, 0,
+                      {0, 0, 0, 0, 0}};
   check(hvx_upload(c, g_cw.d_desc, &d, sizeof(d)), "hvx_upload");
   check(hvx_upload(c, g_cw.d_lev, lev, sizeof(int32_t) * w * h), "hvx_upload");
   check(hvx_upload(c, g_cw.d_states, st, HVX_NUM_CTX), "hvx_upload");
@@ -171,6 +173,10 @@ Void TEncSbac::codeCoeffNxN(TComTU &rTu, TCoeff *pcCoef, const ComponentID compI
   bin->m_bufferedByte = r.buffered_byte;
   bin->m_uiBinsCoded += r.bins * bin->m_binCountIncrement;
   for (UInt i = 0; i < m_numContextModels; i++) m_contextModels[i].m_ucState = st[i];
+  // encodeBin's setBinsCoded(1) (TEncBinCoderCABAC.cpp:203) for every context the writer coded:
+  // determineCabacInitIdx (ContextModel3DBuffer::calcCost) reads it for the next slice's table
+  for (UInt m = 42; m < 202 && m < m_numContextModels; m++)
+    if ((r.coded[(m - 42) >> 5] >> ((m - 42) & 31)) & 1u) m_contextModels[m].setBinsCoded(1);
   g_cw.served++;
   g_cw.nbytes += len;
 }

@@ -356,7 +356,11 @@ def coeff_write(desc, levels, states, regs, cap=1 << 16):
     st = np.zeros(256, np.uint8)
     st[:len(states)] = states
     r = np.zeros(1, _abi.CABAC_REGS)
-    r[0] = (tuple(regs) + (0,))[:6] if not isinstance(regs, np.void) else regs
+    if isinstance(regs, np.void):
+        r[0] = regs
+    else:  # (low, range, bits_left, num_buffered, buffered_byte[, bins[, coded]])
+        t = tuple(regs)
+        r[0] = tuple(t[:6]) + (0,) * (6 - len(t[:6])) + (t[6] if len(t) > 6 else (0,) * 5,)
     out = np.zeros(cap, np.uint8)
     L.hvxo_coeff_write.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int]
     L.hvxo_coeff_write.restype = ctypes.c_int

@@ -2007,6 +2007,7 @@ static void cab_bin(cab_counter *c, int ctx, int v) {
   if (c->w) {
     hvx_cabac_regs *r = c->w;
     r->bins++;
+    if (ctx >= 42 && ctx < 202) r->coded[(ctx - 42) >> 5] |= 1u << ((ctx - 42) & 31);
     const uint32_t lps = kLpsTable[p][(r->range >> 6) & 3];
     r->range -= lps;
     if (v != mps) {

@@ -536,6 +536,8 @@ def check_coeff_write_random(seed, n_streams, max_tus):
         fields = ("low", "range", "bits_left", "num_buffered", "buffered_byte", "bins")
         assert tuple(int(r[k][f]) for f in fields) == \
             tuple(int(rk[f]) if isinstance(rk, np.void) else int(rk[i]) for i, f in enumerate(fields)), (k, r[k], rk)
+        if isinstance(rk, np.void):  # the contexts the run coded (setBinsCoded)
+            np.testing.assert_array_equal(r[k]["coded"], rk["coded"], err_msg=f"run {k} coded")
         np.testing.assert_array_equal(st[k], sk, err_msg=f"run {k}")
         total += len(exp)
     return int(first[-1]), total

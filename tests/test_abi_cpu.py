@@ -266,11 +266,12 @@ def test_new_entry_points_reject_bad_arguments_without_a_gpu():
 def test_cabac_regs_layout_matches_c():
     # hvx_cabac_regs (hvx_types.h) = TEncBinCABAC's registers + the bin count; start() values
     from video_codecs_amd import _abi
-    assert _abi.CABAC_REGS.names == ("low", "range", "bits_left", "num_buffered", "buffered_byte", "bins")
-    assert [_abi.CABAC_REGS.fields[f][1] for f in _abi.CABAC_REGS.names] == [0, 4, 8, 12, 16, 20]
+    assert _abi.CABAC_REGS.names == ("low", "range", "bits_left", "num_buffered", "buffered_byte", "bins", "coded")
+    assert [_abi.CABAC_REGS.fields[f][1] for f in _abi.CABAC_REGS.names] == [0, 4, 8, 12, 16, 20, 24]
     assert _abi.CABAC_START[:5] == (0, 510, 23, 0, 0xFF)
     src = open(os.path.join(ROOT, "include", "hvx_types.h")).read()
     assert "typedef struct hvx_cabac_regs" in src and "uint32_t buffered_byte, bins;" in src
+    assert "uint32_t coded[5];\n} hvx_cabac_regs;" in src
 
 
 def test_sao_layout_matches_c():

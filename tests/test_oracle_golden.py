@@ -160,6 +160,11 @@ def test_coeff_write_golden():
         assert tuple(int(r[k]) for k in ("low", "range", "bits_left", "num_buffered", "buffered_byte")) == \
             tuple(int(x) for x in regs[i, 5:]), (i, r, regs[i])
         np.testing.assert_array_equal(st, g["states_after"][i], err_msg=f"record {i}")
+        # the coded-context map (setBinsCoded): every context whose state moved was coded, and only
+        # residual-syntax models 42..184 appear
+        coded = np.unpackbits(np.asarray(r["coded"], "<u4").view(np.uint8), bitorder="little")[:160]
+        moved = np.flatnonzero(g["states_before"][i][42:202] != g["states_after"][i][42:202])
+        assert coded[moved].all() and not coded[143:].any(), (i, moved, np.flatnonzero(coded))
         carries += int(regs[i, 8] > 1)
     assert carries > 0  # runs of 0xff bytes held back for a carry occur in the stream
 

@@ -124,9 +124,9 @@ COEFF_BITS = np.dtype([("frac_bits", "<u8"), ("rice_stat", "<u4"), ("num_sig", "
 assert COEFF_BITS.itemsize == 16
 # hvx_cabac_regs (hvx_types.h): TEncBinCABAC's registers; CABAC_START = TEncBinCABAC::start()
 CABAC_REGS = np.dtype([("low", "<u4"), ("range", "<u4"), ("bits_left", "<i4"), ("num_buffered", "<i4"),
-                       ("buffered_byte", "<u4"), ("bins", "<u4")])
-assert CABAC_REGS.itemsize == 24
-CABAC_START = (0, 510, 23, 0, 0xFF, 0)
+                       ("buffered_byte", "<u4"), ("bins", "<u4"), ("coded", "<u4", (5,))])
+assert CABAC_REGS.itemsize == 44
+CABAC_START = (0, 510, 23, 0, 0xFF, 0, (0, 0, 0, 0, 0))
 NUM_CTX = 202
 
 # hvx_cu_decision (hvx_types.h)

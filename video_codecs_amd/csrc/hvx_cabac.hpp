@@ -300,6 +300,8 @@ struct Writer {
   uint8_t *out;
   int nout, cap;
   uint32_t bins;         // bins coded (m_uiBinsCoded with m_binCountIncrement 1)
+  uint64_t cd0, cd1;     // contexts coded (setBinsCoded(1)): rows 0..63, 64..127
+  uint32_t cd2;          //   rows 128..142
   __device__ __forceinline__ void put(uint32_t b) {
     if (nout < cap) out[nout] = (uint8_t)b;
     nout++;
@@ -328,6 +330,9 @@ struct Writer {
   // encodeBin (:200) + ContextModel::update
   __device__ __forceinline__ void bin(int row, int v) {
     bins++;
+    if (row < 64) cd0 |= 1ull << row;
+    else if (row < 128) cd1 |= 1ull << (row - 64);
+    else cd2 |= 1u << (row - 128);
     uint8_t &st = col[row * 64];
     const int q = st, mps = q & 1;
     const uint32_t l = lps[(q >> 1) * 4 + ((range >> 6) & 3)];
@@ -523,26 +528,36 @@ static __global__ __launch_bounds__(64) void k_coeff_write(const hvx_tu_desc *__
   cab::states_load(s, states, (size_t)HVX_NUM_CTX, k0, cnt);
   __syncthreads();
   if (lane < cnt) {
+    // every descriptor of the run is validated before anything is coded, so a run refused with
+    // -2 leaves its registers and states untouched (the caller can fall back from a consistent
+    // point).  Unsupported: non-square or non-4..32 TUs, scan types > 2, and persistent Rice
+    // adaptation (its statistic would have to carry across the TUs of a run).
+    bool ok = true;
+    for (int t = stream_first[k]; t < stream_first[k + 1]; t++) {
+      const hvx_tu_desc &d = descs[t];
+      ok = ok && (d.width == 4 || d.width == 8 || d.width == 16 || d.width == 32) && d.height == d.width &&
+           (unsigned)d.scan_type <= 2u && d.persistent_rice == 0;
+    }
     const hvx_cabac_regs r0 = regs[k];
     cab::Writer W{&s.st[lane], &s, lps, r0.low, r0.range, r0.bits_left, r0.num_buffered, r0.buffered_byte,
-                  out + out_off[k], 0, out_cap, r0.bins};
-    bool ok = true;
+                  out + out_off[k], 0, out_cap, r0.bins,
+                  (uint64_t)r0.coded[0] | ((uint64_t)r0.coded[1] << 32), (uint64_t)r0.coded[2] | ((uint64_t)r0.coded[3] << 32),
+                  r0.coded[4]};
     for (int t = stream_first[k]; t < stream_first[k + 1] && ok; t++) {
       const hvx_tu_desc d = descs[t];
-      if ((d.width == 4 || d.width == 8 || d.width == 16 || d.width == 32) && d.height == d.width &&
-          (unsigned)d.scan_type <= 2u) {
-        const int32_t *lv = levels + offs[t];
-        const uint16_t *scan = kScan[d.scan_type] + scan_base(cab::log2_tu(d.width) - 2);
-        uint32_t rice = (uint32_t)d.golomb_rice_stat;
-        cab::coeff_bits(d, [&](int sp) { return lv[scan[sp]]; }, W, rice);
-      } else {
-        ok = false;
-      }
+      const int32_t *lv = levels + offs[t];
+      const uint16_t *scan = kScan[d.scan_type] + scan_base(cab::log2_tu(d.width) - 2);
+      uint32_t rice = (uint32_t)d.golomb_rice_stat;
+      cab::coeff_bits(d, [&](int sp) { return lv[scan[sp]]; }, W, rice);
     }
-    hvx_cabac_regs r1;
-    r1.low = W.low; r1.range = W.range; r1.bits_left = W.bits_left; r1.num_buffered = W.nbuf;
-    r1.buffered_byte = W.buffered; r1.bins = W.bins;
-    regs[k] = r1;
+    if (ok) {
+      hvx_cabac_regs r1;
+      r1.low = W.low; r1.range = W.range; r1.bits_left = W.bits_left; r1.num_buffered = W.nbuf;
+      r1.buffered_byte = W.buffered; r1.bins = W.bins;
+      r1.coded[0] = (uint32_t)W.cd0; r1.coded[1] = (uint32_t)(W.cd0 >> 32);
+      r1.coded[2] = (uint32_t)W.cd1; r1.coded[3] = (uint32_t)(W.cd1 >> 32); r1.coded[4] = W.cd2;
+      regs[k] = r1;
+    }
     out_len[k] = !ok ? -2 : W.nout <= out_cap ? W.nout : -1;
   }
   __syncthreads();

@@ -896,9 +896,10 @@ struct RegCoder {
     const int p = st >> 1, mps = st & 1;
     const int ns = v == mps ? (((p < 62 ? p + 1 : p) << 1) | mps)
                             : ((__builtin_amdgcn_readlane(lps, p) << 1) | (p == 0 ? mps ^ 1 : mps));
-    if (k == 0) r0 = __builtin_amdgcn_writelane(ns, ln, r0);
-    else if (k == 1) r1 = __builtin_amdgcn_writelane(ns, ln, r1);
-    else r2 = __builtin_amdgcn_writelane(ns, ln, r2);
+    const bool mine = lid() == ln;  // v_writelane as a compare + select
+    if (k == 0) r0 = mine ? ns : r0;
+    else if (k == 1) r1 = mine ? ns : r1;
+    else r2 = mine ? ns : r2;
   }
   __device__ __forceinline__ void ep(int n) { frac += 32768ull * (uint32_t)n; }
   __device__ __forceinline__ void ep_bits(uint32_t, int n) { ep(n); }
@@ -918,6 +919,7 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
   const uint16_t *scan = kScan[d.scan_type] + scan_base(ilog2(d.width) - 2);
   int16_t *ls = E.u.cstage;
   for (int i = lid(); i < n; i += 64) ls[i] = coef[scan[i]];
+#ifndef HM_LDS_CODER
   RegCoder L;
   L.load(E.cod[E.cur].st);
   wsync();
@@ -925,6 +927,13 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
   cab::coeff_bits(d, [&](int sp) { return (int)ls[sp]; }, L, rice);
   L.store(E.cod[E.cur].st);
   E.cod[E.cur].frac += L.frac;
+#else
+  CoderLane L{E.cod[E.cur].st, 0};
+  wsync();
+  uint32_t rice = 0;
+  cab::coeff_bits(d, [&](int sp) { return (int)ls[sp]; }, L, rice);
+  E.cod[E.cur].frac += L.frac;
+#endif
   wsync();
 }
 // TEncEntropy::estimateBit (TEncEntropy.cpp:685) from the current coder
