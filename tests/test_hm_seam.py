@@ -63,3 +63,33 @@ def test_hm_encoder_with_hvx_seams(case, monkeypatch):
 
 def test_expected_md5_cases_present():
     assert set(EXPECTED) == set(mk.CASES)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)  # one synchronous single-CTU launch per compressCtu call: correctness, not speed
+@pytest.mark.parametrize("case", ["ldp_rand_qp32"])
+def test_hm_encoder_with_cu_seam(case, monkeypatch):
+    """The L3 boundary: every TEncCu::compressCtu of an unchanged TAppEncoder LDP encode (I + P
+    pictures) served by the HM-exact CTU engine (integration/hm_cu_seam.cpp -> hvx_hm_compress),
+    HM's own encodeCtu / loop filters / SAO / slice writer (with the device deblocking, SAO and
+    residual-writer seams) downstream: the bitstream and reconstruction MD5 of the reference."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if not os.path.exists(EXE):
+        pytest.skip("TAppEncoder_hvx not built (needs /root/reference at build time)")
+    monkeypatch.setenv("HVX_SEAM_CU", "1")
+    monkeypatch.setenv("HVX_SEAM_INTRA", "0")
+    log = []
+    with tempfile.TemporaryDirectory() as tmp:
+        got = mk.encode(EXE, case, tmp, log)
+    print(log[0][-600:])
+    m = re.search(r"hm_cu_seam: (\d+) compressCtu calls served by libhvx \((\d+) pictures\), (\d+) fell through", log[0])
+    assert m, log[0][-2000:]
+    frames = mk.CASES[case][2]
+    ctus = ((mk.W + 63) // 64) * ((mk.H + 63) // 64)
+    assert int(m.group(1)) == frames * ctus and int(m.group(2)) == frames and int(m.group(3)) == 0, m.group(0)
+    assert got == EXPECTED[case], (case, got, EXPECTED[case])
+    # with every CTU decided on the device, HM's own motion search is never reached
+    m = re.search(r"hm_me_seam: (\d+) xMotionEstimation calls served .* (\d+) fell through", log[0])
+    assert m is None or (int(m.group(1)) == 0 and int(m.group(2)) == 0), m.group(0)

@@ -112,17 +112,58 @@ __device__ __forceinline__ int sig_ctx(int pattern, int first_sig, int single, i
   return first_sig + offset;
 }
 
+// firstSignificanceMapContext (getTUEntropyCodingParameters, TComChromaFormat.cpp:96)
+__device__ __forceinline__ int first_sig_ctx(const hvx_tu_desc &d, int n, int ch) {
+  const int single = ch ? 15 : 27;
+  if (d.ts_context && (d.transquant_bypass || d.transform_skip)) return single;
+  if (n == 4) return 0;
+  if (n == 8) return 9 + ((d.scan_type != 0 && !ch) ? 6 : 0);
+  return ch ? 12 : 21;
+}
+
+// The scan geometry coeff_bits reads, from the constant tables: the CG scan (scan_cg[sub]),
+// the grouped scan (raster of scan position sp) and the significance context of a position
+// under a neighbour-CG pattern.  The HM engine substitutes a view of the same values staged in
+// LDS (hvx_hm.hpp code_coeff_nxn), so its serial syntax walk issues no global-memory loads.
+struct ScanTables {
+  const uint8_t *scan_cg;
+  const uint16_t *scan;
+  int lw, ch, first_sig, single;
+  __device__ __forceinline__ ScanTables(const hvx_tu_desc &d) {
+    const int n = d.width, l = log2_tu(n) - 2;
+    lw = l + 2;
+    ch = d.comp ? 1 : 0;
+    scan_cg = kScanCG[d.scan_type] + cg_base(l);
+    scan = kScan[d.scan_type] + scan_base(l);
+    first_sig = first_sig_ctx(d, n, ch);
+    single = ch ? 15 : 27;
+  }
+  __device__ __forceinline__ int cg(int sub) const { return scan_cg[sub]; }
+  __device__ __forceinline__ int raster(int sp) const { return scan[sp]; }
+  __device__ __forceinline__ int sigc(int pattern, int sp) const;
+};
+
+template <class LevAt, class C, class Env>
+__device__ __forceinline__ int coeff_bits_env(const hvx_tu_desc &d, const Env &env, LevAt lev, C &L, uint32_t &rice_stat);
+
+__device__ __forceinline__ int ScanTables::sigc(int pattern, int sp) const {
+  return sig_ctx(pattern, first_sig, single, scan[sp], lw, ch);
+}
+
 // codeCoeffNxN for one square TU.  lev(sp) returns the level at GROUPED SCAN position sp
 // (scan = kScan[scan_type] at the TU's size).  Returns num_sig; frac accumulates in L.
+template <class LevAt, class C>
+__device__ __forceinline__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, C &L, uint32_t &rice_stat) {
+  return coeff_bits_env(d, ScanTables(d), lev, L, rice_stat);
+}
+
 // Coefficient groups are the unit of work: each group's 16 levels are fetched by 16
 // independent loads into registers (fully unrolled, static indices), so a group costs one
 // memory latency, and every later pass over the group reads registers.
-template <class LevAt, class C>
-__device__ __forceinline__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, C &L, uint32_t &rice_stat) {
-  const int n = d.width, lw = log2_tu(n), l = lw - 2, wg = n >> 2, ncg = wg * wg;
+template <class LevAt, class C, class Env>
+__device__ __forceinline__ int coeff_bits_env(const hvx_tu_desc &d, const Env &env, LevAt lev, C &L, uint32_t &rice_stat) {
+  const int n = d.width, lw = log2_tu(n), wg = n >> 2, ncg = wg * wg;
   const int ch = d.comp ? 1 : 0;
-  const uint8_t *scan_cg = kScanCG[d.scan_type] + cg_base(l);
-  const uint16_t *scan = kScan[d.scan_type] + scan_base(l);
   // significant-CG map (raster CG index), the last significant scan position, the count
   uint64_t cgm = 0;
   int num_sig = 0, scan_last = -1;
@@ -131,7 +172,7 @@ __device__ __forceinline__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, C &L,
 #pragma unroll
     for (int k = 0; k < 16; k++) m |= (uint32_t)(lev(sub * 16 + k) != 0) << k;
     if (m) {
-      cgm |= 1ull << scan_cg[sub];
+      cgm |= 1ull << env.cg(sub);
       num_sig += __popc(m);
       scan_last = sub * 16 + 31 - __clz(m);
     }
@@ -139,16 +180,9 @@ __device__ __forceinline__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, C &L,
   if (num_sig == 0) return 0;  // the reference exits here (empty TU); nothing is coded
   const bool be_valid = d.transquant_bypass ? false : (d.sign_hiding != 0);
   if (d.pps_tskip && !d.transquant_bypass && n <= 4) L.bin(kTskip + ch, d.transform_skip ? 1 : 0);
-  // firstSignificanceMapContext (getTUEntropyCodingParameters, TComChromaFormat.cpp:96)
-  const int single = ch ? 15 : 27;
-  int first_sig;
-  if (d.ts_context && (d.transquant_bypass || d.transform_skip)) first_sig = single;
-  else if (n == 4) first_sig = 0;
-  else if (n == 8) first_sig = 9 + ((d.scan_type != 0 && !ch) ? 6 : 0);
-  else first_sig = ch ? 12 : 21;
   // codeLastSignificantXY (:1115)
   {
-    const int r = scan[scan_last];
+    const int r = env.raster(scan_last);
     int py = r >> lw, px = r - (py << lw);
     if (d.scan_type == 2) { const int t = px; px = py; py = t; }
     const int gx = kGroupIdx[px], gy = kGroupIdx[py], gmax = kGroupIdx[n - 1];
@@ -169,7 +203,7 @@ __device__ __forceinline__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, C &L,
   int c1 = 1;
   for (int sub = last_set; sub >= 0; sub--) {
     const int sub_pos = sub << 4;
-    const int cg = scan_cg[sub], cgy = cg / wg, cgx = cg - cgy * wg;
+    const int cg = env.cg(sub), cgy = cg / wg, cgx = cg - cgy * wg;
     int a[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) a[k] = lev(sub_pos + k);
@@ -197,7 +231,7 @@ __device__ __forceinline__ int coeff_bits(const hvx_tu_desc &d, LevAt lev, C &L,
       for (int pin = 15; pin >= 0; pin--) {
         if (is_last_set && pin >= last_pin) continue;
         const int sig = a[pin] != 0;
-        if (pin > 0 || sub == 0 || nnz) L.bin(base_sig + sig_ctx(pattern, first_sig, single, scan[sub_pos + pin], lw, ch), sig);
+        if (pin > 0 || sub == 0 || nnz) L.bin(base_sig + env.sigc(pattern, sub_pos + pin), sig);
         if (sig) {
           nnz++;
           signs = 2 * signs + (uint32_t)(a[pin] < 0);

@@ -135,7 +135,12 @@ union Leaf {
   TuSmem<1> tu1;
   TuSmem<2> tu2;
   IntraScratch in;
-  int16_t cstage[1024];  // codeCoeffNxN's levels in scan order
+  struct {               // codeCoeffNxN's TU staged in scan order (code_coeff_nxn)
+    int16_t lev[1024];   // levels
+    int16_t ras[256];    // raster position (TUs up to 16x16)
+    int32_t sig[256];    // significance context under neighbour-CG patterns 0..3, 6 bits each
+    uint8_t cg[16];      // CG scan -> CG raster
+  } cs;
 };
 
 // the decision's LDS-resident context (TEncCu / TEncSearch / TComTrQuant scalars + coders)
@@ -909,17 +914,44 @@ struct RegCoder {
   }
 };
 
-// codeCoeffNxN on the current coder, levels TU-packed int16: the levels are first staged in
-// LDS in scan order by the whole wave (one memory latency), the syntax walk then reads LDS
+// the scan geometry of a TU staged in LDS (cab::ScanTables' values; TUs up to 16x16)
+struct StagedScan {
+  const uint8_t *cgs;
+  const int16_t *ras;
+  const int32_t *sig;
+  __device__ __forceinline__ int cg(int sub) const { return cgs[sub]; }
+  __device__ __forceinline__ int raster(int sp) const { return ras[sp]; }
+  __device__ __forceinline__ int sigc(int pattern, int sp) const { return (sig[sp] >> (6 * pattern)) & 63; }
+};
+
+// codeCoeffNxN on the current coder, levels TU-packed int16.  The whole wave first stages the TU
+// in LDS in scan order -- levels, raster positions, the significance context of every position
+// under the four neighbour-CG patterns, the CG scan -- with one round of table and level loads;
+// the serial syntax walk then reads LDS only (no global-memory latency on its chain).
 __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_t *coef) {
   HM_PROF(PR_COEF);
   hvx_tu_desc d;
   tu_desc(cu, t, comp, d);
   const int n = d.width * d.width;
   const uint16_t *scan = kScan[d.scan_type] + scan_base(ilog2(d.width) - 2);
-  int16_t *ls = E.u.cstage;
-  for (int i = lid(); i < n; i += 64) ls[i] = coef[scan[i]];
-#ifndef HM_LDS_CODER
+  int16_t *ls = E.u.cs.lev;
+  const bool staged = n <= 256;
+  if (staged) {
+    const cab::ScanTables tab(d);
+    for (int i = lid(); i < n; i += 64) {
+      const int r = scan[i];
+      ls[i] = coef[r];
+      E.u.cs.ras[i] = (int16_t)r;
+      int sc = 0;
+#pragma unroll
+      for (int pat = 0; pat < 4; pat++) sc |= cab::sig_ctx(pat, tab.first_sig, tab.single, r, tab.lw, tab.ch) << (6 * pat);
+      E.u.cs.sig[i] = sc;
+    }
+    if (lid() < (n >> 4)) E.u.cs.cg[lid()] = tab.scan_cg[lid()];
+  } else {
+    for (int i = lid(); i < n; i += 64) ls[i] = coef[scan[i]];
+  }
+#ifdef HM_REG_CODER
   RegCoder L;
   L.load(E.cod[E.cur].st);
   wsync();
@@ -931,7 +963,8 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
   CoderLane L{E.cod[E.cur].st, 0};
   wsync();
   uint32_t rice = 0;
-  cab::coeff_bits(d, [&](int sp) { return (int)ls[sp]; }, L, rice);
+  if (staged) cab::coeff_bits_env(d, StagedScan{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig}, [&](int sp) { return (int)ls[sp]; }, L, rice);
+  else cab::coeff_bits(d, [&](int sp) { return (int)ls[sp]; }, L, rice);
   E.cod[E.cur].frac += L.frac;
 #endif
   wsync();
