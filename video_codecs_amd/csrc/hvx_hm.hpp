@@ -232,15 +232,24 @@ __device__ __forceinline__ void cload(int dst, int src) {
   wsync();
 }
 
+// wave-uniform values read from LDS, moved to scalar registers (HM_SCALAR builds): the serial
+// logic on them becomes scalar arithmetic and branches instead of VALU work under exec masks --
+// measured 7% slower (the readfirstlane round trips lengthen the dependent chains), so off
+#ifdef HM_SCALAR
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+#else
+__device__ __forceinline__ int uni(int v) { return v; }
+#endif
+
 // the coefficient-rate lane of cab::coeff_bits on one coder (models 42..184)
 struct CoderLane {
   uint8_t *st;
   uint64_t frac;
   __device__ __forceinline__ void bin(int row, int v) {
-    uint8_t &s = st[row + cab::kCtxLo];
-    const int q = s;
-    frac += (uint32_t)E.eb[q ^ v];
-    s = E.next[q * 2 + v];
+    uint8_t &s = st[uni(row) + cab::kCtxLo];
+    const int q = uni(s), bv = uni(v);
+    frac += (uint32_t)uni(E.eb[q ^ bv]);
+    s = (uint8_t)uni(E.next[q * 2 + bv]);
   }
   __device__ __forceinline__ void ep(int n) { frac += 32768ull * (uint32_t)n; }
   __device__ __forceinline__ void ep_bits(uint32_t, int n) { ep(n); }
@@ -866,6 +875,12 @@ __device__ void tu_desc(const Cu *cu, const Tu &t, int comp, hvx_tu_desc &d) {
   d.max_log2_tr_range = 15;
   d.bit_depth = 8;
   d.lambda = E.P.tq_lambda[comp];
+#ifdef HM_SCALAR
+  // every field is wave-uniform (read from the CU object in memory): scalar registers
+  int32_t *w = reinterpret_cast<int32_t *>(&d);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(d) / 4); k++) w[k] = __builtin_amdgcn_readfirstlane(w[k]);
+#endif
 }
 // The coefficient contexts of one coder held in registers for the duration of a TU's
 // codeCoeffNxN: row r (model kCtxLo + r) in lane r & 63 of VGPR r >> 6, the entropy-bit table
@@ -919,9 +934,9 @@ struct StagedScan {
   const uint8_t *cgs;
   const int16_t *ras;
   const int32_t *sig;
-  __device__ __forceinline__ int cg(int sub) const { return cgs[sub]; }
-  __device__ __forceinline__ int raster(int sp) const { return ras[sp]; }
-  __device__ __forceinline__ int sigc(int pattern, int sp) const { return (sig[sp] >> (6 * pattern)) & 63; }
+  __device__ __forceinline__ int cg(int sub) const { return uni(cgs[sub]); }
+  __device__ __forceinline__ int raster(int sp) const { return uni(ras[sp]); }
+  __device__ __forceinline__ int sigc(int pattern, int sp) const { return (uni(sig[sp]) >> (6 * pattern)) & 63; }
 };
 
 // codeCoeffNxN on the current coder, levels TU-packed int16.  The whole wave first stages the TU
@@ -963,8 +978,8 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
   CoderLane L{E.cod[E.cur].st, 0};
   wsync();
   uint32_t rice = 0;
-  if (staged) cab::coeff_bits_env(d, StagedScan{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig}, [&](int sp) { return (int)ls[sp]; }, L, rice);
-  else cab::coeff_bits(d, [&](int sp) { return (int)ls[sp]; }, L, rice);
+  if (staged) cab::coeff_bits_env(d, StagedScan{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig}, [&](int sp) { return uni(ls[sp]); }, L, rice);
+  else cab::coeff_bits(d, [&](int sp) { return uni(ls[sp]); }, L, rice);
   E.cod[E.cur].frac += L.frac;
 #endif
   wsync();
