@@ -772,9 +772,59 @@ static void tu_desc(const hm_enc *e, const hm_cu *cu, const tu_t *t, int comp, h
   d->golomb_rice_stat = 0;
   d->lambda = P->tq_lambda[comp];
 }
+#ifdef HVXO_MEMO_STATS
+/* measurement aid (not in the normal build): how often codeCoeffNxN repeats a count it made
+ * recently -- same TU content, same descriptor, same context states before (FIFOs of K entries) */
+#include <stdio.h>
+#define MEMO_KS 6
+static const int memo_k[MEMO_KS] = {1, 2, 4, 8, 16, 64};
+typedef struct { int valid, w, comp, scan, ts; int32_t coef[1024]; uint8_t st[202]; } memo_e;
+static memo_e memo[MEMO_KS][64];
+static int memo_pos[MEMO_KS];
+static long long memo_calls[6], memo_hits[MEMO_KS][6];
+static void memo_report(void) {
+  for (int z = 0; z < 4; z++) {
+    fprintf(stderr, "memo TU %2d: %lld calls;", 4 << z, memo_calls[z]);
+    for (int k = 0; k < MEMO_KS; k++) fprintf(stderr, " K=%d %.1f%%", memo_k[k], memo_calls[z] ? 100.0 * memo_hits[k][z] / memo_calls[z] : 0.0);
+    fprintf(stderr, "\n");
+  }
+}
+/* the context rows codeCoeffNxN of a channel reads or writes (TEncSbac.cpp:62-92 offsets) */
+static int memo_same_ctx(const uint8_t *a, const uint8_t *b, int ch) {
+  static const int lo[7][2] = {{42, 2}, {46, 27}, {90, 15}, {120, 15}, {150, 16}, {174, 4}, {183, 1}};
+  static const int lc[7][2] = {{44, 2}, {74, 16}, {105, 15}, {135, 15}, {166, 8}, {178, 2}, {184, 1}};
+  for (int r = 0; r < 7; r++) {
+    const int o = ch ? lc[r][0] : lo[r][0], k = ch ? lc[r][1] : lo[r][1];
+    if (memcmp(a + o, b + o, k)) return 0;
+  }
+  return 1;
+}
+static void memo_probe(const hvx_tu_desc *d, const int32_t *coef, const uint8_t *st) {
+  static int reg = 0;
+  if (!reg) { reg = 1; atexit(memo_report); }
+  const int z = d->width == 4 ? 0 : d->width == 8 ? 1 : d->width == 16 ? 2 : 3, n = d->width * d->width;
+  memo_calls[z]++;
+  for (int k = 0; k < MEMO_KS; k++) {
+    int hit = 0;
+    for (int i = 0; i < memo_k[k] && !hit; i++) {
+      const memo_e *m = &memo[k][i];
+      hit = m->valid && m->w == d->width && m->comp == d->comp && m->scan == d->scan_type && m->ts == d->transform_skip &&
+            !memcmp(m->coef, coef, 4 * n) && memo_same_ctx(m->st, st, d->comp ? 1 : 0);
+    }
+    if (hit) { memo_hits[k][z]++; continue; }
+    memo_e *m = &memo[k][memo_pos[k]];
+    memo_pos[k] = (memo_pos[k] + 1) % memo_k[k];
+    m->valid = 1; m->w = d->width; m->comp = d->comp; m->scan = d->scan_type; m->ts = d->transform_skip;
+    memcpy(m->coef, coef, 4 * n); memcpy(m->st, st, 202);
+  }
+}
+#endif
 static void code_coeff_nxn(hm_enc *e, const hm_cu *cu, const tu_t *t, int comp, const int32_t *coef) {
   hvx_tu_desc d;
   tu_desc(e, cu, t, comp, &d);
+#ifdef HVXO_MEMO_STATS
+  memo_probe(&d, coef, e->cur->st);
+#endif
   hvx_coeff_bits o;
   hvxo_coeff_bits(&d, coef, e->cur->st, e->pic->entropy_bits, &o);
   e->cur->frac += o.frac_bits;

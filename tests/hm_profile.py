@@ -7,7 +7,10 @@ import numpy as np
 
 from tests import hm_cases
 
-NAMES = ["ME", "MC", "TPL", "TUF", "TUI", "COEF", "EST", "IFP", "IPRED", "DIST", "CTU", "ENC", "TUF4", "TUF8", "TUF16", "TUF32"]
+NAMES = ["ME", "MC", "TPL", "TUF", "TUI", "COEF", "EST", "IFP", "IPRED", "DIST", "CTU", "ENC", "TUF4", "TUF8", "TUF16", "TUF32",
+         "C.desc", "C.stage", "C.walk", "T.in", "T.fwd", "T.out", "xform", "rdoq", "COEF4", "COEF8", "COEF16", "COEF32",
+         "rdoqA", "rdoqB", "rdoqC", "rdoqDE"]
+NPROF = 32
 
 def report(prof, n, head):
     prof = prof.astype(np.float64)
@@ -37,8 +40,8 @@ def bench_profile(pics, steps):
         torch.cuda.synchronize()
         dt = time.time() - t0
         sb = w.eng.reserve(w.n_jobs)
-        st = w.eng.state[:w.n_jobs * sb].view(w.n_jobs, sb)[:, :272].cpu().numpy().copy()
-        prof = st[:, 16:272].copy().view(np.uint64).reshape(w.n_jobs, 2, 16)
+        st = w.eng.state[:w.n_jobs * sb].view(w.n_jobs, sb)[:, :16 + 16 * NPROF].cpu().numpy().copy()
+        prof = st[:, 16:16 + 16 * NPROF].copy().view(np.uint64).reshape(w.n_jobs, 2, NPROF)
         report(prof, w.n_jobs, "bench step %d: %d chains, %.3f s" % (s, w.n_jobs, dt))
 
 

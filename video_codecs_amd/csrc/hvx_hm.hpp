@@ -24,6 +24,10 @@
 // oracle, against the reference's own compressCtu decisions (tests/golden/ctu_ldp_*.bin).
 #pragma once
 #include "hvx_dev.hpp"
+#ifdef HM_PROFILE
+__device__ void hm_prof_add(int cat, uint64_t dt);
+#define HVX_TU_PROF_HOOK(cat, dt) hm_prof_add((cat), (dt))
+#endif
 #include "hvx_tu.hpp"
 #include "hvx_cabac.hpp"
 #include "hvx_estbit.hpp"
@@ -101,10 +105,25 @@ struct IntraScratch {
   int n_cand, pad_;
   uint8_t cand[12];
 };
+// A codeCoeffNxN count of a 4x4 / 8x8 TU, remembered: its result (the bits it added, the context
+// states it left) is a function of the TU's levels, its descriptor fields the walk reads (width,
+// channel, scan, transform skip) and the states of the channel's coefficient contexts before the
+// count.  The RQT counts the same TU from the same states several times (the per-component test
+// from CI_QT_TRAFO_ROOT, the node's single-bits recount, the parent's split recount, the CU's
+// final count), so a chain keeps its last kMemoK counts (FIFO) and replays a repeated one.
+// Context rows 40..187 as 37 dwords; a per-channel byte mask selects the rows the walk touches.
+constexpr int kMemoK = 16, kMemoDw = 37, kMemoDw0 = 10;
+struct CoefMemo {
+  uint32_t key;                   // valid | width | channel | scan | transform skip
+  uint32_t pad_;
+  uint64_t frac;
+  uint32_t coef[32];              // the TU's levels as int16 pairs (TU-packed order)
+  uint32_t before[kMemoDw], after[kMemoDw];
+};
 // per-chain state in HBM
 struct State {
   int dbg[4];  // HM_CHECKS: E.dbg of the last CTU
-  uint64_t prof[2][16];  // HM_PROFILE: per-category clock ticks and calls of the job
+  uint64_t prof[2][32];  // HM_PROFILE: per-category clock ticks and calls of the job
   Cu cu[8];
   Yuv yuv[28];                    // TComYuv sets (kind x depth), addressed through hm_e.yi
   Yuv qt_yuv[4], qt_ts_yuv, tmp_yuv_pred;
@@ -122,6 +141,8 @@ struct State {
   uint8_t win[6144];              // its reconstruction: Y 64x64 | Cb 32x32 | Cr 32x32
   int16_t int2n[2][4][2];         // TEncSearch::m_integerMv2Nx2N
   Coder carry;                    // the RD coder after the chain's last encodeCtu (HVX_HM_RESUME)
+  CoefMemo memo[kMemoK];          // codeCoeffNxN counts of 4x4 / 8x8 TUs the chain made recently
+  int memo_next;
   MeScratch me;                   // leaf scratch outside LDS
   McScratch mc;
   TuSmem<3> tu3;
@@ -157,15 +178,24 @@ struct Enc {
   hvx_estbits est;
   int32_t eb[128];
   uint8_t next[256];
+  uint16_t scan[256];    // the current TU's scan tables (TUs up to 16x16), staged by tu_fwd_l
+  uint8_t scan_cg[16];
   uint32_t avail[4];
   int dbg[4];  // HM_CHECKS: first violated check (code, a, b) of the job
   int stage, stop;  // HM_CHECKS: stop the CTU at debugging stage `stage` (0: never)
-  uint64_t prof[2][16];  // HM_PROFILE accumulators
+  uint64_t prof[2][32];  // HM_PROFILE accumulators
   Leaf u;
 };
 }  // namespace hm
 
 __shared__ hm::Enc hm_e;
+
+#ifdef HM_PROFILE
+__device__ void hm_prof_add(int cat, uint64_t dt) {
+  hm_e.prof[0][cat] += dt;
+  hm_e.prof[1][cat] += 1;
+}
+#endif
 
 namespace hm {
 #define E hm_e
@@ -177,6 +207,10 @@ __device__ __forceinline__ void wsync() { __syncthreads(); }
 __device__ __forceinline__ int lid() { return (int)threadIdx.x; }
 // HM_PROFILE builds accumulate the clock ticks (s_memtime) and calls of the leaf categories
 enum { PR_ME, PR_MC, PR_TPL, PR_TUF, PR_TUI, PR_COEF, PR_EST, PR_IFP, PR_IPRED, PR_DIST, PR_CTU, PR_ENC, PR_N };
+// sub-phases (HM_PROFILE): 12..15 TUF by size; 16 COEF descriptor, 17 COEF staging, 18 COEF walk,
+// 19 TUF copy-in, 20 TUF forward (transform + quantisation), 21 TUF copy-out, 22 transform,
+// 23 RDOQ, 24..27 COEF by size
+enum { PR_COEF_DESC = 16, PR_COEF_STAGE, PR_COEF_WALK, PR_TUF_IN, PR_TUF_FWD, PR_TUF_OUT, PR_XFORM, PR_RDOQ, PR_COEF4 };
 #ifdef HM_PROFILE
 struct ProfScope {
   int cat;
@@ -188,7 +222,11 @@ struct ProfScope {
   }
 };
 #define HM_PROF(c) ProfScope prof_scope_(c)
+#define HM_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define HM_TADD(cat, v) (hm_e.prof[0][(cat)] += __builtin_amdgcn_s_memtime() - (v), hm_e.prof[1][(cat)] += 1)
 #else
+#define HM_T0(v) ((void)0)
+#define HM_TADD(cat, v) ((void)0)
 #define HM_PROF(c) ((void)0)
 #endif
 // HM_CHECKS builds validate the indices and sample positions below, record the first violation
@@ -943,10 +981,59 @@ struct StagedScan {
 // in LDS in scan order -- levels, raster positions, the significance context of every position
 // under the four neighbour-CG patterns, the CG scan -- with one round of table and level loads;
 // the serial syntax walk then reads LDS only (no global-memory latency on its chain).
+// the byte mask of dword k (rows 40 + 4k .. 43 + 4k) over the context rows codeCoeffNxN of channel
+// ch touches (TEncSbac.cpp:62-92: significant-CG, significance, last X / Y, greater-1, greater-2,
+// transform skip)
+__device__ __forceinline__ uint32_t memo_mask(int ch, int k) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const int r = 40 + 4 * k + b;
+    const bool in = ch ? ((r >= 44 && r <= 45) || (r >= 74 && r <= 89) || (r >= 105 && r <= 119) || (r >= 135 && r <= 149) ||
+                          (r >= 166 && r <= 173) || (r >= 178 && r <= 179) || r == 184)
+                       : ((r >= 42 && r <= 43) || (r >= 46 && r <= 72) || (r >= 90 && r <= 104) || (r >= 120 && r <= 134) ||
+                          (r >= 150 && r <= 165) || (r >= 174 && r <= 177) || r == 183);
+    m |= in ? 0xffu << (8 * b) : 0u;
+  }
+  return m;
+}
+
 __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_t *coef) {
   HM_PROF(PR_COEF);
+  HM_T0(t_desc);
   hvx_tu_desc d;
   tu_desc(cu, t, comp, d);
+  HM_TADD(PR_COEF_DESC, t_desc);
+  // the memo (4x4 / 8x8 TUs): one load round for the keys, one per candidate entry
+  const int ch = comp ? 1 : 0, l = lid();
+  const bool memo_on = d.width <= 8;
+  uint32_t cur_st = 0, cur_cf = 0, mask = 0, key = 0;
+  State *S = E.S;
+  if (memo_on) {
+    key = 0x8000u | (uint32_t)d.width | ((uint32_t)ch << 8) | ((uint32_t)d.scan_type << 10) | ((uint32_t)d.transform_skip << 12);
+    const int ndw = d.width * d.width / 2;
+    uint32_t *st32 = reinterpret_cast<uint32_t *>(E.cod[E.cur].st);
+    const uint32_t kk = l < kMemoK ? S->memo[l].key : 0u;
+    if (l < kMemoDw) { cur_st = st32[kMemoDw0 + l]; mask = memo_mask(ch, l); }
+    if (l < ndw) cur_cf = reinterpret_cast<const uint32_t *>(coef)[l];
+    uint64_t cand = __ballot(kk == key);
+    while (cand) {
+      const int e = __builtin_ctzll(cand);
+      cand &= cand - 1;
+      const CoefMemo &m = S->memo[e];
+      const bool diff = (l < kMemoDw && ((m.before[l] ^ cur_st) & mask)) || (l < ndw && m.coef[l] != cur_cf);
+      if (__ballot(diff) == 0) {  // a repeat: replay its result
+        const uint32_t after = l < kMemoDw ? m.after[l] : 0u;
+        const uint64_t f = m.frac;
+        wsync();
+        if (l < kMemoDw) st32[kMemoDw0 + l] = (cur_st & ~mask) | (after & mask);
+        if (l == 0) E.cod[E.cur].frac += f;
+        wsync();
+        return;
+      }
+    }
+  }
+  HM_T0(t_stage);
   const int n = d.width * d.width;
   const uint16_t *scan = kScan[d.scan_type] + scan_base(ilog2(d.width) - 2);
   int16_t *ls = E.u.cs.lev;
@@ -977,12 +1064,27 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
 #else
   CoderLane L{E.cod[E.cur].st, 0};
   wsync();
+  HM_TADD(PR_COEF_STAGE, t_stage);
+  HM_T0(t_walk);
   uint32_t rice = 0;
   if (staged) cab::coeff_bits_env(d, StagedScan{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig}, [&](int sp) { return uni(ls[sp]); }, L, rice);
   else cab::coeff_bits(d, [&](int sp) { return uni(ls[sp]); }, L, rice);
   E.cod[E.cur].frac += L.frac;
 #endif
   wsync();
+  HM_TADD(PR_COEF_WALK, t_walk);
+  HM_TADD(PR_COEF4 + ilog2(d.width) - 2, t_desc);
+#ifndef HM_REG_CODER
+  if (memo_on) {  // remember the count (FIFO slot)
+    const int slot = S->memo_next;
+    CoefMemo &m = S->memo[slot];
+    const uint32_t *st32 = reinterpret_cast<const uint32_t *>(E.cod[E.cur].st);
+    if (l < kMemoDw) { m.before[l] = cur_st; m.after[l] = st32[kMemoDw0 + l]; }
+    if (l < d.width * d.width / 2) m.coef[l] = cur_cf;
+    if (l == 0) { m.key = key; m.frac = L.frac; S->memo_next = slot + 1 == kMemoK ? 0 : slot + 1; }
+    wsync();
+  }
+#endif
 }
 // TEncEntropy::estimateBit (TEncEntropy.cpp:685) from the current coder
 // The entries TEncSbac::estBit writes (exactly those of estbit_update), one per lane: two
@@ -1214,11 +1316,24 @@ __device__ int32_t tu_fwd_l(const hvx_tu_desc &d, const int16_t *resi, int rs, i
 #endif
   TuSmem<L> &s = tu_smem<L>();
   constexpr int N = 4 << L;
-  for (int i = lid(); i < N * N; i += 64) s.a[i] = resi[(i >> (L + 2)) * rs + (i & (N - 1))];
+  HM_T0(t_in);
+  const uint16_t *scan_g = kScan[d.scan_type] + scan_base(L);
+  for (int i = lid(); i < N * N; i += 64) {
+    s.a[i] = resi[(i >> (L + 2)) * rs + (i & (N - 1))];
+    if constexpr (L < 3) E.scan[i] = scan_g[i];
+  }
+  if constexpr (L < 3)
+    if (lid() < (N * N >> 4)) E.scan_cg[lid()] = kScanCG[d.scan_type][cg_base(L) + lid()];
   wsync();
-  const int32_t abs_sum = tu_forward<L>(s, d, &E.est, nullptr);
+  HM_TADD(PR_TUF_IN, t_in);
+  HM_T0(t_fwd);
+  // the RDOQ's serial passes read the staged scan tables (LDS) instead of the constant tables
+  const int32_t abs_sum = L < 3 ? tu_forward<L>(s, d, &E.est, nullptr, E.scan, E.scan_cg) : tu_forward<L>(s, d, &E.est, nullptr);
+  HM_TADD(PR_TUF_FWD, t_fwd);
+  HM_T0(t_out);
   for (int i = lid(); i < N * N; i += 64) coef[i] = (int16_t)s.lev[i];
   wsync();
+  HM_TADD(PR_TUF_OUT, t_out);
   return abs_sum;
 }
 template <int L>
@@ -3163,10 +3278,14 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
   hm_e.slice_start = job.slice_start;
   hm_e.slice_end = job.slice_end;
   hm_e.stop = 0;
-  if (l < 32) hm_e.prof[l >> 4][l & 15] = 0;
+  hm_e.prof[l >> 5][l & 31] = 0;
   const int resume = job.flags & HVX_HM_RESUME;
   if (resume) copy_words(&hm_e.cod[RD(0, CI_CURR_BEST)], &S->carry, (int)sizeof(Coder));
-  else copy_words(S->int2n, job.int2n, (int)sizeof(S->int2n));
+  else {
+    copy_words(S->int2n, job.int2n, (int)sizeof(S->int2n));
+    if (l < kMemoK) S->memo[l].key = 0;  // the count memo starts empty
+    if (l == 0) S->memo_next = 0;
+  }
   wsync();
   const int n = job.n_ctus;
   for (int k = 0; k < n; k++) {
@@ -3177,7 +3296,7 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
     // which compress_ctu left in coder RD(0, CI_CURR_BEST)
     copy_words(&S->carry, &hm_e.cod[RD(0, CI_CURR_BEST)], (int)sizeof(Coder));
     if (l < 4) S->dbg[l] = hm_e.dbg[l];
-    if (l < 32) S->prof[l >> 4][l & 15] = hm_e.prof[l >> 4][l & 15];
+    S->prof[l >> 5][l & 31] = hm_e.prof[l >> 5][l & 31];
     hvx_hm_ctu *o = &out_ctu[slot];
     copy_words(o->p, S->ctu_p, (int)sizeof(Part) * 256);
     copy_words(o->coef, S->ctu_coef, 2 * 6144);

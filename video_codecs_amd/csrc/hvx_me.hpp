@@ -1062,8 +1062,9 @@ __device__ uint32_t me_frac_stage(MeFracSmem<S, NW, TO> &sm, const hvx_me_job &j
           const int y = k / w, x = k - y * w;
           blk[y * S + x] = (uint8_t)me_frac_sample(sm, me_sel3(po, c), ry, fy, x, y);
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        // the wave's lanes read each other's samples: release, wave barrier, acquire (the barrier
+        // alone does not order memory -- with the fences after it the reads could be hoisted)
+        me_sync<1>();
         d = wave_satd(sm.org, S, (const uint8_t *)blk, S, w, h);
       }
     } else {

@@ -323,8 +323,11 @@ __device__ __forceinline__ int32_t rd_level_double(int32_t coef, int qc, int64_t
 // (-ffp-contract=off) keeps every decision identical.  Sign hiding then runs one
 // coefficient group per lane (groups are independent), with the rate deltas recomputed
 // from the packed context state of each position.
+// scan / scan_cg: optional copies of the TU's scan tables (e.g. staged in LDS by a caller that
+// runs many TUs serially: the serial passes then read no global memory); nullptr: kScan / kScanCG
 template <int L>
-__device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits *est, int32_t *arl_out) {
+__device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits *est, int32_t *arl_out,
+                           const uint16_t *scan = nullptr, const uint8_t *scan_cg = nullptr) {
   constexpr int N = 4 << L, NN = N * N, NCG = NN / 16, LOG2 = L + 2;
   const int ch = d.comp ? 1 : 0, comp = d.comp;
   const int ts = tu_transform_shift(d);
@@ -338,13 +341,21 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   escale = escale * ldexp(1.0, -2 * tsn);  // == pow(2.0, -2.0*tsn) exactly
   escale = escale / qc / qc / (1 << 0);
   const double lambda = d.lambda;
-  const TuCoding c = tu_coding<L>(d);
+  TuCoding c = tu_coding<L>(d);
+  if (scan) c.scan = scan;
+  if (scan_cg) c.scan_cg = scan_cg;
   const int64_t lim = (int64_t)2147483647 - ((int64_t)1 << (qbits - 1));
   const int qbits_c = qbits - 7, add_c = 1 << (qbits_c - 1);
   const int lane = lane_id();
   const int sig_off = ch ? 28 : 0;
   int32_t *st = s.a;  // the residual is dead once the forward transform has run
 
+#ifdef HVX_TU_PROF_HOOK
+  uint64_t t_ph = __builtin_amdgcn_s_memtime();
+#define HVX_RDOQ_PHASE(k) do { const uint64_t t_n = __builtin_amdgcn_s_memtime(); HVX_TU_PROF_HOOK(28 + (k), t_n - t_ph); t_ph = t_n; } while (0)
+#else
+#define HVX_RDOQ_PHASE(k) ((void)0)
+#endif
   // ---- A. per-coefficient work across lanes ----
   for (int sp = lane; sp < NN; sp += HVX_WAVE) {
     const int blk = c.scan[sp];
@@ -361,6 +372,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   const int t_a = lane < 6 ? est->levelAbsBits[lane][0] : (lane >= 32 && lane < 38) ? est->levelAbsBits[lane - 32][1] : 0;
   __syncthreads();
 
+  HVX_RDOQ_PHASE(0);
   // ---- B. reverse-scan decisions (wave-uniform) ----
   const uint32_t rice0 = (uint32_t)d.golomb_rice_stat / 4;
   uint32_t rice = rice0, ctx_set = 0, c1_idx = 0, c2_idx = 0;
@@ -504,6 +516,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   }
   __syncthreads();
 
+  HVX_RDOQ_PHASE(1);
   if (last < 0) return 0;  // every level is 0 (written above)
 
   // ---- C. best last position (wave-uniform) ----
@@ -555,6 +568,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   }
   __syncthreads();
 
+  HVX_RDOQ_PHASE(2);
   // ---- D. signs, zeroing past the chosen last position, uiAbsSum (lanes) ----
   int part = 0;
   for (int sp = lane; sp <= last; sp += HVX_WAVE) {
@@ -632,6 +646,8 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
     }
     __syncthreads();
   }
+  HVX_RDOQ_PHASE(3);
+#undef HVX_RDOQ_PHASE
   return abs_sum;
 }
 
@@ -706,7 +722,8 @@ __device__ int32_t tu_quant_plain(TuSmem<L> &s, const hvx_tu_desc &d, int32_t *a
 // transformNxN (:1460) on s.a (the residual as int, raster N*N).  Leaves s.coef (transform
 // output) and s.lev (levels); returns uiAbsSum.
 template <int L>
-__device__ int32_t tu_forward(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits *est, int32_t *arl_out) {
+__device__ int32_t tu_forward(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits *est, int32_t *arl_out,
+                              const uint16_t *scan = nullptr, const uint8_t *scan_cg = nullptr) {
   constexpr int N = 4 << L, NN = N * N;
   if (d.transquant_bypass) {
     int part = 0;
@@ -714,6 +731,9 @@ __device__ int32_t tu_forward(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estb
     __syncthreads();
     return wave_sum_i32(part);
   }
+#ifdef HVX_TU_PROF_HOOK
+  const uint64_t t_x0 = __builtin_amdgcn_s_memtime();
+#endif
   if (d.transform_skip) {
     const int ts = tu_transform_shift(d);
     for (int i = lane_id(); i < NN; i += HVX_WAVE) {
@@ -724,6 +744,9 @@ __device__ int32_t tu_forward(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estb
   } else {
     tu_forward_transform<L>(s, d.use_dst && N == 4);
   }
+#ifdef HVX_TU_PROF_HOOK
+  HVX_TU_PROF_HOOK(22, __builtin_amdgcn_s_memtime() - t_x0);
+#endif
   const int use_rdoq = d.transform_skip ? d.use_rdoq_ts : d.use_rdoq;
   if (use_rdoq) {
     bool need = true;
@@ -736,7 +759,16 @@ __device__ int32_t tu_forward(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estb
         any |= ((int32_t)(((int64_t)abs(s.coef[i]) * kQuantScales[d.qp_rem] + add) >> qbits)) != 0;
       need = wave_sum_i32(any) != 0;
     }
-    if (need) return tu_rdoq<L>(s, d, est, arl_out);
+#ifdef HVX_TU_PROF_HOOK
+    if (need) {
+      const uint64_t t_r0 = __builtin_amdgcn_s_memtime();
+      const int32_t r = tu_rdoq<L>(s, d, est, arl_out, scan, scan_cg);
+      HVX_TU_PROF_HOOK(23, __builtin_amdgcn_s_memtime() - t_r0);
+      return r;
+    }
+#else
+    if (need) return tu_rdoq<L>(s, d, est, arl_out, scan, scan_cg);
+#endif
     for (int i = lane_id(); i < NN; i += HVX_WAVE) {
       s.lev[i] = 0;
       if (arl_out) arl_out[i] = 0;
