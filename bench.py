@@ -440,6 +440,14 @@ def main():
             tr = json.load(open(tr_path)).get("k_hm_compress")
             if tr:
                 traffic = tr["bytes_per_launch"] * units / tr.get("ctus_per_launch", units)
+        # the engine's real limiter, from the SQ counter passes of the same kernel on this round's
+        # tree (scripts/gpu_hm_pmc.sh + scripts/hm_pmc_summary.py): issue fractions of the SIMDs
+        issue = {}
+        pmc_path = os.path.join(ROOT, "profiles", "hm_pmc_r03.json")
+        if os.path.exists(pmc_path):
+            pm = json.load(open(pmc_path))
+            issue = {"simd_issue_frac": pm["simd_issue_frac"], "valu_frac": pm["valu_frac"],
+                     "wave_cycle_split": pm["wave_cycle_split"], "pmc_file": "profiles/hm_pmc_r03.json"}
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -465,10 +473,13 @@ def main():
                        "dpb": "gather of every rank's reconstructed CTUs to rank 0 per step" if world > 1 else "local"},
             # priced against HBM (integer work); the limiter is the serial RD decision
             # chain inside each wave (latency), not bandwidth -- frac << 1
-            "roofline": {"bound": "hbm", "limiter": "latency", "kernel": "k_hm_compress",
+            "roofline": {"bound": "hbm", "limiter": "instruction latency of the serial decision chain (issue + "
+                                                    "dependency waits; see simd_issue_frac / wave_cycle_split)",
+                         "kernel": "k_hm_compress",
                          "achieved": round(achieved, 4), "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / MI355X_HBM_PEAK_GBS, "traffic": traffic,
-                         "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(launch_ms, 3), "b_ctu": bpc},
+                         "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(launch_ms, 3), "b_ctu": bpc,
+                         **issue},
             "cpu_baseline": None,
         }
         if dpb_ok is not None:
