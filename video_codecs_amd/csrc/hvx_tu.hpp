@@ -278,6 +278,12 @@ __device__ __forceinline__ double rd_rate_last(const hvx_estbits *est, double la
 }
 
 __device__ __forceinline__ int rl(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ double rld(double v, int lane) {
+  const uint64_t b = __double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 
 // Per scan position, the RDOQ pass keeps one packed int in s.a:
 //   before the serial pass: the significance context under each of the 4 neighbour-CG
@@ -388,22 +394,34 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
       const int bb = cy < c.wg - 1 ? (int)((sigmask >> (cgblk + c.wg)) & 1) : 0;
       pattern = rr + (bb << 1);
     }
-    // the group's 16 inputs, one per lane (read back with v_readlane)
+    // the group's 16 inputs, one per lane (read back with v_readlane), and everything of a
+    // position's decision that does not depend on the serial c1 / c2 / Rice state, computed
+    // lane-parallel with the serial pass's own operations (same values bit for bit): the
+    // quantised magnitude, the uncoded cost, the distortion term of both candidate levels, the
+    // significance context and its two flag costs
     const int myblk = c.scan[cgp * 16 + (lane & 15)];
     const int ldl = rd_level_double(s.coef[myblk], qc, lim);
     const int infl = st[cgp * 16 + (lane & 15)];
     const int shp = 6 * pattern;
+    const uint32_t q_l = (uint32_t)((ldl + (1 << (qbits - 1))) >> qbits);
+    const uint32_t ma_l = (uint32_t)ecmax < q_l ? (uint32_t)ecmax : q_l;
+    const double e_l = (double)ldl;
+    const double cc0_l = e_l * e_l * escale;
+    const double er1 = (double)sub32(ldl, shl32((int32_t)ma_l, qbits));
+    const double d1_l = er1 * er1 * escale;  // distortion term of level max_abs
+    const double er2 = (double)sub32(ldl, shl32((int32_t)ma_l - 1, qbits));
+    const double d2_l = er2 * er2 * escale;  // ... of level max_abs - 1
+    const int ctxs_l = (infl >> shp) & 63;
+    const double ls0_l = lambda * (double)est->significantBits[ctxs_l][0];
+    const double ls1_l = lambda * (double)est->significantBits[ctxs_l][1];
     int nnz0 = 0;
     bool any = false;
     double coded_ld = 0, uncoded = 0, sig_cost = 0, sig_cost0 = 0;
     int o_lev = 0, o_st = 0;  // lane pin: results of scan position cgp*16 + pin
     for (int pin = 15; pin >= 0; pin--) {
       const int sp = cgp * 16 + pin;
-      const int32_t ld = rl(ldl, pin);
-      const uint32_t q = (uint32_t)((ld + (1 << (qbits - 1))) >> qbits);
-      const uint32_t max_abs = (uint32_t)ecmax < q ? (uint32_t)ecmax : q;
-      const double e = (double)ld;
-      const double cc0 = e * e * escale;
+      const uint32_t max_abs = (uint32_t)rl((int)ma_l, pin);
+      const double cc0 = rld(cc0_l, pin);
       block_uncoded += cc0;
       int32_t out = (int32_t)max_abs;
       double cc = 0.0, cs = 0.0;
@@ -419,18 +437,13 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
         const bool c1ok = c1_idx < 8, c2ok = c2_idx < 1;
         // xGetCodedLevel (:2822)
         const bool is_last = sp == last;
-        int ctx_sig = 0, sb0 = 0, sb1 = 0;
-        if (!is_last) {
-          ctx_sig = (rl(infl, pin) >> shp) & 63;
-          sb0 = rl(t_sb0, ctx_sig);
-          sb1 = rl(t_sb1, ctx_sig);
-        }
+        const int ctx_sig = is_last ? 0 : rl(ctxs_l, pin);
         double cur_sig = 0, cost, cost_sig = 0;
         int sel = 0;
         uint32_t best = 0;
         bool done = false;
         if (!is_last && max_abs < 3) {
-          cost_sig = lambda * (double)sb0;
+          cost_sig = rld(ls0_l, pin);  // lambda * significantBits[ctx][0]
           sel = 1;
           cost = cc0 + cost_sig;
           if (max_abs == 0) done = true;
@@ -438,11 +451,11 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
           cost = 1.7e+308;
         }
         if (!done) {
-          if (!is_last) cur_sig = lambda * (double)sb1;
+          if (!is_last) cur_sig = rld(ls1_l, pin);
           const uint32_t min_abs = max_abs > 1 ? max_abs - 1 : 1;
+          const double dist1 = rld(d1_l, pin), dist2 = rld(d2_l, pin);
           for (int lv = (int)max_abs; lv >= (int)min_abs; lv--) {
-            const double err = (double)sub32(ld, shl32(lv, qbits));
-            double cl = err * err * escale +
+            double cl = (lv == (int)max_abs ? dist1 : dist2) +
                         lambda * (double)rd_ic_rate((uint32_t)lv, (int)rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2);
             cl += cur_sig;
             if (cl < cost) { best = (uint32_t)lv; cost = cl; cost_sig = cur_sig; sel = is_last ? 0 : 2; }
