@@ -521,6 +521,10 @@ def check_coeff_write_random(seed, n_streams, max_tus):
     counts = rng.integers(0, max_tus + 1, n_streams)
     first = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
     descs, levels, _ = random_coeff_tus(seed + 1, int(first[-1]))
+    # the writer refuses persistent Rice adaptation (its statistic would have to carry across the
+    # TUs of a run; include/hvx.h): those runs are checked for the refusal separately
+    descs["persistent_rice"] = 0
+    descs["golomb_rice_stat"] = 0
     states = rng.integers(0, 126, (n_streams, _abi.NUM_CTX)).astype(np.uint8)
     regs = np.zeros(n_streams, _abi.CABAC_REGS)
     regs[:] = _abi.CABAC_START
@@ -861,3 +865,37 @@ def check_sao_random(seed, w=1920, h=1080, luma_only=False):
         assert st[:, c].tobytes() == exp.tobytes(), f"plane {c} statistics"
         np.testing.assert_array_equal(got[c], oracle.sao_apply(pre[c], c, params), err_msg=f"plane {c}")
     return nctu
+
+
+def check_coeff_write_refusals(seed):
+    """Runs holding a TU the writer does not support (persistent Rice, a non-square or 64-wide TU)
+    come back with length -2 and their registers and context states untouched, whatever TUs
+    precede the refused one in the run; the other runs of the launch are written normally."""
+    import torch
+    rng = np.random.default_rng(seed)
+    descs, levels, _ = random_coeff_tus(seed + 1, 12)
+    descs["persistent_rice"] = 0
+    descs["golomb_rice_stat"] = 0
+    descs[5]["persistent_rice"] = 1   # run 1 (TUs 4..7): its second TU is refused
+    descs[10]["height"] = descs[10]["width"] * 2 if descs[10]["width"] < 32 else 16  # run 2: non-square
+    first = np.array([0, 4, 8, 12], np.int32)
+    ns = 3
+    states = rng.integers(0, 126, (ns, _abi.NUM_CTX)).astype(np.uint8)
+    regs = np.zeros(ns, _abi.CABAC_REGS)
+    regs[:] = _abi.CABAC_START
+    off = np.concatenate([[0], np.cumsum([len(l) for l in levels])[:-1]]).astype(np.int64)
+    flat = np.concatenate(levels).astype(np.int32)
+    d_st = torch.from_numpy(states.reshape(-1).copy()).cuda()
+    d_rg = torch.from_numpy(regs.view(np.uint8).copy()).cuda()
+    cap = 1 << 16
+    out = torch.zeros(ns * cap, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(ns, dtype=torch.int32, device="cuda")
+    hvx.coeff_write_batch(hvx.to_device(descs), hvx.to_device(off), hvx.to_device(flat), hvx.to_device(first), ns, d_st,
+                          d_rg, out, hvx.to_device(np.arange(ns, dtype=np.int64) * cap), cap, d_len)
+    torch.cuda.synchronize()
+    lens, r, st = d_len.cpu().numpy(), d_rg.cpu().numpy().view(_abi.CABAC_REGS), d_st.cpu().numpy().reshape(ns, -1)
+    assert lens[0] >= 0 and lens[1] == -2 and lens[2] == -2, lens
+    for k in (1, 2):
+        assert r[k].tobytes() == regs[k].tobytes(), (k, r[k])
+        np.testing.assert_array_equal(st[k], states[k], err_msg=f"run {k}")
+    return True

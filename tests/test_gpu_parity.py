@@ -244,9 +244,16 @@ def test_coeff_write_golden_gpu(torch):
 
 def test_coeff_write_random_gpu(torch):
     # 200 runs of 0..12 random TUs (every size / scan / channel, transform skip, bypass, sign
-    # hiding, extended-precision escapes, persistent Rice) from start() vs the oracle, TU by TU
+    # hiding, extended-precision escapes) from start() vs the oracle, TU by TU, with the
+    # contexts each run coded (hvx_cabac_regs.coded)
     n_tu, n_bytes = gpu_cases.check_coeff_write_random(seed=41, n_streams=200, max_tus=12)
     assert n_tu > 1000 and n_bytes > 100000
+
+
+def test_coeff_write_refusals_gpu(torch):
+    # a run holding an unsupported TU (persistent Rice, non-square) is refused before anything is
+    # coded: length -2, registers and context states untouched
+    assert gpu_cases.check_coeff_write_refusals(seed=5)
 
 
 def test_intra_reference_samples_golden_gpu(torch):
