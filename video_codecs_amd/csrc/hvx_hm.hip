@@ -19,7 +19,13 @@ extern "C" {
 
 int hvx_hm_state_size(size_t *bytes) {
   if (!bytes) return fail(HVX_E_INVALID, "hvx_hm_state_size: NULL");
+#ifdef HM_STATE_ODD_LINES
+  // an odd number of 128-byte lines between consecutive chains' states, so the same field of
+  // different chains falls into different cache sets / memory channels
+  *bytes = ((sizeof(hm::State) + 127) / 128 | 1) * 128;
+#else
   *bytes = (sizeof(hm::State) + 255) / 256 * 256;
+#endif
   return HVX_OK;
 }
 

@@ -98,7 +98,9 @@ struct McScratch {
 };
 struct IntraScratch {
   int16_t unf[intra::kB + 3], filt[intra::kB + 3];
+#ifndef HM_LEAN_LDS
   uint8_t org[64 * 64];
+#endif
   uint32_t satd[36];
   int list[12], mpm[3];
   double cc[10];
@@ -146,6 +148,11 @@ struct State {
   MeScratch me;                   // leaf scratch outside LDS
   McScratch mc;
   TuSmem<3> tu3;
+#ifdef HM_LEAN_LDS
+  TuSmem<2> tu2;                  // HM_LEAN_LDS: the 16x16 TU pipeline's scratch too
+  uint8_t intra_org[64 * 64];     //   and the intra first pass's original
+  int16_t cstage32[1024];         //   and codeCoeffNxN's 32x32 levels
+#endif
 };
 
 // the LDS leaf scratch (one leaf runs at a time): TU pipelines up to 16x16 and the intra
@@ -154,10 +161,16 @@ struct State {
 union Leaf {
   TuSmem<0> tu0;
   TuSmem<1> tu1;
+#ifndef HM_LEAN_LDS
   TuSmem<2> tu2;
+#endif
   IntraScratch in;
   struct {               // codeCoeffNxN's TU staged in scan order (code_coeff_nxn)
+#ifdef HM_LEAN_LDS
+    int16_t lev[256];    // levels (32x32 TUs: State.cstage32)
+#else
     int16_t lev[1024];   // levels
+#endif
     int16_t ras[256];    // raster position (TUs up to 16x16)
     int32_t sig[256];    // significance context under neighbour-CG patterns 0..3, 6 bits each
     uint8_t cg[16];      // CG scan -> CG raster
@@ -183,7 +196,9 @@ struct Enc {
   uint32_t avail[4];
   int dbg[4];  // HM_CHECKS: first violated check (code, a, b) of the job
   int stage, stop;  // HM_CHECKS: stop the CTU at debugging stage `stage` (0: never)
+#ifdef HM_PROFILE
   uint64_t prof[2][32];  // HM_PROFILE accumulators
+#endif
   Leaf u;
 };
 }  // namespace hm
@@ -203,6 +218,8 @@ enum { Y_ORIG, Y_PRED_BEST, Y_PRED_TEMP, Y_RESI_BEST, Y_RESI_TEMP, Y_RECO_BEST, 
 __device__ __forceinline__ Yuv *YB(int kind, int d) { return &E.S->yuv[E.yi[kind][d]]; }
 __device__ __forceinline__ Cu *BEST(int d) { return &E.S->cu[E.best[d]]; }
 __device__ __forceinline__ Cu *TEMP(int d) { return &E.S->cu[E.temp[d]]; }
+// a chain is one wave (its workgroup): the compiler already lowers this to wavefront-scope
+// ordering (no s_barrier, no wait for outstanding stores; checked in the ISA)
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 __device__ __forceinline__ int lid() { return (int)threadIdx.x; }
 // HM_PROFILE builds accumulate the clock ticks (s_memtime) and calls of the leaf categories
@@ -1036,8 +1053,12 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
   HM_T0(t_stage);
   const int n = d.width * d.width;
   const uint16_t *scan = kScan[d.scan_type] + scan_base(ilog2(d.width) - 2);
-  int16_t *ls = E.u.cs.lev;
   const bool staged = n <= 256;
+#ifdef HM_LEAN_LDS
+  int16_t *ls = staged ? E.u.cs.lev : S->cstage32;
+#else
+  int16_t *ls = E.u.cs.lev;
+#endif
   if (staged) {
     const cab::ScanTables tab(d);
     for (int i = lid(); i < n; i += 64) {
@@ -1306,6 +1327,9 @@ __device__ uint32_t yuv_dist(Yuv *a, Yuv *b, int w) {
 template <int L>
 __device__ __forceinline__ TuSmem<L> &tu_smem() {
   if constexpr (L == 3) return E.S->tu3;
+#ifdef HM_LEAN_LDS
+  else if constexpr (L == 2) return E.S->tu2;
+#endif
   else return *reinterpret_cast<TuSmem<L> *>(&E.u);
 }
 template <int L>
@@ -2298,6 +2322,11 @@ __device__ void intra_border(const Cu *cu, const Tu &t, int comp, int16_t *B) {
 __device__ void intra_predict_tu(const Cu *cu, const Tu &t, int comp, int mode, int16_t *pred) {
   HM_PROF(PR_IPRED);
   IntraScratch &is = E.u.in;
+#ifdef HM_LEAN_LDS
+  uint8_t *is_org = E.S->intra_org;
+#else
+  uint8_t *is_org = is.org;
+#endif
   const int n = t.w[comp], log2n = ilog2(n);
   const bool luma = comp == 0;
   intra_border(cu, t, comp, is.unf);
@@ -2323,10 +2352,15 @@ __device__ void intra_predict_tu(const Cu *cu, const Tu &t, int comp, int mode, 
 __device__ void intra_first_pass(const Cu *cu, const Tu &tpu, Yuv *org, int depth) {
   HM_PROF(PR_IFP);
   IntraScratch &is = E.u.in;
+#ifdef HM_LEAN_LDS
+  uint8_t *is_org = E.S->intra_org;
+#else
+  uint8_t *is_org = is.org;
+#endif
   const int n = tpu.w[0], log2n = ilog2(n);
   intra_border(cu, tpu, 0, is.unf);
   intra::filter_border(is.unf, n, log2n, true, true, is.filt);
-  for (int k = lid(); k < n * n; k += 64) is.org[k] = (uint8_t)*yaddr(org, 0, tpu.x0[0] + (k & (n - 1)), tpu.y0[0] + (k >> log2n));
+  for (int k = lid(); k < n * n; k += 64) is_org[k] = (uint8_t)*yaddr(org, 0, tpu.x0[0] + (k & (n - 1)), tpu.y0[0] + (k >> log2n));
   if (lid() < 36) is.satd[lid()] = 0;
   wsync();
   const int dc = intra::dc_value(is.unf, n, log2n);
@@ -2342,7 +2376,7 @@ __device__ void intra_first_pass(const Cu *cu, const Tu &tpu, Yuv *org, int dept
       for (int y = 0; y < 8; y++) {
         int row[8];
         for (int x = 0; x < 8; x++)
-          row[x] = (int)is.org[(r0 + y) * n + c0 + x] - intra::pred_sample(B, n, log2n, md, edge, dc, r0 + y, c0 + x);
+          row[x] = (int)is_org[(r0 + y) * n + c0 + x] - intra::pred_sample(B, n, log2n, md, edge, dc, r0 + y, c0 + x);
         hadamard8(row, d[y]);
       }
       for (int x = 0; x < 8; x++) {
@@ -2356,7 +2390,7 @@ __device__ void intra_first_pass(const Cu *cu, const Tu &tpu, Yuv *org, int dept
       int d[4][4];
       for (int y = 0; y < 4; y++) {
         int row[4];
-        for (int x = 0; x < 4; x++) row[x] = (int)is.org[y * 4 + x] - intra::pred_sample(B, 4, 2, md, edge, dc, y, x);
+        for (int x = 0; x < 4; x++) row[x] = (int)is_org[y * 4 + x] - intra::pred_sample(B, 4, 2, md, edge, dc, y, x);
         hadamard4(row, d[y]);
       }
       for (int x = 0; x < 4; x++) {
@@ -3278,7 +3312,9 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
   hm_e.slice_start = job.slice_start;
   hm_e.slice_end = job.slice_end;
   hm_e.stop = 0;
+#ifdef HM_PROFILE
   hm_e.prof[l >> 5][l & 31] = 0;
+#endif
   const int resume = job.flags & HVX_HM_RESUME;
   if (resume) copy_words(&hm_e.cod[RD(0, CI_CURR_BEST)], &S->carry, (int)sizeof(Coder));
   else {
@@ -3296,7 +3332,9 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
     // which compress_ctu left in coder RD(0, CI_CURR_BEST)
     copy_words(&S->carry, &hm_e.cod[RD(0, CI_CURR_BEST)], (int)sizeof(Coder));
     if (l < 4) S->dbg[l] = hm_e.dbg[l];
+#ifdef HM_PROFILE
     S->prof[l >> 5][l & 31] = hm_e.prof[l >> 5][l & 31];
+#endif
     hvx_hm_ctu *o = &out_ctu[slot];
     copy_words(o->p, S->ctu_p, (int)sizeof(Part) * 256);
     copy_words(o->coef, S->ctu_coef, 2 * 6144);
