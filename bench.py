@@ -383,6 +383,26 @@ def hm_cpu_reference(procs, tmpdir):
             "s_per_ctu_per_core": round(per_ctu, 4)}
 
 
+def build_provenance():
+    """The libhvx.so this run loaded against the sources in the tree: the stamp build_hip()
+    wrote (source digest + library sha256) re-checked here (fresh = the library was built from
+    exactly these sources and is the file that was stamped)."""
+    import hashlib
+    import __graft_entry__ as ge
+    from video_codecs_amd import hvx
+    lib = hvx.LIB_PATH
+    rec = {"lib": os.path.relpath(lib, ROOT), "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]}
+    stamp_path = os.path.join(ROOT, "video_codecs_amd", "libhvx.build.json")
+    if os.path.exists(stamp_path):
+        st = json.load(open(stamp_path))
+        rec["built_utc"] = st.get("built_utc")
+        rec["fresh"] = st.get("source_digest") == ge.source_digest() and \
+            st.get("lib_sha256", "")[:16] == rec["lib_sha256"]
+    else:
+        rec["fresh"] = None
+    return rec
+
+
 def main():
     args = parse()
     import torch
@@ -484,6 +504,7 @@ def main():
         }
         if dpb_ok is not None:
             out["dpb_gather_ok"] = dpb_ok
+        out["build"] = build_provenance()
         if world == 1:
             threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
             if not args.no_cpu_ref:
@@ -594,6 +615,7 @@ def reduced_step(args, rank, world, with_sides):
         }
         if dpb_ok is not None:
             out["dpb_gather_ok"] = dpb_ok
+        out["build"] = build_provenance()
         if with_sides and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(inp.host, an, gpu_res, gpu_dec, gpu_rec, gpu_refpic, args)
         if with_sides and not args.no_1080p:

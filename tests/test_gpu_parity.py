@@ -299,8 +299,9 @@ def test_sao_random_gpu(torch):
 
 def test_ctu_decide_ssim_rdo_gpu(torch):
     # HVX_RD_SSIM (BASELINE config 4's SSIM RD cost): D_ssim per 8x8 block (compute_SSIM floats) and
-    # lambda_2 in the CU quadtree decision, QP 22 and 37, bit-exact vs the oracle incl. the float sums
-    for qp in (22, 37):
+    # lambda_2 in the CU quadtree decision, QP 22 / 27 / 32 / 37 (config 4's sweep), bit-exact vs
+    # the oracle incl. the float sums
+    for qp in (22, 27, 32, 37):
         n, leaves = gpu_cases.check_ctu_decide(seed=9 + qp, width=256, height=136, nref=2, qp=qp, fused=True,
                                                rd_metric=hvx._abi.RD_SSIM)
         assert n == 12 and leaves >= 12

@@ -36,7 +36,12 @@ int hvx_hm_compress(hvx_ctx *ctx, const hvx_hm_picture *d_pics, const hvx_hm_job
   if (n_jobs == 0) return HVX_OK;
   size_t sb = 0;
   hvx_hm_state_size(&sb);
-  hipLaunchKernelGGL(k_hm_compress, dim3(n_jobs), dim3(64), 0, ctx->stream, d_pics, d_jobs, n_jobs, (char *)d_state, sb,
+#ifdef HM_XCD_GROUP
+  const int grid = 8 * ((n_jobs + 7) / 8);
+#else
+  const int grid = n_jobs;
+#endif
+  hipLaunchKernelGGL(k_hm_compress, dim3(grid), dim3(64), 0, ctx->stream, d_pics, d_jobs, n_jobs, (char *)d_state, sb,
                      d_out_ctu, d_out_rec, d_out_coder);
   return launched("k_hm_compress");
 }

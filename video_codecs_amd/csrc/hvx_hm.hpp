@@ -3293,7 +3293,15 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
                                                     int n_jobs, char *state_base, size_t state_bytes, hvx_hm_ctu *out_ctu,
                                                     uint8_t *out_rec, hvx_hm_coder *out_coder) {
   using namespace hm;
+#ifdef HM_XCD_GROUP
+  // workgroups go to the 8 XCDs round-robin (blockIdx % 8): give XCD x the contiguous job range
+  // [x * per, (x + 1) * per), so neighbouring jobs (the row slices of one picture, which read the
+  // same reference windows and neighbour CTUs) share an XCD's L2
+  const int per = (n_jobs + 7) >> 3;
+  const int jid = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+#else
   const int jid = blockIdx.x;
+#endif
   if (jid >= n_jobs) return;
   const int l = threadIdx.x;
   const hvx_hm_job &job = jobs[jid];
