@@ -1221,10 +1221,9 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
 #ifdef HM_GENERIC_WALK
   if (staged) cab::coeff_bits_env(d, StagedScan{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig}, [&](int sp) { return uni(ls[sp]); }, L, rice);
 #else
-  // the mask-driven walk for 4x4 / 8x8 (+2.3% on the bench); 16x16 measured faster on the
-  // generic walk over the staged tables
-  if (staged && n <= 64) coeff_count_staged(d, StagedScan{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig}, ls, L);
-  else if (staged) cab::coeff_bits_env(d, StagedScan{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig}, [&](int sp) { return uni(ls[sp]); }, L, rice);
+  // the mask-driven walk (+2.3% on the bench; a third walk instance in this function, the generic
+  // one for the staged 16x16 TUs, measured 20% slower overall: register pressure)
+  if (staged) coeff_count_staged(d, StagedScan{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig}, ls, L);
 #endif
   else cab::coeff_bits(d, [&](int sp) { return uni(ls[sp]); }, L, rice);
   E.cod[E.cur].frac += L.frac;
