@@ -173,7 +173,7 @@ union Leaf {
 #endif
     int16_t ras[256];    // raster position (TUs up to 16x16)
     int32_t sig[256];    // significance context under neighbour-CG patterns 0..3, 6 bits each
-    uint8_t cg[16];      // CG scan -> CG raster
+    uint8_t cg[64];      // CG scan -> CG raster
   } cs;
 };
 
@@ -984,42 +984,47 @@ struct RegCoder {
   }
 };
 
-// the scan geometry of a TU staged in LDS (cab::ScanTables' values; TUs up to 16x16)
+// the scan geometry of a TU (cab::ScanTables' values): the CG scan staged in LDS for every size;
+// raster positions and packed significance contexts staged in LDS up to 16x16, while a 32x32 TU
+// (big) reads its rasters from the constant scan table and derives the contexts per lane
 struct StagedScan {
   const uint8_t *cgs;
   const int16_t *ras;
   const int32_t *sig;
+  const uint16_t *scan_g;
+  int first_sig, single;
+  bool big;
   __device__ __forceinline__ int cg(int sub) const { return uni(cgs[sub]); }
-  __device__ __forceinline__ int raster(int sp) const { return uni(ras[sp]); }
+  __device__ __forceinline__ int raster(int sp) const { return big ? (int)scan_g[sp] : uni(ras[sp]); }
   __device__ __forceinline__ int sigc(int pattern, int sp) const { return (uni(sig[sp]) >> (6 * pattern)) & 63; }
 };
 
 // cab::coeff_bits_env (codeCoeffNxN under the counter, TEncSbac.cpp:1181-1540) restated for the
-// wave-uniform engine over a TU staged in LDS (up to 16x16): the same bins in the same order on
-// the same contexts, but the significance map is one ballot per 64 positions, and a coefficient
-// group's levels and significance contexts are fetched lane-parallel once (one LDS round) and
-// read back with v_readlane; the greater-1 / escape passes walk the set bits of the group's mask
-// instead of all 16 positions.  Returns num_sig.
+// wave-uniform engine over a TU staged in scan order (every size): the same bins in the same order
+// on the same contexts, but the significant-CG map is one ballot per 64 positions, and a
+// coefficient group's levels and significance contexts are fetched lane-parallel once (one LDS
+// round) and read back with v_readlane; the greater-1 / escape passes walk the set bits of the
+// group's mask instead of all 16 positions.  One instance serves all sizes (a second walk in
+// code_coeff_nxn costs registers across the whole function).  Returns num_sig.
 template <class C>
 __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, const int16_t *ls, C &L) {
   const int n = d.width, lw = cab::log2_tu(n), wg = n >> 2, ncg = wg * wg, nn = n * n;
   const int ch = d.comp ? 1 : 0, l = lid();
-  // significance masks by scan position (64 positions per word)
-  uint64_t msk[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int w = 0; w < 4; w++)
-    if (w * 64 < nn) msk[w] = __ballot(w * 64 + l < nn && ls[w * 64 + l] != 0);
-  auto cgmask = [&](int sub) -> uint32_t { return (uint32_t)(msk[sub >> 2] >> ((sub & 3) * 16)) & 0xffffu; };
+  // significant-CG map, count and last position: one ballot per 64 scan positions (4 groups)
   uint64_t cgm = 0;
   int num_sig = 0, scan_last = -1;
-  for (int sub = 0; sub < ncg; sub++) {
-    const uint32_t m = cgmask(sub);
-    if (m) {
-      cgm |= 1ull << env.cg(sub);
-      num_sig += __popc(m);
-      scan_last = sub * 16 + 31 - __clz(m);
+  const int nw = nn < 64 ? 1 : nn >> 6;
+  for (int w = 0; w < nw; w++) {
+    const uint64_t b = __ballot(w * 64 + l < nn && ls[w * 64 + l] != 0);
+    if (b) {
+      num_sig += __popcll(b);
+      scan_last = w * 64 + 63 - __clzll(b);
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if ((b >> (16 * q)) & 0xffffu) cgm |= 1ull << env.cg(w * 4 + q);
     }
   }
+  (void)ncg;
   if (num_sig == 0) return 0;
   const bool be_valid = d.transquant_bypass ? false : (d.sign_hiding != 0);
   if (d.pps_tskip && !d.transquant_bypass && n <= 4) L.bin(cab::kTskip + ch, d.transform_skip ? 1 : 0);
@@ -1045,10 +1050,11 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
   for (int sub = last_set; sub >= 0; sub--) {
     const int sub_pos = sub << 4;
     const int cg = env.cg(sub), cgy = cg / wg, cgx = cg - cgy * wg;
-    // the group's levels and significance-context words, one position per lane
+    // the group's levels and significance-context words (32x32: raster positions), one position
+    // per lane
     const int lv_l = l < 16 ? (int)ls[sub_pos + l] : 0;
     const int av_l = lv_l < 0 ? -lv_l : lv_l;
-    const int sc_l = l < 16 ? env.sig[sub_pos + l] : 0;
+    const int sc_l = l < 16 ? (env.big ? (int)env.scan_g[sub_pos + l] : env.sig[sub_pos + l]) : 0;
     if (sub == last_set || sub == 0) cgm |= 1ull << cg;
     else {
       const int rr = cgx < wg - 1 ? (int)((cgm >> (cg + 1)) & 1) : 0;
@@ -1056,7 +1062,7 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
       L.bin(base_cg + ((rr + bb) != 0), (int)((cgm >> cg) & 1));
     }
     const bool is_last_set = sub == last_set;
-    const uint32_t m16 = cgmask(sub);
+    const uint32_t m16 = (uint32_t)__ballot(lv_l != 0);
     if ((cgm >> cg) & 1) {
       int pattern = 0;
       if (wg > 1) {
@@ -1064,11 +1070,11 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
         const int bb = cgy < wg - 1 ? (int)((cgm >> (cg + wg)) & 1) : 0;
         pattern = rr + (bb << 1);
       }
-      const int shp = 6 * pattern;
+      const int sc = env.big ? cab::sig_ctx(pattern, env.first_sig, env.single, sc_l, lw, ch) : (sc_l >> (6 * pattern)) & 63;
       int nnz = is_last_set ? 1 : 0;
       for (int pin = is_last_set ? last_pin - 1 : 15; pin >= 0; pin--) {
         const int sig = (int)((m16 >> pin) & 1u);
-        if (pin > 0 || sub == 0 || nnz) L.bin(base_sig + ((__builtin_amdgcn_readlane(sc_l, pin) >> shp) & 63), sig);
+        if (pin > 0 || sub == 0 || nnz) L.bin(base_sig + __builtin_amdgcn_readlane(sc, pin), sig);
         nnz += sig;
       }
     }
@@ -1189,8 +1195,9 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
 #else
   int16_t *ls = E.u.cs.lev;
 #endif
+  const cab::ScanTables tab(d);
+  if (lid() < (n >> 4)) E.u.cs.cg[lid()] = tab.scan_cg[lid()];
   if (staged) {
-    const cab::ScanTables tab(d);
     for (int i = lid(); i < n; i += 64) {
       const int r = scan[i];
       ls[i] = coef[r];
@@ -1200,7 +1207,6 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
       for (int pat = 0; pat < 4; pat++) sc |= cab::sig_ctx(pat, tab.first_sig, tab.single, r, tab.lw, tab.ch) << (6 * pat);
       E.u.cs.sig[i] = sc;
     }
-    if (lid() < (n >> 4)) E.u.cs.cg[lid()] = tab.scan_cg[lid()];
   } else {
     for (int i = lid(); i < n; i += 64) ls[i] = coef[scan[i]];
   }
@@ -1217,15 +1223,16 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
   wsync();
   HM_TADD(PR_COEF_STAGE, t_stage);
   HM_T0(t_walk);
-  uint32_t rice = 0;
+  const StagedScan env{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig, scan, tab.first_sig, tab.single, !staged};
 #ifdef HM_GENERIC_WALK
-  if (staged) cab::coeff_bits_env(d, StagedScan{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig}, [&](int sp) { return uni(ls[sp]); }, L, rice);
-#else
-  // the mask-driven walk (+2.3% on the bench; a third walk instance in this function, the generic
-  // one for the staged 16x16 TUs, measured 20% slower overall: register pressure)
-  if (staged) coeff_count_staged(d, StagedScan{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig}, ls, L);
-#endif
+  uint32_t rice = 0;
+  if (staged) cab::coeff_bits_env(d, env, [&](int sp) { return uni(ls[sp]); }, L, rice);
   else cab::coeff_bits(d, [&](int sp) { return uni(ls[sp]); }, L, rice);
+#else
+  // the mask-driven walk for every size (a third walk instance in this function measured 20%
+  // slower overall: register pressure)
+  coeff_count_staged(d, env, ls, L);
+#endif
   E.cod[E.cur].frac += L.frac;
 #endif
   wsync();
