@@ -601,6 +601,85 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   if (d.sign_hiding && abs_sum >= 2) {
     const double iq = (double)kInvQuantScales[d.qp_rem];
     const int64_t rdf = (int64_t)(iq * iq * (1 << (2 * d.qp_per)) / d.lambda / 16 / (1 << 0) + 0.5);
+#ifndef HVX_SBH_GROUP_PER_LANE
+    if constexpr (L <= 1) {
+      // TUs up to 8x8: every position in its own lane (lane = group * 16 + k).  A group's
+      // first / last non-zero come from its ballot, its level sum (signed, as the reference sums
+      // it: positions outside [first_nz, last_nz] hold 0) from a 16-lane reduction, and the
+      // reverse loop's strict-minimum search from a 16-lane argmin keeping the highest k on ties
+      // (the first minimum the descending loop meets) -- the same change at the same position.
+      const int sub = lane >> 4, k = lane & 15, pos = sub << 4;
+      const bool valid = sub < NCG;
+      const int blk = valid ? c.scan[pos + k] : 0;
+      const int32_t lv = valid ? s.lev[blk] : 0;
+      const int32_t cf = valid ? s.coef[blk] : 0;
+      const int stv = valid ? st[pos + k] : 0;
+      const uint64_t nzm = __ballot(lv != 0);
+      const uint32_t m16 = (uint32_t)(nzm >> pos) & 0xffffu;
+      const int last_nz = m16 ? 31 - __clz(m16) : -1, first_nz = m16 ? __builtin_ctz(m16) : 16;
+      const int top = nzm ? (63 - (int)__clzll(nzm)) >> 4 : -1;
+      int abs_in = lv;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) abs_in += __shfl_xor(abs_in, o, HVX_WAVE);
+      const int lv_first = __shfl(lv, (pos + (first_nz & 15)) & 63, HVX_WAVE);
+      const uint32_t signbit = lv_first > 0 ? 0 : 1;
+      const bool act = valid && last_nz - first_nz >= 4 && signbit != (uint32_t)(abs_in & 1);
+      const bool is_top = sub == top;
+      long long cur = INT64_MAX;
+      int cch = 0;
+      if (act && k <= (is_top ? last_nz : 15)) {
+        const uint32_t lev0 = (uint32_t)abs(lv);
+        const int32_t ld = rd_level_double(cf, qc, lim);
+        const int32_t du = sub32(ld, shl32((int32_t)lev0, qbits)) >> (qbits - 8);
+        const RdCtx x = rd_unpack(stv);
+        const int g0 = est->greaterOneBits[x.ctx_one][0];
+        const int sigd = x.has_sig ? est->significantBits[x.ctx_sig][1] - est->significantBits[x.ctx_sig][0] : 0;
+        int rup = g0, rdown = 0;
+        if (lev0 > 0) {
+          const int g1 = est->greaterOneBits[x.ctx_one][1];
+          const int a0 = est->levelAbsBits[x.ctx_abs][0], a1 = est->levelAbsBits[x.ctx_abs][1];
+          const int now = rd_ic_rate(lev0, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2);
+          rup = rd_ic_rate(lev0 + 1, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2) - now;
+          rdown = rd_ic_rate(lev0 - 1, x.rice, x.c1ok, x.c2ok, g0, g1, a0, a1, ext, max_log2) - now;
+        }
+        if (lv != 0) {
+          const int64_t up = rdf * (-du) + rup;
+          int64_t down = rdf * (du) + rdown - ((abs(lv) == 1) ? sigd : 0);
+          if (is_top && last_nz == k && abs(lv) == 1) down -= (4 << 15);
+          if (up < down) { cur = up; cch = 1; }
+          else { cch = -1; cur = (k == first_nz && abs(lv) == 1) ? INT64_MAX : down; }
+        } else {
+          cur = rdf * (-(abs(du))) + (1 << 15) + rup + sigd;
+          cch = 1;
+          if (k < first_nz) {
+            const uint32_t tsb = cf >= 0 ? 0 : 1;
+            if (tsb != signbit) cur = INT64_MAX;
+          }
+        }
+      }
+      // argmin over the group: the smallest cost, the highest k among equal costs
+      long long bc = cur;
+      int bk = cur < INT64_MAX ? k : -1;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) {
+        const long long oc = __shfl_xor(bc, o, HVX_WAVE);
+        const int ok = __shfl_xor(bk, o, HVX_WAVE);
+        if (oc < bc || (oc == bc && ok > bk)) { bc = oc; bk = ok; }
+      }
+      const int src = (pos + (bk < 0 ? 0 : bk)) & 63;
+      const int min_pos = bk < 0 ? -1 : __shfl(blk, src, HVX_WAVE);
+      int fch = __shfl(cch, src, HVX_WAVE);
+      if (bk < 0) fch = 0;
+      if (act && k == 0) {
+        if (s.lev[min_pos] == ecmax || s.lev[min_pos] == ecmin) fch = -1;
+        if (s.coef[min_pos] >= 0) s.lev[min_pos] += fch;
+        else s.lev[min_pos] -= fch;
+      }
+      __syncthreads();
+      HVX_RDOQ_PHASE(3);
+      return abs_sum;
+    }
+#endif
     const int sub = lane, pos = sub << 4;
     int first_nz = 16, last_nz = -1, abs_in = 0;
     if (sub < NCG) {
