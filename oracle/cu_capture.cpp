@@ -260,10 +260,29 @@ void capture_exit(TComDataCU *ctu) {
   }
   g.nctu++;
 }
+
+// HVX_CAPTURE_POCS=<poc,poc,...>: record only the pictures of these POCs (the others are encoded
+// unrecorded; their reconstructions still enter the capture when a recorded picture references them)
+bool poc_selected(int poc) {
+  const char *s = getenv("HVX_CAPTURE_POCS");
+  if (!s || !*s) return true;
+  for (const char *p = s; *p;) {
+    char *end;
+    const long v = strtol(p, &end, 10);
+    if (end == p) break;
+    if (v == poc) return true;
+    p = *end ? end + 1 : end;
+  }
+  return false;
+}
 }  // namespace
 
 extern "C" void CAT(__wrap_, CU_SYM)(TEncCu *self, TComDataCU *ctu) {
   const int poc = ctu->getSlice()->getPOC();
+  if (!poc_selected(poc)) {
+    CAT(__real_, CU_SYM)(self, ctu);
+    return;
+  }
   if (poc != g.cur_poc) {
     g.cur_poc = poc;
     capture_picture(self, ctu);

@@ -2321,10 +2321,16 @@ void hvxo_mc(const int16_t *const *planes, int ls, int cs, const hvx_mc_job *j, 
  * final cost with fWeight 0.5 for bBi (:3696, :3759).  tgt: int16 pattern plane (sample 0,0). */
 void hvxo_me_full(const int16_t *tgt, int tstride, const uint8_t *refp, int ref_stride, const hvx_me_job *j,
                   hvx_me_result *r) {
+  hvxo_me_full_pat(tgt + j->pu_y * tstride + j->pu_x, tstride, refp, ref_stride, j, r);
+}
+/* the same with the pattern given at the PU's first sample (TComPattern over a TComYuv, e.g. the
+ * bi-prediction target m_cYuvPredTemp at uiPartAddr, stride 64) */
+void hvxo_me_full_pat(const int16_t *pat, int pstride, const uint8_t *refp, int ref_stride, const hvx_me_job *j,
+                      hvx_me_result *r) {
   tz_state t;
   memset(&t, 0, sizeof(t));
   t.org = NULL;
-  t.org16 = tgt + j->pu_y * tstride + j->pu_x; t.so = tstride;
+  t.org16 = pat; t.so = pstride;
   t.ref = refp + j->pu_y * ref_stride + j->pu_x; t.sr = ref_stride;
   t.w = j->w; t.h = j->h;
   const int w = j->w;
@@ -2342,7 +2348,7 @@ void hvxo_me_full(const int16_t *tgt, int tstride, const uint8_t *refp, int ref_
       const uint8_t *c = t.ref + y * ref_stride + x;
       uint32_t s = 0;
       for (int row = 0; row < t.h; row += 1 << sub)
-        for (int col = 0; col < w; col++) s += (uint32_t)abs((int)t.org16[row * tstride + col] - (int)c[row * ref_stride + col]);
+        for (int col = 0; col < w; col++) s += (uint32_t)abs((int)t.org16[row * pstride + col] - (int)c[row * ref_stride + col]);
       s = (s << sub) + mv_cost(&t, x, y);
       if (s < best) { best = s; bx = x; by = y; }
     }

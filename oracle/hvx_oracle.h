@@ -65,6 +65,8 @@ void hvxo_mc(const int16_t *const *planes, int luma_stride, int chroma_stride, c
 /* xMotionEstimation with the integer full search (FastSearch=0 / bBi), int16 pattern plane */
 void hvxo_me_full(const int16_t *tgt, int tstride, const uint8_t *refp, int ref_stride, const hvx_me_job *j,
                   hvx_me_result *r);
+void hvxo_me_full_pat(const int16_t *pat, int pstride, const uint8_t *refp, int ref_stride, const hvx_me_job *j,
+                      hvx_me_result *r);
 /* TComYuv::addAvg per sample, 8-bit (TComYuv.cpp:352) */
 void hvxo_add_avg(const int16_t *a, const int16_t *b, int16_t *dst, int n);
 /* TEncSbac::estBit (TEncSbac.cpp:1726): context states (TEncSbac::m_contextModels order,

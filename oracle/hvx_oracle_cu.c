@@ -580,6 +580,7 @@ static int ep_exgolomb_bins(uint32_t sym, int k) {
 }
 /* codeMvd (:779) */
 static void code_mvd(hm_enc *e, const hm_cu *cu, int rel, int list) {
+  if (e->pic->mvd_l1_zero && list == 1 && cu->p[rel].inter_dir == 3) return;
   const int h = cu->p[rel].mvd[list][0], v = cu->p[rel].mvd[list][1];
   cbin(e, X_MVD + 0, h != 0);
   cbin(e, X_MVD + 0, v != 0);
@@ -594,7 +595,7 @@ static void code_mvp_idx(hm_enc *e, const hm_cu *cu, int rel, int list) { cbin(e
 /* codeInterDir (:729) */
 static void code_inter_dir(hm_enc *e, const hm_cu *cu, int rel) {
   const int d = cu->p[rel].inter_dir - 1, ctx = cu->p[rel].depth;
-  if (cu->p[rel].part == SIZE_2Nx2N || cu->width != 8) { /* getHeight(abs) is the CU height */
+  if (cu->p[rel].part == SIZE_2Nx2N || cu->p[rel].width != 8) { /* getHeight(abs): the CU height at the partition */
     cbin(e, X_INTER_DIR + ctx, d == 2);
   }
   if (d < 2) cbin(e, X_INTER_DIR + 4, d);
@@ -1590,15 +1591,20 @@ static uint32_t template_cost(hm_enc *e, const hm_cu *cu, int ps, int pu, yuv_t 
   (void)mvp_idx;
   return (uint32_t)rd_cost_sad(e, 1 /* m_auiMVPIdxCost[idx][2] */, sad);
 }
+/* xEstimateMvPredAMVP (:3413); *dist_bip (puiDistBiP) takes the best template cost */
 static void est_mvp_amvp(hm_enc *e, hm_cu *cu, int ps, int pu, yuv_t *org, int list, int ref_idx, amvp_t *in, int16_t *pred,
-                         int *mvp_idx, int *mvp_num) {
+                         int *mvp_idx, int *mvp_num, uint32_t *dist_bip) {
   fill_mvp_cand(e, cu, ps, pu, list, ref_idx, in);
   int best = 0;
-  if (in->n <= 1) { pred[0] = in->c[0][0]; pred[1] = in->c[0][1]; *mvp_idx = 0; *mvp_num = in->n; return; }
+  if (in->n <= 1) {
+    pred[0] = in->c[0][0]; pred[1] = in->c[0][1]; *mvp_idx = 0; *mvp_num = in->n;
+    if (e->pic->mvd_l1_zero && list == 1) *dist_bip = template_cost(e, cu, ps, pu, org, list, ref_idx, pred, 0);
+    return;
+  }
   uint32_t best_cost = MAXU32;
   for (int i = 0; i < in->n; i++) {
     const uint32_t c = template_cost(e, cu, ps, pu, org, list, ref_idx, in->c[i], i);
-    if (best_cost > c) { best_cost = c; best = i; }
+    if (best_cost > c) { best_cost = c; best = i; *dist_bip = c; }
   }
   pred[0] = in->c[best][0]; pred[1] = in->c[best][1];
   *mvp_idx = best;
@@ -1685,39 +1691,178 @@ static void merge_estimation(hm_enc *e, hm_cu *cu, int ps, int pu, yuv_t *org, i
     }
   }
 }
+/* xMotionEstimation with bBi (TEncSearch.cpp:3663, :3686-3696, :3710-3712, :3726-3729): the target
+ * is m_cYuvPredTemp = 2 * org - m_acYuvPred[other list] (TComYuv::removeHighFreq, TComYuv.cpp:409,
+ * no clipping: ClipForBiPredMEEnabled is off), the full search of +-BipredSearchRange around the
+ * list's current MV (rcMv on entry), the final cost weighted by 0.5 */
+static void motion_estimation_bi(hm_enc *e, hm_cu *cu, int ps, int pu, yuv_t *org, int list, int ref_idx, const int16_t *pred,
+                                 int16_t *mv, uint32_t *bits, uint32_t *cost) {
+  const hvxo_hm_pic *P = e->pic;
+  int a, w, h, xp, yp;
+  part_index_size(cu, ps, pu, &a, &w, &h);
+  part_position(cu, ps, pu, &xp, &yp, &w, &h);
+  const int rx = xp - cu->x, ry = yp - cu->y;
+  yuv_t *tg = &e->yuv_pred_tmp;
+  const yuv_t *other = &e->yuv_pred_l[1 - list];
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      const int o = (ry + y) * 64 + rx + x;
+      tg->c[0][o] = (int16_t)(2 * org->c[0][o] - other->c[0][o]);
+    }
+  hvx_me_job j;
+  memset(&j, 0, sizeof(j));
+  j.pic_w = P->w; j.pic_h = P->h; j.max_cu = 64;
+  j.cu_x = cu->x; j.cu_y = cu->y;
+  j.pu_x = xp; j.pu_y = yp; j.w = w; j.h = h;
+  j.pred_x = pred[0]; j.pred_y = pred[1];
+  j.center_x = mv[0]; j.center_y = mv[1];
+  j.bits_in = (int32_t)*bits;
+  j.search_range = P->bipred_range;
+  j.lambda_motion = P->lambda_motion;
+  j.flags = HVX_ME_FEN | HVX_ME_HADME | HVX_ME_BI;
+  hvx_me_result r;
+  const int pi = P->ref_plane_idx[list][ref_idx];
+  hvxo_me_full_pat(tg->c[0] + ry * 64 + rx, 64, P->ref_planes8[pi], P->ref_stride8, &j, &r);
+  mv[0] = (int16_t)r.mv_x; mv[1] = (int16_t)r.mv_y;
+  *bits = r.bits;
+  *cost = r.cost;
+}
+/* xGetBlkBits (:3509) */
+static void blk_bits(int ps, int is_p, int pu, int last_mode, uint32_t *b) {
+  static const uint32_t hor[2][3][3] = {{{0, 0, 3}, {0, 0, 0}, {0, 0, 0}}, {{5, 7, 7}, {7, 5, 7}, {6, 6, 6}}};
+  static const uint32_t ver[2][3][3] = {{{0, 2, 3}, {0, 0, 0}, {0, 0, 0}}, {{5, 7, 7}, {5, 5, 7}, {6, 6, 6}}};
+  if (ps == SIZE_2Nx2N || ps == SIZE_NxN) { b[0] = is_p ? 1 : 3; b[1] = 3; b[2] = 5; return; }
+  if (is_p) { b[0] = 3; b[1] = 0; b[2] = 0; return; }
+  const uint32_t *t = (ps == SIZE_2NxN || ps == SIZE_2NxnU || ps == SIZE_2NxnD) ? hor[pu][last_mode] : ver[pu][last_mode];
+  b[0] = t[0]; b[1] = t[1]; b[2] = t[2];
+}
+/* the reference index bits of predInterSearch (:3021-3028) */
+static uint32_t ref_bits(int r, int n) {
+  if (n <= 1) return 0;
+  return (uint32_t)r + 1 - (r == n - 1 ? 1u : 0u);
+}
+/* predInterSearch (:2912), P and B slices */
 static int pred_inter_search(hm_enc *e, hm_cu *cu, yuv_t *org, yuv_t *pred, int use_mrg) {
   const hvxo_hm_pic *P = e->pic;
   const int ps = cu->p[0].part, npart = num_parts_of(ps);
+  const int isb = P->slice_type == B_SLICE, ndir = isb ? 2 : 1;
   int last_mode = 0;
-  (void)last_mode;
+  /* declared outside the PU loop in the reference (:2937-2969): kept across PUs */
+  int16_t mv[2][2] = {{0, 0}, {0, 0}};
+  int ref[2] = {0, 0};
+  int16_t mvtemp[2][4][2], mvpred[2][4][2], mvpredbi[2][4][2];
+  int mvp_idx[2][4], mvp_num[2][4], mvp_idx_bi[2][4];
+  amvp_t amvp[2][4];
+  int best_bip_ref_l1 = 0, best_bip_mvp_l1 = 0;
+  uint32_t bip_dist_temp = MAXU32;
+  memset(mvtemp, 0, sizeof(mvtemp));
+  memset(mvpred, 0, sizeof(mvpred));
   for (int pu = 0; pu < npart; pu++) {
-    uint32_t cost[2] = {MAXU32, MAXU32}, bits[3] = {0, 0, 0};
-    int16_t mv[2][2] = {{0, 0}, {0, 0}};
-    int ref[2] = {0, 0};
-    int16_t mvpred[2][4][2];
-    int mvp_idx[2][4], mvp_num[2][4];
+    uint32_t cost[2] = {MAXU32, MAXU32}, cost_bi = MAXU32, bits[3] = {0, 0, 0};
+    uint32_t best_bip_dist = MAXU32;
+    uint32_t cost_l0[4] = {MAXU32, MAXU32, MAXU32, MAXU32}, bits_l0[4] = {0, 0, 0, 0};
+    int16_t mv_valid_l1[2] = {0, 0};
+    int ref_valid_l1 = 0;
+    uint32_t bits_valid_l1 = MAXU32, cost_valid_l1 = MAXU32;
+    int16_t mvbi[2][2] = {{0, 0}, {0, 0}};
+    int refbi[2] = {0, 0};
+    uint32_t mb[3];
+    blk_bits(ps, !isb, pu, last_mode, mb);
     int a, w, h;
     part_index_size(cu, ps, pu, &a, &w, &h);
-    const uint32_t mb_bits0 = ps == SIZE_2Nx2N ? 1 : 3; /* xGetBlkBits (:3509), P slice */
     const int test_normal = !(use_mrg && cu->width > 8 && npart == 2);
     if (test_normal) {
-      for (int l = 0; l < 1; l++) { /* P slice: one list */
+      /* uni-directional prediction (:3014-3093) */
+      for (int l = 0; l < ndir; l++) {
         for (int r = 0; r < P->nref[l]; r++) {
-          uint32_t bt = mb_bits0, ct;
-          if (P->nref[l] > 1) { bt += (uint32_t)r + 1; if (r == P->nref[l] - 1) bt--; }
-          amvp_t in;
-          est_mvp_amvp(e, cu, ps, pu, org, l, r, &in, mvpred[l][r], &mvp_idx[l][r], &mvp_num[l][r]);
+          uint32_t bt = mb[l] + ref_bits(r, P->nref[l]), ct;
+          uint32_t dist_bip = bip_dist_temp;
+          est_mvp_amvp(e, cu, ps, pu, org, l, r, &amvp[l][r], mvpred[l][r], &mvp_idx[l][r], &mvp_num[l][r], &dist_bip);
+          bip_dist_temp = dist_bip;
           pu_set(cu, ps, pu, PU_MVP_IDX, l, mvp_idx[l][r]);
           pu_set(cu, ps, pu, PU_MVP_NUM, l, mvp_num[l][r]);
+          if (P->mvd_l1_zero && l == 1 && bip_dist_temp < best_bip_dist) {
+            best_bip_dist = bip_dist_temp;
+            best_bip_mvp_l1 = mvp_idx[l][r];
+            best_bip_ref_l1 = r;
+          }
           bt += 1; /* m_auiMVPIdxCost[idx][AMVP_MAX_NUM_CANDS] */
-          int16_t mvt[2];
-          motion_estimation(e, cu, ps, pu, l, r, mvpred[l][r], mvt, &bt, &ct);
-          check_best_mvp(e, &in, mvt, mvpred[l][r], &mvp_idx[l][r], &bt, &ct);
-          if (ct < cost[l]) { cost[l] = ct; bits[l] = bt; mv[l][0] = mvt[0]; mv[l][1] = mvt[1]; ref[l] = r; }
+          if (l == 1 && P->l1_to_l0[r] >= 0) {
+            /* FastMEForGenBLowDelayEnabled (:3042-3055): the L0 search of the same picture, re-costed */
+            const int m = P->l1_to_l0[r];
+            mvtemp[1][r][0] = mvtemp[0][m][0]; mvtemp[1][r][1] = mvtemp[0][m][1];
+            ct = cost_l0[m];
+            ct -= mv_cost_bits(e, bits_l0[m]);
+            bt += eg_bits(mvtemp[1][r][0] - mvpred[1][r][0]) + eg_bits(mvtemp[1][r][1] - mvpred[1][r][1]);
+            ct += mv_cost_bits(e, bt);
+          } else {
+            motion_estimation(e, cu, ps, pu, l, r, mvpred[l][r], mvtemp[l][r], &bt, &ct);
+          }
+          check_best_mvp(e, &amvp[l][r], mvtemp[l][r], mvpred[l][r], &mvp_idx[l][r], &bt, &ct);
+          if (l == 0) { cost_l0[r] = ct; bits_l0[r] = bt; }
+          if (ct < cost[l]) { cost[l] = ct; bits[l] = bt; mv[l][0] = mvtemp[l][r][0]; mv[l][1] = mvtemp[l][r][1]; ref[l] = r; }
+          if (l == 1 && ct < cost_valid_l1 && P->l1_to_l0[r] < 0) {
+            cost_valid_l1 = ct; bits_valid_l1 = bt;
+            mv_valid_l1[0] = mvtemp[l][r][0]; mv_valid_l1[1] = mvtemp[l][r][1];
+            ref_valid_l1 = r;
+          }
+        }
+      }
+      /* bi-directional prediction (:3096-3251), FEN: one iteration */
+      if (isb && !(cu->width == 8 && (w < 8 || h < 8))) { /* isBipredRestriction (TComDataCU.cpp:2773) */
+        mvbi[0][0] = mv[0][0]; mvbi[0][1] = mv[0][1]; mvbi[1][0] = mv[1][0]; mvbi[1][1] = mv[1][1];
+        refbi[0] = ref[0]; refbi[1] = ref[1];
+        memcpy(mvpredbi, mvpred, sizeof(mvpred));
+        memcpy(mvp_idx_bi, mvp_idx, sizeof(mvp_idx));
+        uint32_t motbits[2];
+        if (P->mvd_l1_zero) {
+          const int br = best_bip_ref_l1;
+          pu_set(cu, ps, pu, PU_MVP_IDX, 1, best_bip_mvp_l1);
+          mvp_idx_bi[1][br] = best_bip_mvp_l1;
+          mvpredbi[1][br][0] = amvp[1][br].c[best_bip_mvp_l1][0];
+          mvpredbi[1][br][1] = amvp[1][br].c[best_bip_mvp_l1][1];
+          mvbi[1][0] = mvpredbi[1][br][0]; mvbi[1][1] = mvpredbi[1][br][1];
+          refbi[1] = br;
+          pu_set_mvfield(cu, ps, pu, 1, mvbi[1][0], mvbi[1][1], br);
+          mc_pu(e, cu, ps, pu, 1, &e->yuv_pred_l[1]);
+          motbits[0] = bits[0] - mb[0];
+          motbits[1] = mb[1] + ref_bits(br, P->nref[1]) + 1;
+          bits[2] = mb[2] + motbits[0] + motbits[1];
+          mvtemp[1][br][0] = mvbi[1][0]; mvtemp[1][br][1] = mvbi[1][1];
+        } else {
+          motbits[0] = bits[0] - mb[0];
+          motbits[1] = bits[1] - mb[1];
+          bits[2] = mb[2] + motbits[0] + motbits[1];
+        }
+        /* UseFastEnc: iNumIter 1, the list searched is the costlier uni list */
+        int l = cost[0] <= cost[1] ? 1 : 0;
+        if (!P->mvd_l1_zero) {
+          pu_set_mv(cu, ps, pu, 1 - l, mv[1 - l][0], mv[1 - l][1]);
+          pu_set_ref(cu, ps, pu, 1 - l, ref[1 - l]);
+          mc_pu(e, cu, ps, pu, 1 - l, &e->yuv_pred_l[1 - l]);
+        } else l = 0;
+        int changed = 0;
+        for (int r = 0; r < P->nref[l]; r++) {
+          uint32_t bt = mb[2] + motbits[1 - l] + ref_bits(r, P->nref[l]) + 1, ct;
+          motion_estimation_bi(e, cu, ps, pu, org, l, r, mvpredbi[l][r], mvtemp[l][r], &bt, &ct);
+          check_best_mvp(e, &amvp[l][r], mvtemp[l][r], mvpredbi[l][r], &mvp_idx_bi[l][r], &bt, &ct);
+          if (ct < cost_bi) {
+            changed = 1;
+            mvbi[l][0] = mvtemp[l][r][0]; mvbi[l][1] = mvtemp[l][r][1];
+            refbi[l] = r;
+            cost_bi = ct;
+            motbits[l] = bt - mb[2] - motbits[1 - l];
+            bits[2] = bt;
+          }
+        }
+        if (!changed && cost_bi <= cost[0] && cost_bi <= cost[1]) {
+          check_best_mvp(e, &amvp[0][refbi[0]], mvbi[0], mvpredbi[0][refbi[0]], &mvp_idx_bi[0][refbi[0]], &bits[2], &cost_bi);
+          if (!P->mvd_l1_zero)
+            check_best_mvp(e, &amvp[1][refbi[1]], mvbi[1], mvpredbi[1][refbi[1]], &mvp_idx_bi[1][refbi[1]], &bits[2], &cost_bi);
         }
       }
     }
-    /* clear the PU's motion */
+    /* clear the PU's motion (:3257-3265) */
     pu_set_mvfield(cu, ps, pu, 0, 0, 0, -1);
     pu_set_mvfield(cu, ps, pu, 1, 0, 0, -1);
     pu_set_mvd(cu, ps, pu, 0, 0, 0);
@@ -1725,15 +1870,45 @@ static int pred_inter_search(hm_enc *e, hm_cu *cu, yuv_t *org, yuv_t *pred, int 
     pu_set(cu, ps, pu, PU_MVP_IDX, 0, -1); pu_set(cu, ps, pu, PU_MVP_NUM, 0, -1);
     pu_set(cu, ps, pu, PU_MVP_IDX, 1, -1); pu_set(cu, ps, pu, PU_MVP_NUM, 1, -1);
     uint32_t me_bits = 0;
-    /* list 1 is invalid in P slices (costValidList1 = MAX) */
+    /* list 1 only through a picture list 0 does not hold (:3269-3272) */
+    mv[1][0] = mv_valid_l1[0]; mv[1][1] = mv_valid_l1[1];
+    ref[1] = ref_valid_l1;
+    bits[1] = bits_valid_l1;
+    cost[1] = cost_valid_l1;
     if (test_normal) {
-      pu_set_mv(cu, ps, pu, 0, mv[0][0], mv[0][1]);
-      pu_set_ref(cu, ps, pu, 0, ref[0]);
-      pu_set_mvd(cu, ps, pu, 0, mv[0][0] - mvpred[0][ref[0]][0], mv[0][1] - mvpred[0][ref[0]][1]);
-      pu_set(cu, ps, pu, PU_INTER_DIR, 0, 1);
-      pu_set(cu, ps, pu, PU_MVP_IDX, 0, mvp_idx[0][ref[0]]);
-      pu_set(cu, ps, pu, PU_MVP_NUM, 0, mvp_num[0][ref[0]]);
-      me_bits = bits[0];
+      if (cost_bi <= cost[0] && cost_bi <= cost[1]) {
+        last_mode = 2;
+        pu_set_mv(cu, ps, pu, 0, mvbi[0][0], mvbi[0][1]);
+        pu_set_ref(cu, ps, pu, 0, refbi[0]);
+        pu_set_mv(cu, ps, pu, 1, mvbi[1][0], mvbi[1][1]);
+        pu_set_ref(cu, ps, pu, 1, refbi[1]);
+        pu_set_mvd(cu, ps, pu, 0, mvbi[0][0] - mvpredbi[0][refbi[0]][0], mvbi[0][1] - mvpredbi[0][refbi[0]][1]);
+        pu_set_mvd(cu, ps, pu, 1, mvbi[1][0] - mvpredbi[1][refbi[1]][0], mvbi[1][1] - mvpredbi[1][refbi[1]][1]);
+        pu_set(cu, ps, pu, PU_INTER_DIR, 0, 3);
+        pu_set(cu, ps, pu, PU_MVP_IDX, 0, mvp_idx_bi[0][refbi[0]]);
+        pu_set(cu, ps, pu, PU_MVP_NUM, 0, mvp_num[0][refbi[0]]);
+        pu_set(cu, ps, pu, PU_MVP_IDX, 1, mvp_idx_bi[1][refbi[1]]);
+        pu_set(cu, ps, pu, PU_MVP_NUM, 1, mvp_num[1][refbi[1]]);
+        me_bits = bits[2];
+      } else if (cost[0] <= cost[1]) {
+        last_mode = 0;
+        pu_set_mv(cu, ps, pu, 0, mv[0][0], mv[0][1]);
+        pu_set_ref(cu, ps, pu, 0, ref[0]);
+        pu_set_mvd(cu, ps, pu, 0, mv[0][0] - mvpred[0][ref[0]][0], mv[0][1] - mvpred[0][ref[0]][1]);
+        pu_set(cu, ps, pu, PU_INTER_DIR, 0, 1);
+        pu_set(cu, ps, pu, PU_MVP_IDX, 0, mvp_idx[0][ref[0]]);
+        pu_set(cu, ps, pu, PU_MVP_NUM, 0, mvp_num[0][ref[0]]);
+        me_bits = bits[0];
+      } else {
+        last_mode = 1;
+        pu_set_mv(cu, ps, pu, 1, mv[1][0], mv[1][1]);
+        pu_set_ref(cu, ps, pu, 1, ref[1]);
+        pu_set_mvd(cu, ps, pu, 1, mv[1][0] - mvpred[1][ref[1]][0], mv[1][1] - mvpred[1][ref[1]][1]);
+        pu_set(cu, ps, pu, PU_INTER_DIR, 0, 2);
+        pu_set(cu, ps, pu, PU_MVP_IDX, 1, mvp_idx[1][ref[1]]);
+        pu_set(cu, ps, pu, PU_MVP_NUM, 1, mvp_num[1][ref[1]]);
+        me_bits = bits[1];
+      }
     }
     if (ps != SIZE_2Nx2N) {
       uint32_t me_cost = MAXU32;
@@ -2678,7 +2853,9 @@ static void pic_setup(pic_buf *B, const int32_t *pi, const double *pf, const uin
   B->P.chroma_weight[0] = pf[F_WEIGHT_CB]; B->P.chroma_weight[1] = pf[F_WEIGHT_CR];
   B->P.tq_lambda[0] = pf[F_TQ_LAMBDA_Y]; B->P.tq_lambda[1] = pf[F_TQ_LAMBDA_CB]; B->P.tq_lambda[2] = pf[F_TQ_LAMBDA_CR];
   B->P.lambda_motion = (uint32_t)pi[P_LAMBDA_MOTION];
+  hvxo_hm_derive_lists(&B->P);
   B->P.search_range = 64;
+  B->P.bipred_range = 4;
   B->P.amp = 1;
   B->P.entropy_bits = entropy_bits;
   /* original planes */
@@ -2937,3 +3114,17 @@ void hvxo_hm_pack_parts(hvxo_hm_ctu_data *d, const int16_t *in) {
   }
 }
 size_t hvxo_hm_ctu_data_size(void) { return sizeof(hvxo_hm_ctu_data); }
+
+void hvxo_hm_derive_lists(hvxo_hm_pic *P) {
+  const int isb = P->slice_type == B_SLICE;
+  int gpb = isb && P->nref[0] == P->nref[1];
+  for (int i = 0; gpb && i < P->nref[1]; i++)
+    if (P->ref_poc[1][i] != P->ref_poc[0][i]) gpb = 0;
+  P->mvd_l1_zero = gpb;
+  for (int i = 0; i < 4; i++) {
+    P->l1_to_l0[i] = -1;
+    if (!isb || i >= P->nref[1]) continue;
+    for (int k = 0; k < P->nref[0]; k++)
+      if (P->ref_poc[0][k] == P->ref_poc[1][i]) { P->l1_to_l0[i] = k; break; }
+  }
+}

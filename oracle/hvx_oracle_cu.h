@@ -26,10 +26,13 @@ typedef struct hvxo_hm_pic {
   int chroma_qp[2];
   int max_merge, tmvp, check_ldc, col_from_l0, col_valid, col_poc;
   int col_ref_poc[2][4];
+  int mvd_l1_zero;                      /* TComSlice::getMvdL1ZeroFlag (TEncGOP.cpp:1311-1336) */
+  int l1_to_l0[4];                      /* TComSlice::getList1IdxToList0Idx (TComSlice.cpp:302) */
   const int16_t *col_field;             /* the collocated picture, [ctu][16 blocks of 16x16][8] (cu_capture.cpp) */
   double lambda, sqrt_lambda, chroma_weight[2], tq_lambda[3];
   uint32_t lambda_motion;
   int search_range, amp;
+  int bipred_range;                     /* BipredSearchRange (TEncSearch::m_bipredSearchRange) */
   const int32_t *entropy_bits;          /* ContextModel::m_entropyBits[128] */
   const int16_t *org[3];                /* original, sample (0,0) */
   int org_stride[3];
@@ -40,6 +43,11 @@ typedef struct hvxo_hm_pic {
   const uint8_t *const *ref_planes8;    /* [plane] luma sample (0,0), margin >= 80 */
   int ref_stride8;
 } hvxo_hm_pic;
+
+/* mvd_l1_zero and l1_to_l0 from the slice type and the reference POC lists, as HM derives them:
+ * a B slice whose L1 equals L0 entry by entry (GPB) codes no L1 MVD of bi-predicted PUs
+ * (TEncGOP.cpp:1311-1336); l1_to_l0[i] = the first L0 index of L1 entry i's picture, or -1. */
+void hvxo_hm_derive_lists(hvxo_hm_pic *pic);
 
 /* the picture's CTU data (TComPic::getCtu): opaque, hvxo_hm_ctu_data_size() bytes per CTU */
 typedef struct hvxo_hm_ctu_data hvxo_hm_ctu_data;

@@ -40,8 +40,42 @@ def smooth_frame(w: int, h: int, index: int) -> np.ndarray:
     return np.concatenate(out)
 
 
+def _texture_canvas(cw: int, ch: int, seed: int) -> np.ndarray:
+    """A static detailed texture: splitmix64 noise box-filtered twice (3x3) plus two sinusoids."""
+    n = (splitmix64_stream(seed, cw * ch) >> np.uint64(56)).astype(np.float64).reshape(ch, cw)
+    for _ in range(2):
+        p = np.pad(n, 1, mode="edge")
+        n = sum(p[dy:dy + ch, dx:dx + cw] for dy in range(3) for dx in range(3)) / 9.0
+    y, x = np.mgrid[0:ch, 0:cw].astype(np.float64)
+    return (n - 128.0) * 2.2 + 128.0 + 30 * np.sin(x * 0.21 + y * 0.07) + 20 * np.cos(y * 0.17 - x * 0.05)
+
+
+def texture_frame(w: int, h: int, index: int) -> np.ndarray:
+    """texture -- a detailed background in global motion (2, -1) per frame, two objects of another
+    texture moving on their own paths, per-frame noise of +-4: real uni / bi-prediction choices
+    (used for the randomaccess CTU captures)."""
+    out = []
+    for c, (cw, ch) in enumerate(((w, h), (w // 2, h // 2), (w // 2, h // 2))):
+        s = 1 if c == 0 else 2
+        pad = 96 // s
+        bg = _texture_canvas(cw + 2 * pad, ch + 2 * pad, 0x7E470000 + c)
+        ox, oy = pad + (2 * index) // s, pad - index // s
+        f = bg[oy:oy + ch, ox:ox + cw].copy()
+        obj = _texture_canvas(64 // s, 48 // s, 0x7E471000 + c) * 0.8 + 25
+        for k, (x0, y0, vx, vy) in enumerate(((40, 30, 5, 2), (260, 150, -3, -4))):
+            ax, ay = (x0 + vx * index) // s, (y0 + vy * index) // s
+            oh, ow = obj.shape
+            ys, xs = max(ay, 0), max(ax, 0)
+            ye, xe = min(ay + oh, ch), min(ax + ow, cw)
+            if ye > ys and xe > xs:
+                f[ys:ye, xs:xe] = obj[ys - ay:ye - ay, xs - ax:xe - ax] + 12 * k
+        noise = (splitmix64_stream(0x7E472000 + index * 7 + c, cw * ch) >> np.uint64(61)).astype(np.int64) - 4
+        out.append(np.clip(np.rint(f) + noise.reshape(ch, cw), 0, 255).astype(np.uint8).ravel())
+    return np.concatenate(out)
+
+
 def write_yuv(path: str, kind: str, w: int, h: int, frames: int) -> None:
-    gen = random_frame if kind == "random" else smooth_frame
+    gen = {"random": random_frame, "smooth": smooth_frame, "texture": texture_frame}[kind]
     with open(path, "wb") as f:
         for i in range(frames):
             f.write(gen(w, h, i).tobytes())

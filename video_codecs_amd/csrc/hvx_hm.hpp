@@ -770,7 +770,7 @@ __device__ void code_mvd(const Cu *cu, int rel, int list) {
 }
 __device__ void code_inter_dir(const Cu *cu, int rel) {
   const int d = cu->p[rel].inter_dir - 1, ctx = cu->p[rel].depth;
-  if (cu->p[rel].part == SIZE_2Nx2N || cu->width != 8) cbin(X_INTER_DIR + ctx, d == 2);
+  if (cu->p[rel].part == SIZE_2Nx2N || cu->p[rel].width != 8) cbin(X_INTER_DIR + ctx, d == 2);
   if (d < 2) cbin(X_INTER_DIR + 4, d);
 }
 __device__ void encode_pu_wise(const Cu *cu, int rel) {
