@@ -301,7 +301,8 @@ typedef struct hvx_mc_job {
 /* ---------------------------------------------------------------------------------------
  * HM-exact CTU decision (hvx_hm_compress; TEncCu::compressCtu TEncCu.cpp:228 + the CTU syntax
  * walk TEncCu::encodeCtu :252 that carries the CABAC contexts to the next CTU,
- * TEncSlice.cpp:814-828).  4:2:0 8-bit, the encoder_lowdelay_P_main.cfg tool set (see hvx.h).
+ * TEncSlice.cpp:814-828).  4:2:0 8-bit, the encoder_lowdelay_P_main.cfg / encoder_randomaccess_main.cfg
+ * tool set (see hvx.h): I, P and B slices.
  * ------------------------------------------------------------------------------------- */
 /* An RD coder of TEncCu: TEncSbac's 202 context states (m_ucState) + TEncBinCABACCounter::m_fracBits
  * (TEncSbac::load/store copy both, TEncSbac.cpp:396-425). */
@@ -349,7 +350,7 @@ typedef struct hvx_hm_picture {
   int32_t col_ref_poc[2][4];
   int32_t search_range, amp;
   uint32_t lambda_motion;    /* m_uiLambdaMotionSAD[0] */
-  int32_t pad_;
+  int32_t bipred_range;      /* BipredSearchRange (TEncSearch::m_bipredSearchRange, B slices) */
   double lambda, sqrt_lambda, chroma_weight[2], tq_lambda[3];
   const int16_t *col_field;
   const uint8_t *org[3];
@@ -358,8 +359,18 @@ typedef struct hvx_hm_picture {
   hvx_hm_ctu *ctus;
   const uint8_t *ref8[8];
   const int16_t *ref16[8][3];
-  int32_t ref8_stride, ref16_stride[2], pad2_;
+  int32_t ref8_stride, ref16_stride[2];
+  int32_t mvd_l1_zero;       /* TComSlice::getMvdL1ZeroFlag: L1 = L0 entry by entry (TEncGOP.cpp:1311-1336) */
+  int32_t l1_to_l0[4];       /* TComSlice::getList1IdxToList0Idx (TComSlice.cpp:302), -1: not in L0 */
   const int32_t *entropy_bits;  /* ContextModel::m_entropyBits[128] */
+  /* The cost TEncCu's comparisons use (xCheckBestMode TEncCu.cpp:1444 and the split cost):
+   * HVX_RD_SSE = HM's calcRdCost(bits, SSE); HVX_RD_SSIM = the stvssim encoder's SSIM cost
+   * J = D + lambda_ssim * max(0.5, bits) (rdopt.c:1631), D = sum over the CU's 8x8 luma / 4x4 chroma
+   * blocks of (1 - SSIM) / 4 (compute_SSIM stvssim.c:491, one window per block), lambda_ssim =
+   * lambda_2(QP) * eta^0.85 (stvssim.c:1805, :1707) computed by the caller.  The searches, merge
+   * estimation, RQT and RDOQ keep HM's SSE / SATD costs in both. */
+  int32_t rd_metric, pad3_;
+  double lambda_ssim;
 } hvx_hm_picture;
 
 /* One chain of CTUs decided in raster order by one wave: CTUs first_ctu .. first_ctu+n_ctus-1 of

@@ -16,9 +16,10 @@
 // reconstruction into TComPicYuv rec (xCopyYuv2Pic).  HM's own encodeCtu, loop filters, SAO and
 // slice writer then run on that data unchanged.
 //
-// Served: I and P slices (the engine's tool set: HM's lowdelay_P settings, 4:2:0 8-bit, CTU 64,
-// no dQP / TQ bypass / RDPCM / cross-component prediction / weighted prediction); anything else
-// falls through to the reference's compressCtu (counted).  HVX_SEAM_CU=1 enables the seam.
+// Served: I, P and B slices (the engine's tool set: HM's lowdelay_P / randomaccess settings, 4:2:0
+// 8-bit, CTU 64, no dQP / TQ bypass / RDPCM / cross-component prediction / weighted prediction / PCM /
+// rate control / adaptive search range); anything else falls through to the reference's
+// compressCtu (counted).  HVX_SEAM_CU=1 enables the seam.
 #include <sstream>
 #include <iostream>
 #include <vector>
@@ -162,11 +163,12 @@ bool begin_picture(TEncCu *cu, TComDataCU *ctu) {
   const TComSPS &sps = *s->getSPS();
   const TComPPS &pps = *s->getPPS();
   const int st = s->getSliceType();
-  const bool ok = (st == I_SLICE || st == P_SLICE) && sps.getChromaFormatIdc() == CHROMA_420 &&
+  const bool ok = (st == I_SLICE || st == P_SLICE || st == B_SLICE) && sps.getChromaFormatIdc() == CHROMA_420 &&
                   sps.getBitDepth(CHANNEL_TYPE_LUMA) == 8 && sps.getBitDepth(CHANNEL_TYPE_CHROMA) == 8 &&
                   sps.getMaxCUWidth() == 64 && sps.getMaxCUHeight() == 64 && sps.getMaxTotalCUDepth() == 4 &&
                   !pps.getUseDQP() && !pps.getTransquantBypassEnableFlag() && !pps.getUseWP() &&
-                  !s->getUseChromaQpAdj() && s->getNumRefIdx(REF_PIC_LIST_0) <= 4 &&
+                  !pps.getWPBiPred() && !s->getUseChromaQpAdj() && s->getNumRefIdx(REF_PIC_LIST_0) <= 4 &&
+                  (st != B_SLICE || s->getNumRefIdx(REF_PIC_LIST_1) <= 4) && !sps.getUsePCM() &&
                   pic->getPicSym()->getNumTiles() == 1 && !sps.getScalingListFlag() &&
                   sps.getQuadtreeTULog2MaxSize() == 5 && sps.getQuadtreeTULog2MinSize() == 2 &&
                   sps.getQuadtreeTUMaxDepthInter() == 3 && sps.getQuadtreeTUMaxDepthIntra() == 3 &&
@@ -177,7 +179,9 @@ bool begin_picture(TEncCu *cu, TComDataCU *ctu) {
   const bool tools = cfg->getUseRDOQ() && cfg->getUseRDOQTS() && !cfg->getUseSelectiveRDOQ() && cfg->getFastSearch() == 1 &&
                      cfg->getUseHADME() && cfg->getUseFastEnc() && cfg->getUseFastDecisionForMerge() &&
                      !cfg->getUseEarlySkipDetection() && !cfg->getUseCbfFastMode() && !cfg->getUseEarlyCU() &&
-                     cfg->getUseTransformSkipFast() && !cfg->getUseAdaptQpSelect();
+                     cfg->getUseTransformSkipFast() && !cfg->getUseAdaptQpSelect() && !cfg->getUseRateCtrl() &&
+                     !cfg->getUsePCM() && !cfg->getUseASR() && !cfg->getUseAdaptiveQP() &&
+                     cfg->getFastMEForGenBLowDelayEnabled() && !cfg->getClipForBiPredMeEnabled();
   if (!ok || !tools) return false;
   g.w = sps.getPicWidthInLumaSamples();
   g.h = sps.getPicHeightInLumaSamples();
@@ -189,12 +193,28 @@ bool begin_picture(TEncCu *cu, TComDataCU *ctu) {
   P.poc = s->getPOC();
   P.slice_type = st;
   P.qp = s->getSliceQp();
+  // reference lists: list 0's pictures take planes 0.., a list-1 picture list 0 does not hold the next one
   const int nref = st == I_SLICE ? 0 : s->getNumRefIdx(REF_PIC_LIST_0);
+  const int nref1 = st == B_SLICE ? s->getNumRefIdx(REF_PIC_LIST_1) : 0;
   P.nref[0] = nref;
-  for (int i = 0; i < 4; i++) {
-    P.ref_poc[0][i] = i < nref ? s->getRefPOC(REF_PIC_LIST_0, i) : 0;
-    P.ref_plane[0][i] = i < nref ? i : 0;
-  }
+  P.nref[1] = nref1;
+  TComPic *plane_pic[8] = {};
+  int nplanes = 0;
+  for (int l = 0; l < 2; l++)
+    for (int i = 0; i < 4; i++) {
+      const int n = l ? nref1 : nref;
+      P.ref_poc[l][i] = i < n ? s->getRefPOC(RefPicList(l), i) : 0;
+      P.ref_plane[l][i] = 0;
+      if (i >= n) continue;
+      TComPic *rp = s->getRefPic(RefPicList(l), i);
+      int k = 0;
+      while (k < nplanes && plane_pic[k]->getPOC() != rp->getPOC()) k++;
+      if (k == nplanes) plane_pic[nplanes++] = rp;
+      P.ref_plane[l][i] = k;
+    }
+  P.mvd_l1_zero = st == B_SLICE && s->getMvdL1ZeroFlag();
+  for (int i = 0; i < 4; i++) P.l1_to_l0[i] = (st == B_SLICE && i < nref1) ? s->getList1IdxToList0Idx(i) : -1;
+  P.bipred_range = cu->m_pcPredSearch->m_bipredSearchRange;
   for (int c = 1; c < 3; c++) {
     const QpParam q(*ctu, ComponentID(c));  // getScaledChromaQP of the slice QP
     P.chroma_qp[c - 1] = q.Qp;
@@ -241,9 +261,9 @@ bool begin_picture(TEncCu *cu, TComDataCU *ctu) {
   void *dct = g.ctus.get(nct);
   upload(dct, g.stage.data(), nct);
   P.ctus = (hvx_hm_ctu *)dct;
-  // references: the reconstructed (loop-filtered) reference pictures of list 0
-  for (int i = 0; i < nref; i++) {
-    const RefPlanes &r = ref_planes(i, s->getRefPic(REF_PIC_LIST_0, i));
+  // references: the reconstructed (loop-filtered) reference pictures of both lists
+  for (int i = 0; i < nplanes; i++) {
+    const RefPlanes &r = ref_planes(i, plane_pic[i]);
     P.ref8[i] = r.o8;
     P.ref8_stride = r.s8;
     for (int c = 0; c < 3; c++) P.ref16[i][c] = r.o16[c];
@@ -252,7 +272,7 @@ bool begin_picture(TEncCu *cu, TComDataCU *ctu) {
   }
   // the collocated picture's compressed motion field (xGetColMVP, TComDataCU.cpp:3061)
   if (st != I_SLICE && s->getEnableTMVPFlag()) {
-    TComPic *colp = s->getRefPic(REF_PIC_LIST_0, s->getColRefIdx());
+    TComPic *colp = s->getRefPic(RefPicList(s->isInterB() ? 1 - s->getColFromL0Flag() : 0), s->getColRefIdx());
     TComSlice *cs = colp->getSlice(0);
     P.col_valid = 1;
     P.col_poc = cs->getPOC();

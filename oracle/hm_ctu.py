@@ -30,6 +30,9 @@ def _lib():
         L.hvxo_hm_replay_picture.restype = ctypes.c_int
         L.hvxo_hm_replay_picture.argtypes = [P, P, P, P, P, ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
                                              ctypes.c_int, P, P, P, P, P, P, P]
+        L.hvxo_hm_replay_picture_rd.restype = ctypes.c_int
+        L.hvxo_hm_replay_picture_rd.argtypes = [P, P, P, P, P, ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P, P, P, P, P, P]
         L._hm_ctu_bound = True
     return L
 
@@ -47,8 +50,9 @@ def load(path):
     return golden_io.load(path)
 
 
-def replay(g, pic, mode=0, slice_ctus=0):
-    """Replay picture `pic` of capture g; returns a dict of the restatement's per-CTU outputs."""
+def replay(g, pic, mode=0, slice_ctus=0, rd_metric=0, lambda_ssim=0.0):
+    """Replay picture `pic` of capture g; returns a dict of the restatement's per-CTU outputs.
+    rd_metric 1: the CU decision compares the stvssim SSIM cost (lambda_ssim) instead of HM's."""
     L = _lib()
     pi = np.ascontiguousarray(g["pic_i32"][pic], np.int32)
     pf = np.ascontiguousarray(g["pic_f64"][pic], np.float64)
@@ -76,11 +80,11 @@ def replay(g, pic, mode=0, slice_ctus=0):
            "bits_dist": np.zeros((n, 2), np.uint32), "states": np.zeros((n, 202), np.uint8),
            "frac": np.zeros(n, np.int64)}
     eb = entropy_bits()
-    L.hvxo_hm_replay_picture(_ptr(pi), _ptr(pf), _ptr(org), _ptr(refs), _ptr(np.ascontiguousarray(g["refpic_poc"])),
-                             nref, _ptr(col), _ptr(eb), _ptr(states), _ptr(frac), _ptr(int2n), _ptr(hparts),
-                             _ptr(hcoef), _ptr(hrec), mode, slice_ctus, _ptr(out["parts"]), _ptr(out["coef"]),
-                             _ptr(out["recon"]), _ptr(out["cost"]), _ptr(out["bits_dist"]), _ptr(out["states"]),
-                             _ptr(out["frac"]))
+    L.hvxo_hm_replay_picture_rd(_ptr(pi), _ptr(pf), _ptr(org), _ptr(refs), _ptr(np.ascontiguousarray(g["refpic_poc"])),
+                                nref, _ptr(col), _ptr(eb), _ptr(states), _ptr(frac), _ptr(int2n), _ptr(hparts),
+                                _ptr(hcoef), _ptr(hrec), mode, slice_ctus, int(rd_metric), float(lambda_ssim),
+                                _ptr(out["parts"]), _ptr(out["coef"]), _ptr(out["recon"]), _ptr(out["cost"]),
+                                _ptr(out["bits_dist"]), _ptr(out["states"]), _ptr(out["frac"]))
     return out
 
 

@@ -95,6 +95,7 @@ typedef struct {
   int32_t coef[3][4096];
   uint32_t bits, dist;
   double cost;
+  double dssim;   /* HVX_RD_SSIM: the SSIM distortion of the CU's reconstruction (cu_dssim) */
   int merge_amp;
 } hm_cu;
 
@@ -414,7 +415,7 @@ static void cu_init_est(hm_cu *cu, int qp) {
   memset(cu->coef[0], 0, sizeof(int32_t) * n);
   memset(cu->coef[1], 0, sizeof(int32_t) * (n >> 2));
   memset(cu->coef[2], 0, sizeof(int32_t) * (n >> 2));
-  cu->bits = 0; cu->dist = 0; cu->cost = MAX_DOUBLE;
+  cu->bits = 0; cu->dist = 0; cu->cost = MAX_DOUBLE; cu->dssim = 0;
 }
 /* initSubCU (:623) / initCtu (:434): geometry, then the same resets */
 static void cu_init_sub(hm_cu *cu, const hm_cu *parent, int idx, int depth, int qp) {
@@ -431,6 +432,7 @@ static void cu_init_sub(hm_cu *cu, const hm_cu *parent, int idx, int depth, int 
 static void cu_copy_part_from(hm_cu *dst, const hm_cu *src, int idx, int depth) {
   dst->cost += src->cost;
   dst->dist += src->dist;
+  dst->dssim += src->dssim;
   dst->bits += src->bits;
   const int off = src->nparts * idx;
   memcpy(&dst->p[off], src->p, sizeof(hm_part) * src->nparts);
@@ -1220,6 +1222,53 @@ static double rd_cost(const hm_enc *e, uint32_t bits, uint32_t dist) {
 static double rd_cost_sad(const hm_enc *e, uint32_t bits, uint32_t dist) {
   return floor((double)dist + (floor((double)bits * (double)e->pic->lambda_motion + 0.5) / 65536.0));
 }
+/* The SSIM RD cost of the CU decision (hvx_hm_picture.rd_metric = HVX_RD_SSIM; the stvssim JM
+ * encoder's mode-decision cost, rdopt.c:1631 J = D + lambda * max(0.5, R) with D = 1 - SSIM per
+ * component, distortionSSIM stvssim.c:567-584, and lambda = lambda_2(QP) * eta^0.85, stvssim.c:1805,
+ * :1707), adapted to HEVC CUs: D of a CU = sum over its 8x8 luma blocks of (1 - SSIM) (one 8x8
+ * window, compute_SSIM stvssim.c:491-566) plus over its 4x4 Cb and Cr blocks (one 4x4 window),
+ * each term weighted 1/4 so that a 16x16 area weighs as one JM macroblock; blocks outside the
+ * picture are skipped; the terms are summed in double, luma blocks in raster order, then Cb, Cr.
+ * Only TEncCu's mode and split comparisons use it (xCheckBestMode :1444 and the split cost); the
+ * searches, merge estimation, RQT and RDOQ below keep HM's SSE / SATD costs. */
+static float ssim_block16(const int16_t *o, const int16_t *r, int stride, int wint) {
+  const float C1 = 0.01f * 0.01f * (float)(255 * 255), C2 = 0.03f * 0.03f * (float)(255 * 255);
+  const float wgt = 1.0f / (float)(wint * wint);
+  float mo = 0, me = 0, vo = 0, ve = 0, cov = 0;
+  for (int n = 0; n < wint; n++)
+    for (int m = 0; m < wint; m++) {
+      const int po = o[n * stride + m], pe = r[n * stride + m];
+      mo += wgt * po; me += wgt * pe;
+      vo += wgt * po * po; ve += wgt * pe * pe; cov += wgt * po * pe;
+    }
+  const float varo = fabsf(vo - mo * mo), vare = fabsf(ve - me * me), covo = fabsf(cov - mo * me);
+  float v = (float)((2.0 * mo * me + C1) * (2.0 * covo + C2));
+  v /= (float)(mo * mo + me * me + C1) * (varo + vare + C2);
+  if (v >= 1.0 && v < 1.01) v = 1.0f;
+  return v;
+}
+static double cu_dssim(const hm_enc *e, const hm_cu *cu, yuv_t *org, yuv_t *reco) {
+  const hvxo_hm_pic *P = e->pic;
+  double d = 0;
+  for (int c = 0; c < 3; c++) {
+    const int s = c ? 1 : 0, b = c ? 4 : 8, n = (cu->width >> s) / b;
+    for (int by = 0; by < n; by++)
+      for (int bx = 0; bx < n; bx++) {
+        if (((cu->x >> s) + bx * b) >= (P->w >> s) || ((cu->y >> s) + by * b) >= (P->h >> s)) continue;
+        const float v = ssim_block16(yaddr(org, c, bx * b, by * b), yaddr(reco, c, bx * b, by * b), ystride(c), b);
+        d += 0.25 * (double)(1.0f - v);
+      }
+  }
+  return d;
+}
+/* the cost TEncCu compares: calcRdCost(bits, dist) (SSE) or the SSIM cost */
+static double cu_cost(const hm_enc *e, const hm_cu *cu, uint32_t bits, uint32_t dist) {
+  if (e->pic->rd_metric != 1) return rd_cost(e, bits, dist);
+  return cu->dssim + e->pic->lambda_ssim * ((double)bits > 0.5 ? (double)bits : 0.5);
+}
+static void cu_measure_ssim(const hm_enc *e, hm_cu *cu, yuv_t *org, yuv_t *reco) {
+  if (e->pic->rd_metric == 1) cu->dssim = cu_dssim(e, cu, org, reco);
+}
 static uint32_t mv_cost_bits(const hm_enc *e, uint32_t bits) { return (uint32_t)(e->pic->lambda_motion * bits) >> 16; }
 static uint32_t dist_part(const hm_enc *e, const int16_t *a, int sa, const int16_t *b, int sb, int w, int h, int comp) {
   const uint32_t sse = hvxo_sse(a, sa, b, sb, w, h);
@@ -1527,7 +1576,9 @@ static void enc_res_rd_inter(hm_enc *e, hm_cu *cu, yuv_t *org, yuv_t *pred, yuv_
     code_skip_flag(e, cu, 0);
     code_merge_index(e, cu, 0);
     const uint32_t bits = written_bits(e);
-    cu->bits = bits; cu->dist = dist; cu->cost = rd_cost(e, bits, dist);
+    cu->bits = bits; cu->dist = dist;
+    cu_measure_ssim(e, cu, org, reco);
+    cu->cost = cu_cost(e, cu, bits, dist);
     load(&e->rd[depth][CI_TEMP_BEST], e->cur);
     return;
   }
@@ -1558,7 +1609,9 @@ static void enc_res_rd_inter(hm_enc *e, hm_cu *cu, yuv_t *org, yuv_t *pred, yuv_
   load(&e->rd[depth][CI_TEMP_BEST], e->cur);
   yuv_add_clip(reco, pred, resi_best, W);
   const uint32_t final_dist = yuv_dist(e, reco, org, W);
-  cu->bits = final_bits; cu->dist = final_dist; cu->cost = rd_cost(e, final_bits, final_dist);
+  cu->bits = final_bits; cu->dist = final_dist;
+  cu_measure_ssim(e, cu, org, reco);
+  cu->cost = cu_cost(e, cu, final_bits, final_dist);
 }
 
 /* ============================================================================================
@@ -2527,7 +2580,7 @@ static void check_rd_inter(hm_enc *e, int depth, int ps, int use_mrg) {
   tmp->merge_amp = 1;
   pred_inter_search(e, tmp, e->orig[depth], e->pred_temp[depth], use_mrg);
   enc_res_rd_inter(e, tmp, e->orig[depth], e->pred_temp[depth], e->resi_temp[depth], e->resi_best[depth], e->reco_temp[depth], 0);
-  tmp->cost = rd_cost(e, tmp->bits, tmp->dist);
+  tmp->cost = cu_cost(e, tmp, tmp->bits, tmp->dist);
   check_best_mode(e, depth);
 }
 static void check_rd_intra(hm_enc *e, int depth, int ps) {
@@ -2546,7 +2599,8 @@ static void check_rd_intra(hm_enc *e, int depth, int ps) {
   encode_coeff(e, tmp, 0);
   load(&e->rd[depth][CI_TEMP_BEST], e->cur);
   tmp->bits = written_bits(e);
-  tmp->cost = rd_cost(e, tmp->bits, tmp->dist);
+  cu_measure_ssim(e, tmp, e->orig[depth], e->reco_temp[depth]);
+  tmp->cost = cu_cost(e, tmp, tmp->bits, tmp->dist);
   check_best_mode(e, depth);
 }
 static void derive_test_mode_amp(const hm_cu *best, int parent_ps, int *hor, int *ver, int *mhor, int *mver) {
@@ -2625,7 +2679,7 @@ static void compress_cu(hm_enc *e, int depth, int parent_ps) {
     reset_bits(e);
     code_split_flag(e, best, 0, depth);
     best->bits += written_bits(e);
-    best->cost = rd_cost(e, best->bits, best->dist);
+    best->cost = cu_cost(e, best, best->bits, best->dist);
     load(&e->rd[depth][CI_NEXT_BEST], e->cur);
     sub_branch = 1; /* ECU off */
   } else boundary = 1;
@@ -2659,7 +2713,7 @@ static void compress_cu(hm_enc *e, int depth, int parent_ps) {
       code_split_flag(e, tmp, 0, depth);
       tmp->bits += written_bits(e);
     }
-    tmp->cost = rd_cost(e, tmp->bits, tmp->dist);
+    tmp->cost = cu_cost(e, tmp, tmp->bits, tmp->dist);
     load(&e->rd[depth][CI_TEMP_BEST], e->cur);
     check_best_mode(e, depth);
   }
@@ -2906,11 +2960,24 @@ int hvxo_hm_replay_picture(const int32_t *pi, const double *pf, const uint8_t *o
                            const int16_t *hm_parts, const int32_t *hm_coef, const uint8_t *hm_recon, int mode,
                            int slice_ctus, int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost,
                            uint32_t *out_bits_dist, uint8_t *out_states, int64_t *out_frac) {
+  return hvxo_hm_replay_picture_rd(pi, pf, org, refpics, refpic_poc, n_refpics, col_field, entropy_bits, ctu_states, ctu_frac,
+                                   ctu_int2n, hm_parts, hm_coef, hm_recon, mode, slice_ctus, 0, 0.0, out_parts, out_coef,
+                                   out_recon, out_cost, out_bits_dist, out_states, out_frac);
+}
+int hvxo_hm_replay_picture_rd(const int32_t *pi, const double *pf, const uint8_t *org, const uint8_t *refpics,
+                              const int32_t *refpic_poc, int n_refpics, const int16_t *col_field, const int32_t *entropy_bits,
+                              const uint8_t *ctu_states, const int64_t *ctu_frac, const int16_t *ctu_int2n,
+                              const int16_t *hm_parts, const int32_t *hm_coef, const uint8_t *hm_recon, int mode,
+                              int slice_ctus, int rd_metric, double lambda_ssim, int16_t *out_parts, int32_t *out_coef,
+                              uint8_t *out_recon, double *out_cost, uint32_t *out_bits_dist, uint8_t *out_states,
+                              int64_t *out_frac) {
   (void)refpic_poc;
   tables_init();
   const int w = pi[P_W], h = pi[P_H], wc = (w + 63) / 64, hc = (h + 63) / 64, n = wc * hc;
   pic_buf B;
   pic_setup(&B, pi, pf, org, refpics, n_refpics, col_field, entropy_bits);
+  B.P.rd_metric = rd_metric;
+  B.P.lambda_ssim = lambda_ssim;
   const hvxo_hm_pic P = B.P;
   /* the picture's CTU data and reconstruction (whole CTUs) */
   hvxo_hm_ctu_data *ctus = (hvxo_hm_ctu_data *)calloc((size_t)n, sizeof(hvxo_hm_ctu_data));
@@ -3048,6 +3115,15 @@ int hvxo_hm_chains(const int32_t *pi, const double *pf, const uint8_t *org, cons
                    const int16_t *col_field, const int32_t *entropy_bits, const uint8_t *entry_states, int n_chains,
                    const int32_t *chain_first, int ctus_per_chain, int slice_ctus, int n_threads, int16_t *out_parts,
                    int32_t *out_coef, uint8_t *out_recon, double *out_cost, uint32_t *out_bits_dist) {
+  return hvxo_hm_chains_rd(pi, pf, org, refpics, n_refpics, col_field, entropy_bits, entry_states, n_chains, chain_first,
+                           ctus_per_chain, slice_ctus, n_threads, 0, 0.0, out_parts, out_coef, out_recon, out_cost,
+                           out_bits_dist);
+}
+int hvxo_hm_chains_rd(const int32_t *pi, const double *pf, const uint8_t *org, const uint8_t *refpics, int n_refpics,
+                      const int16_t *col_field, const int32_t *entropy_bits, const uint8_t *entry_states, int n_chains,
+                      const int32_t *chain_first, int ctus_per_chain, int slice_ctus, int n_threads, int rd_metric,
+                      double lambda_ssim, int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost,
+                      uint32_t *out_bits_dist) {
   tables_init();
   hvxo_init_tables();
   if (pi[P_COL_VALID] && !col_field) return -1;
@@ -3058,6 +3134,8 @@ int hvxo_hm_chains(const int32_t *pi, const double *pf, const uint8_t *org, cons
       return -1;
   pic_buf B;
   pic_setup(&B, pi, pf, org, refpics, n_refpics, col_field, entropy_bits);
+  B.P.rd_metric = rd_metric;
+  B.P.lambda_ssim = lambda_ssim;
   hvxo_hm_ctu_data *ctus = (hvxo_hm_ctu_data *)calloc((size_t)n, sizeof(hvxo_hm_ctu_data));
   const int rw = wc * 64, rh = hc * 64;
   int16_t *recb[3];

@@ -33,6 +33,8 @@ typedef struct hvxo_hm_pic {
   uint32_t lambda_motion;
   int search_range, amp;
   int bipred_range;                     /* BipredSearchRange (TEncSearch::m_bipredSearchRange) */
+  int rd_metric;                        /* 0: HM's SSE cost; 1: the stvssim SSIM cost in TEncCu's comparisons */
+  double lambda_ssim;                   /* rd_metric 1: lambda_2(QP) * eta^0.85 (stvssim.c:1805, :1707) */
   const int32_t *entropy_bits;          /* ContextModel::m_entropyBits[128] */
   const int16_t *org[3];                /* original, sample (0,0) */
   int org_stride[3];
@@ -85,6 +87,16 @@ int hvxo_hm_replay_picture(const int32_t *pic_i32, const double *pic_f64, const 
                            int slice_ctus, int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost,
                            uint32_t *out_bits_dist, uint8_t *out_states, int64_t *out_frac);
 
+/* The same with the CU decision's cost selected: rd_metric 0 = HM's SSE cost (as above), 1 = the
+ * stvssim SSIM cost with lambda_ssim (hvxo_hm_pic.rd_metric) */
+int hvxo_hm_replay_picture_rd(const int32_t *pic_i32, const double *pic_f64, const uint8_t *org, const uint8_t *refpics,
+                              const int32_t *refpic_poc, int n_refpics, const int16_t *col_field, const int32_t *entropy_bits,
+                              const uint8_t *ctu_states, const int64_t *ctu_frac, const int16_t *ctu_int2n,
+                              const int16_t *hm_parts, const int32_t *hm_coef, const uint8_t *hm_recon, int mode,
+                              int slice_ctus, int rd_metric, double lambda_ssim, int16_t *out_parts, int32_t *out_coef,
+                              uint8_t *out_recon, double *out_cost, uint32_t *out_bits_dist, uint8_t *out_states,
+                              int64_t *out_frac);
+
 /* Independent SliceMode=1 slice chains (slices of slice_ctus CTUs): chain k decides CTUs
  * chain_first[k] .. + ctus_per_chain - 1 from entry_states (the slice-start contexts) and a zero
  * m_integerMv2Nx2N, carrying both CTU to CTU; the chains run on n_threads threads.  Picture
@@ -93,6 +105,12 @@ int hvxo_hm_chains(const int32_t *pic_i32, const double *pic_f64, const uint8_t 
                    int n_refpics, const int16_t *col_field, const int32_t *entropy_bits, const uint8_t *entry_states,
                    int n_chains, const int32_t *chain_first, int ctus_per_chain, int slice_ctus, int n_threads,
                    int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost, uint32_t *out_bits_dist);
+
+int hvxo_hm_chains_rd(const int32_t *pic_i32, const double *pic_f64, const uint8_t *org, const uint8_t *refpics,
+                      int n_refpics, const int16_t *col_field, const int32_t *entropy_bits, const uint8_t *entry_states,
+                      int n_chains, const int32_t *chain_first, int ctus_per_chain, int slice_ctus, int n_threads,
+                      int rd_metric, double lambda_ssim, int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon,
+                      double *out_cost, uint32_t *out_bits_dist);
 
 #ifdef __cplusplus
 }

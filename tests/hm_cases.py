@@ -10,7 +10,8 @@ from tests import golden_cases as gc
 from video_codecs_amd import _abi
 from video_codecs_amd import hm
 
-CAPTURES = ("ctu_ldp_rand.bin", "ctu_ldp_smooth.bin", "ctu_ldp_slices.bin")
+CAPTURES = ("ctu_ldp_rand.bin", "ctu_ldp_smooth.bin", "ctu_ldp_slices.bin", "ctu_ra_q22.bin", "ctu_ra_q27.bin",
+            "ctu_ra_q32.bin", "ctu_ra_q37.bin")
 # captures encoded with SliceMode=1 SliceArgument=<CTUs per row>: every CTU row is a slice
 ROW_SLICES = {"ctu_ldp_slices.bin"}
 LAST_ENGINE = [None]

@@ -19,6 +19,7 @@ CASES = {  # name: (cfg, yuv kind, frames, qp)
     "ldb_smooth_qp32": ("ldb.cfg", "smooth", 3, 32),  # B slices: bi-prediction, identical-motion shortcut
     "ldp_rand_qp32": ("ldp.cfg", "random", 2, 32),    # uniform random: long TZ raster searches
     "ra_smooth_qp27": ("ra.cfg", "smooth", 9, 27),    # GOP8 hierarchical B: future refs, bBi refinement
+    "ra_texture_qp32": ("ra.cfg", "texture", 9, 32),  # textured content in motion: uni-L0 / uni-L1 / bi AMVP choices
 }
 YUV_FRAMES = max(c[2] for c in CASES.values())
 W, H = 416, 240

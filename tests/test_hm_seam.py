@@ -67,10 +67,10 @@ def test_expected_md5_cases_present():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)  # one synchronous single-CTU launch per compressCtu call: correctness, not speed
-@pytest.mark.parametrize("case", ["ldp_rand_qp32", "ldp_smooth_qp32", "intra_rand_qp32", "intra_smooth_qp22"])
+@pytest.mark.parametrize("case", ["ldp_rand_qp32", "ldp_smooth_qp32", "intra_rand_qp32", "intra_smooth_qp22", "ra_texture_qp32"])
 def test_hm_encoder_with_cu_seam(case, monkeypatch):
-    """The L3 boundary: every TEncCu::compressCtu of an unchanged TAppEncoder LDP encode (I + P
-    pictures) served by the HM-exact CTU engine (integration/hm_cu_seam.cpp -> hvx_hm_compress),
+    """The L3 boundary: every TEncCu::compressCtu of an unchanged TAppEncoder encode (LDP: I + P
+    pictures; RA: I + hierarchical GOP8 B pictures) served by the HM-exact CTU engine (integration/hm_cu_seam.cpp -> hvx_hm_compress),
     HM's own encodeCtu / loop filters / SAO / slice writer (with the device deblocking, SAO and
     residual-writer seams) downstream: the bitstream and reconstruction MD5 of the reference."""
     import torch

@@ -131,3 +131,53 @@ def test_hm_chains_rejects_bad_layout():
                       col_field=g["col_field"][448:896])
     with pytest.raises(ValueError):  # TMVP on without a collocated field
         hm_ctu.chains(pi, pf, g["org"][2 * psz:3 * psz], g["refpic"], g["ctu_states"][56], [0], 1, 7)
+
+
+RA_CAPTURES = ["ctu_ra_q22.bin", "ctu_ra_q27.bin", "ctu_ra_q32.bin", "ctu_ra_q37.bin"]
+
+
+@pytest.mark.parametrize("name", RA_CAPTURES)
+def test_ctu_ra_chained_vs_hm(name):
+    """B slices (encoder_randomaccess_main.cfg, QP 22/27/32/37, textured content in motion): the
+    chained restatement bit-exact on every captured B picture -- uni-L0 / uni-L1 / bi AMVP with
+    the bBi refinement (TEncSearch.cpp:3096-3251), FastMEForGenBLowDelay list-1 reuse, the GPB
+    picture's MvdL1Zero path, combined-bi merge candidates, L1 TMVP."""
+    _replay_all(_load(name), 1, name)
+
+
+def _replay_all(g, mode, name):
+    """Replay every picture of a capture, the pictures on parallel threads (ctypes drops the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    npic = g["pic_i32"].shape[0]
+    with ThreadPoolExecutor(max_workers=min(npic, 8)) as ex:
+        outs = list(ex.map(lambda pic: hm_ctu.replay(g, pic, mode=mode), range(npic)))
+    for pic, out in enumerate(outs):
+        bad = hm_ctu.compare(g, pic, out, verbose=False)
+        assert not bad, (name, pic, bad[:3])
+
+
+def test_ctu_ra_entry_state_vs_hm():
+    """mode 0 on the B pictures of the QP 22 capture: every CTU from HM's own entry state."""
+    _replay_all(_load("ctu_ra_q22.bin"), 0, "ctu_ra_q22.bin")
+
+
+def test_ctu_ra_capture_covers_b_modes():
+    """The RA fixtures exercise the B-slice branches: every inter direction chosen by AMVP (not
+    merge), bi PUs with a coded L1 MVD and GPB pictures (L1 = L0: MvdL1ZeroFlag), lists that
+    share pictures (FastMEForGenB) and disjoint ones (uni-L1 candidates)."""
+    import numpy as np
+    f = {n: i for i, n in enumerate(hm_ctu.PART_FIELDS)}
+    dirs, mvd1, gpb, shared, disjoint = set(), 0, 0, 0, 0
+    for name in RA_CAPTURES:
+        g = _load(name)
+        p = g["ctu_parts"].reshape(-1, 29)
+        amvp = (p[:, f["pred"]] == 0) & (p[:, f["merge"]] == 0)
+        dirs |= set(np.unique(p[amvp, f["inter_dir"]]).tolist())
+        mvd1 += int((amvp & (p[:, f["inter_dir"]] == 3) & ((p[:, f["mvd1x"]] != 0) | (p[:, f["mvd1y"]] != 0))).sum())
+        for pi in g["pic_i32"]:
+            n0, n1 = int(pi[5]), int(pi[6])
+            l0, l1 = list(pi[7:7 + n0]), list(pi[11:11 + n1])
+            gpb += int(l0 == l1)
+            shared += int(bool(set(l0) & set(l1)) and l0 != l1)
+            disjoint += int(any(x not in l0 for x in l1))
+    assert dirs == {1, 2, 3} and mvd1 > 0 and gpb and shared and disjoint, (dirs, mvd1, gpb, shared, disjoint)

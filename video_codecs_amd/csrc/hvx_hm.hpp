@@ -75,6 +75,7 @@ struct Cu {
   int depth, zidx, x, y, nparts, width;
   uint32_t bits, dist;
   double cost;
+  double dssim;  // HVX_RD_SSIM: the SSIM distortion of the CU's reconstruction (cu_dssim)
   int merge_amp, pad_;
   Part p[256];
   int16_t coef[6144];  // Y 4096 | Cb 1024 | Cr 1024, TU-packed
@@ -88,7 +89,10 @@ __device__ __forceinline__ int16_t *yaddr(Yuv *b, int c, int x, int y) { return 
 
 // the leaf scratch of motion search and motion compensation (in the chain state: global memory)
 struct MeScratch {
-  MeFracSmem<64, 1> sm;
+  union {
+    MeFracSmem<64, 1> sm;             // uni search: the original (8-bit) pattern
+    MeFracSmem<64, 1, int16_t> sm16;  // bi refinement: the 2 * org - pred(other list) target
+  };
   uint32_t red[2 * kMeMaxRanges];
   hvx_me_result r;
 };
@@ -129,6 +133,7 @@ struct State {
   Cu cu[8];
   Yuv yuv[28];                    // TComYuv sets (kind x depth), addressed through hm_e.yi
   Yuv qt_yuv[4], qt_ts_yuv, tmp_yuv_pred;
+  int16_t pred_l[2][64 * 64];     // TEncSearch::m_acYuvPred[list] (luma: the bi search's other-list prediction)
   int16_t qt_coef[4][6144];       // m_ppcQTTempCoeff[comp][layer]
   int16_t qt_tu_coef[6144];       // m_pcQTTempTUCoeff (Y | Cb | Cr)
   int16_t shared_pred[6144];      // m_pSharedPredTransformSkip
@@ -177,6 +182,20 @@ union Leaf {
   } cs;
 };
 
+// AMVP candidates of one (list, reference) (AMVPInfo)
+struct Amvp { int n; int16_t c[3][2]; };
+// predInterSearch's per-PU records (TEncSearch.cpp:2937-2995: cMvTemp, cMvPred(Bi), aaiMvpIdx(Bi),
+// aaiMvpNum, aacAMVPInfo, uiCostTempL0, ...): wave-uniform, indexed by list / reference, in LDS
+struct InterSearch {
+  Amvp amvp[2][4];
+  int16_t mvtemp[2][4][2], mvpred[2][4][2], mvpredbi[2][4][2];
+  int mvp_idx[2][4], mvp_num[2][4], mvp_idx_bi[2][4];
+  uint32_t cost_l0[4], bits_l0[4];
+  uint32_t cost[2], bits[3], motbits[2];
+  int16_t mv[2][2], mvbi[2][2];
+  int ref[2], refbi[2];
+};
+
 // the decision's LDS-resident context (TEncCu / TEncSearch / TComTrQuant scalars + coders)
 struct Enc {
   hvx_hm_picture P;
@@ -194,6 +213,8 @@ struct Enc {
   uint16_t scan[256];    // the current TU's scan tables (TUs up to 16x16), staged by tu_fwd_l
   uint8_t scan_cg[16];
   uint32_t avail[4];
+  InterSearch is;
+  float ssim_t[192];     // HVX_RD_SSIM: the (1 - SSIM) terms of a CU's blocks (cu_dssim)
   int dbg[4];  // HM_CHECKS: first violated check (code, a, b) of the job
   int stage, stop;  // HM_CHECKS: stop the CTU at debugging stage `stage` (0: never)
 #ifdef HM_PROFILE
@@ -571,7 +592,7 @@ __device__ void cu_init_est(Cu *cu, int qp) {
   for (int i = lid(); i < (ny >> 1); i += 64) c0[i] = 0;
   uint32_t *c1 = (uint32_t *)(cu->coef + 4096), *c2 = (uint32_t *)(cu->coef + 5120);
   for (int i = lid(); i < (ny >> 3); i += 64) { c1[i] = 0; c2[i] = 0; }
-  cu->bits = 0; cu->dist = 0; cu->cost = kMaxDouble;
+  cu->bits = 0; cu->dist = 0; cu->cost = kMaxDouble; cu->dssim = 0;
   wsync();
 }
 // initSubCU (:623)
@@ -594,11 +615,12 @@ __device__ __forceinline__ void copy_words(void *dst, const void *src, int bytes
 }
 // copyPartFrom (:859)
 __device__ void cu_copy_part_from(Cu *dst, const Cu *src, int idx, int depth) {
-  const double sc = src->cost;
+  const double sc = src->cost, ss = src->dssim;
   const uint32_t sd = src->dist, sb = src->bits;
   const int sn = src->nparts;
   wsync();
   dst->cost += sc;
+  dst->dssim += ss;
   dst->dist += sd;
   dst->bits += sb;
   copy_words(&dst->p[sn * idx], src->p, (int)sizeof(Part) * sn);
@@ -759,6 +781,7 @@ __device__ __forceinline__ int ep_exgolomb_bins(uint32_t sym, int k) {
   return n + 1 + k;
 }
 __device__ void code_mvd(const Cu *cu, int rel, int list) {
+  if (E.P.mvd_l1_zero && list == 1 && cu->p[rel].inter_dir == 3) return;  // TEncSbac.cpp:781
   const int h = cu->p[rel].mvd[list][0], v = cu->p[rel].mvd[list][1];
   cbin(X_MVD + 0, h != 0);
   cbin(X_MVD + 0, v != 0);
@@ -1436,6 +1459,57 @@ __device__ __forceinline__ double rd_cost_sad(uint32_t bits, uint32_t dist) {
   return floor(__dadd_rn((double)dist, floor(__dadd_rn(__dmul_rn((double)bits, (double)E.P.lambda_motion), 0.5)) / 65536.0));
 }
 __device__ __forceinline__ uint32_t mv_cost_bits(uint32_t bits) { return (uint32_t)(E.P.lambda_motion * bits) >> 16; }
+// The SSIM cost of TEncCu's comparisons (HVX_RD_SSIM, include/hvx_types.h; restated by cu_dssim /
+// cu_cost in oracle/hvx_oracle_cu.c): one window per block, compute_SSIM's float order
+// (stvssim.c:491-566) and its [1, 1.01) clamp
+__device__ __forceinline__ float ssim_block16(const int16_t *o, const int16_t *r, int stride, int wint) {
+  const float C1 = 0.01f * 0.01f * (float)(255 * 255), C2 = 0.03f * 0.03f * (float)(255 * 255);
+  const float wgt = 1.0f / (float)(wint * wint);
+  float mo = 0, me = 0, vo = 0, ve = 0, cov = 0;
+  for (int n = 0; n < wint; n++)
+    for (int m = 0; m < wint; m++) {
+      const int po = o[n * stride + m], pe = r[n * stride + m];
+      mo += wgt * po; me += wgt * pe;
+      vo += wgt * po * po; ve += wgt * pe * pe; cov += wgt * po * pe;
+    }
+  const float varo = fabsf(vo - mo * mo), vare = fabsf(ve - me * me), covo = fabsf(cov - mo * me);
+  float v = (float)((2.0 * mo * me + C1) * (2.0 * covo + C2));
+  v /= (float)(mo * mo + me * me + C1) * (varo + vare + C2);
+  if (v >= 1.0 && v < 1.01) v = 1.0f;
+  return v;
+}
+// D of a CU: its 8x8 luma blocks, then 4x4 Cb, Cr blocks, one block per lane; the terms / 4 summed
+// in that order in double (blocks outside the picture skipped)
+__device__ double cu_dssim(const Cu *cu, Yuv *org, Yuv *reco) {
+  const int n = cu->width >> 3, nb = n * n, total = 3 * nb;
+  const int cx = cu->x, cy = cu->y;
+  for (int k = lid(); k < total; k += 64) {
+    const int c = k / nb, i = k - c * nb, by = i / n, bx = i - by * n;
+    const int sh = c ? 1 : 0, b = c ? 4 : 8;
+    const bool in = (cx >> sh) + bx * b < (E.P.w >> sh) && (cy >> sh) + by * b < (E.P.h >> sh);
+    E.ssim_t[k] = in ? 1.0f - ssim_block16(yaddr(org, c, bx * b, by * b), yaddr(reco, c, bx * b, by * b), ystride(c), b) : -1.0f;
+  }
+  wsync();
+  double d = 0;
+  for (int k = 0; k < total; k++) {
+    const float t = E.ssim_t[k];
+    if (t >= 0.0f) d += 0.25 * (double)t;
+  }
+  wsync();
+  return d;
+}
+// the cost TEncCu compares: calcRdCost(bits, dist), or the SSIM cost (dssim already measured)
+__device__ __forceinline__ double cu_cost(double dssim, uint32_t bits, uint32_t dist) {
+  if (E.P.rd_metric != HVX_RD_SSIM) return rd_cost(bits, dist);
+  return dssim + E.P.lambda_ssim * ((double)bits > 0.5 ? (double)bits : 0.5);
+}
+__device__ __forceinline__ double measure_ssim(Cu *cu, Yuv *org, Yuv *reco) {
+  if (E.P.rd_metric != HVX_RD_SSIM) return 0.0;
+  const double d = cu_dssim(cu, org, reco);
+  cu->dssim = d;
+  wsync();
+  return d;
+}
 __device__ uint32_t sse_wave(const int16_t *a, int sa, const int16_t *b, int sb, int w, int h) {
   HM_PROF(PR_DIST);
   uint32_t s = 0;
@@ -1658,6 +1732,19 @@ __device__ void mc_pu(const Cu *cu, int ps, int pu, Yuv *dst) {
     }
   }
 }
+// motionCompensation(pcCU, m_acYuvPred[list], list, pu): uni prediction of one list; only its
+// luma is read (removeHighFreq's other-list prediction of the bi search)
+__device__ void mc_pu_list_luma(const Cu *cu, int ps, int pu, int list, int16_t *dst64) {
+  HM_PROF(PR_MC);
+  int a, w, h, xp, yp;
+  part_index_size(cu, ps, pu, a, w, h);
+  part_position(cu, ps, pu, xp, yp, w, h);
+  const Part &p = cu->p[a];
+  int mx = p.mv[list][0], my = p.mv[list][1];
+  clip_mv(cu, mx, my);
+  const int pl = E.P.ref_plane[list][p.ref[list]];
+  mc_blk(true, E.P.ref16[pl][0], E.P.ref16_stride[0], xp, yp, mx, my, w, h, false, dst64 + (yp - cu->y) * 64 + xp - cu->x, 64);
+}
 __device__ void mc_cu(const Cu *cu, Yuv *dst) {
   const int ps = cu->p[0].part;
   for (int pu = 0; pu < num_parts_of(ps); pu++) mc_pu(cu, ps, pu, dst);
@@ -1838,7 +1925,6 @@ __device__ void merge_candidates(const Cu *cu, int ps, int pu, MergeList &m) {
 // ============================================================================================
 // AMVP: fillMvpCand (TComDataCU.cpp:2623), xAddMVPCand (:2850), xAddMVPCandOrder (:2936)
 // ============================================================================================
-struct Amvp { int n; int16_t c[3][2]; };
 __device__ int add_mvp(Amvp &in, int list, int ref_idx, const Nb &n) {
   if (!n.valid) return 0;
   const Part &q = n.p[n.idx];
@@ -2147,7 +2233,7 @@ __device__ void enc_res_rd_inter(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Yuv *re
     code_skip_flag(cu, 0);
     code_merge_index(cu, 0);
     const uint32_t bits = written_bits();
-    const double cost = rd_cost(bits, dist);
+    const double cost = cu_cost(measure_ssim(cu, org, reco), bits, dist);
     cu->bits = bits; cu->dist = dist; cu->cost = cost;
     cload(RD(depth, CI_TEMP_BEST), E.cur);
     return;
@@ -2174,12 +2260,12 @@ __device__ void enc_res_rd_inter(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Yuv *re
   cload(RD(depth, CI_TEMP_BEST), E.cur);
   yuv_op(YOP_ADD_CLIP, reco, pred, resi_best, W);
   const uint32_t final_dist = yuv_dist(reco, org, W);
-  const double cost = rd_cost(final_bits, final_dist);
+  const double cost = cu_cost(measure_ssim(cu, org, reco), final_bits, final_dist);
   cu->bits = final_bits; cu->dist = final_dist; cu->cost = cost;
 }
 
 // ============================================================================================
-// predInterSearch (TEncSearch.cpp:2912), P slices
+// predInterSearch (TEncSearch.cpp:2912), P and B slices
 // ============================================================================================
 __device__ uint32_t template_cost(const Cu *cu, int ps, int pu, Yuv *org, int list, int ref_idx, const int16_t *mvc) {
   HM_PROF(PR_TPL);
@@ -2201,15 +2287,20 @@ __device__ uint32_t template_cost(const Cu *cu, int ps, int pu, Yuv *org, int li
   wsync();
   return (uint32_t)rd_cost_sad(1, sad);
 }
+// xEstimateMvPredAMVP (:3413); dist_bip (puiDistBiP) takes the best template cost
 __device__ void est_mvp_amvp(Cu *cu, int ps, int pu, Yuv *org, int list, int ref_idx, Amvp &in, int16_t *pred, int &mvp_idx,
-                             int &mvp_num) {
+                             int &mvp_num, uint32_t &dist_bip) {
   fill_mvp_cand(cu, ps, pu, list, ref_idx, in);
   int best = 0;
-  if (in.n <= 1) { pred[0] = in.c[0][0]; pred[1] = in.c[0][1]; mvp_idx = 0; mvp_num = in.n; return; }
+  if (in.n <= 1) {
+    pred[0] = in.c[0][0]; pred[1] = in.c[0][1]; mvp_idx = 0; mvp_num = in.n;
+    if (E.P.mvd_l1_zero && list == 1) dist_bip = template_cost(cu, ps, pu, org, list, ref_idx, in.c[0]);
+    return;
+  }
   uint32_t best_cost = kMaxU32;
   for (int i = 0; i < in.n; i++) {
     const uint32_t c = template_cost(cu, ps, pu, org, list, ref_idx, in.c[i]);
-    if (best_cost > c) { best_cost = c; best = i; }
+    if (best_cost > c) { best_cost = c; best = i; dist_bip = c; }
   }
   pred[0] = in.c[best][0]; pred[1] = in.c[best][1];
   mvp_idx = best;
@@ -2315,38 +2406,212 @@ __device__ void merge_estimation(Cu *cu, int ps, int pu, Yuv *org, int &inter_di
     }
   }
 }
+// xMotionEstimation with bBi (TEncSearch.cpp:3686-3696, :3710-3712, :3726-3729, :3759): the target
+// is 2 * org - m_acYuvPred[other list] (TComYuv::removeHighFreq, TComYuv.cpp:409; unclipped:
+// ClipForBiPredMEEnabled is off), xPatternSearch over +-BipredSearchRange around the list's current
+// MV (rcMv on entry), the fractional refinement on the same int16 target, the cost weighted by 0.5.
+// One candidate point per lane (raster order, first minimum as in k_me_full).
+__device__ void motion_estimation_bi(Cu *cu, int ps, int pu, Yuv *org, int list, int ref_idx, const int16_t *pred,
+                                     int16_t *mv, uint32_t &bits, uint32_t &cost) {
+  HM_PROF(PR_ME);
+  int a, w, h, xp, yp;
+  part_index_size(cu, ps, pu, a, w, h);
+  part_position(cu, ps, pu, xp, yp, w, h);
+  const int rx = xp - cu->x, ry = yp - cu->y;
+  MeFracSmem<64, 1, int16_t> &sm = E.S->me.sm16;
+  const int16_t *o = yaddr(org, 0, rx, ry), *q = E.S->pred_l[1 - list] + ry * 64 + rx;
+  for (int k = lid(); k < w * h; k += 64) {
+    const int y = k / w, x = k - y * w;
+    sm.org[y * 64 + x] = (int16_t)(2 * o[y * 64 + x] - q[y * 64 + x]);
+  }
+  wsync();
+  hvx_me_job j;
+  memset(&j, 0, sizeof(j));
+  j.pic_w = E.P.w; j.pic_h = E.P.h; j.max_cu = 64;
+  j.cu_x = cu->x; j.cu_y = cu->y;
+  j.pu_x = xp; j.pu_y = yp; j.w = w; j.h = h;
+  j.pred_x = pred[0]; j.pred_y = pred[1];
+  j.center_x = mv[0]; j.center_y = mv[1];
+  j.bits_in = (int32_t)bits;
+  j.search_range = E.P.bipred_range;
+  j.lambda_motion = E.P.lambda_motion;
+  j.flags = HVX_ME_FEN | HVX_ME_HADME | HVX_ME_BI;
+  const int pi = E.P.ref_plane[list][ref_idx];
+  const int stride = E.P.ref8_stride;
+  const uint8_t *ref = E.P.ref8[pi] + yp * stride + xp;
+  const MeRange g = me_search_range(j, j.center_x, j.center_y, j.search_range);
+  // FEN subsamples rows when iRows > 8 (:3810); only the specialised SAD widths honour it
+  const bool spec = (w == 4 || w == 8 || w == 16 || w == 32 || w == 64 || w == 12 || w == 24 || w == 48);
+  const int sub = (h > 8 && spec) ? 1 : 0;
+  const int nx = g.r - g.l + 1, np = nx * (g.b - g.t + 1);
+  uint64_t best = ~0ull;
+  for (int p = lid(); p < np; p += 64) {
+    const int py = p / nx, x = g.l + (p - py * nx), y = g.t + py;
+    const uint8_t *r = ref + y * stride + x;
+    uint32_t sad = 0;
+    for (int row = 0; row < h; row += 1 << sub)
+      for (int c = 0; c < w; c++) sad += (uint32_t)abs((int)sm.org[row * 64 + c] - (int)r[row * stride + c]);
+    const uint32_t c = (sad << sub) + me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, 2, x, y);
+    const uint64_t key = ((uint64_t)c << 32) | (uint32_t)p;
+    best = key < best ? key : best;
+  }
+  best = wave_min_u64(best);
+  const int bp = (int)(uint32_t)best, by = bp / nx;
+  const int ix = g.l + (bp - by * nx), iy = g.t + by;
+  const uint32_t sad_int = (uint32_t)(best >> 32) - me_mv_cost(j.lambda_motion, j.pred_x, j.pred_y, 2, ix, iy);
+  me_frac_refine<64, 1, true, int16_t>(j, ref, stride, ix, iy, sad_int, sm, &E.S->me.r);
+  wsync();
+  const hvx_me_result r = E.S->me.r;
+  wsync();
+  HMC(r.mv_x >= -4 * 80 && r.mv_y >= -4 * 80 && r.mv_x < 4 * (E.P.w + 80) && r.mv_y < 4 * (E.P.h + 80), 10, r.mv_x, r.mv_y);
+  mv[0] = (int16_t)r.mv_x; mv[1] = (int16_t)r.mv_y;
+  bits = r.bits;
+  cost = r.cost;
+}
+// xGetBlkBits (:3509)
+__device__ __forceinline__ void blk_bits(int ps, int is_p, int pu, int last_mode, uint32_t *b) {
+  if (ps == SIZE_2Nx2N || ps == SIZE_NxN) { b[0] = is_p ? 1 : 3; b[1] = 3; b[2] = 5; return; }
+  if (is_p) { b[0] = 3; b[1] = 0; b[2] = 0; return; }
+  const bool hor = ps == SIZE_2NxN || ps == SIZE_2NxnU || ps == SIZE_2NxnD;
+  if (pu == 0) { b[0] = 0; b[1] = (hor || last_mode != 0) ? 0 : 2; b[2] = last_mode == 0 ? 3 : 0; return; }
+  // PU 1: {5,7,7} after uni-L0, {7,5,7} (2NxN) / {5,5,7} (Nx2N) after uni-L1, {6,6,6} after bi
+  if (last_mode == 2) { b[0] = b[1] = b[2] = 6; return; }
+  b[0] = (last_mode == 1 && hor) ? 7 : 5;
+  b[1] = last_mode == 0 ? 7 : 5;
+  b[2] = 7;
+}
+// the reference index bits of predInterSearch (:3021-3028)
+__device__ __forceinline__ uint32_t ref_bits(int r, int n) { return n <= 1 ? 0u : (uint32_t)r + 1 - (r == n - 1 ? 1u : 0u); }
 __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
   const int ps = cu->p[0].part, npart = num_parts_of(ps);
+  const int isb = E.P.slice_type == B_SLICE, ndir = isb ? 2 : 1;
+  InterSearch &Q = E.is;
+  int last_mode = 0;
+  // declared before the PU loop in the reference (:2937-2969): carried across the PUs
+  int best_bip_ref_l1 = 0, best_bip_mvp_l1 = 0;
+  uint32_t bip_dist_temp = kMaxU32;
+  Q.mv[0][0] = Q.mv[0][1] = Q.mv[1][0] = Q.mv[1][1] = 0;
+  Q.ref[0] = Q.ref[1] = 0;
   for (int pu = 0; pu < npart; pu++) {
-    uint32_t cost0 = kMaxU32, bits0 = 0;
-    int16_t mv0[2] = {0, 0};
-    int ref0 = 0;
-    int16_t mvpred[4][2];
-    int mvp_idx[4], mvp_num[4];
+    Q.cost[0] = Q.cost[1] = kMaxU32;
+    Q.bits[0] = Q.bits[1] = Q.bits[2] = 0;
+    uint32_t cost_bi = kMaxU32, best_bip_dist = kMaxU32;
+    for (int r = 0; r < 4; r++) { Q.cost_l0[r] = kMaxU32; Q.bits_l0[r] = 0; }
+    int16_t mv_valid_l1[2] = {0, 0};
+    int ref_valid_l1 = 0;
+    uint32_t bits_valid_l1 = kMaxU32, cost_valid_l1 = kMaxU32;
+    Q.mvbi[0][0] = Q.mvbi[0][1] = Q.mvbi[1][0] = Q.mvbi[1][1] = 0;
+    Q.refbi[0] = Q.refbi[1] = 0;
+    uint32_t mb[3];
+    blk_bits(ps, !isb, pu, last_mode, mb);
     int a, w, h;
     part_index_size(cu, ps, pu, a, w, h);
-    const uint32_t mb_bits0 = ps == SIZE_2Nx2N ? 1 : 3;
     const int test_normal = !(use_mrg && cu->width > 8 && npart == 2);
-    const int nref = E.P.nref[0];
     if (test_normal) {
-      for (int r = 0; r < nref; r++) {
-        uint32_t bt = mb_bits0, ct;
-        if (nref > 1) { bt += (uint32_t)r + 1; if (r == nref - 1) bt--; }
-        Amvp in;
-        int16_t pr[2];
-        int pidx, pnum;
-        est_mvp_amvp(cu, ps, pu, org, 0, r, in, pr, pidx, pnum);
-        pu_set(cu, ps, pu, PU_MVP_IDX, 0, pidx);
-        pu_set(cu, ps, pu, PU_MVP_NUM, 0, pnum);
-        bt += 1;
-        int16_t mvt[2];
-        motion_estimation(cu, ps, pu, 0, r, pr, mvt, bt, ct);
-        check_best_mvp(in, mvt, pr, pidx, bt, ct);
-        mvpred[r][0] = pr[0]; mvpred[r][1] = pr[1];
-        mvp_idx[r] = pidx; mvp_num[r] = pnum;
-        if (ct < cost0) { cost0 = ct; bits0 = bt; mv0[0] = mvt[0]; mv0[1] = mvt[1]; ref0 = r; }
+      // uni-directional prediction (:3014-3093)
+      for (int l = 0; l < ndir; l++) {
+        const int nref = E.P.nref[l];
+        for (int r = 0; r < nref; r++) {
+          uint32_t bt = mb[l] + ref_bits(r, nref), ct;
+          int pidx, pnum;
+          est_mvp_amvp(cu, ps, pu, org, l, r, Q.amvp[l][r], Q.mvpred[l][r], pidx, pnum, bip_dist_temp);
+          pu_set(cu, ps, pu, PU_MVP_IDX, l, pidx);
+          pu_set(cu, ps, pu, PU_MVP_NUM, l, pnum);
+          if (E.P.mvd_l1_zero && l == 1 && bip_dist_temp < best_bip_dist) {
+            best_bip_dist = bip_dist_temp;
+            best_bip_mvp_l1 = pidx;
+            best_bip_ref_l1 = r;
+          }
+          bt += 1;  // m_auiMVPIdxCost[idx][AMVP_MAX_NUM_CANDS]
+          const int m = l == 1 ? E.P.l1_to_l0[r] : -1;
+          if (m >= 0) {
+            // FastMEForGenBLowDelayEnabled (:3042-3055): list 0's search of the same picture, re-costed
+            Q.mvtemp[1][r][0] = Q.mvtemp[0][m][0]; Q.mvtemp[1][r][1] = Q.mvtemp[0][m][1];
+            ct = Q.cost_l0[m] - mv_cost_bits(Q.bits_l0[m]);
+            bt += eg_bits(Q.mvtemp[1][r][0] - Q.mvpred[1][r][0]) + eg_bits(Q.mvtemp[1][r][1] - Q.mvpred[1][r][1]);
+            ct += mv_cost_bits(bt);
+          } else {
+            motion_estimation(cu, ps, pu, l, r, Q.mvpred[l][r], Q.mvtemp[l][r], bt, ct);
+          }
+          check_best_mvp(Q.amvp[l][r], Q.mvtemp[l][r], Q.mvpred[l][r], pidx, bt, ct);
+          Q.mvp_idx[l][r] = pidx; Q.mvp_num[l][r] = pnum;
+          if (l == 0) { Q.cost_l0[r] = ct; Q.bits_l0[r] = bt; }
+          if (ct < Q.cost[l]) {
+            Q.cost[l] = ct; Q.bits[l] = bt;
+            Q.mv[l][0] = Q.mvtemp[l][r][0]; Q.mv[l][1] = Q.mvtemp[l][r][1];
+            Q.ref[l] = r;
+          }
+          if (l == 1 && ct < cost_valid_l1 && m < 0) {
+            cost_valid_l1 = ct; bits_valid_l1 = bt;
+            mv_valid_l1[0] = Q.mvtemp[l][r][0]; mv_valid_l1[1] = Q.mvtemp[l][r][1];
+            ref_valid_l1 = r;
+          }
+        }
+      }
+      // bi-directional prediction (:3096-3251); UseFastEnc: one iteration
+      if (isb && !(cu->width == 8 && (w < 8 || h < 8))) {  // isBipredRestriction (TComDataCU.cpp:2773)
+        for (int l = 0; l < 2; l++) {
+          Q.mvbi[l][0] = Q.mv[l][0]; Q.mvbi[l][1] = Q.mv[l][1];
+          Q.refbi[l] = Q.ref[l];
+          for (int r = 0; r < 4; r++) {
+            Q.mvpredbi[l][r][0] = Q.mvpred[l][r][0]; Q.mvpredbi[l][r][1] = Q.mvpred[l][r][1];
+            Q.mvp_idx_bi[l][r] = Q.mvp_idx[l][r];
+          }
+        }
+        if (E.P.mvd_l1_zero) {
+          const int br = best_bip_ref_l1;
+          pu_set(cu, ps, pu, PU_MVP_IDX, 1, best_bip_mvp_l1);
+          Q.mvp_idx_bi[1][br] = best_bip_mvp_l1;
+          Q.mvpredbi[1][br][0] = Q.amvp[1][br].c[best_bip_mvp_l1][0];
+          Q.mvpredbi[1][br][1] = Q.amvp[1][br].c[best_bip_mvp_l1][1];
+          Q.mvbi[1][0] = Q.mvpredbi[1][br][0]; Q.mvbi[1][1] = Q.mvpredbi[1][br][1];
+          Q.refbi[1] = br;
+          pu_set_mvfield(cu, ps, pu, 1, Q.mvbi[1][0], Q.mvbi[1][1], br);
+          mc_pu_list_luma(cu, ps, pu, 1, E.S->pred_l[1]);
+          Q.motbits[0] = Q.bits[0] - mb[0];
+          Q.motbits[1] = mb[1] + ref_bits(br, E.P.nref[1]) + 1;
+          Q.bits[2] = mb[2] + Q.motbits[0] + Q.motbits[1];
+          Q.mvtemp[1][br][0] = Q.mvbi[1][0]; Q.mvtemp[1][br][1] = Q.mvbi[1][1];
+        } else {
+          Q.motbits[0] = Q.bits[0] - mb[0];
+          Q.motbits[1] = Q.bits[1] - mb[1];
+          Q.bits[2] = mb[2] + Q.motbits[0] + Q.motbits[1];
+        }
+        int l = Q.cost[0] <= Q.cost[1] ? 1 : 0;
+        if (!E.P.mvd_l1_zero) {
+          pu_set_mv(cu, ps, pu, 1 - l, Q.mv[1 - l][0], Q.mv[1 - l][1]);
+          pu_set_ref(cu, ps, pu, 1 - l, Q.ref[1 - l]);
+          mc_pu_list_luma(cu, ps, pu, 1 - l, E.S->pred_l[1 - l]);
+        } else l = 0;
+        int changed = 0;
+        const int nref = E.P.nref[l];
+        for (int r = 0; r < nref; r++) {
+          uint32_t bt = mb[2] + Q.motbits[1 - l] + ref_bits(r, nref) + 1, ct;
+          motion_estimation_bi(cu, ps, pu, org, l, r, Q.mvpredbi[l][r], Q.mvtemp[l][r], bt, ct);
+          int pidx = Q.mvp_idx_bi[l][r];
+          check_best_mvp(Q.amvp[l][r], Q.mvtemp[l][r], Q.mvpredbi[l][r], pidx, bt, ct);
+          Q.mvp_idx_bi[l][r] = pidx;
+          if (ct < cost_bi) {
+            changed = 1;
+            Q.mvbi[l][0] = Q.mvtemp[l][r][0]; Q.mvbi[l][1] = Q.mvtemp[l][r][1];
+            Q.refbi[l] = r;
+            cost_bi = ct;
+            Q.motbits[l] = bt - mb[2] - Q.motbits[1 - l];
+            Q.bits[2] = bt;
+          }
+        }
+        if (!changed && cost_bi <= Q.cost[0] && cost_bi <= Q.cost[1]) {
+          for (int k = 0; k < (E.P.mvd_l1_zero ? 1 : 2); k++) {
+            int pidx = Q.mvp_idx_bi[k][Q.refbi[k]];
+            uint32_t b2 = Q.bits[2];
+            check_best_mvp(Q.amvp[k][Q.refbi[k]], Q.mvbi[k], Q.mvpredbi[k][Q.refbi[k]], pidx, b2, cost_bi);
+            Q.bits[2] = b2;
+            Q.mvp_idx_bi[k][Q.refbi[k]] = pidx;
+          }
+        }
       }
     }
+    // clear the PU's motion (:3257-3265)
     pu_set_mvfield(cu, ps, pu, 0, 0, 0, -1);
     pu_set_mvfield(cu, ps, pu, 1, 0, 0, -1);
     pu_set_mvd(cu, ps, pu, 0, 0, 0);
@@ -2354,14 +2619,39 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
     pu_set(cu, ps, pu, PU_MVP_IDX, 0, -1); pu_set(cu, ps, pu, PU_MVP_NUM, 0, -1);
     pu_set(cu, ps, pu, PU_MVP_IDX, 1, -1); pu_set(cu, ps, pu, PU_MVP_NUM, 1, -1);
     uint32_t me_bits = 0;
+    // list 1 alone only through a picture list 0 does not hold (:3269-3272)
+    Q.mv[1][0] = mv_valid_l1[0]; Q.mv[1][1] = mv_valid_l1[1];
+    Q.ref[1] = ref_valid_l1;
+    Q.bits[1] = bits_valid_l1;
+    Q.cost[1] = cost_valid_l1;
     if (test_normal) {
-      pu_set_mv(cu, ps, pu, 0, mv0[0], mv0[1]);
-      pu_set_ref(cu, ps, pu, 0, ref0);
-      pu_set_mvd(cu, ps, pu, 0, mv0[0] - mvpred[ref0][0], mv0[1] - mvpred[ref0][1]);
-      pu_set(cu, ps, pu, PU_INTER_DIR, 0, 1);
-      pu_set(cu, ps, pu, PU_MVP_IDX, 0, mvp_idx[ref0]);
-      pu_set(cu, ps, pu, PU_MVP_NUM, 0, mvp_num[ref0]);
-      me_bits = bits0;
+      if (cost_bi <= Q.cost[0] && cost_bi <= Q.cost[1]) {
+        last_mode = 2;
+        const int r0 = Q.refbi[0], r1 = Q.refbi[1];
+        pu_set_mv(cu, ps, pu, 0, Q.mvbi[0][0], Q.mvbi[0][1]);
+        pu_set_ref(cu, ps, pu, 0, r0);
+        pu_set_mv(cu, ps, pu, 1, Q.mvbi[1][0], Q.mvbi[1][1]);
+        pu_set_ref(cu, ps, pu, 1, r1);
+        pu_set_mvd(cu, ps, pu, 0, Q.mvbi[0][0] - Q.mvpredbi[0][r0][0], Q.mvbi[0][1] - Q.mvpredbi[0][r0][1]);
+        pu_set_mvd(cu, ps, pu, 1, Q.mvbi[1][0] - Q.mvpredbi[1][r1][0], Q.mvbi[1][1] - Q.mvpredbi[1][r1][1]);
+        pu_set(cu, ps, pu, PU_INTER_DIR, 0, 3);
+        pu_set(cu, ps, pu, PU_MVP_IDX, 0, Q.mvp_idx_bi[0][r0]);
+        pu_set(cu, ps, pu, PU_MVP_NUM, 0, Q.mvp_num[0][r0]);
+        pu_set(cu, ps, pu, PU_MVP_IDX, 1, Q.mvp_idx_bi[1][r1]);
+        pu_set(cu, ps, pu, PU_MVP_NUM, 1, Q.mvp_num[1][r1]);
+        me_bits = Q.bits[2];
+      } else {
+        const int l = Q.cost[0] <= Q.cost[1] ? 0 : 1;
+        last_mode = l;
+        const int r = Q.ref[l];
+        pu_set_mv(cu, ps, pu, l, Q.mv[l][0], Q.mv[l][1]);
+        pu_set_ref(cu, ps, pu, l, r);
+        pu_set_mvd(cu, ps, pu, l, Q.mv[l][0] - Q.mvpred[l][r][0], Q.mv[l][1] - Q.mvpred[l][r][1]);
+        pu_set(cu, ps, pu, PU_INTER_DIR, 0, l + 1);
+        pu_set(cu, ps, pu, PU_MVP_IDX, l, Q.mvp_idx[l][r]);
+        pu_set(cu, ps, pu, PU_MVP_NUM, l, Q.mvp_num[l][r]);
+        me_bits = Q.bits[l];
+      }
     }
     if (ps != SIZE_2Nx2N) {
       uint32_t me_cost = kMaxU32;
@@ -3150,7 +3440,8 @@ __device__ void check_rd_inter(int depth, int ps, int use_mrg) {
   pred_inter_search(tmp, YB(Y_ORIG, depth), YB(Y_PRED_TEMP, depth), use_mrg);
   enc_res_rd_inter(tmp, YB(Y_ORIG, depth), YB(Y_PRED_TEMP, depth), YB(Y_RESI_TEMP, depth), YB(Y_RESI_BEST, depth),
                    YB(Y_RECO_TEMP, depth), 0);
-  const double c = rd_cost(tmp->bits, tmp->dist);
+  const double c = cu_cost(tmp->dssim, tmp->bits, tmp->dist);
+  wsync();
   tmp->cost = c;
   check_best_mode(depth);
 }
@@ -3178,7 +3469,7 @@ __device__ void check_rd_intra(int depth, int ps) {
   encode_coeff(tmp, 0);
   cload(RD(depth, CI_TEMP_BEST), E.cur);
   const uint32_t b = written_bits();
-  const double c = rd_cost(b, tmp->dist);
+  const double c = cu_cost(measure_ssim(tmp, YB(Y_ORIG, depth), YB(Y_RECO_TEMP, depth)), b, tmp->dist);
   tmp->bits = b;
   tmp->cost = c;
   check_best_mode(depth);
@@ -3254,7 +3545,7 @@ __device__ void compress_cu(int parent_ps) {
     reset_bits();
     code_split_flag(best, 0, depth);
     const uint32_t b = best->bits + written_bits();
-    const double c = rd_cost(b, best->dist);
+    const double c = cu_cost(best->dssim, b, best->dist);
     wsync();
     best->bits = b;
     best->cost = c;
@@ -3289,7 +3580,7 @@ __device__ void compress_cu(int parent_ps) {
       code_split_flag(tmp, 0, depth);
       b += written_bits();
     }
-    const double c = rd_cost(b, tmp->dist);
+    const double c = cu_cost(tmp->dssim, b, tmp->dist);
     wsync();
     tmp->bits = b;
     tmp->cost = c;

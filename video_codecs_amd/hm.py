@@ -42,10 +42,29 @@ class HmPicture(ctypes.Structure):
                 ("nref", I32 * 2), ("ref_poc", (I32 * 4) * 2), ("ref_plane", (I32 * 4) * 2), ("chroma_qp", I32 * 2),
                 ("max_merge", I32), ("tmvp", I32), ("check_ldc", I32), ("col_from_l0", I32), ("col_valid", I32),
                 ("col_poc", I32), ("col_ref_poc", (I32 * 4) * 2), ("search_range", I32), ("amp", I32),
-                ("lambda_motion", U32), ("pad_", I32), ("lambda_", F64), ("sqrt_lambda", F64), ("chroma_weight", F64 * 2),
+                ("lambda_motion", U32), ("bipred_range", I32), ("lambda_", F64), ("sqrt_lambda", F64), ("chroma_weight", F64 * 2),
                 ("tq_lambda", F64 * 3), ("col_field", P_), ("org", P_ * 3), ("rec", P_ * 3), ("org_stride", I32 * 2),
                 ("rec_stride", I32 * 2), ("ctus", P_), ("ref8", P_ * 8), ("ref16", (P_ * 3) * 8), ("ref8_stride", I32),
-                ("ref16_stride", I32 * 2), ("pad2_", I32), ("entropy_bits", P_)]
+                ("ref16_stride", I32 * 2), ("mvd_l1_zero", I32), ("l1_to_l0", I32 * 4), ("entropy_bits", P_),
+                ("rd_metric", I32), ("pad3_", I32), ("lambda_ssim", F64)]
+
+
+def derive_lists(slice_type, nref, ref_poc):
+    """mvd_l1_zero and l1_to_l0 of a slice from its reference POC lists, as HM derives them
+    (TEncGOP.cpp:1311-1336 GPB check -> setMvdL1ZeroFlag; TComSlice::setList1IdxToList0Idx,
+    TComSlice.cpp:302)."""
+    ref_poc = np.asarray(ref_poc)
+    isb = int(slice_type) == 0
+    n0, n1 = int(nref[0]), int(nref[1])
+    zero = isb and n0 == n1 and all(int(ref_poc[1][i]) == int(ref_poc[0][i]) for i in range(n1))
+    m = [-1] * 4
+    if isb:
+        for i in range(n1):
+            for k in range(n0):
+                if int(ref_poc[0][k]) == int(ref_poc[1][i]):
+                    m[i] = k
+                    break
+    return int(zero), m
 
 
 def pack_parts(rows):
@@ -171,6 +190,13 @@ class DevicePicture:
                         a[i] = v[i].item()
             else:
                 setattr(s, "lambda_" if k == "lambda" else k, v)
+        if "mvd_l1_zero" not in params and "nref" in params:
+            z, m = derive_lists(params["slice_type"], params["nref"], params["ref_poc"])
+            s.mvd_l1_zero = z
+            for i in range(4):
+                s.l1_to_l0[i] = m[i]
+        if "bipred_range" not in params:
+            s.bipred_range = 4  # BipredSearchRange of encoder_randomaccess_main.cfg:36
         self.org_t = org.org
         for c in range(3):
             s.org[c] = self.org_t[c].data_ptr()
