@@ -1231,21 +1231,12 @@ static double rd_cost_sad(const hm_enc *e, uint32_t bits, uint32_t dist) {
  * picture are skipped; the terms are summed in double, luma blocks in raster order, then Cb, Cr.
  * Only TEncCu's mode and split comparisons use it (xCheckBestMode :1444 and the split cost); the
  * searches, merge estimation, RQT and RDOQ below keep HM's SSE / SATD costs. */
+/* one block, one window: compute_SSIM through the pinned hvxo_ssim (tests/golden/ssim.bin) */
 static float ssim_block16(const int16_t *o, const int16_t *r, int stride, int wint) {
-  const float C1 = 0.01f * 0.01f * (float)(255 * 255), C2 = 0.03f * 0.03f * (float)(255 * 255);
-  const float wgt = 1.0f / (float)(wint * wint);
-  float mo = 0, me = 0, vo = 0, ve = 0, cov = 0;
-  for (int n = 0; n < wint; n++)
-    for (int m = 0; m < wint; m++) {
-      const int po = o[n * stride + m], pe = r[n * stride + m];
-      mo += wgt * po; me += wgt * pe;
-      vo += wgt * po * po; ve += wgt * pe * pe; cov += wgt * po * pe;
-    }
-  const float varo = fabsf(vo - mo * mo), vare = fabsf(ve - me * me), covo = fabsf(cov - mo * me);
-  float v = (float)((2.0 * mo * me + C1) * (2.0 * covo + C2));
-  v /= (float)(mo * mo + me * me + C1) * (varo + vare + C2);
-  if (v >= 1.0 && v < 1.01) v = 1.0f;
-  return v;
+  uint8_t o8[64], r8[64];
+  for (int y = 0; y < wint; y++)
+    for (int x = 0; x < wint; x++) { o8[y * wint + x] = (uint8_t)o[y * stride + x]; r8[y * wint + x] = (uint8_t)r[y * stride + x]; }
+  return hvxo_ssim(o8, wint, r8, wint, wint, wint, wint, wint);
 }
 static double cu_dssim(const hm_enc *e, const hm_cu *cu, yuv_t *org, yuv_t *reco) {
   const hvxo_hm_pic *P = e->pic;

@@ -70,7 +70,7 @@ def hm_recon(g, first, w, h):
     return planes
 
 
-def device_picture(g, pic, chained, entropy_bits):
+def device_picture(g, pic, chained, entropy_bits, rd_metric=0, eta=1.0):
     pi, pf = g["pic_i32"][pic], g["pic_f64"][pic]
     w, h = int(pi[P_W]), int(pi[P_H])
     psz = w * h * 3 // 2
@@ -84,10 +84,13 @@ def device_picture(g, pic, chained, entropy_bits):
         col = g["col_field"][k * n * 16:(k + 1) * n * 16]
     rec = None if chained else hm_recon(g, first, w, h)
     ctus = None if chained else hm_ctus(g, first, n)
-    return hm.DevicePicture(org, refs, pic_params(pi, pf), entropy_bits, rec=rec, ctus=ctus, col_field=col)
+    params = pic_params(pi, pf)
+    if rd_metric:
+        params["rd_metric"], params["lambda_ssim"] = rd_metric, hm.lambda_ssim(int(pi[P_QP]), eta)
+    return hm.DevicePicture(org, refs, params, entropy_bits, rec=rec, ctus=ctus, col_field=col)
 
 
-def run_capture(name, mode, pics=None, stage=0):
+def run_capture(name, mode, pics=None, stage=0, rd_metric=0, eta=1.0):
     """Decide the captured pictures on the device.  mode 0: every CTU as its own job from the
     reference's entry state and neighbourhood; mode 1: one chained job per picture.  Returns
     (g, list of (pic, first, n, out_slot0), (ctus, rec, coders))."""
@@ -99,7 +102,7 @@ def run_capture(name, mode, pics=None, stage=0):
     for pi_idx, pic in enumerate(pics):
         pi = g["pic_i32"][pic]
         first, n = int(pi[P_FIRST_CTU]), int(pi[P_NCTU])
-        dps.append(device_picture(g, pic, mode == 1, eb))
+        dps.append(device_picture(g, pic, mode == 1, eb, rd_metric, eta))
         plan.append((pic, first, n, slot))
         wc = (int(pi[P_W]) + 63) // 64
         rows = name in ROW_SLICES
@@ -166,6 +169,28 @@ def run_capture_resumed(name, split):
     torch.cuda.synchronize()
     return g, plan, (out_ctu.cpu().numpy().view(hm.HM_CTU), out_rec.cpu().numpy().reshape(slot, 6144),
                      out_cod.cpu().numpy().view(hm.HM_CODER))
+
+
+def compare_outputs(plan, out, ref_outs):
+    """Mismatches (pic, ctu, what) of the engine's outputs against per-picture restatement outputs
+    (oracle.hm_ctu.replay dicts, one per plan entry): every field, bit for bit (costs included)."""
+    ctus, rec, _ = out
+    bad = []
+    for (pic, first, n, slot), ro in zip(plan, ref_outs):
+        parts = hm.unpack_parts(ctus["p"][slot:slot + n])
+        for a in range(n):
+            c = ctus[slot + a]
+            if not np.array_equal(ro["parts"][a], parts[a]):
+                bad.append((pic, a, "parts"))
+            elif not np.array_equal(ro["coef"][a].astype(np.int16), c["coef"]):
+                bad.append((pic, a, "coef"))
+            elif not np.array_equal(ro["recon"][a], rec[slot + a]):
+                bad.append((pic, a, "recon"))
+            elif (int(ro["bits_dist"][a][0]), int(ro["bits_dist"][a][1])) != (int(c["bits"]), int(c["dist"])):
+                bad.append((pic, a, "bits/dist"))
+            elif float(ro["cost"][a]) != float(c["cost"]):
+                bad.append((pic, a, "cost %r vs %r" % (float(ro["cost"][a]), float(c["cost"]))))
+    return bad
 
 
 def name_rows(g):

@@ -325,3 +325,29 @@ def test_hm_ctu_resume_gpu(torch):
     g, plan, out = hm_cases.run_capture_resumed("ctu_ldp_slices.bin", 3)
     bad = hm_cases.compare(g, plan, out)
     assert not bad, bad[:5]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,eta", [("ctu_ra_q22.bin", 1.0), ("ctu_ra_q27.bin", 0.7), ("ctu_ra_q32.bin", 1.0),
+                                      ("ctu_ra_q37.bin", 1.3)])
+def test_hm_ctu_ssim_rdo_gpu(torch, name, eta):
+    """BASELINE config 4's cost inside the real decision: hvx_hm_compress with HVX_RD_SSIM (TEncCu's
+    mode / split comparisons on J = D_ssim + lambda_2(QP) * eta^0.85 * max(0.5, R), stvssim.c:567,
+    :1805, rdopt.c:1631) on the RA B pictures at QP 22 / 27 / 32 / 37, chained per picture, against
+    the restatement with the same cost (oracle/hvx_oracle_cu.c cu_dssim / cu_cost): every decision,
+    coefficient, reconstruction sample, bit count, distortion and cost bit-exact (the SSIM floats
+    and the double cost included, tighter than north_star's 1e-6); and the cost changes decisions
+    against HM's SSE cost."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import hm_ctu
+    from video_codecs_amd import hm
+    g, plan, out = hm_cases.run_capture(name, 1, rd_metric=1, eta=eta)
+
+    def ref(p):
+        qp = int(g["pic_i32"][p[0]][hm_cases.P_QP])
+        return hm_ctu.replay(g, p[0], 1, rd_metric=1, lambda_ssim=hm.lambda_ssim(qp, eta))
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        refs = list(ex.map(ref, plan))
+    bad = hm_cases.compare_outputs(plan, out, refs)
+    assert not bad, bad[:5]
+    assert hm_cases.compare(g, plan, out), "the SSIM cost decided exactly as HM's SSE cost"

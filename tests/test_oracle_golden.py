@@ -236,3 +236,14 @@ def test_sao_golden():
             np.testing.assert_array_equal(oracle.sao_apply(pre[c], c, params), post[c])
         types |= set(np.unique(params["comp"]["type"]).tolist())
     assert types == {-1, 0, 1, 2, 3, 4}
+
+
+def test_lambda_ssim_matches_stvssim():
+    """The engine's host-side SSIM lambda (video_codecs_amd.hm.lambda_ssim) equals the pinned
+    lambda_2 x adjust_lambda of stvssim.c (oracle hvxo_lambda_2 / hvxo_adjust_lambda, pinned by
+    ssim.bin) for every QP and a range of attention weights."""
+    import oracle
+    from video_codecs_amd import hm
+    for qp in range(52):
+        for eta in (0.5, 0.7, 1.0, 1.3, 2.0):
+            assert hm.lambda_ssim(qp, eta) == oracle.adjust_lambda(oracle.lambda_2(qp), eta), (qp, eta)

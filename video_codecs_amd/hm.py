@@ -67,6 +67,17 @@ def derive_lists(slice_type, nref, ref_poc):
     return int(zero), m
 
 
+def lambda_ssim(qp, eta=1.0):
+    """The stvssim encoder's mode-decision lambda for the SSIM cost (hvx_hm_picture.lambda_ssim):
+    lambda_2(QP) = -a1 * b2 * exp(b1 * (QP - 15)) (stvssim.c:1782-1806, the active line :1805)
+    times the attention weight eta^0.85 (adjust_lambda, stvssim.c:1707).  eta is the caller's
+    (the reference derives it from an OpenCV saliency model that is not vendored); 1 = neutral."""
+    import math
+    a1, b2, b1 = 5.883060266548170e-03, -2.229472265847692e-02, 9.279543980380707e-02
+    lam = -a1 * b2 * math.exp(b1 * (qp - 15))
+    return lam * math.pow(eta, 0.85)
+
+
 def pack_parts(rows):
     """[..., 256, 29] int16 rows (PART_FIELDS order, oracle/cu_capture.cpp) -> HM_PART records."""
     rows = np.asarray(rows)
