@@ -342,45 +342,66 @@ def hm_cpu_port(work, threads, min_seconds=0.0):
             "gpu_parity_ctus": n, "gpu_parity_mismatches": mism, "first_mismatches": first}
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+REF_W, REF_H, REF_FRAMES, REF_POCS = 512, 256, 7, (5, 6)
+
+
 def hm_cpu_reference(procs, tmpdir):
-    """HM-16.5rc1's own TAppEncoder (oracle/_ref, built from /root/reference by oracle/Makefile)
-    on the host cores: `procs` concurrent single-threaded encodes of 416x240 random 4:2:0 YUV
-    (the bench's synthetic recipe) with oracle/hm_ref_bench.cfg -- the bench picture's slice
-    parameters (LDP P, QP 34, QPFactor 0.4624, RDOQ, AMP, FEN, TZ SR 64, row slices).  P-picture
-    CTUs/s = procs x 3 x 28 CTUs / (mean wall time of the 4-frame encode - that of the
-    1-frame, I-only encode)."""
+    """HM-16.5rc1's own encoder (oracle/_ref/TAppEncoder_cutime: the unchanged TAppEncoder with
+    every TEncCu::compressCtu timed, oracle/cu_timer.cpp) on the host cores, on the GPU's workload:
+    `procs` concurrent single-threaded encodes of 512x256 random 4:2:0 YUV (the bench's synthetic
+    recipe; 8x4 whole CTUs) with oracle/hm_ref_bench.cfg and one row per slice (SliceArgument 8):
+    P pictures predicted from the 4 previous frames at the bench picture's slice parameters (QP 34,
+    QPFactor 0.4624, GOP depth > 0: the same lambda), TZ SR 64, RDOQ, AMP, FEN.  The timed pictures
+    are POC 5 and 6 (4 active references each; POCs 0-4 are the pre-roll); their compressCtu time
+    is summed per encode.  value = procs / mean seconds per CTU."""
     import subprocess
     from video_codecs_amd import synth
-    exe = os.path.join(ROOT, "oracle", "_ref", "TAppEncoder")
+    exe = os.path.join(ROOT, "oracle", "_ref", "TAppEncoder_cutime")
     cfg = os.path.join(ROOT, "oracle", "hm_ref_bench.cfg")
     if not os.path.exists(exe):
         return None
-    yuv = os.path.join(tmpdir, "hvx_hm_ref.yuv")
-    with open(yuv, "wb") as f:
-        for i in range(4):
-            f.write(synth.random_frame(416, 240, 5000 + i).tobytes())
-
-    def batch(frames):
-        t0 = time.perf_counter()
-        ps = [subprocess.Popen([exe, "-c", cfg, "-i", yuv, "-wdt", "416", "-hgt", "240", "-fr", "30", "-f", str(frames),
-                                "-b", os.path.join(tmpdir, f"hvx_hm_ref{k}.bin"), "-o", "/dev/null"],
-                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL) for k in range(procs)]
-        ends = []
-        for p in ps:
-            p.wait()
-            ends.append(time.perf_counter() - t0)
-            if p.returncode != 0:
-                raise RuntimeError("TAppEncoder failed")
-        return float(np.mean(ends))
-
-    t1, t4 = batch(1), batch(4)
-    p_ctus = 3 * 28
-    per_ctu = (t4 - t1) / p_ctus
-    return {"value": round(procs / per_ctu, 3), "unit": "CTUs/s", "cores": procs, "kind": "reference",
-            "sample": f"{procs} concurrent TAppEncoder (HM-16.5rc1, oracle/_ref) encodes of 416x240 random YUV, "
-                      f"oracle/hm_ref_bench.cfg: 3 P pictures x 28 CTUs each (QP 34, 1-3 refs); "
-                      f"{t4:.1f} s (4 frames) - {t1:.1f} s (I only) per encode",
-            "s_per_ctu_per_core": round(per_ctu, 4)}
+    per_ctu = []
+    t0 = time.perf_counter()
+    ps = []
+    for k in range(procs):
+        yuv = os.path.join(tmpdir, f"hvx_hm_ref{k}.yuv")
+        with open(yuv, "wb") as f:
+            for i in range(REF_FRAMES):
+                f.write(synth.random_frame(REF_W, REF_H, 5000 + 100 * k + i).tobytes())
+        ps.append(subprocess.Popen([exe, "-c", cfg, "-i", yuv, "-wdt", str(REF_W), "-hgt", str(REF_H), "-fr", "30",
+                                    "-f", str(REF_FRAMES), "--SliceArgument=%d" % (REF_W // 64),
+                                    "-b", os.path.join(tmpdir, f"hvx_hm_ref{k}.bin"), "-o", "/dev/null"],
+                                   stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True))
+    for p in ps:
+        _, err = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError("TAppEncoder_cutime failed: " + err[-500:])
+        secs = ctus = 0
+        for line in err.splitlines():
+            f = line.split()
+            if len(f) == 13 and f[0] == "cu_time" and int(f[2]) in REF_POCS:
+                assert int(f[4]) == 1 and int(f[6]) == 34 and int(f[8]) == 4, line  # P, QP 34, 4 refs
+                ctus += int(f[10])
+                secs += float(f[12])
+        per_ctu.append(secs / ctus)
+    wall = time.perf_counter() - t0
+    s = float(np.mean(per_ctu))
+    return {"value": round(procs / s, 3), "unit": "CTUs/s", "cores": procs, "kind": "reference",
+            "sample": f"{procs} concurrent HM-16.5rc1 TAppEncoder encodes (oracle/_ref/TAppEncoder_cutime, compressCtu "
+                      f"timed) of {REF_W}x{REF_H} random YUV, oracle/hm_ref_bench.cfg with one row per slice: POC "
+                      f"{REF_POCS[0]}-{REF_POCS[-1]} ({len(REF_POCS) * (REF_W // 64) * (REF_H // 64)} whole CTUs per "
+                      f"encode, P, QP 34, 4 refs) after a 5-frame pre-roll; {wall:.0f} s wall",
+            "s_per_ctu_per_core": round(s, 4), "cpu_model": cpu_model(), "cores_present": os.cpu_count()}
 
 
 def build_provenance():

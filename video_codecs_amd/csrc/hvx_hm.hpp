@@ -214,6 +214,7 @@ struct Enc {
   uint8_t scan_cg[16];
   uint32_t avail[4];
   InterSearch is;
+  hvx_tu_desc td;        // the current TU's descriptor (tu_desc)
   float ssim_t[192];     // HVX_RD_SSIM: the (1 - SSIM) terms of a CU's blocks (cu_dssim)
   int dbg[4];  // HM_CHECKS: first violated check (code, a, b) of the job
   int stage, stop;  // HM_CHECKS: stop the CTU at debugging stage `stage` (0: never)
@@ -929,36 +930,37 @@ __device__ int coef_scan_idx(const Cu *cu, int rel, int w, int comp) {
   if (abs(dir - 10) <= 4) return 2;
   return 0;
 }
-__device__ void tu_desc(const Cu *cu, const Tu &t, int comp, hvx_tu_desc &d) {
+// the descriptor of the TU a transform / count / inverse works on (wave-uniform, one at a time):
+// E.td in LDS -- a per-lane copy lived in scratch (7 KB of call-frame traffic per TU call)
+__device__ void tu_desc(const Cu *cu, const Tu &t, int comp) {
+  hvx_tu_desc &d = E.td;
   const int rel = tu_abs_rel_c(t, comp);
-  memset(&d, 0, sizeof(d));
+  const int scan = coef_scan_idx(cu, rel, t.w[comp], comp);
+  const int intra = cu->p[rel].pred == MODE_INTRA;
+  const int ts = cu->p[rel].ts[comp], tr = cu->p[rel].tr_idx;
+  const int qp = comp ? E.P.chroma_qp[comp - 1] : E.slice_qp;
+  const double lam = E.P.tq_lambda[comp];
   d.comp = comp;
   d.width = t.w[comp];
   d.height = t.h[comp];
   d.log2_size = ilog2(t.h[comp]);
-  d.scan_type = coef_scan_idx(cu, rel, t.w[comp], comp);
-  const int intra = cu->p[rel].pred == MODE_INTRA;
+  d.scan_type = scan;
   d.use_dst = comp == 0 && intra && t.w[0] == 4;
-  d.transform_skip = cu->p[rel].ts[comp];
+  d.transform_skip = ts;
   d.is_intra = intra;
-  d.tr_idx = cu->p[rel].tr_idx;
+  d.tr_idx = tr;
   d.ctx_qt_cbf = comp ? tu_depth_rel(t) : (tu_depth_rel(t) == 0 ? 1 : 0);
   d.slice_type = E.P.slice_type;
-  const int qp = comp ? E.P.chroma_qp[comp - 1] : E.slice_qp;
   d.qp_per = qp / 6;
   d.qp_rem = qp % 6;
   d.sign_hiding = 1;
   d.use_rdoq = d.use_rdoq_ts = 1;
-  d.pps_tskip = 1;
+  d.selective_rdoq = d.adaptive_qp_select = d.transquant_bypass = 0;
+  d.golomb_rice_stat = d.persistent_rice = d.extended_precision = d.ts_context = 0;
   d.max_log2_tr_range = 15;
   d.bit_depth = 8;
-  d.lambda = E.P.tq_lambda[comp];
-#ifdef HM_SCALAR
-  // every field is wave-uniform (read from the CU object in memory): scalar registers
-  int32_t *w = reinterpret_cast<int32_t *>(&d);
-#pragma unroll
-  for (int k = 0; k < (int)(sizeof(d) / 4); k++) w[k] = __builtin_amdgcn_readfirstlane(w[k]);
-#endif
+  d.pps_tskip = 1;
+  d.lambda = lam;
 }
 // The coefficient contexts of one coder held in registers for the duration of a TU's
 // codeCoeffNxN: row r (model kCtxLo + r) in lane r & 63 of VGPR r >> 6, the entropy-bit table
@@ -1177,8 +1179,8 @@ __device__ __forceinline__ uint32_t memo_mask(int ch, int k) {
 __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_t *coef) {
   HM_PROF(PR_COEF);
   HM_T0(t_desc);
-  hvx_tu_desc d;
-  tu_desc(cu, t, comp, d);
+  tu_desc(cu, t, comp);
+  const hvx_tu_desc &d = E.td;
   HM_TADD(PR_COEF_DESC, t_desc);
   // the memo (4x4 / 8x8 TUs): one load round for the keys, one per candidate entry
   const int ch = comp ? 1 : 0, l = lid();
@@ -1590,8 +1592,8 @@ __device__ void tu_inv_l(const hvx_tu_desc &d, const int16_t *coef, int16_t *res
 }
 // transformNxN; sets the TU's CBF (TComTrQuant.cpp:1543)
 __device__ int32_t transform_tu(Cu *cu, const Tu &t, int comp, const int16_t *resi, int rs, int16_t *coef) {
-  hvx_tu_desc d;
-  tu_desc(cu, t, comp, d);
+  tu_desc(cu, t, comp);
+  const hvx_tu_desc &d = E.td;
   HMC(d.log2_size >= 2 && d.log2_size <= 5 && t.off[comp] + t.w[comp] * t.h[comp] <= (comp ? 1024 : 4096) &&
           tu_abs_rel(t) + tu_nparts(t, comp) <= cu->nparts, 10, d.log2_size * 100 + comp, t.off[comp]);
   int32_t abs_sum;
@@ -1605,8 +1607,8 @@ __device__ int32_t transform_tu(Cu *cu, const Tu &t, int comp, const int16_t *re
   return abs_sum;
 }
 __device__ void inv_transform_tu(const Cu *cu, const Tu &t, int comp, const int16_t *coef, int16_t *resi, int rs) {
-  hvx_tu_desc d;
-  tu_desc(cu, t, comp, d);
+  tu_desc(cu, t, comp);
+  const hvx_tu_desc &d = E.td;
   switch (d.log2_size) {
     case 2: tu_inv_l<0>(d, coef, resi, rs); break;
     case 3: tu_inv_l<1>(d, coef, resi, rs); break;
