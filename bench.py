@@ -47,7 +47,10 @@ def parse():
     p.add_argument("--cpu-ref-procs", type=int, default=0, help="HM TAppEncoder processes for the reference "
                                                                   "baseline (0: the host's CPU share)")
     p.add_argument("--no-cpu-ref", action="store_true", help="skip the reference HM timing")
-    p.add_argument("--no-reduced", action="store_true", help="skip the reduced-step side measurement")
+    p.add_argument("--reduced", action="store_true", help="also run the reduced picture step of rounds 1-2 "
+                                                          "(hvx_ctu_encode_yuv, side measurement)")
+    p.add_argument("--no-ra", action="store_true", help="skip the config-4 side figure (RA B pictures, SSIM cost)")
+    p.add_argument("--no-slice0", action="store_true", help="skip the SliceMode 0 side figure")
     p.add_argument("--width", type=int, default=3840)
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--nref", type=int, default=4)
@@ -279,6 +282,131 @@ class HmWorkload:
         return pi, pf, org, refs, self.col_field(p)
 
 
+def _chain_jobs(specs, entry):
+    """HM_JOB records: specs = [(pic, first_ctu, n_ctus, slice_start, slice_end, resume)]."""
+    from video_codecs_amd import _abi, hm
+    j = np.zeros(len(specs), hm.HM_JOB)
+    for k, (pic, first, n, s0, s1, resume) in enumerate(specs):
+        j[k]["pic"], j[k]["first_ctu"], j[k]["n_ctus"], j[k]["chained"], j[k]["out"] = pic, first, n, 1, k * n
+        j[k]["slice_start"], j[k]["slice_end"] = s0, s1
+        j[k]["flags"] = _abi.HM_RESUME if resume else 0
+        j[k]["entry"]["st"] = entry
+    return j
+
+
+def _time_chains(eng, job_steps, n_out, warmup):
+    """Launch warmup + timed steps of chain jobs on a private stream; returns (seconds per timed
+    step from HIP events, wall seconds per timed step)."""
+    import torch
+    from video_codecs_amd import hm
+    stream = torch.cuda.Stream()
+    out_ctu = torch.zeros(n_out * hm.HM_CTU.itemsize, dtype=torch.uint8, device="cuda")
+    out_rec = torch.zeros(n_out * 6144, dtype=torch.uint8, device="cuda")
+    dev_jobs = [torch.from_numpy(j.view(np.uint8).reshape(-1).copy()).cuda() for j in job_steps]
+    n_jobs = len(job_steps[0])
+    torch.cuda.synchronize()
+    ev = []
+    t0 = None
+    with torch.cuda.stream(stream):
+        for k, jt in enumerate(dev_jobs):
+            if k == warmup:
+                stream.synchronize()
+                t0 = time.perf_counter()
+            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            e[0].record()
+            eng.launch(jt, n_jobs, out_ctu, out_rec)
+            e[1].record()
+            ev.append(e)
+    stream.synchronize()
+    wall = (time.perf_counter() - t0) / (len(dev_jobs) - warmup)
+    ms = sum(a.elapsed_time(b) for a, b in ev[warmup:]) / (len(dev_jobs) - warmup)
+    return ms * 1e-3, wall
+
+
+def ra_ssim_measure(W, H, pics=60, distinct=12, qps=(22, 27, 32, 37), warmup=1, steps=1):
+    """BASELINE config 4 (side figure): 2160p random-access B pictures with the stvssim SSIM cost in
+    the decision (hvx_hm_compress, HVX_RD_SSIM, eta 1) at QP 22 / 27 / 32 / 37.  The picture is GOP
+    position 2 of encoder_randomaccess_main.cfg (POC 4, TId 1: QP offset 2, QPFactor 0.3536,
+    L0 = {POC 0, 8}, L1 = {8, 0}, TMVP from L1[0], BipredSearchRange 4), `pics` pictures in flight
+    (over `distinct` synthetic frame triples), every CTU row a slice; one step = every chain one
+    CTU.  The B-slice decision is pinned to HM by the RA captures (tests/golden/ctu_ra_q*.bin) and
+    its SSIM cost to the restatement (test_hm_ctu_ssim_rdo_gpu)."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    from video_codecs_amd import _abi, hm, synth
+    wc, hc = (W + 63) // 64, (H + 63) // 64
+    eb = _abi.load_entropy_bits()
+    with ThreadPoolExecutor(8) as ex:
+        host = list(ex.map(lambda i: synth.random_frame(W, H, 7000 + i), range(3 * distinct)))
+    frames = [hm.DeviceFrame(yuv_split(f, W, H)) for f in host]
+    del host
+    col = torch.from_numpy(synthetic_col_field(wc * hc, 77)).cuda()
+    res = {}
+    for base_qp in qps:
+        qp = base_qp + 2
+        prm = hm.slice_params(0, qp, 0.3536)
+        entry = _abi.load_ctx_init_states()[0, qp]
+        prm.update(poc=4, nref=[2, 2], ref_poc=np.array([[0, 8, 0, 0], [8, 0, 0, 0]]),
+                   ref_plane=np.array([[0, 1, 0, 0], [1, 0, 0, 0]]), max_merge=5, tmvp=1, check_ldc=0, col_from_l0=0,
+                   col_valid=1, col_poc=8, col_ref_poc=np.array([[0, -8, -16, -24], [0] * 4]), search_range=64, amp=1,
+                   rd_metric=_abi.RD_SSIM, lambda_ssim=hm.lambda_ssim(qp))
+        pictures = []
+        for p in range(pics):
+            k = p % distinct
+            pictures.append(hm.DevicePicture(frames[3 * k + 2], [frames[3 * k], frames[3 * k + 1]], prm, eb, col_field=col))
+        eng = hm.Engine(pictures)
+        job_steps = [_chain_jobs([(p, r * wc + pos, 1, r * wc, r * wc + wc - 1, pos > 0) for p in range(pics)
+                                  for r in range(hc)], entry) for pos in range(warmup + steps)]
+        sec, wall = _time_chains(eng, job_steps, pics * hc, warmup)
+        res[str(base_qp)] = {"slice_qp": qp, "ctus_per_s": round(pics * hc / sec, 2), "ms_per_step": round(sec * 1e3, 1),
+                             "wall_ms_per_step": round(wall * 1e3, 1), "lambda_ssim": prm["lambda_ssim"]}
+        del eng, pictures
+        torch.cuda.empty_cache()
+    return {"workload": "2160p RA B pictures (GOP position 2: POC 4, L0 {0,8} / L1 {8,0}, bi-pred + bBi refinement), "
+                        "SSIM cost in TEncCu's decisions, eta 1, %d pictures x %d row-slice chains" % (pics, hc),
+            "per_qp": res}
+
+
+def slice_mode0_measure(W, H, chains=2040, distinct=16, nref=4, base_qp=32, warmup=1, steps=1):
+    """Side figure: the headline's P pictures coded with HM's default SliceMode 0 (one slice per
+    picture, encoder_lowdelay_P_main.cfg:63) -- `chains` independent single-slice 2160p pictures in
+    flight, one chain each (its own CTU array and reconstruction; the synthetic frames are shared by
+    `distinct` picture contents), every chain deciding its picture's CTUs in raster order from CTU 0.
+    Shows whether the headline rate depends on the row slices: it depends on the number of
+    independent chains, not on how a picture is sliced."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    from video_codecs_amd import _abi, hm, synth
+    wc, hc = (W + 63) // 64, (H + 63) // 64
+    qp = base_qp + HM_QP_OFFSET
+    eb = _abi.load_entropy_bits()
+    with ThreadPoolExecutor(8) as ex:
+        host = list(ex.map(lambda i: synth.random_frame(W, H, 9000 + i), range(distinct + nref)))
+    frames = [hm.DeviceFrame(yuv_split(f, W, H)) for f in host]
+    del host
+    col = torch.from_numpy(synthetic_col_field(wc * hc, 99)).cuda()
+    prm = hm.slice_params(1, qp, HM_QP_FACTOR)
+    poc = nref + 1
+    prm.update(poc=poc, nref=[nref, 0], ref_poc=np.array([[poc - 1 - k for k in range(4)], [0] * 4]),
+               ref_plane=np.array([list(range(nref)) + [0] * (4 - nref), [0] * 4]), max_merge=5, tmvp=1, check_ldc=1,
+               col_from_l0=1, col_valid=1, col_poc=poc - 1, col_ref_poc=np.array([[poc - 2 - k for k in range(4)], [0] * 4]),
+               search_range=64, amp=1)
+    entry = _abi.load_ctx_init_states()[1, qp]
+    pictures = []
+    for c in range(chains):
+        k = c % distinct
+        pictures.append(hm.DevicePicture(frames[nref + k], [frames[nref + k - 1 - r] for r in range(nref)], prm, eb,
+                                         col_field=col))
+    eng = hm.Engine(pictures)
+    n = wc * hc
+    job_steps = [_chain_jobs([(c, pos, 1, 0, n - 1, pos > 0) for c in range(chains)], entry) for pos in range(warmup + steps)]
+    sec, wall = _time_chains(eng, job_steps, chains, warmup)
+    del eng, pictures
+    torch.cuda.empty_cache()
+    return {"workload": "%d single-slice (SliceMode 0) 2160p P pictures, one chain each, QP %d, %d refs" % (chains, qp, nref),
+            "ctus_per_s": round(chains / sec, 2), "ms_per_step": round(sec * 1e3, 1), "wall_ms_per_step": round(wall * 1e3, 1)}
+
+
 def hm_cpu_port(work, threads, min_seconds=0.0):
     """The oracle's restatement (oracle/hvx_oracle_cu.c hvxo_hm_chains) on picture 0's slice
     chains -- the same CTUs the GPU decided in its warmup + timed steps, on `threads` host threads
@@ -467,7 +595,7 @@ def main():
     if gathered is not None:
         dpb_ok = bool(torch.equal(gathered[0], own))
     reduced = None
-    if not args.no_reduced:
+    if args.reduced:
         reduced = reduced_step(args, rank, world, with_sides=(world == 1))
     if rank == 0:
         units = work.n_jobs * args.ctus
@@ -536,6 +664,12 @@ def main():
                 out["cpu_port"] = port
                 if out["cpu_baseline"] is None:
                     out["cpu_baseline"] = port
+            del work, dpb
+            torch.cuda.empty_cache()
+            if not args.no_ra:
+                out["config4_ra_ssim"] = ra_ssim_measure(W, H)
+            if not args.no_slice0:
+                out["slice_mode0"] = slice_mode0_measure(W, H)
         if reduced is not None:
             out["reduced_step"] = reduced
         print(json.dumps(out), flush=True)

@@ -181,3 +181,43 @@ def test_ctu_ra_capture_covers_b_modes():
             shared += int(bool(set(l0) & set(l1)) and l0 != l1)
             disjoint += int(any(x not in l0 for x in l1))
     assert dirs == {1, 2, 3} and mvd1 > 0 and gpb and shared and disjoint, (dirs, mvd1, gpb, shared, disjoint)
+
+
+def test_slice_params_ra_vs_hm():
+    """hm.slice_params for the random-access B pictures: every RA capture's lambdas, chroma QPs /
+    weights and TrQuant lambdas bit for bit (encoder_randomaccess_main.cfg QPFactors: 0.442 at
+    POC 8 (GOP depth 0), 0.3536 at POC 4 / 2 / 6, 0.68 at odd POCs; depth > 0 below POC 8)."""
+    from tests import hm_cases as hc
+    from video_codecs_amd import hm
+    fac = {8: 0.442, 4: 0.3536, 2: 0.3536, 6: 0.3536, 1: 0.68, 3: 0.68, 5: 0.68, 7: 0.68}
+    for name in RA_CAPTURES:
+        g = _load(name)
+        for pic in range(g["pic_i32"].shape[0]):
+            pi, pf = g["pic_i32"][pic], g["pic_f64"][pic]
+            st, qp, poc = int(pi[3]), int(pi[4]), int(pi[2])
+            assert st == 0, (name, pic, st)
+            mine = hm.slice_params(st, qp, fac[poc % 8 if poc % 8 else 8], gop_depth=0 if poc % 8 == 0 else 1)
+            ref = hc.pic_params(pi, pf)
+            for k in ("lambda", "sqrt_lambda", "lambda_motion"):
+                assert mine[k] == ref[k], (name, pic, k, mine[k], ref[k])
+            for k in ("chroma_qp", "chroma_weight", "tq_lambda"):
+                assert list(mine[k]) == list(ref[k]), (name, pic, k)
+
+
+def test_ctx_init_states_ra_vs_hm():
+    """The RA captures' slice-start states are ctx_init_states.bin rows too: the B slice's own
+    table, or the P table where HM's encoder set cabac_init_flag (TEncSlice::getEncCABACTableIdx,
+    TEncSbac::resetEntropy swaps the B / P initialisation; the capture's table index 2 = no swap)."""
+    import numpy as np
+    from video_codecs_amd import _abi
+    init = _abi.load_ctx_init_states()
+    swapped = 0
+    for name in RA_CAPTURES:
+        g = _load(name)
+        for pic in range(g["pic_i32"].shape[0]):
+            pi = g["pic_i32"][pic]
+            first, st, qp, tab = int(pi[41]), int(pi[3]), int(pi[4]), int(pi[44])
+            eff = st if tab == 2 else tab
+            swapped += eff != st
+            np.testing.assert_array_equal(g["ctu_states"][first], init[eff, qp], err_msg=(name, pic))
+    assert swapped > 0

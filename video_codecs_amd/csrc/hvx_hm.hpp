@@ -182,6 +182,17 @@ union Leaf {
   } cs;
 };
 
+// a TComTU / TComTURecurse node (4:2:0 rectangles relative to the CU).  The nodes live on a stack
+// in LDS (Enc.tstack, TuSlot): wave-uniform, and a per-lane copy lived in scratch (call-frame
+// traffic on every field read through a reference)
+struct Tu {
+  int cu_depth, cu_zidx;
+  int split, section, last_of_level;
+  int rel, step, log2;
+  int trd[3], x0[3], y0[3], w[3], h[3], ow[3], all[3], off[3];
+};
+constexpr int kTuStack = 10;
+
 // AMVP candidates of one (list, reference) (AMVPInfo)
 struct Amvp { int n; int16_t c[3][2]; };
 // predInterSearch's per-PU records (TEncSearch.cpp:2937-2995: cMvTemp, cMvPred(Bi), aaiMvpIdx(Bi),
@@ -215,6 +226,8 @@ struct Enc {
   uint32_t avail[4];
   InterSearch is;
   hvx_tu_desc td;        // the current TU's descriptor (tu_desc)
+  Tu tstack[kTuStack];   // the live TU nodes (TuSlot), innermost last
+  int tsp;
   float ssim_t[192];     // HVX_RD_SSIM: the (1 - SSIM) terms of a CU's blocks (cu_dssim)
   int dbg[4];  // HM_CHECKS: first violated check (code, a, b) of the job
   int stage, stop;  // HM_CHECKS: stop the CTU at debugging stage `stage` (0: never)
@@ -244,6 +257,13 @@ __device__ __forceinline__ Cu *TEMP(int d) { return &E.S->cu[E.temp[d]]; }
 // ordering (no s_barrier, no wait for outstanding stores; checked in the ISA)
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 __device__ __forceinline__ int lid() { return (int)threadIdx.x; }
+// a TU node on the LDS stack for the scope of the object (declared like a local: TU_LOCAL(ch))
+struct TuSlot {
+  Tu &t;
+  __device__ __forceinline__ TuSlot() : t(E.tstack[E.tsp]) { E.tsp = E.tsp + 1; }
+  __device__ __forceinline__ ~TuSlot() { E.tsp = E.tsp - 1; }
+};
+#define TU_LOCAL(name) TuSlot name##_slot_; Tu &name = name##_slot_.t
 // HM_PROFILE builds accumulate the clock ticks (s_memtime) and calls of the leaf categories
 enum { PR_ME, PR_MC, PR_TPL, PR_TUF, PR_TUI, PR_COEF, PR_EST, PR_IFP, PR_IPRED, PR_DIST, PR_CTU, PR_ENC, PR_N };
 // sub-phases (HM_PROFILE): 12..15 TUF by size; 16 COEF descriptor, 17 COEF staging, 18 COEF walk,
@@ -826,12 +846,6 @@ __device__ void encode_pred_info(const Cu *cu, int rel) {
 // ============================================================================================
 // Transform-unit recursion: TComTU / TComTURecurse, 4:2:0 (rectangles relative to the CU)
 // ============================================================================================
-struct Tu {
-  int cu_depth, cu_zidx;
-  int split, section, last_of_level;
-  int rel, step, log2;
-  int trd[3], x0[3], y0[3], w[3], h[3], ow[3], all[3], off[3];
-};
 __device__ __forceinline__ void tu_root(Tu &t, const Cu *cu, int init_tr_depth) {
   const int depth = cu->depth, zidx = cu->zidx, width = cu->width;
   t.cu_depth = depth;
@@ -1349,7 +1363,7 @@ __device__ void encode_transform(const Cu *cu, const Tu &t) {
       if (first || cbf_at(&cu->p[rel], c, trd - 1)) code_qt_cbf(cu, t, c, !subdiv);
   if (subdiv) {
     if constexpr (LV < 3) {
-      Tu ch;
+      TU_LOCAL(ch);
       tu_child(ch, t, 1);
       do encode_transform<LV + 1>(cu, ch); while (tu_next(ch, t));
     } else HMC(false, 21, LV, 0);
@@ -1368,7 +1382,7 @@ __device__ void encode_coeff(const Cu *cu, int rel) {
     if (!(cu->p[rel].merge && cu->p[rel].part == SIZE_2Nx2N)) cbin(X_ROOT_CBF, cu_qt_root_cbf(cu, rel));
     if (!cu_qt_root_cbf(cu, rel)) return;
   }
-  Tu t;
+  TU_LOCAL(t);
   tu_root(t, cu, 0);
   encode_transform<0>(cu, t);
 }
@@ -2020,7 +2034,7 @@ __device__ void encode_inter_residual_qt(const Cu *cu, int comp, const Tu &t) {
   } else {
     if (comp == 3 || cbf_at(&cu->p[rel], comp, cur_tr)) {
       if constexpr (LV < 3) {
-        Tu ch;
+        TU_LOCAL(ch);
         tu_child(ch, t, 0);
         do encode_inter_residual_qt<LV + 1>(cu, comp, ch); while (tu_next(ch, t));
       } else HMC(false, 22, LV, 0);
@@ -2139,7 +2153,7 @@ __device__ void estimate_inter_residual_qt(Cu *cu, Yuv *resi, double *rd, uint32
       int best_cbf[3] = {0, 0, 0};
       for (int c = 0; c < 3; c++)
         if (tu_proc(t, c)) best_cbf[c] = cbf_at(&cu->p[rel], c, trmode);
-      Tu ch;
+      TU_LOCAL(ch);
       tu_child(ch, t, 0);
       const int qparts = ch.step;
       do estimate_inter_residual_qt<LV + 1>(cu, resi, &sub_cost, &sub_bits, &sub_dist, check_full ? nullptr : zero_dist, ch);
@@ -2190,7 +2204,7 @@ __device__ void set_inter_residual_qt_data(Cu *cu, Yuv *resi, int spatial, const
     }
   } else {
     if constexpr (LV < 3) {
-      Tu ch;
+      TU_LOCAL(ch);
       tu_child(ch, t, 0);
       do set_inter_residual_qt_data<LV + 1>(cu, resi, spatial, ch); while (tu_next(ch, t));
     } else HMC(false, 24, LV, 0);
@@ -2241,7 +2255,7 @@ __device__ void enc_res_rd_inter(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Yuv *re
     return;
   }
   yuv_op(YOP_SUB, resi, org, pred, W);
-  Tu t0;
+  TU_LOCAL(t0);
   tu_root(t0, cu, 0);
   double nz_cost = 0;
   uint32_t nz_bits = 0, nz_dist = 0, z_dist = 0;
@@ -2994,7 +3008,7 @@ __device__ void enc_subdiv_cbf_qt(const Cu *cu, const Tu &t, int luma, int chrom
       if (t.all[c] && (trd == 0 || cbf_at(&cu->p[rel], c, trd - 1))) code_qt_cbf(cu, t, c, !subdiv);
   if (subdiv) {
     if constexpr (LV < 3) {
-      Tu ch;
+      TU_LOCAL(ch);
       tu_child(ch, t, 0);
       do enc_subdiv_cbf_qt<LV + 1>(cu, ch, luma, chroma); while (tu_next(ch, t));
     } else HMC(false, 25, LV, 0);
@@ -3006,7 +3020,7 @@ __device__ void enc_coeff_qt(const Cu *cu, const Tu &t, int comp) {
   const int rel = tu_abs_rel(t), trd = tu_depth_rel(t);
   if (cu->p[rel].tr_idx > trd) {
     if constexpr (LV < 3) {
-      Tu ch;
+      TU_LOCAL(ch);
       tu_child(ch, t, 0);
       do enc_coeff_qt<LV + 1>(cu, ch, comp); while (tu_next(ch, t));
     } else HMC(false, 26, LV, 0);
@@ -3091,7 +3105,7 @@ __device__ void recur_intra_luma_qt(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, uint
       double split_cost = 0.0;
       uint32_t split_dist = 0;
       int split_cbf = 0;
-      Tu ch;
+      TU_LOCAL(ch);
       tu_child(ch, t, 0);
       do {
         recur_intra_luma_qt<LV + 1>(cu, org, pred, resi, &split_dist, check_first, &split_cost, ch);
@@ -3135,7 +3149,7 @@ __device__ void set_intra_result_luma(Cu *cu, Yuv *reco, const Tu &t) {
     }
   } else {
     if constexpr (LV < 3) {
-      Tu ch;
+      TU_LOCAL(ch);
       tu_child(ch, t, 0);
       do set_intra_result_luma<LV + 1>(cu, reco, ch); while (tu_next(ch, t));
     } else HMC(false, 28, LV, 0);
@@ -3158,7 +3172,8 @@ __device__ void est_intra_pred_luma_qt(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Y
   uint32_t overall_dist = 0;
   for (int i = lid(); i < cu->nparts; i += 64) cu->p[i].qp = (int8_t)E.slice_qp;
   wsync();
-  Tu tcu, tpu;
+  TU_LOCAL(tcu);
+  TU_LOCAL(tpu);
   tu_root(tcu, cu, 0);
   if (init_trd) tu_child(tpu, tcu, 0);
   else tpu = tcu;
@@ -3307,7 +3322,7 @@ __device__ void recur_intra_chroma_qt(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, ui
   } else {
     if constexpr (LV < 3) {
       int scb = 0, scr = 0;
-      Tu ch;
+      TU_LOCAL(ch);
       tu_child(ch, t, 0);
       const int trd_child = tu_depth_rel(ch);
       do {
@@ -3334,7 +3349,7 @@ __device__ void set_intra_result_chroma(Cu *cu, Yuv *reco, const Tu &t) {
     }
   } else {
     if constexpr (LV < 3) {
-      Tu ch;
+      TU_LOCAL(ch);
       tu_child(ch, t, 0);
       do set_intra_result_chroma<LV + 1>(cu, reco, ch); while (tu_next(ch, t));
     } else HMC(false, 30, LV, 0);
@@ -3343,7 +3358,7 @@ __device__ void set_intra_result_chroma(Cu *cu, Yuv *reco, const Tu &t) {
 __device__ void est_intra_pred_chroma_qt(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Yuv *reco) {
   State *S = E.S;
   const int depth = cu->depth;
-  Tu t;
+  TU_LOCAL(t);
   tu_root(t, cu, 0);
   const int np = t.step;
   int best_mode = 0;
@@ -3640,7 +3655,7 @@ __device__ void encode_cu(int rel, int last_ctu_in_slice) {
       copy_words(view->coef + 4096, ctu->coef + 4096 + (off >> 2), sz * sz >> 1);
       copy_words(view->coef + 5120, ctu->coef + 5120 + (off >> 2), sz * sz >> 1);
       wsync();
-      Tu t;
+      TU_LOCAL(t);
       tu_root(t, view, 0);
       encode_transform<0>(view, t);
     }
@@ -3756,6 +3771,7 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
   hm_e.slice_start = job.slice_start;
   hm_e.slice_end = job.slice_end;
   hm_e.stop = 0;
+  hm_e.tsp = 0;
 #ifdef HM_PROFILE
   hm_e.prof[l >> 5][l & 31] = 0;
 #endif

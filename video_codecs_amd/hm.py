@@ -216,22 +216,34 @@ class DevicePicture:
         recs = []
         for c in range(3):
             sh = 1 if c else 0
+            if rec is None:  # zeroed on the device: no host staging (many pictures in flight)
+                t = torch.zeros((rh >> sh, rw >> sh), dtype=torch.uint8, device=device)
+                self.keep.append(t)
+                recs.append(t)
+                continue
             buf = np.zeros((rh >> sh, rw >> sh), np.uint8)
-            if rec is not None:
-                r = np.asarray(rec[c], np.uint8)
-                buf[:r.shape[0], :r.shape[1]] = r
+            r = np.asarray(rec[c], np.uint8)
+            buf[:r.shape[0], :r.shape[1]] = r
             recs.append(dev(buf))
         self.rec_t = recs
         for c in range(3):
             s.rec[c] = recs[c].data_ptr()
         s.rec_stride[0], s.rec_stride[1] = rw, rw // 2
         n = self.wc * self.hc
-        ct = np.zeros(n, HM_CTU) if ctus is None else np.ascontiguousarray(ctus)
-        assert ct.shape[0] == n
-        self.ctus_t = dev(ct.view(np.uint8).reshape(-1))
+        if ctus is None:
+            self.ctus_t = torch.zeros(n * HM_CTU.itemsize, dtype=torch.uint8, device=device)
+            self.keep.append(self.ctus_t)
+        else:
+            ct = np.ascontiguousarray(ctus)
+            assert ct.shape[0] == n
+            self.ctus_t = dev(ct.view(np.uint8).reshape(-1))
         s.ctus = self.ctus_t.data_ptr()
         if col_field is not None:
-            s.col_field = dev(np.asarray(col_field, np.int16)).data_ptr()
+            if hasattr(col_field, "data_ptr"):  # a device tensor shared by several pictures
+                self.keep.append(col_field)
+                s.col_field = col_field.data_ptr()
+            else:
+                s.col_field = dev(np.asarray(col_field, np.int16)).data_ptr()
         assert len(refs) <= 8
         for i, ref in enumerate(refs):
             if not isinstance(ref, DeviceFrame):
