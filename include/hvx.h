@@ -388,16 +388,35 @@ int hvx_plane_extend(hvx_ctx *ctx, uint8_t *d_plane, int width, int height);
  * Tool set of encoder_lowdelay_P_main.cfg (hvx_types.h hvx_hm_picture): CTU 64, depth 4, TU
  * 4..32 with QuadtreeTUMaxDepthInter/Intra 3, RDOQ + RDOQTS, sign hiding, transform skip with
  * TransformSkipFast, FEN, FDM, AMP, TZ search with HadamardME, TMVP, 5 merge candidates, no
- * ECU/ESD/CFM, no PCM, no delta QP, no lossless, no weighted prediction, P and I slices.
+ * ECU/ESD/CFM, no PCM, no delta QP, no lossless, no weighted prediction; I, P and B slices (B:
+ * encoder_randomaccess_main.cfg's bi-prediction with BipredSearchRange, FastMEForGenBLowDelay,
+ * MvdL1Zero); the TEncCu comparisons on HM's SSE cost or the stvssim SSIM cost (rd_metric).
  * One wave per job (hvx_hm_job): the chain's CTUs are decided in raster order with the contexts
  * carried; d_state = n_jobs * hvx_hm_state_size() bytes of device scratch.  Outputs per CTU
  * slot: d_out_ctu (the CTU's final TComDataCU data and RD totals), d_out_rec (6144 bytes: its
  * pre-loop-filter reconstruction, Y 64x64 | Cb 32x32 | Cr 32x32, 0 outside the picture),
  * d_out_coder (optional: the RD coder after encodeCtu).
+ * Preconditions of every job, checked on the device before it runs (a job violating one is
+ * skipped -- nothing of it is written -- and its status word holds -HVX_HM_BAD_*; read with
+ * hvx_hm_job_status): 0 <= pic < n_pics; the picture's w, h positive multiples of 8 with
+ * w_ctus / h_ctus = ceil(w / 64) / ceil(h / 64); slice_type 0..2 with nref[0] 1..4 (P, B),
+ * nref[1] 0..4 (B only), I without references; every used ref_plane in 0..7 with its planes set;
+ * org / rec / ctus / entropy_bits (and col_field when col_valid) set; 0 <= slice_start <=
+ * first_ctu, n_ctus >= 1, first_ctu + n_ctus - 1 <= slice_end < w_ctus * h_ctus; 0 <= out and,
+ * when n_out > 0 (the slots of the output arrays), out + n_ctus <= n_out.
  * ------------------------------------------------------------------------------------- */
+#define HVX_HM_BAD_PIC 1
+#define HVX_HM_BAD_GEOMETRY 2
+#define HVX_HM_BAD_REFS 3
+#define HVX_HM_BAD_PLANES 4
+#define HVX_HM_BAD_CTUS 5
+#define HVX_HM_BAD_OUT 6
 int hvx_hm_state_size(size_t *bytes);
-int hvx_hm_compress(hvx_ctx *ctx, const hvx_hm_picture *d_pics, const hvx_hm_job *d_jobs, int n_jobs, void *d_state,
-                    hvx_hm_ctu *d_out_ctu, uint8_t *d_out_rec, hvx_hm_coder *d_out_coder);
+int hvx_hm_compress(hvx_ctx *ctx, const hvx_hm_picture *d_pics, int n_pics, const hvx_hm_job *d_jobs, int n_jobs,
+                    int n_out, void *d_state, hvx_hm_ctu *d_out_ctu, uint8_t *d_out_rec, hvx_hm_coder *d_out_coder);
+/* the status word of each of the last launch's jobs (0: ran; -HVX_HM_BAD_*: refused); synchronises
+ * the context's stream */
+int hvx_hm_job_status(hvx_ctx *ctx, const void *d_state, int n_jobs, int32_t *h_status);
 
 #ifdef __cplusplus
 }

@@ -410,7 +410,7 @@ extern "C" void CAT(__wrap_, CU_SYM)(TEncCu *self, TComDataCU *ctu) {
       j.int2n[(l * 4 + i) * 2 + 1] = (int16_t)self->m_pcPredSearch->m_integerMv2Nx2N[l][i].getVer();
     }
   upload(g.job.p, &j, sizeof(j));
-  check(hvx_hm_compress(c, (const hvx_hm_picture *)g.pic.p, (const hvx_hm_job *)g.job.p, 1, g.state.p,
+  check(hvx_hm_compress(c, (const hvx_hm_picture *)g.pic.p, 1, (const hvx_hm_job *)g.job.p, 1, 1, g.state.p,
                         (hvx_hm_ctu *)g.out_ctu.p, (uint8_t *)g.out_rec.p, nullptr),
         "hvx_hm_compress");
   static hvx_hm_ctu o;

@@ -351,3 +351,40 @@ def test_hm_ctu_ssim_rdo_gpu(torch, name, eta):
     bad = hm_cases.compare_outputs(plan, out, refs)
     assert not bad, bad[:5]
     assert hm_cases.compare(g, plan, out), "the SSIM cost decided exactly as HM's SSE cost"
+
+
+@pytest.mark.gpu
+def test_hm_compress_refuses_bad_jobs(torch):
+    """hvx_hm_compress's device-side preconditions (include/hvx.h): jobs with a picture index, CTU
+    range, slice range or output slot out of range are skipped with their HVX_HM_BAD_* status --
+    nothing of theirs is written -- while a valid job of the same launch runs bit-exactly."""
+    import numpy as np
+    from tests import golden_cases as gc
+    from video_codecs_amd import _abi, hm
+    g = gc.load("ctu_ldp_rand.bin")
+    pic = 1
+    pi = g["pic_i32"][pic]
+    first = int(pi[hm_cases.P_FIRST_CTU])
+    eb = _abi.load_entropy_bits()
+    eng = hm.Engine([hm_cases.device_picture(g, pic, False, eb)])
+    n = 28
+
+    def job(**kw):
+        j = np.zeros(1, hm.HM_JOB)
+        j["pic"], j["first_ctu"], j["n_ctus"], j["chained"], j["out"] = 0, 5, 1, 0, 0
+        j["slice_start"], j["slice_end"] = 0, n - 1
+        j["entry"]["st"] = g["ctu_states"][first + 5]
+        j["entry"]["frac"] = np.uint64(int(g["ctu_frac"][first + 5]))
+        j["int2n"] = g["ctu_int2n"][first + 5]
+        for k, v in kw.items():
+            j[k] = v
+        return j
+    jobs = np.concatenate([job(out=0), job(pic=1, out=1), job(first_ctu=n, out=2), job(n_ctus=0, out=3),
+                           job(slice_start=6, out=4), job(slice_end=n, out=5), job(out=6), job(first_ctu=-1, out=0)])
+    out_ctu, out_rec, _ = eng.compress(jobs, 6)  # 6 output slots: job 6 (out=6) is out of range
+    st = eng.job_status(len(jobs))
+    assert list(st) == [0, -1, -5, -5, -5, -5, -6, -5], list(st)
+    # the valid job's CTU equals the reference's; the refused jobs' slots stay untouched (zero)
+    parts = hm.unpack_parts(out_ctu["p"][0:1])
+    assert np.array_equal(parts[0], g["ctu_parts"][first + 5])
+    assert not out_rec[1:6].any() and not out_ctu["coef"][1:6].any()

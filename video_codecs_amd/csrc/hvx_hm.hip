@@ -29,9 +29,9 @@ int hvx_hm_state_size(size_t *bytes) {
   return HVX_OK;
 }
 
-int hvx_hm_compress(hvx_ctx *ctx, const hvx_hm_picture *d_pics, const hvx_hm_job *d_jobs, int n_jobs, void *d_state,
-                    hvx_hm_ctu *d_out_ctu, uint8_t *d_out_rec, hvx_hm_coder *d_out_coder) {
-  if (!ctx || !d_pics || !d_jobs || n_jobs < 0 || !d_state || !d_out_ctu || !d_out_rec)
+int hvx_hm_compress(hvx_ctx *ctx, const hvx_hm_picture *d_pics, int n_pics, const hvx_hm_job *d_jobs, int n_jobs,
+                    int n_out, void *d_state, hvx_hm_ctu *d_out_ctu, uint8_t *d_out_rec, hvx_hm_coder *d_out_coder) {
+  if (!ctx || !d_pics || n_pics < 1 || !d_jobs || n_jobs < 0 || n_out < 0 || !d_state || !d_out_ctu || !d_out_rec)
     return fail(HVX_E_INVALID, "hvx_hm_compress: bad args");
   if (n_jobs == 0) return HVX_OK;
   size_t sb = 0;
@@ -41,9 +41,22 @@ int hvx_hm_compress(hvx_ctx *ctx, const hvx_hm_picture *d_pics, const hvx_hm_job
 #else
   const int grid = n_jobs;
 #endif
-  hipLaunchKernelGGL(k_hm_compress, dim3(grid), dim3(64), 0, ctx->stream, d_pics, d_jobs, n_jobs, (char *)d_state, sb,
-                     d_out_ctu, d_out_rec, d_out_coder);
+  hipLaunchKernelGGL(k_hm_compress, dim3(grid), dim3(64), 0, ctx->stream, d_pics, n_pics, d_jobs, n_jobs, n_out,
+                     (char *)d_state, sb, d_out_ctu, d_out_rec, d_out_coder);
   return launched("k_hm_compress");
+}
+
+int hvx_hm_job_status(hvx_ctx *ctx, const void *d_state, int n_jobs, int32_t *h_status) {
+  if (!ctx || !d_state || n_jobs < 0 || (n_jobs && !h_status)) return fail(HVX_E_INVALID, "hvx_hm_job_status: bad args");
+  if (n_jobs == 0) return HVX_OK;
+  size_t sb = 0;
+  hvx_hm_state_size(&sb);
+  // State.dbg[0] of every job's state (strided): 0 = ran, -HVX_HM_BAD_* = refused
+  if (hipMemcpy2DAsync(h_status, sizeof(int32_t), d_state, sb, sizeof(int32_t), (size_t)n_jobs, hipMemcpyDeviceToHost,
+                       ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess)
+    return fail(HVX_E_HIP, "hvx_hm_job_status: copy failed");
+  return HVX_OK;
 }
 
 }  // extern "C"

@@ -82,10 +82,10 @@ struct Cu {
 };
 __device__ __forceinline__ int coff(int c) { return c == 0 ? 0 : c == 1 ? 4096 : 5120; }
 
-// a TComYuv of a 64x64 CU: Y stride 64 | Cb | Cr stride 32
+// a TComYuv of a CU up to 64x64, packed for the CU being decided (width W = Enc.yw): Y W x W
+// (stride W) | Cb | Cr (W/2 x W/2, stride W/2).  An 8x8 CU's buffer is 192 contiguous bytes (two
+// cache lines) instead of a 64-stride 64x64 layout's sixteen.
 struct Yuv { int16_t s[6144]; };
-__device__ __forceinline__ int ystride(int c) { return c ? 32 : 64; }
-__device__ __forceinline__ int16_t *yaddr(Yuv *b, int c, int x, int y) { return b->s + coff(c) + y * ystride(c) + x; }
 
 // the leaf scratch of motion search and motion compensation (in the chain state: global memory)
 struct MeScratch {
@@ -228,6 +228,7 @@ struct Enc {
   hvx_tu_desc td;        // the current TU's descriptor (tu_desc)
   Tu tstack[kTuStack];   // the live TU nodes (TuSlot), innermost last
   int tsp;
+  int yw;                // the width of the CU whose TComYuv buffers are in use (compress_cu<D>: 64 >> D)
   float ssim_t[192];     // HVX_RD_SSIM: the (1 - SSIM) terms of a CU's blocks (cu_dssim)
   int dbg[4];  // HM_CHECKS: first violated check (code, a, b) of the job
   int stage, stop;  // HM_CHECKS: stop the CTU at debugging stage `stage` (0: never)
@@ -257,6 +258,13 @@ __device__ __forceinline__ Cu *TEMP(int d) { return &E.S->cu[E.temp[d]]; }
 // ordering (no s_barrier, no wait for outstanding stores; checked in the ISA)
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 __device__ __forceinline__ int lid() { return (int)threadIdx.x; }
+// the TComYuv layout of the CU being decided (E.yw)
+__device__ __forceinline__ int ystride(int c) { return c ? E.yw >> 1 : E.yw; }
+__device__ __forceinline__ int ycoff(int c, int w) { return c == 0 ? 0 : c == 1 ? w * w : w * w + (w * w >> 2); }
+__device__ __forceinline__ int16_t *yaddr_w(Yuv *b, int c, int x, int y, int w) {
+  return b->s + ycoff(c, w) + y * (c ? w >> 1 : w) + x;
+}
+__device__ __forceinline__ int16_t *yaddr(Yuv *b, int c, int x, int y) { return yaddr_w(b, c, x, y, E.yw); }
 // a TU node on the LDS stack for the scope of the object (declared like a local: TU_LOCAL(ch))
 struct TuSlot {
   Tu &t;
@@ -1441,7 +1449,7 @@ __device__ void yuv_child_to_parent(Yuv *dst, Yuv *src, int idx, int child_w) {
     const int s = c ? 1 : 0, n = child_w >> s, ox = (idx & 1) * n, oy = (idx >> 1) * n, sh = ilog2(n);
     for (int i = lid(); i < n * n; i += 64) {
       const int y = i >> sh, x = i & (n - 1);
-      *yaddr(dst, c, ox + x, oy + y) = *yaddr(src, c, x, y);
+      *yaddr_w(dst, c, ox + x, oy + y, 2 * child_w) = *yaddr_w(src, c, x, y, child_w);
     }
   }
   wsync();
@@ -2297,7 +2305,7 @@ __device__ uint32_t template_cost(const Cu *cu, int ps, int pu, Yuv *org, int li
   uint32_t s = 0;
   for (int k = lid(); k < w * h; k += 64) {
     const int r = k / w, c = k - r * w;
-    s += (uint32_t)abs((int)pr[k] - (int)o[r * 64 + c]);
+    s += (uint32_t)abs((int)pr[k] - (int)o[r * ystride(0) + c]);
   }
   const uint32_t sad = wave_sum_u32(s);
   wsync();
@@ -2409,7 +2417,8 @@ __device__ void merge_estimation(Cu *cu, int ps, int pu, Yuv *org, int &inter_di
     pu_set_mvfield(cu, ps, pu, 0, m.f[2 * i].mv[0], m.f[2 * i].mv[1], m.f[2 * i].ref);
     pu_set_mvfield(cu, ps, pu, 1, m.f[2 * i + 1].mv[0], m.f[2 * i + 1].mv[1], m.f[2 * i + 1].ref);
     mc_pu(cu, ps, pu, &E.S->tmp_yuv_pred);
-    uint32_t c = wave_satd(yaddr(org, 0, xp - cu->x, yp - cu->y), 64, yaddr(&E.S->tmp_yuv_pred, 0, xp - cu->x, yp - cu->y), 64, w, h);
+    uint32_t c = wave_satd(yaddr(org, 0, xp - cu->x, yp - cu->y), ystride(0), yaddr(&E.S->tmp_yuv_pred, 0, xp - cu->x, yp - cu->y),
+                           ystride(0), w, h);
     uint32_t b = (uint32_t)i + 1;
     if (i == E.P.max_merge - 1) b--;
     c += mv_cost_bits(b);
@@ -2438,7 +2447,7 @@ __device__ void motion_estimation_bi(Cu *cu, int ps, int pu, Yuv *org, int list,
   const int16_t *o = yaddr(org, 0, rx, ry), *q = E.S->pred_l[1 - list] + ry * 64 + rx;
   for (int k = lid(); k < w * h; k += 64) {
     const int y = k / w, x = k - y * w;
-    sm.org[y * 64 + x] = (int16_t)(2 * o[y * 64 + x] - q[y * 64 + x]);
+    sm.org[y * 64 + x] = (int16_t)(2 * o[y * ystride(0) + x] - q[y * 64 + x]);
   }
   wsync();
   hvx_me_job j;
@@ -2675,8 +2684,8 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
       part_position(cu, ps, pu, xp, yp, w, h);
       if (test_normal) {
         mc_pu(cu, ps, pu, &E.S->tmp_yuv_pred);
-        const uint32_t err = wave_satd(yaddr(org, 0, xp - cu->x, yp - cu->y), 64,
-                                       yaddr(&E.S->tmp_yuv_pred, 0, xp - cu->x, yp - cu->y), 64, w, h);
+        const uint32_t err = wave_satd(yaddr(org, 0, xp - cu->x, yp - cu->y), ystride(0),
+                                       yaddr(&E.S->tmp_yuv_pred, 0, xp - cu->x, yp - cu->y), ystride(0), w, h);
         me_cost = err + mv_cost_bits(me_bits);
       }
       const Part save = cu->p[a];
@@ -3145,7 +3154,7 @@ __device__ void set_intra_result_luma(Cu *cu, Yuv *reco, const Tu &t) {
     const int layer = qt_layer(t.log2), w = t.w[0];
     if (w) {
       blk_copy(cu->coef + t.off[0], w, E.S->qt_coef[layer] + t.off[0], w, w, w);
-      blk_copy(yaddr(reco, 0, t.x0[0], t.y0[0]), 64, yaddr(&E.S->qt_yuv[layer], 0, t.x0[0], t.y0[0]), 64, w, w);
+      blk_copy(yaddr(reco, 0, t.x0[0], t.y0[0]), ystride(0), yaddr(&E.S->qt_yuv[layer], 0, t.x0[0], t.y0[0]), ystride(0), w, w);
     }
   } else {
     if constexpr (LV < 3) {
@@ -3345,7 +3354,7 @@ __device__ void set_intra_result_chroma(Cu *cu, Yuv *reco, const Tu &t) {
     const int layer = qt_layer(t.log2), w = t.w[1];
     for (int c = 1; c < 3; c++) {
       blk_copy(cu->coef + coff(c) + t.off[c], w, E.S->qt_coef[layer] + coff(c) + t.off[c], w, w, w);
-      blk_copy(yaddr(reco, c, t.x0[c], t.y0[c]), 32, yaddr(&E.S->qt_yuv[layer], c, t.x0[c], t.y0[c]), 32, w, w);
+      blk_copy(yaddr(reco, c, t.x0[c], t.y0[c]), ystride(c), yaddr(&E.S->qt_yuv[layer], c, t.x0[c], t.y0[c]), ystride(c), w, w);
     }
   } else {
     if constexpr (LV < 3) {
@@ -3509,6 +3518,7 @@ template <int D>
 __device__ void compress_cu(int parent_ps) {
   if (HM_STOPPED) return;
   const int depth = D;
+  E.yw = 64 >> D;
   Cu *best = BEST(depth);
   copy_org_to_yuv(YB(Y_ORIG, depth), best);
   int boundary = 0;
@@ -3588,6 +3598,7 @@ __device__ void compress_cu(int parent_ps) {
         cu_copy_part_from(TEMP(depth), sb, k, nd);
       }
     }
+    E.yw = 64 >> D;  // the children left their own layout
     Cu *tmp = TEMP(depth);
     E.cur = GOON;
     cload(E.cur, RD(nd, CI_NEXT_BEST));
@@ -3740,8 +3751,35 @@ __device__ void compress_ctu(int addr, const Coder *entry_g, int entry_in_lds, C
 #else
 #define HM_KATTR
 #endif
-static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm_picture *__restrict__ pics, const hvx_hm_job *__restrict__ jobs,
-                                                    int n_jobs, char *state_base, size_t state_bytes, hvx_hm_ctu *out_ctu,
+// the preconditions of a job (include/hvx.h hvx_hm_compress): 0 when it may run, else the
+// HVX_HM_BAD_* code of the first violated one (the job is then skipped: nothing is written)
+__device__ int hm_job_check(const hvx_hm_picture *pics, int n_pics, const hvx_hm_job &j, int n_out) {
+  if (j.pic < 0 || j.pic >= n_pics) return HVX_HM_BAD_PIC;
+  const hvx_hm_picture &P = pics[j.pic];
+  if (P.w <= 0 || P.h <= 0 || (P.w & 7) || (P.h & 7) || P.w_ctus != (P.w + 63) / 64 || P.h_ctus != (P.h + 63) / 64)
+    return HVX_HM_BAD_GEOMETRY;
+  if (P.slice_type < 0 || P.slice_type > 2 || P.nref[0] < 0 || P.nref[0] > 4 || P.nref[1] < 0 || P.nref[1] > 4 ||
+      (P.slice_type != 0 && P.nref[1] != 0) || (P.slice_type == 2 && P.nref[0] != 0) || (P.slice_type != 2 && P.nref[0] < 1))
+    return HVX_HM_BAD_REFS;
+  for (int l = 0; l < 2; l++)
+    for (int i = 0; i < P.nref[l]; i++) {
+      const int k = P.ref_plane[l][i];
+      if (k < 0 || k >= 8 || !P.ref8[k] || !P.ref16[k][0] || !P.ref16[k][1] || !P.ref16[k][2]) return HVX_HM_BAD_REFS;
+    }
+  if (!P.org[0] || !P.org[1] || !P.org[2] || !P.rec[0] || !P.rec[1] || !P.rec[2] || !P.ctus || !P.entropy_bits ||
+      (P.col_valid && !P.col_field))
+    return HVX_HM_BAD_PLANES;
+  const int n = P.w_ctus * P.h_ctus;
+  if (j.first_ctu < 0 || j.n_ctus < 1 || j.first_ctu + j.n_ctus > n || j.slice_start < 0 || j.slice_start > j.first_ctu ||
+      j.slice_end < j.first_ctu + j.n_ctus - 1 || j.slice_end >= n)
+    return HVX_HM_BAD_CTUS;
+  if (j.out < 0 || (n_out > 0 && j.out + j.n_ctus > n_out)) return HVX_HM_BAD_OUT;
+  return 0;
+}
+
+static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm_picture *__restrict__ pics, int n_pics,
+                                                    const hvx_hm_job *__restrict__ jobs, int n_jobs, int n_out,
+                                                    char *state_base, size_t state_bytes, hvx_hm_ctu *out_ctu,
                                                     uint8_t *out_rec, hvx_hm_coder *out_coder) {
   using namespace hm;
 #ifdef HM_XCD_GROUP
@@ -3756,6 +3794,12 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
   if (jid >= n_jobs) return;
   const int l = threadIdx.x;
   const hvx_hm_job &job = jobs[jid];
+  State *S = (State *)(state_base + (size_t)jid * state_bytes);
+  {
+    const int bad = hm_job_check(pics, n_pics, job, n_out);
+    if (l < 4) S->dbg[l] = l == 0 ? -bad : 0;  // the job's status word (hvx_hm_job_status)
+    if (bad) return;
+  }
   copy_words(&hm_e.P, &pics[job.pic], (int)sizeof(hvx_hm_picture));
   wsync();
   for (int i = l; i < 128; i += 64) {
@@ -3764,7 +3808,6 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
     hm_e.next[i * 2 + mps] = (uint8_t)(((p < 62 ? p + 1 : p) << 1) | mps);
     hm_e.next[i * 2 + (mps ^ 1)] = (uint8_t)((cab::kTransIdxLps[p] << 1) | (p == 0 ? mps ^ 1 : mps));
   }
-  State *S = (State *)(state_base + (size_t)jid * state_bytes);
   hm_e.S = S;
   if (l < 4) hm_e.dbg[l] = 0;
   hm_e.stage = job.flags >> 8;

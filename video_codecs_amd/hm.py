@@ -295,9 +295,12 @@ class Engine:
         self.reserve(n_jobs)
         P = ctypes.c_void_p
 
+        n_out = out_rec.numel() // 6144
+
         def go():
-            hvx._check(hvx.lib().hvx_hm_compress(hvx.context(), P(self.pics_t.data_ptr()), P(jobs_t.data_ptr()), n_jobs,
-                                                 P(self.state.data_ptr()), P(out_ctu.data_ptr()), P(out_rec.data_ptr()),
+            hvx._check(hvx.lib().hvx_hm_compress(hvx.context(), P(self.pics_t.data_ptr()), len(self.pictures),
+                                                 P(jobs_t.data_ptr()), n_jobs, n_out, P(self.state.data_ptr()),
+                                                 P(out_ctu.data_ptr()), P(out_rec.data_ptr()),
                                                  P(0 if out_cod is None else out_cod.data_ptr())), "hvx_hm_compress")
         cur = torch.cuda.current_stream()
         if cur.cuda_stream:
@@ -311,6 +314,17 @@ class Engine:
         with torch.cuda.stream(self.stream):
             go()
         cur.wait_stream(self.stream)
+
+    def job_status(self, n_jobs):
+        """The status word of each job of the last launch (0: ran; -HVX_HM_BAD_*: refused by the
+        device-side precondition check, include/hvx.h)."""
+        import torch
+        from . import hvx
+        torch.cuda.synchronize()
+        st = np.zeros(n_jobs, np.int32)
+        hvx._check(hvx.lib().hvx_hm_job_status(hvx.context(), ctypes.c_void_p(self.state.data_ptr()), n_jobs,
+                                               st.ctypes.data_as(ctypes.c_void_p)), "hvx_hm_job_status")
+        return st
 
     def compress(self, jobs, n_out):
         """Run the jobs (HM_JOB array); returns (ctus [n_out] HM_CTU, rec [n_out, 6144] uint8,
