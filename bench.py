@@ -41,8 +41,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--pics", type=int, default=60, help="P pictures in flight per GPU (34 slice chains each at 2160p: "
-                                                        "60 -> 2040 chains, two waves per SIMD)")
+    p.add_argument("--pics", type=int, default=62, help="P pictures in flight per GPU (33 slice chains each at 2160p: "
+                                                        "62 -> 2046 chains, two waves per SIMD)")
     p.add_argument("--ctus", type=int, default=1, help="CTUs each slice chain advances per step")
     p.add_argument("--cpu-ref-procs", type=int, default=0, help="HM TAppEncoder processes for the reference "
                                                                   "baseline (0: the host's CPU share)")
@@ -179,7 +179,8 @@ def synthetic_col_field(nctu, seed):
 class HmWorkload:
     """The headline workload on one GPU: `pics` P pictures of W x H random 4:2:0 YUV, picture p
     (POC nref + p) predicted from the nref previous frames, every CTU row a SliceMode=1 slice
-    decided by one chain (one wave); slice parameters of GOP position 2 of the LDP GOP
+    decided by one chain (one wave) -- a partial bottom row continues the chain of the row above
+    it (HVX_HM_SLICE_CTUS) -- with the slice parameters of GOP position 2 of the LDP GOP
     (hm.slice_params).  Step k advances every chain by `ctus` CTUs from where step k-1 left it
     (HVX_HM_RESUME); a chain that reaches its row's end starts the row again as a new slice."""
 
@@ -207,28 +208,41 @@ class HmWorkload:
         self.eng = hm.Engine(self.pictures)
         self.stream = torch.cuda.Stream()
         torch.cuda.synchronize()  # inputs resident before any launch on the workload's stream
-        self.n_jobs = pics * self.hc
+        # the chains of a picture: one per CTU row slice, except that a partial bottom row (2160 =
+        # 33 x 64 + 48) is chained after the row above it -- its first CTU is a picture-boundary CTU
+        # whose searches read TEncSearch::m_integerMv2Nx2N as the row above's last CTU left it
+        # (HVX_HM_SLICE_CTUS: the coder restarts at the slice, the search state carries on)
+        self.merge_last = H % 64 != 0 and self.hc >= 2
+        self.rows = self.hc - 1 if self.merge_last else self.hc
+        self.n_jobs = pics * self.rows
         self.eng.reserve(self.n_jobs)
         self.slots = self.n_jobs * ctus
-        # one device job array per position in the row (the step's first CTU of every chain)
+        # one device job array per step position (the step's first CTU of every chain); the period
+        # is two rows when the last chain spans two
         self.phase_jobs = []
-        for pos in range(0, self.wc, ctus):
+        period = 2 * self.wc if self.merge_last else self.wc
+        for pos in range(0, period, ctus):
             j = np.zeros(self.n_jobs, hm.HM_JOB)
             for p in range(pics):
-                for r in range(self.hc):
-                    k = p * self.hc + r
-                    j[k]["pic"], j[k]["first_ctu"], j[k]["n_ctus"], j[k]["chained"] = p, r * self.wc + pos, ctus, 1
-                    j[k]["out"] = k * ctus
-                    j[k]["slice_start"], j[k]["slice_end"] = r * self.wc, r * self.wc + self.wc - 1
-                    j[k]["flags"] = _abi.HM_RESUME if pos else 0
+                for r in range(self.rows):
+                    k = p * self.rows + r
+                    j[k]["pic"], j[k]["n_ctus"], j[k]["chained"], j[k]["out"] = p, ctus, 1, k * ctus
                     j[k]["entry"]["st"] = self.entry
+                    if self.merge_last and r == self.rows - 1:
+                        j[k]["first_ctu"] = r * self.wc + pos
+                        j[k]["flags"] = _abi.hm_slice_ctus(self.wc) | (_abi.HM_RESUME if pos else 0)
+                    else:
+                        q = pos % self.wc
+                        j[k]["first_ctu"] = r * self.wc + q
+                        j[k]["slice_start"], j[k]["slice_end"] = r * self.wc, r * self.wc + self.wc - 1
+                        j[k]["flags"] = _abi.HM_RESUME if q else 0
             self.phase_jobs.append(torch.from_numpy(j.view(np.uint8).reshape(-1).copy()).cuda())
         self.out_ctu = torch.zeros(self.slots * hm.HM_CTU.itemsize, dtype=torch.uint8, device="cuda")
         self.step_idx = 0
-        # picture 0's chains (slots 0 .. hc*ctus-1): every step's CTU records + reconstruction
+        # picture 0's chains (slots 0 .. rows*ctus-1): every step's CTU records + reconstruction
         # kept for the parity check against the oracle after the timed region
         self.keep_steps = []
-        self.keep_n = self.hc * ctus
+        self.keep_n = self.rows * ctus
 
     def col_field(self, p):
         return synthetic_col_field(self.wc * self.hc, self.base + p) if self.col else None
@@ -323,7 +337,7 @@ def _time_chains(eng, job_steps, n_out, warmup):
     return ms * 1e-3, wall
 
 
-def ra_ssim_measure(W, H, pics=60, distinct=12, qps=(22, 27, 32, 37), warmup=1, steps=1):
+def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, steps=1):
     """BASELINE config 4 (side figure): 2160p random-access B pictures with the stvssim SSIM cost in
     the decision (hvx_hm_compress, HVX_RD_SSIM, eta 1) at QP 22 / 27 / 32 / 37.  The picture is GOP
     position 2 of encoder_randomaccess_main.cfg (POC 4, TId 1: QP offset 2, QPFactor 0.3536,
@@ -355,10 +369,16 @@ def ra_ssim_measure(W, H, pics=60, distinct=12, qps=(22, 27, 32, 37), warmup=1, 
             k = p % distinct
             pictures.append(hm.DevicePicture(frames[3 * k + 2], [frames[3 * k], frames[3 * k + 1]], prm, eb, col_field=col))
         eng = hm.Engine(pictures)
-        job_steps = [_chain_jobs([(p, r * wc + pos, 1, r * wc, r * wc + wc - 1, pos > 0) for p in range(pics)
-                                  for r in range(hc)], entry) for pos in range(warmup + steps)]
-        sec, wall = _time_chains(eng, job_steps, pics * hc, warmup)
-        res[str(base_qp)] = {"slice_qp": qp, "ctus_per_s": round(pics * hc / sec, 2), "ms_per_step": round(sec * 1e3, 1),
+        rows = hc - 1 if H % 64 else hc  # the partial bottom row chained after the row above (HmWorkload)
+        job_steps = []
+        for pos in range(warmup + steps):
+            specs = [(p, r * wc + pos, 1, r * wc, r * wc + wc - 1, pos > 0) for p in range(pics) for r in range(rows)]
+            j = _chain_jobs(specs, entry)
+            if rows < hc:
+                j["flags"][rows - 1::rows] |= _abi.hm_slice_ctus(wc)
+            job_steps.append(j)
+        sec, wall = _time_chains(eng, job_steps, pics * rows, warmup)
+        res[str(base_qp)] = {"slice_qp": qp, "ctus_per_s": round(pics * rows / sec, 2), "ms_per_step": round(sec * 1e3, 1),
                              "wall_ms_per_step": round(wall * 1e3, 1), "lambda_ssim": prm["lambda_ssim"]}
         del eng, pictures
         torch.cuda.empty_cache()
@@ -415,7 +435,7 @@ def hm_cpu_port(work, threads, min_seconds=0.0):
     from oracle import hm_ctu
     from video_codecs_amd import hm
     pi, pf, org, refs, col = work.host_inputs(0)
-    wc, hc = work.wc, work.hc
+    wc, hc = work.wc, work.rows  # the picture's chains (the last may continue into the partial bottom row)
     done = min(work.step_idx * work.ctus, wc)  # CTUs of each row decided by the GPU (first pass)
     chain_first = np.arange(hc, dtype=np.int32) * wc
     hm_ctu.chains(pi, pf, org, refs, work.entry, chain_first[:1], 1, wc, threads=1, col_field=col)  # tables

@@ -392,6 +392,13 @@ typedef struct hvx_hm_job {
 /* hvx_hm_job.flags: continue the chain of the previous launch with the same job index -- the entry
  * coder and m_integerMv2Nx2N come from that job's state (d_state), not from entry / int2n */
 #define HVX_HM_RESUME 1
+/* hvx_hm_job.flags bits 16..30: SliceMode=1 slices of that many CTUs (0: one slice, [slice_start,
+ * slice_end]).  The chain may then run over consecutive slices: each slice's first CTU starts from
+ * `entry` (the slice-start context states) and ends its predecessor without the end-of-slice bin,
+ * while m_integerMv2Nx2N carries from CTU to CTU across the slice boundary, as in TAppEncoder --
+ * where a slice whose first CTU is a picture-boundary CTU (the partial bottom row) reads it. */
+#define HVX_HM_SLICE_CTUS(n) ((int32_t)(n) << 16)
+#define HVX_HM_SLICE_CTUS_OF(flags) (((flags) >> 16) & 0x7fff)
 
 #ifdef __cplusplus
 }

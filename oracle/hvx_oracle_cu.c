@@ -3058,15 +3058,19 @@ typedef struct {
 static void chain_run(chain_job *J, int k) {
   const hvxo_hm_pic *P = J->P;
   const int first = J->chain_first[k];
-  const int s0 = first - first % J->slice_ctus;
-  const int s1 = (s0 + J->slice_ctus < J->n ? s0 + J->slice_ctus : J->n) - 1;
   hvxo_hm_coder cur;
-  memset(&cur, 0, sizeof(cur));
-  memcpy(cur.st, J->entry_states, 202);
   int16_t int2n[16], next2n[16];
   memset(int2n, 0, sizeof(int2n));
   for (int i = 0; i < J->per_chain; i++) {
     const int a = first + i;
+    /* a chain may run over consecutive slices: every slice starts from the slice-start states,
+     * m_integerMv2Nx2N carries on (TEncSlice::compressSlice, TEncSearch member state) */
+    const int s0 = a - a % J->slice_ctus;
+    const int s1 = (s0 + J->slice_ctus < J->n ? s0 + J->slice_ctus : J->n) - 1;
+    if (i == 0 || a == s0) {
+      memset(&cur, 0, sizeof(cur));
+      memcpy(cur.st, J->entry_states, 202);
+    }
     hvxo_hm_coder after;
     hvxo_hm_compress_ctu_slice(P, J->ctus, J->rec, J->rs, a, s0, s1, &cur, int2n, next2n, &after);
     cur = after;
@@ -3120,9 +3124,7 @@ int hvxo_hm_chains_rd(const int32_t *pi, const double *pf, const uint8_t *org, c
   if (pi[P_COL_VALID] && !col_field) return -1;
   const int w = pi[P_W], h = pi[P_H], wc = (w + 63) / 64, hc = (h + 63) / 64, n = wc * hc;
   for (int k = 0; k < n_chains; k++)
-    if (slice_ctus < 1 || chain_first[k] < 0 || chain_first[k] + ctus_per_chain > n ||
-        chain_first[k] % slice_ctus + ctus_per_chain > slice_ctus)
-      return -1;
+    if (slice_ctus < 1 || ctus_per_chain < 1 || chain_first[k] < 0 || chain_first[k] + ctus_per_chain > n) return -1;
   pic_buf B;
   pic_setup(&B, pi, pf, org, refpics, n_refpics, col_field, entropy_bits);
   B.P.rd_metric = rd_metric;

@@ -99,7 +99,8 @@ int hvxo_hm_replay_picture_rd(const int32_t *pic_i32, const double *pic_f64, con
 
 /* Independent SliceMode=1 slice chains (slices of slice_ctus CTUs): chain k decides CTUs
  * chain_first[k] .. + ctus_per_chain - 1 from entry_states (the slice-start contexts) and a zero
- * m_integerMv2Nx2N, carrying both CTU to CTU; the chains run on n_threads threads.  Picture
+ * m_integerMv2Nx2N, carrying both CTU to CTU (a chain crossing into the next slice restarts from
+ * entry_states there and carries m_integerMv2Nx2N on); the chains run on n_threads threads.  Picture
  * arrays as hvxo_hm_replay_picture; outputs per (chain, CTU) in that order. */
 int hvxo_hm_chains(const int32_t *pic_i32, const double *pic_f64, const uint8_t *org, const uint8_t *refpics,
                    int n_refpics, const int16_t *col_field, const int32_t *entropy_bits, const uint8_t *entry_states,

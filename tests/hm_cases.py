@@ -92,7 +92,8 @@ def device_picture(g, pic, chained, entropy_bits, rd_metric=0, eta=1.0):
 
 def run_capture(name, mode, pics=None, stage=0, rd_metric=0, eta=1.0):
     """Decide the captured pictures on the device.  mode 0: every CTU as its own job from the
-    reference's entry state and neighbourhood; mode 1: one chained job per picture.  Returns
+    reference's entry state and neighbourhood; mode 1: one chained job per picture (per row slice
+    for the row-sliced capture); mode 2: one chained job per picture across its row slices.  Returns
     (g, list of (pic, first, n, out_slot0), (ctus, rec, coders))."""
     g = gc.load(name)
     g["_row_slices"] = name in ROW_SLICES
@@ -108,6 +109,8 @@ def run_capture(name, mode, pics=None, stage=0, rd_metric=0, eta=1.0):
         rows = name in ROW_SLICES
         if mode == 0:
             ctus = [(a, 1) for a in range(n)]
+        elif mode == 2:  # one chain over the whole picture, across its row slices (HVX_HM_SLICE_CTUS)
+            ctus = [(0, n)]
         else:
             ctus = [(r, wc) for r in range(0, n, wc)] if rows else [(0, n)]
         for a, cnt in ctus:
@@ -117,6 +120,8 @@ def run_capture(name, mode, pics=None, stage=0, rd_metric=0, eta=1.0):
             j["entry"]["frac"] = np.uint64(int(g["ctu_frac"][first + a]))
             j["int2n"] = g["ctu_int2n"][first + a]
             j["flags"] = stage << 8
+            if rows and mode == 2:
+                j["flags"] |= _abi.hm_slice_ctus(wc)
             if rows:
                 j["slice_start"], j["slice_end"] = a - a % wc, a - a % wc + wc - 1
             else:

@@ -318,6 +318,16 @@ def test_hm_ctu_golden_gpu(torch, name, mode):
 
 
 @pytest.mark.gpu
+def test_hm_ctu_multislice_gpu(torch):
+    """HVX_HM_SLICE_CTUS: one chain per picture over its row slices (each slice restarting from the
+    slice-start states, m_integerMv2Nx2N carried across slice boundaries as in TAppEncoder);
+    bit-exact vs HM on every CTU of the row-sliced capture."""
+    g, plan, out = hm_cases.run_capture("ctu_ldp_slices.bin", 2)
+    bad = hm_cases.compare(g, plan, out)
+    assert not bad, bad[:5]
+
+
+@pytest.mark.gpu
 def test_hm_ctu_resume_gpu(torch):
     """HVX_HM_RESUME (the bench's stepping): every row slice decided in two launches, the second
     continuing from the CABAC state and m_integerMv2Nx2N the first left in the job's state slot;

@@ -126,8 +126,8 @@ def test_hm_chains_rejects_bad_layout():
     g = _load("ctu_ldp_slices.bin")
     pi, pf = g["pic_i32"][2], g["pic_f64"][2]
     psz = int(pi[0]) * int(pi[1]) * 3 // 2
-    with pytest.raises(ValueError):  # a chain crossing its slice's end
-        hm_ctu.chains(pi, pf, g["org"][2 * psz:3 * psz], g["refpic"], g["ctu_states"][56], [5], 3, 7,
+    with pytest.raises(ValueError):  # a chain past the picture's last CTU
+        hm_ctu.chains(pi, pf, g["org"][2 * psz:3 * psz], g["refpic"], g["ctu_states"][56], [26], 3, 7,
                       col_field=g["col_field"][448:896])
     with pytest.raises(ValueError):  # TMVP on without a collocated field
         hm_ctu.chains(pi, pf, g["org"][2 * psz:3 * psz], g["refpic"], g["ctu_states"][56], [0], 1, 7)
@@ -221,3 +221,28 @@ def test_ctx_init_states_ra_vs_hm():
             swapped += eff != st
             np.testing.assert_array_equal(g["ctu_states"][first], init[eff, qp], err_msg=(name, pic))
     assert swapped > 0
+
+
+def test_hm_chains_across_slices_vs_hm():
+    """One chain over consecutive row slices (rows 1-3 of the sliced capture's QP 32 picture, 21
+    CTUs): each slice restarts from the slice-start states while m_integerMv2Nx2N carries across
+    the slice boundary as in TAppEncoder -- every CTU equals HM's, including the partial bottom
+    row, whose boundary CTUs read the carried integer MVs."""
+    import numpy as np
+    g = _load("ctu_ldp_slices.bin")
+    pic = 2
+    pi, pf = g["pic_i32"][pic], g["pic_f64"][pic]
+    w, h = int(pi[0]), int(pi[1])
+    psz = w * h * 3 // 2
+    first, n = int(pi[41]), int(pi[42])
+    wc = (w + 63) // 64
+    col = g["col_field"][n * 16:2 * n * 16]
+    # the chain starts at row 0 from a zero m_integerMv2Nx2N (HM carries the previous picture's, but
+    # a whole CTU's depth-0 2Nx2N searches set it before any search reads it) and runs all 4 rows
+    out = hm_ctu.chains(pi, pf, g["org"][pic * psz:(pic + 1) * psz], g["refpic"], g["ctu_states"][first], [0], n, wc,
+                        threads=1, col_field=col)
+    for a in range(n):
+        np.testing.assert_array_equal(out["parts"][a], g["ctu_parts"][first + a], err_msg=a)
+        np.testing.assert_array_equal(out["coef"][a], g["ctu_coef"][first + a], err_msg=a)
+        np.testing.assert_array_equal(out["recon"][a], g["ctu_recon"][first + a], err_msg=a)
+        assert out["cost"][a] == g["ctu_cost"][first + a], a

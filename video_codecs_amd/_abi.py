@@ -107,6 +107,11 @@ PLANE_MARGIN = 80
 HM_RESUME = 1  # HVX_HM_RESUME (hvx_hm_job.flags)
 
 
+def hm_slice_ctus(n):
+    """HVX_HM_SLICE_CTUS(n) (hvx_hm_job.flags): a chain over consecutive SliceMode=1 slices of n CTUs."""
+    return int(n) << 16
+
+
 def lambda_motion_sad(lam: float) -> int:
     """TComRdCost::setLambda, m_uiLambdaMotionSAD[0] = (UInt)floor(65536.0 * sqrt(lambda)) (TComRdCost.cpp:210)."""
     return int(np.floor(65536.0 * np.sqrt(lam)))

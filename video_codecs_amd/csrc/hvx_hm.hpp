@@ -3770,8 +3770,9 @@ __device__ int hm_job_check(const hvx_hm_picture *pics, int n_pics, const hvx_hm
       (P.col_valid && !P.col_field))
     return HVX_HM_BAD_PLANES;
   const int n = P.w_ctus * P.h_ctus;
-  if (j.first_ctu < 0 || j.n_ctus < 1 || j.first_ctu + j.n_ctus > n || j.slice_start < 0 || j.slice_start > j.first_ctu ||
-      j.slice_end < j.first_ctu + j.n_ctus - 1 || j.slice_end >= n)
+  if (j.first_ctu < 0 || j.n_ctus < 1 || j.first_ctu + j.n_ctus > n) return HVX_HM_BAD_CTUS;
+  if (HVX_HM_SLICE_CTUS_OF(j.flags) == 0 &&
+      (j.slice_start < 0 || j.slice_start > j.first_ctu || j.slice_end < j.first_ctu + j.n_ctus - 1 || j.slice_end >= n))
     return HVX_HM_BAD_CTUS;
   if (j.out < 0 || (n_out > 0 && j.out + j.n_ctus > n_out)) return HVX_HM_BAD_OUT;
   return 0;
@@ -3827,10 +3828,22 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
   }
   wsync();
   const int n = job.n_ctus;
+  const int slice_ctus = HVX_HM_SLICE_CTUS_OF(job.flags), nctu = hm_e.P.w_ctus * hm_e.P.h_ctus;
   for (int k = 0; k < n; k++) {
     const int addr = job.first_ctu + k;
     const int slot = job.out + k;
-    compress_ctu(addr, &job.entry, k > 0 || resume, out_coder ? &out_coder[slot] : nullptr);
+    // a chain over consecutive SliceMode=1 slices: each slice's first CTU starts from the slice-start
+    // coder (entry) while TEncSearch's m_integerMv2Nx2N carries on, as TEncSlice::compressSlice does
+    bool slice_first = false;
+    if (slice_ctus > 0) {
+      const int s0 = addr - addr % slice_ctus;
+      wsync();
+      hm_e.slice_start = s0;
+      hm_e.slice_end = (s0 + slice_ctus < nctu ? s0 + slice_ctus : nctu) - 1;
+      wsync();
+      slice_first = addr == s0;
+    }
+    compress_ctu(addr, &job.entry, (k > 0 || resume) && !slice_first, out_coder ? &out_coder[slot] : nullptr);
     // the next CTU starts from this CTU's encodeCtu state (m_pppcRDSbacCoder[0][CI_CURR_BEST])
     // which compress_ctu left in coder RD(0, CI_CURR_BEST)
     copy_words(&S->carry, &hm_e.cod[RD(0, CI_CURR_BEST)], (int)sizeof(Coder));
