@@ -418,6 +418,26 @@ int hvx_hm_compress(hvx_ctx *ctx, const hvx_hm_picture *d_pics, int n_pics, cons
  * the context's stream */
 int hvx_hm_job_status(hvx_ctx *ctx, const void *d_state, int n_jobs, int32_t *h_status);
 
+/* ---------------------------------------------------------------------------------------
+ * The picture-level steps TEncGOP runs after compressSlice (TEncGOP.cpp:1465-1629), on a picture
+ * whose every CTU hvx_hm_compress has decided (h_pic: the host copy of its hvx_hm_picture; its
+ * ctus and rec complete), in stream order:
+ *   h_dbk != NULL: TComLoopFilter::loopFilterPic (TComLoopFilter.cpp:130) on rec in place, with the
+ *     boundary strengths and QP map derived on the device from the CTU data exactly as
+ *     xDeblockCU / xGetBoundaryStrengthSingle do (:170-557; LFCrossSliceBoundaryFlag on, filter
+ *     enabled; h_dbk->pic_w / pic_h = the picture's).  d_work: 3 * (w/4) * (h/4) bytes that receive
+ *     the bs_ver, bs_hor and QP maps of hvx_deblock (in that order).  NULL = deblocking disabled.
+ *   d_col_field != NULL: TComPic::compressMotion -- the picture's hvx_hm_picture.col_field rows
+ *     ([w_ctus*h_ctus][16][8]) for the pictures that take it as their collocated picture.
+ *   d_ref8 / d_ref16_*: the filtered picture as the engine's reference formats (hvx_hm_picture
+ *     ref8 / ref16, sample (0,0) pointers): 8-bit luma with HVX_PLANE_MARGIN, int16 Y / Cb / Cr with
+ *     80 / 40 samples of border, TComPicYuv::extendPicBorder (TComSlice.cpp:351).  Either may be NULL.
+ * SAO is not applied here (hvx_sao_apply with decided parameters).  w, h multiples of 8.
+ * ------------------------------------------------------------------------------------- */
+int hvx_hm_finish_picture(hvx_ctx *ctx, const hvx_hm_picture *h_pic, const hvx_deblock_params *h_dbk, uint8_t *d_work,
+                          int16_t *d_col_field, uint8_t *d_ref8, int ref8_stride, int16_t *d_ref16_y, int16_t *d_ref16_cb,
+                          int16_t *d_ref16_cr, int ref16_stride_y, int ref16_stride_c);
+
 #ifdef __cplusplus
 }
 #endif

@@ -52,6 +52,7 @@ struct Store {
   std::vector<int32_t> meta;  // per picture: w, h, beta_offset_div2, tc_offset_div2, cb_qp_offset, cr_qp_offset, bypass
   std::vector<uint8_t> pre, post, bs_ver, bs_hor;
   std::vector<int8_t> qp;
+  std::vector<int32_t> poc;
   int n = 0;
   ~Store() {
     const char *out = getenv("HVX_CAPTURE");
@@ -63,6 +64,7 @@ struct Store {
     gw.add("bs_ver", "u8", {(uint32_t)bs_ver.size()}, bs_ver);  // per picture: (w/4)*(h/4), raster
     gw.add("bs_hor", "u8", {(uint32_t)bs_hor.size()}, bs_hor);
     gw.add("qp", "i8", {(uint32_t)qp.size()}, qp);
+    gw.add("poc", "i32", {(uint32_t)n}, poc);
     gw.write(out);
     fprintf(stderr, "deblock_capture: %d pictures\n", n);
   }
@@ -104,10 +106,23 @@ void bs_walk(TComLoopFilter &lf, TComDataCU *cu, UInt abs, UInt depth, DeblockEd
     if (lf.m_aapbEdgeFilter[dir][p] && check) lf.xGetBoundaryStrengthSingle(cu, dir, p);
   }
 }
+// HVX_CAPTURE_POCS=<poc,poc,...>: record the pictures of these POCs (default: the first two deblocked)
+bool keep_picture(int poc) {
+  const char *s = getenv("HVX_CAPTURE_POCS");
+  if (!s || !*s) return g.n < 2;
+  for (const char *p = s; *p;) {
+    char *end;
+    const long v = strtol(p, &end, 10);
+    if (end == p) break;
+    if (v == poc) return true;
+    p = *end ? end + 1 : end;
+  }
+  return false;
+}
 }  // namespace
 
 extern "C" void CAT(__wrap_, LF_SYM)(TComLoopFilter *self, TComPic *pic) {
-  const bool keep = g.n < 2;
+  const bool keep = keep_picture(pic->getPOC());
   if (keep) {
     TComSlice *sl = pic->getSlice(0);
     const TComSPS &sps = *sl->getSPS();
@@ -116,6 +131,7 @@ extern "C" void CAT(__wrap_, LF_SYM)(TComLoopFilter *self, TComPic *pic) {
     g.meta.insert(g.meta.end(), {W, H, sl->getDeblockingFilterBetaOffsetDiv2(), sl->getDeblockingFilterTcOffsetDiv2(),
                                  pps.getQpOffset(COMPONENT_Cb), pps.getQpOffset(COMPONENT_Cr),
                                  pps.getTransquantBypassEnableFlag() ? 1 : 0});
+    g.poc.push_back(pic->getPOC());
     planes(pic, g.pre);
     std::vector<uint8_t> bs[2] = {std::vector<uint8_t>(uw * uh, 0), std::vector<uint8_t>(uw * uh, 0)};
     std::vector<int8_t> qp(uw * uh, 0);

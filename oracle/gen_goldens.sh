@@ -98,6 +98,23 @@ cucap tests/golden/ctu_ldp_smooth.bin $CFG/encoder_lowdelay_P_main.cfg "$TMP/smo
 HVX_CAPTURE="$TMP/cu.bin" $ORC/TAppEncoder_cucap -c $CFG/encoder_lowdelay_P_main.cfg -i "$TMP/smooth4.yuv" -wdt 416 -hgt 240 \
   -fr 30 -f 3 -q 30 --SliceMode=1 --SliceArgument=7 -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
 python3 oracle/compact_ctu.py "$TMP/cu.bin" tests/golden/ctu_ldp_slices.bin
+# B slices: encoder_randomaccess_main.cfg on textured content in motion, QP 22/27/32/37, the
+# recorded POCs chosen to cover GOP8 depths 0-3 (uni-L0 / uni-L1 / bi AMVP choices, bBi refinement)
+python3 oracle/make_yuv.py texture 416 240 9 "$TMP/tex9.yuv"
+for spec in 22:8,4,1,3 27:8,3 32:8,1 37:4,3; do
+  q=${spec%%:*}; pocs=${spec#*:}
+  HVX_CAPTURE_POCS=$pocs HVX_CAPTURE="$TMP/cu.bin" $ORC/TAppEncoder_cucap -c $CFG/encoder_randomaccess_main.cfg \
+    -i "$TMP/tex9.yuv" -wdt 416 -hgt 240 -fr 30 -f 9 -q $q -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+  python3 oracle/compact_ctu.py "$TMP/cu.bin" tests/golden/ctu_ra_q$q.bin
+done
+# the reference loop on the same encodes: loopFilterPic's BS / QP maps and pictures per recorded POC
+dbk() {  # dbk <out.bin> <pocs> <cfg> <yuv> <frames> <qp>
+  HVX_CAPTURE_POCS=$2 HVX_CAPTURE=$1 $ORC/TAppEncoder_dbkcap -c "$3" -i "$4" -wdt 416 -hgt 240 -fr 30 -f "$5" -q "$6" \
+    -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+}
+dbk tests/golden/dbk_ldp_rand.bin   0,1,2 $CFG/encoder_lowdelay_P_main.cfg  "$TMP/rand4.yuv"   3 32
+dbk tests/golden/dbk_ldp_smooth.bin 1,2,3 $CFG/encoder_lowdelay_P_main.cfg  "$TMP/smooth4.yuv" 4 27
+dbk tests/golden/dbk_ra_q32.bin     8,1   $CFG/encoder_randomaccess_main.cfg "$TMP/tex9.yuv"    9 32
 # slice-start CABAC states of every slice type and QP (TEncSbac::resetEntropy)
 make -s -C oracle ctx_init
 ls -la tests/golden

@@ -156,6 +156,40 @@ def chains(pic_i32, pic_f64, org, refpics, entry_states, chain_first, per_chain,
     return out
 
 
+def _lf_lib():
+    L = _lib()
+    if not getattr(L, "_hm_lf_bound", False):
+        P = ctypes.c_void_p
+        L.hvxo_hm_boundary_strength.restype = None
+        L.hvxo_hm_boundary_strength.argtypes = [ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int, P, P, P]
+        L.hvxo_hm_col_field.restype = None
+        L.hvxo_hm_col_field.argtypes = [ctypes.c_int, ctypes.c_int, P, P]
+        L._hm_lf_bound = True
+    return L
+
+
+def boundary_strength(w, h, parts, ref_poc, is_b):
+    """TComLoopFilter's boundary strengths and QP map of a decided picture (hvxo_hm_boundary_strength):
+    parts = [n_ctus, 256, 29] ctu_parts rows, ref_poc = [2, 4]; returns (bs_ver, bs_hor, qp), (h/4, w/4)."""
+    L = _lf_lib()
+    pa = np.ascontiguousarray(parts, np.int16)
+    assert pa.shape == (((w + 63) // 64) * ((h + 63) // 64), 256, 29)
+    rp = np.ascontiguousarray(ref_poc, np.int32).reshape(8)
+    bv, bh = np.zeros((h // 4, w // 4), np.uint8), np.zeros((h // 4, w // 4), np.uint8)
+    qp = np.zeros((h // 4, w // 4), np.int8)
+    L.hvxo_hm_boundary_strength(w, h, _ptr(pa), _ptr(rp), int(bool(is_b)), _ptr(bv), _ptr(bh), _ptr(qp))
+    return bv, bh, qp
+
+
+def col_field(w, h, parts):
+    """TComPic::compressMotion's field of a decided picture (hvxo_hm_col_field): [n_ctus * 16, 8] int16."""
+    L = _lf_lib()
+    pa = np.ascontiguousarray(parts, np.int16)
+    out = np.zeros((pa.shape[0] * 16, 8), np.int16)
+    L.hvxo_hm_col_field(w, h, _ptr(pa), _ptr(out))
+    return out
+
+
 if __name__ == "__main__":
     g = load(sys.argv[1])
     mode = int(sys.argv[2]) if len(sys.argv) > 2 else 0

@@ -548,8 +548,26 @@ static double err_scale(const hvx_tu_desc *tu) {
 }
 
 /* xRateDistOptQuant (:2129-2671) */
+#ifdef HVXO_RDOQ_STATS
+long long hvxo_rdoq_stat[4][3]; /* per log2 size - 2: calls, calls with every rounded level 0, calls with absSum 0 */
+#endif
 static void rdoq(const hvx_tu_desc *tu, const hvx_estbits *est, const int32_t *src, int32_t *dst, int32_t *arl, int32_t *abs_sum) {
   const int w = tu->width, h = tu->height, ch = tu->comp ? 1 : 0, comp = tu->comp;
+#ifdef HVXO_RDOQ_STATS
+  {
+    const int qb = 14 + tu->qp_per + transform_shift(tu), qc = kQuantScales[tu->qp_rem];
+    int anyq = 0;
+    for (int i = 0; i < w * h; i++) {
+      int64_t t = (int64_t)abs(src[i]) * qc;
+      int64_t lim = (int64_t)INT32_MAX - ((int64_t)1 << (qb - 1));
+      int32_t ld = (int32_t)(t < lim ? t : lim);
+      if (((ld + (1 << (qb - 1))) >> qb) > 0) anyq = 1;
+    }
+    const int l = (w == 4 ? 0 : w == 8 ? 1 : w == 16 ? 2 : 3);
+    __atomic_add_fetch(&hvxo_rdoq_stat[l][0], 1, __ATOMIC_RELAXED);
+    if (!anyq) __atomic_add_fetch(&hvxo_rdoq_stat[l][1], 1, __ATOMIC_RELAXED);
+  }
+#endif
   const int lw = w == 4 ? 2 : w == 8 ? 3 : w == 16 ? 4 : 5, lh = h == 4 ? 2 : h == 8 ? 3 : h == 16 ? 4 : 5;
   const int n = w * h, ext = tu->extended_precision, max_log2 = tu->max_log2_tr_range;
   const int ts = transform_shift(tu);

@@ -3199,3 +3199,105 @@ void hvxo_hm_derive_lists(hvxo_hm_pic *P) {
       if (P->ref_poc[0][k] == P->ref_poc[1][i]) { P->l1_to_l0[i] = k; break; }
   }
 }
+
+/* ============================================================================================
+ * Loop filter inputs and compressed motion of a decided picture (hvx_oracle_cu.h)
+ * ========================================================================================== */
+enum { PF_DEPTH = 0, PF_PART = 1, PF_PRED = 2, PF_REF0 = 7, PF_REF1 = 8, PF_MV0X = 9, PF_TR_IDX = 21, PF_CBF_Y = 25,
+       PF_QP = 28 };
+
+/* the z-order index of the 4x4 unit (ux, uy) of a CTU (g_auiRasterToZscan: x bits interleaved below y bits) */
+static int unit_z(int ux, int uy) {
+  int z = 0;
+  for (int b = 0; b < 4; b++) z |= (((ux >> b) & 1) << (2 * b)) | (((uy >> b) & 1) << (2 * b + 1));
+  return z;
+}
+static const int16_t *unit_part(const int16_t *parts, int wc, int x, int y) {
+  const int a = (y >> 6) * wc + (x >> 6);
+  return parts + ((size_t)a * 256 + unit_z((x & 63) >> 2, (y & 63) >> 2)) * HVXO_HM_PART_FIELDS;
+}
+/* the unit's reference picture of list l (TComSlice::getRefPic), by POC; INT32_MIN = none (NULL) */
+static int32_t unit_ref(const int16_t *q, const int32_t *ref_poc, int l) {
+  const int r = q[PF_REF0 + l];
+  return r < 0 ? INT32_MIN : ref_poc[l * 4 + r];
+}
+static int mv_far(const int *a, const int *b) { return abs(a[0] - b[0]) >= 4 || abs(a[1] - b[1]) >= 4; }
+
+/* one unit's edge in direction dir (0 vertical / left, 1 horizontal / top) at luma (x, y) */
+static int unit_bs(const int16_t *parts, int wc, int x, int y, int dir, const int32_t *ref_poc, int is_b) {
+  if (dir == 0 ? (x & 7) : (y & 7)) return 0;  /* only the 8x8 grid is read (xEdgeFilterLuma's iEdge step, :220) */
+  if (dir == 0 ? x == 0 : y == 0) return 0;    /* picture border: bLeftEdge / bTopEdge false (:372, :394) */
+  const int16_t *q = unit_part(parts, wc, x, y);
+  const int cs = 64 >> q[PF_DEPTH];
+  const int r = dir == 0 ? (x & 63) % cs : (y & 63) % cs;  /* position inside the CU along the edge normal */
+  /* xSetEdgefilterTU: every TU's left / top edge (the CU's own included, then kept by
+   * xSetEdgefilterPU's bLeftEdge / bTopEdge, true inside the picture with LFCrossSliceBoundaryFlag);
+   * these edges also carry the "transform edge" mark m_aapucBS tests against the cbfs */
+  const int tsz = cs >> q[PF_TR_IDX];
+  const int tu_edge = r % tsz == 0;
+  /* xSetEdgefilterPU: the internal PU edges of the partition (no transform mark) */
+  int pu_edge = 0;
+  switch (q[PF_PART]) {
+    case 1: pu_edge = dir == 1 && r == cs / 2; break;            /* SIZE_2NxN */
+    case 2: pu_edge = dir == 0 && r == cs / 2; break;            /* SIZE_Nx2N */
+    case 3: pu_edge = r == cs / 2; break;                        /* SIZE_NxN */
+    case 4: pu_edge = dir == 1 && r == cs / 4; break;            /* SIZE_2NxnU */
+    case 5: pu_edge = dir == 1 && r == cs - cs / 4; break;       /* SIZE_2NxnD */
+    case 6: pu_edge = dir == 0 && r == cs / 4; break;            /* SIZE_nLx2N */
+    case 7: pu_edge = dir == 0 && r == cs - cs / 4; break;       /* SIZE_nRx2N */
+    default: break;
+  }
+  if (!tu_edge && !pu_edge) return 0;
+  /* xGetBoundaryStrengthSingle (:417) */
+  const int16_t *p = dir == 0 ? unit_part(parts, wc, x - 4, y) : unit_part(parts, wc, x, y - 4);
+  if (p[PF_PRED] == 1 || q[PF_PRED] == 1) return 2;  /* MODE_INTRA */
+  const int cbf_q = (q[PF_CBF_Y] >> q[PF_TR_IDX]) & 1, cbf_p = (p[PF_CBF_Y] >> p[PF_TR_IDX]) & 1;
+  if (tu_edge && (cbf_q || cbf_p)) return 1;
+  int mp[2][2], mq[2][2];
+  int32_t rp[2], rq[2];
+  for (int l = 0; l < 2; l++) {
+    rp[l] = unit_ref(p, ref_poc, l);
+    rq[l] = unit_ref(q, ref_poc, l);
+    for (int c = 0; c < 2; c++) {
+      mp[l][c] = rp[l] == INT32_MIN ? 0 : p[PF_MV0X + 2 * l + c];
+      mq[l][c] = rq[l] == INT32_MIN ? 0 : q[PF_MV0X + 2 * l + c];
+    }
+  }
+  if (!is_b) return (rp[0] != rq[0] || mv_far(mq[0], mp[0])) ? 1 : 0;
+  if ((rp[0] == rq[0] && rp[1] == rq[1]) || (rp[0] == rq[1] && rp[1] == rq[0])) {
+    if (rp[0] != rp[1]) {
+      if (rp[0] == rq[0]) return (mv_far(mq[0], mp[0]) || mv_far(mq[1], mp[1])) ? 1 : 0;
+      return (mv_far(mq[1], mp[0]) || mv_far(mq[0], mp[1])) ? 1 : 0;
+    }
+    return ((mv_far(mq[0], mp[0]) || mv_far(mq[1], mp[1])) && (mv_far(mq[1], mp[0]) || mv_far(mq[0], mp[1]))) ? 1 : 0;
+  }
+  return 1;
+}
+
+void hvxo_hm_boundary_strength(int w, int h, const int16_t *hm_parts, const int32_t *ref_poc, int is_b,
+                               uint8_t *bs_ver, uint8_t *bs_hor, int8_t *qp) {
+  const int wc = (w + 63) / 64, uw = w / 4, uh = h / 4;
+  for (int uy = 0; uy < uh; uy++)
+    for (int ux = 0; ux < uw; ux++) {
+      const int x = ux * 4, y = uy * 4, i = uy * uw + ux;
+      bs_ver[i] = (uint8_t)unit_bs(hm_parts, wc, x, y, 0, ref_poc, is_b);
+      bs_hor[i] = (uint8_t)unit_bs(hm_parts, wc, x, y, 1, ref_poc, is_b);
+      qp[i] = (int8_t)unit_part(hm_parts, wc, x, y)[PF_QP];
+    }
+}
+
+void hvxo_hm_col_field(int w, int h, const int16_t *hm_parts, int16_t *col_field) {
+  const int wc = (w + 63) / 64, hc = (h + 63) / 64;
+  for (int a = 0; a < wc * hc; a++)
+    for (int b = 0; b < 16; b++) {  /* the 16x16 blocks in z-order (parts 0, 16, 32, ...) */
+      const int bx = (b & 1) | ((b >> 1) & 2), by = ((b >> 1) & 1) | ((b >> 2) & 2);
+      const int x = (a % wc) * 64 + bx * 16, y = (a / wc) * 64 + by * 16;
+      const int16_t *q = hm_parts + ((size_t)a * 256 + b * 16) * HVXO_HM_PART_FIELDS;
+      int16_t *o = col_field + ((size_t)a * 16 + b) * 8;
+      o[0] = (x >= w || y >= h) ? -1 : q[PF_PRED];  /* NUMBER_OF_PART_SIZES outside the picture */
+      o[1] = q[PF_REF0];
+      o[2] = q[PF_REF1];
+      for (int k = 0; k < 4; k++) o[3 + k] = q[PF_MV0X + k];
+      o[7] = 0;
+    }
+}

@@ -113,6 +113,21 @@ int hvxo_hm_chains_rd(const int32_t *pic_i32, const double *pic_f64, const uint8
                       int rd_metric, double lambda_ssim, int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon,
                       double *out_cost, uint32_t *out_bits_dist);
 
+/* The picture-level loop after compressSlice (TEncGOP.cpp:1465-1480) on a decided picture's CTU data
+ * (hm_parts = [n_ctus][256][HVXO_HM_PART_FIELDS], the cu_capture.cpp rows):
+ * hvxo_hm_boundary_strength: TComLoopFilter::loopFilterPic's per-4x4-unit boundary strengths of the
+ *   left (bs_ver) and top (bs_hor) edge, (w/4) x (h/4) raster, 0 off the 8x8 edge grid -- exactly the
+ *   m_aapucBS values xEdgeFilterLuma/Chroma read (xDeblockCU :170, xSetLoopfilterParam :362,
+ *   xSetEdgefilterTU :274, xSetEdgefilterPU :299, xGetBoundaryStrengthSingle :417), with
+ *   LFCrossSliceBoundaryFlag on and the deblocking filter enabled; qp = each unit's QpY (getQP).
+ *   ref_poc = the slice's [2][4] reference POCs (reference identity), is_b = B slice.
+ * hvxo_hm_col_field: TComPic::compressMotion (TComDataCU::compressMV, TComDataCU.cpp:3320): the
+ *   hvx_hm_picture.col_field rows [n_ctus][16][8] the next picture's TMVP reads -- per 16x16 block
+ *   its top-left 4x4 unit's {pred mode (-1 outside the picture), ref idx L0, L1, MV L0 x, y, L1 x, y, 0}. */
+void hvxo_hm_boundary_strength(int w, int h, const int16_t *hm_parts, const int32_t *ref_poc, int is_b,
+                               uint8_t *bs_ver, uint8_t *bs_hor, int8_t *qp);
+void hvxo_hm_col_field(int w, int h, const int16_t *hm_parts, int16_t *col_field);
+
 #ifdef __cplusplus
 }
 #endif

@@ -239,6 +239,50 @@ def compare(g, plan, out):
     return bad
 
 
+# deblocking captures of the same encodes as the CTU captures (oracle/deblock_capture.cpp,
+# oracle/gen_goldens.sh): per recorded POC the picture before / after loopFilterPic, the boundary
+# strengths it used and the QP map
+LOOP_CAPTURES = (("ctu_ldp_rand.bin", "dbk_ldp_rand.bin"), ("ctu_ldp_smooth.bin", "dbk_ldp_smooth.bin"),
+                 ("ctu_ra_q32.bin", "dbk_ra_q32.bin"))
+
+
+def loop_cases(ctu_name, dbk_name):
+    """Per recorded picture: dict(pic = index in the CTU capture, poc, w, h, params (hvx_deblock_params),
+    pre / post (Y, Cb, Cr), bs_ver / bs_hor / qp [h/4, w/4], ref_poc [2, 4], is_b, parts [nctu, 256, 29])."""
+    g, d = gc.load(ctu_name), gc.load(dbk_name)
+    out, po, pu = [], 0, 0
+    for i, poc in enumerate(d["poc"]):
+        w, h, beta, tc, cbo, cro, bypass = (int(v) for v in d["meta"][i])
+        n, nu = w * h * 3 // 2, (w // 4) * (h // 4)
+        pic = [k for k in range(g["pic_i32"].shape[0]) if int(g["pic_i32"][k][P_POC]) == int(poc)][0]
+        pi = g["pic_i32"][pic]
+        first, nctu = int(pi[P_FIRST_CTU]), int(pi[P_NCTU])
+        out.append({"pic": pic, "poc": int(poc), "w": w, "h": h,
+                    "params": _abi.deblock_params(w, h, beta, tc, cbo, cro),
+                    "pre": yuv_split(d["pre"][po:po + n], w, h), "post": yuv_split(d["post"][po:po + n], w, h),
+                    "bs_ver": d["bs_ver"][pu:pu + nu].reshape(h // 4, w // 4),
+                    "bs_hor": d["bs_hor"][pu:pu + nu].reshape(h // 4, w // 4),
+                    "qp": d["qp"][pu:pu + nu].reshape(h // 4, w // 4),
+                    "ref_poc": np.array([pi[P_REFPOC0:P_REFPOC0 + 4], pi[P_REFPOC1:P_REFPOC1 + 4]]),
+                    "is_b": int(pi[P_SLICE_TYPE]) == 0, "parts": g["ctu_parts"][first:first + nctu]})
+        po += n
+        pu += nu
+    return g, out
+
+
+def captured_col_fields(g):
+    """{poc of the collocated picture: its captured compressed motion field [nctu*16, 8]} for every
+    recorded picture that reads one (cu_capture.cpp col_field)."""
+    out, k = {}, 0
+    for pi in g["pic_i32"]:
+        if not int(pi[P_COL_VALID]):
+            continue
+        n = int(pi[P_NCTU])
+        out[int(pi[P_COL_POC])] = g["col_field"][k * n * 16:(k + 1) * n * 16]
+        k += 1
+    return out
+
+
 if __name__ == "__main__":  # debugging aid: python -m tests.hm_cases [mode]
     import sys
     mode = int(sys.argv[1]) if len(sys.argv) > 1 else 0

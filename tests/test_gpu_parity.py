@@ -398,3 +398,44 @@ def test_hm_compress_refuses_bad_jobs(torch):
     parts = hm.unpack_parts(out_ctu["p"][0:1])
     assert np.array_equal(parts[0], g["ctu_parts"][first + 5])
     assert not out_rec[1:6].any() and not out_ctu["coef"][1:6].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ctu_name,dbk_name", hm_cases.LOOP_CAPTURES)
+def test_hm_finish_picture_gpu(torch, ctu_name, dbk_name):
+    """The reference loop on the device: every picture of the capture decided by hvx_hm_compress
+    (chained), then hvx_hm_finish_picture -- boundary strengths + QP map derived from the engine's own
+    CTU data, loopFilterPic in place, compressMotion, the border-extended reference planes -- against
+    the same encode's loopFilterPic capture (BS maps, filtered picture), the restatement's field and the
+    padded planes the next picture would read: all bit-exact, for I, P and B pictures."""
+    from oracle import hm_ctu
+    from video_codecs_amd import hm
+    g, plan, out = hm_cases.run_capture(ctu_name, 1)
+    assert not hm_cases.compare(g, plan, out)
+    eng = hm_cases.LAST_ENGINE[0]
+    _, cases = hm_cases.loop_cases(ctu_name, dbk_name)
+    fields = hm_cases.captured_col_fields(g)
+    for c in cases:
+        w, h = c["w"], c["h"]
+        dp = eng.pictures[c["pic"]]
+        ref = hm.DeviceFrame.blank(w, h)
+        work, col = hm.finish_picture(dp, c["params"], col_field=True, ref_frame=ref)
+        torch.cuda.synchronize()
+        wk = work.cpu().numpy()
+        np.testing.assert_array_equal(wk[0], c["bs_ver"], err_msg="poc %d bs_ver" % c["poc"])
+        np.testing.assert_array_equal(wk[1], c["bs_hor"], err_msg="poc %d bs_hor" % c["poc"])
+        np.testing.assert_array_equal(wk[2].view(np.int8), c["qp"].astype(np.int8))
+        for k in range(3):
+            sh = 1 if k else 0
+            rec = dp.rec_t[k].cpu().numpy()[:h >> sh, :w >> sh]
+            np.testing.assert_array_equal(rec, c["post"][k], err_msg="poc %d plane %d" % (c["poc"], k))
+        want = hm_ctu.col_field(w, h, c["parts"])
+        np.testing.assert_array_equal(col.cpu().numpy(), want)
+        if c["poc"] in fields:
+            np.testing.assert_array_equal(col.cpu().numpy(), fields[c["poc"]])
+        y8, y16, cb16, cr16 = (t.cpu().numpy() for t in ref.planes())
+        m8 = hm.DeviceFrame.M8
+        np.testing.assert_array_equal(y8, np.pad(c["post"][0], m8, mode="edge"))
+        np.testing.assert_array_equal(y16, np.pad(c["post"][0], 80, mode="edge").astype(np.int16))
+        np.testing.assert_array_equal(cb16, np.pad(c["post"][1], 40, mode="edge").astype(np.int16))
+        np.testing.assert_array_equal(cr16, np.pad(c["post"][2], 40, mode="edge").astype(np.int16))

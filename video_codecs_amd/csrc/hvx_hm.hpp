@@ -1031,6 +1031,46 @@ struct RegCoder {
   }
 };
 
+// The bin counter of the coefficient walk with everything a bin touches in lane slices of four
+// VGPRs instead of LDS: the context states of rows 40..187 (the coefficient syntax's, 4 per dword:
+// dword k of the coder in lane k - kMemoDw0), the fractional-bit table E.eb (entry 2p + b in lane p
+// of eb[b]) and the transition table E.next (entries 4p..4p+3 in lane p).  A bin is then three
+// v_readlane's, scalar arithmetic and one lane select -- no dependent LDS round trips on the chain.
+struct RegWalk {
+  int stv, eb0, eb1, nx;
+  uint64_t frac;
+  __device__ __forceinline__ void load(const uint8_t *st) {
+    const int l = lid();
+    stv = l < kMemoDw ? (int)reinterpret_cast<const uint32_t *>(st)[kMemoDw0 + l] : 0;
+    eb0 = E.eb[2 * l];
+    eb1 = E.eb[2 * l + 1];
+    nx = (int)reinterpret_cast<const uint32_t *>(E.next)[l];
+    frac = 0;
+  }
+  __device__ __forceinline__ void store(uint8_t *st) const {
+    const int l = lid();
+    if (l < kMemoDw) reinterpret_cast<uint32_t *>(st)[kMemoDw0 + l] = (uint32_t)stv;
+  }
+  __device__ __forceinline__ void bin(int row, int v) {
+    const int a = __builtin_amdgcn_readfirstlane(row) + cab::kCtxLo;
+    v = __builtin_amdgcn_readfirstlane(v);
+    const int k = (a >> 2) - kMemoDw0, sh = (a & 3) * 8;
+    const uint32_t dw = (uint32_t)__builtin_amdgcn_readlane(stv, k);
+    const int s = (int)((dw >> sh) & 0xffu), p = s >> 1, mps = s & 1;
+    const int e0 = __builtin_amdgcn_readlane(eb0, p), e1 = __builtin_amdgcn_readlane(eb1, p);
+    frac += (uint32_t)((mps ^ v) ? e1 : e0);
+    const uint32_t ns = ((uint32_t)__builtin_amdgcn_readlane(nx, p) >> (8 * ((mps << 1) | v))) & 0xffu;
+    const int nd = (int)((dw & ~(0xffu << sh)) | (ns << sh));
+    stv = lid() == k ? nd : stv;  // v_writelane as a compare + select
+  }
+  __device__ __forceinline__ void ep(int n) { frac += 32768ull * (uint32_t)n; }
+  __device__ __forceinline__ void ep_bits(uint32_t, int n) { ep(n); }
+  __device__ __forceinline__ void eps(uint32_t, int n) { ep(n); }
+  __device__ __forceinline__ void esc(uint32_t symbol, int r, bool limited, int max_log2) {
+    ep(cab::remain_bins(symbol, r, limited, max_log2));
+  }
+};
+
 // the scan geometry of a TU (cab::ScanTables' values): the CG scan staged in LDS for every size;
 // raster positions and packed significance contexts staged in LDS up to 16x16, while a 32x32 TU
 // (big) reads its rasters from the constant scan table and derives the contexts per lane
@@ -1266,7 +1306,12 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
   L.store(E.cod[E.cur].st);
   E.cod[E.cur].frac += L.frac;
 #else
+#ifdef HM_REG_WALK
+  RegWalk L;
+  L.load(E.cod[E.cur].st);
+#else
   CoderLane L{E.cod[E.cur].st, 0};
+#endif
   wsync();
   HM_TADD(PR_COEF_STAGE, t_stage);
   HM_T0(t_walk);
@@ -1279,6 +1324,9 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
   // the mask-driven walk for every size (a third walk instance in this function measured 20%
   // slower overall: register pressure)
   coeff_count_staged(d, env, ls, L);
+#endif
+#ifdef HM_REG_WALK
+  L.store(E.cod[E.cur].st);
 #endif
   E.cod[E.cur].frac += L.frac;
 #endif

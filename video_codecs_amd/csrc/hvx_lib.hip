@@ -23,6 +23,7 @@
 #include "hvx_intra.hpp"
 #include "hvx_deblock.hpp"
 #include "hvx_sao.hpp"
+#include "hvx_hmloop.hpp"
 #include "hvx_host.hpp"
 #include "hvx_tables.hpp"
 
@@ -973,6 +974,62 @@ int hvx_plane_from_pel(hvx_ctx *ctx, const int16_t *d_pel, int pel_stride, int w
   int rc = launched("k_plane_from_pel");
   if (rc) return rc;
   return hvx_plane_extend(ctx, d_plane, width, height);
+}
+
+
+int hvx_hm_finish_picture(hvx_ctx *ctx, const hvx_hm_picture *h_pic, const hvx_deblock_params *h_dbk, uint8_t *d_work,
+                          int16_t *d_col_field, uint8_t *d_ref8, int ref8_stride, int16_t *d_ref16_y, int16_t *d_ref16_cb,
+                          int16_t *d_ref16_cr, int ref16_stride_y, int ref16_stride_c) {
+  if (!ctx || !h_pic) return fail(HVX_E_INVALID, "hvx_hm_finish_picture: NULL argument");
+  const hvx_hm_picture &P = *h_pic;
+  const int w = P.w, h = P.h;
+  if (w <= 0 || h <= 0 || w % 8 || h % 8 || P.w_ctus != (w + 63) / 64 || P.h_ctus != (h + 63) / 64 || !P.ctus ||
+      !P.rec[0] || !P.rec[1] || !P.rec[2] || P.rec_stride[0] < w || P.rec_stride[1] < w / 2)
+    return fail(HVX_E_INVALID, "hvx_hm_finish_picture: bad picture");
+  const bool ref16 = d_ref16_y || d_ref16_cb || d_ref16_cr;
+  if ((ref16 && !(d_ref16_y && d_ref16_cb && d_ref16_cr && ref16_stride_y >= w + 2 * 80 && ref16_stride_c >= w / 2 + 2 * 40)) ||
+      (d_ref8 && (ref8_stride < w + 2 * HVX_PLANE_MARGIN || ref8_stride % 4)))
+    return fail(HVX_E_INVALID, "hvx_hm_finish_picture: bad reference planes");
+  const int nctu = P.w_ctus * P.h_ctus;
+  if (h_dbk) {  // loopFilterPic (TEncGOP.cpp:1465)
+    if (!d_work || h_dbk->pic_w != w || h_dbk->pic_h != h) return fail(HVX_E_INVALID, "hvx_hm_finish_picture: bad deblocking args");
+    LfPic L{w, h, P.w_ctus, P.slice_type == 0 ? 1 : 0, {}};
+    for (int l = 0; l < 2; l++)
+      for (int i = 0; i < 4; i++) L.ref_poc[l][i] = P.ref_poc[l][i];
+    const size_t nu = (size_t)(w / 4) * (h / 4);
+    uint8_t *bv = d_work, *bh = d_work + nu;
+    int8_t *qp = (int8_t *)(d_work + 2 * nu);
+    hipLaunchKernelGGL(k_hm_lf_params, dim3((unsigned)((nu + 255) / 256)), dim3(256), 0, ctx->stream, P.ctus, L, bv, bh, qp);
+    int rc = launched("k_hm_lf_params");
+    if (rc) return rc;
+    rc = hvx_deblock(ctx, P.rec[0], P.rec_stride[0], P.rec[1], P.rec[2], P.rec_stride[1], bv, bh, qp, h_dbk);
+    if (rc) return rc;
+  }
+  if (d_col_field) {  // TComPic::compressMotion (TEncGOP.cpp:1629)
+    hipLaunchKernelGGL(k_hm_col_field, dim3((nctu * 16 + 255) / 256), dim3(256), 0, ctx->stream, P.ctus, w, h, P.w_ctus, nctu,
+                       d_col_field);
+    const int rc = launched("k_hm_col_field");
+    if (rc) return rc;
+  }
+  // the reference formats with extended borders (TComSlice::setRefPicList -> extendPicBorder, TComSlice.cpp:351)
+  if (d_ref8) {
+    const int m = HVX_PLANE_MARGIN;
+    hipLaunchKernelGGL(k_ref_plane<uint8_t>, dim3((w + 2 * m + 255) / 256, h + 2 * m), dim3(256), 0, ctx->stream,
+                       (const uint8_t *)P.rec[0], P.rec_stride[0], w, h, m, d_ref8, ref8_stride);
+    const int rc = launched("k_ref_plane");
+    if (rc) return rc;
+  }
+  if (ref16) {
+    int16_t *dst[3] = {d_ref16_y, d_ref16_cb, d_ref16_cr};
+    for (int c = 0; c < 3; c++) {
+      const int cw = c ? w / 2 : w, ch = c ? h / 2 : h, m = c ? 40 : 80;
+      hipLaunchKernelGGL(k_ref_plane<int16_t>, dim3((cw + 2 * m + 255) / 256, ch + 2 * m), dim3(256), 0, ctx->stream,
+                         (const uint8_t *)P.rec[c], P.rec_stride[c ? 1 : 0], cw, ch, m, dst[c], c ? ref16_stride_c : ref16_stride_y);
+      const int rc = launched("k_ref_plane");
+      if (rc) return rc;
+    }
+  }
+  return HVX_OK;
 }
 
 }  // extern "C"

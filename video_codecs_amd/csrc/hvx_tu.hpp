@@ -363,14 +363,26 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
 #define HVX_RDOQ_PHASE(k) ((void)0)
 #endif
   // ---- A. per-coefficient work across lanes ----
+  bool anyq = false;
   for (int sp = lane; sp < NN; sp += HVX_WAVE) {
     const int blk = c.scan[sp];
-    if (arl_out) arl_out[blk] = d.adaptive_qp_select ? (rd_level_double(s.coef[blk], qc, lim) + add_c) >> qbits_c : 0;
+    const int32_t ld = rd_level_double(s.coef[blk], qc, lim);
+    if (arl_out) arl_out[blk] = d.adaptive_qp_select ? (ld + add_c) >> qbits_c : 0;
+    anyq |= ((ld + (1 << (qbits - 1))) >> qbits) > 0;
     int info = 0;
 #pragma unroll
     for (int pat = 0; pat < 4; pat++) info |= (sig_off + rd_sig_ctx<L>(pat, c, sp, ch)) << (6 * pat);
     st[sp] = info;
   }
+  // every rounded level 0: the decisions all keep level 0 (no last position, nothing to hide), so
+  // the reverse scan would only price them -- its outputs are all-zero levels and uiAbsSum 0
+#ifndef HVX_RDOQ_NO_ZERO_EXIT
+  if (__ballot(anyq) == 0) {
+    for (int i = lane; i < NN; i += HVX_WAVE) s.lev[i] = 0;
+    __syncthreads();
+    return 0;
+  }
+#endif
   // estBits in lane slices: entry [ctx][0] in lane ctx, [ctx][1] in lane 32 + ctx (or own VGPR)
   const int t_sb0 = lane < 44 ? est->significantBits[lane][0] : 0;
   const int t_sb1 = lane < 44 ? est->significantBits[lane][1] : 0;

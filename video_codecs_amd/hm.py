@@ -163,6 +163,32 @@ class DeviceFrame:
             self.ref16_stride[1 if c else 0] = int(p16.shape[1])
 
 
+    @classmethod
+    def blank(cls, w, h, device="cuda"):
+        """A reference frame's padded device planes, uninitialised: filled on the device by
+        finish_picture (hvx_hm_finish_picture) from a decided picture; no original planes."""
+        import torch
+        self = cls.__new__(cls)
+        self.org = None
+        y8 = torch.empty((h + 2 * cls.M8, w + 2 * cls.M8), dtype=torch.uint8, device=device)
+        self.keep = [y8]
+        self.ref8 = y8.data_ptr() + (cls.M8 * y8.shape[1] + cls.M8)
+        self.ref8_stride = int(y8.shape[1])
+        self.ref16, self.ref16_stride = [], [0, 0]
+        for c in range(3):
+            m = cls.M16 if c == 0 else cls.M16C
+            cw, ch = (w, h) if c == 0 else (w // 2, h // 2)
+            p16 = torch.empty((ch + 2 * m, cw + 2 * m), dtype=torch.int16, device=device)
+            self.keep.append(p16)
+            self.ref16.append(p16.data_ptr() + 2 * (m * p16.shape[1] + m))
+            self.ref16_stride[1 if c else 0] = int(p16.shape[1])
+        return self
+
+    def planes(self):
+        """(y8 padded, y16, cb16, cr16 padded) device tensors (reference frames)."""
+        return tuple(self.keep[:4])
+
+
 class DevicePicture:
     """One picture's device-side description (hvx_hm_picture) and the buffers it points at.
 
@@ -344,3 +370,28 @@ class Engine:
         self.last_prof = st[:, 16:528].copy().view(np.uint64).reshape(n, 2, 32)  # State.prof (HM_PROFILE builds)
         return (out_ctu.cpu().numpy().view(HM_CTU), out_rec.cpu().numpy().reshape(n_out, 6144),
                 out_cod.cpu().numpy().view(HM_CODER))
+
+
+def finish_picture(pic, dbk_params=None, col_field=False, ref_frame=None):
+    """hvx_hm_finish_picture on a decided DevicePicture (its ctus / rec complete), enqueued on
+    torch's current stream: deblocking in place with device-derived boundary strengths when
+    dbk_params (hvx_deblock_params) is given, the compressed motion field when col_field, the
+    reference planes into ref_frame (DeviceFrame.blank) when given.  Returns (work, col): the
+    [3, h/4, w/4] uint8 BS-ver / BS-hor / QP maps (or None) and the [nctu*16, 8] int16 field (or None)."""
+    import torch
+    from . import hvx
+    P = ctypes.c_void_p
+    w, h = pic.w, pic.h
+    dev = pic.ctus_t.device
+    work = torch.empty((3, h // 4, w // 4), dtype=torch.uint8, device=dev) if dbk_params is not None else None
+    col = torch.empty((pic.wc * pic.hc * 16, 8), dtype=torch.int16, device=dev) if col_field else None
+    r8, r16, s8, s16 = P(0), [P(0)] * 3, 0, (0, 0)
+    if ref_frame is not None:
+        r8, s8 = P(ref_frame.ref8), ref_frame.ref8_stride
+        r16, s16 = [P(a) for a in ref_frame.ref16], ref_frame.ref16_stride
+    dp = np.ascontiguousarray(dbk_params) if dbk_params is not None else None
+    hvx._check(hvx.lib().hvx_hm_finish_picture(
+        hvx.context(), ctypes.byref(pic.struct), dp.ctypes.data_as(P) if dp is not None else P(0),
+        P(work.data_ptr() if work is not None else 0), P(col.data_ptr() if col is not None else 0),
+        r8, s8, r16[0], r16[1], r16[2], s16[0], s16[1]), "hvx_hm_finish_picture")
+    return work, col
