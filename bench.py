@@ -176,25 +176,82 @@ def synthetic_col_field(nctu, seed):
     return f
 
 
-class HmWorkload:
-    """The headline workload on one GPU: `pics` P pictures of W x H random 4:2:0 YUV, picture p
-    (POC nref + p) predicted from the nref previous frames, every CTU row a SliceMode=1 slice
-    decided by one chain (one wave) -- a partial bottom row continues the chain of the row above
-    it (HVX_HM_SLICE_CTUS) -- with the slice parameters of GOP position 2 of the LDP GOP
-    (hm.slice_params).  Step k advances every chain by `ctus` CTUs from where step k-1 left it
-    (HVX_HM_RESUME); a chain that reaches its row's end starts the row again as a new slice."""
+class HmPlan:
+    """The headline workload's host-side plan (no device): `pics` P pictures of W x H random 4:2:0
+    YUV per rank, picture p (POC nref + p) predicted from the nref previous frames of the rank's own
+    frame range (frames base .. base + nref + pics - 1, base = 1000 + rank * (pics + nref): disjoint
+    across ranks), every CTU row a SliceMode=1 slice decided by one chain -- a partial
+    bottom row continues the chain of the row above it (HVX_HM_SLICE_CTUS) -- with the slice
+    parameters of GOP position 2 of the LDP GOP (hm.slice_params)."""
 
     def __init__(self, W, H, pics, nref, base_qp, ctus, rank, col=True):
-        import torch
-        from video_codecs_amd import _abi, hm, synth
+        from video_codecs_amd import _abi, hm
         self.W, self.H, self.pics, self.nref, self.ctus, self.col = W, H, pics, nref, ctus, col
         self.wc, self.hc = (W + 63) // 64, (H + 63) // 64
         assert self.wc % ctus == 0, "--ctus must divide the CTUs per row"
         self.qp = base_qp + HM_QP_OFFSET
         self.base = rank * (pics + nref) + 1000
         self.params = hm.slice_params(1, self.qp, HM_QP_FACTOR)
-        eb = _abi.load_entropy_bits()
         self.entry = _abi.load_ctx_init_states()[1, self.qp]
+        # the chains of a picture: one per CTU row slice, except that a partial bottom row (2160 =
+        # 33 x 64 + 48) is chained after the row above it -- its first CTU is a picture-boundary CTU
+        # whose searches read TEncSearch::m_integerMv2Nx2N as the row above's last CTU left it
+        # (HVX_HM_SLICE_CTUS: the coder restarts at the slice, the search state carries on)
+        self.merge_last = H % 64 != 0 and self.hc >= 2
+        self.rows = self.hc - 1 if self.merge_last else self.hc
+        self.n_jobs = pics * self.rows
+        self.slots = self.n_jobs * ctus
+
+    def frames(self):
+        """The synthetic frame indices this rank reads (references and current pictures)."""
+        return list(range(self.base, self.base + self.nref + self.pics))
+
+    def col_field(self, p):
+        return synthetic_col_field(self.wc * self.hc, self.base + p) if self.col else None
+
+    def picture_params(self, p):
+        poc, nref = self.nref + p, self.nref
+        q = dict(self.params)
+        q.update(poc=poc, nref=[nref, 0], ref_poc=np.array([[poc - 1 - k for k in range(4)], [0] * 4]),
+                 ref_plane=np.array([list(range(nref)) + [0] * (4 - nref), [0] * 4]), max_merge=5, tmvp=1, check_ldc=1,
+                 col_from_l0=1, col_valid=int(self.col), col_poc=poc - 1,
+                 col_ref_poc=np.array([[poc - 2 - k for k in range(4)], [0] * 4]), search_range=64, amp=1)
+        return q
+
+    def host_inputs(self, p):
+        """Picture p's arrays in the oracle's (cu_capture.cpp) layout: pic_i32, pic_f64, org,
+        reference frames, collocated field."""
+        from video_codecs_amd import synth
+        prm = self.picture_params(p)
+        pi = np.zeros(46, np.int32)
+        pi[0:7] = [self.W, self.H, prm["poc"], 1, self.qp, self.nref, 0]
+        pi[7:11] = prm["ref_poc"][0]
+        pi[15:19] = prm["ref_plane"][0]
+        pi[19:23] = -1
+        pi[23:29] = [1, 0, 1, 1, 5, prm["col_poc"]]
+        pi[29:31] = [4, 0]
+        pi[31:35] = prm["col_ref_poc"][0]
+        pi[39:41] = prm["chroma_qp"]
+        pi[41:43] = [0, self.wc * self.hc]
+        pi[43] = np.array(prm["lambda_motion"], np.uint32).view(np.int32)
+        pi[45] = int(self.col)
+        pf = np.array([prm["lambda"], prm["sqrt_lambda"], *prm["chroma_weight"], *prm["tq_lambda"]], np.float64)
+        org = synth.random_frame(self.W, self.H, self.base + self.nref + p)
+        refs = np.concatenate([synth.random_frame(self.W, self.H, self.base + self.nref + p - 1 - k)
+                               for k in range(self.nref)])
+        return pi, pf, org, refs, self.col_field(p)
+
+
+class HmWorkload(HmPlan):
+    """The headline workload on one GPU (HmPlan's pictures and chains, resident in HBM).  Step k
+    advances every chain by `ctus` CTUs from where step k-1 left it (HVX_HM_RESUME); a chain that
+    reaches its row's end starts the row again as a new slice."""
+
+    def __init__(self, W, H, pics, nref, base_qp, ctus, rank, col=True):
+        import torch
+        from video_codecs_amd import _abi, hm, synth
+        super().__init__(W, H, pics, nref, base_qp, ctus, rank, col)
+        eb = _abi.load_entropy_bits()
         from concurrent.futures import ThreadPoolExecutor
         with ThreadPoolExecutor(8) as ex:
             host = list(ex.map(lambda i: synth.random_frame(W, H, self.base + i), range(nref + pics)))
@@ -208,15 +265,7 @@ class HmWorkload:
         self.eng = hm.Engine(self.pictures)
         self.stream = torch.cuda.Stream()
         torch.cuda.synchronize()  # inputs resident before any launch on the workload's stream
-        # the chains of a picture: one per CTU row slice, except that a partial bottom row (2160 =
-        # 33 x 64 + 48) is chained after the row above it -- its first CTU is a picture-boundary CTU
-        # whose searches read TEncSearch::m_integerMv2Nx2N as the row above's last CTU left it
-        # (HVX_HM_SLICE_CTUS: the coder restarts at the slice, the search state carries on)
-        self.merge_last = H % 64 != 0 and self.hc >= 2
-        self.rows = self.hc - 1 if self.merge_last else self.hc
-        self.n_jobs = pics * self.rows
         self.eng.reserve(self.n_jobs)
-        self.slots = self.n_jobs * ctus
         # one device job array per step position (the step's first CTU of every chain); the period
         # is two rows when the last chain spans two
         self.phase_jobs = []
@@ -244,18 +293,6 @@ class HmWorkload:
         self.keep_steps = []
         self.keep_n = self.rows * ctus
 
-    def col_field(self, p):
-        return synthetic_col_field(self.wc * self.hc, self.base + p) if self.col else None
-
-    def picture_params(self, p):
-        poc, nref = self.nref + p, self.nref
-        q = dict(self.params)
-        q.update(poc=poc, nref=[nref, 0], ref_poc=np.array([[poc - 1 - k for k in range(4)], [0] * 4]),
-                 ref_plane=np.array([list(range(nref)) + [0] * (4 - nref), [0] * 4]), max_merge=5, tmvp=1, check_ldc=1,
-                 col_from_l0=1, col_valid=int(self.col), col_poc=poc - 1,
-                 col_ref_poc=np.array([[poc - 2 - k for k in range(4)], [0] * 4]), search_range=64, amp=1)
-        return q
-
     def step(self, out_rec, events=None):
         """One launch: every chain advances `ctus` CTUs; reconstructed CTUs go to out_rec.  The
         launch, its HIP events and the copies of its records are ordered on the workload's own
@@ -271,29 +308,6 @@ class HmWorkload:
             self.keep_steps.append((pos * self.ctus, self.out_ctu[:self.keep_n * 22544].clone(),
                                     out_rec[:self.keep_n * 6144].clone()))
         self.step_idx += 1
-
-    def host_inputs(self, p):
-        """Picture p's arrays in the oracle's (cu_capture.cpp) layout: pic_i32, pic_f64, org,
-        reference frames, collocated field."""
-        from video_codecs_amd import synth
-        prm = self.picture_params(p)
-        pi = np.zeros(46, np.int32)
-        pi[0:7] = [self.W, self.H, prm["poc"], 1, self.qp, self.nref, 0]
-        pi[7:11] = prm["ref_poc"][0]
-        pi[15:19] = prm["ref_plane"][0]
-        pi[19:23] = -1
-        pi[23:29] = [1, 0, 1, 1, 5, prm["col_poc"]]
-        pi[29:31] = [4, 0]
-        pi[31:35] = prm["col_ref_poc"][0]
-        pi[39:41] = prm["chroma_qp"]
-        pi[41:43] = [0, self.wc * self.hc]
-        pi[43] = np.array(prm["lambda_motion"], np.uint32).view(np.int32)
-        pi[45] = int(self.col)
-        pf = np.array([prm["lambda"], prm["sqrt_lambda"], *prm["chroma_weight"], *prm["tq_lambda"]], np.float64)
-        org = synth.random_frame(self.W, self.H, self.base + self.nref + p)
-        refs = np.concatenate([synth.random_frame(self.W, self.H, self.base + self.nref + p - 1 - k)
-                               for k in range(self.nref)])
-        return pi, pf, org, refs, self.col_field(p)
 
 
 def _chain_jobs(specs, entry):

@@ -142,3 +142,76 @@ def test_two_rank_dpb_gather_gloo(tmp_path):
         np.testing.assert_array_equal(own, exp)
         assert int(np.load(tmp_path / f"t{r}.npy")[1]) == STEPS + WARMUP
     assert not np.array_equal(dpb[0], dpb[1])
+
+
+# ---- the headline's orchestration (bench.HmPlan / HmWorkload) with the HM-exact restatement ----
+HW, HH, HPICS, HNREF = 128, 112, 2, 2  # 2 x 2 CTUs: one chain per picture over both row slices
+
+
+def _hm_step(plan):
+    """One bench step with every chain run to its end on the CPU restatement (hvxo_hm_chains): the
+    reconstructed CTUs of every picture's chains in the bench's DPB slot order (chain k of picture
+    p -> slots (p * rows + k) * per_chain ...)."""
+    from oracle import hm_ctu
+    per_chain = plan.wc * (2 if plan.merge_last else 1)
+    out = np.zeros((plan.n_jobs * per_chain, 6144), np.uint8)
+    for p in range(plan.pics):
+        pi, pf, org, refs, col = plan.host_inputs(p)
+        first = np.arange(plan.rows, dtype=np.int32) * plan.wc
+        r = hm_ctu.chains(pi, pf, org, refs, plan.entry, first, per_chain, plan.wc, threads=1, col_field=col)
+        out[p * plan.rows * per_chain:(p + 1) * plan.rows * per_chain] = r["recon"]
+    return out
+
+
+def _hm_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from video_codecs_amd.dpb import DpbGather
+    plan = bench.HmPlan(HW, HH, HPICS, HNREF, QP, (HW + 63) // 64, rank)
+    per_chain = plan.wc * (2 if plan.merge_last else 1)
+    g = DpbGather(world, rank, (plan.n_jobs * per_chain * 6144,), "cpu")
+
+    def step():  # bench.main's step: decide into the DPB buffer, then the asynchronous gather
+        g.buffer().numpy()[:] = _hm_step(plan).reshape(-1)
+        g.send()
+
+    elapsed = bench.timed_steps(step, STEPS - 1, WARMUP, world, "cpu", g.drain)
+    units = plan.n_jobs * per_chain
+    value = bench.aggregate(units, STEPS - 1, world, elapsed)
+    own, gathered = g.last()
+    np.save(os.path.join(outdir, f"own{rank}.npy"), own.numpy())
+    if rank == 0:
+        np.save(os.path.join(outdir, "dpb.npy"), np.stack([t.numpy() for t in gathered]))
+    np.save(os.path.join(outdir, f"meta{rank}.npy"), np.array([elapsed, value, units, g.k] + plan.frames(), np.float64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_hm_workload_gloo(tmp_path):
+    """bench.py's headline orchestration on two ranks (gloo): each rank decides its own pictures
+    (disjoint synthetic frame ranges, HmPlan), chained across the partial bottom row's slice as the
+    GPU chains are, through the HM-exact restatement; the per-step DPB gather leaves every rank's
+    reconstructed CTUs on rank 0, identical to that rank's own buffer and to a single-process run of
+    its plan; the timed region ends with the same max-over-ranks time on both ranks and the
+    whole-job value counts the CTUs of both."""
+    import torch.multiprocessing as tmp
+    import bench
+    world = 2
+    tmp.spawn(_hm_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    metas = [np.load(tmp_path / f"meta{r}.npy") for r in range(world)]
+    assert metas[0][0] == metas[1][0]  # max over ranks
+    units = int(metas[0][2])
+    assert units == HPICS * 4
+    assert metas[0][1] == pytest.approx(units * (STEPS - 1) * world / metas[0][0])
+    frames = [set(int(f) for f in m[4:]) for m in metas]
+    assert len(frames[0]) == len(frames[1]) == HPICS + HNREF and not frames[0] & frames[1]
+    dpb = np.load(tmp_path / "dpb.npy")
+    for r in range(world):
+        own = np.load(tmp_path / f"own{r}.npy")
+        assert int(metas[r][3]) == STEPS  # pictures sent: warmup + timed
+        np.testing.assert_array_equal(dpb[r], own)
+        exp = _hm_step(bench.HmPlan(HW, HH, HPICS, HNREF, QP, (HW + 63) // 64, r))
+        np.testing.assert_array_equal(own.reshape(-1, 6144), exp)
+    assert not np.array_equal(dpb[0], dpb[1])
