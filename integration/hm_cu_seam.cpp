@@ -93,12 +93,18 @@ struct RefPlanes {
 };
 
 struct CuSeam {
-  int enabled = -1;
-  long long served = 0, fallback = 0, pictures = 0;
+  int enabled = -1, batch = -1;
+  long long served = 0, fallback = 0, pictures = 0, batched = 0, launches = 0, state_mismatch = 0;
   int cur_poc = -1000000;
   bool cur_ok = false;
   int w = 0, h = 0, wc = 0, hc = 0;
-  DevBuf org[3], rec[3], ctus, col, eb, pic, job, state, out_ctu, out_rec;
+  DevBuf org[3], rec[3], ctus, col, eb, pic, job, state, out_ctu, out_rec, out_cod;
+  // batched mode: every chain of the picture decided by one launch at its first compressCtu call
+  bool pic_batched = false;
+  std::vector<hvx_hm_ctu> b_ctu;
+  std::vector<uint8_t> b_rec;
+  std::vector<hvx_hm_coder> b_cod;
+  std::vector<uint8_t> slice_first;  // per CTU: a slice starts here (the entry state is resetEntropy's)
   std::vector<RefPlanes> refs = std::vector<RefPlanes>(8);
   hvx_hm_picture P;
   std::vector<uint8_t> stage;
@@ -106,11 +112,18 @@ struct CuSeam {
     if (enabled == 1)
       fprintf(stderr, "hm_cu_seam: %lld compressCtu calls served by libhvx (%lld pictures), %lld fell through\n", served,
               pictures, fallback);
+    if (enabled == 1 && batch == 1)
+      fprintf(stderr, "hm_cu_seam batched: %lld CTUs from %lld launches, %lld entry-state mismatches\n", batched, launches,
+              state_mismatch);
   }
   bool on() {
     if (enabled < 0) {
       const char *e = getenv("HVX_SEAM_CU");
       enabled = (e && e[0] == '1') ? 1 : 0;
+    }
+    if (batch < 0) {
+      const char *e = getenv("HVX_SEAM_CU_BATCH");
+      batch = (e && e[0] == '1') ? 1 : 0;
     }
     return enabled == 1;
   }
@@ -371,6 +384,79 @@ void write_rec(TComDataCU *ctu, const uint8_t *w) {
       for (int x = 0; x < cs && x0 + x < pw; x++) a[(y0 + y) * s + x0 + x] = src[y * cs + x];
   }
 }
+
+// The throughput form of the seam (HVX_SEAM_CU_BATCH=1): at a picture's first compressCtu call
+// every slice of the picture is decided in ONE launch, one chain per slice (TEncSlice::
+// compressSlice's CTU loop, TEncSlice.cpp:727-897, for all slices at once), the chains' outputs
+// kept for the following calls.  A slice whose first CTU is a picture-boundary CTU (it reads
+// TEncSearch::m_integerMv2Nx2N as the previous CTU left it) runs in the previous slice's chain
+// (HVX_HM_SLICE_CTUS).  Every slice starts from the same resetEntropy state (one slice type and
+// QP per picture): the entry state of the picture's first CTU.  Only SliceMode 0 / 1 (whole
+// CTUs) pictures batch.
+bool batch_picture(TEncCu *self, TComDataCU *ctu) {
+  TComSlice *s = ctu->getSlice();
+  const int n = g.wc * g.hc;
+  const int mode = s->getSliceMode();
+  if (ctu->getCtuRsAddr() != 0 || (mode != 0 && mode != 1) || s->getSliceSegmentMode() != 0) return false;
+  const int S = mode == 0 ? n : (int)s->getSliceArgument();
+  if (S <= 0) return false;
+  auto boundary = [&](int a) { return ((a % g.wc) + 1) * 64 > g.w || ((a / g.wc) + 1) * 64 > g.h; };
+  std::vector<hvx_hm_job> jobs;
+  hvx_hm_job j;
+  memset(&j, 0, sizeof(j));
+  TEncSbac *sb = self->m_pppcRDSbacCoder[0][CI_CURR_BEST];
+  for (int i = 0; i < HVX_NUM_CTX; i++) j.entry.st[i] = i < (int)sb->m_numContextModels ? sb->m_contextModels[i].m_ucState : 0;
+  j.entry.frac = ((TEncBinCABAC *)sb->m_pcBinIf)->m_fracBits;
+  for (int l = 0; l < 2; l++)
+    for (int i = 0; i < 4; i++) {
+      j.int2n[(l * 4 + i) * 2] = (int16_t)self->m_pcPredSearch->m_integerMv2Nx2N[l][i].getHor();
+      j.int2n[(l * 4 + i) * 2 + 1] = (int16_t)self->m_pcPredSearch->m_integerMv2Nx2N[l][i].getVer();
+    }
+  j.chained = 1;
+  g.slice_first.assign(n, 0);
+  for (int a0 = 0; a0 < n; a0 += S) {
+    const int a1 = std::min(a0 + S, n) - 1;
+    g.slice_first[a0] = 1;
+    if (a0 > 0 && boundary(a0)) {  // continue the previous chain into this slice
+      hvx_hm_job &p = jobs.back();
+      p.n_ctus = a1 - p.first_ctu + 1;
+      p.flags = HVX_HM_SLICE_CTUS(S);
+      continue;
+    }
+    j.first_ctu = a0;
+    j.n_ctus = a1 - a0 + 1;
+    j.out = a0;  // output slot = CTU address
+    j.slice_start = a0;
+    j.slice_end = a1;
+    j.flags = 0;
+    jobs.push_back(j);
+  }
+  hvx_ctx *c = hvx_seam_ctx();
+  size_t sb_bytes = 0;
+  check(hvx_hm_state_size(&sb_bytes), "hvx_hm_state_size");
+  g.state.get(sb_bytes * jobs.size());
+  g.job.get(sizeof(hvx_hm_job) * jobs.size());
+  g.out_ctu.get(sizeof(hvx_hm_ctu) * n);
+  g.out_rec.get((size_t)6144 * n);
+  g.out_cod.get(sizeof(hvx_hm_coder) * n);
+  upload(g.job.p, jobs.data(), sizeof(hvx_hm_job) * jobs.size());
+  check(hvx_hm_compress(c, (const hvx_hm_picture *)g.pic.p, 1, (const hvx_hm_job *)g.job.p, (int)jobs.size(), n, g.state.p,
+                        (hvx_hm_ctu *)g.out_ctu.p, (uint8_t *)g.out_rec.p, (hvx_hm_coder *)g.out_cod.p),
+        "hvx_hm_compress");
+  std::vector<int32_t> st(jobs.size());
+  check(hvx_hm_job_status(c, g.state.p, (int)jobs.size(), st.data()), "hvx_hm_job_status");
+  for (size_t k = 0; k < st.size(); k++)
+    if (st[k]) { fprintf(stderr, "hm_cu_seam: batched job %zu refused (%d)\n", k, st[k]); abort(); }
+  g.b_ctu.resize(n);
+  g.b_rec.resize((size_t)6144 * n);
+  g.b_cod.resize(n);
+  check(hvx_download(c, g.b_ctu.data(), g.out_ctu.p, sizeof(hvx_hm_ctu) * n), "hvx_download");
+  check(hvx_download(c, g.b_rec.data(), g.out_rec.p, (size_t)6144 * n), "hvx_download");
+  check(hvx_download(c, g.b_cod.data(), g.out_cod.p, sizeof(hvx_hm_coder) * n), "hvx_download");
+  check(hvx_sync(c), "hvx_sync");
+  g.launches++;
+  return true;
+}
 }  // namespace
 
 extern "C" void CAT(__wrap_, CU_SYM)(TEncCu *self, TComDataCU *ctu) {
@@ -382,10 +468,28 @@ extern "C" void CAT(__wrap_, CU_SYM)(TEncCu *self, TComDataCU *ctu) {
   if (poc != g.cur_poc) {
     g.cur_poc = poc;
     g.cur_ok = begin_picture(self, ctu);
+    g.pic_batched = g.cur_ok && g.batch == 1 && batch_picture(self, ctu);
   }
   if (!g.cur_ok) {
     g.fallback++;
     CAT(__real_, CU_SYM)(self, ctu);
+    return;
+  }
+  if (g.pic_batched) {
+    const int a = ctu->getCtuRsAddr();
+    // the entry coder HM holds now must be the one the device chain carried into this CTU (the
+    // previous CTU's encodeCtu state), except at slice starts (resetEntropy)
+    if (a > 0 && !g.slice_first[a]) {
+      TEncSbac *sb = self->m_pppcRDSbacCoder[0][CI_CURR_BEST];
+      bool same = ((TEncBinCABAC *)sb->m_pcBinIf)->m_fracBits == g.b_cod[a - 1].frac;
+      for (int i = 0; i < (int)sb->m_numContextModels && i < HVX_NUM_CTX; i++)
+        same = same && sb->m_contextModels[i].m_ucState == g.b_cod[a - 1].st[i];
+      if (!same) g.state_mismatch++;
+    }
+    write_ctu(ctu, g.b_ctu[a]);
+    write_rec(ctu, &g.b_rec[(size_t)6144 * a]);
+    g.served++;
+    g.batched++;
     return;
   }
   hvx_ctx *c = hvx_seam_ctx();

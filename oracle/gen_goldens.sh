@@ -107,6 +107,10 @@ for spec in 22:8,4,1,3 27:8,3 32:8,1 37:4,3; do
     -i "$TMP/tex9.yuv" -wdt 416 -hgt 240 -fr 30 -f 9 -q $q -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
   python3 oracle/compact_ctu.py "$TMP/cu.bin" tests/golden/ctu_ra_q$q.bin
 done
+# a closed reference loop (SAO off: each reference is the deblocked reconstruction)
+HVX_CAPTURE="$TMP/cu.bin" $ORC/TAppEncoder_cucap -c $CFG/encoder_lowdelay_P_main.cfg -i "$TMP/smooth4.yuv" -wdt 416 -hgt 240 \
+  -fr 30 -f 3 -q 27 --SAO=0 -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+python3 oracle/compact_ctu.py "$TMP/cu.bin" tests/golden/ctu_ldp_nosao.bin
 # the reference loop on the same encodes: loopFilterPic's BS / QP maps and pictures per recorded POC
 dbk() {  # dbk <out.bin> <pocs> <cfg> <yuv> <frames> <qp>
   HVX_CAPTURE_POCS=$2 HVX_CAPTURE=$1 $ORC/TAppEncoder_dbkcap -c "$3" -i "$4" -wdt 416 -hgt 240 -fr 30 -f "$5" -q "$6" \

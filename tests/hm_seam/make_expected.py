@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 from oracle import make_yuv  # noqa: E402
 
-CASES = {  # name: (cfg, yuv kind, frames, qp)
+CASES = {  # name: (cfg, yuv kind, frames, qp[, width, height, extra encoder args])
     "intra_rand_qp32": ("intra.cfg", "random", 1, 32),
     "intra_smooth_qp22": ("intra.cfg", "smooth", 1, 22),
     "ldp_smooth_qp32": ("ldp.cfg", "smooth", 3, 32),
@@ -20,25 +20,35 @@ CASES = {  # name: (cfg, yuv kind, frames, qp)
     "ldp_rand_qp32": ("ldp.cfg", "random", 2, 32),    # uniform random: long TZ raster searches
     "ra_smooth_qp27": ("ra.cfg", "smooth", 9, 27),    # GOP8 hierarchical B: future refs, bBi refinement
     "ra_texture_qp32": ("ra.cfg", "texture", 9, 32),  # textured content in motion: uni-L0 / uni-L1 / bi AMVP choices
+    # BASELINE configs 2/3 size: 1080p, CTU-row slices (the throughput seam's chains; the partial
+    # bottom row continues the chain of the row above)
+    "ldp_smooth_1080p_qp32": ("ldp.cfg", "smooth", 2, 32, 1920, 1080, ["--SliceMode=1", "--SliceArgument=30"]),
 }
 YUV_FRAMES = max(c[2] for c in CASES.values())
 W, H = 416, 240
 
 
+def case_size(case):
+    c = CASES[case]
+    return (c[4], c[5]) if len(c) > 4 else (W, H)
+
+
 def encode(binary, case, tmp, log=None):
     """Encode `case` with `binary`; the encoder's stderr (the seams' call counters) is appended
     to the list `log` when given."""
-    cfg, kind, frames, qp = CASES[case]
-    yuv = os.path.join(tmp, f"{kind}.yuv")
+    cfg, kind, frames, qp = CASES[case][:4]
+    extra = CASES[case][6] if len(CASES[case]) > 6 else []
+    w, h = case_size(case)
+    yuv = os.path.join(tmp, f"{kind}_{w}x{h}.yuv")
     if not os.path.exists(yuv):
-        make_yuv.write_yuv(yuv, kind, W, H, YUV_FRAMES)
+        make_yuv.write_yuv(yuv, kind, w, h, YUV_FRAMES if (w, h) == (W, H) else frames)
     bs, rec = os.path.join(tmp, case + ".bin"), os.path.join(tmp, case + ".rec.yuv")
     # the encoder's per-picture lines go to HVX_SEAM_LOG_DIR/<case>.log when set (progress of a long run)
     log_dir = os.environ.get("HVX_SEAM_LOG_DIR")
     out = open(os.path.join(log_dir, case + ".log"), "w") if log_dir else subprocess.DEVNULL
     try:
-        p = subprocess.run([binary, "-c", os.path.join(HERE, cfg), "-i", yuv, "-wdt", str(W), "-hgt", str(H), "-fr",
-                            "30", "-f", str(frames), "-q", str(qp), "-b", bs, "-o", rec],
+        p = subprocess.run([binary, "-c", os.path.join(HERE, cfg), "-i", yuv, "-wdt", str(w), "-hgt", str(h), "-fr",
+                            "30", "-f", str(frames), "-q", str(qp), "-b", bs, "-o", rec] + list(extra),
                            stdout=out, stderr=subprocess.PIPE, text=True)
     finally:
         if log_dir:
@@ -53,7 +63,11 @@ def encode(binary, case, tmp, log=None):
 
 if __name__ == "__main__":
     exe = os.path.join(ROOT, "oracle", "_ref", "TAppEncoder")
+    path = os.path.join(HERE, "expected_md5.json")
+    res = json.load(open(path)) if os.path.exists(path) else {}
+    todo = sys.argv[1:] or list(CASES)
     with tempfile.TemporaryDirectory() as tmp:
-        res = {c: encode(exe, c, tmp) for c in CASES}
-    json.dump(res, open(os.path.join(HERE, "expected_md5.json"), "w"), indent=1)
+        for c in todo:
+            res[c] = encode(exe, c, tmp)
+    json.dump(res, open(path, "w"), indent=1)
     print(json.dumps(res, indent=1))

@@ -439,3 +439,53 @@ def test_hm_finish_picture_gpu(torch, ctu_name, dbk_name):
         np.testing.assert_array_equal(y16, np.pad(c["post"][0], 80, mode="edge").astype(np.int16))
         np.testing.assert_array_equal(cb16, np.pad(c["post"][1], 40, mode="edge").astype(np.int16))
         np.testing.assert_array_equal(cr16, np.pad(c["post"][2], 40, mode="edge").astype(np.int16))
+
+
+@pytest.mark.gpu
+def test_hm_closed_loop_gpu(torch):
+    """A GOP segment run entirely on the device (SAO off, tests/golden/ctu_ldp_nosao.bin): the I
+    picture decided by hvx_hm_compress, finished by hvx_hm_finish_picture (deblocking from the
+    engine's own CTU data, compressMotion, padded reference planes); each P picture then decided
+    against the references and the collocated field the device produced -- no reference-encoder
+    data enters after the first picture except the originals and the slice-start states.  Every
+    CTU of every picture bit-exact vs HM, and each device reference plane equals the reference
+    picture HM handed the next pictures."""
+    from video_codecs_amd import _abi, hm
+    g = gc.load("ctu_ldp_nosao.bin")
+    g["_row_slices"] = False
+    eb = _abi.load_entropy_bits()
+    refs_by_poc, cols_by_poc = {}, {}
+    for pic, pi in enumerate(g["pic_i32"]):
+        poc, w, h = int(pi[hm_cases.P_POC]), int(pi[hm_cases.P_W]), int(pi[hm_cases.P_H])
+        first, n = int(pi[hm_cases.P_FIRST_CTU]), int(pi[hm_cases.P_NCTU])
+        psz = w * h * 3 // 2
+        org = hm_cases.yuv_split(g["org"][pic * psz:(pic + 1) * psz], w, h)
+        params = hm_cases.pic_params(pi, g["pic_f64"][pic])
+        nref0 = int(pi[hm_cases.P_NREF0])
+        refs = [refs_by_poc[int(p)] for p in g["refpic_poc"] if int(p) in refs_by_poc]
+        assert all(int(g["refpic_poc"][params["ref_plane"][0][i]]) in refs_by_poc for i in range(nref0))
+        col = cols_by_poc[int(pi[hm_cases.P_COL_POC])] if int(pi[hm_cases.P_COL_VALID]) else None
+        dp = hm.DevicePicture(org, refs, params, eb, col_field=col)
+        job = np.zeros(1, hm.HM_JOB)
+        job["pic"], job["first_ctu"], job["n_ctus"], job["chained"], job["out"] = 0, 0, n, 1, 0
+        job["entry"]["st"] = g["ctu_states"][first]
+        job["entry"]["frac"] = np.uint64(int(g["ctu_frac"][first]))
+        job["int2n"] = g["ctu_int2n"][first]
+        job["slice_start"], job["slice_end"] = 0, n - 1
+        out = hm.Engine([dp]).compress(job, n)
+        bad = hm_cases.compare(g, [(pic, first, n, 0)], out)
+        assert not bad, (poc, bad[:4])
+        ref = hm.DeviceFrame.blank(w, h)
+        _, col_t = hm.finish_picture(dp, _abi.deblock_params(w, h), col_field=True, ref_frame=ref)
+        torch.cuda.synchronize()
+        refs_by_poc[poc], cols_by_poc[poc] = ref, col_t
+        if poc in list(g["refpic_poc"]):
+            k = list(g["refpic_poc"]).index(poc)
+            want = hm_cases.yuv_split(g["refpic"][k * psz:(k + 1) * psz], w, h)
+            y8, y16, cb16, cr16 = (t.cpu().numpy() for t in ref.planes())
+            m8 = hm.DeviceFrame.M8
+            np.testing.assert_array_equal(y8[m8:m8 + h, m8:m8 + w], want[0])
+            np.testing.assert_array_equal(y16[80:80 + h, 80:80 + w], want[0].astype(np.int16))
+            np.testing.assert_array_equal(cb16[40:40 + h // 2, 40:40 + w // 2], want[1].astype(np.int16))
+            np.testing.assert_array_equal(cr16[40:40 + h // 2, 40:40 + w // 2], want[2].astype(np.int16))
+    assert len(refs_by_poc) == 3

@@ -25,7 +25,7 @@ EXPECTED = json.load(open(os.path.join(ROOT, "tests", "hm_seam", "expected_md5.j
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)  # ~1M synchronous per-call offloads per encode: correctness, not speed
-@pytest.mark.parametrize("case", sorted(mk.CASES))
+@pytest.mark.parametrize("case", [c for c in sorted(mk.CASES) if mk.case_size(c) == (mk.W, mk.H)])
 def test_hm_encoder_with_hvx_seams(case, monkeypatch):
     import torch
     if not torch.cuda.is_available():
@@ -67,7 +67,8 @@ def test_expected_md5_cases_present():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)  # one synchronous single-CTU launch per compressCtu call: correctness, not speed
-@pytest.mark.parametrize("case", ["ldp_rand_qp32", "ldp_smooth_qp32", "intra_rand_qp32", "intra_smooth_qp22", "ra_texture_qp32"])
+@pytest.mark.parametrize("case", ["ldp_rand_qp32", "ldp_smooth_qp32", "intra_rand_qp32", "intra_smooth_qp22", "ra_smooth_qp27",
+                                  "ra_texture_qp32"])
 def test_hm_encoder_with_cu_seam(case, monkeypatch):
     """The L3 boundary: every TEncCu::compressCtu of an unchanged TAppEncoder encode (LDP: I + P
     pictures; RA: I + hierarchical GOP8 B pictures) served by the HM-exact CTU engine (integration/hm_cu_seam.cpp -> hvx_hm_compress),
@@ -87,9 +88,44 @@ def test_hm_encoder_with_cu_seam(case, monkeypatch):
     m = re.search(r"hm_cu_seam: (\d+) compressCtu calls served by libhvx \((\d+) pictures\), (\d+) fell through", log[0])
     assert m, log[0][-2000:]
     frames = mk.CASES[case][2]
-    ctus = ((mk.W + 63) // 64) * ((mk.H + 63) // 64)
+    w, h = mk.case_size(case)
+    ctus = ((w + 63) // 64) * ((h + 63) // 64)
     assert int(m.group(1)) == frames * ctus and int(m.group(2)) == frames and int(m.group(3)) == 0, m.group(0)
     assert got == EXPECTED[case], (case, got, EXPECTED[case])
     # with every CTU decided on the device, HM's own motion search is never reached
     m = re.search(r"hm_me_seam: (\d+) xMotionEstimation calls served .* (\d+) fell through", log[0])
     assert m is None or (int(m.group(1)) == 0 and int(m.group(2)) == 0), m.group(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("case", ["ldp_smooth_1080p_qp32", "ra_texture_qp32"])
+def test_hm_encoder_with_cu_seam_batched(case, monkeypatch):
+    """The throughput form of the CTU seam (HVX_SEAM_CU_BATCH=1): at each picture's first
+    compressCtu call every slice of the picture is decided by ONE hvx_hm_compress launch (one chain
+    per slice; the 1080p encode's CTU-row slices, its partial bottom row continuing the chain of
+    the row above), and the unchanged TAppEncoder's later compressCtu calls take the kept results.
+    The bitstream and reconstruction MD5 of the reference at BASELINE's 1080p size (configs 2/3)
+    and on the random-access B pictures, 0 fall-throughs, one launch per picture, and the entry
+    coder HM holds before every CTU equal to the state the device chain carried into it."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if not os.path.exists(EXE):
+        pytest.skip("TAppEncoder_hvx not built (needs /root/reference at build time)")
+    monkeypatch.setenv("HVX_SEAM_CU", "1")
+    monkeypatch.setenv("HVX_SEAM_CU_BATCH", "1")
+    monkeypatch.setenv("HVX_SEAM_INTRA", "0")
+    log = []
+    with tempfile.TemporaryDirectory() as tmp:
+        got = mk.encode(EXE, case, tmp, log)
+    print(log[0][-600:])
+    frames = mk.CASES[case][2]
+    w, h = mk.case_size(case)
+    ctus = ((w + 63) // 64) * ((h + 63) // 64)
+    m = re.search(r"hm_cu_seam: (\d+) compressCtu calls served by libhvx \((\d+) pictures\), (\d+) fell through", log[0])
+    assert m and int(m.group(1)) == frames * ctus and int(m.group(3)) == 0, log[0][-2000:]
+    m = re.search(r"hm_cu_seam batched: (\d+) CTUs from (\d+) launches, (\d+) entry-state mismatches", log[0])
+    assert m and int(m.group(1)) == frames * ctus and int(m.group(2)) == frames and int(m.group(3)) == 0, log[0][-2000:]
+    assert got == EXPECTED[case], (case, got, EXPECTED[case])
+

@@ -53,3 +53,30 @@ def test_col_field_vs_reference(ctu_name):
         np.testing.assert_array_equal(hm_ctu.col_field(w, h, g["ctu_parts"][first:first + n]), fields[poc])
         n_checked += 1
     assert n_checked >= 2
+
+
+def test_closed_loop_references_vs_reference():
+    """With SAO off (tests/golden/ctu_ldp_nosao.bin) a reference picture is the deblocked
+    reconstruction: the restatement's boundary strengths from each decided picture's CTU data,
+    applied by the oracle's loopFilterPic to its reconstruction, give exactly the reference
+    picture the reference encoder hands the next pictures (the capture's refpic of that POC)."""
+    from tests import golden_cases as gc
+    from video_codecs_amd import _abi
+    g = gc.load("ctu_ldp_nosao.bin")
+    checked = 0
+    for pic, pi in enumerate(g["pic_i32"]):
+        poc, w, h = int(pi[hm_cases.P_POC]), int(pi[hm_cases.P_W]), int(pi[hm_cases.P_H])
+        if poc not in list(g["refpic_poc"]):
+            continue
+        first, n = int(pi[hm_cases.P_FIRST_CTU]), int(pi[hm_cases.P_NCTU])
+        rp = np.array([pi[hm_cases.P_REFPOC0:hm_cases.P_REFPOC0 + 4], pi[hm_cases.P_REFPOC1:hm_cases.P_REFPOC1 + 4]])
+        bv, bh, qp = hm_ctu.boundary_strength(w, h, g["ctu_parts"][first:first + n], rp, int(pi[hm_cases.P_SLICE_TYPE]) == 0)
+        rec = [p[:h >> (1 if c else 0), :w >> (1 if c else 0)].copy() for c, p in enumerate(hm_cases.hm_recon(g, first, w, h))]
+        got = oracle.deblock(*rec, bv.reshape(-1), bh.reshape(-1), qp.reshape(-1), _abi.deblock_params(w, h))
+        k = list(g["refpic_poc"]).index(poc)
+        psz = w * h * 3 // 2
+        want = hm_cases.yuv_split(g["refpic"][k * psz:(k + 1) * psz], w, h)
+        for c in range(3):
+            np.testing.assert_array_equal(got[c], want[c])
+        checked += 1
+    assert checked == 2

@@ -1,5 +1,7 @@
 // hvx_hm.hip -- the HM-exact CTU decision of libhvx.so (its own translation unit: the engine is
 // one large kernel, compiled apart from the leaf-kernel library in hvx_lib.hip).
+// the engine's tool set has no extended precision processing: RDOQ's rate is the branch-free form
+#define HVX_TU_NO_EXT 1
 #include <hip/hip_runtime.h>
 
 #include <cstring>

@@ -236,6 +236,22 @@ __device__ __forceinline__ int rd_ic_rate(uint32_t level, int rice, bool c1ok, b
   return rate;
 }
 
+// xGetICRate (:2891) without branches (the rate of one candidate level; lanes are different
+// TUs, so every branch of the reference's form would be divergent).  Not for the limited-prefix
+// (extended precision) escape code, which keeps rd_ic_rate.
+__device__ __forceinline__ int rd_ic_rate_bf(uint32_t level, uint32_t rice, bool c1ok, bool c2ok, int g0, int g1, int a0,
+                                             int a1) {
+  const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
+  const uint32_t symbol = level - base, r3 = 3u << rice;
+  const int small = (int)(((symbol >> rice) + 1 + rice) << 15);
+  const uint32_t v = ((symbol - r3) >> rice) + 1;
+  const uint32_t len = rice + (31u - (uint32_t)__clz(v));
+  const int big = (int)((3 + len + 1 - rice + len) << 15);
+  const int esc = (symbol < r3 ? small : big) + (c1ok ? g1 + (c2ok ? a1 : 0) : 0);
+  const int lo = level == 1 ? g0 : g1 + a0;  // level 2 below base (c1ok && c2ok)
+  return level == 0 ? 0 : 32768 + (level >= base ? esc : lo);
+}
+
 // getSigCtxInc (:2717) for square TUs (log2 width = log2 height = LOG2)
 template <int L>
 __device__ __forceinline__ int rd_sig_ctx_raster(int pattern, int first_sig, int raster, int ch);
@@ -283,6 +299,27 @@ __device__ __forceinline__ double rld(double v, int lane) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, lane);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// The c1 / c2 / Rice / c1Idx / c2Idx update after a position's decision (:2281-2330)
+__device__ __forceinline__ void rd_step(uint32_t level, int &c1, int &c2, uint32_t &c1_idx, uint32_t &c2_idx, uint32_t &rice,
+                                        bool persistent) {
+  const bool c1ok = c1_idx < 8, c2ok = c2_idx < 1;
+  const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
+  if (level >= base && level > 3u * (1u << rice)) rice = persistent ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
+  if (level >= 1) c1_idx++;
+  if (level > 1) { c1 = 0; c2 += (c2 < 2); c2_idx++; }
+  else if (c1 < 3 && c1 > 0 && level) c1++;
+}
+// xGetICRate: the branch-free form when extended precision is compiled out (HVX_TU_NO_EXT)
+__device__ __forceinline__ int rd_rate(uint32_t level, uint32_t rice, bool c1ok, bool c2ok, int g0, int g1, int a0, int a1,
+                                       int ext, int max_log2) {
+#ifdef HVX_TU_NO_EXT
+  (void)ext; (void)max_log2;
+  return rd_ic_rate_bf(level, rice, c1ok, c2ok, g0, g1, a0, a1);
+#else
+  return rd_ic_rate(level, (int)rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2);
+#endif
 }
 
 // Per scan position, the RDOQ pass keeps one packed int in s.a:
@@ -393,6 +430,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   HVX_RDOQ_PHASE(0);
   // ---- B. reverse-scan decisions (wave-uniform) ----
   const uint32_t rice0 = (uint32_t)d.golomb_rice_stat / 4;
+  const bool persistent = d.persistent_rice != 0;
   uint32_t rice = rice0, ctx_set = 0, c1_idx = 0, c2_idx = 0;
   int c1 = 1, c2 = 0, last = -1, cg_last = -1;
   double block_uncoded = 0, base_cost = 0;
@@ -430,24 +468,18 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
     bool any = false;
     double coded_ld = 0, uncoded = 0, sig_cost = 0, sig_cost0 = 0;
     int o_lev = 0, o_st = 0;  // lane pin: results of scan position cgp*16 + pin
-    for (int pin = 15; pin >= 0; pin--) {
-      const int sp = cgp * 16 + pin;
-      const uint32_t max_abs = (uint32_t)rl((int)ma_l, pin);
-      const double cc0 = rld(cc0_l, pin);
-      block_uncoded += cc0;
-      int32_t out = (int32_t)max_abs;
-      double cc = 0.0, cs = 0.0;
-      int stv = 0;
-      if (max_abs > 0 && last < 0) {
-        last = sp;
-        ctx_set = (comp ? 4 : 0) + ((comp == 0 && (sp >> 4) > 0) ? 2 : 0);
-        cg_last = cgp;
-      }
-      if (last >= 0) {
+    // the reference's per-position decision on the serial state (xGetCodedLevel :2822 and the
+    // c1 / c2 / Rice updates :2281-2330), for positions pin_hi .. 0 of a group holding or
+    // following the last significant position; the group-end reset is the caller's
+    auto serial_from = [&](int pin_hi) {
+      for (int pin = pin_hi; pin >= 0; pin--) {
+        const int sp = cgp * 16 + pin;
+        const uint32_t max_abs = (uint32_t)rl((int)ma_l, pin);
+        const double cc0 = rld(cc0_l, pin);
+        block_uncoded += cc0;
         const int ctx_one = 4 * (int)ctx_set + c1, ctx_abs = (int)ctx_set + c2;
         const int g0 = rl(t_g, ctx_one), g1 = rl(t_g, ctx_one + 32), a0 = rl(t_a, ctx_abs), a1 = rl(t_a, ctx_abs + 32);
         const bool c1ok = c1_idx < 8, c2ok = c2_idx < 1;
-        // xGetCodedLevel (:2822)
         const bool is_last = sp == last;
         const int ctx_sig = is_last ? 0 : rl(ctxs_l, pin);
         double cur_sig = 0, cost, cost_sig = 0;
@@ -464,43 +496,153 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
         }
         if (!done) {
           if (!is_last) cur_sig = rld(ls1_l, pin);
-          const uint32_t min_abs = max_abs > 1 ? max_abs - 1 : 1;
           const double dist1 = rld(d1_l, pin), dist2 = rld(d2_l, pin);
-          for (int lv = (int)max_abs; lv >= (int)min_abs; lv--) {
-            double cl = (lv == (int)max_abs ? dist1 : dist2) +
-                        lambda * (double)rd_ic_rate((uint32_t)lv, (int)rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2);
-            cl += cur_sig;
-            if (cl < cost) { best = (uint32_t)lv; cost = cl; cost_sig = cur_sig; sel = is_last ? 0 : 2; }
-          }
+          // the candidates max_abs and (max_abs > 1) max_abs - 1, tried in that order with the
+          // strict comparison of the reference's loop; both costs are formed independently
+          const bool two = max_abs > 1;
+          const uint32_t lv2 = two ? max_abs - 1 : max_abs;
+          const int r1 = rd_rate(max_abs, rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2);
+          const int r2 = rd_rate(lv2, rice, c1ok, c2ok, g0, g1, a0, a1, ext, max_log2);
+          double cl1 = dist1 + lambda * (double)r1;
+          cl1 += cur_sig;
+          double cl2 = dist2 + lambda * (double)r2;
+          cl2 += cur_sig;
+          if (cl1 < cost) { best = max_abs; cost = cl1; cost_sig = cur_sig; sel = is_last ? 0 : 2; }
+          if (two && cl2 < cost) { best = lv2; cost = cl2; cost_sig = cur_sig; sel = is_last ? 0 : 2; }
         }
-        cc = cost;
-        cs = cost_sig;
-        const uint32_t level = best;
-        stv = rd_pack(ctx_one, ctx_abs, (int)rice, c1ok, c2ok, !is_last, ctx_sig, sel);
-        out = (int32_t)level;
+        const double cc = cost, cs = cost_sig;
+        const int stv = rd_pack(ctx_one, ctx_abs, (int)rice, c1ok, c2ok, !is_last, ctx_sig, sel);
         base_cost += cc;
-        const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
-        if (level >= base && level > 3u * (1u << rice)) rice = d.persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
-        if (level >= 1) c1_idx++;
-        if (level > 1) { c1 = 0; c2 += (c2 < 2); c2_idx++; }
-        else if (c1 < 3 && c1 > 0 && level) c1++;
-        if (pin == 0 && sp > 0) {
-          ctx_set = (comp ? 4 : 0) + ((comp == 0 && ((sp - 1) >> 4) > 0) ? 2 : 0) + (c1 == 0 ? 1 : 0);
-          c1 = 1; c2 = 0; c1_idx = 0; c2_idx = 0;
-          rice = rice0;
+        rd_step(best, c1, c2, c1_idx, c2_idx, rice, persistent);
+        sig_cost += cs;
+        if (pin == 0) sig_cost0 = cs;
+        if (best) {
+          any = true;
+          coded_ld += cc - cs;
+          uncoded += cc0;
+          if (pin != 0) nnz0++;
         }
+        if (lane == pin) { o_lev = (int32_t)best; o_st = stv; }
+      }
+    };
+    // the decided positions: from the last significant one (its group) or the whole group
+    int start = 15;
+    if (last < 0) {
+      const uint64_t nz = __ballot(lane < 16 && ma_l > 0);
+      start = nz ? 63 - (int)__clzll(nz) : -1;
+      if (nz) {
+        last = cgp * 16 + start;
+        ctx_set = (comp ? 4 : 0) + ((comp == 0 && cgp > 0) ? 2 : 0);
+        cg_last = cgp;
+      }
+    }
+    // above it: uncoded costs only (every level there is 0)
+    for (int pin = 15; pin > start; pin--) {
+      const double cc0 = rld(cc0_l, pin);
+      block_uncoded += cc0;
+      base_cost += cc0;
+    }
+    if (start >= 0) {
+#ifdef HVX_RDOQ_SERIAL_B
+      serial_from(start);
+#else
+      // Speculation: the serial state at each decided position assuming every earlier decision
+      // kept max_abs (scalar, integers only); every position's decision then evaluated
+      // lane-parallel from its predicted state with the serial pass's own operations.  A
+      // decision whose state update differs from max_abs's invalidates the predictions below
+      // it: the positions up to the first such one are taken as decided, the rest of the group
+      // runs the serial pass from the true state.
+      int pst_l = 0;
+      {
+        int c1s = c1, c2s = c2;
+        uint32_t c1is = c1_idx, c2is = c2_idx, rs = rice;
+        for (int pin = start; pin >= 0; pin--) {
+          const int pk = c1s | (c2s << 2) | ((int)c1is << 4) | ((int)c2is << 9) | ((int)rs << 14);
+          pst_l = lane == pin ? pk : pst_l;
+          rd_step((uint32_t)rl((int)ma_l, pin), c1s, c2s, c1is, c2is, rs, persistent);
+        }
+      }
+      const int c1p = pst_l & 3, c2p = (pst_l >> 2) & 3;
+      const uint32_t c1ip = (uint32_t)(pst_l >> 4) & 31, c2ip = (uint32_t)(pst_l >> 9) & 31, rp = (uint32_t)(pst_l >> 14) & 31;
+      const int ctx_one_l = 4 * (int)ctx_set + c1p, ctx_abs_l = (int)ctx_set + c2p;
+      const int g0l = __shfl(t_g, ctx_one_l, HVX_WAVE), g1l = __shfl(t_g, ctx_one_l + 32, HVX_WAVE);
+      const int a0l = __shfl(t_a, ctx_abs_l, HVX_WAVE), a1l = __shfl(t_a, ctx_abs_l + 32, HVX_WAVE);
+      const bool c1okl = c1ip < 8, c2okl = c2ip < 1;
+      const int pin_l = lane & 15;
+      const bool is_last_l = cgp * 16 + pin_l == last;
+      const int ctx_sig_l = is_last_l ? 0 : ctxs_l;
+      double cur_sig = 0, cost, cost_sig = 0;
+      int sel = 0;
+      uint32_t best = 0;
+      bool done = false;
+      if (!is_last_l && ma_l < 3) {
+        cost_sig = ls0_l;
+        sel = 1;
+        cost = cc0_l + cost_sig;
+        if (ma_l == 0) done = true;
       } else {
-        base_cost += cc0;
+        cost = 1.7e+308;
       }
-      sig_cost += cs;
-      if (pin == 0) sig_cost0 = cs;
-      if (out) {
-        any = true;
-        coded_ld += cc - cs;
-        uncoded += cc0;
-        if (pin != 0) nnz0++;
+      if (!done) {
+        if (!is_last_l) cur_sig = ls1_l;
+        const bool two = ma_l > 1;
+        const uint32_t lv2 = two ? ma_l - 1 : ma_l;
+        const int r1 = rd_rate(ma_l, rp, c1okl, c2okl, g0l, g1l, a0l, a1l, ext, max_log2);
+        const int r2 = rd_rate(lv2, rp, c1okl, c2okl, g0l, g1l, a0l, a1l, ext, max_log2);
+        double cl1 = d1_l + lambda * (double)r1;
+        cl1 += cur_sig;
+        double cl2 = d2_l + lambda * (double)r2;
+        cl2 += cur_sig;
+        if (cl1 < cost) { best = ma_l; cost = cl1; cost_sig = cur_sig; sel = is_last_l ? 0 : 2; }
+        if (two && cl2 < cost) { best = lv2; cost = cl2; cost_sig = cur_sig; sel = is_last_l ? 0 : 2; }
       }
-      if (lane == pin) { o_lev = out; o_st = stv; }
+      const double dlt_l = cost - cost_sig;  // coded_ld's term (the serial pass's cc - cs)
+      const int stv_l = rd_pack(ctx_one_l, ctx_abs_l, (int)rp, c1okl, c2okl, !is_last_l, ctx_sig_l, sel);
+      bool ok;
+      {
+        int a1c = c1p, a2c = c2p, b1c = c1p, b2c = c2p;
+        uint32_t a1i = c1ip, a2i = c2ip, ar = rp, b1i = c1ip, b2i = c2ip, br = rp;
+        rd_step(best, a1c, a2c, a1i, a2i, ar, persistent);
+        rd_step(ma_l, b1c, b2c, b1i, b2i, br, persistent);
+        ok = a1c == b1c && a2c == b2c && a1i == b1i && a2i == b2i && ar == br;
+      }
+      const uint64_t bad = __ballot(lane <= start && !ok);
+      const int f = bad ? 63 - (int)__clzll(bad) : -1;  // the first position (in scan order) whose update differs
+      const uint32_t nzm = (uint32_t)__ballot(lane <= start && best != 0);
+      const int lo = f < 0 ? 0 : f;
+      for (int pin = start; pin >= lo; pin--) {
+        const double cc0 = rld(cc0_l, pin);
+        block_uncoded += cc0;
+        const double cc = rld(cost, pin), cs = rld(cost_sig, pin);
+        base_cost += cc;
+        sig_cost += cs;
+        if (pin == 0) sig_cost0 = cs;
+        if ((nzm >> pin) & 1u) {
+          any = true;
+          coded_ld += rld(dlt_l, pin);
+          uncoded += cc0;
+          if (pin != 0) nnz0++;
+        }
+      }
+      if (lane <= start && lane >= lo) { o_lev = (int32_t)best; o_st = stv_l; }
+      if (f < 0) {  // every prediction held: the state after position 0 is the predicted one
+        const int pk = rl(pst_l, 0);
+        c1 = pk & 3; c2 = (pk >> 2) & 3; c1_idx = (uint32_t)(pk >> 4) & 31; c2_idx = (uint32_t)(pk >> 9) & 31;
+        rice = (uint32_t)(pk >> 14) & 31;
+        rd_step((uint32_t)rl((int)best, 0), c1, c2, c1_idx, c2_idx, rice, persistent);
+      } else {  // the true state after position f, then the serial pass for the rest of the group
+        const int pk = rl(pst_l, f);
+        c1 = pk & 3; c2 = (pk >> 2) & 3; c1_idx = (uint32_t)(pk >> 4) & 31; c2_idx = (uint32_t)(pk >> 9) & 31;
+        rice = (uint32_t)(pk >> 14) & 31;
+        rd_step((uint32_t)rl((int)best, f), c1, c2, c1_idx, c2_idx, rice, persistent);
+        if (f > 0) serial_from(f - 1);
+      }
+#endif
+      if (cgp > 0) {  // the next group's context set and counters (:2262-2266)
+        ctx_set = (comp ? 4 : 0) + ((comp == 0 && cgp - 1 > 0) ? 2 : 0) + (c1 == 0 ? 1 : 0);
+        c1 = 1; c2 = 0; c1_idx = 0; c2_idx = 0;
+        rice = rice0;
+      }
     }
     if (any) sigmask |= 1ull << cgblk;
     int cgrate = 0;
@@ -984,22 +1126,6 @@ static __global__ __launch_bounds__(64) void k_tu(const hvx_tu_desc *__restrict_
 // =======================================================================================
 __device__ __forceinline__ size_t tu_il(int t, int sp, int NN, int G) {
   return ((size_t)(t / G) * NN + sp) * G + (t % G);
-}
-
-// xGetICRate (:2891) without branches (the rate of one candidate level; lanes are different
-// TUs, so every branch of the reference's form would be divergent).  Not for the limited-prefix
-// (extended precision) escape code, which keeps rd_ic_rate.
-__device__ __forceinline__ int rd_ic_rate_bf(uint32_t level, uint32_t rice, bool c1ok, bool c2ok, int g0, int g1, int a0,
-                                             int a1) {
-  const uint32_t base = c1ok ? (c2ok ? 3u : 2u) : 1u;
-  const uint32_t symbol = level - base, r3 = 3u << rice;
-  const int small = (int)(((symbol >> rice) + 1 + rice) << 15);
-  const uint32_t v = ((symbol - r3) >> rice) + 1;
-  const uint32_t len = rice + (31u - (uint32_t)__clz(v));
-  const int big = (int)((3 + len + 1 - rice + len) << 15);
-  const int esc = (symbol < r3 ? small : big) + (c1ok ? g1 + (c2ok ? a1 : 0) : 0);
-  const int lo = level == 1 ? g0 : g1 + a0;  // level 2 below base (c1ok && c2ok)
-  return level == 0 ? 0 : 32768 + (level >= base ? esc : lo);
 }
 
 // xRateDistOptQuant (:2129-2671) for one TU by one lane.  ldI/cxI/lev/st: the TU's
