@@ -550,6 +550,7 @@ static double err_scale(const hvx_tu_desc *tu) {
 /* xRateDistOptQuant (:2129-2671) */
 #ifdef HVXO_RDOQ_STATS
 long long hvxo_rdoq_stat[4][3]; /* per log2 size - 2: calls, calls with every rounded level 0, calls with absSum 0 */
+long long hvxo_rdoq_spec[4][3]; /* per log2 size - 2: decided positions, positions after a speculation miss, groups with a miss */
 #endif
 static void rdoq(const hvx_tu_desc *tu, const hvx_estbits *est, const int32_t *src, int32_t *dst, int32_t *arl, int32_t *abs_sum) {
   const int w = tu->width, h = tu->height, ch = tu->comp ? 1 : 0, comp = tu->comp;
@@ -603,7 +604,13 @@ static void rdoq(const hvx_tu_desc *tu, const hvx_estbits *est, const int32_t *s
   const int ncg = n >> 4;
   const int sig_off = ch ? 28 : 0;
 
+#ifdef HVXO_RDOQ_STATS
+  const int sl = (w == 4 ? 0 : w == 8 ? 1 : w == 16 ? 2 : 3);
+#endif
   for (int cgp = ncg - 1; cgp >= 0; cgp--) {
+#ifdef HVXO_RDOQ_STATS
+    int spec_missed = 0;
+#endif
     int cgblk = (int)cp.scan_cg[cgp];
     int cy = cgblk / cp.wg, cx = cgblk - cy * cp.wg;
     int nnz_before0 = 0;
@@ -649,6 +656,17 @@ static void rdoq(const hvx_tu_desc *tu, const hvx_estbits *est, const int32_t *s
         }
         dst[blk] = (int32_t)level;
         base_cost += cost_coeff[sp];
+#ifdef HVXO_RDOQ_STATS
+        {  /* would the state update with max_abs have matched the one with the decided level? */
+          uint32_t b0 = (c1_idx < 8) ? (2 + (c2_idx < 1)) : 1;
+          int r_a = level >= b0 && level > 3u * (1u << rice), r_b = max_abs >= b0 && max_abs > 3u * (1u << rice);
+          int same = r_a == r_b && (level >= 1) == (max_abs >= 1) && (level > 1) == (max_abs > 1) &&
+                     (level == 1) == (max_abs == 1);
+          __atomic_add_fetch(&hvxo_rdoq_spec[sl][0], 1, __ATOMIC_RELAXED);
+          if (spec_missed) __atomic_add_fetch(&hvxo_rdoq_spec[sl][1], 1, __ATOMIC_RELAXED);
+          if (!same && !spec_missed) { spec_missed = 1; __atomic_add_fetch(&hvxo_rdoq_spec[sl][2], 1, __ATOMIC_RELAXED); }
+        }
+#endif
         uint32_t base = (c1_idx < 8) ? (2 + (c2_idx < 1)) : 1;
         if (level >= base && level > 3u * (1u << rice)) rice = tu->persistent_rice ? rice + 1 : (rice + 1 < 4 ? rice + 1 : 4);
         if (level >= 1) c1_idx++;

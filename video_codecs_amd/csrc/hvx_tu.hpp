@@ -301,6 +301,10 @@ __device__ __forceinline__ double rld(double v, int lane) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// speculative rounds of the RDOQ reverse scan before the serial fallback (tu_rdoq)
+#ifndef HVX_RDOQ_ROUNDS
+#define HVX_RDOQ_ROUNDS 3
+#endif
 // The c1 / c2 / Rice / c1Idx / c2Idx update after a position's decision (:2281-2330)
 __device__ __forceinline__ void rd_step(uint32_t level, int &c1, int &c2, uint32_t &c1_idx, uint32_t &c2_idx, uint32_t &rice,
                                         bool persistent) {
@@ -546,68 +550,79 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
 #ifdef HVX_RDOQ_SERIAL_B
       serial_from(start);
 #else
-      // Speculation: the serial state at each decided position assuming every earlier decision
-      // kept max_abs (scalar, integers only); every position's decision then evaluated
-      // lane-parallel from its predicted state with the serial pass's own operations.  A
-      // decision whose state update differs from max_abs's invalidates the predictions below
-      // it: the positions up to the first such one are taken as decided, the rest of the group
-      // runs the serial pass from the true state.
-      int pst_l = 0;
-      {
-        int c1s = c1, c2s = c2;
-        uint32_t c1is = c1_idx, c2is = c2_idx, rs = rice;
-        for (int pin = start; pin >= 0; pin--) {
-          const int pk = c1s | (c2s << 2) | ((int)c1is << 4) | ((int)c2is << 9) | ((int)rs << 14);
-          pst_l = lane == pin ? pk : pst_l;
-          rd_step((uint32_t)rl((int)ma_l, pin), c1s, c2s, c1is, c2is, rs, persistent);
-        }
-      }
-      const int c1p = pst_l & 3, c2p = (pst_l >> 2) & 3;
-      const uint32_t c1ip = (uint32_t)(pst_l >> 4) & 31, c2ip = (uint32_t)(pst_l >> 9) & 31, rp = (uint32_t)(pst_l >> 14) & 31;
-      const int ctx_one_l = 4 * (int)ctx_set + c1p, ctx_abs_l = (int)ctx_set + c2p;
-      const int g0l = __shfl(t_g, ctx_one_l, HVX_WAVE), g1l = __shfl(t_g, ctx_one_l + 32, HVX_WAVE);
-      const int a0l = __shfl(t_a, ctx_abs_l, HVX_WAVE), a1l = __shfl(t_a, ctx_abs_l + 32, HVX_WAVE);
-      const bool c1okl = c1ip < 8, c2okl = c2ip < 1;
-      const int pin_l = lane & 15;
-      const bool is_last_l = cgp * 16 + pin_l == last;
-      const int ctx_sig_l = is_last_l ? 0 : ctxs_l;
-      double cur_sig = 0, cost, cost_sig = 0;
-      int sel = 0;
+      // Speculation in rounds: the serial state at each decided position is predicted from guessed
+      // levels of the positions before it (scalar, integers only), and every position's decision
+      // is then evaluated lane-parallel from its predicted state with the serial pass's own
+      // operations.  The guesses start at max_abs and are the previous round's decisions after
+      // that.  A position whose state update from its decision differs from the one from its
+      // guess invalidates the predictions below it; every position down to the first such one is
+      // exact (its predecessors' updates all matched).  After the last round the rest of the
+      // group runs the serial pass from the true state.
+      uint32_t guess = ma_l;
+      int pst_l = 0, f = -1;
+      double cost = 0, cost_sig = 0;
       uint32_t best = 0;
-      bool done = false;
-      if (!is_last_l && ma_l < 3) {
-        cost_sig = ls0_l;
-        sel = 1;
-        cost = cc0_l + cost_sig;
-        if (ma_l == 0) done = true;
-      } else {
-        cost = 1.7e+308;
-      }
-      if (!done) {
-        if (!is_last_l) cur_sig = ls1_l;
-        const bool two = ma_l > 1;
-        const uint32_t lv2 = two ? ma_l - 1 : ma_l;
-        const int r1 = rd_rate(ma_l, rp, c1okl, c2okl, g0l, g1l, a0l, a1l, ext, max_log2);
-        const int r2 = rd_rate(lv2, rp, c1okl, c2okl, g0l, g1l, a0l, a1l, ext, max_log2);
-        double cl1 = d1_l + lambda * (double)r1;
-        cl1 += cur_sig;
-        double cl2 = d2_l + lambda * (double)r2;
-        cl2 += cur_sig;
-        if (cl1 < cost) { best = ma_l; cost = cl1; cost_sig = cur_sig; sel = is_last_l ? 0 : 2; }
-        if (two && cl2 < cost) { best = lv2; cost = cl2; cost_sig = cur_sig; sel = is_last_l ? 0 : 2; }
+      int stv_l = 0;
+      for (int round = 0;; round++) {
+        {
+          int c1s = c1, c2s = c2;
+          uint32_t c1is = c1_idx, c2is = c2_idx, rs = rice;
+          for (int pin = start; pin >= 0; pin--) {
+            const int pk = c1s | (c2s << 2) | ((int)c1is << 4) | ((int)c2is << 9) | ((int)rs << 14);
+            pst_l = lane == pin ? pk : pst_l;
+            rd_step((uint32_t)rl((int)guess, pin), c1s, c2s, c1is, c2is, rs, persistent);
+          }
+        }
+        const int c1p = pst_l & 3, c2p = (pst_l >> 2) & 3;
+        const uint32_t c1ip = (uint32_t)(pst_l >> 4) & 31, c2ip = (uint32_t)(pst_l >> 9) & 31, rp = (uint32_t)(pst_l >> 14) & 31;
+        const int ctx_one_l = 4 * (int)ctx_set + c1p, ctx_abs_l = (int)ctx_set + c2p;
+        const int g0l = __shfl(t_g, ctx_one_l, HVX_WAVE), g1l = __shfl(t_g, ctx_one_l + 32, HVX_WAVE);
+        const int a0l = __shfl(t_a, ctx_abs_l, HVX_WAVE), a1l = __shfl(t_a, ctx_abs_l + 32, HVX_WAVE);
+        const bool c1okl = c1ip < 8, c2okl = c2ip < 1;
+        const int pin_l = lane & 15;
+        const bool is_last_l = cgp * 16 + pin_l == last;
+        const int ctx_sig_l = is_last_l ? 0 : ctxs_l;
+        double cur_sig = 0;
+        cost_sig = 0;
+        int sel = 0;
+        best = 0;
+        bool done = false;
+        if (!is_last_l && ma_l < 3) {
+          cost_sig = ls0_l;
+          sel = 1;
+          cost = cc0_l + cost_sig;
+          if (ma_l == 0) done = true;
+        } else {
+          cost = 1.7e+308;
+        }
+        if (!done) {
+          if (!is_last_l) cur_sig = ls1_l;
+          const bool two = ma_l > 1;
+          const uint32_t lv2 = two ? ma_l - 1 : ma_l;
+          const int r1 = rd_rate(ma_l, rp, c1okl, c2okl, g0l, g1l, a0l, a1l, ext, max_log2);
+          const int r2 = rd_rate(lv2, rp, c1okl, c2okl, g0l, g1l, a0l, a1l, ext, max_log2);
+          double cl1 = d1_l + lambda * (double)r1;
+          cl1 += cur_sig;
+          double cl2 = d2_l + lambda * (double)r2;
+          cl2 += cur_sig;
+          if (cl1 < cost) { best = ma_l; cost = cl1; cost_sig = cur_sig; sel = is_last_l ? 0 : 2; }
+          if (two && cl2 < cost) { best = lv2; cost = cl2; cost_sig = cur_sig; sel = is_last_l ? 0 : 2; }
+        }
+        stv_l = rd_pack(ctx_one_l, ctx_abs_l, (int)rp, c1okl, c2okl, !is_last_l, ctx_sig_l, sel);
+        bool ok;
+        {
+          int a1c = c1p, a2c = c2p, b1c = c1p, b2c = c2p;
+          uint32_t a1i = c1ip, a2i = c2ip, ar = rp, b1i = c1ip, b2i = c2ip, br = rp;
+          rd_step(best, a1c, a2c, a1i, a2i, ar, persistent);
+          rd_step(guess, b1c, b2c, b1i, b2i, br, persistent);
+          ok = a1c == b1c && a2c == b2c && a1i == b1i && a2i == b2i && ar == br;
+        }
+        const uint64_t bad = __ballot(lane <= start && !ok);
+        f = bad ? 63 - (int)__clzll(bad) : -1;  // the first position (in scan order) whose update differs
+        if (f <= 0 || round == HVX_RDOQ_ROUNDS - 1) break;
+        guess = best;
       }
       const double dlt_l = cost - cost_sig;  // coded_ld's term (the serial pass's cc - cs)
-      const int stv_l = rd_pack(ctx_one_l, ctx_abs_l, (int)rp, c1okl, c2okl, !is_last_l, ctx_sig_l, sel);
-      bool ok;
-      {
-        int a1c = c1p, a2c = c2p, b1c = c1p, b2c = c2p;
-        uint32_t a1i = c1ip, a2i = c2ip, ar = rp, b1i = c1ip, b2i = c2ip, br = rp;
-        rd_step(best, a1c, a2c, a1i, a2i, ar, persistent);
-        rd_step(ma_l, b1c, b2c, b1i, b2i, br, persistent);
-        ok = a1c == b1c && a2c == b2c && a1i == b1i && a2i == b2i && ar == br;
-      }
-      const uint64_t bad = __ballot(lane <= start && !ok);
-      const int f = bad ? 63 - (int)__clzll(bad) : -1;  // the first position (in scan order) whose update differs
       const uint32_t nzm = (uint32_t)__ballot(lane <= start && best != 0);
       const int lo = f < 0 ? 0 : f;
       for (int pin = start; pin >= lo; pin--) {
