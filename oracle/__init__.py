@@ -485,3 +485,46 @@ def sao_apply(src, comp, params):
     p = np.ascontiguousarray(params, _abi.SAO_CTU)
     L.hvxo_sao_apply(_p(s), s.shape[1], _p(d), d.shape[1], w, h, int(comp), _p(p))
     return d
+
+
+def sao_decide(w, h, stats, lambdas, slice_enabled, sao_states, frac_lo, slice_ctus=0, test_off=0):
+    """hvxo_sao_decide: SAO's RD decision of a picture.  stats [nctu, 3, 5, 64] int64 (diff[32],
+    count[32]); returns (coded [nctu, 3, 8] int32, recon SAO_CTU [nctu], slice_enabled (3,), total cost)."""
+    L = lib()
+    P = ctypes.c_void_p
+    L.hvxo_sao_decide.restype = ctypes.c_double
+    L.hvxo_sao_decide.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, P]
+    st = _c(stats, np.int64)
+    n = st.shape[0]
+    lam = _c(np.asarray(lambdas, np.float64), np.float64)
+    en = np.ascontiguousarray(np.asarray(slice_enabled, np.int32))
+    ss = np.ascontiguousarray(np.asarray(sao_states, np.uint8))
+    out = np.zeros((n, 3, 8), np.int32)
+    recon = np.zeros(n, _abi.SAO_CTU)
+    total = L.hvxo_sao_decide(int(w), int(h), _p(st), _p(lam), _p(en), _p(ss), int(frac_lo), _p(_abi.load_entropy_bits()),
+                              int(slice_ctus), int(test_off), _p(out), _p(recon))
+    return out, recon, en.copy(), total
+
+
+def sao_pic_params(layer, disabled_rate, rate, rate_chroma):
+    """hvxo_sao_pic_params (decidePicParams): slice-enabled flags (Y, Cb, Cr)."""
+    L = lib()
+    P = ctypes.c_void_p
+    L.hvxo_sao_pic_params.restype = None
+    L.hvxo_sao_pic_params.argtypes = [ctypes.c_int, P, ctypes.c_double, ctypes.c_double, P]
+    dr = np.ascontiguousarray(np.asarray(disabled_rate, np.float64).reshape(21))
+    en = np.zeros(3, np.int32)
+    L.hvxo_sao_pic_params(int(layer), _p(dr), float(rate), float(rate_chroma), _p(en))
+    return en
+
+
+def sao_update_rates(layer, recon, rate, rate_chroma, disabled_rate):
+    """hvxo_sao_update_rates: decideBlkParams' SAO-off rates after a picture; returns the new [3, 7]."""
+    L = lib()
+    P = ctypes.c_void_p
+    L.hvxo_sao_update_rates.restype = None
+    L.hvxo_sao_update_rates.argtypes = [ctypes.c_int, P, ctypes.c_int, ctypes.c_double, ctypes.c_double, P]
+    dr = np.ascontiguousarray(np.asarray(disabled_rate, np.float64).reshape(21).copy())
+    r = np.ascontiguousarray(recon, _abi.SAO_CTU)
+    L.hvxo_sao_update_rates(int(layer), _p(r), len(r), float(rate), float(rate_chroma), _p(dr))
+    return dr.reshape(3, 7)

@@ -119,6 +119,22 @@ dbk() {  # dbk <out.bin> <pocs> <cfg> <yuv> <frames> <qp>
 dbk tests/golden/dbk_ldp_rand.bin   0,1,2 $CFG/encoder_lowdelay_P_main.cfg  "$TMP/rand4.yuv"   3 32
 dbk tests/golden/dbk_ldp_smooth.bin 1,2,3 $CFG/encoder_lowdelay_P_main.cfg  "$TMP/smooth4.yuv" 4 27
 dbk tests/golden/dbk_ra_q32.bin     8,1   $CFG/encoder_randomaccess_main.cfg "$TMP/tex9.yuv"    9 32
+# SAO's RD decision: SAOProcess inputs / decided parameters per picture (oracle/saodec_capture.cpp)
+python3 oracle/make_yuv.py texture 416 240 4 "$TMP/tex4.yuv"
+sdec() {  # sdec <out.bin> <cfg> <yuv> <frames> <qp> [extra args...]
+  local out=$1 cfg=$2 yuv=$3 frames=$4 qp=$5; shift 5
+  HVX_CAPTURE=$out $ORC/TAppEncoder_saodec -c "$cfg" -i "$yuv" -wdt 416 -hgt 240 -fr 30 -f "$frames" -q "$qp" \
+    -b "$TMP/str.bin" -o "$TMP/rec.yuv" "$@" > "$TMP/log.txt"
+}
+sdec "$TMP/sd_ldp.bin"    $CFG/encoder_lowdelay_P_main.cfg   "$TMP/smooth4.yuv" 4 32
+sdec "$TMP/sd_ra.bin"     $CFG/encoder_randomaccess_main.cfg "$TMP/tex9.yuv"    9 27
+sdec "$TMP/sd_tex22.bin"  $CFG/encoder_lowdelay_P_main.cfg   "$TMP/tex4.yuv"    4 22
+sdec "$TMP/sd_rand37.bin" $CFG/encoder_lowdelay_P_main.cfg   "$TMP/rand4.yuv"   3 37
+sdec "$TMP/sd_intra.bin"  $CFG/encoder_intra_main.cfg        "$TMP/tex4.yuv"    2 27
+sdec "$TMP/sd_slices.bin" $CFG/encoder_lowdelay_P_main.cfg   "$TMP/tex4.yuv"    3 27 --SliceMode=1 --SliceArgument=5 \
+  --TestSAODisableAtPictureLevel=1
+python3 oracle/compact_saodec.py tests/golden/saodec.bin 0:"$TMP/sd_ldp.bin" 0:"$TMP/sd_ra.bin" 0:"$TMP/sd_tex22.bin" \
+  0:"$TMP/sd_rand37.bin" 0:"$TMP/sd_intra.bin" 5:"$TMP/sd_slices.bin"
 # slice-start CABAC states of every slice type and QP (TEncSbac::resetEntropy)
 make -s -C oracle ctx_init
 ls -la tests/golden

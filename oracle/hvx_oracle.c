@@ -2848,3 +2848,401 @@ void hvxo_sao_apply(const uint8_t *src, int ss, uint8_t *dst, int ds, int w, int
         }
     }
 }
+
+/* ============================================================================================
+ * SAO RD decision (TEncSampleAdaptiveOffset.cpp:332-889), 8-bit: DISTORTION_PRECISION_ADJUSTMENT(0)
+ * = 0, offset step log2 0, max offset 7 (getMaxOffsetQVal)
+ * ========================================================================================== */
+typedef struct { int mode, type, aux, offset[32]; } sao_offset_t; /* SAOOffset (modeIdc, typeIdc, typeAuxInfo) */
+typedef struct { sao_offset_t c[3]; } sao_blk_t;                  /* SAOBlkParam */
+typedef struct { uint8_t st[2]; uint64_t frac; } sao_coder_t;      /* the RD counter: sao_merge, sao_type_idx */
+typedef struct { const int32_t *eb; const double *lambda; const int *en; } sao_env_t;
+
+static void sao_bin(const sao_env_t *e, sao_coder_t *c, int ctx, int v) { /* TEncBinCABACCounter::encodeBin */
+  const int s = c->st[ctx], p = s >> 1, mps = s & 1;
+  c->frac += (uint64_t)(uint32_t)e->eb[s ^ v];
+  if (v == mps) c->st[ctx] = (uint8_t)(((p < 62 ? p + 1 : p) << 1) | mps);
+  else c->st[ctx] = (uint8_t)((kTransIdxLps[p] << 1) | (p == 0 ? mps ^ 1 : mps));
+}
+static void sao_ep(sao_coder_t *c, int n) { c->frac += 32768ull * (uint64_t)n; }
+static uint32_t sao_written(const sao_coder_t *c) { return (uint32_t)(c->frac >> 15); }
+static void sao_reset_bits(sao_coder_t *c) { c->frac &= 32767; }
+
+/* codeSaoMaxUvlc (TEncSbac.cpp:1548) with maxSymbol 7 */
+static void sao_max_uvlc(sao_coder_t *c, int code) { sao_ep(c, code == 0 ? 1 : code + (code < 7 ? 1 : 0)); }
+/* codeSAOOffsetParam (:1605) */
+static void sao_code_offset(const sao_env_t *e, sao_coder_t *c, int comp, const sao_offset_t *p) {
+  if (!e->en[comp]) return;
+  const int first = comp != 2;  /* first component of its channel type */
+  if (first) {
+    const int sym = p->mode == 0 ? 0 : p->type == 4 ? 1 : 2;
+    sao_bin(e, c, 1, sym != 0); /* codeSaoTypeIdx */
+    if (sym) sao_ep(c, 1);
+  }
+  if (p->mode == 1) {
+    int off[4], k = 0;
+    const int ncls = p->type == 4 ? 4 : 5;
+    for (int i = 0; i < ncls; i++) {
+      if (p->type != 4 && i == 2) continue; /* SAO_CLASS_EO_PLAIN */
+      off[k++] = p->offset[p->type == 4 ? (p->aux + i) % 32 : i];
+    }
+    for (int i = 0; i < 4; i++) sao_max_uvlc(c, off[i] < 0 ? -off[i] : off[i]);
+    if (p->type == 4) {
+      for (int i = 0; i < 4; i++)
+        if (off[i]) sao_ep(c, 1);
+      sao_ep(c, 5); /* sao_band_position */
+    } else if (first) {
+      sao_ep(c, 2); /* sao_eo_class */
+    }
+  }
+}
+/* codeSAOBlkParam (:1683) */
+static void sao_code_blk(const sao_env_t *e, sao_coder_t *c, const sao_blk_t *b, int left, int above, int only_merge) {
+  int is_left = 0, is_above = 0;
+  if (left) {
+    is_left = b->c[0].mode == 2 && b->c[0].type == 0;
+    sao_bin(e, c, 0, is_left);
+  }
+  if (above && !is_left) {
+    is_above = b->c[0].mode == 2 && b->c[0].type == 1;
+    sao_bin(e, c, 0, is_above);
+  }
+  if (only_merge) return;
+  if (!is_left && !is_above)
+    for (int k = 0; k < 3; k++) sao_code_offset(e, c, k, &b->c[k]);
+}
+
+static int64_t sao_est_dist(int64_t count, int64_t offset, int64_t diff) { return (count * offset * offset - diff * offset * 2) >> 0; }
+/* estIterOffset (:414) */
+static int sao_iter_offset(int type, double lambda, int in, int64_t count, int64_t diff, int64_t *best_dist, double *best_cost) {
+  int it = in, out = 0;
+  double min_cost = lambda;
+  while (it != 0) {
+    int64_t rate = type == 4 ? (abs(it) + 2) : (abs(it) + 1);
+    if (abs(it) == 7) rate--;
+    const int64_t dist = sao_est_dist(count, (int64_t)it, diff);
+    const double cost = ((double)dist + lambda * (double)rate);
+    if (cost < min_cost) {
+      min_cost = cost;
+      out = it;
+      *best_dist = dist;
+      *best_cost = cost;
+    }
+    it = it > 0 ? it - 1 : it + 1;
+  }
+  return out;
+}
+/* deriveOffsets (:447) */
+static void sao_derive_offsets(double lambda, int type, const int64_t *diff, const int64_t *count, int *q, int *aux) {
+  memset(q, 0, 32 * sizeof(int));
+  const int ncls = type == 4 ? 32 : 5;
+  for (int i = 0; i < ncls; i++) {
+    if (type != 4 && i == 2) continue;
+    if (count[i] == 0) continue;
+    const double x = (double)diff[i] / (double)count[i];
+    int v = (int)(x >= 0 ? (double)(int)(x + 0.5) : (double)(int)(x - 0.5)); /* xRoundIbdi, 8-bit */
+    q[i] = v < -7 ? -7 : v > 7 ? 7 : v;
+  }
+  if (type != 4) {
+    for (int i = 0; i < 5; i++) {
+      if ((i == 0 || i == 1) && q[i] < 0) q[i] = 0;
+      if ((i == 3 || i == 4) && q[i] > 0) q[i] = 0;
+      if (q[i] != 0) {
+        int64_t d = 0;
+        double cst = 0;
+        q[i] = sao_iter_offset(type, lambda, q[i], count[i], diff[i], &d, &cst);
+      }
+    }
+    *aux = 0;
+  } else {
+    int64_t dist_bo[32];
+    double cost_bo[32];
+    memset(dist_bo, 0, sizeof(dist_bo));
+    for (int i = 0; i < 32; i++) {
+      cost_bo[i] = lambda;
+      if (q[i] != 0) q[i] = sao_iter_offset(type, lambda, q[i], count[i], diff[i], &dist_bo[i], &cost_bo[i]);
+    }
+    double min_cost = 1.7e308;
+    for (int b = 0; b < 32 - 4 + 1; b++) {
+      double cst = cost_bo[b];
+      cst += cost_bo[b + 1];
+      cst += cost_bo[b + 2];
+      cst += cost_bo[b + 3];
+      if (cst < min_cost) { min_cost = cst; *aux = b; }
+    }
+    int keep[32];
+    memset(keep, 0, sizeof(keep));
+    for (int i = 0; i < 4; i++) keep[(*aux + i) % 32] = q[(*aux + i) % 32];
+    memcpy(q, keep, sizeof(keep));
+  }
+}
+/* getDistortion (:370) on de-quantised offsets */
+static int64_t sao_distortion(int type, int aux, const int *inv, const int64_t *diff, const int64_t *count) {
+  int64_t d = 0;
+  if (type != 4) {
+    for (int i = 0; i < 5; i++) d += sao_est_dist(count[i], inv[i], diff[i]);
+  } else {
+    for (int i = aux; i < aux + 4; i++) {
+      const int b = i % 32;
+      d += sao_est_dist(count[b], inv[b], diff[b]);
+    }
+  }
+  return d;
+}
+/* TComSampleAdaptiveOffset::invertQuantOffsets (TComSampleAdaptiveOffset.cpp:167), step 1 */
+static void sao_invert(int type, int aux, int *dst, const int *src) {
+  int coded[32];
+  memcpy(coded, src, sizeof(coded));
+  memset(dst, 0, 32 * sizeof(int));
+  if (type == 4) {
+    for (int i = 0; i < 4; i++) dst[(aux + i) % 32] = coded[(aux + i) % 32];
+  } else {
+    for (int i = 0; i < 5; i++) dst[i] = coded[i];
+  }
+}
+
+/* deriveModeNewRDO (:566) */
+static void sao_mode_new(const sao_env_t *e, const int64_t *st, sao_blk_t *merge[2], sao_coder_t *coders, int in_label,
+                         sao_blk_t *mode, double *norm_cost) {
+  enum { CUR = 1, NEXT = 2, MID = 3, TEMP = 4 };
+  sao_coder_t go;
+  int64_t dist[3], mdist[3] = {0, 0, 0};
+  sao_offset_t test[3];
+  int inv[32];
+  double min_cost, cost;
+  memset(test, 0, sizeof(test));
+  mode->c[0].mode = 0;
+  go = coders[in_label];
+  sao_code_blk(e, &go, mode, merge[0] != NULL, merge[1] != NULL, 1);
+  coders[MID] = go;
+  { /* luma */
+    mode->c[0].mode = 0;
+    sao_reset_bits(&go);
+    sao_code_offset(e, &go, 0, &mode->c[0]);
+    mdist[0] = 0;
+    min_cost = e->lambda[0] * ((double)sao_written(&go));
+    coders[TEMP] = go;
+    if (e->en[0]) {
+      for (int t = 0; t < 5; t++) {
+        test[0].mode = 1;
+        test[0].type = t;
+        const int64_t *s = st + (size_t)(0 * 5 + t) * 64;
+        sao_derive_offsets(e->lambda[0], t, s, s + 32, test[0].offset, &test[0].aux);
+        sao_invert(t, test[0].aux, inv, test[0].offset);
+        dist[0] = sao_distortion(t, test[0].aux, inv, s, s + 32);
+        go = coders[MID];
+        sao_reset_bits(&go);
+        sao_code_offset(e, &go, 0, &test[0]);
+        const int rate = (int)sao_written(&go);
+        cost = (double)dist[0] + e->lambda[0] * ((double)rate);
+        if (cost < min_cost) {
+          min_cost = cost;
+          mdist[0] = dist[0];
+          mode->c[0] = test[0];
+          coders[TEMP] = go;
+        }
+      }
+    }
+    go = coders[TEMP];
+    coders[MID] = go;
+  }
+  /* chroma: "off" as the initial cost */
+  cost = 0;
+  uint32_t prev = 0;
+  sao_reset_bits(&go);
+  for (int k = 1; k < 3; k++) {
+    mode->c[k].mode = 0;
+    mdist[k] = 0;
+    sao_code_offset(e, &go, k, &mode->c[k]);
+    const uint32_t now = sao_written(&go);
+    cost += e->lambda[k] * (now - prev);
+    prev = now;
+  }
+  min_cost = cost;
+  for (int t = 0; t < 5; t++) {
+    go = coders[MID];
+    sao_reset_bits(&go);
+    prev = 0;
+    cost = 0;
+    for (int k = 1; k < 3; k++) {
+      if (!e->en[k]) {
+        test[k].mode = 0;
+        dist[k] = 0;
+        continue;
+      }
+      test[k].mode = 1;
+      test[k].type = t;
+      const int64_t *s = st + (size_t)(k * 5 + t) * 64;
+      sao_derive_offsets(e->lambda[k], t, s, s + 32, test[k].offset, &test[k].aux);
+      sao_invert(t, test[k].aux, inv, test[k].offset);
+      dist[k] = sao_distortion(t, test[k].aux, inv, s, s + 32);
+      sao_code_offset(e, &go, k, &test[k]);
+      const uint32_t now = sao_written(&go);
+      cost += dist[k] + (e->lambda[k] * (now - prev));
+      prev = now;
+    }
+    if (cost < min_cost) {
+      min_cost = cost;
+      for (int k = 1; k < 3; k++) {
+        mdist[k] = dist[k];
+        mode->c[k] = test[k];
+      }
+    }
+  }
+  /* re-generated rate and normalised cost */
+  *norm_cost = 0;
+  for (int k = 0; k < 3; k++) *norm_cost += (double)mdist[k] / e->lambda[k];
+  go = coders[in_label];
+  sao_reset_bits(&go);
+  sao_code_blk(e, &go, mode, merge[0] != NULL, merge[1] != NULL, 0);
+  *norm_cost += (double)sao_written(&go);
+  coders[5] = go; /* the go-on coder after the mode's final coding (m_pcRDGoOnSbacCoder) */
+}
+
+/* deriveModeMergeRDO (:709) */
+static void sao_mode_merge(const sao_env_t *e, const int64_t *st, sao_blk_t *merge[2], sao_coder_t *coders, int in_label,
+                           sao_blk_t *mode, double *norm_cost) {
+  enum { TEMP = 4 };
+  *norm_cost = 1.7e308;
+  for (int mt = 0; mt < 2; mt++) {
+    if (!merge[mt]) continue;
+    sao_blk_t test = *merge[mt];
+    double nd = 0;
+    for (int k = 0; k < 3; k++) {
+      test.c[k].mode = 2;
+      test.c[k].type = mt;
+      const sao_offset_t *m = &merge[mt]->c[k];
+      if (m->mode != 0) {
+        const int64_t *s = st + (size_t)(k * 5 + m->type) * 64;
+        nd += (((double)sao_distortion(m->type, m->aux, m->offset, s, s + 32)) / e->lambda[k]);
+      }
+    }
+    sao_coder_t go = coders[in_label];
+    sao_reset_bits(&go);
+    sao_code_blk(e, &go, &test, merge[0] != NULL, merge[1] != NULL, 0);
+    const int rate = (int)sao_written(&go);
+    const double cost = nd + (double)rate;
+    if (cost < *norm_cost) {
+      *norm_cost = cost;
+      *mode = test;
+      coders[TEMP] = go;
+    }
+  }
+  coders[5] = coders[TEMP];
+}
+
+double hvxo_sao_decide(int w, int h, const int64_t *stats, const double *lambdas, int *slice_enabled,
+                       const uint8_t *sao_states, int frac_lo, const int32_t *entropy_bits, int slice_ctus, int test_off,
+                       int32_t *out, hvx_sao_ctu *recon_out) {
+  enum { PIC_INIT = 0, CUR = 1, NEXT = 2, GO = 5 };
+  const int wc = (w + 63) / 64, hc = (h + 63) / 64, n = wc * hc;
+  const sao_env_t e = {entropy_bits, lambdas, slice_enabled};
+  sao_coder_t coders[6];
+  memset(coders, 0, sizeof(coders));
+  coders[PIC_INIT].st[0] = sao_states[0];
+  coders[PIC_INIT].st[1] = sao_states[1];
+  coders[PIC_INIT].frac = (uint64_t)frac_lo;
+  const int all_off = !slice_enabled[0] && !slice_enabled[1] && !slice_enabled[2];
+  sao_blk_t *coded = (sao_blk_t *)calloc((size_t)n, sizeof(sao_blk_t));
+  sao_blk_t *recon = (sao_blk_t *)calloc((size_t)n, sizeof(sao_blk_t));
+  coders[GO] = coders[PIC_INIT];
+  double total = 0;
+  for (int a = 0; a < n; a++) {
+    if (all_off) continue; /* codedParams reset: every component off */
+    coders[CUR] = coders[GO];
+    sao_blk_t *merge[2] = {NULL, NULL};
+    const int x = a % wc, y = a / wc, s0 = slice_ctus > 0 ? a - a % slice_ctus : 0;
+    if (x > 0 && a - 1 >= s0) merge[0] = &recon[a - 1];   /* getMergeList: left, same slice */
+    if (y > 0 && a - wc >= s0) merge[1] = &recon[a - wc]; /* above */
+    const int64_t *st = stats + (size_t)a * 960;
+    double min_cost = 1.7e308, cost;
+    sao_blk_t mode;
+    memset(&mode, 0, sizeof(mode));
+    for (int m = 1; m < 3; m++) { /* SAO_MODE_OFF is covered by the NEW mode's comparisons */
+      if (m == 1) sao_mode_new(&e, st, merge, coders, CUR, &mode, &cost);
+      else sao_mode_merge(&e, st, merge, coders, CUR, &mode, &cost);
+      if (cost < min_cost) {
+        min_cost = cost;
+        coded[a] = mode;
+        coders[NEXT] = coders[GO];
+      }
+    }
+    total += min_cost;
+    coders[GO] = coders[NEXT];
+    /* reconstructBlkSAOParam */
+    recon[a] = coded[a];
+    for (int k = 0; k < 3; k++) {
+      sao_offset_t *o = &recon[a].c[k];
+      if (o->mode == 1) sao_invert(o->type, o->aux, o->offset, o->offset);
+      else if (o->mode == 2) *o = merge[o->type]->c[k];
+    }
+  }
+  if (!all_off && total >= 0 && test_off) { /* the coded parameters only: offsetCTU has run (:840-859) */
+    memset(coded, 0, (size_t)n * sizeof(sao_blk_t));
+    slice_enabled[0] = slice_enabled[1] = slice_enabled[2] = 0;
+  }
+  for (int a = 0; a < n; a++)
+    for (int k = 0; k < 3; k++) {
+      const sao_offset_t *o = &coded[a].c[k];
+      int32_t *r = out + ((size_t)a * 3 + k) * 8;
+      memset(r, 0, 8 * sizeof(int32_t));
+      r[0] = o->mode;
+      if (o->mode != 0) {
+        r[1] = o->type;
+        if (o->mode == 1) {
+          r[2] = o->aux;
+          if (o->type == 4)
+            for (int i = 0; i < 4; i++) r[3 + i] = o->offset[(o->aux + i) % 32];
+          else
+            for (int i = 0; i < 5; i++) r[3 + i] = o->offset[i];
+        }
+      }
+      if (recon_out) {
+        const sao_offset_t *q = &recon[a].c[k];
+        hvx_sao_offset *d = &recon_out[a].comp[k];
+        memset(d, 0, sizeof(*d));
+        d->type = (int8_t)(q->mode == 0 ? -1 : q->type);
+        if (q->mode != 0) {
+          if (q->type == 4) {
+            d->band = (uint8_t)q->aux;
+            for (int i = 0; i < 4; i++) d->offset[i] = (int8_t)q->offset[(q->aux + i) % 32];
+          } else {
+            d->offset[0] = (int8_t)q->offset[0];
+            d->offset[1] = (int8_t)q->offset[1];
+            d->offset[2] = (int8_t)q->offset[3];
+            d->offset[3] = (int8_t)q->offset[4];
+          }
+        }
+      }
+    }
+  free(coded);
+  free(recon);
+  return total;
+}
+
+void hvxo_sao_pic_params(int layer, const double *disabled_rate, double rate, double rate_chroma, int *slice_enabled) {
+  for (int k = 0; k < 3; k++) {
+    slice_enabled[k] = 1;
+    if (rate > 0.0) {
+      if (rate_chroma > 0.0) {
+        if (layer > 0 && disabled_rate[k * 7 + layer - 1] > (k == 0 ? rate : rate_chroma)) slice_enabled[k] = 0;
+      } else {
+        if (layer > 0 && disabled_rate[0] > rate) slice_enabled[k] = 0;
+      }
+    }
+  }
+}
+
+void hvxo_sao_update_rates(int layer, const hvx_sao_ctu *recon, int nctu, double rate, double rate_chroma,
+                           double *disabled_rate) {
+  if (!(rate > 0.0)) return;
+  int off[3] = {0, 0, 0};
+  for (int k = 0; k < 3; k++)
+    for (int a = 0; a < nctu; a++)
+      if (recon[a].comp[k].type < 0) off[k]++;
+  if (rate_chroma > 0.0) {
+    for (int k = 0; k < 3; k++) disabled_rate[k * 7 + layer] = (double)off[k] / (double)nctu;
+  } else if (layer == 0) {
+    disabled_rate[0] = (double)(off[0] + off[1] + off[2]) / (double)(nctu * 3);
+  }
+}

@@ -131,6 +131,28 @@ void hvxo_sao_stats(const uint8_t *org, int os, const uint8_t *rec, int rs, int 
 void hvxo_sao_apply(const uint8_t *src, int ss, uint8_t *dst, int ds, int w, int h, int comp,
                     const hvx_sao_ctu *params);
 
+/* SAO's RD decision (TEncSampleAdaptiveOffset::decideBlkParams, TEncSampleAdaptiveOffset.cpp:763,
+ * with deriveModeNewRDO :566, deriveModeMergeRDO :709, deriveOffsets :447, estIterOffset :414,
+ * getDistortion :370 and the SAO syntax rate of TEncSbac::codeSAOBlkParam TEncSbac.cpp:1683 on the
+ * RD counter), 8-bit 4:2:0, one tile.  stats = [ctu][comp 3][type 5][diff 32, count 32] (int64);
+ * slice_enabled = decidePicParams' flags (Y, Cb, Cr); sao_states = the sao_merge / sao_type_idx
+ * context states of the picture-start coder and frac_lo the low 15 bits of its fractional bit
+ * count; slice_ctus = CTUs per slice (SliceMode 1; 0: one slice; merges stay inside a slice);
+ * test_off = bTestSAODisableAtPictureLevel.  out = [ctu][comp][mode (0 off, 1 new, 2 merge), type,
+ * band position, offsets of EO classes 0..4 / of the 4 bands]; recon (optional) = the parameters
+ * offsetCTU applied, merges resolved ([ctu][comp] hvx_sao_ctu form; kept when the picture-level test
+ * then disables SAO, which clears only the coded parameters and slice_enabled, as the reference
+ * does).  Returns decideBlkParams' total cost. */
+double hvxo_sao_decide(int w, int h, const int64_t *stats, const double *lambdas, int *slice_enabled,
+                       const uint8_t *sao_states, int frac_lo, const int32_t *entropy_bits, int slice_ctus, int test_off,
+                       int32_t *out, hvx_sao_ctu *recon);
+/* decidePicParams (:332): the slice-enabled flags of a picture at temporal layer `layer` from the
+ * SAO-off rates of the earlier pictures (disabled_rate [3][7]); and decideBlkParams' rate update
+ * (:861-888) from a decided picture's reconstructed parameters (recon: [ctu][comp]). */
+void hvxo_sao_pic_params(int layer, const double *disabled_rate, double rate, double rate_chroma, int *slice_enabled);
+void hvxo_sao_update_rates(int layer, const hvx_sao_ctu *recon, int nctu, double rate, double rate_chroma,
+                           double *disabled_rate);
+
 /* boundary strengths of hvx_ctu_decide's CU trees (the bench step's deblocking input); cu/dec =
  * nctu*85 records of the whole picture, maps (pic_w/4) x (pic_h/4) */
 void hvxo_ctu_bs(const hvx_cu_result *cu, const hvx_cu_decision *dec, int pic_w, int pic_h, uint8_t *bs_ver,

@@ -203,3 +203,19 @@ def sao_cases(g):
         pc += nctu
     assert po == len(g["pre"]) and pc == len(g["params"])
     return out
+
+
+def saodec_cases(g):
+    """SAOProcess decision records (oracle/saodec_capture.cpp via compact_saodec.py): per picture a dict
+    of w, h, nctu, layer, test_off, enabled_out (3,), sao_states (2,), frac_lo, slice_ctus, lambdas (3,),
+    rate, rate_chroma, rates_before / rates_after [3, 7], stats [nctu, 3, 5, 64] int32, params [nctu, 3, 8]."""
+    out, po = [], 0
+    for m, f in zip(g["meta"], g["f64"]):
+        w, h, n, layer, toff, e0, e1, e2, sm, stt, flo, _nsl, sc = (int(v) for v in m)
+        out.append({"w": w, "h": h, "nctu": n, "layer": layer, "test_off": toff, "enabled_out": [e0, e1, e2],
+                    "sao_states": [sm, stt], "frac_lo": flo, "slice_ctus": sc, "lambdas": f[:3], "rate": float(f[3]),
+                    "rate_chroma": float(f[4]), "rates_before": f[5:26].reshape(3, 7), "rates_after": f[26:47].reshape(3, 7),
+                    "stats": g["stats"][po:po + n], "params": g["params"][po:po + n]})
+        po += n
+    assert po == g["stats"].shape[0]
+    return out

@@ -1,0 +1,28 @@
+"""SAO's RD decision, CPU restatement (oracle/hvx_oracle.c hvxo_sao_decide / hvxo_sao_pic_params /
+hvxo_sao_update_rates) against the reference's own SAOProcess decisions (tests/golden/saodec.bin,
+oracle/saodec_capture.cpp): LDP / RA / intra encodes of smooth, textured and random content at QP
+22-37, temporal layers 0-3 (slice-level enables from the earlier pictures' SAO-off rates), six
+row-sliced pictures with TestSAODisableAtPictureLevel."""
+import numpy as np
+
+import oracle
+from tests import golden_cases as gc
+
+
+def test_sao_decision_vs_reference():
+    cases = gc.saodec_cases(gc.load("saodec.bin"))
+    assert len(cases) == 25
+    modes = np.zeros(3, np.int64)
+    types = np.zeros(5, np.int64)
+    for c in cases:
+        en = oracle.sao_pic_params(c["layer"], c["rates_before"], c["rate"], c["rate_chroma"])
+        out, recon, en_out, _ = oracle.sao_decide(c["w"], c["h"], c["stats"], c["lambdas"], en, c["sao_states"], c["frac_lo"],
+                                                 c["slice_ctus"], c["test_off"])
+        np.testing.assert_array_equal(out, c["params"])  # every CTU's coded mode, type, band, offsets
+        assert list(en_out) == c["enabled_out"]
+        np.testing.assert_array_equal(oracle.sao_update_rates(c["layer"], recon, c["rate"], c["rate_chroma"],
+                                                              c["rates_before"]), c["rates_after"])
+        modes += np.bincount(c["params"][:, :, 0].ravel(), minlength=3)
+        p = c["params"][:, :, :2].reshape(-1, 2)
+        types += np.bincount(p[p[:, 0] == 1, 1], minlength=5)
+    assert (modes > 50).all() and (types > 3).all(), (modes, types)

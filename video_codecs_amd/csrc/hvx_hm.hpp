@@ -1217,6 +1217,165 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
   return num_sig;
 }
 
+// The same count with each coefficient group's context-coded bins resolved in ROUNDS instead of
+// one after the other: every bin of a group (significance flags, lane = position; greater-1
+// flags, the lane of their level) is known from the levels before any is counted -- its context
+// (the greater-1 context from c1 in closed form: 0 after a greater-1 bin of the group, else
+// min(1 + j, 3) for the j-th) and its value -- and a bin's cost and state update depend only on
+// the bins before it ON THE SAME CONTEXT.  So each bin gets its rank among the group's earlier
+// bins of its context, and round r updates every context's r-th bin at once (different contexts:
+// no conflicts); a group takes max-rank + 1 rounds of one LDS state read / table read / state
+// write instead of one such chain per bin.  The bin costs are integers, summed in any order.  The
+// last position, the CG flag, greater-2 and the bypass bins stay on the serial counter.
+__device__ int coeff_count_par(const hvx_tu_desc &d, const StagedScan &env, const int16_t *ls, CoderLane &L) {
+  const int n = d.width, lw = cab::log2_tu(n), wg = n >> 2, nn = n * n;
+  const int ch = d.comp ? 1 : 0, l = lid();
+  uint64_t cgm = 0;
+  int num_sig = 0, scan_last = -1;
+  const int nw = nn < 64 ? 1 : nn >> 6;
+  for (int w = 0; w < nw; w++) {
+    const uint64_t b = __ballot(w * 64 + l < nn && ls[w * 64 + l] != 0);
+    if (b) {
+      num_sig += __popcll(b);
+      scan_last = w * 64 + 63 - __clzll(b);
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if ((b >> (16 * q)) & 0xffffu) cgm |= 1ull << env.cg(w * 4 + q);
+    }
+  }
+  if (num_sig == 0) return 0;
+  const bool be_valid = d.transquant_bypass ? false : (d.sign_hiding != 0);
+  if (d.pps_tskip && !d.transquant_bypass && n <= 4) L.bin(cab::kTskip + ch, d.transform_skip ? 1 : 0);
+  {  // codeLastSignificantXY (:1115)
+    const int r = env.raster(scan_last);
+    int py = r >> lw, px = r - (py << lw);
+    if (d.scan_type == 2) { const int t = px; px = py; py = t; }
+    const int gx = kGroupIdx[px], gy = kGroupIdx[py], gmax = kGroupIdx[n - 1];
+    const int cw = lw - 2;
+    const int off = ch ? 0 : cw * 3 + ((cw + 1) >> 2), sh = ch ? cw : (cw + 3) >> 2;
+    const int bx = cab::kLastX + ch * 15 + off, by = cab::kLastY + ch * 15 + off;
+    int k;
+    for (k = 0; k < gx; k++) L.bin(bx + (k >> sh), 1);
+    if (gx < gmax) L.bin(bx + (k >> sh), 0);
+    for (k = 0; k < gy; k++) L.bin(by + (k >> sh), 1);
+    if (gy < gmax) L.bin(by + (k >> sh), 0);
+    if (gx > 3) L.ep((gx - 2) >> 1);
+    if (gy > 3) L.ep((gy - 2) >> 1);
+  }
+  const int base_cg = cab::kSigCG + ch * 2, base_sig = cab::kSig + (ch ? 28 : 0);
+  const int last_set = scan_last >> 4, last_pin = scan_last & 15;
+  bool c1_zero = false;  // c1 == 0 after the previous coded group (its context set's +1)
+  uint32_t fpart = 0;    // this lane's share of the context-coded bin costs
+  uint8_t *st = L.st + cab::kCtxLo;
+  for (int sub = last_set; sub >= 0; sub--) {
+    const int sub_pos = sub << 4;
+    const int cg = env.cg(sub), cgy = cg / wg, cgx = cg - cgy * wg;
+    const int lv_l = l < 16 ? (int)ls[sub_pos + l] : 0;
+    const int av_l = lv_l < 0 ? -lv_l : lv_l;
+    const int sc_l = l < 16 ? (env.big ? (int)env.scan_g[sub_pos + l] : env.sig[sub_pos + l]) : 0;
+    if (sub == last_set || sub == 0) cgm |= 1ull << cg;
+    else {
+      const int rr = cgx < wg - 1 ? (int)((cgm >> (cg + 1)) & 1) : 0;
+      const int bb = cgy < wg - 1 ? (int)((cgm >> (cg + wg)) & 1) : 0;
+      L.bin(base_cg + ((rr + bb) != 0), (int)((cgm >> cg) & 1));
+    }
+    const bool is_last_set = sub == last_set;
+    const uint32_t m16 = (uint32_t)__ballot(lv_l != 0);
+    // significance flags: lane p codes position p (descending), pin 0 only if a flag above it (or
+    // the last position) is 1, or in group 0
+    bool a1 = false;
+    int row1 = 0, val1 = 0, rank1 = 0;
+    if ((cgm >> cg) & 1) {
+      int pattern = 0;
+      if (wg > 1) {
+        const int rr = cgx < wg - 1 ? (int)((cgm >> (cg + 1)) & 1) : 0;
+        const int bb = cgy < wg - 1 ? (int)((cgm >> (cg + wg)) & 1) : 0;
+        pattern = rr + (bb << 1);
+      }
+      const int sc = env.big ? cab::sig_ctx(pattern, env.first_sig, env.single, sc_l, lw, ch) : (sc_l >> (6 * pattern)) & 63;
+      const int start = is_last_set ? last_pin - 1 : 15;
+      const bool pin0 = sub == 0 || is_last_set || (m16 & ((2u << start) - 2u)) != 0;
+      a1 = l <= start && (l > 0 || pin0);
+      row1 = base_sig + sc;
+      val1 = lv_l != 0;
+      for (int q = start; q > 0; q--) {  // earlier (higher) positions on the same context
+        const int sq = __builtin_amdgcn_readlane(sc, q);
+        rank1 += (q > l && sq == sc) ? 1 : 0;
+      }
+    }
+    const int nnz = __popc(m16);
+    // greater-1 flags of the first 8 non-zero levels (descending), in their levels' lanes
+    bool a2 = false;
+    int row2 = 0, val2 = 0, rank2 = 0;
+    uint32_t gmask = 0;
+    int set = 0;
+    if (nnz) {
+      set = (ch ? 4 : 0) + ((!ch && sub > 0) ? 2 : 0) + (c1_zero ? 1 : 0);
+      const int j = l < 16 ? __popc(m16 >> (l + 1)) : 64;  // index among the group's non-zero levels
+      a2 = l < 16 && lv_l != 0 && j < 8;
+      gmask = (uint32_t)__ballot(a2 && av_l > 1);
+      const bool g_before = l < 15 ? (gmask >> (l + 1)) != 0 : false;
+      const int c1 = g_before ? 0 : (j + 1 < 3 ? j + 1 : 3);
+      row2 = cab::kOne + 4 * set + c1;
+      val2 = av_l > 1;
+      if (c1 == 0) {
+        const int hp = 31 - __clz(gmask);  // the first greater-1 bin's position
+        rank2 = j - (__popc(m16 >> (hp + 1)) + 1);
+      } else {
+        rank2 = c1 == 3 ? j - 2 : 0;
+      }
+      c1_zero = gmask != 0;
+    }
+    // the rounds
+    int mr = (a1 ? rank1 : -1) > (a2 ? rank2 : -1) ? (a1 ? rank1 : -1) : (a2 ? rank2 : -1);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { const int t = __shfl_xor(mr, o, HVX_WAVE); mr = t > mr ? t : mr; }
+    for (int r = 0; r <= mr; r++) {
+      if (a1 && rank1 == r) {
+        const int q = st[row1];
+        fpart += (uint32_t)E.eb[q ^ val1];
+        st[row1] = E.next[q * 2 + val1];
+      }
+      if (a2 && rank2 == r) {
+        const int q = st[row2];
+        fpart += (uint32_t)E.eb[q ^ val2];
+        st[row2] = E.next[q * 2 + val2];
+      }
+    }
+    if (nnz == 0) continue;
+    const int last_nz = 31 - __clz(m16), first_nz = __builtin_ctz(m16);
+    const bool hidden = (last_nz - first_nz) >= 4;  // SBH_THRESHOLD
+    bool escape = nnz > 8;
+    if (gmask) {
+      const int hp = 31 - __clz(gmask);
+      const int first_c2_abs = __builtin_amdgcn_readlane(av_l, hp);
+      if (__popc(gmask) > 1) escape = true;
+      const int gt2 = first_c2_abs > 2;
+      L.bin(cab::kAbs + set, gt2);
+      if (gt2) escape = true;
+    }
+    L.ep((be_valid && hidden) ? nnz - 1 : nnz);  // signs (the first one hidden)
+    if (escape) {  // Rice parameter from 0 (no persistent adaptation in the engine's tool set)
+      int rice = 0, first2 = 1, idx = 0;
+      uint32_t all = m16;
+      while (all) {
+        const int pin = 31 - __clz(all);
+        all &= ~(1u << pin);
+        const int av = __builtin_amdgcn_readlane(av_l, pin);
+        const int base = idx < 8 ? 2 + first2 : 1;
+        if (av >= base) {
+          L.ep(cab::remain_bins((uint32_t)(av - base), rice, d.extended_precision != 0, d.max_log2_tr_range));
+          if (av > (3 << rice)) rice = rice + 1 < 4 ? rice + 1 : 4;
+        }
+        if (av >= 2) first2 = 0;
+        idx++;
+      }
+    }
+  }
+  L.frac += wave_sum_u32(fpart);
+  return num_sig;
+}
+
 // codeCoeffNxN on the current coder, levels TU-packed int16.  The whole wave first stages the TU
 // in LDS in scan order -- levels, raster positions, the significance context of every position
 // under the four neighbour-CG patterns, the CG scan -- with one round of table and level loads;
@@ -1323,7 +1482,11 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
 #else
   // the mask-driven walk for every size (a third walk instance in this function measured 20%
   // slower overall: register pressure)
+#ifdef HM_WALK_SERIAL
   coeff_count_staged(d, env, ls, L);
+#else
+  coeff_count_par(d, env, ls, L);
+#endif
 #endif
 #ifdef HM_REG_WALK
   L.store(E.cod[E.cur].st);
