@@ -301,6 +301,12 @@ int hvx_sao_stats(hvx_ctx *ctx, const uint8_t *d_org_y, const uint8_t *d_org_cb,
 int hvx_sao_apply(hvx_ctx *ctx, const uint8_t *d_src_y, const uint8_t *d_src_cb, const uint8_t *d_src_cr,
                   int src_y_stride, int src_c_stride, uint8_t *d_dst_y, uint8_t *d_dst_cb, uint8_t *d_dst_cr,
                   int dst_y_stride, int dst_c_stride, int pic_w, int pic_h, const hvx_sao_ctu *d_params);
+/* SAO's RD decision for n_jobs pictures, one wave each (TEncSampleAdaptiveOffset::decideBlkParams
+ * TEncSampleAdaptiveOffset.cpp:763: deriveModeNewRDO :566 / deriveModeMergeRDO :709 per CTU in raster
+ * order, deriveOffsets :447 with estIterOffset :414, getDistortion :370, the SAO syntax rate
+ * TEncSbac::codeSAOBlkParam TEncSbac.cpp:1683 on the RD counter carried CTU to CTU, the picture-level
+ * disable test :846): the coded and the applied (merge-resolved, hvx_sao_apply-ready) parameters. */
+int hvx_sao_decide(hvx_ctx *ctx, const hvx_sao_decide_job *d_jobs, int n_jobs);
 
 /* ---------------------------------------------------------------------------------------
  * CTU analysis pass over a whole picture (hvx_types.h): d_cur = sample (0,0) of the current

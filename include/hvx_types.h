@@ -279,6 +279,27 @@ typedef struct hvx_sao_stat {
   int64_t count[HVX_SAO_CLASSES];
 } hvx_sao_stat;                    /* 512 bytes; a picture: [ctu][comp 3][type 5] */
 
+/* One picture's SAO RD decision (hvx_sao_decide: TEncSampleAdaptiveOffset::decideBlkParams,
+ * TEncSampleAdaptiveOffset.cpp:763), 8-bit 4:2:0, one tile.  Device pointers; the job array itself
+ * is on the device. */
+typedef struct hvx_sao_decide_job {
+  int32_t pic_w, pic_h;
+  int32_t slice_ctus;              /* CTUs per slice (SliceMode 1), 0: one slice -- merges stay in a slice */
+  int32_t test_off;                /* bTestSAODisableAtPictureLevel */
+  int32_t slice_enabled[3];        /* decidePicParams' flags Y, Cb, Cr (host: the SAO-off rates of earlier pictures) */
+  int32_t frac_lo;                 /* low 15 bits of the picture-start RD coder's fractional bit count */
+  uint8_t sao_states[2];           /* its sao_merge_left/up_flag and sao_type_idx context states (m_ucState) */
+  uint8_t pad_[6];
+  double lambda[3];                /* SAOProcess's lambdas */
+  const hvx_sao_stat *stats;       /* [ctu][3][5] statistics (hvx_sao_stats) */
+  const int32_t *entropy_bits;     /* ContextModel::m_entropyBits[128] */
+  int32_t *coded;                  /* out [ctu][3][8]: mode (0 off, 1 new, 2 merge), type (EO 0-3 / BO 4, or merge
+                                      0 left / 1 above), band position, offsets of EO classes 0..4 / of the 4 bands */
+  hvx_sao_ctu *recon;              /* out [ctu]: the parameters offsetCTU applies (merges resolved) */
+  int32_t *slice_enabled_out;      /* out [3]: cleared when the picture-level test disables SAO */
+  double *total_cost;              /* out: decideBlkParams' total cost */
+} hvx_sao_decide_job;
+
 /* One PU's motion compensation (TComPrediction::motionCompensation for one partition, no
  * weighted prediction; TComPrediction.cpp:517-722).  Lists with ref >= 0 are used: both ->
  * bi-prediction (14-bit intermediates + TComYuv::addAvg), unless HVX_MC_B_SLICE is set and the

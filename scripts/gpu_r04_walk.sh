@@ -3,6 +3,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 600 --timeout-method thread -m gpu \
-  -k "hm_" > gpurun_out/parity_hm.log 2>&1; rc=$?; tail -3 gpurun_out/parity_hm.log
+  -k "hm_ or sao_decide" > gpurun_out/parity_hm.log 2>&1; rc=$?; tail -3 gpurun_out/parity_hm.log
 [ $rc -eq 0 ] || exit $rc
 bash scripts/gpu_hm_ab.sh "$@"

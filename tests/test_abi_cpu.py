@@ -61,6 +61,23 @@ int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(hvx_tu_des
                     hvx.SSIM_JOB.itemsize, hvx.STVSSIM_JOB.itemsize, _abi.ME_JOB.fields["lambda_motion"][1]]
 
 
+def test_sao_decide_job_layout_matches_c():
+    prog = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "hvx.h"
+int main(){printf("%zu %zu %zu %zu %zu\n", sizeof(hvx_sao_decide_job), offsetof(hvx_sao_decide_job, sao_states),
+ offsetof(hvx_sao_decide_job, lambda), offsetof(hvx_sao_decide_job, stats), offsetof(hvx_sao_decide_job, total_cost)); return 0;}
+"""
+    tmp = "/tmp/hvx_saodec_layout"
+    with open(tmp + ".c", "w") as f:
+        f.write(prog)
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), tmp + ".c", "-o", tmp])
+    vals = [int(x) for x in subprocess.check_output([tmp]).split()]
+    J = _abi.SAO_DECIDE_JOB
+    assert vals == [J.itemsize, J.fields["sao_states"][1], J.fields["lambda"][1], J.fields["stats"][1], J.fields["total_cost"][1]]
+
+
 def test_golden_estbits_layout():
     from tests import golden_cases as gc
     g = gc.load("tu_ldp.bin")

@@ -26,3 +26,22 @@ def test_sao_decision_vs_reference():
         p = c["params"][:, :, :2].reshape(-1, 2)
         types += np.bincount(p[p[:, 0] == 1, 1], minlength=5)
     assert (modes > 50).all() and (types > 3).all(), (modes, types)
+
+
+def test_sao_picture_logic_host_vs_reference():
+    """The product's host side of the SAO decision (video_codecs_amd.hm: decidePicParams' slice
+    enables, the SAO-off rate update) against the captures, and the context indices of the two SAO
+    contexts against the captured picture-start states (resetEntropy)."""
+    from video_codecs_amd import _abi, hm
+    cases = gc.saodec_cases(gc.load("saodec.bin"))
+    init = _abi.load_ctx_init_states()
+    for c in cases:
+        en = hm.sao_slice_enabled(c["layer"], c["rates_before"], c["rate"], c["rate_chroma"])
+        assert en == list(oracle.sao_pic_params(c["layer"], c["rates_before"], c["rate"], c["rate_chroma"]))
+        _, recon, _, _ = oracle.sao_decide(c["w"], c["h"], c["stats"], c["lambdas"], en, c["sao_states"], c["frac_lo"],
+                                           c["slice_ctus"], c["test_off"])
+        np.testing.assert_array_equal(hm.sao_update_rates(c["layer"], recon, c["rates_before"], c["rate"], c["rate_chroma"]),
+                                      c["rates_after"])
+        # the picture-start SAO states are resetEntropy's for some slice type and QP
+        assert any(init[t, q, hm.SAO_CTX_MERGE] == c["sao_states"][0] and init[t, q, hm.SAO_CTX_TYPE] == c["sao_states"][1]
+                   for t in range(3) for q in range(52))

@@ -178,6 +178,12 @@ SAO_CTU = np.dtype([("comp", SAO_OFFSET, (3,))])
 assert SAO_CTU.itemsize == 24
 SAO_STAT = np.dtype([("diff", "<i8", (32,)), ("count", "<i8", (32,))])
 assert SAO_STAT.itemsize == 512
+# hvx_sao_decide_job (hvx_types.h)
+SAO_DECIDE_JOB = np.dtype([("pic_w", "<i4"), ("pic_h", "<i4"), ("slice_ctus", "<i4"), ("test_off", "<i4"),
+                           ("slice_enabled", "<i4", (3,)), ("frac_lo", "<i4"), ("sao_states", "u1", (2,)), ("pad_", "u1", (6,)),
+                           ("lambda", "<f8", (3,)), ("stats", "<u8"), ("entropy_bits", "<u8"), ("coded", "<u8"),
+                           ("recon", "<u8"), ("slice_enabled_out", "<u8"), ("total_cost", "<u8")])
+assert SAO_DECIDE_JOB.itemsize == 112
 
 
 def sao_ctu_params(rows):

@@ -24,6 +24,7 @@
 #include "hvx_deblock.hpp"
 #include "hvx_sao.hpp"
 #include "hvx_hmloop.hpp"
+#include "hvx_saodec.hpp"
 #include "hvx_host.hpp"
 #include "hvx_tables.hpp"
 
@@ -1030,6 +1031,14 @@ int hvx_hm_finish_picture(hvx_ctx *ctx, const hvx_hm_picture *h_pic, const hvx_d
     }
   }
   return HVX_OK;
+}
+
+
+int hvx_sao_decide(hvx_ctx *ctx, const hvx_sao_decide_job *d_jobs, int n_jobs) {
+  if (!ctx || (n_jobs > 0 && !d_jobs) || n_jobs < 0) return fail(HVX_E_INVALID, "hvx_sao_decide: bad args");
+  if (n_jobs == 0) return HVX_OK;
+  hipLaunchKernelGGL(k_sao_decide, dim3(n_jobs), dim3(64), 0, ctx->stream, d_jobs, n_jobs);
+  return launched("k_sao_decide");
 }
 
 }  // extern "C"

@@ -395,3 +395,85 @@ def finish_picture(pic, dbk_params=None, col_field=False, ref_frame=None):
         P(work.data_ptr() if work is not None else 0), P(col.data_ptr() if col is not None else 0),
         r8, s8, r16[0], r16[1], r16[2], s16[0], s16[1]), "hvx_hm_finish_picture")
     return work, col
+
+
+# ---------------------------------------------------------------------------------------------
+# SAO's picture-level host logic around hvx_sao_decide (TEncSampleAdaptiveOffset.cpp)
+# ---------------------------------------------------------------------------------------------
+SAO_CTX_MERGE, SAO_CTX_TYPE = 181, 182  # m_cSaoMergeSCModel / m_cSaoTypeIdxSCModel in TEncSbac's context order
+
+
+def sao_slice_enabled(layer, disabled_rate, rate=0.75, rate_chroma=0.5):
+    """decidePicParams (:332): SAO on/off per component (Y, Cb, Cr) for a picture at temporal layer
+    `layer`, from the SAO-off CTU rates of the last picture of the layer below (disabled_rate [3, 7])."""
+    dr = np.asarray(disabled_rate, np.float64).reshape(3, 7)
+    en = [1, 1, 1]
+    for k in range(3):
+        if rate > 0.0:
+            if rate_chroma > 0.0:
+                if layer > 0 and dr[k, layer - 1] > (rate if k == 0 else rate_chroma):
+                    en[k] = 0
+            elif layer > 0 and dr[0, 0] > rate:
+                en[k] = 0
+    return en
+
+
+def sao_update_rates(layer, recon, disabled_rate, rate=0.75, rate_chroma=0.5):
+    """decideBlkParams' SAO-off rate update (:861-888) from a picture's applied parameters (SAO_CTU
+    records); returns the new [3, 7] array."""
+    dr = np.array(np.asarray(disabled_rate, np.float64).reshape(3, 7))
+    if not rate > 0.0:
+        return dr
+    r = np.asarray(recon).view(_abi.SAO_CTU)
+    off = [int((r["comp"][:, k]["type"] < 0).sum()) for k in range(3)]
+    n = len(r)
+    if rate_chroma > 0.0:
+        for k in range(3):
+            dr[k, layer] = off[k] / n
+    elif layer == 0:
+        dr[0, 0] = (off[0] + off[1] + off[2]) / (n * 3)
+    return dr
+
+
+def sao_picture(pic, layer, disabled_rate, slice_type, qp, rate=0.75, rate_chroma=0.5, slice_ctus=0, test_off=0,
+                sao_states=None):
+    """SAOProcess (TEncGOP.cpp:1500) on a decided, deblocked DevicePicture, all on the device:
+    hvx_sao_stats of the reconstruction against the original, decidePicParams on the host
+    (sao_slice_enabled), hvx_sao_decide (the RD decision from resetEntropy's SAO states at the
+    slice type / QP -- or sao_states, the slice-start states of the two SAO contexts, when the slice
+    used the other initialisation table -- the slice lambdas = the TrQuant lambdas), hvx_sao_apply into the picture's
+    reconstruction.  Returns (the new SAO-off rates [3, 7], coded [nctu, 3, 8], applied SAO_CTU,
+    slice-enabled flags)."""
+    import torch
+    from . import hvx
+    w, h, n = pic.w, pic.h, pic.wc * pic.hc
+    dev = pic.ctus_t.device
+    s = pic.struct
+    org = [(pic.org_t[0].data_ptr(), s.org_stride[0]), (pic.org_t[1].data_ptr(), s.org_stride[1]),
+           (pic.org_t[2].data_ptr(), s.org_stride[1])]
+    src_t = [t.clone() for t in pic.rec_t]  # offsetCTU reads SAOProcess's copy of the deblocked picture
+    src = [(src_t[c].data_ptr(), s.rec_stride[1 if c else 0]) for c in range(3)]
+    dst = [(pic.rec_t[c].data_ptr(), s.rec_stride[1 if c else 0]) for c in range(3)]
+    stats = torch.empty(n * 15 * _abi.SAO_STAT.itemsize, dtype=torch.uint8, device=dev)
+    hvx.sao_stats(org, src, w, h, stats)
+    en = sao_slice_enabled(layer, disabled_rate, rate, rate_chroma)
+    init = _abi.load_ctx_init_states()[slice_type, qp]
+    eb = torch.from_numpy(_abi.load_entropy_bits().astype(np.int32)).to(dev)
+    coded = torch.zeros((n, 3, 8), dtype=torch.int32, device=dev)
+    recon = torch.zeros(n * _abi.SAO_CTU.itemsize, dtype=torch.uint8, device=dev)
+    en_out = torch.zeros(3, dtype=torch.int32, device=dev)
+    tot = torch.zeros(1, dtype=torch.float64, device=dev)
+    j = np.zeros(1, _abi.SAO_DECIDE_JOB)
+    j["pic_w"], j["pic_h"], j["slice_ctus"], j["test_off"] = w, h, slice_ctus, test_off
+    j["slice_enabled"], j["frac_lo"] = en, 0
+    j["sao_states"] = [init[SAO_CTX_MERGE], init[SAO_CTX_TYPE]] if sao_states is None else list(sao_states)
+    j["lambda"] = [s.tq_lambda[0], s.tq_lambda[1], s.tq_lambda[2]]
+    j["stats"], j["entropy_bits"], j["coded"] = stats.data_ptr(), eb.data_ptr(), coded.data_ptr()
+    j["recon"], j["slice_enabled_out"], j["total_cost"] = recon.data_ptr(), en_out.data_ptr(), tot.data_ptr()
+    jt = torch.from_numpy(j.view(np.uint8).reshape(-1).copy()).to(dev)
+    hvx.sao_decide(jt, 1)
+    hvx.sao_apply(src, dst, w, h, recon)
+    torch.cuda.synchronize()
+    rec_h = recon.cpu().numpy().view(_abi.SAO_CTU)
+    return (sao_update_rates(layer, rec_h, disabled_rate, rate, rate_chroma), coded.cpu().numpy(), rec_h,
+            list(en_out.cpu().numpy()))

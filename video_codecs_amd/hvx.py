@@ -49,7 +49,7 @@ def lib():
             "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
             "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_coeff_write_batch": [P, P, P, P, P, I, P, P, P, P, I, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P],
             "hvx_intra_pred_batch": [P, P, I, P, I, P, P, P], "hvx_deblock": [P, P, I, P, P, I, P, P, P, P], "hvx_sao_stats": [P, P, P, P, I, I, P, P, P, I, I, I, I, P], "hvx_sao_apply": [P, P, P, P, I, I, P, P, P, I, I, I, I, P], "hvx_intra_search_batch": [P, P, P, I, P, I, P, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
-            "hvx_free": [P, P], "hvx_hm_state_size": [ctypes.POINTER(ctypes.c_size_t)], "hvx_hm_compress": [P, P, I, P, I, I, P, P, P, P], "hvx_hm_job_status": [P, P, I, P], "hvx_hm_finish_picture": [P, P, P, P, P, P, I, P, P, P, I, I], "hvx_upload": [P, P, P, ctypes.c_size_t], "hvx_download": [P, P, P, ctypes.c_size_t],
+            "hvx_free": [P, P], "hvx_hm_state_size": [ctypes.POINTER(ctypes.c_size_t)], "hvx_hm_compress": [P, P, I, P, I, I, P, P, P, P], "hvx_hm_job_status": [P, P, I, P], "hvx_hm_finish_picture": [P, P, P, P, P, P, I, P, P, P, I, I], "hvx_sao_decide": [P, P, I], "hvx_upload": [P, P, P, ctypes.c_size_t], "hvx_download": [P, P, P, ctypes.c_size_t],
         }.items():
             f = getattr(L, name)
             f.argtypes = args
@@ -257,6 +257,12 @@ def sao_apply(src, dst, pic_w, pic_h, params):
     v = ctypes.c_void_p
     _check(lib().hvx_sao_apply(context(), v(sy), v(scb), v(scr), int(sys_), int(scs), v(dy), v(dcb), v(dcr), int(dys),
                                int(dcs), int(pic_w), int(pic_h), _ptr(params)), "hvx_sao_apply")
+
+
+def sao_decide(jobs_t, n_jobs):
+    """hvx_sao_decide: n_jobs pictures' SAO RD decisions (jobs_t = device tensor of
+    _abi.SAO_DECIDE_JOB records whose pointers are device pointers)."""
+    _check(lib().hvx_sao_decide(context(), _ptr(jobs_t), int(n_jobs)), "hvx_sao_decide")
 
 
 def plane_from_pel(pel, pel_stride, width, height, plane):
