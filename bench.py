@@ -441,6 +441,33 @@ def slice_mode0_measure(W, H, chains=2040, distinct=16, nref=4, base_qp=32, warm
             "ctus_per_s": round(chains / sec, 2), "ms_per_step": round(sec * 1e3, 1), "wall_ms_per_step": round(wall * 1e3, 1)}
 
 
+def hm_1080p_measure(pics=128, nref=4, base_qp=32, warmup=1, steps=1):
+    """Side figure (BASELINE configs 2/3 size): the headline's decision on 1080p random 4:2:0 P
+    pictures -- HmWorkload at 1920x1080, `pics` pictures x 16 chains (17 CTU rows, the partial 17th
+    chained after the 16th) = 2048 chains, one CTU per chain per step."""
+    import torch
+    work = HmWorkload(1920, 1080, pics, nref, base_qp, 1, rank=0)
+    out_rec = torch.zeros(work.slots * 6144, dtype=torch.uint8, device="cuda")
+    for _ in range(warmup):
+        work.step(out_rec)
+    torch.cuda.synchronize()
+    evs = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        work.step(out_rec, ev)
+        evs.append(ev)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    sec = sum(a.elapsed_time(b) for a, b in evs) / steps * 1e-3
+    n = work.n_jobs
+    del work, out_rec
+    torch.cuda.empty_cache()
+    return {"workload": "%d 1080p P pictures x %d row-slice chains, QP %d, %d refs (HM-exact decision, as the headline)" % (
+        pics, n // pics, base_qp + HM_QP_OFFSET, nref), "ctus_per_s": round(n / sec, 2), "ms_per_step": round(sec * 1e3, 1),
+        "wall_ms_per_step": round(wall * 1e3, 1)}
+
+
 def hm_cpu_port(work, threads, min_seconds=0.0):
     """The oracle's restatement (oracle/hvx_oracle_cu.c hvxo_hm_chains) on picture 0's slice
     chains -- the same CTUs the GPU decided in its warmup + timed steps, on `threads` host threads
@@ -704,6 +731,8 @@ def main():
                 out["config4_ra_ssim"] = ra_ssim_measure(W, H)
             if not args.no_slice0:
                 out["slice_mode0"] = slice_mode0_measure(W, H)
+            if not args.no_1080p:
+                out["hm_1080p"] = hm_1080p_measure()
         if reduced is not None:
             out["reduced_step"] = reduced
         print(json.dumps(out), flush=True)
