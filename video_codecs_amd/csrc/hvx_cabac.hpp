@@ -80,9 +80,10 @@ __device__ __forceinline__ int remain_bins(uint32_t symbol, int r, bool limited,
     }
     return (int)(prefix + 3 + suffix_len + r);
   }
-  int len = r;
-  uint32_t cn = symbol - (3u << r);
-  while (cn >= (1u << len)) cn -= (1u << (len++));
+  // the reference's loop `while (cn >= (1 << len)) cn -= 1 << len++` from len = r runs
+  // floor(log2(((symbol - (3 << r)) >> r) + 1)) times (the closed form of rd_ic_rate, hvx_tu.hpp)
+  const uint32_t v = ((symbol - (3u << r)) >> r) + 1;
+  const int len = r + (31 - __clz(v));
   return 3 + len + 1 - r + len;
 }
 

@@ -1482,10 +1482,10 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
 #else
   // the mask-driven walk for every size (a third walk instance in this function measured 20%
   // slower overall: register pressure)
-#ifdef HM_WALK_SERIAL
-  coeff_count_staged(d, env, ls, L);
+#ifdef HM_WALK_ROUNDS
+  coeff_count_par(d, env, ls, L);  // measured no faster than the serial walk
 #else
-  coeff_count_par(d, env, ls, L);
+  coeff_count_staged(d, env, ls, L);
 #endif
 #endif
 #ifdef HM_REG_WALK
