@@ -90,7 +90,7 @@ def device_picture(g, pic, chained, entropy_bits, rd_metric=0, eta=1.0):
     return hm.DevicePicture(org, refs, params, entropy_bits, rec=rec, ctus=ctus, col_field=col)
 
 
-def run_capture(name, mode, pics=None, stage=0, rd_metric=0, eta=1.0):
+def run_capture(name, mode, pics=None, stage=0, rd_metric=0, eta=1.0, serial=False):
     """Decide the captured pictures on the device.  mode 0: every CTU as its own job from the
     reference's entry state and neighbourhood; mode 1: one chained job per picture (per row slice
     for the row-sliced capture); mode 2: one chained job per picture across its row slices.  Returns
@@ -130,6 +130,11 @@ def run_capture(name, mode, pics=None, stage=0, rd_metric=0, eta=1.0):
         slot += n
     eng = hm.Engine(dps)
     LAST_ENGINE[:] = [eng]
+    if serial:  # debugging aid: one launch per job, so that a faulting job is the last one announced
+        for i, j in enumerate(jobs):
+            print("hm_cases: launching job %d of %d" % (i, len(jobs)), flush=True)
+            out = eng.compress(j, slot)
+        return g, plan, out
     out = eng.compress(np.concatenate(jobs), slot)
     return g, plan, out
 

@@ -1,6 +1,6 @@
 """Debugging aid: decide the captured CTUs with a libhvx build selected by HVX_LIB_PATH (e.g. an
 HM_CHECKS build) and print the first failed engine check per job (State.dbg: code, a, b) and the
-first mismatches against the reference.  python -m tests.hm_debug [capture] [mode] [pics]"""
+first mismatches against the reference.  python -m tests.hm_debug [capture] [mode] [pics] [serial]"""
 import sys
 
 import numpy as np
@@ -12,7 +12,8 @@ def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "ctu_ldp_rand.bin"
     mode = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     pics = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else None
-    g, plan, out = hm_cases.run_capture(name, mode, pics)
+    serial = len(sys.argv) > 4 and sys.argv[4] == "serial"
+    g, plan, out = hm_cases.run_capture(name, mode, pics, serial=serial)
     dbg = hm_cases.LAST_ENGINE[0].last_debug
     bad_jobs = np.flatnonzero(dbg[:, 0])
     print("%s mode %d: %d jobs, %d with a failed check" % (name, mode, len(dbg), len(bad_jobs)))

@@ -298,6 +298,13 @@ struct ProfScope {
 #endif
 // HM_CHECKS builds validate the indices and sample positions below, record the first violation
 // in E.dbg and keep the access inside its buffer (a debugging aid; off in the product build)
+// HM_TRACE builds print the chain's progress from lane 0 (a debugging aid for faults: the last
+// line of a job before the fault names the step it died in)
+#ifdef HM_TRACE
+#define HM_TR(tag, a, b) do { if (lid() == 0) printf("HMTRACE j%d ctu%d %s %d %d\n", (int)blockIdx.x, hm_e.ctu_addr, (tag), (int)(a), (int)(b)); } while (0)
+#else
+#define HM_TR(tag, a, b) ((void)0)
+#endif
 #ifdef HM_CHECKS
 __device__ __noinline__ void hm_fail(int code, int a, int b) {
   if (E.dbg[0] == 0) { E.dbg[0] = code; E.dbg[1] = a; E.dbg[2] = b; }
@@ -2274,6 +2281,7 @@ __device__ void estimate_inter_residual_qt(Cu *cu, Yuv *resi, double *rd, uint32
   int32_t abs_sum[3] = {0, 0, 0};
   int best_mode[3] = {0, 0, 0};
   const int layer = qt_layer(l2);
+  HM_TR("rqt", LV * 100 + l2, rel);
   cload(RD(depth, CI_QT_TRAFO_ROOT), E.cur);
   if (check_full) {
     double min_cost[3] = {kMaxDouble, kMaxDouble, kMaxDouble};
@@ -2303,6 +2311,7 @@ __device__ void estimate_inter_residual_qt(Cu *cu, Yuv *resi, double *rd, uint32
           blk_copy(best_res, w, qres, qs, w, h);
         }
         const int32_t cur_abs = transform_tu(cu, t, comp, pres, ystride(comp), cur_coef);
+        HM_TR("rqt_tf", comp * 10 + mode, cur_abs);
         int32_t cabs = cur_abs;
         if (first || cur_abs == 0) {
           non_dist = weigh(sse_wave(pres, ystride(comp), nullptr, 0, w, h), comp);
@@ -2319,7 +2328,9 @@ __device__ void estimate_inter_residual_qt(Cu *cu, Yuv *resi, double *rd, uint32
           code_qt_cbf(cu, t, comp, 1);
           code_coeff_nxn(cu, t, comp, cur_coef);
           cur_bits = written_bits();
+          HM_TR("rqt_cnt", comp * 10 + mode, cur_bits);
           inv_transform_tu(cu, t, comp, cur_coef, qres, qs);
+          HM_TR("rqt_inv", comp * 10 + mode, 0);
           cur_dist = dist_part(qres, qs, pres, ystride(comp), w, h, comp);
           cur_cost = rd_cost(cur_bits, cur_dist);
         } else if (mode == 1) {
@@ -2344,6 +2355,7 @@ __device__ void estimate_inter_residual_qt(Cu *cu, Yuv *resi, double *rd, uint32
       }
       set_ts_range(cu, comp, crel, np, best_mode[comp]);
       set_cbf_range(cu, comp, crel, np, (abs_sum[comp] > 0 ? 1 : 0) << trmode);
+      HM_TR("rqt_comp", comp, abs_sum[comp]);
     }
     cload(E.cur, RD(depth, CI_QT_TRAFO_ROOT));
     reset_bits();
@@ -2605,7 +2617,10 @@ __device__ void motion_estimation(Cu *cu, int ps, int pu, int list, int ref_idx,
   wsync();
   const hvx_me_result r = ms.r;
   wsync();
-  HMC(r.mv_x >= -4 * 80 && r.mv_y >= -4 * 80 && r.mv_x < 4 * (E.P.w + 80) && r.mv_y < 4 * (E.P.h + 80), 9, r.mv_x, r.mv_y);
+  // the block the result points at lies inside the reference plane's margin (HVX_PLANE_MARGIN 80)
+  HMC(4 * xp + r.mv_x >= -4 * 80 && 4 * yp + r.mv_y >= -4 * 80 && 4 * (xp + w) + r.mv_x <= 4 * (E.P.w + 80) &&
+          4 * (yp + h) + r.mv_y <= 4 * (E.P.h + 80),
+      9, r.mv_x, r.mv_y);
   if (ps == SIZE_2Nx2N) { E.S->int2n[list][ref_idx][0] = (int16_t)r.mv_int_x; E.S->int2n[list][ref_idx][1] = (int16_t)r.mv_int_y; }
   mv[0] = (int16_t)r.mv_x; mv[1] = (int16_t)r.mv_y;
   bits = r.bits;
@@ -2751,6 +2766,7 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
           uint32_t bt = mb[l] + ref_bits(r, nref), ct;
           int pidx, pnum;
           est_mvp_amvp(cu, ps, pu, org, l, r, Q.amvp[l][r], Q.mvpred[l][r], pidx, pnum, bip_dist_temp);
+          HM_TR("amvp", pu * 100 + l * 10 + r, pidx);
           pu_set(cu, ps, pu, PU_MVP_IDX, l, pidx);
           pu_set(cu, ps, pu, PU_MVP_NUM, l, pnum);
           if (E.P.mvd_l1_zero && l == 1 && bip_dist_temp < best_bip_dist) {
@@ -2768,6 +2784,7 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
             ct += mv_cost_bits(bt);
           } else {
             motion_estimation(cu, ps, pu, l, r, Q.mvpred[l][r], Q.mvtemp[l][r], bt, ct);
+            HM_TR("me", pu * 100 + l * 10 + r, Q.mvtemp[l][r][0] * 10000 + Q.mvtemp[l][r][1]);
           }
           check_best_mvp(Q.amvp[l][r], Q.mvtemp[l][r], Q.mvpred[l][r], pidx, bt, ct);
           Q.mvp_idx[l][r] = pidx; Q.mvp_num[l][r] = pnum;
@@ -2898,6 +2915,7 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
         const uint32_t err = wave_satd(yaddr(org, 0, xp - cu->x, yp - cu->y), ystride(0),
                                        yaddr(&E.S->tmp_yuv_pred, 0, xp - cu->x, yp - cu->y), ystride(0), w, h);
         me_cost = err + mv_cost_bits(me_bits);
+        HM_TR("p_satd", pu, me_cost);
       }
       const Part save = cu->p[a];
       int mrg_dir = 0, mrg_idx = 0;
@@ -2905,6 +2923,7 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
       uint32_t mrg_cost = kMaxU32;
       MergeList ml;
       merge_estimation(cu, ps, pu, org, mrg_dir, mrg, mrg_idx, mrg_cost, ml);
+      HM_TR("p_mrg", pu, mrg_idx);
       if (mrg_cost < me_cost) {
         pu_set(cu, ps, pu, PU_MERGE, 0, 1);
         pu_set(cu, ps, pu, PU_MERGE_IDX, 0, mrg_idx);
@@ -2923,6 +2942,7 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
       }
     }
     mc_pu(cu, ps, pu, pred);
+    HM_TR("p_mc", pu, ps);
   }
 }
 
@@ -3638,6 +3658,7 @@ __device__ void check_rd_merge2nx2n(int depth) {
   MergeList m;
   merge_candidates(TEMP(depth), SIZE_2Nx2N, 0, m);
   const int n = m.n;
+  HM_TR("m_cands", n, depth);
   int buf = 0;  // mergeCandBuffer bits
   int best_is_skip = 0;
   for (int nores = 0; nores < 2; nores++) {
@@ -3659,9 +3680,12 @@ __device__ void check_rd_merge2nx2n(int depth) {
         p.mv[1][0] = f1.mv[0]; p.mv[1][1] = f1.mv[1]; p.ref[1] = (int8_t)f1.ref;
       }
       wsync();
+      HM_TR("m_set", k, nores);
       mc_cu(tmp, YB(Y_PRED_TEMP, depth));
+      HM_TR("m_mc", k, nores);
       enc_res_rd_inter(tmp, YB(Y_ORIG, depth), YB(Y_PRED_TEMP, depth), YB(Y_RESI_TEMP, depth), YB(Y_RESI_BEST, depth),
                        YB(Y_RECO_TEMP, depth), nores != 0);
+      HM_TR("m_rqt", k, nores);
       if (nores == 0 && !cu_qt_root_cbf(tmp, 0)) buf |= 1 << k;
       check_best_mode(depth);
       reinit_temp(depth);
@@ -3675,6 +3699,7 @@ __device__ void check_rd_inter(int depth, int ps, int use_mrg) {
   cu_set_all(tmp, F_PRED, MODE_INTER);
   tmp->merge_amp = 1;
   pred_inter_search(tmp, YB(Y_ORIG, depth), YB(Y_PRED_TEMP, depth), use_mrg);
+  HM_TR("i_pis", ps, depth);
   enc_res_rd_inter(tmp, YB(Y_ORIG, depth), YB(Y_PRED_TEMP, depth), YB(Y_RESI_TEMP, depth), YB(Y_RESI_BEST, depth),
                    YB(Y_RECO_TEMP, depth), 0);
   const double c = cu_cost(tmp->dssim, tmp->bits, tmp->dist);
@@ -3731,6 +3756,7 @@ __device__ void compress_cu(int parent_ps) {
   const int depth = D;
   E.yw = 64 >> D;
   Cu *best = BEST(depth);
+  HM_TR("cu", best->x * 10000 + best->y, D);
   copy_org_to_yuv(YB(Y_ORIG, depth), best);
   int boundary = 0;
   const int rx = best->x + best->width - 1, by = best->y + best->width - 1;
@@ -3739,38 +3765,40 @@ __device__ void compress_cu(int parent_ps) {
     reinit_temp(depth);
     if (E.P.slice_type != I_SLICE) {
       check_rd_merge2nx2n(depth);
+      HM_TR("merge", best->x * 10000 + best->y, D);
       reinit_temp(depth);
-      check_rd_inter(depth, SIZE_2Nx2N, 0);
+      check_rd_inter(depth, SIZE_2Nx2N, 0); HM_TR("inter", SIZE_2Nx2N, D);
       reinit_temp(depth);
     }
     reinit_temp(depth);
     if (E.P.slice_type != I_SLICE) {
-      check_rd_inter(depth, SIZE_Nx2N, 0);
+      check_rd_inter(depth, SIZE_Nx2N, 0); HM_TR("inter", SIZE_Nx2N, D);
       reinit_temp(depth);
-      check_rd_inter(depth, SIZE_2NxN, 0);
+      check_rd_inter(depth, SIZE_2NxN, 0); HM_TR("inter", SIZE_2NxN, D);
       reinit_temp(depth);
       if (E.P.amp && depth < 3) {
         int hor = 0, ver = 0, mhor = 0, mver = 0;
         derive_test_mode_amp(BEST(depth), parent_ps, hor, ver, mhor, mver);
         if (hor) {
-          check_rd_inter(depth, SIZE_2NxnU, 0); reinit_temp(depth);
-          check_rd_inter(depth, SIZE_2NxnD, 0); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_2NxnU, 0); HM_TR("inter", SIZE_2NxnU, D); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_2NxnD, 0); HM_TR("inter", SIZE_2NxnD, D); reinit_temp(depth);
         } else if (mhor) {
-          check_rd_inter(depth, SIZE_2NxnU, 1); reinit_temp(depth);
-          check_rd_inter(depth, SIZE_2NxnD, 1); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_2NxnU, 1); HM_TR("inter", SIZE_2NxnU, D); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_2NxnD, 1); HM_TR("inter", SIZE_2NxnD, D); reinit_temp(depth);
         }
         if (ver) {
-          check_rd_inter(depth, SIZE_nLx2N, 0); reinit_temp(depth);
-          check_rd_inter(depth, SIZE_nRx2N, 0); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_nLx2N, 0); HM_TR("inter", SIZE_nLx2N, D); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_nRx2N, 0); HM_TR("inter", SIZE_nRx2N, D); reinit_temp(depth);
         } else if (mver) {
-          check_rd_inter(depth, SIZE_nLx2N, 1); reinit_temp(depth);
-          check_rd_inter(depth, SIZE_nRx2N, 1); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_nLx2N, 1); HM_TR("inter", SIZE_nLx2N, D); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_nRx2N, 1); HM_TR("inter", SIZE_nRx2N, D); reinit_temp(depth);
         }
       }
     }
     best = BEST(depth);
     if (E.P.slice_type == I_SLICE || (best->p[0].cbf[0] || best->p[0].cbf[1] || best->p[0].cbf[2])) {
       check_rd_intra(depth, SIZE_2Nx2N);
+      HM_TR("intra", 0, D);
       reinit_temp(depth);
       if (depth == 3 && TEMP(depth)->width > 4) {
         check_rd_intra(depth, SIZE_NxN);
@@ -3828,6 +3856,7 @@ __device__ void compress_cu(int parent_ps) {
   }
   cu_copy_to_pic(BEST(depth));
   yuv_to_pic(YB(Y_RECO_BEST, depth), BEST(depth));
+  HM_TR("cu_end", 0, D);
 }
 
 // ============================================================================================
@@ -3932,6 +3961,7 @@ __device__ void compress_ctu(int addr, const Coder *entry_g, int entry_in_lds, C
     compress_cu<0>(SIZE_NONE);
   }
   HM_STAGE(5);
+  HM_TR("decided", 0, 0);
   if (HM_STOPPED) return;
   // encodeCtu on m_pppcRDSbacCoder[0][CI_CURR_BEST] after resetBits (TEncSlice.cpp:821-828)
   E.cur = RD(0, CI_CURR_BEST);
@@ -4055,6 +4085,7 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
       slice_first = addr == s0;
     }
     compress_ctu(addr, &job.entry, (k > 0 || resume) && !slice_first, out_coder ? &out_coder[slot] : nullptr);
+    HM_TR("ctu_done", addr, k);
     // the next CTU starts from this CTU's encodeCtu state (m_pppcRDSbacCoder[0][CI_CURR_BEST])
     // which compress_ctu left in coder RD(0, CI_CURR_BEST)
     copy_words(&S->carry, &hm_e.cod[RD(0, CI_CURR_BEST)], (int)sizeof(Coder));
