@@ -564,6 +564,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
       uint32_t best = 0;
       int stv_l = 0;
       for (int round = 0;; round++) {
+#ifdef HVX_RDOQ_SCAN_PREDICT
         {
           int c1s = c1, c2s = c2;
           uint32_t c1is = c1_idx, c2is = c2_idx, rs = rice;
@@ -573,6 +574,36 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
             rd_step((uint32_t)rl((int)guess, pin), c1s, c2s, c1is, c2is, rs, persistent);
           }
         }
+#else
+        {
+          // rd_step's updates in closed form over the positions decided before this lane's (pins
+          // start .. pin+1): c1Idx / c2Idx count the levels >= 1 / > 1, c2 saturates at 2, c1 is 0
+          // after a level > 1 and otherwise counts the 1s up to 3 (from a nonzero start); the Rice
+          // parameter can only move at a level > 3 (a level > 3 << rice is always >= base), so it
+          // is scanned over those positions alone
+          const int pin_l = lane & 15;
+          const uint32_t mdec = (2u << start) - 1u;
+          const uint32_t above = mdec & ~((2u << pin_l) - 1u);
+          const uint32_t nzg = (uint32_t)__ballot(lane < 16 && guess >= 1u) & mdec;
+          const uint32_t g1g = (uint32_t)__ballot(lane < 16 && guess > 1u) & mdec;
+          const int n_nz = __popc(nzg & above), n_g1 = __popc(g1g & above);
+          const int c2s = c2 + n_g1 < 2 ? c2 + n_g1 : 2;
+          const int c1n = c1 + (n_nz - n_g1);
+          const int c1s = n_g1 ? 0 : (c1 == 0 ? 0 : (c1n < 3 ? c1n : 3));
+          uint32_t rs = rice;
+          uint32_t big = (uint32_t)__ballot(lane < 16 && guess > 3u) & mdec;
+          if (big) {
+            uint32_t r = rice;
+            while (big) {
+              const int p = 31 - (int)__clz(big);
+              big &= ~(1u << p);
+              if ((uint32_t)rl((int)guess, p) > 3u * (1u << r)) r = persistent ? r + 1 : (r + 1 < 4 ? r + 1 : 4);
+              if (pin_l < p) rs = r;
+            }
+          }
+          pst_l = c1s | (c2s << 2) | ((int)(c1_idx + n_nz) << 4) | ((int)(c2_idx + n_g1) << 9) | ((int)rs << 14);
+        }
+#endif
         const int c1p = pst_l & 3, c2p = (pst_l >> 2) & 3;
         const uint32_t c1ip = (uint32_t)(pst_l >> 4) & 31, c2ip = (uint32_t)(pst_l >> 9) & 31, rp = (uint32_t)(pst_l >> 14) & 31;
         const int ctx_one_l = 4 * (int)ctx_set + c1p, ctx_abs_l = (int)ctx_set + c2p;
