@@ -1204,6 +1204,34 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
       if (gt2) escape = true;
     }
     L.ep((be_valid && hidden) ? nnz - 1 : nnz);  // signs (the first one hidden)
+#ifndef HM_ESC_SERIAL
+    if (escape) {
+      // the escape codes' bin counts lane-parallel (bypass bins: only their total counts): a level's
+      // base (idx < 8 ? 2 + first2 : 1) from the set bits before it; the Rice parameter (from 0, no
+      // persistent adaptation in the engine's tool set) moves only at a level > 3 << rice, which is
+      // always >= base, so it is scanned over the levels > 3 alone
+      const int pin_l = l & 15;
+      const uint32_t before = m16 & ~((2u << pin_l) - 1u);
+      const uint32_t ge2 = (uint32_t)__ballot(l < 16 && av_l >= 2);
+      const int base_l = __popc(before) < 8 ? 2 + ((ge2 & before) ? 0 : 1) : 1;
+      int rice_l = 0;
+      uint32_t big = (uint32_t)__ballot(l < 16 && av_l > 3);
+      if (big) {
+        int r = 0;
+        while (big) {
+          const int p = 31 - __clz(big);
+          big &= ~(1u << p);
+          if (__builtin_amdgcn_readlane(av_l, p) > (3 << r)) r = r + 1 < 4 ? r + 1 : 4;
+          if (pin_l < p) rice_l = r;
+        }
+      }
+      const uint32_t nb = l < 16 && av_l >= base_l
+                              ? (uint32_t)cab::remain_bins((uint32_t)(av_l - base_l), rice_l, d.extended_precision != 0,
+                                                           d.max_log2_tr_range)
+                              : 0u;
+      L.ep((int)wave_sum_u32(nb));
+    }
+#else
     if (escape) {  // Rice parameter from 0 (no persistent adaptation in the engine's tool set)
       int rice = 0, first2 = 1, idx = 0;
       uint32_t all = m16;
@@ -1220,6 +1248,7 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
         idx++;
       }
     }
+#endif
   }
   return num_sig;
 }

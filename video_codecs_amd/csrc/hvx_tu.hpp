@@ -301,9 +301,11 @@ __device__ __forceinline__ double rld(double v, int lane) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-// speculative rounds of the RDOQ reverse scan before the serial fallback (tu_rdoq)
+// speculative rounds of the RDOQ reverse scan before the serial fallback (tu_rdoq).  Each round
+// makes at least one more position exact (the first mispredicted one is decided from an exact
+// state), so 16 rounds always finish a group: the serial fallback is then never reached
 #ifndef HVX_RDOQ_ROUNDS
-#define HVX_RDOQ_ROUNDS 3
+#define HVX_RDOQ_ROUNDS 16
 #endif
 // The c1 / c2 / Rice / c1Idx / c2Idx update after a position's decision (:2281-2330)
 __device__ __forceinline__ void rd_step(uint32_t level, int &c1, int &c2, uint32_t &c1_idx, uint32_t &c2_idx, uint32_t &rice,
