@@ -289,12 +289,20 @@ struct ProfScope {
   }
 };
 #define HM_PROF(c) ProfScope prof_scope_(c)
+#ifdef HM_PROF_WALK  // the walk's phases in slots 12..15 (instead of the forward transform by size)
+#define HM_WT0(v) uint64_t v = __builtin_amdgcn_s_memtime()
+#define HM_WTADD(k, v) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); hm_e.prof[0][12 + (k)] += n_ - (v); hm_e.prof[1][12 + (k)] += 1; v = n_; } while (0)
+#endif
 #define HM_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define HM_TADD(cat, v) (hm_e.prof[0][(cat)] += __builtin_amdgcn_s_memtime() - (v), hm_e.prof[1][(cat)] += 1)
 #else
 #define HM_T0(v) ((void)0)
 #define HM_TADD(cat, v) ((void)0)
 #define HM_PROF(c) ((void)0)
+#endif
+#ifndef HM_WT0
+#define HM_WT0(v) ((void)0)
+#define HM_WTADD(k, v) ((void)0)
 #endif
 // HM_CHECKS builds validate the indices and sample positions below, record the first violation
 // in E.dbg and keep the access inside its buffer (a debugging aid; off in the product build)
@@ -1104,6 +1112,7 @@ template <class C>
 __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, const int16_t *ls, C &L) {
   const int n = d.width, lw = cab::log2_tu(n), wg = n >> 2, ncg = wg * wg, nn = n * n;
   const int ch = d.comp ? 1 : 0, l = lid();
+  HM_WT0(wt_);
   // significant-CG map, count and last position: one ballot per 64 scan positions (4 groups)
   uint64_t cgm = 0;
   int num_sig = 0, scan_last = -1;
@@ -1138,6 +1147,7 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
     if (gx > 3) L.ep((gx - 2) >> 1);
     if (gy > 3) L.ep((gy - 2) >> 1);
   }
+  HM_WTADD(0, wt_);
   const int base_cg = cab::kSigCG + ch * 2, base_sig = cab::kSig + (ch ? 28 : 0);
   const int last_set = scan_last >> 4, last_pin = scan_last & 15;
   int c1 = 1;
@@ -1173,6 +1183,7 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
       }
     }
     const int nnz = __popc(m16);
+    HM_WTADD(1, wt_);
     if (nnz == 0) continue;
     // greater-1 / greater-2 over the group's non-zero levels in reverse scan order (first 8)
     const int last_nz = 31 - __clz(m16), first_nz = __builtin_ctz(m16);
@@ -1203,6 +1214,7 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
       L.bin(cab::kAbs + set, gt2);
       if (gt2) escape = true;
     }
+    HM_WTADD(2, wt_);
     L.ep((be_valid && hidden) ? nnz - 1 : nnz);  // signs (the first one hidden)
 #ifndef HM_ESC_SERIAL
     if (escape) {
@@ -1249,6 +1261,7 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
       }
     }
 #endif
+    HM_WTADD(3, wt_);
   }
   return num_sig;
 }
@@ -1823,7 +1836,7 @@ __device__ __forceinline__ TuSmem<L> &tu_smem() {
 template <int L>
 __device__ int32_t tu_fwd_l(const hvx_tu_desc &d, const int16_t *resi, int rs, int16_t *coef) {
   HM_PROF(PR_TUF);
-#ifdef HM_PROFILE
+#if defined(HM_PROFILE) && !defined(HM_PROF_WALK) && !defined(HVX_RDOQ_PROF_SUB)
   ProfScope prof_size_(12 + L);
 #endif
   TuSmem<L> &s = tu_smem<L>();

@@ -405,6 +405,13 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
 #else
 #define HVX_RDOQ_PHASE(k) ((void)0)
 #endif
+// sub-phases of the reverse scan (profile builds with HVX_RDOQ_PROF_SUB: slots 12..15)
+#if defined(HVX_TU_PROF_HOOK) && defined(HVX_RDOQ_PROF_SUB)
+  uint64_t t_sb = __builtin_amdgcn_s_memtime();
+#define HVX_RDOQ_SUB(k) do { const uint64_t t_n = __builtin_amdgcn_s_memtime(); HVX_TU_PROF_HOOK(12 + (k), t_n - t_sb); t_sb = t_n; } while (0)
+#else
+#define HVX_RDOQ_SUB(k) ((void)0)
+#endif
   // ---- A. per-coefficient work across lanes ----
   bool anyq = false;
   for (int sp = lane; sp < NN; sp += HVX_WAVE) {
@@ -434,6 +441,9 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   __syncthreads();
 
   HVX_RDOQ_PHASE(0);
+#if defined(HVX_TU_PROF_HOOK) && defined(HVX_RDOQ_PROF_SUB)
+  t_sb = __builtin_amdgcn_s_memtime();
+#endif
   // ---- B. reverse-scan decisions (wave-uniform) ----
   const uint32_t rice0 = (uint32_t)d.golomb_rice_stat / 4;
   const bool persistent = d.persistent_rice != 0;
@@ -531,6 +541,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
         if (lane == pin) { o_lev = (int32_t)best; o_st = stv; }
       }
     };
+    HVX_RDOQ_SUB(0);
     // the decided positions: from the last significant one (its group) or the whole group
     int start = 15;
     if (last < 0) {
@@ -655,6 +666,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
         if (f <= 0 || round == HVX_RDOQ_ROUNDS - 1) break;
         guess = best;
       }
+      HVX_RDOQ_SUB(1);
       const double dlt_l = cost - cost_sig;  // coded_ld's term (the serial pass's cc - cs)
       const uint32_t nzm = (uint32_t)__ballot(lane <= start && best != 0);
       const int lo = f < 0 ? 0 : f;
@@ -686,6 +698,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
         if (f > 0) serial_from(f - 1);
       }
 #endif
+      HVX_RDOQ_SUB(2);
       if (cgp > 0) {  // the next group's context set and counters (:2262-2266)
         ctx_set = (comp ? 4 : 0) + ((comp == 0 && cgp - 1 > 0) ? 2 : 0) + (c1 == 0 ? 1 : 0);
         c1 = 1; c2 = 0; c1_idx = 0; c2_idx = 0;
@@ -728,6 +741,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
       st[cgp * 16 + lane] = o_st;
     }
     if (lane == 0) s.cgr[cgp] = cgrate;
+    HVX_RDOQ_SUB(3);
   }
   __syncthreads();
 
