@@ -121,7 +121,7 @@ struct IntraScratch {
 constexpr int kMemoK = 16, kMemoDw = 37, kMemoDw0 = 10;
 struct CoefMemo {
   uint32_t key;                   // valid | width | channel | scan | transform skip
-  uint32_t pad_;
+  uint32_t hash;                  // memo_hash of the entry's levels and masked context states
   uint64_t frac;
   uint32_t coef[32];              // the TU's levels as int16 pairs (TU-packed order)
   uint32_t before[kMemoDw], after[kMemoDw];
@@ -228,6 +228,10 @@ struct Enc {
   hvx_tu_desc td;        // the current TU's descriptor (tu_desc)
   Tu tstack[kTuStack];   // the live TU nodes (TuSlot), innermost last
   int tsp;
+#ifndef HM_MEMO_HBM
+  uint32_t memo_key[kMemoK], memo_hash[kMemoK];  // the count memo's index (S->memo keys / hashes)
+  int memo_next;
+#endif
   int yw;                // the width of the CU whose TComYuv buffers are in use (compress_cu<D>: 64 >> D)
   float ssim_t[192];     // HVX_RD_SSIM: the (1 - SSIM) terms of a CU's blocks (cu_dssim)
   int dbg[4];  // HM_CHECKS: first violated check (code, a, b) of the job
@@ -1446,33 +1450,50 @@ __device__ __forceinline__ uint32_t memo_mask(int ch, int k) {
   return m;
 }
 
+// the memo index's content hash: murmur3-mixed lane words (masked context-state dwords, packed
+// levels) summed over the wave
+__device__ __forceinline__ uint32_t memo_mix(uint32_t x) {
+  x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t memo_hash(uint32_t st_masked, uint32_t cf) {
+  const uint32_t l = (uint32_t)lid();
+  return wave_sum_u32(memo_mix(st_masked ^ (l * 0x9e3779b9u)) + memo_mix(cf ^ (l * 0x7f4a7c15u + 0x2545f491u)));
+}
 __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_t *coef) {
   HM_PROF(PR_COEF);
   HM_T0(t_desc);
   tu_desc(cu, t, comp);
   const hvx_tu_desc &d = E.td;
   HM_TADD(PR_COEF_DESC, t_desc);
-  // the memo (4x4 / 8x8 TUs): one load round for the keys, one per candidate entry
+  // the memo (4x4 / 8x8 TUs)
   const int ch = comp ? 1 : 0, l = lid();
   const bool memo_on = d.width <= 8;
-  uint32_t cur_st = 0, cur_cf = 0, mask = 0, key = 0;
+  uint32_t cur_st = 0, cur_cf = 0, mask = 0, key = 0, hash = 0;
   State *S = E.S;
   if (memo_on) {
     key = 0x8000u | (uint32_t)d.width | ((uint32_t)ch << 8) | ((uint32_t)d.scan_type << 10) | ((uint32_t)d.transform_skip << 12);
     const int ndw = d.width * d.width / 2;
     uint32_t *st32 = reinterpret_cast<uint32_t *>(E.cod[E.cur].st);
-    const uint32_t kk = l < kMemoK ? S->memo[l].key : 0u;
     if (l < kMemoDw) { cur_st = st32[kMemoDw0 + l]; mask = memo_mask(ch, l); }
     if (l < ndw) cur_cf = reinterpret_cast<const uint32_t *>(coef)[l];
+#ifdef HM_MEMO_HBM  // one HBM round for the keys, one per candidate entry
+    const uint32_t kk = l < kMemoK ? S->memo[l].key : 0u;
     uint64_t cand = __ballot(kk == key);
+#else
+    // the index in LDS: keys and a hash of the levels and masked context states; only an entry whose
+    // hash matches is read from HBM, and compared in full there (a hash is never trusted alone)
+    hash = memo_hash(cur_st & mask, cur_cf);
+    uint64_t cand = __ballot(l < kMemoK && E.memo_key[l < kMemoK ? l : 0] == key && E.memo_hash[l < kMemoK ? l : 0] == hash);
+#endif
     while (cand) {
       const int e = __builtin_ctzll(cand);
       cand &= cand - 1;
       const CoefMemo &m = S->memo[e];
+      const uint32_t after = l < kMemoDw ? m.after[l] : 0u;  // read with the comparands (one round)
+      const uint64_t f = m.frac;
       const bool diff = (l < kMemoDw && ((m.before[l] ^ cur_st) & mask)) || (l < ndw && m.coef[l] != cur_cf);
       if (__ballot(diff) == 0) {  // a repeat: replay its result
-        const uint32_t after = l < kMemoDw ? m.after[l] : 0u;
-        const uint64_t f = m.frac;
         wsync();
         if (l < kMemoDw) st32[kMemoDw0 + l] = (cur_st & ~mask) | (after & mask);
         if (l == 0) E.cod[E.cur].frac += f;
@@ -1492,7 +1513,20 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
 #endif
   const cab::ScanTables tab(d);
   if (lid() < (n >> 4)) E.u.cs.cg[lid()] = tab.scan_cg[lid()];
-  if (staged) {
+  if (memo_on) {
+    // 4x4 / 8x8: every level is already in cur_cf (two per lane, raster order): staged by a lane
+    // shuffle instead of a second read of the coefficients from the chain state
+    const int r = l < n ? scan[l] : 0;
+    const uint32_t v = (uint32_t)__shfl((int)cur_cf, r >> 1, HVX_WAVE);
+    if (l < n) {
+      ls[l] = (int16_t)(r & 1 ? v >> 16 : v & 0xffffu);
+      E.u.cs.ras[l] = (int16_t)r;
+      int sc = 0;
+#pragma unroll
+      for (int pat = 0; pat < 4; pat++) sc |= cab::sig_ctx(pat, tab.first_sig, tab.single, r, tab.lw, tab.ch) << (6 * pat);
+      E.u.cs.sig[l] = sc;
+    }
+  } else if (staged) {
     for (int i = lid(); i < n; i += 64) {
       const int r = scan[i];
       ls[i] = coef[r];
@@ -1547,12 +1581,25 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
   HM_TADD(PR_COEF4 + ilog2(d.width) - 2, t_desc);
 #ifndef HM_REG_CODER
   if (memo_on) {  // remember the count (FIFO slot)
+#ifdef HM_MEMO_HBM
     const int slot = S->memo_next;
+#else
+    const int slot = E.memo_next;
+#endif
     CoefMemo &m = S->memo[slot];
     const uint32_t *st32 = reinterpret_cast<const uint32_t *>(E.cod[E.cur].st);
     if (l < kMemoDw) { m.before[l] = cur_st; m.after[l] = st32[kMemoDw0 + l]; }
     if (l < d.width * d.width / 2) m.coef[l] = cur_cf;
-    if (l == 0) { m.key = key; m.frac = L.frac; S->memo_next = slot + 1 == kMemoK ? 0 : slot + 1; }
+#ifdef HM_MEMO_HBM
+    if (l == 0) { m.key = key; m.hash = hash; m.frac = L.frac; S->memo_next = slot + 1 == kMemoK ? 0 : slot + 1; }
+#else
+    const int nx = slot + 1 == kMemoK ? 0 : slot + 1;
+    if (l == 0) { m.key = key; m.hash = hash; m.frac = L.frac; S->memo_next = nx; }
+    wsync();
+    E.memo_key[slot] = key;
+    E.memo_hash[slot] = hash;
+    E.memo_next = nx;
+#endif
     wsync();
   }
 #endif
@@ -4103,11 +4150,20 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
   hm_e.prof[l >> 5][l & 31] = 0;
 #endif
   const int resume = job.flags & HVX_HM_RESUME;
-  if (resume) copy_words(&hm_e.cod[RD(0, CI_CURR_BEST)], &S->carry, (int)sizeof(Coder));
-  else {
+  if (resume) {
+    copy_words(&hm_e.cod[RD(0, CI_CURR_BEST)], &S->carry, (int)sizeof(Coder));
+#ifndef HM_MEMO_HBM
+    if (l < kMemoK) { hm_e.memo_key[l] = S->memo[l].key; hm_e.memo_hash[l] = S->memo[l].hash; }
+    hm_e.memo_next = S->memo_next;
+#endif
+  } else {
     copy_words(S->int2n, job.int2n, (int)sizeof(S->int2n));
     if (l < kMemoK) S->memo[l].key = 0;  // the count memo starts empty
     if (l == 0) S->memo_next = 0;
+#ifndef HM_MEMO_HBM
+    if (l < kMemoK) { hm_e.memo_key[l] = 0; hm_e.memo_hash[l] = 0; }
+    hm_e.memo_next = 0;
+#endif
   }
   wsync();
   const int n = job.n_ctus;
