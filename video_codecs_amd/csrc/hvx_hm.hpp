@@ -1460,10 +1460,11 @@ __device__ __forceinline__ uint32_t memo_hash(uint32_t st_masked, uint32_t cf) {
   const uint32_t l = (uint32_t)lid();
   return wave_sum_u32(memo_mix(st_masked ^ (l * 0x9e3779b9u)) + memo_mix(cf ^ (l * 0x7f4a7c15u + 0x2545f491u)));
 }
-__device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_t *coef) {
+// desc_ready: E.td already describes this TU and component (the caller's transformNxN just made it)
+__device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_t *coef, bool desc_ready = false) {
   HM_PROF(PR_COEF);
   HM_T0(t_desc);
-  tu_desc(cu, t, comp);
+  if (!desc_ready) tu_desc(cu, t, comp);
   const hvx_tu_desc &d = E.td;
   HM_TADD(PR_COEF_DESC, t_desc);
   // the memo (4x4 / 8x8 TUs)
@@ -1935,8 +1936,9 @@ __device__ int32_t transform_tu(Cu *cu, const Tu &t, int comp, const int16_t *re
   set_cbf_range(cu, comp, tu_abs_rel(t), tu_nparts(t, comp), (abs_sum > 0 ? 1 : 0) << tu_depth_rel(t));
   return abs_sum;
 }
-__device__ void inv_transform_tu(const Cu *cu, const Tu &t, int comp, const int16_t *coef, int16_t *resi, int rs) {
-  tu_desc(cu, t, comp);
+__device__ void inv_transform_tu(const Cu *cu, const Tu &t, int comp, const int16_t *coef, int16_t *resi, int rs,
+                                 bool desc_ready = false) {
+  if (!desc_ready) tu_desc(cu, t, comp);
   const hvx_tu_desc &d = E.td;
   switch (d.log2_size) {
     case 2: tu_inv_l<0>(d, coef, resi, rs); break;
@@ -2415,10 +2417,10 @@ __device__ void estimate_inter_residual_qt(Cu *cu, Yuv *resi, double *rd, uint32
             reset_bits();
           }
           code_qt_cbf(cu, t, comp, 1);
-          code_coeff_nxn(cu, t, comp, cur_coef);
+          code_coeff_nxn(cu, t, comp, cur_coef, true);  // E.td from transform_tu above
           cur_bits = written_bits();
           HM_TR("rqt_cnt", comp * 10 + mode, cur_bits);
-          inv_transform_tu(cu, t, comp, cur_coef, qres, qs);
+          inv_transform_tu(cu, t, comp, cur_coef, qres, qs, true);
           HM_TR("rqt_inv", comp * 10 + mode, 0);
           cur_dist = dist_part(qres, qs, pres, ystride(comp), w, h, comp);
           cur_cost = rd_cost(cur_bits, cur_dist);
@@ -3262,7 +3264,7 @@ __device__ void intra_coding_tu(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, uint32_t
   HMCU(cu, 74);
   const int32_t abs_sum = transform_tu(cu, t, comp, pr, s, coef);
   HMCU(cu, 75);
-  if (abs_sum > 0) inv_transform_tu(cu, t, comp, coef, pr, s);
+  if (abs_sum > 0) inv_transform_tu(cu, t, comp, coef, pr, s, true);  // E.td from transform_tu
   else {
     blk_copy(coef, w, nullptr, 0, w, h);
     blk_copy(pr, s, nullptr, 0, w, h);
