@@ -118,13 +118,28 @@ struct IntraScratch {
 // from CI_QT_TRAFO_ROOT, the node's single-bits recount, the parent's split recount, the CU's
 // final count), so a chain keeps its last kMemoK counts (FIFO) and replays a repeated one.
 // Context rows 40..187 as 37 dwords; a per-channel byte mask selects the rows the walk touches.
-constexpr int kMemoK = 16, kMemoDw = 37, kMemoDw0 = 10;
+#ifndef HM_MEMO_K
+#define HM_MEMO_K 16
+#endif
+#ifndef HM_MEMO_B
+#define HM_MEMO_B 8
+#endif
+constexpr int kMemoK = HM_MEMO_K, kMemoDw = 37, kMemoDw0 = 10;
 struct CoefMemo {
   uint32_t key;                   // valid | width | channel | scan | transform skip
   uint32_t hash;                  // memo_hash of the entry's levels and masked context states
   uint64_t frac;
   uint32_t coef[32];              // the TU's levels as int16 pairs (TU-packed order)
   uint32_t before[kMemoDw], after[kMemoDw];
+};
+// 16x16 / 32x32 counts (HM_MEMO_BIG): a short FIFO of their own -- the RQT counts a TU once while
+// choosing its mode and again for the node's total (the coefficient contexts unchanged between)
+constexpr int kMemoB = HM_MEMO_B;
+struct CoefMemoBig {
+  uint32_t key, hash;
+  uint64_t frac;
+  uint32_t before[kMemoDw], after[kMemoDw];
+  uint32_t coef[512];             // int16 pairs (TU-packed order); dword k * 64 + lane
 };
 // per-chain state in HBM
 struct State {
@@ -150,6 +165,8 @@ struct State {
   Coder carry;                    // the RD coder after the chain's last encodeCtu (HVX_HM_RESUME)
   CoefMemo memo[kMemoK];          // codeCoeffNxN counts of 4x4 / 8x8 TUs the chain made recently
   int memo_next;
+  CoefMemoBig memob[kMemoB];      // ... and of 16x16 / 32x32 TUs
+  int memob_next;
   MeScratch me;                   // leaf scratch outside LDS
   McScratch mc;
   TuSmem<3> tu3;
@@ -231,6 +248,8 @@ struct Enc {
 #ifndef HM_MEMO_HBM
   uint32_t memo_key[kMemoK], memo_hash[kMemoK];  // the count memo's index (S->memo keys / hashes)
   int memo_next;
+  uint32_t memob_key[kMemoB], memob_hash[kMemoB];
+  int memob_next;
 #endif
   int yw;                // the width of the CU whose TComYuv buffers are in use (compress_cu<D>: 64 >> D)
   float ssim_t[192];     // HVX_RD_SSIM: the (1 - SSIM) terms of a CU's blocks (cu_dssim)
@@ -1503,6 +1522,57 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
       }
     }
   }
+#ifndef HM_NO_MEMO_BIG
+  int bslot = -1;
+  if (d.width >= 16) {  // the 16x16 / 32x32 memo: same index scheme, levels compared from registers
+    key = 0x8000u | (uint32_t)d.width | ((uint32_t)ch << 8) | ((uint32_t)d.scan_type << 10) | ((uint32_t)d.transform_skip << 12);
+    const int nper = d.width == 16 ? 2 : 8;
+    uint32_t *st32 = reinterpret_cast<uint32_t *>(E.cod[E.cur].st);
+    if (l < kMemoDw) { cur_st = st32[kMemoDw0 + l]; mask = memo_mask(ch, l); }
+    const uint32_t *c32 = reinterpret_cast<const uint32_t *>(coef);
+    uint32_t cf[8];
+    uint32_t hs = memo_mix((cur_st & mask) ^ ((uint32_t)l * 0x9e3779b9u));
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      cf[k] = 0;
+      if (k < nper) {
+        cf[k] = c32[k * 64 + l];
+        hs += memo_mix(cf[k] ^ ((uint32_t)(k * 64 + l) * 0x7f4a7c15u + 0x2545f491u));
+      }
+    }
+    hash = wave_sum_u32(hs);
+    uint64_t cand = __ballot(l < kMemoB && E.memob_key[l < kMemoB ? l : 0] == key && E.memob_hash[l < kMemoB ? l : 0] == hash);
+    while (cand) {
+      const int e = __builtin_ctzll(cand);
+      cand &= cand - 1;
+      const CoefMemoBig &m = S->memob[e];
+      const uint32_t after = l < kMemoDw ? m.after[l] : 0u;
+      const uint64_t f = m.frac;
+      bool diff = l < kMemoDw && ((m.before[l] ^ cur_st) & mask);
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (k < nper) diff |= m.coef[k * 64 + l] != cf[k];
+      if (__ballot(diff) == 0) {  // a repeat: replay its result
+        wsync();
+        if (l < kMemoDw) st32[kMemoDw0 + l] = (cur_st & ~mask) | (after & mask);
+        if (l == 0) E.cod[E.cur].frac += f;
+        wsync();
+        return;
+      }
+    }
+    // a miss: the entry takes the levels and the entry states now (no copy held across the walk)
+    bslot = E.memob_next;
+    CoefMemoBig &m = S->memob[bslot];
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (k < nper) m.coef[k * 64 + l] = cf[k];
+    if (l < kMemoDw) m.before[l] = cur_st;
+    if (l == 0) m.key = 0;
+    wsync();
+    E.memob_key[bslot] = 0;  // invalid until its count is in
+    wsync();
+  }
+#endif
   HM_T0(t_stage);
   const int n = d.width * d.width;
   const uint16_t *scan = kScan[d.scan_type] + scan_base(ilog2(d.width) - 2);
@@ -1603,6 +1673,20 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
 #endif
     wsync();
   }
+#ifndef HM_NO_MEMO_BIG
+  if (bslot >= 0) {  // the 16x16 / 32x32 entry's count
+    CoefMemoBig &m = S->memob[bslot];
+    const uint32_t *st32 = reinterpret_cast<const uint32_t *>(E.cod[E.cur].st);
+    if (l < kMemoDw) m.after[l] = st32[kMemoDw0 + l];
+    const int nx = bslot + 1 == kMemoB ? 0 : bslot + 1;
+    if (l == 0) { m.key = key; m.hash = hash; m.frac = L.frac; S->memob_next = nx; }
+    wsync();
+    E.memob_key[bslot] = key;
+    E.memob_hash[bslot] = hash;
+    E.memob_next = nx;
+    wsync();
+  }
+#endif
 #endif
 }
 // TEncEntropy::estimateBit (TEncEntropy.cpp:685) from the current coder
@@ -4157,6 +4241,8 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
 #ifndef HM_MEMO_HBM
     if (l < kMemoK) { hm_e.memo_key[l] = S->memo[l].key; hm_e.memo_hash[l] = S->memo[l].hash; }
     hm_e.memo_next = S->memo_next;
+    if (l < kMemoB) { hm_e.memob_key[l] = S->memob[l].key; hm_e.memob_hash[l] = S->memob[l].hash; }
+    hm_e.memob_next = S->memob_next;
 #endif
   } else {
     copy_words(S->int2n, job.int2n, (int)sizeof(S->int2n));
@@ -4165,6 +4251,9 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
 #ifndef HM_MEMO_HBM
     if (l < kMemoK) { hm_e.memo_key[l] = 0; hm_e.memo_hash[l] = 0; }
     hm_e.memo_next = 0;
+    if (l < kMemoB) { S->memob[l].key = 0; hm_e.memob_key[l] = 0; hm_e.memob_hash[l] = 0; }
+    if (l == 0) S->memob_next = 0;
+    hm_e.memob_next = 0;
 #endif
   }
   wsync();
