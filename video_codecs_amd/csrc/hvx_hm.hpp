@@ -119,10 +119,10 @@ struct IntraScratch {
 // final count), so a chain keeps its last kMemoK counts (FIFO) and replays a repeated one.
 // Context rows 40..187 as 37 dwords; a per-channel byte mask selects the rows the walk touches.
 #ifndef HM_MEMO_K
-#define HM_MEMO_K 16
+#define HM_MEMO_K 64
 #endif
 #ifndef HM_MEMO_B
-#define HM_MEMO_B 8
+#define HM_MEMO_B 16
 #endif
 constexpr int kMemoK = HM_MEMO_K, kMemoDw = 37, kMemoDw0 = 10;
 struct CoefMemo {
