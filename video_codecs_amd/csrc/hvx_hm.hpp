@@ -1199,11 +1199,30 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
       }
       const int sc = env.big ? cab::sig_ctx(pattern, env.first_sig, env.single, sc_l, lw, ch) : (sc_l >> (6 * pattern)) & 63;
       int nnz = is_last_set ? 1 : 0;
+#ifndef HM_WALK_NO_PF
+      // the group's significance contexts fetched into lanes once (one LDS round) and written back
+      // once: a flag's bin reads its state with v_readlane and forwards the new state to every lane
+      // on the same context, leaving one LDS round (the tables) on the chain per bin
+      const int row_l = base_sig + (l < 16 ? sc : 0) + cab::kCtxLo;
+      int q_l = L.st[row_l];
+      for (int pin = is_last_set ? last_pin - 1 : 15; pin >= 0; pin--) {
+        const int sig = (int)((m16 >> pin) & 1u);
+        if (pin > 0 || sub == 0 || nnz) {
+          const int row = __builtin_amdgcn_readlane(row_l, pin), q = __builtin_amdgcn_readlane(q_l, pin);
+          L.frac += (uint32_t)E.eb[q ^ sig];
+          const int ns = E.next[q * 2 + sig];
+          q_l = row_l == row ? ns : q_l;
+        }
+        nnz += sig;
+      }
+      if (l < 16) L.st[row_l] = (uint8_t)q_l;
+#else
       for (int pin = is_last_set ? last_pin - 1 : 15; pin >= 0; pin--) {
         const int sig = (int)((m16 >> pin) & 1u);
         if (pin > 0 || sub == 0 || nnz) L.bin(base_sig + __builtin_amdgcn_readlane(sc, pin), sig);
         nnz += sig;
       }
+#endif
     }
     const int nnz = __popc(m16);
     HM_WTADD(1, wt_);
@@ -1218,12 +1237,26 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
     int first_c2_abs = 0;
     bool have_c2 = false;
     uint32_t rest = m16;
+#ifndef HM_WALK_NO_PF
+    // the four greater-1 contexts of the set in lanes 0..3, the same way
+    const int row1_l = base_one + (l & 3) + cab::kCtxLo;
+    int q1_l = L.st[row1_l];
+#endif
     for (int idx = 0; rest && idx < 8; idx++) {
       const int pin = 31 - __clz(rest);
       rest &= ~(1u << pin);
       const int av = __builtin_amdgcn_readlane(av_l, pin);
       const int gt1 = av > 1;
+#ifndef HM_WALK_NO_PF
+      {
+        const int q = __builtin_amdgcn_readlane(q1_l, c1);
+        L.frac += (uint32_t)E.eb[q ^ gt1];
+        const int ns = E.next[q * 2 + gt1];
+        q1_l = (l & 3) == c1 ? ns : q1_l;
+      }
+#else
       L.bin(base_one + c1, gt1);
+#endif
       if (gt1) {
         c1 = 0;
         if (!have_c2) { have_c2 = true; first_c2_abs = av; }
@@ -1232,6 +1265,9 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
         c1++;
       }
     }
+#ifndef HM_WALK_NO_PF
+    if (l < 4) L.st[row1_l] = (uint8_t)q1_l;
+#endif
     if (c1 == 0 && have_c2) {
       const int gt2 = first_c2_abs > 2;
       L.bin(cab::kAbs + set, gt2);
