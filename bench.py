@@ -29,8 +29,6 @@ sys.path.insert(0, ROOT)
 
 MI355X_HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters
 METRIC = "64\u00d764 CTUs/s (ME+transform+RDOQ) on 2160p YUV, 1\u21928 MI355X; bit-exact vs HM"
-# the reduced step of rounds 1-2 (side measurement): bit-exact against its own HM-pinned restatement
-REDUCED_METRIC = "64\u00d764 CTUs/s (ME+transform+RDOQ) on 2160p YUV; bit-exact vs HM-pinned oracle (oracle/hvx_oracle.c)"
 # the bench picture: GOP position 2 of tests/hm_seam/ldp.cfg's LDP GOP at base QP 32 -> QP 34,
 # QPFactor 0.4624, GOP depth 1 (TEncSlice.cpp:320-374)
 HM_QP_OFFSET, HM_QP_FACTOR = 2, 0.4624
@@ -47,21 +45,14 @@ def parse():
     p.add_argument("--cpu-ref-procs", type=int, default=0, help="HM TAppEncoder processes for the reference "
                                                                   "baseline (0: the host's CPU share)")
     p.add_argument("--no-cpu-ref", action="store_true", help="skip the reference HM timing")
-    p.add_argument("--reduced", action="store_true", help="also run the reduced picture step of rounds 1-2 "
-                                                          "(hvx_ctu_encode_yuv, side measurement)")
     p.add_argument("--no-ra", action="store_true", help="skip the config-4 side figure (RA B pictures, SSIM cost)")
     p.add_argument("--no-slice0", action="store_true", help="skip the SliceMode 0 side figure")
     p.add_argument("--width", type=int, default=3840)
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--nref", type=int, default=4)
     p.add_argument("--qp", type=int, default=32)
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the reduced step's CPU sample")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--no-intra", action="store_true", help="skip the intra first-pass side measurement")
-    p.add_argument("--no-ssim", action="store_true", help="skip the SSIM-RDO side measurement")
     p.add_argument("--no-1080p", action="store_true", help="skip the 1080p side measurement")
-    p.add_argument("--no-sao", action="store_true", help="skip the SAO side measurement")
-    p.add_argument("--no-cabac", action="store_true", help="skip the CABAC residual writer side measurement")
     return p.parse_args()
 
 
@@ -71,40 +62,6 @@ def b_ctu(nref):
     int16 levels and the 16 B-per-4x4 MV/mode field (53,248 B at N_ref = 4)."""
     S = 64 * 64 * 3 // 2
     return S * (1 + nref + 1) + 2 * S + 16 * (64 * 64 // 16)
-
-
-def luma_plane(w, h, index):
-    from video_codecs_amd import synth  # synthetic-input recipe (BASELINE.md section 3)
-    return synth.luma_plane(w, h, index)
-
-
-def yuv_planes(w, h, index):
-    from video_codecs_amd import synth
-    return synth.yuv_planes(w, h, index)
-
-
-class YuvInputs:
-    """A segment's current picture and references as device-resident padded Y/Cb/Cr planes, with the
-    origin-pointer tables hvx_ctu_encode_yuv reads (references' Y; their Cb then their Cr)."""
-
-    def __init__(self, W, H, frames):
-        import torch
-        from video_codecs_amd import _abi, hvx
-        pl = [yuv_planes(W, H, f) for f in frames]
-        self.host = pl
-        self.cur = [torch.from_numpy(x).cuda() for x in pl[-1]]
-        self.refs = [[torch.from_numpy(x).cuda() for x in p] for p in pl[:-1]]
-        mc = _abi.PLANE_MARGIN // 2
-        self.ptr_y = torch.tensor([hvx.plane_origin_ptr(r[0], W) for r in self.refs], dtype=torch.int64).cuda()
-        self.ptr_c = torch.tensor([hvx.plane_origin_ptr(r[c], W // 2, mc) for c in (1, 2) for r in self.refs],
-                                  dtype=torch.int64).cuda()
-
-
-def segment_frames(rank, nref):
-    """Frame indices of rank's independent GOP segment: nref references, then the current picture
-    (closed segments, one per GPU; no data-path collective)."""
-    base = rank * (nref + 1)
-    return list(range(base, base + nref + 1))
 
 
 def timed_steps(step, steps, warmup, world, device, sync, before=None):
@@ -132,21 +89,6 @@ def timed_steps(step, steps, warmup, world, device, sync, before=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
-
-
-def phase_pass(step, steps, sync):
-    """Per-launch HIP-event times of `steps` extra steps with timing switched on (each phase is a
-    begin/end event pair on its launch's own stream).  Run after the headline's timed region."""
-    from video_codecs_amd import hvx
-    sync()
-    hvx.set_timing(True)
-    hvx.phase_times(reset=True)
-    for _ in range(steps):
-        step()
-    sync()
-    phases = hvx.phase_times(reset=True)
-    hvx.set_timing(False)
-    return phases
 
 
 def aggregate(units_per_step, steps, world, elapsed):
@@ -655,9 +597,6 @@ def main():
     dpb_ok = None
     if gathered is not None:
         dpb_ok = bool(torch.equal(gathered[0], own))
-    reduced = None
-    if args.reduced:
-        reduced = reduced_step(args, rank, world, with_sides=(world == 1))
     if rank == 0:
         units = work.n_jobs * args.ctus
         value = aggregate(units, args.steps, world, elapsed)
@@ -733,379 +672,9 @@ def main():
                 out["slice_mode0"] = slice_mode0_measure(W, H)
             if not args.no_1080p:
                 out["hm_1080p"] = hm_1080p_measure()
-        if reduced is not None:
-            out["reduced_step"] = reduced
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def reduced_step(args, rank, world, with_sides):
-    """The reduced picture step of rounds 1-2 (hvx_ctu_encode_yuv, DESIGN.md sections 3-3a): its
-    measurement dict, CPU sample (with_sides) and side measurements; timed like the headline."""
-    import torch
-    from video_codecs_amd import _abi, hvx
-    from video_codecs_amd.dpb import DpbGather
-
-    W, H, nref = args.width, args.height, args.nref
-    inp = YuvInputs(W, H, segment_frames(rank, nref))
-    cur_t = inp.cur[0]
-    an = hvx.CtuAnalyzer(W, H, nref, args.qp, chroma=True)
-    nctu = an.nctu
-    # the reference picture (Y | Cb | Cr padded planes in one buffer): one gather per picture
-    dpb = DpbGather(world, rank, (hvx.yuv_bytes(W, H),), "cuda")
-    recon = hvx.yuv_views(torch.zeros(hvx.yuv_bytes(W, H), dtype=torch.uint8, device="cuda"), W, H)
-
-    def step():
-        # one picture: analysis (ME + Y/Cb/Cr TU pipelines) -> CU decision + reconstruction ->
-        # deblocked reference picture -> DPB gather of that reference
-        an.encode_yuv(inp.cur, inp.ptr_y, inp.ptr_c, recon, hvx.yuv_views(dpb.buffer(), W, H))
-        dpb.send()
-
-    def sync():
-        dpb.drain()
-        torch.cuda.synchronize()
-
-    # headline: per-phase timing OFF (no event pairs, no host wait on the previous step's events)
-    hvx.set_timing(False)
-    elapsed = timed_steps(step, args.steps, args.warmup, world, "cuda", sync)
-    # per-phase HIP-event times in a separate, instrumented pass after the timed region
-    phases = phase_pass(step, args.steps, sync)
-    gpu_res, gpu_dec = an.results(), an.decisions()
-    own, gathered = dpb.last()
-    gpu_rec = [x.cpu().numpy() for x in recon]
-    gpu_refpic = [x.cpu().numpy() for x in hvx.yuv_views(own, W, H)]
-    dpb_ok = None
-    if gathered is not None:  # rank 0 holds every rank's picture; its own slot must be its own
-        dpb_ok = bool(torch.equal(gathered[0], own))
-
-    if rank == 0:
-        value = aggregate(nctu, args.steps, world, elapsed)
-        # roofline of the dominant kernel = the longest single launch of the step, timed with
-        # HIP events on the launch stream (a begin/end pair around exactly one launch; the pass
-        # runs on 3 streams, so phases overlap and their sum exceeds ms_per_step).
-        # Algorithmic bytes per launch = SURVEY 8(d)'s per-CTU figure (4:2:0, DESIGN.md "Roofline")
-        # x the CTUs one launch covers (every launch of the pass covers the picture).
-        single = {k: p for k, p, nl in zip(hvx.PHASE_KERNELS, hvx.PHASES, hvx.PHASE_LAUNCHES) if nl == 1}
-        kernel = max(single, key=lambda k: phases[single[k]])
-        launch_ms = phases[single[kernel]] / args.steps
-        bpc = b_ctu(nref)
-        bytes_per_launch = bpc * nctu
-        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-        traffic = None
-        tr_path = os.path.join(ROOT, "profiles", "hbm_traffic_r02.json")  # PMC passes of this round's tree
-        if os.path.exists(tr_path):
-            tr = json.load(open(tr_path)).get(kernel)
-            if tr:
-                traffic = tr["bytes_per_launch"]
-        step_s = elapsed / args.steps
-        out = {
-            "metric": REDUCED_METRIC,
-            "value": round(value, 2),
-            "unit": "CTUs/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic: splitmix64 uniform random 8-bit 4:2:0 YUV (BASELINE.md sec. 3), independent segment per rank",
-            "config": {"workload": "CTU mode decision, 4:2:0: 85 CUs x TZ+frac ME vs %d refs, luma+chroma MC, Y/Cb/Cr TU "
-                                   "RDOQ/dequant/IT, CABAC coefficient rate, CU quadtree RD decision, Y/Cb/Cr "
-                                   "reconstruction, deblocked reference picture" % nref,
-                       "resolution": f"{W}x{H}", "ctus_per_frame": nctu, "qp": args.qp, "search_range": 64,
-                       "n_ref": nref, "parallelism": f"segments x{world}",
-                       "dpb": "gather of every rank's deblocked reference picture to rank 0 per step" if world > 1 else "local"},
-            "phase_ms_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()},
-            # priced against HBM (integer work, SURVEY 8(d)); the measured limiter is VALU issue for
-            # the searches (SQ: VALU busy ~90% of the launch) and the serial per-lane decision chain
-            # for RDOQ / CABAC counting -- not bandwidth (frac << 1, PMC traffic in profiles/)
-            "roofline": {"bound": "hbm", "limiter": "valu-issue" if kernel.startswith("k_me") else "latency",
-                         "kernel": kernel, "achieved": round(achieved, 3),
-                         "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / MI355X_HBM_PEAK_GBS,
-                         "traffic": traffic, "bytes_per_launch": bytes_per_launch,
-                         "avg_launch_ms": round(launch_ms, 3), "b_ctu": bpc,
-                         "path_achieved_gbs": round(bpc * nctu / step_s / 1e9, 3),
-                         "path_frac": bpc * nctu / step_s / 1e9 / MI355X_HBM_PEAK_GBS},
-            "cpu_baseline": None,
-        }
-        if dpb_ok is not None:
-            out["dpb_gather_ok"] = dpb_ok
-        out["build"] = build_provenance()
-        if with_sides and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(inp.host, an, gpu_res, gpu_dec, gpu_rec, gpu_refpic, args)
-        if with_sides and not args.no_1080p:
-            out["step_1080p"] = step_1080p_measure(nref, args.qp, args.steps)
-        if with_sides and not args.no_ssim:
-            out["ssim_rdo"] = ssim_rdo_measure(inp, W, H, nref, args.steps)
-        if with_sides and not args.no_sao:
-            out["sao"] = sao_measure(W, H, args.steps)
-        if with_sides and not args.no_cabac:
-            out["cabac_write"] = cabac_write_measure(args.steps)
-        if with_sides and not args.no_intra:
-            out["intra_first_pass"] = intra_measure(cur_t, inp.refs[0][0], W, H, float(an.params["lambda"][0]),
-                                                    args.steps)
-        return out
-    return None
-
-
-def step_1080p_measure(nref, qp, steps):
-    """Side measurement (BASELINE configs 2-3 geometry, not the headline): the same picture step on a
-    1920x1080 picture (510 CTUs, the bottom CTU row 56 lines high) -- CTUs/s and ms per picture."""
-    import torch
-    from video_codecs_amd import hvx
-    W, H = 1920, 1080
-    inp = YuvInputs(W, H, [100 + f for f in range(nref + 1)])
-    an = hvx.CtuAnalyzer(W, H, nref, qp, chroma=True)
-    recon = [torch.zeros_like(x) for x in inp.cur]
-    refpic = [torch.zeros_like(x) for x in inp.cur]
-    an.encode_yuv(inp.cur, inp.ptr_y, inp.ptr_c, recon, refpic)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        an.encode_yuv(inp.cur, inp.ptr_y, inp.ptr_c, recon, refpic)
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / steps * 1e3
-    return {"resolution": f"{W}x{H}", "ctus_per_frame": an.nctu, "ms_per_picture": round(ms, 3),
-            "ctus_per_s": round(an.nctu / ms * 1e3, 1)}
-
-
-def ssim_rdo_measure(inp, W, H, nref, steps):
-    """Side measurement (BASELINE config 4's RD cost, not the headline): the same 4:2:0 picture step
-    with the SSIM CU decision (HVX_RD_SSIM: D = sum of 1 - SSIM over the luma 8x8 blocks,
-    lambda_2(qp)) at QP 22, 27, 32, 37 -- wall time per picture and the leaf CUs chosen (vs the SSE
-    decision at that QP)."""
-    import torch
-    from video_codecs_amd import _abi, hvx
-    res = {}
-    recon = [torch.zeros_like(x) for x in inp.cur]
-    refpic = [torch.zeros_like(x) for x in inp.cur]
-    for qp in (22, 27, 32, 37):
-        leaves = {}
-        for metric in (_abi.RD_SSIM, _abi.RD_SSE):
-            an = hvx.CtuAnalyzer(W, H, nref, qp, rd_metric=metric, chroma=True)
-            an.encode_yuv(inp.cur, inp.ptr_y, inp.ptr_c, recon, refpic)
-            torch.cuda.synchronize()
-            if metric == _abi.RD_SSIM:
-                t0 = time.perf_counter()
-                for _ in range(steps):
-                    an.encode_yuv(inp.cur, inp.ptr_y, inp.ptr_c, recon, refpic)
-                torch.cuda.synchronize()
-                ms = (time.perf_counter() - t0) / steps * 1e3
-            leaves[metric] = int(an.decisions()["leaf"].sum())
-            del an
-        res[str(qp)] = {"ms_per_picture": round(ms, 3), "ctus_per_s": round(((W + 63) // 64) * ((H + 63) // 64) / ms * 1e3, 1),
-                        "lambda_ssim": _abi.lambda_ssim(qp), "leaf_cus_ssim": leaves[_abi.RD_SSIM],
-                        "leaf_cus_sse": leaves[_abi.RD_SSE]}
-    return res
-
-
-def sao_measure(W, H, steps):
-    """Side measurement (not the headline): hvx_sao_stats + hvx_sao_apply over a whole 4:2:0
-    picture (Y, Cb, Cr) with random parameters -- wall time per picture of each kernel and its
-    HBM rate against the algorithmic bytes (stats: read original + deblocked picture; apply:
-    read the deblocked picture, write the output picture; 1.5 B per luma sample each)."""
-    import torch
-    from video_codecs_amd import _abi, hvx, synth
-    y = synth.luma_plane(W, H, 200)
-    M = _abi.PLANE_MARGIN
-    planes = [torch.from_numpy(np.ascontiguousarray(y[M:M + h, M:M + w])).cuda()
-              for (w, h) in ((W, H), (W // 2, H // 2), (W // 2, H // 2))]
-    org = [torch.roll(p, 1, 1).contiguous() for p in planes]
-    dst = [torch.empty_like(p) for p in planes]
-    view = lambda ts: [(t.data_ptr(), t.shape[1]) for t in ts]  # noqa: E731
-    nctu = ((W + 63) // 64) * ((H + 63) // 64)
-    rng = np.random.default_rng(7)
-    rows = np.zeros((nctu, 3, 6), np.int32)
-    rows[:, :, 0] = rng.integers(-1, 5, (nctu, 3))
-    rows[:, :, 1] = rng.integers(0, 32, (nctu, 3))
-    rows[:, :, 2:6] = rng.integers(-7, 8, (nctu, 3, 4))
-    prm = hvx.to_device(_abi.sao_ctu_params(rows))
-    stats = torch.empty(nctu * 15 * _abi.SAO_STAT.itemsize, dtype=torch.uint8, device="cuda")
-    res = {}
-    for name, fn in (("stats", lambda: hvx.sao_stats(view(org), view(planes), W, H, stats)),
-                     ("apply", lambda: hvx.sao_apply(view(planes), view(dst), W, H, prm))):
-        fn()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            fn()
-        torch.cuda.synchronize()
-        ms = (time.perf_counter() - t0) / steps * 1e3
-        gbs = 2 * 1.5 * W * H / (ms * 1e-3) / 1e9
-        res[name] = {"ms_per_picture": round(ms, 4), "algorithmic_gbs": round(gbs, 1),
-                     "frac_hbm": round(gbs / MI355X_HBM_PEAK_GBS, 4)}
-    return res
-
-
-def cabac_write_measure(steps, n_runs=2040, seed=9):
-    """Side measurement (not the headline): hvx_coeff_write_batch writing the
-    residual syntax of a 2160p picture's worth of TUs through TEncBinCABAC, one run per CTU (16
-    luma 16x16 + 8 chroma 8x8 TUs; synthetic levels: 30% non-zero, magnitudes 1-3 with 10%
-    escapes up to 40, random signs), every run from TEncBinCABAC::start() and the same context
-    snapshot -- wall time per launch, TUs/s and output MB/s.  Runs are serial inside (the coder's
-    registers), parallel across runs."""
-    import torch
-    from video_codecs_amd import _abi, hvx
-    rng = np.random.default_rng(seed)
-    sizes = np.tile(np.array([16] * 16 + [8] * 8), n_runs)
-    comps = np.tile(np.array([0] * 16 + [1] * 4 + [2] * 4), n_runs)
-    n = len(sizes)
-    d = np.zeros(n, _abi.TU_DESC)
-    d["width"] = d["height"] = sizes
-    d["log2_size"] = np.log2(sizes).astype(np.int32)
-    d["comp"] = comps
-    d["sign_hiding"] = 1
-    d["pps_tskip"] = 1
-    d["max_log2_tr_range"] = 15
-    d["bit_depth"] = 8
-    lev = []
-    for w in sizes:
-        a = (rng.random(w * w) < 0.3) * rng.integers(1, 4, w * w)
-        a = np.where(rng.random(w * w) < 0.1, a * rng.integers(1, 14, w * w), a)
-        a[0] = max(a[0], 1)
-        lev.append(np.where(rng.random(w * w) < 0.5, -a, a).astype(np.int32))
-    off = np.concatenate([[0], np.cumsum(sizes * sizes)[:-1]]).astype(np.int64)
-    first = np.arange(n_runs + 1, dtype=np.int32) * 24
-    st0 = np.tile(rng.integers(0, 126, _abi.NUM_CTX).astype(np.uint8), n_runs)
-    rg0 = np.zeros(n_runs, _abi.CABAC_REGS)
-    rg0[:] = _abi.CABAC_START
-    cap = 1 << 14
-    d_desc, d_off, d_lev = hvx.to_device(d), hvx.to_device(off), hvx.to_device(np.concatenate(lev))
-    d_first, d_oo = hvx.to_device(first), hvx.to_device(np.arange(n_runs, dtype=np.int64) * cap)
-    d_st = torch.from_numpy(st0).cuda()
-    d_rg = torch.from_numpy(rg0.view(np.uint8).copy()).cuda()
-    out = torch.empty(n_runs * cap, dtype=torch.uint8, device="cuda")
-    d_len = torch.empty(n_runs, dtype=torch.int32, device="cuda")
-    st0_d, rg0_d = d_st.clone(), d_rg.clone()
-
-    def run():
-        d_st.copy_(st0_d)
-        d_rg.copy_(rg0_d)
-        hvx.coeff_write_batch(d_desc, d_off, d_lev, d_first, n_runs, d_st, d_rg, out, d_oo, cap, d_len)
-
-    run()
-    torch.cuda.synchronize()
-    nbytes = int(d_len.sum().item())
-    assert (d_len >= 0).all().item()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        run()
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / steps * 1e3
-    return {"runs": n_runs, "tus": n, "bytes": nbytes, "ms_per_launch": round(ms, 3),
-            "tus_per_s": round(n / ms * 1e3, 1), "output_mb_per_s": round(nbytes / ms / 1e3, 2)}
-
-
-def intra_measure(cur_t, rec_t, W, H, lam, steps):
-    """Side measurement (not the headline): hvx_intra_search_batch -- estIntraPredLumaQT's first
-    pass -- over every luma PU of the picture at all five PU sizes (341 PUs per CTU,
-    video_codecs_amd/intra_grid.py), the current picture as the original and a reference picture
-    as the reconstructed neighbours.  Wall time per picture after a warmup launch."""
-    import math
-    import torch
-    from video_codecs_amd import _abi, hvx, intra_grid
-    jobs = intra_grid.picture_first_pass_jobs(W, H, math.sqrt(lam))
-    dev = {l: hvx.to_device(j) for l, j in jobs.items()}
-    total = sum(len(j) for j in jobs.values())
-    out = torch.empty(max(len(j) for j in jobs.values()) * _abi.INTRA_RESULT.itemsize, dtype=torch.uint8, device="cuda")
-    eb = torch.from_numpy(_abi.load_entropy_bits().copy()).cuda()
-    org, rec = hvx.plane_origin_ptr(cur_t, W), hvx.plane_origin_ptr(rec_t, W)
-    stride = cur_t.shape[1]
-
-    def one(sizes):
-        for l in sizes:
-            hvx.intra_search_batch(org, rec, stride, dev[l], len(jobs[l]), eb, out)
-    one(jobs)
-    hvx.sync()
-    per_size = {}
-    for l in jobs:  # each PU size alone (the per-size share of the picture time)
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            one([l])
-        hvx.sync()
-        per_size[str(1 << l)] = round((time.perf_counter() - t0) / steps * 1e3, 3)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        one(jobs)
-    hvx.sync()
-    ms = (time.perf_counter() - t0) / steps * 1e3
-    return {"kernel": "k_intra_search", "pus_per_picture": total,
-            "pus_by_size": {str(1 << l): len(j) for l, j in jobs.items()}, "ms_by_size": per_size,
-            "ms_per_picture": round(ms, 3),
-            "pus_per_s": round(total / ms * 1e3, 1),
-            "ctus_per_s": round(((W + 63) // 64) * ((H + 63) // 64) / ms * 1e3, 1)}
-
-
-def cpu_baseline(host, an, gpu_res, gpu_dec, gpu_rec, gpu_refpic, args):
-    """The oracle (scalar C port of the same step) on a bounded sample of the same picture's CTUs
-    in raster order, one CTU per call on each of the host threads (ctypes releases the GIL around
-    the C call; CTUs are independent and write disjoint reconstruction blocks); also checks the
-    GPU's CU results, CU decisions and reconstructed Y/Cb/Cr samples of every sampled CTU, and the
-    whole reference picture."""
-    import itertools
-    import threading
-    from concurrent.futures import ThreadPoolExecutor
-    import oracle
-    from video_codecs_amd import _abi
-    nref = args.nref
-    est7 = _abi.estbits_p_yuv(oracle.estbits_update)
-    st, eb = _abi.load_ctx_p_states(), _abi.load_entropy_bits()
-    ncx = (args.width + 63) // 64
-    M, Mc = _abi.PLANE_MARGIN, _abi.PLANE_MARGIN // 2
-    cur, refs = host[nref], host[:nref]
-    refs3 = ([r[0] for r in refs], [r[1] for r in refs], [r[2] for r in refs])
-    rec = [np.zeros_like(x) for x in cur]
-    # the host threads the box gives this job (OMP_NUM_THREADS = the CPU share, 16 on a 1-GPU box)
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
-    out = {}
-    ctr, lock = itertools.count(), threading.Lock()
-
-    def one(c):
-        r, d = oracle.ctu_decide_yuv(cur, refs3, an.params, est7, st, eb, c % ncx, c // ncx, rec)
-        out[c] = (r, d)
-
-    one(0)  # the oracle's lazily built tables, before any thread runs
-    t0 = time.perf_counter()
-
-    def worker():
-        while time.perf_counter() - t0 <= args.cpu_seconds:
-            with lock:
-                c = next(ctr) + 1
-            if c >= an.nctu:
-                return
-            one(c)
-
-    with ThreadPoolExecutor(threads) as ex:
-        for f in [ex.submit(worker) for _ in range(threads)]:
-            f.result()
-    dt = time.perf_counter() - t0
-    n_done, mismatches = len(out), 0
-    for c, (r, d) in out.items():
-        cx, cy = c % ncx, c // ncx
-        same = r.tobytes() == gpu_res[c].tobytes() and d.tobytes() == gpu_dec[c].tobytes()
-        for k in range(3):
-            m, s = (M, 64) if k == 0 else (Mc, 32)
-            w, h = (args.width, args.height) if k == 0 else (args.width // 2, args.height // 2)
-            ys = slice(m + cy * s, m + min(h, cy * s + s))
-            xs = slice(m + cx * s, m + min(w, cx * s + s))
-            same = same and np.array_equal(rec[k][ys, xs], gpu_rec[k][ys, xs])
-        mismatches += 0 if same else 1
-    W, H = args.width, args.height
-    bv, bh = oracle.ctu_bs(gpu_res.reshape(-1), gpu_dec.reshape(-1), W, H)
-    qp = np.full(len(bv), int(an.params["qp"][0]), np.int8)
-    inner = [gpu_rec[0][M:M + H, M:M + W], gpu_rec[1][Mc:Mc + H // 2, Mc:Mc + W // 2],
-             gpu_rec[2][Mc:Mc + H // 2, Mc:Mc + W // 2]]
-    dy, dcb, dcr = oracle.deblock(inner[0], inner[1], inner[2], bv, bh, qp, _abi.deblock_params(W, H))
-    refpic_ok = all(bool(np.array_equal(gpu_refpic[k], np.pad(p, M if k == 0 else Mc, mode="edge")))
-                    for k, p in enumerate((dy, dcb, dcr)))
-    return {"value": round((n_done - 1) / dt, 3), "unit": "CTUs/s", "cores": threads, "kind": "port",
-            "sample": f"first {n_done} CTUs (raster) of the same 2160p 4:2:0 picture on {threads} host threads, "
-                      f"{dt:.1f} s timed (CTU 0 untimed), oracle/hvx_oracle.c",
-            "gpu_parity_ctus": n_done, "gpu_parity_mismatches": mismatches,
-            "gpu_ref_picture_ok": refpic_ok}
 
 
 if __name__ == "__main__":

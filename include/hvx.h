@@ -37,14 +37,6 @@
  *                         arithmetic coder TEncBinCABAC (TEncBinCoderCABAC.cpp:200-460): the residual
  *                         syntax of TU runs written as CABAC bytes (TEncSlice::encodeSlice path)
  *   hvx_me_full_batch     TEncSearch::xMotionEstimation with xPatternSearch (:3786), incl. bBi
- *   hvx_ctu_analyze       TEncCu::compressCtu's inter 2Nx2N analysis for every CU of every CTU
- *                         (TEncCu.cpp:228,349,1291 -> predInterSearch/encodeResAndCalcRdInterCU):
- *                         the bench workload, composition of the kernels above
- *   hvx_ctu_decide        TEncCu::xCompressCU's depth decision (TEncCu.cpp:349-877, xCheckBestMode
- *                         :1166) over the analysed CUs, then TComYuv::addClip + copyToPic of the
- *                         chosen leaves (the reconstructed picture) and extendPicBorder
- *   hvx_ctu_encode        hvx_ctu_analyze + hvx_ctu_decide as one schedule (TEncSlice::compressSlice's
- *                         compressCtu loop over a picture, TEncSlice.cpp:814)
  *   hvx_intra_pred_batch  TComPrediction::initIntraPatternChType (TComPattern.cpp:115, reference
  *                         samples + smoothing) + predIntraAng (TComPrediction.cpp:455)
  *   hvx_intra_search_batch TEncSearch::estIntraPredLumaQT's first pass (TEncSearch.cpp:2244-2323):
@@ -307,72 +299,6 @@ int hvx_sao_apply(hvx_ctx *ctx, const uint8_t *d_src_y, const uint8_t *d_src_cb,
  * TEncSbac::codeSAOBlkParam TEncSbac.cpp:1683 on the RD counter carried CTU to CTU, the picture-level
  * disable test :846): the coded and the applied (merge-resolved, hvx_sao_apply-ready) parameters. */
 int hvx_sao_decide(hvx_ctx *ctx, const hvx_sao_decide_job *d_jobs, int n_jobs);
-
-/* ---------------------------------------------------------------------------------------
- * CTU analysis pass over a whole picture (hvx_types.h): d_cur = sample (0,0) of the current
- * 8-bit padded plane, d_refs = device array of n_ref reference-plane origins, d_est4 = device
- * array of 4 luma estBits tables (TU 4x4..32x32), d_out = nctu*85 hvx_cu_result.  The
- * caller allocates a device workspace of hvx_ctu_workspace_size() bytes.  Planes carry the
- * HVX_PLANE_MARGIN border and a stride that is a multiple of 4 (HVX_E_INVALID otherwise).
- * ------------------------------------------------------------------------------------- */
-int hvx_ctu_workspace_size(int pic_w, int pic_h, int n_ref, size_t *bytes);
-int hvx_ctu_analyze(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
-                    const hvx_ctu_params *h_params, const hvx_estbits *d_est4, void *d_workspace, size_t ws_bytes,
-                    hvx_cu_result *d_out);
-/* Optional per-launch timing of hvx_ctu_analyze with HIP events on the launch stream.  Phases:
- * 0 integer ME of the 64x64 depth (k_ctu_me_jobs + k_me_int_ctu), 1..3 integer + fractional
- * ME of the 32/16/8 depths (k_ctu_me_jobs + k_me_ctu), 4 fractional ME of the 64x64 depth
- * (k_me_frac_ctu), 5 MC/residual (k_ctu_pred_resid), 6..8 TU 32x32 (k_tu_fwd, k_tu_rdoq,
- * k_tu_fin), 9..11 TU 16x16, 12..14 TU 8x8, 15 per-CU sums (k_ctu_finalize); hvx_ctu_decide:
- * 16 coefficient rate (3 x k_coeff_bits), 17 CU tree + reconstruction (k_ctu_decide, k_ctu_recon,
- * border extension), 18 reference picture (k_ctu_bs, deblocking, border extension).  Accumulated ms. */
-#define HVX_NPHASE 19
-int hvx_set_timing(hvx_ctx *ctx, int on);
-int hvx_phase_times(hvx_ctx *ctx, double *ms_out, int n, int reset);
-
-/* ---------------------------------------------------------------------------------------
- * CU decision + reconstruction after hvx_ctu_analyze (same workspace, same stream order):
- * counts every TU's coefficient rate (codeCoeffNxN under TEncBinCABACCounter, as
- * hvx_coeff_bits_batch) from one RD-coder context snapshot d_ctx_states (HVX_NUM_CTX bytes,
- * device) with d_entropy_bits (128 int32, device), then runs TEncCu::xCompressCU's depth
- * recursion per CTU (hvx_types.h hvx_cu_decision; d_cu = hvx_ctu_analyze's output, d_dec =
- * nctu*85 records) and writes the luma of the chosen leaves, clip(pred + reconstructed
- * residual), into d_recon (sample (0,0) of an 8-bit padded plane with the same stride as
- * d_cur), borders extended as TComPicYuv::extendPicBorder.  When d_ref_pic is not NULL it also
- * writes the REFERENCE picture there (may equal d_recon: in place): that reconstruction deblocked
- * (boundary strengths of the decided CU/TU trees as TComLoopFilter's xSetEdgefilterTU/PU +
- * xGetBoundaryStrengthSingle give them, slice QP, luma loopFilterPic as hvx_deblock) with its
- * borders extended again -- the next picture's reference (TEncGOP.cpp:1465).
- * Picture width and height must be multiples of 8.
- * ------------------------------------------------------------------------------------- */
-int hvx_ctu_decide(hvx_ctx *ctx, const uint8_t *d_cur, int stride, const hvx_ctu_params *h_params,
-                   const uint8_t *d_ctx_states, const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes,
-                   const hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic);
-
-/* The whole picture step: hvx_ctu_analyze + hvx_ctu_decide with the same results, scheduled
- * together (each TU size class's coefficient rate is counted on that class's stream as soon as
- * its TU pipeline ends, overlapping the remaining motion searches). */
-int hvx_ctu_encode(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
-                   const hvx_ctu_params *h_params, const hvx_estbits *d_est4, const uint8_t *d_ctx_states,
-                   const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes, hvx_cu_result *d_cu,
-                   hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic);
-
-/* The whole picture step at 4:2:0 (YUV): hvx_ctu_encode plus, for every CU, the chroma of
- * TEncSearch::encodeResAndCalcRdInterCU -- Cb/Cr motion compensation at the chosen MV (4-tap,
- * 1/8 sample, TComPrediction::xPredInterBlk), the Cb and Cr TUs (half the luma TU) through
- * transformNxN (RDOQ with the chroma QP and lambda_chroma, chroma estBits) + invTransformNxN, their
- * coefficient rate and cbf flags, xEstimateInterResidualQT's forced-zero test per TU and component
- * with chroma distortions weighted by chroma_weight (TComRdCost::getDistPart), the qt_root_cbf test
- * and the leaf distortion over all three components; the leaves' Y, Cb and Cr are reconstructed and,
- * with d_ref_pic, deblocked (loopFilterPic luma + chroma) and border-extended.  h_params->chroma_format
- * must be 1 (hvx_ctu_analyze / _decide / _encode require 0); d_est7 = 7 device estBits tables
- * (luma TU 4x4..32x32, chroma TU 4x4..16x16); h_chroma (host struct of device pointers, hvx_types.h)
- * gives the chroma planes.  hvx_cu_result keeps the luma sums; hvx_cu_decision.cbf carries the
- * chroma TU flags in bits 4..11. */
-int hvx_ctu_encode_yuv(hvx_ctx *ctx, const uint8_t *d_cur, const uint8_t *const *d_refs, int stride,
-                       const hvx_chroma_planes *h_chroma, const hvx_ctu_params *h_params, const hvx_estbits *d_est7,
-                       const uint8_t *d_ctx_states, const int32_t *d_entropy_bits, void *d_workspace, size_t ws_bytes,
-                       hvx_cu_result *d_cu, hvx_cu_decision *d_dec, uint8_t *d_recon, uint8_t *d_ref_pic);
 
 /* ---------------------------------------------------------------------------------------
  * Picture upload: HM int16 plane (width x height samples, any stride, device copy) ->

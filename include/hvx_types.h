@@ -118,87 +118,11 @@ typedef struct hvx_me_result {
   uint32_t cost;              /* ruiCost on exit */
 } hvx_me_result;
 
-/* ---------------------------------------------------------------------------------------
- * CTU analysis pass (the bench workload; see DESIGN.md "CTU analysis pass").
- * For every 64x64 CTU and every CU of depth 0..3 (85 square CUs) lying inside the picture:
- * uni-prediction ME (hvx_me_job semantics) against each reference, best reference =
- * first minimum of the ME cost, luma motion compensation at the chosen quarter-pel MV,
- * residual, then every min(CU,32)^2 luma TU of the CU through transformNxN (RDOQ) +
- * invTransformNxN + SSE.  CU index inside a CTU: depth-major, raster inside each depth
- * (0 | 1..4 | 5..20 | 21..84).
- * ------------------------------------------------------------------------------------- */
-#define HVX_CUS_PER_CTU 85
-typedef struct hvx_ctu_params {
-  int32_t pic_w, pic_h;      /* luma samples */
-  int32_t n_ref;             /* reference pictures (<= 8) */
-  int32_t qp;                /* slice QP (luma) */
-  int32_t search_range;      /* 64 */
-  int32_t me_flags;          /* HVX_ME_* */
-  int32_t slice_type;        /* HM SliceType (1 = P) */
-  uint32_t lambda_motion;    /* floor(65536*sqrt(lambda)) */
-  double lambda;             /* RD lambda (TComTrQuant m_dLambda for luma) */
-  double lambda_ssim;        /* HVX_RD_SSIM: the SSIM-RDO lambda (stvssim.c lambda_2 :1805 x attention eta^0.85) */
-  int32_t rd_metric;         /* hvx_ctu_decide's CU-level distortion: HVX_RD_SSE (HM) or HVX_RD_SSIM */
-  int32_t chroma_format;     /* 0: luma only (hvx_ctu_analyze/decide/encode); 1: 4:2:0 (hvx_ctu_encode_yuv) */
-  int32_t qp_chroma;         /* chroma QP: getScaledChromaQP(qp + chroma offset) (g_aucChromaScale, 4:2:0) */
-  int32_t pad_;
-  double lambda_chroma;      /* RDOQ lambda of Cb/Cr: lambda / chroma_weight (TEncSlice::setUpLambda, RDOQ_CHROMA_LAMBDA) */
-  double chroma_weight;      /* TComRdCost::m_distortionWeight[Cb/Cr] = pow(2, (qp - qp_chroma) / 3) */
-} hvx_ctu_params;
-/* HVX_RD_SSIM (BASELINE config 4): the CU quadtree decision of hvx_ctu_decide
- * weighs D_ssim = sum over the CU's 8x8 blocks of 1 - SSIM(original, reconstruction) (compute_SSIM,
- * stvssim.c:491, one 8x8 window; distortionSSIM :567) against lambda_ssim * bits, the stvssim RD
- * form J = D + lambda * R (rdopt.c:1631); the TU-level residual decisions stay on SSE as in HM. */
+/* CU-level distortion of the HM engine's mode / split comparisons (hvx_hm_picture.rd_metric):
+ * HVX_RD_SSE = HM's calcRdCost(bits, SSE); HVX_RD_SSIM = the stvssim encoder's SSIM cost (SURVEY 8(a)
+ * a20-a22, BASELINE config 4; see hvx_hm_picture). */
 #define HVX_RD_SSE 0
 #define HVX_RD_SSIM 1
-
-typedef struct hvx_cu_result {
-  int32_t valid;             /* CU inside the picture */
-  int32_t ref;               /* chosen reference index */
-  int32_t mv_x, mv_y;        /* quarter-pel MV */
-  uint32_t me_cost;          /* ruiCost of the chosen reference */
-  uint32_t sse;              /* sum over the CU's TUs of residual-domain SSE after coding */
-  int32_t abs_sum;           /* sum of uiAbsSum over the CU's TUs */
-  int32_t n_tu;
-} hvx_cu_result;
-
-/* CU decision over the analysed CTU (hvx_ctu_decide; DESIGN.md "CU decision").  Per CU, the residual
- * decisions of TEncSearch::encodeResAndCalcRdInterCU (TEncSearch.cpp:4341-4421) for its luma TUs:
- * xEstimateInterResidualQT's forced-zero test per TU (:4647-4768; cbf=0 + zero-residual distortion
- * against cbf=1 + counted coefficients + coded distortion), the TU tree's rate counted once
- * (:4973-4984), the qt_root_cbf test (:4361-4366) and the distortion of the clipped
- * reconstruction (:4408-4417); leaf bits = the ME's ruiBits + that residual rate (fracBits >> 15).
- * Then TEncCu::xCompressCU's depth recursion (TEncCu.cpp:349-877) with split_cu_flag bits
- * (TEncSbac.cpp:613; context from the left/above CU depths inside the CTU, TComDataCU.cpp:1487)
- * added as TEncCu.cpp:681,797 do, costs by TComRdCost::calcRdCost (TComRdCost.cpp:57:
- * floor(dist + bits*lambda + 0.5)) and a split taken only on a strictly smaller cost
- * (xCheckBestMode :1166).  All rates from one context snapshot.  One record per CU, same order
- * as hvx_cu_result. */
-typedef struct hvx_cu_decision {
-  uint64_t coef_frac;        /* sum over the CU's TUs (all components) of the counted coefficient rate (15-bit fixed point) */
-  uint32_t bits, dist;       /* the CU coded as a leaf (without its split_cu_flag); 4:2:0: dist = luma SSE + each
-                                chroma SSE times chroma_weight, truncated (TComRdCost::getDistPart) */
-  uint32_t best_bits, best_dist; /* the chosen sub-tree rooted at this CU, split flags included */
-  int32_t split;             /* 1: the sub-tree rooted here splits (forced for CUs crossing the picture edge) */
-  int32_t leaf;              /* 1: a leaf of the CTU's final CU tree (its samples are in the reconstruction) */
-  int32_t cbf;               /* bit t: luma TU t of the CU is coded; 4:2:0 also bit 4 + t: Cb TU t, bit 8 + t: Cr TU t,
-                                and bit 12 + t / 16 + t: that Cb / Cr TU (4x4, 8x8 CU) is coded in transform-skip
-                                mode (0: qt_root_cbf 0, prediction only) */
-  float ssim_dist;           /* HVX_RD_SSIM: D_ssim of the CU as a leaf (8x8 blocks in raster order, float sum) */
-  float best_ssim_dist;      /* HVX_RD_SSIM: D_ssim of the chosen sub-tree (children in z-order) */
-  int32_t pad_;
-} hvx_cu_decision;
-
-/* The chroma planes of hvx_ctu_encode_yuv (4:2:0): device origins (sample (0,0)) of 8-bit padded
- * planes of half the luma size with margin HVX_PLANE_MARGIN / 2 and stride c_stride (a multiple of 4).
- * refs_c: device array of 2 * n_ref origins, the references' Cb planes then their Cr planes. */
-typedef struct hvx_chroma_planes {
-  const uint8_t *cur_cb, *cur_cr;
-  const uint8_t *const *refs_c;
-  uint8_t *recon_cb, *recon_cr;
-  uint8_t *ref_pic_cb, *ref_pic_cr;  /* NULL when no reference picture is written */
-  int32_t c_stride, pad_;
-} hvx_chroma_planes;
 
 /* One intra block: TComPrediction::initIntraPatternChType's reference
  * samples (TComPattern.cpp:115-360: fillReferenceSamples :364 substitution + the [1 2 1] /

@@ -57,7 +57,6 @@ def lib():
         L.hvxo_lambda_2.argtypes = [I]
         L.hvxo_adjust_lambda.restype = D
         L.hvxo_adjust_lambda.argtypes = [D, D]
-        L.hvxo_ctu_analyze.argtypes = [P, P, I, P, P, I, I, P]
         L.hvxo_estbits_update.argtypes = [P, P, P, I, I, I, P]
         L.hvxo_mc.argtypes = [P, I, I, P, P]
         L.hvxo_me_full.argtypes = [P, I, P, I, P, P]
@@ -192,72 +191,6 @@ def stvssim(org_frames, rec_frames, dirs, w, h, wint, overlap, gama, comp):
     return float(ret), s1.value, s2.value, s3.value
 
 
-def ctu_analyze(cur_plane, ref_planes, params, est4, ctu_x, ctu_y, margin=_abi.PLANE_MARGIN):
-    """hvxo_ctu_analyze for one CTU: padded uint8 planes -> 85 CU_RESULT records."""
-    c = _c(cur_plane, np.uint8)
-    refs = [_c(r, np.uint8) for r in ref_planes]
-    off = margin * c.shape[1] + margin
-    rp = (ctypes.c_void_p * len(refs))(*[r.ctypes.data + off for r in refs])
-    p = np.ascontiguousarray(params, dtype=_abi.CTU_PARAMS).reshape(1)
-    e = _c(est4, np.int32).reshape(-1)
-    out = np.zeros(_abi.CUS_PER_CTU, _abi.CU_RESULT)
-    lib().hvxo_ctu_analyze(ctypes.c_void_p(c.ctypes.data + off), rp, c.shape[1], _p(p), _p(e), ctu_x, ctu_y, _p(out))
-    return out
-
-
-def ctu_decide(cur_plane, ref_planes, params, est4, states, entropy_bits, ctu_x, ctu_y, recon_plane,
-               margin=_abi.PLANE_MARGIN):
-    """hvxo_ctu_decide for one CTU: -> (85 CU_RESULT, 85 CU_DECISION); the leaves' luma is
-    written into recon_plane (a padded uint8 plane like cur_plane, modified in place)."""
-    L = lib()
-    c = _c(cur_plane, np.uint8)
-    refs = [_c(r, np.uint8) for r in ref_planes]
-    off = margin * c.shape[1] + margin
-    rp = (ctypes.c_void_p * len(refs))(*[r.ctypes.data + off for r in refs])
-    p = np.ascontiguousarray(params, dtype=_abi.CTU_PARAMS).reshape(1)
-    e = _c(est4, np.int32).reshape(-1)
-    st = _c(states, np.uint8)
-    eb = _c(entropy_bits, np.int32)
-    assert recon_plane.dtype == np.uint8 and recon_plane.flags.c_contiguous and recon_plane.shape == c.shape
-    out = np.zeros(_abi.CUS_PER_CTU, _abi.CU_RESULT)
-    dec = np.zeros(_abi.CUS_PER_CTU, _abi.CU_DECISION)
-    L.hvxo_ctu_decide.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
-                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
-                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-    L.hvxo_ctu_decide(ctypes.c_void_p(c.ctypes.data + off), rp, c.shape[1], _p(p), _p(e), _p(st), _p(eb), ctu_x, ctu_y,
-                      _p(out), _p(dec), ctypes.c_void_p(recon_plane.ctypes.data + off), c.shape[1])
-    return out, dec
-
-
-def ctu_decide_yuv(cur3, refs3, params, est7, states, entropy_bits, ctu_x, ctu_y, recon3, margin=_abi.PLANE_MARGIN):
-    """hvxo_ctu_decide_yuv for one CTU (4:2:0): cur3 / recon3 = (Y, Cb, Cr) padded uint8 planes (chroma
-    margin margin // 2), refs3 = (list of Y planes, list of Cb planes, list of Cr planes), est7 = 7 estBits
-    tables (luma 4x4..32x32, chroma 4x4..16x16) -> (85 CU_RESULT, 85 CU_DECISION); the leaves' samples are
-    written into recon3 (modified in place)."""
-    L = lib()
-    P = ctypes.c_void_p
-    cs = [_c(x, np.uint8) for x in cur3]
-    offs = [margin * cs[0].shape[1] + margin, (margin // 2) * cs[1].shape[1] + margin // 2]
-    ptr = lambda a, c: a.ctypes.data + offs[1 if c else 0]  # noqa: E731
-    cur_p = (P * 3)(*[ptr(cs[c], c) for c in range(3)])
-    keep = [[_c(r, np.uint8) for r in refs3[c]] for c in range(3)]
-    rp = [(P * len(keep[c]))(*[ptr(r, c) for r in keep[c]]) for c in range(3)]
-    for c in range(3):
-        assert recon3[c].dtype == np.uint8 and recon3[c].flags.c_contiguous and recon3[c].shape == cs[c].shape
-    rec_p = (P * 3)(*[ptr(recon3[c], c) for c in range(3)])
-    p = np.ascontiguousarray(params, dtype=_abi.CTU_PARAMS).reshape(1)
-    e = _c(est7, np.int32).reshape(-1)
-    st = _c(states, np.uint8)
-    eb = _c(entropy_bits, np.int32)
-    out = np.zeros(_abi.CUS_PER_CTU, _abi.CU_RESULT)
-    dec = np.zeros(_abi.CUS_PER_CTU, _abi.CU_DECISION)
-    I = ctypes.c_int
-    L.hvxo_ctu_decide_yuv.argtypes = [P, P, P, P, I, I, P, P, P, P, I, I, P, P, P, I, I]
-    L.hvxo_ctu_decide_yuv(cur_p, rp[0], rp[1], rp[2], cs[0].shape[1], cs[1].shape[1], _p(p), _p(e), _p(st), _p(eb),
-                          ctu_x, ctu_y, _p(out), _p(dec), rec_p, cs[0].shape[1], cs[1].shape[1])
-    return out, dec
-
-
 def lambda_2(qp):
     return float(lib().hvxo_lambda_2(int(qp)))
 
@@ -298,18 +231,6 @@ def mc(planes, luma_stride, chroma_stride, job):
     out = np.zeros(w * h + 2 * (w // 2) * (h // 2), np.int16)
     lib().hvxo_mc(ptrs, int(luma_stride), int(chroma_stride), _p(j), _p(out))
     return out
-
-
-def chroma_block_epel(plane, x, y, mvx, mvy, w, h, margin=_abi.PLANE_MARGIN // 2):
-    """hvxo_chroma_block_epel on a padded uint8 chroma plane (sample (x, y) relative to its origin)."""
-    c = _c(plane, np.uint8)
-    out = np.zeros(w * h, np.int16)
-    L = lib()
-    L.hvxo_chroma_block_epel.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
-    L.hvxo_chroma_block_epel(ctypes.c_void_p(c.ctypes.data + margin * c.shape[1] + margin), c.shape[1], x, y, mvx, mvy,
-                             w, h, _p(out), w)
-    return out.reshape(h, w)
 
 
 def add_avg(a, b):
@@ -446,18 +367,6 @@ def deblock(y, cb, cr, bs_ver, bs_hor, qp, params):
     p = np.ascontiguousarray(params)
     L.hvxo_deblock(_p(y), y.shape[1], _p(cb), _p(cr), cb.shape[1], _p(bv), _p(bh), _p(q), _p(p))
     return y, cb, cr
-
-
-def ctu_bs(cu, dec, pic_w, pic_h):
-    """hvxo_ctu_bs: (bs_ver, bs_hor) maps of a whole analysed + decided picture."""
-    L = lib()
-    L.hvxo_ctu_bs.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int] * 2 + [ctypes.c_void_p] * 2
-    c = np.ascontiguousarray(cu, dtype=_abi.CU_RESULT).reshape(-1)
-    d = np.ascontiguousarray(dec, dtype=_abi.CU_DECISION).reshape(-1)
-    bv = np.zeros((pic_h // 4) * (pic_w // 4), np.uint8)
-    bh = np.zeros_like(bv)
-    L.hvxo_ctu_bs(_p(c), _p(d), int(pic_w), int(pic_h), _p(bv), _p(bh))
-    return bv, bh
 
 
 def sao_stats(org, rec, comp):

@@ -296,40 +296,6 @@ void hvxo_luma_block_qpel(const uint8_t *ref, int stride, int x, int y, int mvx,
     }
 }
 
-/* xPredInterBlk (TComPrediction.cpp:668) for a 4:2:0 chroma block of an 8-bit plane, uni-prediction:
- * the luma quarter-pel MV in 1/8 chroma samples, the 4-tap filters (TComInterpolationFilter.cpp:67),
- * filterHor / filterVer alone (first and last stage) or filterHor (first) then filterVer (last). */
-void hvxo_chroma_block_epel(const uint8_t *ref, int stride, int x, int y, int mvx, int mvy, int w, int h, int16_t *out,
-                            int os) {
-  static const int8_t cf[8][4] = {{0, 64, 0, 0},   {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
-                                  {-4, 36, 36, -4}, {-4, 28, 46, -6}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
-  const int fx = mvx & 7, fy = mvy & 7, ix = x + (mvx >> 3), iy = y + (mvy >> 3);
-  for (int r = 0; r < h; r++)
-    for (int c = 0; c < w; c++) {
-      const uint8_t *p = ref + (iy + r) * stride + ix + c;
-      int v;
-      if (!fx && !fy) v = p[0];
-      else if (!fy) {
-        int s = 0;
-        for (int k = 0; k < 4; k++) s += cf[fx][k] * p[k - 1];
-        v = clip_pel((s + 32) >> 6);
-      } else if (!fx) {
-        int s = 0;
-        for (int k = 0; k < 4; k++) s += cf[fy][k] * p[(k - 1) * stride];
-        v = clip_pel((s + 32) >> 6);
-      } else {
-        int s2 = 0;
-        for (int t = 0; t < 4; t++) {
-          int s = 0;
-          for (int k = 0; k < 4; k++) s += cf[fx][k] * p[(t - 1) * stride + k - 1];
-          s2 += cf[fy][t] * (int16_t)(s - IF_OFFS);
-        }
-        v = clip_pel((s2 + (1 << 11) + (IF_OFFS << 6)) >> 12);
-      }
-      out[r * os + c] = (int16_t)v;
-    }
-}
-
 /* ============================================================================================
  * Transforms: xTrMxN / xITrMxN (TComTrQuant.cpp:860-987).  Partial butterflies (:388-848) are
  * exact integer matrix products; written here as the products they compute.
@@ -1391,462 +1357,6 @@ double hvxo_lambda_2(int qp) {
 double hvxo_adjust_lambda(double lambda, double eta) { return lambda * pow(eta, 0.85); }
 
 /* ============================================================================================
- * CTU analysis pass (hvx_types.h): composition of the restated kernels above.
- * ========================================================================================== */
-void hvxo_ctu_tu_desc(const hvx_ctu_params *p, int cu_size, int log2, hvx_tu_desc *d) {
-  memset(d, 0, sizeof(*d));
-  d->comp = 0;
-  d->width = d->height = 1 << log2;
-  d->log2_size = log2;
-  d->tr_idx = cu_size > 32 ? 1 : 0;     /* a 64x64 CU is coded with a split transform tree */
-  d->ctx_qt_cbf = 0;                    /* luma getCtxQtCbf at transform depth >= 1 */
-  d->slice_type = p->slice_type;
-  d->qp_per = p->qp / 6;
-  d->qp_rem = p->qp % 6;
-  d->sign_hiding = 1;
-  d->use_rdoq = d->use_rdoq_ts = 1;
-  d->pps_tskip = 1;                     /* TransformSkip=1 (cfg): 4x4 TUs code transform_skip_flag */
-  d->max_log2_tr_range = 15;
-  d->bit_depth = 8;
-  d->lambda = p->lambda;
-}
-
-/* the Cb/Cr TU of a CU (4:2:0, half the luma TU): chroma QP and the chroma RDOQ lambda, chroma
- * getCtxQtCbf = the transform depth (TComDataCU.cpp:1503) */
-void hvxo_ctu_tu_desc_chroma(const hvx_ctu_params *p, int comp, int cu_size, int log2, hvx_tu_desc *d) {
-  hvxo_ctu_tu_desc(p, cu_size, log2, d);
-  d->comp = comp;
-  d->ctx_qt_cbf = cu_size > 32 ? 1 : 0;
-  d->qp_per = p->qp_chroma / 6;
-  d->qp_rem = p->qp_chroma % 6;
-  d->lambda = p->lambda_chroma;
-}
-
-/* chroma planes of the 4:2:0 analysis (hvx_chroma_planes in host form) */
-typedef struct {
-  const uint8_t *cur[2];
-  const uint8_t *const *refs[2];
-  int stride;
-} ctu_chroma;
-
-/* The analysis of one CTU; with ex != NULL it also keeps, per TU of every CU, the counted
- * coefficient rate, uiAbsSum, the coded (residual-domain) SSE and the zero-residual distortion,
- * and per CU the ME bits of the chosen reference, the prediction and the reconstructed residual
- * (64x64 per CU). */
-typedef struct {
-  const uint8_t *states;
-  const int32_t *eb;
-  /* [cu][comp][tu]: comp 0 luma, 1 Cb, 2 Cr (4:2:0 only) */
-  uint64_t coef_frac[HVX_CUS_PER_CTU][3][4];
-  int32_t abs_sum[HVX_CUS_PER_CTU][3][4];
-  uint32_t sse[HVX_CUS_PER_CTU][3][4], zdist[HVX_CUS_PER_CTU][3][4];
-  uint32_t me_bits[HVX_CUS_PER_CTU];
-  uint8_t *pred;  /* HVX_CUS_PER_CTU * 4096 luma, then HVX_CUS_PER_CTU * 2 * 1024 chroma */
-  int16_t *rres;  /* same layout */
-  /* the transform-skip mode of the 4x4 chroma TUs of the 8x8 CUs: [cu][comp - 1] */
-  uint64_t ts_frac[HVX_CUS_PER_CTU][2];
-  int32_t ts_abs[HVX_CUS_PER_CTU][2];
-  uint32_t ts_sse[HVX_CUS_PER_CTU][2];
-  int16_t ts_rres[HVX_CUS_PER_CTU][2][16];
-} ctu_extra;
-#define EX_CHROMA(ci, c) (HVX_CUS_PER_CTU * 4096 + ((ci) * 2 + (c) - 1) * 1024)
-
-/* one component's TUs of a CU: residual (org - pred), transformNxN (RDOQ) + invTransformNxN + SSE
- * per TU; with ex, the counted rate (own copy of the snapshot), uiAbsSum, SSEs, prediction and
- * reconstructed residual.  Returns the summed (sse, abs_sum) through the pointers. */
-static void ctu_comp_tus(const uint8_t *org, int ostride, const int16_t *pred, int ps, int S, const hvx_tu_desc *td,
-                         const hvx_estbits *e, ctu_extra *ex, int ci, int comp, uint32_t *sse_sum, int32_t *abs_total,
-                         int *n_tu) {
-  const int T = td->width;
-  int16_t resi[32 * 32], rec[32 * 32];
-  for (int ty = 0; ty < S; ty += T)
-    for (int tx = 0; tx < S; tx += T) {
-      for (int yy = 0; yy < T; yy++)
-        for (int xx = 0; xx < T; xx++)
-          resi[yy * T + xx] = (int16_t)((int)org[(ty + yy) * ostride + tx + xx] - pred[(ty + yy) * ps + tx + xx]);
-      int32_t temp[1024], lev[1024], abs_sum = 0;
-      hvxo_transform_nxn(td, e, resi, T, temp, lev, NULL, &abs_sum);
-      hvxo_inv_transform_nxn(td, lev, rec, T);
-      uint32_t sse = 0;
-      for (int k = 0; k < T * T; k++) { int df = resi[k] - rec[k]; sse += (uint32_t)(df * df); }
-      if (ex) {
-        const int ti = (ty / T) * (S / T) + tx / T;
-        uint8_t st[HVX_NUM_CTX];
-        hvx_coeff_bits cb;
-        memcpy(st, ex->states, sizeof(st)); /* every TU counts from the same snapshot */
-        hvxo_coeff_bits(td, lev, st, ex->eb, &cb);
-        uint32_t zd = 0;
-        for (int k = 0; k < T * T; k++) zd += (uint32_t)(resi[k] * resi[k]);
-        ex->coef_frac[ci][comp][ti] = cb.frac_bits;
-        ex->abs_sum[ci][comp][ti] = abs_sum;
-        ex->sse[ci][comp][ti] = sse;
-        ex->zdist[ci][comp][ti] = zd;
-        const size_t base = comp ? (size_t)EX_CHROMA(ci, comp) : (size_t)ci * 4096;
-        const int es = comp ? 32 : 64;
-        for (int yy = 0; yy < T; yy++)
-          for (int xx = 0; xx < T; xx++) {
-            ex->pred[base + (ty + yy) * es + tx + xx] = (uint8_t)pred[(ty + yy) * ps + tx + xx];
-            ex->rres[base + (ty + yy) * es + tx + xx] = rec[yy * T + xx];
-          }
-      }
-      *sse_sum += sse;
-      *abs_total += abs_sum;
-      (*n_tu)++;
-    }
-}
-
-static void ctu_analyze_core(const uint8_t *cur, const uint8_t *const *refs, int stride, const ctu_chroma *cc,
-                             const hvx_ctu_params *p, const hvx_estbits *est, int ctu_x, int ctu_y, hvx_cu_result *out,
-                             ctu_extra *ex) {
-  int imv[HVX_CUS_PER_CTU][8][2];
-  int base = 0;
-  for (int d = 0; d < 4; d++) {
-    const int S = 64 >> d, g = 1 << d;
-    for (int j = 0; j < g * g; j++) {
-      const int cy = j / g, cx = j % g, ci = base + j;
-      const int x = ctu_x * 64 + cx * S, y = ctu_y * 64 + cy * S;
-      hvx_cu_result *r = &out[ci];
-      memset(r, 0, sizeof(*r));
-      r->valid = (x + S <= p->pic_w) && (y + S <= p->pic_h);
-      if (!r->valid) continue;
-      const int parent = d ? (base - (g / 2) * (g / 2)) + (cy / 2) * (g / 2) + (cx / 2) : -1;
-      uint32_t best_cost = 0;
-      hvx_me_result best;
-      memset(&best, 0, sizeof(best));
-      for (int ref = 0; ref < p->n_ref; ref++) {
-        hvx_me_job jb;
-        memset(&jb, 0, sizeof(jb));
-        jb.pic_w = p->pic_w; jb.pic_h = p->pic_h; jb.max_cu = 64;
-        jb.cu_x = jb.pu_x = x; jb.cu_y = jb.pu_y = y; jb.w = jb.h = S;
-        jb.use_int2nx2n = parent >= 0 && out[parent].valid;
-        if (jb.use_int2nx2n) { jb.i2_x = imv[parent][ref][0]; jb.i2_y = imv[parent][ref][1]; }
-        jb.search_range = p->search_range;
-        jb.lambda_motion = p->lambda_motion;
-        jb.flags = p->me_flags;
-        hvx_me_result mr;
-        hvxo_motion_estimation(cur, stride, refs[ref], stride, &jb, &mr);
-        imv[ci][ref][0] = mr.mv_int_x;
-        imv[ci][ref][1] = mr.mv_int_y;
-        if (ref == 0 || mr.cost < best_cost) { best_cost = mr.cost; best = mr; r->ref = ref; }
-      }
-      if (ex) ex->me_bits[ci] = best.bits;
-      r->mv_x = best.mv_x; r->mv_y = best.mv_y; r->me_cost = best_cost;
-      int16_t pred[64 * 64];
-      hvxo_luma_block_qpel(refs[r->ref], stride, x, y, best.mv_x, best.mv_y, S, S, pred, 64);
-      const int T = S < 32 ? S : 32, log2 = T == 4 ? 2 : T == 8 ? 3 : T == 16 ? 4 : 5;
-      hvx_tu_desc td;
-      hvxo_ctu_tu_desc(p, S, log2, &td);
-      ctu_comp_tus(cur + y * stride + x, stride, pred, 64, S, &td, &est[log2 - 2], ex, ci, 0, &r->sse, &r->abs_sum,
-                   &r->n_tu);
-      if (cc) {  /* 4:2:0: the Cb / Cr TUs (half size) after the luma; hvx_cu_result keeps the luma sums */
-        uint32_t cs = 0;
-        int32_t ca = 0;
-        int cn = 0;
-        for (int c = 1; c <= 2; c++) {
-          int16_t cp[32 * 32];
-          hvxo_chroma_block_epel(cc->refs[c - 1][r->ref], cc->stride, x / 2, y / 2, best.mv_x, best.mv_y, S / 2, S / 2,
-                                 cp, 32);
-          hvx_tu_desc tc;
-          hvxo_ctu_tu_desc_chroma(p, c, S, log2 - 1, &tc);
-          const uint8_t *org = cc->cur[c - 1] + (y / 2) * cc->stride + x / 2;
-          ctu_comp_tus(org, cc->stride, cp, 32, S / 2, &tc, &est[4 + log2 - 3], ex, ci, c, &cs, &ca, &cn);
-          if (S == 8 && ex) {
-            /* xEstimateInterResidualQT's second mode of a 4x4 TU (TEncSearch.cpp:4516-4565,
-             * TransformSkip=1): the same residual through transformNxN with transform skip (RDOQTS) */
-            int16_t resi[16], rec[16];
-            for (int k = 0; k < 16; k++) resi[k] = (int16_t)((int)org[(k / 4) * cc->stride + k % 4] - cp[(k / 4) * 32 + k % 4]);
-            tc.transform_skip = 1;
-            int32_t temp[16], lev[16], abs_sum = 0;
-            hvxo_transform_nxn(&tc, &est[4], resi, 4, temp, lev, NULL, &abs_sum);
-            hvxo_inv_transform_nxn(&tc, lev, rec, 4);
-            uint32_t sse = 0;
-            for (int k = 0; k < 16; k++) { int df = resi[k] - rec[k]; sse += (uint32_t)(df * df); }
-            uint8_t st[HVX_NUM_CTX];
-            hvx_coeff_bits cb;
-            memcpy(st, ex->states, sizeof(st));
-            hvxo_coeff_bits(&tc, lev, st, ex->eb, &cb);
-            ex->ts_frac[ci][c - 1] = cb.frac_bits;
-            ex->ts_abs[ci][c - 1] = abs_sum;
-            ex->ts_sse[ci][c - 1] = sse;
-            memcpy(ex->ts_rres[ci][c - 1], rec, sizeof(rec));
-          }
-        }
-      }
-    }
-    base += g * g;
-  }
-}
-
-void hvxo_ctu_analyze(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
-                      const hvx_estbits *est, int ctu_x, int ctu_y, hvx_cu_result *out) {
-  ctu_analyze_core(cur, refs, stride, NULL, p, est, ctu_x, ctu_y, out, NULL);
-}
-
-/* ---- CU decision: TEncCu::xCompressCU's depth recursion (TEncCu.cpp:349-877) ---- */
-typedef struct {
-  const hvx_ctu_params *p;
-  const ctu_chroma *cc;  /* 4:2:0, else NULL */
-  const hvx_cu_result *cu;
-  const ctu_extra *ex;
-  hvx_cu_decision *dec;
-  uint8_t depth[8][8]; /* final CU depth per 8x8 of the CTU (TComDataCU::getDepth) */
-  int ctu_x, ctu_y;
-  const uint8_t *cur;  /* sample (0,0) of the original */
-  int stride;
-} decide_ctx;
-
-/* TComRdCost::calcRdCost, DF_DEFAULT lossy (TComRdCost.cpp:57-120) */
-static double rd_cost(uint32_t bits, uint32_t dist, double lambda) {
-  return floor((double)dist + (double)bits * lambda + 0.5);
-}
-
-/* split_cu_flag bits: TEncSbac::codeSplitFlag (TEncSbac.cpp:613) counted alone (resetBits ..
- * getNumberOfWrittenBits, TEncCu.cpp:681,797), context TComDataCU::getCtxSplitFlag
- * (TComDataCU.cpp:1487) from the left / above CU depths; neighbours outside the CTU count as
- * unavailable here (the CTUs are analysed independently) */
-static uint32_t split_flag_bits(const decide_ctx *c, int d, int x8, int y8, int bin) {
-  int ctx = 0;
-  if (x8 > 0 && c->depth[y8][x8 - 1] > d) ctx++;
-  if (y8 > 0 && c->depth[y8 - 1][x8] > d) ctx++;
-  const uint8_t st = c->ex->states[ctx]; /* models 0..2: split flag */
-  return (uint32_t)c->ex->eb[st ^ bin] >> 15;
-}
-
-/* TComRdCost::getDistPart of a chroma block: m_distortionWeight * SSE, truncated (TComRdCost.cpp:443-446) */
-static uint32_t wdist(double w, uint32_t sse) { return (uint32_t)(w * (double)sse); }
-
-/* TEncSearch::encodeResAndCalcRdInterCU's residual decisions for the CU's TUs (transform depth
- * 1 in a 64x64 CU, else 0), per TU and component (Y, and at 4:2:0 Cb, Cr): the forced-zero test of
- * xEstimateInterResidualQT (TEncSearch.cpp:4647-4768: cbf=0 with the zero-residual distortion against
- * cbf=1 + the counted coefficients with the coded distortion, each counted alone; chroma distortions
- * weighted per TU by getDistPart), the TU tree's rate counted once (:4973-4984), the qt_root_cbf test
- * (:4361-4366), then the distortion of the clipped reconstruction (:4408-4417, chroma weighted per
- * component).  Context models: luma qt_cbf 28 + getCtxQtCbf (TComDataCU.cpp:1503, 1 at transform
- * depth 0), chroma qt_cbf 33 + the transform depth, qt_root_cbf 41 (TEncSbac::codeQtRootCbfZero :1097).
- * A 4x4 chroma TU (8x8 CU) also tries its transform-skip mode (TransformSkip=1, :4516-4565,
- * 4741-4753): chosen when its coded cost is <= mode 0's best.  The chroma cbf of the 64x64 root
- * node and split_transform_flag are not counted (no RQT here). */
-static void leaf_eval(const decide_ctx *c, int ci, int S, int x, int y, hvx_cu_decision *o) {
-  const ctu_extra *ex = c->ex;
-  const int T = S < 32 ? S : 32, ntu = (S / T) * (S / T), ncomp = c->cc ? 3 : 1;
-  const double lam = c->p->lambda, w = c->p->chroma_weight;
-  uint64_t tree = 0, cf = 0;
-  uint32_t nz_dist = 0, zero_dist = 0;
-  int cbf = 0;
-  for (int t = 0; t < ntu; t++)
-    for (int comp = 0; comp < ncomp; comp++) {
-      const int m_cbf = comp ? 33 + (S > 32 ? 1 : 0) : 28 + (S > 32 ? 0 : 1);
-      const uint32_t c0 = (uint32_t)ex->eb[ex->states[m_cbf] ^ 0], c1 = (uint32_t)ex->eb[ex->states[m_cbf] ^ 1];
-      uint64_t tf = c0;
-      uint32_t td = comp ? wdist(w, ex->zdist[ci][comp][t]) : ex->zdist[ci][comp][t];
-      zero_dist += td;
-      cf += ex->coef_frac[ci][comp][t];
-      if (ex->abs_sum[ci][comp][t] > 0) {
-        const uint64_t f1 = c1 + ex->coef_frac[ci][comp][t];
-        const uint32_t sd = comp ? wdist(w, ex->sse[ci][comp][t]) : ex->sse[ci][comp][t];
-        if (!(rd_cost(c0 >> 15, td, lam) < rd_cost((uint32_t)(f1 >> 15), sd, lam))) {
-          tf = f1;
-          td = sd;
-          cbf |= 1 << (4 * comp + t);
-        }
-      }
-      if (comp && T == 8 && ex->ts_abs[ci][comp - 1] > 0) {
-        /* the transform-skip mode (:4741-4753): its coded cost replaces mode 0's best on <= */
-        const uint64_t f2 = c1 + ex->ts_frac[ci][comp - 1];
-        const uint32_t sd = wdist(w, ex->ts_sse[ci][comp - 1]);
-        if (rd_cost((uint32_t)(f2 >> 15), sd, lam) <= rd_cost((uint32_t)(tf >> 15), td, lam)) {
-          tf = f2;
-          td = sd;
-          cbf |= (1 << (4 * comp + t)) | (1 << (8 + 4 * comp + t));
-        }
-      }
-      tree += tf;
-      nz_dist += td;
-    }
-  const uint32_t r0 = (uint32_t)ex->eb[ex->states[41] ^ 0], r1 = (uint32_t)ex->eb[ex->states[41] ^ 1];
-  if (rd_cost(r0 >> 15, zero_dist, lam) < rd_cost((uint32_t)(tree >> 15), nz_dist, lam)) cbf = 0;
-  uint32_t dist = 0;
-  for (int yy = 0; yy < S; yy++)
-    for (int xx = 0; xx < S; xx++) {
-      const int t = (yy / T) * (S / T) + xx / T, k = ci * 4096 + yy * 64 + xx;
-      const int rec = clip_pel(ex->pred[k] + (((cbf >> t) & 1) ? ex->rres[k] : 0));
-      const int df = (int)c->cur[(y + yy) * c->stride + x + xx] - rec;
-      dist += (uint32_t)(df * df);
-    }
-  for (int comp = 1; comp < ncomp; comp++) {
-    const int Sc = S / 2, Tc = T / 2;
-    uint32_t cd = 0;
-    for (int yy = 0; yy < Sc; yy++)
-      for (int xx = 0; xx < Sc; xx++) {
-        const int t = (yy / Tc) * (Sc / Tc) + xx / Tc, k = EX_CHROMA(ci, comp) + yy * 32 + xx;
-        const int rr = ((cbf >> (8 + 4 * comp + t)) & 1) ? ex->ts_rres[ci][comp - 1][yy * 4 + xx] : ex->rres[k];
-        const int rec = clip_pel(ex->pred[k] + (((cbf >> (4 * comp + t)) & 1) ? rr : 0));
-        const int df = (int)c->cc->cur[comp - 1][(y / 2 + yy) * c->cc->stride + x / 2 + xx] - rec;
-        cd += (uint32_t)(df * df);
-      }
-    dist += wdist(w, cd);
-  }
-  o->coef_frac = cf;
-  o->cbf = cbf;
-  o->bits = ex->me_bits[ci] + (uint32_t)((cbf ? r1 + tree : r0) >> 15);
-  o->dist = dist;
-  o->ssim_dist = 0.0f;
-  if (c->p->rd_metric == HVX_RD_SSIM) {
-    /* D_ssim: distortionSSIM's 1 - compute_SSIM (stvssim.c:567-575) per 8x8 block of the CU's luma
-     * (one 8x8 window each), summed in raster block order as float */
-    float dsum = 0.0f;
-    for (int by = 0; by < S / 8; by++)
-      for (int bx = 0; bx < S / 8; bx++) {
-        uint8_t rb[64];
-        for (int r = 0; r < 8; r++)
-          for (int q = 0; q < 8; q++) {
-            const int yy = by * 8 + r, xx = bx * 8 + q, t = (yy / T) * (S / T) + xx / T, k = ci * 4096 + yy * 64 + xx;
-            rb[r * 8 + q] = (uint8_t)clip_pel(ex->pred[k] + (((cbf >> t) & 1) ? ex->rres[k] : 0));
-          }
-        const float sv = hvxo_ssim(c->cur + (y + by * 8) * c->stride + x + bx * 8, c->stride, rb, 8, 8, 8, 8, 8);
-        dsum += 1.0f - sv;
-      }
-    o->ssim_dist = dsum;
-  }
-}
-
-/* the CU-level RD cost: calcRdCost for HVX_RD_SSE; D_ssim + lambda_ssim * R for HVX_RD_SSIM
- * (stvssim's J = D + lambda R, rdopt.c:1631) */
-static double cu_cost(const hvx_ctu_params *p, uint32_t bits, uint32_t dist, float sdist) {
-  if (p->rd_metric == HVX_RD_SSIM) return (double)sdist + p->lambda_ssim * (double)bits;
-  return rd_cost(bits, dist, p->lambda);
-}
-
-/* returns 0 if the CU lies wholly outside the picture; else fills bits and dist of its best tree */
-static int decide_node(decide_ctx *c, int d, int j, uint32_t *bits, uint32_t *dist, float *sdist) {
-  static const int base[4] = {0, 1, 5, 21};
-  const int g = 1 << d, S = 64 >> d, cx = j % g, cy = j / g, ci = base[d] + j;
-  const int x = c->ctu_x * 64 + cx * S, y = c->ctu_y * 64 + cy * S;
-  const int x8 = cx * S / 8, y8 = cy * S / 8, n8 = S / 8;
-  if (x >= c->p->pic_w || y >= c->p->pic_h) return 0;
-  hvx_cu_decision *o = &c->dec[ci];
-  const int valid = c->cu[ci].valid;
-  uint32_t lb = 0, ld = 0;
-  float ls = 0.0f;
-  if (valid) {
-    leaf_eval(c, ci, S, x, y, o);
-    lb = o->bits + (d < 3 ? split_flag_bits(c, d, x8, y8, 0) : 0);
-    ld = o->dist;
-    ls = o->ssim_dist;
-  }
-  int split = !valid;
-  uint32_t sb = 0, sd = 0;
-  float ss = 0.0f;
-  if (d < 3) {
-    for (int k = 0; k < 4; k++) {
-      uint32_t b, dd;
-      float sv;
-      const int cj = (2 * cy + (k >> 1)) * (2 * g) + 2 * cx + (k & 1);
-      if (decide_node(c, d + 1, cj, &b, &dd, &sv)) { sb += b; sd += dd; ss += sv; }
-    }
-    if (valid) sb += split_flag_bits(c, d, x8, y8, 1); /* no split flag at a boundary CU */
-    if (valid && cu_cost(c->p, sb, sd, ss) < cu_cost(c->p, lb, ld, ls)) split = 1;
-  }
-  o->split = split;
-  o->best_bits = split ? sb : lb;
-  o->best_dist = split ? sd : ld;
-  o->best_ssim_dist = split ? ss : ls;
-  if (!split) {
-    for (int yy = 0; yy < n8; yy++)
-      for (int xx = 0; xx < n8; xx++) c->depth[y8 + yy][x8 + xx] = (uint8_t)d;
-  }
-  *bits = o->best_bits;
-  *dist = o->best_dist;
-  *sdist = o->best_ssim_dist;
-  return 1;
-}
-
-static void ctu_decide_core(const uint8_t *cur, const uint8_t *const *refs, int stride, const ctu_chroma *cc,
-                            const hvx_ctu_params *p, const hvx_estbits *est, const uint8_t *states, const int32_t *eb,
-                            int ctu_x, int ctu_y, hvx_cu_result *out_cu, hvx_cu_decision *out_dec, uint8_t *recon,
-                            int recon_stride, uint8_t *const *recon_c, int recon_c_stride) {
-  ctu_extra *ex = (ctu_extra *)calloc(1, sizeof(ctu_extra));
-  ex->states = states;
-  ex->eb = eb;
-  ex->pred = (uint8_t *)calloc(HVX_CUS_PER_CTU * 6144, 1);
-  ex->rres = (int16_t *)calloc(HVX_CUS_PER_CTU * 6144, sizeof(int16_t));
-  ctu_analyze_core(cur, refs, stride, cc, p, est, ctu_x, ctu_y, out_cu, ex);
-  decide_ctx c;
-  memset(&c, 0, sizeof(c));
-  c.p = p; c.cc = cc; c.cu = out_cu; c.ex = ex; c.dec = out_dec; c.ctu_x = ctu_x; c.ctu_y = ctu_y;
-  c.cur = cur; c.stride = stride;
-  memset(out_dec, 0, sizeof(hvx_cu_decision) * HVX_CUS_PER_CTU);
-  uint32_t b, d;
-  float sd;
-  decide_node(&c, 0, 0, &b, &d, &sd);
-  static const int base[4] = {0, 1, 5, 21};
-  /* the final tree, top-down: a CU is a leaf when it is reached (the root, or a child of a
-   * reached CU that splits), lies in the picture and does not split itself */
-  {
-    int reached[HVX_CUS_PER_CTU];
-    memset(reached, 0, sizeof(reached));
-    reached[0] = 1;
-    for (int dd = 0; dd < 4; dd++) {
-      const int g = 1 << dd, S = 64 >> dd;
-      for (int j = 0; j < g * g; j++) {
-        const int ci = base[dd] + j, x = ctu_x * 64 + (j % g) * S, y = ctu_y * 64 + (j / g) * S;
-        if (!reached[ci] || x >= p->pic_w || y >= p->pic_h) continue;
-        if (!out_dec[ci].split) { out_dec[ci].leaf = 1; continue; }
-        for (int k = 0; k < 4 && dd < 3; k++)
-          reached[base[dd + 1] + (2 * (j / g) + (k >> 1)) * (2 * g) + 2 * (j % g) + (k & 1)] = 1;
-      }
-    }
-  }
-  for (int dd = 0; dd < 4; dd++) {
-    const int g = 1 << dd, S = 64 >> dd;
-    for (int j = 0; j < g * g; j++) {
-      if (!out_dec[base[dd] + j].leaf) continue;
-      const int x = ctu_x * 64 + (j % g) * S, y = ctu_y * 64 + (j / g) * S;
-      const int ci = base[dd] + j, T = S < 32 ? S : 32, cbf = out_dec[ci].cbf;
-      for (int yy = 0; yy < S; yy++)
-        for (int xx = 0; xx < S; xx++) {
-          const int t = (yy / T) * (S / T) + xx / T, k = ci * 4096 + yy * 64 + xx;
-          recon[(y + yy) * recon_stride + x + xx] = (uint8_t)clip_pel(ex->pred[k] + (((cbf >> t) & 1) ? ex->rres[k] : 0));
-        }
-      for (int comp = 1; cc && comp <= 2; comp++) {
-        const int Sc = S / 2, Tc = T / 2;
-        for (int yy = 0; yy < Sc; yy++)
-          for (int xx = 0; xx < Sc; xx++) {
-            const int t = (yy / Tc) * (Sc / Tc) + xx / Tc, k = EX_CHROMA(ci, comp) + yy * 32 + xx;
-            const int rr = ((cbf >> (8 + 4 * comp + t)) & 1) ? ex->ts_rres[ci][comp - 1][yy * 4 + xx] : ex->rres[k];
-            recon_c[comp - 1][(y / 2 + yy) * recon_c_stride + x / 2 + xx] =
-                (uint8_t)clip_pel(ex->pred[k] + (((cbf >> (4 * comp + t)) & 1) ? rr : 0));
-          }
-      }
-    }
-  }
-  free(ex->pred);
-  free(ex->rres);
-  free(ex);
-}
-
-void hvxo_ctu_decide(const uint8_t *cur, const uint8_t *const *refs, int stride, const hvx_ctu_params *p,
-                     const hvx_estbits *est, const uint8_t *states, const int32_t *eb, int ctu_x, int ctu_y,
-                     hvx_cu_result *out_cu, hvx_cu_decision *out_dec, uint8_t *recon, int recon_stride) {
-  ctu_decide_core(cur, refs, stride, NULL, p, est, states, eb, ctu_x, ctu_y, out_cu, out_dec, recon, recon_stride, NULL,
-                  0);
-}
-
-void hvxo_ctu_decide_yuv(const uint8_t *const *cur3, const uint8_t *const *refs, const uint8_t *const *refs_cb,
-                         const uint8_t *const *refs_cr, int stride, int c_stride, const hvx_ctu_params *p,
-                         const hvx_estbits *est, const uint8_t *states, const int32_t *eb, int ctu_x, int ctu_y,
-                         hvx_cu_result *out_cu, hvx_cu_decision *out_dec, uint8_t *const *recon3, int recon_stride,
-                         int recon_c_stride) {
-  ctu_chroma cc;
-  cc.cur[0] = cur3[1]; cc.cur[1] = cur3[2];
-  cc.refs[0] = refs_cb; cc.refs[1] = refs_cr;
-  cc.stride = c_stride;
-  ctu_decide_core(cur3[0], refs, stride, &cc, p, est, states, eb, ctu_x, ctu_y, out_cu, out_dec, recon3[0], recon_stride,
-                  recon3 + 1, recon_c_stride);
-}
-
-
-/* ============================================================================================
  * estBit: TLibEncoder/TEncSbac.cpp:1726-1950 (estCBFBit :1751, estSignificantCoeffGroupMapBit
  * :1778, estSignificantMapBit :1797, estLastSignificantPositionBit :1860,
  * estSignificantCoefficientsBit :1920); context buffer order = the TEncSbac constructor;
@@ -2725,48 +2235,6 @@ void hvxo_deblock(uint8_t *y, int ys, uint8_t *cb, uint8_t *cr, int cs, const ui
         }
       }
   }
-}
-
-/* ============================================================================================
- * Boundary strengths of the analysed picture (the bench step's deblocking input): what
- * TComLoopFilter's xSetEdgefilterTU/PU (TComLoopFilter.cpp:274-359) and xGetBoundaryStrengthSingle
- * (:417-557) give for hvx_ctu_decide's CU trees -- 2Nx2N inter CUs of a P slice, luma TUs of
- * min(CU, 32): an edge is a CU or TU boundary (all of them transform edges); bs 1 when either side's
- * TU has a coded luma block, else when the two sides use different reference pictures or their
- * MVs differ by >= 4 quarter samples in x or y; 0 at the picture border and off the 8x8 grid.
- * ========================================================================================== */
-static void unit_block(const hvx_cu_decision *dec, int nctu_x, int ux, int uy, int *ctu, int *ci, int *t) {
-  const int c = (uy / 16) * nctu_x + ux / 16, lx = ux % 16, ly = uy % 16;
-  static const int base[4] = {0, 1, 5, 21};
-  for (int d = 0; d < 4; d++) {
-    const int su = 16 >> d, j = (ly / su) * (1 << d) + lx / su, k = base[d] + j;
-    if (dec[(size_t)c * HVX_CUS_PER_CTU + k].leaf || d == 3) {
-      const int tu = su < 8 ? su : 8;
-      *ctu = c; *ci = k;
-      *t = ((ly % su) / tu) * (su / tu) + (lx % su) / tu;
-      return;
-    }
-  }
-}
-
-void hvxo_ctu_bs(const hvx_cu_result *cu, const hvx_cu_decision *dec, int pic_w, int pic_h, uint8_t *bs_ver,
-                 uint8_t *bs_hor) {
-  const int uw = pic_w / 4, uh = pic_h / 4, nctu_x = (pic_w + 63) / 64;
-  for (int uy = 0; uy < uh; uy++)
-    for (int ux = 0; ux < uw; ux++)
-      for (int dir = 0; dir < 2; dir++) {
-        uint8_t *o = dir ? &bs_hor[uy * uw + ux] : &bs_ver[uy * uw + ux];
-        *o = 0;
-        if (dir == 0 ? (ux % 2 || ux == 0) : (uy % 2 || uy == 0)) continue;
-        int cq, kq, tq, cp, kp, tp;
-        unit_block(dec, nctu_x, ux, uy, &cq, &kq, &tq);
-        unit_block(dec, nctu_x, dir ? ux : ux - 1, dir ? uy - 1 : uy, &cp, &kp, &tp);
-        if (cq == cp && kq == kp && tq == tp) continue; /* not a transform / CU edge */
-        const hvx_cu_decision *dq = &dec[(size_t)cq * HVX_CUS_PER_CTU + kq], *dp = &dec[(size_t)cp * HVX_CUS_PER_CTU + kp];
-        const hvx_cu_result *rq = &cu[(size_t)cq * HVX_CUS_PER_CTU + kq], *rp = &cu[(size_t)cp * HVX_CUS_PER_CTU + kp];
-        if (((dq->cbf >> tq) & 1) || ((dp->cbf >> tp) & 1)) *o = 1;
-        else *o = (rq->ref != rp->ref || abs(rq->mv_x - rp->mv_x) >= 4 || abs(rq->mv_y - rp->mv_y) >= 4) ? 1 : 0;
-      }
 }
 
 /* =====================================================================================

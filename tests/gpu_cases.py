@@ -198,136 +198,6 @@ def check_tu_random(seed, n):
     return True
 
 
-# ------------------------------------------------------------------------------ CTU analysis pass
-def check_ctu_pass(seed, width, height, nref, qp, max_ctus=None):
-    """hvx_ctu_analyze over a whole picture vs hvxo_ctu_analyze per CTU (bit-exact)."""
-    torch = _torch()
-    cur = padded_plane(make_yuv.random_frame(width, height, seed)[:width * height].reshape(height, width))
-    refs = []
-    for k in range(nref):
-        if k % 2:
-            img = make_yuv.smooth_frame(width, height, seed + k)[:width * height].reshape(height, width)
-        else:
-            img = make_yuv.random_frame(width, height, seed + 10 + k)[:width * height].reshape(height, width)
-        refs.append(padded_plane(img))
-    an = hvx.CtuAnalyzer(width, height, nref, qp)
-    cur_t = torch.from_numpy(cur).cuda()
-    ref_t = [torch.from_numpy(r).cuda() for r in refs]
-    ptrs = torch.tensor([hvx.plane_origin_ptr(t, width) for t in ref_t], dtype=torch.int64).cuda()
-    an.run(cur_t, ptrs)
-    torch.cuda.synchronize()
-    got = an.results()
-    ncx = (width + 63) // 64
-    est = _abi.load_estbits_p_luma()
-    n = an.nctu if max_ctus is None else min(max_ctus, an.nctu)
-    for c in range(n):
-        exp = oracle.ctu_analyze(cur, refs, an.params, est, c % ncx, c // ncx)
-        for ci in range(_abi.CUS_PER_CTU):
-            assert got[c][ci].tobytes() == exp[ci].tobytes(), (c, ci, got[c][ci], exp[ci])
-    return n
-
-
-def check_ctu_decide(seed, width, height, nref, qp, fused=False, rd_metric=0):
-    """hvx_ctu_analyze + hvx_ctu_decide over a whole picture vs hvxo_ctu_decide per CTU: CU
-    results, decision records and the reconstructed picture incl. its extended border (bit-exact)."""
-    torch = _torch()
-    cur = padded_plane(make_yuv.random_frame(width, height, seed)[:width * height].reshape(height, width))
-    refs = [padded_plane((make_yuv.smooth_frame if k % 2 else make_yuv.random_frame)(width, height, seed + 10 + k)
-                         [:width * height].reshape(height, width)) for k in range(nref)]
-    an = hvx.CtuAnalyzer(width, height, nref, qp, rd_metric=rd_metric)
-    cur_t = torch.from_numpy(cur).cuda()
-    ref_t = [torch.from_numpy(r).cuda() for r in refs]
-    ptrs = torch.tensor([hvx.plane_origin_ptr(t, width) for t in ref_t], dtype=torch.int64).cuda()
-    recon_t = torch.zeros_like(cur_t)
-    refpic_t = torch.zeros_like(cur_t)
-    if fused:
-        an.encode(cur_t, ptrs, recon_t, refpic_t)
-    else:
-        an.run(cur_t, ptrs)
-        an.decide(cur_t, recon_t, ref_pic=refpic_t)
-    torch.cuda.synchronize()
-    got_cu, got_dec, got_rec = an.results(), an.decisions(), recon_t.cpu().numpy()
-    est, st, eb = _abi.load_estbits_p_luma(), _abi.load_ctx_p_states(), _abi.load_entropy_bits()
-    ncx = (width + 63) // 64
-    exp_rec = np.zeros_like(cur)
-    n_leaf = 0
-    for c in range(an.nctu):
-        cu, dec = oracle.ctu_decide(cur, refs, an.params, est, st, eb, c % ncx, c // ncx, exp_rec)
-        assert got_cu[c].tobytes() == cu.tobytes(), c
-        for ci in range(_abi.CUS_PER_CTU):
-            assert got_dec[c][ci].tobytes() == dec[ci].tobytes(), (c, ci, got_dec[c][ci], dec[ci])
-        n_leaf += int(dec["leaf"].sum())
-    M = _abi.PLANE_MARGIN
-    inner = exp_rec[M:M + height, M:M + width]
-    np.testing.assert_array_equal(got_rec, np.pad(inner, M, mode="edge"))  # extendPicBorder
-    # the reference picture: boundary strengths of the decided trees + luma deblocking
-    bv, bh = oracle.ctu_bs(got_cu.reshape(-1), got_dec.reshape(-1), width, height)
-    qp = np.full(len(bv), int(an.params["qp"][0]), np.int8)
-    zc = np.zeros((height // 2, width // 2), np.uint8)
-    dy, _, _ = oracle.deblock(inner, zc, zc, bv, bh, qp, _abi.deblock_params(width, height))
-    np.testing.assert_array_equal(refpic_t.cpu().numpy(), np.pad(dy, M, mode="edge"))
-    return an.nctu, n_leaf
-
-
-def yuv_padded(frame, width, height):
-    """planar 4:2:0 frame bytes -> (Y, Cb, Cr) padded planes (margins M and M // 2, replicated borders)."""
-    n, c = width * height, (width // 2) * (height // 2)
-    y = frame[:n].reshape(height, width)
-    cb = frame[n:n + c].reshape(height // 2, width // 2)
-    cr = frame[n + c:n + 2 * c].reshape(height // 2, width // 2)
-    return np.pad(y, M, mode="edge"), np.pad(cb, M // 2, mode="edge"), np.pad(cr, M // 2, mode="edge")
-
-
-def check_ctu_encode_yuv(seed, width, height, nref, qp):
-    """hvx_ctu_encode_yuv over a whole 4:2:0 picture vs hvxo_ctu_decide_yuv per CTU: CU results,
-    decision records (chroma cbf flags and weighted distortion included), the reconstructed Y/Cb/Cr
-    planes incl. their extended borders and the reference picture (bit-exact)."""
-    torch = _torch()
-    cur = yuv_padded(make_yuv.random_frame(width, height, seed), width, height)
-    refs = [yuv_padded((make_yuv.smooth_frame if k % 2 else make_yuv.random_frame)(width, height, seed + 10 + k),
-                       width, height) for k in range(nref)]
-    an = hvx.CtuAnalyzer(width, height, nref, qp, chroma=True)
-    cur_t = [torch.from_numpy(x).cuda() for x in cur]
-    ref_t = [[torch.from_numpy(r[c]).cuda() for r in refs] for c in range(3)]
-    ptr_y = torch.tensor([hvx.plane_origin_ptr(t, width) for t in ref_t[0]], dtype=torch.int64).cuda()
-    ptr_c = torch.tensor([hvx.plane_origin_ptr(t, width // 2, M // 2) for t in ref_t[1] + ref_t[2]],
-                         dtype=torch.int64).cuda()
-    recon_t = [torch.zeros_like(x) for x in cur_t]
-    refpic_t = [torch.zeros_like(x) for x in cur_t]
-    an.encode_yuv(cur_t, ptr_y, ptr_c, recon_t, refpic_t)
-    torch.cuda.synchronize()
-    got_cu, got_dec = an.results(), an.decisions()
-    est7 = _abi.estbits_p_yuv(oracle.estbits_update)
-    st, eb = _abi.load_ctx_p_states(), _abi.load_entropy_bits()
-    ncx = (width + 63) // 64
-    exp_rec = [np.zeros_like(x) for x in cur]
-    n_leaf = n_cbf_c = n_ts_c = 0
-    refs3 = ([r[0] for r in refs], [r[1] for r in refs], [r[2] for r in refs])
-    for c in range(an.nctu):
-        cu, dec = oracle.ctu_decide_yuv(cur, refs3, an.params, est7, st, eb, c % ncx, c // ncx, exp_rec)
-        assert got_cu[c].tobytes() == cu.tobytes(), c
-        for ci in range(_abi.CUS_PER_CTU):
-            assert got_dec[c][ci].tobytes() == dec[ci].tobytes(), (c, ci, got_dec[c][ci], dec[ci])
-        n_leaf += int(dec["leaf"].sum())
-        n_cbf_c += int(((dec["cbf"] >> 4) & 0xff)[dec["leaf"] == 1].astype(bool).sum())
-        n_ts_c += int(((dec["cbf"] >> 12) & 0xff).astype(bool).sum())
-    inner = []
-    for k in range(3):
-        m = M if k == 0 else M // 2
-        w, h = (width, height) if k == 0 else (width // 2, height // 2)
-        inner.append(exp_rec[k][m:m + h, m:m + w])
-        np.testing.assert_array_equal(recon_t[k].cpu().numpy(), np.pad(inner[k], m, mode="edge"), err_msg=str(k))
-    # the reference picture: loopFilterPic of the reconstruction (luma bs 0/1; chroma edges need bs 2)
-    bv, bh = oracle.ctu_bs(got_cu.reshape(-1), got_dec.reshape(-1), width, height)
-    qpm = np.full(len(bv), int(an.params["qp"][0]), np.int8)
-    dy, dcb, dcr = oracle.deblock(inner[0], inner[1].copy(), inner[2].copy(), bv, bh, qpm,
-                                  _abi.deblock_params(width, height))
-    for k, d in enumerate((dy, dcb, dcr)):
-        np.testing.assert_array_equal(refpic_t[k].cpu().numpy(), np.pad(d, M if k == 0 else M // 2, mode="edge"))
-    return an.nctu, n_leaf, n_cbf_c, n_ts_c
-
-
-# ------------------------------------------------------------------------------------------- MC
 def mc_planes(rng, W, H, n_ref):
     """HM-like int16 4:2:0 reference planes (margins 80 luma / 40 chroma, borders replicated),
     smooth random content.  Returns [(array, origin_offset)] * 3*n_ref, strides."""

@@ -99,42 +99,6 @@ def test_estbits_update_host_golden():
         hvx.estbits_update(states[0], eb, rice[0], 64, 64, 0, before[0])
 
 
-def test_oracle_ctu_decide_tree():
-    # the oracle's CU decision: the analysis records equal hvxo_ctu_analyze's, the leaves tile
-    # every in-picture sample exactly once, the root's best tree totals its leaves, and the
-    # reconstruction is close to the original (QP 32 on random content: PSNR well above 20 dB)
-    import oracle
-    from oracle import make_yuv
-    from video_codecs_amd import _abi
-    W, H = 200, 136
-    pad = lambda img: np.pad(img, _abi.PLANE_MARGIN, mode="edge")
-    cur = pad(make_yuv.smooth_frame(W, H, 3)[:W * H].reshape(H, W))
-    refs = [pad(make_yuv.smooth_frame(W, H, 4)[:W * H].reshape(H, W))]
-    p = _abi.ctu_params(W, H, 1, 32)
-    est, st, eb = _abi.load_estbits_p_luma(), _abi.load_ctx_p_states(), _abi.load_entropy_bits()
-    rec = np.zeros_like(cur)
-    cover = np.zeros((H, W), np.int32)
-    for c in (0, 3, 11):  # interior, right-edge (x 192..199) and bottom-right corner CTUs
-        cx, cy = c % 4, c // 4
-        cu, dec = oracle.ctu_decide(cur, refs, p, est, st, eb, cx, cy, rec)
-        np.testing.assert_array_equal(cu, oracle.ctu_analyze(cur, refs, p, est, cx, cy))
-        bits = dist = 0
-        for ci in np.nonzero(dec["leaf"])[0]:
-            d = 0 if ci == 0 else 1 if ci < 5 else 2 if ci < 21 else 3
-            j = ci - (0, 1, 5, 21)[d]
-            S, g = 64 >> d, 1 << d
-            x, y = cx * 64 + (j % g) * S, cy * 64 + (j // g) * S
-            assert cu[ci]["valid"] and x + S <= W and y + S <= H
-            cover[y:y + S, x:x + S] += 1
-            dist += int(dec[ci]["dist"])
-        assert int(dec[0]["best_dist"]) == dist
-        ys, xs = slice(cy * 64, min(H, cy * 64 + 64)), slice(cx * 64, min(W, cx * 64 + 64))
-        assert (cover[ys, xs] == 1).all()
-        M = _abi.PLANE_MARGIN
-        diff = rec[M:M + H, M:M + W][ys, xs].astype(float) - cur[M:M + H, M:M + W][ys, xs]
-        assert 10 * np.log10(255 ** 2 / max(np.mean(diff ** 2), 1e-9)) > 20
-
-
 def test_intra_struct_layouts_match_c():
     prog = r"""
 #include <stdio.h>
@@ -187,46 +151,6 @@ def test_oracle_deblock_random_smoke():
     assert (out[0] != y).any() and (out[1] != cb).any()
 
 
-def test_oracle_ctu_bs_edges():
-    # boundary strengths of decided trees: only on the 8x8 grid, never at the picture border, at
-    # most 1 (inter P slice), and exactly at CU/TU boundaries -- never inside one transform block
-    import oracle
-    from oracle import make_yuv
-    from video_codecs_amd import _abi
-    W, H = 128, 128
-    pad = lambda img: np.pad(img, _abi.PLANE_MARGIN, mode="edge")  # noqa: E731
-    cur = pad(make_yuv.random_frame(W, H, 5)[:W * H].reshape(H, W))
-    refs = [pad(make_yuv.smooth_frame(W, H, 6)[:W * H].reshape(H, W))]
-    p = _abi.ctu_params(W, H, 1, 32)
-    est, st, eb = _abi.load_estbits_p_luma(), _abi.load_ctx_p_states(), _abi.load_entropy_bits()
-    rec = np.zeros_like(cur)
-    cus, decs = [], []
-    for c in range(4):
-        cu, dec = oracle.ctu_decide(cur, refs, p, est, st, eb, c % 2, c // 2, rec)
-        cus.append(cu)
-        decs.append(dec)
-    bv, bh = oracle.ctu_bs(np.concatenate(cus), np.concatenate(decs), W, H)
-    bv, bh = bv.reshape(H // 4, W // 4), bh.reshape(H // 4, W // 4)
-    assert bv.max() <= 1 and bh.max() <= 1 and bv.any() and bh.any()
-    assert not bv[:, 1::2].any() and not bv[:, 0].any() and not bh[1::2, :].any() and not bh[0, :].any()
-    # block id of every 4x4 unit: (ctu, leaf CU, TU) -- edges with bs 1 separate different blocks
-    dec_all = np.concatenate(decs)
-    block = np.zeros((H // 4, W // 4), np.int64)
-    for uy in range(H // 4):
-        for ux in range(W // 4):
-            c = (uy // 16) * 2 + ux // 16
-            for d in range(4):
-                su = 16 >> d
-                k = (0, 1, 5, 21)[d] + ((uy % 16) // su) * (1 << d) + (ux % 16) // su
-                if dec_all[c * 85 + k]["leaf"]:
-                    tu = min(su, 8)
-                    t = (((uy % 16) % su) // tu) * (su // tu) + ((ux % 16) % su) // tu
-                    block[uy, ux] = (c * 85 + k) * 16 + t
-                    break
-    assert not (bv[:, 1:] & (block[:, 1:] == block[:, :-1])).any()
-    assert not (bh[1:, :] & (block[1:, :] == block[:-1, :])).any()
-
-
 def test_lambda_ssim_matches_stvssim():
     # the product-side SSIM-RDO lambda (video_codecs_amd/_abi.py) is the oracle's lambda_2 /
     # adjust_lambda (pinned to stvssim.c by tests/golden/ssim.bin)
@@ -234,30 +158,6 @@ def test_lambda_ssim_matches_stvssim():
     for qp in (0, 15, 22, 27, 32, 37, 51):
         assert _abi.lambda_ssim(qp) == oracle.lambda_2(qp)
         assert abs(_abi.lambda_ssim(qp, 0.7) - oracle.adjust_lambda(oracle.lambda_2(qp), 0.7)) <= 1e-18
-
-
-def test_oracle_ctu_decide_ssim_mode():
-    # HVX_RD_SSIM: the leaves' D_ssim are in [0, blocks], the tree's D_ssim totals its leaves' (up to
-    # float association), and a larger lambda never produces more leaves (bits get dearer)
-    import oracle
-    from oracle import make_yuv
-    W, H = 128, 64
-    pad = lambda img: np.pad(img, _abi.PLANE_MARGIN, mode="edge")  # noqa: E731
-    cur = pad(make_yuv.smooth_frame(W, H, 7)[:W * H].reshape(H, W))
-    refs = [pad(make_yuv.smooth_frame(W, H, 8)[:W * H].reshape(H, W))]
-    est, st, eb = _abi.load_estbits_p_luma(), _abi.load_ctx_p_states(), _abi.load_entropy_bits()
-    n_leaves = []
-    for lam in (_abi.lambda_ssim(32), 1e3 * _abi.lambda_ssim(32)):
-        p = _abi.ctu_params(W, H, 1, 32, rd_metric=_abi.RD_SSIM, lam_ssim=lam)
-        rec = np.zeros_like(cur)
-        cu, dec = oracle.ctu_decide(cur, refs, p, est, st, eb, 0, 0, rec)
-        leaves = np.nonzero(dec["leaf"])[0]
-        for ci in leaves:
-            S = 64 >> (0 if ci == 0 else 1 if ci < 5 else 2 if ci < 21 else 3)
-            assert 0.0 <= dec[ci]["ssim_dist"] <= (S // 8) ** 2 + 1e-3
-        assert abs(float(dec[0]["best_ssim_dist"]) - float(dec["ssim_dist"][leaves].sum())) < 1e-3
-        n_leaves.append(len(leaves))
-    assert n_leaves[1] <= n_leaves[0]
 
 
 def test_new_entry_points_reject_bad_arguments_without_a_gpu():
@@ -273,7 +173,6 @@ def test_new_entry_points_reject_bad_arguments_without_a_gpu():
     assert L.hvx_intra_search_batch(P(0), P(0), P(0), 64, P(0), 1, P(0), P(0)) == E_INVALID
     assert L.hvx_deblock(P(0), P(0), 64, P(0), P(0), 32, P(0), P(0), P(0), P(0)) == E_INVALID
     assert b"hvx_deblock" in L.hvx_last_error()
-    assert L.hvx_ctu_decide(P(0), P(0), 0, P(0), P(0), P(0), P(0), ctypes.c_size_t(0), P(0), P(0), P(0), P(0)) == E_INVALID
     # the CABAC residual writer: NULL context, negative run count / capacity
     assert L.hvx_coeff_write_batch(P(0), P(0), P(0), P(0), P(0), 1, P(0), P(0), P(0), P(0), 64, P(0)) == E_INVALID
     assert b"hvx_coeff_write_batch" in L.hvx_last_error()

@@ -1,11 +1,11 @@
 """The multi-rank path of bench.py on CPU: world_size-2 torch.distributed over gloo.
 
-bench.py shards the CTU analysis pass by independent GOP segments: each rank
-analyses its own frames, the timed region is bracketed by barriers on every rank, the time
-is the MAX over ranks and the value counts the units of ALL ranks.  Here the per-rank step is
-the CPU restatement of the same pass (oracle/hvx_oracle.c) on a small picture, so the
-orchestration (segment assignment, barrier + max-over-ranks timing, aggregation) is tested
-without a GPU.  The gloo rendezvous uses 127.0.0.1.
+bench.py shards independent pictures across ranks: each rank decides its own
+pictures, the timed region is bracketed by barriers on every rank, the time is the MAX over ranks
+and the value counts the units of ALL ranks.  Here the per-rank step is the CPU restatement of the
+HM-exact decision (oracle/hvx_oracle_cu.c) on small pictures, so the orchestration (picture
+assignment, barrier + max-over-ranks timing, aggregation, DPB gather) is tested without a GPU.
+The gloo rendezvous uses 127.0.0.1.
 """
 import os
 import socket
@@ -22,126 +22,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _analyze(planes):
-    import oracle
-    from video_codecs_amd import _abi
-    params = _abi.ctu_params(W, H, NREF, QP)
-    est = _abi.load_estbits_p_luma()
-    ncx, ncy = (W + 63) // 64, (H + 63) // 64
-    return np.stack([oracle.ctu_analyze(planes[NREF], planes[:NREF], params, est, c % ncx, c // ncx)
-                     for c in range(ncx * ncy)])
-
-
-def _worker(rank, world, port, outdir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    import bench
-    frames = bench.segment_frames(rank, NREF)
-    planes = [bench.luma_plane(W, H, f) for f in frames]
-    box = {}
-
-    def step():
-        box["res"] = _analyze(planes)
-
-    elapsed = bench.timed_steps(step, STEPS, WARMUP, world, "cpu", lambda: None)
-    nctu = box["res"].shape[0]
-    value = bench.aggregate(nctu, STEPS, world, elapsed)
-    np.save(os.path.join(outdir, f"res{rank}.npy"), box["res"].view(np.uint8))
-    np.save(os.path.join(outdir, f"meta{rank}.npy"), np.array([elapsed, value, nctu] + frames, dtype=np.float64))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def test_two_rank_segments_gloo(tmp_path):
-    import torch.multiprocessing as tmp
-    world = 2
-    tmp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    metas = [np.load(tmp_path / f"meta{r}.npy") for r in range(world)]
-    res = [np.load(tmp_path / f"res{r}.npy") for r in range(world)]
-    # max-over-ranks timing: every rank ends with the same elapsed and the same whole-job value
-    assert metas[0][0] == metas[1][0]
-    nctu = int(metas[0][2])
-    assert metas[0][1] == pytest.approx(nctu * STEPS * world / metas[0][0])
-    # disjoint segments: rank r analyses frames r*(nref+1) .. r*(nref+1)+nref
-    f0, f1 = [int(x) for x in metas[0][3:]], [int(x) for x in metas[1][3:]]
-    assert f0 == [0, 1] and f1 == [2, 3] and not set(f0) & set(f1)
-    assert res[0].tobytes() != res[1].tobytes()
-    # each rank's result is exactly the single-process result for its own segment
-    import bench
-    for r, frames in ((0, f0), (1, f1)):
-        exp = _analyze([bench.luma_plane(W, H, f) for f in frames])
-        assert res[r].tobytes() == exp.view(np.uint8).tobytes()
-
-
 def test_segment_and_aggregate_contract():
     import bench
-    segs = [bench.segment_frames(r, 4) for r in range(8)]
-    flat = [f for s in segs for f in s]
-    assert len(flat) == len(set(flat)) == 40  # 8 closed, disjoint segments of nref+1 frames
+    plans = [bench.HmPlan(3840, 2160, 62, 4, 32, 1, r) for r in range(8)]
+    flat = [f for p in plans for f in p.frames()]
+    assert len(flat) == len(set(flat)) == 8 * 66  # 8 ranks, disjoint synthetic frame ranges
     assert bench.aggregate(2040, 10, 8, 2.0) == 2040 * 10 * 8 / 2.0
     assert bench.b_ctu(4) == 6144 * 6 + 2 * 6144 + 16 * 256 == 53248  # SURVEY 8(d), LDP 4 refs
-
-
-def _decide_picture(planes, rec_flat):
-    """The oracle's full 4:2:0 step (analysis + CU decision + reconstruction) into rec_flat (one
-    Y | Cb | Cr picture buffer, the layout the bench step gathers)."""
-    import oracle
-    from video_codecs_amd import _abi, hvx
-    params = _abi.ctu_params(W, H, NREF, QP, chroma=True)
-    est7 = _abi.estbits_p_yuv(oracle.estbits_update)
-    st, eb = _abi.load_ctx_p_states(), _abi.load_entropy_bits()
-    rec = hvx.yuv_views(rec_flat, W, H)
-    refs = planes[:NREF]
-    refs3 = ([r[0] for r in refs], [r[1] for r in refs], [r[2] for r in refs])
-    ncx, ncy = (W + 63) // 64, (H + 63) // 64
-    for c in range(ncx * ncy):
-        oracle.ctu_decide_yuv(planes[NREF], refs3, params, est7, st, eb, c % ncx, c // ncx, rec)
-
-
-def _dpb_worker(rank, world, port, outdir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    import bench
-    from video_codecs_amd.dpb import DpbGather
-    from video_codecs_amd import hvx
-    planes = [bench.yuv_planes(W, H, f) for f in bench.segment_frames(rank, NREF)]
-    g = DpbGather(world, rank, (hvx.yuv_bytes(W, H),), "cpu")
-
-    def step():  # the bench step's shape: decide into the DPB buffer, then the async gather
-        _decide_picture(planes, g.buffer().numpy())
-        g.send()
-
-    elapsed = bench.timed_steps(step, STEPS, WARMUP, world, "cpu", g.drain)
-    own, gathered = g.last()
-    np.save(os.path.join(outdir, f"own{rank}.npy"), own.numpy())
-    if rank == 0:
-        np.save(os.path.join(outdir, "dpb.npy"), np.stack([t.numpy() for t in gathered]))
-    np.save(os.path.join(outdir, f"t{rank}.npy"), np.array([elapsed, g.k]))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def test_two_rank_dpb_gather_gloo(tmp_path):
-    # the per-picture DPB gather (SURVEY 8(e)): after STEPS + WARMUP pictures through two
-    # alternating buffers, rank 0 holds each rank's latest 4:2:0 reconstruction (one Y | Cb | Cr
-    # buffer per picture), and that reconstruction is exactly the single-process one of the rank's
-    # own segment
-    import torch.multiprocessing as tmp
-    world = 2
-    tmp.spawn(_dpb_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    dpb = np.load(tmp_path / "dpb.npy")
-    assert dpb.shape[0] == world
-    import bench
-    for r in range(world):
-        own = np.load(tmp_path / f"own{r}.npy")
-        np.testing.assert_array_equal(dpb[r], own)
-        exp = np.zeros_like(own)
-        _decide_picture([bench.yuv_planes(W, H, f) for f in bench.segment_frames(r, NREF)], exp)
-        np.testing.assert_array_equal(own, exp)
-        assert int(np.load(tmp_path / f"t{r}.npy")[1]) == STEPS + WARMUP
-    assert not np.array_equal(dpb[0], dpb[1])
 
 
 # ---- the headline's orchestration (bench.HmPlan / HmWorkload) with the HM-exact restatement ----

@@ -141,50 +141,6 @@ def test_plane_from_pel_gpu(torch):
     np.testing.assert_array_equal(plane.cpu().numpy().reshape(H + 2 * M, W + 2 * M), exp)
 
 
-def test_ctu_pass_gpu(torch):
-    # 320x200: 20 CTUs incl. a partial bottom row (only 8x8 CUs valid there) and 2 references
-    assert gpu_cases.check_ctu_pass(seed=21, width=320, height=200, nref=2, qp=32) == 20
-
-
-def test_ctu_decide_gpu(torch):
-    # analysis + coefficient rate + CU tree + reconstruction; 200x136 has partial CTUs on both
-    # edges (forced splits, CUs outside the picture)
-    n, leaves = gpu_cases.check_ctu_decide(seed=5, width=200, height=136, nref=2, qp=32)
-    assert n == 12 and leaves > 12
-
-
-def test_ctu_encode_fused_gpu(torch):
-    # hvx_ctu_encode (the bench step's schedule) gives hvx_ctu_analyze + hvx_ctu_decide's results
-    n, leaves = gpu_cases.check_ctu_decide(seed=9, width=264, height=200, nref=3, qp=27, fused=True)
-    assert n == 20 and leaves > 20
-
-
-def test_ctu_encode_yuv_gpu(torch):
-    # 4:2:0 step: chroma MC, Cb/Cr TUs (4x4..16x16) through RDOQ + rate, chroma-weighted decisions,
-    # Y/Cb/Cr reconstruction and reference picture; a 264x200 picture exercises partial CTUs
-    n_ctu, n_leaf, n_cbf_c, n_ts = gpu_cases.check_ctu_encode_yuv(seed=41, width=264, height=200, nref=2, qp=27)
-    assert n_ctu == 20 and n_leaf > 20 and n_cbf_c > 0
-    print("yuv: %d leaves, %d coded chroma TUs, %d 4x4 chroma TUs in transform-skip mode" % (n_leaf, n_cbf_c, n_ts))
-
-
-def test_ctu_encode_yuv_qp_sweep_gpu(torch):
-    n_ts = 0
-    for qp in (22, 37):
-        n_ts += gpu_cases.check_ctu_encode_yuv(seed=qp, width=192, height=128, nref=1, qp=qp)[3]
-    print("yuv qp sweep: %d 4x4 chroma TUs in transform-skip mode" % n_ts)
-
-
-def test_ctu_decide_qp_sweep_gpu(torch):
-    for qp in (22, 37):
-        n, leaves = gpu_cases.check_ctu_decide(seed=qp, width=128, height=128, nref=1, qp=qp)
-        assert n == 4 and leaves >= 4
-
-
-def test_ctu_pass_qp_sweep_gpu(torch):
-    for qp in (22, 27, 37):
-        assert gpu_cases.check_ctu_pass(seed=qp, width=192, height=128, nref=1, qp=qp) == 6
-
-
 def test_estbits_batch_golden_gpu(torch):
     g = gc.load("estbit.bin")
     meta, states, rice, before, after, eb = g["meta"], g["states"], g["rice"], g["before"], g["after"], g["entropy_bits"]
@@ -295,16 +251,6 @@ def test_sao_random_gpu(torch):
     assert gpu_cases.check_sao_random(seed=51) == 510
     assert gpu_cases.check_sao_random(seed=52, w=1000, h=600) == 160
     assert gpu_cases.check_sao_random(seed=53, w=512, h=256, luma_only=True) == 32
-
-
-def test_ctu_decide_ssim_rdo_gpu(torch):
-    # HVX_RD_SSIM (BASELINE config 4's SSIM RD cost): D_ssim per 8x8 block (compute_SSIM floats) and
-    # lambda_2 in the CU quadtree decision, QP 22 / 27 / 32 / 37 (config 4's sweep), bit-exact vs
-    # the oracle incl. the float sums
-    for qp in (22, 27, 32, 37):
-        n, leaves = gpu_cases.check_ctu_decide(seed=9 + qp, width=256, height=136, nref=2, qp=qp, fused=True,
-                                               rd_metric=hvx._abi.RD_SSIM)
-        assert n == 12 and leaves >= 12
 
 
 @pytest.mark.parametrize("mode", [0, 1])

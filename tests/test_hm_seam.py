@@ -23,9 +23,16 @@ EXE = os.path.join(ROOT, "oracle", "_ref", "TAppEncoder_hvx")
 EXPECTED = json.load(open(os.path.join(ROOT, "tests", "hm_seam", "expected_md5.json")))
 
 
+# The leaf seams make ~1M synchronous per-call offloads per encode (correctness, not speed), and
+# every leaf kernel they serve is pinned by the golden tests of test_gpu_parity.py: one intra encode
+# (the intra prediction seam) and one B-slice encode (bi-prediction MC, B-slice ME, every other
+# leaf seam) keep the end-to-end check inside the GPU suite's time budget.
+LEAF_SEAM_CASES = ("intra_rand_qp32", "ldb_smooth_qp32")
+
+
 @pytest.mark.gpu
-@pytest.mark.timeout(600)  # ~1M synchronous per-call offloads per encode: correctness, not speed
-@pytest.mark.parametrize("case", [c for c in sorted(mk.CASES) if mk.case_size(c) == (mk.W, mk.H)])
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("case", LEAF_SEAM_CASES)
 def test_hm_encoder_with_hvx_seams(case, monkeypatch):
     import torch
     if not torch.cuda.is_available():
@@ -66,9 +73,8 @@ def test_expected_md5_cases_present():
 
 
 @pytest.mark.gpu
-@pytest.mark.timeout(900)  # one synchronous single-CTU launch per compressCtu call: correctness, not speed
-@pytest.mark.parametrize("case", ["ldp_rand_qp32", "ldp_smooth_qp32", "intra_rand_qp32", "intra_smooth_qp22", "ra_smooth_qp27",
-                                  "ra_texture_qp32"])
+@pytest.mark.timeout(600)  # one synchronous single-CTU launch per compressCtu call: correctness, not speed
+@pytest.mark.parametrize("case", ["intra_rand_qp32", "ldp_rand_qp32", "ra_smooth_qp27"])
 def test_hm_encoder_with_cu_seam(case, monkeypatch):
     """The L3 boundary: every TEncCu::compressCtu of an unchanged TAppEncoder encode (LDP: I + P
     pictures; RA: I + hierarchical GOP8 B pictures) served by the HM-exact CTU engine (integration/hm_cu_seam.cpp -> hvx_hm_compress),
@@ -98,8 +104,8 @@ def test_hm_encoder_with_cu_seam(case, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.timeout(900)
-@pytest.mark.parametrize("case", ["ldp_smooth_1080p_qp32", "ra_texture_qp32"])
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("case", ["ldp_smooth_1080p_qp32", "ra_texture_qp32", "ldp_smooth_qp32", "intra_smooth_qp22"])
 def test_hm_encoder_with_cu_seam_batched(case, monkeypatch):
     """The throughput form of the CTU seam (HVX_SEAM_CU_BATCH=1): at each picture's first
     compressCtu call every slice of the picture is decided by ONE hvx_hm_compress launch (one chain

@@ -31,19 +31,10 @@ assert ME_RESULT.itemsize == 48
 
 ME_FEN, ME_HADME, ME_SMOOTHMV, ME_BI = 1, 2, 4, 8
 
-CTU_PARAMS = np.dtype([("pic_w", "<i4"), ("pic_h", "<i4"), ("n_ref", "<i4"), ("qp", "<i4"), ("search_range", "<i4"),
-                       ("me_flags", "<i4"), ("slice_type", "<i4"), ("lambda_motion", "<u4"), ("lambda", "<f8"),
-                       ("lambda_ssim", "<f8"), ("rd_metric", "<i4"), ("chroma_format", "<i4"), ("qp_chroma", "<i4"),
-                       ("pad_", "<i4"), ("lambda_chroma", "<f8"), ("chroma_weight", "<f8")], align=True)
-assert CTU_PARAMS.itemsize == 80
 # g_aucChromaScale[CHROMA_420] (TComRom.cpp:536)
 CHROMA_SCALE_420 = tuple(range(30)) + (29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37) + tuple(range(38, 52))
 assert len(CHROMA_SCALE_420) == 58
-RD_SSE, RD_SSIM = 0, 1
-CU_RESULT = np.dtype([("valid", "<i4"), ("ref", "<i4"), ("mv_x", "<i4"), ("mv_y", "<i4"), ("me_cost", "<u4"),
-                      ("sse", "<u4"), ("abs_sum", "<i4"), ("n_tu", "<i4")])
-assert CU_RESULT.itemsize == 32
-CUS_PER_CTU = 85
+RD_SSE, RD_SSIM = 0, 1  # hvx_hm_picture.rd_metric
 
 
 def load_estbits_p_luma():
@@ -84,24 +75,6 @@ def chroma_qp(qp, offset=0):
     return qp if q < 0 else CHROMA_SCALE_420[min(q, 57)]
 
 
-def ctu_params(pic_w, pic_h, n_ref, qp, lam=None, search_range=64, slice_type=1, rd_metric=0, lam_ssim=None,
-               chroma=False):
-    """HM-style P-slice parameters; lambda defaults to 0.57*2^((qp-12)/3) (TEncSlice::initEncSlice form).
-    rd_metric RD_SSIM selects the SSIM CU decision with lambda_ssim(qp) unless lam_ssim is given.
-    chroma: 4:2:0 (hvx_ctu_encode_yuv) with TEncSlice::setUpLambda's chroma weight and RDOQ lambda."""
-    import math
-    p = np.zeros(1, CTU_PARAMS)
-    p["rd_metric"] = rd_metric
-    p["lambda_ssim"] = lambda_ssim(qp) if lam_ssim is None else lam_ssim
-    lam = 0.57 * 2.0 ** ((qp - 12) / 3.0) if lam is None else lam
-    p["pic_w"], p["pic_h"], p["n_ref"], p["qp"] = pic_w, pic_h, n_ref, qp
-    p["search_range"], p["me_flags"], p["slice_type"] = search_range, ME_FEN | ME_HADME | ME_SMOOTHMV, slice_type
-    p["lambda_motion"], p["lambda"] = lambda_motion_sad(lam), lam
-    qpc = chroma_qp(qp)
-    w = math.pow(2.0, (qp - qpc) / 3.0)  # TEncSlice.cpp:159
-    p["chroma_format"], p["qp_chroma"], p["chroma_weight"], p["lambda_chroma"] = int(chroma), qpc, w, lam / w
-    return p
-
 # picture layout: 8-bit padded planes, HM TComPicYuv geometry (margin = MaxCU + 16 = 80)
 PLANE_MARGIN = 80
 HM_RESUME = 1  # HVX_HM_RESUME (hvx_hm_job.flags)
@@ -134,11 +107,6 @@ assert CABAC_REGS.itemsize == 44
 CABAC_START = (0, 510, 23, 0, 0xFF, 0, (0, 0, 0, 0, 0))
 NUM_CTX = 202
 
-# hvx_cu_decision (hvx_types.h)
-CU_DECISION = np.dtype([("coef_frac", "<u8"), ("bits", "<u4"), ("dist", "<u4"), ("best_bits", "<u4"),
-                        ("best_dist", "<u4"), ("split", "<i4"), ("leaf", "<i4"), ("cbf", "<i4"), ("ssim_dist", "<f4"),
-                        ("best_ssim_dist", "<f4"), ("pad_", "<i4")])
-assert CU_DECISION.itemsize == 48
 
 
 def load_ctx_p_states():

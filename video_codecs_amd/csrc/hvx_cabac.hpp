@@ -508,37 +508,6 @@ static __global__ __launch_bounds__(64) void k_coeff_bits(const hvx_tu_desc *__r
   }
 }
 
-// The CTU decision's variant (hvx_ctu_decide): one size class of the CTU pass, levels read from
-// the RDOQ's interleaved scan-order array (G = 64 TUs per group: lane l of block b counts TU
-// b*64 + l, whose element sp sits at ((b*NN + sp)*64 + l) -- the 64 lanes of every level load
-// touch 64 consecutive words), every TU from the same snapshot.
-template <int L>
-static __global__ __launch_bounds__(64) void k_coeff_bits_il(const hvx_tu_desc *__restrict__ descs, int n,
-                                                      const int32_t *__restrict__ levI,
-                                                      const int32_t *__restrict__ entropy_bits,
-                                                      const uint8_t *__restrict__ snapshot,
-                                                      hvx_coeff_bits *__restrict__ out) {
-  constexpr int N = 4 << L, NN = N * N;
-  __shared__ cab::Shared s;
-  const int lane = threadIdx.x, tu0 = blockIdx.x * 64, cnt = min(64, n - tu0), t = tu0 + lane;
-  cab::init_tables(s, entropy_bits);
-  cab::states_load(s, snapshot, 0, tu0, cnt);
-  __syncthreads();
-  if (lane >= cnt) return;
-  const hvx_tu_desc d = descs[t];
-  hvx_coeff_bits r{0, (uint32_t)d.golomb_rice_stat, 0xffffffffu};
-  if (d.width == N && d.height == N && (unsigned)d.scan_type <= 2u) {
-    const int32_t *lv = levI + tu_il(t, 0, NN, 64);
-    cab::Lane Lc{&s.st[lane], &s, 0};
-    uint32_t rice = (uint32_t)d.golomb_rice_stat;
-    const int ns = cab::coeff_bits(d, [&](int sp) { return lv[(size_t)sp * 64]; }, Lc, rice);
-    r.frac_bits = Lc.frac;
-    r.rice_stat = rice;
-    r.num_sig = (uint32_t)ns;
-  }
-  out[t] = r;
-}
-
 // Runs per wave: the runs of a wave take different branches bin by bin (MPS / LPS, bypass lengths,
 // renormalisation, writeOut), and the wave executes the union; fewer runs per wave spread the
 // runs over more SIMDs, each wave still alone on its SIMD for a picture's worth of runs.

@@ -53,7 +53,7 @@ int hvx_hm_job_status(hvx_ctx *ctx, const void *d_state, int n_jobs, int32_t *h_
   if (n_jobs == 0) return HVX_OK;
   size_t sb = 0;
   hvx_hm_state_size(&sb);
-  // State.dbg[0] of every job's state (strided): 0 = ran, -HVX_HM_BAD_* = refused
+  // State.status[0] of every job's state (strided): 0 = ran, -HVX_HM_BAD_* = refused
   if (hipMemcpy2DAsync(h_status, sizeof(int32_t), d_state, sb, sizeof(int32_t), (size_t)n_jobs, hipMemcpyDeviceToHost,
                        ctx->stream) != hipSuccess ||
       hipStreamSynchronize(ctx->stream) != hipSuccess)

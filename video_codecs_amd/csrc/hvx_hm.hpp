@@ -124,6 +124,9 @@ struct IntraScratch {
 #ifndef HM_MEMO_B
 #define HM_MEMO_B 16
 #endif
+#if defined(HM_MEMO_HBM) && !defined(HM_NO_MEMO_BIG)
+#define HM_NO_MEMO_BIG  // the 16x16 / 32x32 memo has only the LDS-index form
+#endif
 constexpr int kMemoK = HM_MEMO_K, kMemoDw = 37, kMemoDw0 = 10;
 struct CoefMemo {
   uint32_t key;                   // valid | width | channel | scan | transform skip
@@ -143,7 +146,8 @@ struct CoefMemoBig {
 };
 // per-chain state in HBM
 struct State {
-  int dbg[4];  // HM_CHECKS: E.dbg of the last CTU
+  int status[4];  // [0]: the job's status word (hvx_hm_job_status: 0 ran, -HVX_HM_BAD_* refused)
+  int dbg[4];     // HM_CHECKS: E.dbg of the last CTU
   uint64_t prof[2][32];  // HM_PROFILE: per-category clock ticks and calls of the job
   Cu cu[8];
   Yuv yuv[28];                    // TComYuv sets (kind x depth), addressed through hm_e.yi
@@ -288,13 +292,6 @@ __device__ __forceinline__ int16_t *yaddr_w(Yuv *b, int c, int x, int y, int w) 
   return b->s + ycoff(c, w) + y * (c ? w >> 1 : w) + x;
 }
 __device__ __forceinline__ int16_t *yaddr(Yuv *b, int c, int x, int y) { return yaddr_w(b, c, x, y, E.yw); }
-// a TU node on the LDS stack for the scope of the object (declared like a local: TU_LOCAL(ch))
-struct TuSlot {
-  Tu &t;
-  __device__ __forceinline__ TuSlot() : t(E.tstack[E.tsp]) { E.tsp = E.tsp + 1; }
-  __device__ __forceinline__ ~TuSlot() { E.tsp = E.tsp - 1; }
-};
-#define TU_LOCAL(name) TuSlot name##_slot_; Tu &name = name##_slot_.t
 // HM_PROFILE builds accumulate the clock ticks (s_memtime) and calls of the leaf categories
 enum { PR_ME, PR_MC, PR_TPL, PR_TUF, PR_TUI, PR_COEF, PR_EST, PR_IFP, PR_IPRED, PR_DIST, PR_CTU, PR_ENC, PR_N };
 // sub-phases (HM_PROFILE): 12..15 TUF by size; 16 COEF descriptor, 17 COEF staging, 18 COEF walk,
@@ -350,6 +347,22 @@ __device__ __noinline__ void hm_fail(int code, int a, int b) {
 #define HM_STAGE(k) ((void)0)
 #define HM_STOPPED 0
 #endif
+
+// a TU node on the LDS stack for the scope of the object (declared like a local: TU_LOCAL(ch))
+// (the deepest nesting is 6 nodes: est_intra_pred_luma_qt's CU and PU nodes + four RQT levels, or
+// an RQT level's children + encode_inter_residual_qt's descent; HM_CHECKS builds bound it)
+__device__ __forceinline__ int tu_push() {
+  const int k = E.tsp;
+  HMC(k >= 0 && k < kTuStack, 90, k, 0);
+  E.tsp = k + 1;
+  return HM_CHECKING ? (k < 0 ? 0 : k >= kTuStack ? kTuStack - 1 : k) : k;
+}
+struct TuSlot {
+  Tu &t;
+  __device__ __forceinline__ TuSlot() : t(E.tstack[tu_push()]) {}
+  __device__ __forceinline__ ~TuSlot() { E.tsp = E.tsp - 1; }
+};
+#define TU_LOCAL(name) TuSlot name##_slot_; Tu &name = name##_slot_.t
 
 // ============================================================================================
 // CABAC bit counter over the coders in LDS (cbin/cep/ctrm/reset_bits/written_bits/load)
@@ -2925,7 +2938,10 @@ __device__ void motion_estimation_bi(Cu *cu, int ps, int pu, Yuv *org, int list,
   wsync();
   const hvx_me_result r = E.S->me.r;
   wsync();
-  HMC(r.mv_x >= -4 * 80 && r.mv_y >= -4 * 80 && r.mv_x < 4 * (E.P.w + 80) && r.mv_y < 4 * (E.P.h + 80), 10, r.mv_x, r.mv_y);
+  // the block the vector points at stays inside the padded reference (as check 9: clipMv allows
+  // up to -(x + 72) samples, so the vector itself is not bounded by the margin)
+  HMC(4 * xp + r.mv_x >= -4 * 80 && 4 * yp + r.mv_y >= -4 * 80 && 4 * (xp + w) + r.mv_x <= 4 * (E.P.w + 80) &&
+          4 * (yp + h) + r.mv_y <= 4 * (E.P.h + 80), 10, r.mv_x, r.mv_y);
   mv[0] = (int16_t)r.mv_x; mv[1] = (int16_t)r.mv_y;
   bits = r.bits;
   cost = r.cost;
@@ -4250,7 +4266,8 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
   State *S = (State *)(state_base + (size_t)jid * state_bytes);
   {
     const int bad = hm_job_check(pics, n_pics, job, n_out);
-    if (l < 4) S->dbg[l] = l == 0 ? -bad : 0;  // the job's status word (hvx_hm_job_status)
+    if (l < 4) S->status[l] = l == 0 ? -bad : 0;  // the job's status word (hvx_hm_job_status)
+    if (l < 4) S->dbg[l] = 0;
     if (bad) return;
   }
   copy_words(&hm_e.P, &pics[job.pic], (int)sizeof(hvx_hm_picture));

@@ -10,20 +10,6 @@ struct hvx_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
-  // hvx_ctu_analyze / hvx_ctu_encode run their independent branches on three more streams (fork/join events)
-  hipStream_t aux[3] = {};
-  hipEvent_t fj[8] = {};
-  // HVX_SERIAL_STREAMS=1: every branch on ctx->stream (profiling: isolated per-kernel times)
-  bool serial = false;
-  // optional per-phase timing of hvx_ctu_analyze: a begin/end event pair on the launch's own
-  // stream around every timed launch, folded into phase_ms[phase] (phases may overlap)
-  int timing = 0;
-  static constexpr int kMaxTimed = 48;
-  hipEvent_t tev[2 * kMaxTimed] = {};
-  int tphase[kMaxTimed] = {};
-  int ntev = 0;
-  bool ev_ok = false;
-  double phase_ms[HVX_NPHASE] = {};
   // staging for the host-memory single-TU forms
   char *scratch = nullptr;
   char *pinned = nullptr;

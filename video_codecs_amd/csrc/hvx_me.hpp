@@ -535,27 +535,6 @@ static __global__ __launch_bounds__(64) void k_me_int(const uint8_t *const *__re
   me_int_job<0, 0, 1>(j, cur_planes, ref_planes, stride, org, red, out + jid);
 }
 
-// CTU-pass view: block b = (ctu * ncu + cu) * nref + ref of one depth -> job slot
-// ((ctu * 85 + first + cu) * nref + ref)
-__device__ __forceinline__ size_t me_ctu_slot(int b, int nref, int ncu, int first) {
-  const int ref = b % nref, cu = (b / nref) % ncu, ctu = b / (nref * ncu);
-  return ((size_t)ctu * HVX_CUS_PER_CTU + first + cu) * nref + ref;
-}
-
-// CTU pass: square SxS jobs of one depth (FEN shift SUB decided on the host), NW waves per job
-template <int S, int SUB, int NW>
-static __global__ __launch_bounds__(64 * NW) void k_me_int_ctu(const uint8_t *const *__restrict__ cur_planes,
-                                                       const uint8_t *const *__restrict__ ref_planes, int stride,
-                                                       const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
-                                                       int nref, int ncu, int first) {
-  __shared__ __attribute__((aligned(16))) uint8_t org[S * S];
-  __shared__ uint32_t red[2 * kMeMaxRanges * NW];
-  const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
-  const hvx_me_job j = jobs[slot];
-  if (j.w > 0 && (j.w != S || j.h != S)) return;  // not this depth's shape (cannot happen in the pass)
-  me_int_job<S, SUB, NW>(j, cur_planes, ref_planes, stride, org, red, out + slot);
-}
-
 // ======================================================================================
 // fractional refinement
 // ======================================================================================
@@ -1148,70 +1127,6 @@ static __global__ __launch_bounds__(256) void k_me_frac(const uint8_t *const *__
   if (jid >= n) return;
   const hvx_me_job j = jobs[jid];
   me_frac_job<64, 4, true>(j, cur_planes, ref_planes, stride, sm, out + jid);
-}
-
-// CTU pass: square SxS jobs of one depth, NW waves per job
-template <int S, int NW>
-static __global__ __launch_bounds__(64 * NW) void k_me_frac_ctu(const uint8_t *const *__restrict__ cur_planes,
-                                                        const uint8_t *const *__restrict__ ref_planes, int stride,
-                                                        const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
-                                                        int nref, int ncu, int first) {
-  __shared__ MeFracSmem<S, NW> sm;
-  const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
-  const hvx_me_job j = jobs[slot];
-  me_frac_job<S, NW, false>(j, cur_planes, ref_planes, stride, sm, out + slot);
-}
-
-// CTU pass, fused: TZ integer search then the fractional refinement of the same job in one
-// workgroup (the original block stays in LDS, the integer result in registers) -- used for
-// the 32/16/8 depths, where the separate kernels' per-job reloads dominated.  The 8x8 form is
-// held to 72 VGPRs (7 waves per SIMD instead of 6, no spill): its launch is 8% shorter; the same
-// bound on the 16x16 form spills and slows the step.
-// one (CU, reference) job of the CTU pass: TZ integer search then the fractional refinement in
-// the same workgroup; writes out[slot] (a defined zero result for a CU outside the picture)
-template <int S, int SUB, int NW>
-__device__ __forceinline__ void me_ctu_job(const uint8_t *const *__restrict__ cur_planes,
-                                           const uint8_t *const *__restrict__ ref_planes, int stride,
-                                           const hvx_me_job &j, hvx_me_result *__restrict__ out, size_t slot,
-                                           MeFracSmem<S, NW> &sm, uint32_t *red) {
-  if (j.w <= 0 || j.h <= 0) {
-    if (me_tid<NW>() == 0) { hvx_me_result z; memset(&z, 0, sizeof(z)); out[slot] = z; }
-    return;
-  }
-  const uint8_t *cur = cur_planes[j.cur_idx] + j.pu_y * stride + j.pu_x;
-  for (int k = me_tid<NW>(); k < S * S; k += HVX_WAVE * NW) {
-    const int y = k / S, x = k - y * S;
-    sm.org[y * S + x] = cur[y * stride + x];
-  }
-  me_sync<NW>();
-  MeInt m;
-  m.org = sm.org; m.red = red; m.par = 0; m.os = S;
-  me_ref_setup(m, j, ref_planes[j.ref_idx], stride);
-  m.sub = SUB;
-  m.rows = S >> SUB;
-  m.gw = S >> 2;
-  m.lam = j.lambda_motion;
-  m.px = j.pred_x; m.py = j.pred_y;
-  me_tz<S, SUB, NW>(j, m);
-  const uint32_t sad_int = m.best_sad - me_mv_cost(m.lam, m.px, m.py, 2, m.best_x, m.best_y);
-#ifdef HVX_EXP_NOFRAC
-  if (me_tid<NW>() == 0) { hvx_me_result r{}; r.mv_int_x = m.best_x; r.mv_int_y = m.best_y; r.sad_int = sad_int; r.cost = sad_int; out[slot] = r; }
-  return;
-#endif
-  me_frac_refine<S, NW, false, uint8_t>(j, m.ref, stride, m.best_x, m.best_y, sad_int, sm, out + slot);
-}
-
-template <int S, int SUB, int NW>
-static __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(S == 8 ? 7 : 1))) void k_me_ctu(const uint8_t *const *__restrict__ cur_planes,
-                                                   const uint8_t *const *__restrict__ ref_planes, int stride,
-                                                   const hvx_me_job *__restrict__ jobs, hvx_me_result *__restrict__ out,
-                                                   int nref, int ncu, int first) {
-  __shared__ MeFracSmem<S, NW> sm;
-  __shared__ uint32_t red[2 * kMeMaxRanges * NW];
-  const size_t slot = me_ctu_slot(blockIdx.x, nref, ncu, first);
-  const hvx_me_job j = jobs[slot];
-  if (j.w > 0 && (j.w != S || j.h != S)) return;
-  me_ctu_job<S, SUB, NW>(cur_planes, ref_planes, stride, j, out, slot, sm, red);
 }
 
 // ======================================================================================

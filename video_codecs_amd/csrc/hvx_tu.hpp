@@ -1816,229 +1816,3 @@ static __global__ __launch_bounds__(64) void k_tu_fin(const hvx_tu_desc *__restr
     }
   }
 }
-
-// =======================================================================================
-// Small TUs of the CTU pass (4x4, 8x8), ONE TU PER LANE for the whole forward / finishing
-// stages: a wave-per-TU launch leaves most lanes idle on 16 or 64 coefficients and costs a
-// workgroup per TU.  The TU's samples live in the lane's registers, the 2-D transforms are
-// the same integer products as tu_forward_transform / tu_inverse_transform (xTrMxN / xITrMxN)
-// with the matrix read as wave-uniform constants, and the scan-order arrays are the
-// interleaved ones of the lane-parallel RDOQ (G = 64: lane-consecutive words).  Only the CTU
-// pass's TUs take these kernels: RDOQ on (no bypass, no selective RDOQ, no ARL), inter, so
-// the scan is the up-right diagonal one, resolved at compile time.
-// =======================================================================================
-// raster index (row-major N x N, N = 4 << L) of grouped diagonal scan position sp
-template <int L>
-__host__ __device__ constexpr int diag_raster(int sp) {
-  constexpr int N = 4 << L, G = 1 << L;
-  const int cg = sp >> 4, k = sp & 15;
-  int cgy = 0, cgx = 0, n = 0;
-  for (int d = 0; d < 2 * G - 1; d++) {
-    int y = d < G - 1 ? d : G - 1, x = d - y;
-    while (y >= 0 && x < G) {
-      if (n == cg) { cgy = y; cgx = x; }
-      n++; y--; x++;
-    }
-  }
-  int ky = 0, kx = 0;
-  n = 0;
-  for (int d = 0; d < 7; d++) {
-    int y = d < 3 ? d : 3, x = d - y;
-    while (y >= 0 && x < 4) {
-      if (n == k) { ky = y; kx = x; }
-      n++; y--; x++;
-    }
-  }
-  return (cgy * 4 + ky) * N + cgx * 4 + kx;
-}
-
-template <int L>
-__device__ __forceinline__ int lane_mat(bool dst, int k, int x) {  // wave-uniform (k, x) in unrolled loops
-  constexpr int N = 4 << L;
-  if (L == 0 && dst) return kDst4[k * 4 + x];
-  return kMat[mat_base(L) + k * N + x];
-}
-
-// A lane's whole TU as 16-byte vector accesses (the TU regions are 16-byte aligned: offsets are
-// multiples of NN elements): one memory instruction per 8 residuals / 16 prediction samples
-// instead of one per element, each of which touched 64 different lines across the wave.
-template <int NN>
-__device__ __forceinline__ void lane_ld_i16(const int16_t *p, int32_t (&r)[NN]) {
-  const uint4 *q = reinterpret_cast<const uint4 *>(p);
-#pragma unroll
-  for (int k = 0; k < NN / 8; k++) {
-    const uint4 v = q[k];
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int e = 0; e < 4; e++) { r[8 * k + 2 * e] = (int16_t)(w[e] & 0xffffu); r[8 * k + 2 * e + 1] = (int32_t)w[e] >> 16; }
-  }
-}
-template <int NN>
-__device__ __forceinline__ void lane_ld_u8(const uint8_t *p, int32_t (&r)[NN]) {
-  const uint4 *q = reinterpret_cast<const uint4 *>(p);
-#pragma unroll
-  for (int k = 0; k < NN / 16; k++) {
-    const uint4 v = q[k];
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int e = 0; e < 16; e++) r[16 * k + e] = (int32_t)((w[e >> 2] >> (8 * (e & 3))) & 0xffu);
-  }
-}
-template <int NN>
-__device__ __forceinline__ void lane_st_i16(int16_t *p, const int32_t (&r)[NN]) {
-  uint4 *q = reinterpret_cast<uint4 *>(p);
-#pragma unroll
-  for (int k = 0; k < NN / 8; k++) {
-    uint32_t w[4];
-#pragma unroll
-    for (int e = 0; e < 4; e++) w[e] = __builtin_amdgcn_perm((uint32_t)r[8 * k + 2 * e + 1], (uint32_t)r[8 * k + 2 * e], 0x05040100u);
-    q[k] = make_uint4(w[0], w[1], w[2], w[3]);
-  }
-}
-
-template <int L>
-static __global__ __launch_bounds__(64) void k_tu_fwd_lane(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
-                                                    int n, const int16_t *__restrict__ res_in, uint32_t *__restrict__ ldI,
-                                                    uint32_t *__restrict__ cxI, int8_t *__restrict__ flags) {
-  constexpr int N = 4 << L, NN = N * N, LOG2 = L + 2;
-  const int t = blockIdx.x * 64 + lane_id();
-  if (t >= n) return;
-  const hvx_tu_desc d = descs[t];
-  if (d.width != N || d.height != N) return;
-  int32_t r[NN];
-  lane_ld_i16<NN>(res_in + offs[t], r);
-  int32_t c[NN];
-  if (d.transform_skip) {  // xTransformSkip
-    const int ts = tu_transform_shift(d);
-#pragma unroll
-    for (int i = 0; i < NN; i++) c[i] = ts >= 0 ? shl32(r[i], ts) : (r[i] + (1 << (-ts - 1))) >> -ts;
-  } else {  // xTrMxN: rows then columns
-    const bool dst = d.use_dst && N == 4;
-    constexpr int s1 = LOG2 - 1, s2 = LOG2 + 6;
-    constexpr int a1 = s1 > 0 ? 1 << (s1 - 1) : 0, a2 = 1 << (s2 - 1);
-    int32_t tmp[NN];
-#pragma unroll
-    for (int y = 0; y < N; y++)
-#pragma unroll
-      for (int u = 0; u < N; u++) {
-        int acc = 0;
-#pragma unroll
-        for (int x = 0; x < N; x++) acc += lane_mat<L>(dst, u, x) * r[y * N + x];
-        tmp[y * N + u] = (acc + a1) >> s1;
-      }
-#pragma unroll
-    for (int v = 0; v < N; v++)
-#pragma unroll
-      for (int u = 0; u < N; u++) {
-        int acc = 0;
-#pragma unroll
-        for (int y = 0; y < N; y++) acc += lane_mat<L>(dst, v, y) * tmp[y * N + u];
-        c[v * N + u] = (acc + a2) >> s2;
-      }
-  }
-  const int ts = tu_transform_shift(d);
-  const int qbits = 14 + d.qp_per + ts;
-  const int qc = kQuantScales[d.qp_rem];
-  const int64_t lim = (int64_t)2147483647 - ((int64_t)1 << (qbits - 1));
-  const TuCoding cd = tu_coding<L>(d);
-  const int ch = d.comp ? 1 : 0, sig_off = ch ? 28 : 0;
-#pragma unroll
-  for (int sp = 0; sp < NN; sp++) {
-    const int blk = diag_raster<L>(sp);
-    const int32_t cf = c[blk];
-    const int32_t ld = rd_level_double(cf, qc, lim);
-    const size_t il = tu_il(t, sp, NN, 64);
-    ldI[il] = (uint32_t)ld | (cf < 0 ? 0x80000000u : 0u);
-    uint32_t cx = 0;
-#pragma unroll
-    for (int p = 0; p < 4; p++) cx |= (uint32_t)(sig_off + rd_sig_ctx_raster<L>(p, cd.first_sig, blk, ch)) << (6 * p);
-    cxI[il] = cx;
-  }
-  flags[t] = 1;
-}
-
-template <int L>
-static __global__ __launch_bounds__(64) void k_tu_fin_lane(const hvx_tu_desc *__restrict__ descs, const int64_t *__restrict__ offs,
-                                                    int n, const int16_t *__restrict__ res_in,
-                                                    const int32_t *__restrict__ levI, int32_t *__restrict__ lev_io,
-                                                    int16_t *__restrict__ res_out, uint32_t *__restrict__ sse_out,
-                                                    const uint8_t *__restrict__ pred, uint32_t *__restrict__ zd_out,
-                                                    uint32_t *__restrict__ csse_out) {
-  constexpr int N = 4 << L, NN = N * N;
-  const int t = blockIdx.x * 64 + lane_id();
-  if (t >= n) return;
-  const hvx_tu_desc d = descs[t];
-  if (d.width != N || d.height != N) return;
-  const int64_t off = offs[t];
-  int32_t lv[NN];
-#pragma unroll
-  for (int sp = 0; sp < NN; sp++) lv[diag_raster<L>(sp)] = levI[tu_il(t, sp, NN, 64)];
-#pragma unroll
-  for (int i = 0; i < NN; i++) lev_io[off + i] = lv[i];
-  // xDeQuant (flat scaling), then xITransformSkip or xITrMxN (tu_inverse)
-  const int ts = tu_transform_shift(d);
-  const int max_log2 = d.max_log2_tr_range;
-  const int32_t tmin = -(1 << max_log2), tmax = (1 << max_log2) - 1;
-  const int right = 6 - (ts + d.qp_per);
-  const int scale = kInvQuantScales[d.qp_rem];
-  int tib = 32 + right - 7;
-  if (max_log2 + 1 < tib) tib = max_log2 + 1;
-  const int32_t imin = -(1 << (tib - 1)), imax = (1 << (tib - 1)) - 1;
-#pragma unroll
-  for (int i = 0; i < NN; i++) {
-    const int32_t cq = clip3(imin, imax, lv[i]);
-    const int32_t v = right > 0 ? (cq * scale + (1 << (right - 1))) >> right : shl32(cq * scale, -right);
-    lv[i] = clip3(tmin, tmax, v);
-  }
-  int32_t rr[NN];
-  if (d.transform_skip) {
-#pragma unroll
-    for (int i = 0; i < NN; i++) {
-      const int32_t v = lv[i];
-      rr[i] = (int16_t)(ts >= 0 ? (v + (ts == 0 ? 0 : 1 << (ts - 1))) >> ts : shl32(v, -ts));
-    }
-  } else {
-    const bool dst = d.use_dst && N == 4;
-    int32_t tmp[NN];
-#pragma unroll
-    for (int y = 0; y < N; y++)
-#pragma unroll
-      for (int u = 0; u < N; u++) {
-        int acc = 0;
-#pragma unroll
-        for (int v = 0; v < N; v++) acc += lane_mat<L>(dst, v, y) * lv[v * N + u];
-        tmp[y * N + u] = clip3(-32768, 32767, (acc + 64) >> 7);
-      }
-#pragma unroll
-    for (int y = 0; y < N; y++)
-#pragma unroll
-      for (int x = 0; x < N; x++) {
-        int acc = 0;
-#pragma unroll
-        for (int u = 0; u < N; u++) acc += lane_mat<L>(dst, u, x) * tmp[y * N + u];
-        rr[y * N + x] = (int16_t)clip3(-32768, 32767, (acc + 2048) >> 12);
-      }
-  }
-  lane_st_i16<NN>(res_out + off, rr);
-  int32_t rin[NN];
-  lane_ld_i16<NN>(res_in + off, rin);
-  uint32_t sse = 0, z = 0, cs = 0;
-#pragma unroll
-  for (int i = 0; i < NN; i++) {
-    const int r = rr[i], ri = rin[i];
-    sse += (uint32_t)((ri - r) * (ri - r));
-    z += (uint32_t)(ri * ri);
-  }
-  if (pred) {
-    int32_t pv[NN];
-    lane_ld_u8<NN>(pred + off, pv);
-#pragma unroll
-    for (int i = 0; i < NN; i++) {
-      const int p = pv[i], v = p + rr[i], e = rin[i] + p - (v < 0 ? 0 : v > 255 ? 255 : v);
-      cs += (uint32_t)(e * e);
-    }
-  }
-  if (sse_out) sse_out[t] = sse;
-  if (zd_out) zd_out[t] = z;
-  if (pred && csse_out) csse_out[t] = cs;
-}

@@ -365,9 +365,9 @@ class Engine:
         out_cod = torch.zeros(n_out * HM_CODER.itemsize, dtype=torch.uint8, device=self.device)
         self.launch(jobs_t, n, out_ctu, out_rec, out_cod)
         torch.cuda.synchronize()
-        st = self.state[:n * sb].view(n, sb)[:, :528].cpu().numpy().copy()
-        self.last_debug = st[:, :16].copy().view(np.int32).reshape(n, 4)  # State.dbg (HM_CHECKS builds)
-        self.last_prof = st[:, 16:528].copy().view(np.uint64).reshape(n, 2, 32)  # State.prof (HM_PROFILE builds)
+        st = self.state[:n * sb].view(n, sb)[:, :544].cpu().numpy().copy()  # State.status | dbg | prof
+        self.last_debug = st[:, 16:32].copy().view(np.int32).reshape(n, 4)  # State.dbg (HM_CHECKS builds)
+        self.last_prof = st[:, 32:544].copy().view(np.uint64).reshape(n, 2, 32)  # State.prof (HM_PROFILE builds)
         return (out_ctu.cpu().numpy().view(HM_CTU), out_rec.cpu().numpy().reshape(n_out, 6144),
                 out_cod.cpu().numpy().view(HM_CODER))
 

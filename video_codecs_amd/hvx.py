@@ -40,12 +40,6 @@ def lib():
             "hvx_me_batch": [P, P, P, I, P, I, P], "hvx_ssim_batch": [P, P, P, P, I, P],
             "hvx_stvssim_batch": [P, P, P, P, P, I, P],
             "hvx_plane_from_pel": [P, P, I, I, I, P], "hvx_plane_extend": [P, P, I, I],
-            "hvx_ctu_workspace_size": [I, I, I, ctypes.POINTER(ctypes.c_size_t)],
-            "hvx_ctu_analyze": [P, P, P, I, P, P, P, ctypes.c_size_t, P],
-            "hvx_ctu_decide": [P, P, I, P, P, P, P, ctypes.c_size_t, P, P, P, P],
-            "hvx_ctu_encode": [P, P, P, I, P, P, P, P, P, ctypes.c_size_t, P, P, P, P],
-            "hvx_ctu_encode_yuv": [P, P, P, I, P, P, P, P, P, P, ctypes.c_size_t, P, P, P, P],
-            "hvx_set_timing": [P, I], "hvx_phase_times": [P, ctypes.POINTER(ctypes.c_double), I, I],
             "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
             "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_coeff_write_batch": [P, P, P, P, P, I, P, P, P, P, I, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P],
             "hvx_intra_pred_batch": [P, P, I, P, I, P, P, P], "hvx_deblock": [P, P, I, P, P, I, P, P, P, P], "hvx_sao_stats": [P, P, P, P, I, I, P, P, P, I, I, I, I, P], "hvx_sao_apply": [P, P, P, P, I, I, P, P, P, I, I, I, I, P], "hvx_intra_search_batch": [P, P, P, I, P, I, P, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
@@ -271,139 +265,6 @@ def plane_from_pel(pel, pel_stride, width, height, plane):
 
 def plane_extend(plane, width, height):
     _check(lib().hvx_plane_extend(context(), _ptr(plane), width, height), "hvx_plane_extend")
-
-
-def ctu_workspace_size(pic_w, pic_h, n_ref):
-    n = ctypes.c_size_t()
-    _check(lib().hvx_ctu_workspace_size(pic_w, pic_h, n_ref, ctypes.byref(n)), "hvx_ctu_workspace_size")
-    return n.value
-
-
-class ChromaPlanes(ctypes.Structure):
-    """hvx_chroma_planes (hvx_types.h): device origins of the 4:2:0 chroma planes."""
-    _fields_ = [("cur_cb", ctypes.c_void_p), ("cur_cr", ctypes.c_void_p), ("refs_c", ctypes.c_void_p),
-                ("recon_cb", ctypes.c_void_p), ("recon_cr", ctypes.c_void_p), ("ref_pic_cb", ctypes.c_void_p),
-                ("ref_pic_cr", ctypes.c_void_p), ("c_stride", ctypes.c_int32), ("pad_", ctypes.c_int32)]
-
-
-class CtuAnalyzer:
-    """Device-resident CTU analysis pass (hvx_ctu_analyze) for one picture geometry; chroma=True:
-    the 4:2:0 step (hvx_ctu_encode_yuv, encode_yuv)."""
-
-    def __init__(self, pic_w, pic_h, n_ref, qp, lam=None, est4=None, rd_metric=_abi.RD_SSE, ctx=None, chroma=False):
-        """ctx: a private hvx_ctx (new_context()) for an analyzer that runs concurrently with
-        others on the same GPU; None = the shared per-device context."""
-        import torch
-        self._c = ctx
-        self.chroma = chroma
-        self.params = _abi.ctu_params(pic_w, pic_h, n_ref, qp, lam, rd_metric=rd_metric, chroma=chroma)
-        self.pic_w, self.pic_h, self.n_ref = pic_w, pic_h, n_ref
-        self.stride = pic_w + 2 * _abi.PLANE_MARGIN
-        self.c_stride = pic_w // 2 + _abi.PLANE_MARGIN
-        self.nctu = ((pic_w + 63) // 64) * ((pic_h + 63) // 64)
-        self.ws_bytes = ctu_workspace_size(pic_w, pic_h, n_ref)
-        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device="cuda")
-        if est4 is None:
-            est4 = _abi.estbits_p_yuv(estbits_update) if chroma else _abi.load_estbits_p_luma()
-        self.est = torch.from_numpy(np.ascontiguousarray(est4, np.int32).reshape(-1)).cuda()
-        self.out = torch.zeros(self.nctu * _abi.CUS_PER_CTU * _abi.CU_RESULT.itemsize, dtype=torch.uint8, device="cuda")
-
-    def ctx(self):
-        return context() if self._c is None else bind(self._c)
-
-    def run(self, cur_plane, ref_planes_ptrs):
-        """cur_plane: padded uint8 device tensor; ref_planes_ptrs: int64 device tensor of origin pointers."""
-        origin = plane_origin_ptr(cur_plane, self.pic_w)
-        p = np.ascontiguousarray(self.params)
-        _check(lib().hvx_ctu_analyze(self.ctx(), ctypes.c_void_p(origin), _ptr(ref_planes_ptrs), self.stride,
-                                     p.ctypes.data_as(ctypes.c_void_p), _ptr(self.est), _ptr(self.ws),
-                                     self.ws_bytes, _ptr(self.out)), "hvx_ctu_analyze")
-
-    def results(self):
-        return from_device(self.out, _abi.CU_RESULT).reshape(self.nctu, _abi.CUS_PER_CTU)
-
-    def _rate_model(self, states=None, entropy_bits=None):
-        import torch
-        if not hasattr(self, "dec"):
-            st = _abi.load_ctx_p_states() if states is None else states
-            eb = _abi.load_entropy_bits() if entropy_bits is None else entropy_bits
-            self.states = torch.from_numpy(np.ascontiguousarray(st, np.uint8)).cuda()
-            self.eb = torch.from_numpy(np.ascontiguousarray(eb, np.int32)).cuda()
-            self.dec = torch.zeros(self.nctu * _abi.CUS_PER_CTU * _abi.CU_DECISION.itemsize, dtype=torch.uint8,
-                                   device="cuda")
-
-    def encode(self, cur_plane, ref_planes_ptrs, recon_plane, ref_pic=None):
-        """hvx_ctu_encode: run() + decide() as one schedule (same results)."""
-        self._rate_model()
-        p = np.ascontiguousarray(self.params)
-        _check(lib().hvx_ctu_encode(self.ctx(), ctypes.c_void_p(plane_origin_ptr(cur_plane, self.pic_w)),
-                                    _ptr(ref_planes_ptrs), self.stride, p.ctypes.data_as(ctypes.c_void_p),
-                                    _ptr(self.est), _ptr(self.states), _ptr(self.eb), _ptr(self.ws), self.ws_bytes,
-                                    _ptr(self.out), _ptr(self.dec),
-                                    ctypes.c_void_p(plane_origin_ptr(recon_plane, self.pic_w)),
-                                    ctypes.c_void_p(0 if ref_pic is None else plane_origin_ptr(ref_pic, self.pic_w))),
-               "hvx_ctu_encode")
-
-    def encode_yuv(self, cur3, ref_ptrs_y, ref_ptrs_c, recon3, ref_pic3=None):
-        """hvx_ctu_encode_yuv: cur3 / recon3 / ref_pic3 = (Y, Cb, Cr) padded uint8 device tensors (chroma:
-        half size, margin PLANE_MARGIN // 2); ref_ptrs_y = int64 device tensor of the references' Y
-        origins, ref_ptrs_c = int64 device tensor of their Cb origins then their Cr origins."""
-        assert self.chroma
-        self._rate_model()
-        w2 = self.pic_w // 2
-        co = lambda t: plane_origin_ptr(t, w2, _abi.PLANE_MARGIN // 2)  # noqa: E731
-        cp = ChromaPlanes(co(cur3[1]), co(cur3[2]), ref_ptrs_c.data_ptr(), co(recon3[1]), co(recon3[2]),
-                          0 if ref_pic3 is None else co(ref_pic3[1]), 0 if ref_pic3 is None else co(ref_pic3[2]),
-                          self.c_stride, 0)
-        p = np.ascontiguousarray(self.params)
-        _check(lib().hvx_ctu_encode_yuv(self.ctx(), ctypes.c_void_p(plane_origin_ptr(cur3[0], self.pic_w)),
-                                        _ptr(ref_ptrs_y), self.stride, ctypes.byref(cp),
-                                        p.ctypes.data_as(ctypes.c_void_p), _ptr(self.est), _ptr(self.states),
-                                        _ptr(self.eb), _ptr(self.ws), self.ws_bytes, _ptr(self.out), _ptr(self.dec),
-                                        ctypes.c_void_p(plane_origin_ptr(recon3[0], self.pic_w)),
-                                        ctypes.c_void_p(0 if ref_pic3 is None else plane_origin_ptr(ref_pic3[0],
-                                                                                                     self.pic_w))),
-               "hvx_ctu_encode_yuv")
-
-    def decide(self, cur_plane, recon_plane, states=None, entropy_bits=None, ref_pic=None):
-        """hvx_ctu_decide after run(): CU tree of every CTU + the reconstructed picture (the leaves'
-        luma, borders extended) into recon_plane (padded uint8 device tensor shaped like cur_plane);
-        with ref_pic, also the deblocked reference picture."""
-        self._rate_model(states, entropy_bits)
-        p = np.ascontiguousarray(self.params)
-        _check(lib().hvx_ctu_decide(self.ctx(), ctypes.c_void_p(plane_origin_ptr(cur_plane, self.pic_w)), self.stride,
-                                    p.ctypes.data_as(ctypes.c_void_p), _ptr(self.states), _ptr(self.eb), _ptr(self.ws),
-                                    self.ws_bytes, _ptr(self.out), _ptr(self.dec),
-                                    ctypes.c_void_p(plane_origin_ptr(recon_plane, self.pic_w)),
-                                    ctypes.c_void_p(0 if ref_pic is None else plane_origin_ptr(ref_pic, self.pic_w))),
-               "hvx_ctu_decide")
-
-    def decisions(self):
-        return from_device(self.dec, _abi.CU_DECISION).reshape(self.nctu, _abi.CUS_PER_CTU)
-
-
-PHASES = ("me_d0", "me_d1", "me_d2", "me_d3", "frac_d0", "mc_resid",
-          "tu32_fwd", "tu32_rdoq", "tu32_fin", "tu16_fwd", "tu16_rdoq", "tu16_fin", "tu8_fwd", "tu8_rdoq", "tu8_fin",
-          "finalize", "coeff_bits", "decide_recon", "ref_picture")
-# the kernel each phase times (plus the tiny k_ctu_me_jobs in me_dN) and its timed launches per
-# hvx_ctu_encode_yuv call (the 4:2:0 bench step: tu16 = luma 16x16 + chroma 16x16, tu8 = luma 8x8 +
-# chroma 8x8 + chroma 4x4, coeff_bits = one count per TU class); phases run on 4 streams and may
-# overlap (DESIGN.md "Where the time goes")
-PHASE_LAUNCHES = (1, 1, 1, 1, 1, 3, 1, 1, 1, 2, 2, 2, 3, 3, 3, 1, 6, 4, 3)
-PHASE_KERNELS = ("k_me_int_ctu<64,1,4>", "k_me_ctu<32,1,2>", "k_me_ctu<16,1,1>", "k_me_ctu<8,0,1>",
-                 "k_me_frac_ctu<64,4>", "k_ctu_pred_resid", "k_tu_fwd<3>", "k_tu_rdoq<3>", "k_tu_fin<3,2>",
-                 "k_tu_fwd<2>", "k_tu_rdoq<2>", "k_tu_fin<2,2>", "k_tu_fwd<1>", "k_tu_rdoq<1>", "k_tu_fin<1,2>",
-                 "k_ctu_finalize", "k_coeff_bits_il", "k_ctu_leaf+k_ctu_decide", "k_ctu_bs+k_deblock")
-
-
-def set_timing(on, ctx=None):
-    _check(lib().hvx_set_timing(context() if ctx is None else ctx, int(on)), "hvx_set_timing")
-
-
-def phase_times(reset=True, ctx=None):
-    buf = (ctypes.c_double * len(PHASES))()
-    _check(lib().hvx_phase_times(context() if ctx is None else ctx, buf, len(PHASES), int(reset)), "hvx_phase_times")
-    return dict(zip(PHASES, list(buf)))
 
 
 def sync():
