@@ -165,23 +165,33 @@ class HmPlan:
         reference frames, collocated field."""
         from video_codecs_amd import synth
         prm = self.picture_params(p)
-        pi = np.zeros(46, np.int32)
-        pi[0:7] = [self.W, self.H, prm["poc"], 1, self.qp, self.nref, 0]
-        pi[7:11] = prm["ref_poc"][0]
-        pi[15:19] = prm["ref_plane"][0]
-        pi[19:23] = -1
-        pi[23:29] = [1, 0, 1, 1, 5, prm["col_poc"]]
-        pi[29:31] = [4, 0]
-        pi[31:35] = prm["col_ref_poc"][0]
-        pi[39:41] = prm["chroma_qp"]
-        pi[41:43] = [0, self.wc * self.hc]
-        pi[43] = np.array(prm["lambda_motion"], np.uint32).view(np.int32)
-        pi[45] = int(self.col)
-        pf = np.array([prm["lambda"], prm["sqrt_lambda"], *prm["chroma_weight"], *prm["tq_lambda"]], np.float64)
+        pi, pf = host_pic_arrays(self.W, self.H, prm, self.qp, col_nref=(4, 0) if self.col else (0, 0))
         org = synth.random_frame(self.W, self.H, self.base + self.nref + p)
         refs = np.concatenate([synth.random_frame(self.W, self.H, self.base + self.nref + p - 1 - k)
                                for k in range(self.nref)])
         return pi, pf, org, refs, self.col_field(p)
+
+
+def host_pic_arrays(W, H, prm, qp, col_nref=(4, 0)):
+    """A picture's slice parameters (hm.DevicePicture's params dict) as the restatement's pic_i32 /
+    pic_f64 arrays (oracle/cu_capture.cpp layout: hm_cases.P_* fields)."""
+    pi = np.zeros(46, np.int32)
+    nref = prm["nref"]
+    pi[0:7] = [W, H, prm["poc"], prm["slice_type"], qp, nref[0], nref[1]]
+    pi[7:11] = [int(prm["ref_poc"][0][k]) if k < nref[0] else -1 for k in range(4)]
+    pi[11:15] = [int(prm["ref_poc"][1][k]) if k < nref[1] else -1 for k in range(4)]
+    pi[15:19] = [int(prm["ref_plane"][0][k]) if k < nref[0] else -1 for k in range(4)]
+    pi[19:23] = [int(prm["ref_plane"][1][k]) if k < nref[1] else -1 for k in range(4)]
+    pi[23:29] = [prm["col_from_l0"], 0, prm["check_ldc"], prm["tmvp"], prm["max_merge"], prm["col_poc"]]
+    pi[29:31] = col_nref
+    pi[31:35] = prm["col_ref_poc"][0]
+    pi[35:39] = prm["col_ref_poc"][1]
+    pi[39:41] = prm["chroma_qp"]
+    pi[41:43] = [0, ((W + 63) // 64) * ((H + 63) // 64)]
+    pi[43] = np.array(prm["lambda_motion"], np.uint32).view(np.int32)
+    pi[45] = int(prm["col_valid"])
+    pf = np.array([prm["lambda"], prm["sqrt_lambda"], *prm["chroma_weight"], *prm["tq_lambda"]], np.float64)
+    return pi, pf
 
 
 class HmWorkload(HmPlan):
@@ -264,9 +274,10 @@ def _chain_jobs(specs, entry):
     return j
 
 
-def _time_chains(eng, job_steps, n_out, warmup):
+def _time_chains(eng, job_steps, n_out, warmup, keep=0):
     """Launch warmup + timed steps of chain jobs on a private stream; returns (seconds per timed
-    step from HIP events, wall seconds per timed step)."""
+    step from HIP events, wall seconds per timed step, kept) -- kept: per step, copies of the first
+    `keep` output slots (HM_CTU records, reconstructions) for a parity check after the timing."""
     import torch
     from video_codecs_amd import hm
     stream = torch.cuda.Stream()
@@ -275,7 +286,7 @@ def _time_chains(eng, job_steps, n_out, warmup):
     dev_jobs = [torch.from_numpy(j.view(np.uint8).reshape(-1).copy()).cuda() for j in job_steps]
     n_jobs = len(job_steps[0])
     torch.cuda.synchronize()
-    ev = []
+    ev, kept = [], []
     t0 = None
     with torch.cuda.stream(stream):
         for k, jt in enumerate(dev_jobs):
@@ -287,30 +298,63 @@ def _time_chains(eng, job_steps, n_out, warmup):
             eng.launch(jt, n_jobs, out_ctu, out_rec)
             e[1].record()
             ev.append(e)
+            if keep:
+                kept.append((out_ctu[:keep * hm.HM_CTU.itemsize].clone(), out_rec[:keep * 6144].clone()))
     stream.synchronize()
     wall = (time.perf_counter() - t0) / (len(dev_jobs) - warmup)
     ms = sum(a.elapsed_time(b) for a, b in ev[warmup:]) / (len(dev_jobs) - warmup)
-    return ms * 1e-3, wall
+    return ms * 1e-3, wall, kept
 
 
-def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, steps=1):
+def compare_chain_ctus(port, dev_parts, dev_coef, dev_rec, dev_cost, dev_bd):
+    """Mismatches between the restatement's outputs (hm_ctu.chains, CTU o) and the device's records
+    of the same CTUs (arrays indexed o): partitions, coefficients, reconstruction, totals."""
+    from video_codecs_amd import hm
+    mism, first = 0, []
+    for o in range(len(dev_parts)):
+        what = None
+        if not np.array_equal(port["parts"][o], dev_parts[o]):
+            d = np.argwhere(port["parts"][o] != dev_parts[o])
+            z, f = int(d[0][0]), int(d[0][1])
+            what = "part z=%d %s port=%d gpu=%d (%d fields differ)" % (z, hm.PART_FIELDS[f], port["parts"][o][z, f],
+                                                                      dev_parts[o][z, f], len(d))
+        elif not np.array_equal(port["coef"][o].astype(np.int16), dev_coef[o]):
+            what = "coef"
+        elif not np.array_equal(port["recon"][o], dev_rec[o]):
+            what = "recon"
+        elif port["cost"][o] != dev_cost[o] or not np.array_equal(port["bits_dist"][o], dev_bd[o]):
+            what = "totals port=(%s,%r) gpu=(%s,%r)" % (list(port["bits_dist"][o]), port["cost"][o], list(dev_bd[o]),
+                                                      dev_cost[o])
+        if what:
+            mism += 1
+            if len(first) < 4:
+                first.append("ctu %d: %s" % (o, what))
+    return mism, first
+
+
+def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, steps=10, parity_threads=16):
     """BASELINE config 4 (side figure): 2160p random-access B pictures with the stvssim SSIM cost in
     the decision (hvx_hm_compress, HVX_RD_SSIM, eta 1) at QP 22 / 27 / 32 / 37.  The picture is GOP
     position 2 of encoder_randomaccess_main.cfg (POC 4, TId 1: QP offset 2, QPFactor 0.3536,
     L0 = {POC 0, 8}, L1 = {8, 0}, TMVP from L1[0], BipredSearchRange 4), `pics` pictures in flight
-    (over `distinct` synthetic frame triples), every CTU row a slice; one step = every chain one
-    CTU.  The B-slice decision is pinned to HM by the RA captures (tests/golden/ctu_ra_q*.bin) and
-    its SSIM cost to the restatement (test_hm_ctu_ssim_rdo_gpu)."""
+    (over `distinct` synthetic frame triples), every CTU row a slice (the partial bottom row chained
+    after the row above); one step = every chain one CTU, `steps` timed steps after `warmup`.  The
+    B-slice decision is pinned to HM by the RA captures (tests/golden/ctu_ra_q*.bin); here every
+    CTU of picture 0's chains the GPU decided is re-decided by the restatement with the same SSIM
+    cost (oracle/hvx_oracle_cu.c hvxo_hm_chains_rd) and compared bit for bit."""
     import torch
     from concurrent.futures import ThreadPoolExecutor
+    import oracle  # noqa: F401  (test infrastructure: the parity checker, after the timing)
+    from oracle import hm_ctu
     from video_codecs_amd import _abi, hm, synth
     wc, hc = (W + 63) // 64, (H + 63) // 64
     eb = _abi.load_entropy_bits()
     with ThreadPoolExecutor(8) as ex:
         host = list(ex.map(lambda i: synth.random_frame(W, H, 7000 + i), range(3 * distinct)))
     frames = [hm.DeviceFrame(yuv_split(f, W, H)) for f in host]
-    del host
-    col = torch.from_numpy(synthetic_col_field(wc * hc, 77)).cuda()
+    col_h = synthetic_col_field(wc * hc, 77)
+    col = torch.from_numpy(col_h).cuda()
+    rows = hc - 1 if H % 64 else hc  # the partial bottom row chained after the row above (HmWorkload)
     res = {}
     for base_qp in qps:
         qp = base_qp + 2
@@ -325,7 +369,6 @@ def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, 
             k = p % distinct
             pictures.append(hm.DevicePicture(frames[3 * k + 2], [frames[3 * k], frames[3 * k + 1]], prm, eb, col_field=col))
         eng = hm.Engine(pictures)
-        rows = hc - 1 if H % 64 else hc  # the partial bottom row chained after the row above (HmWorkload)
         job_steps = []
         for pos in range(warmup + steps):
             specs = [(p, r * wc + pos, 1, r * wc, r * wc + wc - 1, pos > 0) for p in range(pics) for r in range(rows)]
@@ -333,17 +376,36 @@ def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, 
             if rows < hc:
                 j["flags"][rows - 1::rows] |= _abi.hm_slice_ctus(wc)
             job_steps.append(j)
-        sec, wall = _time_chains(eng, job_steps, pics * rows, warmup)
-        res[str(base_qp)] = {"slice_qp": qp, "ctus_per_s": round(pics * rows / sec, 2), "ms_per_step": round(sec * 1e3, 1),
-                             "wall_ms_per_step": round(wall * 1e3, 1), "lambda_ssim": prm["lambda_ssim"]}
+        sec, wall, kept = _time_chains(eng, job_steps, pics * rows, warmup, keep=rows)
         del eng, pictures
         torch.cuda.empty_cache()
+        # parity: picture 0's `rows` chains, CTUs 0 .. warmup + steps - 1 of each, on the restatement
+        done = warmup + steps
+        pi, pf = host_pic_arrays(W, H, prm, qp, col_nref=(4, 0))
+        t0 = time.perf_counter()
+        port = hm_ctu.chains(pi, pf, host[2], np.concatenate([host[0], host[1]]), entry,
+                             np.arange(rows, dtype=np.int32) * wc, done, wc, threads=parity_threads, col_field=col_h,
+                             rd_metric=_abi.RD_SSIM, lambda_ssim=prm["lambda_ssim"])
+        port_s = time.perf_counter() - t0
+        dev = [(ct.cpu().numpy().view(hm.HM_CTU), rc.cpu().numpy().reshape(rows, 6144)) for ct, rc in kept]
+        order = [(k, s) for k in range(rows) for s in range(done)]  # the port's CTU order: chain-major
+        mism, first = compare_chain_ctus(
+            port, np.stack([hm.unpack_parts(dev[s][0][k]["p"]) for k, s in order]),
+            np.stack([dev[s][0][k]["coef"] for k, s in order]), np.stack([dev[s][1][k] for k, s in order]),
+            np.array([dev[s][0][k]["cost"] for k, s in order]),
+            np.array([[dev[s][0][k]["bits"], dev[s][0][k]["dist"]] for k, s in order], np.uint32))
+        res[str(base_qp)] = {"slice_qp": qp, "ctus_per_s": round(pics * rows / sec, 2), "ms_per_step": round(sec * 1e3, 1),
+                             "wall_ms_per_step": round(wall * 1e3, 1), "lambda_ssim": prm["lambda_ssim"],
+                             "gpu_parity_ctus": len(order), "gpu_parity_mismatches": mism, "first_mismatches": first,
+                             "port_ctus_per_s": round(len(order) / port_s, 2)}
     return {"workload": "2160p RA B pictures (GOP position 2: POC 4, L0 {0,8} / L1 {8,0}, bi-pred + bBi refinement), "
-                        "SSIM cost in TEncCu's decisions, eta 1, %d pictures x %d row-slice chains" % (pics, hc),
+                        "SSIM cost in TEncCu's decisions, eta 1, %d pictures x %d row-slice chains, %d timed steps after %d "
+                        "warmup; parity: picture 0's chains re-decided by oracle/hvx_oracle_cu.c on %d host threads"
+                        % (pics, rows, steps, warmup, parity_threads),
             "per_qp": res}
 
 
-def slice_mode0_measure(W, H, chains=2040, distinct=16, nref=4, base_qp=32, warmup=1, steps=1):
+def slice_mode0_measure(W, H, chains=2040, distinct=16, nref=4, base_qp=32, warmup=1, steps=10):
     """Side figure: the headline's P pictures coded with HM's default SliceMode 0 (one slice per
     picture, encoder_lowdelay_P_main.cfg:63) -- `chains` independent single-slice 2160p pictures in
     flight, one chain each (its own CTU array and reconstruction; the synthetic frames are shared by
@@ -376,14 +438,14 @@ def slice_mode0_measure(W, H, chains=2040, distinct=16, nref=4, base_qp=32, warm
     eng = hm.Engine(pictures)
     n = wc * hc
     job_steps = [_chain_jobs([(c, pos, 1, 0, n - 1, pos > 0) for c in range(chains)], entry) for pos in range(warmup + steps)]
-    sec, wall = _time_chains(eng, job_steps, chains, warmup)
+    sec, wall, _ = _time_chains(eng, job_steps, chains, warmup)
     del eng, pictures
     torch.cuda.empty_cache()
     return {"workload": "%d single-slice (SliceMode 0) 2160p P pictures, one chain each, QP %d, %d refs" % (chains, qp, nref),
             "ctus_per_s": round(chains / sec, 2), "ms_per_step": round(sec * 1e3, 1), "wall_ms_per_step": round(wall * 1e3, 1)}
 
 
-def hm_1080p_measure(pics=128, nref=4, base_qp=32, warmup=1, steps=1):
+def hm_1080p_measure(pics=128, nref=4, base_qp=32, warmup=1, steps=10):
     """Side figure (BASELINE configs 2/3 size): the headline's decision on 1080p random 4:2:0 P
     pictures -- HmWorkload at 1920x1080, `pics` pictures x 16 chains (17 CTU rows, the partial 17th
     chained after the 16th) = 2048 chains, one CTU per chain per step."""
@@ -410,13 +472,36 @@ def hm_1080p_measure(pics=128, nref=4, base_qp=32, warmup=1, steps=1):
         "wall_ms_per_step": round(wall * 1e3, 1)}
 
 
-def hm_cpu_port(work, threads, min_seconds=0.0):
+def _kept_records(work, positions):
+    """The GPU's records of picture 0's chains from HmWorkload.keep_steps: {(chain, position):
+    (parts, coef, recon, cost, (bits, dist))} for the chain positions in `positions` (first pass)."""
+    from video_codecs_amd import hm
+    got = {}
+    for pos, ct, rc in work.keep_steps:
+        c = ct.cpu().numpy().view(hm.HM_CTU).reshape(work.rows, work.ctus)
+        r = rc.cpu().numpy().reshape(work.rows, work.ctus, 6144)
+        for k in range(work.rows):
+            for i in range(work.ctus):
+                key = (k, pos + i)
+                if pos + i in positions[k] and key not in got:
+                    got[key] = (hm.unpack_parts(c[k, i]["p"]), c[k, i]["coef"], r[k, i], c[k, i]["cost"],
+                                (c[k, i]["bits"], c[k, i]["dist"]))
+    return got
+
+
+def _compare_port(port, got, order):
+    recs = [got[key] for key in order]
+    return compare_chain_ctus(port, np.stack([g[0] for g in recs]), np.stack([g[1] for g in recs]),
+                              np.stack([g[2] for g in recs]), np.array([g[3] for g in recs]),
+                              np.array([g[4] for g in recs], np.uint32))
+
+
+def hm_cpu_port(work, threads):
     """The oracle's restatement (oracle/hvx_oracle_cu.c hvxo_hm_chains) on picture 0's slice
     chains -- the same CTUs the GPU decided in its warmup + timed steps, on `threads` host threads
     -- and the bit-exact comparison of every one of them with the GPU's records."""
     import oracle  # noqa: F401  (test infrastructure: the checker and the port baseline)
     from oracle import hm_ctu
-    from video_codecs_amd import hm
     pi, pf, org, refs, col = work.host_inputs(0)
     wc, hc = work.wc, work.rows  # the picture's chains (the last may continue into the partial bottom row)
     done = min(work.step_idx * work.ctus, wc)  # CTUs of each row decided by the GPU (first pass)
@@ -426,51 +511,60 @@ def hm_cpu_port(work, threads, min_seconds=0.0):
     out = hm_ctu.chains(pi, pf, org, refs, work.entry, chain_first, done, wc, threads=threads, col_field=col)
     dt = time.perf_counter() - t0
     n = hc * done
-    # the GPU's records of the same CTUs: step s decided row position keep_steps[s][0] ..
-    dev_parts = np.zeros((hc, done, 256, 29), np.int16)
-    dev_coef = np.zeros((hc, done, 6144), np.int16)
-    dev_rec = np.zeros((hc, done, 6144), np.uint8)
-    dev_cost = np.zeros((hc, done), np.float64)
-    dev_bd = np.zeros((hc, done, 2), np.uint32)
-    seen = np.zeros(done, bool)
-    for pos, ct, rc in work.keep_steps:
-        if pos >= done or seen[pos]:
-            continue
-        c = ct.cpu().numpy().view(hm.HM_CTU).reshape(hc, work.ctus)
-        r = rc.cpu().numpy().reshape(hc, work.ctus, 6144)
-        for i in range(work.ctus):
-            if pos + i < done:
-                dev_parts[:, pos + i] = hm.unpack_parts(c[:, i]["p"])
-                dev_coef[:, pos + i] = c[:, i]["coef"]
-                dev_rec[:, pos + i] = r[:, i]
-                dev_cost[:, pos + i] = c[:, i]["cost"]
-                dev_bd[:, pos + i, 0], dev_bd[:, pos + i, 1] = c[:, i]["bits"], c[:, i]["dist"]
-                seen[pos + i] = True
-    mism, first = 0, []
-    for k in range(hc):
-        for i in range(done):
-            o = k * done + i
-            what = None
-            if not np.array_equal(out["parts"][o], dev_parts[k, i]):
-                d = np.argwhere(out["parts"][o] != dev_parts[k, i])
-                z, f = int(d[0][0]), int(d[0][1])
-                what = "part z=%d %s port=%d gpu=%d (%d fields differ)" % (z, hm.PART_FIELDS[f], out["parts"][o][z, f],
-                                                                          dev_parts[k, i][z, f], len(d))
-            elif not np.array_equal(out["coef"][o].astype(np.int16), dev_coef[k, i]):
-                what = "coef"
-            elif not np.array_equal(out["recon"][o], dev_rec[k, i]):
-                what = "recon"
-            elif out["cost"][o] != dev_cost[k, i] or not np.array_equal(out["bits_dist"][o], dev_bd[k, i]):
-                what = "totals port=(%s,%r) gpu=(%s,%r)" % (list(out["bits_dist"][o]), out["cost"][o], list(dev_bd[k, i]),
-                                                          dev_cost[k, i])
-            if what:
-                mism += 1
-                if len(first) < 4:
-                    first.append("row %d ctu %d: %s" % (k, i, what))
+    got = _kept_records(work, [set(range(done))] * hc)
+    mism, first = _compare_port(out, got, [(k, i) for k in range(hc) for i in range(done)])
     return {"value": round(n / dt, 3), "unit": "CTUs/s", "cores": threads, "kind": "port",
             "sample": f"picture 0's {hc} slice chains x {done} CTUs ({n} CTUs) through oracle/hvx_oracle_cu.c "
                       f"hvxo_hm_chains on {threads} host threads, {dt:.1f} s",
             "gpu_parity_ctus": n, "gpu_parity_mismatches": mism, "first_mismatches": first}
+
+
+def hm_merged_chain_parity(threads, W=256, H=176, nref=4, base_qp=32):
+    """The headline's chain layout to the end of a picture, which its timed window does not reach:
+    a small picture (W/64 CTUs per row, a 48-line partial bottom row) stepped by HmWorkload until
+    every chain is done -- the full rows, and the last full row's chain continuing into the partial
+    row through HVX_HM_SLICE_CTUS + HVX_HM_RESUME -- every CTU compared with the restatement."""
+    import torch
+    from oracle import hm_ctu
+    work = HmWorkload(W, H, 1, nref, base_qp, 1, rank=0)
+    out_rec = torch.zeros(work.slots * 6144, dtype=torch.uint8, device="cuda")
+    for _ in range(2 * work.wc):
+        work.step(out_rec)
+    torch.cuda.synchronize()
+    pi, pf, org, refs, col = work.host_inputs(0)
+    wc, rows = work.wc, work.rows
+    full = hm_ctu.chains(pi, pf, org, refs, work.entry, np.arange(rows - 1, dtype=np.int32) * wc, wc, wc, threads=threads,
+                         col_field=col)
+    last = hm_ctu.chains(pi, pf, org, refs, work.entry, np.array([(rows - 1) * wc], np.int32), 2 * wc, wc, threads=1,
+                         col_field=col)
+    port = {k: np.concatenate([full[k], last[k]]) for k in full}
+    positions = [set(range(wc))] * (rows - 1) + [set(range(2 * wc))]
+    got = _kept_records(work, positions)
+    order = [(k, i) for k in range(rows - 1) for i in range(wc)] + [(rows - 1, i) for i in range(2 * wc)]
+    mism, first = _compare_port(port, got, order)
+    del work, out_rec
+    torch.cuda.empty_cache()
+    return {"picture": f"{W}x{H}", "chains": rows, "ctus": len(order), "partial_row_ctus": wc,
+            "gpu_parity_mismatches": mism, "first_mismatches": first}
+
+
+def physical_cores():
+    """Physical cores of the host (unique (physical id, core id) pairs of /proc/cpuinfo)."""
+    cores, phys, core = set(), None, None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                core = line.split(":", 1)[1].strip()
+            elif not line.strip() and phys is not None and core is not None:
+                cores.add((phys, core))
+                phys = core = None
+        if phys is not None and core is not None:
+            cores.add((phys, core))
+    except OSError:
+        pass
+    return len(cores) or (os.cpu_count() or 1)
 
 
 def cpu_model():
@@ -532,7 +626,12 @@ def hm_cpu_reference(procs, tmpdir):
                       f"timed) of {REF_W}x{REF_H} random YUV, oracle/hm_ref_bench.cfg with one row per slice: POC "
                       f"{REF_POCS[0]}-{REF_POCS[-1]} ({len(REF_POCS) * (REF_W // 64) * (REF_H // 64)} whole CTUs per "
                       f"encode, P, QP 34, 4 refs) after a 5-frame pre-roll; {wall:.0f} s wall",
-            "s_per_ctu_per_core": round(s, 4), "cpu_model": cpu_model(), "cores_present": os.cpu_count()}
+            "s_per_ctu_per_core": round(s, 4), "cpu_model": cpu_model(), "cores_present": os.cpu_count(),
+            # the whole host at the measured per-core rate (an estimate: the job's CPU share is 16 threads,
+            # so all physical cores are not run here; shared caches / memory bandwidth are not modelled)
+            "whole_host_estimate": {"physical_cores": physical_cores(),
+                                    "ctus_per_s": round(physical_cores() / s, 1),
+                                    "basis": "physical_cores / s_per_ctu_per_core"}}
 
 
 def build_provenance():
@@ -661,6 +760,7 @@ def main():
                                                        os.environ.get("TMPDIR", "/tmp"))
             if not args.no_cpu:
                 port = hm_cpu_port(work, threads)
+                port["merged_chain"] = hm_merged_chain_parity(threads)
                 out["cpu_port"] = port
                 if out["cpu_baseline"] is None:
                     out["cpu_baseline"] = port

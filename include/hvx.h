@@ -349,6 +349,14 @@ int hvx_hm_compress(hvx_ctx *ctx, const hvx_hm_picture *d_pics, int n_pics, cons
 /* the status word of each of the last launch's jobs (0: ran; -HVX_HM_BAD_*: refused); synchronises
  * the context's stream */
 int hvx_hm_job_status(hvx_ctx *ctx, const void *d_state, int n_jobs, int32_t *h_status);
+/* The slice data of decided pictures: TEncSlice::encodeSlice's CTU loop
+ * (TEncSlice.cpp:920) through TEncBinCABAC -- per CTU the SAO syntax (TEncSbac::codeSAOBlkParam
+ * TEncSbac.cpp:1683) and TEncCu::encodeCtu (TEncCu.cpp:252: xEncodeCU :940, finishCU :885) -- one wave
+ * per slice (hvx_types.h hvx_hm_slice).  d_state = n_slices * hvx_hm_state_size() bytes of scratch;
+ * d_out = n_slices results.  The caller ends each slice as encodeSlice does: the terminating bin 1,
+ * TEncBinCABAC::finish (TEncBinCoderCABAC.cpp:81) and the byte alignment, from the result's registers. */
+int hvx_hm_write_slices(hvx_ctx *ctx, const hvx_hm_picture *d_pics, int n_pics, const hvx_hm_slice *d_slices,
+                        int n_slices, void *d_state, hvx_hm_slice_result *d_out);
 
 /* ---------------------------------------------------------------------------------------
  * The picture-level steps TEncGOP runs after compressSlice (TEncGOP.cpp:1465-1629), on a picture

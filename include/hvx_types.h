@@ -343,6 +343,33 @@ typedef struct hvx_hm_job {
  * while m_integerMv2Nx2N carries from CTU to CTU across the slice boundary, as in TAppEncoder --
  * where a slice whose first CTU is a picture-boundary CTU (the partial bottom row) reads it. */
 #define HVX_HM_SLICE_CTUS(n) ((int32_t)(n) << 16)
+
+/* One slice's data written by hvx_hm_write_slices (TEncSlice::encodeSlice, TEncSlice.cpp:920): CTUs
+ * first_ctu .. first_ctu + n_ctus - 1 (raster) of picture pic, whose ctus array holds the decided
+ * CTUs (hvx_hm_compress chained jobs, or a caller's TComDataCU data); each CTU's SAO syntax when
+ * sao_enabled (the slice's sao flags Y / Cb / Cr) from sao_coded ([ctu][3][8] of the picture, the
+ * layout of hvx_sao_decide_job.coded), then its CU syntax, from the slice-start context states
+ * `entry` (resetEntropy).  The completed bytes go to out (at most out_cap). */
+typedef struct hvx_hm_slice {
+  int32_t pic, first_ctu, n_ctus, out_cap;
+  int32_t sao_enabled[3], pad_;
+  const int32_t *sao_coded;
+  uint8_t *out;
+  hvx_hm_coder entry;
+} hvx_hm_slice;
+/* The writer's state after the slice's last CTU (before its terminating end_of_slice_segment_flag 1
+ * and TEncBinCABAC::finish, which the caller codes from these registers): TEncBinCABAC's m_uiLow,
+ * m_uiRange, m_bitsLeft, m_numBufferedBytes, m_bufferedByte, m_uiBinsCoded; the bytes written
+ * (n_bytes > out_cap: the output was truncated at out_cap); status 0, or -HVX_HM_BAD_* (nothing
+ * written); the context states after the slice and the models it coded (bit m % 32 of word m / 32). */
+typedef struct hvx_hm_slice_result {
+  uint32_t low, range;
+  int32_t bits_left, num_buffered;
+  uint32_t buffered_byte, bins;
+  int32_t n_bytes, status;
+  uint32_t coded[7], pad_;
+  uint8_t states[208];
+} hvx_hm_slice_result;
 #define HVX_HM_SLICE_CTUS_OF(flags) (((flags) >> 16) & 0x7fff)
 
 #ifdef __cplusplus

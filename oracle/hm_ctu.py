@@ -126,16 +126,16 @@ def compare(g, pic, out, verbose=True, slice_ctus=0):
 
 
 def chains(pic_i32, pic_f64, org, refpics, entry_states, chain_first, per_chain, slice_ctus, threads=1,
-           col_field=None):
-    """Independent SliceMode=1 slice chains through the restatement (hvxo_hm_chains): chain k decides
-    CTUs chain_first[k] .. + per_chain - 1 from entry_states.  Arrays as in replay(); outputs per
-    (chain, CTU)."""
+           col_field=None, rd_metric=0, lambda_ssim=0.0):
+    """Independent SliceMode=1 slice chains through the restatement (hvxo_hm_chains_rd): chain k decides
+    CTUs chain_first[k] .. + per_chain - 1 from entry_states; rd_metric 1: the SSIM cost (lambda_ssim)
+    in the CU decision.  Arrays as in replay(); outputs per (chain, CTU)."""
     L = _lib()
     if not getattr(L, "_hm_chains_bound", False):
         P = ctypes.c_void_p
-        L.hvxo_hm_chains.restype = ctypes.c_int
-        L.hvxo_hm_chains.argtypes = [P, P, P, P, ctypes.c_int, P, P, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
-                                     ctypes.c_int, P, P, P, P, P]
+        L.hvxo_hm_chains_rd.restype = ctypes.c_int
+        L.hvxo_hm_chains_rd.argtypes = [P, P, P, P, ctypes.c_int, P, P, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P, P, P, P]
         L._hm_chains_bound = True
     pi = np.ascontiguousarray(pic_i32, np.int32)
     pf = np.ascontiguousarray(pic_f64, np.float64)
@@ -146,11 +146,12 @@ def chains(pic_i32, pic_f64, org, refpics, entry_states, chain_first, per_chain,
            "bits_dist": np.zeros((n, 2), np.uint32)}
     refs = np.ascontiguousarray(refpics, np.uint8)
     nref = refs.size // (int(pi[0]) * int(pi[1]) * 3 // 2)
-    r = L.hvxo_hm_chains(_ptr(pi), _ptr(pf), _ptr(np.ascontiguousarray(org, np.uint8)), _ptr(refs), nref,
-                     _ptr(None if col_field is None else np.ascontiguousarray(col_field, np.int16)),
-                     _ptr(entropy_bits()), _ptr(np.ascontiguousarray(entry_states, np.uint8)), len(first), _ptr(first),
-                     per_chain, slice_ctus, threads, _ptr(out["parts"]), _ptr(out["coef"]), _ptr(out["recon"]),
-                     _ptr(out["cost"]), _ptr(out["bits_dist"]))
+    r = L.hvxo_hm_chains_rd(_ptr(pi), _ptr(pf), _ptr(np.ascontiguousarray(org, np.uint8)), _ptr(refs), nref,
+                            _ptr(None if col_field is None else np.ascontiguousarray(col_field, np.int16)),
+                            _ptr(entropy_bits()), _ptr(np.ascontiguousarray(entry_states, np.uint8)), len(first),
+                            _ptr(first), per_chain, slice_ctus, threads, int(rd_metric), float(lambda_ssim),
+                            _ptr(out["parts"]), _ptr(out["coef"]), _ptr(out["recon"]), _ptr(out["cost"]),
+                            _ptr(out["bits_dist"]))
     if r < 0:
         raise ValueError("hvxo_hm_chains rejected the chain layout")
     return out

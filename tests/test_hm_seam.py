@@ -68,6 +68,23 @@ def test_hm_encoder_with_hvx_seams(case, monkeypatch):
         assert m and int(m.group(1)) > 100000 and int(m.group(2)) == 0, log[0][-2000:]
 
 
+def slices_of(case):
+    """slices per encode: SliceMode=1 slices of SliceArgument CTUs, or one per picture"""
+    frames = mk.CASES[case][2]
+    w, h = mk.case_size(case)
+    ctus = ((w + 63) // 64) * ((h + 63) // 64)
+    extra = mk.CASES[case][6] if len(mk.CASES[case]) > 6 else []
+    arg = [int(a.split("=")[1]) for a in extra if a.startswith("--SliceArgument=")]
+    return frames * (-(-ctus // arg[0]) if arg else 1)
+
+
+def check_slice_seam(case, log):
+    """every slice of the encode was written by the device slice writer (hm_slice_seam.cpp ->
+    hvx_hm_write_slices): SAO + CU syntax through the device TEncBinCABAC, 0 fall-throughs"""
+    m = re.search(r"hm_slice_seam: (\d+) slices written by libhvx \((\d+) bytes\), (\d+) fell through", log)
+    assert m and int(m.group(1)) == slices_of(case) and int(m.group(2)) > 0 and int(m.group(3)) == 0, log[-2000:]
+
+
 def test_expected_md5_cases_present():
     assert set(EXPECTED) == set(mk.CASES)
 
@@ -86,6 +103,7 @@ def test_hm_encoder_with_cu_seam(case, monkeypatch):
     if not os.path.exists(EXE):
         pytest.skip("TAppEncoder_hvx not built (needs /root/reference at build time)")
     monkeypatch.setenv("HVX_SEAM_CU", "1")
+    monkeypatch.setenv("HVX_SEAM_SLICE", "1")
     monkeypatch.setenv("HVX_SEAM_INTRA", "0")
     log = []
     with tempfile.TemporaryDirectory() as tmp:
@@ -98,6 +116,7 @@ def test_hm_encoder_with_cu_seam(case, monkeypatch):
     ctus = ((w + 63) // 64) * ((h + 63) // 64)
     assert int(m.group(1)) == frames * ctus and int(m.group(2)) == frames and int(m.group(3)) == 0, m.group(0)
     assert got == EXPECTED[case], (case, got, EXPECTED[case])
+    check_slice_seam(case, log[0])
     # with every CTU decided on the device, HM's own motion search is never reached
     m = re.search(r"hm_me_seam: (\d+) xMotionEstimation calls served .* (\d+) fell through", log[0])
     assert m is None or (int(m.group(1)) == 0 and int(m.group(2)) == 0), m.group(0)
@@ -121,6 +140,7 @@ def test_hm_encoder_with_cu_seam_batched(case, monkeypatch):
         pytest.skip("TAppEncoder_hvx not built (needs /root/reference at build time)")
     monkeypatch.setenv("HVX_SEAM_CU", "1")
     monkeypatch.setenv("HVX_SEAM_CU_BATCH", "1")
+    monkeypatch.setenv("HVX_SEAM_SLICE", "1")
     monkeypatch.setenv("HVX_SEAM_INTRA", "0")
     log = []
     with tempfile.TemporaryDirectory() as tmp:
@@ -134,4 +154,5 @@ def test_hm_encoder_with_cu_seam_batched(case, monkeypatch):
     m = re.search(r"hm_cu_seam batched: (\d+) CTUs from (\d+) launches, (\d+) entry-state mismatches", log[0])
     assert m and int(m.group(1)) == frames * ctus and int(m.group(2)) == frames and int(m.group(3)) == 0, log[0][-2000:]
     assert got == EXPECTED[case], (case, got, EXPECTED[case])
+    check_slice_seam(case, log[0])
 

@@ -10,10 +10,96 @@
 
 #include "hvx_dev.hpp"
 #include "hvx_hm.hpp"
+#include "hvx_hmwrite.hpp"
 #include "hvx_host.hpp"
 #include "hvx_tables.hpp"
 
 using namespace hvxi;
+
+
+// hvx_hm_write_slices: one workgroup (one wave) per slice
+static __global__ __launch_bounds__(64) void k_hm_write_slices(const hvx_hm_picture *__restrict__ pics, int n_pics,
+                                                               const hvx_hm_slice *__restrict__ slices, int n_slices,
+                                                               char *state_base, size_t state_bytes,
+                                                               hvx_hm_slice_result *__restrict__ res) {
+  using namespace hm;
+  const int jid = blockIdx.x;
+  if (jid >= n_slices) return;
+  const int l = threadIdx.x;
+  const hvx_hm_slice &j = slices[jid];
+  hvx_hm_slice_result *o = &res[jid];
+  int bad = 0;
+  if (j.pic < 0 || j.pic >= n_pics) bad = HVX_HM_BAD_PIC;
+  else {
+    const hvx_hm_picture &P = pics[j.pic];
+    const int n = P.w_ctus * P.h_ctus;
+    if (P.w <= 0 || P.h <= 0 || (P.w & 7) || (P.h & 7) || P.w_ctus != (P.w + 63) / 64 || P.h_ctus != (P.h + 63) / 64 ||
+        !P.ctus)
+      bad = HVX_HM_BAD_GEOMETRY;
+    else if (j.first_ctu < 0 || j.n_ctus < 1 || j.first_ctu + j.n_ctus > n) bad = HVX_HM_BAD_CTUS;
+    else if (!j.out || j.out_cap < 0 || ((j.sao_enabled[0] | j.sao_enabled[1] | j.sao_enabled[2]) && !j.sao_coded))
+      bad = HVX_HM_BAD_OUT;
+  }
+  if (bad) {
+    if (l == 0) o->status = -bad;
+    return;
+  }
+  State *S = (State *)(state_base + (size_t)jid * state_bytes);
+  copy_words(&hm_e.P, &pics[j.pic], (int)sizeof(hvx_hm_picture));
+  wsync();
+  for (int i = l; i < 128; i += 64) {
+    hm_e.eb[i] = hm_e.P.entropy_bits ? hm_e.P.entropy_bits[i] : 0;
+    const int p = i >> 1, mps = i & 1;
+    hm_e.next[i * 2 + mps] = (uint8_t)(((p < 62 ? p + 1 : p) << 1) | mps);
+    hm_e.next[i * 2 + (mps ^ 1)] = (uint8_t)((cab::kTransIdxLps[p] << 1) | (p == 0 ? mps ^ 1 : mps));
+  }
+  hm_e.S = S;
+  if (l < 4) hm_e.dbg[l] = 0;
+  hm_e.stage = 0;
+  hm_e.stop = 0;
+  hm_e.tsp = 0;
+  hm_e.slice_start = j.first_ctu;
+  hm_e.slice_end = j.first_ctu + j.n_ctus - 1;
+  hm_e.slice_qp = hm_e.P.qp;
+  for (int d = 0; d < 4; d++) {
+    hm_e.best[d] = d;
+    hm_e.temp[d] = 4 + d;
+    for (int k = 0; k < 7; k++) hm_e.yi[k][d] = k * 4 + d;
+  }
+  // TEncBinCABAC::start() and the slice-start contexts
+  hm_w.low = 0; hm_w.range = 510; hm_w.bits_left = 23; hm_w.nbuf = 0; hm_w.buffered = 0xff; hm_w.bins = 0;
+  hm_w.nout = 0; hm_w.cap = j.out_cap; hm_w.out = j.out;
+  if (l < 7) hm_w.coded[l] = 0;
+  for (int i = l; i < HVX_NUM_CTX; i += 64) hm_w.st[i] = j.entry.st[i];
+  wsync();
+  const int sao = j.sao_enabled[0] | j.sao_enabled[1] | j.sao_enabled[2];
+  const int en[3] = {j.sao_enabled[0], j.sao_enabled[1], j.sao_enabled[2]};
+  for (int k = 0; k < j.n_ctus; k++) {
+    const int addr = j.first_ctu + k;
+    hm_e.ctu_addr = addr;
+    hm_e.ctu_x = addr % hm_e.P.w_ctus;
+    hm_e.ctu_y = addr / hm_e.P.w_ctus;
+    // the CTU's data (TComPic::getCtu): the current CTU's partitions and its depth-0 view
+    const hvx_hm_ctu *src = &hm_e.P.ctus[addr];
+    Cu *v = &S->view;
+    wsync();
+    v->depth = 0; v->zidx = 0; v->width = 64; v->nparts = 256;
+    v->x = hm_e.ctu_x * 64; v->y = hm_e.ctu_y * 64;
+    copy_words(S->ctu_p, src->p, (int)sizeof(Part) * 256);
+    copy_words(v->p, src->p, (int)sizeof(Part) * 256);
+    copy_words(v->coef, src->coef, 2 * 6144);
+    wsync();
+    if (sao) write_sao(j.sao_coded, en, addr, j.first_ctu);
+    write_cu<0>(0, addr == hm_e.slice_end);
+  }
+  wsync();
+  if (l == 0) {
+    o->low = hm_w.low; o->range = hm_w.range; o->bits_left = hm_w.bits_left; o->num_buffered = hm_w.nbuf;
+    o->buffered_byte = hm_w.buffered; o->bins = hm_w.bins; o->n_bytes = hm_w.nout; o->status = 0; o->pad_ = 0;
+  }
+  if (l < 7) o->coded[l] = hm_w.coded[l];
+  for (int i = l; i < 208; i += 64) o->states[i] = i < HVX_NUM_CTX ? hm_w.st[i] : 0;
+}
 
 int hvx_hm_module_init() { return upload_tables(); }
 
@@ -59,6 +145,18 @@ int hvx_hm_job_status(hvx_ctx *ctx, const void *d_state, int n_jobs, int32_t *h_
       hipStreamSynchronize(ctx->stream) != hipSuccess)
     return fail(HVX_E_HIP, "hvx_hm_job_status: copy failed");
   return HVX_OK;
+}
+
+int hvx_hm_write_slices(hvx_ctx *ctx, const hvx_hm_picture *d_pics, int n_pics, const hvx_hm_slice *d_slices,
+                        int n_slices, void *d_state, hvx_hm_slice_result *d_out) {
+  if (!ctx || !d_pics || n_pics < 1 || !d_slices || n_slices < 0 || !d_state || !d_out)
+    return fail(HVX_E_INVALID, "hvx_hm_write_slices: bad args");
+  if (n_slices == 0) return HVX_OK;
+  size_t sb = 0;
+  hvx_hm_state_size(&sb);
+  hipLaunchKernelGGL(k_hm_write_slices, dim3(n_slices), dim3(64), 0, ctx->stream, d_pics, n_pics, d_slices, n_slices,
+                     (char *)d_state, sb, d_out);
+  return launched("k_hm_write_slices");
 }
 
 }  // extern "C"

@@ -47,7 +47,8 @@ constexpr int DM_CHROMA_IDX = 36;
 // context offsets in TEncSbac::m_contextModels (TEncSbac.cpp:62-92)
 enum {
   X_SPLIT = 0, X_SKIP = 3, X_MERGE_FLAG = 6, X_MERGE_IDX = 7, X_PART = 8, X_PRED = 12, X_INTRA = 13, X_CHROMA = 14,
-  X_INTER_DIR = 19, X_REF = 24, X_MVD = 26, X_QT_CBF = 28, X_SUBDIV = 38, X_ROOT_CBF = 41, X_MVP = 180
+  X_INTER_DIR = 19, X_REF = 24, X_MVD = 26, X_QT_CBF = 28, X_SUBDIV = 38, X_ROOT_CBF = 41, X_MVP = 180,
+  X_SAO_MERGE = 181, X_SAO_TYPE = 182
 };
 constexpr int GOON = 36;  // m_pcRDGoOnSbacCoder; rd coders are d * 6 + ci
 __device__ __forceinline__ int RD(int d, int ci) { return d * CI_NUM + ci; }
@@ -742,164 +743,210 @@ __device__ void cu_sane(const Cu *cu, int code) {
 #endif
 
 // ============================================================================================
-// Syntax elements counted by TEncBinCABACCounter (TEncSbac.cpp:427-1104)
+// Syntax elements (TEncSbac.cpp:427-1104) on a bin sink: the RD counter of the decision
+// (CountSink: TEncBinCABACCounter on E.cod[E.cur], only the number of bypass bins matters) or the
+// slice writer (hvx_hmwrite.hpp: TEncBinCABAC, the bypass bins' values written msb first)
 // ============================================================================================
-__device__ void code_split_flag(const Cu *cu, int rel, int depth) {
+struct CountSink {
+  static constexpr bool kValues = false;  // the bypass bins' values are not needed
+  __device__ __forceinline__ void bin(int ctx, int v) const { cbin(ctx, v); }
+  __device__ __forceinline__ void eps(uint32_t, int n) const { cep(n); }
+  __device__ __forceinline__ void trm(int v) const { ctrm(v); }
+};
+template <class K = CountSink>
+__device__ void code_split_flag(const Cu *cu, int rel, int depth, K k = K()) {
   if (depth == 3) return;
   const Nb l = get_pu_left(cu, cu->zidx + rel), a = get_pu_above(cu, cu->zidx + rel, 0);
   const int ctx = (l.valid && l.p[l.idx].depth > depth) + (a.valid && a.p[a.idx].depth > depth);
-  cbin(X_SPLIT + ctx, cu->p[rel].depth > depth);
+  k.bin(X_SPLIT + ctx, cu->p[rel].depth > depth);
 }
-__device__ void code_skip_flag(const Cu *cu, int rel) {
+template <class K = CountSink>
+__device__ void code_skip_flag(const Cu *cu, int rel, K k = K()) {
   if (E.P.slice_type == I_SLICE) return;
   const Nb l = get_pu_left(cu, cu->zidx + rel), a = get_pu_above(cu, cu->zidx + rel, 0);
   const int ctx = (l.valid && l.p[l.idx].skip) + (a.valid && a.p[a.idx].skip);
-  cbin(X_SKIP + ctx, cu->p[rel].skip ? 1 : 0);
+  k.bin(X_SKIP + ctx, cu->p[rel].skip ? 1 : 0);
 }
-__device__ void code_merge_index(const Cu *cu, int rel) {
+template <class K = CountSink>
+__device__ void code_merge_index(const Cu *cu, int rel, K k = K()) {
   const int idx = cu->p[rel].merge_idx, n = E.P.max_merge;
   if (n > 1)
     for (int i = 0; i < n - 1; i++) {
       const int sym = i == idx ? 0 : 1;
-      if (i == 0) cbin(X_MERGE_IDX, sym);
-      else cep(1);
+      if (i == 0) k.bin(X_MERGE_IDX, sym);
+      else k.eps((uint32_t)sym, 1);
       if (!sym) break;
     }
 }
-__device__ void code_pred_mode(const Cu *cu, int rel) {
+template <class K = CountSink>
+__device__ void code_pred_mode(const Cu *cu, int rel, K k = K()) {
   if (E.P.slice_type == I_SLICE) return;
-  cbin(X_PRED, cu->p[rel].pred == MODE_INTRA);
+  k.bin(X_PRED, cu->p[rel].pred == MODE_INTRA);
 }
-__device__ void code_part_size(const Cu *cu, int rel, int depth) {
+template <class K = CountSink>
+__device__ void code_part_size(const Cu *cu, int rel, int depth, K k = K()) {
   const int ps = cu->p[rel].part;
   if (cu->p[rel].pred == MODE_INTRA) {
-    if (depth == 3) cbin(X_PART + 0, ps == SIZE_2Nx2N);
+    if (depth == 3) k.bin(X_PART + 0, ps == SIZE_2Nx2N);
     return;
   }
   const int amp = E.P.amp && depth < 3;
   switch (ps) {
-    case SIZE_2Nx2N: cbin(X_PART + 0, 1); break;
+    case SIZE_2Nx2N: k.bin(X_PART + 0, 1); break;
     case SIZE_2NxN: case SIZE_2NxnU: case SIZE_2NxnD:
-      cbin(X_PART + 0, 0);
-      cbin(X_PART + 1, 1);
+      k.bin(X_PART + 0, 0);
+      k.bin(X_PART + 1, 1);
       if (amp) {
-        if (ps == SIZE_2NxN) cbin(X_PART + 3, 1);
-        else { cbin(X_PART + 3, 0); cep(1); }
+        if (ps == SIZE_2NxN) k.bin(X_PART + 3, 1);
+        else { k.bin(X_PART + 3, 0); k.eps(ps == SIZE_2NxnU ? 0u : 1u, 1); }
       }
       break;
     case SIZE_Nx2N: case SIZE_nLx2N: case SIZE_nRx2N:
-      cbin(X_PART + 0, 0);
-      cbin(X_PART + 1, 0);
-      if (depth == 3 && cu->p[rel].width != 8) cbin(X_PART + 2, 1);
+      k.bin(X_PART + 0, 0);
+      k.bin(X_PART + 1, 0);
+      if (depth == 3 && cu->p[rel].width != 8) k.bin(X_PART + 2, 1);
       if (amp) {
-        if (ps == SIZE_Nx2N) cbin(X_PART + 3, 1);
-        else { cbin(X_PART + 3, 0); cep(1); }
+        if (ps == SIZE_Nx2N) k.bin(X_PART + 3, 1);
+        else { k.bin(X_PART + 3, 0); k.eps(ps == SIZE_nLx2N ? 0u : 1u, 1); }
       }
       break;
     case SIZE_NxN:
-      if (depth == 3 && cu->p[rel].width != 8) { cbin(X_PART + 0, 0); cbin(X_PART + 1, 0); cbin(X_PART + 2, 0); }
+      if (depth == 3 && cu->p[rel].width != 8) { k.bin(X_PART + 0, 0); k.bin(X_PART + 1, 0); k.bin(X_PART + 2, 0); }
       break;
     default: break;
   }
 }
-// getIntraDirPredictor (TComDataCU.cpp:1401): the predictor index of dir, -1 when not an MPM
-__device__ int intra_mpm_index(const Cu *cu, int rel, int dir) {
+// getIntraDirPredictor (TComDataCU.cpp:1401): the three most probable luma modes of a PU
+__device__ void intra_mpm_list(const Cu *cu, int rel, int p[3]) {
   const Nb l = get_pu_left(cu, cu->zidx + rel), a = get_pu_above(cu, cu->zidx + rel, 1);
   const int ld = (l.valid && l.p[l.idx].pred == MODE_INTRA) ? l.p[l.idx].idir[0] : 1;
   const int ad = (a.valid && a.p[a.idx].pred == MODE_INTRA) ? a.p[a.idx].idir[0] : 1;
-  int p0, p1, p2;
   if (ld == ad) {
-    if (ld > 1) { p0 = ld; p1 = ((ld + 29) % 32) + 2; p2 = ((ld - 1) % 32) + 2; }
-    else { p0 = 0; p1 = 1; p2 = 26; }
+    if (ld > 1) { p[0] = ld; p[1] = ((ld + 29) % 32) + 2; p[2] = ((ld - 1) % 32) + 2; }
+    else { p[0] = 0; p[1] = 1; p[2] = 26; }
   } else {
-    p0 = ld; p1 = ad;
-    p2 = (ld && ad) ? 0 : ((ld + ad) < 2 ? 26 : 1);
+    p[0] = ld; p[1] = ad;
+    p[2] = (ld && ad) ? 0 : ((ld + ad) < 2 ? 26 : 1);
   }
-  int idx = -1;
-  if (dir == p0) idx = 0;
-  if (dir == p1) idx = 1;
-  if (dir == p2) idx = 2;
-  return idx;
 }
-// codeIntraDirLumaAng (:643)
-__device__ void code_intra_dir_luma(const Cu *cu, int rel, int multiple) {
+// codeIntraDirLumaAng (:643): the MPM flags of the PUs, then per PU the MPM index (truncated
+// unary, bypass) or the 5-bit remaining mode (the MPMs sorted and stepped over)
+template <class K = CountSink>
+__device__ void code_intra_dir_luma(const Cu *cu, int rel, int multiple, K k = K()) {
   const int npu = (multiple && cu->p[rel].part == SIZE_NxN) ? 4 : 1;
   const int off = (256 >> (2 * cu->p[rel].depth)) >> 2;
-  int pidx0 = -1, pidx1 = -1, pidx2 = -1, pidx3 = -1;
+  int pidx[4] = {-1, -1, -1, -1}, rem[4] = {0, 0, 0, 0};
   for (int j = 0; j < npu; j++) {
-    const int pi = intra_mpm_index(cu, rel + off * j, cu->p[rel + off * j].idir[0]);
-    if (j == 0) pidx0 = pi; else if (j == 1) pidx1 = pi; else if (j == 2) pidx2 = pi; else pidx3 = pi;
-    cbin(X_INTRA, pi != -1);
+    int p[3];
+    intra_mpm_list(cu, rel + off * j, p);
+    int dir = cu->p[rel + off * j].idir[0], pi = -1;
+    for (int i = 0; i < 3; i++)
+      if (dir == p[i]) pi = i;
+    if (K::kValues && pi < 0) {
+      if (p[0] > p[1]) { const int t = p[0]; p[0] = p[1]; p[1] = t; }
+      if (p[0] > p[2]) { const int t = p[0]; p[0] = p[2]; p[2] = t; }
+      if (p[1] > p[2]) { const int t = p[1]; p[1] = p[2]; p[2] = t; }
+      for (int i = 2; i >= 0; i--) dir = dir > p[i] ? dir - 1 : dir;
+      rem[j] = dir;
+    }
+    pidx[j] = pi;
+    k.bin(X_INTRA, pi != -1);
   }
   for (int j = 0; j < npu; j++) {
-    const int pi = j == 0 ? pidx0 : j == 1 ? pidx1 : j == 2 ? pidx2 : pidx3;
-    if (pi != -1) cep(pi ? 2 : 1);
-    else cep(5);
+    if (pidx[j] != -1) {
+      if (pidx[j]) k.eps(2u | (uint32_t)(pidx[j] - 1), 2);
+      else k.eps(0u, 1);
+    } else k.eps((uint32_t)rem[j], 5);
   }
 }
-__device__ void code_intra_dir_chroma(const Cu *cu, int rel) {
-  if (cu->p[rel].idir[1] == DM_CHROMA_IDX) cbin(X_CHROMA, 0);
-  else { cbin(X_CHROMA, 1); cep(2); }
+// codeIntraDirChroma (:700): DM, or the index among getAllowedChromaDir's first four
+template <class K = CountSink>
+__device__ void code_intra_dir_chroma(const Cu *cu, int rel, K k = K()) {
+  const int dc = cu->p[rel].idir[1];
+  if (dc == DM_CHROMA_IDX) { k.bin(X_CHROMA, 0); return; }
+  k.bin(X_CHROMA, 1);
+  int sym = 0;
+  if constexpr (K::kValues) {
+    const int lm = cu->p[rel].idir[0];
+    int allowed[4] = {0, 26, 10, 1};
+    for (int i = 0; i < 4; i++)
+      if (allowed[i] == lm) { allowed[i] = 34; break; }
+    for (int i = 0; i < 4; i++)
+      if (dc == allowed[i]) { sym = i; break; }
+  }
+  k.eps((uint32_t)sym, 2);
 }
-__device__ void code_ref_idx(const Cu *cu, int rel, int list) {
+template <class K = CountSink>
+__device__ void code_ref_idx(const Cu *cu, int rel, int list, K k = K()) {
   int r = cu->p[rel].ref[list];
-  cbin(X_REF + 0, r == 0 ? 0 : 1);
+  k.bin(X_REF + 0, r == 0 ? 0 : 1);
   if (r > 0) {
     const int n = E.P.nref[list] - 2;
     r--;
     for (int i = 0; i < n; i++) {
       const int sym = i == r ? 0 : 1;
-      if (i == 0) cbin(X_REF + 1, sym);
-      else cep(1);
+      if (i == 0) k.bin(X_REF + 1, sym);
+      else k.eps((uint32_t)sym, 1);
       if (!sym) break;
     }
   }
 }
-__device__ __forceinline__ int ep_exgolomb_bins(uint32_t sym, int k) {
+// xWriteEpExGolomb (TEncSbac.cpp:307): the k-th order Exp-Golomb code of sym as one bypass string
+template <class K>
+__device__ __forceinline__ void ep_exgolomb(uint32_t sym, int count, K k) {
+  uint32_t bins = 0;
   int n = 0;
-  while (sym >= (1u << k)) { n++; sym -= 1u << k; k++; }
-  return n + 1 + k;
+  while (sym >= (1u << count)) { bins = 2 * bins + 1; n++; sym -= 1u << count; count++; }
+  bins = 2 * bins;
+  n++;
+  bins = (bins << count) | sym;
+  n += count;
+  k.eps(bins, n);
 }
-__device__ void code_mvd(const Cu *cu, int rel, int list) {
+template <class K = CountSink>
+__device__ void code_mvd(const Cu *cu, int rel, int list, K k = K()) {
   if (E.P.mvd_l1_zero && list == 1 && cu->p[rel].inter_dir == 3) return;  // TEncSbac.cpp:781
   const int h = cu->p[rel].mvd[list][0], v = cu->p[rel].mvd[list][1];
-  cbin(X_MVD + 0, h != 0);
-  cbin(X_MVD + 0, v != 0);
+  k.bin(X_MVD + 0, h != 0);
+  k.bin(X_MVD + 0, v != 0);
   const int ah = abs(h), av = abs(v);
-  if (h) cbin(X_MVD + 1, ah > 1);
-  if (v) cbin(X_MVD + 1, av > 1);
-  if (h) { if (ah > 1) cep(ep_exgolomb_bins((uint32_t)(ah - 2), 1)); cep(1); }
-  if (v) { if (av > 1) cep(ep_exgolomb_bins((uint32_t)(av - 2), 1)); cep(1); }
+  if (h) k.bin(X_MVD + 1, ah > 1);
+  if (v) k.bin(X_MVD + 1, av > 1);
+  if (h) { if (ah > 1) ep_exgolomb((uint32_t)(ah - 2), 1, k); k.eps(h < 0 ? 1u : 0u, 1); }
+  if (v) { if (av > 1) ep_exgolomb((uint32_t)(av - 2), 1, k); k.eps(v < 0 ? 1u : 0u, 1); }
 }
-__device__ void code_inter_dir(const Cu *cu, int rel) {
+template <class K = CountSink>
+__device__ void code_inter_dir(const Cu *cu, int rel, K k = K()) {
   const int d = cu->p[rel].inter_dir - 1, ctx = cu->p[rel].depth;
-  if (cu->p[rel].part == SIZE_2Nx2N || cu->p[rel].width != 8) cbin(X_INTER_DIR + ctx, d == 2);
-  if (d < 2) cbin(X_INTER_DIR + 4, d);
+  if (cu->p[rel].part == SIZE_2Nx2N || cu->p[rel].width != 8) k.bin(X_INTER_DIR + ctx, d == 2);
+  if (d < 2) k.bin(X_INTER_DIR + 4, d);
 }
-__device__ void encode_pu_wise(const Cu *cu, int rel) {
+template <class K = CountSink>
+__device__ void encode_pu_wise(const Cu *cu, int rel, K k = K()) {
   const int ps = cu->p[rel].part, npu = num_parts_of(ps);
   const int off16 = ps == 0 ? 0 : ps == 1 ? 8 : ps == 2 ? 4 : ps == 3 ? 4 : ps == 4 ? 2 : ps == 5 ? 10 : ps == 6 ? 1 : 5;
   const int puoff = (off16 << ((4 - cu->p[rel].depth) << 1)) >> 4;
   for (int pu = 0, sub = rel; pu < npu; pu++, sub += puoff) {
-    cbin(X_MERGE_FLAG, cu->p[sub].merge ? 1 : 0);
-    if (cu->p[sub].merge) code_merge_index(cu, sub);
+    k.bin(X_MERGE_FLAG, cu->p[sub].merge ? 1 : 0);
+    if (cu->p[sub].merge) code_merge_index(cu, sub, k);
     else {
-      if (E.P.slice_type == B_SLICE) code_inter_dir(cu, sub);
+      if (E.P.slice_type == B_SLICE) code_inter_dir(cu, sub, k);
       for (int l = 0; l < 2; l++)
         if (E.P.nref[l] > 0) {
           const int dir = cu->p[sub].inter_dir;
-          if (E.P.nref[l] != 1 && (dir & (1 << l))) code_ref_idx(cu, sub, l);
-          if (dir & (1 << l)) code_mvd(cu, sub, l);
-          if (dir & (1 << l)) cbin(X_MVP, cu->p[sub].mvp_idx[l] ? 1 : 0);
+          if (E.P.nref[l] != 1 && (dir & (1 << l))) code_ref_idx(cu, sub, l, k);
+          if (dir & (1 << l)) code_mvd(cu, sub, l, k);
+          if (dir & (1 << l)) k.bin(X_MVP, cu->p[sub].mvp_idx[l] ? 1 : 0);
         }
     }
   }
 }
-__device__ void encode_pred_info(const Cu *cu, int rel) {
+template <class K = CountSink>
+__device__ void encode_pred_info(const Cu *cu, int rel, K k = K()) {
   if (cu->p[rel].pred == MODE_INTRA) {
-    code_intra_dir_luma(cu, rel, 1);
-    code_intra_dir_chroma(cu, rel);
-  } else encode_pu_wise(cu, rel);
+    code_intra_dir_luma(cu, rel, 1, k);
+    code_intra_dir_chroma(cu, rel, k);
+  } else encode_pu_wise(cu, rel, k);
 }
 
 // ============================================================================================
@@ -978,13 +1025,14 @@ __device__ int qt_min_log2(const Cu *cu, int rel) {
   const int m = l2 - (3 - 1 + isplit);
   return m > 5 ? 5 : m;
 }
-__device__ void code_qt_cbf(const Cu *cu, const Tu &t, int comp, int lowest) {
+template <class K = CountSink>
+__device__ void code_qt_cbf(const Cu *cu, const Tu &t, int comp, int lowest, K k = K()) {
   const int ch = comp ? 1 : 0;
   const int depth = tu_depth_rel(t);
   const int ctx = ch ? depth : (depth == 0 ? 1 : 0);
   const int can_split = t.w[comp] >= 8 && t.h[comp] >= 8;
   const int lowest_depth = depth + ((!lowest && !can_split) ? 1 : 0);
-  cbin(X_QT_CBF + ch * 5 + ctx, cbf_at(&cu->p[tu_abs_rel_c(t, comp)], comp, lowest_depth));
+  k.bin(X_QT_CBF + ch * 5 + ctx, cbf_at(&cu->p[tu_abs_rel_c(t, comp)], comp, lowest_depth));
 }
 __device__ void code_qt_cbf_zero(const Tu &t, int ch) {
   const int depth = tu_depth_rel(t);
