@@ -119,10 +119,14 @@ typedef struct hvx_me_result {
 } hvx_me_result;
 
 /* CU-level distortion of the HM engine's mode / split comparisons (hvx_hm_picture.rd_metric):
- * HVX_RD_SSE = HM's calcRdCost(bits, SSE); HVX_RD_SSIM = the stvssim encoder's SSIM cost (SURVEY 8(a)
- * a20-a22, BASELINE config 4; see hvx_hm_picture). */
+ * HVX_RD_SSE = HM's calcRdCost(bits, SSE); HVX_RD_SSIM = the stvssim encoder's distortionSSIM cost,
+ * HVX_RD_STVSSIM = its active distortionstVSSIM cost (BASELINE config 4; see
+ * hvx_hm_picture). */
 #define HVX_RD_SSE 0
 #define HVX_RD_SSIM 1
+#define HVX_RD_STVSSIM 2
+/* HVX_RD_STVSSIM: the most previous pictures of the stVSSIM history (REFNUM 26 - 1, att_stv.h) */
+#define HVX_STV_HIST 25
 
 /* One intra block: TComPrediction::initIntraPatternChType's reference
  * samples (TComPattern.cpp:115-360: fillReferenceSamples :364 substitution + the [1 2 1] /
@@ -316,6 +320,21 @@ typedef struct hvx_hm_picture {
    * estimation, RQT and RDOQ keep HM's SSE / SATD costs in both. */
   int32_t rd_metric, pad3_;
   double lambda_ssim;
+  /* HVX_RD_STVSSIM (distortionstVSSIM, stvssim.c:831-855, active by att_stv.h:5 / rdopt.c:223):
+   * D of a CU = the sum over its 16x16 luma areas (one JM macroblock each, raster order) of
+   * (1 - stVSSIM_Y) + (1 - stVSSIM_Cb) + (1 - stVSSIM_Cr) (WeightY/Cb/Cr 1, encoder.cfg:289-291),
+   * compute_stVSSIM (:587) over the area's 16x16 luma (8x8 windows stepped by SSIMOverlapSize 4,
+   * encoder.cfg:280) and 8x8 Cb, Cr blocks; an 8x8 CU is one 8x8 luma window + 4x4 chroma windows,
+   * weighted 1/4.  The 3-D terms read the co-located samples of hist_n (<= HVX_STV_HIST) previous
+   * pictures in coding order, most recent first (storeRefAndEncFrames :362, img->number + 1 frames
+   * with the current one): hist[6k + c] = picture k's original component c, hist[6k + 3 + c] = its
+   * final reconstruction, 8-bit, strides hist_stride[0] (luma) / [1] (chroma) -- Cr's history is read
+   * from the Cb planes, as compute_stVSSIM is called with comp 1 for both chroma components (:846,
+   * :850).  dirs: the direction map (pic_directions2: orientation in radians, one float per 4x4
+   * luma block, dirs_stride floats per row of blocks; getDirection_macroblock :1369). */
+  const uint8_t *const *hist;
+  const float *dirs;
+  int32_t hist_n, dirs_stride, hist_stride[2];
 } hvx_hm_picture;
 
 /* One chain of CTUs decided in raster order by one wave: CTUs first_ctu .. first_ctu+n_ctus-1 of

@@ -33,12 +33,39 @@ def _lib():
         L.hvxo_hm_replay_picture_rd.restype = ctypes.c_int
         L.hvxo_hm_replay_picture_rd.argtypes = [P, P, P, P, P, ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
                                                 ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P, P, P, P, P, P]
+        L.hvxo_hm_replay_picture_stv.restype = ctypes.c_int
+        L.hvxo_hm_replay_picture_stv.argtypes = [P, P, P, P, P, ctypes.c_int, P, P, P, P, P, P, P, P, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P, P, P, P, P, P, P]
         L._hm_ctu_bound = True
     return L
 
 
 def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+class Stv(ctypes.Structure):
+    """hvxo_stv (hvx_oracle_cu.h): the stVSSIM history and direction map of rd_metric 2."""
+    _fields_ = [("hist", ctypes.c_void_p), ("hist_n", ctypes.c_int), ("hist_stride", ctypes.c_int * 2),
+                ("dirs", ctypes.c_void_p), ("dirs_stride", ctypes.c_int)]
+
+
+def stv_struct(hist, dirs):
+    """(hvxo_stv, keep-alive list) from hist = [(org Y, Cb, Cr, rec Y, Cb, Cr) uint8 planes of the previous
+    pictures, most recent first] and dirs = float32 [h/4, w/4] (or None)."""
+    keep = [np.ascontiguousarray(p, np.uint8) for fr in hist for p in fr]
+    ptrs = (ctypes.c_void_p * max(1, len(keep)))(*[k.ctypes.data for k in keep])
+    st = Stv()
+    st.hist = ctypes.cast(ptrs, ctypes.c_void_p)
+    st.hist_n = len(hist)
+    if hist:
+        st.hist_stride[0], st.hist_stride[1] = keep[0].shape[1], keep[1].shape[1]
+    if dirs is not None:
+        d = np.ascontiguousarray(dirs, np.float32)
+        keep.append(d)
+        st.dirs, st.dirs_stride = d.ctypes.data, d.shape[1]
+    keep.append(ptrs)
+    return st, keep
 
 
 def entropy_bits():
@@ -50,9 +77,10 @@ def load(path):
     return golden_io.load(path)
 
 
-def replay(g, pic, mode=0, slice_ctus=0, rd_metric=0, lambda_ssim=0.0):
+def replay(g, pic, mode=0, slice_ctus=0, rd_metric=0, lambda_ssim=0.0, stv=None):
     """Replay picture `pic` of capture g; returns a dict of the restatement's per-CTU outputs.
-    rd_metric 1: the CU decision compares the stvssim SSIM cost (lambda_ssim) instead of HM's."""
+    rd_metric 1 / 2: the CU decision compares the stvssim SSIM / stVSSIM cost (lambda_ssim) instead of
+    HM's; stv = (hist, dirs) of rd_metric 2 (stv_struct)."""
     L = _lib()
     pi = np.ascontiguousarray(g["pic_i32"][pic], np.int32)
     pf = np.ascontiguousarray(g["pic_f64"][pic], np.float64)
@@ -80,11 +108,14 @@ def replay(g, pic, mode=0, slice_ctus=0, rd_metric=0, lambda_ssim=0.0):
            "bits_dist": np.zeros((n, 2), np.uint32), "states": np.zeros((n, 202), np.uint8),
            "frac": np.zeros(n, np.int64)}
     eb = entropy_bits()
-    L.hvxo_hm_replay_picture_rd(_ptr(pi), _ptr(pf), _ptr(org), _ptr(refs), _ptr(np.ascontiguousarray(g["refpic_poc"])),
-                                nref, _ptr(col), _ptr(eb), _ptr(states), _ptr(frac), _ptr(int2n), _ptr(hparts),
-                                _ptr(hcoef), _ptr(hrec), mode, slice_ctus, int(rd_metric), float(lambda_ssim),
-                                _ptr(out["parts"]), _ptr(out["coef"]), _ptr(out["recon"]), _ptr(out["cost"]),
-                                _ptr(out["bits_dist"]), _ptr(out["states"]), _ptr(out["frac"]))
+    st, keep = stv_struct(*stv) if stv is not None else (None, None)
+    L.hvxo_hm_replay_picture_stv(_ptr(pi), _ptr(pf), _ptr(org), _ptr(refs), _ptr(np.ascontiguousarray(g["refpic_poc"])),
+                                 nref, _ptr(col), _ptr(eb), _ptr(states), _ptr(frac), _ptr(int2n), _ptr(hparts),
+                                 _ptr(hcoef), _ptr(hrec), mode, slice_ctus, int(rd_metric), float(lambda_ssim),
+                                 ctypes.addressof(st) if st is not None else None,
+                                 _ptr(out["parts"]), _ptr(out["coef"]), _ptr(out["recon"]), _ptr(out["cost"]),
+                                 _ptr(out["bits_dist"]), _ptr(out["states"]), _ptr(out["frac"]))
+    del keep
     return out
 
 
@@ -126,16 +157,16 @@ def compare(g, pic, out, verbose=True, slice_ctus=0):
 
 
 def chains(pic_i32, pic_f64, org, refpics, entry_states, chain_first, per_chain, slice_ctus, threads=1,
-           col_field=None, rd_metric=0, lambda_ssim=0.0):
-    """Independent SliceMode=1 slice chains through the restatement (hvxo_hm_chains_rd): chain k decides
-    CTUs chain_first[k] .. + per_chain - 1 from entry_states; rd_metric 1: the SSIM cost (lambda_ssim)
-    in the CU decision.  Arrays as in replay(); outputs per (chain, CTU)."""
+           col_field=None, rd_metric=0, lambda_ssim=0.0, stv=None):
+    """Independent SliceMode=1 slice chains through the restatement (hvxo_hm_chains_stv): chain k decides
+    CTUs chain_first[k] .. + per_chain - 1 from entry_states; rd_metric 1 / 2: the SSIM / stVSSIM cost
+    (lambda_ssim; stv = (hist, dirs)) in the CU decision.  Arrays as in replay(); outputs per (chain, CTU)."""
     L = _lib()
     if not getattr(L, "_hm_chains_bound", False):
         P = ctypes.c_void_p
-        L.hvxo_hm_chains_rd.restype = ctypes.c_int
-        L.hvxo_hm_chains_rd.argtypes = [P, P, P, P, ctypes.c_int, P, P, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
-                                        ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P, P, P, P]
+        L.hvxo_hm_chains_stv.restype = ctypes.c_int
+        L.hvxo_hm_chains_stv.argtypes = [P, P, P, P, ctypes.c_int, P, P, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P, P, P, P, P]
         L._hm_chains_bound = True
     pi = np.ascontiguousarray(pic_i32, np.int32)
     pf = np.ascontiguousarray(pic_f64, np.float64)
@@ -146,12 +177,15 @@ def chains(pic_i32, pic_f64, org, refpics, entry_states, chain_first, per_chain,
            "bits_dist": np.zeros((n, 2), np.uint32)}
     refs = np.ascontiguousarray(refpics, np.uint8)
     nref = refs.size // (int(pi[0]) * int(pi[1]) * 3 // 2)
-    r = L.hvxo_hm_chains_rd(_ptr(pi), _ptr(pf), _ptr(np.ascontiguousarray(org, np.uint8)), _ptr(refs), nref,
-                            _ptr(None if col_field is None else np.ascontiguousarray(col_field, np.int16)),
-                            _ptr(entropy_bits()), _ptr(np.ascontiguousarray(entry_states, np.uint8)), len(first),
-                            _ptr(first), per_chain, slice_ctus, threads, int(rd_metric), float(lambda_ssim),
-                            _ptr(out["parts"]), _ptr(out["coef"]), _ptr(out["recon"]), _ptr(out["cost"]),
-                            _ptr(out["bits_dist"]))
+    st, keep = stv_struct(*stv) if stv is not None else (None, None)
+    r = L.hvxo_hm_chains_stv(_ptr(pi), _ptr(pf), _ptr(np.ascontiguousarray(org, np.uint8)), _ptr(refs), nref,
+                             _ptr(None if col_field is None else np.ascontiguousarray(col_field, np.int16)),
+                             _ptr(entropy_bits()), _ptr(np.ascontiguousarray(entry_states, np.uint8)), len(first),
+                             _ptr(first), per_chain, slice_ctus, threads, int(rd_metric), float(lambda_ssim),
+                             ctypes.addressof(st) if st is not None else None,
+                             _ptr(out["parts"]), _ptr(out["coef"]), _ptr(out["recon"]), _ptr(out["cost"]),
+                             _ptr(out["bits_dist"]))
+    del keep
     if r < 0:
         raise ValueError("hvxo_hm_chains rejected the chain layout")
     return out

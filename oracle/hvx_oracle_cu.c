@@ -1252,13 +1252,73 @@ static double cu_dssim(const hm_enc *e, const hm_cu *cu, yuv_t *org, yuv_t *reco
   }
   return d;
 }
-/* the cost TEncCu compares: calcRdCost(bits, dist) (SSE) or the SSIM cost */
+/* The stVSSIM RD cost (rd_metric 2 = HVX_RD_STVSSIM; include/hvx_types.h hvx_hm_picture.hist): the
+ * stvssim encoder's active distortion, distortionstVSSIM (stvssim.c:831-855, att_stv.h:5, rdopt.c:223),
+ * per JM macroblock -- a 16x16 luma area of the CU with its 8x8 Cb, Cr blocks, in raster order --
+ * D_mb = (1 - stVSSIM_Y) * WeightY + (1 - stVSSIM_Cb) * WeightCb + (1 - stVSSIM_Cr) * WeightCr, the
+ * weights 1 (encoder.cfg:289-291) in double, and stVSSIM = compute_stVSSIM's stvssimValue (:587-830:
+ * 8x8 windows stepped by SSIMOverlapSize 4, encoder.cfg:280) over hist_n + 1 frames (the history, most
+ * recent first, then the CU's own original / reconstruction), through the pinned hvxo_stvssim
+ * (tests/golden/ssim.bin).  Cr reads Cb's history planes: compute_stVSSIM is called with comp 1 for
+ * both chroma components (:846, :850).  An 8x8 CU (smaller than a macroblock) is one 8x8 luma window
+ * and 4x4 chroma windows (compute_stVSSIM's wint 4 filters), weighted 1/4. */
+static float stv_term(const hm_enc *e, yuv_t *org, yuv_t *reco, int c, int lx, int ly, int px, int py, int bw, int wint) {
+  const hvxo_hm_pic *P = e->pic;
+  const int used = P->hist_n + 1, hc = c == 2 ? 1 : c, s = c ? 1 : 0, uv = c ? 2 : 1, dw = bw * uv;
+  static __thread uint8_t ob[26][256], rb[26][256];
+  static __thread float dm[32 * 32];
+  const uint8_t *op[26], *rp[26];
+  for (int o = 0; o < used; o++) {
+    for (int y = 0; y < bw; y++)
+      for (int x = 0; x < bw; x++) {
+        if (o < used - 1) {
+          const int st = P->hist_stride[s];
+          ob[o][y * bw + x] = P->hist[6 * o + hc][(py + y) * st + px + x];
+          rb[o][y * bw + x] = P->hist[6 * o + 3 + hc][(py + y) * st + px + x];
+        } else {
+          ob[o][y * bw + x] = (uint8_t)yaddr(org, c, lx, ly)[y * ystride(c) + x];
+          rb[o][y * bw + x] = (uint8_t)yaddr(reco, c, lx, ly)[y * ystride(c) + x];
+        }
+      }
+    op[o] = ob[o];
+    rp[o] = rb[o];
+  }
+  for (int y = 0; y < dw; y++)
+    for (int x = 0; x < dw; x++)
+      dm[y * dw + x] = P->dirs ? P->dirs[((py * uv + y) >> 2) * P->dirs_stride + ((px * uv + x) >> 2)] : 0.0f;
+  float ss, s3, stv;
+  hvxo_stvssim(op, rp, bw, dm, dw, bw, bw, wint, 4, used, c ? 1 : 0, &ss, &s3, &stv);
+  return 1.0f - stv;
+}
+static double cu_dstv(const hm_enc *e, const hm_cu *cu, yuv_t *org, yuv_t *reco) {
+  const hvxo_hm_pic *P = e->pic;
+  if (cu->width == 8) {
+    const float dy = stv_term(e, org, reco, 0, 0, 0, cu->x, cu->y, 8, 8);
+    const float du = stv_term(e, org, reco, 1, 0, 0, cu->x >> 1, cu->y >> 1, 4, 4);
+    const float dv = stv_term(e, org, reco, 2, 0, 0, cu->x >> 1, cu->y >> 1, 4, 4);
+    return 0.25 * ((double)dy * 1.0 + (double)du * 1.0 + (double)dv * 1.0);
+  }
+  const int n = cu->width >> 4;
+  double d = 0;
+  for (int my = 0; my < n; my++)
+    for (int mx = 0; mx < n; mx++) {
+      const int x = cu->x + 16 * mx, y = cu->y + 16 * my;
+      if (x >= P->w || y >= P->h) continue;
+      const float dy = stv_term(e, org, reco, 0, 16 * mx, 16 * my, x, y, 16, 8);
+      const float du = stv_term(e, org, reco, 1, 8 * mx, 8 * my, x >> 1, y >> 1, 8, 8);
+      const float dv = stv_term(e, org, reco, 2, 8 * mx, 8 * my, x >> 1, y >> 1, 8, 8);
+      d += (double)dy * 1.0 + (double)du * 1.0 + (double)dv * 1.0;
+    }
+  return d;
+}
+/* the cost TEncCu compares: calcRdCost(bits, dist) (SSE) or the SSIM / stVSSIM cost */
 static double cu_cost(const hm_enc *e, const hm_cu *cu, uint32_t bits, uint32_t dist) {
-  if (e->pic->rd_metric != 1) return rd_cost(e, bits, dist);
+  if (e->pic->rd_metric == 0) return rd_cost(e, bits, dist);
   return cu->dssim + e->pic->lambda_ssim * ((double)bits > 0.5 ? (double)bits : 0.5);
 }
 static void cu_measure_ssim(const hm_enc *e, hm_cu *cu, yuv_t *org, yuv_t *reco) {
   if (e->pic->rd_metric == 1) cu->dssim = cu_dssim(e, cu, org, reco);
+  else if (e->pic->rd_metric == 2) cu->dssim = cu_dstv(e, cu, org, reco);
 }
 static uint32_t mv_cost_bits(const hm_enc *e, uint32_t bits) { return (uint32_t)(e->pic->lambda_motion * bits) >> 16; }
 static uint32_t dist_part(const hm_enc *e, const int16_t *a, int sa, const int16_t *b, int sb, int w, int h, int comp) {
@@ -2962,6 +3022,28 @@ int hvxo_hm_replay_picture_rd(const int32_t *pi, const double *pf, const uint8_t
                               int slice_ctus, int rd_metric, double lambda_ssim, int16_t *out_parts, int32_t *out_coef,
                               uint8_t *out_recon, double *out_cost, uint32_t *out_bits_dist, uint8_t *out_states,
                               int64_t *out_frac) {
+  return hvxo_hm_replay_picture_stv(pi, pf, org, refpics, refpic_poc, n_refpics, col_field, entropy_bits, ctu_states,
+                                    ctu_frac, ctu_int2n, hm_parts, hm_coef, hm_recon, mode, slice_ctus, rd_metric,
+                                    lambda_ssim, NULL, out_parts, out_coef, out_recon, out_cost, out_bits_dist, out_states,
+                                    out_frac);
+}
+static void set_stv(hvxo_hm_pic *P, const hvxo_stv *stv) {
+  P->hist = NULL; P->hist_n = 0; P->hist_stride[0] = P->hist_stride[1] = 0; P->dirs = NULL; P->dirs_stride = 0;
+  if (!stv) return;
+  P->hist = stv->hist;
+  P->hist_n = stv->hist_n < 0 ? 0 : stv->hist_n > 25 ? 25 : stv->hist_n;
+  P->hist_stride[0] = stv->hist_stride[0];
+  P->hist_stride[1] = stv->hist_stride[1];
+  P->dirs = stv->dirs;
+  P->dirs_stride = stv->dirs_stride;
+}
+int hvxo_hm_replay_picture_stv(const int32_t *pi, const double *pf, const uint8_t *org, const uint8_t *refpics,
+                               const int32_t *refpic_poc, int n_refpics, const int16_t *col_field, const int32_t *entropy_bits,
+                               const uint8_t *ctu_states, const int64_t *ctu_frac, const int16_t *ctu_int2n,
+                               const int16_t *hm_parts, const int32_t *hm_coef, const uint8_t *hm_recon, int mode,
+                               int slice_ctus, int rd_metric, double lambda_ssim, const hvxo_stv *stv, int16_t *out_parts,
+                               int32_t *out_coef, uint8_t *out_recon, double *out_cost, uint32_t *out_bits_dist,
+                               uint8_t *out_states, int64_t *out_frac) {
   (void)refpic_poc;
   tables_init();
   const int w = pi[P_W], h = pi[P_H], wc = (w + 63) / 64, hc = (h + 63) / 64, n = wc * hc;
@@ -2969,6 +3051,7 @@ int hvxo_hm_replay_picture_rd(const int32_t *pi, const double *pf, const uint8_t
   pic_setup(&B, pi, pf, org, refpics, n_refpics, col_field, entropy_bits);
   B.P.rd_metric = rd_metric;
   B.P.lambda_ssim = lambda_ssim;
+  set_stv(&B.P, stv);
   const hvxo_hm_pic P = B.P;
   /* the picture's CTU data and reconstruction (whole CTUs) */
   hvxo_hm_ctu_data *ctus = (hvxo_hm_ctu_data *)calloc((size_t)n, sizeof(hvxo_hm_ctu_data));
@@ -3119,6 +3202,15 @@ int hvxo_hm_chains_rd(const int32_t *pi, const double *pf, const uint8_t *org, c
                       const int32_t *chain_first, int ctus_per_chain, int slice_ctus, int n_threads, int rd_metric,
                       double lambda_ssim, int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon, double *out_cost,
                       uint32_t *out_bits_dist) {
+  return hvxo_hm_chains_stv(pi, pf, org, refpics, n_refpics, col_field, entropy_bits, entry_states, n_chains, chain_first,
+                            ctus_per_chain, slice_ctus, n_threads, rd_metric, lambda_ssim, NULL, out_parts, out_coef,
+                            out_recon, out_cost, out_bits_dist);
+}
+int hvxo_hm_chains_stv(const int32_t *pi, const double *pf, const uint8_t *org, const uint8_t *refpics, int n_refpics,
+                       const int16_t *col_field, const int32_t *entropy_bits, const uint8_t *entry_states, int n_chains,
+                       const int32_t *chain_first, int ctus_per_chain, int slice_ctus, int n_threads, int rd_metric,
+                       double lambda_ssim, const hvxo_stv *stv, int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon,
+                       double *out_cost, uint32_t *out_bits_dist) {
   tables_init();
   hvxo_init_tables();
   if (pi[P_COL_VALID] && !col_field) return -1;
@@ -3129,6 +3221,7 @@ int hvxo_hm_chains_rd(const int32_t *pi, const double *pf, const uint8_t *org, c
   pic_setup(&B, pi, pf, org, refpics, n_refpics, col_field, entropy_bits);
   B.P.rd_metric = rd_metric;
   B.P.lambda_ssim = lambda_ssim;
+  set_stv(&B.P, stv);
   hvxo_hm_ctu_data *ctus = (hvxo_hm_ctu_data *)calloc((size_t)n, sizeof(hvxo_hm_ctu_data));
   const int rw = wc * 64, rh = hc * 64;
   int16_t *recb[3];

@@ -33,8 +33,13 @@ typedef struct hvxo_hm_pic {
   uint32_t lambda_motion;
   int search_range, amp;
   int bipred_range;                     /* BipredSearchRange (TEncSearch::m_bipredSearchRange) */
-  int rd_metric;                        /* 0: HM's SSE cost; 1: the stvssim SSIM cost in TEncCu's comparisons */
-  double lambda_ssim;                   /* rd_metric 1: lambda_2(QP) * eta^0.85 (stvssim.c:1805, :1707) */
+  int rd_metric;                        /* 0: HM's SSE cost; 1: the stvssim SSIM cost, 2: its stVSSIM cost in
+                                           TEncCu's comparisons (include/hvx_types.h HVX_RD_*) */
+  double lambda_ssim;                   /* rd_metric 1, 2: lambda_2(QP) * eta^0.85 (stvssim.c:1805, :1707) */
+  const uint8_t *const *hist;           /* rd_metric 2: the stVSSIM history (hvx_hm_picture.hist layout) */
+  int hist_n, hist_stride[2];
+  const float *dirs;                    /* rd_metric 2: direction map, one float per 4x4 luma block */
+  int dirs_stride;
   const int32_t *entropy_bits;          /* ContextModel::m_entropyBits[128] */
   const int16_t *org[3];                /* original, sample (0,0) */
   int org_stride[3];
@@ -97,6 +102,23 @@ int hvxo_hm_replay_picture_rd(const int32_t *pic_i32, const double *pic_f64, con
                               uint8_t *out_recon, double *out_cost, uint32_t *out_bits_dist, uint8_t *out_states,
                               int64_t *out_frac);
 
+/* The stVSSIM inputs of rd_metric 2 (hvx_hm_picture.hist / dirs, include/hvx_types.h): hist[6k + c]
+ * original / hist[6k + 3 + c] reconstruction of the k-th most recent previous picture (8-bit, strides
+ * hist_stride[0] luma / [1] chroma), k < hist_n <= 25; dirs: orientation per 4x4 luma block. */
+typedef struct hvxo_stv {
+  const uint8_t *const *hist;
+  int hist_n, hist_stride[2];
+  const float *dirs;
+  int dirs_stride;
+} hvxo_stv;
+int hvxo_hm_replay_picture_stv(const int32_t *pic_i32, const double *pic_f64, const uint8_t *org, const uint8_t *refpics,
+                               const int32_t *refpic_poc, int n_refpics, const int16_t *col_field, const int32_t *entropy_bits,
+                               const uint8_t *ctu_states, const int64_t *ctu_frac, const int16_t *ctu_int2n,
+                               const int16_t *hm_parts, const int32_t *hm_coef, const uint8_t *hm_recon, int mode,
+                               int slice_ctus, int rd_metric, double lambda_ssim, const hvxo_stv *stv, int16_t *out_parts,
+                               int32_t *out_coef, uint8_t *out_recon, double *out_cost, uint32_t *out_bits_dist,
+                               uint8_t *out_states, int64_t *out_frac);
+
 /* Independent SliceMode=1 slice chains (slices of slice_ctus CTUs): chain k decides CTUs
  * chain_first[k] .. + ctus_per_chain - 1 from entry_states (the slice-start contexts) and a zero
  * m_integerMv2Nx2N, carrying both CTU to CTU (a chain crossing into the next slice restarts from
@@ -112,6 +134,11 @@ int hvxo_hm_chains_rd(const int32_t *pic_i32, const double *pic_f64, const uint8
                       int n_chains, const int32_t *chain_first, int ctus_per_chain, int slice_ctus, int n_threads,
                       int rd_metric, double lambda_ssim, int16_t *out_parts, int32_t *out_coef, uint8_t *out_recon,
                       double *out_cost, uint32_t *out_bits_dist);
+int hvxo_hm_chains_stv(const int32_t *pic_i32, const double *pic_f64, const uint8_t *org, const uint8_t *refpics,
+                       int n_refpics, const int16_t *col_field, const int32_t *entropy_bits, const uint8_t *entry_states,
+                       int n_chains, const int32_t *chain_first, int ctus_per_chain, int slice_ctus, int n_threads,
+                       int rd_metric, double lambda_ssim, const hvxo_stv *stv, int16_t *out_parts, int32_t *out_coef,
+                       uint8_t *out_recon, double *out_cost, uint32_t *out_bits_dist);
 
 /* The picture-level loop after compressSlice (TEncGOP.cpp:1465-1480) on a decided picture's CTU data
  * (hm_parts = [n_ctus][256][HVXO_HM_PART_FIELDS], the cu_capture.cpp rows):

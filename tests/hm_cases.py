@@ -70,6 +70,45 @@ def hm_recon(g, first, w, h):
     return planes
 
 
+RA_CODING_ORDER = (0, 8, 4, 2, 1, 3, 6, 5, 7)  # encoder_randomaccess_main.cfg GOP8, first GOP
+
+
+def stv_history(g, pic):
+    """The stVSSIM history of an RA capture's picture (hvx_hm_picture.hist): the pictures coded before it
+    (RA_CODING_ORDER), most recent first, each (org Y, Cb, Cr, rec Y, Cb, Cr) -- originals regenerated
+    (oracle/make_yuv.py texture, the captures' input, gen_goldens.sh), reconstructions = the capture's
+    final reference pictures, or for a non-reference picture the capture's own pre-loop-filter
+    reconstruction (its original when the capture holds neither) -- and the direction map from the picture's collocated field (hm.stv_direction_map)."""
+    from oracle import make_yuv
+    pi = g["pic_i32"][pic]
+    w, h = int(pi[P_W]), int(pi[P_H])
+    psz = w * h * 3 // 2
+    poc = int(pi[P_POC])
+    order = list(RA_CODING_ORDER)
+    prev = order[:order.index(poc)][::-1][:_abi.STV_HIST]
+    refpoc = [int(q) for q in g["refpic_poc"]]
+    cap = [int(q) for q in g["pic_i32"][:, P_POC]]
+    frames = []
+    for q in prev:
+        org = yuv_split(np.asarray(make_yuv.texture_frame(w, h, q), np.uint8), w, h)
+        if q in refpoc:
+            r = refpoc.index(q)
+            rec = yuv_split(g["refpic"][r * psz:(r + 1) * psz], w, h)
+        elif q in cap:
+            k = cap.index(q)
+            full = hm_recon(g, int(g["pic_i32"][k][P_FIRST_CTU]), w, h)
+            rec = (full[0][:h, :w], full[1][:h // 2, :w // 2], full[2][:h // 2, :w // 2])
+        else:  # a picture the capture holds no reconstruction of: its original stands in
+            rec = org
+        frames.append(tuple(np.ascontiguousarray(p) for p in (*org, *rec)))
+    col = None
+    if int(pi[P_COL_VALID]):
+        n = int(pi[P_NCTU])
+        k = sum(1 for q in range(pic) if int(g["pic_i32"][q][P_COL_VALID]))
+        col = g["col_field"][k * n * 16:(k + 1) * n * 16]
+    return frames, hm.stv_direction_map(col, w, h)
+
+
 def device_picture(g, pic, chained, entropy_bits, rd_metric=0, eta=1.0):
     pi, pf = g["pic_i32"][pic], g["pic_f64"][pic]
     w, h = int(pi[P_W]), int(pi[P_H])
@@ -85,9 +124,12 @@ def device_picture(g, pic, chained, entropy_bits, rd_metric=0, eta=1.0):
     rec = None if chained else hm_recon(g, first, w, h)
     ctus = None if chained else hm_ctus(g, first, n)
     params = pic_params(pi, pf)
+    stv = None
     if rd_metric:
         params["rd_metric"], params["lambda_ssim"] = rd_metric, hm.lambda_ssim(int(pi[P_QP]), eta)
-    return hm.DevicePicture(org, refs, params, entropy_bits, rec=rec, ctus=ctus, col_field=col)
+        if rd_metric == _abi.RD_STVSSIM:
+            stv = hm.StvHistory(*stv_history(g, pic))
+    return hm.DevicePicture(org, refs, params, entropy_bits, rec=rec, ctus=ctus, col_field=col, stv=stv)
 
 
 def run_capture(name, mode, pics=None, stage=0, rd_metric=0, eta=1.0, serial=False):

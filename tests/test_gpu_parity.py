@@ -284,8 +284,7 @@ def test_hm_ctu_resume_gpu(torch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,eta", [("ctu_ra_q22.bin", 1.0), ("ctu_ra_q27.bin", 0.7), ("ctu_ra_q32.bin", 1.0),
-                                      ("ctu_ra_q37.bin", 1.3)])
+@pytest.mark.parametrize("name,eta", [("ctu_ra_q37.bin", 1.3)])  # the active cost's sweep: test_hm_ctu_stvssim_rdo_gpu
 def test_hm_ctu_ssim_rdo_gpu(torch, name, eta):
     """BASELINE config 4's cost inside the real decision: hvx_hm_compress with HVX_RD_SSIM (TEncCu's
     mode / split comparisons on J = D_ssim + lambda_2(QP) * eta^0.85 * max(0.5, R), stvssim.c:567,
@@ -307,6 +306,32 @@ def test_hm_ctu_ssim_rdo_gpu(torch, name, eta):
     bad = hm_cases.compare_outputs(plan, out, refs)
     assert not bad, bad[:5]
     assert hm_cases.compare(g, plan, out), "the SSIM cost decided exactly as HM's SSE cost"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,eta", [("ctu_ra_q22.bin", 1.0), ("ctu_ra_q27.bin", 0.7), ("ctu_ra_q32.bin", 1.0),
+                                      ("ctu_ra_q37.bin", 1.3)])
+def test_hm_ctu_stvssim_rdo_gpu(torch, name, eta):
+    """BASELINE config 4 with the reference's ACTIVE cost (att_stv.h:5 -> distortionstVSSIM,
+    stvssim.c:831-855): hvx_hm_compress with HVX_RD_STVSSIM on the RA B pictures at QP 22 / 27 / 32 / 37,
+    each with its stVSSIM history (the pictures coded before it, tests/hm_cases.stv_history: up to 4
+    previous frames here) and direction map, chained per picture, against the restatement (cu_dstv
+    through the pinned hvxo_stvssim): every decision, coefficient, reconstruction sample, bit count,
+    distortion and double cost bit-exact; and the cost decides differently from HM's SSE cost."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import hm_ctu
+    from video_codecs_amd import _abi, hm
+    g, plan, out = hm_cases.run_capture(name, 1, rd_metric=_abi.RD_STVSSIM, eta=eta)
+
+    def ref(p):
+        qp = int(g["pic_i32"][p[0]][hm_cases.P_QP])
+        return hm_ctu.replay(g, p[0], 1, rd_metric=_abi.RD_STVSSIM, lambda_ssim=hm.lambda_ssim(qp, eta),
+                             stv=hm_cases.stv_history(g, p[0]))
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        refs = list(ex.map(ref, plan))
+    bad = hm_cases.compare_outputs(plan, out, refs)
+    assert not bad, bad[:5]
+    assert hm_cases.compare(g, plan, out), "the stVSSIM cost decided exactly as HM's SSE cost"
 
 
 @pytest.mark.gpu

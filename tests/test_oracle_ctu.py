@@ -11,6 +11,8 @@ leaves for the next CTU.
 import pytest
 
 from oracle import hm_ctu
+from tests import golden_cases as gc
+from tests import hm_cases
 
 CAPTURES = ["ctu_ldp_rand.bin", "ctu_ldp_smooth.bin"]
 
@@ -246,3 +248,64 @@ def test_hm_chains_across_slices_vs_hm():
         np.testing.assert_array_equal(out["coef"][a], g["ctu_coef"][first + a], err_msg=a)
         np.testing.assert_array_equal(out["recon"][a], g["ctu_recon"][first + a], err_msg=a)
         assert out["cost"][a] == g["ctu_cost"][first + a], a
+
+
+def test_stv_orientation_known_answers():
+    """getOrientation (stvssim.c:1317) bins of the stVSSIM direction map: x == 0 -> pi/2 (bin 16),
+    y == 0 -> 0, diagonals pi/4 (bin 8) and 3pi/4 (bin 24, atan < 0 + pi), and a shallow vector."""
+    from video_codecs_amd import hm
+    assert hm.stv_orientation(0, 0) == 16 and hm.stv_orientation(0, -7) == 16
+    assert hm.stv_orientation(5, 0) == 0 and hm.stv_orientation(-5, 0) == 0
+    assert hm.stv_orientation(3, 3) == 8 and hm.stv_orientation(-3, -3) == 8
+    assert hm.stv_orientation(-2, 2) == 24
+    assert hm.stv_orientation(10, 1) == 1  # atan(0.1) = 0.0997 rad, nearest pi/32 = 0.0982
+
+
+def test_stv_direction_map_layout():
+    """hm.stv_direction_map: the z-order 16x16 blocks of a col field land on their 4x4 luma blocks;
+    chooseOrient's vote (bin / 2, first maximum); intra / outside / no-motion blocks map to 0."""
+    import numpy as np
+    from video_codecs_amd import hm
+    w, h = 128, 72
+    wc, hc = 2, 2
+    col = np.zeros((wc * hc * 16, 8), np.int16)
+    col[:, 0] = 1  # intra everywhere
+    col[:, 1:3] = -1
+    # CTU 1, z-order block 3 (bx 1, by 1): L0 (0, 5) vertical -> bin 16 -> orients2[8] = pi/2
+    r = 1 * 16 + 3
+    col[r, 0], col[r, 1], col[r, 3], col[r, 4] = 0, 0, 0, 5
+    # CTU 2 (x 0, y 64), block 0: L0 (4, 4) and L1 (-4, 4): one vote each, bins 4 and 12 -> first max = 4
+    r = 2 * 16
+    col[r, 0], col[r, 1], col[r, 2], col[r, 3:7] = 0, 0, 0, (4, 4, -4, 4)
+    m = hm.stv_direction_map(col, w, h)
+    assert m.shape == (18, 32) and m.dtype == np.float32
+    f = np.float32
+    assert np.all(m[4:8, 20:24] == f(f(f(3.1415926) * f(8)) / f(16)))
+    assert m[16, 0] == f(f(f(3.1415926) * f(4)) / f(16))
+    assert m[17, 3] == m[16, 0]  # the bottom CTU row is cut at h / 4
+    m[4:8, 20:24] = 0
+    m[16:18, 0:4] = 0
+    assert not m.any()
+
+
+def test_ctu_stvssim_cost_reads_history_and_map():
+    """The restatement's stVSSIM cost (rd_metric 2, oracle cu_dstv) on an RA B picture with a 4-frame
+    history: it decides differently from the plain SSIM cost, and both the history and the direction map
+    change its costs (the 3-D terms read them), while a rerun is identical."""
+    import numpy as np
+    from oracle import hm_ctu
+    from video_codecs_amd import hm
+    g = gc.load("ctu_ra_q32.bin")
+    pic = 1
+    qp = int(g["pic_i32"][pic][hm_cases.P_QP])
+    lam = hm.lambda_ssim(qp, 1.0)
+    frames, dirs = hm_cases.stv_history(g, pic)
+    assert len(frames) == 4 and dirs.any()
+    a = hm_ctu.replay(g, pic, 1, rd_metric=2, lambda_ssim=lam, stv=(frames, dirs))
+    assert np.array_equal(a["cost"], hm_ctu.replay(g, pic, 1, rd_metric=2, lambda_ssim=lam, stv=(frames, dirs))["cost"])
+    s = hm_ctu.replay(g, pic, 1, rd_metric=1, lambda_ssim=lam)
+    assert (a["parts"] != s["parts"]).any()
+    flat = [tuple(np.zeros_like(p) for p in f) for f in frames]
+    assert not np.array_equal(a["cost"], hm_ctu.replay(g, pic, 1, rd_metric=2, lambda_ssim=lam, stv=(flat, dirs))["cost"])
+    assert not np.array_equal(a["cost"], hm_ctu.replay(g, pic, 1, rd_metric=2, lambda_ssim=lam,
+                                                       stv=(frames, np.zeros_like(dirs)))["cost"])

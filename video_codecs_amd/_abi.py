@@ -34,7 +34,8 @@ ME_FEN, ME_HADME, ME_SMOOTHMV, ME_BI = 1, 2, 4, 8
 # g_aucChromaScale[CHROMA_420] (TComRom.cpp:536)
 CHROMA_SCALE_420 = tuple(range(30)) + (29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37) + tuple(range(38, 52))
 assert len(CHROMA_SCALE_420) == 58
-RD_SSE, RD_SSIM = 0, 1  # hvx_hm_picture.rd_metric
+RD_SSE, RD_SSIM, RD_STVSSIM = 0, 1, 2  # hvx_hm_picture.rd_metric
+STV_HIST = 25  # HVX_STV_HIST: previous pictures of the stVSSIM history
 
 
 def load_estbits_p_luma():

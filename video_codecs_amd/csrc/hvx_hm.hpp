@@ -34,6 +34,7 @@ __device__ void hm_prof_add(int cat, uint64_t dt);
 #include "hvx_mc.hpp"
 #include "hvx_intra.hpp"
 #include "hvx_me.hpp"
+#include "hvx_ssimw.hpp"
 
 namespace hm {
 
@@ -2011,14 +2012,135 @@ __device__ double cu_dssim(const Cu *cu, Yuv *org, Yuv *reco) {
   wsync();
   return d;
 }
-// the cost TEncCu compares: calcRdCost(bits, dist), or the SSIM cost (dssim already measured)
+// The stVSSIM cost (HVX_RD_STVSSIM, include/hvx_types.h hvx_hm_picture.hist; restated by cu_dstv in
+// oracle/hvx_oracle_cu.c): distortionstVSSIM (stvssim.c:831-855) per 16x16 luma area of the CU.
+// One lane per window (compute_stVSSIM's loop body :655-811 in its float order): the four directional
+// 3-D SSIMs over the history frames (most recent first) and then the CU's own original /
+// reconstruction, accumulated in one pass over the samples (each accumulator receives its own terms in
+// the reference's order), the direction vote of calOrit (:336) on the map, and the plain SSIM of the
+// current frame; the window's ssim * ssim3d goes to E.ssim_t, averaged per block in window order.
+__device__ float stv_window(int c, int wint, int lx, int ly, int px, int py, const int16_t *org, const int16_t *rec,
+                            int ystr) {
+  const int used = E.P.hist_n + 1, hc = c == 2 ? 1 : c, uv = c ? 2 : 1;
+  const float wa = 0.6f, wb = 1.0f - wa;
+  float wgta[4], wgtb[4];
+  if (wint == 4) {
+    wgta[0] = wgta[2] = wgta[1] = wgta[3] = wa / (wint * (used));
+    wgtb[0] = wgtb[2] = wgtb[1] = wgtb[3] = wb / ((wint * wint - wint) * (used));
+  } else {
+    wgta[0] = wgta[2] = wa / (3 * wint * (used));
+    wgta[1] = wgta[3] = wa / ((3 * wint - 2) * (used));
+    wgtb[0] = wgtb[2] = wb / ((wint * wint - 3 * wint) * (used));
+    wgtb[1] = wgtb[3] = wb / ((wint * wint - 3 * wint + 2) * (used));
+  }
+  const float C1 = 0.01f * 0.01f * (float)(255 * 255), C2 = 0.03f * 0.03f * (float)(255 * 255);
+  float mo[4] = {0, 0, 0, 0}, me[4] = {0, 0, 0, 0}, vo[4] = {0, 0, 0, 0}, ve[4] = {0, 0, 0, 0}, cv[4] = {0, 0, 0, 0};
+  const int hs = E.P.hist_stride[c ? 1 : 0];
+  for (int o = 0; o < used; o++) {
+    const bool cur = o == used - 1;
+    const uint8_t *ho = cur ? nullptr : E.P.hist[6 * o + hc] + (size_t)py * hs + px;
+    const uint8_t *hr = cur ? nullptr : E.P.hist[6 * o + 3 + hc] + (size_t)py * hs + px;
+    for (int n = 0; n < wint; n++)
+      for (int m = 0; m < wint; m++) {
+        const int po = cur ? org[(ly + n) * ystr + lx + m] : ho[n * hs + m];
+        const int pe = cur ? rec[(ly + n) * ystr + lx + m] : hr[n * hs + m];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const float wgt = orient_weight(k, wint, n, m, wgta[k], wgtb[k]);
+          mo[k] += wgt * po; me[k] += wgt * pe;
+          vo[k] += wgt * po * po; ve[k] += wgt * pe * pe; cv[k] += wgt * po * pe;
+        }
+      }
+  }
+  float s3[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const float varo = fabsf(vo[k] - mo[k] * mo[k]), vare = fabsf(ve[k] - me[k] * me[k]);
+    const float covo = fabsf(cv[k] - mo[k] * me[k]);
+    float v = (float)((2.0 * mo[k] * me[k] + C1) * (2.0 * covo + C2));
+    v /= (float)(mo[k] * mo[k] + me[k] * me[k] + C1) * (varo + vare + C2);
+    s3[k] = v;
+    if (s3[k] >= 1.0 && s3[k] < 1.01) s3[k] = 1.0f;
+  }
+  // calOrit over the window's samples (the map is per 4x4 luma block; chroma reads luma coordinates)
+  const float kOrient[4] = {0, 3.1415926f / 4, 3.1415926f / 2, 3.1415926f * 3 / 4};
+  short orit[4] = {0, 0, 0, 0};
+  for (int n = 0; n < wint; n++)
+    for (int m = 0; m < wint; m++) {
+      const float od = E.P.dirs ? E.P.dirs[(((py + n) * uv) >> 2) * E.P.dirs_stride + (((px + m) * uv) >> 2)] : 0.0f;
+      float dn[4], dx = 10000.0f;
+      for (int q = 0; q < 4; q++) { dn[q] = (float)fabs(od - kOrient[q]); if (dn[q] < dx) dx = dn[q]; }
+      for (int q = 0; q < 4; q++) if (fabs(dx - dn[q]) < 0.01f) orit[q]++;
+    }
+  short tmp = 0, inx = 0;
+  for (int q = 0; q < 4; q++) if (orit[q] > tmp) { tmp = orit[q]; inx = (short)q; }
+  int q;
+  for (q = 0; q < 4; ++q) if ((tmp - orit[q]) < 10 && inx != q) break;
+  const float t3 = q == 4 ? s3[inx] : (s3[inx] + s3[q]) / 2;
+  // the plain SSIM of the current frame (:758-807), no clamp
+  const float wgt = 1.0f / (wint * wint);
+  float a = 0, b = 0, va = 0, vb = 0, cab = 0;
+  for (int n = 0; n < wint; n++)
+    for (int m = 0; m < wint; m++) {
+      const int po = org[(ly + n) * ystr + lx + m], pe = rec[(ly + n) * ystr + lx + m];
+      a += wgt * po; b += wgt * pe;
+      va += wgt * po * po; vb += wgt * pe * pe; cab += wgt * po * pe;
+    }
+  const float varo = fabsf(va - a * a), vare = fabsf(vb - b * b), covo = fabsf(cab - a * b);
+  float ts = (float)((2.0 * a * b + C1) * (2.0 * covo + C2));
+  ts /= (float)(a * a + b * b + C1) * (varo + vare + C2);
+  return ts * t3;
+}
+// stvssimx of one block from its window terms (:817-824) -> 1 - stVSSIM (distortionstVSSIM :840)
+__device__ __forceinline__ float stv_block(const float *t, int nw) {
+  float x = 0;
+  for (int k = 0; k < nw; k++) x += t[k];
+  x /= (float)nw;
+  if (x >= 1.0 && x < 1.01) x = 1.0f;
+  return 1.0f - x;
+}
+// D of a CU: tasks = per 16x16 area (raster) its 9 luma windows then the Cb and Cr window; an 8x8
+// CU: one luma, one Cb, one Cr window (4x4 chroma), weighted 1/4
+__device__ double cu_dstv(const Cu *cu, Yuv *org, Yuv *reco) {
+  const bool small = cu->width == 8;
+  const int n = small ? 1 : cu->width >> 4, per = small ? 3 : 11, total = n * n * per;
+  for (int k = lid(); k < total; k += 64) {
+    const int mb = k / per, w = k - mb * per, my = mb / n, mx = mb - my * n;
+    int c, wint, lx, ly;
+    if (small) {
+      c = w; wint = c ? 4 : 8; lx = 0; ly = 0;
+    } else if (w < 9) {
+      c = 0; wint = 8; lx = 16 * mx + 4 * (w % 3); ly = 16 * my + 4 * (w / 3);
+    } else {
+      c = w - 8; wint = 8; lx = 8 * mx; ly = 8 * my;
+    }
+    const int sh = c ? 1 : 0;
+    const bool in = cu->x + 16 * mx < E.P.w && cu->y + 16 * my < E.P.h;
+    E.ssim_t[k] = in ? stv_window(c, wint, lx, ly, (cu->x >> sh) + lx, (cu->y >> sh) + ly, yaddr(org, c, 0, 0),
+                                  yaddr(reco, c, 0, 0), ystride(c))
+                     : 0.0f;
+  }
+  wsync();
+  double d = 0;
+  for (int mb = 0; mb < n * n; mb++) {
+    const int my = mb / n, mx = mb - my * n;
+    if (cu->x + 16 * mx >= E.P.w || cu->y + 16 * my >= E.P.h) continue;
+    const float *t = E.ssim_t + mb * per;
+    const float dy = stv_block(t, small ? 1 : 9), du = stv_block(t + (small ? 1 : 9), 1), dv = stv_block(t + (small ? 2 : 10), 1);
+    const double dm = (double)dy * 1.0 + (double)du * 1.0 + (double)dv * 1.0;
+    d += small ? 0.25 * dm : dm;
+  }
+  wsync();
+  return d;
+}
+// the cost TEncCu compares: calcRdCost(bits, dist), or the SSIM / stVSSIM cost (dssim already measured)
 __device__ __forceinline__ double cu_cost(double dssim, uint32_t bits, uint32_t dist) {
-  if (E.P.rd_metric != HVX_RD_SSIM) return rd_cost(bits, dist);
+  if (E.P.rd_metric == HVX_RD_SSE) return rd_cost(bits, dist);
   return dssim + E.P.lambda_ssim * ((double)bits > 0.5 ? (double)bits : 0.5);
 }
 __device__ __forceinline__ double measure_ssim(Cu *cu, Yuv *org, Yuv *reco) {
-  if (E.P.rd_metric != HVX_RD_SSIM) return 0.0;
-  const double d = cu_dssim(cu, org, reco);
+  if (E.P.rd_metric == HVX_RD_SSE) return 0.0;
+  const double d = E.P.rd_metric == HVX_RD_STVSSIM ? cu_dstv(cu, org, reco) : cu_dssim(cu, org, reco);
   cu->dssim = d;
   wsync();
   return d;

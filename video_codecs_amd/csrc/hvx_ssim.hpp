@@ -8,6 +8,7 @@
 // reference does.  Float literals/promotions follow the reference (double where it uses 2.0).
 #pragma once
 #include "hvx_dev.hpp"
+#include "hvx_ssimw.hpp"
 
 __device__ __forceinline__ float ssim_window(const uint8_t *o, int so, const uint8_t *r, int sr, int wint) {
   const float C1 = 0.01f * 0.01f * (float)(255 * 255), C2 = 0.03f * 0.03f * (float)(255 * 255);
@@ -53,22 +54,6 @@ static __global__ __launch_bounds__(64) void k_ssim(const uint8_t *__restrict__ 
     if (dist >= 1.0 && dist < 1.01) dist = 1.0f;
     out[jid] = dist;
   }
-}
-
-__device__ __forceinline__ float orient_weight(int k, int beta, int y, int x, float wa, float wb) {
-  if (wa < 0) wa = 1.0f;
-  if (wb < 0) wb = 1.0f;
-  if (wa < wb) { const float c = wb; wb = wa; wa = c; }
-  bool on;
-  if (beta == 4) {
-    on = k == 0 ? x == beta / 2 - 1 : k == 1 ? x + y == beta - 1 : k == 2 ? y == beta / 2 - 1 : x == y;
-  } else {
-    on = k == 0 ? (x >= beta / 2 - 1 && x <= beta / 2 + 1)
-       : k == 1 ? (x + y - beta >= -2 && x + y - beta <= 0)
-       : k == 2 ? (y >= beta / 2 - 1 && y <= beta / 2 + 1)
-       : abs(x - y) <= 1;
-  }
-  return on ? wa : wb;
 }
 
 static __global__ __launch_bounds__(64) void k_stvssim(const uint8_t *const *__restrict__ hist_org,

@@ -46,7 +46,8 @@ class HmPicture(ctypes.Structure):
                 ("tq_lambda", F64 * 3), ("col_field", P_), ("org", P_ * 3), ("rec", P_ * 3), ("org_stride", I32 * 2),
                 ("rec_stride", I32 * 2), ("ctus", P_), ("ref8", P_ * 8), ("ref16", (P_ * 3) * 8), ("ref8_stride", I32),
                 ("ref16_stride", I32 * 2), ("mvd_l1_zero", I32), ("l1_to_l0", I32 * 4), ("entropy_bits", P_),
-                ("rd_metric", I32), ("pad3_", I32), ("lambda_ssim", F64)]
+                ("rd_metric", I32), ("pad3_", I32), ("lambda_ssim", F64), ("hist", P_), ("dirs", P_),
+                ("hist_n", I32), ("dirs_stride", I32), ("hist_stride", I32 * 2)]
 
 
 def derive_lists(slice_type, nref, ref_poc):
@@ -76,6 +77,91 @@ def lambda_ssim(qp, eta=1.0):
     a1, b2, b1 = 5.883060266548170e-03, -2.229472265847692e-02, 9.279543980380707e-02
     lam = -a1 * b2 * math.exp(b1 * (qp - 15))
     return lam * math.pow(eta, 0.85)
+
+
+def stv_orientation(x, y):
+    """getOrientation (stvssim.c:1317): the ORIENTS=32 bin of a motion vector's direction, float32 as the
+    reference computes it (atan in double of the float ratio, cast back to float)."""
+    import math
+    f = np.float32
+    pi = f(3.1415926)
+    if x == 0:
+        ddd = f(pi / f(2))
+    elif y == 0:
+        ddd = f(0)
+    else:
+        ddd = f(math.atan(float(f(f(y) / f(x)))))
+        if ddd < 0:
+            ddd = f(ddd + pi)
+    best, idx = f(10000.0), 0
+    for i in range(32):
+        o = f(0) if i == 0 else f(f(pi * f(i)) / f(32))
+        d = f(abs(float(f(ddd - o))))
+        if d < best:
+            best, idx = d, i
+    return idx
+
+
+def stv_direction_map(col_field, w, h):
+    """The stVSSIM direction map (pic_directions2) of a picture as the HEVC adaptation defines it
+    (include/hvx_types.h hvx_hm_picture.dirs): one float per 4x4 luma block, [h/4, w/4].  JM derives it
+    per macroblock from the L0 motion of its 16x16 / 16x8 / 8x16 partitions (getDirection_macroblock
+    stvssim.c:1369, getMV_macroblock :1264, md_high.c:127-181); here the votes are the motion of the
+    co-located 16x16 block of the collocated picture's compressed motion field (col_field rows
+    [ctu][16 z-order blocks][8]: L0 if its ref idx >= 0, then L1), each getOrientation'd
+    (ORIENTS 32 bins) and voted by chooseOrient (:1347: bin / 2 into ORIENTS2 16, the first maximum) ->
+    orients2[bin]; a block without motion (intra, outside, no collocated picture) gets orients2[0] = 0,
+    as JM's map starts (get_mem2Dfloat zero-fills).  col_field None: the all-zero map."""
+    f = np.float32
+    pi = f(3.1415926)
+    bw, bh = w // 4, h // 4
+    out = np.zeros((bh, bw), np.float32)
+    if col_field is None:
+        return out
+    col = np.asarray(col_field).reshape(-1, 16, 8)
+    wc = (w + 63) // 64
+    for a in range(col.shape[0]):
+        for b in range(16):
+            r = col[a, b]
+            votes = [stv_orientation(int(r[3 + 2 * l]), int(r[4 + 2 * l])) for l in range(2) if r[0] >= 0 and r[1 + l] >= 0]
+            cnt = [0] * 16
+            for v in votes:
+                cnt[v // 2] += 1
+            tmp, idx = 0, 0
+            for i in range(16):
+                if cnt[i] > tmp:
+                    tmp, idx = cnt[i], i
+            val = f(0) if idx == 0 else f(f(pi * f(idx)) / f(16))
+            bx, by = (b & 1) | ((b >> 1) & 2), ((b >> 1) & 1) | ((b >> 2) & 2)
+            x0, y0 = ((a % wc) * 64 + bx * 16) // 4, ((a // wc) * 64 + by * 16) // 4
+            out[y0:min(y0 + 4, bh), x0:min(x0 + 4, bw)] = val
+    return out
+
+
+class StvHistory:
+    """The stVSSIM inputs of a picture decided with HVX_RD_STVSSIM (hvx_hm_picture.hist / dirs): frames =
+    the previous pictures in coding order, most recent first (at most HVX_STV_HIST), each (org Y, Cb, Cr,
+    rec Y, Cb, Cr) uint8 planes (numpy arrays or device tensors of the picture's size); dirs = float32
+    [h/4, w/4] direction map (stv_direction_map) or None."""
+
+    def __init__(self, frames, dirs=None, device="cuda"):
+        import torch
+        assert len(frames) <= _abi.STV_HIST
+        self.keep, ptrs = [], []
+        for fr in frames:
+            assert len(fr) == 6
+            for p in fr:
+                t = p if hasattr(p, "data_ptr") else torch.from_numpy(np.ascontiguousarray(p, np.uint8)).to(device)
+                assert t.dtype == torch.uint8 and t.is_contiguous()
+                self.keep.append(t)
+                ptrs.append(t.data_ptr())
+        self.n = len(frames)
+        self.stride = (int(self.keep[0].shape[1]), int(self.keep[1].shape[1])) if frames else (0, 0)
+        self.table = torch.tensor(ptrs or [0], dtype=torch.int64, device=device)
+        self.dirs = None
+        if dirs is not None:
+            self.dirs = dirs if hasattr(dirs, "data_ptr") else torch.from_numpy(np.ascontiguousarray(dirs, np.float32)).to(device)
+        self.dirs_stride = int(self.dirs.shape[1]) if self.dirs is not None else 0
 
 
 def pack_parts(rows):
@@ -195,9 +281,11 @@ class DevicePicture:
     org: (Y, Cb, Cr) uint8 arrays or a DeviceFrame; refs: reference pictures (indexed by
     ref_plane), each (Y, Cb, Cr) uint8 arrays or a DeviceFrame; params: the slice / RD scalars (see
     HmPicture); rec: optional (Y, Cb, Cr) uint8 initial reconstruction; ctus: optional HM_CTU
-    array (the picture's CTU data); col_field: optional int16 [nctu*16, 8] collocated motion field."""
+    array (the picture's CTU data); col_field: optional int16 [nctu*16, 8] collocated motion field;
+    stv: the StvHistory of a picture decided with HVX_RD_STVSSIM."""
 
-    def __init__(self, org, refs, params, entropy_bits, rec=None, ctus=None, col_field=None, device="cuda"):
+    def __init__(self, org, refs, params, entropy_bits, rec=None, ctus=None, col_field=None, device="cuda",
+                 stv=None):
         import torch
         self.keep = []
         if not isinstance(org, DeviceFrame):
@@ -281,6 +369,12 @@ class DevicePicture:
                 s.ref16[i][c] = ref.ref16[c]
             s.ref16_stride[0], s.ref16_stride[1] = ref.ref16_stride
         s.entropy_bits = dev(np.asarray(entropy_bits, np.int32)).data_ptr()
+        if stv is not None:  # HVX_RD_STVSSIM: the history table and the direction map
+            self.keep.append(stv)
+            s.hist, s.hist_n = stv.table.data_ptr(), stv.n
+            s.hist_stride[0], s.hist_stride[1] = stv.stride
+            if stv.dirs is not None:
+                s.dirs, s.dirs_stride = stv.dirs.data_ptr(), stv.dirs_stride
         self.struct = s
 
     def ctus(self):
