@@ -34,6 +34,14 @@ METRIC = "64\u00d764 CTUs/s (ME+transform+RDOQ) on 2160p YUV, 1\u21928 MI355X; b
 HM_QP_OFFSET, HM_QP_FACTOR = 2, 0.4624
 
 
+T_START = time.perf_counter()
+
+
+def progress(msg):
+    """A progress line on stderr (the JSON result is the only stdout line)."""
+    print("bench[%6.1fs]: %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -298,6 +306,8 @@ def _time_chains(eng, job_steps, n_out, warmup, keep=0):
             eng.launch(jt, n_jobs, out_ctu, out_rec)
             e[1].record()
             ev.append(e)
+            e[1].synchronize()
+            progress("side-figure step %d/%d: %.1f ms" % (k + 1, len(dev_jobs), e[0].elapsed_time(e[1])))
             if keep:
                 kept.append((out_ctu[:keep * hm.HM_CTU.itemsize].clone(), out_rec[:keep * 6144].clone()))
     stream.synchronize()
@@ -332,16 +342,32 @@ def compare_chain_ctus(port, dev_parts, dev_coef, dev_rec, dev_cost, dev_bd):
     return mism, first
 
 
+def stv_history_frames(W, H, n=25, seed=8000):
+    """A synthetic stVSSIM history (hvx_hm_picture.hist) of n previous pictures, most recent first: random
+    4:2:0 originals and reconstructions = original + a seeded +-3 perturbation (clipped)."""
+    from video_codecs_amd import synth
+    rng = np.random.default_rng(seed)
+    out = []
+    for k in range(n):
+        org = yuv_split(synth.random_frame(W, H, seed + k), W, H)
+        rec = [np.clip(p.astype(np.int16) + rng.integers(-3, 4, p.shape, dtype=np.int16), 0, 255).astype(np.uint8)
+               for p in org]
+        out.append(tuple(np.ascontiguousarray(p) for p in (*org, *rec)))
+    return out
+
+
 def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, steps=10, parity_threads=16):
-    """BASELINE config 4 (side figure): 2160p random-access B pictures with the stvssim SSIM cost in
-    the decision (hvx_hm_compress, HVX_RD_SSIM, eta 1) at QP 22 / 27 / 32 / 37.  The picture is GOP
-    position 2 of encoder_randomaccess_main.cfg (POC 4, TId 1: QP offset 2, QPFactor 0.3536,
-    L0 = {POC 0, 8}, L1 = {8, 0}, TMVP from L1[0], BipredSearchRange 4), `pics` pictures in flight
-    (over `distinct` synthetic frame triples), every CTU row a slice (the partial bottom row chained
-    after the row above); one step = every chain one CTU, `steps` timed steps after `warmup`.  The
-    B-slice decision is pinned to HM by the RA captures (tests/golden/ctu_ra_q*.bin); here every
-    CTU of picture 0's chains the GPU decided is re-decided by the restatement with the same SSIM
-    cost (oracle/hvx_oracle_cu.c hvxo_hm_chains_rd) and compared bit for bit."""
+    """BASELINE config 4 (side figure): 2160p random-access B pictures with the stvssim encoder's active
+    stVSSIM cost in the decision (hvx_hm_compress, HVX_RD_STVSSIM: distortionstVSSIM stvssim.c:831 over a
+    full 25-picture history + the current picture, the direction map from the collocated field, eta 1)
+    at QP 22 / 27 / 32 / 37.  The picture is GOP position 2 of encoder_randomaccess_main.cfg in the
+    fourth GOP (POC 28, coding index 26, TId 1: QP offset 2, QPFactor 0.3536, L0 = {24, 32}, L1 = {32,
+    24}, TMVP from L1[0], BipredSearchRange 4), `pics` pictures in flight (over `distinct` synthetic frame
+    triples, one shared synthetic history), every CTU row a slice (the partial bottom row chained after
+    the row above); one step = every chain one CTU, `steps` timed steps after `warmup`.  The B-slice
+    decision is pinned to HM by the RA captures (tests/golden/ctu_ra_q*.bin); here every CTU of picture
+    0's chains the GPU decided is re-decided by the restatement with the same cost and history
+    (oracle/hvx_oracle_cu.c hvxo_hm_chains_stv) and compared bit for bit."""
     import torch
     from concurrent.futures import ThreadPoolExecutor
     import oracle  # noqa: F401  (test infrastructure: the parity checker, after the timing)
@@ -354,20 +380,24 @@ def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, 
     frames = [hm.DeviceFrame(yuv_split(f, W, H)) for f in host]
     col_h = synthetic_col_field(wc * hc, 77)
     col = torch.from_numpy(col_h).cuda()
+    hist = stv_history_frames(W, H)
+    dirs = hm.stv_direction_map(col_h, W, H)
+    stv = hm.StvHistory(hist, dirs)
     rows = hc - 1 if H % 64 else hc  # the partial bottom row chained after the row above (HmWorkload)
     res = {}
     for base_qp in qps:
         qp = base_qp + 2
         prm = hm.slice_params(0, qp, 0.3536)
         entry = _abi.load_ctx_init_states()[0, qp]
-        prm.update(poc=4, nref=[2, 2], ref_poc=np.array([[0, 8, 0, 0], [8, 0, 0, 0]]),
+        prm.update(poc=28, nref=[2, 2], ref_poc=np.array([[24, 32, 0, 0], [32, 24, 0, 0]]),
                    ref_plane=np.array([[0, 1, 0, 0], [1, 0, 0, 0]]), max_merge=5, tmvp=1, check_ldc=0, col_from_l0=0,
-                   col_valid=1, col_poc=8, col_ref_poc=np.array([[0, -8, -16, -24], [0] * 4]), search_range=64, amp=1,
-                   rd_metric=_abi.RD_SSIM, lambda_ssim=hm.lambda_ssim(qp))
+                   col_valid=1, col_poc=32, col_ref_poc=np.array([[24, 16, 8, 0], [0] * 4]), search_range=64, amp=1,
+                   rd_metric=_abi.RD_STVSSIM, lambda_ssim=hm.lambda_ssim(qp))
         pictures = []
         for p in range(pics):
             k = p % distinct
-            pictures.append(hm.DevicePicture(frames[3 * k + 2], [frames[3 * k], frames[3 * k + 1]], prm, eb, col_field=col))
+            pictures.append(hm.DevicePicture(frames[3 * k + 2], [frames[3 * k], frames[3 * k + 1]], prm, eb, col_field=col,
+                                             stv=stv))
         eng = hm.Engine(pictures)
         job_steps = []
         for pos in range(warmup + steps):
@@ -383,9 +413,10 @@ def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, 
         done = warmup + steps
         pi, pf = host_pic_arrays(W, H, prm, qp, col_nref=(4, 0))
         t0 = time.perf_counter()
+        progress("config 4 QP %d: restatement parity (%d chains x %d CTUs)" % (base_qp, rows, done))
         port = hm_ctu.chains(pi, pf, host[2], np.concatenate([host[0], host[1]]), entry,
                              np.arange(rows, dtype=np.int32) * wc, done, wc, threads=parity_threads, col_field=col_h,
-                             rd_metric=_abi.RD_SSIM, lambda_ssim=prm["lambda_ssim"])
+                             rd_metric=_abi.RD_STVSSIM, lambda_ssim=prm["lambda_ssim"], stv=(hist, dirs))
         port_s = time.perf_counter() - t0
         dev = [(ct.cpu().numpy().view(hm.HM_CTU), rc.cpu().numpy().reshape(rows, 6144)) for ct, rc in kept]
         order = [(k, s) for k in range(rows) for s in range(done)]  # the port's CTU order: chain-major
@@ -398,11 +429,12 @@ def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, 
                              "wall_ms_per_step": round(wall * 1e3, 1), "lambda_ssim": prm["lambda_ssim"],
                              "gpu_parity_ctus": len(order), "gpu_parity_mismatches": mism, "first_mismatches": first,
                              "port_ctus_per_s": round(len(order) / port_s, 2)}
-    return {"workload": "2160p RA B pictures (GOP position 2: POC 4, L0 {0,8} / L1 {8,0}, bi-pred + bBi refinement), "
-                        "SSIM cost in TEncCu's decisions, eta 1, %d pictures x %d row-slice chains, %d timed steps after %d "
-                        "warmup; parity: picture 0's chains re-decided by oracle/hvx_oracle_cu.c on %d host threads"
-                        % (pics, rows, steps, warmup, parity_threads),
-            "per_qp": res}
+    return {"workload": "2160p RA B pictures (GOP position 2 of the fourth GOP: POC 28, L0 {24,32} / L1 {32,24}, bi-pred "
+                        "+ bBi refinement), stVSSIM cost (distortionstVSSIM over a 25-picture history, direction map from "
+                        "the collocated field) in TEncCu's decisions, eta 1, %d pictures x %d row-slice chains, %d timed "
+                        "steps after %d warmup; parity: picture 0's chains re-decided by oracle/hvx_oracle_cu.c on %d host "
+                        "threads" % (pics, rows, steps, warmup, parity_threads),
+            "rd_metric": "HVX_RD_STVSSIM", "hist_n": len(hist), "per_qp": res}
 
 
 def slice_mode0_measure(W, H, chains=2040, distinct=16, nref=4, base_qp=32, warmup=1, steps=10):
@@ -682,6 +714,8 @@ def main():
         with torch.cuda.stream(work.stream):  # the gather reads what this step's launch wrote
             work.step(dpb.buffer(), ev)
             dpb.send()
+        if rank == 0:  # a progress line per launch queued (the queue runs at most a step or two ahead)
+            progress("headline step %d queued" % work.step_idx)
 
     def sync():
         dpb.drain()
@@ -756,10 +790,13 @@ def main():
         if world == 1:
             threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
             if not args.no_cpu_ref:
+                progress("reference HM on the host cores")
                 out["cpu_baseline"] = hm_cpu_reference(args.cpu_ref_procs or threads,
                                                        os.environ.get("TMPDIR", "/tmp"))
             if not args.no_cpu:
+                progress("restatement parity of the headline's CTUs")
                 port = hm_cpu_port(work, threads)
+                progress("merged bottom chain parity")
                 port["merged_chain"] = hm_merged_chain_parity(threads)
                 out["cpu_port"] = port
                 if out["cpu_baseline"] is None:
@@ -767,10 +804,13 @@ def main():
             del work, dpb
             torch.cuda.empty_cache()
             if not args.no_ra:
+                progress("config 4 (RA, stVSSIM cost)")
                 out["config4_ra_ssim"] = ra_ssim_measure(W, H)
             if not args.no_slice0:
+                progress("SliceMode 0 side figure")
                 out["slice_mode0"] = slice_mode0_measure(W, H)
             if not args.no_1080p:
+                progress("1080p side figure")
                 out["hm_1080p"] = hm_1080p_measure()
         print(json.dumps(out), flush=True)
     if world > 1:
