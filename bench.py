@@ -383,6 +383,11 @@ def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, 
     hist = stv_history_frames(W, H)
     dirs = hm.stv_direction_map(col_h, W, H)
     stv = hm.StvHistory(hist, dirs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stv.prepare(W, H)  # the history sums, once per history (once per picture in an encode)
+    torch.cuda.synchronize()
+    prep_ms = (time.perf_counter() - t0) * 1e3
     rows = hc - 1 if H % 64 else hc  # the partial bottom row chained after the row above (HmWorkload)
     res = {}
     for base_qp in qps:
@@ -434,7 +439,7 @@ def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, 
                         "the collocated field) in TEncCu's decisions, eta 1, %d pictures x %d row-slice chains, %d timed "
                         "steps after %d warmup; parity: picture 0's chains re-decided by oracle/hvx_oracle_cu.c on %d host "
                         "threads" % (pics, rows, steps, warmup, parity_threads),
-            "rd_metric": "HVX_RD_STVSSIM", "hist_n": len(hist), "per_qp": res}
+            "rd_metric": "HVX_RD_STVSSIM", "hist_n": len(hist), "stv_prepare_ms": round(prep_ms, 1), "per_qp": res}
 
 
 def slice_mode0_measure(W, H, chains=2040, distinct=16, nref=4, base_qp=32, warmup=1, steps=10):

@@ -357,6 +357,15 @@ int hvx_hm_job_status(hvx_ctx *ctx, const void *d_state, int n_jobs, int32_t *h_
  * TEncBinCABAC::finish (TEncBinCoderCABAC.cpp:81) and the byte alignment, from the result's registers. */
 int hvx_hm_write_slices(hvx_ctx *ctx, const hvx_hm_picture *d_pics, int n_pics, const hvx_hm_slice *d_slices,
                         int n_slices, void *d_state, hvx_hm_slice_result *d_out);
+/* HVX_RD_STVSSIM's history part, once per picture (hvx_hm_picture.stv_sums): compute_stVSSIM's
+ * (stvssim.c:651-702) five directional accumulators of every window after the hist_n history frames,
+ * for the windows the CU decision can evaluate -- luma 8x8 windows and chroma 8x8 / 4x4 windows on the
+ * 4-sample grid -- from h_pic's hist / hist_n / hist_stride / w / h (host copy of the descriptor).
+ * Layout (floats): luma [(h-8)/4+1][(w-8)/4+1][4 directions][mo, me, vo, ve, cov], then chroma 8x8
+ * [(h/2-8)/4+1][(w/2-8)/4+1][4][5], then chroma 4x4 [(h/2-4)/4+1][(w/2-4)/4+1][4][5]; chroma from the Cb
+ * history planes (which Cr reads too, hvx_types.h).  d_sums: hvx_hm_stv_sums_size bytes. */
+int hvx_hm_stv_sums_size(int w, int h, size_t *bytes);
+int hvx_hm_stv_prepare(hvx_ctx *ctx, const hvx_hm_picture *h_pic, float *d_sums);
 
 /* ---------------------------------------------------------------------------------------
  * The picture-level steps TEncGOP runs after compressSlice (TEncGOP.cpp:1465-1629), on a picture

@@ -331,9 +331,12 @@ typedef struct hvx_hm_picture {
    * final reconstruction, 8-bit, strides hist_stride[0] (luma) / [1] (chroma) -- Cr's history is read
    * from the Cb planes, as compute_stVSSIM is called with comp 1 for both chroma components (:846,
    * :850).  dirs: the direction map (pic_directions2: orientation in radians, one float per 4x4
-   * luma block, dirs_stride floats per row of blocks; getDirection_macroblock :1369). */
+   * luma block, dirs_stride floats per row of blocks; getDirection_macroblock :1369).
+   * stv_sums (optional, hvx_hm_stv_prepare): the history frames' part of every window's five
+   * directional sums, so a window adds only the current picture's samples (the same float sequence). */
   const uint8_t *const *hist;
   const float *dirs;
+  const float *stv_sums;
   int32_t hist_n, dirs_stride, hist_stride[2];
 } hvx_hm_picture;
 

@@ -109,7 +109,7 @@ def stv_history(g, pic):
     return frames, hm.stv_direction_map(col, w, h)
 
 
-def device_picture(g, pic, chained, entropy_bits, rd_metric=0, eta=1.0):
+def device_picture(g, pic, chained, entropy_bits, rd_metric=0, eta=1.0, stv_prepare=True):
     pi, pf = g["pic_i32"][pic], g["pic_f64"][pic]
     w, h = int(pi[P_W]), int(pi[P_H])
     psz = w * h * 3 // 2
@@ -129,10 +129,12 @@ def device_picture(g, pic, chained, entropy_bits, rd_metric=0, eta=1.0):
         params["rd_metric"], params["lambda_ssim"] = rd_metric, hm.lambda_ssim(int(pi[P_QP]), eta)
         if rd_metric == _abi.RD_STVSSIM:
             stv = hm.StvHistory(*stv_history(g, pic))
+            if stv_prepare:  # the history sums precomputed (hvx_hm_stv_prepare), else summed per window
+                stv.prepare(w, h)
     return hm.DevicePicture(org, refs, params, entropy_bits, rec=rec, ctus=ctus, col_field=col, stv=stv)
 
 
-def run_capture(name, mode, pics=None, stage=0, rd_metric=0, eta=1.0, serial=False):
+def run_capture(name, mode, pics=None, stage=0, rd_metric=0, eta=1.0, serial=False, stv_prepare=True):
     """Decide the captured pictures on the device.  mode 0: every CTU as its own job from the
     reference's entry state and neighbourhood; mode 1: one chained job per picture (per row slice
     for the row-sliced capture); mode 2: one chained job per picture across its row slices.  Returns
@@ -145,7 +147,7 @@ def run_capture(name, mode, pics=None, stage=0, rd_metric=0, eta=1.0, serial=Fal
     for pi_idx, pic in enumerate(pics):
         pi = g["pic_i32"][pic]
         first, n = int(pi[P_FIRST_CTU]), int(pi[P_NCTU])
-        dps.append(device_picture(g, pic, mode == 1, eb, rd_metric, eta))
+        dps.append(device_picture(g, pic, mode == 1, eb, rd_metric, eta, stv_prepare))
         plan.append((pic, first, n, slot))
         wc = (int(pi[P_W]) + 63) // 64
         rows = name in ROW_SLICES

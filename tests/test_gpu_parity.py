@@ -309,19 +309,21 @@ def test_hm_ctu_ssim_rdo_gpu(torch, name, eta):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,eta", [("ctu_ra_q22.bin", 1.0), ("ctu_ra_q27.bin", 0.7), ("ctu_ra_q32.bin", 1.0),
-                                      ("ctu_ra_q37.bin", 1.3)])
-def test_hm_ctu_stvssim_rdo_gpu(torch, name, eta):
+@pytest.mark.parametrize("name,eta,prep", [("ctu_ra_q22.bin", 1.0, True), ("ctu_ra_q27.bin", 0.7, True),
+                                           ("ctu_ra_q32.bin", 1.0, True), ("ctu_ra_q37.bin", 1.3, False)])
+def test_hm_ctu_stvssim_rdo_gpu(torch, name, eta, prep):
     """BASELINE config 4 with the reference's ACTIVE cost (att_stv.h:5 -> distortionstVSSIM,
     stvssim.c:831-855): hvx_hm_compress with HVX_RD_STVSSIM on the RA B pictures at QP 22 / 27 / 32 / 37,
     each with its stVSSIM history (the pictures coded before it, tests/hm_cases.stv_history: up to 4
     previous frames here) and direction map, chained per picture, against the restatement (cu_dstv
     through the pinned hvxo_stvssim): every decision, coefficient, reconstruction sample, bit count,
-    distortion and double cost bit-exact; and the cost decides differently from HM's SSE cost."""
+    distortion and double cost bit-exact; and the cost decides differently from HM's SSE cost.  prep:
+    the history part of the window sums precomputed per picture (hvx_hm_stv_prepare), else summed by
+    the engine per window."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import hm_ctu
     from video_codecs_amd import _abi, hm
-    g, plan, out = hm_cases.run_capture(name, 1, rd_metric=_abi.RD_STVSSIM, eta=eta)
+    g, plan, out = hm_cases.run_capture(name, 1, rd_metric=_abi.RD_STVSSIM, eta=eta, stv_prepare=prep)
 
     def ref(p):
         qp = int(g["pic_i32"][p[0]][hm_cases.P_QP])

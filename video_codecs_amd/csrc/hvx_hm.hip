@@ -101,6 +101,27 @@ static __global__ __launch_bounds__(64) void k_hm_write_slices(const hvx_hm_pict
   for (int i = l; i < 208; i += 64) o->states[i] = i < HVX_NUM_CTX ? hm_w.st[i] : 0;
 }
 
+// hvx_hm_stv_prepare: one thread per window of the three stv_sums tables (hm::stv_hist_acc)
+static __global__ __launch_bounds__(256) void k_stv_hist(const uint8_t *const *__restrict__ hist, int n_hist, int w, int h,
+                                                         int hs_y, int hs_c, float *__restrict__ sums) {
+  using namespace hm;
+  const int nx0 = (w - 8) / 4 + 1, ny0 = (h - 8) / 4 + 1, nx1 = ((w >> 1) - 8) / 4 + 1, ny1 = ((h >> 1) - 8) / 4 + 1;
+  const int nx2 = ((w >> 1) - 4) / 4 + 1, ny2 = ((h >> 1) - 4) / 4 + 1;
+  const long n0 = (long)nx0 * ny0, n1 = (long)nx1 * ny1, n2 = (long)nx2 * ny2;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n0 + n1 + n2) return;
+  int c, wint, px, py;
+  if (i < n0) { c = 0; wint = 8; py = (int)(i / nx0) * 4; px = (int)(i % nx0) * 4; }
+  else if (i < n0 + n1) { c = 1; wint = 8; py = (int)((i - n0) / nx1) * 4; px = (int)((i - n0) % nx1) * 4; }
+  else { c = 1; wint = 4; py = (int)((i - n0 - n1) / nx2) * 4; px = (int)((i - n0 - n1) % nx2) * 4; }
+  float wgta[4], wgtb[4], acc[20];
+  stv_weights(wint, n_hist + 1, wgta, wgtb);
+  for (int k = 0; k < 20; k++) acc[k] = 0.0f;
+  stv_hist_acc(hist, n_hist, c, c ? hs_c : hs_y, wint, px, py, wgta, wgtb, acc);
+  float *o = sums + 20 * i;
+  for (int k = 0; k < 20; k++) o[k] = acc[k];
+}
+
 int hvx_hm_module_init() { return upload_tables(); }
 
 extern "C" {
@@ -145,6 +166,26 @@ int hvx_hm_job_status(hvx_ctx *ctx, const void *d_state, int n_jobs, int32_t *h_
       hipStreamSynchronize(ctx->stream) != hipSuccess)
     return fail(HVX_E_HIP, "hvx_hm_job_status: copy failed");
   return HVX_OK;
+}
+
+int hvx_hm_stv_sums_size(int w, int h, size_t *bytes) {
+  if (!bytes || w < 16 || h < 16 || (w & 7) || (h & 7)) return fail(HVX_E_INVALID, "hvx_hm_stv_sums_size: bad args");
+  const size_t n = (size_t)((w - 8) / 4 + 1) * ((h - 8) / 4 + 1) + (size_t)((w / 2 - 8) / 4 + 1) * ((h / 2 - 8) / 4 + 1) +
+                   (size_t)((w / 2 - 4) / 4 + 1) * ((h / 2 - 4) / 4 + 1);
+  *bytes = n * 20 * sizeof(float);
+  return HVX_OK;
+}
+
+int hvx_hm_stv_prepare(hvx_ctx *ctx, const hvx_hm_picture *h_pic, float *d_sums) {
+  size_t bytes = 0;
+  if (!ctx || !h_pic || !d_sums || hvx_hm_stv_sums_size(h_pic->w, h_pic->h, &bytes) != HVX_OK ||
+      h_pic->hist_n < 0 || h_pic->hist_n > HVX_STV_HIST || (h_pic->hist_n > 0 && !h_pic->hist) ||
+      (h_pic->hist_n > 0 && (h_pic->hist_stride[0] < h_pic->w || h_pic->hist_stride[1] < h_pic->w / 2)))
+    return fail(HVX_E_INVALID, "hvx_hm_stv_prepare: bad args");
+  const long n = (long)(bytes / (20 * sizeof(float)));
+  hipLaunchKernelGGL(k_stv_hist, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, h_pic->hist, h_pic->hist_n,
+                     h_pic->w, h_pic->h, h_pic->hist_stride[0], h_pic->hist_stride[1], d_sums);
+  return launched("k_stv_hist");
 }
 
 int hvx_hm_write_slices(hvx_ctx *ctx, const hvx_hm_picture *d_pics, int n_pics, const hvx_hm_slice *d_slices,

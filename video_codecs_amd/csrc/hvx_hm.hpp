@@ -1994,7 +1994,7 @@ __device__ __forceinline__ float ssim_block16(const int16_t *o, const int16_t *r
 }
 // D of a CU: its 8x8 luma blocks, then 4x4 Cb, Cr blocks, one block per lane; the terms / 4 summed
 // in that order in double (blocks outside the picture skipped)
-__device__ double cu_dssim(const Cu *cu, Yuv *org, Yuv *reco) {
+__device__ __noinline__ double cu_dssim(const Cu *cu, Yuv *org, Yuv *reco) {
   const int n = cu->width >> 3, nb = n * n, total = 3 * nb;
   const int cx = cu->x, cy = cu->y;
   for (int k = lid(); k < total; k += 64) {
@@ -2012,18 +2012,9 @@ __device__ double cu_dssim(const Cu *cu, Yuv *org, Yuv *reco) {
   wsync();
   return d;
 }
-// The stVSSIM cost (HVX_RD_STVSSIM, include/hvx_types.h hvx_hm_picture.hist; restated by cu_dstv in
-// oracle/hvx_oracle_cu.c): distortionstVSSIM (stvssim.c:831-855) per 16x16 luma area of the CU.
-// One lane per window (compute_stVSSIM's loop body :655-811 in its float order): the four directional
-// 3-D SSIMs over the history frames (most recent first) and then the CU's own original /
-// reconstruction, accumulated in one pass over the samples (each accumulator receives its own terms in
-// the reference's order), the direction vote of calOrit (:336) on the map, and the plain SSIM of the
-// current frame; the window's ssim * ssim3d goes to E.ssim_t, averaged per block in window order.
-__device__ float stv_window(int c, int wint, int lx, int ly, int px, int py, const int16_t *org, const int16_t *rec,
-                            int ystr) {
-  const int used = E.P.hist_n + 1, hc = c == 2 ? 1 : c, uv = c ? 2 : 1;
+// compute_stVSSIM's directional weights for `used` frames (stvssim.c:615-640)
+__device__ __forceinline__ void stv_weights(int wint, int used, float *wgta, float *wgtb) {
   const float wa = 0.6f, wb = 1.0f - wa;
-  float wgta[4], wgtb[4];
   if (wint == 4) {
     wgta[0] = wgta[2] = wgta[1] = wgta[3] = wa / (wint * (used));
     wgtb[0] = wgtb[2] = wgtb[1] = wgtb[3] = wb / ((wint * wint - wint) * (used));
@@ -2033,32 +2024,76 @@ __device__ float stv_window(int c, int wint, int lx, int ly, int px, int py, con
     wgtb[0] = wgtb[2] = wb / ((wint * wint - 3 * wint) * (used));
     wgtb[1] = wgtb[3] = wb / ((wint * wint - 3 * wint + 2) * (used));
   }
-  const float C1 = 0.01f * 0.01f * (float)(255 * 255), C2 = 0.03f * 0.03f * (float)(255 * 255);
-  float mo[4] = {0, 0, 0, 0}, me[4] = {0, 0, 0, 0}, vo[4] = {0, 0, 0, 0}, ve[4] = {0, 0, 0, 0}, cv[4] = {0, 0, 0, 0};
-  const int hs = E.P.hist_stride[c ? 1 : 0];
-  for (int o = 0; o < used; o++) {
-    const bool cur = o == used - 1;
-    const uint8_t *ho = cur ? nullptr : E.P.hist[6 * o + hc] + (size_t)py * hs + px;
-    const uint8_t *hr = cur ? nullptr : E.P.hist[6 * o + 3 + hc] + (size_t)py * hs + px;
+}
+// the history frames' terms of one window's 4 x 5 directional sums (:665-699 for o < used - 1),
+// added to acc[k * 5 + {mo, me, vo, ve, cov}]: every accumulator receives its terms in the
+// reference's (o, n, m) order.  hist[6o + hc] / hist[6o + 3 + hc]: original / reconstruction plane
+__device__ __forceinline__ void stv_hist_acc(const uint8_t *const *hist, int n_hist, int hc, int hs, int wint, int px,
+                                             int py, const float *wgta, const float *wgtb, float *acc) {
+  for (int o = 0; o < n_hist; o++) {
+    const uint8_t *ho = hist[6 * o + hc] + (size_t)py * hs + px;
+    const uint8_t *hr = hist[6 * o + 3 + hc] + (size_t)py * hs + px;
     for (int n = 0; n < wint; n++)
       for (int m = 0; m < wint; m++) {
-        const int po = cur ? org[(ly + n) * ystr + lx + m] : ho[n * hs + m];
-        const int pe = cur ? rec[(ly + n) * ystr + lx + m] : hr[n * hs + m];
+        const int po = ho[n * hs + m], pe = hr[n * hs + m];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           const float wgt = orient_weight(k, wint, n, m, wgta[k], wgtb[k]);
-          mo[k] += wgt * po; me[k] += wgt * pe;
-          vo[k] += wgt * po * po; ve[k] += wgt * pe * pe; cv[k] += wgt * po * pe;
+          acc[k * 5 + 0] += wgt * po; acc[k * 5 + 1] += wgt * pe;
+          acc[k * 5 + 2] += wgt * po * po; acc[k * 5 + 3] += wgt * pe * pe; acc[k * 5 + 4] += wgt * po * pe;
         }
       }
   }
+}
+// the window's record in hvx_hm_picture.stv_sums (include/hvx.h hvx_hm_stv_prepare): c 0 luma 8x8, else
+// chroma 8x8 / 4x4 (wint), origin (px, py) on the 4-sample grid of the component
+__device__ __forceinline__ size_t stv_sums_window(int c, int wint, int px, int py, int w, int h) {
+  const int nx0 = (w - 8) / 4 + 1, ny0 = (h - 8) / 4 + 1;
+  if (c == 0) return (size_t)(py >> 2) * nx0 + (px >> 2);
+  const int nx1 = ((w >> 1) - 8) / 4 + 1, ny1 = ((h >> 1) - 8) / 4 + 1, nx2 = ((w >> 1) - 4) / 4 + 1;
+  if (wint == 8) return (size_t)ny0 * nx0 + (size_t)(py >> 2) * nx1 + (px >> 2);
+  return (size_t)ny0 * nx0 + (size_t)ny1 * nx1 + (size_t)(py >> 2) * nx2 + (px >> 2);
+}
+// The stVSSIM cost (HVX_RD_STVSSIM, include/hvx_types.h hvx_hm_picture.hist; restated by cu_dstv in
+// oracle/hvx_oracle_cu.c): distortionstVSSIM (stvssim.c:831-855) per 16x16 luma area of the CU.
+// One lane per window (compute_stVSSIM's loop body :655-811 in its float order): the four directional
+// 3-D SSIMs over the history frames (most recent first: from the picture's precomputed stv_sums, or
+// summed here) and then the CU's own original / reconstruction, the direction vote of calOrit (:336)
+// on the map, and the plain SSIM of the current frame; the window's ssim * ssim3d goes to E.ssim_t,
+// averaged per block in window order.
+__device__ float stv_window(int c, int wint, int lx, int ly, int px, int py, const int16_t *org, const int16_t *rec,
+                            int ystr) {
+  const int used = E.P.hist_n + 1, hc = c == 2 ? 1 : c, uv = c ? 2 : 1;
+  float wgta[4], wgtb[4];
+  stv_weights(wint, used, wgta, wgtb);
+  const float C1 = 0.01f * 0.01f * (float)(255 * 255), C2 = 0.03f * 0.03f * (float)(255 * 255);
+  float acc[20];
+  if (E.P.stv_sums) {
+    const float *t = E.P.stv_sums + 20 * stv_sums_window(c, wint, px, py, E.P.w, E.P.h);
+#pragma unroll
+    for (int i = 0; i < 20; i++) acc[i] = t[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 20; i++) acc[i] = 0.0f;
+    stv_hist_acc(E.P.hist, E.P.hist_n, hc, E.P.hist_stride[c ? 1 : 0], wint, px, py, wgta, wgtb, acc);
+  }
+  for (int n = 0; n < wint; n++)  // o = used - 1: the current picture
+    for (int m = 0; m < wint; m++) {
+      const int po = org[(ly + n) * ystr + lx + m], pe = rec[(ly + n) * ystr + lx + m];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const float wgt = orient_weight(k, wint, n, m, wgta[k], wgtb[k]);
+        acc[k * 5 + 0] += wgt * po; acc[k * 5 + 1] += wgt * pe;
+        acc[k * 5 + 2] += wgt * po * po; acc[k * 5 + 3] += wgt * pe * pe; acc[k * 5 + 4] += wgt * po * pe;
+      }
+    }
   float s3[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const float varo = fabsf(vo[k] - mo[k] * mo[k]), vare = fabsf(ve[k] - me[k] * me[k]);
-    const float covo = fabsf(cv[k] - mo[k] * me[k]);
-    float v = (float)((2.0 * mo[k] * me[k] + C1) * (2.0 * covo + C2));
-    v /= (float)(mo[k] * mo[k] + me[k] * me[k] + C1) * (varo + vare + C2);
+    const float mo = acc[k * 5], me = acc[k * 5 + 1], vo = acc[k * 5 + 2], ve = acc[k * 5 + 3], cv = acc[k * 5 + 4];
+    const float varo = fabsf(vo - mo * mo), vare = fabsf(ve - me * me), covo = fabsf(cv - mo * me);
+    float v = (float)((2.0 * mo * me + C1) * (2.0 * covo + C2));
+    v /= (float)(mo * mo + me * me + C1) * (varo + vare + C2);
     s3[k] = v;
     if (s3[k] >= 1.0 && s3[k] < 1.01) s3[k] = 1.0f;
   }
@@ -2101,7 +2136,7 @@ __device__ __forceinline__ float stv_block(const float *t, int nw) {
 }
 // D of a CU: tasks = per 16x16 area (raster) its 9 luma windows then the Cb and Cr window; an 8x8
 // CU: one luma, one Cb, one Cr window (4x4 chroma), weighted 1/4
-__device__ double cu_dstv(const Cu *cu, Yuv *org, Yuv *reco) {
+__device__ __noinline__ double cu_dstv(const Cu *cu, Yuv *org, Yuv *reco) {
   const bool small = cu->width == 8;
   const int n = small ? 1 : cu->width >> 4, per = small ? 3 : 11, total = n * n * per;
   for (int k = lid(); k < total; k += 64) {
@@ -2138,8 +2173,9 @@ __device__ __forceinline__ double cu_cost(double dssim, uint32_t bits, uint32_t 
   if (E.P.rd_metric == HVX_RD_SSE) return rd_cost(bits, dist);
   return dssim + E.P.lambda_ssim * ((double)bits > 0.5 ? (double)bits : 0.5);
 }
+// the SSIM measurements stay out of line: the SSE decision (the headline) keeps its callers' code
 __device__ __forceinline__ double measure_ssim(Cu *cu, Yuv *org, Yuv *reco) {
-  if (E.P.rd_metric == HVX_RD_SSE) return 0.0;
+  if (__builtin_expect(E.P.rd_metric == HVX_RD_SSE, 1)) return 0.0;
   const double d = E.P.rd_metric == HVX_RD_STVSSIM ? cu_dstv(cu, org, reco) : cu_dssim(cu, org, reco);
   cu->dssim = d;
   wsync();

@@ -47,7 +47,7 @@ class HmPicture(ctypes.Structure):
                 ("rec_stride", I32 * 2), ("ctus", P_), ("ref8", P_ * 8), ("ref16", (P_ * 3) * 8), ("ref8_stride", I32),
                 ("ref16_stride", I32 * 2), ("mvd_l1_zero", I32), ("l1_to_l0", I32 * 4), ("entropy_bits", P_),
                 ("rd_metric", I32), ("pad3_", I32), ("lambda_ssim", F64), ("hist", P_), ("dirs", P_),
-                ("hist_n", I32), ("dirs_stride", I32), ("hist_stride", I32 * 2)]
+                ("stv_sums", P_), ("hist_n", I32), ("dirs_stride", I32), ("hist_stride", I32 * 2)]
 
 
 def derive_lists(slice_type, nref, ref_poc):
@@ -162,6 +162,23 @@ class StvHistory:
         if dirs is not None:
             self.dirs = dirs if hasattr(dirs, "data_ptr") else torch.from_numpy(np.ascontiguousarray(dirs, np.float32)).to(device)
         self.dirs_stride = int(self.dirs.shape[1]) if self.dirs is not None else 0
+        self.sums = None
+
+    def prepare(self, w, h):
+        """hvx_hm_stv_prepare: the history frames' part of every window's directional sums, once for
+        the pictures this history serves (hvx_hm_picture.stv_sums); asynchronous on the context's
+        stream."""
+        import torch
+        from . import hvx
+        n = ctypes.c_size_t()
+        hvx._check(hvx.lib().hvx_hm_stv_sums_size(w, h, ctypes.byref(n)), "hvx_hm_stv_sums_size")
+        self.sums = torch.empty(n.value // 4, dtype=torch.float32, device=self.table.device)
+        s = HmPicture()
+        s.w, s.h, s.hist, s.hist_n = w, h, self.table.data_ptr(), self.n
+        s.hist_stride[0], s.hist_stride[1] = self.stride
+        hvx._check(hvx.lib().hvx_hm_stv_prepare(hvx.context(), ctypes.byref(s), ctypes.c_void_p(self.sums.data_ptr())),
+                   "hvx_hm_stv_prepare")
+        return self
 
 
 def pack_parts(rows):
@@ -375,6 +392,8 @@ class DevicePicture:
             s.hist_stride[0], s.hist_stride[1] = stv.stride
             if stv.dirs is not None:
                 s.dirs, s.dirs_stride = stv.dirs.data_ptr(), stv.dirs_stride
+            if stv.sums is not None:
+                s.stv_sums = stv.sums.data_ptr()
         self.struct = s
 
     def ctus(self):
