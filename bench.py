@@ -742,7 +742,7 @@ def main():
         bytes_per_launch = bpc * units
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         traffic = None
-        tr_path = os.path.join(ROOT, "profiles", "hbm_traffic_r04c.json")  # PMC passes of this round's tree
+        tr_path = os.path.join(ROOT, "profiles", "hbm_traffic_r05.json")  # PMC passes of this round's tree
         if os.path.exists(tr_path):
             tr = json.load(open(tr_path)).get("k_hm_compress")
             if tr:
@@ -750,11 +750,11 @@ def main():
         # the engine's real limiter, from the SQ counter passes of the same kernel on this round's
         # tree (scripts/gpu_hm_pmc.sh + scripts/hm_pmc_summary.py): issue fractions of the SIMDs
         issue = {}
-        pmc_path = os.path.join(ROOT, "profiles", "hm_pmc_r04c.json")
+        pmc_path = os.path.join(ROOT, "profiles", "hm_pmc_r05.json")
         if os.path.exists(pmc_path):
             pm = json.load(open(pmc_path))
             issue = {"simd_issue_frac": pm["simd_issue_frac"], "valu_frac": pm["valu_frac"],
-                     "wave_cycle_split": pm["wave_cycle_split"], "pmc_file": "profiles/hm_pmc_r04c.json"}
+                     "wave_cycle_split": pm["wave_cycle_split"], "pmc_file": "profiles/hm_pmc_r05.json"}
         out = {
             "metric": METRIC,
             "value": round(value, 2),
