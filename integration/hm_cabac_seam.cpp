@@ -31,8 +31,6 @@
 #include <cmath>
 #include <limits>
 #include <memory>
-#define private public
-#define protected public
 #include "TLibCommon/CommonDef.h"
 #include "TLibCommon/ContextModel.h"
 #include "TLibCommon/TComBitStream.h"
@@ -42,8 +40,7 @@
 #include "TLibEncoder/TEncSbac.h"
 #include "TLibEncoder/TEncBinCoderCABAC.h"
 #include "TLibEncoder/TEncBinCoderCABACCounter.h"
-#undef private
-#undef protected
+#include "hm_access.hpp"
 #include "hvx.h"
 
 #define CW_SYM _ZN8TEncSbac12codeCoeffNxNER6TComTUPi11ComponentID
@@ -143,8 +140,9 @@ Void TEncSbac::codeCoeffNxN(TComTU &rTu, TCoeff *pcCoef, const ComponentID compI
   for (Int i = 0; i < w * h; i++) lev[i] = (int32_t)pcCoef[i];
   uint8_t st[HVX_NUM_CTX];
   memset(st, 0, sizeof(st));
-  for (UInt i = 0; i < m_numContextModels; i++) st[i] = m_contextModels[i].m_ucState;
-  hvx_cabac_regs r = {bin->m_uiLow, bin->m_uiRange, bin->m_bitsLeft, bin->m_numBufferedBytes, bin->m_bufferedByte, 0,
+  for (UInt i = 0; i < m_numContextModels; i++) st[i] = hm_ctx_state(m_contextModels[i]);
+  hvx_cabac_regs r = {HM(bin, TEncBinCABAC_low), HM(bin, TEncBinCABAC_range), HM(bin, TEncBinCABAC_bits_left),
+                      HM(bin, TEncBinCABAC_n_buffered), HM(bin, TEncBinCABAC_buffered_byte), 0,
                       {0, 0, 0, 0, 0}};
   check(hvx_upload(c, g_cw.d_desc, &d, sizeof(d)), "hvx_upload");
   check(hvx_upload(c, g_cw.d_lev, lev, sizeof(int32_t) * w * h), "hvx_upload");
@@ -165,14 +163,14 @@ Void TEncSbac::codeCoeffNxN(TComTU &rTu, TCoeff *pcCoef, const ComponentID compI
     check(hvx_download(c, g_cw.bytes.data(), g_cw.d_out, (size_t)len), "hvx_download");
     check(hvx_sync(c), "hvx_sync");
   }
-  for (int32_t i = 0; i < len; i++) bin->m_pcTComBitIf->write(g_cw.bytes[i], 8);  // writeOut's output
-  bin->m_uiLow = r.low;
-  bin->m_uiRange = r.range;
-  bin->m_bitsLeft = r.bits_left;
-  bin->m_numBufferedBytes = r.num_buffered;
-  bin->m_bufferedByte = r.buffered_byte;
-  bin->m_uiBinsCoded += r.bins * bin->m_binCountIncrement;
-  for (UInt i = 0; i < m_numContextModels; i++) m_contextModels[i].m_ucState = st[i];
+  for (int32_t i = 0; i < len; i++) HM(bin, TEncBinCABAC_bitif)->write(g_cw.bytes[i], 8);  // writeOut's output
+  HM(bin, TEncBinCABAC_low) = r.low;
+  HM(bin, TEncBinCABAC_range) = r.range;
+  HM(bin, TEncBinCABAC_bits_left) = r.bits_left;
+  HM(bin, TEncBinCABAC_n_buffered) = r.num_buffered;
+  HM(bin, TEncBinCABAC_buffered_byte) = r.buffered_byte;
+  HM(bin, TEncBinCABAC_bins) += r.bins * HM(bin, TEncBinCABAC_bin_inc);
+  for (UInt i = 0; i < m_numContextModels; i++) hm_set_ctx_state(m_contextModels[i], st[i]);
   // encodeBin's setBinsCoded(1) (TEncBinCoderCABAC.cpp:203) for every context the writer coded:
   // determineCabacInitIdx (ContextModel3DBuffer::calcCost) reads it for the next slice's table
   for (UInt m = 42; m < 202 && m < m_numContextModels; m++)

@@ -35,8 +35,6 @@
 #include <cmath>
 #include <limits>
 #include <memory>
-#define private public
-#define protected public
 #include "TLibCommon/CommonDef.h"
 #include "TLibCommon/ContextModel.h"
 #include "TLibCommon/TComRom.h"
@@ -50,8 +48,7 @@
 #include "TLibEncoder/TEncSearch.h"
 #include "TLibEncoder/TEncSbac.h"
 #include "TLibEncoder/TEncBinCoderCABAC.h"
-#undef private
-#undef protected
+#include "hm_access.hpp"
 #include "hvx.h"
 
 #define CU_SYM _ZN6TEncCu11compressCtuEP10TComDataCU
@@ -188,7 +185,7 @@ bool begin_picture(TEncCu *cu, TComDataCU *ctu) {
                   sps.getUseStrongIntraSmoothing() && !pps.getConstrainedIntraPred() && pps.getSignHideFlag() &&
                   pps.getUseTransformSkip() && pps.getPpsRangeExtension().getLog2MaxTransformSkipBlockSize() == 2;
   // the encoder tool set the engine decides with (encoder_lowdelay_P_main.cfg's search and RD options)
-  TEncCfg *cfg = cu->m_pcEncCfg;
+  TEncCfg *cfg = HM(cu, TEncCu_cfg);
   const bool tools = cfg->getUseRDOQ() && cfg->getUseRDOQTS() && !cfg->getUseSelectiveRDOQ() && cfg->getFastSearch() == 1 &&
                      cfg->getUseHADME() && cfg->getUseFastEnc() && cfg->getUseFastDecisionForMerge() &&
                      !cfg->getUseEarlySkipDetection() && !cfg->getUseCbfFastMode() && !cfg->getUseEarlyCU() &&
@@ -227,7 +224,7 @@ bool begin_picture(TEncCu *cu, TComDataCU *ctu) {
     }
   P.mvd_l1_zero = st == B_SLICE && s->getMvdL1ZeroFlag();
   for (int i = 0; i < 4; i++) P.l1_to_l0[i] = (st == B_SLICE && i < nref1) ? s->getList1IdxToList0Idx(i) : -1;
-  P.bipred_range = cu->m_pcPredSearch->m_bipredSearchRange;
+  P.bipred_range = HM(HM(cu, TEncCu_search), TEncSearch_bipred_range);
   for (int c = 1; c < 3; c++) {
     const QpParam q(*ctu, ComponentID(c));  // getScaledChromaQP of the slice QP
     P.chroma_qp[c - 1] = q.Qp;
@@ -236,14 +233,14 @@ bool begin_picture(TEncCu *cu, TComDataCU *ctu) {
   P.tmvp = s->getEnableTMVPFlag();
   P.check_ldc = s->getCheckLDC();
   P.col_from_l0 = s->getColFromL0Flag();
-  P.search_range = cu->m_pcEncCfg->getSearchRange();
+  P.search_range = HM(cu, TEncCu_cfg)->getSearchRange();
   P.amp = sps.getUseAMP();
-  P.lambda_motion = cu->m_pcRdCost->m_uiLambdaMotionSAD[0];
-  P.lambda = cu->m_pcRdCost->getLambda();
-  P.sqrt_lambda = cu->m_pcRdCost->m_sqrtLambda;
-  P.chroma_weight[0] = cu->m_pcRdCost->m_distortionWeight[1];
-  P.chroma_weight[1] = cu->m_pcRdCost->m_distortionWeight[2];
-  for (int c = 0; c < 3; c++) P.tq_lambda[c] = cu->m_pcTrQuant->m_lambdas[c];
+  P.lambda_motion = HM(HM(cu, TEncCu_rdcost), TComRdCost_lambda_motion_sad)[0];
+  P.lambda = HM(cu, TEncCu_rdcost)->getLambda();
+  P.sqrt_lambda = HM(HM(cu, TEncCu_rdcost), TComRdCost_sqrt_lambda);
+  P.chroma_weight[0] = HM(HM(cu, TEncCu_rdcost), TComRdCost_dist_weight)[1];
+  P.chroma_weight[1] = HM(HM(cu, TEncCu_rdcost), TComRdCost_dist_weight)[2];
+  for (int c = 0; c < 3; c++) P.tq_lambda[c] = HM(HM(cu, TEncCu_trquant), TComTrQuant_lambdas)[c];
   // the original (8-bit planes, stride = width)
   for (int c = 0; c < 3; c++) {
     const ComponentID id = ComponentID(c);
@@ -317,7 +314,11 @@ bool begin_picture(TEncCu *cu, TComDataCU *ctu) {
   }
   // ContextModel::m_entropyBits (the counter's rate table)
   int32_t ebits[128];
-  for (int i = 0; i < 128; i++) ebits[i] = (int32_t)ContextModel::m_entropyBits[i];
+  for (int i = 0; i < 128; i++) {  // m_entropyBits[state byte i], through a model in that state
+    ContextModel m;
+    hm_set_ctx_state(m, (UChar)i);
+    ebits[i] = (int32_t)m.getEntropyBits(0);
+  }
   void *deb = g.eb.get(sizeof(ebits));
   upload(deb, ebits, sizeof(ebits));
   P.entropy_bits = (const int32_t *)deb;
@@ -336,39 +337,39 @@ bool begin_picture(TEncCu *cu, TComDataCU *ctu) {
 void write_ctu(TComDataCU *ctu, const hvx_hm_ctu &o) {
   for (int z = 0; z < 256; z++) {
     const hvx_hm_part &p = o.p[z];
-    ctu->m_puhDepth[z] = (UChar)p.depth;
-    ctu->m_puhWidth[z] = ctu->m_puhHeight[z] = p.width;
-    ctu->m_pePartSize[z] = p.part;
-    ctu->m_pePredMode[z] = p.pred;
-    ctu->m_skipFlag[z] = p.skip != 0;
-    ctu->m_pbMergeFlag[z] = p.merge != 0;
-    ctu->m_puhMergeIndex[z] = (UChar)p.merge_idx;
-    ctu->m_puhInterDir[z] = (UChar)p.inter_dir;
+    ctu->getDepth()[z] = (UChar)p.depth;
+    ctu->getWidth()[z] = ctu->getHeight()[z] = p.width;
+    ctu->getPartitionSize()[z] = p.part;
+    ctu->getPredictionMode()[z] = p.pred;
+    ctu->getSkipFlag()[z] = p.skip != 0;
+    ctu->getMergeFlag()[z] = p.merge != 0;
+    ctu->getMergeIndex()[z] = (UChar)p.merge_idx;
+    ctu->getInterDir()[z] = (UChar)p.inter_dir;
     for (int l = 0; l < 2; l++) {
-      TComCUMvField &f = ctu->m_acCUMvField[l];
-      f.m_pcMv[z] = TComMv(p.mv[l][0], p.mv[l][1]);
-      f.m_pcMvd[z] = TComMv(p.mvd[l][0], p.mvd[l][1]);
-      f.m_piRefIdx[z] = p.ref[l];
-      ctu->m_apiMVPIdx[l][z] = p.mvp_idx[l];
-      ctu->m_apiMVPNum[l][z] = p.mvp_num[l];
+      TComCUMvField *f = ctu->getCUMvField(RefPicList(l));
+      const_cast<TComMv &>(f->getMv(z)) = TComMv(p.mv[l][0], p.mv[l][1]);
+      const_cast<TComMv &>(f->getMvd(z)) = TComMv(p.mvd[l][0], p.mvd[l][1]);
+      HM(f, TComCUMvField_ref_idx)[z] = p.ref[l];
+      ctu->getMVPIdx(RefPicList(l))[z] = p.mvp_idx[l];
+      ctu->getMVPNum(RefPicList(l))[z] = p.mvp_num[l];
     }
-    ctu->m_puhIntraDir[CHANNEL_TYPE_LUMA][z] = p.idir[0];
-    ctu->m_puhIntraDir[CHANNEL_TYPE_CHROMA][z] = p.idir[1];
-    ctu->m_puhTrIdx[z] = (UChar)p.tr_idx;
+    ctu->getIntraDir(CHANNEL_TYPE_LUMA)[z] = p.idir[0];
+    ctu->getIntraDir(CHANNEL_TYPE_CHROMA)[z] = p.idir[1];
+    ctu->getTransformIdx()[z] = (UChar)p.tr_idx;
     for (int c = 0; c < 3; c++) {
-      ctu->m_puhTransformSkip[c][z] = p.ts[c];
-      ctu->m_puhCbf[c][z] = p.cbf[c];
+      ctu->getTransformSkip(ComponentID(c))[z] = p.ts[c];
+      ctu->getCbf(ComponentID(c))[z] = p.cbf[c];
     }
-    ctu->m_phQP[z] = p.qp;
+    ctu->getQP()[z] = p.qp;
   }
   for (int c = 0; c < 3; c++) {
     const int n = c ? 1024 : 4096, off = c == 0 ? 0 : c == 1 ? 4096 : 5120;
-    TCoeff *dst = ctu->m_pcTrCoeff[c];
+    TCoeff *dst = ctu->getCoeff(ComponentID(c));
     for (int i = 0; i < n; i++) dst[i] = o.coef[off + i];
   }
-  ctu->m_uiTotalBits = o.bits;
-  ctu->m_uiTotalDistortion = o.dist;
-  ctu->m_dTotalCost = o.cost;
+  ctu->getTotalBits() = o.bits;
+  ctu->getTotalDistortion() = o.dist;
+  ctu->getTotalCost() = o.cost;
 }
 
 // xCopyYuv2Pic of the CTU's reconstruction (the window; samples outside the picture are not written)
@@ -404,13 +405,13 @@ bool batch_picture(TEncCu *self, TComDataCU *ctu) {
   std::vector<hvx_hm_job> jobs;
   hvx_hm_job j;
   memset(&j, 0, sizeof(j));
-  TEncSbac *sb = self->m_pppcRDSbacCoder[0][CI_CURR_BEST];
-  for (int i = 0; i < HVX_NUM_CTX; i++) j.entry.st[i] = i < (int)sb->m_numContextModels ? sb->m_contextModels[i].m_ucState : 0;
-  j.entry.frac = ((TEncBinCABAC *)sb->m_pcBinIf)->m_fracBits;
+  TEncSbac *sb = HM(self, TEncCu_rdcoders)[0][CI_CURR_BEST];
+  for (int i = 0; i < HVX_NUM_CTX; i++) j.entry.st[i] = i < (int)HM(sb, TEncSbac_n_models) ? hm_ctx_state(HM(sb, TEncSbac_models)[i]) : 0;
+  j.entry.frac = HM((TEncBinCABAC *)HM(sb, TEncSbac_bin), TEncBinCABAC_frac);
   for (int l = 0; l < 2; l++)
     for (int i = 0; i < 4; i++) {
-      j.int2n[(l * 4 + i) * 2] = (int16_t)self->m_pcPredSearch->m_integerMv2Nx2N[l][i].getHor();
-      j.int2n[(l * 4 + i) * 2 + 1] = (int16_t)self->m_pcPredSearch->m_integerMv2Nx2N[l][i].getVer();
+      j.int2n[(l * 4 + i) * 2] = (int16_t)HM(HM(self, TEncCu_search), TEncSearch_int2n)[l][i].getHor();
+      j.int2n[(l * 4 + i) * 2 + 1] = (int16_t)HM(HM(self, TEncCu_search), TEncSearch_int2n)[l][i].getVer();
     }
   j.chained = 1;
   g.slice_first.assign(n, 0);
@@ -480,10 +481,10 @@ extern "C" void CAT(__wrap_, CU_SYM)(TEncCu *self, TComDataCU *ctu) {
     // the entry coder HM holds now must be the one the device chain carried into this CTU (the
     // previous CTU's encodeCtu state), except at slice starts (resetEntropy)
     if (a > 0 && !g.slice_first[a]) {
-      TEncSbac *sb = self->m_pppcRDSbacCoder[0][CI_CURR_BEST];
-      bool same = ((TEncBinCABAC *)sb->m_pcBinIf)->m_fracBits == g.b_cod[a - 1].frac;
-      for (int i = 0; i < (int)sb->m_numContextModels && i < HVX_NUM_CTX; i++)
-        same = same && sb->m_contextModels[i].m_ucState == g.b_cod[a - 1].st[i];
+      TEncSbac *sb = HM(self, TEncCu_rdcoders)[0][CI_CURR_BEST];
+      bool same = HM((TEncBinCABAC *)HM(sb, TEncSbac_bin), TEncBinCABAC_frac) == g.b_cod[a - 1].frac;
+      for (int i = 0; i < (int)HM(sb, TEncSbac_n_models) && i < HVX_NUM_CTX; i++)
+        same = same && hm_ctx_state(HM(sb, TEncSbac_models)[i]) == g.b_cod[a - 1].st[i];
       if (!same) g.state_mismatch++;
     }
     write_ctu(ctu, g.b_ctu[a]);
@@ -505,13 +506,13 @@ extern "C" void CAT(__wrap_, CU_SYM)(TEncCu *self, TComDataCU *ctu) {
   j.slice_start = (int)s->getSliceCurStartCtuTsAddr();  // one tile: TS order = raster order
   j.slice_end = (int)s->getSliceCurEndCtuTsAddr() - 1;
   // the RD coder the decision starts from and the search's integer 2Nx2N MVs (cu_capture.cpp)
-  TEncSbac *sb = self->m_pppcRDSbacCoder[0][CI_CURR_BEST];
-  for (int i = 0; i < HVX_NUM_CTX; i++) j.entry.st[i] = i < (int)sb->m_numContextModels ? sb->m_contextModels[i].m_ucState : 0;
-  j.entry.frac = ((TEncBinCABAC *)sb->m_pcBinIf)->m_fracBits;
+  TEncSbac *sb = HM(self, TEncCu_rdcoders)[0][CI_CURR_BEST];
+  for (int i = 0; i < HVX_NUM_CTX; i++) j.entry.st[i] = i < (int)HM(sb, TEncSbac_n_models) ? hm_ctx_state(HM(sb, TEncSbac_models)[i]) : 0;
+  j.entry.frac = HM((TEncBinCABAC *)HM(sb, TEncSbac_bin), TEncBinCABAC_frac);
   for (int l = 0; l < 2; l++)
     for (int i = 0; i < 4; i++) {
-      j.int2n[(l * 4 + i) * 2] = (int16_t)self->m_pcPredSearch->m_integerMv2Nx2N[l][i].getHor();
-      j.int2n[(l * 4 + i) * 2 + 1] = (int16_t)self->m_pcPredSearch->m_integerMv2Nx2N[l][i].getVer();
+      j.int2n[(l * 4 + i) * 2] = (int16_t)HM(HM(self, TEncCu_search), TEncSearch_int2n)[l][i].getHor();
+      j.int2n[(l * 4 + i) * 2 + 1] = (int16_t)HM(HM(self, TEncCu_search), TEncSearch_int2n)[l][i].getVer();
     }
   upload(g.job.p, &j, sizeof(j));
   check(hvx_hm_compress(c, (const hvx_hm_picture *)g.pic.p, 1, (const hvx_hm_job *)g.job.p, 1, 1, g.state.p,

@@ -25,16 +25,13 @@
 #include <cmath>
 #include <limits>
 #include <memory>
-#define private public
-#define protected public
 #include "TLibCommon/CommonDef.h"
 #include "TLibCommon/TComPrediction.h"
 #include "TLibCommon/TComDataCU.h"
 #include "TLibCommon/TComTU.h"
 #include "TLibCommon/TComPic.h"
 #include "TLibCommon/TComSlice.h"
-#undef private
-#undef protected
+#include "hm_access.hpp"
 #include "hvx.h"
 
 #define PRED_SYM _ZN14TComPrediction12predIntraAngE11ComponentIDjPsjS1_jR6TComTUbbbb
@@ -109,7 +106,7 @@ extern "C" void CAT(__wrap_, PRED_SYM)(TComPrediction *self, ComponentID compID,
   g.init();
   hvx_ctx *c = hvx_seam_ctx();
   // HM's unfiltered border around the block at (1, 1) of the staging plane (stride 2n+1 buffer)
-  const Pel *B = self->m_piYuvExt[compID][PRED_BUF_UNFILTERED];
+  const Pel *B = HM(self, TComPrediction_yuv_ext)[compID][PRED_BUF_UNFILTERED];
   const int s = 2 * n + 1;
   uint8_t *P = g.plane.data();
   P[0] = (uint8_t)B[0];

@@ -23,8 +23,6 @@
 #include <cmath>
 #include <limits>
 #include <memory>
-#define private public
-#define protected public
 #include "TLibCommon/CommonDef.h"
 #include "TLibCommon/TComRom.h"
 #include "TLibCommon/TComLoopFilter.h"
@@ -33,8 +31,7 @@
 #include "TLibCommon/TComPic.h"
 #include "TLibCommon/TComPicYuv.h"
 #include "TLibCommon/TComSlice.h"
-#undef private
-#undef protected
+#include "hm_access.hpp"
 #include "hvx.h"
 
 #define LF_SYM _ZN14TComLoopFilter13loopFilterPicEP7TComPic
@@ -64,14 +61,14 @@ void bs_walk(TComLoopFilter &lf, TComDataCU *cu, UInt abs, UInt depth, DeblockEd
     }
     return;
   }
-  lf.xSetLoopfilterParam(cu, abs);
+  HM(&lf, TComLoopFilter_set_param)(cu, abs);
   TComTURecurse tu(cu, abs);
-  lf.xSetEdgefilterTU(tu);
-  lf.xSetEdgefilterPU(cu, abs);
+  HM(&lf, TComLoopFilter_set_tu)(tu);
+  HM(&lf, TComLoopFilter_set_pu)(cu, abs);
   const UInt pels = sps.getMaxCUWidth() >> sps.getMaxTotalCUDepth();
   for (UInt p = abs; p < abs + cur; p++) {
     const UInt chk = pels == 4 ? ((dir == EDGE_VER && p % 2 == 0) || (dir == EDGE_HOR && (p - ((p >> 2) << 2)) / 2 == 0)) : 1;
-    if (lf.m_aapbEdgeFilter[dir][p] && chk) lf.xGetBoundaryStrengthSingle(cu, dir, p);
+    if (HM(&lf, TComLoopFilter_edge)[dir][p] && chk) HM(&lf, TComLoopFilter_bs_single)(cu, dir, p);
   }
 }
 
@@ -113,19 +110,19 @@ extern "C" void CAT(__wrap_, LF_SYM)(TComLoopFilter *self, TComPic *pic) {
   {
     TComLoopFilter lf;
     lf.create(sps.getMaxTotalCUDepth());
-    lf.setCfg(self->m_bLFCrossTileBoundary);
+    lf.setCfg(HM(self, TComLoopFilter_cross_tile));
     const int ctu_w = sps.getMaxCUWidth(), ctus_x = (W + ctu_w - 1) / ctu_w;
     for (int dir = 0; dir < 2; dir++)
       for (UInt a = 0; a < pic->getNumberOfCtusInFrame(); a++) {
         TComDataCU *ctu = pic->getCtu(a);
-        memset(lf.m_aapucBS[dir], 0, lf.m_uiNumPartitions);
-        memset(lf.m_aapbEdgeFilter[dir], 0, lf.m_uiNumPartitions);
+        memset(HM(&lf, TComLoopFilter_bs)[dir], 0, HM(&lf, TComLoopFilter_n_parts));
+        memset(HM(&lf, TComLoopFilter_edge)[dir], 0, HM(&lf, TComLoopFilter_n_parts));
         bs_walk(lf, ctu, 0, 0, (DeblockEdgeDir)dir);
         const int x0 = (a % ctus_x) * ctu_w, y0 = (a / ctus_x) * ctu_w;
-        for (UInt p = 0; p < lf.m_uiNumPartitions; p++) {
+        for (UInt p = 0; p < HM(&lf, TComLoopFilter_n_parts); p++) {
           const int x = x0 + g_auiRasterToPelX[g_auiZscanToRaster[p]], y = y0 + g_auiRasterToPelY[g_auiZscanToRaster[p]];
           if (x >= W || y >= H) continue;
-          g.bs[dir][(y / 4) * uw + x / 4] = lf.m_aapucBS[dir][p];
+          g.bs[dir][(y / 4) * uw + x / 4] = HM(&lf, TComLoopFilter_bs)[dir][p];
           if (dir == 0) g.qp[(y / 4) * uw + x / 4] = (int8_t)ctu->getQP(p);
         }
       }

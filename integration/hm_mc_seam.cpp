@@ -23,8 +23,6 @@
 #include <cmath>
 #include <limits>
 #include <memory>
-#define private public
-#define protected public
 #include "TLibCommon/CommonDef.h"
 #include "TLibCommon/TComPrediction.h"
 #include "TLibCommon/TComDataCU.h"
@@ -32,8 +30,7 @@
 #include "TLibCommon/TComPicYuv.h"
 #include "TLibCommon/TComSlice.h"
 #include "TLibCommon/TComYuv.h"
-#undef private
-#undef protected
+#include "hm_access.hpp"
 #include "hvx.h"
 
 #define MC_SYM _ZN14TComPrediction18motionCompensationEP10TComDataCUP7TComYuv10RefPicListi

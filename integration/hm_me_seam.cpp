@@ -36,8 +36,6 @@
 #include <cmath>
 #include <limits>
 #include <memory>
-#define private public
-#define protected public
 #include "TLibCommon/CommonDef.h"
 #include "TLibCommon/TComDataCU.h"
 #include "TLibCommon/TComPic.h"
@@ -46,8 +44,7 @@
 #include "TLibCommon/TComYuv.h"
 #include "TLibEncoder/TEncSearch.h"
 #include "TLibEncoder/TEncCfg.h"
-#undef private
-#undef protected
+#include "hm_access.hpp"
 #include "hvx.h"
 
 #define ME_SYM _ZN10TEncSearch17xMotionEstimationEP10TComDataCUP7TComYuvi10RefPicListP6TComMviRS5_RjS8_b
@@ -168,7 +165,7 @@ Void TEncSearch::xMotionEstimation(TComDataCU *pcCU, TComYuv *pcYuvOrg, Int iPar
   }
   j.bits_in = (int32_t)ruiBits;
   j.search_range = iSrchRng;
-  j.lambda_motion = m_pcRdCost->m_uiLambdaMotionSAD[0];
+  j.lambda_motion = HM(m_pcRdCost, TComRdCost_lambda_motion_sad)[0];
   j.flags = (m_pcEncCfg->getUseFastEnc() ? HVX_ME_FEN : 0) | (m_pcEncCfg->getUseHADME() ? HVX_ME_HADME : 0) |
             (m_pcEncCfg->getFastMEAssumingSmootherMVEnabled() ? HVX_ME_SMOOTHMV : 0) | (bBi ? HVX_ME_BI : 0);
   const TComMv centre = bBi ? rcMv : *pcMvPred;  // xSetSearchRange centre (:3723-3730)

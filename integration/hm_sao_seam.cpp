@@ -29,8 +29,6 @@
 #include <cmath>
 #include <limits>
 #include <memory>
-#define private public
-#define protected public
 #include "TLibCommon/CommonDef.h"
 #include "TLibCommon/TComPic.h"
 #include "TLibCommon/TComPicSym.h"
@@ -38,8 +36,7 @@
 #include "TLibCommon/TComSlice.h"
 #include "TLibCommon/TComSampleAdaptiveOffset.h"
 #include "TLibEncoder/TEncSampleAdaptiveOffset.h"
-#undef private
-#undef protected
+#include "hm_access.hpp"
 #include "hvx.h"
 
 #define SAO_SYM _ZN24TEncSampleAdaptiveOffset10SAOProcessEP7TComPicPbPKdbddb
@@ -123,22 +120,22 @@ extern "C" void CAT(__wrap_, SAO_SYM)(TEncSampleAdaptiveOffset *self, TComPic *p
                                        const Double *lambdas, const Bool testOff, const Double rate,
                                        const Double rateChroma, Bool preDbf) {
   const TComSPS &sps = pic->getPicSym()->getSPS();
-  const int W = self->m_picWidth, H = self->m_picHeight;
+  const int W = HM(self, TComSao_width), H = HM(self, TComSao_height);
   const bool ok = !preDbf && pic->getChromaFormat() == CHROMA_420 && sps.getBitDepth(CHANNEL_TYPE_LUMA) == 8 &&
                   sps.getBitDepth(CHANNEL_TYPE_CHROMA) == 8 && W % 8 == 0 && H % 8 == 0 &&
                   pic->getNumAllocatedSlice() == 1 && pic->getPicSym()->getNumTiles() == 1 &&
-                  self->m_maxCUWidth == 64 && self->m_maxCUHeight == 64;
+                  HM(self, TComSao_ctu_w) == 64 && HM(self, TComSao_ctu_h) == 64;
   if (!ok) {
     g.fell++;
     CAT(__real_, SAO_SYM)(self, pic, sliceEnabled, lambdas, testOff, rate, rateChroma, preDbf);
     return;
   }
   hvx_ctx *c = hvx_seam_ctx();
-  const int nctu = self->m_numCTUsPic;
+  const int nctu = HM(self, TComSao_n_ctus);
   // SAOProcess :243-249
   TComPicYuv *orgYuv = pic->getPicYuvOrg(), *resYuv = pic->getPicYuvRec();
-  memcpy(self->m_lambda, lambdas, sizeof(self->m_lambda));
-  TComPicYuv *srcYuv = self->m_tempPicYuv;
+  memcpy(HM(self, TEncSao_lambda), lambdas, sizeof(HM(self, TEncSao_lambda)));
+  TComPicYuv *srcYuv = HM(self, TComSao_temp_yuv);
   resYuv->copyToPic(srcYuv);
   srcYuv->setBorderExtension(false);
   srcYuv->extendPicBorder();
@@ -164,18 +161,18 @@ extern "C" void CAT(__wrap_, SAO_SYM)(TEncSampleAdaptiveOffset *self, TComPic *p
     for (int k = 0; k < 3; k++)
       for (int t = 0; t < NUM_SAO_NEW_TYPES; t++) {
         const hvx_sao_stat &s = g.stats[((size_t)u * 3 + k) * HVX_SAO_TYPES + t];
-        SAOStatData &d = self->m_statData[u][k][t];
+        SAOStatData &d = HM(self, TEncSao_stat)[u][k][t];
         for (int i = 0; i < MAX_NUM_SAO_CLASSES; i++) { d.diff[i] = s.diff[i]; d.count[i] = s.count[i]; }
       }
   // :257-262 the reference's decisions; its offsetCTU calls are recorded, not applied
-  self->decidePicParams(sliceEnabled, pic->getSlice(0)->getDepth(), rate, rateChroma);
+  HM(self, TEncSao_decide_pic)(sliceEnabled, pic->getSlice(0)->getDepth(), rate, rateChroma);
   SAOBlkParam *reconParams = new SAOBlkParam[nctu];
   hvx_sao_ctu off;
   memset(&off, 0, sizeof(off));
   for (int k = 0; k < 3; k++) off.comp[k].type = HVX_SAO_OFF;
   g.params.assign(nctu, off);
   g.deferring = true;
-  self->decideBlkParams(pic, sliceEnabled, self->m_statData, srcYuv, resYuv, reconParams,
+  HM(self, TEncSao_decide_blk)(pic, sliceEnabled, HM(self, TEncSao_stat), srcYuv, resYuv, reconParams,
                         pic->getPicSym()->getSAOBlkParam(), testOff, rate, rateChroma);
   g.deferring = false;
   delete[] reconParams;

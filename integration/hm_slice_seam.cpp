@@ -29,8 +29,6 @@
 #include <cmath>
 #include <limits>
 #include <memory>
-#define private public
-#define protected public
 #include "TLibCommon/CommonDef.h"
 #include "TLibCommon/ContextModel.h"
 #include "TLibCommon/TComRom.h"
@@ -44,8 +42,7 @@
 #include "TLibEncoder/TEncSbac.h"
 #include "TLibEncoder/TEncBinCoderCABAC.h"
 #include "TLibEncoder/TEncEntropy.h"
-#undef private
-#undef protected
+#include "hm_access.hpp"
 #include "hvx.h"
 
 #define SLICE_SYM _ZN9TEncSlice11encodeSliceEP7TComPicP19TComOutputBitstreamRj
@@ -95,40 +92,40 @@ SliceSeam g;
 void upload(void *d, const void *h, size_t n) { check(hvx_upload(hvx_seam_ctx(), d, h, n), "hvx_upload"); }
 
 // the decided CTU as TComDataCU holds it (copyToPic, TComDataCU.cpp:945) -> hvx_hm_ctu
-void pack_ctu(const TComDataCU *ctu, hvx_hm_ctu &o) {
+void pack_ctu(TComDataCU *ctu, hvx_hm_ctu &o) {
   memset(&o, 0, sizeof(o));
   for (int z = 0; z < 256; z++) {
     hvx_hm_part &p = o.p[z];
-    p.depth = (int8_t)ctu->m_puhDepth[z];
-    p.width = ctu->m_puhWidth[z];
-    p.part = (int8_t)ctu->m_pePartSize[z];
-    p.pred = (int8_t)ctu->m_pePredMode[z];
-    p.skip = ctu->m_skipFlag[z] ? 1 : 0;
-    p.merge = ctu->m_pbMergeFlag[z] ? 1 : 0;
-    p.merge_idx = (int8_t)ctu->m_puhMergeIndex[z];
-    p.inter_dir = (int8_t)ctu->m_puhInterDir[z];
+    p.depth = (int8_t)ctu->getDepth(z);
+    p.width = ctu->getWidth(z);
+    p.part = (int8_t)ctu->getPartitionSize(z);
+    p.pred = (int8_t)ctu->getPredictionMode(z);
+    p.skip = ctu->getSkipFlag(z) ? 1 : 0;
+    p.merge = ctu->getMergeFlag(z) ? 1 : 0;
+    p.merge_idx = (int8_t)ctu->getMergeIndex(z);
+    p.inter_dir = (int8_t)ctu->getInterDir(z);
     for (int l = 0; l < 2; l++) {
-      const TComCUMvField &f = ctu->m_acCUMvField[l];
-      p.mv[l][0] = (int16_t)f.m_pcMv[z].getHor();
-      p.mv[l][1] = (int16_t)f.m_pcMv[z].getVer();
-      p.mvd[l][0] = (int16_t)f.m_pcMvd[z].getHor();
-      p.mvd[l][1] = (int16_t)f.m_pcMvd[z].getVer();
-      p.ref[l] = (int8_t)f.m_piRefIdx[z];
-      p.mvp_idx[l] = (int8_t)ctu->m_apiMVPIdx[l][z];
-      p.mvp_num[l] = (int8_t)ctu->m_apiMVPNum[l][z];
+      const TComCUMvField *f = ctu->getCUMvField(RefPicList(l));
+      p.mv[l][0] = (int16_t)f->getMv(z).getHor();
+      p.mv[l][1] = (int16_t)f->getMv(z).getVer();
+      p.mvd[l][0] = (int16_t)f->getMvd(z).getHor();
+      p.mvd[l][1] = (int16_t)f->getMvd(z).getVer();
+      p.ref[l] = (int8_t)f->getRefIdx(z);
+      p.mvp_idx[l] = (int8_t)ctu->getMVPIdx(RefPicList(l))[z];
+      p.mvp_num[l] = (int8_t)ctu->getMVPNum(RefPicList(l))[z];
     }
-    p.idir[0] = ctu->m_puhIntraDir[CHANNEL_TYPE_LUMA][z];
-    p.idir[1] = ctu->m_puhIntraDir[CHANNEL_TYPE_CHROMA][z];
-    p.tr_idx = (int8_t)ctu->m_puhTrIdx[z];
+    p.idir[0] = ctu->getIntraDir(CHANNEL_TYPE_LUMA, z);
+    p.idir[1] = ctu->getIntraDir(CHANNEL_TYPE_CHROMA, z);
+    p.tr_idx = (int8_t)ctu->getTransformIdx(z);
     for (int c = 0; c < 3; c++) {
-      p.ts[c] = ctu->m_puhTransformSkip[c][z];
-      p.cbf[c] = ctu->m_puhCbf[c][z];
+      p.ts[c] = ctu->getTransformSkip(z, ComponentID(c));
+      p.cbf[c] = ctu->getCbf(z, ComponentID(c));
     }
-    p.qp = ctu->m_phQP[z];
+    p.qp = ctu->getQP(z);
   }
   for (int c = 0; c < 3; c++) {
     const int n = c ? 1024 : 4096, off = c == 0 ? 0 : c == 1 ? 4096 : 5120;
-    const TCoeff *src = ctu->m_pcTrCoeff[c];
+    const TCoeff *src = ctu->getCoeff(ComponentID(c));
     for (int i = 0; i < n; i++) o.coef[off + i] = (int16_t)src[i];
   }
 }
@@ -189,15 +186,17 @@ extern "C" void CAT(__wrap_, SLICE_SYM)(TEncSlice *self, TComPic *pic, TComOutpu
   const int start = (int)s->getSliceSegmentCurStartCtuTsAddr(), bound = (int)s->getSliceSegmentCurEndCtuTsAddr();
   const int wc = (int)sym->getFrameWidthInCtus(), nctu = (int)sym->getNumberOfCtusInFrame();
   // TEncSlice::encodeSlice's set-up (TEncSlice.cpp:930-938)
-  self->m_pcSbacCoder->init((TEncBinIf *)self->m_pcBinCABAC);
-  self->m_pcEntropyCoder->setEntropyCoder(self->m_pcSbacCoder);
-  self->m_pcEntropyCoder->resetEntropy(s);
+  TEncSbac *sb = HM(self, TEncSlice_sbac);
+  TEncBinCABAC *bin = HM(self, TEncSlice_cabac);
+  TEncEntropy *ent = HM(self, TEncSlice_entropy);
+  sb->init((TEncBinIf *)bin);
+  ent->setEntropyCoder(sb);
+  ent->resetEntropy(s);
   num_bins = 0;
-  self->m_pcBinCABAC->setBinCountingEnableFlag(true);
-  self->m_pcBinCABAC->setBinsCoded(0);
+  bin->setBinCountingEnableFlag(true);
+  bin->setBinsCoded(0);
   TComOutputBitstream &bs = subs[pic->getSubstreamForCtuAddr(sym->getCtuTsToRsAddrMap(start), true, s)];
-  self->m_pcEntropyCoder->setBitstream(&bs);
-  TEncSbac *sb = self->m_pcSbacCoder;
+  ent->setBitstream(&bs);
 
   // the picture as the writer reads it (hvx_hm_picture: geometry, slice parameters, the CTU array)
   hvx_hm_picture P;
@@ -242,7 +241,7 @@ extern "C" void CAT(__wrap_, SLICE_SYM)(TEncSlice *self, TComPic *pic, TComOutpu
   const int cap = 1 << 24;
   j.out = (uint8_t *)g.out.get(cap);
   j.out_cap = cap;
-  for (int i = 0; i < HVX_NUM_CTX; i++) j.entry.st[i] = i < (int)sb->m_numContextModels ? sb->m_contextModels[i].m_ucState : 0;
+  for (int i = 0; i < HVX_NUM_CTX; i++) j.entry.st[i] = i < (int)HM(sb, TEncSbac_n_models) ? hm_ctx_state(HM(sb, TEncSbac_models)[i]) : 0;
   void *djob = g.job.get(sizeof(j));
   upload(djob, &j, sizeof(j));
   size_t sbytes = 0;
@@ -262,29 +261,29 @@ extern "C" void CAT(__wrap_, SLICE_SYM)(TEncSlice *self, TComPic *pic, TComOutpu
   if (r.n_bytes) check(hvx_download(hvx_seam_ctx(), bytes.data(), j.out, bytes.size()), "hvx_download");
   // the bytes TEncBinCABAC::writeOut wrote, then its registers, bin count and the contexts
   for (uint8_t b : bytes) bs.write(b, 8);
-  TEncBinCABAC *bin = self->m_pcBinCABAC;
-  bin->m_uiLow = r.low;
-  bin->m_uiRange = r.range;
-  bin->m_bitsLeft = r.bits_left;
-  bin->m_numBufferedBytes = r.num_buffered;
-  bin->m_bufferedByte = r.buffered_byte;
-  bin->m_uiBinsCoded += r.bins * bin->m_binCountIncrement;
-  for (int m = 0; m < (int)sb->m_numContextModels && m < HVX_NUM_CTX; m++) {
-    sb->m_contextModels[m].m_ucState = r.states[m];
-    if ((r.coded[m >> 5] >> (m & 31)) & 1u) sb->m_contextModels[m].setBinsCoded(1);
+  HM(bin, TEncBinCABAC_low) = r.low;
+  HM(bin, TEncBinCABAC_range) = r.range;
+  HM(bin, TEncBinCABAC_bits_left) = r.bits_left;
+  HM(bin, TEncBinCABAC_n_buffered) = r.num_buffered;
+  HM(bin, TEncBinCABAC_buffered_byte) = r.buffered_byte;
+  HM(bin, TEncBinCABAC_bins) += r.bins * HM(bin, TEncBinCABAC_bin_inc);
+  ContextModel *models = HM(sb, TEncSbac_models);
+  for (int m = 0; m < (int)HM(sb, TEncSbac_n_models) && m < HVX_NUM_CTX; m++) {
+    hm_set_ctx_state(models[m], r.states[m]);
+    if ((r.coded[m >> 5] >> (m & 31)) & 1u) models[m].setBinsCoded(1);
   }
   // the end of the slice (TEncSlice.cpp:1084-1090) and of encodeSlice (:1097-1114)
-  self->m_pcEntropyCoder->encodeTerminatingBit(1);
-  self->m_pcEntropyCoder->encodeSliceFinish();
+  ent->encodeTerminatingBit(1);
+  ent->encodeSliceFinish();
   bs.writeByteAlignment();
 #if ADAPTIVE_QP_SELECTION
-  if (self->m_pcCfg->getUseAdaptQpSelect()) self->m_pcTrQuant->storeSliceQpNext(s);
+  if (HM(self, TEncSlice_cfg)->getUseAdaptQpSelect()) HM(self, TEncSlice_trquant)->storeSliceQpNext(s);
 #endif
   if (s->getPPS()->getCabacInitPresentFlag() && !s->getPPS()->getDependentSliceSegmentsEnabledFlag())
-    self->m_encCABACTableIdx = self->m_pcEntropyCoder->determineCabacInitIdx(s);
+    HM(self, TEncSlice_cabac_idx) = ent->determineCabacInitIdx(s);
   else
-    self->m_encCABACTableIdx = s->getSliceType();
-  num_bins = self->m_pcBinCABAC->getBinsCoded();
+    HM(self, TEncSlice_cabac_idx) = s->getSliceType();
+  num_bins = bin->getBinsCoded();
   g.served++;
   g.bytes += r.n_bytes;
 }

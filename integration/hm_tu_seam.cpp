@@ -26,16 +26,13 @@
 #include <cmath>
 #include <limits>
 #include <memory>
-#define private public
-#define protected public
 #include "TLibCommon/CommonDef.h"
 #include "TLibCommon/TComTrQuant.h"
 #include "TLibCommon/TComDataCU.h"
 #include "TLibCommon/TComTU.h"
 #include "TLibCommon/TComSlice.h"
 #include "TLibCommon/TComChromaFormat.h"
-#undef private
-#undef protected
+#include "hm_access.hpp"
 #include "hvx.h"
 
 #define FWD_SYM _ZN11TComTrQuant12transformNxNER6TComTU11ComponentIDPsjPiS4_RiRK7QpParam
@@ -95,10 +92,10 @@ static void fill_desc(TComTrQuant *self, TComTU &rTu, ComponentID compID, const 
   d.qp_per = qp.per;
   d.qp_rem = qp.rem;
   d.sign_hiding = sl->getPPS()->getSignHideFlag() ? 1 : 0;
-  d.use_rdoq = self->m_useRDOQ;
-  d.use_rdoq_ts = self->m_useRDOQTS;
-  d.selective_rdoq = self->m_useSelectiveRDOQ;
-  d.adaptive_qp_select = self->m_bUseAdaptQpSelect;
+  d.use_rdoq = HM(self, TComTrQuant_rdoq);
+  d.use_rdoq_ts = HM(self, TComTrQuant_rdoq_ts);
+  d.selective_rdoq = HM(self, TComTrQuant_selective_rdoq);
+  d.adaptive_qp_select = HM(self, TComTrQuant_adapt_qp);
   d.transquant_bypass = cu->getCUTransquantBypass(idx) ? 1 : 0;
   d.golomb_rice_stat = self->m_pcEstBitsSbac->golombRiceAdaptationStatistics[rTu.getGolombRiceStatisticsIndex(compID)];
   d.persistent_rice = sps->getSpsRangeExtension().getPersistentRiceAdaptationEnabledFlag() ? 1 : 0;
@@ -106,7 +103,7 @@ static void fill_desc(TComTrQuant *self, TComTU &rTu, ComponentID compID, const 
   d.ts_context = sps->getSpsRangeExtension().getTransformSkipContextEnabledFlag() ? 1 : 0;
   d.max_log2_tr_range = sps->getMaxLog2TrDynamicRange(ch);
   d.bit_depth = sps->getBitDepth(ch);
-  d.lambda = self->m_dLambda;
+  d.lambda = HM(self, TComTrQuant_lambda);
 }
 
 extern "C" void CAT(__wrap_, FWD_SYM)(TComTrQuant *self, TComTU &rTu, ComponentID compID, Pel *res, UInt stride,
