@@ -1,12 +1,14 @@
 """The writer rank's shared decoded-picture buffer.
 
-CTUs shard across GPUs by independent closed GOP segments, one per rank.  After every picture
-each rank's reference picture -- the padded 8-bit plane hvx_ctu_decide wrote: the reconstruction
-deblocked, borders extended, i.e. a ready reference picture -- is gathered to rank 0 with ONE torch.distributed
-gather per picture (RCCL over xGMI on the GPUs; gloo in the CPU tests).  The gather is the only
-data-path collective of the path.  It is asynchronous and the reconstruction buffers are
-double-buffered, so picture k+1 is analysed while picture k's samples move; a buffer is handed
-out again only after the gather that read it has completed.  Rank 0 keeps one plane per rank.
+CTUs shard across GPUs by independent GOP segments (pictures), one set per rank.  After every
+decision launch each rank's reconstructed CTU windows of that launch (hvx_hm_compress's d_out_rec:
+per CTU the pre-loop-filter Y | Cb | Cr window, 6144 bytes) are gathered to rank 0 with ONE
+torch.distributed gather (RCCL over xGMI on the GPUs; gloo in the CPU tests) -- the shared DPB the
+writer rank assembles pictures in.  The gather is the only data-path collective of the path; a
+rank's own reference pictures for its segments are made locally (hvx_hm_finish_picture) and never
+cross xGMI.  It is asynchronous and the output buffers are double-buffered, so launch k+1 decides
+while launch k's windows move; a buffer is handed out again only after the gather that read it has
+completed.  Rank 0 keeps one buffer per rank.
 """
 
 
@@ -22,7 +24,7 @@ class DpbGather:
         self.pending = [None] * nbuf
 
     def buffer(self):
-        """The reconstruction buffer of the current picture (waits for the gather that last read it)."""
+        """The output buffer of the current launch (waits for the gather that last read it)."""
         b = self.k % self.nbuf
         if self.pending[b] is not None:
             self.pending[b].wait()
@@ -30,7 +32,7 @@ class DpbGather:
         return self.recon[b]
 
     def send(self):
-        """Gather the current picture to rank 0 (no-op on one rank) and advance; returns its buffer index."""
+        """Gather the current launch's windows to rank 0 (no-op on one rank) and advance; returns its buffer index."""
         import torch.distributed as dist
         b = self.k % self.nbuf
         if self.world > 1:
