@@ -509,6 +509,44 @@ def hm_1080p_measure(pics=128, nref=4, base_qp=32, warmup=1, steps=10):
         "wall_ms_per_step": round(wall * 1e3, 1)}
 
 
+def slice_writer_measure(work, done, cap=1 << 18):
+    """Side figure: the slice data of the headline's decided CTUs written on the device
+    (hvx_hm_write_slices: TEncSlice::encodeSlice's CTU loop, every CTU's CU syntax through
+    TEncBinCABAC, one wave per slice) -- every chain's first `done` CTUs as one slice from the
+    slice-start context states, all 2046 slices in one launch, timed with HIP events."""
+    import torch
+    from video_codecs_amd import hm
+    wc = work.wc
+    n = work.n_jobs
+    out = torch.zeros(n * cap, dtype=torch.uint8, device="cuda")
+    sl = np.zeros(n, hm.HM_SLICE)
+    for p in range(work.pics):
+        for r in range(work.rows):
+            k = p * work.rows + r
+            sl[k]["pic"], sl[k]["first_ctu"], sl[k]["n_ctus"], sl[k]["out_cap"] = p, r * wc, done, cap
+            sl[k]["out"] = out.data_ptr() + k * cap
+            sl[k]["entry"]["st"] = work.entry
+    sl_t = torch.from_numpy(sl.view(np.uint8).reshape(-1).copy()).cuda()
+    res_t = torch.zeros(n * hm.HM_SLICE_RESULT.itemsize, dtype=torch.uint8, device="cuda")
+    ms = []
+    with torch.cuda.stream(work.stream):
+        for rep in range(3):
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+            work.eng.write_slices_launch(sl_t, n, res_t)
+            ev[1].record()
+            ev[1].synchronize()
+            ms.append(ev[0].elapsed_time(ev[1]))
+    res = res_t.cpu().numpy().view(hm.HM_SLICE_RESULT)
+    assert (res["status"] == 0).all() and (res["n_bytes"] <= cap).all(), "hvx_hm_write_slices refused a slice"
+    t = min(ms) * 1e-3
+    nbytes = int(res["n_bytes"].sum())
+    return {"workload": "%d slices x %d decided CTUs of the headline's pictures (CU syntax + coefficients through "
+                        "TEncBinCABAC, no SAO), one launch, best of 3" % (n, done),
+            "ctus_per_s": round(n * done / t, 1), "launch_ms": round(t * 1e3, 2), "bytes": nbytes,
+            "bits_per_ctu": round(8.0 * nbytes / (n * done), 1), "bins_per_ctu": round(float(res["bins"].sum()) / (n * done), 1)}
+
+
 def _kept_records(work, positions):
     """The GPU's records of picture 0's chains from HmWorkload.keep_steps: {(chain, position):
     (parts, coef, recon, cost, (bits, dist))} for the chain positions in `positions` (first pass)."""
@@ -798,6 +836,8 @@ def main():
                 progress("reference HM on the host cores")
                 out["cpu_baseline"] = hm_cpu_reference(args.cpu_ref_procs or threads,
                                                        os.environ.get("TMPDIR", "/tmp"))
+            progress("slice writer side figure")
+            out["slice_writer"] = slice_writer_measure(work, args.warmup + args.steps)
             if not args.no_cpu:
                 progress("restatement parity of the headline's CTUs")
                 port = hm_cpu_port(work, threads)

@@ -270,3 +270,26 @@ def test_hm_picture_layout_matches_header(tmp_path):
     got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     want = [ctypes.sizeof(hm.HmPicture)] + [getattr(hm.HmPicture, f).offset for f in fields]
     assert got == want
+
+
+def test_hm_record_layouts_match_header(tmp_path):
+    """The numpy records of the engine's and the slice writer's device structs (hm.HM_JOB, HM_CTU,
+    HM_SLICE, HM_SLICE_RESULT) have the C sizes and field offsets of include/hvx_types.h."""
+    import subprocess
+    from video_codecs_amd import hm
+    recs = {"hvx_hm_job": hm.HM_JOB, "hvx_hm_ctu": hm.HM_CTU, "hvx_hm_slice": hm.HM_SLICE,
+            "hvx_hm_slice_result": hm.HM_SLICE_RESULT}
+    src = tmp_path / "rec.c"
+    body = ""
+    for cn, dt in recs.items():
+        body += 'printf("%%zu ", sizeof(%s));' % cn
+        for f in dt.names:
+            body += 'printf("%%zu ", offsetof(%s, %s));' % (cn, f)
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "hvx_types.h"\nint main(void){' + body + "return 0;}\n")
+    exe = tmp_path / "rec"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    want = []
+    for dt in recs.values():
+        want += [dt.itemsize] + [dt.fields[f][1] for f in dt.names]
+    assert got == want

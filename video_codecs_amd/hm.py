@@ -33,6 +33,15 @@ HM_JOB = np.dtype([("pic", "<i4"), ("first_ctu", "<i4"), ("n_ctus", "<i4"), ("ch
                    ("int2n", "<i2", 16)], align=True)
 assert HM_JOB.itemsize == 280
 
+HM_SLICE = np.dtype([("pic", "<i4"), ("first_ctu", "<i4"), ("n_ctus", "<i4"), ("out_cap", "<i4"),
+                     ("sao_enabled", "<i4", 3), ("pad_", "<i4"), ("sao_coded", "<u8"), ("out", "<u8"),
+                     ("entry", HM_CODER)], align=True)
+assert HM_SLICE.itemsize == 264
+HM_SLICE_RESULT = np.dtype([("low", "<u4"), ("range", "<u4"), ("bits_left", "<i4"), ("num_buffered", "<i4"),
+                            ("buffered_byte", "<u4"), ("bins", "<u4"), ("n_bytes", "<i4"), ("status", "<i4"),
+                            ("coded", "<u4", 7), ("pad_", "<u4"), ("states", "u1", 208)])
+assert HM_SLICE_RESULT.itemsize == 272
+
 P_, I32, U32, F64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_double
 
 
@@ -464,6 +473,35 @@ class Engine:
         hvx._check(hvx.lib().hvx_hm_job_status(hvx.context(), ctypes.c_void_p(self.state.data_ptr()), n_jobs,
                                                st.ctypes.data_as(ctypes.c_void_p)), "hvx_hm_job_status")
         return st
+
+    def write_slices_launch(self, slices_t, n, res_t):
+        """Enqueue hvx_hm_write_slices on torch's current stream: device HM_SLICE array slices_t (their
+        out pointers into device buffers), n slices, HM_SLICE_RESULT bytes res_t."""
+        from . import hvx
+        self.reserve(n)
+        P = ctypes.c_void_p
+        hvx._check(hvx.lib().hvx_hm_write_slices(hvx.context(), P(self.pics_t.data_ptr()), len(self.pictures),
+                                                 P(slices_t.data_ptr()), n, P(self.state.data_ptr()),
+                                                 P(res_t.data_ptr())), "hvx_hm_write_slices")
+
+    def write_slices(self, specs, cap=1 << 20):
+        """The slice data of decided pictures (TEncSlice::encodeSlice's CTU loop through TEncBinCABAC):
+        specs = [(pic, first_ctu, n_ctus, entry_states)] (no SAO); returns [(bytes, HM_SLICE_RESULT)]."""
+        import torch
+        n = len(specs)
+        out = torch.zeros(n * cap, dtype=torch.uint8, device=self.device)
+        sl = np.zeros(n, HM_SLICE)
+        for k, (pic, first, cnt, entry) in enumerate(specs):
+            sl[k]["pic"], sl[k]["first_ctu"], sl[k]["n_ctus"], sl[k]["out_cap"] = pic, first, cnt, cap
+            sl[k]["out"] = out.data_ptr() + k * cap
+            sl[k]["entry"]["st"] = entry
+        sl_t = torch.from_numpy(sl.view(np.uint8).reshape(-1).copy()).to(self.device)
+        res_t = torch.zeros(n * HM_SLICE_RESULT.itemsize, dtype=torch.uint8, device=self.device)
+        self.write_slices_launch(sl_t, n, res_t)
+        torch.cuda.synchronize()
+        res = res_t.cpu().numpy().view(HM_SLICE_RESULT)
+        o = out.cpu().numpy().reshape(n, cap)
+        return [(o[k, :min(int(res[k]["n_bytes"]), cap)].tobytes(), res[k]) for k in range(n)]
 
     def compress(self, jobs, n_out):
         """Run the jobs (HM_JOB array); returns (ctus [n_out] HM_CTU, rec [n_out, 6144] uint8,

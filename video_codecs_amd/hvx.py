@@ -43,7 +43,7 @@ def lib():
             "hvx_estbits_update": [P, P, P, I, I, I, P], "hvx_estbits_batch": [P, P, P, P, P, I, P],
             "hvx_mc_batch": [P, P, I, I, P, I, P], "hvx_coeff_bits_batch": [P, P, P, I, P, P, P, P], "hvx_coeff_write_batch": [P, P, P, P, P, I, P, P, P, P, I, P], "hvx_me_full_batch": [P, P, I, P, I, P, I, P],
             "hvx_intra_pred_batch": [P, P, I, P, I, P, P, P], "hvx_deblock": [P, P, I, P, P, I, P, P, P, P], "hvx_sao_stats": [P, P, P, P, I, I, P, P, P, I, I, I, I, P], "hvx_sao_apply": [P, P, P, P, I, I, P, P, P, I, I, I, I, P], "hvx_intra_search_batch": [P, P, P, I, P, I, P, P], "hvx_alloc": [P, ctypes.c_size_t, ctypes.POINTER(P)],
-            "hvx_free": [P, P], "hvx_hm_state_size": [ctypes.POINTER(ctypes.c_size_t)], "hvx_hm_compress": [P, P, I, P, I, I, P, P, P, P], "hvx_hm_job_status": [P, P, I, P], "hvx_hm_stv_sums_size": [I, I, ctypes.POINTER(ctypes.c_size_t)], "hvx_hm_stv_prepare": [P, P, P], "hvx_hm_finish_picture": [P, P, P, P, P, P, I, P, P, P, I, I], "hvx_sao_decide": [P, P, I], "hvx_upload": [P, P, P, ctypes.c_size_t], "hvx_download": [P, P, P, ctypes.c_size_t],
+            "hvx_free": [P, P], "hvx_hm_state_size": [ctypes.POINTER(ctypes.c_size_t)], "hvx_hm_compress": [P, P, I, P, I, I, P, P, P, P], "hvx_hm_job_status": [P, P, I, P], "hvx_hm_stv_sums_size": [I, I, ctypes.POINTER(ctypes.c_size_t)], "hvx_hm_stv_prepare": [P, P, P], "hvx_hm_write_slices": [P, P, I, P, I, P, P], "hvx_hm_finish_picture": [P, P, P, P, P, P, I, P, P, P, I, I], "hvx_sao_decide": [P, P, I], "hvx_upload": [P, P, P, ctypes.c_size_t], "hvx_download": [P, P, P, ctypes.c_size_t],
         }.items():
             f = getattr(L, name)
             f.argtypes = args
