@@ -102,3 +102,105 @@ def test_two_rank_hm_workload_gloo(tmp_path):
         exp = _hm_step(bench.HmPlan(HW, HH, HPICS, HNREF, QP, (HW + 63) // 64, r))
         np.testing.assert_array_equal(own.reshape(-1, 6144), exp)
     assert not np.array_equal(dpb[0], dpb[1])
+
+
+# ---- closed GOP segments per rank (config 5's unit), decided by the restatement ----
+def _closed_segment(g, rank):
+    """The LDP segment of tests/golden/ctu_ldp_nosao.bin (I, P, P; SAO off) decided in closed loop by
+    the restatement: every picture from the capture's original and slice-start states only, each P
+    picture against the reference pictures this loop made (restatement decisions -> boundary
+    strengths -> oracle loopFilterPic), never the capture's.  Returns [(poc, parts, recon planes,
+    reference planes)]."""
+    import oracle
+    from oracle import hm_ctu
+    from tests import hm_cases
+    from video_codecs_amd import _abi
+    made = {}
+    out = []
+    gl = dict(g)
+    refpoc = [int(p) for p in g["refpic_poc"]]
+    for pic, pi in enumerate(g["pic_i32"]):
+        poc, w, h = int(pi[hm_cases.P_POC]), int(pi[hm_cases.P_W]), int(pi[hm_cases.P_H])
+        first, n = int(pi[hm_cases.P_FIRST_CTU]), int(pi[hm_cases.P_NCTU])
+        psz = w * h * 3 // 2
+        # the references this loop made, in the capture's reference-plane slots
+        rp = np.array(g["refpic"], copy=True)
+        for k, q in enumerate(refpoc):
+            if q in made:
+                rp[k * psz:(k + 1) * psz] = np.concatenate([p.reshape(-1) for p in made[q]])
+            elif q < poc:
+                raise AssertionError("reference POC %d not made yet" % q)
+        gl["refpic"] = rp
+        r = hm_ctu.replay(gl, pic, mode=1)
+        rec = [np.zeros((h >> (1 if c else 0), w >> (1 if c else 0)), np.uint8) for c in range(3)]
+        wc = (w + 63) // 64
+        for a in range(n):
+            ax, ay = a % wc, a // wc
+            t = r["recon"][a]
+            yy, xx = min(64, h - ay * 64), min(64, w - ax * 64)
+            rec[0][ay * 64:ay * 64 + yy, ax * 64:ax * 64 + xx] = t[:4096].reshape(64, 64)[:yy, :xx]
+            for c in (1, 2):
+                cpl = t[4096 + (c - 1) * 1024:4096 + c * 1024].reshape(32, 32)
+                rec[c][ay * 32:ay * 32 + yy // 2, ax * 32:ax * 32 + xx // 2] = cpl[:yy // 2, :xx // 2]
+        rpoc = np.array([pi[hm_cases.P_REFPOC0:hm_cases.P_REFPOC0 + 4], pi[hm_cases.P_REFPOC1:hm_cases.P_REFPOC1 + 4]])
+        bv, bh, qp = hm_ctu.boundary_strength(w, h, r["parts"], rpoc, int(pi[hm_cases.P_SLICE_TYPE]) == 0)
+        ref = oracle.deblock(*rec, bv.reshape(-1), bh.reshape(-1), qp.reshape(-1), _abi.deblock_params(w, h))
+        made[poc] = ref
+        out.append((poc, r["parts"], rec, ref))
+    return out
+
+
+def _closed_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tests import golden_cases as gc
+    from video_codecs_amd.dpb import DpbGather
+    g = gc.load("ctu_ldp_nosao.bin")
+    w, h = int(g["pic_i32"][0][0]), int(g["pic_i32"][0][1])
+    seg = _closed_segment(g, rank)
+    # every finished reference picture of the rank's segment goes to rank 0's DPB
+    dpb = DpbGather(world, rank, (w * h * 3 // 2,), "cpu")
+    got = []
+    for poc, _, _, ref in seg:
+        buf = dpb.buffer()
+        buf.copy_(torch.from_numpy(np.concatenate([p.reshape(-1) for p in ref])))
+        b = dpb.send()
+        dpb.drain()
+        if rank == 0:
+            got.append(np.stack([t.numpy().copy() for t in dpb.dpb[b]]))
+    np.save(os.path.join(outdir, f"closed_parts{rank}.npy"), np.stack([s[1] for s in seg]))
+    if rank == 0:
+        np.save(os.path.join(outdir, "closed_dpb.npy"), np.stack(got))
+        np.save(os.path.join(outdir, "closed_refs0.npy"),
+                np.stack([np.concatenate([p.reshape(-1) for p in s[3]]) for s in seg]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_closed_segments_gloo(tmp_path):
+    """Config 5's unit on two ranks (gloo): each rank encodes a closed LDP segment (I, P, P) with the
+    restatement -- every P picture decided against the reference pictures its own loop made (the
+    restatement's decisions, boundary strengths and loopFilterPic), not the capture's -- and every
+    picture equals HM's own decisions (tests/golden/ctu_ldp_nosao.bin, SAO off); every finished
+    reference picture goes to rank 0 through DpbGather, where each rank's copy equals that rank's."""
+    import torch.multiprocessing as tmp
+    from tests import golden_cases as gc
+    from tests import hm_cases
+    world = 2
+    tmp.spawn(_closed_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    g = gc.load("ctu_ldp_nosao.bin")
+    for r in range(world):
+        parts = np.load(tmp_path / f"closed_parts{r}.npy")
+        for pic, pi in enumerate(g["pic_i32"]):
+            first, n = int(pi[hm_cases.P_FIRST_CTU]), int(pi[hm_cases.P_NCTU])
+            np.testing.assert_array_equal(parts[pic], g["ctu_parts"][first:first + n], err_msg=f"rank {r} pic {pic}")
+    dpb, refs0 = np.load(tmp_path / "closed_dpb.npy"), np.load(tmp_path / "closed_refs0.npy")
+    assert dpb.shape[:2] == (3, world)
+    for k in range(3):
+        for r in range(world):
+            np.testing.assert_array_equal(dpb[k, r], refs0[k])  # the same segment on both ranks here
+    # the made references equal HM's reference pictures
+    psz = refs0.shape[1]
+    for k, q in enumerate(int(p) for p in g["refpic_poc"]):
+        np.testing.assert_array_equal(refs0[q], g["refpic"][k * psz:(k + 1) * psz])
