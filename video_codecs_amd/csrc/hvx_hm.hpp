@@ -242,6 +242,10 @@ struct Enc {
   int pad_;
   Coder cod[37];
   hvx_estbits est;
+#ifndef HM_NO_EST_MEMO
+  uint32_t est_key;      // (w | h << 8 | ch << 16) + 1 of the last estimate_bit (0: none this CTU)
+  uint32_t est_st[38];   // its coder's context states 28 .. 179 (every byte estBit reads)
+#endif
   int32_t eb[128];
   uint8_t next[256];
   uint16_t scan[256];    // the current TU's scan tables (TUs up to 16x16), staged by tu_fwd_l
@@ -1789,13 +1793,28 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
 }
 // TEncEntropy::estimateBit (TEncEntropy.cpp:685) from the current coder
 // The entries TEncSbac::estBit writes (exactly those of estbit_update), one per lane: two
-// rounds of 64 entries instead of ~200 serial table reads by the whole wave
+// rounds of 64 entries instead of ~200 serial table reads by the whole wave.
+// The call overwrites a fixed set of entries with values that depend only on (w, h, ch) and the
+// context states 28 .. 179, so a call whose inputs equal the previous call's leaves the table as
+// it is (the RQT's transform-skip pass re-estimates from the state its first pass loaded, and the
+// intra searches re-estimate from restored states): such a call returns after one compare.
 __device__ void estimate_bit(int w, int h, int ch) {
   HM_PROF(PR_EST);
   const uint8_t *st = E.cod[E.cur].st;
   hvx_estbits *e = &E.est;
 #define EB(ctx, v) E.eb[st[(ctx)] ^ (v)]
   const int l = lid(), b = l & 1;
+#ifndef HM_NO_EST_MEMO
+  static_assert(HVX_CTX_QT_CBF >= 28 && HVX_CTX_ABS + 6 <= 180, "estBit's context range");
+  {
+    const uint32_t key = (uint32_t)(w | h << 8 | ch << 16) + 1;
+    const uint32_t cur = l < 38 ? reinterpret_cast<const uint32_t *>(st)[7 + l] : 0;
+    const bool same = __ballot(l < 38 && cur != E.est_st[l]) == 0;
+    if (E.est_key == key && same) return;
+    if (l < 38) E.est_st[l] = cur;
+    if (l == 0) E.est_key = key;
+  }
+#endif
   // round 1: cbf (20), root cbf (8), sig CG (4), significance (<= 28)
   if (l < 20) e->blockCbpBits[l >> 1][b] = EB(HVX_CTX_QT_CBF + (l >> 1), b);
   else if (l < 28) e->blockRootCbpBits[(l - 20) >> 1][b] = EB(HVX_CTX_QT_ROOT_CBF + ((l - 20) >> 1), b);
@@ -4365,6 +4384,9 @@ __device__ void compress_ctu(int addr, const Coder *entry_g, int entry_in_lds, C
   // estBits start from zero per CTU like the restatement (every table entry RDOQ reads is
   // rewritten by estimateBit before its first use)
   for (int i = lid(); i < (int)(sizeof(hvx_estbits) / 4); i += 64) ((uint32_t *)&E.est)[i] = 0;
+#ifndef HM_NO_EST_MEMO
+  if (lid() == 0) E.est_key = 0;
+#endif
   wsync();
   // initCtu of the picture's CTU and the depth-0 best/temp CUs
   for (int k = 0; k < 2; k++) {
