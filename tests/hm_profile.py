@@ -40,8 +40,9 @@ def bench_profile(pics, steps):
         torch.cuda.synchronize()
         dt = time.time() - t0
         sb = w.eng.reserve(w.n_jobs)
-        st = w.eng.state[:w.n_jobs * sb].view(w.n_jobs, sb)[:, :16 + 16 * NPROF].cpu().numpy().copy()
-        prof = st[:, 16:16 + 16 * NPROF].copy().view(np.uint64).reshape(w.n_jobs, 2, NPROF)
+        # State.status[4] | dbg[4] | prof[2][32] (csrc/hvx_hm.hpp)
+        st = w.eng.state[:w.n_jobs * sb].view(w.n_jobs, sb)[:, :32 + 16 * NPROF].cpu().numpy().copy()
+        prof = st[:, 32:32 + 16 * NPROF].copy().view(np.uint64).reshape(w.n_jobs, 2, NPROF)
         report(prof, w.n_jobs, "bench step %d: %d chains, %.3f s" % (s, w.n_jobs, dt))
 
 

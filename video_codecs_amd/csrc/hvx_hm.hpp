@@ -146,6 +146,28 @@ struct CoefMemoBig {
   uint32_t before[kMemoDw], after[kMemoDw];
   uint32_t coef[512];             // int16 pairs (TU-packed order); dword k * 64 + lane
 };
+#ifndef HM_NO_RQT_MEMO
+// The inter residual memo (enc_res_rd_inter): xEstimateInterResidualQT and the residual decision
+// after it depend only on the CU's residual and the RD coder they start from
+// (m_pppcRDSbacCoder[depth][CI_CURR_BEST]); within one CU the residual is fixed by the PUs' motion
+// (the merge candidates, the 2Nx2N search and the merge candidates of the other partitions repeat
+// motion: ~30% of the inter RQTs on the LDP / RA captures).  An entry per CU depth holds the first
+// kRqK distinct (partition, motion, start coder) keys of the CU being decided and what the RQT left
+// that is read afterwards: every partition's tr_idx / transform-skip / cbf bytes, the CU's
+// coefficients (unless the residual was dropped) and resi_best.  Entry layout: header (64 dwords:
+// the start coder's 54 dwords, 6 key dwords, the "dropped" flag) | 8 B per partition | coefficients
+// Y | Cb | Cr (1.5 W^2 int16) | resi_best (1.5 W^2 int16, the packed TComYuv).  Two entries catch
+// 99% of the repeats (the restatement's count on the captures).  The helpers stay out of line: inlined
+// they change how enc_res_rd_inter inlines the RQT root, and that build ran 2.3% slower.
+constexpr int kRqK = 2;
+__host__ __device__ constexpr int rq_entry_bytes(int d) {
+  return 256 + 8 * (256 >> (2 * d)) + 2 * 3 * (64 >> d) * (64 >> d);
+}
+__host__ __device__ constexpr int rq_depth_off(int d) {
+  return d == 0 ? 0 : rq_depth_off(d - 1) + kRqK * rq_entry_bytes(d - 1);
+}
+constexpr int kRqBytes = rq_depth_off(4);
+#endif
 // per-chain state in HBM
 struct State {
   int status[4];  // [0]: the job's status word (hvx_hm_job_status: 0 ran, -HVX_HM_BAD_* refused)
@@ -173,6 +195,10 @@ struct State {
   int memo_next;
   CoefMemoBig memob[kMemoB];      // ... and of 16x16 / 32x32 TUs
   int memob_next;
+#ifndef HM_NO_RQT_MEMO
+  alignas(16) uint8_t rq_data[kRqBytes];  // the inter residual memo's entries (per CU depth)
+  int rq_n[4];                            // ... entries held for the CU being decided at each depth
+#endif
   MeScratch me;                   // leaf scratch outside LDS
   McScratch mc;
   TuSmem<3> tu3;
@@ -2242,7 +2268,7 @@ __device__ __forceinline__ TuSmem<L> &tu_smem() {
 template <int L>
 __device__ int32_t tu_fwd_l(const hvx_tu_desc &d, const int16_t *resi, int rs, int16_t *coef) {
   HM_PROF(PR_TUF);
-#if defined(HM_PROFILE) && !defined(HM_PROF_WALK) && !defined(HVX_RDOQ_PROF_SUB)
+#if defined(HM_PROFILE) && !defined(HM_PROF_WALK) && !defined(HVX_RDOQ_PROF_SUB) && !defined(HM_PROF_RQT)
   ProfScope prof_size_(12 + L);
 #endif
   TuSmem<L> &s = tu_smem<L>();
@@ -2916,6 +2942,120 @@ __device__ void clear_residual_fields(Cu *cu) {
   }
   wsync();
 }
+#ifndef HM_NO_RQT_MEMO
+__device__ __forceinline__ uint8_t *rq_entry(int depth, int k) {
+  int off = 0;
+  for (int d = 0; d < depth; d++) off += kRqK * rq_entry_bytes(d);
+  return E.S->rq_data + off + k * rq_entry_bytes(depth);
+}
+// the partitions the memo covers (one or two PUs)
+__device__ __forceinline__ int rqt_keyed(const Cu *cu) {
+  const int ps = cu->p[0].part;
+  return ps >= SIZE_2Nx2N && ps <= SIZE_nRx2N && ps != SIZE_NxN;
+}
+// this lane's word of the memo key: lanes 0-53 the start coder (m_pppcRDSbacCoder[depth]
+// [CI_CURR_BEST]), 54-59 the partition and the PUs' motion (a list a PU does not use contributes
+// nothing)
+__device__ uint32_t rqt_key_word(const Cu *cu) {
+  const int l = lid();
+  const int ps = cu->p[0].part;
+  if (l < 54) return reinterpret_cast<const uint32_t *>(&E.cod[RD(cu->depth, CI_CURR_BEST)])[l];
+  const int npu = ps == SIZE_2Nx2N ? 1 : 2;
+  uint32_t w[6] = {(uint32_t)ps, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    if (j >= npu) break;
+    int a, pw, ph;
+    part_index_size(cu, ps, j, a, pw, ph);
+    const Part &p = cu->p[a];
+    const int dir = p.inter_dir;
+    w[0] |= (uint32_t)(dir & 3) << (4 + 2 * j);
+#pragma unroll
+    for (int li = 0; li < 2; li++) {
+      const int used = (dir >> li) & 1;
+      const uint32_t ref = used ? (uint32_t)(uint8_t)p.ref[li] : 0xffu;
+      const int slot = 2 * j + li;  // refs: word 0 bits 8.., the last in word 1
+      if (slot < 3) w[0] |= ref << (8 + 8 * slot);
+      else w[1] = ref;
+      w[2 + slot] = used ? ((uint32_t)(uint16_t)p.mv[li][0] | (uint32_t)(uint16_t)p.mv[li][1] << 16) : 0;
+    }
+  }
+  const int i = l - 54;  // selects, not an indexed (scratch) read
+  return i == 0 ? w[0] : i == 1 ? w[1] : i == 2 ? w[2] : i == 3 ? w[3] : i == 4 ? w[4] : i == 5 ? w[5] : 0u;
+}
+// the entry of this CU whose key equals the lanes' key words, or -1
+__device__ __noinline__ int rqt_memo_find(const Cu *cu, int depth) {
+  if (!rqt_keyed(cu)) return -1;
+  const uint32_t key = rqt_key_word(cu);
+  const int n = E.S->rq_n[depth];
+  for (int k = 0; k < n; k++) {
+    const uint32_t *h = reinterpret_cast<const uint32_t *>(rq_entry(depth, k));
+    if (__ballot(lid() < 60 && h[lid()] != key) == 0) return k;
+  }
+  return -1;
+}
+__device__ __forceinline__ void cpy64(void *dst, const void *src, int n_int16) {
+  uint2 *d = reinterpret_cast<uint2 *>(dst);
+  const uint2 *s = reinterpret_cast<const uint2 *>(src);
+  for (int i = lid(); i < n_int16 / 4; i += 64) d[i] = s[i];
+}
+// the residual fields and (unless dropped) coefficients of entry k into the CU
+__device__ __noinline__ void rqt_memo_replay(Cu *cu, int depth, int k) {
+  const uint8_t *e = rq_entry(depth, k);
+  const int np = cu->nparts, W = cu->width, W2 = W * W;
+  const uint2 *pp = reinterpret_cast<const uint2 *>(e + 256);
+  for (int i = lid(); i < np; i += 64) {
+    const uint2 v = pp[i];
+    Part &p = cu->p[i];
+    p.tr_idx = (int8_t)(v.x & 0xff);
+    p.ts[0] = (uint8_t)(v.x >> 8); p.ts[1] = (uint8_t)(v.x >> 16); p.ts[2] = (uint8_t)(v.x >> 24);
+    p.cbf[0] = (uint8_t)v.y; p.cbf[1] = (uint8_t)(v.y >> 8); p.cbf[2] = (uint8_t)(v.y >> 16);
+  }
+  if (!reinterpret_cast<const uint32_t *>(e)[60]) {
+    const int16_t *c = reinterpret_cast<const int16_t *>(e + 256 + 8 * np);
+    cpy64(cu->coef, c, W2);
+    cpy64(cu->coef + coff(1), c + W2, W2 >> 2);
+    cpy64(cu->coef + coff(2), c + W2 + (W2 >> 2), W2 >> 2);
+  }
+  wsync();
+}
+// a new entry (while the CU has fewer than kRqK): the key, the residual fields, the coefficients
+__device__ __noinline__ int rqt_memo_store(const Cu *cu, int depth, int dropped) {
+  if (!rqt_keyed(cu)) return -1;
+  const int n = E.S->rq_n[depth];
+  if (n >= kRqK) return -1;
+  const uint32_t key = rqt_key_word(cu);  // recomputed: nothing stays live across the RQT
+  uint8_t *e = rq_entry(depth, n);
+  const int np = cu->nparts, W = cu->width, W2 = W * W;
+  uint32_t *h = reinterpret_cast<uint32_t *>(e);
+  if (lid() < 60) h[lid()] = key;
+  if (lid() == 60) h[60] = (uint32_t)dropped;
+  uint2 *pp = reinterpret_cast<uint2 *>(e + 256);
+  for (int i = lid(); i < np; i += 64) {
+    const Part &p = cu->p[i];
+    pp[i] = make_uint2((uint32_t)(uint8_t)p.tr_idx | (uint32_t)p.ts[0] << 8 | (uint32_t)p.ts[1] << 16 | (uint32_t)p.ts[2] << 24,
+                       (uint32_t)p.cbf[0] | (uint32_t)p.cbf[1] << 8 | (uint32_t)p.cbf[2] << 16);
+  }
+  if (!dropped) {
+    int16_t *c = reinterpret_cast<int16_t *>(e + 256 + 8 * np);
+    cpy64(c, cu->coef, W2);
+    cpy64(c + W2, cu->coef + coff(1), W2 >> 2);
+    cpy64(c + W2 + (W2 >> 2), cu->coef + coff(2), W2 >> 2);
+  }
+  wsync();
+  return n;
+}
+// resi_best of entry k (packed, 1.5 W^2 int16): to = 1 into the entry (and the entry counts from
+// now on), 0 out of it
+__device__ __noinline__ void rqt_memo_resi(const Cu *cu, int depth, int k, Yuv *resi_best, int to) {
+  uint8_t *e = rq_entry(depth, k);
+  const int W2 = cu->width * cu->width;
+  int16_t *r = reinterpret_cast<int16_t *>(e + 256 + 8 * cu->nparts) + W2 + (W2 >> 1);
+  if (to) cpy64(r, resi_best->s, W2 + (W2 >> 1));
+  else cpy64(resi_best->s, r, W2 + (W2 >> 1));
+  wsync();
+}
+#endif
 __device__ void enc_res_rd_inter(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Yuv *resi_best, Yuv *reco, int skip_residual) {
   const int W = cu->width, depth = cu->depth;
   if (skip_residual) {
@@ -2937,22 +3077,59 @@ __device__ void enc_res_rd_inter(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Yuv *re
   yuv_op(YOP_SUB, resi, org, pred, W);
   TU_LOCAL(t0);
   tu_root(t0, cu, 0);
-  double nz_cost = 0;
-  uint32_t nz_bits = 0, nz_dist = 0, z_dist = 0;
   E.cur = GOON;
   cload(E.cur, RD(depth, CI_CURR_BEST));
-  estimate_inter_residual_qt<0>(cu, resi, &nz_cost, &nz_bits, &nz_dist, &z_dist, t0);
-  reset_bits();
-  cbin(X_ROOT_CBF, 0);
-  const uint32_t zero_bits = written_bits();
-  const double zero_cost = rd_cost(zero_bits, z_dist);
-  if (zero_cost < nz_cost || !cu_qt_root_cbf(cu, 0)) clear_residual_fields(cu);
-  else set_inter_residual_qt_data<0>(cu, nullptr, 0, t0);
+#if defined(HM_PROFILE) && defined(HM_PROF_RQT)  // slots 12: the RQT + decision + final count, 13: replays, 14: stores, 15: lookups
+  ProfScope prof_rqt_(12);
+#define HM_RQT_T0(v) HM_T0(v)
+#define HM_RQT_TADD(c, v) HM_TADD(c, v)
+#else
+#define HM_RQT_T0(v) ((void)0)
+#define HM_RQT_TADD(c, v) ((void)0)
+#endif
+#ifndef HM_NO_RQT_MEMO
+  HM_RQT_T0(t_find);
+  const int hit = rqt_memo_find(cu, depth);
+  HM_RQT_TADD(15, t_find);
+  int slot = -1;
+  if (hit >= 0) {
+    HM_RQT_T0(t_rep);
+    rqt_memo_replay(cu, depth, hit);
+    HM_RQT_TADD(13, t_rep);
+  } else
+#endif
+  {
+    double nz_cost = 0;
+    uint32_t nz_bits = 0, nz_dist = 0, z_dist = 0;
+    estimate_inter_residual_qt<0>(cu, resi, &nz_cost, &nz_bits, &nz_dist, &z_dist, t0);
+    reset_bits();
+    cbin(X_ROOT_CBF, 0);
+    const uint32_t zero_bits = written_bits();
+    const double zero_cost = rd_cost(zero_bits, z_dist);
+    const int dropped = zero_cost < nz_cost || !cu_qt_root_cbf(cu, 0);
+    if (dropped) clear_residual_fields(cu);
+    else set_inter_residual_qt_data<0>(cu, nullptr, 0, t0);
+#ifndef HM_NO_RQT_MEMO
+    HM_RQT_T0(t_st);
+    slot = rqt_memo_store(cu, depth, dropped);
+    HM_RQT_TADD(14, t_st);
+#endif
+  }
   cload(E.cur, RD(depth, CI_CURR_BEST));
   uint32_t final_bits = 0;
   add_symbol_bits_inter(cu, &final_bits);
   if (!cu_qt_root_cbf(cu, 0)) yuv_op(YOP_CLEAR, resi_best, nullptr, nullptr, W);
+#ifndef HM_NO_RQT_MEMO
+  else if (hit >= 0) rqt_memo_resi(cu, depth, hit, resi_best, 0);
+#endif
   else set_inter_residual_qt_data<0>(cu, resi_best, 1, t0);
+#ifndef HM_NO_RQT_MEMO
+  if (slot >= 0) {
+    if (cu_qt_root_cbf(cu, 0)) rqt_memo_resi(cu, depth, slot, resi_best, 1);
+    if (lid() == 0) E.S->rq_n[depth] = slot + 1;
+    wsync();
+  }
+#endif
   cload(RD(depth, CI_TEMP_BEST), E.cur);
   yuv_op(YOP_ADD_CLIP, reco, pred, resi_best, W);
   const uint32_t final_dist = yuv_dist(reco, org, W);
@@ -4209,6 +4386,9 @@ __device__ void compress_cu(int parent_ps) {
   E.yw = 64 >> D;
   Cu *best = BEST(depth);
   HM_TR("cu", best->x * 10000 + best->y, D);
+#ifndef HM_NO_RQT_MEMO
+  if (lid() == 0) E.S->rq_n[D] = 0;  // the inter residual memo holds this CU's RQTs only
+#endif
   copy_org_to_yuv(YB(Y_ORIG, depth), best);
   int boundary = 0;
   const int rx = best->x + best->width - 1, by = best->y + best->width - 1;
