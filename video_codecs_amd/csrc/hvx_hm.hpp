@@ -4678,6 +4678,12 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
     if (l < 4) S->dbg[l] = 0;
     if (bad) return;
   }
+#ifndef HM_NO_LDS_ZERO
+  // the wave's LDS record starts zeroed, so nothing the decision reads before writing it (every
+  // such read is a bug) depends on what the previous workgroup on this CU left there
+  for (int i = l; i < (int)(sizeof(Enc) / 4); i += 64) reinterpret_cast<uint32_t *>(&hm_e)[i] = 0;
+  wsync();
+#endif
   copy_words(&hm_e.P, &pics[job.pic], (int)sizeof(hvx_hm_picture));
   wsync();
   for (int i = l; i < 128; i += 64) {

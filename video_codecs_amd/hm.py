@@ -429,7 +429,8 @@ class Engine:
         sb = state_size()
         if self.state is None or self.state.numel() < n_jobs * sb:
             old = self.state
-            self.state = torch.empty(n_jobs * sb, dtype=torch.uint8, device=self.device)
+            # zeroed: no field a job reads before writing can depend on an earlier allocation's bytes
+            self.state = torch.zeros(n_jobs * sb, dtype=torch.uint8, device=self.device)
             if old is not None:
                 self.state[:old.numel()].copy_(old)
         return sb
