@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--qp", type=int, default=32)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-1080p", action="store_true", help="skip the 1080p side measurement")
+    p.add_argument("--no-closed", action="store_true", help="skip the closed-loop LDP segment side figure (config 5: "
+                                                            "120 segments of 1920x1088 I + 2 P pictures, ~2 minutes)")
     return p.parse_args()
 
 
@@ -482,6 +484,143 @@ def slice_mode0_measure(W, H, chains=2040, distinct=16, nref=4, base_qp=32, warm
             "ctus_per_s": round(chains / sec, 2), "ms_per_step": round(sec * 1e3, 1), "wall_ms_per_step": round(wall * 1e3, 1)}
 
 
+# encoder_lowdelay_P_main.cfg:24-27: Frame1..4 QP offset and QPFactor; GOP position 4 has depth 0
+LDP_GOP = {1: (3, 0.4624, 2), 2: (2, 0.4624, 1), 3: (3, 0.4624, 2), 4: (1, 0.578, 0)}
+LDP_SAO_LAYER = {0: 0, 1: 2, 2: 1, 3: 2, 4: 0}
+
+
+def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=6, threads=16, parity=True):
+    """Side figure (config 5): closed LDP segments decided entirely on the device --
+    `segs` segments in flight (W x H random 4:2:0 originals, one CTU row per slice: segs x H/64
+    chains), each an I picture and then P pictures decided against references the device made
+    (hvx_hm_compress -> hvx_hm_finish_picture: deblocking with device boundary strengths and the
+    collocated motion field -> hm.sao_picture -> the padded reference planes), the LDP GOP's QP
+    offsets / QPFactors / reference lists (encoder_lowdelay_P_main.cfg:24-27, first GOP).  Each
+    picture's chains advance `ctus_step` CTUs per launch until their rows are done; then every
+    segment's picture is finished into its next reference.  Reported: the P pictures' CTUs per second
+    over their decision launches plus their loop filters / SAO / reference builds (wall clock), and a
+    restatement parity sample: segment 0's last P picture re-decided by the restatement on 16 host
+    threads against the device-made references and collocated field, every CTU compared."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    from video_codecs_amd import _abi, hm, synth
+    assert H % 64 == 0 and W % 64 == 0, "whole CTUs (no picture-boundary CTU reads the search state across slices)"
+    wc, hc = W // 64, H // 64
+    assert wc % ctus_step == 0
+    n = wc * hc
+    eb = _abi.load_entropy_bits()
+    init = _abi.load_ctx_init_states()
+    dbk = _abi.deblock_params(W, H)
+    with ThreadPoolExecutor(8) as ex:
+        orgs = list(ex.map(lambda i: synth.random_frame(W, H, 30000 + i), range(segs * pics)))
+    org_frames = [hm.DeviceFrame(yuv_split(f, W, H)) for f in orgs]
+    refs = [[] for _ in range(segs)]  # per segment: device-made reference frames, most recent first
+    cols = [None] * segs
+    rates = [np.zeros((3, 7)) for _ in range(segs)]
+    stream = torch.cuda.Stream()
+    out_ctu = torch.zeros(segs * hc * ctus_step * hm.HM_CTU.itemsize, dtype=torch.uint8, device="cuda")
+    out_rec = torch.zeros(segs * hc * ctus_step * 6144, dtype=torch.uint8, device="cuda")
+    per_pic, kept, last = [], {}, None
+    t_p = 0.0
+    for t in range(pics):
+        if t == 0:
+            qp, st_idx = base_qp, 2
+            prm = hm.slice_params(2, qp, 0.57 * (1.0 - min(0.5, 0.05 * 3)), gop_depth=0)  # I: 0.57 * dLambda_scale
+            prm.update(poc=0, nref=[0, 0], ref_poc=np.zeros((2, 4), int), ref_plane=np.zeros((2, 4), int), max_merge=5,
+                       tmvp=1, check_ldc=1, col_from_l0=1, col_valid=0, col_poc=0, col_ref_poc=np.zeros((2, 4), int),
+                       search_range=64, amp=1)
+            col_nref = (0, 0)
+        else:
+            off, fac, depth = LDP_GOP[t]
+            qp, st_idx = base_qp + off, 1
+            nr = min(t, 4)
+            prm = hm.slice_params(1, qp, fac, gop_depth=depth)
+            prm.update(poc=t, nref=[nr, 0], ref_poc=np.array([[t - 1 - k if k < nr else 0 for k in range(4)], [0] * 4]),
+                       ref_plane=np.array([[k if k < nr else 0 for k in range(4)], [0] * 4]), max_merge=5, tmvp=1,
+                       check_ldc=1, col_from_l0=1, col_valid=1, col_poc=t - 1,
+                       col_ref_poc=np.array([[t - 2 - k if k < min(t - 1, 4) else 0 for k in range(4)], [0] * 4]),
+                       search_range=64, amp=1)
+            col_nref = (min(t - 1, 4), 0)
+        entry = init[st_idx, qp]
+        col_read = cols[0]  # the collocated field segment 0's picture reads (the parity sample's)
+        pictures = [hm.DevicePicture(org_frames[s * pics + t], refs[s][:4], prm, eb, col_field=cols[s]) for s in range(segs)]
+        eng = hm.Engine(pictures)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        launch_s = 0.0
+        with torch.cuda.stream(stream):
+            for L in range(wc // ctus_step):
+                specs = [(s, r * wc + L * ctus_step, ctus_step, r * wc, r * wc + wc - 1, L > 0)
+                         for s in range(segs) for r in range(hc)]
+                jt = torch.from_numpy(_chain_jobs(specs, entry).view(np.uint8).reshape(-1).copy()).cuda()
+                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                e[0].record()
+                eng.launch(jt, len(specs), out_ctu, out_rec)
+                e[1].record()
+                e[1].synchronize()
+                launch_s += e[0].elapsed_time(e[1]) * 1e-3
+                if t == pics - 1 and parity:  # segment 0's chains (jobs 0 .. hc-1): the pre-loop-filter records
+                    kept[L] = (out_ctu[:hc * ctus_step * hm.HM_CTU.itemsize].cpu().numpy().view(hm.HM_CTU).reshape(hc, ctus_step),
+                               out_rec[:hc * ctus_step * 6144].cpu().numpy().reshape(hc, ctus_step, 6144))
+                progress("closed loop: picture %d launch %d/%d %.1f s" % (t, L + 1, wc // ctus_step, e[0].elapsed_time(e[1]) * 1e-3))
+            t1 = time.perf_counter()
+            for s in range(segs):
+                dp = pictures[s]
+                _, col_t = hm.finish_picture(dp, dbk, col_field=True)
+                st0 = entry
+                rates[s], _, _, _ = hm.sao_picture(dp, LDP_SAO_LAYER[t], rates[s], int(prm["slice_type"]), qp,
+                                                   sao_states=(st0[hm.SAO_CTX_MERGE], st0[hm.SAO_CTX_TYPE]))
+                ref = hm.DeviceFrame.blank(W, H)
+                hm.finish_picture(dp, None, ref_frame=ref)
+                refs[s].insert(0, ref)
+                cols[s] = col_t
+        stream.synchronize()
+        t2 = time.perf_counter()
+        per_pic.append({"poc": t, "slice": "I" if t == 0 else "P", "qp": qp, "decision_s": round(launch_s, 3),
+                        "decision_wall_s": round(t1 - t0, 3), "loop_s": round(t2 - t1, 3),
+                        "ctus_per_s": round(segs * n / (t2 - t0), 1)})
+        progress("closed loop: picture %d done (%d CTUs, decision %.1f s, loop filters + SAO + references %.1f s)" % (
+            t, segs * n, launch_s, t2 - t1))
+        if t > 0:
+            t_p += t2 - t0
+        if t == pics - 1:
+            last = (prm, qp, col_nref, entry, col_read)
+        del eng
+    res = {"workload": "%d closed LDP segments (I + %d P pictures, %dx%d random 4:2:0 originals, one CTU row per slice: "
+                       "%d chains), every P picture decided against device-made references (deblocked + SAO) and the "
+                       "device's collocated field; %d CTUs per chain per launch" % (segs, pics - 1, W, H, segs * hc, ctus_step),
+           "ctus_per_s": round(segs * n * (pics - 1) / t_p, 2), "basis": "P pictures: decision launches + loop filters / "
+           "SAO / reference builds, wall clock", "pictures": per_pic}
+    if parity:
+        import oracle  # noqa: F401  (test infrastructure: the checker)
+        from oracle import hm_ctu
+        prm, qp, col_nref, entry, col_read = last
+        pi, pf = host_pic_arrays(W, H, prm, qp, col_nref=col_nref)
+        ref_host = []
+        for ref in refs[0][1:1 + prm["nref"][0]]:  # the references the last picture read (refs[0][0] is its own)
+            y8, _, cb16, cr16 = (x.cpu().numpy() for x in ref.planes())
+            m8 = hm.DeviceFrame.M8
+            ref_host.append(np.concatenate([y8[m8:m8 + H, m8:m8 + W].reshape(-1), cb16[40:40 + H // 2, 40:40 + W // 2]
+                                            .astype(np.uint8).reshape(-1), cr16[40:40 + H // 2, 40:40 + W // 2].astype(np.uint8).reshape(-1)]))
+        col_host = col_read.cpu().numpy() if col_read is not None else None
+        t0 = time.perf_counter()
+        progress("closed loop: restatement parity (%d chains x %d CTUs)" % (hc, wc))
+        port = hm_ctu.chains(pi, pf, orgs[pics - 1], np.concatenate(ref_host), entry, np.arange(hc, dtype=np.int32) * wc,
+                             wc, wc, threads=threads, col_field=col_host)
+        got = {}
+        for L, (ct, rc) in kept.items():
+            for k in range(hc):
+                for i in range(ctus_step):
+                    got[(k, L * ctus_step + i)] = (hm.unpack_parts(ct[k, i]["p"]), ct[k, i]["coef"], rc[k, i], ct[k, i]["cost"],
+                                                  (ct[k, i]["bits"], ct[k, i]["dist"]))
+        mism, first = _compare_port(port, got, [(k, i) for k in range(hc) for i in range(wc)])
+        res.update(gpu_parity_ctus=hc * wc, gpu_parity_mismatches=mism, first_mismatches=first,
+                   parity_s=round(time.perf_counter() - t0, 1))
+    del pictures, refs, org_frames
+    torch.cuda.empty_cache()
+    return res
+
+
 def hm_1080p_measure(pics=128, nref=4, base_qp=32, warmup=1, steps=10):
     """Side figure (BASELINE configs 2/3 size): the headline's decision on 1080p random 4:2:0 P
     pictures -- HmWorkload at 1920x1080, `pics` pictures x 16 chains (17 CTU rows, the partial 17th
@@ -857,6 +996,9 @@ def main():
             if not args.no_1080p:
                 progress("1080p side figure")
                 out["hm_1080p"] = hm_1080p_measure()
+            if not args.no_closed:
+                progress("closed-loop LDP segments (config 5)")
+                out["closed_loop"] = closed_loop_measure(threads=threads, parity=not args.no_cpu)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
