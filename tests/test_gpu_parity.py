@@ -415,6 +415,20 @@ def test_hm_finish_picture_gpu(torch, ctu_name, dbk_name):
 
 
 @pytest.mark.gpu
+def test_closed_loop_segments_gpu(torch):
+    """The bench's closed-loop figure in miniature (bench.closed_loop_measure): two LDP segments of
+    256x192 random pictures (I, P, P), every P picture decided against the references and collocated
+    field the device made from the pictures before it (deblocking + SAO on the device), the chains
+    stepped 2 CTUs per launch; segment 0's last P picture re-decided by the restatement against the
+    downloaded device references: every CTU equal."""
+    import bench
+    hvx.context()
+    r = bench.closed_loop_measure(256, 192, segs=2, pics=3, base_qp=32, ctus_step=2, threads=4)
+    assert [p["slice"] for p in r["pictures"]] == ["I", "P", "P"]
+    assert r["gpu_parity_ctus"] == 12 and r["gpu_parity_mismatches"] == 0, r["first_mismatches"]
+
+
+@pytest.mark.gpu
 def test_hm_closed_loop_gpu(torch):
     """A GOP segment run entirely on the device (SAO off, tests/golden/ctu_ldp_nosao.bin): the I
     picture decided by hvx_hm_compress, finished by hvx_hm_finish_picture (deblocking from the
