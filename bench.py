@@ -973,32 +973,42 @@ def main():
             threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
             if not args.no_cpu_ref:
                 progress("reference HM on the host cores")
-                out["cpu_baseline"] = hm_cpu_reference(args.cpu_ref_procs or threads,
-                                                       os.environ.get("TMPDIR", "/tmp"))
-            progress("slice writer side figure")
-            out["slice_writer"] = slice_writer_measure(work, args.warmup + args.steps)
+                try:
+                    out["cpu_baseline"] = hm_cpu_reference(args.cpu_ref_procs or threads,
+                                                           os.environ.get("TMPDIR", "/tmp"))
+                except Exception as e:  # noqa: BLE001  (the port figure below stands in)
+                    progress("reference HM timing failed: %s: %s" % (type(e).__name__, e))
+            def side(key, what, fn):
+                # a side figure that raises is reported as such; the headline line is never lost
+                progress(what)
+                try:
+                    out[key] = fn()
+                except Exception as e:  # noqa: BLE001
+                    out[key] = {"error": "%s: %s" % (type(e).__name__, e)}
+                    progress("%s failed: %s" % (what, out[key]["error"]))
+
+            side("slice_writer", "slice writer side figure", lambda: slice_writer_measure(work, args.warmup + args.steps))
             if not args.no_cpu:
-                progress("restatement parity of the headline's CTUs")
-                port = hm_cpu_port(work, threads)
-                progress("merged bottom chain parity")
-                port["merged_chain"] = hm_merged_chain_parity(threads)
-                out["cpu_port"] = port
-                if out["cpu_baseline"] is None:
-                    out["cpu_baseline"] = port
+                def port_figure():
+                    progress("restatement parity of the headline's CTUs")
+                    port = hm_cpu_port(work, threads)
+                    progress("merged bottom chain parity")
+                    port["merged_chain"] = hm_merged_chain_parity(threads)
+                    return port
+                side("cpu_port", "the restatement's port figure", port_figure)
+                if out["cpu_baseline"] is None and "error" not in out["cpu_port"]:
+                    out["cpu_baseline"] = out["cpu_port"]
             del work, dpb
             torch.cuda.empty_cache()
             if not args.no_ra:
-                progress("config 4 (RA, stVSSIM cost)")
-                out["config4_ra_ssim"] = ra_ssim_measure(W, H)
+                side("config4_ra_ssim", "config 4 (RA, stVSSIM cost)", lambda: ra_ssim_measure(W, H))
             if not args.no_slice0:
-                progress("SliceMode 0 side figure")
-                out["slice_mode0"] = slice_mode0_measure(W, H)
+                side("slice_mode0", "SliceMode 0 side figure", lambda: slice_mode0_measure(W, H))
             if not args.no_1080p:
-                progress("1080p side figure")
-                out["hm_1080p"] = hm_1080p_measure()
+                side("hm_1080p", "1080p side figure", hm_1080p_measure)
             if not args.no_closed:
-                progress("closed-loop LDP segments (config 5)")
-                out["closed_loop"] = closed_loop_measure(threads=threads, parity=not args.no_cpu)
+                side("closed_loop", "closed-loop LDP segments (config 5)",
+                     lambda: closed_loop_measure(threads=threads, parity=not args.no_cpu))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
