@@ -489,10 +489,10 @@ LDP_GOP = {1: (3, 0.4624, 2), 2: (2, 0.4624, 1), 3: (3, 0.4624, 2), 4: (1, 0.578
 LDP_SAO_LAYER = {0: 0, 1: 2, 2: 1, 3: 2, 4: 0}
 
 
-def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=6, threads=16, parity=True):
+def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=6, threads=16, parity=True, rows=1):
     """Side figure (config 5): closed LDP segments decided entirely on the device --
-    `segs` segments in flight (W x H random 4:2:0 originals, one CTU row per slice: segs x H/64
-    chains), each an I picture and then P pictures decided against references the device made
+    `segs` segments in flight (W x H random 4:2:0 originals, `rows` CTU rows per slice, one chain
+    per slice), each an I picture and then P pictures decided against references the device made
     (hvx_hm_compress -> hvx_hm_finish_picture: deblocking with device boundary strengths and the
     collocated motion field -> hm.sao_picture -> the padded reference planes), the LDP GOP's QP
     offsets / QPFactors / reference lists (encoder_lowdelay_P_main.cfg:24-27, first GOP).  Each
@@ -504,9 +504,13 @@ def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=
     import torch
     from concurrent.futures import ThreadPoolExecutor
     from video_codecs_amd import _abi, hm, synth
-    assert H % 64 == 0 and W % 64 == 0, "whole CTUs (no picture-boundary CTU reads the search state across slices)"
-    wc, hc = W // 64, H // 64
-    assert wc % ctus_step == 0
+    # a partial bottom CTU row must share its slice (its chain) with the row above: its picture-boundary
+    # CTUs read TEncSearch::m_integerMv2Nx2N as the CTU before them left it
+    assert W % 64 == 0 and (H % 64 == 0 or rows >= 2)
+    wc, hc = W // 64, (H + 63) // 64
+    assert hc % rows == 0
+    nch, cl = hc // rows, rows * wc  # chains per picture, CTUs per chain (one slice each)
+    assert cl % ctus_step == 0
     n = wc * hc
     eb = _abi.load_entropy_bits()
     init = _abi.load_ctx_init_states()
@@ -518,8 +522,8 @@ def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=
     cols = [None] * segs
     rates = [np.zeros((3, 7)) for _ in range(segs)]
     stream = torch.cuda.Stream()
-    out_ctu = torch.zeros(segs * hc * ctus_step * hm.HM_CTU.itemsize, dtype=torch.uint8, device="cuda")
-    out_rec = torch.zeros(segs * hc * ctus_step * 6144, dtype=torch.uint8, device="cuda")
+    out_ctu = torch.zeros(segs * nch * ctus_step * hm.HM_CTU.itemsize, dtype=torch.uint8, device="cuda")
+    out_rec = torch.zeros(segs * nch * ctus_step * 6144, dtype=torch.uint8, device="cuda")
     per_pic, kept, last = [], {}, None
     t_p = 0.0
     for t in range(pics):
@@ -549,9 +553,9 @@ def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=
         t0 = time.perf_counter()
         launch_s = 0.0
         with torch.cuda.stream(stream):
-            for L in range(wc // ctus_step):
-                specs = [(s, r * wc + L * ctus_step, ctus_step, r * wc, r * wc + wc - 1, L > 0)
-                         for s in range(segs) for r in range(hc)]
+            for L in range(cl // ctus_step):
+                specs = [(s, c * cl + L * ctus_step, ctus_step, c * cl, c * cl + cl - 1, L > 0)
+                         for s in range(segs) for c in range(nch)]
                 jt = torch.from_numpy(_chain_jobs(specs, entry).view(np.uint8).reshape(-1).copy()).cuda()
                 e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 e[0].record()
@@ -560,9 +564,9 @@ def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=
                 e[1].synchronize()
                 launch_s += e[0].elapsed_time(e[1]) * 1e-3
                 if t == pics - 1 and parity:  # segment 0's chains (jobs 0 .. hc-1): the pre-loop-filter records
-                    kept[L] = (out_ctu[:hc * ctus_step * hm.HM_CTU.itemsize].cpu().numpy().view(hm.HM_CTU).reshape(hc, ctus_step),
-                               out_rec[:hc * ctus_step * 6144].cpu().numpy().reshape(hc, ctus_step, 6144))
-                progress("closed loop: picture %d launch %d/%d %.1f s" % (t, L + 1, wc // ctus_step, e[0].elapsed_time(e[1]) * 1e-3))
+                    kept[L] = (out_ctu[:nch * ctus_step * hm.HM_CTU.itemsize].cpu().numpy().view(hm.HM_CTU).reshape(nch, ctus_step),
+                               out_rec[:nch * ctus_step * 6144].cpu().numpy().reshape(nch, ctus_step, 6144))
+                progress("closed loop: picture %d launch %d/%d %.1f s" % (t, L + 1, cl // ctus_step, e[0].elapsed_time(e[1]) * 1e-3))
             t1 = time.perf_counter()
             for s in range(segs):
                 dp = pictures[s]
@@ -586,9 +590,10 @@ def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=
         if t == pics - 1:
             last = (prm, qp, col_nref, entry, col_read)
         del eng
-    res = {"workload": "%d closed LDP segments (I + %d P pictures, %dx%d random 4:2:0 originals, one CTU row per slice: "
+    res = {"workload": "%d closed LDP segments (I + %d P pictures, %dx%d random 4:2:0 originals, %d CTU row(s) per slice: "
                        "%d chains), every P picture decided against device-made references (deblocked + SAO) and the "
-                       "device's collocated field; %d CTUs per chain per launch" % (segs, pics - 1, W, H, segs * hc, ctus_step),
+                       "device's collocated field; %d CTUs per chain per launch" % (segs, pics - 1, W, H, rows, segs * nch,
+                                                                                   ctus_step),
            "ctus_per_s": round(segs * n * (pics - 1) / t_p, 2), "basis": "P pictures: decision launches + loop filters / "
            "SAO / reference builds, wall clock", "pictures": per_pic}
     if parity:
@@ -604,17 +609,17 @@ def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=
                                             .astype(np.uint8).reshape(-1), cr16[40:40 + H // 2, 40:40 + W // 2].astype(np.uint8).reshape(-1)]))
         col_host = col_read.cpu().numpy() if col_read is not None else None
         t0 = time.perf_counter()
-        progress("closed loop: restatement parity (%d chains x %d CTUs)" % (hc, wc))
-        port = hm_ctu.chains(pi, pf, orgs[pics - 1], np.concatenate(ref_host), entry, np.arange(hc, dtype=np.int32) * wc,
-                             wc, wc, threads=threads, col_field=col_host)
+        progress("closed loop: restatement parity (%d chains x %d CTUs)" % (nch, cl))
+        port = hm_ctu.chains(pi, pf, orgs[pics - 1], np.concatenate(ref_host), entry, np.arange(nch, dtype=np.int32) * cl,
+                             cl, cl, threads=threads, col_field=col_host)
         got = {}
         for L, (ct, rc) in kept.items():
-            for k in range(hc):
+            for k in range(nch):
                 for i in range(ctus_step):
                     got[(k, L * ctus_step + i)] = (hm.unpack_parts(ct[k, i]["p"]), ct[k, i]["coef"], rc[k, i], ct[k, i]["cost"],
                                                   (ct[k, i]["bits"], ct[k, i]["dist"]))
-        mism, first = _compare_port(port, got, [(k, i) for k in range(hc) for i in range(wc)])
-        res.update(gpu_parity_ctus=hc * wc, gpu_parity_mismatches=mism, first_mismatches=first,
+        mism, first = _compare_port(port, got, [(k, i) for k in range(nch) for i in range(cl)])
+        res.update(gpu_parity_ctus=nch * cl, gpu_parity_mismatches=mism, first_mismatches=first,
                    parity_s=round(time.perf_counter() - t0, 1))
     del pictures, refs, org_frames
     torch.cuda.empty_cache()
