@@ -489,6 +489,26 @@ LDP_GOP = {1: (3, 0.4624, 2), 2: (2, 0.4624, 1), 3: (3, 0.4624, 2), 4: (1, 0.578
 LDP_SAO_LAYER = {0: 0, 1: 2, 2: 1, 3: 2, 4: 0}
 
 
+def closed_loop_geometry(W, H, rows, ctus_step):
+    """The closed-loop figure's slicing: (CTUs per row, CTU rows, chains per picture, CTUs per chain).
+    One chain per slice of `rows` CTU rows; a partial bottom row must share its slice with the row
+    above (its picture-boundary CTUs read TEncSearch::m_integerMv2Nx2N as the CTU before them left it,
+    DESIGN.md section 5)."""
+    assert W % 64 == 0 and (H % 64 == 0 or rows >= 2), "a partial bottom row needs a slice of >= 2 rows"
+    wc, hc = W // 64, (H + 63) // 64
+    assert hc % rows == 0, "equal slices"
+    nch, cl = hc // rows, rows * wc
+    assert cl % ctus_step == 0, "whole launches per chain"
+    return wc, hc, nch, cl
+
+
+def closed_loop_specs(segs, nch, cl, launch, ctus_step):
+    """_chain_jobs specs of launch `launch` of a closed-loop picture set: every segment's chains,
+    `ctus_step` CTUs each from CTU launch * ctus_step of its slice, resumed after the first launch."""
+    return [(s, c * cl + launch * ctus_step, ctus_step, c * cl, c * cl + cl - 1, launch > 0)
+            for s in range(segs) for c in range(nch)]
+
+
 def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=6, threads=16, parity=True, rows=1):
     """Side figure (config 5): closed LDP segments decided entirely on the device --
     `segs` segments in flight (W x H random 4:2:0 originals, `rows` CTU rows per slice, one chain
@@ -504,13 +524,7 @@ def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=
     import torch
     from concurrent.futures import ThreadPoolExecutor
     from video_codecs_amd import _abi, hm, synth
-    # a partial bottom CTU row must share its slice (its chain) with the row above: its picture-boundary
-    # CTUs read TEncSearch::m_integerMv2Nx2N as the CTU before them left it
-    assert W % 64 == 0 and (H % 64 == 0 or rows >= 2)
-    wc, hc = W // 64, (H + 63) // 64
-    assert hc % rows == 0
-    nch, cl = hc // rows, rows * wc  # chains per picture, CTUs per chain (one slice each)
-    assert cl % ctus_step == 0
+    wc, hc, nch, cl = closed_loop_geometry(W, H, rows, ctus_step)  # chains per picture, CTUs per chain
     n = wc * hc
     eb = _abi.load_entropy_bits()
     init = _abi.load_ctx_init_states()
@@ -554,8 +568,7 @@ def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=
         launch_s = 0.0
         with torch.cuda.stream(stream):
             for L in range(cl // ctus_step):
-                specs = [(s, c * cl + L * ctus_step, ctus_step, c * cl, c * cl + cl - 1, L > 0)
-                         for s in range(segs) for c in range(nch)]
+                specs = closed_loop_specs(segs, nch, cl, L, ctus_step)
                 jt = torch.from_numpy(_chain_jobs(specs, entry).view(np.uint8).reshape(-1).copy()).cuda()
                 e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 e[0].record()

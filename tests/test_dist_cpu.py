@@ -204,3 +204,25 @@ def test_two_rank_closed_segments_gloo(tmp_path):
     psz = refs0.shape[1]
     for k, q in enumerate(int(p) for p in g["refpic_poc"]):
         np.testing.assert_array_equal(refs0[q], g["refpic"][k * psz:(k + 1) * psz])
+
+
+def test_closed_loop_geometry_and_jobs():
+    """bench.closed_loop_measure's slicing (CPU): at 1088p one chain per CTU row; at 2160p two rows
+    per slice, the partial bottom row inside the last slice (a one-row slicing is refused); every
+    launch's jobs advance every chain by the same CTUs, and the launches of a picture cover each
+    slice's CTUs exactly once, resumed after the first."""
+    import bench
+    assert bench.closed_loop_geometry(1920, 1088, 1, 6) == (30, 17, 17, 30)
+    assert bench.closed_loop_geometry(3840, 2160, 2, 8) == (60, 34, 17, 120)
+    with pytest.raises(AssertionError):
+        bench.closed_loop_geometry(3840, 2160, 1, 6)
+    wc, hc, nch, cl = bench.closed_loop_geometry(3840, 2160, 2, 8)
+    seen = {}
+    for L in range(cl // 8):
+        for seg, first, n, s0, s1, resume in bench.closed_loop_specs(3, nch, cl, L, 8):
+            assert s0 <= first and first + n - 1 <= s1 and s1 - s0 + 1 == cl and resume == (L > 0)
+            for a in range(first, first + n):
+                seen[(seg, a)] = seen.get((seg, a), 0) + 1
+    assert sorted(seen) == [(s, a) for s in range(3) for a in range(wc * hc)] and set(seen.values()) == {1}
+    # encoder_lowdelay_P_main.cfg:24-27 (Frame1..4: QP offset, QPFactor)
+    assert [bench.LDP_GOP[k][:2] for k in (1, 2, 3, 4)] == [(3, 0.4624), (2, 0.4624), (3, 0.4624), (1, 0.578)]
