@@ -415,6 +415,20 @@ def test_hm_finish_picture_gpu(torch, ctu_name, dbk_name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("w,h", [(200, 176), (136, 184)])
+def test_hm_partial_ctus_gpu(torch, w, h):
+    """Pictures whose right CTU column and bottom CTU row are both partial (8 / 56 px wide, 48 / 56
+    lines high), decided the bench's way (HmWorkload: one chain per row slice, the partial bottom row
+    continuing the chain of the row above) to the end of the picture: every CTU equal to the
+    restatement's (boundary-forced splits, clipped search windows and MVs, TMVP at the edges)."""
+    import bench
+    hvx.context()
+    r = bench.hm_merged_chain_parity(4, W=w, H=h)
+    assert r["gpu_parity_mismatches"] == 0, r["first_mismatches"]
+    assert r["ctus"] == ((w + 63) // 64) * ((h + 63) // 64)
+
+
+@pytest.mark.gpu
 def test_closed_loop_segments_gpu(torch):
     """The bench's closed-loop figure in miniature (bench.closed_loop_measure): two LDP segments of
     256x192 random pictures (I, P, P), every P picture decided against the references and collocated
