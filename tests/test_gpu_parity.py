@@ -429,6 +429,19 @@ def test_hm_partial_ctus_gpu(torch, w, h):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("base_qp", [0, 49])
+def test_hm_extreme_qp_gpu(torch, base_qp):
+    """The decision at the ends of the QP range (slice QP 2 and 51: the bench picture's GOP offset on
+    base QP 0 / 49) on random content: at QP 2 the levels run into the thousands (escape codes with
+    the Rice parameter at its cap, RDOQ's max / max-1 candidates far from 0), at QP 51 almost every
+    level is 0 -- a 256x176 picture decided to the end, every CTU equal to the restatement's."""
+    import bench
+    hvx.context()
+    r = bench.hm_merged_chain_parity(4, base_qp=base_qp)
+    assert r["gpu_parity_mismatches"] == 0, r["first_mismatches"]
+
+
+@pytest.mark.gpu
 def test_closed_loop_segments_gpu(torch):
     """The bench's closed-loop figure in miniature (bench.closed_loop_measure): two LDP segments of
     256x192 random pictures (I, P, P), every P picture decided against the references and collocated
