@@ -23,6 +23,10 @@ CASES = {  # name: (cfg, yuv kind, frames, qp[, width, height, extra encoder arg
     # BASELINE configs 2/3 size: 1080p, CTU-row slices (the throughput seam's chains; the partial
     # bottom row continues the chain of the row above)
     "ldp_smooth_1080p_qp32": ("ldp.cfg", "smooth", 2, 32, 1920, 1080, ["--SliceMode=1", "--SliceArgument=30"]),
+    # the ends of the QP range on random content: levels in the thousands (escape codes, the Rice
+    # parameter at its cap) and almost nothing coded
+    "ldp_rand_qp4": ("ldp.cfg", "random", 2, 4),
+    "ldp_rand_qp51": ("ldp.cfg", "random", 2, 51),
 }
 YUV_FRAMES = max(c[2] for c in CASES.values())
 W, H = 416, 240
