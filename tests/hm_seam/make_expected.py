@@ -27,6 +27,8 @@ CASES = {  # name: (cfg, yuv kind, frames, qp[, width, height, extra encoder arg
     # parameter at its cap) and almost nothing coded
     "ldp_rand_qp4": ("ldp.cfg", "random", 2, 4),
     "ldp_rand_qp51": ("ldp.cfg", "random", 2, 51),
+    # the search parameters the engine takes from the encoder: a smaller TZ window, AMP off
+    "ldp_rand_sr16_noamp_qp32": ("ldp.cfg", "random", 2, 32, 416, 240, ["--SearchRange=16", "--AMP=0"]),
 }
 YUV_FRAMES = max(c[2] for c in CASES.values())
 W, H = 416, 240
