@@ -24,11 +24,11 @@ CASES = {  # name: (cfg, yuv kind, frames, qp[, width, height, extra encoder arg
     # bottom row continues the chain of the row above)
     "ldp_smooth_1080p_qp32": ("ldp.cfg", "smooth", 2, 32, 1920, 1080, ["--SliceMode=1", "--SliceArgument=30"]),
     # the ends of the QP range on random content: levels in the thousands (escape codes, the Rice
-    # parameter at its cap) and almost nothing coded
-    "ldp_rand_qp4": ("ldp.cfg", "random", 2, 4),
-    "ldp_rand_qp51": ("ldp.cfg", "random", 2, 51),
+    # parameter at its cap) and almost nothing coded; 208x120 (a partial CTU column and row)
+    "ldp_rand_qp4": ("ldp.cfg", "random", 2, 4, 208, 120),
+    "ldp_rand_qp51": ("ldp.cfg", "random", 2, 51, 208, 120),
     # the search parameters the engine takes from the encoder: a smaller TZ window, AMP off
-    "ldp_rand_sr16_noamp_qp32": ("ldp.cfg", "random", 2, 32, 416, 240, ["--SearchRange=16", "--AMP=0"]),
+    "ldp_rand_sr16_noamp_qp32": ("ldp.cfg", "random", 2, 32, 208, 120, ["--SearchRange=16", "--AMP=0"]),
 }
 YUV_FRAMES = max(c[2] for c in CASES.values())
 W, H = 416, 240
