@@ -211,7 +211,7 @@ struct State {
 
 // the LDS leaf scratch (one leaf runs at a time): TU pipelines up to 16x16 and the intra
 // first pass.  The 32x32 TU pipeline, motion search and motion compensation keep theirs in the
-// chain state (global memory), which holds the LDS footprint of a chain's wave near 16 KB
+// chain state (global memory), which holds the LDS footprint of a chain's wave under 20 KB (8 waves per CU)
 union Leaf {
   TuSmem<0> tu0;
   TuSmem<1> tu1;
