@@ -85,6 +85,21 @@ def check_slice_seam(case, log):
     assert m and int(m.group(1)) == slices_of(case) and int(m.group(2)) > 0 and int(m.group(3)) == 0, log[-2000:]
 
 
+DECODER = os.path.join(ROOT, "oracle", "_ref", "TAppDecoder")
+
+
+def conformance(case, tmp):
+    """SURVEY 4's conformance check: the reference decoder (HM-16.5rc1 TAppDecoder, built from the
+    reference sources) decodes the device-written bitstream to exactly the encoder's reconstruction."""
+    if not os.path.exists(DECODER):
+        return
+    dec = os.path.join(tmp, case + ".dec.yuv")
+    p = subprocess.run([DECODER, "-b", os.path.join(tmp, case + ".bin"), "-o", dec], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr[-2000:]
+    rec = open(os.path.join(tmp, case + ".rec.yuv"), "rb").read()
+    assert open(dec, "rb").read() == rec, (case, "decoded pictures differ from the encoder's reconstruction")
+
+
 def test_expected_md5_cases_present():
     assert set(EXPECTED) == set(mk.CASES)
 
@@ -148,6 +163,7 @@ def test_hm_encoder_with_cu_seam_batched(case, monkeypatch):
     log = []
     with tempfile.TemporaryDirectory() as tmp:
         got = mk.encode(EXE, case, tmp, log)
+        conformance(case, tmp)
     print(log[0][-600:])
     frames = mk.CASES[case][2]
     w, h = mk.case_size(case)
