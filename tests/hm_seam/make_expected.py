@@ -29,6 +29,10 @@ CASES = {  # name: (cfg, yuv kind, frames, qp[, width, height, extra encoder arg
     "ldp_rand_qp51": ("ldp.cfg", "random", 2, 51, 208, 120),
     # the search parameters the engine takes from the encoder: a smaller TZ window, AMP off
     "ldp_rand_sr16_noamp_qp32": ("ldp.cfg", "random", 2, 32, 208, 120, ["--SearchRange=16", "--AMP=0"]),
+    # camera content: the 3-frame QCIF clip the reference's JM trees ship (jm14.1/bin/foreman_part_qcif.yuv,
+    # a data fixture, tests/golden/foreman_part_qcif.yuv), P and B slices
+    "foreman_ldp_qp27": ("ldp.cfg", "foreman", 3, 27, 176, 144),
+    "foreman_ldb_qp32": ("ldb.cfg", "foreman", 3, 32, 176, 144),
 }
 YUV_FRAMES = max(c[2] for c in CASES.values())
 W, H = 416, 240
@@ -46,7 +50,9 @@ def encode(binary, case, tmp, log=None):
     extra = CASES[case][6] if len(CASES[case]) > 6 else []
     w, h = case_size(case)
     yuv = os.path.join(tmp, f"{kind}_{w}x{h}.yuv")
-    if not os.path.exists(yuv):
+    if kind == "foreman":  # the reference's own clip (176x144, 3 frames)
+        yuv = os.path.join(ROOT, "tests", "golden", "foreman_part_qcif.yuv")
+    elif not os.path.exists(yuv):
         make_yuv.write_yuv(yuv, kind, w, h, YUV_FRAMES if (w, h) == (W, H) else frames)
     bs, rec = os.path.join(tmp, case + ".bin"), os.path.join(tmp, case + ".rec.yuv")
     # the encoder's per-picture lines go to HVX_SEAM_LOG_DIR/<case>.log when set (progress of a long run)
