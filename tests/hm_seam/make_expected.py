@@ -33,6 +33,7 @@ CASES = {  # name: (cfg, yuv kind, frames, qp[, width, height, extra encoder arg
     # a data fixture, tests/golden/foreman_part_qcif.yuv), P and B slices
     "foreman_ldp_qp27": ("ldp.cfg", "foreman", 3, 27, 176, 144),
     "foreman_ldb_qp32": ("ldb.cfg", "foreman", 3, 32, 176, 144),
+    "foreman_intra_qp22": ("intra.cfg", "foreman", 3, 22, 176, 144),
 }
 YUV_FRAMES = max(c[2] for c in CASES.values())
 W, H = 416, 240

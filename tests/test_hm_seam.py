@@ -143,7 +143,7 @@ def test_hm_encoder_with_cu_seam(case, monkeypatch):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("case", ["ldp_smooth_1080p_qp32", "ra_texture_qp32", "ldp_smooth_qp32", "intra_smooth_qp22",
                                   "ldp_rand_qp4", "ldp_rand_qp51", "ldp_rand_sr16_noamp_qp32", "foreman_ldp_qp27",
-                                  "foreman_ldb_qp32"])
+                                  "foreman_ldb_qp32", "foreman_intra_qp22"])
 def test_hm_encoder_with_cu_seam_batched(case, monkeypatch):
     """The throughput form of the CTU seam (HVX_SEAM_CU_BATCH=1): at each picture's first
     compressCtu call every slice of the picture is decided by ONE hvx_hm_compress launch (one chain
