@@ -581,16 +581,16 @@ def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=
                                out_rec[:nch * ctus_step * 6144].cpu().numpy().reshape(nch, ctus_step, 6144))
                 progress("closed loop: picture %d launch %d/%d %.1f s" % (t, L + 1, cl // ctus_step, e[0].elapsed_time(e[1]) * 1e-3))
             t1 = time.perf_counter()
-            for s in range(segs):
-                dp = pictures[s]
-                _, col_t = hm.finish_picture(dp, dbk, col_field=True)
-                st0 = entry
-                rates[s], _, _, _ = hm.sao_picture(dp, LDP_SAO_LAYER[t], rates[s], int(prm["slice_type"]), qp,
-                                                   sao_states=(st0[hm.SAO_CTX_MERGE], st0[hm.SAO_CTX_TYPE]))
+            for s in range(segs):  # deblocking (device boundary strengths) and the collocated field
+                _, cols[s] = hm.finish_picture(pictures[s], dbk, col_field=True)
+            # SAO: every segment's decision in one launch (one wave per picture)
+            sao = hm.sao_pictures(pictures, [LDP_SAO_LAYER[t]] * segs, rates, [int(prm["slice_type"])] * segs, [qp] * segs,
+                                  sao_states=[(entry[hm.SAO_CTX_MERGE], entry[hm.SAO_CTX_TYPE])] * segs)
+            for s in range(segs):  # the padded reference planes the next picture searches
+                rates[s] = sao[s][0]
                 ref = hm.DeviceFrame.blank(W, H)
-                hm.finish_picture(dp, None, ref_frame=ref)
+                hm.finish_picture(pictures[s], None, ref_frame=ref)
                 refs[s].insert(0, ref)
-                cols[s] = col_t
         stream.synchronize()
         t2 = time.perf_counter()
         per_pic.append({"poc": t, "slice": "I" if t == 0 else "P", "qp": qp, "decision_s": round(launch_s, 3),

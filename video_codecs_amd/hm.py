@@ -596,36 +596,59 @@ def sao_picture(pic, layer, disabled_rate, slice_type, qp, rate=0.75, rate_chrom
     used the other initialisation table -- the slice lambdas = the TrQuant lambdas), hvx_sao_apply into the picture's
     reconstruction.  Returns (the new SAO-off rates [3, 7], coded [nctu, 3, 8], applied SAO_CTU,
     slice-enabled flags)."""
+    return sao_pictures([pic], [layer], [disabled_rate], [slice_type], [qp], rate, rate_chroma, slice_ctus, test_off,
+                        [sao_states])[0]
+
+
+def sao_pictures(pics, layers, disabled_rates, slice_types, qps, rate=0.75, rate_chroma=0.5, slice_ctus=0, test_off=0,
+                 sao_states=None):
+    """sao_picture over several independent pictures (e.g. the same POC of many GOP segments): the
+    statistics and offsets per picture, the RD decisions of all of them in ONE hvx_sao_decide launch
+    (one wave per picture, concurrently), one synchronisation.  Per picture the same operations and
+    results as sao_picture; returns the list of its return tuples."""
     import torch
     from . import hvx
-    w, h, n = pic.w, pic.h, pic.wc * pic.hc
-    dev = pic.ctus_t.device
-    s = pic.struct
-    org = [(pic.org_t[0].data_ptr(), s.org_stride[0]), (pic.org_t[1].data_ptr(), s.org_stride[1]),
-           (pic.org_t[2].data_ptr(), s.org_stride[1])]
-    src_t = [t.clone() for t in pic.rec_t]  # offsetCTU reads SAOProcess's copy of the deblocked picture
-    src = [(src_t[c].data_ptr(), s.rec_stride[1 if c else 0]) for c in range(3)]
-    dst = [(pic.rec_t[c].data_ptr(), s.rec_stride[1 if c else 0]) for c in range(3)]
-    stats = torch.empty(n * 15 * _abi.SAO_STAT.itemsize, dtype=torch.uint8, device=dev)
-    hvx.sao_stats(org, src, w, h, stats)
-    en = sao_slice_enabled(layer, disabled_rate, rate, rate_chroma)
-    init = _abi.load_ctx_init_states()[slice_type, qp]
+    if sao_states is None:
+        sao_states = [None] * len(pics)
+    dev = pics[0].ctus_t.device
     eb = torch.from_numpy(_abi.load_entropy_bits().astype(np.int32)).to(dev)
-    coded = torch.zeros((n, 3, 8), dtype=torch.int32, device=dev)
-    recon = torch.zeros(n * _abi.SAO_CTU.itemsize, dtype=torch.uint8, device=dev)
-    en_out = torch.zeros(3, dtype=torch.int32, device=dev)
-    tot = torch.zeros(1, dtype=torch.float64, device=dev)
-    j = np.zeros(1, _abi.SAO_DECIDE_JOB)
-    j["pic_w"], j["pic_h"], j["slice_ctus"], j["test_off"] = w, h, slice_ctus, test_off
-    j["slice_enabled"], j["frac_lo"] = en, 0
-    j["sao_states"] = [init[SAO_CTX_MERGE], init[SAO_CTX_TYPE]] if sao_states is None else list(sao_states)
-    j["lambda"] = [s.tq_lambda[0], s.tq_lambda[1], s.tq_lambda[2]]
-    j["stats"], j["entropy_bits"], j["coded"] = stats.data_ptr(), eb.data_ptr(), coded.data_ptr()
-    j["recon"], j["slice_enabled_out"], j["total_cost"] = recon.data_ptr(), en_out.data_ptr(), tot.data_ptr()
-    jt = torch.from_numpy(j.view(np.uint8).reshape(-1).copy()).to(dev)
-    hvx.sao_decide(jt, 1)
-    hvx.sao_apply(src, dst, w, h, recon)
+    keep, outs = [], []
+    jobs = np.zeros(len(pics), _abi.SAO_DECIDE_JOB)
+    for k, pic in enumerate(pics):
+        w, h, n = pic.w, pic.h, pic.wc * pic.hc
+        s = pic.struct
+        org = [(pic.org_t[0].data_ptr(), s.org_stride[0]), (pic.org_t[1].data_ptr(), s.org_stride[1]),
+               (pic.org_t[2].data_ptr(), s.org_stride[1])]
+        src_t = [t.clone() for t in pic.rec_t]  # offsetCTU reads SAOProcess's copy of the deblocked picture
+        src = [(src_t[c].data_ptr(), s.rec_stride[1 if c else 0]) for c in range(3)]
+        dst = [(pic.rec_t[c].data_ptr(), s.rec_stride[1 if c else 0]) for c in range(3)]
+        stats = torch.empty(n * 15 * _abi.SAO_STAT.itemsize, dtype=torch.uint8, device=dev)
+        hvx.sao_stats(org, src, w, h, stats)
+        en = sao_slice_enabled(layers[k], disabled_rates[k], rate, rate_chroma)
+        init = _abi.load_ctx_init_states()[slice_types[k], qps[k]]
+        coded = torch.zeros((n, 3, 8), dtype=torch.int32, device=dev)
+        recon = torch.zeros(n * _abi.SAO_CTU.itemsize, dtype=torch.uint8, device=dev)
+        en_out = torch.zeros(3, dtype=torch.int32, device=dev)
+        tot = torch.zeros(1, dtype=torch.float64, device=dev)
+        j = jobs[k:k + 1]
+        j["pic_w"], j["pic_h"], j["slice_ctus"], j["test_off"] = w, h, slice_ctus, test_off
+        j["slice_enabled"], j["frac_lo"] = en, 0
+        st = sao_states[k]
+        j["sao_states"] = [init[SAO_CTX_MERGE], init[SAO_CTX_TYPE]] if st is None else list(st)
+        j["lambda"] = [s.tq_lambda[0], s.tq_lambda[1], s.tq_lambda[2]]
+        j["stats"], j["entropy_bits"], j["coded"] = stats.data_ptr(), eb.data_ptr(), coded.data_ptr()
+        j["recon"], j["slice_enabled_out"], j["total_cost"] = recon.data_ptr(), en_out.data_ptr(), tot.data_ptr()
+        keep.append((src_t, stats, tot))
+        outs.append((src, dst, w, h, coded, recon, en_out))
+    jt = torch.from_numpy(jobs.view(np.uint8).reshape(-1).copy()).to(dev)
+    hvx.sao_decide(jt, len(pics))
+    for src, dst, w, h, _, recon, _ in outs:
+        hvx.sao_apply(src, dst, w, h, recon)
     torch.cuda.synchronize()
-    rec_h = recon.cpu().numpy().view(_abi.SAO_CTU)
-    return (sao_update_rates(layer, rec_h, disabled_rate, rate, rate_chroma), coded.cpu().numpy(), rec_h,
-            list(en_out.cpu().numpy()))
+    res = []
+    for k, (_, _, _, _, coded, recon, en_out) in enumerate(outs):
+        rec_h = recon.cpu().numpy().view(_abi.SAO_CTU)
+        res.append((sao_update_rates(layers[k], rec_h, disabled_rates[k], rate, rate_chroma), coded.cpu().numpy(), rec_h,
+                    list(en_out.cpu().numpy())))
+    del keep
+    return res
