@@ -47,21 +47,25 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--pics", type=int, default=62, help="P pictures in flight per GPU (33 slice chains each at 2160p: "
-                                                        "62 -> 2046 chains, two waves per SIMD)")
-    p.add_argument("--ctus", type=int, default=1, help="CTUs each slice chain advances per step")
+    p.add_argument("--workload", choices=("auto", "steady", "closed"), default="auto",
+                   help="steady: the 2160p steady-state P pictures (the N=1 headline); closed: BASELINE config 5 -- "
+                        "closed LDP segments per rank with the DPB gather of finished pictures (the N>1 default)")
+    p.add_argument("--pics", type=int, default=62, help="steady: P pictures in flight per GPU (33 slice chains each at "
+                                                        "2160p: 62 -> 2046 chains, two waves per SIMD)")
+    p.add_argument("--ctus", type=int, default=1, help="steady: CTUs each slice chain advances per step")
+    p.add_argument("--segs", type=int, default=120, help="closed: segments per GPU (17 row-slice chains each at 1088p)")
+    p.add_argument("--closed-ctus", type=int, default=6, help="closed: CTUs each chain advances per step (launch)")
     p.add_argument("--cpu-ref-procs", type=int, default=0, help="HM TAppEncoder processes for the reference "
                                                                   "baseline (0: the host's CPU share)")
     p.add_argument("--no-cpu-ref", action="store_true", help="skip the reference HM timing")
-    p.add_argument("--no-ra", action="store_true", help="skip the config-4 side figure (RA B pictures, SSIM cost)")
-    p.add_argument("--no-slice0", action="store_true", help="skip the SliceMode 0 side figure")
+    p.add_argument("--no-ra", action="store_true", help="skip the config-4 side figure (closed RA segments, stVSSIM cost)")
     p.add_argument("--width", type=int, default=3840)
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--nref", type=int, default=4)
     p.add_argument("--qp", type=int, default=32)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-1080p", action="store_true", help="skip the 1080p side measurement")
-    p.add_argument("--no-closed", action="store_true", help="skip the closed-loop LDP segment side figure (config 5: "
+    p.add_argument("--no-closed", action="store_true", help="skip the config-5 side figure (closed LDP segments: "
                                                             "120 segments of 1920x1088 I + 2 P pictures, ~2 minutes)")
     return p.parse_args()
 
@@ -183,25 +187,8 @@ class HmPlan:
 
 
 def host_pic_arrays(W, H, prm, qp, col_nref=(4, 0)):
-    """A picture's slice parameters (hm.DevicePicture's params dict) as the restatement's pic_i32 /
-    pic_f64 arrays (oracle/cu_capture.cpp layout: hm_cases.P_* fields)."""
-    pi = np.zeros(46, np.int32)
-    nref = prm["nref"]
-    pi[0:7] = [W, H, prm["poc"], prm["slice_type"], qp, nref[0], nref[1]]
-    pi[7:11] = [int(prm["ref_poc"][0][k]) if k < nref[0] else -1 for k in range(4)]
-    pi[11:15] = [int(prm["ref_poc"][1][k]) if k < nref[1] else -1 for k in range(4)]
-    pi[15:19] = [int(prm["ref_plane"][0][k]) if k < nref[0] else -1 for k in range(4)]
-    pi[19:23] = [int(prm["ref_plane"][1][k]) if k < nref[1] else -1 for k in range(4)]
-    pi[23:29] = [prm["col_from_l0"], 0, prm["check_ldc"], prm["tmvp"], prm["max_merge"], prm["col_poc"]]
-    pi[29:31] = col_nref
-    pi[31:35] = prm["col_ref_poc"][0]
-    pi[35:39] = prm["col_ref_poc"][1]
-    pi[39:41] = prm["chroma_qp"]
-    pi[41:43] = [0, ((W + 63) // 64) * ((H + 63) // 64)]
-    pi[43] = np.array(prm["lambda_motion"], np.uint32).view(np.int32)
-    pi[45] = int(prm["col_valid"])
-    pf = np.array([prm["lambda"], prm["sqrt_lambda"], *prm["chroma_weight"], *prm["tq_lambda"]], np.float64)
-    return pi, pf
+    from video_codecs_amd import gop
+    return gop.host_pic_arrays(W, H, prm, qp, col_nref)
 
 
 class HmWorkload(HmPlan):
@@ -272,52 +259,6 @@ class HmWorkload(HmPlan):
         self.step_idx += 1
 
 
-def _chain_jobs(specs, entry):
-    """HM_JOB records: specs = [(pic, first_ctu, n_ctus, slice_start, slice_end, resume)]."""
-    from video_codecs_amd import _abi, hm
-    j = np.zeros(len(specs), hm.HM_JOB)
-    for k, (pic, first, n, s0, s1, resume) in enumerate(specs):
-        j[k]["pic"], j[k]["first_ctu"], j[k]["n_ctus"], j[k]["chained"], j[k]["out"] = pic, first, n, 1, k * n
-        j[k]["slice_start"], j[k]["slice_end"] = s0, s1
-        j[k]["flags"] = _abi.HM_RESUME if resume else 0
-        j[k]["entry"]["st"] = entry
-    return j
-
-
-def _time_chains(eng, job_steps, n_out, warmup, keep=0):
-    """Launch warmup + timed steps of chain jobs on a private stream; returns (seconds per timed
-    step from HIP events, wall seconds per timed step, kept) -- kept: per step, copies of the first
-    `keep` output slots (HM_CTU records, reconstructions) for a parity check after the timing."""
-    import torch
-    from video_codecs_amd import hm
-    stream = torch.cuda.Stream()
-    out_ctu = torch.zeros(n_out * hm.HM_CTU.itemsize, dtype=torch.uint8, device="cuda")
-    out_rec = torch.zeros(n_out * 6144, dtype=torch.uint8, device="cuda")
-    dev_jobs = [torch.from_numpy(j.view(np.uint8).reshape(-1).copy()).cuda() for j in job_steps]
-    n_jobs = len(job_steps[0])
-    torch.cuda.synchronize()
-    ev, kept = [], []
-    t0 = None
-    with torch.cuda.stream(stream):
-        for k, jt in enumerate(dev_jobs):
-            if k == warmup:
-                stream.synchronize()
-                t0 = time.perf_counter()
-            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            e[0].record()
-            eng.launch(jt, n_jobs, out_ctu, out_rec)
-            e[1].record()
-            ev.append(e)
-            e[1].synchronize()
-            progress("side-figure step %d/%d: %.1f ms" % (k + 1, len(dev_jobs), e[0].elapsed_time(e[1])))
-            if keep:
-                kept.append((out_ctu[:keep * hm.HM_CTU.itemsize].clone(), out_rec[:keep * 6144].clone()))
-    stream.synchronize()
-    wall = (time.perf_counter() - t0) / (len(dev_jobs) - warmup)
-    ms = sum(a.elapsed_time(b) for a, b in ev[warmup:]) / (len(dev_jobs) - warmup)
-    return ms * 1e-3, wall, kept
-
-
 def compare_chain_ctus(port, dev_parts, dev_coef, dev_rec, dev_cost, dev_bd):
     """Mismatches between the restatement's outputs (hm_ctu.chains, CTU o) and the device's records
     of the same CTUs (arrays indexed o): partitions, coefficients, reconstruction, totals."""
@@ -344,298 +285,216 @@ def compare_chain_ctus(port, dev_parts, dev_coef, dev_rec, dev_cost, dev_bd):
     return mism, first
 
 
-def stv_history_frames(W, H, n=25, seed=8000):
-    """A synthetic stVSSIM history (hvx_hm_picture.hist) of n previous pictures, most recent first: random
-    4:2:0 originals and reconstructions = original + a seeded +-3 perturbation (clipped)."""
-    from video_codecs_amd import synth
-    rng = np.random.default_rng(seed)
-    out = []
-    for k in range(n):
-        org = yuv_split(synth.random_frame(W, H, seed + k), W, H)
-        rec = [np.clip(p.astype(np.int16) + rng.integers(-3, 4, p.shape, dtype=np.int16), 0, 255).astype(np.uint8)
-               for p in org]
-        out.append(tuple(np.ascontiguousarray(p) for p in (*org, *rec)))
-    return out
+def closed_seed(rank, segs, s, poc):
+    """The synthetic frame index of segment s's picture `poc` on `rank`: disjoint across segments and
+    ranks (BASELINE.md sec. 3 recipe, synth.random_frame)."""
+    return 30000 + (rank * segs + s) * 64 + poc
 
 
-def ra_ssim_measure(W, H, pics=62, distinct=12, qps=(22, 27, 32, 37), warmup=1, steps=10, parity_threads=16):
-    """BASELINE config 4 (side figure): 2160p random-access B pictures with the stvssim encoder's active
-    stVSSIM cost in the decision (hvx_hm_compress, HVX_RD_STVSSIM: distortionstVSSIM stvssim.c:831 over a
-    full 25-picture history + the current picture, the direction map from the collocated field, eta 1)
-    at QP 22 / 27 / 32 / 37.  The picture is GOP position 2 of encoder_randomaccess_main.cfg in the
-    fourth GOP (POC 28, coding index 26, TId 1: QP offset 2, QPFactor 0.3536, L0 = {24, 32}, L1 = {32,
-    24}, TMVP from L1[0], BipredSearchRange 4), `pics` pictures in flight (over `distinct` synthetic frame
-    triples, one shared synthetic history), every CTU row a slice (the partial bottom row chained after
-    the row above); one step = every chain one CTU, `steps` timed steps after `warmup`.  The B-slice
-    decision is pinned to HM by the RA captures (tests/golden/ctu_ra_q*.bin); here every CTU of picture
-    0's chains the GPU decided is re-decided by the restatement with the same cost and history
-    (oracle/hvx_oracle_cu.c hvxo_hm_chains_stv) and compared bit for bit."""
-    import torch
-    from concurrent.futures import ThreadPoolExecutor
-    import oracle  # noqa: F401  (test infrastructure: the parity checker, after the timing)
-    from oracle import hm_ctu
-    from video_codecs_amd import _abi, hm, synth
-    wc, hc = (W + 63) // 64, (H + 63) // 64
-    eb = _abi.load_entropy_bits()
-    with ThreadPoolExecutor(8) as ex:
-        host = list(ex.map(lambda i: synth.random_frame(W, H, 7000 + i), range(3 * distinct)))
-    frames = [hm.DeviceFrame(yuv_split(f, W, H)) for f in host]
-    col_h = synthetic_col_field(wc * hc, 77)
-    col = torch.from_numpy(col_h).cuda()
-    hist = stv_history_frames(W, H)
-    dirs = hm.stv_direction_map(col_h, W, H)
-    stv = hm.StvHistory(hist, dirs)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    stv.prepare(W, H)  # the history sums, once per history (once per picture in an encode)
-    torch.cuda.synchronize()
-    prep_ms = (time.perf_counter() - t0) * 1e3
-    rows = hc - 1 if H % 64 else hc  # the partial bottom row chained after the row above (HmWorkload)
-    res = {}
-    for base_qp in qps:
-        qp = base_qp + 2
-        prm = hm.slice_params(0, qp, 0.3536)
-        entry = _abi.load_ctx_init_states()[0, qp]
-        prm.update(poc=28, nref=[2, 2], ref_poc=np.array([[24, 32, 0, 0], [32, 24, 0, 0]]),
-                   ref_plane=np.array([[0, 1, 0, 0], [1, 0, 0, 0]]), max_merge=5, tmvp=1, check_ldc=0, col_from_l0=0,
-                   col_valid=1, col_poc=32, col_ref_poc=np.array([[24, 16, 8, 0], [0] * 4]), search_range=64, amp=1,
-                   rd_metric=_abi.RD_STVSSIM, lambda_ssim=hm.lambda_ssim(qp))
-        pictures = []
-        for p in range(pics):
-            k = p % distinct
-            pictures.append(hm.DevicePicture(frames[3 * k + 2], [frames[3 * k], frames[3 * k + 1]], prm, eb, col_field=col,
-                                             stv=stv))
-        eng = hm.Engine(pictures)
-        job_steps = []
-        for pos in range(warmup + steps):
-            specs = [(p, r * wc + pos, 1, r * wc, r * wc + wc - 1, pos > 0) for p in range(pics) for r in range(rows)]
-            j = _chain_jobs(specs, entry)
-            if rows < hc:
-                j["flags"][rows - 1::rows] |= _abi.hm_slice_ctus(wc)
-            job_steps.append(j)
-        sec, wall, kept = _time_chains(eng, job_steps, pics * rows, warmup, keep=rows)
-        del eng, pictures
-        torch.cuda.empty_cache()
-        # parity: picture 0's `rows` chains, CTUs 0 .. warmup + steps - 1 of each, on the restatement
-        done = warmup + steps
-        pi, pf = host_pic_arrays(W, H, prm, qp, col_nref=(4, 0))
+class ClosedWorkload:
+    """Closed GOP segments on one GPU (BASELINE config 5's unit; config 4 with the stVSSIM cost):
+    `len(base_qps)` segments of W x H random 4:2:0 originals made on the device (synth.random_frame_torch,
+    frame indices closed_seed: distinct per segment and rank), the first `n_pics` pictures of HM's
+    `kind` ('ldp' / 'ra') segment structure, every picture decided by hvx_hm_compress against the
+    references its own segment's loop made on the device (video_codecs_amd/gop.py ClosedSegments:
+    deblocking + SAO + slice writer + cabac_init choice + padded references), chains of `rows` CTU rows
+    stepping `ctus_step` CTUs per launch.  dpb: a DpbGather -- after every picture each segment's
+    finished (deblocked + SAO) reconstruction is gathered to rank 0.  One step() = one launch (and, after
+    a picture's last launch, its loop)."""
+
+    def __init__(self, W, H, base_qps, n_pics, rank, kind="ldp", rows=1, ctus_step=6, rd_metric=0, dpb=None,
+                 device="cuda", segments_cls=None):
+        import torch
+        from video_codecs_amd import gop, synth
+        self.W, self.H, self.rank, self.kind = W, H, rank, kind
+        segs = len(base_qps)
+        self.plan = gop.load_plan(kind, n_pics)
+        self.frames = {}
+        for s in range(segs):
+            for g in self.plan:
+                f = synth.random_frame_torch(W, H, closed_seed(rank, segs, s, g.poc), device)
+                ysz, csz = W * H, W * H // 4
+                self.frames[(s, g.poc)] = (f[:ysz].view(H, W), f[ysz:ysz + csz].view(H // 2, W // 2),
+                                           f[ysz + csz:].view(H // 2, W // 2))
+        self.dpb, self.gathered = dpb, []
+        self.cs = (segments_cls or gop.ClosedSegments)(
+            self.plan, W, H, list(base_qps), lambda s, poc: self.frames[(s, poc)], rows=rows, ctus_step=ctus_step,
+            rd_metric=rd_metric, on_finished=self._finished if dpb is not None else None, device=device)
+        self.cs.launch_events = []
+        self.stream = torch.cuda.Stream() if device != "cpu" else None
+        self.units_per_step = segs * self.cs.nch * self.cs.ctus_step
+        if device != "cpu":
+            torch.cuda.synchronize()
+
+    def _finished(self, t, recs):
+        """The DPB gather of picture t: every segment's final reconstruction into the rank's send buffer,
+        then one asynchronous gather to rank 0 (video_codecs_amd/dpb.py)."""
+        buf = self.dpb.buffer()
+        W, H = self.W, self.H
+        psz, ysz, csz = W * H * 3 // 2, W * H, W * H // 4
+        for s, (y, cb, cr) in enumerate(recs):
+            o = s * psz
+            buf[o:o + ysz].copy_(y.reshape(-1))
+            buf[o + ysz:o + ysz + csz].copy_(cb.reshape(-1))
+            buf[o + ysz + csz:o + psz].copy_(cr.reshape(-1))
+        self.dpb.send()
+        self.gathered.append(t)
+
+    def step(self):
+        import contextlib
+        import torch
+        with torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext():
+            self.cs.step()
+
+    def launch_seconds(self, first=0):
+        """(seconds, CTUs, algorithmic bytes) of the decision launches from launch `first` on (HIP events)."""
+        from video_codecs_amd import gop
+        sec = ctus = byt = 0
+        for t, n, (a, b) in self.cs.launch_events[first:]:
+            sec += a.elapsed_time(b) * 1e-3
+            ctus += n
+            g = self.plan[t]
+            byt += n * b_ctu(len(g.ref_pocs()) if g.slice_type != gop.I_SLICE else 0)
+        return sec, ctus, byt
+
+    def workload(self):
+        cs = self.cs
+        return ("%d closed %s segments (HM's %s structure: %s; %dx%d random 4:2:0 originals, %d CTU row(s) per slice: "
+                "%d chains) decided entirely on the device: every picture against the references its own segment's "
+                "loop made (deblocking + SAO + slice writer + cabac_init choice), %d CTUs per chain per launch" % (
+                    len(cs.segs), self.kind.upper(), "encoder_lowdelay_P_main" if self.kind == "ldp" else
+                    "encoder_randomaccess_main", "POC " + ",".join(str(g.poc) for g in self.plan), self.W, self.H,
+                    cs.rows, len(cs.segs) * cs.nch, cs.ctus_step))
+
+
+class ClosedParity:
+    """A restatement parity sample of a ClosedWorkload: segment `seg`'s picture `t` -- its inputs (the
+    device-made references, collocated field, history, slice parameters) captured when the picture is set
+    up, the device's CTU records of `chains` captured after each launch -- re-decided by
+    oracle/hvx_oracle_cu.c after the run (test infrastructure: the checker, outside any timed region)."""
+
+    def __init__(self, work, t, seg, chains):
+        self.work, self.t, self.seg, self.chains = work, t, seg, chains
+        self.inputs, self.got = None, {}
+        cs = work.cs
+        begin, after = cs.begin, cs.after_launch
+
+        def hooked_begin():
+            begin()
+            if cs.t == self.t:
+                self._capture_inputs()
+
+        def hooked_after(L):
+            after(L)
+            if cs.t == self.t:
+                from video_codecs_amd import hm
+                ct = cs.out_ctu.cpu().numpy().view(hm.HM_CTU)
+                rc = cs.out_rec.cpu().numpy().reshape(-1, 6144)
+                for c in self.chains:
+                    k = self.seg * cs.nch + c
+                    for i in range(cs.ctus_step):
+                        self.got[(c, L * cs.ctus_step + i)] = (ct[k * cs.ctus_step + i], rc[k * cs.ctus_step + i])
+        cs.begin, cs.after_launch = hooked_begin, hooked_after
+
+    def _capture_inputs(self):
+        from video_codecs_amd import _abi, gop, hm
+        cs, s, W, H = self.work.cs, self.seg, self.work.W, self.work.H
+        prm, qp, entry, table, planes, col_nref = cs.picture_params(s, self.t)
+        seg = cs.segs[s]
+        refs = []
+        m8 = hm.DeviceFrame.M8
+        for p in planes:
+            y8, _, cb16, cr16 = (x.cpu().numpy() for x in seg.dpb[p].planes())
+            refs.append(np.concatenate([y8[m8:m8 + H, m8:m8 + W].reshape(-1), cb16[40:40 + H // 2, 40:40 + W // 2]
+                                        .astype(np.uint8).reshape(-1), cr16[40:40 + H // 2, 40:40 + W // 2].astype(np.uint8).reshape(-1)]))
+        g = self.work.plan[self.t]
+        col = seg.cols[g.col_poc].cpu().numpy() if g.col_poc is not None else None
+        stv = None
+        if cs.rd_metric == _abi.RD_STVSSIM:
+            stv = ([tuple(x.cpu().numpy() for x in fr) for fr in seg.hist[:_abi.STV_HIST]], gop.stv_direction_map(col, W, H))
+        org = np.concatenate([x.cpu().numpy().reshape(-1) for x in self.work.frames[(s, g.poc)]])
+        self.inputs = (prm, qp, entry, col_nref, refs, col, stv, org)
+
+    def check(self, threads):
+        """Re-decide the sampled chains on the host and compare every CTU: (ctus, mismatches, first, seconds)."""
+        import oracle  # noqa: F401  (test infrastructure: the checker, after the timing)
+        from oracle import hm_ctu
+        from video_codecs_amd import gop
+        prm, qp, entry, col_nref, refs, col, stv, org = self.inputs
+        cs, W, H = self.work.cs, self.work.W, self.work.H
+        pi, pf = gop.host_pic_arrays(W, H, prm, qp, col_nref=col_nref)
         t0 = time.perf_counter()
-        progress("config 4 QP %d: restatement parity (%d chains x %d CTUs)" % (base_qp, rows, done))
-        port = hm_ctu.chains(pi, pf, host[2], np.concatenate([host[0], host[1]]), entry,
-                             np.arange(rows, dtype=np.int32) * wc, done, wc, threads=parity_threads, col_field=col_h,
-                             rd_metric=_abi.RD_STVSSIM, lambda_ssim=prm["lambda_ssim"], stv=(hist, dirs))
-        port_s = time.perf_counter() - t0
-        dev = [(ct.cpu().numpy().view(hm.HM_CTU), rc.cpu().numpy().reshape(rows, 6144)) for ct, rc in kept]
-        order = [(k, s) for k in range(rows) for s in range(done)]  # the port's CTU order: chain-major
-        mism, first = compare_chain_ctus(
-            port, np.stack([hm.unpack_parts(dev[s][0][k]["p"]) for k, s in order]),
-            np.stack([dev[s][0][k]["coef"] for k, s in order]), np.stack([dev[s][1][k] for k, s in order]),
-            np.array([dev[s][0][k]["cost"] for k, s in order]),
-            np.array([[dev[s][0][k]["bits"], dev[s][0][k]["dist"]] for k, s in order], np.uint32))
-        res[str(base_qp)] = {"slice_qp": qp, "ctus_per_s": round(pics * rows / sec, 2), "ms_per_step": round(sec * 1e3, 1),
-                             "wall_ms_per_step": round(wall * 1e3, 1), "lambda_ssim": prm["lambda_ssim"],
-                             "gpu_parity_ctus": len(order), "gpu_parity_mismatches": mism, "first_mismatches": first,
-                             "port_ctus_per_s": round(len(order) / port_s, 2)}
-    return {"workload": "2160p RA B pictures (GOP position 2 of the fourth GOP: POC 28, L0 {24,32} / L1 {32,24}, bi-pred "
-                        "+ bBi refinement), stVSSIM cost (distortionstVSSIM over a 25-picture history, direction map from "
-                        "the collocated field) in TEncCu's decisions, eta 1, %d pictures x %d row-slice chains, %d timed "
-                        "steps after %d warmup; parity: picture 0's chains re-decided by oracle/hvx_oracle_cu.c on %d host "
-                        "threads" % (pics, rows, steps, warmup, parity_threads),
-            "rd_metric": "HVX_RD_STVSSIM", "hist_n": len(hist), "stv_prepare_ms": round(prep_ms, 1), "per_qp": res}
+        port = hm_ctu.chains(pi, pf, org, np.concatenate(refs) if refs else np.zeros(1, np.uint8), entry,
+                             np.array(self.chains, np.int32) * cs.cl, cs.cl, cs.cl, threads=threads, col_field=col,
+                             rd_metric=prm.get("rd_metric", 0), lambda_ssim=prm.get("lambda_ssim", 0.0), stv=stv)
+        from video_codecs_amd import hm
+        got = {k: (hm.unpack_parts(v[0]["p"]), v[0]["coef"], v[1], v[0]["cost"], (v[0]["bits"], v[0]["dist"]))
+               for k, v in self.got.items()}
+        order = [(c, i) for c in self.chains for i in range(cs.cl)]
+        mism, first = _compare_port(port, got, order)
+        return len(order), mism, first, round(time.perf_counter() - t0, 1)
 
 
-def slice_mode0_measure(W, H, chains=2040, distinct=16, nref=4, base_qp=32, warmup=1, steps=10):
-    """Side figure: the headline's P pictures coded with HM's default SliceMode 0 (one slice per
-    picture, encoder_lowdelay_P_main.cfg:63) -- `chains` independent single-slice 2160p pictures in
-    flight, one chain each (its own CTU array and reconstruction; the synthetic frames are shared by
-    `distinct` picture contents), every chain deciding its picture's CTUs in raster order from CTU 0.
-    Shows whether the headline rate depends on the row slices: it depends on the number of
-    independent chains, not on how a picture is sliced."""
+def closed_figure(work, threads, parity=None, first_timed_pic=1):
+    """Run every launch of a ClosedWorkload; report the pictures from `first_timed_pic` on (decision
+    launches by HIP events + their loops, wall clock) and the parity samples."""
     import torch
-    from concurrent.futures import ThreadPoolExecutor
-    from video_codecs_amd import _abi, hm, synth
-    wc, hc = (W + 63) // 64, (H + 63) // 64
-    qp = base_qp + HM_QP_OFFSET
-    eb = _abi.load_entropy_bits()
-    with ThreadPoolExecutor(8) as ex:
-        host = list(ex.map(lambda i: synth.random_frame(W, H, 9000 + i), range(distinct + nref)))
-    frames = [hm.DeviceFrame(yuv_split(f, W, H)) for f in host]
-    del host
-    col = torch.from_numpy(synthetic_col_field(wc * hc, 99)).cuda()
-    prm = hm.slice_params(1, qp, HM_QP_FACTOR)
-    poc = nref + 1
-    prm.update(poc=poc, nref=[nref, 0], ref_poc=np.array([[poc - 1 - k for k in range(4)], [0] * 4]),
-               ref_plane=np.array([list(range(nref)) + [0] * (4 - nref), [0] * 4]), max_merge=5, tmvp=1, check_ldc=1,
-               col_from_l0=1, col_valid=1, col_poc=poc - 1, col_ref_poc=np.array([[poc - 2 - k for k in range(4)], [0] * 4]),
-               search_range=64, amp=1)
-    entry = _abi.load_ctx_init_states()[1, qp]
-    pictures = []
-    for c in range(chains):
-        k = c % distinct
-        pictures.append(hm.DevicePicture(frames[nref + k], [frames[nref + k - 1 - r] for r in range(nref)], prm, eb,
-                                         col_field=col))
-    eng = hm.Engine(pictures)
-    n = wc * hc
-    job_steps = [_chain_jobs([(c, pos, 1, 0, n - 1, pos > 0) for c in range(chains)], entry) for pos in range(warmup + steps)]
-    sec, wall, _ = _time_chains(eng, job_steps, chains, warmup)
-    del eng, pictures
-    torch.cuda.empty_cache()
-    return {"workload": "%d single-slice (SliceMode 0) 2160p P pictures, one chain each, QP %d, %d refs" % (chains, qp, nref),
-            "ctus_per_s": round(chains / sec, 2), "ms_per_step": round(sec * 1e3, 1), "wall_ms_per_step": round(wall * 1e3, 1)}
-
-
-# encoder_lowdelay_P_main.cfg:24-27: Frame1..4 QP offset and QPFactor; GOP position 4 has depth 0
-LDP_GOP = {1: (3, 0.4624, 2), 2: (2, 0.4624, 1), 3: (3, 0.4624, 2), 4: (1, 0.578, 0)}
-LDP_SAO_LAYER = {0: 0, 1: 2, 2: 1, 3: 2, 4: 0}
-
-
-def closed_loop_geometry(W, H, rows, ctus_step):
-    """The closed-loop figure's slicing: (CTUs per row, CTU rows, chains per picture, CTUs per chain).
-    One chain per slice of `rows` CTU rows; a partial bottom row must share its slice with the row
-    above (its picture-boundary CTUs read TEncSearch::m_integerMv2Nx2N as the CTU before them left it,
-    DESIGN.md section 5)."""
-    assert W % 64 == 0 and (H % 64 == 0 or rows >= 2), "a partial bottom row needs a slice of >= 2 rows"
-    wc, hc = W // 64, (H + 63) // 64
-    assert hc % rows == 0, "equal slices"
-    nch, cl = hc // rows, rows * wc
-    assert cl % ctus_step == 0, "whole launches per chain"
-    return wc, hc, nch, cl
-
-
-def closed_loop_specs(segs, nch, cl, launch, ctus_step):
-    """_chain_jobs specs of launch `launch` of a closed-loop picture set: every segment's chains,
-    `ctus_step` CTUs each from CTU launch * ctus_step of its slice, resumed after the first launch."""
-    return [(s, c * cl + launch * ctus_step, ctus_step, c * cl, c * cl + cl - 1, launch > 0)
-            for s in range(segs) for c in range(nch)]
-
-
-def closed_loop_measure(W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=6, threads=16, parity=True, rows=1):
-    """Side figure (config 5): closed LDP segments decided entirely on the device --
-    `segs` segments in flight (W x H random 4:2:0 originals, `rows` CTU rows per slice, one chain
-    per slice), each an I picture and then P pictures decided against references the device made
-    (hvx_hm_compress -> hvx_hm_finish_picture: deblocking with device boundary strengths and the
-    collocated motion field -> hm.sao_picture -> the padded reference planes), the LDP GOP's QP
-    offsets / QPFactors / reference lists (encoder_lowdelay_P_main.cfg:24-27, first GOP).  Each
-    picture's chains advance `ctus_step` CTUs per launch until their rows are done; then every
-    segment's picture is finished into its next reference.  Reported: the P pictures' CTUs per second
-    over their decision launches plus their loop filters / SAO / reference builds (wall clock), and a
-    restatement parity sample: segment 0's last P picture re-decided by the restatement on 16 host
-    threads against the device-made references and collocated field, every CTU compared."""
-    import torch
-    from concurrent.futures import ThreadPoolExecutor
-    from video_codecs_amd import _abi, hm, synth
-    wc, hc, nch, cl = closed_loop_geometry(W, H, rows, ctus_step)  # chains per picture, CTUs per chain
-    n = wc * hc
-    eb = _abi.load_entropy_bits()
-    init = _abi.load_ctx_init_states()
-    dbk = _abi.deblock_params(W, H)
-    with ThreadPoolExecutor(8) as ex:
-        orgs = list(ex.map(lambda i: synth.random_frame(W, H, 30000 + i), range(segs * pics)))
-    org_frames = [hm.DeviceFrame(yuv_split(f, W, H)) for f in orgs]
-    refs = [[] for _ in range(segs)]  # per segment: device-made reference frames, most recent first
-    cols = [None] * segs
-    rates = [np.zeros((3, 7)) for _ in range(segs)]
-    stream = torch.cuda.Stream()
-    out_ctu = torch.zeros(segs * nch * ctus_step * hm.HM_CTU.itemsize, dtype=torch.uint8, device="cuda")
-    out_rec = torch.zeros(segs * nch * ctus_step * 6144, dtype=torch.uint8, device="cuda")
-    per_pic, kept, last = [], {}, None
-    t_p = 0.0
-    for t in range(pics):
-        if t == 0:
-            qp, st_idx = base_qp, 2
-            prm = hm.slice_params(2, qp, 0.57 * (1.0 - min(0.5, 0.05 * 3)), gop_depth=0)  # I: 0.57 * dLambda_scale
-            prm.update(poc=0, nref=[0, 0], ref_poc=np.zeros((2, 4), int), ref_plane=np.zeros((2, 4), int), max_merge=5,
-                       tmvp=1, check_ldc=1, col_from_l0=1, col_valid=0, col_poc=0, col_ref_poc=np.zeros((2, 4), int),
-                       search_range=64, amp=1)
-            col_nref = (0, 0)
-        else:
-            off, fac, depth = LDP_GOP[t]
-            qp, st_idx = base_qp + off, 1
-            nr = min(t, 4)
-            prm = hm.slice_params(1, qp, fac, gop_depth=depth)
-            prm.update(poc=t, nref=[nr, 0], ref_poc=np.array([[t - 1 - k if k < nr else 0 for k in range(4)], [0] * 4]),
-                       ref_plane=np.array([[k if k < nr else 0 for k in range(4)], [0] * 4]), max_merge=5, tmvp=1,
-                       check_ldc=1, col_from_l0=1, col_valid=1, col_poc=t - 1,
-                       col_ref_poc=np.array([[t - 2 - k if k < min(t - 1, 4) else 0 for k in range(4)], [0] * 4]),
-                       search_range=64, amp=1)
-            col_nref = (min(t - 1, 4), 0)
-        entry = init[st_idx, qp]
-        col_read = cols[0]  # the collocated field segment 0's picture reads (the parity sample's)
-        pictures = [hm.DevicePicture(org_frames[s * pics + t], refs[s][:4], prm, eb, col_field=cols[s]) for s in range(segs)]
-        eng = hm.Engine(pictures)
+    t_run = 0.0
+    per_pic = []
+    nl = work.cs.launches
+    for t in range(len(work.plan)):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        launch_s = 0.0
-        with torch.cuda.stream(stream):
-            for L in range(cl // ctus_step):
-                specs = closed_loop_specs(segs, nch, cl, L, ctus_step)
-                jt = torch.from_numpy(_chain_jobs(specs, entry).view(np.uint8).reshape(-1).copy()).cuda()
-                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                e[0].record()
-                eng.launch(jt, len(specs), out_ctu, out_rec)
-                e[1].record()
-                e[1].synchronize()
-                launch_s += e[0].elapsed_time(e[1]) * 1e-3
-                if t == pics - 1 and parity:  # segment 0's chains (jobs 0 .. hc-1): the pre-loop-filter records
-                    kept[L] = (out_ctu[:nch * ctus_step * hm.HM_CTU.itemsize].cpu().numpy().view(hm.HM_CTU).reshape(nch, ctus_step),
-                               out_rec[:nch * ctus_step * 6144].cpu().numpy().reshape(nch, ctus_step, 6144))
-                progress("closed loop: picture %d launch %d/%d %.1f s" % (t, L + 1, cl // ctus_step, e[0].elapsed_time(e[1]) * 1e-3))
-            t1 = time.perf_counter()
-            for s in range(segs):  # deblocking (device boundary strengths) and the collocated field
-                _, cols[s] = hm.finish_picture(pictures[s], dbk, col_field=True)
-            # SAO: every segment's decision in one launch (one wave per picture)
-            sao = hm.sao_pictures(pictures, [LDP_SAO_LAYER[t]] * segs, rates, [int(prm["slice_type"])] * segs, [qp] * segs,
-                                  sao_states=[(entry[hm.SAO_CTX_MERGE], entry[hm.SAO_CTX_TYPE])] * segs)
-            for s in range(segs):  # the padded reference planes the next picture searches
-                rates[s] = sao[s][0]
-                ref = hm.DeviceFrame.blank(W, H)
-                hm.finish_picture(pictures[s], None, ref_frame=ref)
-                refs[s].insert(0, ref)
-        stream.synchronize()
-        t2 = time.perf_counter()
-        per_pic.append({"poc": t, "slice": "I" if t == 0 else "P", "qp": qp, "decision_s": round(launch_s, 3),
-                        "decision_wall_s": round(t1 - t0, 3), "loop_s": round(t2 - t1, 3),
-                        "ctus_per_s": round(segs * n / (t2 - t0), 1)})
-        progress("closed loop: picture %d done (%d CTUs, decision %.1f s, loop filters + SAO + references %.1f s)" % (
-            t, segs * n, launch_s, t2 - t1))
-        if t > 0:
-            t_p += t2 - t0
-        if t == pics - 1:
-            last = (prm, qp, col_nref, entry, col_read)
-        del eng
-    res = {"workload": "%d closed LDP segments (I + %d P pictures, %dx%d random 4:2:0 originals, %d CTU row(s) per slice: "
-                       "%d chains), every P picture decided against device-made references (deblocked + SAO) and the "
-                       "device's collocated field; %d CTUs per chain per launch" % (segs, pics - 1, W, H, rows, segs * nch,
-                                                                                   ctus_step),
-           "ctus_per_s": round(segs * n * (pics - 1) / t_p, 2), "basis": "P pictures: decision launches + loop filters / "
-           "SAO / reference builds, wall clock", "pictures": per_pic}
-    if parity:
-        import oracle  # noqa: F401  (test infrastructure: the checker)
-        from oracle import hm_ctu
-        prm, qp, col_nref, entry, col_read = last
-        pi, pf = host_pic_arrays(W, H, prm, qp, col_nref=col_nref)
-        ref_host = []
-        for ref in refs[0][1:1 + prm["nref"][0]]:  # the references the last picture read (refs[0][0] is its own)
-            y8, _, cb16, cr16 = (x.cpu().numpy() for x in ref.planes())
-            m8 = hm.DeviceFrame.M8
-            ref_host.append(np.concatenate([y8[m8:m8 + H, m8:m8 + W].reshape(-1), cb16[40:40 + H // 2, 40:40 + W // 2]
-                                            .astype(np.uint8).reshape(-1), cr16[40:40 + H // 2, 40:40 + W // 2].astype(np.uint8).reshape(-1)]))
-        col_host = col_read.cpu().numpy() if col_read is not None else None
-        t0 = time.perf_counter()
-        progress("closed loop: restatement parity (%d chains x %d CTUs)" % (nch, cl))
-        port = hm_ctu.chains(pi, pf, orgs[pics - 1], np.concatenate(ref_host), entry, np.arange(nch, dtype=np.int32) * cl,
-                             cl, cl, threads=threads, col_field=col_host)
-        got = {}
-        for L, (ct, rc) in kept.items():
-            for k in range(nch):
-                for i in range(ctus_step):
-                    got[(k, L * ctus_step + i)] = (hm.unpack_parts(ct[k, i]["p"]), ct[k, i]["coef"], rc[k, i], ct[k, i]["cost"],
-                                                  (ct[k, i]["bits"], ct[k, i]["dist"]))
-        mism, first = _compare_port(port, got, [(k, i) for k in range(nch) for i in range(cl)])
-        res.update(gpu_parity_ctus=nch * cl, gpu_parity_mismatches=mism, first_mismatches=first,
-                   parity_s=round(time.perf_counter() - t0, 1))
-    del pictures, refs, org_frames
-    torch.cuda.empty_cache()
+        for _ in range(nl):
+            work.step()
+            progress("closed %s: picture %d (POC %d) launch %d/%d" % (work.kind, t, work.plan[t].poc, work.cs.L or nl, nl))
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        sec = sum(a.elapsed_time(b) * 1e-3 for tt, _, (a, b) in work.cs.launch_events if tt == t)
+        log = work.cs.log[t]
+        n = len(work.cs.segs) * work.cs.nch * work.cs.cl
+        per_pic.append(dict(log, decision_s=round(sec, 3), wall_s=round(wall, 3), ctus=n, ctus_per_s=round(n / wall, 1)))
+        if t >= first_timed_pic:
+            t_run += wall
+    n_timed = sum(p["ctus"] for p in per_pic[first_timed_pic:])
+    res = {"workload": work.workload(), "ctus_per_s": round(n_timed / t_run, 2) if t_run else None,
+           "basis": "pictures %s: decision launches + loop filters / SAO / slice writer / reference builds, wall clock" % (
+               ",".join(str(p["poc"]) for p in per_pic[first_timed_pic:])), "pictures": per_pic}
+    for key, par in (parity or {}).items():
+        progress("closed %s: restatement parity %s" % (work.kind, key))
+        n, mism, first, secs = par.check(threads)
+        res.setdefault("parity", {})[key] = {"ctus": n, "mismatches": mism, "first_mismatches": first, "seconds": secs}
+    return res
+
+
+def config5_measure(threads, W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_step=6, parity=True):
+    """Side figure, BASELINE config 5's unit on one GPU: the same ClosedWorkload the multi-GPU bench times
+    per rank (LDP, 120 segments of 1920x1088, I + P pictures); parity: segment 0's last picture."""
+    work = ClosedWorkload(W, H, [base_qp] * segs, pics, rank=0, kind="ldp", ctus_step=ctus_step)
+    par = {"seg0_poc%d" % work.plan[-1].poc: ClosedParity(work, pics - 1, 0, list(range(work.cs.nch)))} if parity else None
+    res = closed_figure(work, threads, par)
+    del work
+    return res
+
+
+def config4_measure(threads, W=1920, H=1088, segs_per_qp=30, qps=(22, 27, 32, 37), pics=3, ctus_step=6, parity=True):
+    """Side figure, BASELINE config 4 as an encode: closed random-access segments (HM's
+    encoder_randomaccess_main structure: I, then POC 8, 4, ... of the first GOP8) decided with the
+    stvssim encoder's active cost (HVX_RD_STVSSIM: distortionstVSSIM over the segment's own history of
+    originals and final reconstructions in coding order, lambda_2(QP) * eta^0.85 with eta 1), the four
+    base QPs' segments side by side in the same launches; per QP a restatement parity sample of its first
+    segment's last picture (3 of its slice chains)."""
+    from video_codecs_amd import _abi
+    base = [q for q in qps for _ in range(segs_per_qp)]
+    work = ClosedWorkload(W, H, base, pics, rank=0, kind="ra", ctus_step=ctus_step, rd_metric=_abi.RD_STVSSIM)
+    nch = work.cs.nch
+    par = {"qp%d" % q: ClosedParity(work, pics - 1, k * segs_per_qp, sorted({0, nch // 2, nch - 1}))
+           for k, q in enumerate(qps)} if parity else None
+    res = closed_figure(work, threads, par)
+    # per base QP: the B pictures' rate (every segment of one QP decides the same CTUs per picture)
+    res["rd_metric"] = "HVX_RD_STVSSIM"
+    res["history_pictures"] = [min(t, _abi.STV_HIST) for t in range(pics)]
+    del work
     return res
 
 
@@ -886,6 +745,44 @@ def build_provenance():
     return rec
 
 
+def closed_main(args, rank, world, device="cuda", segments_cls=None, size=(1920, 1088)):
+    """The closed-segment workload timed by the contract (BASELINE config 5; the N>1 default): every rank
+    encodes its own `segs` closed LDP segments of 1920x1088 random originals (ClosedWorkload, frame
+    indices disjoint across ranks), one step = one decision launch (`closed_ctus` CTUs per chain, the
+    picture's loop after its last launch), and after every picture each segment's finished picture is
+    gathered to rank 0's DPB over RCCL.  W warmup steps, K timed steps, max over ranks; value = the CTUs
+    all ranks decided in the timed steps / that time (weak scaling)."""
+    import math
+    import torch
+    from video_codecs_amd.dpb import DpbGather
+    (W, H), segs = size, args.segs
+    launches = W // 64 // args.closed_ctus  # one CTU row per slice: launches per picture
+    n_pics = math.ceil((args.warmup + args.steps) / launches) + 1
+    dpb = DpbGather(world, rank, (segs * W * H * 3 // 2,), device)
+    work = ClosedWorkload(W, H, [args.qp] * segs, n_pics, rank, kind="ldp", ctus_step=args.closed_ctus, dpb=dpb,
+                          device=device, segments_cls=segments_cls)
+    marks = {}
+
+    def sync():
+        if device != "cpu":
+            torch.cuda.synchronize()
+        dpb.drain()
+        if device != "cpu":
+            torch.cuda.synchronize()
+
+    def step():
+        work.step()
+        if rank == 0:
+            progress("closed step %d (picture %d launch %d/%d)" % (len(work.cs.launch_events), work.cs.t - (work.cs.L == 0),
+                                                                    work.cs.L or launches, launches))
+    elapsed = timed_steps(step, args.steps, args.warmup, world, device, sync,
+                          before=lambda: marks.__setitem__("first", len(work.cs.launch_events)))
+    sec, ctus, byt = work.launch_seconds(marks["first"])
+    own, gathered = dpb.last()
+    dpb_ok = bool(torch.equal(gathered[0], own)) if gathered is not None else None
+    return work, elapsed, sec, ctus, byt, dpb_ok, len(work.gathered)
+
+
 def main():
     args = parse()
     import torch
@@ -898,58 +795,72 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local_rank)
     from video_codecs_amd import hvx
-    from video_codecs_amd.dpb import DpbGather
-
-    W, H, nref = args.width, args.height, args.nref
     hvx.context()
-    work = HmWorkload(W, H, args.pics, nref, args.qp, args.ctus, rank)
-    dpb = DpbGather(world, rank, (work.slots * 6144,), "cuda")
-    events = []
+    kind = args.workload if args.workload != "auto" else ("closed" if world > 1 else "steady")
+    W, H, nref = args.width, args.height, args.nref
+    if kind == "steady":
+        work = HmWorkload(W, H, args.pics, nref, args.qp, args.ctus, rank)
+        out_rec = torch.zeros(work.slots * 6144, dtype=torch.uint8, device="cuda")
+        events = []
 
-    def step():
-        ev = None
-        if timing[0]:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            events.append(ev)
-        with torch.cuda.stream(work.stream):  # the gather reads what this step's launch wrote
-            work.step(dpb.buffer(), ev)
-            dpb.send()
-        if rank == 0:  # a progress line per launch queued (the queue runs at most a step or two ahead)
-            progress("headline step %d queued" % work.step_idx)
+        def step():
+            ev = None
+            if timing[0]:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                events.append(ev)
+            work.step(out_rec, ev)
+            if rank == 0:  # a progress line per launch queued (the queue runs at most a step or two ahead)
+                progress("headline step %d queued" % work.step_idx)
 
-    def sync():
-        dpb.drain()
-        torch.cuda.synchronize()
-
-    timing = [False]
-    elapsed = timed_steps(step, args.steps, args.warmup, world, "cuda", sync,
-                          before=lambda: timing.__setitem__(0, True))
-    timing[0] = False
-    launch_ms = sum(a.elapsed_time(b) for a, b in events) / max(1, len(events))
-    own, gathered = dpb.last()
-    dpb_ok = None
-    if gathered is not None:
-        dpb_ok = bool(torch.equal(gathered[0], own))
-    if rank == 0:
-        units = work.n_jobs * args.ctus
-        value = aggregate(units, args.steps, world, elapsed)
-        bpc = b_ctu(nref)
-        bytes_per_launch = bpc * units
+        timing = [False]
+        elapsed = timed_steps(step, args.steps, args.warmup, world, "cuda", torch.cuda.synchronize,
+                              before=lambda: timing.__setitem__(0, True))
+        launch_ms = sum(a.elapsed_time(b) for a, b in events) / max(1, len(events))
+        units_per_step = work.n_jobs * args.ctus
+        bytes_per_launch = b_ctu(nref) * units_per_step
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-        traffic = None
-        tr_path = os.path.join(ROOT, "profiles", "hbm_traffic_r05.json")  # PMC passes of this round's tree
-        if os.path.exists(tr_path):
+        config = {"workload": "HM-16.5rc1 TEncCu::compressCtu + encodeCtu, bit-exact: merge/skip, AMVP+TMVP, TZ "
+                              "SR64 + frac ME vs %d refs, 2NxN/Nx2N/AMP, RQT + RDOQ + transform skip, "
+                              "intra-in-inter, CABAC context carry; SliceMode=1 row slices; steady state (synthetic "
+                              "references)" % nref,
+                  "resolution": f"{W}x{H}", "ctus_per_frame": work.wc * work.hc, "pictures_per_gpu": args.pics,
+                  "slice_chains_per_gpu": work.n_jobs, "ctus_per_chain_per_step": args.ctus,
+                  "slice": "P, QP %d (base %d + GOP offset %d), QPFactor %g, lambda %.6f" % (
+                      work.qp, args.qp, HM_QP_OFFSET, HM_QP_FACTOR, work.params["lambda"]),
+                  "n_ref": nref, "parallelism": f"pictures x{world}", "dpb": "local"}
+        data = ("synthetic: splitmix64 uniform random 8-bit 4:2:0 YUV (BASELINE.md sec. 3), the previous 4 frames as "
+                "references, seeded synthetic collocated motion field; own pictures per rank")
+        dpb_ok = None
+    else:
+        work, elapsed, sec, ctus, byt, dpb_ok, n_gathered = closed_main(args, rank, world)
+        units_per_step = work.units_per_step
+        launch_ms = sec / args.steps * 1e3
+        bytes_per_launch = byt / args.steps
+        achieved = byt / sec / 1e9
+        W, H = work.W, work.H
+        config = {"workload": "BASELINE config 5: " + work.workload() + "; after every picture each segment's finished "
+                              "(deblocked + SAO) picture is gathered to rank 0's DPB (RCCL over xGMI)",
+                  "resolution": f"{W}x{H}", "segments_per_gpu": len(work.cs.segs),
+                  "slice_chains_per_gpu": len(work.cs.segs) * work.cs.nch, "ctus_per_chain_per_step": work.cs.ctus_step,
+                  "pictures": [dict(p) for p in work.cs.log], "parallelism": f"closed segments x{world}",
+                  "dpb": "each finished picture of every segment gathered to rank 0 (%d pictures x %d segments per "
+                         "rank)" % (n_gathered, len(work.cs.segs)) if world > 1 else "local",
+                  "n1_comparable": "the N=1 line's config5_closed_segments figure (the same per-GPU workload)"}
+        data = ("synthetic: splitmix64 uniform random 8-bit 4:2:0 originals made on the device (BASELINE.md sec. 3), "
+                "frame indices disjoint per segment and rank; references made by each segment's own loop")
+    if rank == 0:
+        value = aggregate(units_per_step, args.steps, world, elapsed)
+        traffic, issue = None, {}
+        tr_path = os.path.join(ROOT, "profiles", "hbm_traffic_r06.json")  # PMC passes of this round's tree
+        if kind == "steady" and os.path.exists(tr_path):
             tr = json.load(open(tr_path)).get("k_hm_compress")
             if tr:
-                traffic = tr["bytes_per_launch"] * units / tr.get("ctus_per_launch", units)
-        # the engine's real limiter, from the SQ counter passes of the same kernel on this round's
-        # tree (scripts/gpu_hm_pmc.sh + scripts/hm_pmc_summary.py): issue fractions of the SIMDs
-        issue = {}
-        pmc_path = os.path.join(ROOT, "profiles", "hm_pmc_r05.json")
+                traffic = tr["bytes_per_launch"] * units_per_step / tr.get("ctus_per_launch", units_per_step)
+        pmc_path = os.path.join(ROOT, "profiles", "hm_pmc_r06.json")
         if os.path.exists(pmc_path):
             pm = json.load(open(pmc_path))
             issue = {"simd_issue_frac": pm["simd_issue_frac"], "valu_frac": pm["valu_frac"],
-                     "wave_cycle_split": pm["wave_cycle_split"], "pmc_file": "profiles/hm_pmc_r05.json"}
+                     "wave_cycle_split": pm["wave_cycle_split"], "pmc_file": "profiles/hm_pmc_r06.json"}
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -962,17 +873,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: splitmix64 uniform random 8-bit 4:2:0 YUV (BASELINE.md sec. 3), the previous 4 frames "
-                    "as references, seeded synthetic collocated motion field; own pictures per rank",
-            "config": {"workload": "HM-16.5rc1 TEncCu::compressCtu + encodeCtu, bit-exact: merge/skip, AMVP+TMVP, TZ "
-                                   "SR64 + frac ME vs %d refs, 2NxN/Nx2N/AMP, RQT + RDOQ + transform skip, "
-                                   "intra-in-inter, CABAC context carry; SliceMode=1 row slices" % nref,
-                       "resolution": f"{W}x{H}", "ctus_per_frame": work.wc * work.hc, "pictures_per_gpu": args.pics,
-                       "slice_chains_per_gpu": work.n_jobs, "ctus_per_chain_per_step": args.ctus,
-                       "slice": "P, QP %d (base %d + GOP offset %d), QPFactor %g, lambda %.6f" % (
-                           work.qp, args.qp, HM_QP_OFFSET, HM_QP_FACTOR, work.params["lambda"]),
-                       "n_ref": nref, "parallelism": f"pictures x{world}",
-                       "dpb": "gather of every rank's reconstructed CTUs to rank 0 per step" if world > 1 else "local"},
+            "data": data,
+            "config": config,
             # priced against HBM (integer work); the limiter is the serial RD decision
             # chain inside each wave (latency), not bandwidth -- frac << 1
             "roofline": {"bound": "hbm", "limiter": "instruction latency of the serial decision chain (issue + "
@@ -980,14 +882,15 @@ def main():
                          "kernel": "k_hm_compress",
                          "achieved": round(achieved, 4), "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / MI355X_HBM_PEAK_GBS, "traffic": traffic,
-                         "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(launch_ms, 3), "b_ctu": bpc,
+                         "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(launch_ms, 3),
+                         "b_ctu": b_ctu(nref) if kind == "steady" else "per picture: b_ctu(distinct refs)",
                          **issue},
             "cpu_baseline": None,
         }
         if dpb_ok is not None:
             out["dpb_gather_ok"] = dpb_ok
         out["build"] = build_provenance()
-        if world == 1:
+        if world == 1 and kind == "steady":
             threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
             if not args.no_cpu_ref:
                 progress("reference HM on the host cores")
@@ -996,6 +899,7 @@ def main():
                                                            os.environ.get("TMPDIR", "/tmp"))
                 except Exception as e:  # noqa: BLE001  (the port figure below stands in)
                     progress("reference HM timing failed: %s: %s" % (type(e).__name__, e))
+
             def side(key, what, fn):
                 # a side figure that raises is reported as such; the headline line is never lost
                 progress(what)
@@ -1016,17 +920,18 @@ def main():
                 side("cpu_port", "the restatement's port figure", port_figure)
                 if out["cpu_baseline"] is None and "error" not in out["cpu_port"]:
                     out["cpu_baseline"] = out["cpu_port"]
-            del work, dpb
+            del work, out_rec
             torch.cuda.empty_cache()
             if not args.no_ra:
-                side("config4_ra_ssim", "config 4 (RA, stVSSIM cost)", lambda: ra_ssim_measure(W, H))
-            if not args.no_slice0:
-                side("slice_mode0", "SliceMode 0 side figure", lambda: slice_mode0_measure(W, H))
+                side("config4_ra_stvssim", "config 4 (closed RA segments, stVSSIM cost)",
+                     lambda: config4_measure(threads, parity=not args.no_cpu))
+                torch.cuda.empty_cache()
+            if not args.no_closed:
+                side("config5_closed_segments", "config 5 unit (closed LDP segments)",
+                     lambda: config5_measure(threads, parity=not args.no_cpu))
+                torch.cuda.empty_cache()
             if not args.no_1080p:
                 side("hm_1080p", "1080p side figure", hm_1080p_measure)
-            if not args.no_closed:
-                side("closed_loop", "closed-loop LDP segments (config 5)",
-                     lambda: closed_loop_measure(threads=threads, parity=not args.no_cpu))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

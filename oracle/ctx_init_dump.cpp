@@ -1,7 +1,7 @@
 // ctx_init_dump.cpp -- writes the CABAC context states TEncSbac::resetEntropy (TEncSbac.cpp:105)
 // gives the 202 models of the RD / slice coder at the start of a slice, for every slice type
-// (B, P, I as HM's SliceType 0, 1, 2) and slice QP 0..51, into video_codecs_amd/data/
-// ctx_init_states.bin ([3][52][202] bytes, constructor order TEncSbac.cpp:62-92).  The states are
+// (B, P, I as HM's SliceType 0, 1, 2) and slice QP 0..51, into tests/golden/ctx_init_states.bin
+// (TEST FIXTURE: it pins video_codecs_amd/cabac_init.py, which derives the same states) ([3][52][202] bytes, constructor order TEncSbac.cpp:62-92).  The states are
 // what HM's own code computes (ContextModel::init over its initialisation tables); this
 // harness only builds a slice for it.  Build + run: make -C oracle ctx_init (needs /root/reference).
 #include <cstdio>

@@ -138,3 +138,13 @@ python3 oracle/compact_saodec.py tests/golden/saodec.bin 0:"$TMP/sd_ldp.bin" 0:"
 # slice-start CABAC states of every slice type and QP (TEncSbac::resetEntropy)
 make -s -C oracle ctx_init
 ls -la tests/golden
+# closed RA segments for the closed-segment harness (video_codecs_amd/gop.py): every picture of a 17-frame
+# 128x64 encode (I + two GOP8s, SAO on, SliceMode 0) at QP 27 and 37
+python3 oracle/make_yuv.py texture 128 64 17 "$TMP/tex128.yuv"
+for q in 27 37; do
+  HVX_CAPTURE="$TMP/cu.bin" $ORC/TAppEncoder_cucap -c $CFG/encoder_randomaccess_main.cfg -i "$TMP/tex128.yuv" -wdt 128 \
+    -hgt 64 -fr 30 -f 17 -q $q -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+  python3 oracle/compact_ctu.py "$TMP/cu.bin" tests/golden/ctu_ra_closed_q$q.bin
+done
+# HM's slice set-up of closed LDP / RA segments (tests/golden/gop_plans.json)
+oracle/gen_gop_plans.sh

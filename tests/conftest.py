@@ -22,7 +22,7 @@ def _gpu_rank(item):
         if "cu_seam" in n:
             return 2
         return 4
-    if "test_gpu_parity.py" in n and ("test_hm_" in n or "sao_decide" in n):
+    if "test_gop_gpu.py" in n or ("test_gpu_parity.py" in n and ("test_hm_" in n or "sao_decide" in n)):
         return 0
     return 3
 

@@ -104,125 +104,85 @@ def test_two_rank_hm_workload_gloo(tmp_path):
     assert not np.array_equal(dpb[0], dpb[1])
 
 
-# ---- closed GOP segments per rank (config 5's unit), decided by the restatement ----
-def _closed_segment(g, rank):
-    """The LDP segment of tests/golden/ctu_ldp_nosao.bin (I, P, P; SAO off) decided in closed loop by
-    the restatement: every picture from the capture's original and slice-start states only, each P
-    picture against the reference pictures this loop made (restatement decisions -> boundary
-    strengths -> oracle loopFilterPic), never the capture's.  Returns [(poc, parts, recon planes,
-    reference planes)]."""
-    import oracle
-    from oracle import hm_ctu
-    from tests import hm_cases
-    from video_codecs_amd import _abi
-    made = {}
-    out = []
-    gl = dict(g)
-    refpoc = [int(p) for p in g["refpic_poc"]]
-    for pic, pi in enumerate(g["pic_i32"]):
-        poc, w, h = int(pi[hm_cases.P_POC]), int(pi[hm_cases.P_W]), int(pi[hm_cases.P_H])
-        first, n = int(pi[hm_cases.P_FIRST_CTU]), int(pi[hm_cases.P_NCTU])
-        psz = w * h * 3 // 2
-        # the references this loop made, in the capture's reference-plane slots
-        rp = np.array(g["refpic"], copy=True)
-        for k, q in enumerate(refpoc):
-            if q in made:
-                rp[k * psz:(k + 1) * psz] = np.concatenate([p.reshape(-1) for p in made[q]])
-            elif q < poc:
-                raise AssertionError("reference POC %d not made yet" % q)
-        gl["refpic"] = rp
-        r = hm_ctu.replay(gl, pic, mode=1)
-        rec = [np.zeros((h >> (1 if c else 0), w >> (1 if c else 0)), np.uint8) for c in range(3)]
-        wc = (w + 63) // 64
-        for a in range(n):
-            ax, ay = a % wc, a // wc
-            t = r["recon"][a]
-            yy, xx = min(64, h - ay * 64), min(64, w - ax * 64)
-            rec[0][ay * 64:ay * 64 + yy, ax * 64:ax * 64 + xx] = t[:4096].reshape(64, 64)[:yy, :xx]
-            for c in (1, 2):
-                cpl = t[4096 + (c - 1) * 1024:4096 + c * 1024].reshape(32, 32)
-                rec[c][ay * 32:ay * 32 + yy // 2, ax * 32:ax * 32 + xx // 2] = cpl[:yy // 2, :xx // 2]
-        rpoc = np.array([pi[hm_cases.P_REFPOC0:hm_cases.P_REFPOC0 + 4], pi[hm_cases.P_REFPOC1:hm_cases.P_REFPOC1 + 4]])
-        bv, bh, qp = hm_ctu.boundary_strength(w, h, r["parts"], rpoc, int(pi[hm_cases.P_SLICE_TYPE]) == 0)
-        ref = oracle.deblock(*rec, bv.reshape(-1), bh.reshape(-1), qp.reshape(-1), _abi.deblock_params(w, h))
-        made[poc] = ref
-        out.append((poc, r["parts"], rec, ref))
-    return out
+# ---- config 5: closed GOP segments per rank (bench.closed_main), decided by the restatement ----
+CW, CH, CSEGS, CSTEP = 128, 64, 2, 1  # 2 segments of 128x64 per rank, 1 CTU per chain per step
+
+
+def _closed_args(warmup, steps):
+    import argparse
+    return argparse.Namespace(segs=CSEGS, closed_ctus=CSTEP, warmup=warmup, steps=steps, qp=32)
 
 
 def _closed_worker(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import torch
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from tests import golden_cases as gc
-    from video_codecs_amd.dpb import DpbGather
-    g = gc.load("ctu_ldp_nosao.bin")
-    w, h = int(g["pic_i32"][0][0]), int(g["pic_i32"][0][1])
-    seg = _closed_segment(g, rank)
-    # every finished reference picture of the rank's segment goes to rank 0's DPB
-    dpb = DpbGather(world, rank, (w * h * 3 // 2,), "cpu")
-    got = []
-    for poc, _, _, ref in seg:
-        buf = dpb.buffer()
-        buf.copy_(torch.from_numpy(np.concatenate([p.reshape(-1) for p in ref])))
-        b = dpb.send()
-        dpb.drain()
-        if rank == 0:
-            got.append(np.stack([t.numpy().copy() for t in dpb.dpb[b]]))
-    np.save(os.path.join(outdir, f"closed_parts{rank}.npy"), np.stack([s[1] for s in seg]))
+    import bench
+    from tests.segment_port import PortSegments
+    gathered = []
+    work, elapsed, sec, ctus, byt, dpb_ok, n_gathered = bench.closed_main(
+        _closed_args(2, 4), rank, world, device="cpu", segments_cls=PortSegments, size=(CW, CH))
+    # every finished picture of the rank's segments, in the order they were gathered
+    own = np.stack([np.concatenate([np.concatenate([p.numpy().reshape(-1) for p in r["rec"]]) for r in res])
+                    for res in work.cs.finished_log])
+    np.save(os.path.join(outdir, f"own{rank}.npy"), own)
     if rank == 0:
-        np.save(os.path.join(outdir, "closed_dpb.npy"), np.stack(got))
-        np.save(os.path.join(outdir, "closed_refs0.npy"),
-                np.stack([np.concatenate([p.reshape(-1) for p in s[3]]) for s in seg]))
+        np.save(os.path.join(outdir, "dpb_last.npy"), np.stack([t.numpy() for t in work.dpb.last()[1]]))
+    parts = np.stack([np.stack([r["parts"] for r in res]) for res in work.cs.finished_log])
+    np.save(os.path.join(outdir, f"parts{rank}.npy"), parts)
+    seeds = [bench.closed_seed(rank, CSEGS, s, g.poc) for s in range(CSEGS) for g in work.plan]
+    np.save(os.path.join(outdir, f"meta{rank}.npy"), np.array([elapsed, ctus, n_gathered, int(bool(dpb_ok))] + seeds,
+                                                               np.float64))
+    dist.barrier()
     dist.destroy_process_group()
 
 
 def test_two_rank_closed_segments_gloo(tmp_path):
-    """Config 5's unit on two ranks (gloo): each rank encodes a closed LDP segment (I, P, P) with the
-    restatement -- every P picture decided against the reference pictures its own loop made (the
-    restatement's decisions, boundary strengths and loopFilterPic), not the capture's -- and every
-    picture equals HM's own decisions (tests/golden/ctu_ldp_nosao.bin, SAO off); every finished
-    reference picture goes to rank 0 through DpbGather, where each rank's copy equals that rank's."""
+    """BASELINE config 5's multi-GPU path (bench.closed_main) on two ranks over gloo, with the
+    restatement standing in for the device (tests/segment_port.py): each rank encodes its OWN closed LDP
+    segments (frame indices disjoint across ranks: bench.closed_seed), every P picture decided against
+    the references its own loop made; after every picture each segment's finished (deblocked) picture is
+    gathered to rank 0.  Checks: the same max-over-ranks time on both ranks; the timed CTUs = K steps of
+    every chain; the two ranks' pictures differ; rank 0's DPB holds each rank's finished pictures
+    bit-exactly; and each rank's decisions equal a single-process run of its segments."""
     import torch.multiprocessing as tmp
-    from tests import golden_cases as gc
-    from tests import hm_cases
+    import bench
+    from tests.segment_port import PortSegments
     world = 2
     tmp.spawn(_closed_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    g = gc.load("ctu_ldp_nosao.bin")
+    metas = [np.load(tmp_path / f"meta{r}.npy") for r in range(world)]
+    assert metas[0][0] == metas[1][0]  # max over ranks
+    assert int(metas[0][1]) == CSEGS * 1 * CSTEP * 4  # one chain per 128x64 picture, 4 timed steps
+    assert all(int(m[3]) == 1 for m in metas[:1])  # rank 0's own slot of the gather equals its buffer
+    assert not set(metas[0][4:]) & set(metas[1][4:])  # disjoint synthetic frames
+    owns = [np.load(tmp_path / f"own{r}.npy") for r in range(world)]
+    assert owns[0].shape == owns[1].shape and int(metas[0][2]) == owns[0].shape[0] == 3  # I, P, P finished
+    assert not np.array_equal(owns[0], owns[1])
+    last = np.load(tmp_path / "dpb_last.npy")  # rank 0's DPB after the last gather: every rank's last picture
     for r in range(world):
-        parts = np.load(tmp_path / f"closed_parts{r}.npy")
-        for pic, pi in enumerate(g["pic_i32"]):
-            first, n = int(pi[hm_cases.P_FIRST_CTU]), int(pi[hm_cases.P_NCTU])
-            np.testing.assert_array_equal(parts[pic], g["ctu_parts"][first:first + n], err_msg=f"rank {r} pic {pic}")
-    dpb, refs0 = np.load(tmp_path / "closed_dpb.npy"), np.load(tmp_path / "closed_refs0.npy")
-    assert dpb.shape[:2] == (3, world)
-    for k in range(3):
-        for r in range(world):
-            np.testing.assert_array_equal(dpb[k, r], refs0[k])  # the same segment on both ranks here
-    # the made references equal HM's reference pictures
-    psz = refs0.shape[1]
-    for k, q in enumerate(int(p) for p in g["refpic_poc"]):
-        np.testing.assert_array_equal(refs0[q], g["refpic"][k * psz:(k + 1) * psz])
+        np.testing.assert_array_equal(last[r], owns[r][-1])
+    # a single-process run of rank 1's segments decides the same CTUs and makes the same pictures
+    work, *_ = bench.closed_main(_closed_args(2, 4), 1, 1, device="cpu", segments_cls=PortSegments, size=(CW, CH))
+    parts1 = np.load(tmp_path / "parts1.npy")
+    np.testing.assert_array_equal(np.stack([np.stack([r["parts"] for r in res]) for res in work.cs.finished_log]), parts1)
 
 
-def test_closed_loop_geometry_and_jobs():
-    """bench.closed_loop_measure's slicing (CPU): at 1088p one chain per CTU row; at 2160p two rows
-    per slice, the partial bottom row inside the last slice (a one-row slicing is refused); every
-    launch's jobs advance every chain by the same CTUs, and the launches of a picture cover each
-    slice's CTUs exactly once, resumed after the first."""
-    import bench
-    assert bench.closed_loop_geometry(1920, 1088, 1, 6) == (30, 17, 17, 30)
-    assert bench.closed_loop_geometry(3840, 2160, 2, 8) == (60, 34, 17, 120)
-    with pytest.raises(AssertionError):
-        bench.closed_loop_geometry(3840, 2160, 1, 6)
-    wc, hc, nch, cl = bench.closed_loop_geometry(3840, 2160, 2, 8)
-    seen = {}
-    for L in range(cl // 8):
-        for seg, first, n, s0, s1, resume in bench.closed_loop_specs(3, nch, cl, L, 8):
-            assert s0 <= first and first + n - 1 <= s1 and s1 - s0 + 1 == cl and resume == (L > 0)
-            for a in range(first, first + n):
-                seen[(seg, a)] = seen.get((seg, a), 0) + 1
-    assert sorted(seen) == [(s, a) for s in range(3) for a in range(wc * hc)] and set(seen.values()) == {1}
-    # encoder_lowdelay_P_main.cfg:24-27 (Frame1..4: QP offset, QPFactor)
-    assert [bench.LDP_GOP[k][:2] for k in (1, 2, 3, 4)] == [(3, 0.4624), (2, 0.4624), (3, 0.4624), (1, 0.578)]
+def test_closed_port_segment_vs_hm():
+    """The closed-segment orchestration (gop.ClosedSegments' picture set-up, reference lists, DPB and
+    collocated-field bookkeeping) with the restatement deciding: HM's own closed LDP encode (I, P, P,
+    416x240, SAO off, one slice per picture: tests/golden/ctu_ldp_nosao.bin) is reproduced CTU for CTU,
+    every P picture decided against the references this loop made."""
+    from tests import golden_cases as gc
+    from tests import hm_cases
+    from tests.segment_port import PortSegments
+    from video_codecs_amd import gop
+    g = gc.load("ctu_ldp_nosao.bin")
+    psz = 416 * 240 * 3 // 2
+    plan = gop.load_plan("ldp", 3)
+    cs = PortSegments(plan, 416, 240, [27], lambda s, poc: hm_cases.yuv_split(g["org"][poc * psz:(poc + 1) * psz], 416, 240),
+                      rows=4, threads=4)
+    while cs.t < 3:
+        cs.step()
+    for pic, res in enumerate(cs.finished_log):
+        first, n = int(g["pic_i32"][pic][hm_cases.P_FIRST_CTU]), int(g["pic_i32"][pic][hm_cases.P_NCTU])
+        np.testing.assert_array_equal(res[0]["parts"], g["ctu_parts"][first:first + n], err_msg=f"pic {pic}")

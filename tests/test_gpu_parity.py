@@ -443,16 +443,23 @@ def test_hm_extreme_qp_gpu(torch, base_qp):
 
 @pytest.mark.gpu
 def test_closed_loop_segments_gpu(torch):
-    """The bench's closed-loop figure in miniature (bench.closed_loop_measure): two LDP segments of
-    256x192 random pictures (I, P, P), every P picture decided against the references and collocated
-    field the device made from the pictures before it (deblocking + SAO on the device), the chains
-    stepped 2 CTUs per launch; segment 0's last P picture re-decided by the restatement against the
-    downloaded device references: every CTU equal."""
+    """The bench's closed-segment figures in miniature (bench.ClosedWorkload, the per-rank workload of the
+    multi-GPU bench): config 5 -- two LDP segments of 256x192 random pictures (I, P, P), every P picture
+    decided against the references, collocated field and cabac_init table the device loop made
+    (deblocking + SAO + slice writer), the chains stepped 2 CTUs per launch -- and config 4 -- two RA
+    segments of 128x64 (I, POC 8, POC 4) with the stVSSIM cost over their own history; each figure's last
+    picture re-decided by the restatement from the device's references, field and history: every CTU equal."""
     import bench
     hvx.context()
-    r = bench.closed_loop_measure(256, 192, segs=2, pics=3, base_qp=32, ctus_step=2, threads=4)
+    r = bench.config5_measure(4, W=256, H=192, segs=2, pics=3, ctus_step=2)
     assert [p["slice"] for p in r["pictures"]] == ["I", "P", "P"]
-    assert r["gpu_parity_ctus"] == 12 and r["gpu_parity_mismatches"] == 0, r["first_mismatches"]
+    assert all(p["slice_data_bytes"] > 0 for p in r["pictures"])
+    par = r["parity"]["seg0_poc2"]
+    assert par["ctus"] == 12 and par["mismatches"] == 0, par["first_mismatches"]
+    r = bench.config4_measure(4, W=128, H=64, segs_per_qp=1, qps=(27, 37), pics=3, ctus_step=1)
+    assert [p["poc"] for p in r["pictures"]] == [0, 8, 4] and [p["slice"] for p in r["pictures"]] == ["I", "B", "B"]
+    for q in ("qp27", "qp37"):
+        assert r["parity"][q]["ctus"] == 2 and r["parity"][q]["mismatches"] == 0, r["parity"][q]
 
 
 @pytest.mark.gpu

@@ -53,11 +53,16 @@ def test_ctu_capture_covers_modes():
 
 
 def test_ctx_init_states_vs_hm():
-    """video_codecs_amd/data/ctx_init_states.bin (TEncSbac::resetEntropy of every slice type / QP,
-    oracle/ctx_init_dump.cpp) equals the slice-start states the captures recorded."""
+    """The library's slice-start states (video_codecs_amd/cabac_init.py, derived from the
+    initialisation values) equal HM's own resetEntropy output for every slice type / QP
+    (tests/golden/ctx_init_states.bin, oracle/ctx_init_dump.cpp) and the slice-start states the
+    captures recorded."""
     import numpy as np
     from video_codecs_amd import _abi
+    import os
     init = _abi.load_ctx_init_states()
+    hm_dump = np.fromfile(os.path.join(os.path.dirname(__file__), "golden", "ctx_init_states.bin"), np.uint8)
+    np.testing.assert_array_equal(init, hm_dump.reshape(3, 52, 202))
     for name in CAPTURES + ["ctu_ldp_slices.bin"]:
         g = _load(name)
         wc = (int(g["pic_i32"][0][0]) + 63) // 64

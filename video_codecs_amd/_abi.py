@@ -38,29 +38,6 @@ RD_SSE, RD_SSIM, RD_STVSSIM = 0, 1, 2  # hvx_hm_picture.rd_metric
 STV_HIST = 25  # HVX_STV_HIST: previous pictures of the stVSSIM history
 
 
-def load_estbits_p_luma():
-    """4 x 224 int32 luma inter estBits tables (video_codecs_amd/data/README.md)."""
-    import os
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "estbits_p_luma.bin")
-    return np.fromfile(p, dtype="<i4").reshape(4, ESTBITS_INTS)
-
-
-def estbits_p_yuv(update):
-    """7 x 224 int32: the 4 luma tables (load_estbits_p_luma) + chroma TU 4x4, 8x8, 16x16 tables, each
-    TEncSbac::estBit (TEncSbac.cpp:1726) of the same context snapshot (ctx_p_states.bin) at chroma
-    channel type on top of the luma table of its size (every entry the chroma RDOQ reads is written by
-    that call).  update = an estbits_update(states, entropy_bits, rice, w, h, ch, est_in) callable:
-    the library's host restatement or the oracle's."""
-    luma = load_estbits_p_luma()
-    st, eb = load_ctx_p_states(), load_entropy_bits()
-    out = [t.copy() for t in luma]
-    for log2 in (2, 3, 4):
-        base = luma[log2 - 2]
-        rice = base[-4:].astype(np.uint32)
-        out.append(np.asarray(update(st, eb, rice, 1 << log2, 1 << log2, 1, base), np.int32).reshape(-1))
-    return np.stack(out)
-
-
 def lambda_ssim(qp, eta=1.0):
     """The SSIM-RDO lambda of stvssim.c: lambda_2 (:1782-1806, active form :1805)
     -a1*b2*exp(b1*(qp-15)), times the attention weight eta^0.85 (adjust_lambda :1707)."""
@@ -108,14 +85,6 @@ assert CABAC_REGS.itemsize == 44
 CABAC_START = (0, 510, 23, 0, 0xFF, 0, (0, 0, 0, 0, 0))
 NUM_CTX = 202
 
-
-
-def load_ctx_p_states():
-    """202 CABAC context states (TEncSbac::m_contextModels order) of HM's RD coder in a P-slice
-    (video_codecs_amd/data/README.md)."""
-    import os
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "ctx_p_states.bin")
-    return np.fromfile(p, dtype=np.uint8)
 
 
 def load_entropy_bits():
@@ -174,7 +143,7 @@ def deblock_params(w, h, beta_offset_div2=0, tc_offset_div2=0, cb_qp_offset=0, c
 
 def load_ctx_init_states():
     """uint8 [3 slice types (B, P, I)][52 QP][HVX_NUM_CTX]: the CABAC context states at the start of
-    a slice (TEncSbac::resetEntropy, TEncSbac.cpp:105; video_codecs_amd/data/README.md)."""
-    import os
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "ctx_init_states.bin")
-    return np.fromfile(p, dtype=np.uint8).reshape(3, 52, 202)
+    a slice (TEncSbac::resetEntropy, TEncSbac.cpp:105), derived in the library from the HEVC
+    initialisation values (video_codecs_amd/cabac_init.py)."""
+    from . import cabac_init
+    return cabac_init.ctx_init_states()

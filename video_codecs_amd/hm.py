@@ -276,6 +276,17 @@ class DeviceFrame:
 
 
     @classmethod
+    def original(cls, planes, device="cuda"):
+        """An original picture's device planes only (Y, Cb, Cr uint8; no reference planes): what a
+        picture being decided reads.  planes: numpy arrays or device tensors."""
+        import torch
+        self = cls.__new__(cls)
+        self.org = [p if hasattr(p, "data_ptr") else torch.from_numpy(np.ascontiguousarray(p, np.uint8)).to(device)
+                    for p in planes]
+        self.keep, self.ref8, self.ref8_stride, self.ref16, self.ref16_stride = [], 0, 0, [], [0, 0]
+        return self
+
+    @classmethod
     def blank(cls, w, h, device="cuda"):
         """A reference frame's padded device planes, uninitialised: filled on the device by
         finish_picture (hvx_hm_finish_picture) from a decided picture; no original planes."""

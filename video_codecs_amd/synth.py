@@ -20,6 +20,27 @@ def random_frame(w, h, index):
     return (splitmix64_stream(0x5EED0000 + index, w * h * 3 // 2) >> np.uint64(56)).astype(np.uint8)
 
 
+def random_frame_torch(w, h, index, device="cuda"):
+    """random_frame computed with torch int64 arithmetic on `device` (the bench's many closed segments
+    make their originals on the GPU): the same splitmix64 stream -- multiplications wrap modulo 2^64,
+    the logical right shifts are arithmetic shifts masked to the low bits -- so the bytes are identical
+    (tests/test_abi_cpu.py checks them against random_frame)."""
+    import torch
+
+    def c(v):  # a uint64 constant as the int64 of the same bits
+        return v - (1 << 64) if v >= 1 << 63 else v
+
+    def shr(z, s):
+        return (z >> s) & ((1 << (64 - s)) - 1)
+    n = w * h * 3 // 2
+    k = torch.arange(1, n + 1, dtype=torch.int64, device=device)
+    z = c(0x5EED0000 + index) + k * c(0x9E3779B97F4A7C15)
+    z = (z ^ shr(z, 30)) * c(0xBF58476D1CE4E5B9)
+    z = (z ^ shr(z, 27)) * c(0x94D049BB133111EB)
+    z = z ^ shr(z, 31)
+    return shr(z, 56).to(torch.uint8)
+
+
 def luma_plane(w, h, index, margin=80):
     """The frame's luma as an 8-bit padded plane (HVX_PLANE_MARGIN border, edges replicated)."""
     y = random_frame(w, h, index)[: w * h].reshape(h, w)
