@@ -162,6 +162,13 @@ bool supported(TEncSlice *self, TComPic *pic, TComSlice *s) {
   if (sps.getBitDepth(CHANNEL_TYPE_LUMA) != 8 || sps.getBitDepth(CHANNEL_TYPE_CHROMA) != 8) return false;
   if (sps.getUsePCM() || s->getSliceSegmentCurStartCtuTsAddr() != s->getSliceCurStartCtuTsAddr()) return false;
   if (pps.getPpsRangeExtension().getLog2MaxTransformSkipBlockSize() != 2) return false;  // transform_skip_flag: 4x4
+  // the syntax the device writer hard-codes (hm_cu_seam.cpp begin_picture's tool check): sign hiding on and the
+  // transform_skip_flag coded (hvx_tu_desc sign_hiding / pps_tskip), the TU quadtree 32..4 to depth 3
+  // (write_transform's split flags), an 8x8 minimum CU (the split flag is skipped only at depth 3)
+  if (!pps.getSignHideFlag() || !pps.getUseTransformSkip()) return false;
+  if (sps.getQuadtreeTULog2MaxSize() != 5 || sps.getQuadtreeTULog2MinSize() != 2 || sps.getQuadtreeTUMaxDepthInter() != 3 ||
+      sps.getQuadtreeTUMaxDepthIntra() != 3 || sps.getMaxTotalCUDepth() != 4)
+    return false;
   if (sps.getSpsRangeExtension().getRdpcmEnabledFlag(RDPCM_SIGNAL_IMPLICIT) ||
       sps.getSpsRangeExtension().getRdpcmEnabledFlag(RDPCM_SIGNAL_EXPLICIT) ||
       sps.getSpsRangeExtension().getPersistentRiceAdaptationEnabledFlag() ||

@@ -2081,7 +2081,11 @@ static void intra_border(hm_enc *e, const hm_cu *cu, const tu_t *t, int comp, in
   const int W = (e->pic->w >> s), H = (e->pic->h >> s);
   const int n = w;
   for (int k = 0; k <= 4 * n; k++) raw[k] = 0;
-#define REC(x, y) (((x) >= 0 && (y) >= 0 && (x) < W + 8 && (y) < H + 8) ? *rec_at(e, c, (x), (y)) : 0)
+  /* reads stay inside the whole-CTU reconstruction buffer (unavailable units are substituted by
+     hvxo_intra_fill, so what is read there does not matter) */
+  const int RW = (((e->pic->w + 63) >> 6) << 6) >> s, RH = (((e->pic->h + 63) >> 6) << 6) >> s;
+  (void)W; (void)H;
+#define REC(x, y) (((x) >= 0 && (y) >= 0 && (x) < RW && (y) < RH) ? *rec_at(e, c, (x), (y)) : 0)
   raw[0] = REC(x0 - 1, y0 - 1);
   for (int k = 0; k < 2 * n; k++) raw[1 + k] = REC(x0 + k, y0 - 1);
   for (int k = 0; k < 2 * n; k++) raw[2 * n + 1 + k] = REC(x0 - 1, y0 + k);

@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 R=$(pwd); mkdir -p gpurun_out
 rocprofv3 --list-avail > gpurun_out/avail.txt 2>&1; grep -oE "SQC?_[A-Z_0-9]+" gpurun_out/avail.txt | sort -u > gpurun_out/avail_sq.txt; grep -E "ICACHE|IFETCH" gpurun_out/avail_sq.txt | head -20
-B="$R/bench.py --steps 1 --warmup 0 --no-cpu --no-cpu-ref --no-ra --no-slice0 --no-1080p --no-closed"
+B="$R/bench.py --steps 1 --warmup 0 --no-cpu --no-cpu-ref --no-ra --no-1080p --no-closed"
 C=$(grep -xE "SQ_IFETCH|SQC_ICACHE_HITS|SQC_ICACHE_MISSES|SQ_WAVES" gpurun_out/avail_sq.txt | head -4 | tr '\n' ' ')
 echo "counters: $C"
 [ -n "$C" ] || exit 0

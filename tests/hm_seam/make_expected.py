@@ -29,6 +29,9 @@ CASES = {  # name: (cfg, yuv kind, frames, qp[, width, height, extra encoder arg
     "ldp_rand_qp51": ("ldp.cfg", "random", 2, 51, 208, 120),
     # the search parameters the engine takes from the encoder: a smaller TZ window, AMP off
     "ldp_rand_sr16_noamp_qp32": ("ldp.cfg", "random", 2, 32, 208, 120, ["--SearchRange=16", "--AMP=0"]),
+    # a tool the device decision and writer do not implement (sign hiding off): both seams must fall
+    # through to HM's own code and the encode stays the reference's
+    "ldp_rand_nosbh_qp32": ("ldp.cfg", "random", 2, 32, 208, 120, ["--SignHideFlag=0"]),
     # camera content: the 3-frame QCIF clip the reference's JM trees ship (jm14.1/bin/foreman_part_qcif.yuv,
     # a data fixture, tests/golden/foreman_part_qcif.yuv), P and B slices
     "foreman_ldp_qp27": ("ldp.cfg", "foreman", 3, 27, 176, 144),

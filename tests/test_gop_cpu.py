@@ -61,6 +61,19 @@ def test_cabac_init_choice_basics():
     assert list(cabac_init.coded_flags([1, 0, 0, 0, 0, 0, 1 << 9])[[0, 1, 201]]) == [1, 0, 1]
 
 
+def test_cabac_init_choice_equals_hm():
+    """determine_cabac_init_idx == HM's TEncSbac::determineCabacInitIdx (TEncSbac.cpp:162) on 3000 seeded
+    writer states / coded-context sets over every QP, B and P slices (tests/golden/cabac_init_choice.bin,
+    oracle/cabac_init_choice.cpp run on HM-16.5rc1's own library)."""
+    import os
+    rec = np.dtype([("qp", "<i4"), ("st", "<i4"), ("states", "u1", 202), ("coded", "u1", 202), ("choice", "<i4")])
+    g = np.fromfile(os.path.join(os.path.dirname(__file__), "golden", "cabac_init_choice.bin"), rec)
+    assert len(g) == 3000 and set(np.unique(g["choice"])) == {gop.B_SLICE, gop.P_SLICE}
+    eb = hm._abi.load_entropy_bits()
+    got = [cabac_init.determine_cabac_init_idx(int(r["st"]), r["states"], r["coded"], int(r["qp"]), eb) for r in g]
+    np.testing.assert_array_equal(np.array(got), g["choice"])
+
+
 def test_stv_direction_map_vectorised_equals_reference_form():
     rng = np.random.default_rng(5)
     for w, h in ((128, 64), (200, 136)):

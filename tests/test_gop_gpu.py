@@ -75,22 +75,32 @@ def test_closed_ra_segments_vs_hm(torch):
     hvx.context()
     gs = [gc.load("ctu_ra_closed_q27.bin"), gc.load("ctu_ra_closed_q37.bin")]
     plan = gop.load_plan("ra", 17)
-    cs = gop.ClosedSegments(plan, 128, 64, [27, 37], _capture_org_fn(gs))
+    finals = {}
+
+    def finished(t, recs):  # every finished (deblocked + SAO) picture, for the reference-picture check
+        for s, r in enumerate(recs):
+            finals[(s, plan[t].poc)] = np.concatenate([x.cpu().numpy().reshape(-1) for x in r])
+    cs = gop.ClosedSegments(plan, 128, 64, [27, 37], _capture_org_fn(gs), on_finished=finished)
     kept = Kept(cs)
     while cs.t < len(plan):
         cs.step()
     torch.cuda.synchronize()
     pocs = [g.poc for g in plan]
-    bad = []
+    bad, tables = [], []
     for s, g in enumerate(gs):
         t_of_pic = [pocs.index(int(pi[hm_cases.P_POC])) for pi in g["pic_i32"]]
         bad += _compare_with_capture(g, kept.out, t_of_pic, s, 2)
+        psz = 128 * 64 * 3 // 2
+        for k, q in enumerate(int(p) for p in g["refpic_poc"]):  # HM's reference pictures (after SAO)
+            if not np.array_equal(finals[(s, q)], g["refpic"][k * psz:(k + 1) * psz]):
+                bad.append((s, q, "finished picture"))
         # the CABAC initialisation table of every picture (cabac_init_flag from the device writer's states)
         want = [cabac_init.resolve_table(int(pi[hm_cases.P_SLICE_TYPE]), int(pi[hm_cases.P_CABAC_TABLE])) for pi in g["pic_i32"]]
         got = [cs.segs[s].tables[t] for t in t_of_pic]
-        assert got == want, (s, got, want)
+        if got != want:
+            tables.append((s, got, want))
         assert all(b > 0 for b in cs.segs[s].bytes)
-    assert not bad, bad[:6]
+    assert not bad and not tables, ([b for b in bad if b[2] == "finished picture"], bad[:6], tables)
 
 
 @pytest.mark.gpu

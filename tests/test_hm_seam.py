@@ -92,7 +92,7 @@ def conformance(case, tmp):
     """SURVEY 4's conformance check: the reference decoder (HM-16.5rc1 TAppDecoder, built from the
     reference sources) decodes the device-written bitstream to exactly the encoder's reconstruction."""
     if not os.path.exists(DECODER):
-        return
+        pytest.fail("oracle/_ref/TAppDecoder missing: the conformance check cannot run")
     dec = os.path.join(tmp, case + ".dec.yuv")
     p = subprocess.run([DECODER, "-b", os.path.join(tmp, case + ".bin"), "-o", dec], capture_output=True, text=True)
     assert p.returncode == 0, p.stderr[-2000:]
@@ -125,6 +125,7 @@ def test_hm_encoder_with_cu_seam(case, monkeypatch):
     log = []
     with tempfile.TemporaryDirectory() as tmp:
         got = mk.encode(EXE, case, tmp, log)
+        conformance(case, tmp)
     print(log[0][-600:])
     m = re.search(r"hm_cu_seam: (\d+) compressCtu calls served by libhvx \((\d+) pictures\), (\d+) fell through", log[0])
     assert m, log[0][-2000:]
@@ -141,7 +142,8 @@ def test_hm_encoder_with_cu_seam(case, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("case", ["ldp_smooth_1080p_qp32", "ra_texture_qp32", "ldp_smooth_qp32", "intra_smooth_qp22",
+@pytest.mark.parametrize("case", ["ldp_smooth_1080p_qp32", "ra_texture_qp32", "ra_smooth_qp27", "ldp_smooth_qp32",
+                                  "intra_smooth_qp22",
                                   "ldp_rand_qp4", "ldp_rand_qp51", "ldp_rand_sr16_noamp_qp32", "foreman_ldp_qp27",
                                   "foreman_ldb_qp32", "foreman_intra_qp22"])
 def test_hm_encoder_with_cu_seam_batched(case, monkeypatch):
@@ -176,3 +178,30 @@ def test_hm_encoder_with_cu_seam_batched(case, monkeypatch):
     assert got == EXPECTED[case], (case, got, EXPECTED[case])
     check_slice_seam(case, log[0])
 
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_hm_seams_fall_through_unsupported_tools(monkeypatch):
+    """An encode with a tool the device path does not implement (SignHideFlag=0): the CTU seam's and
+    the slice seam's tool checks refuse every picture / slice, HM's own compressCtu and encodeSlice run,
+    and the bitstream and reconstruction are the reference's."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if not os.path.exists(EXE):
+        pytest.skip("TAppEncoder_hvx not built (needs /root/reference at build time)")
+    case = "ldp_rand_nosbh_qp32"
+    monkeypatch.setenv("HVX_SEAM_CU", "1")
+    monkeypatch.setenv("HVX_SEAM_CU_BATCH", "1")
+    monkeypatch.setenv("HVX_SEAM_SLICE", "1")
+    monkeypatch.setenv("HVX_SEAM_INTRA", "0")
+    log = []
+    with tempfile.TemporaryDirectory() as tmp:
+        got = mk.encode(EXE, case, tmp, log)
+        conformance(case, tmp)
+    assert got == EXPECTED[case], (case, got, EXPECTED[case])
+    m = re.search(r"hm_slice_seam: (\d+) slices written by libhvx \((\d+) bytes\), (\d+) fell through", log[0])
+    assert m and int(m.group(1)) == 0 and int(m.group(3)) == slices_of(case), log[0][-2000:]
+    m = re.search(r"hm_cu_seam: (\d+) compressCtu calls served by libhvx \((\d+) pictures\), (\d+) fell through", log[0])
+    assert m and int(m.group(1)) == 0 and int(m.group(3)) > 0, log[0][-2000:]

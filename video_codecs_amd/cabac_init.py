@@ -167,8 +167,8 @@ def table_cost(states, coded, table, qp, entropy_bits):
 def determine_cabac_init_idx(slice_type, states, coded, qp, entropy_bits):
     """TEncSbac::determineCabacInitIdx: for an I slice I_SLICE, else B_SLICE or P_SLICE, whichever
     table's cost is lower (B first, strict <).  states: the writer's 202 context states after the
-    slice; coded: 202 flags (ContextModel::m_binsCoded, never cleared by resetEntropy, so they
-    accumulate over every slice the writer coded); qp: the slice QP."""
+    slice; coded: 202 flags (ContextModel::m_binsCoded of that slice: ContextModel3DBuffer::initBuffer,
+    ContextModel3DBuffer.cpp:74, clears them at every slice start); qp: the slice QP."""
     if int(slice_type) == I_SLICE:
         return I_SLICE
     best, best_t = None, B_SLICE

@@ -128,13 +128,7 @@ extern "C" {
 
 int hvx_hm_state_size(size_t *bytes) {
   if (!bytes) return fail(HVX_E_INVALID, "hvx_hm_state_size: NULL");
-#ifdef HM_STATE_ODD_LINES
-  // an odd number of 128-byte lines between consecutive chains' states, so the same field of
-  // different chains falls into different cache sets / memory channels
-  *bytes = ((sizeof(hm::State) + 127) / 128 | 1) * 128;
-#else
   *bytes = (sizeof(hm::State) + 255) / 256 * 256;
-#endif
   return HVX_OK;
 }
 
@@ -145,11 +139,7 @@ int hvx_hm_compress(hvx_ctx *ctx, const hvx_hm_picture *d_pics, int n_pics, cons
   if (n_jobs == 0) return HVX_OK;
   size_t sb = 0;
   hvx_hm_state_size(&sb);
-#ifdef HM_XCD_GROUP
-  const int grid = 8 * ((n_jobs + 7) / 8);
-#else
   const int grid = n_jobs;
-#endif
   hipLaunchKernelGGL(k_hm_compress, dim3(grid), dim3(64), 0, ctx->stream, d_pics, n_pics, d_jobs, n_jobs, n_out,
                      (char *)d_state, sb, d_out_ctu, d_out_rec, d_out_coder);
   return launched("k_hm_compress");

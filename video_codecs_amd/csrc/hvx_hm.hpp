@@ -104,9 +104,7 @@ struct McScratch {
 };
 struct IntraScratch {
   int16_t unf[intra::kB + 3], filt[intra::kB + 3];
-#ifndef HM_LEAN_LDS
   uint8_t org[64 * 64];
-#endif
   uint32_t satd[36];
   int list[12], mpm[3];
   double cc[10];
@@ -126,9 +124,6 @@ struct IntraScratch {
 #ifndef HM_MEMO_B
 #define HM_MEMO_B 16
 #endif
-#if defined(HM_MEMO_HBM) && !defined(HM_NO_MEMO_BIG)
-#define HM_NO_MEMO_BIG  // the 16x16 / 32x32 memo has only the LDS-index form
-#endif
 constexpr int kMemoK = HM_MEMO_K, kMemoDw = 37, kMemoDw0 = 10;
 struct CoefMemo {
   uint32_t key;                   // valid | width | channel | scan | transform skip
@@ -146,7 +141,6 @@ struct CoefMemoBig {
   uint32_t before[kMemoDw], after[kMemoDw];
   uint32_t coef[512];             // int16 pairs (TU-packed order); dword k * 64 + lane
 };
-#ifndef HM_NO_RQT_MEMO
 // The inter residual memo (enc_res_rd_inter): xEstimateInterResidualQT and the residual decision
 // after it depend only on the CU's residual and the RD coder they start from
 // (m_pppcRDSbacCoder[depth][CI_CURR_BEST]); within one CU the residual is fixed by the PUs' motion
@@ -167,7 +161,6 @@ __host__ __device__ constexpr int rq_depth_off(int d) {
   return d == 0 ? 0 : rq_depth_off(d - 1) + kRqK * rq_entry_bytes(d - 1);
 }
 constexpr int kRqBytes = rq_depth_off(4);
-#endif
 // per-chain state in HBM
 struct State {
   int status[4];  // [0]: the job's status word (hvx_hm_job_status: 0 ran, -HVX_HM_BAD_* refused)
@@ -195,18 +188,11 @@ struct State {
   int memo_next;
   CoefMemoBig memob[kMemoB];      // ... and of 16x16 / 32x32 TUs
   int memob_next;
-#ifndef HM_NO_RQT_MEMO
   alignas(16) uint8_t rq_data[kRqBytes];  // the inter residual memo's entries (per CU depth)
   int rq_n[4];                            // ... entries held for the CU being decided at each depth
-#endif
   MeScratch me;                   // leaf scratch outside LDS
   McScratch mc;
   TuSmem<3> tu3;
-#ifdef HM_LEAN_LDS
-  TuSmem<2> tu2;                  // HM_LEAN_LDS: the 16x16 TU pipeline's scratch too
-  uint8_t intra_org[64 * 64];     //   and the intra first pass's original
-  int16_t cstage32[1024];         //   and codeCoeffNxN's 32x32 levels
-#endif
 };
 
 // the LDS leaf scratch (one leaf runs at a time): TU pipelines up to 16x16 and the intra
@@ -215,16 +201,10 @@ struct State {
 union Leaf {
   TuSmem<0> tu0;
   TuSmem<1> tu1;
-#ifndef HM_LEAN_LDS
   TuSmem<2> tu2;
-#endif
   IntraScratch in;
   struct {               // codeCoeffNxN's TU staged in scan order (code_coeff_nxn)
-#ifdef HM_LEAN_LDS
-    int16_t lev[256];    // levels (32x32 TUs: State.cstage32)
-#else
     int16_t lev[1024];   // levels
-#endif
     int16_t ras[256];    // raster position (TUs up to 16x16)
     int32_t sig[256];    // significance context under neighbour-CG patterns 0..3, 6 bits each
     uint8_t cg[64];      // CG scan -> CG raster
@@ -268,10 +248,8 @@ struct Enc {
   int pad_;
   Coder cod[37];
   hvx_estbits est;
-#ifndef HM_NO_EST_MEMO
   uint32_t est_key;      // (w | h << 8 | ch << 16) + 1 of the last estimate_bit (0: none this CTU)
   uint32_t est_st[38];   // its coder's context states 28 .. 179 (every byte estBit reads)
-#endif
   int32_t eb[128];
   uint8_t next[256];
   uint16_t scan[256];    // the current TU's scan tables (TUs up to 16x16), staged by tu_fwd_l
@@ -281,12 +259,10 @@ struct Enc {
   hvx_tu_desc td;        // the current TU's descriptor (tu_desc)
   Tu tstack[kTuStack];   // the live TU nodes (TuSlot), innermost last
   int tsp;
-#ifndef HM_MEMO_HBM
   uint32_t memo_key[kMemoK], memo_hash[kMemoK];  // the count memo's index (S->memo keys / hashes)
   int memo_next;
   uint32_t memob_key[kMemoB], memob_hash[kMemoB];
   int memob_next;
-#endif
   int yw;                // the width of the CU whose TComYuv buffers are in use (compress_cu<D>: 64 >> D)
   float ssim_t[192];     // HVX_RD_SSIM: the (1 - SSIM) terms of a CU's blocks (cu_dssim)
   int dbg[4];  // HM_CHECKS: first violated check (code, a, b) of the job
@@ -341,10 +317,6 @@ struct ProfScope {
   }
 };
 #define HM_PROF(c) ProfScope prof_scope_(c)
-#ifdef HM_PROF_WALK  // the walk's phases in slots 12..15 (instead of the forward transform by size)
-#define HM_WT0(v) uint64_t v = __builtin_amdgcn_s_memtime()
-#define HM_WTADD(k, v) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); hm_e.prof[0][12 + (k)] += n_ - (v); hm_e.prof[1][12 + (k)] += 1; v = n_; } while (0)
-#endif
 #define HM_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define HM_TADD(cat, v) (hm_e.prof[0][(cat)] += __builtin_amdgcn_s_memtime() - (v), hm_e.prof[1][(cat)] += 1)
 #else
@@ -358,13 +330,6 @@ struct ProfScope {
 #endif
 // HM_CHECKS builds validate the indices and sample positions below, record the first violation
 // in E.dbg and keep the access inside its buffer (a debugging aid; off in the product build)
-// HM_TRACE builds print the chain's progress from lane 0 (a debugging aid for faults: the last
-// line of a job before the fault names the step it died in)
-#ifdef HM_TRACE
-#define HM_TR(tag, a, b) do { if (lid() == 0) printf("HMTRACE j%d ctu%d %s %d %d\n", (int)blockIdx.x, hm_e.ctu_addr, (tag), (int)(a), (int)(b)); } while (0)
-#else
-#define HM_TR(tag, a, b) ((void)0)
-#endif
 #ifdef HM_CHECKS
 __device__ __noinline__ void hm_fail(int code, int a, int b) {
   if (E.dbg[0] == 0) { E.dbg[0] = code; E.dbg[1] = a; E.dbg[2] = b; }
@@ -420,14 +385,9 @@ __device__ __forceinline__ void cload(int dst, int src) {
   wsync();
 }
 
-// wave-uniform values read from LDS, moved to scalar registers (HM_SCALAR builds): the serial
-// logic on them becomes scalar arithmetic and branches instead of VALU work under exec masks --
-// measured 7% slower (the readfirstlane round trips lengthen the dependent chains), so off
-#ifdef HM_SCALAR
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-#else
+// a wave-uniform value read from LDS (a marker: moving these to scalar registers with readfirstlane
+// was measured 7% slower -- the round trips lengthen the dependent chains)
 __device__ __forceinline__ int uni(int v) { return v; }
-#endif
 
 // the coefficient-rate lane of cab::coeff_bits on one coder (models 42..184)
 struct CoderLane {
@@ -1291,7 +1251,6 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
       }
       const int sc = env.big ? cab::sig_ctx(pattern, env.first_sig, env.single, sc_l, lw, ch) : (sc_l >> (6 * pattern)) & 63;
       int nnz = is_last_set ? 1 : 0;
-#ifndef HM_WALK_NO_PF
       // the group's significance contexts fetched into lanes once (one LDS round) and written back
       // once: a flag's bin reads its state with v_readlane and forwards the new state to every lane
       // on the same context, leaving one LDS round (the tables) on the chain per bin
@@ -1308,13 +1267,6 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
         nnz += sig;
       }
       if (l < 16) L.st[row_l] = (uint8_t)q_l;
-#else
-      for (int pin = is_last_set ? last_pin - 1 : 15; pin >= 0; pin--) {
-        const int sig = (int)((m16 >> pin) & 1u);
-        if (pin > 0 || sub == 0 || nnz) L.bin(base_sig + __builtin_amdgcn_readlane(sc, pin), sig);
-        nnz += sig;
-      }
-#endif
     }
     const int nnz = __popc(m16);
     HM_WTADD(1, wt_);
@@ -1329,26 +1281,20 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
     int first_c2_abs = 0;
     bool have_c2 = false;
     uint32_t rest = m16;
-#ifndef HM_WALK_NO_PF
     // the four greater-1 contexts of the set in lanes 0..3, the same way
     const int row1_l = base_one + (l & 3) + cab::kCtxLo;
     int q1_l = L.st[row1_l];
-#endif
     for (int idx = 0; rest && idx < 8; idx++) {
       const int pin = 31 - __clz(rest);
       rest &= ~(1u << pin);
       const int av = __builtin_amdgcn_readlane(av_l, pin);
       const int gt1 = av > 1;
-#ifndef HM_WALK_NO_PF
       {
         const int q = __builtin_amdgcn_readlane(q1_l, c1);
         L.frac += (uint32_t)E.eb[q ^ gt1];
         const int ns = E.next[q * 2 + gt1];
         q1_l = (l & 3) == c1 ? ns : q1_l;
       }
-#else
-      L.bin(base_one + c1, gt1);
-#endif
       if (gt1) {
         c1 = 0;
         if (!have_c2) { have_c2 = true; first_c2_abs = av; }
@@ -1357,9 +1303,7 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
         c1++;
       }
     }
-#ifndef HM_WALK_NO_PF
     if (l < 4) L.st[row1_l] = (uint8_t)q1_l;
-#endif
     if (c1 == 0 && have_c2) {
       const int gt2 = first_c2_abs > 2;
       L.bin(cab::kAbs + set, gt2);
@@ -1367,7 +1311,6 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
     }
     HM_WTADD(2, wt_);
     L.ep((be_valid && hidden) ? nnz - 1 : nnz);  // signs (the first one hidden)
-#ifndef HM_ESC_SERIAL
     if (escape) {
       // the escape codes' bin counts lane-parallel (bypass bins: only their total counts): a level's
       // base (idx < 8 ? 2 + first2 : 1) from the set bits before it; the Rice parameter (from 0, no
@@ -1394,24 +1337,6 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
                               : 0u;
       L.ep((int)wave_sum_u32(nb));
     }
-#else
-    if (escape) {  // Rice parameter from 0 (no persistent adaptation in the engine's tool set)
-      int rice = 0, first2 = 1, idx = 0;
-      uint32_t all = m16;
-      while (all) {
-        const int pin = 31 - __clz(all);
-        all &= ~(1u << pin);
-        const int av = __builtin_amdgcn_readlane(av_l, pin);
-        const int base = idx < 8 ? 2 + first2 : 1;
-        if (av >= base) {
-          L.ep(cab::remain_bins((uint32_t)(av - base), rice, d.extended_precision != 0, d.max_log2_tr_range));
-          if (av > (3 << rice)) rice = rice + 1 < 4 ? rice + 1 : 4;
-        }
-        if (av >= 2) first2 = 0;
-        idx++;
-      }
-    }
-#endif
     HM_WTADD(3, wt_);
   }
   return num_sig;
@@ -1625,15 +1550,10 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
     uint32_t *st32 = reinterpret_cast<uint32_t *>(E.cod[E.cur].st);
     if (l < kMemoDw) { cur_st = st32[kMemoDw0 + l]; mask = memo_mask(ch, l); }
     if (l < ndw) cur_cf = reinterpret_cast<const uint32_t *>(coef)[l];
-#ifdef HM_MEMO_HBM  // one HBM round for the keys, one per candidate entry
-    const uint32_t kk = l < kMemoK ? S->memo[l].key : 0u;
-    uint64_t cand = __ballot(kk == key);
-#else
     // the index in LDS: keys and a hash of the levels and masked context states; only an entry whose
     // hash matches is read from HBM, and compared in full there (a hash is never trusted alone)
     hash = memo_hash(cur_st & mask, cur_cf);
     uint64_t cand = __ballot(l < kMemoK && E.memo_key[l < kMemoK ? l : 0] == key && E.memo_hash[l < kMemoK ? l : 0] == hash);
-#endif
     while (cand) {
       const int e = __builtin_ctzll(cand);
       cand &= cand - 1;
@@ -1650,7 +1570,6 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
       }
     }
   }
-#ifndef HM_NO_MEMO_BIG
   int bslot = -1;
   if (d.width >= 16) {  // the 16x16 / 32x32 memo: same index scheme, levels compared from registers
     key = 0x8000u | (uint32_t)d.width | ((uint32_t)ch << 8) | ((uint32_t)d.scan_type << 10) | ((uint32_t)d.transform_skip << 12);
@@ -1700,16 +1619,11 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
     E.memob_key[bslot] = 0;  // invalid until its count is in
     wsync();
   }
-#endif
   HM_T0(t_stage);
   const int n = d.width * d.width;
   const uint16_t *scan = kScan[d.scan_type] + scan_base(ilog2(d.width) - 2);
   const bool staged = n <= 256;
-#ifdef HM_LEAN_LDS
-  int16_t *ls = staged ? E.u.cs.lev : S->cstage32;
-#else
   int16_t *ls = E.u.cs.lev;
-#endif
   const cab::ScanTables tab(d);
   if (lid() < (n >> 4)) E.u.cs.cg[lid()] = tab.scan_cg[lid()];
   if (memo_on) {
@@ -1738,70 +1652,32 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
   } else {
     for (int i = lid(); i < n; i += 64) ls[i] = coef[scan[i]];
   }
-#ifdef HM_REG_CODER
-  RegCoder L;
-  L.load(E.cod[E.cur].st);
-  wsync();
-  uint32_t rice = 0;
-  cab::coeff_bits(d, [&](int sp) { return (int)ls[sp]; }, L, rice);
-  L.store(E.cod[E.cur].st);
-  E.cod[E.cur].frac += L.frac;
-#else
-#ifdef HM_REG_WALK
-  RegWalk L;
-  L.load(E.cod[E.cur].st);
-#else
   CoderLane L{E.cod[E.cur].st, 0};
-#endif
   wsync();
   HM_TADD(PR_COEF_STAGE, t_stage);
   HM_T0(t_walk);
   const StagedScan env{E.u.cs.cg, E.u.cs.ras, E.u.cs.sig, scan, tab.first_sig, tab.single, !staged};
-#ifdef HM_GENERIC_WALK
-  uint32_t rice = 0;
-  if (staged) cab::coeff_bits_env(d, env, [&](int sp) { return uni(ls[sp]); }, L, rice);
-  else cab::coeff_bits(d, [&](int sp) { return uni(ls[sp]); }, L, rice);
-#else
   // the mask-driven walk for every size (a third walk instance in this function measured 20%
   // slower overall: register pressure)
-#ifdef HM_WALK_ROUNDS
-  coeff_count_par(d, env, ls, L);  // measured no faster than the serial walk
-#else
   coeff_count_staged(d, env, ls, L);
-#endif
-#endif
-#ifdef HM_REG_WALK
-  L.store(E.cod[E.cur].st);
-#endif
   E.cod[E.cur].frac += L.frac;
-#endif
   wsync();
   HM_TADD(PR_COEF_WALK, t_walk);
   HM_TADD(PR_COEF4 + ilog2(d.width) - 2, t_desc);
-#ifndef HM_REG_CODER
   if (memo_on) {  // remember the count (FIFO slot)
-#ifdef HM_MEMO_HBM
-    const int slot = S->memo_next;
-#else
     const int slot = E.memo_next;
-#endif
     CoefMemo &m = S->memo[slot];
     const uint32_t *st32 = reinterpret_cast<const uint32_t *>(E.cod[E.cur].st);
     if (l < kMemoDw) { m.before[l] = cur_st; m.after[l] = st32[kMemoDw0 + l]; }
     if (l < d.width * d.width / 2) m.coef[l] = cur_cf;
-#ifdef HM_MEMO_HBM
-    if (l == 0) { m.key = key; m.hash = hash; m.frac = L.frac; S->memo_next = slot + 1 == kMemoK ? 0 : slot + 1; }
-#else
     const int nx = slot + 1 == kMemoK ? 0 : slot + 1;
     if (l == 0) { m.key = key; m.hash = hash; m.frac = L.frac; S->memo_next = nx; }
     wsync();
     E.memo_key[slot] = key;
     E.memo_hash[slot] = hash;
     E.memo_next = nx;
-#endif
     wsync();
   }
-#ifndef HM_NO_MEMO_BIG
   if (bslot >= 0) {  // the 16x16 / 32x32 entry's count
     CoefMemoBig &m = S->memob[bslot];
     const uint32_t *st32 = reinterpret_cast<const uint32_t *>(E.cod[E.cur].st);
@@ -1814,8 +1690,6 @@ __device__ void code_coeff_nxn(const Cu *cu, const Tu &t, int comp, const int16_
     E.memob_next = nx;
     wsync();
   }
-#endif
-#endif
 }
 // TEncEntropy::estimateBit (TEncEntropy.cpp:685) from the current coder
 // The entries TEncSbac::estBit writes (exactly those of estbit_update), one per lane: two
@@ -1830,7 +1704,6 @@ __device__ void estimate_bit(int w, int h, int ch) {
   hvx_estbits *e = &E.est;
 #define EB(ctx, v) E.eb[st[(ctx)] ^ (v)]
   const int l = lid(), b = l & 1;
-#ifndef HM_NO_EST_MEMO
   static_assert(HVX_CTX_QT_CBF >= 28 && HVX_CTX_ABS + 6 <= 180, "estBit's context range");
   {
     const uint32_t key = (uint32_t)(w | h << 8 | ch << 16) + 1;
@@ -1840,7 +1713,6 @@ __device__ void estimate_bit(int w, int h, int ch) {
     if (l < 38) E.est_st[l] = cur;
     if (l == 0) E.est_key = key;
   }
-#endif
   // round 1: cbf (20), root cbf (8), sig CG (4), significance (<= 28)
   if (l < 20) e->blockCbpBits[l >> 1][b] = EB(HVX_CTX_QT_CBF + (l >> 1), b);
   else if (l < 28) e->blockRootCbpBits[(l - 20) >> 1][b] = EB(HVX_CTX_QT_ROOT_CBF + ((l - 20) >> 1), b);
@@ -2260,9 +2132,6 @@ __device__ uint32_t yuv_dist(Yuv *a, Yuv *b, int w) {
 template <int L>
 __device__ __forceinline__ TuSmem<L> &tu_smem() {
   if constexpr (L == 3) return E.S->tu3;
-#ifdef HM_LEAN_LDS
-  else if constexpr (L == 2) return E.S->tu2;
-#endif
   else return *reinterpret_cast<TuSmem<L> *>(&E.u);
 }
 template <int L>
@@ -2756,7 +2625,6 @@ __device__ void estimate_inter_residual_qt(Cu *cu, Yuv *resi, double *rd, uint32
   int32_t abs_sum[3] = {0, 0, 0};
   int best_mode[3] = {0, 0, 0};
   const int layer = qt_layer(l2);
-  HM_TR("rqt", LV * 100 + l2, rel);
   cload(RD(depth, CI_QT_TRAFO_ROOT), E.cur);
   if (check_full) {
     double min_cost[3] = {kMaxDouble, kMaxDouble, kMaxDouble};
@@ -2786,7 +2654,6 @@ __device__ void estimate_inter_residual_qt(Cu *cu, Yuv *resi, double *rd, uint32
           blk_copy(best_res, w, qres, qs, w, h);
         }
         const int32_t cur_abs = transform_tu(cu, t, comp, pres, ystride(comp), cur_coef);
-        HM_TR("rqt_tf", comp * 10 + mode, cur_abs);
         int32_t cabs = cur_abs;
         if (first || cur_abs == 0) {
           non_dist = weigh(sse_wave(pres, ystride(comp), nullptr, 0, w, h), comp);
@@ -2803,9 +2670,7 @@ __device__ void estimate_inter_residual_qt(Cu *cu, Yuv *resi, double *rd, uint32
           code_qt_cbf(cu, t, comp, 1);
           code_coeff_nxn(cu, t, comp, cur_coef, true);  // E.td from transform_tu above
           cur_bits = written_bits();
-          HM_TR("rqt_cnt", comp * 10 + mode, cur_bits);
           inv_transform_tu(cu, t, comp, cur_coef, qres, qs, true);
-          HM_TR("rqt_inv", comp * 10 + mode, 0);
           cur_dist = dist_part(qres, qs, pres, ystride(comp), w, h, comp);
           cur_cost = rd_cost(cur_bits, cur_dist);
         } else if (mode == 1) {
@@ -2830,7 +2695,6 @@ __device__ void estimate_inter_residual_qt(Cu *cu, Yuv *resi, double *rd, uint32
       }
       set_ts_range(cu, comp, crel, np, best_mode[comp]);
       set_cbf_range(cu, comp, crel, np, (abs_sum[comp] > 0 ? 1 : 0) << trmode);
-      HM_TR("rqt_comp", comp, abs_sum[comp]);
     }
     cload(E.cur, RD(depth, CI_QT_TRAFO_ROOT));
     reset_bits();
@@ -2942,7 +2806,6 @@ __device__ void clear_residual_fields(Cu *cu) {
   }
   wsync();
 }
-#ifndef HM_NO_RQT_MEMO
 __device__ __forceinline__ uint8_t *rq_entry(int depth, int k) {
   int off = 0;
   for (int d = 0; d < depth; d++) off += kRqK * rq_entry_bytes(d);
@@ -3055,7 +2918,6 @@ __device__ __noinline__ void rqt_memo_resi(const Cu *cu, int depth, int k, Yuv *
   else cpy64(resi_best->s, r, W2 + (W2 >> 1));
   wsync();
 }
-#endif
 __device__ void enc_res_rd_inter(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Yuv *resi_best, Yuv *reco, int skip_residual) {
   const int W = cu->width, depth = cu->depth;
   if (skip_residual) {
@@ -3079,15 +2941,8 @@ __device__ void enc_res_rd_inter(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Yuv *re
   tu_root(t0, cu, 0);
   E.cur = GOON;
   cload(E.cur, RD(depth, CI_CURR_BEST));
-#if defined(HM_PROFILE) && defined(HM_PROF_RQT)  // slots 12: the RQT + decision + final count, 13: replays, 14: stores, 15: lookups
-  ProfScope prof_rqt_(12);
-#define HM_RQT_T0(v) HM_T0(v)
-#define HM_RQT_TADD(c, v) HM_TADD(c, v)
-#else
 #define HM_RQT_T0(v) ((void)0)
 #define HM_RQT_TADD(c, v) ((void)0)
-#endif
-#ifndef HM_NO_RQT_MEMO
   HM_RQT_T0(t_find);
   const int hit = rqt_memo_find(cu, depth);
   HM_RQT_TADD(15, t_find);
@@ -3097,7 +2952,6 @@ __device__ void enc_res_rd_inter(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Yuv *re
     rqt_memo_replay(cu, depth, hit);
     HM_RQT_TADD(13, t_rep);
   } else
-#endif
   {
     double nz_cost = 0;
     uint32_t nz_bits = 0, nz_dist = 0, z_dist = 0;
@@ -3109,27 +2963,21 @@ __device__ void enc_res_rd_inter(Cu *cu, Yuv *org, Yuv *pred, Yuv *resi, Yuv *re
     const int dropped = zero_cost < nz_cost || !cu_qt_root_cbf(cu, 0);
     if (dropped) clear_residual_fields(cu);
     else set_inter_residual_qt_data<0>(cu, nullptr, 0, t0);
-#ifndef HM_NO_RQT_MEMO
     HM_RQT_T0(t_st);
     slot = rqt_memo_store(cu, depth, dropped);
     HM_RQT_TADD(14, t_st);
-#endif
   }
   cload(E.cur, RD(depth, CI_CURR_BEST));
   uint32_t final_bits = 0;
   add_symbol_bits_inter(cu, &final_bits);
   if (!cu_qt_root_cbf(cu, 0)) yuv_op(YOP_CLEAR, resi_best, nullptr, nullptr, W);
-#ifndef HM_NO_RQT_MEMO
   else if (hit >= 0) rqt_memo_resi(cu, depth, hit, resi_best, 0);
-#endif
   else set_inter_residual_qt_data<0>(cu, resi_best, 1, t0);
-#ifndef HM_NO_RQT_MEMO
   if (slot >= 0) {
     if (cu_qt_root_cbf(cu, 0)) rqt_memo_resi(cu, depth, slot, resi_best, 1);
     if (lid() == 0) E.S->rq_n[depth] = slot + 1;
     wsync();
   }
-#endif
   cload(RD(depth, CI_TEMP_BEST), E.cur);
   yuv_op(YOP_ADD_CLIP, reco, pred, resi_best, W);
   const uint32_t final_dist = yuv_dist(reco, org, W);
@@ -3395,7 +3243,6 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
           uint32_t bt = mb[l] + ref_bits(r, nref), ct;
           int pidx, pnum;
           est_mvp_amvp(cu, ps, pu, org, l, r, Q.amvp[l][r], Q.mvpred[l][r], pidx, pnum, bip_dist_temp);
-          HM_TR("amvp", pu * 100 + l * 10 + r, pidx);
           pu_set(cu, ps, pu, PU_MVP_IDX, l, pidx);
           pu_set(cu, ps, pu, PU_MVP_NUM, l, pnum);
           if (E.P.mvd_l1_zero && l == 1 && bip_dist_temp < best_bip_dist) {
@@ -3413,7 +3260,6 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
             ct += mv_cost_bits(bt);
           } else {
             motion_estimation(cu, ps, pu, l, r, Q.mvpred[l][r], Q.mvtemp[l][r], bt, ct);
-            HM_TR("me", pu * 100 + l * 10 + r, Q.mvtemp[l][r][0] * 10000 + Q.mvtemp[l][r][1]);
           }
           check_best_mvp(Q.amvp[l][r], Q.mvtemp[l][r], Q.mvpred[l][r], pidx, bt, ct);
           Q.mvp_idx[l][r] = pidx; Q.mvp_num[l][r] = pnum;
@@ -3544,7 +3390,6 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
         const uint32_t err = wave_satd(yaddr(org, 0, xp - cu->x, yp - cu->y), ystride(0),
                                        yaddr(&E.S->tmp_yuv_pred, 0, xp - cu->x, yp - cu->y), ystride(0), w, h);
         me_cost = err + mv_cost_bits(me_bits);
-        HM_TR("p_satd", pu, me_cost);
       }
       const Part save = cu->p[a];
       int mrg_dir = 0, mrg_idx = 0;
@@ -3552,7 +3397,6 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
       uint32_t mrg_cost = kMaxU32;
       MergeList ml;
       merge_estimation(cu, ps, pu, org, mrg_dir, mrg, mrg_idx, mrg_cost, ml);
-      HM_TR("p_mrg", pu, mrg_idx);
       if (mrg_cost < me_cost) {
         pu_set(cu, ps, pu, PU_MERGE, 0, 1);
         pu_set(cu, ps, pu, PU_MERGE_IDX, 0, mrg_idx);
@@ -3571,7 +3415,6 @@ __device__ void pred_inter_search(Cu *cu, Yuv *org, Yuv *pred, int use_mrg) {
       }
     }
     mc_pu(cu, ps, pu, pred);
-    HM_TR("p_mc", pu, ps);
   }
 }
 
@@ -3640,11 +3483,7 @@ __device__ void intra_border(const Cu *cu, const Tu &t, int comp, int16_t *B) {
 __device__ void intra_predict_tu(const Cu *cu, const Tu &t, int comp, int mode, int16_t *pred) {
   HM_PROF(PR_IPRED);
   IntraScratch &is = E.u.in;
-#ifdef HM_LEAN_LDS
-  uint8_t *is_org = E.S->intra_org;
-#else
   uint8_t *is_org = is.org;
-#endif
   const int n = t.w[comp], log2n = ilog2(n);
   const bool luma = comp == 0;
   intra_border(cu, t, comp, is.unf);
@@ -3670,11 +3509,7 @@ __device__ void intra_predict_tu(const Cu *cu, const Tu &t, int comp, int mode, 
 __device__ void intra_first_pass(const Cu *cu, const Tu &tpu, Yuv *org, int depth) {
   HM_PROF(PR_IFP);
   IntraScratch &is = E.u.in;
-#ifdef HM_LEAN_LDS
-  uint8_t *is_org = E.S->intra_org;
-#else
   uint8_t *is_org = is.org;
-#endif
   const int n = tpu.w[0], log2n = ilog2(n);
   intra_border(cu, tpu, 0, is.unf);
   intra::filter_border(is.unf, n, log2n, true, true, is.filt);
@@ -4287,7 +4122,6 @@ __device__ void check_rd_merge2nx2n(int depth) {
   MergeList m;
   merge_candidates(TEMP(depth), SIZE_2Nx2N, 0, m);
   const int n = m.n;
-  HM_TR("m_cands", n, depth);
   int buf = 0;  // mergeCandBuffer bits
   int best_is_skip = 0;
   for (int nores = 0; nores < 2; nores++) {
@@ -4309,12 +4143,9 @@ __device__ void check_rd_merge2nx2n(int depth) {
         p.mv[1][0] = f1.mv[0]; p.mv[1][1] = f1.mv[1]; p.ref[1] = (int8_t)f1.ref;
       }
       wsync();
-      HM_TR("m_set", k, nores);
       mc_cu(tmp, YB(Y_PRED_TEMP, depth));
-      HM_TR("m_mc", k, nores);
       enc_res_rd_inter(tmp, YB(Y_ORIG, depth), YB(Y_PRED_TEMP, depth), YB(Y_RESI_TEMP, depth), YB(Y_RESI_BEST, depth),
                        YB(Y_RECO_TEMP, depth), nores != 0);
-      HM_TR("m_rqt", k, nores);
       if (nores == 0 && !cu_qt_root_cbf(tmp, 0)) buf |= 1 << k;
       check_best_mode(depth);
       reinit_temp(depth);
@@ -4328,7 +4159,6 @@ __device__ void check_rd_inter(int depth, int ps, int use_mrg) {
   cu_set_all(tmp, F_PRED, MODE_INTER);
   tmp->merge_amp = 1;
   pred_inter_search(tmp, YB(Y_ORIG, depth), YB(Y_PRED_TEMP, depth), use_mrg);
-  HM_TR("i_pis", ps, depth);
   enc_res_rd_inter(tmp, YB(Y_ORIG, depth), YB(Y_PRED_TEMP, depth), YB(Y_RESI_TEMP, depth), YB(Y_RESI_BEST, depth),
                    YB(Y_RECO_TEMP, depth), 0);
   const double c = cu_cost(tmp->dssim, tmp->bits, tmp->dist);
@@ -4385,10 +4215,7 @@ __device__ void compress_cu(int parent_ps) {
   const int depth = D;
   E.yw = 64 >> D;
   Cu *best = BEST(depth);
-  HM_TR("cu", best->x * 10000 + best->y, D);
-#ifndef HM_NO_RQT_MEMO
   if (lid() == 0) E.S->rq_n[D] = 0;  // the inter residual memo holds this CU's RQTs only
-#endif
   copy_org_to_yuv(YB(Y_ORIG, depth), best);
   int boundary = 0;
   const int rx = best->x + best->width - 1, by = best->y + best->width - 1;
@@ -4397,40 +4224,38 @@ __device__ void compress_cu(int parent_ps) {
     reinit_temp(depth);
     if (E.P.slice_type != I_SLICE) {
       check_rd_merge2nx2n(depth);
-      HM_TR("merge", best->x * 10000 + best->y, D);
       reinit_temp(depth);
-      check_rd_inter(depth, SIZE_2Nx2N, 0); HM_TR("inter", SIZE_2Nx2N, D);
+      check_rd_inter(depth, SIZE_2Nx2N, 0);
       reinit_temp(depth);
     }
     reinit_temp(depth);
     if (E.P.slice_type != I_SLICE) {
-      check_rd_inter(depth, SIZE_Nx2N, 0); HM_TR("inter", SIZE_Nx2N, D);
+      check_rd_inter(depth, SIZE_Nx2N, 0);
       reinit_temp(depth);
-      check_rd_inter(depth, SIZE_2NxN, 0); HM_TR("inter", SIZE_2NxN, D);
+      check_rd_inter(depth, SIZE_2NxN, 0);
       reinit_temp(depth);
       if (E.P.amp && depth < 3) {
         int hor = 0, ver = 0, mhor = 0, mver = 0;
         derive_test_mode_amp(BEST(depth), parent_ps, hor, ver, mhor, mver);
         if (hor) {
-          check_rd_inter(depth, SIZE_2NxnU, 0); HM_TR("inter", SIZE_2NxnU, D); reinit_temp(depth);
-          check_rd_inter(depth, SIZE_2NxnD, 0); HM_TR("inter", SIZE_2NxnD, D); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_2NxnU, 0); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_2NxnD, 0); reinit_temp(depth);
         } else if (mhor) {
-          check_rd_inter(depth, SIZE_2NxnU, 1); HM_TR("inter", SIZE_2NxnU, D); reinit_temp(depth);
-          check_rd_inter(depth, SIZE_2NxnD, 1); HM_TR("inter", SIZE_2NxnD, D); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_2NxnU, 1); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_2NxnD, 1); reinit_temp(depth);
         }
         if (ver) {
-          check_rd_inter(depth, SIZE_nLx2N, 0); HM_TR("inter", SIZE_nLx2N, D); reinit_temp(depth);
-          check_rd_inter(depth, SIZE_nRx2N, 0); HM_TR("inter", SIZE_nRx2N, D); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_nLx2N, 0); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_nRx2N, 0); reinit_temp(depth);
         } else if (mver) {
-          check_rd_inter(depth, SIZE_nLx2N, 1); HM_TR("inter", SIZE_nLx2N, D); reinit_temp(depth);
-          check_rd_inter(depth, SIZE_nRx2N, 1); HM_TR("inter", SIZE_nRx2N, D); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_nLx2N, 1); reinit_temp(depth);
+          check_rd_inter(depth, SIZE_nRx2N, 1); reinit_temp(depth);
         }
       }
     }
     best = BEST(depth);
     if (E.P.slice_type == I_SLICE || (best->p[0].cbf[0] || best->p[0].cbf[1] || best->p[0].cbf[2])) {
       check_rd_intra(depth, SIZE_2Nx2N);
-      HM_TR("intra", 0, D);
       reinit_temp(depth);
       if (depth == 3 && TEMP(depth)->width > 4) {
         check_rd_intra(depth, SIZE_NxN);
@@ -4488,7 +4313,6 @@ __device__ void compress_cu(int parent_ps) {
   }
   cu_copy_to_pic(BEST(depth));
   yuv_to_pic(YB(Y_RECO_BEST, depth), BEST(depth));
-  HM_TR("cu_end", 0, D);
 }
 
 // ============================================================================================
@@ -4564,9 +4388,7 @@ __device__ void compress_ctu(int addr, const Coder *entry_g, int entry_in_lds, C
   // estBits start from zero per CTU like the restatement (every table entry RDOQ reads is
   // rewritten by estimateBit before its first use)
   for (int i = lid(); i < (int)(sizeof(hvx_estbits) / 4); i += 64) ((uint32_t *)&E.est)[i] = 0;
-#ifndef HM_NO_EST_MEMO
   if (lid() == 0) E.est_key = 0;
-#endif
   wsync();
   // initCtu of the picture's CTU and the depth-0 best/temp CUs
   for (int k = 0; k < 2; k++) {
@@ -4596,7 +4418,6 @@ __device__ void compress_ctu(int addr, const Coder *entry_g, int entry_in_lds, C
     compress_cu<0>(SIZE_NONE);
   }
   HM_STAGE(5);
-  HM_TR("decided", 0, 0);
   if (HM_STOPPED) return;
   // encodeCtu on m_pppcRDSbacCoder[0][CI_CURR_BEST] after resetBits (TEncSlice.cpp:821-828)
   E.cur = RD(0, CI_CURR_BEST);
@@ -4659,15 +4480,7 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
                                                     char *state_base, size_t state_bytes, hvx_hm_ctu *out_ctu,
                                                     uint8_t *out_rec, hvx_hm_coder *out_coder) {
   using namespace hm;
-#ifdef HM_XCD_GROUP
-  // workgroups go to the 8 XCDs round-robin (blockIdx % 8): give XCD x the contiguous job range
-  // [x * per, (x + 1) * per), so neighbouring jobs (the row slices of one picture, which read the
-  // same reference windows and neighbour CTUs) share an XCD's L2
-  const int per = (n_jobs + 7) >> 3;
-  const int jid = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-#else
   const int jid = blockIdx.x;
-#endif
   if (jid >= n_jobs) return;
   const int l = threadIdx.x;
   const hvx_hm_job &job = jobs[jid];
@@ -4678,12 +4491,10 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
     if (l < 4) S->dbg[l] = 0;
     if (bad) return;
   }
-#ifndef HM_NO_LDS_ZERO
   // the wave's LDS record starts zeroed, so nothing the decision reads before writing it (every
   // such read is a bug) depends on what the previous workgroup on this CU left there
   for (int i = l; i < (int)(sizeof(Enc) / 4); i += 64) reinterpret_cast<uint32_t *>(&hm_e)[i] = 0;
   wsync();
-#endif
   copy_words(&hm_e.P, &pics[job.pic], (int)sizeof(hvx_hm_picture));
   wsync();
   for (int i = l; i < 128; i += 64) {
@@ -4705,23 +4516,19 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
   const int resume = job.flags & HVX_HM_RESUME;
   if (resume) {
     copy_words(&hm_e.cod[RD(0, CI_CURR_BEST)], &S->carry, (int)sizeof(Coder));
-#ifndef HM_MEMO_HBM
     if (l < kMemoK) { hm_e.memo_key[l] = S->memo[l].key; hm_e.memo_hash[l] = S->memo[l].hash; }
     hm_e.memo_next = S->memo_next;
     if (l < kMemoB) { hm_e.memob_key[l] = S->memob[l].key; hm_e.memob_hash[l] = S->memob[l].hash; }
     hm_e.memob_next = S->memob_next;
-#endif
   } else {
     copy_words(S->int2n, job.int2n, (int)sizeof(S->int2n));
     if (l < kMemoK) S->memo[l].key = 0;  // the count memo starts empty
     if (l == 0) S->memo_next = 0;
-#ifndef HM_MEMO_HBM
     if (l < kMemoK) { hm_e.memo_key[l] = 0; hm_e.memo_hash[l] = 0; }
     hm_e.memo_next = 0;
     if (l < kMemoB) { S->memob[l].key = 0; hm_e.memob_key[l] = 0; hm_e.memob_hash[l] = 0; }
     if (l == 0) S->memob_next = 0;
     hm_e.memob_next = 0;
-#endif
   }
   wsync();
   const int n = job.n_ctus;
@@ -4741,7 +4548,6 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
       slice_first = addr == s0;
     }
     compress_ctu(addr, &job.entry, (k > 0 || resume) && !slice_first, out_coder ? &out_coder[slot] : nullptr);
-    HM_TR("ctu_done", addr, k);
     // the next CTU starts from this CTU's encodeCtu state (m_pppcRDSbacCoder[0][CI_CURR_BEST])
     // which compress_ctu left in coder RD(0, CI_CURR_BEST)
     copy_words(&S->carry, &hm_e.cod[RD(0, CI_CURR_BEST)], (int)sizeof(Coder));

@@ -441,11 +441,7 @@ __device__ void me_tz(const hvx_me_job &j, MeInt &m) {
   }
   if (m.best_dist == 1) { m.best_dist = 0; me_2point<S, SUB, NW>(m, g0); }
   // raster (step 5) over the re-centred range, lists of kMeMaxList points
-#ifdef HVX_EXP_NORASTER
-  if (false) {
-#else
   if (m.best_dist > 5) {
-#endif
     m.best_dist = 5;
     const int nx = (g.r - g.l) / 5 + 1, ny = (g.b - g.t) / 5 + 1, n = nx * ny;
     const float rnx = 1.0f / (float)nx;

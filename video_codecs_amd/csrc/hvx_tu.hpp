@@ -406,12 +406,7 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
 #define HVX_RDOQ_PHASE(k) ((void)0)
 #endif
 // sub-phases of the reverse scan (profile builds with HVX_RDOQ_PROF_SUB: slots 12..15)
-#if defined(HVX_TU_PROF_HOOK) && defined(HVX_RDOQ_PROF_SUB)
-  uint64_t t_sb = __builtin_amdgcn_s_memtime();
-#define HVX_RDOQ_SUB(k) do { const uint64_t t_n = __builtin_amdgcn_s_memtime(); HVX_TU_PROF_HOOK(12 + (k), t_n - t_sb); t_sb = t_n; } while (0)
-#else
 #define HVX_RDOQ_SUB(k) ((void)0)
-#endif
   // ---- A. per-coefficient work across lanes ----
   bool anyq = false;
   for (int sp = lane; sp < NN; sp += HVX_WAVE) {
@@ -426,13 +421,11 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   }
   // every rounded level 0: the decisions all keep level 0 (no last position, nothing to hide), so
   // the reverse scan would only price them -- its outputs are all-zero levels and uiAbsSum 0
-#ifndef HVX_RDOQ_NO_ZERO_EXIT
   if (__ballot(anyq) == 0) {
     for (int i = lane; i < NN; i += HVX_WAVE) s.lev[i] = 0;
     __syncthreads();
     return 0;
   }
-#endif
   // estBits in lane slices: entry [ctx][0] in lane ctx, [ctx][1] in lane 32 + ctx (or own VGPR)
   const int t_sb0 = lane < 44 ? est->significantBits[lane][0] : 0;
   const int t_sb1 = lane < 44 ? est->significantBits[lane][1] : 0;
@@ -441,9 +434,6 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   __syncthreads();
 
   HVX_RDOQ_PHASE(0);
-#if defined(HVX_TU_PROF_HOOK) && defined(HVX_RDOQ_PROF_SUB)
-  t_sb = __builtin_amdgcn_s_memtime();
-#endif
   // ---- B. reverse-scan decisions (wave-uniform) ----
   const uint32_t rice0 = (uint32_t)d.golomb_rice_stat / 4;
   const bool persistent = d.persistent_rice != 0;
@@ -560,9 +550,6 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
       base_cost += cc0;
     }
     if (start >= 0) {
-#ifdef HVX_RDOQ_SERIAL_B
-      serial_from(start);
-#else
       // Speculation in rounds: the serial state at each decided position is predicted from guessed
       // levels of the positions before it (scalar, integers only), and every position's decision
       // is then evaluated lane-parallel from its predicted state with the serial pass's own
@@ -577,17 +564,6 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
       uint32_t best = 0;
       int stv_l = 0;
       for (int round = 0;; round++) {
-#ifdef HVX_RDOQ_SCAN_PREDICT
-        {
-          int c1s = c1, c2s = c2;
-          uint32_t c1is = c1_idx, c2is = c2_idx, rs = rice;
-          for (int pin = start; pin >= 0; pin--) {
-            const int pk = c1s | (c2s << 2) | ((int)c1is << 4) | ((int)c2is << 9) | ((int)rs << 14);
-            pst_l = lane == pin ? pk : pst_l;
-            rd_step((uint32_t)rl((int)guess, pin), c1s, c2s, c1is, c2is, rs, persistent);
-          }
-        }
-#else
         {
           // rd_step's updates in closed form over the positions decided before this lane's (pins
           // start .. pin+1): c1Idx / c2Idx count the levels >= 1 / > 1, c2 saturates at 2, c1 is 0
@@ -616,7 +592,6 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
           }
           pst_l = c1s | (c2s << 2) | ((int)(c1_idx + n_nz) << 4) | ((int)(c2_idx + n_g1) << 9) | ((int)rs << 14);
         }
-#endif
         const int c1p = pst_l & 3, c2p = (pst_l >> 2) & 3;
         const uint32_t c1ip = (uint32_t)(pst_l >> 4) & 31, c2ip = (uint32_t)(pst_l >> 9) & 31, rp = (uint32_t)(pst_l >> 14) & 31;
         const int ctx_one_l = 4 * (int)ctx_set + c1p, ctx_abs_l = (int)ctx_set + c2p;
@@ -697,7 +672,6 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
         rd_step((uint32_t)rl((int)best, f), c1, c2, c1_idx, c2_idx, rice, persistent);
         if (f > 0) serial_from(f - 1);
       }
-#endif
       HVX_RDOQ_SUB(2);
       if (cgp > 0) {  // the next group's context set and counters (:2262-2266)
         ctx_set = (comp ? 4 : 0) + ((comp == 0 && cgp - 1 > 0) ? 2 : 0) + (c1 == 0 ? 1 : 0);
@@ -817,7 +791,6 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
   if (d.sign_hiding && abs_sum >= 2) {
     const double iq = (double)kInvQuantScales[d.qp_rem];
     const int64_t rdf = (int64_t)(iq * iq * (1 << (2 * d.qp_per)) / d.lambda / 16 / (1 << 0) + 0.5);
-#ifndef HVX_SBH_GROUP_PER_LANE
     if constexpr (L <= 1) {
       // TUs up to 8x8: every position in its own lane (lane = group * 16 + k).  A group's
       // first / last non-zero come from its ballot, its level sum (signed, as the reference sums
@@ -895,7 +868,6 @@ __device__ int32_t tu_rdoq(TuSmem<L> &s, const hvx_tu_desc &d, const hvx_estbits
       HVX_RDOQ_PHASE(3);
       return abs_sum;
     }
-#endif
     const int sub = lane, pos = sub << 4;
     int first_nz = 16, last_nz = -1, abs_in = 0;
     if (sub < NCG) {

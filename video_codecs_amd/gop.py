@@ -186,7 +186,6 @@ class Segment:
         self.base_qp, self.seed = base_qp, seed
         self.dpb, self.cols, self.lists = {}, {}, {}   # POC -> reference frame / motion field / (nref, ref POCs)
         self.rates = np.zeros((3, 7))                   # SAO-off rates per temporal layer (decidePicParams)
-        self.coded = np.zeros(202, np.uint8)            # the slice writer's m_binsCoded flags
         self.enc_table = I_SLICE                        # TEncSlice::m_encCABACTableIdx
         self.hist = []                                  # stVSSIM history, most recent first
         self.tables, self.bytes = [], []                # per coded picture: CABAC table used, slice data bytes
@@ -296,18 +295,29 @@ class ClosedSegments:
     # ---- one step: one launch (and the picture's loop after its last launch) -------------------
     def step(self):
         """Launch L of picture t; after the picture's last launch, finish() it.  Returns the CTUs
-        this launch decided."""
-        if self.L == 0:
-            self.begin()
-        self.launch(self.L)
-        self.after_launch(self.L)
-        n = len(self.segs) * self.nch * self.ctus_step
-        self.ctus_decided += n
-        self.L += 1
-        if self.L == self.launches:
-            self.finish()
-            self.L = 0
-            self.t += 1
+        this launch decided.  Every allocation and kernel of the step is ordered on one stream
+        (torch's current stream, or the segments' own when that is the null stream), so no buffer is
+        released to the caching allocator while a kernel of another stream still reads it."""
+        import contextlib
+        ctx = contextlib.nullcontext()
+        if self.device != "cpu":
+            import torch
+            if torch.cuda.current_stream().cuda_stream == 0:
+                if getattr(self, "_stream", None) is None:
+                    self._stream = torch.cuda.Stream()
+                ctx = torch.cuda.stream(self._stream)
+        with ctx:
+            if self.L == 0:
+                self.begin()
+            self.launch(self.L)
+            self.after_launch(self.L)
+            n = len(self.segs) * self.nch * self.ctus_step
+            self.ctus_decided += n
+            self.L += 1
+            if self.L == self.launches:
+                self.finish()
+                self.L = 0
+                self.t += 1
         return n
 
     def launch(self, L):
@@ -319,6 +329,7 @@ class ClosedSegments:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         self.eng.launch(jt, len(self.segs) * self.nch, self.out_ctu, self.out_rec)
+        self._jobs = jt  # held until the next launch (the kernel reads it asynchronously)
         if ev is not None:
             ev[1].record()
             self.launch_events.append((self.t, len(self.segs) * self.nch * self.ctus_step, ev))
@@ -391,7 +402,7 @@ class ClosedSegments:
     def write_slices(self, sao):
         """encodeSlice of every slice of picture t (hvx_hm_write_slices, one launch for all segments):
         the slice data bytes per segment, and each segment's next cabac_init table
-        (determineCabacInitIdx over the last slice's final states and the writer's coded flags)."""
+        (determineCabacInitIdx over the last slice's final states and coded contexts)."""
         import torch
         n_sl = len(self.segs) * self.nch
         cap = max(1 << 16, self.cl * 12288)
@@ -404,7 +415,11 @@ class ClosedSegments:
             if sao is not None:
                 coded_t = torch.from_numpy(np.ascontiguousarray(sao[s][1], np.int32)).to(self.device)
                 keep.append(coded_t)
-                en = [int(x) for x in sao[s][3]]
+                # the slice header carries one chroma flag, Cb's (TEncGOP.cpp:1504-1508): when the rates
+                # of decidePicParams disabled only one chroma component, Cr's offsets are applied but
+                # not written
+                e = [int(x) for x in sao[s][3]]
+                en = [e[0], e[1], e[1]]
             for c in range(self.nch):
                 k = s * self.nch + c
                 sl[k]["pic"], sl[k]["first_ctu"], sl[k]["n_ctus"], sl[k]["out_cap"] = s, c * self.cl, self.cl, cap
@@ -420,10 +435,11 @@ class ClosedSegments:
         nbytes = []
         for s, seg in enumerate(self.segs):
             r = res[s * self.nch:(s + 1) * self.nch]
-            for k in range(self.nch):
-                seg.coded |= cabac_init.coded_flags(r[k]["coded"])
+            # determineCabacInitIdx after the picture's last slice (TEncSlice.cpp:1096-1099): that slice's
+            # final states and the contexts it coded (resetEntropy -> initBuffer clears m_binsCoded)
             seg.enc_table = cabac_init.determine_cabac_init_idx(self.plan[self.t].slice_type, r[-1]["states"][:202],
-                                                                seg.coded, self.cur[s]["qp"], self.eb)
+                                                                cabac_init.coded_flags(r[-1]["coded"]),
+                                                                self.cur[s]["qp"], self.eb)
             nbytes.append(int(r["n_bytes"].sum()))
         self.last_slices = (out, res, cap)
         return nbytes
