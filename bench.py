@@ -1,18 +1,22 @@
 #!/usr/bin/env python3
 """Benchmark: 64x64 CTUs/s of HM-16.5rc1's CU mode decision on 2160p random YUV, bit-exact vs HM.
 
-One step = one launch of hvx_hm_compress (include/hvx.h) over every SliceMode=1 slice of P
-pictures in flight: a 3840x2160 4:2:0 picture has 34 CTU rows, each row a slice; with 22 pictures
-per GPU that is 748 slice chains, one wave each, and a step advances every chain by --ctus CTUs
-(default 1), each CTU TEncCu::compressCtu + encodeCtu exactly as HM decides it: merge/skip, AMVP
-+ TZ search + fractional refinement against 4 references, 2NxN/Nx2N/AMP, the RQT with RDOQ and
-transform skip, intra-in-inter, the CABAC context carry.  The chains' CABAC
-state and CTU data stay in HBM between steps (HVX_HM_RESUME).  Inputs are resident in HBM before
-timing starts; each picture's reference frames are the previous synthetic frames.
+N = 1 (the headline, `--workload steady`): one step = one launch of hvx_hm_compress (include/hvx.h)
+over every SliceMode=1 slice of P pictures in flight: a 3840x2160 4:2:0 picture has 34 CTU rows
+(33 slice chains: the partial bottom row continues the chain above it); with 62 pictures per GPU
+that is 2046 slice chains, one wave each, and a step advances every chain by --ctus CTUs (default 1),
+each CTU TEncCu::compressCtu + encodeCtu exactly as HM decides it: merge/skip, AMVP + TZ search +
+fractional refinement against 4 references, 2NxN/Nx2N/AMP, the RQT with RDOQ and transform skip,
+intra-in-inter, the CABAC context carry.  The chains' CABAC state and CTU data
+stay in HBM between steps (HVX_HM_RESUME).  Inputs are resident in HBM before timing starts; each
+picture's reference frames are the previous synthetic frames.
 
-Multi-GPU (torch.distributed.run): one rank per GPU, each rank decides its own pictures (different
-synthetic frames); per step every rank's reconstructed CTUs are gathered to rank 0's shared DPB
-(video_codecs_amd/dpb.py, RCCL over xGMI, asynchronous, double-buffered); weak scaling.
+N > 1 (torch.distributed.run; `--workload closed`, BASELINE config 5): one rank per GPU, each rank
+encodes its own closed LDP GOP segments (gop.ClosedSegments: disjoint frame indices, references made
+by each segment's own loop on the device); after every picture each rank's finished (deblocked + SAO)
+pictures are gathered to rank 0's shared DPB (video_codecs_amd/dpb.py, RCCL over xGMI, asynchronous,
+double-buffered); weak scaling.  The same per-GPU workload at N = 1 is the N = 1 line's
+`config5_closed_segments` figure.
 
 Contract: python bench.py --gpus N --steps K --warmup W  -> one JSON line on rank 0.
 """

@@ -7,6 +7,10 @@
   YUV (tests/golden/ctu_ra_closed_q*.bin), and so does every picture's CABAC initialisation table.
 - test_closed_ldp_segment_vs_hm: the LDP configuration (I, P, P at 416x240, one slice per picture, SAO on)
   against HM's encode (tests/golden/ctu_ldp_rand.bin).
+- test_closed_ldp_row_slices_vs_hm: a closed LDP segment of 448x256 with one slice per CTU row (SliceMode 1,
+  SliceArgument 7: four slices per picture), SAO on: every CTU, finished picture and CABAC table equals
+  HM's encode (tests/golden/ctu_ldp_closed_slices.bin).  Each slice after the first is written with the
+  table the slice before it chose, as HM writes them (gop.ClosedSegments.write_slices).
 - test_closed_ra_stvssim_full_history: config 4 as an encode -- a closed RA segment decided with the
   stvssim encoder's active cost (HVX_RD_STVSSIM) over the segment's own history of originals and final
   reconstructions, up to the full 25 pictures (POC 28, coding index 26): every picture re-decided by the
@@ -116,6 +120,39 @@ def test_closed_ldp_segment_vs_hm(torch):
     torch.cuda.synchronize()
     bad = _compare_with_capture(g, kept.out, [0, 1, 2], 0, 28)
     assert not bad, bad[:6]
+
+
+@pytest.mark.gpu
+def test_closed_ldp_row_slices_vs_hm(torch):
+    from video_codecs_amd import cabac_init, gop, hvx
+    hvx.context()
+    g = gc.load("ctu_ldp_closed_slices.bin")
+    plan = gop.load_plan("ldp", 3)
+    finals, chains = {}, []
+
+    def finished(t, recs):
+        finals[plan[t].poc] = np.concatenate([x.cpu().numpy().reshape(-1) for x in recs[0]])
+    cs = gop.ClosedSegments(plan, 448, 256, [30], _capture_org_fn([g]), rows=1, on_finished=finished)
+    assert cs.nch == 4 and cs.cl == 7
+    kept = Kept(cs)
+    while cs.t < len(plan):
+        cs.step()
+        if cs.L == 0 and cs.last_slices is not None:  # the table each slice of the picture was written with
+            chains.append([int(x) for x in cs.last_slices[3][0]])
+    torch.cuda.synchronize()
+    bad = []
+    for pic in range(3):
+        first = int(g["pic_i32"][pic][hm_cases.P_FIRST_CTU])
+        ctus = np.stack([kept.out[(pic, 0, a)][0] for a in range(28)])
+        rec = np.stack([kept.out[(pic, 0, a)][1] for a in range(28)])
+        bad += [(pic,) + b[1:] for b in hm_cases.compare(g, [(pic, first, 28, 0)], (ctus, rec, None))]
+    psz = 448 * 256 * 3 // 2
+    for k, q in enumerate(int(p) for p in g["refpic_poc"]):
+        if not np.array_equal(finals[q], g["refpic"][k * psz:(k + 1) * psz]):
+            bad.append((q, "finished picture"))
+    want = [cabac_init.resolve_table(int(pi[hm_cases.P_SLICE_TYPE]), int(pi[hm_cases.P_CABAC_TABLE])) for pi in g["pic_i32"]]
+    assert not bad and cs.segs[0].tables == want, (bad[:6], cs.segs[0].tables, want, chains)
+    assert len(chains) == 3 and all(len(c) == 4 for c in chains)
 
 
 @pytest.mark.gpu

@@ -277,8 +277,12 @@ struct Enc {
 __shared__ hm::Enc hm_e;
 
 #ifdef HM_PROFILE
+// s_memtime is the shader clock of the XCD the wave runs on: a wave that the driver preempts and
+// restores elsewhere can read an earlier time at the end of a scope than at its start.  Such an
+// interval counts as 0 ticks (it was what wrapped the round-5 accumulators to ~1.8e19).
+__device__ __forceinline__ uint64_t hm_prof_dt(uint64_t t0, uint64_t t1) { return (int64_t)(t1 - t0) > 0 ? t1 - t0 : 0; }
 __device__ void hm_prof_add(int cat, uint64_t dt) {
-  hm_e.prof[0][cat] += dt;
+  hm_e.prof[0][cat] += (int64_t)dt > 0 ? dt : 0;
   hm_e.prof[1][cat] += 1;
 }
 #endif
@@ -312,13 +316,13 @@ struct ProfScope {
   uint64_t t0;
   __device__ __forceinline__ explicit ProfScope(int c) : cat(c), t0(__builtin_amdgcn_s_memtime()) {}
   __device__ __forceinline__ ~ProfScope() {
-    hm_e.prof[0][cat] += __builtin_amdgcn_s_memtime() - t0;
+    hm_e.prof[0][cat] += hm_prof_dt(t0, __builtin_amdgcn_s_memtime());
     hm_e.prof[1][cat] += 1;
   }
 };
 #define HM_PROF(c) ProfScope prof_scope_(c)
 #define HM_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#define HM_TADD(cat, v) (hm_e.prof[0][(cat)] += __builtin_amdgcn_s_memtime() - (v), hm_e.prof[1][(cat)] += 1)
+#define HM_TADD(cat, v) (hm_e.prof[0][(cat)] += hm_prof_dt((v), __builtin_amdgcn_s_memtime()), hm_e.prof[1][(cat)] += 1)
 #else
 #define HM_T0(v) ((void)0)
 #define HM_TADD(cat, v) ((void)0)

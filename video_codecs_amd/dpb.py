@@ -1,14 +1,16 @@
 """The writer rank's shared decoded-picture buffer.
 
-CTUs shard across GPUs by independent GOP segments (pictures), one set per rank.  After every
-decision launch each rank's reconstructed CTU windows of that launch (hvx_hm_compress's d_out_rec:
-per CTU the pre-loop-filter Y | Cb | Cr window, 6144 bytes) are gathered to rank 0 with ONE
-torch.distributed gather (RCCL over xGMI on the GPUs; gloo in the CPU tests) -- the shared DPB the
-writer rank assembles pictures in.  The gather is the only data-path collective of the path; a
-rank's own reference pictures for its segments are made locally (hvx_hm_finish_picture) and never
-cross xGMI.  It is asynchronous and the output buffers are double-buffered, so launch k+1 decides
-while launch k's windows move; a buffer is handed out again only after the gather that read it has
-completed.  Rank 0 keeps one buffer per rank.
+The multi-GPU path shards closed GOP segments across ranks (bench.closed_main, gop.ClosedSegments):
+every rank encodes its own segments -- disjoint frame indices -- with references its own loop made
+(hvx_hm_finish_picture + SAO on the device), so no reference picture and no decision input crosses
+xGMI.  What does cross is each finished picture: after a picture's deblocking and SAO
+(TEncGOP.cpp:1465, :1500) the rank's finished reconstructions of that POC (all its segments, the
+planes as TComPicYuv holds them before extension, Y | Cb | Cr per segment) are gathered to rank 0
+with ONE torch.distributed gather (RCCL over xGMI on the GPUs; gloo in the CPU tests) -- the shared
+DPB the writer rank outputs from.  It is the only data-path collective of the path.  The gather is
+asynchronous and the buffers are double-buffered, so picture t+1 decides while picture t moves; a
+buffer is handed out again only after the gather that read it has completed.  Rank 0 keeps one
+buffer per rank.
 """
 
 
@@ -24,7 +26,7 @@ class DpbGather:
         self.pending = [None] * nbuf
 
     def buffer(self):
-        """The output buffer of the current launch (waits for the gather that last read it)."""
+        """The output buffer of the current picture (waits for the gather that last read it)."""
         b = self.k % self.nbuf
         if self.pending[b] is not None:
             self.pending[b].wait()
@@ -32,7 +34,7 @@ class DpbGather:
         return self.recon[b]
 
     def send(self):
-        """Gather the current launch's windows to rank 0 (no-op on one rank) and advance; returns its buffer index."""
+        """Gather the current picture's finished planes to rank 0 (no-op on one rank) and advance; returns its buffer index."""
         import torch.distributed as dist
         b = self.k % self.nbuf
         if self.world > 1:

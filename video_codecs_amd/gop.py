@@ -224,6 +224,8 @@ class ClosedSegments:
         self.ctus_decided = 0
         self.launch_events = None      # a list: (picture, CTUs, (start, end) HIP events) per launch
         self.finished_log = None       # a list: every picture's loop() results (kept when set)
+        self.last_slices = None        # the last picture's slice writes: (bytes, results, capacity, tables used)
+        self.write_passes = 0
 
     # ---- picture set-up (TEncGOP / TEncSlice::initEncSlice) --------------------------------------
     def picture_params(self, s, t):
@@ -400,16 +402,26 @@ class ClosedSegments:
         return out
 
     def write_slices(self, sao):
-        """encodeSlice of every slice of picture t (hvx_hm_write_slices, one launch for all segments):
-        the slice data bytes per segment, and each segment's next cabac_init table
-        (determineCabacInitIdx over the last slice's final states and coded contexts)."""
+        """encodeSlice of every slice of picture t (hvx_hm_write_slices, all segments' slices per launch):
+        the slice data bytes per segment, and each segment's next cabac_init table.
+
+        HM writes a picture's slices one after another, and each encodeSlice ends with
+        determineCabacInitIdx (TEncSlice.cpp:1096-1099) over that slice's final states and coded
+        contexts; slice k > 0 is written with the table the slice before it chose (TEncGOP.cpp:1559
+        takes m_encCABACTableIdx for every slice header, TEncSbac::resetEntropy initialises from it)
+        while the decision used the previous picture's choice for all of them (TEncGOP.cpp:1246).
+        Here every slice is written at once with a guessed table (slice 0: the picture's table; slice
+        k > 0: what slice k - 1 chose in the previous pass) and, from the first slice whose guess was
+        wrong, the rest are written again -- one pass when the guesses hold, at most one per slice."""
         import torch
-        n_sl = len(self.segs) * self.nch
+        n_seg = len(self.segs)
+        n_sl = n_seg * self.nch
         cap = max(1 << 16, self.cl * 12288)
         out = torch.zeros(n_sl * cap, dtype=torch.uint8, device=self.device)
         sl = np.zeros(n_sl, hm.HM_SLICE)
         keep = []
-        for s in range(len(self.segs)):
+        st = self.plan[self.t].slice_type
+        for s in range(n_seg):
             coded_t = None
             en = [0, 0, 0]
             if sao is not None:
@@ -426,20 +438,40 @@ class ClosedSegments:
                 sl[k]["out"] = out.data_ptr() + k * cap
                 sl[k]["sao_enabled"] = en
                 sl[k]["sao_coded"] = coded_t.data_ptr() if coded_t is not None else 0
-                sl[k]["entry"]["st"] = self.cur[s]["entry"]
-        sl_t = torch.from_numpy(sl.view(np.uint8).reshape(-1).copy()).to(self.device)
-        res_t = torch.zeros(n_sl * hm.HM_SLICE_RESULT.itemsize, dtype=torch.uint8, device=self.device)
-        self.eng.write_slices_launch(sl_t, n_sl, res_t)
-        res = res_t.cpu().numpy().view(hm.HM_SLICE_RESULT)
-        assert (res["status"] == 0).all() and (res["n_bytes"] <= cap).all(), "hvx_hm_write_slices refused a slice"
+        used = [[self.cur[s]["table"]] * self.nch for s in range(n_seg)]   # the table each slice is written with
+        res = np.zeros(n_sl, hm.HM_SLICE_RESULT)
+        chosen = [[None] * self.nch for _ in range(n_seg)]                 # determineCabacInitIdx after each slice
+        todo = list(range(n_sl))
+        self.write_passes = 0
+        while todo:
+            for k in todo:
+                s, c = divmod(k, self.nch)
+                sl[k]["entry"]["st"] = cabac_init.slice_start_states(cabac_init.resolve_table(st, used[s][c]),
+                                                                     self.cur[s]["qp"])
+            sl_t = torch.from_numpy(sl[todo].view(np.uint8).reshape(-1).copy()).to(self.device)
+            res_t = torch.zeros(len(todo) * hm.HM_SLICE_RESULT.itemsize, dtype=torch.uint8, device=self.device)
+            self.eng.write_slices_launch(sl_t, len(todo), res_t)
+            r = res_t.cpu().numpy().view(hm.HM_SLICE_RESULT)
+            assert (r["status"] == 0).all() and (r["n_bytes"] <= cap).all(), "hvx_hm_write_slices refused a slice"
+            res[todo] = r
+            self.write_passes += 1
+            for k in todo:
+                s, c = divmod(k, self.nch)
+                chosen[s][c] = cabac_init.determine_cabac_init_idx(st, res[k]["states"][:202],
+                                                                   cabac_init.coded_flags(res[k]["coded"]),
+                                                                   self.cur[s]["qp"], self.eb)
+            again = []
+            for s in range(n_seg):
+                for c in range(1, self.nch):
+                    if used[s][c] != chosen[s][c - 1]:   # slices < c are final: rewrite c.. with new guesses
+                        for j in range(c, self.nch):
+                            used[s][j] = chosen[s][j - 1]
+                            again.append(s * self.nch + j)
+                        break
+            todo = again
         nbytes = []
         for s, seg in enumerate(self.segs):
-            r = res[s * self.nch:(s + 1) * self.nch]
-            # determineCabacInitIdx after the picture's last slice (TEncSlice.cpp:1096-1099): that slice's
-            # final states and the contexts it coded (resetEntropy -> initBuffer clears m_binsCoded)
-            seg.enc_table = cabac_init.determine_cabac_init_idx(self.plan[self.t].slice_type, r[-1]["states"][:202],
-                                                                cabac_init.coded_flags(r[-1]["coded"]),
-                                                                self.cur[s]["qp"], self.eb)
-            nbytes.append(int(r["n_bytes"].sum()))
-        self.last_slices = (out, res, cap)
+            seg.enc_table = chosen[s][-1]
+            nbytes.append(int(res[s * self.nch:(s + 1) * self.nch]["n_bytes"].sum()))
+        self.last_slices = (out, res, cap, used)
         return nbytes
