@@ -363,12 +363,21 @@ class ClosedWorkload:
 
     def workload(self):
         cs = self.cs
+        cost = ""
+        if cs.rd_metric == _abi_mod().RD_STVSSIM:
+            cost = ("; cost: the stvssim encoder's distortionstVSSIM over each segment's own device history (its "
+                    "originals and final reconstructions in coding order)")
         return ("%d closed %s segments (HM's %s structure: %s; %dx%d random 4:2:0 originals, %d CTU row(s) per slice: "
                 "%d chains) decided entirely on the device: every picture against the references its own segment's "
-                "loop made (deblocking + SAO + slice writer + cabac_init choice), %d CTUs per chain per launch" % (
+                "loop made (deblocking + SAO + slice writer + cabac_init choice), %d CTUs per chain per launch%s" % (
                     len(cs.segs), self.kind.upper(), "encoder_lowdelay_P_main" if self.kind == "ldp" else
                     "encoder_randomaccess_main", "POC " + ",".join(str(g.poc) for g in self.plan), self.W, self.H,
-                    cs.rows, len(cs.segs) * cs.nch, cs.ctus_step))
+                    cs.rows, len(cs.segs) * cs.nch, cs.ctus_step, cost))
+
+
+def _abi_mod():
+    from video_codecs_amd import _abi
+    return _abi
 
 
 class ClosedParity:

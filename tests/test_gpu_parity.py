@@ -545,59 +545,3 @@ def test_sao_decide_gpu(torch):
                                                           c["frac_lo"], c["slice_ctus"], c["test_off"])
         assert recon.cpu().numpy().tobytes() == o_recon.tobytes()
         assert float(tot.cpu().numpy()[0]) == o_tot
-
-
-@pytest.mark.gpu
-def test_hm_closed_loop_sao_gpu(torch):
-    """The whole reference loop of the LDP configuration on the device, SAO on (the reference cfg's
-    default; tests/golden/ctu_ldp_rand.bin, I + P + P pictures): each picture decided by
-    hvx_hm_compress against device-made references and collocated fields, then deblocked with
-    device-derived boundary strengths (hvx_hm_finish_picture), SAO statistics / RD decision / offsets
-    on the device (hm.sao_picture: hvx_sao_stats, hvx_sao_decide, hvx_sao_apply, decidePicParams'
-    SAO-off rates carried picture to picture), and written as the next pictures' reference planes.
-    Every CTU of every picture bit-exact vs HM, and every device reference equals the reference
-    picture HM handed the next pictures (deblocked + SAO)."""
-    from video_codecs_amd import _abi, hm
-    g = gc.load("ctu_ldp_rand.bin")
-    g["_row_slices"] = False
-    eb = _abi.load_entropy_bits()
-    layers = {0: 0, 1: 2, 2: 1, 3: 2}  # encoder_lowdelay_P_main.cfg GOP positions (POC 0: the I picture)
-    refs_by_poc, cols_by_poc = {}, {}
-    rates = np.zeros((3, 7))
-    n_sao_new = 0
-    for pic, pi in enumerate(g["pic_i32"]):
-        poc, w, h = int(pi[hm_cases.P_POC]), int(pi[hm_cases.P_W]), int(pi[hm_cases.P_H])
-        first, n = int(pi[hm_cases.P_FIRST_CTU]), int(pi[hm_cases.P_NCTU])
-        psz = w * h * 3 // 2
-        org = hm_cases.yuv_split(g["org"][pic * psz:(pic + 1) * psz], w, h)
-        params = hm_cases.pic_params(pi, g["pic_f64"][pic])
-        refs = [refs_by_poc[int(p)] for p in g["refpic_poc"] if int(p) in refs_by_poc]
-        col = cols_by_poc[int(pi[hm_cases.P_COL_POC])] if int(pi[hm_cases.P_COL_VALID]) else None
-        dp = hm.DevicePicture(org, refs, params, eb, col_field=col)
-        job = np.zeros(1, hm.HM_JOB)
-        job["pic"], job["first_ctu"], job["n_ctus"], job["chained"], job["out"] = 0, 0, n, 1, 0
-        job["entry"]["st"] = g["ctu_states"][first]
-        job["entry"]["frac"] = np.uint64(int(g["ctu_frac"][first]))
-        job["int2n"] = g["ctu_int2n"][first]
-        job["slice_start"], job["slice_end"] = 0, n - 1
-        out = hm.Engine([dp]).compress(job, n)
-        bad = hm_cases.compare(g, [(pic, first, n, 0)], out)
-        assert not bad, (poc, bad[:4])
-        _, col_t = hm.finish_picture(dp, _abi.deblock_params(w, h), col_field=True)
-        st0 = g["ctu_states"][first]  # the slice-start states (resetEntropy), as SAO's picture-start coder has them
-        rates, coded, _, _ = hm.sao_picture(dp, layers[poc], rates, int(pi[hm_cases.P_SLICE_TYPE]), int(pi[hm_cases.P_QP]),
-                                            sao_states=(st0[hm.SAO_CTX_MERGE], st0[hm.SAO_CTX_TYPE]))
-        n_sao_new += int((coded[:, :, 0] == 1).sum())
-        ref = hm.DeviceFrame.blank(w, h)
-        hm.finish_picture(dp, None, ref_frame=ref)
-        torch.cuda.synchronize()
-        refs_by_poc[poc], cols_by_poc[poc] = ref, col_t
-        if poc in list(g["refpic_poc"]):
-            k = list(g["refpic_poc"]).index(poc)
-            want = hm_cases.yuv_split(g["refpic"][k * psz:(k + 1) * psz], w, h)
-            y8, y16, cb16, cr16 = (t.cpu().numpy() for t in ref.planes())
-            m8 = hm.DeviceFrame.M8
-            np.testing.assert_array_equal(y8[m8:m8 + h, m8:m8 + w], want[0], err_msg="poc %d Y" % poc)
-            np.testing.assert_array_equal(cb16[40:40 + h // 2, 40:40 + w // 2], want[1].astype(np.int16))
-            np.testing.assert_array_equal(cr16[40:40 + h // 2, 40:40 + w // 2], want[2].astype(np.int16))
-    assert len(refs_by_poc) == 3

@@ -224,8 +224,8 @@ class ClosedSegments:
         self.ctus_decided = 0
         self.launch_events = None      # a list: (picture, CTUs, (start, end) HIP events) per launch
         self.finished_log = None       # a list: every picture's loop() results (kept when set)
-        self.last_slices = None        # the last picture's slice writes: (bytes, results, capacity, tables used)
-        self.write_passes = 0
+        self.last_slices = None        # the last picture's slice writes: (bytes, results, capacity, tables
+                                       # each slice was written with, the result index of each slice)
 
     # ---- picture set-up (TEncGOP / TEncSlice::initEncSlice) --------------------------------------
     def picture_params(self, s, t):
@@ -402,28 +402,35 @@ class ClosedSegments:
         return out
 
     def write_slices(self, sao):
-        """encodeSlice of every slice of picture t (hvx_hm_write_slices, all segments' slices per launch):
+        """encodeSlice of every slice of picture t (hvx_hm_write_slices, one launch for all segments):
         the slice data bytes per segment, and each segment's next cabac_init table.
 
         HM writes a picture's slices one after another, and each encodeSlice ends with
         determineCabacInitIdx (TEncSlice.cpp:1096-1099) over that slice's final states and coded
         contexts; slice k > 0 is written with the table the slice before it chose (TEncGOP.cpp:1559
         takes m_encCABACTableIdx for every slice header, TEncSbac::resetEntropy initialises from it)
-        while the decision used the previous picture's choice for all of them (TEncGOP.cpp:1246).
-        Here every slice is written at once with a guessed table (slice 0: the picture's table; slice
-        k > 0: what slice k - 1 chose in the previous pass) and, from the first slice whose guess was
-        wrong, the rest are written again -- one pass when the guesses hold, at most one per slice."""
+        while the decision used the previous picture's choice for all of them (TEncGOP.cpp:1246).  A
+        slice's data depends only on its own CTUs and the table it starts from, and a P / B slice can
+        start from two tables (B's or P's), so every slice after the first is written from both in the
+        same launch and the chain of choices is then followed on the host: the first slice from the
+        picture's table, each next one from what the slice before it chose."""
         import torch
         n_seg = len(self.segs)
-        n_sl = n_seg * self.nch
-        cap = max(1 << 16, self.cl * 12288)
-        out = torch.zeros(n_sl * cap, dtype=torch.uint8, device=self.device)
-        sl = np.zeros(n_sl, hm.HM_SLICE)
-        keep = []
         st = self.plan[self.t].slice_type
+        cands = [cabac_init.B_SLICE, cabac_init.P_SLICE] if st != I_SLICE else [I_SLICE]
+        jobs = []  # (segment, slice, table)
+        for s in range(n_seg):
+            for c in range(self.nch):
+                for tab in ([self.cur[s]["table"]] if c == 0 else cands):
+                    jobs.append((s, c, tab))
+        n = len(jobs)
+        cap = max(1 << 16, self.cl * 12288)
+        out = torch.zeros(n * cap, dtype=torch.uint8, device=self.device)
+        sl = np.zeros(n, hm.HM_SLICE)
+        keep, en, coded = [], [], []
         for s in range(n_seg):
             coded_t = None
-            en = [0, 0, 0]
+            e3 = [0, 0, 0]
             if sao is not None:
                 coded_t = torch.from_numpy(np.ascontiguousarray(sao[s][1], np.int32)).to(self.device)
                 keep.append(coded_t)
@@ -431,47 +438,34 @@ class ClosedSegments:
                 # of decidePicParams disabled only one chroma component, Cr's offsets are applied but
                 # not written
                 e = [int(x) for x in sao[s][3]]
-                en = [e[0], e[1], e[1]]
-            for c in range(self.nch):
-                k = s * self.nch + c
-                sl[k]["pic"], sl[k]["first_ctu"], sl[k]["n_ctus"], sl[k]["out_cap"] = s, c * self.cl, self.cl, cap
-                sl[k]["out"] = out.data_ptr() + k * cap
-                sl[k]["sao_enabled"] = en
-                sl[k]["sao_coded"] = coded_t.data_ptr() if coded_t is not None else 0
-        used = [[self.cur[s]["table"]] * self.nch for s in range(n_seg)]   # the table each slice is written with
-        res = np.zeros(n_sl, hm.HM_SLICE_RESULT)
-        chosen = [[None] * self.nch for _ in range(n_seg)]                 # determineCabacInitIdx after each slice
-        todo = list(range(n_sl))
-        self.write_passes = 0
-        while todo:
-            for k in todo:
-                s, c = divmod(k, self.nch)
-                sl[k]["entry"]["st"] = cabac_init.slice_start_states(cabac_init.resolve_table(st, used[s][c]),
-                                                                     self.cur[s]["qp"])
-            sl_t = torch.from_numpy(sl[todo].view(np.uint8).reshape(-1).copy()).to(self.device)
-            res_t = torch.zeros(len(todo) * hm.HM_SLICE_RESULT.itemsize, dtype=torch.uint8, device=self.device)
-            self.eng.write_slices_launch(sl_t, len(todo), res_t)
-            r = res_t.cpu().numpy().view(hm.HM_SLICE_RESULT)
-            assert (r["status"] == 0).all() and (r["n_bytes"] <= cap).all(), "hvx_hm_write_slices refused a slice"
-            res[todo] = r
-            self.write_passes += 1
-            for k in todo:
-                s, c = divmod(k, self.nch)
-                chosen[s][c] = cabac_init.determine_cabac_init_idx(st, res[k]["states"][:202],
-                                                                   cabac_init.coded_flags(res[k]["coded"]),
-                                                                   self.cur[s]["qp"], self.eb)
-            again = []
-            for s in range(n_seg):
-                for c in range(1, self.nch):
-                    if used[s][c] != chosen[s][c - 1]:   # slices < c are final: rewrite c.. with new guesses
-                        for j in range(c, self.nch):
-                            used[s][j] = chosen[s][j - 1]
-                            again.append(s * self.nch + j)
-                        break
-            todo = again
-        nbytes = []
+                e3 = [e[0], e[1], e[1]]
+            en.append(e3)
+            coded.append(coded_t.data_ptr() if coded_t is not None else 0)
+        for k, (s, c, tab) in enumerate(jobs):
+            sl[k]["pic"], sl[k]["first_ctu"], sl[k]["n_ctus"], sl[k]["out_cap"] = s, c * self.cl, self.cl, cap
+            sl[k]["out"] = out.data_ptr() + k * cap
+            sl[k]["sao_enabled"] = en[s]
+            sl[k]["sao_coded"] = coded[s]
+            sl[k]["entry"]["st"] = cabac_init.slice_start_states(cabac_init.resolve_table(st, tab), self.cur[s]["qp"])
+        sl_t = torch.from_numpy(sl.view(np.uint8).reshape(-1).copy()).to(self.device)
+        res_t = torch.zeros(n * hm.HM_SLICE_RESULT.itemsize, dtype=torch.uint8, device=self.device)
+        self.eng.write_slices_launch(sl_t, n, res_t)
+        res = res_t.cpu().numpy().view(hm.HM_SLICE_RESULT)
+        assert (res["status"] == 0).all() and (res["n_bytes"] <= cap).all(), "hvx_hm_write_slices refused a slice"
+        at = {j: k for k, j in enumerate(jobs)}
+        nbytes, used, final = [], [], []
         for s, seg in enumerate(self.segs):
-            seg.enc_table = chosen[s][-1]
-            nbytes.append(int(res[s * self.nch:(s + 1) * self.nch]["n_bytes"].sum()))
-        self.last_slices = (out, res, cap, used)
+            tab, tabs, nb, ks = self.cur[s]["table"], [], 0, []
+            for c in range(self.nch):
+                k = at[(s, c, tab if c == 0 else cabac_init.resolve_table(st, tab))]
+                tabs.append(tab)
+                ks.append(k)
+                nb += int(res[k]["n_bytes"])
+                tab = cabac_init.determine_cabac_init_idx(st, res[k]["states"][:202], cabac_init.coded_flags(res[k]["coded"]),
+                                                          self.cur[s]["qp"], self.eb)
+            seg.enc_table = tab
+            nbytes.append(nb)
+            used.append(tabs)
+            final.append(ks)
+        self.last_slices = (out, res, cap, used, final)
         return nbytes
