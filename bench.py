@@ -791,6 +791,17 @@ def closed_main(args, rank, world, device="cuda", segments_cls=None, size=(1920,
     elapsed = timed_steps(step, args.steps, args.warmup, world, device, sync,
                           before=lambda: marks.__setitem__("first", len(work.cs.launch_events)))
     sec, ctus, byt = work.launch_seconds(marks["first"])
+    # per picture of the timed launches: the decision launches' HIP-event time and CTUs (rank 0's)
+    per = {}
+    for t, n, (a, b) in work.cs.launch_events[marks["first"]:]:
+        d = per.setdefault(t, [0, 0.0, 0])
+        d[0] += 1
+        d[1] += a.elapsed_time(b) * 1e-3
+        d[2] += n
+    work.timed_pictures = [{"poc": work.plan[t].poc, "slice": "IPB"[(2, 1, 0).index(work.plan[t].slice_type)],
+                            "refs": len(work.plan[t].ref_pocs()), "launches": d[0], "ctus": d[2],
+                            "decision_s": round(d[1], 3), "decision_ctus_per_s": round(d[2] / d[1], 1)}
+                           for t, d in sorted(per.items())]
     own, gathered = dpb.last()
     dpb_ok = bool(torch.equal(gathered[0], own)) if gathered is not None else None
     return work, elapsed, sec, ctus, byt, dpb_ok, len(work.gathered)
@@ -855,10 +866,13 @@ def main():
                               "(deblocked + SAO) picture is gathered to rank 0's DPB (RCCL over xGMI)",
                   "resolution": f"{W}x{H}", "segments_per_gpu": len(work.cs.segs),
                   "slice_chains_per_gpu": len(work.cs.segs) * work.cs.nch, "ctus_per_chain_per_step": work.cs.ctus_step,
-                  "pictures": [dict(p) for p in work.cs.log], "parallelism": f"closed segments x{world}",
+                  "pictures": [dict(p) for p in work.cs.log], "timed_pictures": work.timed_pictures,
+                  "parallelism": f"closed segments x{world}",
                   "dpb": "each finished picture of every segment gathered to rank 0 (%d pictures x %d segments per "
                          "rank)" % (n_gathered, len(work.cs.segs)) if world > 1 else "local",
-                  "n1_comparable": "the N=1 line's config5_closed_segments figure (the same per-GPU workload)"}
+                  "n1_comparable": "the N=1 line's config5_closed_segments figure (the same per-GPU workload; compare "
+                                   "timed_pictures' per-POC rates with its pictures' -- the reference count grows "
+                                   "with the POC)"}
         data = ("synthetic: splitmix64 uniform random 8-bit 4:2:0 originals made on the device (BASELINE.md sec. 3), "
                 "frame indices disjoint per segment and rank; references made by each segment's own loop")
     if rank == 0:
