@@ -148,3 +148,13 @@ for q in 27 37; do
 done
 # HM's slice set-up of closed LDP / RA segments (tests/golden/gop_plans.json)
 oracle/gen_gop_plans.sh
+# closed segments with one slice per CTU row (gop.ClosedSegments' per-slice cabac_init chain): LDP
+# 448x256 (four slices per picture, QP 30) and RA 192x128 (I + one GOP8, two slices per picture, QP 32)
+python3 oracle/make_yuv.py texture 448 256 3 "$TMP/tex448.yuv"
+HVX_CAPTURE="$TMP/cu.bin" $ORC/TAppEncoder_cucap -c $CFG/encoder_lowdelay_P_main.cfg -i "$TMP/tex448.yuv" -wdt 448 -hgt 256 \
+  -fr 30 -f 3 -q 30 --SliceMode=1 --SliceArgument=7 -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+python3 oracle/compact_ctu.py "$TMP/cu.bin" tests/golden/ctu_ldp_closed_slices.bin
+python3 oracle/make_yuv.py texture 192 128 9 "$TMP/tex192.yuv"
+HVX_CAPTURE="$TMP/cu.bin" $ORC/TAppEncoder_cucap -c $CFG/encoder_randomaccess_main.cfg -i "$TMP/tex192.yuv" -wdt 192 -hgt 128 \
+  -fr 30 -f 9 -q 32 --SliceMode=1 --SliceArgument=3 -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+python3 oracle/compact_ctu.py "$TMP/cu.bin" tests/golden/ctu_ra_closed_slices.bin

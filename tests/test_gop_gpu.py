@@ -7,10 +7,11 @@
   YUV (tests/golden/ctu_ra_closed_q*.bin), and so does every picture's CABAC initialisation table.
 - test_closed_ldp_segment_vs_hm: the LDP configuration (I, P, P at 416x240, one slice per picture, SAO on)
   against HM's encode (tests/golden/ctu_ldp_rand.bin).
-- test_closed_ldp_row_slices_vs_hm: a closed LDP segment of 448x256 with one slice per CTU row (SliceMode 1,
-  SliceArgument 7: four slices per picture), SAO on: every CTU, finished picture and CABAC table equals
-  HM's encode (tests/golden/ctu_ldp_closed_slices.bin).  Each slice after the first is written with the
-  table the slice before it chose, as HM writes them (gop.ClosedSegments.write_slices).
+- test_closed_ldp_row_slices_vs_hm / test_closed_ra_row_slices_vs_hm: closed LDP (448x256, four slices
+  per picture) and RA (192x128, I + GOP8, two slices per picture) segments with one slice per CTU row
+  (SliceMode 1), SAO on: every CTU, finished picture and CABAC table equals HM's encode
+  (tests/golden/ctu_{ldp,ra}_closed_slices.bin).  Each slice after the first is written with the table
+  the slice before it chose, as HM writes them (gop.ClosedSegments.write_slices).
 - test_closed_ra_stvssim_full_history: config 4 as an encode -- a closed RA segment decided with the
   stvssim encoder's active cost (HVX_RD_STVSSIM) over the segment's own history of originals and final
   reconstructions, up to the full 25 pictures (POC 28, coding index 26): every picture re-decided by the
@@ -122,37 +123,50 @@ def test_closed_ldp_segment_vs_hm(torch):
     assert not bad, bad[:6]
 
 
-@pytest.mark.gpu
-def test_closed_ldp_row_slices_vs_hm(torch):
+def _closed_row_slices(torch, name, kind, W, H, qp):
+    """A closed segment with one slice per CTU row against HM's encode of the same YUV (capture `name`):
+    every CTU, finished picture and CABAC table; returns the tables each picture's slices were written with."""
     from video_codecs_amd import cabac_init, gop, hvx
     hvx.context()
-    g = gc.load("ctu_ldp_closed_slices.bin")
-    plan = gop.load_plan("ldp", 3)
+    g = gc.load(name)
+    n_pic = g["pic_i32"].shape[0]
+    plan = gop.load_plan(kind, n_pic)
     finals, chains = {}, []
 
     def finished(t, recs):
         finals[plan[t].poc] = np.concatenate([x.cpu().numpy().reshape(-1) for x in recs[0]])
-    cs = gop.ClosedSegments(plan, 448, 256, [30], _capture_org_fn([g]), rows=1, on_finished=finished)
-    assert cs.nch == 4 and cs.cl == 7
+    cs = gop.ClosedSegments(plan, W, H, [qp], _capture_org_fn([g]), rows=1, on_finished=finished)
+    assert cs.nch == H // 64 and cs.cl == W // 64
     kept = Kept(cs)
     while cs.t < len(plan):
         cs.step()
         if cs.L == 0 and cs.last_slices is not None:  # the table each slice of the picture was written with
             chains.append([int(x) for x in cs.last_slices[3][0]])
     torch.cuda.synchronize()
-    bad = []
-    for pic in range(3):
-        first = int(g["pic_i32"][pic][hm_cases.P_FIRST_CTU])
-        ctus = np.stack([kept.out[(pic, 0, a)][0] for a in range(28)])
-        rec = np.stack([kept.out[(pic, 0, a)][1] for a in range(28)])
-        bad += [(pic,) + b[1:] for b in hm_cases.compare(g, [(pic, first, 28, 0)], (ctus, rec, None))]
-    psz = 448 * 256 * 3 // 2
+    pocs = [p.poc for p in plan]
+    t_of_pic = [pocs.index(int(pi[hm_cases.P_POC])) for pi in g["pic_i32"]]
+    bad = _compare_with_capture(g, kept.out, t_of_pic, 0, cs.nch * cs.cl)
+    psz = W * H * 3 // 2
     for k, q in enumerate(int(p) for p in g["refpic_poc"]):
         if not np.array_equal(finals[q], g["refpic"][k * psz:(k + 1) * psz]):
-            bad.append((q, "finished picture"))
+            bad.append((0, q, "finished picture"))
     want = [cabac_init.resolve_table(int(pi[hm_cases.P_SLICE_TYPE]), int(pi[hm_cases.P_CABAC_TABLE])) for pi in g["pic_i32"]]
-    assert not bad and cs.segs[0].tables == want, (bad[:6], cs.segs[0].tables, want, chains)
-    assert len(chains) == 3 and all(len(c) == 4 for c in chains)
+    got = [cs.segs[0].tables[t] for t in t_of_pic]
+    assert not bad and got == want, (bad[:6], got, want, chains)
+    assert len(chains) == n_pic and all(len(c) == cs.nch for c in chains)
+    return chains
+
+
+@pytest.mark.gpu
+def test_closed_ldp_row_slices_vs_hm(torch):
+    _closed_row_slices(torch, "ctu_ldp_closed_slices.bin", "ldp", 448, 256, 30)
+
+
+@pytest.mark.gpu
+def test_closed_ra_row_slices_vs_hm(torch):
+    """RA (I + one GOP8, B slices) at 192x128 with two row slices per picture, QP 32
+    (tests/golden/ctu_ra_closed_slices.bin)."""
+    _closed_row_slices(torch, "ctu_ra_closed_slices.bin", "ra", 192, 128, 32)
 
 
 @pytest.mark.gpu
