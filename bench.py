@@ -103,7 +103,7 @@ def timed_steps(step, steps, warmup, world, device, sync, before=None):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if dist.get_backend() != "gloo" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
@@ -816,8 +816,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local_rank)
+        # RCCL over xGMI; HVX_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU
+        dist.init_process_group(os.environ.get("HVX_DIST_BACKEND", "nccl"), init_method="env://")
+    torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
     from video_codecs_amd import hvx
     hvx.context()
     kind = args.workload if args.workload != "auto" else ("closed" if world > 1 else "steady")

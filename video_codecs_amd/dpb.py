@@ -37,7 +37,15 @@ class DpbGather:
         """Gather the current picture's finished planes to rank 0 (no-op on one rank) and advance; returns its buffer index."""
         import torch.distributed as dist
         b = self.k % self.nbuf
-        if self.world > 1:
+        if self.world > 1 and dist.get_backend() == "gloo" and self.recon[b].is_cuda:
+            # gloo gathers host tensors only (the rehearsal of several ranks on one GPU): staged, synchronous
+            got = [self.recon[b].new_empty(self.recon[b].shape, device="cpu") for _ in range(self.world)] \
+                if self.rank == 0 else None
+            dist.gather(self.recon[b].cpu(), got, dst=0)
+            if self.rank == 0:
+                for r in range(self.world):
+                    self.dpb[b][r].copy_(got[r])
+        elif self.world > 1:
             self.pending[b] = dist.gather(self.recon[b], self.dpb[b] if self.rank == 0 else None, dst=0,
                                           async_op=True)
         self.k += 1
