@@ -47,12 +47,7 @@ static __global__ __launch_bounds__(64) void k_hm_write_slices(const hvx_hm_pict
   State *S = (State *)(state_base + (size_t)jid * state_bytes);
   copy_words(&hm_e.P, &pics[j.pic], (int)sizeof(hvx_hm_picture));
   wsync();
-  for (int i = l; i < 128; i += 64) {
-    hm_e.eb[i] = hm_e.P.entropy_bits ? hm_e.P.entropy_bits[i] : 0;
-    const int p = i >> 1, mps = i & 1;
-    hm_e.next[i * 2 + mps] = (uint8_t)(((p < 62 ? p + 1 : p) << 1) | mps);
-    hm_e.next[i * 2 + (mps ^ 1)] = (uint8_t)((cab::kTransIdxLps[p] << 1) | (p == 0 ? mps ^ 1 : mps));
-  }
+  hm_fill_pk(hm_e.P.entropy_bits, l);
   hm_e.S = S;
   if (l < 4) hm_e.dbg[l] = 0;
   hm_e.stage = 0;

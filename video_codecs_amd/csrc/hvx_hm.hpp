@@ -250,8 +250,9 @@ struct Enc {
   hvx_estbits est;
   uint32_t est_key;      // (w | h << 8 | ch << 16) + 1 of the last estimate_bit (0: none this CTU)
   uint32_t est_st[38];   // its coder's context states 28 .. 179 (every byte estBit reads)
-  int32_t eb[128];
-  uint8_t next[256];
+  // one LDS word per (CABAC state q, bin v), entry 2q + v: the next state (ContextModel::update) in
+  // bits 24..31, ContextModel::m_entropyBits[q ^ v] in bits 0..23 -- a counted bin is one LDS read
+  uint32_t pk[256];
   uint16_t scan[256];    // the current TU's scan tables (TUs up to 16x16), staged by tu_fwd_l
   uint8_t scan_cg[16];
   uint32_t avail[4];
@@ -276,6 +277,16 @@ struct Enc {
 
 __shared__ hm::Enc hm_e;
 
+// Enc.pk from ContextModel::m_entropyBits (eb: 128 int32, or nullptr: zeros) and the state
+// transitions of ContextModel::updateMPS / updateLPS; lane l fills entries l, l + 64, l + 128, l + 192
+__device__ __forceinline__ void hm_fill_pk(const int32_t *eb, int l) {
+  for (int j = l; j < 256; j += 64) {
+    const int q = j >> 1, v = j & 1, p = q >> 1, mps = q & 1;
+    const int ns = v == mps ? (((p < 62 ? p + 1 : p) << 1) | mps) : ((cab::kTransIdxLps[p] << 1) | (p == 0 ? mps ^ 1 : mps));
+    hm_e.pk[j] = ((uint32_t)ns << 24) | ((eb ? (uint32_t)eb[q ^ v] : 0u) & 0xffffffu);
+  }
+}
+
 #ifdef HM_PROFILE
 // s_memtime is the shader clock of the XCD the wave runs on: a wave that the driver preempts and
 // restores elsewhere can read an earlier time at the end of a scope than at its start.  Such an
@@ -289,6 +300,9 @@ __device__ void hm_prof_add(int cat, uint64_t dt) {
 
 namespace hm {
 #define E hm_e
+// the packed table's two halves (Enc.pk)
+__device__ __forceinline__ uint32_t ebits(int x) { return E.pk[2 * x] & 0xffffffu; }
+__device__ __forceinline__ int nstate(int j) { return (int)(E.pk[j] >> 24); }
 enum { Y_ORIG, Y_PRED_BEST, Y_PRED_TEMP, Y_RESI_BEST, Y_RESI_TEMP, Y_RECO_BEST, Y_RECO_TEMP };
 __device__ __forceinline__ Yuv *YB(int kind, int d) { return &E.S->yuv[E.yi[kind][d]]; }
 __device__ __forceinline__ Cu *BEST(int d) { return &E.S->cu[E.best[d]]; }
@@ -371,11 +385,12 @@ struct TuSlot {
 __device__ __forceinline__ void cbin(int ctx, int v) {
   Coder &c = E.cod[E.cur];
   const int s = c.st[ctx];
-  c.frac += (uint32_t)E.eb[s ^ v];
-  c.st[ctx] = E.next[s * 2 + v];
+  const uint32_t pv = E.pk[s * 2 + v];
+  c.frac += pv & 0xffffffu;
+  c.st[ctx] = (uint8_t)(pv >> 24);
 }
 __device__ __forceinline__ void cep(int n) { E.cod[E.cur].frac += 32768ull * (uint32_t)n; }
-__device__ __forceinline__ void ctrm(int v) { E.cod[E.cur].frac += (uint32_t)E.eb[126 ^ v]; }
+__device__ __forceinline__ void ctrm(int v) { E.cod[E.cur].frac += ebits(126 ^ v); }
 __device__ __forceinline__ void reset_bits() { E.cod[E.cur].frac &= 32767; }
 __device__ __forceinline__ uint32_t written_bits() { return (uint32_t)(E.cod[E.cur].frac >> 15); }
 __device__ __forceinline__ void cload(int dst, int src) {
@@ -400,8 +415,9 @@ struct CoderLane {
   __device__ __forceinline__ void bin(int row, int v) {
     uint8_t &s = st[uni(row) + cab::kCtxLo];
     const int q = uni(s), bv = uni(v);
-    frac += (uint32_t)uni(E.eb[q ^ bv]);
-    s = (uint8_t)uni(E.next[q * 2 + bv]);
+    const uint32_t pv = (uint32_t)uni((int)E.pk[q * 2 + bv]);
+    frac += pv & 0xffffffu;
+    s = (uint8_t)(pv >> 24);
   }
   __device__ __forceinline__ void ep(int n) { frac += 32768ull * (uint32_t)n; }
   __device__ __forceinline__ void ep_bits(uint32_t, int n) { ep(n); }
@@ -1078,93 +1094,6 @@ __device__ void tu_desc(const Cu *cu, const Tu &t, int comp) {
   d.pps_tskip = 1;
   d.lambda = lam;
 }
-// The coefficient contexts of one coder held in registers for the duration of a TU's
-// codeCoeffNxN: row r (model kCtxLo + r) in lane r & 63 of VGPR r >> 6, the entropy-bit table
-// and transIdxLPS likewise; every bin is a few v_readlane / v_writelane on a wave-uniform
-// index instead of three dependent LDS round trips (ContextModel::update, TEncBinCABACCounter).
-struct RegCoder {
-  int r0, r1, r2, eb0, eb1, lps;
-  uint64_t frac;
-  __device__ __forceinline__ void load(const uint8_t *st) {
-    const int l = lid();
-    r0 = st[cab::kCtxLo + l];
-    r1 = st[cab::kCtxLo + 64 + l];
-    r2 = l < cab::kRows - 128 ? st[cab::kCtxLo + 128 + l] : 0;
-    eb0 = E.eb[l];
-    eb1 = E.eb[64 + l];
-    lps = cab::kTransIdxLps[l];
-    frac = 0;
-  }
-  __device__ __forceinline__ void store(uint8_t *st) const {
-    const int l = lid();
-    st[cab::kCtxLo + l] = (uint8_t)r0;
-    st[cab::kCtxLo + 64 + l] = (uint8_t)r1;
-    if (l < cab::kRows - 128) st[cab::kCtxLo + 128 + l] = (uint8_t)r2;
-  }
-  __device__ __forceinline__ void bin(int row, int v) {
-    row = __builtin_amdgcn_readfirstlane(row);
-    v = __builtin_amdgcn_readfirstlane(v);
-    const int k = row >> 6, ln = row & 63;
-    const int st = k == 0 ? __builtin_amdgcn_readlane(r0, ln) : k == 1 ? __builtin_amdgcn_readlane(r1, ln)
-                                                                        : __builtin_amdgcn_readlane(r2, ln);
-    const int i = st ^ v;
-    frac += (uint32_t)(i < 64 ? __builtin_amdgcn_readlane(eb0, i) : __builtin_amdgcn_readlane(eb1, i - 64));
-    const int p = st >> 1, mps = st & 1;
-    const int ns = v == mps ? (((p < 62 ? p + 1 : p) << 1) | mps)
-                            : ((__builtin_amdgcn_readlane(lps, p) << 1) | (p == 0 ? mps ^ 1 : mps));
-    const bool mine = lid() == ln;  // v_writelane as a compare + select
-    if (k == 0) r0 = mine ? ns : r0;
-    else if (k == 1) r1 = mine ? ns : r1;
-    else r2 = mine ? ns : r2;
-  }
-  __device__ __forceinline__ void ep(int n) { frac += 32768ull * (uint32_t)n; }
-  __device__ __forceinline__ void ep_bits(uint32_t, int n) { ep(n); }
-  __device__ __forceinline__ void eps(uint32_t, int n) { ep(n); }
-  __device__ __forceinline__ void esc(uint32_t symbol, int r, bool limited, int max_log2) {
-    ep(cab::remain_bins(symbol, r, limited, max_log2));
-  }
-};
-
-// The bin counter of the coefficient walk with everything a bin touches in lane slices of four
-// VGPRs instead of LDS: the context states of rows 40..187 (the coefficient syntax's, 4 per dword:
-// dword k of the coder in lane k - kMemoDw0), the fractional-bit table E.eb (entry 2p + b in lane p
-// of eb[b]) and the transition table E.next (entries 4p..4p+3 in lane p).  A bin is then three
-// v_readlane's, scalar arithmetic and one lane select -- no dependent LDS round trips on the chain.
-struct RegWalk {
-  int stv, eb0, eb1, nx;
-  uint64_t frac;
-  __device__ __forceinline__ void load(const uint8_t *st) {
-    const int l = lid();
-    stv = l < kMemoDw ? (int)reinterpret_cast<const uint32_t *>(st)[kMemoDw0 + l] : 0;
-    eb0 = E.eb[2 * l];
-    eb1 = E.eb[2 * l + 1];
-    nx = (int)reinterpret_cast<const uint32_t *>(E.next)[l];
-    frac = 0;
-  }
-  __device__ __forceinline__ void store(uint8_t *st) const {
-    const int l = lid();
-    if (l < kMemoDw) reinterpret_cast<uint32_t *>(st)[kMemoDw0 + l] = (uint32_t)stv;
-  }
-  __device__ __forceinline__ void bin(int row, int v) {
-    const int a = __builtin_amdgcn_readfirstlane(row) + cab::kCtxLo;
-    v = __builtin_amdgcn_readfirstlane(v);
-    const int k = (a >> 2) - kMemoDw0, sh = (a & 3) * 8;
-    const uint32_t dw = (uint32_t)__builtin_amdgcn_readlane(stv, k);
-    const int s = (int)((dw >> sh) & 0xffu), p = s >> 1, mps = s & 1;
-    const int e0 = __builtin_amdgcn_readlane(eb0, p), e1 = __builtin_amdgcn_readlane(eb1, p);
-    frac += (uint32_t)((mps ^ v) ? e1 : e0);
-    const uint32_t ns = ((uint32_t)__builtin_amdgcn_readlane(nx, p) >> (8 * ((mps << 1) | v))) & 0xffu;
-    const int nd = (int)((dw & ~(0xffu << sh)) | (ns << sh));
-    stv = lid() == k ? nd : stv;  // v_writelane as a compare + select
-  }
-  __device__ __forceinline__ void ep(int n) { frac += 32768ull * (uint32_t)n; }
-  __device__ __forceinline__ void ep_bits(uint32_t, int n) { ep(n); }
-  __device__ __forceinline__ void eps(uint32_t, int n) { ep(n); }
-  __device__ __forceinline__ void esc(uint32_t symbol, int r, bool limited, int max_log2) {
-    ep(cab::remain_bins(symbol, r, limited, max_log2));
-  }
-};
-
 // the scan geometry of a TU (cab::ScanTables' values): the CG scan staged in LDS for every size;
 // raster positions and packed significance contexts staged in LDS up to 16x16, while a 32x32 TU
 // (big) reads its rasters from the constant scan table and derives the contexts per lane
@@ -1264,8 +1193,9 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
         const int sig = (int)((m16 >> pin) & 1u);
         if (pin > 0 || sub == 0 || nnz) {
           const int row = __builtin_amdgcn_readlane(row_l, pin), q = __builtin_amdgcn_readlane(q_l, pin);
-          L.frac += (uint32_t)E.eb[q ^ sig];
-          const int ns = E.next[q * 2 + sig];
+          const uint32_t pv = E.pk[q * 2 + sig];
+          L.frac += pv & 0xffffffu;
+          const int ns = (int)(pv >> 24);
           q_l = row_l == row ? ns : q_l;
         }
         nnz += sig;
@@ -1295,8 +1225,9 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
       const int gt1 = av > 1;
       {
         const int q = __builtin_amdgcn_readlane(q1_l, c1);
-        L.frac += (uint32_t)E.eb[q ^ gt1];
-        const int ns = E.next[q * 2 + gt1];
+        const uint32_t pv = E.pk[q * 2 + gt1];
+        L.frac += pv & 0xffffffu;
+        const int ns = (int)(pv >> 24);
         q1_l = (l & 3) == c1 ? ns : q1_l;
       }
       if (gt1) {
@@ -1343,165 +1274,6 @@ __device__ int coeff_count_staged(const hvx_tu_desc &d, const StagedScan &env, c
     }
     HM_WTADD(3, wt_);
   }
-  return num_sig;
-}
-
-// The same count with each coefficient group's context-coded bins resolved in ROUNDS instead of
-// one after the other: every bin of a group (significance flags, lane = position; greater-1
-// flags, the lane of their level) is known from the levels before any is counted -- its context
-// (the greater-1 context from c1 in closed form: 0 after a greater-1 bin of the group, else
-// min(1 + j, 3) for the j-th) and its value -- and a bin's cost and state update depend only on
-// the bins before it ON THE SAME CONTEXT.  So each bin gets its rank among the group's earlier
-// bins of its context, and round r updates every context's r-th bin at once (different contexts:
-// no conflicts); a group takes max-rank + 1 rounds of one LDS state read / table read / state
-// write instead of one such chain per bin.  The bin costs are integers, summed in any order.  The
-// last position, the CG flag, greater-2 and the bypass bins stay on the serial counter.
-__device__ int coeff_count_par(const hvx_tu_desc &d, const StagedScan &env, const int16_t *ls, CoderLane &L) {
-  const int n = d.width, lw = cab::log2_tu(n), wg = n >> 2, nn = n * n;
-  const int ch = d.comp ? 1 : 0, l = lid();
-  uint64_t cgm = 0;
-  int num_sig = 0, scan_last = -1;
-  const int nw = nn < 64 ? 1 : nn >> 6;
-  for (int w = 0; w < nw; w++) {
-    const uint64_t b = __ballot(w * 64 + l < nn && ls[w * 64 + l] != 0);
-    if (b) {
-      num_sig += __popcll(b);
-      scan_last = w * 64 + 63 - __clzll(b);
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        if ((b >> (16 * q)) & 0xffffu) cgm |= 1ull << env.cg(w * 4 + q);
-    }
-  }
-  if (num_sig == 0) return 0;
-  const bool be_valid = d.transquant_bypass ? false : (d.sign_hiding != 0);
-  if (d.pps_tskip && !d.transquant_bypass && n <= 4) L.bin(cab::kTskip + ch, d.transform_skip ? 1 : 0);
-  {  // codeLastSignificantXY (:1115)
-    const int r = env.raster(scan_last);
-    int py = r >> lw, px = r - (py << lw);
-    if (d.scan_type == 2) { const int t = px; px = py; py = t; }
-    const int gx = kGroupIdx[px], gy = kGroupIdx[py], gmax = kGroupIdx[n - 1];
-    const int cw = lw - 2;
-    const int off = ch ? 0 : cw * 3 + ((cw + 1) >> 2), sh = ch ? cw : (cw + 3) >> 2;
-    const int bx = cab::kLastX + ch * 15 + off, by = cab::kLastY + ch * 15 + off;
-    int k;
-    for (k = 0; k < gx; k++) L.bin(bx + (k >> sh), 1);
-    if (gx < gmax) L.bin(bx + (k >> sh), 0);
-    for (k = 0; k < gy; k++) L.bin(by + (k >> sh), 1);
-    if (gy < gmax) L.bin(by + (k >> sh), 0);
-    if (gx > 3) L.ep((gx - 2) >> 1);
-    if (gy > 3) L.ep((gy - 2) >> 1);
-  }
-  const int base_cg = cab::kSigCG + ch * 2, base_sig = cab::kSig + (ch ? 28 : 0);
-  const int last_set = scan_last >> 4, last_pin = scan_last & 15;
-  bool c1_zero = false;  // c1 == 0 after the previous coded group (its context set's +1)
-  uint32_t fpart = 0;    // this lane's share of the context-coded bin costs
-  uint8_t *st = L.st + cab::kCtxLo;
-  for (int sub = last_set; sub >= 0; sub--) {
-    const int sub_pos = sub << 4;
-    const int cg = env.cg(sub), cgy = cg / wg, cgx = cg - cgy * wg;
-    const int lv_l = l < 16 ? (int)ls[sub_pos + l] : 0;
-    const int av_l = lv_l < 0 ? -lv_l : lv_l;
-    const int sc_l = l < 16 ? (env.big ? (int)env.scan_g[sub_pos + l] : env.sig[sub_pos + l]) : 0;
-    if (sub == last_set || sub == 0) cgm |= 1ull << cg;
-    else {
-      const int rr = cgx < wg - 1 ? (int)((cgm >> (cg + 1)) & 1) : 0;
-      const int bb = cgy < wg - 1 ? (int)((cgm >> (cg + wg)) & 1) : 0;
-      L.bin(base_cg + ((rr + bb) != 0), (int)((cgm >> cg) & 1));
-    }
-    const bool is_last_set = sub == last_set;
-    const uint32_t m16 = (uint32_t)__ballot(lv_l != 0);
-    // significance flags: lane p codes position p (descending), pin 0 only if a flag above it (or
-    // the last position) is 1, or in group 0
-    bool a1 = false;
-    int row1 = 0, val1 = 0, rank1 = 0;
-    if ((cgm >> cg) & 1) {
-      int pattern = 0;
-      if (wg > 1) {
-        const int rr = cgx < wg - 1 ? (int)((cgm >> (cg + 1)) & 1) : 0;
-        const int bb = cgy < wg - 1 ? (int)((cgm >> (cg + wg)) & 1) : 0;
-        pattern = rr + (bb << 1);
-      }
-      const int sc = env.big ? cab::sig_ctx(pattern, env.first_sig, env.single, sc_l, lw, ch) : (sc_l >> (6 * pattern)) & 63;
-      const int start = is_last_set ? last_pin - 1 : 15;
-      const bool pin0 = sub == 0 || is_last_set || (m16 & ((2u << start) - 2u)) != 0;
-      a1 = l <= start && (l > 0 || pin0);
-      row1 = base_sig + sc;
-      val1 = lv_l != 0;
-      for (int q = start; q > 0; q--) {  // earlier (higher) positions on the same context
-        const int sq = __builtin_amdgcn_readlane(sc, q);
-        rank1 += (q > l && sq == sc) ? 1 : 0;
-      }
-    }
-    const int nnz = __popc(m16);
-    // greater-1 flags of the first 8 non-zero levels (descending), in their levels' lanes
-    bool a2 = false;
-    int row2 = 0, val2 = 0, rank2 = 0;
-    uint32_t gmask = 0;
-    int set = 0;
-    if (nnz) {
-      set = (ch ? 4 : 0) + ((!ch && sub > 0) ? 2 : 0) + (c1_zero ? 1 : 0);
-      const int j = l < 16 ? __popc(m16 >> (l + 1)) : 64;  // index among the group's non-zero levels
-      a2 = l < 16 && lv_l != 0 && j < 8;
-      gmask = (uint32_t)__ballot(a2 && av_l > 1);
-      const bool g_before = l < 15 ? (gmask >> (l + 1)) != 0 : false;
-      const int c1 = g_before ? 0 : (j + 1 < 3 ? j + 1 : 3);
-      row2 = cab::kOne + 4 * set + c1;
-      val2 = av_l > 1;
-      if (c1 == 0) {
-        const int hp = 31 - __clz(gmask);  // the first greater-1 bin's position
-        rank2 = j - (__popc(m16 >> (hp + 1)) + 1);
-      } else {
-        rank2 = c1 == 3 ? j - 2 : 0;
-      }
-      c1_zero = gmask != 0;
-    }
-    // the rounds
-    int mr = (a1 ? rank1 : -1) > (a2 ? rank2 : -1) ? (a1 ? rank1 : -1) : (a2 ? rank2 : -1);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { const int t = __shfl_xor(mr, o, HVX_WAVE); mr = t > mr ? t : mr; }
-    for (int r = 0; r <= mr; r++) {
-      if (a1 && rank1 == r) {
-        const int q = st[row1];
-        fpart += (uint32_t)E.eb[q ^ val1];
-        st[row1] = E.next[q * 2 + val1];
-      }
-      if (a2 && rank2 == r) {
-        const int q = st[row2];
-        fpart += (uint32_t)E.eb[q ^ val2];
-        st[row2] = E.next[q * 2 + val2];
-      }
-    }
-    if (nnz == 0) continue;
-    const int last_nz = 31 - __clz(m16), first_nz = __builtin_ctz(m16);
-    const bool hidden = (last_nz - first_nz) >= 4;  // SBH_THRESHOLD
-    bool escape = nnz > 8;
-    if (gmask) {
-      const int hp = 31 - __clz(gmask);
-      const int first_c2_abs = __builtin_amdgcn_readlane(av_l, hp);
-      if (__popc(gmask) > 1) escape = true;
-      const int gt2 = first_c2_abs > 2;
-      L.bin(cab::kAbs + set, gt2);
-      if (gt2) escape = true;
-    }
-    L.ep((be_valid && hidden) ? nnz - 1 : nnz);  // signs (the first one hidden)
-    if (escape) {  // Rice parameter from 0 (no persistent adaptation in the engine's tool set)
-      int rice = 0, first2 = 1, idx = 0;
-      uint32_t all = m16;
-      while (all) {
-        const int pin = 31 - __clz(all);
-        all &= ~(1u << pin);
-        const int av = __builtin_amdgcn_readlane(av_l, pin);
-        const int base = idx < 8 ? 2 + first2 : 1;
-        if (av >= base) {
-          L.ep(cab::remain_bins((uint32_t)(av - base), rice, d.extended_precision != 0, d.max_log2_tr_range));
-          if (av > (3 << rice)) rice = rice + 1 < 4 ? rice + 1 : 4;
-        }
-        if (av >= 2) first2 = 0;
-        idx++;
-      }
-    }
-  }
-  L.frac += wave_sum_u32(fpart);
   return num_sig;
 }
 
@@ -1706,7 +1478,7 @@ __device__ void estimate_bit(int w, int h, int ch) {
   HM_PROF(PR_EST);
   const uint8_t *st = E.cod[E.cur].st;
   hvx_estbits *e = &E.est;
-#define EB(ctx, v) E.eb[st[(ctx)] ^ (v)]
+#define EB(ctx, v) (int32_t)ebits(st[(ctx)] ^ (v))
   const int l = lid(), b = l & 1;
   static_assert(HVX_CTX_QT_CBF >= 28 && HVX_CTX_ABS + 6 <= 180, "estBit's context range");
   {
@@ -3584,7 +3356,7 @@ __device__ void intra_first_pass(const Cu *cu, const Tu &tpu, Yuv *org, int dept
   const Coder &cb = E.cod[RD(depth, CI_CURR_BEST)];
   const uint64_t frac = (uint64_t)(uint32_t)(cb.frac & 32767);
   const int st = cb.st[X_INTRA] & 127;
-  const uint64_t eb_mpm = (uint64_t)(uint32_t)E.eb[st ^ 1], eb_no = (uint64_t)(uint32_t)E.eb[st];
+  const uint64_t eb_mpm = (uint64_t)ebits(st ^ 1), eb_no = (uint64_t)ebits(st);
   for (int m = 0; m < 35; m++) {
     const int idx = m == mp0 ? 0 : m == mp1 ? 1 : m == mp2 ? 2 : -1;
     const uint64_t total = frac + (idx >= 0 ? eb_mpm : eb_no) + 32768ull * (uint64_t)(idx < 0 ? 5 : idx ? 2 : 1);
@@ -4501,12 +4273,7 @@ static __global__ __launch_bounds__(64) HM_KATTR void k_hm_compress(const hvx_hm
   wsync();
   copy_words(&hm_e.P, &pics[job.pic], (int)sizeof(hvx_hm_picture));
   wsync();
-  for (int i = l; i < 128; i += 64) {
-    hm_e.eb[i] = hm_e.P.entropy_bits[i];
-    const int p = i >> 1, mps = i & 1;
-    hm_e.next[i * 2 + mps] = (uint8_t)(((p < 62 ? p + 1 : p) << 1) | mps);
-    hm_e.next[i * 2 + (mps ^ 1)] = (uint8_t)((cab::kTransIdxLps[p] << 1) | (p == 0 ? mps ^ 1 : mps));
-  }
+  hm_fill_pk(hm_e.P.entropy_bits, l);
   hm_e.S = S;
   if (l < 4) hm_e.dbg[l] = 0;
   hm_e.stage = job.flags >> 8;

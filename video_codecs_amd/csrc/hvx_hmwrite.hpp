@@ -85,7 +85,7 @@ __device__ void sw_bin(int ctx, int v) {
   } else {
     SW.range = r;
   }
-  SW.st[ctx] = E.next[q * 2 + v];
+  SW.st[ctx] = (uint8_t)nstate(q * 2 + v);
 }
 // encodeAlignedBinsEP (:334): only with range == 256
 __device__ void sw_aligned(uint32_t vals, int n) {
