@@ -85,3 +85,54 @@ def test_stv_direction_map_vectorised_equals_reference_form():
         col[:, 3:7] = rng.integers(-40, 41, (n * 16, 4))
         col[rng.random(n * 16) < 0.1, 3:5] = 0
         np.testing.assert_array_equal(gop.stv_direction_map(col, w, h), hm.stv_direction_map(col, w, h))
+
+
+def test_write_slices_follows_hm_slice_chain():
+    """ClosedSegments.write_slices' host side with the writer stubbed (results drawn per (segment,
+    slice, start table)): every P / B slice after the first is written from both tables in one launch,
+    and the chain of choices followed afterwards equals HM's one-slice-after-another order --
+    TEncGOP.cpp:1559 (slice k written with what slice k - 1 chose), TEncSlice.cpp:1096-1099
+    (determineCabacInitIdx after each slice) -- simulated sequentially here."""
+    import torch
+    plan = gop.load_plan("ldp", 3)
+    cs = gop.ClosedSegments(plan, 64 * 3, 64 * 6, [27, 37], org_fn=None, rows=1, device="cpu")
+    cs.t = 1
+    st = plan[1].slice_type
+    eb = hm._abi.load_entropy_bits()
+    start = {t: {q: cabac_init.slice_start_states(t, q) for q in range(52)} for t in (0, 1, 2)}
+
+    def result(s, c, table):
+        r = np.random.default_rng(1000 * s + 10 * c + table)
+        out = np.zeros(1, hm.HM_SLICE_RESULT)[0]
+        out["states"][:202] = r.integers(0, 126, 202)
+        out["coded"] = r.integers(0, 1 << 32, 7, dtype=np.uint64).astype(np.uint32)
+        out["n_bytes"] = 100 + 10 * c + table
+        return out
+
+    class FakeEngine:
+        launches = 0
+
+        def write_slices_launch(self, sl_t, n, res_t):
+            FakeEngine.launches += 1
+            sl = sl_t.numpy().view(hm.HM_SLICE)
+            res = res_t.numpy().view(hm.HM_SLICE_RESULT)
+            for k in range(n):
+                s, c = int(sl[k]["pic"]), int(sl[k]["first_ctu"]) // cs.cl
+                qp = cs.cur[s]["qp"]
+                table = [t for t in (0, 1) if np.array_equal(sl[k]["entry"]["st"], start[t][qp])]
+                assert len(table) == 1
+                res[k] = result(s, c, table[0])
+    cs.eng = FakeEngine()
+    cs.cur = [dict(qp=q, table=t) for q, t in ((27 + 3, 1), (37 + 3, 0))]
+    nbytes = cs.write_slices(None)
+    assert FakeEngine.launches == 1 and cs.nch == 6
+    for s, seg in enumerate(cs.segs):
+        tab, used, nb = cs.cur[s]["table"], [], 0
+        for c in range(cs.nch):
+            t = cabac_init.resolve_table(st, tab)
+            used.append(t)
+            r = result(s, c, t)
+            nb += int(r["n_bytes"])
+            tab = cabac_init.determine_cabac_init_idx(st, r["states"][:202], cabac_init.coded_flags(r["coded"]), cs.cur[s]["qp"], eb)
+        assert cs.last_slices[3][s] == used and seg.enc_table == tab and nbytes[s] == nb
+    assert any(len(set(u)) > 1 for u in cs.last_slices[3])  # the chain departs from the picture's table
