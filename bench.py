@@ -873,7 +873,9 @@ def main():
                          "rank)" % (n_gathered, len(work.cs.segs)) if world > 1 else "local",
                   "n1_comparable": "the N=1 line's config5_closed_segments figure (the same per-GPU workload; compare "
                                    "timed_pictures' per-POC rates with its pictures' -- the reference count grows "
-                                   "with the POC)"}
+                                   "with the POC); this exact line at N=1 (--workload closed --steps 20 --warmup 5): "
+                                   "1412.3 CTUs/s, profiles/bench_closed_r06c.log -- scaling efficiency at N is "
+                                   "value / (N x that), not value / (N x the steady-state headline)"}
         data = ("synthetic: splitmix64 uniform random 8-bit 4:2:0 originals made on the device (BASELINE.md sec. 3), "
                 "frame indices disjoint per segment and rank; references made by each segment's own loop")
     if rank == 0:
