@@ -490,7 +490,8 @@ def config5_measure(threads, W=1920, H=1088, segs=120, pics=3, base_qp=32, ctus_
     return res
 
 
-def config4_measure(threads, W=1920, H=1088, segs_per_qp=30, qps=(22, 27, 32, 37), pics=3, ctus_step=6, parity=True):
+def config4_measure(threads, W=1920, H=1088, segs_per_qp=30, qps=(22, 27, 32, 37), pics=3, ctus_step=6, parity=True,
+                    rows=1):
     """Side figure, BASELINE config 4 as an encode: closed random-access segments (HM's
     encoder_randomaccess_main structure: I, then POC 8, 4, ... of the first GOP8) decided with the
     stvssim encoder's active cost (HVX_RD_STVSSIM: distortionstVSSIM over the segment's own history of
@@ -499,7 +500,7 @@ def config4_measure(threads, W=1920, H=1088, segs_per_qp=30, qps=(22, 27, 32, 37
     segment's last picture (3 of its slice chains)."""
     from video_codecs_amd import _abi
     base = [q for q in qps for _ in range(segs_per_qp)]
-    work = ClosedWorkload(W, H, base, pics, rank=0, kind="ra", ctus_step=ctus_step, rd_metric=_abi.RD_STVSSIM)
+    work = ClosedWorkload(W, H, base, pics, rank=0, kind="ra", rows=rows, ctus_step=ctus_step, rd_metric=_abi.RD_STVSSIM)
     nch = work.cs.nch
     par = {"qp%d" % q: ClosedParity(work, pics - 1, k * segs_per_qp, sorted({0, nch // 2, nch - 1}))
            for k, q in enumerate(qps)} if parity else None
