@@ -158,3 +158,8 @@ python3 oracle/make_yuv.py texture 192 128 9 "$TMP/tex192.yuv"
 HVX_CAPTURE="$TMP/cu.bin" $ORC/TAppEncoder_cucap -c $CFG/encoder_randomaccess_main.cfg -i "$TMP/tex192.yuv" -wdt 192 -hgt 128 \
   -fr 30 -f 9 -q 32 --SliceMode=1 --SliceArgument=3 -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
 python3 oracle/compact_ctu.py "$TMP/cu.bin" tests/golden/ctu_ra_closed_slices.bin
+# a closed LDP segment long enough for four references (POC 4..8), 128x64, QP 32, one slice per picture
+python3 oracle/make_yuv.py texture 128 64 9 "$TMP/tex128x9.yuv"
+HVX_CAPTURE="$TMP/cu.bin" $ORC/TAppEncoder_cucap -c $CFG/encoder_lowdelay_P_main.cfg -i "$TMP/tex128x9.yuv" -wdt 128 -hgt 64 \
+  -fr 30 -f 9 -q 32 -b "$TMP/str.bin" -o "$TMP/rec.yuv" > "$TMP/log.txt"
+python3 oracle/compact_ctu.py "$TMP/cu.bin" tests/golden/ctu_ldp_closed_4ref.bin

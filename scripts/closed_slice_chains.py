@@ -11,5 +11,5 @@ from tests import test_gop_gpu as t  # noqa: E402
 
 out = {}
 for name, kind, w, h, qp in (("ctu_ldp_closed_slices.bin", "ldp", 448, 256, 30), ("ctu_ra_closed_slices.bin", "ra", 192, 128, 32)):
-    out[name] = t._closed_row_slices(torch, name, kind, w, h, qp)
+    out[name] = t._closed_vs_capture(torch, name, kind, w, h, qp)
 print(json.dumps(out))

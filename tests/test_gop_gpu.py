@@ -12,6 +12,8 @@
   (SliceMode 1), SAO on: every CTU, finished picture and CABAC table equals HM's encode
   (tests/golden/ctu_{ldp,ra}_closed_slices.bin).  Each slice after the first is written with the table
   the slice before it chose, as HM writes them (gop.ClosedSegments.write_slices).
+- test_closed_ldp_four_refs_vs_hm: LDP I + 8 P pictures (128x64, QP 32), four device-made references
+  from POC 4 on, against HM's encode (tests/golden/ctu_ldp_closed_4ref.bin).
 - test_closed_ra_stvssim_full_history: config 4 as an encode -- a closed RA segment decided with the
   stvssim encoder's active cost (HVX_RD_STVSSIM) over the segment's own history of originals and final
   reconstructions, up to the full 25 pictures (POC 28, coding index 26): every picture re-decided by the
@@ -123,9 +125,10 @@ def test_closed_ldp_segment_vs_hm(torch):
     assert not bad, bad[:6]
 
 
-def _closed_row_slices(torch, name, kind, W, H, qp):
-    """A closed segment with one slice per CTU row against HM's encode of the same YUV (capture `name`):
-    every CTU, finished picture and CABAC table; returns the tables each picture's slices were written with."""
+def _closed_vs_capture(torch, name, kind, W, H, qp):
+    """A closed segment with one slice per CTU row (one slice when the picture is one row) against HM's
+    encode of the same YUV (capture `name`): every CTU, finished picture and CABAC table; returns the
+    tables each picture's slices were written with."""
     from video_codecs_amd import cabac_init, gop, hvx
     hvx.context()
     g = gc.load(name)
@@ -159,14 +162,21 @@ def _closed_row_slices(torch, name, kind, W, H, qp):
 
 @pytest.mark.gpu
 def test_closed_ldp_row_slices_vs_hm(torch):
-    _closed_row_slices(torch, "ctu_ldp_closed_slices.bin", "ldp", 448, 256, 30)
+    _closed_vs_capture(torch, "ctu_ldp_closed_slices.bin", "ldp", 448, 256, 30)
 
 
 @pytest.mark.gpu
 def test_closed_ra_row_slices_vs_hm(torch):
     """RA (I + one GOP8, B slices) at 192x128 with two row slices per picture, QP 32
     (tests/golden/ctu_ra_closed_slices.bin)."""
-    _closed_row_slices(torch, "ctu_ra_closed_slices.bin", "ra", 192, 128, 32)
+    _closed_vs_capture(torch, "ctu_ra_closed_slices.bin", "ra", 192, 128, 32)
+
+
+@pytest.mark.gpu
+def test_closed_ldp_four_refs_vs_hm(torch):
+    """LDP I + 8 P pictures at 128x64, QP 32: from POC 4 on every P picture searches four references the
+    device made (tests/golden/ctu_ldp_closed_4ref.bin) -- the headline's reference count in a closed loop."""
+    _closed_vs_capture(torch, "ctu_ldp_closed_4ref.bin", "ldp", 128, 64, 32)
 
 
 @pytest.mark.gpu
